@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: ResNet-50 (ImageNet-shaped, synthetic data, random init)
+data-parallel training on N MI355X GPUs, bf16 compute with fp32 master weights,
+bucketed RCCL all-reduce overlapped with backward.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
+
+Prints ONE JSON line on rank 0.  ``value`` is whole-job samples/s (all ranks),
+``scaling`` is weak (fixed per-GPU batch).  ``--model wdl`` runs the
+Wide&Deep-Criteo-shape configuration instead (secondary metric).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--batch', type=int, default=256, help='per-GPU batch')
+    p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl'])
+    p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    p.add_argument('--bucket-mb', type=float, default=32)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.parallel import comm as C
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    assert world == args.gpus or world == 1, 'launch with --nproc-per-node == --gpus'
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+
+    if args.model == 'resnet50':
+        from hetu_61a7_amd.models import resnet50_imagenet
+        B = args.batch
+        x = ht.Variable(name='x')
+        y_ = ht.Variable(name='y_')
+        loss, logits = resnet50_imagenet(x, y_, 1000)
+        opt = ht.optim.MomentumOptimizer(learning_rate=0.1 / max(world, 1), momentum=0.9)
+        train_op = opt.minimize(loss)
+        kw = dict(mixed_precision=args.dtype, bucket_mb=args.bucket_mb, seed=1234)
+        if world > 1:
+            ex = ht.Executor({'train': [loss, train_op]}, dist_strategy=ht.dist.DataParallel('allreduce'), **kw)
+        else:
+            ex = ht.Executor({'train': [loss, train_op]}, ctx=ht.gpu(local), **kw)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000 + rank)
+        dt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+        X = torch.randn((B, 3, 224, 224), generator=g, device=dev).to(dt)
+        X = X.contiguous(memory_format=torch.channels_last)
+        lab = torch.randint(0, 1000, (B,), generator=g, device=dev)
+        Y = torch.nn.functional.one_hot(lab, 1000).to(dt)
+        feed = {x: X, y_: Y}
+        metric = 'samples/sec (whole node) ResNet-50 AllReduce'
+        cfg = {'model': 'ResNet-50 (ImageNet-shaped, v1.5)', 'global_batch': B * world, 'seq_len': None,
+               'image': '3x224x224', 'parallelism': 'dp%d' % world, 'optimizer': 'momentum-sgd',
+               'per_gpu_batch': B}
+        step = lambda: ex.run('train', feed_dict=feed)
+        samples_per_step = B * world
+    else:
+        from hetu_61a7_amd.models.ctr import wdl_criteo_bench
+        step, samples_per_step, cfg, metric = wdl_criteo_bench(args, world, rank, local)
+
+    def barrier():
+        if world > 1:
+            C.world().barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt_s = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt_s], dtype=torch.float64, device=dev)
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_s = float(t.item())
+    ms = dt_s * 1000.0 / args.steps
+    value = samples_per_step * args.steps / dt_s
+    if rank == 0:
+        out = {'metric': metric, 'value': round(value, 2), 'unit': 'samples/s', 'n_gpus': world,
+               'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
+               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+               'dtype': args.dtype, 'data': 'synthetic (random-init weights)', 'config': cfg}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        C.destroy()
+
+
+if __name__ == '__main__':
+    main()

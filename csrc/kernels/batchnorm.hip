@@ -1,0 +1,389 @@
+// BatchNorm for channels-last activations ([M, C], M = N*H*W) on gfx950.
+//
+// Replaces the reference's cuDNN BN path (src/ops/CudnnBn.cu:22-194) with a
+// three-kernel schedule per direction, fused with the ops that surround BN in
+// ResNet:
+//   fwd:  partial stats (Welford-merge) -> finalize (running stats, fold affine
+//         into a,b) -> apply y = relu?(x*a + b (+ residual))
+//   bwd:  partial sums of dy' and dy'*xhat (dy' = dy masked by y>0 when ReLU was
+//         fused) -> finalize (dscale, dbias, fold dx = A*dy' + B*x + C) -> apply
+//         (also emits d(residual) = dy' when a residual add was fused).
+// Each streaming kernel moves 16 B per lane (8 bf16 or 4 fp32 channels).
+#include "common.h"
+
+namespace hetu {
+
+// ---------------------------------------------------------------------------
+// geometry: a block covers W vector-columns (W*VEC channels) x RP rows/pass.
+struct BnGeom {
+  int W, RP, tiles, chunks;
+  int64_t rows_per_chunk;
+};
+
+static BnGeom bn_geom(int64_t M, int C, int vec) {
+  BnGeom g;
+  int cv = C / vec;
+  g.W = cv < 64 ? cv : 64;
+  g.RP = 256 / g.W;
+  g.tiles = (cv + g.W - 1) / g.W;
+  int want = (int)((2048 + g.tiles - 1) / g.tiles);
+  int64_t max_chunks = (M + g.RP - 1) / g.RP;
+  if (want > max_chunks) want = (int)max_chunks;
+  if (want < 1) want = 1;
+  g.chunks = want;
+  g.rows_per_chunk = (M + g.chunks - 1) / g.chunks;
+  return g;
+}
+
+// partial statistics: ws_mean/ws_m2 [chunks][C]; counts derivable on host side
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x, int64_t M, int C,
+                                                         int W, int RP, int64_t rows_per_chunk,
+                                                         float* __restrict__ ws_mean,
+                                                         float* __restrict__ ws_m2) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float sh_s[256 * V];
+  __shared__ float sh_q[256 * V];
+  const int t = threadIdx.x;
+  const int col = t % W, rsub = t / W;
+  const int vc = blockIdx.y * W + col;  // vector column
+  const bool active = (rsub < RP) && (vc * V < C);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > M) r1 = M;
+  float s[V], q[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; }
+  if (active) {
+    for (int64_t r = r0 + rsub; r < r1; r += RP) {
+      float v[V];
+      load_vec<T>(x + r * C + (int64_t)vc * V, v);
+#pragma unroll
+      for (int i = 0; i < V; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) { sh_s[t * V + i] = s[i]; sh_q[t * V + i] = q[i]; }
+  __syncthreads();
+  // one thread per channel of the tile folds the RP row-partials
+  const int nch = W * V;
+  if (t < nch) {
+    const int c_local = t, colw = c_local / V, lane_i = c_local % V;
+    float S = 0.f, Q = 0.f;
+    for (int rr = 0; rr < RP; ++rr) {
+      int tt = rr * W + colw;
+      S += sh_s[tt * V + lane_i];
+      Q += sh_q[tt * V + lane_i];
+    }
+    const int c = blockIdx.y * W * V + c_local;
+    const float n = (float)(r1 > r0 ? (r1 - r0) : 0);
+    if (c < C) {
+      float mean = n > 0 ? S / n : 0.f;
+      float m2 = n > 0 ? fmaxf(Q - S * mean, 0.f) : 0.f;
+      ws_mean[(int64_t)blockIdx.x * C + c] = mean;
+      ws_m2[(int64_t)blockIdx.x * C + c] = m2;
+    }
+  }
+}
+
+// Chan merge of chunk partials; writes save_mean/save_invstd, running stats and
+// folded affine (a = scale*invstd, b = bias - mean*a).
+__global__ void bn_stats_finalize(const float* __restrict__ ws_mean, const float* __restrict__ ws_m2,
+                                  int chunks, int64_t rows_per_chunk, int64_t M, int C,
+                                  const float* __restrict__ scale, const float* __restrict__ bias,
+                                  float* __restrict__ run_mean, float* __restrict__ run_var,
+                                  float factor, float eps, float* __restrict__ save_mean,
+                                  float* __restrict__ save_invstd, float* __restrict__ fold_a,
+                                  float* __restrict__ fold_b) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int p = 0; p < chunks; ++p) {
+    int64_t r0 = (int64_t)p * rows_per_chunk;
+    int64_t r1 = r0 + rows_per_chunk;
+    if (r1 > M) r1 = M;
+    float nb = (float)(r1 > r0 ? r1 - r0 : 0);
+    if (nb <= 0.f) continue;
+    float mb = ws_mean[(int64_t)p * C + c], qb = ws_m2[(int64_t)p * C + c];
+    float nn = n + nb;
+    float d = mb - mean;
+    mean += d * (nb / nn);
+    m2 += qb + d * d * (n * nb / nn);
+    n = nn;
+  }
+  float var = n > 0.f ? m2 / n : 0.f;
+  float invstd = rsqrtf(var + eps);
+  save_mean[c] = mean;
+  save_invstd[c] = invstd;
+  if (run_mean != nullptr) {
+    float unb = n > 1.f ? m2 / (n - 1.f) : var;
+    run_mean[c] = (1.f - factor) * run_mean[c] + factor * mean;
+    run_var[c] = (1.f - factor) * run_var[c] + factor * unb;
+  }
+  float a = scale[c] * invstd;
+  fold_a[c] = a;
+  fold_b[c] = bias[c] - mean * a;
+}
+
+// inference: fold running stats
+__global__ void bn_infer_fold(const float* __restrict__ run_mean, const float* __restrict__ run_var,
+                              const float* __restrict__ scale, const float* __restrict__ bias, int C,
+                              float eps, float* __restrict__ fold_a, float* __restrict__ fold_b) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = scale[c] * rsqrtf(run_var[c] + eps);
+  fold_a[c] = a;
+  fold_b[c] = bias[c] - run_mean[c] * a;
+}
+
+template <typename T, bool RELU, bool RES>
+__global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T* __restrict__ res,
+                                                 const float* __restrict__ fa,
+                                                 const float* __restrict__ fb, T* __restrict__ y,
+                                                 int64_t nvec, int C) {
+  constexpr int V = Vec<T>::N;
+  const int cv = C / V;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * V;
+    float v[V];
+    load_vec<T>(x + i * V, v);
+    float r[V];
+    if (RES) load_vec<T>(res + i * V, r);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float o = v[k] * fa[c0 + k] + fb[c0 + k];
+      if (RES) o += r[k];
+      if (RELU) o = fmaxf(o, 0.f);
+      v[k] = o;
+    }
+    store_vec<T>(y + i * V, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ y,
+                                                       const T* __restrict__ x,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, int64_t M,
+                                                       int C, int W, int RP, int64_t rows_per_chunk,
+                                                       float* __restrict__ ws_sdy,
+                                                       float* __restrict__ ws_sdyx) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float sh_s[256 * V];
+  __shared__ float sh_q[256 * V];
+  const int t = threadIdx.x;
+  const int col = t % W, rsub = t / W;
+  const int vc = blockIdx.y * W + col;
+  const bool active = (rsub < RP) && (vc * V < C);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > M) r1 = M;
+  float s[V], q[V], mu[V], is[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) { mu[i] = mean[vc * V + i]; is[i] = invstd[vc * V + i]; }
+    for (int64_t r = r0 + rsub; r < r1; r += RP) {
+      const int64_t off = r * C + (int64_t)vc * V;
+      float g[V], xv[V];
+      load_vec<T>(dy + off, g);
+      load_vec<T>(x + off, xv);
+      if (RELU) {
+        float yv[V];
+        load_vec<T>(y + off, yv);
+#pragma unroll
+        for (int i = 0; i < V; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        s[i] += g[i];
+        q[i] += g[i] * (xv[i] - mu[i]) * is[i];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) { sh_s[t * V + i] = s[i]; sh_q[t * V + i] = q[i]; }
+  __syncthreads();
+  const int nch = W * V;
+  if (t < nch) {
+    const int colw = t / V, lane_i = t % V;
+    float S = 0.f, Q = 0.f;
+    for (int rr = 0; rr < RP; ++rr) {
+      int tt = rr * W + colw;
+      S += sh_s[tt * V + lane_i];
+      Q += sh_q[tt * V + lane_i];
+    }
+    const int c = blockIdx.y * W * V + t;
+    if (c < C) {
+      ws_sdy[(int64_t)blockIdx.x * C + c] = S;
+      ws_sdyx[(int64_t)blockIdx.x * C + c] = Q;
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize(const float* __restrict__ ws_sdy, const float* __restrict__ ws_sdyx,
+                                int chunks, int64_t M, int C, const float* __restrict__ scale,
+                                const float* __restrict__ mean, const float* __restrict__ invstd,
+                                float* __restrict__ dscale, float* __restrict__ dbias,
+                                float* __restrict__ cA, float* __restrict__ cB,
+                                float* __restrict__ cC) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sdy = 0.f, sdyx = 0.f;
+  for (int p = 0; p < chunks; ++p) {
+    sdy += ws_sdy[(int64_t)p * C + c];
+    sdyx += ws_sdyx[(int64_t)p * C + c];
+  }
+  if (dscale) dscale[c] = sdyx;
+  if (dbias) dbias[c] = sdy;
+  const float invM = 1.f / (float)M;
+  const float is = invstd[c];
+  const float k1 = scale[c] * is;
+  const float B = -k1 * is * sdyx * invM;
+  cA[c] = k1;
+  cB[c] = B;
+  cC[c] = -k1 * sdy * invM - mean[c] * B;
+}
+
+template <typename T, bool RELU, bool DRES>
+__global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ y,
+                                                     const T* __restrict__ x,
+                                                     const float* __restrict__ cA,
+                                                     const float* __restrict__ cB,
+                                                     const float* __restrict__ cC,
+                                                     T* __restrict__ dx, T* __restrict__ dres,
+                                                     int64_t nvec, int C) {
+  constexpr int V = Vec<T>::N;
+  const int cv = C / V;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * V;
+    float g[V], xv[V];
+    load_vec<T>(dy + i * V, g);
+    load_vec<T>(x + i * V, xv);
+    if (RELU) {
+      float yv[V];
+      load_vec<T>(y + i * V, yv);
+#pragma unroll
+      for (int k = 0; k < V; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if (DRES) store_vec<T>(dres + i * V, g);
+    float o[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) o[k] = cA[c0 + k] * g[k] + cB[c0 + k] * xv[k] + cC[c0 + k];
+    store_vec<T>(dx + i * V, o);
+  }
+}
+
+}  // namespace hetu
+
+using namespace hetu;
+
+// workspace floats needed: 2 * chunks * C + 2 * C  (partials + fold)
+HETU_API int64_t hetu_bn_workspace_floats(int64_t M, int C, int is_bf16) {
+  BnGeom g = bn_geom(M, C, is_bf16 ? 8 : 4);
+  return 2 * (int64_t)g.chunks * C + 3 * (int64_t)C;
+}
+
+template <typename T>
+static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
+                       const float* bias, float* run_mean, float* run_var, float factor, float eps,
+                       float* save_mean, float* save_invstd, float* ws, int relu, int training,
+                       hipStream_t st) {
+  constexpr int V = Vec<T>::N;
+  if (C % V != 0) return (int)hipErrorInvalidValue;
+  BnGeom g = bn_geom(M, C, V);
+  float* fa = ws + 2 * (int64_t)g.chunks * C;
+  float* fb = fa + C;
+  if (training) {
+    float* wm = ws;
+    float* wq = ws + (int64_t)g.chunks * C;
+    hipLaunchKernelGGL(bn_stats_partial<T>, dim3(g.chunks, g.tiles), dim3(256), 0, st,
+                       (const T*)x, M, C, g.W, g.RP, g.rows_per_chunk, wm, wq);
+    hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 255) / 256), dim3(256), 0, st, wm, wq,
+                       g.chunks, g.rows_per_chunk, M, C, scale, bias, run_mean, run_var, factor,
+                       eps, save_mean, save_invstd, fa, fb);
+  } else {
+    hipLaunchKernelGGL(bn_infer_fold, dim3((C + 255) / 256), dim3(256), 0, st, run_mean, run_var,
+                       scale, bias, C, eps, fa, fb);
+  }
+  int64_t nvec = M * C / V;
+  int grid = stream_grid(nvec, 256, 4);
+  const T* xr = (const T*)x;
+  const T* rr = (const T*)res;
+  T* yr = (T*)y;
+  if (relu && res)
+    hipLaunchKernelGGL((bn_apply<T, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply<T, true, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply<T, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_apply<T, false, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+// x,y,res: [M,C] channels-last; res may be null; run_* may be null (no update)
+HETU_API int hetu_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int is_bf16,
+                         const float* scale, const float* bias, float* run_mean, float* run_var,
+                         float factor, float eps, float* save_mean, float* save_invstd, float* ws,
+                         int relu, int training, hipStream_t st) {
+  if (is_bf16)
+    return bn_fwd_impl<bf16>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
+                             save_mean, save_invstd, ws, relu, training, st);
+  return bn_fwd_impl<float>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
+                            save_mean, save_invstd, ws, relu, training, st);
+}
+
+template <typename T>
+static int bn_bwd_impl(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M,
+                       int C, const float* scale, const float* mean, const float* invstd,
+                       float* dscale, float* dbias, float* ws, int relu, hipStream_t st) {
+  constexpr int V = Vec<T>::N;
+  if (C % V != 0) return (int)hipErrorInvalidValue;
+  BnGeom g = bn_geom(M, C, V);
+  float* w1 = ws;
+  float* w2 = ws + (int64_t)g.chunks * C;
+  float* cA = ws + 2 * (int64_t)g.chunks * C;
+  float* cB = cA + C;
+  float* cC = cB + C;
+  if (relu)
+    hipLaunchKernelGGL((bn_bwd_partial<T, true>), dim3(g.chunks, g.tiles), dim3(256), 0, st,
+                       (const T*)dy, (const T*)y, (const T*)x, mean, invstd, M, C, g.W, g.RP,
+                       g.rows_per_chunk, w1, w2);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial<T, false>), dim3(g.chunks, g.tiles), dim3(256), 0, st,
+                       (const T*)dy, (const T*)y, (const T*)x, mean, invstd, M, C, g.W, g.RP,
+                       g.rows_per_chunk, w1, w2);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, w1, w2, g.chunks, M,
+                     C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
+  int64_t nvec = M * C / V;
+  int grid = stream_grid(nvec, 256, 4);
+  const T *dyr = (const T*)dy, *yr = (const T*)y, *xr = (const T*)x;
+  T *dxr = (T*)dx, *drr = (T*)dres;
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_bwd_apply<T, true, true>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply<T, true, false>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
+  else if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply<T, false, true>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply<T, false, false>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+// dy,y,x,dx,dres: [M,C]; y only read when relu; dres may be null
+HETU_API int hetu_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres,
+                         int64_t M, int C, int is_bf16, const float* scale, const float* mean,
+                         const float* invstd, float* dscale, float* dbias, float* ws, int relu,
+                         hipStream_t st) {
+  if (is_bf16)
+    return bn_bwd_impl<bf16>(dy, y, x, dx, dres, M, C, scale, mean, invstd, dscale, dbias, ws, relu, st);
+  return bn_bwd_impl<float>(dy, y, x, dx, dres, M, C, scale, mean, invstd, dscale, dbias, ws, relu, st);
+}

@@ -1,0 +1,143 @@
+// Embedding gather, row scatter-add and row-sparse optimizer updates.
+//
+// Replaces src/ops/EmbeddingLookup.cu (one THREAD per id copying a whole row
+// serially), IndexedSlices.cu and OptimizersSparse.cu.  Here one 64-lane wave
+// moves one row with 16-byte lanes (8 bf16 / 4 fp32 per lane), ids are int64
+// (no float-encoded ids), out-of-range ids produce zero rows like
+// the reference.  Sparse updates run on de-duplicated rows (unique ids), so
+// every row is owned by exactly one wave: no atomics, deterministic.
+#include "common.h"
+
+namespace hetu {
+
+template <typename T>
+__global__ void __launch_bounds__(256) gather_rows_k(const T* __restrict__ table, const int64_t* __restrict__ ids,
+                                                      T* __restrict__ out, int64_t n, int64_t dim,
+                                                      int64_t nrows) {
+  constexpr int V = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
+    const int64_t id = ids[r];
+    const bool ok = id >= 0 && id < nrows;
+    T* o = out + r * dim;
+    if (dim % V == 0) {
+      for (int64_t j = lane * V; j < dim; j += 64 * V) {
+        float v[V];
+        if (ok) load_vec<T>(table + id * dim + j, v);
+        else {
+#pragma unroll
+          for (int k = 0; k < V; ++k) v[k] = 0.f;
+        }
+        store_vec<T>(o + j, v);
+      }
+    } else {
+      for (int64_t j = lane; j < dim; j += 64) o[j] = ok ? table[id * dim + j] : from_f<T>(0.f);
+    }
+  }
+}
+
+// dst[ids[r], :] += src[r, :]  (fp32 destination, atomics; used for dense grads)
+template <typename T>
+__global__ void __launch_bounds__(256) scatter_add_rows_k(float* __restrict__ dst, const int64_t* __restrict__ ids,
+                                                           const T* __restrict__ src, int64_t n,
+                                                           int64_t dim, int64_t nrows) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
+    const int64_t id = ids[r];
+    if (id < 0 || id >= nrows) continue;
+    for (int64_t j = lane; j < dim; j += 64) atomicAdd(dst + id * dim + j, to_f(src[r * dim + j]));
+  }
+}
+
+// segment sum by inverse map: out[inv[r], :] += src[r, :] into fp32 out (dedup)
+// identical to scatter_add but kept separate for clarity of intent.
+
+enum { SP_SGD = 0, SP_MOMENTUM = 1, SP_NESTEROV = 2, SP_ADAGRAD = 3, SP_ADAM = 4, SP_ADAMW = 5 };
+
+template <int MODE>
+__global__ void __launch_bounds__(256) sparse_opt_k(float* __restrict__ table, float* __restrict__ s1,
+                                                     float* __restrict__ s2, const int64_t* __restrict__ ids,
+                                                     const float* __restrict__ g, int64_t n, int64_t dim,
+                                                     int64_t nrows, float lr, float l2, float mu,
+                                                     float b1, float b2, float b1t, float b2t,
+                                                     float eps, float wd) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
+    const int64_t id = ids[r];
+    if (id < 0 || id >= nrows) continue;
+    for (int64_t j = lane; j < dim; j += 64) {
+      const int64_t o = id * dim + j;
+      float p = table[o];
+      float gr = g[r * dim + j] + l2 * p;
+      if (MODE == SP_SGD) {
+        p -= lr * gr;
+      } else if (MODE == SP_MOMENTUM) {
+        float v = mu * s1[o] - lr * gr;
+        s1[o] = v;
+        p += v;
+      } else if (MODE == SP_NESTEROV) {
+        float t = lr * gr;
+        float v = mu * (s1[o] - t);
+        s1[o] = v;
+        p += v - t;
+      } else if (MODE == SP_ADAGRAD) {
+        float a = s1[o] + gr * gr;
+        s1[o] = a;
+        p -= lr * gr / (sqrtf(a) + eps);
+      } else {
+        float m = b1 * s1[o] + (1.f - b1) * gr;
+        float v = b2 * s2[o] + (1.f - b2) * gr * gr;
+        s1[o] = m;
+        s2[o] = v;
+        float u = (m / (1.f - b1t)) / (sqrtf(v / (1.f - b2t)) + eps);
+        p -= (MODE == SP_ADAM) ? lr * u : lr * (u + wd * p);
+      }
+      table[o] = p;
+    }
+  }
+}
+
+}  // namespace hetu
+
+using namespace hetu;
+
+static inline int rows_blocks(int64_t n) {
+  int64_t b = (n + 3) / 4;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+HETU_API int hetu_gather_rows(const void* table, const int64_t* ids, void* out, int64_t n,
+                              int64_t dim, int64_t nrows, int is_bf16, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (is_bf16) hipLaunchKernelGGL(gather_rows_k<bf16>, dim3(rows_blocks(n)), dim3(256), 0, st, (const bf16*)table, ids, (bf16*)out, n, dim, nrows);
+  else hipLaunchKernelGGL(gather_rows_k<float>, dim3(rows_blocks(n)), dim3(256), 0, st, (const float*)table, ids, (float*)out, n, dim, nrows);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_scatter_add_rows(float* dst, const int64_t* ids, const void* src, int64_t n,
+                                   int64_t dim, int64_t nrows, int src_bf16, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (src_bf16) hipLaunchKernelGGL(scatter_add_rows_k<bf16>, dim3(rows_blocks(n)), dim3(256), 0, st, dst, ids, (const bf16*)src, n, dim, nrows);
+  else hipLaunchKernelGGL(scatter_add_rows_k<float>, dim3(rows_blocks(n)), dim3(256), 0, st, dst, ids, (const float*)src, n, dim, nrows);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_sparse_opt(int mode, float* table, float* s1, float* s2, const int64_t* ids,
+                             const float* g, int64_t n, int64_t dim, int64_t nrows, float lr,
+                             float l2, float mu, float b1, float b2, float b1t, float b2t,
+                             float eps, float wd, hipStream_t st) {
+  if (n <= 0) return 0;
+  dim3 grid(rows_blocks(n));
+#define SPC(M) case M: hipLaunchKernelGGL(sparse_opt_k<M>, grid, dim3(256), 0, st, table, s1, s2, ids, g, n, dim, nrows, lr, l2, mu, b1, b2, b1t, b2t, eps, wd); break;
+  switch (mode) {
+    SPC(SP_SGD) SPC(SP_MOMENTUM) SPC(SP_NESTEROV) SPC(SP_ADAGRAD) SPC(SP_ADAM) SPC(SP_ADAMW)
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef SPC
+  HETU_LAUNCH_CHECK();
+  return 0;
+}

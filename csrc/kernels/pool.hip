@@ -1,0 +1,292 @@
+// Pooling and axis reductions for channels-last tensors on gfx950.
+//
+// Replaces MaxPool.cu / AvgPool.cu / CudnnMaxPool.cu / CudnnAvgPool.cu (NCHW,
+// one thread per output, backward with atomics) and ReduceSumAxisZero.cu /
+// ReduceSum.cu / Conv2dReduceSum.cu (per-call cudaMalloc + H2D metadata).
+//   * max-pool fwd stores the winning tap (uint8) so the backward is a
+//     deterministic GATHER: each input element sums the <= ceil(k/s)^2 windows
+//     that selected it -- no atomics.
+//   * avg-pool fwd/bwd likewise gather-based.
+//   * reduce_mid: y[b, c] = scale * sum_r x[b, r, c] covers bias gradients
+//     (B = 1), global average pooling (R = H*W) and reduce-over-axis-0; long R is
+//     split across workgroups with fp32 partial slabs and a second pass.
+#include "common.h"
+
+namespace hetu {
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y,
+                                                      uint8_t* __restrict__ idx, int N, int H, int W,
+                                                      int C, int Ho, int Wo, int kh, int kw, int sh,
+                                                      int sw, int ph, int pw) {
+  const int64_t total = (int64_t)N * Ho * Wo * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int wo = (int)(t % Wo); t /= Wo;
+    int ho = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int a = 0; a < kh; ++a) {
+      int h = ho * sh - ph + a;
+      if (h < 0 || h >= H) continue;
+      for (int b = 0; b < kw; ++b) {
+        int w = wo * sw - pw + b;
+        if (w < 0 || w >= W) continue;
+        float v = to_f(x[(((int64_t)n * H + h) * W + w) * C + c]);
+        if (v > best) { best = v; bi = a * kw + b; }
+      }
+    }
+    y[i] = from_f<T>(best);
+    if (idx) idx[i] = (uint8_t)bi;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                      T* __restrict__ dx, int N, int H, int W, int C,
+                                                      int Ho, int Wo, int kh, int kw, int sh, int sw,
+                                                      int ph, int pw) {
+  const int64_t total = (int64_t)N * H * W * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int w = (int)(t % W); t /= W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    int ho0 = (h + ph - kh + sh) / sh; if (h + ph - kh + 1 < 0) ho0 = 0;
+    int ho1 = (h + ph) / sh; if (ho1 >= Ho) ho1 = Ho - 1;
+    int wo0 = (w + pw - kw + sw) / sw; if (w + pw - kw + 1 < 0) wo0 = 0;
+    int wo1 = (w + pw) / sw; if (wo1 >= Wo) wo1 = Wo - 1;
+    float acc = 0.f;
+    for (int ho = ho0; ho <= ho1; ++ho) {
+      int a = h + ph - ho * sh;
+      if (a < 0 || a >= kh) continue;
+      for (int wo = wo0; wo <= wo1; ++wo) {
+        int b = w + pw - wo * sw;
+        if (b < 0 || b >= kw) continue;
+        int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C + c;
+        if (idx[o] == (uint8_t)(a * kw + b)) acc += to_f(dy[o]);
+      }
+    }
+    dx[i] = from_f<T>(acc);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N,
+                                                      int H, int W, int C, int Ho, int Wo, int kh,
+                                                      int kw, int sh, int sw, int ph, int pw) {
+  const int64_t total = (int64_t)N * Ho * Wo * C;
+  const float inv = 1.f / (float)(kh * kw);  // count_include_pad semantics (cuDNN default)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int wo = (int)(t % Wo); t /= Wo;
+    int ho = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    float s = 0.f;
+    for (int a = 0; a < kh; ++a) {
+      int h = ho * sh - ph + a;
+      if (h < 0 || h >= H) continue;
+      for (int b = 0; b < kw; ++b) {
+        int w = wo * sw - pw + b;
+        if (w < 0 || w >= W) continue;
+        s += to_f(x[(((int64_t)n * H + h) * W + w) * C + c]);
+      }
+    }
+    y[i] = from_f<T>(s * inv);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) avgpool_bwd_k(const T* __restrict__ dy, T* __restrict__ dx, int N,
+                                                      int H, int W, int C, int Ho, int Wo, int kh,
+                                                      int kw, int sh, int sw, int ph, int pw) {
+  const int64_t total = (int64_t)N * H * W * C;
+  const float inv = 1.f / (float)(kh * kw);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int w = (int)(t % W); t /= W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    int ho0 = (h + ph - kh + sh) / sh; if (h + ph - kh + 1 < 0) ho0 = 0;
+    int ho1 = (h + ph) / sh; if (ho1 >= Ho) ho1 = Ho - 1;
+    int wo0 = (w + pw - kw + sw) / sw; if (w + pw - kw + 1 < 0) wo0 = 0;
+    int wo1 = (w + pw) / sw; if (wo1 >= Wo) wo1 = Wo - 1;
+    float acc = 0.f;
+    for (int ho = ho0; ho <= ho1; ++ho) {
+      int a = h + ph - ho * sh;
+      if (a < 0 || a >= kh) continue;
+      for (int wo = wo0; wo <= wo1; ++wo) {
+        int b = w + pw - wo * sw;
+        if (b < 0 || b >= kw) continue;
+        acc += to_f(dy[(((int64_t)n * Ho + ho) * Wo + wo) * C + c]);
+      }
+    }
+    dx[i] = from_f<T>(acc * inv);
+  }
+}
+
+// y[b, c] = scale * sum_{r in chunk} x[b, r, c]; partial (fp32) when chunks > 1
+template <typename T>
+__global__ void __launch_bounds__(256) reduce_mid_k(const T* __restrict__ x, float* __restrict__ part,
+                                                     int64_t B, int64_t R, int64_t C,
+                                                     int64_t rows_per_chunk) {
+  const int64_t c = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rsub = threadIdx.x >> 6;  // 4 row lanes
+  const int64_t b = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.z * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > R) r1 = R;
+  __shared__ float sh[256];
+  float s = 0.f;
+  if (c < C)
+    for (int64_t r = r0 + rsub; r < r1; r += 4) s += to_f(x[(b * R + r) * C + c]);
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  if (rsub == 0 && c < C) {
+    s = sh[threadIdx.x] + sh[threadIdx.x + 64] + sh[threadIdx.x + 128] + sh[threadIdx.x + 192];
+    part[((int64_t)blockIdx.z * B + b) * C + c] = s;
+  }
+}
+
+template <typename TO>
+__global__ void reduce_mid_final_k(const float* __restrict__ part, TO* __restrict__ y, int64_t BC,
+                                   int chunks, float scale) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < BC;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * BC + i];
+    y[i] = from_f<TO>(s * scale);
+  }
+}
+
+// y[r] = scale * sum_c x[r, c]  (one wave per row)
+template <typename T, typename TO>
+__global__ void __launch_bounds__(256) reduce_last_k(const T* __restrict__ x, TO* __restrict__ y, int64_t R,
+                                                      int64_t C, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  float s = 0.f;
+  for (int64_t j = lane; j < C; j += 64) s += to_f(x[row * C + j]);
+  s = wave_sum(s);
+  if (lane == 0) y[row] = from_f<TO>(s * scale);
+}
+
+// broadcast y[b, r, c] = scale * x[b, c] (global-avg-pool backward)
+template <typename T>
+__global__ void bcast_mid_k(const T* __restrict__ x, T* __restrict__ y, int64_t B, int64_t R,
+                            int64_t C, float scale) {
+  const int64_t total = B * R * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t c = i % C, b = i / (R * C);
+    y[i] = from_f<T>(to_f(x[b * C + c]) * scale);
+  }
+}
+
+}  // namespace hetu
+
+using namespace hetu;
+
+HETU_API int hetu_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H, int W, int C,
+                              int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw,
+                              int is_bf16, hipStream_t st) {
+  int64_t total = (int64_t)N * Ho * Wo * C;
+  int grid = stream_grid(total, 256, 2);
+  if (is_bf16) hipLaunchKernelGGL(maxpool_fwd_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, idx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  else hipLaunchKernelGGL(maxpool_fwd_k<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, idx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int N, int H, int W,
+                              int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph,
+                              int pw, int is_bf16, hipStream_t st) {
+  int64_t total = (int64_t)N * H * W * C;
+  int grid = stream_grid(total, 256, 2);
+  if (is_bf16) hipLaunchKernelGGL(maxpool_bwd_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)dy, idx, (bf16*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  else hipLaunchKernelGGL(maxpool_bwd_k<float>, dim3(grid), dim3(256), 0, st, (const float*)dy, idx, (float*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo,
+                              int kh, int kw, int sh, int sw, int ph, int pw, int is_bf16,
+                              hipStream_t st) {
+  int64_t total = (int64_t)N * Ho * Wo * C;
+  int grid = stream_grid(total, 256, 2);
+  if (is_bf16) hipLaunchKernelGGL(avgpool_fwd_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  else hipLaunchKernelGGL(avgpool_fwd_k<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int C, int Ho, int Wo,
+                              int kh, int kw, int sh, int sw, int ph, int pw, int is_bf16,
+                              hipStream_t st) {
+  int64_t total = (int64_t)N * H * W * C;
+  int grid = stream_grid(total, 256, 2);
+  if (is_bf16) hipLaunchKernelGGL(avgpool_bwd_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)dy, (bf16*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  else hipLaunchKernelGGL(avgpool_bwd_k<float>, dim3(grid), dim3(256), 0, st, (const float*)dy, (float*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+// workspace: chunks * B * C floats; returns needed floats when ws == null
+HETU_API int64_t hetu_reduce_mid_ws(int64_t B, int64_t R, int64_t C) {
+  int64_t ctiles = (C + 63) / 64;
+  int64_t blocks = ctiles * B;
+  int64_t chunks = blocks >= 1024 ? 1 : (1024 + blocks - 1) / blocks;
+  int64_t maxc = (R + 63) / 64;
+  if (chunks > maxc) chunks = maxc;
+  if (chunks < 1) chunks = 1;
+  return chunks * B * C;
+}
+
+HETU_API int hetu_reduce_mid(const void* x, void* y, int64_t B, int64_t R, int64_t C, float scale,
+                             int x_bf16, int y_bf16, float* ws, hipStream_t st) {
+  int64_t ctiles = (C + 63) / 64;
+  int64_t blocks = ctiles * B;
+  int64_t chunks = blocks >= 1024 ? 1 : (1024 + blocks - 1) / blocks;
+  int64_t maxc = (R + 63) / 64;
+  if (chunks > maxc) chunks = maxc;
+  if (chunks < 1) chunks = 1;
+  int64_t rpc = (R + chunks - 1) / chunks;
+  dim3 grid((unsigned)ctiles, (unsigned)B, (unsigned)chunks);
+  if (x_bf16) hipLaunchKernelGGL(reduce_mid_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ws, B, R, C, rpc);
+  else hipLaunchKernelGGL(reduce_mid_k<float>, grid, dim3(256), 0, st, (const float*)x, ws, B, R, C, rpc);
+  int g2 = stream_grid(B * C, 256, 1);
+  if (y_bf16) hipLaunchKernelGGL(reduce_mid_final_k<bf16>, dim3(g2), dim3(256), 0, st, ws, (bf16*)y, B * C, (int)chunks, scale);
+  else hipLaunchKernelGGL(reduce_mid_final_k<float>, dim3(g2), dim3(256), 0, st, ws, (float*)y, B * C, (int)chunks, scale);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_reduce_last(const void* x, void* y, int64_t R, int64_t C, float scale, int x_bf16,
+                              int y_bf16, hipStream_t st) {
+  dim3 grid((unsigned)((R + 3) / 4));
+  if (x_bf16 && y_bf16) hipLaunchKernelGGL((reduce_last_k<bf16, bf16>), grid, dim3(256), 0, st, (const bf16*)x, (bf16*)y, R, C, scale);
+  else if (x_bf16) hipLaunchKernelGGL((reduce_last_k<bf16, float>), grid, dim3(256), 0, st, (const bf16*)x, (float*)y, R, C, scale);
+  else if (y_bf16) hipLaunchKernelGGL((reduce_last_k<float, bf16>), grid, dim3(256), 0, st, (const float*)x, (bf16*)y, R, C, scale);
+  else hipLaunchKernelGGL((reduce_last_k<float, float>), grid, dim3(256), 0, st, (const float*)x, (float*)y, R, C, scale);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_bcast_mid(const void* x, void* y, int64_t B, int64_t R, int64_t C, float scale,
+                            int is_bf16, hipStream_t st) {
+  int grid = stream_grid(B * R * C, 256, 2);
+  if (is_bf16) hipLaunchKernelGGL(bcast_mid_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, B, R, C, scale);
+  else hipLaunchKernelGGL(bcast_mid_k<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, B, R, C, scale);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}

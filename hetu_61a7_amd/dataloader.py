@@ -1,0 +1,232 @@
+"""Dataloaders (reference ``python/hetu/dataloader.py:11-257``).
+
+A ``Dataloader`` owns one split of host data; ``dataloader_op([...])`` is the
+graph source that yields the batch for the split being run.  Batches are
+staged in a ring of pinned host buffers and copied to HBM with
+``hipMemcpyAsync`` on a side stream one step ahead (prefetch depth 2), the
+consumer stream waits on an event.  Under data parallelism each rank reads its
+own shard (the reference's ``set_dp_rank`` hook is never called, SURVEY §0.2;
+here the executor calls it).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .ops.node import Op
+from . import ndarray
+
+
+class Dataloader(object):
+    def __init__(self, raw_data, batch_size, name='default', func=None, drop_last=True,
+                 shuffle=False, dtype=None):
+        self.func = func if func else (lambda x: x)
+        data = self.func(raw_data)
+        if isinstance(data, torch.Tensor):
+            data = data.numpy()
+        data = np.asarray(data)
+        if dtype is not None:
+            data = data.astype(dtype)
+        elif data.dtype == np.float64:
+            data = data.astype(np.float32)
+        self.raw_data = data
+        self.batch_size = batch_size
+        self.drop_last = drop_last
+        self.shuffle = shuffle
+        self.name = str(name)
+        self.dp_rank, self.dp_nrank = 0, None
+        self.parts = None
+        self.cur_part = None
+        self.slices = None
+        self.initialized = False
+        self.device = None
+        self._stream = None
+
+    def set_dp_rank(self, dp_rank, dp_nrank):
+        self.dp_rank, self.dp_nrank = dp_rank, dp_nrank
+
+    def set_mp_parts(self, cur_part, parts):
+        self.cur_part, self.parts = cur_part, parts
+
+    def init_states(self, device=None):
+        if self.initialized:
+            return
+        data = self.raw_data
+        if self.dp_nrank is not None and self.dp_nrank > 1:
+            cur = data.shape[0] // self.dp_nrank
+            data = data[cur * self.dp_rank: cur * (self.dp_rank + 1)]
+        self.data = data
+        self.samples_num = len(data)
+        if self.drop_last:
+            self.batch_num = self.samples_num // self.batch_size
+        else:
+            self.batch_num = (self.samples_num + self.batch_size - 1) // self.batch_size
+        self.batch_num = max(self.batch_num, 1)
+        self.shape = (self.batch_size,) + tuple(data.shape[1:])
+        self.set_slices()
+        self.device = device
+        self.batch_index = 0
+        self.order = np.arange(self.samples_num)
+        self._ring = []
+        self._pending = None
+        if device is not None and device.type == 'cuda':
+            self._stream = torch.cuda.Stream(device=device)
+        self.initialized = True
+
+    def set_slices(self):
+        if self.parts is None:
+            return
+        new_shape, slcs = [], []
+        for i, d in enumerate(self.shape):
+            if i in self.parts:
+                part = d // self.parts[i]
+                st = part * self.cur_part[i]
+                en = st + part
+            else:
+                st, en = 0, d
+            slcs.append(slice(st, en))
+            new_shape.append(en - st)
+        self.slices = tuple(slcs)
+        self.shape = tuple(new_shape)
+
+    def reshape_tensor(self, tensor):
+        return tensor if self.slices is None else tensor[self.slices]
+
+    def _host_batch(self, idx):
+        if idx == 0 and self.shuffle:
+            np.random.shuffle(self.order)
+        st = idx * self.batch_size
+        en = min(st + self.batch_size, self.samples_num)
+        sel = self.order[st:en] if self.shuffle else slice(st, en)
+        b = self.data[sel]
+        if self.slices is not None:
+            b = b[(slice(None),) + self.slices[1:]]
+        return np.ascontiguousarray(b)
+
+    def _stage(self, idx):
+        b = torch.from_numpy(self._host_batch(idx))
+        if self.device is None or self.device.type != 'cuda':
+            return (b, None)
+        hb = b.pin_memory()
+        with torch.cuda.stream(self._stream):
+            db = hb.to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        return (db, ev, hb)
+
+    def get_arr(self):
+        """Current batch on the device; prefetches the next one."""
+        if self._pending is None:
+            self._pending = self._stage(self.batch_index)
+        cur = self._pending
+        nxt = (self.batch_index + 1) % self.batch_num
+        self._pending = self._stage(nxt)
+        self.batch_index = nxt
+        t = cur[0]
+        if len(cur) > 1 and cur[1] is not None:
+            torch.cuda.current_stream().wait_event(cur[1])
+            t.record_stream(torch.cuda.current_stream())
+        return t
+
+    def get_next_arr(self):
+        return self.get_arr()
+
+    def get_cur_shape(self):
+        return self.shape
+
+
+class DataloaderOp(Op):
+    def __init__(self, dataloaders):
+        super().__init__(DataloaderOp, [], ndarray.cpu(0))
+        self.dataloaders = {dl.name: dl for dl in dataloaders}
+        self.name = 'DataloaderOp%d(%s)' % (self.id, '_'.join(self.dataloaders.keys()))
+        self.keep_fp32 = False
+
+    @property
+    def desc(self):
+        return self.name
+
+    def set_dp_rank(self, dp_rank, dp_nrank):
+        for d in self.dataloaders.values():
+            d.set_dp_rank(dp_rank, dp_nrank)
+
+    def set_mp_parts(self, cur_part, parts):
+        for d in self.dataloaders.values():
+            d.set_mp_parts(cur_part, parts)
+
+    def get_batch_num(self, name):
+        dl = self.dataloaders.get(name)
+        if dl is None:
+            return None
+        if not dl.initialized:
+            dl.init_states(None)
+        return dl.batch_num
+
+    def get_arr(self, name, config=None):
+        dl = self.dataloaders[name]
+        if not dl.initialized:
+            dl.init_states(config.device if config is not None else None)
+        t = dl.get_arr()
+        if config is not None and config.mixed_precision and t.is_cuda and t.dtype == torch.float32 \
+                and not self.keep_fp32:
+            t = t.to(torch.bfloat16)
+        return t
+
+    def get_next_arr(self, name):
+        return self.get_arr(name)
+
+    def get_cur_shape(self, name):
+        return self.dataloaders[name].get_cur_shape()
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        raise AssertionError('dataloader values are provided by the executor')
+
+    def gradient(self, output_grad):
+        return None
+
+    def infer_shape(self, input_shapes):
+        raise NotImplementedError
+
+    def forward_hook(self, config):
+        self.ctx = config.context
+        self.on_gpu = ndarray.is_gpu_ctx(self.ctx)
+        self.on_cpu = not self.on_gpu
+
+    def backward_hook(self, config):
+        if config.comm_mode in ('AllReduce', 'Hybrid', 'PS') and config.nrank > 1:
+            self.set_dp_rank(config.rank, config.nrank)
+        for d in self.dataloaders.values():
+            if d.initialized:
+                continue
+            d.init_states(config.device)
+
+
+def dataloader_op(dataloaders):
+    return DataloaderOp(dataloaders)
+
+
+class GNNDataLoaderOp(Op):
+    """Graph-sampling source (GraphMix hook in the reference; GraphMix itself is
+    not shipped).  Feeds batches produced by a user ``handler``."""
+
+    graph = None
+
+    def __init__(self, handler, ctx=None):
+        super().__init__(GNNDataLoaderOp, [], ctx or ndarray.cpu(0))
+        self.handler = handler
+
+    def get_batch_num(self, name):
+        return None
+
+    def get_arr(self, name, config=None):
+        return self.handler(GNNDataLoaderOp.graph)
+
+    def gradient(self, output_grad):
+        return None
+
+    def infer_shape(self, input_shapes):
+        raise NotImplementedError
+
+    @classmethod
+    def step(cls, graph):
+        cls.graph = graph

@@ -1,0 +1,68 @@
+"""Forward-graph fusion pass, run by ``Optimizer.minimize`` before autodiff.
+
+Rewrites (in place, preserving the identity of the user-visible output node):
+  relu(batch_norm(x))             -> fused BN+ReLU          (one pass fwd, one bwd)
+  relu(batch_norm(x) + r)         -> fused BN+add+ReLU      (ResNet block tail)
+  relu(r + batch_norm(x))         -> fused BN+add+ReLU
+These are the memory-bound op chains that dominate ResNet time outside the
+convolutions; the reference runs each as its own cuDNN/elementwise call.
+Only applied when the intermediate values have no other consumer.
+"""
+from __future__ import annotations
+
+import os
+
+from .ops.node import Op
+
+
+def _consumers(roots):
+    from .ops.executor import find_topo_sort
+    topo = find_topo_sort(roots)
+    cons = {n: [] for n in topo}
+    for n in topo:
+        for i in n.inputs:
+            cons.setdefault(i, []).append(n)
+    return topo, cons
+
+
+def fuse_forward(roots):
+    if os.environ.get('HETU_FUSE', '1') == '0':
+        return 0
+    from .ops.basic import ReluOp, AddOp
+    from .ops.nn import Batch_NormalizationOp
+    topo, cons = _consumers(roots)
+    root_set = set(roots)
+    fused = 0
+    for n in topo:
+        if not isinstance(n, ReluOp) or n in root_set:
+            continue
+        src = n.inputs[0]
+        if isinstance(src, Batch_NormalizationOp) and not src.relu and not src.has_residual \
+                and len(cons.get(src, [])) == 1 and src not in root_set:
+            _become_bn(n, src, relu=True, residual=None)
+            fused += 1
+        elif isinstance(src, AddOp) and len(cons.get(src, [])) == 1 and src not in root_set:
+            a, b = src.inputs
+            for bn, res in ((a, b), (b, a)):
+                if isinstance(bn, Batch_NormalizationOp) and not bn.relu and not bn.has_residual \
+                        and len(cons.get(bn, [])) == 1 and bn not in root_set and bn is not res:
+                    _become_bn(n, bn, relu=True, residual=res)
+                    fused += 1
+                    break
+    return fused
+
+
+def _become_bn(node, bn, relu, residual):
+    """Turn ``node`` (a ReluOp) into a fused BN op with bn's inputs/attributes."""
+    from .ops.nn import Batch_NormalizationOp
+    keep_id, keep_name = node.id, node.name
+    node.__class__ = Batch_NormalizationOp
+    node.__dict__.update({k: v for k, v in bn.__dict__.items() if k not in ('id', 'name', 'inputs')})
+    node.inputs = list(bn.inputs[:3]) + ([residual] if residual is not None else [])
+    node.relu = relu
+    node.has_residual = residual is not None
+    node.op_type = 'Batch_NormalizationOp'
+    node.id, node.name = keep_id, keep_name
+    node.running_mean = bn.running_mean
+    node.running_var = bn.running_var
+    node.fused_from = bn

@@ -1,0 +1,79 @@
+"""Python bindings of the hand-written HIP kernels (reference ``gpu_links/*``).
+
+Every function takes/returns torch tensors.  On a ROCm device the HIP kernel
+from ``libhetu_kernels.so`` runs on the *current* HIP stream (so the executor's
+stream routing and hipGraph capture apply); on CPU the same math runs through a
+plain torch reference implementation (the CPU backend, used by the CPU configs
+and as the numerics oracle in tests).
+
+On a GPU the native path is mandatory: if the library is missing the call
+raises instead of silently falling back (``HETU_NATIVE=0`` disables it
+explicitly, for A/B measurements only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from .._base import kernels_lib, has_kernels
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+F32 = ctypes.c_float
+
+_NATIVE_DISABLED = os.environ.get('HETU_NATIVE', '1') == '0'
+_cache = {}
+
+
+def fn(name, argtypes, restype=ctypes.c_int):
+    f = _cache.get(name)
+    if f is None:
+        lib = kernels_lib()
+        f = getattr(lib, name)
+        f.argtypes = argtypes
+        f.restype = restype
+        _cache[name] = f
+    return f
+
+
+def native(*tensors) -> bool:
+    """True when the HIP path must be used for these tensors."""
+    for t in tensors:
+        if isinstance(t, torch.Tensor):
+            if not t.is_cuda:
+                return False
+            if _NATIVE_DISABLED:
+                return False
+            return True
+    return False
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def is_bf16(t) -> int:
+    return 1 if t.dtype == torch.bfloat16 else 0
+
+
+def check(ret, name=''):
+    if ret != 0:
+        raise RuntimeError('HIP kernel %s failed with hipError %d' % (name, ret))
+
+
+def supported_float(t) -> bool:
+    return t.dtype in (torch.float32, torch.bfloat16)
+
+
+def available() -> bool:
+    return has_kernels()
+
+
+from . import elementwise, norm, softmax, optim, pool, sparse, reduce  # noqa: E402,F401

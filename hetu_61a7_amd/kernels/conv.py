@@ -1,0 +1,80 @@
+"""2-D convolution (logical NCHW, physical channels-last on the GPU).
+
+The forward/backward-data/backward-filter entry points dispatch per shape to
+the hand-written implicit-GEMM MFMA kernel (``conv.hip``) when it has been
+selected for that shape, otherwise to the vendor convolution (MIOpen) through
+torch.  Selection is by measurement (``conv_autotune``) -- a kernel is only
+used where it is at least as fast.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+CL = torch.channels_last
+_USE_IGEMM = os.environ.get('HETU_CONV', 'auto')
+
+
+def _match(x, w):
+    if x.dtype != w.dtype:
+        if w.dtype == torch.bfloat16 or x.dtype == torch.bfloat16:
+            x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
+        else:
+            w = w.to(x.dtype)
+    return x, w
+
+
+def conv2d(x, w, b, stride, padding):
+    x, w = _match(x, w)
+    if x.is_cuda:
+        x = x.contiguous(memory_format=CL)
+        w = w.contiguous(memory_format=CL)
+        from . import conv_igemm
+        y = conv_igemm.try_forward(x, w, stride, padding)
+        if y is None:
+            y = F.conv2d(x, w, None, stride, padding)
+        if b is not None:
+            from .elementwise import binary
+            n, c, h, ww = y.shape
+            y = binary('add', y.permute(0, 2, 3, 1), b.to(y.dtype).contiguous()).permute(0, 3, 1, 2)
+        return y
+    y = F.conv2d(x, w, b.to(x.dtype) if b is not None else None, stride, padding)
+    return y
+
+
+def conv2d_backward_data(g, w, x_shape, stride, padding):
+    g, w = _match(g, w)
+    if g.is_cuda:
+        g = g.contiguous(memory_format=CL)
+        w = w.contiguous(memory_format=CL)
+        from . import conv_igemm
+        dx = conv_igemm.try_backward_data(g, w, x_shape, stride, padding)
+        if dx is not None:
+            return dx
+    xs = torch.empty(x_shape, dtype=g.dtype, device=g.device)
+    if g.is_cuda:
+        xs = xs.contiguous(memory_format=CL)
+    dx, _, _ = torch.ops.aten.convolution_backward(
+        g, xs, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [True, False, False])
+    return dx
+
+
+def conv2d_backward_filter(g, x, w_shape, stride, padding):
+    g, x = _match(g, x)
+    if g.is_cuda:
+        g = g.contiguous(memory_format=CL)
+        x = x.contiguous(memory_format=CL)
+        from . import conv_igemm
+        dw = conv_igemm.try_backward_filter(g, x, w_shape, stride, padding)
+        if dw is not None:
+            return dw
+    ws = torch.empty(w_shape, dtype=g.dtype, device=g.device)
+    if g.is_cuda:
+        ws = ws.contiguous(memory_format=CL)
+    _, dw, _ = torch.ops.aten.convolution_backward(
+        g, x, ws, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [False, True, False])
+    return dw

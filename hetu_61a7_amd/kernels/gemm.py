@@ -1,0 +1,53 @@
+"""GEMM entry points.
+
+``matmul(a, b, ta, tb, bias, activation)``: 2-D product with optional fused bias
+and ReLU/GELU epilogue.  bf16 shapes that the hand-written MFMA kernel
+(``gemm.hip``: 256x256x64 tiles, 8 waves, LDS double buffer, XCD-aware block
+remap, fused epilogue) supports run there; everything else is a plain library
+GEMM (hipBLASLt through torch) followed by the elementwise epilogue kernel.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import native
+
+_MFMA = os.environ.get('HETU_GEMM', 'auto')
+
+
+def _match(a, b):
+    if a.dtype != b.dtype:
+        if torch.bfloat16 in (a.dtype, b.dtype):
+            return a.to(torch.bfloat16), b.to(torch.bfloat16)
+        return a.to(torch.float32), b.to(torch.float32)
+    return a, b
+
+
+def _tr(t, f):
+    return t.transpose(-1, -2) if f else t
+
+
+def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
+    a, b = _match(a, b)
+    if native(a) and _MFMA != 'off':
+        from . import gemm_mfma
+        y = gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)
+        if y is not None:
+            return y
+    y = torch.matmul(_tr(a, ta), _tr(b, tb))
+    if bias is not None or activation is not None:
+        from .elementwise import binary, unary
+        if bias is not None:
+            y = binary('add', y, bias.to(y.dtype).contiguous())
+        if activation == 'relu':
+            y = unary('relu', y)
+        elif activation == 'gelu':
+            y = unary('gelu', y)
+    return y
+
+
+def bmm(a, b, ta=False, tb=False):
+    a, b = _match(a, b)
+    return torch.matmul(_tr(a, ta), _tr(b, tb))

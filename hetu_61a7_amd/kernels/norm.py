@@ -1,0 +1,135 @@
+"""BatchNorm (channels-last, fused ReLU / residual) bindings (``batchnorm.hip``)."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import fn, native, stream_ptr, is_bf16, check, P, I64, I32, F32
+
+
+def _as_rows(x):
+    """View x as [M, C] channels-last rows; returns (rows, restore_fn) or None."""
+    if x.dim() == 2:
+        if x.is_contiguous():
+            return x, x.shape
+        return None
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        n, c, h, w = x.shape
+        return x.permute(0, 2, 3, 1).reshape(n * h * w, c), x.shape
+    return None
+
+
+def _like_rows(x):
+    if x.dim() == 4:
+        return torch.empty_like(x, memory_format=torch.channels_last)
+    return torch.empty_like(x)
+
+
+def _ws(M, C, bf, device):
+    f = fn('hetu_bn_workspace_floats', [I64, I32, I32], restype=I64)
+    n = f(M, C, bf)
+    return torch.empty(n, dtype=torch.float32, device=device)
+
+
+def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
+               relu=False, residual=None):
+    """Returns (y, save_mean, save_invstd).  ``factor`` = weight of the new batch
+    statistics in the running average."""
+    C = x.shape[1]
+    if native(x) and x.dtype in (torch.float32, torch.bfloat16):
+        if x.dim() == 4 and not x.is_contiguous(memory_format=torch.channels_last):
+            x = x.contiguous(memory_format=torch.channels_last)
+        if residual is not None and residual.dim() == 4:
+            residual = residual.contiguous(memory_format=torch.channels_last)
+        rows = _as_rows(x)
+        vec = 8 if x.dtype == torch.bfloat16 else 4
+        if rows is not None and C % vec == 0:
+            xr, _ = rows
+            M = xr.shape[0]
+            y = _like_rows(x)
+            save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+            ws = _ws(M, C, is_bf16(x), x.device)
+            f = fn('hetu_bn_fwd', [P, P, P, I64, I32, I32, P, P, P, P, F32, F32, P, P, P, I32, I32, P])
+            check(f(x.data_ptr(), residual.data_ptr() if residual is not None else None, y.data_ptr(),
+                    M, C, is_bf16(x), scale.data_ptr(), bias.data_ptr(),
+                    running_mean.data_ptr() if running_mean is not None else None,
+                    running_var.data_ptr() if running_var is not None else None,
+                    float(factor), float(eps), save_mean.data_ptr(), save_invstd.data_ptr(),
+                    ws.data_ptr(), int(relu), int(training), stream_ptr()), 'bn_fwd')
+            return y, save_mean, save_invstd
+    # torch reference (CPU backend / unsupported layouts)
+    xf = x.float()
+    dims = [0] + list(range(2, x.dim()))
+    shape = [1, C] + [1] * (x.dim() - 2)
+    if training:
+        mean = xf.mean(dims)
+        var = xf.var(dims, unbiased=False)
+        if running_mean is not None:
+            n = x.numel() // C
+            unb = var * n / max(n - 1, 1)
+            running_mean.mul_(1 - factor).add_(factor * mean)
+            running_var.mul_(1 - factor).add_(factor * unb)
+    else:
+        mean, var = running_mean, running_var
+    invstd = torch.rsqrt(var + eps)
+    y = (xf - mean.view(shape)) * (invstd * scale.float()).view(shape) + bias.float().view(shape)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    y = y.to(x.dtype)
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        y = y.contiguous(memory_format=torch.channels_last)
+    return y, mean.float(), invstd.float()
+
+
+def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=False):
+    """Returns (dx, dscale, dbias, dres)."""
+    C = x.shape[1]
+    if native(x) and x.dtype in (torch.float32, torch.bfloat16):
+        cl = torch.channels_last
+        if x.dim() == 4:
+            x = x.contiguous(memory_format=cl)
+            dy = dy.contiguous(memory_format=cl)
+            if relu:
+                y = y.contiguous(memory_format=cl)
+        else:
+            dy = dy.contiguous()
+        vec = 8 if x.dtype == torch.bfloat16 else 4
+        if C % vec == 0 and dy.dtype == x.dtype:
+            M = x.numel() // C
+            dx = _like_rows(x)
+            dres = _like_rows(x) if want_dres else None
+            dscale = torch.empty(C, dtype=torch.float32, device=x.device)
+            dbias = torch.empty(C, dtype=torch.float32, device=x.device)
+            ws = _ws(M, C, is_bf16(x), x.device)
+            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, I32, P])
+            check(f(dy.data_ptr(), y.data_ptr() if relu else None, x.data_ptr(), dx.data_ptr(),
+                    dres.data_ptr() if dres is not None else None, M, C, is_bf16(x),
+                    scale.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(),
+                    dscale.data_ptr(), dbias.data_ptr(), ws.data_ptr(), int(relu), stream_ptr()),
+                  'bn_bwd')
+            return dx, dscale, dbias, dres
+    dims = [0] + list(range(2, x.dim()))
+    shape = [1, C] + [1] * (x.dim() - 2)
+    g = dy.float()
+    if relu:
+        g = torch.where(y > 0, g, torch.zeros_like(g))
+    xhat = (x.float() - save_mean.view(shape)) * save_invstd.view(shape)
+    M = x.numel() // C
+    dbias = g.sum(dims)
+    dscale = (g * xhat).sum(dims)
+    dx = (scale.float() * save_invstd).view(shape) * (g - dbias.view(shape) / M - xhat * dscale.view(shape) / M)
+    dres = g.to(x.dtype) if want_dres else None
+    dx = dx.to(x.dtype)
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        dx = dx.contiguous(memory_format=torch.channels_last)
+        if dres is not None:
+            dres = dres.contiguous(memory_format=torch.channels_last)
+    return dx, dscale, dbias, dres
+
+
+def layer_norm_ref(x, gamma, beta, eps):
+    return F.layer_norm(x.float(), x.shape[-1:], gamma.float() if gamma is not None else None,
+                        beta.float() if beta is not None else None, eps).to(x.dtype)

@@ -1,0 +1,79 @@
+"""Axis reductions (``pool.hip`` reduce_mid / reduce_last / bcast_mid)."""
+from __future__ import annotations
+
+import torch
+
+from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32, F32
+
+
+def reduce_mid(x3: torch.Tensor, scale: float = 1.0, out_dtype=None) -> torch.Tensor:
+    """x3 [B, R, C] contiguous -> [B, C] = scale * sum over R."""
+    B, R, C = x3.shape
+    out_dtype = out_dtype or x3.dtype
+    if native(x3) and supported_float(x3) and out_dtype in (torch.float32, torch.bfloat16):
+        x3 = x3.contiguous()
+        wsf = fn('hetu_reduce_mid_ws', [I64, I64, I64], restype=I64)
+        ws = torch.empty(wsf(B, R, C), dtype=torch.float32, device=x3.device)
+        y = torch.empty((B, C), dtype=out_dtype, device=x3.device)
+        f = fn('hetu_reduce_mid', [P, P, I64, I64, I64, F32, I32, I32, P, P])
+        check(f(x3.data_ptr(), y.data_ptr(), B, R, C, float(scale), is_bf16(x3),
+                1 if out_dtype == torch.bfloat16 else 0, ws.data_ptr(), stream_ptr()), 'reduce_mid')
+        return y
+    return (x3.float().sum(1) * scale).to(out_dtype)
+
+
+def reduce_last(x2: torch.Tensor, scale: float = 1.0, out_dtype=None) -> torch.Tensor:
+    R, C = x2.shape
+    out_dtype = out_dtype or x2.dtype
+    if native(x2) and supported_float(x2) and out_dtype in (torch.float32, torch.bfloat16):
+        x2 = x2.contiguous()
+        y = torch.empty((R,), dtype=out_dtype, device=x2.device)
+        f = fn('hetu_reduce_last', [P, P, I64, I64, F32, I32, I32, P])
+        check(f(x2.data_ptr(), y.data_ptr(), R, C, float(scale), is_bf16(x2),
+                1 if out_dtype == torch.bfloat16 else 0, stream_ptr()), 'reduce_last')
+        return y
+    return (x2.float().sum(1) * scale).to(out_dtype)
+
+
+def sum_to_shape(g: torch.Tensor, shape) -> torch.Tensor:
+    """Reduce a broadcast gradient back to ``shape`` (numpy broadcasting rules)."""
+    shape = tuple(shape)
+    if tuple(g.shape) == shape:
+        return g
+    nd = g.dim()
+    full = (1,) * (nd - len(shape)) + shape
+    # fast path: leading-dims reduction (bias / row-broadcast) -> reduce_mid
+    k = 0
+    while k < nd and full[k] == 1 and g.shape[k] != 1:
+        k += 1
+    if all(full[i] == g.shape[i] for i in range(k, nd)) and g.is_contiguous():
+        lead = 1
+        for i in range(k):
+            lead *= g.shape[i]
+        inner = g.numel() // max(lead, 1)
+        return reduce_mid(g.reshape(1, lead, inner)).reshape(shape)
+    dims = [i for i in range(nd) if full[i] == 1 and g.shape[i] != 1]
+    r = g.float().sum(dim=dims, keepdim=True) if dims else g.float()
+    return r.reshape(shape).to(g.dtype)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """x logical NCHW -> [N, C] mean over H*W (channels-last fast path)."""
+    N, C, H, W = x.shape
+    if native(x) and supported_float(x):
+        xc = x.contiguous(memory_format=torch.channels_last)
+        return reduce_mid(xc.permute(0, 2, 3, 1).reshape(N, H * W, C), 1.0 / (H * W))
+    return x.float().mean((2, 3)).to(x.dtype)
+
+
+def global_avg_pool_backward(dy: torch.Tensor, x_shape) -> torch.Tensor:
+    N, C, H, W = x_shape
+    if native(dy) and supported_float(dy):
+        dy = dy.contiguous()
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device,
+                         memory_format=torch.channels_last)
+        f = fn('hetu_bcast_mid', [P, P, I64, I64, I64, F32, I32, P])
+        check(f(dy.data_ptr(), dx.data_ptr(), N, H * W, C, 1.0 / (H * W), is_bf16(dy),
+                stream_ptr()), 'bcast_mid')
+        return dx
+    return (dy.reshape(N, C, 1, 1).float() / (H * W)).expand(N, C, H, W).to(dy.dtype).contiguous()

@@ -1,0 +1,49 @@
+"""Embedding gather / row scatter-add / dedup (``embedding.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32
+
+
+def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """out[..., :] = table[ids[...], :]; out-of-range ids give zero rows."""
+    dim = table.shape[-1]
+    idx = ids.reshape(-1).long()
+    out_shape = tuple(ids.shape) + (dim,)
+    if native(table) and supported_float(table) and table.is_contiguous():
+        idx = idx.contiguous()
+        out = torch.empty(out_shape, dtype=table.dtype, device=table.device)
+        f = fn('hetu_gather_rows', [P, P, P, I64, I64, I64, I32, P])
+        check(f(table.data_ptr(), idx.data_ptr(), out.data_ptr(), idx.numel(), dim,
+                table.shape[0], is_bf16(table), stream_ptr()), 'gather_rows')
+        return out
+    valid = (idx >= 0) & (idx < table.shape[0])
+    safe = torch.where(valid, idx, torch.zeros_like(idx))
+    out = table[safe] * valid.unsqueeze(1).to(table.dtype)
+    return out.reshape(out_shape)
+
+
+def scatter_add_rows(dst: torch.Tensor, ids: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """dst[ids[r], :] += src[r, :] (fp32 dst)."""
+    dim = dst.shape[-1]
+    idx = ids.reshape(-1).long()
+    src2 = src.reshape(-1, dim)
+    if native(dst) and dst.dtype == torch.float32 and supported_float(src2) and dst.is_contiguous():
+        idx = idx.contiguous()
+        src2 = src2.contiguous()
+        f = fn('hetu_scatter_add_rows', [P, P, P, I64, I64, I64, I32, P])
+        check(f(dst.data_ptr(), idx.data_ptr(), src2.data_ptr(), idx.numel(), dim, dst.shape[0],
+                is_bf16(src2), stream_ptr()), 'scatter_add_rows')
+        return dst
+    valid = (idx >= 0) & (idx < dst.shape[0])
+    dst.index_add_(0, idx[valid], src2[valid].to(dst.dtype))
+    return dst
+
+
+def dedup_rows(idx: torch.Tensor, vals: torch.Tensor):
+    """Unique ids and the per-unique-id sum of their rows (fp32)."""
+    uniq, inv = torch.unique(idx, sorted=True, return_inverse=True)
+    merged = torch.zeros((uniq.numel(), vals.shape[-1]), dtype=torch.float32, device=vals.device)
+    scatter_add_rows(merged, inv, vals)
+    return uniq, merged

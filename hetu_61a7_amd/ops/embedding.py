@@ -1,0 +1,65 @@
+"""Embedding lookup with row-sparse gradients (reference EmbeddingLookUp.py:11-149).
+
+Forward: wave-per-row vectorised HIP gather.  Backward: an ``IndexedSlices``
+(ids, grad rows) that the optimizer applies as a row-sparse update after a
+device-side de-duplication -- the dense table gradient is never materialised.
+When the table is PS/HET-cache managed the lookup is served by the PS op
+(``ops.ps``) instead.
+"""
+from __future__ import annotations
+
+import torch
+
+from .node import Op
+from .. import ndarray
+from ..kernels import sparse as KS
+
+
+class EmbeddingLookUp(Op):
+    def __init__(self, embedding, index, ctx=None):
+        super().__init__(EmbeddingLookUp, [embedding, index], ctx)
+        embedding.is_embed = True
+        self.grad_node = None
+        self.out_dtype = None  # set to bf16 under mixed precision
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        table, idx = input_vals
+        out = KS.gather_rows(table, idx)
+        if self.out_dtype is not None and out.dtype != self.out_dtype:
+            from ..kernels.elementwise import cast
+            out = cast(out, self.out_dtype)
+        return out
+
+    def gradient(self, output_grad):
+        self.grad_node = embedding_lookup_gradient_op(output_grad, self.inputs[1], self.inputs[0], ctx=self.raw_ctx)
+        return [self.grad_node, None]
+
+    def infer_shape(self, input_shapes):
+        return tuple(input_shapes[1]) + (input_shapes[0][-1],)
+
+
+class EmbeddingLookUp_Gradient(Op):
+    shape_only_inputs = (2,)
+
+    def __init__(self, vectors, index, embed_ref, ctx=None):
+        super().__init__(EmbeddingLookUp_Gradient, [vectors, index, embed_ref], ctx)
+        self.use_indexed_slices = True
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, idx, shape = input_vals
+        width = tuple(shape)[-1]
+        return ndarray.IndexedSlices(idx.reshape(-1), g.reshape(-1, width), tuple(shape))
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[2]
+
+
+def embedding_lookup_op(embedding, index, ctx=None):
+    return EmbeddingLookUp(embedding, index, ctx=ctx)
+
+
+def embedding_lookup_gradient_op(vectors, index, embed_shape, ctx=None):
+    return EmbeddingLookUp_Gradient(vectors, index, embed_shape, ctx=ctx)

@@ -1,0 +1,242 @@
+"""Matrix products (reference MatrixMult.py, Linear.py, Addmm.py, Baddbmm.py,
+BatchMatrixMult.py, CuSparse.py; SURVEY §2.4 "Linear algebra").
+
+``matmul``/``linear`` run on the hand-written bf16 MFMA GEMM (``gemm.hip``,
+fused bias/activation epilogue) where it has been selected for the shape, and
+on hipBLASLt otherwise (plain library GEMM).  Mixed precision: when either
+operand is bf16 both are computed in bf16 with fp32 accumulation.
+"""
+from __future__ import annotations
+
+import torch
+
+from .node import Op
+from ..kernels import gemm as KG
+
+
+def _tr(t, flag):
+    return t.transpose(-1, -2) if flag else t
+
+
+class MatMulOp(Op):
+    def __init__(self, a, b, trans_A=False, trans_B=False, ctx=None):
+        super().__init__(MatMulOp, [a, b], ctx)
+        self.matmul_attr_trans_A, self.matmul_attr_trans_B = trans_A, trans_B
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        a, b = input_vals
+        return KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B)
+
+    def gradient(self, output_grad):
+        ta, tb = self.matmul_attr_trans_A, self.matmul_attr_trans_B
+        A, B, G = self.inputs[0], self.inputs[1], output_grad
+        c = self.raw_ctx
+        if not ta and not tb:
+            return [matmul_op(G, B, False, True, ctx=c), matmul_op(A, G, True, False, ctx=c)]
+        if ta and not tb:
+            return [matmul_op(B, G, False, True, ctx=c), matmul_op(A, G, False, False, ctx=c)]
+        if not ta and tb:
+            return [matmul_op(G, B, False, False, ctx=c), matmul_op(G, A, True, False, ctx=c)]
+        return [matmul_op(B, G, True, True, ctx=c), matmul_op(G, A, True, True, ctx=c)]
+
+    def infer_shape(self, input_shapes):
+        a, b = input_shapes
+        m = a[1] if self.matmul_attr_trans_A else a[0]
+        n = b[0] if self.matmul_attr_trans_B else b[1]
+        return (m, n)
+
+
+def matmul_op(node_A, node_B, trans_A=False, trans_B=False, ctx=None):
+    return MatMulOp(node_A, node_B, trans_A, trans_B, ctx=ctx)
+
+
+class LinearOp(Op):
+    """A @ B + bias with the bias (and optional activation) fused in the GEMM
+    epilogue."""
+
+    def __init__(self, a, b, bias, trans_A=False, trans_B=False, activation=None, ctx=None):
+        super().__init__(LinearOp, [a, b, bias], ctx)
+        self.matmul_attr_trans_A, self.matmul_attr_trans_B = trans_A, trans_B
+        self.activation = activation
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        a, b, bias = input_vals
+        return KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias=bias,
+                         activation=self.activation)
+
+    def gradient(self, output_grad):
+        from .reduce import reducesumaxiszero_op
+        from .basic import relu_gradient_op, gelu_gradient_op
+        G = output_grad
+        if self.activation == 'relu':
+            G = relu_gradient_op(self, output_grad, ctx=self.raw_ctx)
+        elif self.activation == 'gelu':
+            pre = LinearOp(self.inputs[0], self.inputs[1], self.inputs[2], self.matmul_attr_trans_A,
+                           self.matmul_attr_trans_B, None, ctx=self.raw_ctx)
+            G = gelu_gradient_op(pre, output_grad, ctx=self.raw_ctx)
+        mm = MatMulOp(self.inputs[0], self.inputs[1], self.matmul_attr_trans_A, self.matmul_attr_trans_B)
+        ga, gb = mm.gradient(G)
+        return [ga, gb, reducesumaxiszero_op(G, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return MatMulOp.infer_shape(self, input_shapes[:2])
+
+
+def linear_op(node_A, node_B, bias, trans_A=False, trans_B=False, activation=None, ctx=None):
+    return LinearOp(node_A, node_B, bias, trans_A, trans_B, activation, ctx=ctx)
+
+
+class AddmmOp(Op):
+    """beta * input + alpha * (A @ B)."""
+
+    def __init__(self, inp, a, b, alpha=1.0, beta=1.0, ctx=None):
+        super().__init__(AddmmOp, [inp, a, b], ctx)
+        self.alpha, self.beta = alpha, beta
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        c, a, b = input_vals
+        r = KG.matmul(a, b, False, False)
+        if self.alpha != 1.0:
+            r = r * self.alpha
+        return r + (c.to(r.dtype) * self.beta if self.beta != 1.0 else c.to(r.dtype))
+
+    def gradient(self, output_grad):
+        from .basic import mul_byconst_op
+        c = self.raw_ctx
+        ga = matmul_op(output_grad, self.inputs[2], False, True, ctx=c)
+        gb = matmul_op(self.inputs[1], output_grad, True, False, ctx=c)
+        if self.alpha != 1.0:
+            ga, gb = mul_byconst_op(ga, self.alpha, ctx=c), mul_byconst_op(gb, self.alpha, ctx=c)
+        return [addmm_gradient_op(self.inputs[0], output_grad, self.beta, ctx=c), ga, gb]
+
+    def infer_shape(self, input_shapes):
+        return (input_shapes[1][0], input_shapes[2][1])
+
+
+class AddmmGradientOp(Op):
+    shape_only_inputs = (0,)
+
+    def __init__(self, inp, grad, beta=1.0, ctx=None):
+        super().__init__(AddmmGradientOp, [inp, grad], ctx)
+        self.beta = beta
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels.reduce import sum_to_shape
+        shape, g = input_vals
+        r = sum_to_shape(g, tuple(shape))
+        return r * self.beta if self.beta != 1.0 else r
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+def addmm_op(node_A, node_B, node_C, alpha=1.0, beta=1.0, ctx=None):
+    return AddmmOp(node_A, node_B, node_C, alpha, beta, ctx=ctx)
+
+
+def addmm_gradient_op(node_input, node_grad, beta=1.0, ctx=None):
+    return AddmmGradientOp(node_input, node_grad, beta, ctx=ctx)
+
+
+class BatchMatMulOp(Op):
+    def __init__(self, a, b, trans_A=False, trans_B=False, ctx=None):
+        super().__init__(BatchMatMulOp, [a, b], ctx)
+        self.matmul_attr_trans_A, self.matmul_attr_trans_B = trans_A, trans_B
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        a, b = input_vals
+        return KG.bmm(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B)
+
+    def gradient(self, output_grad):
+        ta, tb = self.matmul_attr_trans_A, self.matmul_attr_trans_B
+        A, B, G = self.inputs[0], self.inputs[1], output_grad
+        c = self.raw_ctx
+        if not ta and not tb:
+            return [batch_matmul_op(G, B, False, True, ctx=c), batch_matmul_op(A, G, True, False, ctx=c)]
+        if ta and not tb:
+            return [batch_matmul_op(B, G, False, True, ctx=c), batch_matmul_op(A, G, False, False, ctx=c)]
+        if not ta and tb:
+            return [batch_matmul_op(G, B, False, False, ctx=c), batch_matmul_op(G, A, True, False, ctx=c)]
+        return [batch_matmul_op(B, G, True, True, ctx=c), batch_matmul_op(G, A, True, True, ctx=c)]
+
+    def infer_shape(self, input_shapes):
+        a, b = input_shapes
+        m = a[-1] if self.matmul_attr_trans_A else a[-2]
+        n = b[-2] if self.matmul_attr_trans_B else b[-1]
+        return tuple(a[:-2]) + (m, n)
+
+
+def batch_matmul_op(node_A, node_B, trans_A=False, trans_B=False, ctx=None):
+    return BatchMatMulOp(node_A, node_B, trans_A, trans_B, ctx=ctx)
+
+
+class BaddbmmOp(Op):
+    def __init__(self, inp, a, b, alpha=1.0, beta=1.0, ctx=None):
+        super().__init__(BaddbmmOp, [inp, a, b], ctx)
+        self.alpha, self.beta = alpha, beta
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        c, a, b = input_vals
+        r = KG.bmm(a, b, False, False)
+        return r * self.alpha + c.to(r.dtype) * self.beta
+
+    def gradient(self, output_grad):
+        from .basic import mul_byconst_op
+        c = self.raw_ctx
+        ga = mul_byconst_op(batch_matmul_op(output_grad, self.inputs[2], False, True, ctx=c), self.alpha, ctx=c)
+        gb = mul_byconst_op(batch_matmul_op(self.inputs[1], output_grad, True, False, ctx=c), self.alpha, ctx=c)
+        return [addmm_gradient_op(self.inputs[0], output_grad, self.beta, ctx=c), ga, gb]
+
+    def infer_shape(self, input_shapes):
+        return tuple(input_shapes[1][:-1]) + (input_shapes[2][-1],)
+
+
+def baddbmm_op(node_A, node_B, node_C, alpha=1.0, beta=1.0, ctx=None):
+    return BaddbmmOp(node_A, node_B, node_C, alpha, beta, ctx=ctx)
+
+
+class CsrmvOp(Op):
+    def __init__(self, a, b, trans=False, ctx=None):
+        super().__init__(CsrmvOp, [a, b], ctx)
+        self.trans = trans
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels import spmm as KSP
+        return KSP.csrmv(input_vals[0], input_vals[1], self.trans)
+
+    def gradient(self, output_grad):
+        return [None, csrmv_op(self.inputs[0], output_grad, not self.trans, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        s = input_shapes[0]
+        return (s[1],) if self.trans else (s[0],)
+
+
+class CsrmmOp(Op):
+    def __init__(self, a, b, trans_A=False, trans_B=False, ctx=None):
+        super().__init__(CsrmmOp, [a, b], ctx)
+        self.trans_A, self.trans_B = trans_A, trans_B
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels import spmm as KSP
+        return KSP.csrmm(input_vals[0], input_vals[1], self.trans_A, self.trans_B)
+
+    def gradient(self, output_grad):
+        return [None, csrmm_op(self.inputs[0], output_grad, not self.trans_A, False, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        a, b = input_shapes
+        m = a[1] if self.trans_A else a[0]
+        n = b[0] if self.trans_B else b[1]
+        return (m, n)
+
+
+def csrmv_op(node_A, node_B, trans=False, ctx=None):
+    return CsrmvOp(node_A, node_B, trans, ctx=ctx)
+
+
+def csrmm_op(node_A, node_B, trans_A=False, trans_B=False, ctx=None):
+    return CsrmmOp(node_A, node_B, trans_A, trans_B, ctx=ctx)

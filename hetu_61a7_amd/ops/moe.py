@@ -1,0 +1,329 @@
+"""MoE routing operators (reference LayoutTransform.py, ReverseLayoutTransform.py,
+ReverseLayoutTransformNoGate.py, BalanceAssignment.py, SamGroupSum.py,
+SamMax.py, GroupTopKIdx.py; SURVEY §2.4 "MoE routing", §3.6).
+
+``indices_s``/``location_s``/``gates`` are the per-choice lists produced by the
+gates (one node per top-k slot), exactly as in the reference layers.
+Dispatch/combine are slot-indexed gathers (``kernels.moe``) -- deterministic,
+no atomics on the forward combine.
+"""
+from __future__ import annotations
+
+import torch
+
+from .node import Op
+from ..kernels import moe as KM
+
+
+def _stack(vals):
+    return torch.stack([v.reshape(-1) for v in vals], 1)
+
+
+class LayoutTransformOp(Op):
+    def __init__(self, x, indices_s, location_s, capacity, num_experts, ctx=None):
+        indices_s = list(indices_s) if isinstance(indices_s, (list, tuple)) else [indices_s]
+        location_s = list(location_s) if isinstance(location_s, (list, tuple)) else [location_s]
+        super().__init__(LayoutTransformOp, [x] + indices_s + location_s, ctx)
+        self.k = len(indices_s)
+        self.capacity, self.num_experts = int(capacity), int(num_experts)
+
+    def _idx(self, vals):
+        k = self.k
+        return _stack(vals[1:1 + k]), _stack(vals[1 + k:1 + 2 * k])
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        idx, loc = self._idx(input_vals)
+        x = input_vals[0]
+        return KM.layout_transform(x.reshape(x.shape[0], -1), idx, loc, self.capacity, self.num_experts)
+
+    def gradient(self, output_grad):
+        k = self.k
+        g = LayoutTransformGradientOp(output_grad, self.inputs[1:1 + k], self.inputs[1 + k:1 + 2 * k],
+                                      self.capacity, ctx=self.raw_ctx)
+        return [g] + [None] * (2 * k)
+
+    def infer_shape(self, input_shapes):
+        return (self.num_experts * self.capacity, input_shapes[0][-1])
+
+
+class LayoutTransformGradientOp(Op):
+    def __init__(self, grad, indices_s, location_s, capacity, ctx=None):
+        indices_s = list(indices_s) if isinstance(indices_s, (list, tuple)) else [indices_s]
+        location_s = list(location_s) if isinstance(location_s, (list, tuple)) else [location_s]
+        super().__init__(LayoutTransformGradientOp, [grad] + indices_s + location_s, ctx)
+        self.k, self.capacity = len(indices_s), int(capacity)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        k = self.k
+        idx, loc = _stack(input_vals[1:1 + k]), _stack(input_vals[1 + k:1 + 2 * k])
+        return KM.layout_transform_backward(input_vals[0], idx, loc, self.capacity)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return None
+
+
+def layout_transform_op(input, indices_s, location_s, capacity, total_experts, ctx=None):
+    return LayoutTransformOp(input, indices_s, location_s, capacity, total_experts, ctx=ctx)
+
+
+def layout_transform_gradient_op(input, indice, location, capacity, ctx=None):
+    return LayoutTransformGradientOp(input, indice, location, capacity, ctx=ctx)
+
+
+class ReverseLayoutTransformOp(Op):
+    """Gate-weighted combine of expert outputs back to token order."""
+
+    def __init__(self, y, indices_s, location_s, gates, capacity, num_experts, ctx=None):
+        indices_s = list(indices_s) if isinstance(indices_s, (list, tuple)) else [indices_s]
+        location_s = list(location_s) if isinstance(location_s, (list, tuple)) else [location_s]
+        gates = (list(gates) if isinstance(gates, (list, tuple)) else [gates]) if gates is not None else []
+        super().__init__(ReverseLayoutTransformOp, [y] + indices_s + location_s + gates, ctx)
+        self.k = len(indices_s)
+        self.has_gate = len(gates) > 0
+        self.capacity, self.num_experts = int(capacity), int(num_experts)
+
+    def _parts(self, vals):
+        k = self.k
+        idx = _stack(vals[1:1 + k])
+        loc = _stack(vals[1 + k:1 + 2 * k])
+        gates = _stack(vals[1 + 2 * k:1 + 3 * k]) if self.has_gate else None
+        return idx, loc, gates
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        idx, loc, gates = self._parts(input_vals)
+        return KM.reverse_layout_transform(input_vals[0], idx, loc, gates, self.capacity)
+
+    def gradient(self, output_grad):
+        k = self.k
+        ins = self.inputs
+        gd = ReverseLayoutTransformGradientDataOp(output_grad, ins[1:1 + k], ins[1 + k:1 + 2 * k],
+                                                  ins[1 + 2 * k:1 + 3 * k] if self.has_gate else None,
+                                                  self.capacity, self.num_experts, ctx=self.raw_ctx)
+        grads = [gd] + [None] * (2 * k)
+        if self.has_gate:
+            for j in range(k):
+                grads.append(ReverseLayoutTransformGradientGateOp(output_grad, ins[0], ins[1 + j], ins[1 + k + j],
+                                                                  self.capacity, ctx=self.raw_ctx))
+        return grads
+
+    def infer_shape(self, input_shapes):
+        return (input_shapes[1][0], input_shapes[0][-1])
+
+
+class ReverseLayoutTransformGradientDataOp(Op):
+    def __init__(self, grad, indices_s, location_s, gates, capacity, num_experts, ctx=None):
+        indices_s = list(indices_s) if isinstance(indices_s, (list, tuple)) else [indices_s]
+        location_s = list(location_s) if isinstance(location_s, (list, tuple)) else [location_s]
+        gates = (list(gates) if isinstance(gates, (list, tuple)) else [gates]) if gates is not None else []
+        super().__init__(ReverseLayoutTransformGradientDataOp, [grad] + indices_s + location_s + gates, ctx)
+        self.k, self.has_gate = len(indices_s), len(gates) > 0
+        self.capacity, self.num_experts = int(capacity), int(num_experts)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        k = self.k
+        idx, loc = _stack(input_vals[1:1 + k]), _stack(input_vals[1 + k:1 + 2 * k])
+        gates = _stack(input_vals[1 + 2 * k:1 + 3 * k]) if self.has_gate else None
+        return KM.reverse_layout_transform_backward_data(input_vals[0], idx, loc, gates, self.capacity,
+                                                         self.capacity * self.num_experts)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return (self.capacity * self.num_experts, input_shapes[0][-1])
+
+
+class ReverseLayoutTransformGradientGateOp(Op):
+    def __init__(self, grad, y, indices, locations, capacity, ctx=None):
+        super().__init__(ReverseLayoutTransformGradientGateOp, [grad, y, indices, locations], ctx)
+        self.capacity = int(capacity)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, y, idx, loc = input_vals
+        return KM.reverse_layout_transform_backward_gate(g, y, idx.reshape(-1, 1), loc.reshape(-1, 1),
+                                                         self.capacity).reshape(idx.shape)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[2]
+
+
+def reverse_layout_transform_op(input, indices_s, location_s, gates, capacity, num_experts, ctx=None):
+    return ReverseLayoutTransformOp(input, indices_s, location_s, gates, capacity, num_experts, ctx=ctx)
+
+
+def reverse_layout_transform_gradient_data_op(input, indices, locations, gates, capacity, num_experts, ctx=None):
+    return ReverseLayoutTransformGradientDataOp(input, indices, locations, gates, capacity, num_experts, ctx=ctx)
+
+
+def reverse_layout_transform_gradient_gate_op(combined_output, expert_output, indices, locations, capacity, ctx=None):
+    return ReverseLayoutTransformGradientGateOp(combined_output, expert_output, indices, locations, capacity, ctx=ctx)
+
+
+def reverse_layout_transform_no_gate_op(input, indices_s, location_s, capacity, num_experts, ctx=None):
+    return ReverseLayoutTransformOp(input, indices_s, location_s, None, capacity, num_experts, ctx=ctx)
+
+
+def reverse_layout_transform_no_gate_gradient_op(input, indices, locations, capacity, num_experts, ctx=None):
+    return ReverseLayoutTransformGradientDataOp(input, indices, locations, None, capacity, num_experts, ctx=ctx)
+
+
+class BalanceAssignmentOp(Op):
+    """BASE-layer balanced token->expert assignment (auction algorithm,
+    reference BalanceAssignment.py:11-85) run on device: returns for each
+    expert the indices of the tokens assigned to it ([E, T/E])."""
+
+    def __init__(self, scores, max_iterations=100, ctx=None):
+        super().__init__(BalanceAssignmentOp, [scores], ctx)
+        self.max_iterations = max_iterations
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels.moe import balanced_assignment
+        return balanced_assignment(input_vals[0], self.max_iterations)
+
+    def gradient(self, output_grad):
+        return [None]
+
+    def infer_shape(self, input_shapes):
+        T, E = input_shapes[0]
+        return (T,)
+
+
+def balance_assignment_op(node, ctx=None):
+    return BalanceAssignmentOp(node, ctx=ctx)
+
+
+class SamGroupSumOp(Op):
+    """Sum of gate probabilities per GPU group ([T, E] -> [T, G])."""
+
+    def __init__(self, gate, num_local_gpus, ctx=None):
+        super().__init__(SamGroupSumOp, [gate], ctx)
+        self.num_local_gpus = num_local_gpus
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g = input_vals[0]
+        T, E = g.shape
+        G = self.num_local_gpus
+        return g.float().reshape(T, G, E // G).sum(-1)
+
+    def gradient(self, output_grad):
+        return [SamGroupSumGradOp(output_grad, self.inputs[0], self.num_local_gpus, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return (input_shapes[0][0], self.num_local_gpus)
+
+
+class SamGroupSumGradOp(Op):
+    shape_only_inputs = (1,)
+
+    def __init__(self, grad, ref, num_local_gpus, ctx=None):
+        super().__init__(SamGroupSumGradOp, [grad, ref], ctx)
+        self.num_local_gpus = num_local_gpus
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, shape = input_vals
+        T, E = tuple(shape)
+        G = self.num_local_gpus
+        return g.float().unsqueeze(-1).expand(T, G, E // G).reshape(T, E)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[1]
+
+
+def sam_group_sum_op(node, num_local_gpus, ctx=None):
+    return SamGroupSumOp(node, num_local_gpus, ctx=ctx)
+
+
+def _sam_mask(x, top1_group, topk_idx, n):
+    T, E = x.shape
+    g = top1_group.reshape(-1).long()
+    cols = torch.arange(E, device=x.device).unsqueeze(0)
+    outside = (cols < (g * n).unsqueeze(1)) | (cols >= ((g + 1) * n).unsqueeze(1))
+    ref = torch.gather(x.float(), 1, topk_idx.reshape(-1, 1).long())
+    diff = x.float() - ref
+    return outside & (diff > 0), diff
+
+
+class SamMaxOp(Op):
+    """SAM alignment loss: max(0, g_j - g_topk) for experts outside the chosen group."""
+
+    def __init__(self, gates, top1_group, topk_idx, num_local_gpus, ctx=None):
+        super().__init__(SamMaxOp, [gates, top1_group, topk_idx], ctx)
+        self.num_local_gpus = num_local_gpus
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x, grp, tk = input_vals
+        m, diff = _sam_mask(x, grp, tk, self.num_local_gpus)
+        return torch.where(m, diff, torch.zeros_like(diff))
+
+    def gradient(self, output_grad):
+        return [sammax_grad_op(output_grad, self.inputs[0], self.inputs[1], self.inputs[2], self.num_local_gpus,
+                               ctx=self.raw_ctx), None, None]
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+class SamMaxGradOp(Op):
+    def __init__(self, grad, gates, top1_group, topk_idx, num_local_gpus, ctx=None):
+        super().__init__(SamMaxGradOp, [grad, gates, top1_group, topk_idx], ctx)
+        self.num_local_gpus = num_local_gpus
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, x, grp, tk = input_vals
+        m, _ = _sam_mask(x, grp, tk, self.num_local_gpus)
+        gm = torch.where(m, g.float(), torch.zeros_like(g, dtype=torch.float32))
+        out = gm.clone()
+        out.scatter_add_(1, tk.reshape(-1, 1).long(), -gm.sum(1, keepdim=True))
+        return out
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[1]
+
+
+def sam_max_op(node_A, node_B, node_C, num_local_gpus, ctx=None):
+    return SamMaxOp(node_A, node_B, node_C, num_local_gpus, ctx=ctx)
+
+
+def sammax_grad_op(node_A, node_B, node_C, node_D, num_local_gpus, ctx=None):
+    return SamMaxGradOp(node_A, node_B, node_C, node_D, num_local_gpus, ctx=ctx)
+
+
+class GroupTopKIdxOp(Op):
+    """Top-k expert ids restricted to the group chosen per row (reference
+    GroupTopKIdx.cu: group g spans experts [g*n, (g+1)*n))."""
+
+    def __init__(self, x, top1_group, topk=1, num_local_gpus=8, ctx=None):
+        super().__init__(GroupTopKIdxOp, [x, top1_group], ctx)
+        self.k, self.num_local_gpus = topk, num_local_gpus
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x, grp = input_vals
+        n = self.num_local_gpus
+        g = grp.reshape(-1).long()
+        T, E = x.shape
+        cols = torch.arange(E, device=x.device).unsqueeze(0)
+        inside = (cols >= (g * n).unsqueeze(1)) & (cols < ((g + 1) * n).unsqueeze(1))
+        masked = torch.where(inside, x.float(), torch.full_like(x, -1e4, dtype=torch.float32))
+        return torch.topk(masked, self.k, dim=1)[1]
+
+    def gradient(self, output_grad):
+        return [None, None]
+
+    def infer_shape(self, input_shapes):
+        return (input_shapes[0][0], self.k)
+
+
+def group_topk_idx_op(node_A, node_B, topk, num_local_gpus, ctx=None):
+    return GroupTopKIdxOp(node_A, node_B, topk, num_local_gpus, ctx=ctx)

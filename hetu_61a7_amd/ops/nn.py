@@ -1,0 +1,592 @@
+"""Convolution, pooling, normalisation and dropout operators.
+
+Parity: reference gpu_ops Conv2d.py, Conv2dAddBias.py, AvgPool.py, MaxPool.py,
+BatchNorm.py, LayerNorm.py, InstanceNorm2d.py, Dropout.py, Dropout2d.py
+(SURVEY §2.4 "Conv / pool / norm / dropout").
+
+MI355X design:
+* activations are logically NCHW (same API/shapes as Hetu) but physically
+  channels-last (NHWC) on the GPU, which is what MFMA implicit-GEMM convs and
+  the BN/pool kernels want;
+* BatchNorm keeps fp32 statistics/affine while activations may be bf16, and is
+  fused with the ReLU / residual-add that follow it in ResNets
+  (``fused_bn_relu_op``, ``fused_bn_add_relu_op``); the backward consumes the
+  saved mean/invstd through the executor's aux channel (no recompute);
+* dropout masks are regenerated in the backward from a per-call Philox seed
+  (reference ``Dropout.py:46-49`` recompute semantics), never stored.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .node import Op
+from ..kernels import norm as KN
+from ..kernels import pool as KP
+from ..kernels import conv as KC
+from ..kernels import layernorm as KLN
+from ..kernels import dropout as KD
+
+
+class AuxResult(object):
+    """Value plus auxiliary tensors saved for a gradient op."""
+    __slots__ = ('value', 'aux')
+
+    def __init__(self, value, aux):
+        self.value = value
+        self.aux = aux
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+# ---------------------------------------------------------------------------
+# convolution
+class Conv2dOp(Op):
+    def __init__(self, x, w, padding=0, stride=1, ctx=None):
+        super().__init__(Conv2dOp, [x, w], ctx)
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x, w = input_vals
+        return KC.conv2d(x, w, None, self.stride, self.padding)
+
+    def gradient(self, output_grad):
+        return [conv2d_gradient_of_data_op(self.inputs[1], output_grad, self.inputs[0], self.padding, self.stride, ctx=self.raw_ctx),
+                conv2d_gradient_of_filter_op(self.inputs[0], output_grad, self.inputs[1], self.padding, self.stride, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        n, c, h, w = input_shapes[0]
+        f, _, kh, kw = input_shapes[1]
+        ho = (h + 2 * self.padding[0] - kh) // self.stride[0] + 1
+        wo = (w + 2 * self.padding[1] - kw) // self.stride[1] + 1
+        return (n, f, ho, wo)
+
+
+class Conv2d_Gradient_of_DataOp(Op):
+    shape_only_inputs = (2,)
+
+    def __init__(self, w, grad, x_ref, padding=0, stride=1, ctx=None):
+        super().__init__(Conv2d_Gradient_of_DataOp, [w, grad, x_ref], ctx)
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        w, g, xshape = input_vals
+        return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[2]
+
+
+class Conv2d_Gradient_of_FilterOp(Op):
+    shape_only_inputs = (2,)
+
+    def __init__(self, x, grad, w_ref, padding=0, stride=1, ctx=None):
+        super().__init__(Conv2d_Gradient_of_FilterOp, [x, grad, w_ref], ctx)
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x, g, wshape = input_vals
+        return KC.conv2d_backward_filter(g, x, tuple(wshape), self.stride, self.padding)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[2]
+
+
+def conv2d_op(node_A, node_B, padding=0, stride=1, ctx=None):
+    return Conv2dOp(node_A, node_B, padding, stride, ctx=ctx)
+
+
+def conv2d_gradient_of_data_op(node_A, node_B, node_C, padding=0, stride=1, ctx=None):
+    """(filter, grad_y, input_x_ref)"""
+    return Conv2d_Gradient_of_DataOp(node_A, node_B, node_C, padding, stride, ctx=ctx)
+
+
+def conv2d_gradient_of_filter_op(input_X, gradient_Y, input_filter, padding=0, stride=1, ctx=None):
+    return Conv2d_Gradient_of_FilterOp(input_X, gradient_Y, input_filter, padding, stride, ctx=ctx)
+
+
+class Conv2dAddBiasOp(Op):
+    def __init__(self, x, w, b, padding=0, stride=1, ctx=None):
+        super().__init__(Conv2dAddBiasOp, [x, w, b], ctx)
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x, w, b = input_vals
+        return KC.conv2d(x, w, b, self.stride, self.padding)
+
+    def gradient(self, output_grad):
+        from .shape import conv2d_reducesum_op
+        return [conv2d_gradient_of_data_op(self.inputs[1], output_grad, self.inputs[0], self.padding, self.stride, ctx=self.raw_ctx),
+                conv2d_gradient_of_filter_op(self.inputs[0], output_grad, self.inputs[1], self.padding, self.stride, ctx=self.raw_ctx),
+                conv2d_reducesum_op(output_grad, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return Conv2dOp.infer_shape(self, input_shapes[:2])
+
+
+def conv2d_add_bias_op(node_A, node_B, bias, padding=0, stride=1, ctx=None):
+    return Conv2dAddBiasOp(node_A, node_B, bias, padding, stride, ctx=ctx)
+
+
+# ---------------------------------------------------------------------------
+# pooling
+class Max_Pool2dOp(Op):
+    def __init__(self, x, kh, kw, padding, stride, ctx=None):
+        super().__init__(Max_Pool2dOp, [x], ctx)
+        self.kh, self.kw = kh, kw
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        y, idx = KP.maxpool2d(input_vals[0], self.kh, self.kw, self.stride[0], self.stride[1],
+                              self.padding[0], self.padding[1])
+        return AuxResult(y, (idx, tuple(input_vals[0].shape)))
+
+    def gradient(self, output_grad):
+        return [max_pool2d_gradient_op(self, output_grad, self.inputs[0], self.kh, self.kw,
+                                       self.padding, self.stride, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        n, c, h, w = input_shapes[0]
+        return (n, c, (h + 2 * self.padding[0] - self.kh) // self.stride[0] + 1,
+                (w + 2 * self.padding[1] - self.kw) // self.stride[1] + 1)
+
+
+class Max_Pool2d_GradientOp(Op):
+    aux_inputs = (0,)
+    shape_only_inputs = (2,)
+
+    def __init__(self, out, grad, x, kh, kw, padding, stride, ctx=None):
+        super().__init__(Max_Pool2d_GradientOp, [out, grad, x], ctx)
+        self.kh, self.kw = kh, kw
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        (idx, xshape), g, _ = input_vals
+        return KP.maxpool2d_backward(g, idx, xshape, self.kh, self.kw, self.stride[0],
+                                     self.stride[1], self.padding[0], self.padding[1])
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[2]
+
+
+def max_pool2d_op(node_A, kernel_H, kernel_W, padding, stride, ctx=None):
+    return Max_Pool2dOp(node_A, kernel_H, kernel_W, padding, stride, ctx=ctx)
+
+
+def max_pool2d_gradient_op(node_out, node_out_gradient, node_in, kernel_H, kernel_W, padding, stride, ctx=None):
+    return Max_Pool2d_GradientOp(node_out, node_out_gradient, node_in, kernel_H, kernel_W, padding, stride, ctx=ctx)
+
+
+class Avg_Pool2dOp(Op):
+    def __init__(self, x, kh, kw, padding, stride, ctx=None):
+        super().__init__(Avg_Pool2dOp, [x], ctx)
+        self.kh, self.kw = kh, kw
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x = input_vals[0]
+        n, c, h, w = x.shape
+        if self.kh == h and self.kw == w and self.padding == (0, 0):
+            from ..kernels import reduce as KR
+            return KR.global_avg_pool(x).reshape(n, c, 1, 1)
+        return KP.avgpool2d(x, self.kh, self.kw, self.stride[0], self.stride[1],
+                            self.padding[0], self.padding[1])
+
+    def gradient(self, output_grad):
+        return [avg_pool2d_gradient_op(self, output_grad, self.inputs[0], self.kh, self.kw,
+                                       self.padding, self.stride, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return Max_Pool2dOp.infer_shape(self, input_shapes)
+
+
+class Avg_Pool2d_GradientOp(Op):
+    shape_only_inputs = (0, 2)
+
+    def __init__(self, out, grad, x, kh, kw, padding, stride, ctx=None):
+        super().__init__(Avg_Pool2d_GradientOp, [out, grad, x], ctx)
+        self.kh, self.kw = kh, kw
+        self.padding, self.stride = _pair(padding), _pair(stride)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        _, g, xshape = input_vals
+        n, c, h, w = tuple(xshape)
+        if self.kh == h and self.kw == w and self.padding == (0, 0):
+            from ..kernels import reduce as KR
+            return KR.global_avg_pool_backward(g.reshape(n, c), tuple(xshape))
+        return KP.avgpool2d_backward(g, tuple(xshape), self.kh, self.kw, self.stride[0],
+                                     self.stride[1], self.padding[0], self.padding[1])
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[2]
+
+
+def avg_pool2d_op(node_A, kernel_H, kernel_W, padding, stride, ctx=None):
+    return Avg_Pool2dOp(node_A, kernel_H, kernel_W, padding, stride, ctx=ctx)
+
+
+def avg_pool2d_gradient_op(node_out, node_out_gradient, node_in, kernel_H, kernel_W, padding, stride, ctx=None):
+    return Avg_Pool2d_GradientOp(node_out, node_out_gradient, node_in, kernel_H, kernel_W, padding, stride, ctx=ctx)
+
+
+# ---------------------------------------------------------------------------
+# batch normalisation (+ fused ReLU / residual)
+class Batch_NormalizationOp(Op):
+    def __init__(self, x, scale, bias, momentum=0.1, eps=1e-5, relu=False, residual=None, ctx=None):
+        inputs = [x, scale, bias] + ([residual] if residual is not None else [])
+        super().__init__(Batch_NormalizationOp, inputs, ctx)
+        self.momentum, self.eps = momentum, eps
+        self.relu, self.has_residual = relu, residual is not None
+        self.running_mean = None
+        self.running_var = None
+        self.inference = False
+
+    def _init_running(self, C, device):
+        if self.running_mean is None or self.running_mean.device != device:
+            self.running_mean = torch.zeros(C, dtype=torch.float32, device=device)
+            self.running_var = torch.ones(C, dtype=torch.float32, device=device)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None, inference=None):
+        x, scale, bias = input_vals[:3]
+        res = input_vals[3] if self.has_residual else None
+        self._init_running(x.shape[1], x.device)
+        training = not (self.inference if inference is None else inference)
+        y, mean, invstd = KN.bn_forward(x, scale.float(), bias.float(), self.running_mean,
+                                        self.running_var, self.momentum, self.eps, training,
+                                        relu=self.relu, residual=res)
+        if not training:
+            return y
+        return AuxResult(y, (mean, invstd))
+
+    def gradient(self, output_grad):
+        g = Batch_Normalization_GradientOp(output_grad, self.inputs[0], self.inputs[1], self,
+                                           self.eps, ctx=self.raw_ctx)
+        out = [batch_normalization_gradient_of_data_op(g, self.inputs[0], ctx=self.raw_ctx),
+               batch_normalization_gradient_of_scale_op(g, self.inputs[1], ctx=self.raw_ctx),
+               batch_normalization_gradient_of_bias_op(g, self.inputs[2], ctx=self.raw_ctx)]
+        if self.has_residual:
+            out.append(BNGradSelectOp(g, 3, ctx=self.raw_ctx))
+        return out
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+class Batch_Normalization_GradientOp(Op):
+    """Computes (dx, dscale, dbias[, dresidual]) in one fused kernel pass."""
+    aux_inputs = (3,)
+    value_and_aux_inputs = (3,)
+
+    def __init__(self, out_gradient, x, scale, forward_node, eps, ctx=None):
+        super().__init__(Batch_Normalization_GradientOp, [out_gradient, x, scale, forward_node], ctx)
+        self.forward_node = forward_node
+        self.eps = eps
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, x, scale, (y, (mean, invstd)) = input_vals
+        fw = self.forward_node
+        dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
+                                                 relu=fw.relu, want_dres=fw.has_residual)
+        return (dx, dscale, dbias, dres)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[1]
+
+
+class BNGradSelectOp(Op):
+    def __init__(self, g, index, ctx=None):
+        super().__init__(BNGradSelectOp, [g], ctx)
+        self.index = index
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        return input_vals[0][self.index]
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return None
+
+
+def batch_normalization_op(node_in, bn_scale, bn_bias, momentum=0.1, eps=1e-5, ctx=None):
+    return Batch_NormalizationOp(node_in, bn_scale, bn_bias, momentum, eps, ctx=ctx)
+
+
+def fused_bn_relu_op(node_in, bn_scale, bn_bias, momentum=0.1, eps=1e-5, ctx=None):
+    """relu(batch_norm(x)) in one kernel pass (and one fused backward)."""
+    return Batch_NormalizationOp(node_in, bn_scale, bn_bias, momentum, eps, relu=True, ctx=ctx)
+
+
+def fused_bn_add_relu_op(node_in, bn_scale, bn_bias, residual, momentum=0.1, eps=1e-5, ctx=None):
+    """relu(batch_norm(x) + residual) -- the ResNet block tail."""
+    return Batch_NormalizationOp(node_in, bn_scale, bn_bias, momentum, eps, relu=True,
+                                 residual=residual, ctx=ctx)
+
+
+def batch_normalization_gradient_op(out_gradient, in_node, bn_scale, forward_node, eps, ctx=None):
+    return Batch_Normalization_GradientOp(out_gradient, in_node, bn_scale, forward_node, eps, ctx=ctx)
+
+
+def batch_normalization_gradient_of_data_op(bn_gradient, in_arr, ctx=None):
+    op = BNGradSelectOp(bn_gradient, 0, ctx=ctx)
+    op.op_type = 'Batch_Normalization_Gradient_of_DataOp'
+    return op
+
+
+def batch_normalization_gradient_of_scale_op(bn_gradient, in_scale, ctx=None):
+    op = BNGradSelectOp(bn_gradient, 1, ctx=ctx)
+    op.op_type = 'Batch_Normalization_Gradient_of_ScaleOp'
+    return op
+
+
+def batch_normalization_gradient_of_bias_op(bn_gradient, in_bias, ctx=None):
+    op = BNGradSelectOp(bn_gradient, 2, ctx=ctx)
+    op.op_type = 'Batch_Normalization_Gradient_of_BiasOp'
+    return op
+
+
+# ---------------------------------------------------------------------------
+# layer normalisation
+class Layer_NormalizationOp(Op):
+    def __init__(self, x, scale, bias, eps=0.01, ctx=None):
+        super().__init__(Layer_NormalizationOp, [x, scale, bias], ctx)
+        self.eps = eps
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x, g, b = input_vals
+        y, mean, rstd = KLN.layer_norm(x, g, b, self.eps)
+        return AuxResult(y, (mean, rstd))
+
+    def gradient(self, output_grad):
+        gn = Layer_Normalization_GradientOp(output_grad, self.inputs[0], self.inputs[1], self, self.eps, ctx=self.raw_ctx)
+        return [layer_normalization_gradient_of_data_op(gn, self.inputs[0], ctx=self.raw_ctx),
+                layer_normalization_gradient_of_scale_op(gn, self.inputs[1], ctx=self.raw_ctx),
+                layer_normalization_gradient_of_bias_op(gn, self.inputs[2], ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+class Layer_Normalization_GradientOp(Op):
+    aux_inputs = (3,)
+
+    def __init__(self, out_gradient, x, scale, forward_node, eps, ctx=None):
+        super().__init__(Layer_Normalization_GradientOp, [out_gradient, x, scale, forward_node], ctx)
+        self.eps = eps
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        dy, x, g, (mean, rstd) = input_vals
+        return KLN.layer_norm_backward(dy, x, g, mean, rstd)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[1]
+
+
+def layer_normalization_op(node_in, ln_scale, ln_bias, eps=0.01, ctx=None):
+    return Layer_NormalizationOp(node_in, ln_scale, ln_bias, eps, ctx=ctx)
+
+
+def layer_normalization_gradient_op(out_gradient, in_node, ln_scale, forward_node, eps, ctx=None):
+    return Layer_Normalization_GradientOp(out_gradient, in_node, ln_scale, forward_node, eps, ctx=ctx)
+
+
+def _sel(g, i, name, ctx):
+    op = BNGradSelectOp(g, i, ctx=ctx)
+    op.op_type = name
+    return op
+
+
+def layer_normalization_gradient_of_data_op(ln_gradient, in_arr, ctx=None):
+    return _sel(ln_gradient, 0, 'Layer_Normalization_Gradient_of_DataOp', ctx)
+
+
+def layer_normalization_gradient_of_scale_op(ln_gradient, in_scale, ctx=None):
+    return _sel(ln_gradient, 1, 'Layer_Normalization_Gradient_of_ScaleOp', ctx)
+
+
+def layer_normalization_gradient_of_bias_op(ln_gradient, in_bias, ctx=None):
+    return _sel(ln_gradient, 2, 'Layer_Normalization_Gradient_of_BiasOp', ctx)
+
+
+class Instance_Normalization2dOp(Op):
+    def __init__(self, x, eps=1e-7, ctx=None):
+        super().__init__(Instance_Normalization2dOp, [x], ctx)
+        self.eps = eps
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x = input_vals[0].float()
+        mean = x.mean((2, 3), keepdim=True)
+        var = x.var((2, 3), unbiased=False, keepdim=True)
+        rstd = torch.rsqrt(var + self.eps)
+        return AuxResult(((x - mean) * rstd).to(input_vals[0].dtype), (mean, rstd))
+
+    def gradient(self, output_grad):
+        return [instance_normalization2d_gradient_op(output_grad, self.inputs[0], self, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+class Instance_Normalization2d_GradientOp(Op):
+    aux_inputs = (2,)
+
+    def __init__(self, grad, x, forward_node, ctx=None):
+        super().__init__(Instance_Normalization2d_GradientOp, [grad, x, forward_node], ctx)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, x, (mean, rstd) = input_vals
+        gf, xf = g.float(), x.float()
+        xhat = (xf - mean) * rstd
+        m = gf.mean((2, 3), keepdim=True)
+        mx = (gf * xhat).mean((2, 3), keepdim=True)
+        return (rstd * (gf - m - xhat * mx)).to(x.dtype)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[1]
+
+
+def instance_normalization2d_op(node_in, eps=0.01, ctx=None):
+    return Instance_Normalization2dOp(node_in, eps, ctx=ctx)
+
+
+def instance_normalization2d_gradient_op(out_gradient, in_node, forward_node, ctx=None):
+    return Instance_Normalization2d_GradientOp(out_gradient, in_node, forward_node, ctx=ctx)
+
+
+# ---------------------------------------------------------------------------
+# dropout (Philox, recompute mask in backward)
+_SEED_COUNTER = [int(time.time() * 1000) & 0xFFFFFFF]
+
+
+def _next_seed():
+    _SEED_COUNTER[0] = (_SEED_COUNTER[0] * 6364136223846793005 + 1442695040888963407) & ((1 << 62) - 1)
+    return _SEED_COUNTER[0]
+
+
+class DropoutOp(Op):
+    def __init__(self, x, keep_prob, recompute=True, inplace=False, ctx=None):
+        super().__init__(DropoutOp, [x], ctx)
+        self.keep_prob, self.recompute = keep_prob, recompute
+        self.inference = False
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x = input_vals[0]
+        if self.inference or self.keep_prob >= 1.0:
+            return AuxResult(x, 0)
+        seed = _next_seed()
+        return AuxResult(KD.dropout(x, self.keep_prob, seed), seed)
+
+    def gradient(self, output_grad):
+        return [dropout_gradient_recompute_op(output_grad, self.keep_prob, self, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+class Dropout_Gradient_recomputeOp(Op):
+    aux_inputs = (1,)
+
+    def __init__(self, grad, keep_prob, forward_node, ctx=None):
+        super().__init__(Dropout_Gradient_recomputeOp, [grad, forward_node], ctx)
+        self.keep_prob = keep_prob
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, seed = input_vals
+        if self.keep_prob >= 1.0 or seed == 0:
+            return g
+        return KD.dropout(g, self.keep_prob, seed)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+def dropout_op(node_in, keep_prob, recompute=True, inplace=False, ctx=None):
+    return DropoutOp(node_in, keep_prob, recompute, inplace, ctx=ctx)
+
+
+def dropout_gradient_recompute_op(node_in, keep_prob, forward_node, ctx=None):
+    return Dropout_Gradient_recomputeOp(node_in, keep_prob, forward_node, ctx=ctx)
+
+
+def dropout_gradient_op(node_in, keep_prob, forward_node, ctx=None):
+    return Dropout_Gradient_recomputeOp(node_in, keep_prob, forward_node, ctx=ctx)
+
+
+class Dropout2dOp(Op):
+    """Channel dropout: whole (n, c) planes zeroed."""
+
+    def __init__(self, x, keep_prob, ctx=None):
+        super().__init__(Dropout2dOp, [x], ctx)
+        self.keep_prob = keep_prob
+        self.inference = False
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x = input_vals[0]
+        if self.inference:
+            return AuxResult(x, None)
+        n, c = x.shape[:2]
+        seed = _next_seed()
+        g = torch.Generator(device=x.device)
+        g.manual_seed(seed & 0x7FFFFFFF)
+        mask = (torch.rand((n, c, 1, 1), generator=g, device=x.device) < self.keep_prob).to(x.dtype) / self.keep_prob
+        return AuxResult(x * mask, mask)
+
+    def gradient(self, output_grad):
+        return [dropout2d_gradient_op(output_grad, self.keep_prob, self, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+class Dropout2d_GradientOp(Op):
+    aux_inputs = (1,)
+
+    def __init__(self, grad, keep_prob, forward_node, ctx=None):
+        super().__init__(Dropout2d_GradientOp, [grad, forward_node], ctx)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, mask = input_vals
+        return g if mask is None else g * mask
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+def dropout2d_op(node_in, keep_prob, ctx=None):
+    return Dropout2dOp(node_in, keep_prob, ctx=ctx)
+
+
+def dropout2d_gradient_op(node_in, keep_prob, forward_node, ctx=None):
+    return Dropout2d_GradientOp(node_in, keep_prob, forward_node, ctx=ctx)

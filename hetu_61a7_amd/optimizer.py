@@ -1,0 +1,377 @@
+"""Optimizers and the OptimizerOp (reference ``python/hetu/optimizer.py:13-555``).
+
+MI355X design:
+
+* All dense trainable parameters of one ``OptimizerOp`` live in ONE flat fp32
+  buffer (parameters are views into it) laid out in *gradient arrival order*
+  (reverse topological order of the backward pass).  Gradients are written into a
+  matching flat fp32 buffer as soon as they are produced.
+* Data parallel: the flat gradient buffer is cut into contiguous buckets
+  (default 32 MB); a bucket's RCCL SUM all-reduce is launched asynchronously the
+  moment its last gradient lands, so communication overlaps the rest of the
+  backward pass.  The reference issues one blocking NCCL call per parameter with
+  a host-side event sync (``optimizer.py:145-163``, ``executor.py:1034-1036``).
+* The update is ONE fused HIP launch over the whole flat buffer
+  (``kernels/optimizer.hip``), which can also emit the bf16 compute copy of the
+  weights (mixed precision: fp32 master weights, bf16 MFMA operands).
+* Row-sparse (embedding) gradients are de-duplicated on device and applied with
+  the row-sparse update kernels; parameters named ``expert*`` are excluded from
+  the data-parallel all-reduce (MoE expert parallelism, reference
+  ``optimizer.py:150-152``).
+* Update rules and the AllReduce SUM semantics match the reference exactly.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .ops.node import Op
+from . import ndarray
+from .kernels import optim as KO
+from .kernels import sparse as KSP
+
+
+class Optimizer(object):
+    def __init__(self, learning_rate, l2reg=0):
+        self.learning_rate = learning_rate
+        self.l2reg = l2reg
+        self.params = None
+        self.tensors = None
+        self.initiated = False
+        self.name = 'Optimizer'
+        self.betats_updated = False
+
+    # reference API -----------------------------------------------------------------
+    @staticmethod
+    def get_var_list(loss):
+        from .ops.variable import PlaceholderOp
+        from .ops.executor import find_topo_sort
+        return [n for n in find_topo_sort([loss]) if isinstance(n, PlaceholderOp) and n.trainable]
+
+    def get_config(self):
+        """Wire format for the PS server optimizer (reference optimizer.py:91-101)."""
+        return (0, (self.learning_rate,), 1)
+
+    def minimize(self, loss, var_list=None):
+        from .ops.executor import gradients
+        from .graph_opt import fuse_forward
+        fuse_forward([loss])
+        self.loss = loss
+        if not var_list:
+            var_list = self.get_var_list(loss)
+        self.params = var_list
+        grads, self.backward2forward, self.forward2backward = gradients(loss, self.params, return_all=True)
+        return OptimizerOp(grads, self)
+
+    def get_learning_rate(self):
+        lr = self.learning_rate
+        if hasattr(lr, 'get'):
+            return lr.get()
+        return lr
+
+    # flat update -------------------------------------------------------------------
+    mode = 'sgd'
+    n_states = 0
+
+    def hyper(self, step):
+        return dict(lr=self.get_learning_rate(), l2=self.l2reg)
+
+    def dense_update(self, flat, step, dyn=None):
+        KO.optimizer_flat(self.mode, flat.param, flat.grad, flat.s1, flat.s2, flat.shadow,
+                          gscale=flat.gscale, seg_off=flat.seg_off, seg_off_host=flat.seg_host,
+                          norms_ws=flat.norms_ws, dyn=dyn, **self.hyper(step))
+
+    def sparse_update(self, table, state, ids, grads, step):
+        h = self.hyper(step)
+        h.pop('seg_off', None)
+        KO.sparse_update(self.mode if self.mode != 'lamb' else 'adamw', table, ids, grads,
+                         state.get('s1'), state.get('s2'), **h)
+
+    def __deepcopy__(self, memo):
+        return self
+
+
+class SGDOptimizer(Optimizer):
+    def __init__(self, learning_rate=0.01, l2reg=0):
+        super().__init__(learning_rate, l2reg)
+        self.name = 'SGD'
+
+    def get_config(self):
+        return (0, (self.get_learning_rate(),), 1)
+
+
+class MomentumOptimizer(Optimizer):
+    def __init__(self, learning_rate=0.01, momentum=0.9, nesterov=False, l2reg=0):
+        super().__init__(learning_rate, l2reg)
+        self.momentum, self.nesterov = momentum, nesterov
+        self.name = 'Momentum'
+        self.mode = 'nesterov' if nesterov else 'momentum'
+        self.n_states = 1
+
+    def hyper(self, step):
+        return dict(lr=self.get_learning_rate(), l2=self.l2reg, mu=self.momentum)
+
+    def get_config(self):
+        return (1, (self.get_learning_rate(), self.momentum, float(self.nesterov)), 3)
+
+
+class AdaGradOptimizer(Optimizer):
+    def __init__(self, learning_rate=0.01, initial_accumulator_value=0.0, eps=1e-7, l2reg=0):
+        super().__init__(learning_rate, l2reg)
+        self.initial_accumulator_value, self.eps = initial_accumulator_value, eps
+        self.name = 'AdaGrad'
+        self.mode = 'adagrad'
+        self.n_states = 1
+        self.state_init = (initial_accumulator_value, 0.0)
+
+    def hyper(self, step):
+        return dict(lr=self.get_learning_rate(), l2=self.l2reg, eps=self.eps)
+
+    def get_config(self):
+        return (2, (self.get_learning_rate(), self.initial_accumulator_value, self.eps), 3)
+
+
+class AdamOptimizer(Optimizer):
+    def __init__(self, learning_rate=0.01, beta1=0.9, beta2=0.999, epsilon=1e-7, l2reg=0):
+        super().__init__(learning_rate, l2reg)
+        self.beta1, self.beta2, self.epsilon = beta1, beta2, epsilon
+        self.name = 'Adam'
+        self.mode = 'adam'
+        self.n_states = 2
+
+    def hyper(self, step):
+        return dict(lr=self.get_learning_rate(), l2=self.l2reg, beta1=self.beta1, beta2=self.beta2,
+                    beta1t=self.beta1 ** step, beta2t=self.beta2 ** step, eps=self.epsilon)
+
+    def get_config(self):
+        return (3, (self.get_learning_rate(), self.beta1, self.beta2, self.epsilon), 4)
+
+
+class AdamWOptimizer(AdamOptimizer):
+    def __init__(self, learning_rate=0.01, beta1=0.9, beta2=0.999, epsilon=1e-7, weight_decay=0):
+        super().__init__(learning_rate, beta1, beta2, epsilon, 0)
+        self.weight_decay = weight_decay
+        self.name = 'AdamW'
+        self.mode = 'adamw'
+
+    def hyper(self, step):
+        h = super().hyper(step)
+        h['wd'] = self.weight_decay
+        return h
+
+
+class LambOptimizer(AdamWOptimizer):
+    def __init__(self, learning_rate=0.01, beta1=0.9, beta2=0.999, epsilon=1e-7, weight_decay=0):
+        super().__init__(learning_rate, beta1, beta2, epsilon, weight_decay)
+        self.name = 'Lamb'
+        self.mode = 'lamb'
+
+
+# ---------------------------------------------------------------------------
+class FlatGroup(object):
+    """Flat fp32 storage for a set of dense parameters (one per device)."""
+
+    def __init__(self, params: List[Op], values: Dict[Op, torch.Tensor], n_states: int,
+                 state_init=(0.0, 0.0), shadow: bool = False, device=None):
+        self.params = params
+        self.offsets = {}
+        off = 0
+        for p in params:
+            self.offsets[p] = (off, values[p].numel(), tuple(values[p].shape))
+            off += values[p].numel()
+        self.numel = off
+        dev = device
+        self.param = torch.empty(max(off, 1), dtype=torch.float32, device=dev)
+        for p in params:
+            o, n, shp = self.offsets[p]
+            self.param[o:o + n].copy_(values[p].reshape(-1).float())
+        self.grad = torch.zeros_like(self.param)
+        self.s1 = torch.full_like(self.param, state_init[0]) if n_states >= 1 else None
+        self.s2 = torch.full_like(self.param, state_init[1]) if n_states >= 2 else None
+        self.shadow = None
+        if shadow:
+            self.shadow = self.param.to(torch.bfloat16)
+        self.gscale = 1.0
+        offs = [self.offsets[p][0] for p in params] + [off]
+        self.seg_host = offs
+        self.seg_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+        self.norms_ws = torch.zeros(2 * max(len(params), 1), dtype=torch.float32, device=dev)
+
+    def view(self, p, which='param'):
+        o, n, shp = self.offsets[p]
+        buf = getattr(self, which)
+        return buf[o:o + n].view(shp)
+
+
+class Bucket(object):
+    __slots__ = ('start', 'end', 'pending', 'total', 'work')
+
+    def __init__(self, start, end, total):
+        self.start, self.end, self.total = start, end, total
+        self.pending = total
+        self.work = None
+
+
+class OptimizerOp(Op):
+    def __init__(self, grads, optimizer):
+        super().__init__(OptimizerOp, [g for g in grads if g is not None], None)
+        self.name = 'Optimizer_%s' % optimizer.name
+        self.optimizer = optimizer
+        self.all_params = list(optimizer.params)
+        self.param_of_input = [p for p, g in zip(optimizer.params, grads) if g is not None]
+        self.step = 0
+        self.flat: Optional[FlatGroup] = None
+        self.sparse_state = {}
+        self.comm = None
+        self.dp = False
+        self.buckets: List[Bucket] = []
+        self.bucket_of = {}
+        self.bucket_bytes = 32 << 20
+        self.allreduce_mode = 'sum'
+        self.ps_params = set()
+
+    # ----------------------------------------------------------------------------
+    def gradient(self, output_grad):
+        return None
+
+    def infer_shape(self, input_shapes):
+        return None
+
+    def backward_hook(self, config):
+        # data parallel wiring: AllReduce / Hybrid modes all-reduce dense grads
+        self.config = config
+        if config.comm_mode in ('AllReduce', 'Hybrid') and config.nrank > 1:
+            self.dp = True
+            self.comm = config.comm
+        self.bucket_bytes = int(getattr(config, 'bucket_mb', 32) * (1 << 20))
+
+    def forward_hook(self, config):
+        self.ctx = config.context
+        self.on_gpu = ndarray.is_gpu_ctx(self.ctx)
+        self.on_cpu = not self.on_gpu
+
+    def excluded_from_dp(self, p) -> bool:
+        return p.name.startswith('expert') or getattr(p, 'no_dp', False)
+
+    # ---- build flat storage in arrival order (called by the SubExecutor) ---------
+    def setup(self, config, arrival_order: List[int]):
+        if self.flat is not None:
+            return
+        opt = self.optimizer
+        values = config.placeholder_to_arr_map
+        dense, sparse = [], []
+        for i in arrival_order:
+            p = self.param_of_input[i]
+            g = self.inputs[i]
+            if p in self.ps_params:
+                continue
+            if g.use_indexed_slices or getattr(p, 'is_embed', False) and g.use_indexed_slices:
+                sparse.append(p)
+            else:
+                dense.append(p)
+        amp = config.mixed_precision
+        self.flat = FlatGroup(dense, values, opt.n_states, getattr(opt, 'state_init', (0.0, 0.0)),
+                              shadow=amp, device=self.ctx.torch_device if self.ctx else None)
+        for p in dense:
+            values[p] = self.flat.view(p, 'param')
+            if amp:
+                config.compute_values[p] = self.flat.view(p, 'shadow')
+        for p in sparse:
+            st = {}
+            t = values[p]
+            if opt.n_states >= 1:
+                st['s1'] = torch.full_like(t, getattr(opt, 'state_init', (0.0,))[0])
+            if opt.n_states >= 2:
+                st['s2'] = torch.zeros_like(t)
+            self.sparse_state[p] = st
+        # buckets over the flat gradient (contiguous, arrival order)
+        self.slot = {}
+        for i, p in enumerate(self.param_of_input):
+            self.slot[i] = p
+        if self.dp:
+            self._make_buckets(dense)
+
+    def _make_buckets(self, dense):
+        cap = max(self.bucket_bytes // 4, 1)
+        cur_start, cur_n, members = 0, 0, []
+        self.buckets = []
+        for p in dense:
+            if self.excluded_from_dp(p):
+                continue
+            o, n, _ = self.flat.offsets[p]
+            if members and (o != cur_start + cur_n or cur_n + n > cap):
+                self._close_bucket(cur_start, cur_n, members)
+                cur_start, cur_n, members = o, 0, []
+            if not members:
+                cur_start = o
+            members.append(p)
+            cur_n += n
+        if members:
+            self._close_bucket(cur_start, cur_n, members)
+
+    def _close_bucket(self, start, n, members):
+        b = Bucket(start, start + n, len(members))
+        self.buckets.append(b)
+        for p in members:
+            self.bucket_of[p] = b
+
+    # ---- called by the executor as each gradient is produced ---------------------
+    def on_grad_ready(self, i, value):
+        p = self.param_of_input[i]
+        if p in self.ps_params:
+            return
+        if isinstance(value, ndarray.IndexedSlices) or p in self.sparse_state:
+            if self.dp and isinstance(value, ndarray.IndexedSlices) and not self.excluded_from_dp(p):
+                value = _allgather_slices(self.comm, value)
+            self._pending_sparse.append((p, value))
+            return
+        dst = self.flat.view(p, 'grad')
+        if value.shape != dst.shape:
+            value = value.reshape(dst.shape)
+        dst.copy_(value)
+        if self.dp:
+            b = self.bucket_of.get(p)
+            if b is not None:
+                b.pending -= 1
+                if b.pending == 0:
+                    b.work = self.comm.all_reduce(self.flat.grad[b.start:b.end], self.allreduce_mode,
+                                                  async_op=True)
+
+    def begin_step(self):
+        self._pending_sparse = []
+        for b in self.buckets:
+            b.pending = b.total
+            b.work = None
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        self.step += 1
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()
+            elif self.dp:
+                # a bucket whose grads never arrived this step (should not happen)
+                self.comm.all_reduce(self.flat.grad[b.start:b.end], self.allreduce_mode)
+        if self.flat is not None and self.flat.numel > 0:
+            self.optimizer.dense_update(self.flat, self.step, getattr(self, 'dyn', None))
+        for p, sl in self._pending_sparse:
+            table = self.config.placeholder_to_arr_map[p]
+            uniq, merged = sl.deduplicate().indices, sl.values
+            if self.optimizer.mode == 'lamb':
+                pass
+            self.optimizer.sparse_update(table, self.sparse_state.get(p, {}), uniq, merged, self.step)
+        self._pending_sparse = []
+        lr = self.optimizer.learning_rate
+        return None
+
+
+def _allgather_slices(comm, sl):
+    idx = sl._t(sl.indices).reshape(-1).contiguous()
+    val = sl._t(sl.values).reshape(idx.numel(), -1).contiguous()
+    oi = torch.empty((idx.numel() * comm.nrank,), dtype=idx.dtype, device=idx.device)
+    ov = torch.empty((val.shape[0] * comm.nrank, val.shape[1]), dtype=val.dtype, device=val.device)
+    comm.all_gather(oi, idx)
+    comm.all_gather(ov, val)
+    return ndarray.IndexedSlices(oi, ov, sl.dense_shape)

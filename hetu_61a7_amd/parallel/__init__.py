@@ -1,0 +1,4 @@
+"""Parallelism: RCCL communicators, data/pipeline/tensor/expert parallel
+strategies, the dispatch lowering pass and the Galvatron-style planner."""
+from . import comm
+from .strategies import DataParallel, ModelParallel4CNN, ModelParallel4LM, OneWeirdTrick4CNN, Strategy

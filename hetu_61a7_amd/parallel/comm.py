@@ -1,0 +1,180 @@
+"""RCCL communicators over xGMI (reference communicator/mpi_nccl_comm.py:24-342,
+src/communication/mpi_nccl_communication.cu).
+
+One process per GPU.  ``torch.distributed`` with backend ``nccl`` *is* RCCL on
+ROCm; rendezvous uses the TCP store (``MASTER_ADDR``/``MASTER_PORT``) instead of
+MPI, and ``RANK/WORLD_SIZE/LOCAL_RANK`` (or the ``OMPI_COMM_WORLD_*``
+equivalents, so ``mpirun`` still works).  On CPU-only processes the same API
+runs on gloo, which is what the multi-process CPU tests use.
+
+Semantics kept from the reference: AllReduce is a SUM (users scale the lr),
+AllToAll exchanges equal ``numel/nranks`` chunks, sub-group communicators are
+cached per device/rank set.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Dict, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..context import dist_env
+
+_GROUPS: Dict[Tuple[int, ...], 'Communicator'] = {}
+_WORLD: Optional['Communicator'] = None
+
+
+def backend_for_device(dev_is_gpu: bool) -> str:
+    return 'nccl' if dev_is_gpu else 'gloo'
+
+
+def init_process_group(use_gpu: Optional[bool] = None, timeout_s: int = 1800) -> 'Communicator':
+    """Initialise the global communicator (idempotent)."""
+    global _WORLD
+    if _WORLD is not None:
+        return _WORLD
+    rank, world, local = dist_env()
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+    if not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29517')
+        os.environ.setdefault('RANK', str(rank))
+        os.environ.setdefault('WORLD_SIZE', str(world))
+        kw = dict(backend=backend_for_device(use_gpu), rank=rank, world_size=world,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if use_gpu:
+            kw['device_id'] = torch.device('cuda', torch.cuda.current_device())
+        try:
+            dist.init_process_group(**kw)
+        except TypeError:
+            kw.pop('device_id', None)
+            dist.init_process_group(**kw)
+    _WORLD = Communicator(None, use_gpu=use_gpu)
+    return _WORLD
+
+
+def world() -> Optional['Communicator']:
+    return _WORLD
+
+
+def is_initialized() -> bool:
+    return _WORLD is not None
+
+
+def new_group_comm(ranks: Optional[Sequence[int]] = None) -> 'Communicator':
+    """Cached sub-group communicator (every rank must call in the same order)."""
+    w = init_process_group()
+    if ranks is None:
+        return w
+    key = tuple(sorted(int(r) for r in ranks))
+    if len(key) == w.nrank:
+        return w
+    if key not in _GROUPS:
+        _GROUPS[key] = Communicator(key, use_gpu=w.use_gpu)
+    return _GROUPS[key]
+
+
+_RED = {'sum': dist.ReduceOp.SUM, 'max': dist.ReduceOp.MAX, 'min': dist.ReduceOp.MIN,
+        'prod': dist.ReduceOp.PRODUCT}
+
+
+class Communicator(object):
+    """A (sub-)group of ranks: collectives on the calling stream.
+
+    All methods take torch tensors; ``async_op=True`` returns a work handle
+    (RCCL runs on its own stream ordered after the current stream, so compute
+    keeps flowing -- the overlap the reference gets from its nccl_stream).
+    """
+
+    def __init__(self, ranks: Optional[Tuple[int, ...]], use_gpu: bool = True):
+        self.use_gpu = use_gpu
+        self.ranks = ranks
+        self.group = dist.new_group(list(ranks)) if ranks is not None else None
+        self.rank = dist.get_rank(self.group) if (ranks is None or dist.get_rank() in ranks) else -1
+        self.nrank = dist.get_world_size(self.group) if ranks is None or self.rank >= 0 else len(ranks)
+        self.global_rank = dist.get_rank()
+        self.local_rank = dist_env()[2]
+        self.device_id = self.local_rank
+
+    # -- helpers ------------------------------------------------------------------
+    def _g(self, r):
+        """group rank -> global rank"""
+        return r if self.ranks is None else self.ranks[r]
+
+    def _avg(self, t, op):
+        if op == 'mean':
+            t.div_(self.nrank)
+
+    # -- collectives ------------------------------------------------------------------
+    def all_reduce(self, t: torch.Tensor, op: str = 'sum', async_op: bool = False):
+        if op == 'mean':
+            w = dist.all_reduce(t, dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+            if async_op:
+                return _PostDiv(w, t, self.nrank)
+            t.div_(self.nrank)
+            return None
+        return dist.all_reduce(t, _RED[op], group=self.group, async_op=async_op)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        """out = concat over ranks along dim 0."""
+        return dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group, async_op=async_op)
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = 'sum', async_op: bool = False):
+        return dist.reduce_scatter_tensor(out, inp.contiguous(), _RED.get(op, dist.ReduceOp.SUM),
+                                          group=self.group, async_op=async_op)
+
+    def broadcast(self, t: torch.Tensor, root: int = 0, async_op: bool = False):
+        return dist.broadcast(t, self._g(root), group=self.group, async_op=async_op)
+
+    def reduce(self, t: torch.Tensor, root: int = 0, op: str = 'sum', async_op: bool = False):
+        return dist.reduce(t, self._g(root), _RED[op], group=self.group, async_op=async_op)
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        """Equal ``numel/nranks`` chunks along dim 0 (reference AllToAll semantics)."""
+        return dist.all_to_all_single(out, inp.contiguous(), group=self.group, async_op=async_op)
+
+    def send(self, t: torch.Tensor, dst: int):
+        return dist.isend(t.contiguous(), self._g(dst), group=self.group)
+
+    def recv(self, t: torch.Tensor, src: int):
+        return dist.irecv(t, self._g(src), group=self.group)
+
+    def batch_p2p(self, ops):
+        """ops: list of ('send'|'recv', tensor, peer) issued as one RCCL group
+        (reference GroupStart/GroupEnd around pipeline send/recv)."""
+        if not ops:
+            return []
+        p2p = [dist.P2POp(dist.isend if k == 'send' else dist.irecv, t, self._g(p), group=self.group)
+               for k, t, p in ops]
+        return dist.batch_isend_irecv(p2p)
+
+    def barrier(self):
+        if self.use_gpu:
+            dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier(group=self.group)
+
+    def __repr__(self):
+        return 'Communicator(rank=%d, nrank=%d, ranks=%s)' % (self.rank, self.nrank, self.ranks)
+
+
+class _PostDiv(object):
+    def __init__(self, work, t, n):
+        self.work, self.t, self.n = work, t, n
+
+    def wait(self):
+        self.work.wait()
+        self.t.div_(self.n)
+
+
+def destroy():
+    global _WORLD
+    _GROUPS.clear()
+    _WORLD = None
+    if dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,187 @@
+"""HIP kernel numerics vs plain PyTorch fp32 references (run on MI355X)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from hetu_61a7_amd import _base
+from hetu_61a7_amd.kernels import elementwise as KE, norm as KN, softmax as KS, optim as KO
+from hetu_61a7_amd.kernels import pool as KP, reduce as KR, sparse as KSP, layernorm as KLN, dropout as KD
+
+DEV = 'cuda'
+
+
+def test_native_library_loaded():
+    assert _base.has_kernels(), 'libhetu_kernels.so must load on the GPU box'
+
+
+def _tol(dt):
+    return dict(rtol=2e-2, atol=2e-2) if dt == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('op', ['relu', 'sigmoid', 'tanh', 'exp', 'gelu', 'abs', 'neg', 'sqrt', 'add_c', 'mul_c'])
+def test_unary(op, dt):
+    x = torch.randn(1000003, device=DEV).to(dt)
+    if op == 'sqrt':
+        x = x.abs() + 0.1
+    y = KE.unary(op, x, 0.5)
+    ref = KE._ref_unary(op, x.float(), 0.5, 0.0)
+    torch.testing.assert_close(y.float(), ref, **_tol(dt))
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('op', ['add', 'sub', 'mul', 'relu_grad', 'gelu_grad', 'tanh_grad'])
+def test_binary_modes(op, dt):
+    a = torch.randn(512, 768, device=DEV).to(dt)
+    b = torch.randn(512, 768, device=DEV).to(dt)
+    row = torch.randn(768, device=DEV)
+    torch.testing.assert_close(KE.binary(op, a, b).float(), KE._ref_binary(op, a.float(), b.float(), 0.0), **_tol(dt))
+    if op in ('add', 'mul', 'sub'):
+        torch.testing.assert_close(KE.binary(op, a, row).float(),
+                                   KE._ref_binary(op, a.float(), row.to(dt).float(), 0.0), **_tol(dt))
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('relu,res', [(False, False), (True, False), (True, True)])
+def test_batchnorm_nhwc(dt, relu, res):
+    N, C, H, W = 8, 64, 14, 14
+    x = torch.randn(N, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(N, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last) if res else None
+    scale = torch.rand(C, device=DEV) + 0.5
+    bias = torch.randn(C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    y, mean, invstd = KN.bn_forward(x, scale, bias, rm, rv, 0.1, 1e-5, True, relu=relu, residual=r)
+    xf = x.float().requires_grad_(True)
+    sf = scale.clone().requires_grad_(True)
+    bf = bias.clone().requires_grad_(True)
+    rf = r.float().requires_grad_(True) if res else None
+    rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    ref = F.batch_norm(xf, rm2, rv2, sf, bf, True, 0.1, 1e-5)
+    if res:
+        ref = ref + rf
+    if relu:
+        ref = torch.relu(ref)
+    torch.testing.assert_close(y.float(), ref, **_tol(dt))
+    torch.testing.assert_close(rm, rm2, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(rv, rv2, rtol=1e-3, atol=1e-3)
+    dy = torch.randn_like(ref).to(dt).contiguous(memory_format=torch.channels_last)
+    ref.backward(dy.float())
+    dx, ds, db, dres = KN.bn_backward(dy, y, x, scale, mean, invstd, relu=relu, want_dres=res)
+    tol = dict(rtol=5e-2, atol=5e-2) if dt == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(dx.float(), xf.grad, **tol)
+    torch.testing.assert_close(ds, sf.grad, rtol=2e-2, atol=2e-1 if dt == torch.bfloat16 else 1e-2)
+    torch.testing.assert_close(db, bf.grad, rtol=2e-2, atol=2e-1 if dt == torch.bfloat16 else 1e-2)
+    if res:
+        torch.testing.assert_close(dres.float(), rf.grad, **tol)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_softmax_and_ce(dt):
+    x = torch.randn(300, 1000, device=DEV).to(dt)
+    lab = F.one_hot(torch.randint(0, 1000, (300,), device=DEV), 1000).float()
+    torch.testing.assert_close(KS.softmax(x).float(), torch.softmax(x.float(), -1), **_tol(dt))
+    loss, lse = KS.softmax_ce(x, lab)
+    ref = -(lab * torch.log_softmax(x.float(), -1)).sum(-1)
+    torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+    g = torch.rand(300, device=DEV)
+    dx = KS.softmax_ce_backward(x, lab, g, lse)
+    refd = g[:, None] * (torch.softmax(x.float(), -1) - lab)
+    torch.testing.assert_close(dx.float(), refd, **_tol(dt))
+    ids = torch.randint(0, 1000, (300,), device=DEV)
+    ids[::7] = -1
+    ls, lse2 = KS.softmax_ce_sparse(x, ids, -1)
+    valid = ids >= 0
+    refs = torch.where(valid, F.cross_entropy(x.float(), ids.clamp_min(0), reduction='none'), torch.zeros(300, device=DEV))
+    torch.testing.assert_close(ls, refs, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('mode', ['sgd', 'momentum', 'nesterov', 'adagrad', 'adam', 'adamw', 'lamb'])
+def test_flat_optimizer(mode):
+    n = 100003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    s1 = torch.rand(n, device=DEV)
+    s2 = torch.rand(n, device=DEV)
+    sh = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    offs = torch.tensor([0, 1000, 50000, n], dtype=torch.int64, device=DEV)
+    ws = torch.zeros(6, device=DEV)
+    kw = dict(lr=0.01, mu=0.9, beta1=0.9, beta2=0.999, beta1t=0.9 ** 3, beta2t=0.999 ** 3, eps=1e-7, wd=0.01, l2=0.001)
+    P2, G2, A, Bs = p.cpu().clone(), g.cpu().clone(), s1.cpu().clone(), s2.cpu().clone()
+    KO.optimizer_flat(mode, p, g, s1, s2, sh, seg_off=offs, seg_off_host=offs.cpu().tolist(), norms_ws=ws, **kw)
+    KO.optimizer_flat(mode, P2, G2, A, Bs, None, seg_off=None, seg_off_host=offs.cpu().tolist(), **kw)
+    torch.testing.assert_close(p.cpu(), P2, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(sh.float().cpu(), P2, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_pooling(dt):
+    x = torch.randn(4, 64, 56, 56, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    y, idx = KP.maxpool2d(x, 3, 3, 2, 2, 1, 1)
+    xf = x.float().requires_grad_(True)
+    ref = F.max_pool2d(xf, 3, 2, 1)
+    torch.testing.assert_close(y.float(), ref, **_tol(dt))
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    dx = KP.maxpool2d_backward(dy.to(dt), idx, x.shape, 3, 3, 2, 2, 1, 1)
+    torch.testing.assert_close(dx.float(), xf.grad, **_tol(dt))
+    ya = KP.avgpool2d(x, 2, 2, 2, 2, 0, 0)
+    torch.testing.assert_close(ya.float(), F.avg_pool2d(x.float(), 2, 2), **_tol(dt))
+    gp = KR.global_avg_pool(x)
+    torch.testing.assert_close(gp.float(), x.float().mean((2, 3)), **_tol(dt))
+
+
+def test_reductions():
+    x = torch.randn(64, 1000, 37, device=DEV)
+    torch.testing.assert_close(KR.reduce_mid(x), x.sum(1), rtol=1e-4, atol=1e-3)
+    y = torch.randn(5000, 300, device=DEV)
+    torch.testing.assert_close(KR.reduce_last(y), y.sum(1), rtol=1e-4, atol=1e-3)
+    g = torch.randn(32, 16, 128, device=DEV)
+    torch.testing.assert_close(KR.sum_to_shape(g, (128,)), g.sum((0, 1)), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_embedding_gather_scatter(dt):
+    table = torch.randn(10000, 128, device=DEV).to(dt)
+    ids = torch.randint(-5, 10005, (4096,), device=DEV)
+    out = KSP.gather_rows(table, ids)
+    valid = (ids >= 0) & (ids < 10000)
+    ref = torch.where(valid[:, None], table[ids.clamp(0, 9999)].float(), torch.zeros(1, device=DEV))
+    torch.testing.assert_close(out.float(), ref)
+    dst = torch.zeros(10000, 128, device=DEV)
+    src = torch.randn(4096, 128, device=DEV)
+    KSP.scatter_add_rows(dst, ids, src)
+    ref2 = torch.zeros(10000, 128, device=DEV)
+    ref2.index_add_(0, ids[valid], src[valid])
+    torch.testing.assert_close(dst, ref2, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_layernorm(dt):
+    x = torch.randn(2048, 768, device=DEV).to(dt)
+    gm = torch.rand(768, device=DEV) + 0.5
+    bt = torch.randn(768, device=DEV)
+    y, mean, rstd = KLN.layer_norm(x, gm, bt, 1e-5)
+    xf = x.float().requires_grad_(True)
+    gf, bf = gm.clone().requires_grad_(True), bt.clone().requires_grad_(True)
+    ref = F.layer_norm(xf, (768,), gf, bf, 1e-5)
+    torch.testing.assert_close(y.float(), ref, **_tol(dt))
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    dx, dg, db = KLN.layer_norm_backward(dy.to(dt), x, gm, mean, rstd)
+    tol = dict(rtol=5e-2, atol=5e-2) if dt == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(dx.float(), xf.grad, **tol)
+    torch.testing.assert_close(dg, gf.grad, rtol=2e-2, atol=5e-1 if dt == torch.bfloat16 else 1e-2)
+    torch.testing.assert_close(db, bf.grad, rtol=2e-2, atol=5e-1 if dt == torch.bfloat16 else 1e-2)
+
+
+def test_dropout_mask_recompute():
+    x = torch.ones(1 << 20, device=DEV)
+    y1 = KD.dropout(x, 0.7, 1234)
+    y2 = KD.dropout(x, 0.7, 1234)
+    assert torch.equal(y1, y2)
+    keep = (y1 != 0).float().mean().item()
+    assert abs(keep - 0.7) < 0.01
+    torch.testing.assert_close(y1[y1 != 0], torch.full_like(y1[y1 != 0], 1 / 0.7))

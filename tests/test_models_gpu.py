@@ -1,0 +1,71 @@
+"""End-to-end model steps on the GPU (native HIP kernels) vs the CPU backend."""
+import numpy as np
+import pytest
+import torch
+
+import hetu_61a7_amd as ht
+
+pytestmark = pytest.mark.gpu
+
+
+def _logreg(ctx, X, Y, steps=10):
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    W = ht.init.zeros((784, 10), name='W')
+    b = ht.init.zeros((10,), name='b')
+    loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.linear_op(x, W, b), y_), [0])
+    train = ht.optim.SGDOptimizer(0.1).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ctx)
+    return [float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]) for _ in range(steps)]
+
+
+def test_logreg_gpu_matches_cpu():
+    rng = np.random.RandomState(0)
+    X = rng.randn(128, 784).astype(np.float32)
+    Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 128)]
+    a = _logreg(ht.cpu(0), X, Y)
+    b = _logreg(ht.gpu(0), X, Y)
+    np.testing.assert_allclose(a, b, rtol=1e-4)
+
+
+def test_resnet50_bf16_step():
+    from hetu_61a7_amd.models import resnet50_imagenet
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    loss, logits = resnet50_imagenet(x, y_, 1000)
+    train = ht.optim.MomentumOptimizer(0.05, 0.9).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16')
+    rng = np.random.RandomState(0)
+    X = rng.randn(8, 3, 224, 224).astype(np.float32)
+    Y = np.eye(1000, dtype=np.float32)[rng.randint(0, 1000, 8)]
+    ls = [float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]) for _ in range(5)]
+    assert np.isfinite(ls).all()
+    assert ls[-1] < ls[0]
+
+
+def test_resnet_cifar_gpu_vs_cpu_fp32():
+    from hetu_61a7_amd.models.resnet import resnet_cifar
+    rng = np.random.RandomState(1)
+    X = rng.randn(8, 3, 32, 32).astype(np.float32)
+    Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 8)]
+    res = []
+    for ctx in (ht.cpu(0), ht.gpu(0)):
+        x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+        loss, _ = resnet_cifar(x, y_, 18, 10)
+        train = ht.optim.SGDOptimizer(0.01).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ctx, seed=7)
+        res.append([float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]) for _ in range(3)])
+    np.testing.assert_allclose(res[0], res[1], rtol=2e-3, atol=2e-3)
+
+
+def test_hipgraph_mlp_matches_eager():
+    rng = np.random.RandomState(2)
+    X = rng.randn(64, 3072).astype(np.float32)
+    Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 64)]
+    out = []
+    for g in (False, True):
+        x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+        from hetu_61a7_amd.models import mlp
+        loss, _ = mlp(x, y_)
+        train = ht.optim.AdamOptimizer(1e-3).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, use_hipgraph=g)
+        out.append([float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]) for _ in range(8)])
+    np.testing.assert_allclose(out[0], out[1], rtol=1e-4, atol=1e-5)

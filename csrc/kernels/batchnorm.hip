@@ -26,7 +26,7 @@ static BnGeom bn_geom(int64_t M, int C, int vec) {
   g.W = cv < 64 ? cv : 64;
   g.RP = 256 / g.W;
   g.tiles = (cv + g.W - 1) / g.W;
-  int want = (int)((2048 + g.tiles - 1) / g.tiles);
+  int want = (int)((1024 + g.tiles - 1) / g.tiles);
   int64_t max_chunks = (M + g.RP - 1) / g.RP;
   if (want > max_chunks) want = (int)max_chunks;
   if (want < 1) want = 1;
@@ -87,42 +87,60 @@ __global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x,
 }
 
 // Chan merge of chunk partials; writes save_mean/save_invstd, running stats and
-// folded affine (a = scale*invstd, b = bias - mean*a).
-__global__ void bn_stats_finalize(const float* __restrict__ ws_mean, const float* __restrict__ ws_m2,
+// folded affine (a = scale*invstd, b = bias - mean*a).  Block = 16 channels x 16
+// lanes; each lane merges chunks/16 partials, lanes are merged through LDS.
+__global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict__ ws_mean, const float* __restrict__ ws_m2,
                                   int chunks, int64_t rows_per_chunk, int64_t M, int C,
                                   const float* __restrict__ scale, const float* __restrict__ bias,
                                   float* __restrict__ run_mean, float* __restrict__ run_var,
                                   float factor, float eps, float* __restrict__ save_mean,
                                   float* __restrict__ save_invstd, float* __restrict__ fold_a,
                                   float* __restrict__ fold_b) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float sh_n[256], sh_m[256], sh_q[256];
+  const int cl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int p = 0; p < chunks; ++p) {
-    int64_t r0 = (int64_t)p * rows_per_chunk;
-    int64_t r1 = r0 + rows_per_chunk;
-    if (r1 > M) r1 = M;
-    float nb = (float)(r1 > r0 ? r1 - r0 : 0);
-    if (nb <= 0.f) continue;
-    float mb = ws_mean[(int64_t)p * C + c], qb = ws_m2[(int64_t)p * C + c];
-    float nn = n + nb;
-    float d = mb - mean;
-    mean += d * (nb / nn);
-    m2 += qb + d * d * (n * nb / nn);
-    n = nn;
+  if (c < C) {
+    for (int p = lane; p < chunks; p += 16) {
+      int64_t r0 = (int64_t)p * rows_per_chunk;
+      int64_t r1 = r0 + rows_per_chunk;
+      if (r1 > M) r1 = M;
+      float nb = (float)(r1 > r0 ? r1 - r0 : 0);
+      if (nb <= 0.f) continue;
+      float mb = ws_mean[(int64_t)p * C + c], qb = ws_m2[(int64_t)p * C + c];
+      float nn = n + nb;
+      float d = mb - mean;
+      mean += d * (nb / nn);
+      m2 += qb + d * d * (n * nb / nn);
+      n = nn;
+    }
   }
-  float var = n > 0.f ? m2 / n : 0.f;
-  float invstd = rsqrtf(var + eps);
-  save_mean[c] = mean;
-  save_invstd[c] = invstd;
-  if (run_mean != nullptr) {
-    float unb = n > 1.f ? m2 / (n - 1.f) : var;
-    run_mean[c] = (1.f - factor) * run_mean[c] + factor * mean;
-    run_var[c] = (1.f - factor) * run_var[c] + factor * unb;
+  sh_n[threadIdx.x] = n; sh_m[threadIdx.x] = mean; sh_q[threadIdx.x] = m2;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    for (int l = 1; l < 16; ++l) {
+      const int t = l * 16 + cl;
+      float nb = sh_n[t];
+      if (nb <= 0.f) continue;
+      float nn = n + nb;
+      float d = sh_m[t] - mean;
+      mean += d * (nb / nn);
+      m2 += sh_q[t] + d * d * (n * nb / nn);
+      n = nn;
+    }
+    float var = n > 0.f ? m2 / n : 0.f;
+    float invstd = rsqrtf(var + eps);
+    save_mean[c] = mean;
+    save_invstd[c] = invstd;
+    if (run_mean != nullptr) {
+      float unb = n > 1.f ? m2 / (n - 1.f) : var;
+      run_mean[c] = (1.f - factor) * run_mean[c] + factor * mean;
+      run_var[c] = (1.f - factor) * run_var[c] + factor * unb;
+    }
+    float a = scale[c] * invstd;
+    fold_a[c] = a;
+    fold_b[c] = bias[c] - mean * a;
   }
-  float a = scale[c] * invstd;
-  fold_a[c] = a;
-  fold_b[c] = bias[c] - mean * a;
 }
 
 // inference: fold running stats
@@ -225,28 +243,36 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
   }
 }
 
-__global__ void bn_bwd_finalize(const float* __restrict__ ws_sdy, const float* __restrict__ ws_sdyx,
+__global__ void __launch_bounds__(256) bn_bwd_finalize(const float* __restrict__ ws_sdy, const float* __restrict__ ws_sdyx,
                                 int chunks, int64_t M, int C, const float* __restrict__ scale,
                                 const float* __restrict__ mean, const float* __restrict__ invstd,
                                 float* __restrict__ dscale, float* __restrict__ dbias,
                                 float* __restrict__ cA, float* __restrict__ cB,
                                 float* __restrict__ cC) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float s1[256], s2[256];
+  const int cl = threadIdx.x & 15, lane = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float sdy = 0.f, sdyx = 0.f;
-  for (int p = 0; p < chunks; ++p) {
-    sdy += ws_sdy[(int64_t)p * C + c];
-    sdyx += ws_sdyx[(int64_t)p * C + c];
+  if (c < C) {
+    for (int p = lane; p < chunks; p += 16) {
+      sdy += ws_sdy[(int64_t)p * C + c];
+      sdyx += ws_sdyx[(int64_t)p * C + c];
+    }
   }
-  if (dscale) dscale[c] = sdyx;
-  if (dbias) dbias[c] = sdy;
-  const float invM = 1.f / (float)M;
-  const float is = invstd[c];
-  const float k1 = scale[c] * is;
-  const float B = -k1 * is * sdyx * invM;
-  cA[c] = k1;
-  cB[c] = B;
-  cC[c] = -k1 * sdy * invM - mean[c] * B;
+  s1[threadIdx.x] = sdy; s2[threadIdx.x] = sdyx;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    for (int l = 1; l < 16; ++l) { sdy += s1[l * 16 + cl]; sdyx += s2[l * 16 + cl]; }
+    if (dscale) dscale[c] = sdyx;
+    if (dbias) dbias[c] = sdy;
+    const float invM = 1.f / (float)M;
+    const float is = invstd[c];
+    const float k1 = scale[c] * is;
+    const float B = -k1 * is * sdyx * invM;
+    cA[c] = k1;
+    cB[c] = B;
+    cC[c] = -k1 * sdy * invM - mean[c] * B;
+  }
 }
 
 template <typename T, bool RELU, bool DRES>
@@ -304,7 +330,7 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
     float* wq = ws + (int64_t)g.chunks * C;
     hipLaunchKernelGGL(bn_stats_partial<T>, dim3(g.chunks, g.tiles), dim3(256), 0, st,
                        (const T*)x, M, C, g.W, g.RP, g.rows_per_chunk, wm, wq);
-    hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 255) / 256), dim3(256), 0, st, wm, wq,
+    hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 15) / 16), dim3(256), 0, st, wm, wq,
                        g.chunks, g.rows_per_chunk, M, C, scale, bias, run_mean, run_var, factor,
                        eps, save_mean, save_invstd, fa, fb);
   } else {
@@ -360,7 +386,7 @@ static int bn_bwd_impl(const void* dy, const void* y, const void* x, void* dx, v
     hipLaunchKernelGGL((bn_bwd_partial<T, false>), dim3(g.chunks, g.tiles), dim3(256), 0, st,
                        (const T*)dy, (const T*)y, (const T*)x, mean, invstd, M, C, g.W, g.RP,
                        g.rows_per_chunk, w1, w2);
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, w1, w2, g.chunks, M,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, w1, w2, g.chunks, M,
                      C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
   int64_t nvec = M * C / V;
   int grid = stream_grid(nvec, 256, 4);

@@ -23,11 +23,18 @@ class BaseInit(object):
         return self.generate(seed + node.id, device)
 
     def generate(self, seed, device='cpu') -> torch.Tensor:
-        t = torch.empty(self.shape, dtype=torch.float32, device=device)
-        g = torch.Generator(device=device)
+        # Values are drawn on the host (same numbers on every device type and every
+        # data-parallel rank) unless the tensor is huge (embedding tables), where
+        # the device's own counter-based generator fills HBM directly.
+        numel = 1
+        for s in self.shape:
+            numel *= int(s)
+        gen_dev = torch.device('cpu') if numel < (1 << 26) else torch.device(device)
+        t = torch.empty(self.shape, dtype=torch.float32, device=gen_dev)
+        g = torch.Generator(device=gen_dev)
         g.manual_seed(int(seed) & 0x7FFFFFFF)
         self.init_on_device(t, g)
-        return t
+        return t.to(device)
 
     def init_on_device(self, t, gen):
         raise NotImplementedError

@@ -171,6 +171,12 @@ class HetuConfig(object):
             elif world > 1 and dist_strategy is None and pipeline is None:
                 comm_mode = None
         self.comm_mode = comm_mode
+        if ndarray.is_gpu_ctx(self.context) and not torch.cuda.is_available():
+            # CPU-only process (tests / gloo rehearsal of the distributed path)
+            self.context = ndarray.cpu(0)
+            for n in find_topo_sort(eval_node_list):
+                if ndarray.is_gpu_ctx(n.ctx):
+                    n.ctx = self.context
         if self.context is not None and ndarray.is_gpu_ctx(self.context) and torch.cuda.is_available():
             torch.cuda.set_device(self.context.device_id)
 
@@ -274,6 +280,10 @@ class Executor(object):
                 self.subexecutor[k] = make_pipeline_subexecutor(config.pipeline, k, v, config)
             else:
                 self.subexecutor[k] = SubExecutor(k, v, config)
+        if timing:
+            for sub in self.subexecutor.values():
+                if hasattr(sub, 'enable_timer'):
+                    sub.enable_timer(timing)
 
     # reference API ------------------------------------------------------------------------
     @property
@@ -508,6 +518,9 @@ class SubExecutor(object):
             vals[n] = r
             if r is not None:
                 shapes[n] = _shape_of(r)
+                if _CHECK_LAYOUT and isinstance(r, torch.Tensor) and r.dim() == 4 and r.is_cuda \
+                        and not r.is_contiguous(memory_format=torch.channels_last):
+                    _LAYOUT_MISSES[n.op_type] = _LAYOUT_MISSES.get(n.op_type, 0) + 1
             hooks = self.grad_hooks.get(n)
             if hooks:
                 for op, j in hooks:
@@ -553,6 +566,14 @@ class SubExecutor(object):
     def clearTimer(self):
         if self.timer is not None:
             self.timer.clear()
+
+
+_CHECK_LAYOUT = os.environ.get('HETU_CHECK_LAYOUT', '0') == '1'
+_LAYOUT_MISSES = {}
+
+
+def layout_report():
+    return dict(_LAYOUT_MISSES)
 
 
 def _shape_of(v):

@@ -1,0 +1,81 @@
+"""Multi-process data-parallel tests on CPU (gloo, world_size 2).
+
+Parallel-equivalence pattern of the reference (examples/runner/parallel/
+validate_results.py): DP with SUM all-reduce and lr/N must reproduce the
+single-process baseline on the concatenated batch.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mlp_losses(X, Y, lr, steps, dp=False, bucket_mb=32):
+    import hetu_61a7_amd as ht
+    rng = np.random.RandomState(11)
+    w1 = (rng.randn(20, 32) * 0.3).astype(np.float32)
+    w2 = (rng.randn(32, 4) * 0.3).astype(np.float32)
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    W1 = ht.Variable(name='w1', value=w1)
+    B1 = ht.Variable(name='b1', value=np.zeros(32, np.float32))
+    W2 = ht.Variable(name='w2', value=w2)
+    h = ht.relu_op(ht.linear_op(x, W1, B1))
+    loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(h, W2), y_), [0])
+    train = ht.optim.MomentumOptimizer(lr, 0.9).minimize(loss)
+    kw = dict(bucket_mb=bucket_mb)
+    if dp:
+        ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'), **kw)
+    else:
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.cpu(0), **kw)
+    out = []
+    for _ in range(steps):
+        out.append(float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]))
+    params = {n.name: v.numpy().copy() for n, v in ex.config.placeholder_to_arr_map.items() if n.trainable}
+    return out, params
+
+
+def _worker(rank, world, port, X, Y, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), HETU_USE_CONFIG='0')
+    n = X.shape[0] // world
+    sl = slice(rank * n, (rank + 1) * n)
+    # tiny bucket so several buckets are exercised
+    losses, params = _mlp_losses(X[sl], Y[sl], 0.1 / world, 5, dp=True, bucket_mb=0.001)
+    q.put((rank, losses, params))
+    from hetu_61a7_amd.parallel import comm
+    comm.destroy()
+
+
+def test_dp_allreduce_matches_single_process():
+    rng = np.random.RandomState(0)
+    X = rng.randn(32, 20).astype(np.float32)
+    Y = np.eye(4, dtype=np.float32)[rng.randint(0, 4, 32)]
+    # baseline: one process on the full batch (mean loss), lr 0.1
+    _, base_params = _mlp_losses(X, Y, 0.1, 5)
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, X, Y, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    res.sort()
+    # SUM all-reduce of per-shard mean-loss grads with lr/N == full-batch mean with lr
+    for name, v in base_params.items():
+        np.testing.assert_allclose(res[0][2][name], v, rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(res[1][2][name], v, rtol=1e-4, atol=1e-5)

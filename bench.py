@@ -103,8 +103,8 @@ def main():
         dt_s = float(t.item())
     ms = dt_s * 1000.0 / args.steps
     if args.op_profile and args.model == 'resnet50' and rank == 0:
-        s = ex.logOut(args.op_profile + '.node', log_level='node', clear=False)
-        t = ex.logOut(args.op_profile, log_level='type')
+        s = ex.logOut(args.op_profile + '.node', log_level='node', clear=False, name='train')
+        t = ex.logOut(args.op_profile, log_level='type', name='train')
         print('op-type ms/step:', sorted(t.items(), key=lambda kv: -kv[1])[:25], file=sys.stderr)
         from hetu_61a7_amd.ops.executor import layout_report
         print('non-channels-last 4D outputs:', layout_report(), file=sys.stderr)

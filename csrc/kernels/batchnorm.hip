@@ -76,70 +76,54 @@ __global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x,
       Q += sh_q[tt * V + lane_i];
     }
     const int c = blockIdx.y * W * V + c_local;
-    const float n = (float)(r1 > r0 ? (r1 - r0) : 0);
     if (c < C) {
-      float mean = n > 0 ? S / n : 0.f;
-      float m2 = n > 0 ? fmaxf(Q - S * mean, 0.f) : 0.f;
-      ws_mean[(int64_t)blockIdx.x * C + c] = mean;
-      ws_m2[(int64_t)blockIdx.x * C + c] = m2;
+      ws_mean[(int64_t)blockIdx.x * C + c] = S;  // raw per-chunk sums; merged in fp64
+      ws_m2[(int64_t)blockIdx.x * C + c] = Q;
     }
   }
 }
 
-// Chan merge of chunk partials; writes save_mean/save_invstd, running stats and
-// folded affine (a = scale*invstd, b = bias - mean*a).  Block = 16 channels x 16
-// lanes; each lane merges chunks/16 partials, lanes are merged through LDS.
-__global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict__ ws_mean, const float* __restrict__ ws_m2,
+// Merge of the chunk sums in fp64 (mean = S/n, var = Q/n - mean^2); writes
+// save_mean/save_invstd, running stats and the folded affine a = scale*invstd,
+// b = bias - mean*a.  Block = 16 channels x 16 lanes, independent loads per lane.
+__global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict__ ws_s, const float* __restrict__ ws_q,
                                   int chunks, int64_t rows_per_chunk, int64_t M, int C,
                                   const float* __restrict__ scale, const float* __restrict__ bias,
                                   float* __restrict__ run_mean, float* __restrict__ run_var,
                                   float factor, float eps, float* __restrict__ save_mean,
                                   float* __restrict__ save_invstd, float* __restrict__ fold_a,
                                   float* __restrict__ fold_b) {
-  __shared__ float sh_n[256], sh_m[256], sh_q[256];
+  __shared__ double sh_s[256], sh_q[256];
   const int cl = threadIdx.x & 15, lane = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
+  double S = 0.0, Q = 0.0;
   if (c < C) {
+#pragma unroll 4
     for (int p = lane; p < chunks; p += 16) {
-      int64_t r0 = (int64_t)p * rows_per_chunk;
-      int64_t r1 = r0 + rows_per_chunk;
-      if (r1 > M) r1 = M;
-      float nb = (float)(r1 > r0 ? r1 - r0 : 0);
-      if (nb <= 0.f) continue;
-      float mb = ws_mean[(int64_t)p * C + c], qb = ws_m2[(int64_t)p * C + c];
-      float nn = n + nb;
-      float d = mb - mean;
-      mean += d * (nb / nn);
-      m2 += qb + d * d * (n * nb / nn);
-      n = nn;
+      S += (double)ws_s[(int64_t)p * C + c];
+      Q += (double)ws_q[(int64_t)p * C + c];
     }
   }
-  sh_n[threadIdx.x] = n; sh_m[threadIdx.x] = mean; sh_q[threadIdx.x] = m2;
+  sh_s[threadIdx.x] = S;
+  sh_q[threadIdx.x] = Q;
   __syncthreads();
   if (lane == 0 && c < C) {
-    for (int l = 1; l < 16; ++l) {
-      const int t = l * 16 + cl;
-      float nb = sh_n[t];
-      if (nb <= 0.f) continue;
-      float nn = n + nb;
-      float d = sh_m[t] - mean;
-      mean += d * (nb / nn);
-      m2 += sh_q[t] + d * d * (n * nb / nn);
-      n = nn;
-    }
-    float var = n > 0.f ? m2 / n : 0.f;
-    float invstd = rsqrtf(var + eps);
-    save_mean[c] = mean;
+    for (int l = 1; l < 16; ++l) { S += sh_s[l * 16 + cl]; Q += sh_q[l * 16 + cl]; }
+    const double n = (double)M;
+    const double mean = S / n;
+    double var = Q / n - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = rsqrtf((float)var + eps);
+    save_mean[c] = (float)mean;
     save_invstd[c] = invstd;
     if (run_mean != nullptr) {
-      float unb = n > 1.f ? m2 / (n - 1.f) : var;
-      run_mean[c] = (1.f - factor) * run_mean[c] + factor * mean;
+      const float unb = n > 1.0 ? (float)(var * n / (n - 1.0)) : (float)var;
+      run_mean[c] = (1.f - factor) * run_mean[c] + factor * (float)mean;
       run_var[c] = (1.f - factor) * run_var[c] + factor * unb;
     }
-    float a = scale[c] * invstd;
-    fold_a[c] = a;
-    fold_b[c] = bias[c] - mean * a;
+    const float aa = scale[c] * invstd;
+    fold_a[c] = aa;
+    fold_b[c] = bias[c] - (float)mean * aa;
   }
 }
 
@@ -181,11 +165,13 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
 
 // ---------------------------------------------------------------------------
 // backward
-template <typename T, bool RELU>
+template <typename T, int RELU>
 __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ y,
                                                        const T* __restrict__ x,
                                                        const float* __restrict__ mean,
-                                                       const float* __restrict__ invstd, int64_t M,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ fa,
+                                                       const float* __restrict__ fb, int64_t M,
                                                        int C, int W, int RP, int64_t rows_per_chunk,
                                                        float* __restrict__ ws_sdy,
                                                        float* __restrict__ ws_sdyx) {
@@ -199,22 +185,28 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
   int64_t r1 = r0 + rows_per_chunk;
   if (r1 > M) r1 = M;
-  float s[V], q[V], mu[V], is[V];
+  float s[V], q[V], mu[V], is[V], ka[V], kb[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; }
   if (active) {
 #pragma unroll
-    for (int i = 0; i < V; ++i) { mu[i] = mean[vc * V + i]; is[i] = invstd[vc * V + i]; }
+    for (int i = 0; i < V; ++i) {
+      mu[i] = mean[vc * V + i]; is[i] = invstd[vc * V + i];
+      if (RELU == 2) { ka[i] = fa[vc * V + i]; kb[i] = fb[vc * V + i]; }
+    }
     for (int64_t r = r0 + rsub; r < r1; r += RP) {
       const int64_t off = r * C + (int64_t)vc * V;
       float g[V], xv[V];
       load_vec<T>(dy + off, g);
       load_vec<T>(x + off, xv);
-      if (RELU) {
+      if (RELU == 1) {
         float yv[V];
         load_vec<T>(y + off, yv);
 #pragma unroll
         for (int i = 0; i < V; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+      } else if (RELU == 2) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) g[i] = (xv[i] * ka[i] + kb[i]) > 0.f ? g[i] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -275,12 +267,14 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize(const float* __restrict__
   }
 }
 
-template <typename T, bool RELU, bool DRES>
+template <typename T, int RELU, bool DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ y,
                                                      const T* __restrict__ x,
                                                      const float* __restrict__ cA,
                                                      const float* __restrict__ cB,
                                                      const float* __restrict__ cC,
+                                                     const float* __restrict__ fa,
+                                                     const float* __restrict__ fb,
                                                      T* __restrict__ dx, T* __restrict__ dres,
                                                      int64_t nvec, int C) {
   constexpr int V = Vec<T>::N;
@@ -291,11 +285,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
     float g[V], xv[V];
     load_vec<T>(dy + i * V, g);
     load_vec<T>(x + i * V, xv);
-    if (RELU) {
+    if (RELU == 1) {
       float yv[V];
       load_vec<T>(y + i * V, yv);
 #pragma unroll
       for (int k = 0; k < V; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    } else if (RELU == 2) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) g[k] = (xv[k] * fa[c0 + k] + fb[c0 + k]) > 0.f ? g[k] : 0.f;
     }
     if (DRES) store_vec<T>(dres + i * V, g);
     float o[V];
@@ -309,10 +306,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
 
 using namespace hetu;
 
-// workspace floats needed: 2 * chunks * C + 2 * C  (partials + fold)
+// workspace floats needed: 2 * chunks * C + 5 * C  (partials + fold/bwd coefficients)
 HETU_API int64_t hetu_bn_workspace_floats(int64_t M, int C, int is_bf16) {
   BnGeom g = bn_geom(M, C, is_bf16 ? 8 : 4);
-  return 2 * (int64_t)g.chunks * C + 3 * (int64_t)C;
+  return 2 * (int64_t)g.chunks * C + 5 * (int64_t)C;
 }
 
 template <typename T>
@@ -366,10 +363,40 @@ HETU_API int hetu_bn_fwd(const void* x, const void* res, void* y, int64_t M, int
                             save_mean, save_invstd, ws, relu, training, st);
 }
 
+template <typename T, int RELU>
+static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const T* x, T* dx, T* dres,
+                          int64_t M, int C, const float* mean, const float* invstd,
+                          const float* fa, const float* fb, float* w1, float* w2, float* cA,
+                          float* cB, float* cC, const float* scale, float* dscale, float* dbias,
+                          hipStream_t st) {
+  constexpr int V = Vec<T>::N;
+  hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, x,
+                     mean, invstd, fa, fb, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, w1, w2, g.chunks, M,
+                     C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
+  int64_t nvec = M * C / V;
+  int grid = stream_grid(nvec, 256, 4);
+  if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, fa, fb, dx, dres, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, fa, fb, dx, dres, nvec, C);
+}
+
+__global__ void bn_fold_k(const float* __restrict__ scale, const float* __restrict__ bias,
+                          const float* __restrict__ mean, const float* __restrict__ invstd, int C,
+                          float* __restrict__ fa, float* __restrict__ fb) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a = scale[c] * invstd[c];
+  fa[c] = a;
+  fb[c] = bias[c] - mean[c] * a;
+}
+
 template <typename T>
 static int bn_bwd_impl(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M,
-                       int C, const float* scale, const float* mean, const float* invstd,
-                       float* dscale, float* dbias, float* ws, int relu, hipStream_t st) {
+                       int C, const float* scale, const float* bias, const float* mean,
+                       const float* invstd, float* dscale, float* dbias, float* ws, int relu,
+                       hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
@@ -378,38 +405,29 @@ static int bn_bwd_impl(const void* dy, const void* y, const void* x, void* dx, v
   float* cA = ws + 2 * (int64_t)g.chunks * C;
   float* cB = cA + C;
   float* cC = cB + C;
-  if (relu)
-    hipLaunchKernelGGL((bn_bwd_partial<T, true>), dim3(g.chunks, g.tiles), dim3(256), 0, st,
-                       (const T*)dy, (const T*)y, (const T*)x, mean, invstd, M, C, g.W, g.RP,
-                       g.rows_per_chunk, w1, w2);
-  else
-    hipLaunchKernelGGL((bn_bwd_partial<T, false>), dim3(g.chunks, g.tiles), dim3(256), 0, st,
-                       (const T*)dy, (const T*)y, (const T*)x, mean, invstd, M, C, g.W, g.RP,
-                       g.rows_per_chunk, w1, w2);
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, w1, w2, g.chunks, M,
-                     C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
-  int64_t nvec = M * C / V;
-  int grid = stream_grid(nvec, 256, 4);
+  float* fa = cC + C;
+  float* fb = fa + C;
   const T *dyr = (const T*)dy, *yr = (const T*)y, *xr = (const T*)x;
   T *dxr = (T*)dx, *drr = (T*)dres;
-  if (relu && dres)
-    hipLaunchKernelGGL((bn_bwd_apply<T, true, true>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
-  else if (relu)
-    hipLaunchKernelGGL((bn_bwd_apply<T, true, false>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
-  else if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply<T, false, true>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply<T, false, false>), dim3(grid), dim3(256), 0, st, dyr, yr, xr, cA, cB, cC, dxr, drr, nvec, C);
+  // mask source: the saved output y when a residual was added (mask depends on it),
+  // otherwise recomputed from x (one less stream to read)
+  int mode = !relu ? 0 : ((dres || !bias) ? 1 : 2);
+  if (mode == 2)
+    hipLaunchKernelGGL(bn_fold_k, dim3((C + 255) / 256), dim3(256), 0, st, scale, bias, mean, invstd, C, fa, fb);
+  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, fa, fb, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, fa, fb, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  else bn_bwd_launch<T, 2>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, fa, fb, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
   HETU_LAUNCH_CHECK();
   return 0;
 }
 
 // dy,y,x,dx,dres: [M,C]; y only read when relu; dres may be null
+// bias may be null (then the ReLU mask is read from y)
 HETU_API int hetu_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres,
-                         int64_t M, int C, int is_bf16, const float* scale, const float* mean,
-                         const float* invstd, float* dscale, float* dbias, float* ws, int relu,
-                         hipStream_t st) {
+                         int64_t M, int C, int is_bf16, const float* scale, const float* bias,
+                         const float* mean, const float* invstd, float* dscale, float* dbias,
+                         float* ws, int relu, hipStream_t st) {
   if (is_bf16)
-    return bn_bwd_impl<bf16>(dy, y, x, dx, dres, M, C, scale, mean, invstd, dscale, dbias, ws, relu, st);
-  return bn_bwd_impl<float>(dy, y, x, dx, dres, M, C, scale, mean, invstd, dscale, dbias, ws, relu, st);
+    return bn_bwd_impl<bf16>(dy, y, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
+  return bn_bwd_impl<float>(dy, y, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
 }

@@ -84,7 +84,7 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
     return y, mean.float(), invstd.float()
 
 
-def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=False):
+def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=False, bias=None):
     """Returns (dx, dscale, dbias, dres)."""
     C = x.shape[1]
     if native(x) and x.dtype in (torch.float32, torch.bfloat16):
@@ -104,10 +104,11 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
             dscale = torch.empty(C, dtype=torch.float32, device=x.device)
             dbias = torch.empty(C, dtype=torch.float32, device=x.device)
             ws = _ws(M, C, is_bf16(x), x.device)
-            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, I32, P])
+            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P])
             check(f(dy.data_ptr(), y.data_ptr() if relu else None, x.data_ptr(), dx.data_ptr(),
                     dres.data_ptr() if dres is not None else None, M, C, is_bf16(x),
-                    scale.data_ptr(), save_mean.data_ptr(), save_invstd.data_ptr(),
+                    scale.data_ptr(), bias.float().contiguous().data_ptr() if bias is not None else None,
+                    save_mean.data_ptr(), save_invstd.data_ptr(),
                     dscale.data_ptr(), dbias.data_ptr(), ws.data_ptr(), int(relu), stream_ptr()),
                   'bn_bwd')
             return dx, dscale, dbias, dres

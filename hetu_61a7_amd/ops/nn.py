@@ -277,7 +277,7 @@ class Batch_NormalizationOp(Op):
 
     def gradient(self, output_grad):
         g = Batch_Normalization_GradientOp(output_grad, self.inputs[0], self.inputs[1], self,
-                                           self.eps, ctx=self.raw_ctx)
+                                           self.eps, ctx=self.raw_ctx, bias=self.inputs[2])
         out = [batch_normalization_gradient_of_data_op(g, self.inputs[0], ctx=self.raw_ctx),
                batch_normalization_gradient_of_scale_op(g, self.inputs[1], ctx=self.raw_ctx),
                batch_normalization_gradient_of_bias_op(g, self.inputs[2], ctx=self.raw_ctx)]
@@ -294,16 +294,18 @@ class Batch_Normalization_GradientOp(Op):
     aux_inputs = (3,)
     value_and_aux_inputs = (3,)
 
-    def __init__(self, out_gradient, x, scale, forward_node, eps, ctx=None):
-        super().__init__(Batch_Normalization_GradientOp, [out_gradient, x, scale, forward_node], ctx)
+    def __init__(self, out_gradient, x, scale, forward_node, eps, ctx=None, bias=None):
+        super().__init__(Batch_Normalization_GradientOp,
+                         [out_gradient, x, scale, forward_node] + ([bias] if bias is not None else []), ctx)
         self.forward_node = forward_node
         self.eps = eps
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        g, x, scale, (y, (mean, invstd)) = input_vals
+        g, x, scale, (y, (mean, invstd)) = input_vals[:4]
+        bias = input_vals[4] if len(input_vals) > 4 else None
         fw = self.forward_node
         dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
-                                                 relu=fw.relu, want_dres=fw.has_residual)
+                                                 relu=fw.relu, want_dres=fw.has_residual, bias=bias)
         return (dx, dscale, dbias, dres)
 
     def gradient(self, output_grad):

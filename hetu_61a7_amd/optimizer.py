@@ -186,14 +186,13 @@ class FlatGroup(object):
         dev = device
         self.param = torch.empty(max(off, 1), dtype=torch.float32, device=dev)
         for p in params:
-            o, n, shp = self.offsets[p]
-            self.param[o:o + n].copy_(values[p].reshape(-1).float())
+            self.view(p, 'param').copy_(values[p].float())
         self.grad = torch.zeros_like(self.param)
         self.s1 = torch.full_like(self.param, state_init[0]) if n_states >= 1 else None
         self.s2 = torch.full_like(self.param, state_init[1]) if n_states >= 2 else None
         self.shadow = None
         if shadow:
-            self.shadow = self.param.to(torch.bfloat16)
+            self.shadow = self.param.to(torch.bfloat16)  # same (channels-last) layout
         self.gscale = 1.0
         offs = [self.offsets[p][0] for p in params] + [off]
         self.seg_host = offs
@@ -201,8 +200,15 @@ class FlatGroup(object):
         self.norms_ws = torch.zeros(2 * max(len(params), 1), dtype=torch.float32, device=dev)
 
     def view(self, p, which='param'):
+        """View of parameter ``p`` inside a flat buffer.  4-D (conv) weights are
+        laid out channels-last ([Cout, kh, kw, Cin] in memory) so the bf16 copy
+        feeds the NHWC convolutions directly and their (channels-last) weight
+        gradients land in the flat gradient buffer with a contiguous copy."""
         o, n, shp = self.offsets[p]
         buf = getattr(self, which)
+        if len(shp) == 4:
+            co, ci, kh, kw = shp
+            return buf[o:o + n].view(co, kh, kw, ci).permute(0, 3, 1, 2)
         return buf[o:o + n].view(shp)
 
 

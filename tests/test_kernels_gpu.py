@@ -69,7 +69,7 @@ def test_batchnorm_nhwc(dt, relu, res):
     torch.testing.assert_close(rv, rv2, rtol=1e-3, atol=1e-3)
     dy = torch.randn_like(ref).to(dt).contiguous(memory_format=torch.channels_last)
     ref.backward(dy.float())
-    dx, ds, db, dres = KN.bn_backward(dy, y, x, scale, mean, invstd, relu=relu, want_dres=res)
+    dx, ds, db, dres = KN.bn_backward(dy, y, x, scale, mean, invstd, relu=relu, want_dres=res, bias=bias)
     tol = dict(rtol=5e-2, atol=5e-2) if dt == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(dx.float(), xf.grad, **tol)
     torch.testing.assert_close(ds, sf.grad, rtol=2e-2, atol=2e-1 if dt == torch.bfloat16 else 1e-2)

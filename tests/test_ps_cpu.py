@@ -1,0 +1,123 @@
+"""PS semantics over the shared-memory van, multi-process on one host (reference
+tests/pstests/test_apis.py pattern: one process per role, DMLC_* env)."""
+import os
+import socket
+import uuid
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _env(port, nw, ns=1):
+    return dict(DMLC_PS_ROOT_PORT=str(port), DMLC_NUM_WORKER=str(nw), DMLC_NUM_SERVER=str(ns),
+                HETU_PS_HEAP_GB='0.25')
+
+
+def _server(env):
+    os.environ.update(env)
+    os.environ['DMLC_ROLE'] = 'server'
+    from hetu_61a7_amd.ps import server
+    server.server_init()
+    server.server_finish(timeout_s=120)
+
+
+def _worker(env, q, tmpdir):
+    os.environ.update(env)
+    os.environ['DMLC_ROLE'] = 'worker'
+    from hetu_61a7_amd.ps import worker, CacheSparseTable
+    ag = worker.worker_init()
+    r, n = ag.rank(), ag.nrank()
+    out = {}
+    # dense: every worker pushes ones; after a barrier everyone pulls n
+    ag.InitTensor(1, 0, 1000, 1, 0, 0.0, 0.0, 0)
+    ag.Wait(1)
+    ones = torch.ones(1000)
+    ag.Push(1, ones)
+    ag.Wait(1)
+    ag.BarrierWorker()
+    v = torch.zeros(1000)
+    ag.Pull(1, v)
+    ag.Wait(1)
+    out['dense'] = float(v.mean())
+    # sparse rows
+    ag.InitTensor(2, 1, 50, 4, 0, 1.0, 0.0, 0)
+    ids = torch.tensor([r, 10 + r, 10 + r], dtype=torch.int64)
+    ag.SparsePush(2, ids, torch.ones(3, 4))
+    ag.Wait(2)
+    ag.BarrierWorker()
+    got = torch.zeros(3, 4)
+    ag.SparsePull(2, torch.tensor([0, 10, 49], dtype=torch.int64), got)
+    ag.Wait(2)
+    out['sparse'] = got[:, 0].tolist()
+    # DDPushPull returns the post-push value
+    res = torch.zeros(1000)
+    ag.DDPushPull(1, ones, res)
+    ag.Wait(1)
+    out['ddpp_min'] = float(res.min())
+    ag.BarrierWorker()
+    # HET cache: bounded staleness + push on bound
+    ag.InitTensor(3, 2, 100, 8, 0, 0.0, 0.0, 0)
+    cache = CacheSparseTable(limit=20, length=100, width=8, node_id=3, policy='LFUOpt', bound=1)
+    keys = torch.tensor([5, 6, 5], dtype=torch.int64)
+    dest = torch.zeros(3, 8)
+    cache.embedding_lookup(keys, dest, sync=True)
+    for _ in range(3):
+        cache.embedding_update(keys[:2], torch.ones(2, 8), sync=True)
+    cache.flush()
+    ag.BarrierWorker()
+    cache.embedding_lookup(torch.tensor([5], dtype=torch.int64), dest[:1], sync=True)
+    out['cache_row5'] = float(dest[0, 0])
+    out['cache_size'] = cache.size()
+    # SSP (tolerance 0 == BSP clocks)
+    ag.ssp_init(7, n, 0)
+    ag.BarrierWorker()
+    ag.ssp_sync(7, 1)
+    # PReduce partner matching
+    partners = ag.preduce_get_partner(9, r, n, 2000.0)
+    out['partners'] = sorted(partners)
+    if r == 0:
+        ag.SaveParam(2, tmpdir)
+    ag.BarrierWorker()
+    ag.Clear(2)
+    ag.BarrierWorker()
+    if r == 0:
+        ag.LoadParam(2, tmpdir)
+    ag.BarrierWorker()
+    got2 = torch.zeros(1, 4)
+    ag.SparsePull(2, torch.tensor([10], dtype=torch.int64), got2)
+    ag.Wait(2)
+    out['reloaded'] = float(got2[0, 0])
+    out['loads'] = ag.getLoads()
+    q.put((r, out))
+    worker.worker_finish()
+
+
+def test_ps_roles_and_psfs(tmp_path):
+    port = 20000 + (uuid.uuid4().int % 20000)
+    nw = 2
+    env = _env(port, nw)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    srv = ctx.Process(target=_server, args=(env,))
+    srv.start()
+    ws = [ctx.Process(target=_worker, args=(env, q, str(tmp_path))) for _ in range(nw)]
+    for w in ws:
+        w.start()
+    res = dict(q.get(timeout=120) for _ in ws)
+    for w in ws:
+        w.join(60)
+        assert w.exitcode == 0
+    srv.join(60)
+    assert srv.exitcode == 0
+    for r in range(nw):
+        o = res[r]
+        assert o['dense'] == pytest.approx(float(nw))
+        # rows 0 and 10 got one push / two pushes from worker 0; row 49 untouched (init 1.0)
+        assert o['sparse'] == [2.0, 3.0, 1.0]
+        assert o['ddpp_min'] >= nw + 1
+        assert o['partners'] == list(range(nw))
+        assert o['reloaded'] == pytest.approx(3.0)
+        # each worker: 3 updates of +1 on row 5 -> 2*3 = 6 on the server
+        assert o['cache_row5'] == pytest.approx(2 * 3.0)

@@ -1,0 +1,486 @@
+// bf16 MFMA GEMM and implicit-GEMM convolution for gfx950 (CDNA4).
+//
+// Replaces the reference's cuBLAS Sgemm / SgemmStridedBatched call sites
+// (src/ops/MatrixMult.cu:22-26, BatchMatrixMult.cu:31-36, Linear.cu:50-55,
+// Addmm.cu:29, Baddbmm.cu:37) and cuDNN convolution (CudnnConv2d.cu:54-245,
+// CudnnConv2dAddBias.cu:93), SURVEY.md §2.7.
+//
+// One kernel template, operand "loaders" as policies:
+//   C[M,N] = alpha * sum_k  Am[m,k] * Bn[n,k]  (+ beta*Cin) (+ bias) -> act
+// Each operand is either K-contiguous ("KMAJ", LDS image [rows][64] with a
+// 16-byte-chunk XOR swizzle, fragments via ds_read_b128) or MN-contiguous
+// (LDS image [64 k][128 rows], 256-byte rows with the T10 XOR, fragments via
+// ds_read_b64_tr_b16 -- the hardware transpose read), so all four transpose
+// modes and the three conv passes use the same main loop with no transpose
+// pass over memory.
+//
+// Geometry: 128x128x64 block tile, 256 threads = 4 waves (2 M x 2 N), each wave
+// 64x64 = 4x4 mfma_f32_16x16x32_bf16 tiles; LDS double buffer (2 x 32 KiB),
+// register-staged prefetch of tile k+1 during the MFMAs of tile k, one barrier
+// per K-tile.  Operand roles are swapped (A_op = N side, B_op = M side) so the
+// accumulator holds 4 consecutive N columns per lane -> 8/16-byte stores.
+// Block ids are remapped so that consecutive tiles share an XCD's L2, then
+// grouped 8 tiles along M for operand reuse.  Split-K over gridDim.z with
+// fp32 atomics for the long-K weight-gradient GEMMs.
+#include "common.h"
+
+namespace hetu {
+namespace gemm {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * BK * 2;  // 16 KiB per operand tile
+
+__device__ __forceinline__ v8s zero8() { return v8s{0, 0, 0, 0, 0, 0, 0, 0}; }
+__device__ __forceinline__ v8s ld8(const bf16* p) { return *reinterpret_cast<const v8s*>(p); }
+
+// ---- LDS images -------------------------------------------------------------------------
+// K-major: [128 rows][64 k] bf16, 128-B rows, chunk c (0..7) of row r at ((c ^ (r&7)) << 4)
+__device__ __forceinline__ int offk(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+// MN-major: [64 k][128 cols] bf16, 256-B rows, chunk c (0..15), T10 image (b)
+__device__ __forceinline__ int offmn(int k, int c) {
+  return k * 256 + ((c ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4);
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ void lds_store(char* lds, const v8s* reg, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int off = KMAJ ? offk((tid >> 3) + 32 * i, tid & 7) : offmn((tid >> 4) + 16 * i, tid & 15);
+    *reinterpret_cast<v8s*>(lds + off) = reg[i];
+  }
+}
+
+// fragment of 16 rows (row block rb) x 32 k (k-step s): lane holds row (lane&15),
+// k = 32s + 8(lane>>4) + j, j = 0..7
+template <bool KMAJ>
+__device__ __forceinline__ v8s lds_frag(const char* lds, int rb, int s, int lane) {
+  if constexpr (KMAJ) {
+    int r = rb * 16 + (lane & 15);
+    int c = s * 4 + (lane >> 4);
+    return *reinterpret_cast<const v8s*>(lds + offk(r, c));
+  } else {
+    int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    int c = rb * 2 + (p >> 1);
+    int k1 = s * 32 + 8 * g + q;
+    const char* a1 = lds + offmn(k1, c) + 8 * (p & 1);
+    const char* a2 = lds + offmn(k1 + 4, c) + 8 * (p & 1);
+    v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
+    v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
+    return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+// ---- operand loaders ------------------------------------------------------------------
+// Each thread owns 4 16-byte chunks of the 128x64 tile.  KMAJ: rows (tid>>3)+32i,
+// chunk tid&7 (k = k0 + 8*(tid&7)).  MN: k rows (tid>>4)+16i, chunk tid&15
+// (cols r0 + 8*(tid&15)).
+
+// plain row-major operand with contiguous K: element (r, k) at base[r*ld + k]
+struct PlainK {
+  static constexpr bool KMAJ = true;
+  const bf16* base; int64_t ld, rows, K, bstride;
+  int64_t roff[4]; bool rok[4]; int ch;
+  __device__ void init(int64_t r0, int tid, int64_t batch) {
+    base += batch * bstride;
+    ch = tid & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t r = r0 + (tid >> 3) + 32 * i;
+      rok[i] = r < rows;
+      roff[i] = r * ld;
+    }
+  }
+  __device__ void load(int64_t k0, v8s* reg) const {
+    int64_t k = k0 + ch * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) reg[i] = (rok[i] && k < K) ? ld8(base + roff[i] + k) : zero8();
+  }
+};
+
+// plain operand stored [K][rows]: element (r, k) at base[k*ld + r]
+struct PlainMN {
+  static constexpr bool KMAJ = false;
+  const bf16* base; int64_t ld, rows, K, bstride;
+  int64_t col; bool cok; int kr;
+  __device__ void init(int64_t r0, int tid, int64_t batch) {
+    base += batch * bstride;
+    col = r0 + (tid & 15) * 8;
+    cok = col < rows;
+    kr = tid >> 4;
+  }
+  __device__ void load(int64_t k0, v8s* reg) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t k = k0 + kr + 16 * i;
+      reg[i] = (cok && k < K) ? ld8(base + k * ld + col) : zero8();
+    }
+  }
+};
+
+struct ConvGeom {
+  int N, H, W, C, K, KH, KW, sh, sw, ph, pw, OH, OW;  // C = in channels, K = out channels
+};
+
+// forward, M side: rows = output pixels, k = (kh, kw, ci), ci fastest
+struct ConvFwdA {
+  static constexpr bool KMAJ = true;
+  const bf16* x; ConvGeom g; int64_t Ktot, rows;
+  int64_t nb[4]; int ih0[4], iw0[4]; bool rok[4]; int ch;
+  __device__ void init(int64_t r0, int tid, int64_t) {
+    ch = tid & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t r = r0 + (tid >> 3) + 32 * i;
+      rok[i] = r < rows;
+      int64_t rr = rok[i] ? r : 0;
+      int ow = (int)(rr % g.OW);
+      int64_t t = rr / g.OW;
+      int oh = (int)(t % g.OH);
+      int64_t n = t / g.OH;
+      nb[i] = n * g.H;
+      ih0[i] = oh * g.sh - g.ph;
+      iw0[i] = ow * g.sw - g.pw;
+    }
+  }
+  __device__ void load(int64_t k0, v8s* reg) const {
+    int64_t k = k0 + ch * 8;
+    int tap = (int)(k / g.C);
+    int ci = (int)(k - (int64_t)tap * g.C);
+    int kh = tap / g.KW, kw = tap - kh * g.KW;
+    bool kok = k < Ktot;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int ih = ih0[i] + kh, iw = iw0[i] + kw;
+      bool ok = kok && rok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      reg[i] = ok ? ld8(x + ((nb[i] + ih) * g.W + iw) * g.C + ci) : zero8();
+    }
+  }
+};
+
+// data gradient, M side: rows = input pixels (n, ih, iw), k = (kh, kw, co)
+struct ConvDgradA {
+  static constexpr bool KMAJ = true;
+  const bf16* dy; ConvGeom g; int64_t Ktot, rows;
+  int64_t nb[4]; int ih[4], iw[4]; bool rok[4]; int ch;
+  __device__ void init(int64_t r0, int tid, int64_t) {
+    ch = tid & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t r = r0 + (tid >> 3) + 32 * i;
+      rok[i] = r < rows;
+      int64_t rr = rok[i] ? r : 0;
+      iw[i] = (int)(rr % g.W);
+      int64_t t = rr / g.W;
+      ih[i] = (int)(t % g.H);
+      nb[i] = (t / g.H) * g.OH;
+    }
+  }
+  __device__ void load(int64_t k0, v8s* reg) const {
+    int64_t k = k0 + ch * 8;
+    int tap = (int)(k / g.K);
+    int co = (int)(k - (int64_t)tap * g.K);
+    int kh = tap / g.KW, kw = tap - kh * g.KW;
+    bool kok = k < Ktot;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int th = ih[i] + g.ph - kh, tw = iw[i] + g.pw - kw;
+      int oh = th / g.sh, ow = tw / g.sw;
+      bool ok = kok && rok[i] && th >= 0 && tw >= 0 && oh * g.sh == th && ow * g.sw == tw &&
+                oh < g.OH && ow < g.OW;
+      reg[i] = ok ? ld8(dy + ((nb[i] + oh) * g.OW + ow) * g.K + co) : zero8();
+    }
+  }
+};
+
+// data gradient, N side: cols = ci, k rows = (kh, kw, co): w[co][kh][kw][ci]
+struct ConvDgradB {
+  static constexpr bool KMAJ = false;
+  const bf16* w; ConvGeom g; int64_t Ktot;
+  int col; bool cok; int kr;
+  __device__ void init(int64_t r0, int tid, int64_t) {
+    col = (int)r0 + (tid & 15) * 8;
+    cok = col < g.C;
+    kr = tid >> 4;
+  }
+  __device__ void load(int64_t k0, v8s* reg) const {
+    const int taps = g.KH * g.KW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t k = k0 + kr + 16 * i;
+      int tap = (int)(k / g.K);
+      int co = (int)(k - (int64_t)tap * g.K);
+      reg[i] = (cok && k < Ktot) ? ld8(w + ((int64_t)co * taps + tap) * g.C + col) : zero8();
+    }
+  }
+};
+
+// weight gradient, N side: cols = (kh, kw, ci), k rows = output pixels
+struct ConvWgradB {
+  static constexpr bool KMAJ = false;
+  const bf16* x; ConvGeom g; int64_t P;  // P = N*OH*OW
+  int kh, kw, ci; bool cok; int kr;
+  __device__ void init(int64_t r0, int tid, int64_t) {
+    int col = (int)r0 + (tid & 15) * 8;
+    cok = col < g.KH * g.KW * g.C;
+    int tap = col / g.C;
+    ci = col - tap * g.C;
+    kh = tap / g.KW;
+    kw = tap - kh * g.KW;
+    kr = tid >> 4;
+  }
+  __device__ void load(int64_t k0, v8s* reg) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t p = k0 + kr + 16 * i;
+      int ow = (int)(p % g.OW);
+      int64_t t = p / g.OW;
+      int oh = (int)(t % g.OH);
+      int64_t n = t / g.OH;
+      int ih = oh * g.sh - g.ph + kh, iw = ow * g.sw - g.pw + kw;
+      bool ok = cok && p < P && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      reg[i] = ok ? ld8(x + ((n * g.H + ih) * g.W + iw) * g.C + ci) : zero8();
+    }
+  }
+};
+
+// ---- epilogue ------------------------------------------------------------------------
+struct Epi {
+  void* C; const void* Cin; const float* bias;
+  int64_t ldc, ldcin, sC, sCin;
+  float alpha, beta;
+  int act;        // 0 none, 1 relu, 2 gelu(erf)
+  int out_f32;    // C dtype
+  int cin_f32;    // Cin dtype
+  int atomic;     // fp32 atomicAdd into C (split-K / accumulate)
+  int bias_on_m;  // bias indexed by m instead of n
+};
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 2) return 0.5f * v * (1.f + erff(v * 0.70710678118f));
+  return v;
+}
+
+template <class LA, class LB>
+__global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
+                                                  int64_t K, int tiles_m, int tiles_n, int ktps) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2 * TILE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+
+  // XCD-aware bijective remap, then group-of-8 along M for L2 reuse
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int gid = wg / per_group, first_m = gid * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+
+  const int64_t batch = blockIdx.y;
+  la.init((int64_t)tm * BM, tid, batch);
+  lb.init((int64_t)tn * BN, tid, batch);
+
+  const int nkt = (int)((K + BK - 1) / BK);
+  const int kt0 = blockIdx.z * ktps;
+  const int kt1 = min(kt0 + ktps, nkt);
+
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  v8s ra[4], rb[4];
+  if (kt0 < kt1) {
+    la.load((int64_t)kt0 * BK, ra);
+    lb.load((int64_t)kt0 * BK, rb);
+    lds_store<LA::KMAJ>(smem[0], ra, tid);
+    lds_store<LB::KMAJ>(smem[0] + TILE_BYTES, rb, tid);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) {
+      la.load((int64_t)(kt + 1) * BK, ra);
+      lb.load((int64_t)(kt + 1) * BK, rb);
+    }
+    const char* As = smem[cur];
+    const char* Bs = smem[cur] + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v8s mf[4], nf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mf[i] = lds_frag<LA::KMAJ>(As, wm * 4 + i, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nf[j] = lds_frag<LB::KMAJ>(Bs, wn * 4 + j, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[j], mf[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      lds_store<LA::KMAJ>(smem[cur ^ 1], ra, tid);
+      lds_store<LB::KMAJ>(smem[cur ^ 1] + TILE_BYTES, rb, tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[m][n..n+3]
+  char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
+  const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= N) continue;
+      float v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float x = acc[i][j][t] * ep.alpha;
+        if (ep.bias) x += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
+        if (Cinb && n + t < N) {
+          int64_t o = m * ep.ldcin + n + t;
+          float c = ep.cin_f32 ? ((const float*)Cinb)[o] : to_f(((const bf16*)Cinb)[o]);
+          x += ep.beta * c;
+        }
+        v[t] = act_f(x, ep.act);
+      }
+      const int64_t o = m * ep.ldc + n;
+      if (ep.atomic) {
+        float* Cf = (float*)Cb;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (n + t < N) unsafeAtomicAdd(Cf + o + t, v[t]);
+      } else if (ep.out_f32) {
+        float* Cf = (float*)Cb;
+        if (n + 3 < N && (o & 3) == 0) {
+          *reinterpret_cast<float4*>(Cf + o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          for (int t = 0; t < 4; ++t)
+            if (n + t < N) Cf[o + t] = v[t];
+        }
+      } else {
+        unsigned short* Ch = (unsigned short*)Cb;
+        if (n + 3 < N && (o & 3) == 0) {
+          uint2 pk;
+          pk.x = (uint32_t)f_to_bf16_bits(v[0]) | ((uint32_t)f_to_bf16_bits(v[1]) << 16);
+          pk.y = (uint32_t)f_to_bf16_bits(v[2]) | ((uint32_t)f_to_bf16_bits(v[3]) << 16);
+          *reinterpret_cast<uint2*>(Ch + o) = pk;
+        } else {
+          for (int t = 0; t < 4; ++t)
+            if (n + t < N) Ch[o + t] = f_to_bf16_bits(v[t]);
+        }
+      }
+    }
+  }
+}
+
+template <class LA, class LB>
+static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
+                  int batch, int splitk, hipStream_t st) {
+  int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+  int nkt = (int)((K + BK - 1) / BK);
+  if (splitk < 1) splitk = 1;
+  if (splitk > nkt) splitk = nkt > 0 ? nkt : 1;
+  int ktps = (nkt + splitk - 1) / splitk;
+  splitk = (nkt + ktps - 1) / ktps;
+  if (splitk < 1) splitk = 1;
+  dim3 grid(tiles_m * tiles_n, batch, splitk);
+  hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), 0, st, la, lb, ep, M, N, K, tiles_m,
+                     tiles_n, ktps);
+  return (int)hipGetLastError();
+}
+
+}  // namespace gemm
+}  // namespace hetu
+
+using namespace hetu;
+using namespace hetu::gemm;
+
+// C[b] = alpha * op(A[b]) @ op(B[b]) (+ beta * Cin[b]) (+ bias) -> act.
+// a_kmaj: A stored [M][K] (else [K][M]); b_kmaj: B stored [N][K] (else [K][N]).
+// Requirements (checked by the caller): the contiguous dim of each operand and its
+// leading dimension are multiples of 8 elements, 16-byte aligned bases.
+HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* Cin,
+                            const float* bias, int64_t M, int64_t N, int64_t K, int64_t lda,
+                            int64_t ldb, int64_t ldc, int64_t ldcin, int a_kmaj, int b_kmaj,
+                            int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
+                            float alpha, float beta, int act, int out_f32, int cin_f32,
+                            int bias_on_m, int splitk, int atomic, hipStream_t st) {
+  Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32,
+         atomic || splitk > 1, bias_on_m};
+  const bf16* a = (const bf16*)A;
+  const bf16* b = (const bf16*)B;
+  if (a_kmaj && b_kmaj)
+    return launch(PlainK{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
+  if (a_kmaj && !b_kmaj)
+    return launch(PlainK{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
+  if (!a_kmaj && b_kmaj)
+    return launch(PlainMN{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
+  return launch(PlainMN{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
+}
+
+static ConvGeom geom(int N, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
+                     int pw) {
+  ConvGeom g{N, H, W, C, K, KH, KW, sh, sw, ph, pw, 0, 0};
+  g.OH = (H + 2 * ph - KH) / sh + 1;
+  g.OW = (W + 2 * pw - KW) / sw + 1;
+  return g;
+}
+
+// y[N,OH,OW,K] (NHWC) = conv(x[N,H,W,C] NHWC, w[K,KH,KW,C]) (+bias[K]) -> act.  C % 8 == 0.
+HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const float* bias, int N,
+                                int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
+                                int pw, int act, hipStream_t st) {
+  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  int64_t M = (int64_t)N * g.OH * g.OW, Kt = (int64_t)KH * KW * C;
+  Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0};
+  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
+    return launch(PlainK{(const bf16*)x, C, M, C, 0}, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M,
+                  K, Kt, 1, 1, st);
+  ConvFwdA la{(const bf16*)x, g, Kt, M};
+  return launch(la, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M, K, Kt, 1, 1, st);
+}
+
+// dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[K,KH,KW,C]).  K % 8 == 0, C % 8 == 0.
+HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, int N, int H, int W,
+                                  int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
+                                  hipStream_t st) {
+  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  int64_t M = (int64_t)N * H * W, Kt = (int64_t)KH * KW * K;
+  Epi ep{dx, nullptr, nullptr, C, 0, 0, 0, 1.f, 0.f, 0, 0, 0, 0, 0};
+  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
+    return launch(PlainK{(const bf16*)dy, K, M, K, 0}, PlainMN{(const bf16*)w, C, C, K, 0}, ep, M,
+                  C, K, 1, 1, st);
+  ConvDgradA la{(const bf16*)dy, g, Kt, M};
+  ConvDgradB lb{(const bf16*)w, g, Kt};
+  return launch(la, lb, ep, M, C, Kt, 1, 1, st);
+}
+
+// dw[K, KH*KW*C] (fp32, accumulated with atomics: zero it first or accumulate) =
+// sum over output pixels dy^T x_im2col.
+HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int N, int H, int W,
+                                  int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
+                                  int splitk, hipStream_t st) {
+  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  int64_t P = (int64_t)N * g.OH * g.OW, Nc = (int64_t)KH * KW * C;
+  Epi ep{dw, nullptr, nullptr, Nc, 0, 0, 0, 1.f, 0.f, 0, 1, 0, 1, 0};
+  PlainMN la{(const bf16*)dy, K, K, P, 0};
+  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
+    return launch(la, PlainMN{(const bf16*)x, C, C, P, 0}, ep, K, Nc, P, 1, splitk, st);
+  ConvWgradB lb{(const bf16*)x, g, P};
+  return launch(la, lb, ep, K, Nc, P, 1, splitk, st);
+}

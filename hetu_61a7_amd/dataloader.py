@@ -165,7 +165,10 @@ class DataloaderOp(Op):
     def get_arr(self, name, config=None):
         dl = self.dataloaders[name]
         if not dl.initialized:
-            dl.init_states(config.device if config is not None else None)
+            dev = config.device if config is not None else None
+            if getattr(self, 'host_feed', False):
+                dev = torch.device('cpu')
+            dl.init_states(dev)
         t = dl.get_arr()
         if config is not None and config.mixed_precision and t.is_cuda and t.dtype == torch.float32 \
                 and not self.keep_fp32:

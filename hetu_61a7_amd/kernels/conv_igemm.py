@@ -1,18 +1,86 @@
-"""Implicit-GEMM MFMA convolution dispatch (``conv.hip``).
+"""Implicit-GEMM MFMA convolution (``csrc/kernels/gemm.hip``), NHWC bf16.
 
-Placeholder selection table: returns None (vendor path) until the HIP kernel
-for a shape class is built and measured faster.
+forward  : M = N*OH*OW pixels, N = Cout, K = KH*KW*Cin (im2col on the fly)
+dgrad    : M = N*H*W pixels,  N = Cin,  K = KH*KW*Cout (stride handled by
+           zero-filling the taps that do not hit an output pixel)
+wgrad    : M = Cout, N = KH*KW*Cin, K = N*OH*OW, split-K with fp32 atomics
+           straight into an fp32 gradient.
+
+Shapes with Cin or Cout not a multiple of 8 (the 3-channel stem) return None
+and run on the vendor path.  ``HETU_CONV=vendor`` forces the vendor path.
 """
 from __future__ import annotations
 
+import os
 
-def try_forward(x, w, stride, padding):
-    return None
+import torch
+
+from . import fn, stream_ptr, check, P, I32
+
+MODE = os.environ.get('HETU_CONV', 'hip')
+CL = torch.channels_last
+_GEOM = [I32] * 11
+
+
+def _ok(a, b, *channels):
+    return (MODE == 'hip' and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and
+            a.is_contiguous(memory_format=CL) and b.is_contiguous(memory_format=CL) and
+            all(c % 8 == 0 for c in channels) and a.data_ptr() % 16 == 0 and
+            b.data_ptr() % 16 == 0)
+
+
+def _out_hw(H, W, KH, KW, stride, padding):
+    return (H + 2 * padding[0] - KH) // stride[0] + 1, (W + 2 * padding[1] - KW) // stride[1] + 1
+
+
+def try_forward(x, w, stride, padding, bias=None, act=None):
+    if not _ok(x, w, x.shape[1], w.shape[0]):
+        return None
+    N, C, H, W = x.shape
+    K, _, KH, KW = w.shape
+    OH, OW = _out_hw(H, W, KH, KW, stride, padding)
+    y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
+    f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, P])
+    check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+            bias.float().contiguous().data_ptr() if bias is not None else None,
+            N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
+            {None: 0, 'relu': 1}[act], stream_ptr()), 'conv_fwd')
+    return y.permute(0, 3, 1, 2)
 
 
 def try_backward_data(g, w, x_shape, stride, padding):
-    return None
+    if not _ok(g, w, x_shape[1], w.shape[0]):
+        return None
+    N, C, H, W = x_shape
+    K, _, KH, KW = w.shape
+    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
+    f = fn('hetu_conv_dgrad_bf16', [P, P, P] + _GEOM + [P])
+    check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
+            padding[0], padding[1], stream_ptr()), 'conv_dgrad')
+    return dx.permute(0, 3, 1, 2)
 
 
-def try_backward_filter(g, x, w_shape, stride, padding):
-    return None
+def _splitk(M, Nc, P_):
+    tiles = ((M + 127) // 128) * ((Nc + 127) // 128)
+    ktiles = (P_ + 63) // 64
+    want = max(1, (2048 + tiles - 1) // tiles)  # ~8 blocks per CU in flight
+    return int(min(want, max(1, ktiles // 8)))
+
+
+def try_backward_filter(g, x, w_shape, stride, padding, out=None):
+    """Returns the fp32 weight gradient (channels-last), accumulating into ``out``
+    when given (it must then be a zeroed / partial fp32 CL tensor)."""
+    if not _ok(x, g, x.shape[1], g.shape[1]):
+        return None
+    N, C, H, W = x.shape
+    K, _, KH, KW = w_shape
+    OH, OW = g.shape[2], g.shape[3]
+    if out is None:
+        dw = torch.zeros((K, KH, KW, C), dtype=torch.float32, device=g.device)
+    else:
+        dw = out.permute(0, 2, 3, 1)
+        assert dw.is_contiguous() and dw.dtype == torch.float32
+    f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, P])
+    check(f(g.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
+            padding[0], padding[1], _splitk(K, KH * KW * C, N * OH * OW), stream_ptr()), 'conv_wgrad')
+    return dw.permute(0, 3, 1, 2)

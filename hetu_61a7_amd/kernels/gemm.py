@@ -2,8 +2,9 @@
 
 ``matmul(a, b, ta, tb, bias, activation)``: 2-D product with optional fused bias
 and ReLU/GELU epilogue.  bf16 shapes that the hand-written MFMA kernel
-(``gemm.hip``: 256x256x64 tiles, 8 waves, LDS double buffer, XCD-aware block
-remap, fused epilogue) supports run there; everything else is a plain library
+(``gemm.hip``: 128x128x64 tiles, 4 waves, LDS double buffer, hardware
+transpose reads for MN-contiguous operands, XCD-aware block remap, fused
+epilogue) supports run there; everything else is a plain library
 GEMM (hipBLASLt through torch) followed by the elementwise epilogue kernel.
 """
 from __future__ import annotations
@@ -50,4 +51,9 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
 
 def bmm(a, b, ta=False, tb=False):
     a, b = _match(a, b)
+    if native(a) and _MFMA != 'off':
+        from . import gemm_mfma
+        y = gemm_mfma.try_bmm(a, b, ta, tb)
+        if y is not None:
+            return y
     return torch.matmul(_tr(a, ta), _tr(b, tb))

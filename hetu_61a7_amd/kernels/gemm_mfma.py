@@ -1,6 +1,118 @@
-"""Shape selection for the hand-written MFMA GEMM (filled in with gemm.hip)."""
+"""Bindings of the hand-written bf16 MFMA GEMM (``csrc/kernels/gemm.hip``).
+
+Every transpose mode is handled in-kernel (K-contiguous operands are read
+row-wise from LDS, MN-contiguous ones through the hardware transpose read), so
+a transposed view never costs a copy.  Shapes whose contiguous extent or
+leading dimension is not a multiple of 8 elements return ``None`` and the
+caller uses the library GEMM.
+"""
 from __future__ import annotations
 
+import os
 
-def try_gemm(a, b, ta, tb, bias, activation):
+import torch
+
+from . import fn, stream_ptr, check, P, I64, I32, F32
+
+_ACT = {None: 0, 'relu': 1, 'gelu': 2}
+_ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64, I64,
+         F32, F32, I32, I32, I32, I32, I32, I32, P]
+MODE = os.environ.get('HETU_GEMM', 'hip')  # 'hip' | 'vendor'
+
+
+def _operand(t, rows_dim_last):
+    """Describe a 2-D (or batched 3-D) operand view.  ``t`` is viewed as
+    [..., R, K] (rows first) -> returns (kmaj, ld, batch_stride) or None."""
+    sr, sk = t.stride(-2), t.stride(-1)
+    R, K = t.shape[-2], t.shape[-1]
+    bs = t.stride(0) if t.dim() == 3 else 0
+    if sk == 1 or K == 1:
+        ld = sr if R > 1 else max(K, 8)
+        if K % 8 or ld % 8:
+            return None
+        return True, ld, bs
+    if sr == 1 or R == 1:
+        ld = sk if K > 1 else max(R, 8)
+        if R % 8 or ld % 8:
+            return None
+        return False, ld, bs
     return None
+
+
+def _aligned(*ts):
+    return all(t.data_ptr() % 16 == 0 for t in ts)
+
+
+def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None,
+         accumulate=False, splitk=1, bias_on_m=False):
+    """out[M,N] = alpha * a[M,K] @ b[K,N] (+beta*cin) (+bias) -> act, a/b arbitrary
+    strided views (batched 3-D allowed).  Returns None if unsupported."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        return None
+    if a.dim() != b.dim() or a.dim() not in (2, 3):
+        return None
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    if b.shape[-2] != K:
+        raise ValueError('gemm shape mismatch %s @ %s' % (tuple(a.shape), tuple(b.shape)))
+    batch = a.shape[0] if a.dim() == 3 else 1
+    if a.dim() == 3 and b.shape[0] != batch:
+        return None
+    da = _operand(a, False)
+    db = _operand(b.transpose(-1, -2), False)  # view as [N, K]
+    if da is None or db is None or not _aligned(a, b):
+        return None
+    odt = out_dtype or (out.dtype if out is not None else torch.bfloat16)
+    if out is None:
+        shape = (batch, M, N) if a.dim() == 3 else (M, N)
+        out = (torch.zeros if (accumulate or splitk > 1) else torch.empty)(shape, dtype=odt, device=a.device)
+    if out.stride(-1) != 1 or (out.dim() == 3 and out.dim() != a.dim()):
+        return None
+    if (accumulate or splitk > 1) and out.dtype != torch.float32:
+        return None
+    ldc = out.stride(-2) if M > 1 else N
+    sC = out.stride(0) if out.dim() == 3 else 0
+    cin_t, ldcin, sCin = None, 0, 0
+    if cin is not None and beta != 0.0:
+        cin_t = cin.expand_as(out) if cin.shape != out.shape else cin
+        if cin_t.stride(-1) != 1:
+            cin_t = cin_t.contiguous()
+        ldcin = cin_t.stride(-2)
+        sCin = cin_t.stride(0) if cin_t.dim() == 3 else 0
+    bias_t = bias.float().contiguous() if bias is not None else None
+    f = fn('hetu_gemm_bf16', _ARGS)
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), cin_t.data_ptr() if cin_t is not None else None,
+            bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, ldcin,
+            int(da[0]), int(db[0]), batch, da[2], db[2], sC, sCin, float(alpha), float(beta),
+            _ACT[act], int(out.dtype == torch.float32),
+            int(cin_t is not None and cin_t.dtype == torch.float32), int(bias_on_m), int(splitk),
+            int(accumulate), stream_ptr()), 'gemm_bf16')
+    return out
+
+
+def try_gemm(a, b, ta, tb, bias=None, activation=None):
+    if MODE != 'hip':
+        return None
+    A = a.transpose(-1, -2) if ta else a
+    B = b.transpose(-1, -2) if tb else b
+    return gemm(A, B, bias=bias, act=activation)
+
+
+def try_bmm(a, b, ta, tb):
+    if MODE != 'hip':
+        return None
+    A = a.transpose(-1, -2) if ta else a
+    B = b.transpose(-1, -2) if tb else b
+    lead = A.shape[:-2]
+    if B.shape[:-2] != lead or len(lead) == 0:
+        return None
+    if len(lead) > 1:
+        try:
+            A = A.view(-1, *A.shape[-2:])
+            B = B.view(-1, *B.shape[-2:])
+        except RuntimeError:
+            return None
+    y = gemm(A, B)
+    if y is None:
+        return None
+    return y.view(*lead, *y.shape[-2:])

@@ -22,8 +22,18 @@ class EmbeddingLookUp(Op):
         self.grad_node = None
         self.out_dtype = None  # set to bf16 under mixed precision
 
+    def forward_hook(self, config):
+        Op.forward_hook(self, config)
+        if config.mixed_precision and ndarray.is_gpu_ctx(self.ctx):
+            self.out_dtype = torch.bfloat16
+        if getattr(self.inputs[0], 'ps_managed', False):
+            # ids are consumed on the host by the PS / HET cache
+            self.inputs[1].host_feed = True
+
     def compute(self, input_vals, output_val=None, stream_handle=None):
         table, idx = input_vals
+        if not isinstance(table, torch.Tensor):  # PS / HET-cache managed table
+            return table.lookup(idx, self.out_dtype)
         out = KS.gather_rows(table, idx)
         if self.out_dtype is not None and out.dtype != self.out_dtype:
             from ..kernels.elementwise import cast

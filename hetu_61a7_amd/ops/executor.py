@@ -236,6 +236,11 @@ class HetuConfig(object):
     def init_param(self, node: PlaceholderOp):
         if node in self.placeholder_to_arr_map:
             return self.placeholder_to_arr_map[node]
+        if getattr(node, 'ps_managed', False):
+            from ..ps.table import PSTable
+            t = PSTable(node, self)
+            self.placeholder_to_arr_map[node] = t
+            return t
         dev = node.ctx.torch_device if isinstance(node.ctx, ndarray.DLContext) else self.device
         t = node.initial_value(self.seed, dev)
         if t.dtype == torch.float64:
@@ -248,6 +253,8 @@ class HetuConfig(object):
         if v is not None:
             return v
         t = self.placeholder_to_arr_map[node]
+        if not isinstance(t, torch.Tensor):
+            return t
         if self.mixed_precision and t.dtype == torch.float32 and t.is_cuda and not node.trainable \
                 and t.dim() >= 2:
             v = t.to(torch.bfloat16)
@@ -450,6 +457,8 @@ class SubExecutor(object):
                 arr = arr.astype(np.float32)
             t = torch.from_numpy(np.ascontiguousarray(arr))
         dev = node.ctx.torch_device if isinstance(node.ctx, ndarray.DLContext) else self.config.device
+        if getattr(node, 'host_feed', False):
+            dev = torch.device('cpu')
         if t.device != dev:
             t = t.to(dev, non_blocking=True)
         if self.config.mixed_precision and t.is_cuda and t.dtype == torch.float32 and \

@@ -253,6 +253,16 @@ class OptimizerOp(Op):
             self.dp = True
             self.comm = config.comm
         self.bucket_bytes = int(getattr(config, 'bucket_mb', 32) * (1 << 20))
+        # PS placement (reference optimizer.py:145-163, Variable.py:55-81): embedding
+        # tables (row-sparse grads) live on the PS in PS and Hybrid modes; in pure PS
+        # mode the dense parameters are held there too (one flat key).
+        self.ps_dense = None
+        self.ps_dense_wanted = config.comm_mode == 'PS'
+        if config.comm_mode in ('PS', 'Hybrid'):
+            for p, g in zip(self.param_of_input, self.inputs):
+                if getattr(p, 'is_embed', False) and g.use_indexed_slices:
+                    p.ps_managed = True
+                    self.ps_params.add(p)
 
     def forward_hook(self, config):
         self.ctx = config.context
@@ -299,6 +309,10 @@ class OptimizerOp(Op):
             self.slot[i] = p
         if self.dp:
             self._make_buckets(dense)
+        if self.ps_dense_wanted and self.flat.numel > 0:
+            from .ps.table import PSDense
+            # key space: node ids are < 2^20; the flat dense key sits above them
+            self.ps_dense = PSDense(self.flat, (1 << 20) + self.id, config)
 
     def _make_buckets(self, dense):
         cap = max(self.bucket_bytes // 4, 1)
@@ -328,6 +342,9 @@ class OptimizerOp(Op):
     def on_grad_ready(self, i, value):
         p = self.param_of_input[i]
         if p in self.ps_params:
+            table = self.config.placeholder_to_arr_map[p]
+            table.stage_grad(value, self.optimizer.get_learning_rate())
+            self._pending_ps.append(table)
             return
         if isinstance(value, ndarray.IndexedSlices) or p in self.sparse_state:
             if self.dp and isinstance(value, ndarray.IndexedSlices) and not self.excluded_from_dp(p):
@@ -348,6 +365,7 @@ class OptimizerOp(Op):
 
     def begin_step(self):
         self._pending_sparse = []
+        self._pending_ps = []
         for b in self.buckets:
             b.pending = b.total
             b.work = None
@@ -360,8 +378,13 @@ class OptimizerOp(Op):
             elif self.dp:
                 # a bucket whose grads never arrived this step (should not happen)
                 self.comm.all_reduce(self.flat.grad[b.start:b.end], self.allreduce_mode)
-        if self.flat is not None and self.flat.numel > 0:
+        if self.ps_dense is not None:
+            self.ps_dense.step(self.optimizer.get_learning_rate())
+        elif self.flat is not None and self.flat.numel > 0:
             self.optimizer.dense_update(self.flat, self.step, getattr(self, 'dyn', None))
+        for table in self._pending_ps:
+            table.flush_grad()
+        self._pending_ps = []
         for p, sl in self._pending_sparse:
             table = self.config.placeholder_to_arr_map[p]
             uniq, merged = sl.deduplicate().indices, sl.values

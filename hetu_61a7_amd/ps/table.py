@@ -1,0 +1,219 @@
+"""Worker-side handles of PS-managed parameters (reference
+``gpu_ops/ParameterServerCommunicate.py:13-338`` and ``Variable.py:55-81``).
+
+``PSTable``   an embedding table that lives on the PS server (host DRAM),
+              optionally fronted by the HET cache.  Lookups return device rows;
+              gradients are pre-multiplied by ``-lr`` on the GPU, staged through
+              pinned host memory and pushed asynchronously (the server adds them,
+              as in the reference where server-side optimizers are unused).
+``PSDense``   the whole flat dense parameter buffer of an optimizer as ONE PS
+              key: one DDPushPull per step instead of one request per tensor.
+
+Synchronisation (reference ``bsp``): -1 ASP, 0 BSP (worker barrier between
+push and pull), >0 SSP with that staleness bound.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import worker as psw
+from .worker import PARAM_DENSE, PARAM_SPARSE, PARAM_CACHE
+
+
+def _pinned(n, dtype=torch.float32):
+    t = torch.empty(n, dtype=dtype)
+    if torch.cuda.is_available():
+        t = t.pin_memory()
+    return t
+
+
+class _Staging(object):
+    """Grow-only pinned buffer + an event guarding its reuse."""
+
+    def __init__(self, dtype=torch.float32):
+        self.buf = None
+        self.dtype = dtype
+        self.event = None
+
+    def get(self, n):
+        if self.event is not None:
+            self.event.synchronize()
+            self.event = None
+        if self.buf is None or self.buf.numel() < n:
+            self.buf = _pinned(max(n, 1), self.dtype)
+        return self.buf[:n]
+
+    def guard(self):
+        if torch.cuda.is_available():
+            self.event = torch.cuda.Event()
+            self.event.record()
+
+
+class PSTable(object):
+    def __init__(self, node, config):
+        self.node = node
+        self.key = node.id
+        self.agent = psw.get_agent()
+        self.rows = int(node.shape[0])
+        self.width = int(torch.Size(node.shape[1:]).numel())
+        self.shape = tuple(node.shape)
+        self.device = config.device
+        self.bsp = config.bsp
+        policy = config.cstable_policy
+        ptype = PARAM_CACHE if policy else PARAM_SPARSE
+        init = node.initializer
+        if init is None:
+            raise ValueError('PS-managed table %s needs an initializer' % node.name)
+        self.agent.init_tensor(self.key, ptype, self.shape, init, config.seed + self.key)
+        self.cache = None
+        if policy:
+            from .cstable import CacheSparseTable
+            limit = max(self.rows // 10, 1)
+            self.cache = CacheSparseTable(limit, self.rows, self.width, self.key, policy,
+                                          config.cache_bound)
+        else:
+            self.agent.BarrierWorker()
+        self.out_stage = _Staging()
+        self.grad_stage = _Staging()
+        self.pending = None
+        self.pending_push = None
+        self.version = 0
+
+    # tensor-like attributes the graph code may query
+    @property
+    def dtype(self):
+        return torch.float32
+
+    def numel(self):
+        return self.rows * self.width
+
+    def _wait_push(self):
+        if self.pending is not None:
+            if self.cache is not None:
+                self.cache.wait(self.pending)
+            else:
+                self.agent.WaitTicket(self.pending)
+            self.pending = None
+            self.pending_push = None
+
+    def lookup(self, idx, out_dtype=None):
+        ids = idx.reshape(-1)
+        if ids.is_cuda:
+            ids = ids.cpu()
+        ids = ids.long().contiguous()
+        self._wait_push()
+        dest = self.out_stage.get(ids.numel() * self.width).view(-1, self.width)
+        if self.cache is not None:
+            self.cache.embedding_lookup(ids, dest, sync=True)
+        else:
+            t = self.agent.SparsePull(self.key, ids, dest)
+            self.agent.WaitTicket(t)
+        if self.device.type == 'cuda':
+            out = dest.to(self.device, non_blocking=True)
+            self.out_stage.guard()
+            if out_dtype is not None and out_dtype != out.dtype:
+                out = out.to(out_dtype)
+        else:
+            out = dest.clone()
+        return out.view(*idx.shape, self.width)
+
+    def stage_grad(self, slices, lr):
+        """Scale by -lr on the device and start the D2H copy (called as soon as the
+        gradient exists, so it overlaps the rest of backward)."""
+        ids = slices.indices.reshape(-1)
+        if ids.is_cuda:
+            ids = ids.cpu()
+        vals = slices.values.reshape(-1, self.width)
+        scaled = vals.float() * (-lr)
+        host = self.grad_stage.get(scaled.numel()).view(-1, self.width)
+        host.copy_(scaled, non_blocking=True)
+        self.grad_stage.guard()
+        self.pending_push = (ids.long().contiguous(), host)
+
+    def flush_grad(self):
+        """Push the staged gradient (after its D2H copy completed)."""
+        if self.pending_push is None:
+            return
+        ids, host = self.pending_push
+        if self.grad_stage.event is not None:
+            self.grad_stage.event.synchronize()
+        if self.cache is not None:
+            self.pending = self.cache.embedding_update(ids, host)
+        else:
+            self.pending = self.agent.SparsePush(self.key, ids, host)
+        self.pending_push = None
+        self.version += 1
+        if self.bsp == 0:
+            self._wait_push()
+            if self.cache is not None:
+                self.cache.flush()
+            self.agent.BarrierWorker()
+        elif self.bsp and self.bsp > 0:
+            self._wait_push()
+            self.agent.ssp_sync(self.key, self.version)
+
+    def to_dense(self):
+        """Full table (host) -- checkpointing / tests."""
+        self._wait_push()
+        if self.cache is not None:
+            self.cache.flush()
+        out = torch.empty(self.rows, self.width)
+        ids = torch.arange(self.rows, dtype=torch.int64)
+        t = self.agent.SparsePull(self.key, ids, out)
+        self.agent.WaitTicket(t)
+        return out.view(self.shape)
+
+
+class PSDense(object):
+    """Flat dense parameters held by the PS (pure PS mode)."""
+
+    def __init__(self, flat, key, config):
+        self.flat = flat
+        self.key = key
+        self.agent = psw.get_agent()
+        self.bsp = config.bsp
+        n = flat.numel
+        self.agent.InitTensor(key, PARAM_DENSE, n, 1, 0, 0.0, 0.0, 0)
+        # worker 0 publishes its initial values; everyone starts from them
+        if self.agent.rank() == 0:
+            host = flat.param.detach().float().cpu().contiguous()
+            t = self.agent.Push(key, host)
+            self.agent.WaitTicket(t)
+        self.agent.BarrierWorker()
+        self.push_buf = _pinned(n)
+        self.pull_buf = _pinned(n)
+        self._pull_into_device()
+        if self.bsp and self.bsp > 0:
+            self.agent.ssp_init(key, self.agent.nrank(), self.bsp)
+        self.version = 0
+
+    def _pull_into_device(self):
+        t = self.agent.Pull(self.key, self.pull_buf)
+        self.agent.WaitTicket(t)
+        self.flat.param.copy_(self.pull_buf[:self.flat.numel], non_blocking=True)
+        if self.flat.shadow is not None:
+            self.flat.shadow.copy_(self.flat.param)
+
+    def step(self, lr):
+        n = self.flat.numel
+        g = self.flat.grad[:n]
+        self.push_buf[:n].copy_(g * (-lr), non_blocking=True)
+        if torch.cuda.is_available() and g.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        self.version += 1
+        if self.bsp == 0:
+            t = self.agent.Push(self.key, self.push_buf)
+            self.agent.WaitTicket(t)
+            self.agent.BarrierWorker()
+            self._pull_into_device()
+        elif self.bsp and self.bsp > 0:
+            t = self.agent.Push(self.key, self.push_buf)
+            self.agent.WaitTicket(t)
+            self.agent.ssp_sync(self.key, self.version)
+            self._pull_into_device()
+        else:
+            t = self.agent.DDPushPull(self.key, self.push_buf, self.pull_buf)
+            self.agent.WaitTicket(t)
+            self.flat.param.copy_(self.pull_buf[:n], non_blocking=True)
+            if self.flat.shadow is not None:
+                self.flat.shadow.copy_(self.flat.param)

@@ -87,48 +87,53 @@ class PSAgent(object):
         check(lib('hps_load_param')(int(node_id), path.encode()), 'LoadParam')
 
     # ---- PSFs (async; buffers must stay alive until Wait) -------------------------------
-    def _keep(self, key, *ts):
-        self.keepalive.setdefault(key, []).extend(ts)
+    def _issue(self, key, ticket, *ts):
+        if ticket < 0:
+            raise RuntimeError('PS request on key %d failed: %d' % (key, ticket))
+        self.keepalive[ticket] = (key, ts)
+        return ticket
 
     def Pull(self, node_id, arr):
-        self._keep(node_id, arr)
-        return lib('hps_async_dense_pull')(int(node_id), ptr(arr), arr.numel())
+        return self._issue(node_id, lib('hps_async_dense_pull')(int(node_id), ptr(arr), arr.numel()), arr)
 
     def Push(self, node_id, arr):
-        self._keep(node_id, arr)
-        return lib('hps_async_dense_push')(int(node_id), ptr(arr), arr.numel())
+        return self._issue(node_id, lib('hps_async_dense_push')(int(node_id), ptr(arr), arr.numel()), arr)
 
     def DDPushPull(self, node_id, in_arr, out_arr):
-        self._keep(node_id, in_arr, out_arr)
-        return lib('hps_async_dd_pushpull')(int(node_id), ptr(in_arr), ptr(out_arr), in_arr.numel())
+        return self._issue(node_id, lib('hps_async_dd_pushpull')(int(node_id), ptr(in_arr), ptr(out_arr),
+                                                                   in_arr.numel()), in_arr, out_arr)
 
     def SparsePull(self, node_id, index, value):
-        self._keep(node_id, index, value)
-        return lib('hps_async_sparse_pull')(int(node_id), ptr(index), index.numel(), ptr(value))
+        return self._issue(node_id, lib('hps_async_sparse_pull')(int(node_id), ptr(index), index.numel(),
+                                                                   ptr(value)), index, value)
 
     def SparsePush(self, node_id, index, value):
-        self._keep(node_id, index, value)
-        return lib('hps_async_sparse_push')(int(node_id), ptr(index), index.numel(), ptr(value))
+        return self._issue(node_id, lib('hps_async_sparse_push')(int(node_id), ptr(index), index.numel(),
+                                                                   ptr(value)), index, value)
 
     def SDPushPull(self, node_id, index, in_arr, out_arr):
-        self._keep(node_id, index, in_arr, out_arr)
-        return lib('hps_async_sd_pushpull')(int(node_id), ptr(index), index.numel(), ptr(in_arr),
-                                            ptr(out_arr), out_arr.numel())
+        return self._issue(node_id, lib('hps_async_sd_pushpull')(int(node_id), ptr(index), index.numel(),
+                                                                   ptr(in_arr), ptr(out_arr), out_arr.numel()),
+                           index, in_arr, out_arr)
 
     def SSPushPull(self, node_id, in_index, in_arr, out_index, out_arr):
-        self._keep(node_id, in_index, in_arr, out_index, out_arr)
-        return lib('hps_async_ss_pushpull')(int(node_id), ptr(in_index), in_index.numel(), ptr(in_arr),
-                                            ptr(out_index), out_index.numel(), ptr(out_arr))
+        return self._issue(node_id, lib('hps_async_ss_pushpull')(int(node_id), ptr(in_index), in_index.numel(),
+                                                                   ptr(in_arr), ptr(out_index), out_index.numel(),
+                                                                   ptr(out_arr)),
+                           in_index, in_arr, out_index, out_arr)
 
     def Wait(self, node_id):
         lib('hps_wait_key')(int(node_id))
-        self.keepalive.pop(node_id, None)
+        for t in [t for t, (k, _) in self.keepalive.items() if k == node_id]:
+            del self.keepalive[t]
 
     def wait(self, node_id):
         self.Wait(node_id)
 
     def WaitTicket(self, ticket):
-        return lib('hps_wait')(int(ticket))
+        r = lib('hps_wait')(int(ticket))
+        self.keepalive.pop(ticket, None)
+        return r
 
     # ---- sync versions (used by the HET cache glue and tests) ---------------------------
     def pull_sync(self, node_id, arr):

@@ -4,6 +4,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+export PYTHONPATH=$PWD${PYTHONPATH:+:$PYTHONPATH}
+df -h /dev/shm; free -g | head -2
 export TMPDIR=/tmp
 STEPS=${STEPS:-20}
 echo "== build" ; make -C csrc -j16 > gpurun_out/build.log 2>&1 || { echo build failed; tail -20 gpurun_out/build.log; exit 1; }

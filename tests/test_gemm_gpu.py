@@ -1,0 +1,81 @@
+"""Hand-written MFMA GEMM / implicit-GEMM conv vs plain PyTorch fp32."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from hetu_61a7_amd.kernels import gemm_mfma as G, conv_igemm as CI
+
+DEV = 'cuda'
+CL = torch.channels_last
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
+
+
+@pytest.mark.parametrize('ta', [False, True])
+@pytest.mark.parametrize('tb', [False, True])
+@pytest.mark.parametrize('mnk', [(256, 256, 256), (200, 136, 72), (1000, 8, 520), (64, 1032, 4096)])
+def test_gemm_modes(ta, tb, mnk):
+    M, N, K = mnk
+    a = torch.randn(K, M, device=DEV).bfloat16().t() if ta else torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16().t() if tb else torch.randn(K, N, device=DEV).bfloat16()
+    y = G.gemm(a, b)
+    assert y is not None
+    ref = a.float() @ b.float()
+    assert _rel(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize('act', [None, 'relu', 'gelu'])
+def test_gemm_epilogue(act):
+    M, N, K = 384, 264, 128
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    cin = torch.randn(M, N, device=DEV)
+    y = G.gemm(a, b, bias=bias, act=act, alpha=0.5, beta=2.0, cin=cin, out_dtype=torch.float32)
+    ref = 0.5 * (a.float() @ b.float()) + bias + 2.0 * cin
+    if act == 'relu':
+        ref = torch.relu(ref)
+    elif act == 'gelu':
+        ref = F.gelu(ref)
+    assert _rel(y, ref) < 1e-2
+
+
+def test_gemm_batched_and_splitk():
+    a = torch.randn(6, 128, 64, device=DEV).bfloat16()
+    b = torch.randn(6, 128, 64, device=DEV).bfloat16().transpose(1, 2)  # [6, 64, 128]
+    y = G.try_bmm(a, b, False, False)
+    assert _rel(y, a.float() @ b.float()) < 1e-2
+    x = torch.randn(8192, 96, device=DEV).bfloat16()
+    g = torch.randn(8192, 136, device=DEV).bfloat16()
+    out = torch.zeros(96, 136, device=DEV)
+    G.gemm(x.t(), g, out=out, accumulate=True, splitk=16)
+    assert _rel(out, x.float().t() @ g.float()) < 1e-2
+
+
+CONV_SHAPES = [  # N, C, H, K, k, stride, pad
+    (4, 64, 14, 64, 1, 1, 0), (4, 64, 14, 128, 3, 1, 1), (4, 128, 15, 64, 3, 2, 1),
+    (2, 256, 14, 128, 1, 2, 0), (2, 8, 32, 64, 7, 2, 3), (3, 72, 9, 40, 3, 1, 0)]
+
+
+@pytest.mark.parametrize('shape', CONV_SHAPES)
+def test_conv_passes(shape):
+    N, C, H, K, k, s, p = shape
+    x = torch.randn(N, C, H, H, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(K, C, k, k, device=DEV) * 0.1).bfloat16().contiguous(memory_format=CL)
+    y = CI.try_forward(x, w, (s, s), (p, p))
+    xf = x.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    ref = F.conv2d(xf, wf, None, s, p)
+    assert y is not None and y.is_contiguous(memory_format=CL)
+    assert _rel(y, ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
+    ref.backward(dy.float())
+    dx = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p))
+    assert dx is not None and _rel(dx, xf.grad) < 1e-2
+    dw = CI.try_backward_filter(dy, x, w.shape, (s, s), (p, p))
+    assert dw is not None and dw.dtype == torch.float32
+    assert _rel(dw, wf.grad) < 1e-2

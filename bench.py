@@ -27,7 +27,9 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=5)
-    p.add_argument('--batch', type=int, default=256, help='per-GPU batch')
+    p.add_argument('--batch', type=int, default=None, help='per-GPU batch (256 resnet50, 128 wdl)')
+    p.add_argument('--criteo-rows', type=int, default=0, help='embedding rows (default: full Criteo 33762577)')
+    p.add_argument('--cache', default='LFUOpt')
     p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl'])
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     p.add_argument('--bucket-mb', type=float, default=32)
@@ -35,8 +37,25 @@ def parse():
     return p.parse_args()
 
 
+def start_ps_server(world, local):
+    """One PS server process per node, started by local rank 0 BEFORE any GPU
+    initialisation in this process (the server never touches the GPU)."""
+    import subprocess
+    os.environ.setdefault('DMLC_PS_ROOT_PORT', str(int(os.environ.get('MASTER_PORT', '29500')) + 7))
+    os.environ['DMLC_NUM_WORKER'] = str(world)
+    os.environ.setdefault('DMLC_NUM_SERVER', '1')
+    os.environ.setdefault('HETU_PS_HEAP_GB', '24')
+    if local != 0:
+        return None
+    env = dict(os.environ, DMLC_ROLE='server')
+    return subprocess.Popen([sys.executable, '-m', 'hetu_61a7_amd.ps'], env=env)
+
+
 def main():
     args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    server = start_ps_server(world, local) if args.model == 'wdl' else None
     import torch
     import hetu_61a7_amd as ht
     from hetu_61a7_amd.parallel import comm as C
@@ -48,9 +67,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
+    finish = None
     if args.model == 'resnet50':
         from hetu_61a7_amd.models import resnet50_imagenet
-        B = args.batch
+        B = args.batch or 256
         x = ht.Variable(name='x')
         y_ = ht.Variable(name='y_')
         loss, logits = resnet50_imagenet(x, y_, 1000)
@@ -78,7 +98,7 @@ def main():
         samples_per_step = B * world
     else:
         from hetu_61a7_amd.models.ctr import wdl_criteo_bench
-        step, samples_per_step, cfg, metric = wdl_criteo_bench(args, world, rank, local)
+        step, samples_per_step, cfg, metric, finish = wdl_criteo_bench(args, world, rank, local)
 
     def barrier():
         if world > 1:
@@ -115,6 +135,13 @@ def main():
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
                'dtype': args.dtype, 'data': 'synthetic (random-init weights)', 'config': cfg}
         print(json.dumps(out), flush=True)
+    if rank == 0 and os.environ.get('HETU_AUTOTUNE_DUMP'):
+        from hetu_61a7_amd.kernels import autotune
+        autotune.dump(os.environ['HETU_AUTOTUNE_DUMP'])
+    if finish is not None:
+        finish()
+    if server is not None:
+        server.wait(timeout=120)
     if world > 1:
         C.destroy()
 

@@ -333,6 +333,10 @@ class Exec {
     std::unique_lock<std::mutex> g(mu_);
     done_.wait(g, [&] { return pending_.find(t) == pending_.end(); });
   }
+  void drain() {
+    std::unique_lock<std::mutex> g(mu_);
+    done_.wait(g, [&] { return pending_.empty(); });
+  }
 
  private:
   void run() {
@@ -381,6 +385,17 @@ static Exec* exec() {
 using namespace hc;
 
 extern "C" {
+
+// wait for every queued cache operation (called by hps_finalize before the PS
+// segment is unmapped, so no cache thread can touch it afterwards)
+void hc_drain_all() {
+  Exec* e;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    e = g_exec;
+  }
+  if (e) e->drain();
+}
 
 // policy: 0 LRU, 1 LFU, 2 LFUOpt
 int hc_create(int policy, int64_t limit, int64_t rows, int64_t width, int key, int64_t pull_bound,

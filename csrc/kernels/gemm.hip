@@ -23,6 +23,7 @@
 // grouped 8 tiles along M for operand reuse.  Split-K over gridDim.z with
 // fp32 atomics for the long-K weight-gradient GEMMs.
 #include "common.h"
+#include <algorithm>
 
 namespace hetu {
 namespace gemm {
@@ -258,6 +259,8 @@ struct Epi {
   int cin_f32;    // Cin dtype
   int atomic;     // fp32 atomicAdd into C (split-K / accumulate)
   int bias_on_m;  // bias indexed by m instead of n
+  float* slab;    // split-K: fp32 partial tiles, slab z at slab + z*slab_stride (ld = N)
+  int64_t slab_stride;
 };
 
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -336,6 +339,29 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   }
 
   // epilogue: lane holds C[m][n..n+3]
+  if (ep.slab) {  // split-K partial: plain fp32 stores into this slice's slab
+    float* S = ep.slab + blockIdx.z * ep.slab_stride;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
+        if (n >= N) continue;
+        float* d = S + m * N + n;
+        if (n + 3 < N && (N & 3) == 0) {
+          *reinterpret_cast<float4*>(d) =
+              make_float4(acc[i][j][0] * ep.alpha, acc[i][j][1] * ep.alpha, acc[i][j][2] * ep.alpha,
+                          acc[i][j][3] * ep.alpha);
+        } else {
+          for (int t = 0; t < 4; ++t)
+            if (n + t < N) d[t] = acc[i][j][t] * ep.alpha;
+        }
+      }
+    }
+    return;
+  }
   char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
   const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
 #pragma unroll
@@ -388,6 +414,27 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   }
 }
 
+// dst[m][n] (ld ldd, fp32 or bf16) (+)= sum_z slab[z][m][n]
+__global__ void splitk_reduce_k(const float* __restrict__ slab, int64_t stride, int nz,
+                                void* dst, int64_t M, int64_t N, int64_t ldd, int out_f32,
+                                int accumulate) {
+  const int64_t total = M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < nz; ++z) v += slab[z * stride + i];
+    const int64_t m = i / N, n = i - m * N;
+    const int64_t o = m * ldd + n;
+    if (out_f32) {
+      float* d = (float*)dst;
+      d[o] = accumulate ? d[o] + v : v;
+    } else {
+      unsigned short* d = (unsigned short*)dst;
+      d[o] = f_to_bf16_bits(accumulate ? bf16_bits_to_f(d[o]) + v : v);
+    }
+  }
+}
+
 template <class LA, class LB>
 static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
                   int batch, int splitk, hipStream_t st) {
@@ -399,9 +446,31 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
   splitk = (nkt + ktps - 1) / ktps;
   if (splitk < 1) splitk = 1;
   dim3 grid(tiles_m * tiles_n, batch, splitk);
-  hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), 0, st, la, lb, ep, M, N, K, tiles_m,
+  if (ep.slab && splitk > 1) {
+    Epi e2 = ep;
+    e2.slab_stride = M * N;
+    hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K, tiles_m,
+                       tiles_n, ktps);
+    int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, ep.slab, M * N, splitk, ep.C, M,
+                       N, ep.ldc, ep.out_f32, ep.atomic);
+    return (int)hipGetLastError();
+  }
+  Epi e1 = ep;
+  e1.slab = nullptr;
+  if (splitk > 1) e1.atomic = 1;
+  hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m,
                      tiles_n, ktps);
   return (int)hipGetLastError();
+}
+
+// split count: ~2 blocks per CU in flight, each slice at least 8 K-tiles
+static int pick_splitk(int64_t M, int64_t N, int64_t K) {
+  int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int64_t ktiles = (K + BK - 1) / BK;
+  int64_t want = (512 + tiles - 1) / tiles;
+  int64_t cap = std::max<int64_t>(1, ktiles / 8);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(want, cap), 64));
 }
 
 }  // namespace gemm
@@ -419,9 +488,9 @@ HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* C
                             int64_t ldb, int64_t ldc, int64_t ldcin, int a_kmaj, int b_kmaj,
                             int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
                             float alpha, float beta, int act, int out_f32, int cin_f32,
-                            int bias_on_m, int splitk, int atomic, hipStream_t st) {
-  Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32,
-         atomic || splitk > 1, bias_on_m};
+                            int bias_on_m, int splitk, int atomic, float* ws, hipStream_t st) {
+  Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32, atomic,
+         bias_on_m, ws, 0};
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   if (a_kmaj && b_kmaj)
@@ -447,7 +516,7 @@ HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const flo
                                 int pw, int act, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t M = (int64_t)N * g.OH * g.OW, Kt = (int64_t)KH * KW * C;
-  Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0};
+  Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0, nullptr, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(PlainK{(const bf16*)x, C, M, C, 0}, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M,
                   K, Kt, 1, 1, st);
@@ -461,7 +530,7 @@ HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, int N
                                   hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t M = (int64_t)N * H * W, Kt = (int64_t)KH * KW * K;
-  Epi ep{dx, nullptr, nullptr, C, 0, 0, 0, 1.f, 0.f, 0, 0, 0, 0, 0};
+  Epi ep{dx, nullptr, nullptr, C, 0, 0, 0, 1.f, 0.f, 0, 0, 0, 0, 0, nullptr, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(PlainK{(const bf16*)dy, K, M, K, 0}, PlainMN{(const bf16*)w, C, C, K, 0}, ep, M,
                   C, K, 1, 1, st);
@@ -470,14 +539,16 @@ HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, int N
   return launch(la, lb, ep, M, C, Kt, 1, 1, st);
 }
 
-// dw[K, KH*KW*C] (fp32, accumulated with atomics: zero it first or accumulate) =
-// sum over output pixels dy^T x_im2col.
+HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }
+
+// dw[K, KH*KW*C] fp32 (+)= sum over output pixels dy^T x_im2col.  Split-K over
+// the pixel axis into fp32 slabs (ws: splitk*K*KH*KW*C floats) + one reduce; no atomics.
 HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int N, int H, int W,
                                   int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-                                  int splitk, hipStream_t st) {
+                                  int splitk, int accumulate, float* ws, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t P = (int64_t)N * g.OH * g.OW, Nc = (int64_t)KH * KW * C;
-  Epi ep{dw, nullptr, nullptr, Nc, 0, 0, 0, 1.f, 0.f, 0, 1, 0, 1, 0};
+  Epi ep{dw, nullptr, nullptr, Nc, 0, 0, 0, 1.f, 0.f, 0, 1, 0, accumulate, 0, splitk > 1 ? ws : nullptr, 0};
   PlainMN la{(const bf16*)dy, K, K, P, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(la, PlainMN{(const bf16*)x, C, C, P, 0}, ep, K, Nc, P, 1, splitk, st);

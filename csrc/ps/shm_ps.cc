@@ -297,6 +297,8 @@ using namespace hps;
 
 extern "C" {
 
+void hc_drain_all();
+
 int hps_init(int role, const char* name, int num_workers, int num_servers, uint64_t heap_bytes) {
   if (H) return 0;
   ROLE = role;
@@ -369,6 +371,9 @@ int hps_init(int role, const char* name, int num_workers, int num_servers, uint6
 
 int hps_finalize() {
   if (!H) return 0;
+  const bool dbg = getenv("HETU_PS_DEBUG") != nullptr;
+  if (dbg) fprintf(stderr, "[hps] finalize role=%d\n", ROLE);
+  hc_drain_all();
   if (HB) {
     HB_STOP = true;
     HB->join();
@@ -379,7 +384,9 @@ int hps_finalize() {
     delete POOL;
     POOL = nullptr;
   }
+  if (dbg) fprintf(stderr, "[hps] pool stopped\n");
   if (ROLE == 2) H->finalized.fetch_add(1);
+  if (dbg) fprintf(stderr, "[hps] finalized count bumped\n");
   munmap(BASE, MAP_BYTES);
   if (ROLE == 1) shm_unlink(NAME.c_str());
   H = nullptr;

@@ -1,0 +1,54 @@
+"""Per-shape kernel selection by measurement.
+
+``choose(key, {name: fn})`` times every candidate once per key (events on the
+current stream, a few repetitions after a warm call) and caches the fastest.
+Used to pick, per convolution / GEMM shape, between the hand-written MFMA
+kernels and the vendor library, so a hand-written kernel runs exactly where it
+is at least as fast.  Never measures inside a hipGraph capture (returns the
+first candidate there; warm-up steps run eagerly before capture).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_decisions = {}
+_times = {}
+REPS = int(os.environ.get('HETU_AUTOTUNE_REPS', '3'))
+
+
+def choose(key, candidates):
+    d = _decisions.get(key)
+    if d is not None:
+        return d
+    names = list(candidates)
+    if len(names) == 1 or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
+        return names[0]
+    times = {}
+    for n in names:
+        f = candidates[n]
+        if f() is None:  # unsupported shape
+            continue
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(REPS):
+            f()
+        e.record()
+        e.synchronize()
+        times[n] = s.elapsed_time(e) / REPS
+    best = min(times, key=times.get) if times else names[-1]
+    _decisions[key] = best
+    _times[key] = times
+    return best
+
+
+def report():
+    """{key: (chosen, {candidate: ms})} -- for profiles/ and logs."""
+    return {k: (_decisions[k], _times.get(k, {})) for k in _decisions}
+
+
+def dump(path):
+    with open(path, 'w') as f:
+        for k, (c, t) in report().items():
+            f.write('%s -> %s  %s\n' % (k, c, ' '.join('%s=%.1fus' % (n, v * 1e3) for n, v in t.items())))

@@ -1,10 +1,11 @@
 """2-D convolution (logical NCHW, physical channels-last on the GPU).
 
 The forward/backward-data/backward-filter entry points dispatch per shape to
-the hand-written implicit-GEMM MFMA kernel (``conv.hip``) when it has been
-selected for that shape, otherwise to the vendor convolution (MIOpen) through
-torch.  Selection is by measurement (``conv_autotune``) -- a kernel is only
-used where it is at least as fast.
+the hand-written implicit-GEMM MFMA kernel (``gemm.hip`` via ``conv_igemm``)
+or to the vendor convolution (MIOpen through torch).  ``HETU_CONV=auto``
+(default) selects per shape by measurement (``autotune.choose``), so the
+hand-written kernel runs exactly where it is at least as fast; ``hip`` /
+``vendor`` force one side.
 """
 from __future__ import annotations
 
@@ -16,7 +17,22 @@ import torch.nn.functional as F
 from . import native
 
 CL = torch.channels_last
-_USE_IGEMM = os.environ.get('HETU_CONV', 'auto')
+MODE = os.environ.get('HETU_CONV', 'auto')  # hip | vendor | auto (per-shape measured choice)
+
+
+def _pick(key, hip, vendor):
+    if MODE == 'hip':
+        r = hip()
+        return r if r is not None else vendor()
+    if MODE == 'vendor':
+        return vendor()
+    from .autotune import choose
+    c = choose(key, {'hip': hip, 'vendor': vendor})
+    if c == 'hip':
+        r = hip()
+        if r is not None:
+            return r
+    return vendor()
 
 
 def _match(x, w):
@@ -34,9 +50,9 @@ def conv2d(x, w, b, stride, padding):
         x = x.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
         from . import conv_igemm
-        y = conv_igemm.try_forward(x, w, stride, padding)
-        if y is None:
-            y = F.conv2d(x, w, None, stride, padding)
+        y = _pick(('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding)),
+                  lambda: conv_igemm.try_forward(x, w, stride, padding),
+                  lambda: F.conv2d(x, w, None, stride, padding))
         if b is not None:
             from .elementwise import binary
             n, c, h, ww = y.shape
@@ -52,9 +68,13 @@ def conv2d_backward_data(g, w, x_shape, stride, padding):
         g = g.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
         from . import conv_igemm
-        dx = conv_igemm.try_backward_data(g, w, x_shape, stride, padding)
-        if dx is not None:
-            return dx
+        return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding)),
+                     lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding),
+                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding))
+    return _vendor_dgrad(g, w, x_shape, stride, padding)
+
+
+def _vendor_dgrad(g, w, x_shape, stride, padding):
     xs = torch.empty(x_shape, dtype=g.dtype, device=g.device)
     if g.is_cuda:
         xs = xs.contiguous(memory_format=CL)
@@ -69,9 +89,13 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding):
         g = g.contiguous(memory_format=CL)
         x = x.contiguous(memory_format=CL)
         from . import conv_igemm
-        dw = conv_igemm.try_backward_filter(g, x, w_shape, stride, padding)
-        if dw is not None:
-            return dw
+        return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
+                     lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding),
+                     lambda: _vendor_wgrad(g, x, w_shape, stride, padding))
+    return _vendor_wgrad(g, x, w_shape, stride, padding)
+
+
+def _vendor_wgrad(g, x, w_shape, stride, padding):
     ws = torch.empty(w_shape, dtype=g.dtype, device=g.device)
     if g.is_cuda:
         ws = ws.contiguous(memory_format=CL)

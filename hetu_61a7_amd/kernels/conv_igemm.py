@@ -15,15 +15,15 @@ import os
 
 import torch
 
-from . import fn, stream_ptr, check, P, I32
+from . import fn, stream_ptr, check, P, I32, I64
 
-MODE = os.environ.get('HETU_CONV', 'hip')
+MODE = os.environ.get('HETU_CONV', 'auto')
 CL = torch.channels_last
 _GEOM = [I32] * 11
 
 
 def _ok(a, b, *channels):
-    return (MODE == 'hip' and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and
+    return (MODE != 'vendor' and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and
             a.is_contiguous(memory_format=CL) and b.is_contiguous(memory_format=CL) and
             all(c % 8 == 0 for c in channels) and a.data_ptr() % 16 == 0 and
             b.data_ptr() % 16 == 0)
@@ -61,10 +61,7 @@ def try_backward_data(g, w, x_shape, stride, padding):
 
 
 def _splitk(M, Nc, P_):
-    tiles = ((M + 127) // 128) * ((Nc + 127) // 128)
-    ktiles = (P_ + 63) // 64
-    want = max(1, (2048 + tiles - 1) // tiles)  # ~8 blocks per CU in flight
-    return int(min(want, max(1, ktiles // 8)))
+    return int(fn('hetu_gemm_pick_splitk', [I64, I64, I64])(M, Nc, P_))
 
 
 def try_backward_filter(g, x, w_shape, stride, padding, out=None):
@@ -75,12 +72,20 @@ def try_backward_filter(g, x, w_shape, stride, padding, out=None):
     N, C, H, W = x.shape
     K, _, KH, KW = w_shape
     OH, OW = g.shape[2], g.shape[3]
+    accumulate = out is not None
     if out is None:
-        dw = torch.zeros((K, KH, KW, C), dtype=torch.float32, device=g.device)
+        dw = torch.empty((K, KH, KW, C), dtype=torch.float32, device=g.device)
     else:
         dw = out.permute(0, 2, 3, 1)
         assert dw.is_contiguous() and dw.dtype == torch.float32
-    f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, P])
+    Nc = KH * KW * C
+    sk = _splitk(K, Nc, N * OH * OW)
+    ws = torch.empty(sk * K * Nc, dtype=torch.float32, device=g.device) if sk > 1 else None
+    if sk == 1 and not accumulate:
+        dw.zero_()
+        accumulate = True  # single slice accumulates straight into dw
+    f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, I32, P, P])
     check(f(g.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
-            padding[0], padding[1], _splitk(K, KH * KW * C, N * OH * OW), stream_ptr()), 'conv_wgrad')
+            padding[0], padding[1], sk, int(accumulate), ws.data_ptr() if ws is not None else None,
+            stream_ptr()), 'conv_wgrad')
     return dw.permute(0, 3, 1, 2)

@@ -15,7 +15,11 @@ import torch
 
 from . import native
 
-_MFMA = os.environ.get('HETU_GEMM', 'auto')
+_MFMA = os.environ.get('HETU_GEMM', 'auto')  # hip | vendor(off) | auto (measured per shape)
+
+
+def _sig(t):
+    return (tuple(t.shape), tuple(t.stride()))
 
 
 def _match(a, b):
@@ -32,11 +36,24 @@ def _tr(t, f):
 
 def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     a, b = _match(a, b)
-    if native(a) and _MFMA != 'off':
+    if native(a) and _MFMA not in ('off', 'vendor'):
         from . import gemm_mfma
-        y = gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)
-        if y is not None:
-            return y
+        hip = lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)
+        if _MFMA == 'hip':
+            y = hip()
+            if y is not None:
+                return y
+        elif a.dtype == torch.bfloat16:
+            from .autotune import choose
+            key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
+            if choose(key, {'hip': hip, 'vendor': lambda: _vendor(a, b, ta, tb, bias, activation)}) == 'hip':
+                y = hip()
+                if y is not None:
+                    return y
+    return _vendor(a, b, ta, tb, bias, activation)
+
+
+def _vendor(a, b, ta, tb, bias, activation):
     y = torch.matmul(_tr(a, ta), _tr(b, tb))
     if bias is not None or activation is not None:
         from .elementwise import binary, unary
@@ -51,9 +68,18 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
 
 def bmm(a, b, ta=False, tb=False):
     a, b = _match(a, b)
-    if native(a) and _MFMA != 'off':
+    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16:
         from . import gemm_mfma
-        y = gemm_mfma.try_bmm(a, b, ta, tb)
-        if y is not None:
-            return y
+        hip = lambda: gemm_mfma.try_bmm(a, b, ta, tb)
+        if _MFMA == 'hip':
+            y = hip()
+            if y is not None:
+                return y
+        else:
+            from .autotune import choose
+            key = ('bmm', _sig(a), _sig(b), ta, tb)
+            if choose(key, {'hip': hip, 'vendor': lambda: torch.matmul(_tr(a, ta), _tr(b, tb))}) == 'hip':
+                y = hip()
+                if y is not None:
+                    return y
     return torch.matmul(_tr(a, ta), _tr(b, tb))

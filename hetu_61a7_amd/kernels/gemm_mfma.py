@@ -16,8 +16,8 @@ from . import fn, stream_ptr, check, P, I64, I32, F32
 
 _ACT = {None: 0, 'relu': 1, 'gelu': 2}
 _ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64, I64,
-         F32, F32, I32, I32, I32, I32, I32, I32, P]
-MODE = os.environ.get('HETU_GEMM', 'hip')  # 'hip' | 'vendor'
+         F32, F32, I32, I32, I32, I32, I32, I32, P, P]
+MODE = os.environ.get('HETU_GEMM', 'auto')
 
 
 def _operand(t, rows_dim_last):
@@ -65,10 +65,10 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
     odt = out_dtype or (out.dtype if out is not None else torch.bfloat16)
     if out is None:
         shape = (batch, M, N) if a.dim() == 3 else (M, N)
-        out = (torch.zeros if (accumulate or splitk > 1) else torch.empty)(shape, dtype=odt, device=a.device)
+        out = (torch.zeros if accumulate else torch.empty)(shape, dtype=odt, device=a.device)
     if out.stride(-1) != 1 or (out.dim() == 3 and out.dim() != a.dim()):
         return None
-    if (accumulate or splitk > 1) and out.dtype != torch.float32:
+    if accumulate and splitk == 1 and out.dtype != torch.float32:
         return None
     ldc = out.stride(-2) if M > 1 else N
     sC = out.stride(0) if out.dim() == 3 else 0
@@ -80,18 +80,25 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
         ldcin = cin_t.stride(-2)
         sCin = cin_t.stride(0) if cin_t.dim() == 3 else 0
     bias_t = bias.float().contiguous() if bias is not None else None
+    ws = None
+    if splitk > 1:
+        if bias is not None or act is not None or cin_t is not None:
+            return None
+        ws = torch.empty(splitk * batch * M * N, dtype=torch.float32, device=a.device)
+        if batch > 1:
+            return None
     f = fn('hetu_gemm_bf16', _ARGS)
     check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), cin_t.data_ptr() if cin_t is not None else None,
             bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, ldcin,
             int(da[0]), int(db[0]), batch, da[2], db[2], sC, sCin, float(alpha), float(beta),
             _ACT[act], int(out.dtype == torch.float32),
             int(cin_t is not None and cin_t.dtype == torch.float32), int(bias_on_m), int(splitk),
-            int(accumulate), stream_ptr()), 'gemm_bf16')
+            int(accumulate), ws.data_ptr() if ws is not None else None, stream_ptr()), 'gemm_bf16')
     return out
 
 
 def try_gemm(a, b, ta, tb, bias=None, activation=None):
-    if MODE != 'hip':
+    if MODE in ('vendor', 'off'):
         return None
     A = a.transpose(-1, -2) if ta else a
     B = b.transpose(-1, -2) if tb else b
@@ -99,7 +106,7 @@ def try_gemm(a, b, ta, tb, bias=None, activation=None):
 
 
 def try_bmm(a, b, ta, tb):
-    if MODE != 'hip':
+    if MODE in ('vendor', 'off'):
         return None
     A = a.transpose(-1, -2) if ta else a
     B = b.transpose(-1, -2) if tb else b

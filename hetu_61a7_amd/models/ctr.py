@@ -168,3 +168,43 @@ def synthetic_criteo(n, feature_dimension=CRITEO_ROWS, seed=0, zipf=1.05):
     sparse = (offs + ranks).astype(np.int64)
     labels = (rng.random((n, 1)) < 0.25).astype(np.float32)
     return dense, sparse, labels
+
+
+def wdl_criteo_bench(args, world, rank, local):
+    """Benchmark step for the BASELINE Wide&Deep-Criteo configuration: full
+    33.76M x 128 embedding on the PS (host DRAM) behind an LFUOpt HET cache with
+    bound 3 (reference examples/ctr/tests/hybrid_wdl_criteo.sh), dense MLP on
+    the GPU (RCCL all-reduce when world > 1), SGD lr 0.01, per-worker batch 128.
+    Returns (step_fn, samples_per_step, config, metric, finish_fn)."""
+    import torch
+    import hetu_61a7_amd as ht
+    rows = int(getattr(args, 'criteo_rows', 0) or CRITEO_ROWS)
+    B = args.batch or 128
+    xd, xs, y_ = ht.Variable(name='dense_input'), ht.Variable(name='sparse_input'), ht.Variable(name='y_')
+    loss, y, _, train = wdl_criteo(xd, xs, y_, feature_dimension=rows, embedding_size=128, learning_rate=0.01)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(local), comm_mode='Hybrid',
+                     cstable_policy=getattr(args, 'cache', 'LFUOpt'), cache_bound=3, bsp=-1,
+                     mixed_precision=args.dtype, seed=1234)
+    nb = 64
+    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + rank)
+    dev = torch.device('cuda', local)
+    D = torch.from_numpy(dense).to(dev)
+    L = torch.from_numpy(labels).to(dev)
+    S = torch.from_numpy(sparse)
+    it = [0]
+
+    def step():
+        i = it[0] % nb
+        it[0] += 1
+        sl = slice(i * B, (i + 1) * B)
+        ex.run('train', feed_dict={xd: D[sl], xs: S[sl], y_: L[sl]})
+
+    def finish():
+        from ..ps import worker
+        ex.config.ps_comm.BarrierWorker()
+        worker.worker_finish()
+
+    cfg = {'model': 'Wide&Deep (Criteo-shaped, %d x 128 embedding)' % rows, 'global_batch': B * world,
+           'seq_len': None, 'parallelism': 'hybrid: PS(1 server)+HET cache lfuopt/3 + dp%d' % world,
+           'optimizer': 'sgd', 'per_gpu_batch': B}
+    return step, B * world, cfg, 'samples/sec (whole node) Wide&Deep-Criteo PS + HET cache', finish

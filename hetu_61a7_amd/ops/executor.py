@@ -73,11 +73,27 @@ def sum_node_list(node_list, ctx=None):
     return sum_op(node_list, ctx=ctx)
 
 
+def _mark_backward(roots, start_id, origin):
+    stack = [r for r in roots if r is not None]
+    while stack:
+        n = stack.pop()
+        if n.id < start_id or getattr(n, 'bw_of', None) is not None:
+            continue
+        n.bw_of = origin
+        stack.extend(i for i in n.inputs if i is not None)
+
+
 def gradients(output_node, node_list, insert_grad=None, return_all=False):
-    """Reverse-mode autodiff (reference executor.py:1066-1181)."""
+    """Reverse-mode autodiff (reference executor.py:1066-1181).
+
+    Every node created while differentiating forward node X is tagged
+    ``bw_of = X`` -- the pipeline partitioner places it on X's stage."""
     from .basic import oneslike_op
+    from . import node as _N
+    start = _N.G_NODE_ID
     if insert_grad is None:
         insert_grad = oneslike_op(output_node, ctx=output_node.raw_ctx)
+    _mark_backward([insert_grad], start, output_node)
     node_to_grads = {output_node: [insert_grad]}
     node_to_output_grad = {}
     backward2forward = {}
@@ -86,11 +102,13 @@ def gradients(output_node, node_list, insert_grad=None, return_all=False):
     for node in reversed(topo):
         if node not in node_to_grads:
             continue
+        start = _N.G_NODE_ID
         grad = sum_node_list(node_to_grads[node], ctx=node.raw_ctx)
         node_to_output_grad[node] = grad
         if grad is None:
             continue
         input_grads = node.gradient(grad)
+        _mark_backward([grad] + list(input_grads or []), start, node)
         if input_grads is None:
             continue
         forward2backward[node] = [g for g in input_grads if g is not None]
@@ -161,6 +179,10 @@ class HetuConfig(object):
             self.context = ctx
             self.node_strategy = {}
             self.device_group = None
+        if pipeline is not None:
+            # one process per GPU: this rank's device is its own GPU ordinal
+            self.context = ndarray.gpu(local) if torch.cuda.is_available() else ndarray.cpu(0)
+            launch_mpi = launch_ps = False
         if comm_mode is None:
             if launch_mpi and launch_ps:
                 comm_mode = 'Hybrid'

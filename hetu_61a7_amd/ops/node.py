@@ -135,6 +135,13 @@ class Op(object):
 
     # hooks (reference Node.py:192-213) ------------------------------------------
     def forward_hook(self, config):
+        if getattr(config, 'pipeline', None) is not None:
+            # pipeline: each process computes only its own stage, on its own
+            # device; cross-stage edges are p2p messages, not transfer ops
+            self.ctx = config.context
+            self.on_gpu = ndarray.is_gpu_ctx(self.ctx)
+            self.on_cpu = not self.on_gpu
+            return
         if self.ctx is None:
             self.ctx = config.context
         elif isinstance(self.ctx, DeviceGroup):

@@ -1,0 +1,356 @@
+"""Pipeline-parallel sub-executors: GPipe, PipeDream (1F1B) and HetPipe.
+
+Reference: ``pipeline_subexecutor.py:13-130`` (stage partition),
+``gpipe_subexecutor.py:8-123`` (all forwards, then all backwards, one update),
+``pipedream_subexecutor.py:25-48`` (1F1B generator) and ``:51-372``,
+HetPipe = PipeDream + PS-held weights (``:77-83,149-176``); SURVEY §2.3 S6-S8.
+
+MI355X design
+-------------
+* One process per GPU.  A *stage* is the device set of a ``with
+  ht.context(...)`` block; a stage with several devices is data-parallel
+  inside (replica ``r`` of stage ``s`` talks to replica ``r`` of stage
+  ``s+1``), and its parameter gradients are all-reduced over the replica
+  group with the same bucketed RCCL path as plain DP.
+* Partitioning is automatic: forward nodes go to their context's stage, every
+  node created while differentiating forward node X goes to X's stage (the
+  ``bw_of`` tag written by ``gradients``), and every cross-stage edge becomes
+  one point-to-point message (RCCL send/recv over xGMI; gloo on CPU).  Sends
+  are asynchronous, receives block, so any schedule in which each stage
+  processes micro-batches in the same order is deadlock-free.
+* Schedules: ``gpipe`` (F0..Fm-1, B0..Bm-1), ``pipedream`` (1F1B: warm-up of
+  ``stages - s - 1`` forwards then alternate, cooldown), ``hetpipe`` (1F1B plus
+  a PS sync of the stage's dense parameters each step).  Gradients of a step
+  are accumulated over micro-batches and applied once (pipeline flush), which
+  keeps the step semantics of the non-pipelined model.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import ndarray
+from ..ops.node import Op
+from ..ops.variable import PlaceholderOp
+from ..ops.executor import find_topo_sort, AuxResult, _shape_of
+
+_DT = {0: torch.float32, 1: torch.bfloat16, 2: torch.float16, 3: torch.int64, 4: torch.int32}
+_DT_INV = {v: k for k, v in _DT.items()}
+HDR = 10
+
+
+def _dev_key(ctx):
+    if isinstance(ctx, ndarray.DLContext):
+        return (ctx.hostname, 'gpu' if ndarray.is_gpu_ctx(ctx) else 'cpu', ctx.device_id)
+    return ctx
+
+
+def _group_key(raw_ctx):
+    if raw_ctx is None:
+        return None
+    return tuple(_dev_key(d) for d in raw_ctx.all_devices())
+
+
+class _P2P(object):
+    """Async tensor send (header + payload) / blocking receive over torch.distributed."""
+
+    def __init__(self, device):
+        self.device = device
+        self.pending = []
+
+    def send(self, t, dst):
+        t = t.contiguous()
+        hdr = torch.zeros(HDR, dtype=torch.int64)
+        hdr[0] = t.dim()
+        hdr[1] = _DT_INV[t.dtype]
+        hdr[2:2 + t.dim()] = torch.tensor(list(t.shape), dtype=torch.int64)
+        hdr = hdr.to(t.device)
+        self.pending.append((dist.isend(hdr, dst), hdr))
+        self.pending.append((dist.isend(t, dst), t))
+
+    def recv(self, src):
+        hdr = torch.zeros(HDR, dtype=torch.int64, device=self.device)
+        dist.irecv(hdr, src).wait()
+        h = hdr.tolist()
+        nd, dt = int(h[0]), _DT[int(h[1])]
+        out = torch.empty(tuple(int(x) for x in h[2:2 + nd]), dtype=dt, device=self.device)
+        dist.irecv(out, src).wait()
+        return out
+
+    def flush(self):
+        for w, _ in self.pending:
+            w.wait()
+        self.pending = []
+
+
+def pipedream_schedule(stage, nstages, m):
+    """1F1B order for one stage: list of ('F'|'B', micro-batch)."""
+    warm = min(nstages - stage - 1, m)
+    order = [('F', i) for i in range(warm)]
+    f, b = warm, 0
+    while b < m:
+        if f < m:
+            order.append(('F', f))
+            f += 1
+        order.append(('B', b))
+        b += 1
+    return order
+
+
+def gpipe_schedule(stage, nstages, m):
+    return [('F', i) for i in range(m)] + [('B', i) for i in range(m)]
+
+
+class PipelineSubExecutor(object):
+    def __init__(self, kind, name, eval_node_list, config):
+        from ..optimizer import OptimizerOp
+        assert kind in ('gpipe', 'pipedream', 'hetpipe'), kind
+        self.kind, self.name, self.config = kind, name, config
+        self.eval_node_list = list(eval_node_list)
+        topo = find_topo_sort(self.eval_node_list)
+        self.opt_nodes = [n for n in topo if isinstance(n, OptimizerOp)]
+        self.inference = not self.opt_nodes
+
+        # ---- stages ----------------------------------------------------------------------
+        order = []
+        for n in topo:
+            if isinstance(n, OptimizerOp) or getattr(n, 'bw_of', None) is not None:
+                continue
+            k = _group_key(n.raw_ctx)
+            if k is not None and k not in order:
+                order.append(k)
+        assert order, 'pipeline needs nodes placed with ht.context(...)'
+        self.stage_keys = order
+        self.nstages = len(order)
+        stage_of: Dict[Op, int] = {}
+        for n in topo:
+            if isinstance(n, OptimizerOp):
+                continue
+            origin = getattr(n, 'bw_of', None)
+            while origin is not None and getattr(origin, 'bw_of', None) is not None:
+                origin = origin.bw_of
+            src = origin if origin is not None else n
+            k = _group_key(src.raw_ctx)
+            if k is None:
+                k = order[-1]
+            stage_of[n] = order.index(k)
+        self.stage_of = stage_of
+
+        # ---- my stage / replica ------------------------------------------------------------
+        rank = config.rank
+        self.stage = self.replica = None
+        for s, key in enumerate(order):
+            devs = [d for d in key if d[1] == 'gpu']
+            ids = [d[2] for d in devs]
+            if config.local_rank in ids:
+                self.stage, self.replica = s, ids.index(config.local_rank)
+        assert self.stage is not None, 'rank %d has no pipeline stage' % rank
+        self.nreplica = len([d for d in order[self.stage] if d[1] == 'gpu'])
+        # global rank of (stage, replica): ranks are GPU ordinals on one node
+        self.rank_of = lambda s, r: [d[2] for d in order[s] if d[1] == 'gpu'][r]
+
+        # ---- phases and local node lists ----------------------------------------------------
+        backward = set()
+        for n in topo:
+            if isinstance(n, OptimizerOp):
+                continue
+            if getattr(n, 'bw_of', None) is not None or any(i in backward for i in n.inputs):
+                backward.add(n)
+        self.backward = backward
+        mine = [n for n in topo if stage_of.get(n) == self.stage]
+        self.params = [n for n in mine if isinstance(n, PlaceholderOp) and n.is_param]
+        self.feeds = [n for n in mine if isinstance(n, PlaceholderOp) and not n.is_param]
+        from ..dataloader import DataloaderOp
+        self.loaders = [n for n in mine if isinstance(n, DataloaderOp)]
+        comp = [n for n in mine if not isinstance(n, (PlaceholderOp, DataloaderOp))]
+        self.fwd = [n for n in comp if n not in backward]
+        self.bwd = [n for n in comp if n in backward]
+
+        # ---- messages ---------------------------------------------------------------------
+        self.recv_msgs = {'F': [], 'B': []}
+        self.send_msgs = {'F': [], 'B': []}
+        seen = set()
+        for n in topo:
+            if n not in stage_of:
+                continue
+            for inp in n.inputs:
+                if inp is None or inp not in stage_of:
+                    continue
+                a, b = stage_of[inp], stage_of[n]
+                if a == b or (inp, b) in seen:
+                    continue
+                seen.add((inp, b))
+                phase = 'B' if inp in backward else 'F'
+                if phase == 'F':
+                    assert a < b, 'forward edge %s -> %s goes to an earlier stage' % (inp.name, n.name)
+                else:
+                    assert a > b, 'backward edge %s -> %s goes to a later stage' % (inp.name, n.name)
+                if b == self.stage:
+                    self.recv_msgs[phase].append((inp.id, a, inp))
+                if a == self.stage:
+                    self.send_msgs[phase].append((b, inp.id, inp))
+        for ph in ('F', 'B'):
+            self.recv_msgs[ph].sort(key=lambda t: (t[1], t[0]))
+            self.send_msgs[ph].sort(key=lambda t: (t[0], t[1]))
+
+        # replica groups: dist.new_group is collective over the world, so every
+        # rank creates every stage's group in the same order
+        self.replica_comms = {}
+        if any(len([d for d in k if d[1] == 'gpu']) > 1 for k in order) and dist.is_initialized():
+            from . import comm as C
+            for s, key in enumerate(order):
+                ranks = [d[2] for d in key if d[1] == 'gpu']
+                if len(ranks) > 1:
+                    self.replica_comms[s] = C.new_group_comm(ranks)
+
+        # ---- parameters, local optimizer ----------------------------------------------------
+        for p in self.params:
+            config.init_param(p)
+        self.opt = None
+        if self.opt_nodes:
+            self._build_local_optimizer()
+        self.p2p = _P2P(config.device)
+        self.step_count = 0
+
+    # ---------------------------------------------------------------------------------------
+    def _build_local_optimizer(self):
+        from ..optimizer import OptimizerOp
+        import copy
+        gop = self.opt_nodes[0]
+        local = [(p, g) for p, g in zip(gop.param_of_input, gop.inputs) if self.stage_of.get(g) == self.stage]
+        self.local_grads = {g: i for i, (p, g) in enumerate(local)}
+        if not local:
+            return
+        opt = copy.copy(gop.optimizer)
+        opt.params = [p for p, _ in local]
+        op = OptimizerOp.__new__(OptimizerOp)
+        OptimizerOp.__init__(op, [g for _, g in local], opt)
+        op.forward_hook(self.config)
+        op.config = self.config
+        op.bucket_bytes = int(getattr(self.config, 'bucket_mb', 32) * (1 << 20))
+        op.ps_dense = None
+        op.ps_dense_wanted = False
+        if self.nreplica > 1:
+            op.comm = self.replica_comms[self.stage]
+            op.dp = True
+        op.setup(self.config, list(range(len(local))))
+        self.opt = op
+        if self.kind == 'hetpipe' and self.config.ps_comm is not None:
+            from ..ps.table import PSDense
+            op.ps_dense = PSDense(op.flat, (1 << 21) + self.stage, self.config)
+
+    # ---------------------------------------------------------------------------------------
+    def _compute(self, nodes, vals, aux):
+        for n in nodes:
+            args = []
+            so = set(getattr(n, 'shape_only_inputs', ()))
+            ax = set(getattr(n, 'aux_inputs', ()))
+            va = set(getattr(n, 'value_and_aux_inputs', ()))
+            for k, inp in enumerate(n.inputs):
+                if k in so:
+                    args.append(_shape_of(vals[inp]))
+                elif k in va:
+                    args.append((vals[inp], aux[inp]))
+                elif k in ax:
+                    args.append(aux[inp])
+                else:
+                    args.append(vals[inp])
+            r = n.compute(args)
+            if isinstance(r, AuxResult):
+                aux[n] = r.aux
+                r = r.value
+            vals[n] = r
+
+    def _peer(self, stage):
+        return self.rank_of(stage, self.replica if self.nreplica > 1 else 0)
+
+    def _phase(self, ph, mb, state):
+        vals, aux = state
+        for _, src, node in self.recv_msgs[ph]:
+            vals[node] = self.p2p.recv(self._peer(src))
+        self._compute(self.fwd if ph == 'F' else self.bwd, vals, aux)
+        for dst, _, node in self.send_msgs[ph]:
+            v = vals[node]
+            if isinstance(v, ndarray.IndexedSlices):
+                v = v.to_dense()
+            self.p2p.send(v, self._peer(dst))
+
+    def run(self, eval_node_list=None, feed_dict=None, convert_to_numpy_ret_vals=False, batch_num=None, **kw):
+        cfg = self.config
+        feed_dict = feed_dict or {}
+        m = int(batch_num or 1)
+        for n in find_topo_sort(self.eval_node_list):
+            if hasattr(n, 'inference'):
+                n.inference = self.inference
+        states = []
+        for mb in range(m):
+            vals, aux = {}, {}
+            for p in self.params:
+                vals[p] = cfg.compute_value(p)
+            for n in self.feeds:
+                if n in feed_dict:
+                    v = feed_dict[n]
+                    v = v.tensor if isinstance(v, ndarray.NDArray) else v
+                    v = torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v)
+                    chunk = v.shape[0] // m
+                    v = v[mb * chunk:(mb + 1) * chunk]
+                    if v.dtype == torch.float64:
+                        v = v.float()
+                    vals[n] = v.to(cfg.device)
+            states.append((vals, aux))
+        if self.inference:
+            sched = [('F', i) for i in range(m)]
+        elif self.kind == 'gpipe':
+            sched = gpipe_schedule(self.stage, self.nstages, m)
+        else:
+            sched = pipedream_schedule(self.stage, self.nstages, m)
+        acc = {}
+        results = [None] * m
+        for ph, mb in sched:
+            vals, aux = states[mb]
+            if ph == 'F':
+                for d in self.loaders:
+                    vals[d] = d.get_arr(self.name, cfg)
+            self._phase(ph, mb, states[mb])
+            if ph == 'B' or self.inference:
+                results[mb] = self._outputs(vals, convert_to_numpy_ret_vals)
+                if self.opt is not None:
+                    for g, i in self.local_grads.items():
+                        v = vals.get(g)
+                        if v is None:
+                            continue
+                        if isinstance(v, ndarray.IndexedSlices):
+                            v = v.to_dense()
+                        acc[i] = v.float() if i not in acc else acc[i] + v.float()
+                states[mb] = None
+        self.p2p.flush()
+        if self.opt is not None and acc:
+            op = self.opt
+            op.begin_step()
+            for i in range(len(op.inputs)):
+                if i in acc:
+                    op.on_grad_ready(i, acc[i])
+            op.compute([])
+        self.step_count += 1
+        return results
+
+    def _outputs(self, vals, convert):
+        out = []
+        for n in self.eval_node_list:
+            v = vals.get(n)
+            if v is None or not isinstance(v, torch.Tensor):
+                out.append(None)
+            elif convert:
+                out.append(v.detach().float().cpu().numpy())
+            else:
+                out.append(ndarray.NDArray(v))
+        return out
+
+    @property
+    def batch_num(self):
+        nums = [d.get_batch_num(self.name) for d in self.loaders]
+        nums = [x for x in nums if x is not None]
+        return min(nums) if nums else None

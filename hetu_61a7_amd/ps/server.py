@@ -6,7 +6,7 @@ finalised.  The scheduler role has nothing to coordinate on one node beyond
 what the segment's header does (barriers, heartbeats, SSP, PReduce) and simply
 returns.
 
-    python -m hetu_61a7_amd.ps.server         # DMLC_ROLE=server
+    python -m hetu_61a7_amd.ps                # DMLC_ROLE=server
 """
 from __future__ import annotations
 
@@ -49,9 +49,17 @@ def scheduler_finish():
     _ROLE = None
 
 
-def run_server():
+def run_server(poll_s=2.0):
+    """Serve until all workers finalised; exits early if the launcher died
+    (re-parented process), so a crashed job never leaves a server behind."""
+    global _ROLE
     server_init()
-    server_finish()
+    parent = os.getppid()
+    while lib('hps_server_wait_shutdown')(float(poll_s)) != 0:
+        if os.getppid() != parent:
+            break
+    lib('hps_finalize')()
+    _ROLE = None
 
 
 if __name__ == '__main__':

@@ -49,8 +49,19 @@ class _Staging(object):
             self.event.record()
 
 
+_LIVE = []
+
+
+def close_all():
+    """Drain outstanding pushes of every PS table (before the worker finalises)."""
+    for t in _LIVE:
+        t.close()
+    _LIVE.clear()
+
+
 class PSTable(object):
     def __init__(self, node, config):
+        _LIVE.append(self)
         self.node = node
         self.key = node.id
         self.agent = psw.get_agent()
@@ -151,6 +162,12 @@ class PSTable(object):
         elif self.bsp and self.bsp > 0:
             self._wait_push()
             self.agent.ssp_sync(self.key, self.version)
+
+    def close(self):
+        self.flush_grad()
+        self._wait_push()
+        if self.cache is not None:
+            self.cache.flush()
 
     def to_dense(self):
         """Full table (host) -- checkpointing / tests."""

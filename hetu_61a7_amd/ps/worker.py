@@ -209,6 +209,8 @@ def get_agent():
 def worker_finish():
     global _AGENT
     if _AGENT is not None:
+        from .table import close_all
+        close_all()
         _AGENT.finalize()
         _AGENT = None
 

@@ -15,9 +15,9 @@
 // pass over memory.
 //
 // Geometry: 128x128x64 block tile, 256 threads = 4 waves (2 M x 2 N), each wave
-// 64x64 = 4x4 mfma_f32_16x16x32_bf16 tiles; LDS double buffer (2 x 32 KiB),
-// register-staged prefetch of tile k+1 during the MFMAs of tile k, one barrier
-// per K-tile.  Operand roles are swapped (A_op = N side, B_op = M side) so the
+// 64x64 = 4x4 mfma_f32_16x16x32_bf16 tiles; LDS double buffer (2 x 32 KiB)
+// filled by global_load_lds (16 B/lane, swizzle applied on the source address),
+// tile k+1 in flight during the MFMAs of tile k, one barrier per K-tile.  Operand roles are swapped (A_op = N side, B_op = M side) so the
 // accumulator holds 4 consecutive N columns per lane -> 8/16-byte stores.
 // Block ids are remapped so that consecutive tiles share an XCD's L2, then
 // grouped 8 tiles along M for operand reuse.  Split-K over gridDim.z with
@@ -36,8 +36,8 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = 128 * BK * 2;  // 16 KiB per operand tile
 
-__device__ __forceinline__ v8s zero8() { return v8s{0, 0, 0, 0, 0, 0, 0, 0}; }
-__device__ __forceinline__ v8s ld8(const bf16* p) { return *reinterpret_cast<const v8s*>(p); }
+
+
 
 // ---- LDS images -------------------------------------------------------------------------
 // K-major: [128 rows][64 k] bf16, 128-B rows, chunk c (0..7) of row r at ((c ^ (r&7)) << 4)
@@ -47,13 +47,13 @@ __device__ __forceinline__ int offmn(int k, int c) {
   return k * 256 + ((c ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4);
 }
 
-template <bool KMAJ>
-__device__ __forceinline__ void lds_store(char* lds, const v8s* reg, int tid) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int off = KMAJ ? offk((tid >> 3) + 32 * i, tid & 7) : offmn((tid >> 4) + 16 * i, tid & 15);
-    *reinterpret_cast<v8s*>(lds + off) = reg[i];
-  }
+// Zero chunk that out-of-range / padding lanes stage from (global_load_lds has no
+// per-lane predicate: the lane still writes its LDS slot, so it reads zeros).
+__device__ __attribute__((aligned(64))) bf16 g_zero_chunk[32];
+
+__device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
 // fragment of 16 rows (row block rb) x 32 k (k-step s): lane holds row (lane&15),
@@ -77,29 +77,36 @@ __device__ __forceinline__ v8s lds_frag(const char* lds, int rb, int s, int lane
 }
 
 // ---- operand loaders ------------------------------------------------------------------
-// Each thread owns 4 16-byte chunks of the 128x64 tile.  KMAJ: rows (tid>>3)+32i,
-// chunk tid&7 (k = k0 + 8*(tid&7)).  MN: k rows (tid>>4)+16i, chunk tid&15
-// (cols r0 + 8*(tid&15)).
+// The 128x64 tile is staged by 16 global_load_lds instructions (4 per wave), each
+// filling 1 KiB of LDS lane-linearly: instruction i of wave w covers LDS bytes
+// [4096w + 1024i, +1024).  The swizzle is applied on the SOURCE side: lane l of
+// that instruction fetches the logical chunk that belongs at its physical slot.
+//   KMAJ: row r = 32w + 8i + (l>>3), physical chunk l&7, logical c = (l&7) ^ (l>>3)
+//   MN  : k   = 16w + 4i + (l>>4), physical chunk l&15, logical
+//         c = (l&15) ^ (((l>>4)&3)<<2 | i)
+// Loaders return, per instruction i, the global address of that chunk (or the
+// zero chunk).
+
+__device__ __forceinline__ const bf16* zchunk() { return g_zero_chunk; }
 
 // plain row-major operand with contiguous K: element (r, k) at base[r*ld + k]
 struct PlainK {
   static constexpr bool KMAJ = true;
   const bf16* base; int64_t ld, rows, K, bstride;
   int64_t roff[4]; bool rok[4]; int ch;
-  __device__ void init(int64_t r0, int tid, int64_t batch) {
+  __device__ void init(int64_t r0, int w, int l, int64_t batch) {
     base += batch * bstride;
-    ch = tid & 7;
+    ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + (tid >> 3) + 32 * i;
+      int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
       rok[i] = r < rows;
       roff[i] = r * ld;
     }
   }
-  __device__ void load(int64_t k0, v8s* reg) const {
+  __device__ const bf16* src(int64_t k0, int i) const {
     int64_t k = k0 + ch * 8;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) reg[i] = (rok[i] && k < K) ? ld8(base + roff[i] + k) : zero8();
+    return (rok[i] && k < K) ? base + roff[i] + k : zchunk();
   }
 };
 
@@ -107,19 +114,20 @@ struct PlainK {
 struct PlainMN {
   static constexpr bool KMAJ = false;
   const bf16* base; int64_t ld, rows, K, bstride;
-  int64_t col; bool cok; int kr;
-  __device__ void init(int64_t r0, int tid, int64_t batch) {
+  int64_t col[4]; bool cok[4]; int kr;
+  __device__ void init(int64_t r0, int w, int l, int64_t batch) {
     base += batch * bstride;
-    col = r0 + (tid & 15) * 8;
-    cok = col < rows;
-    kr = tid >> 4;
-  }
-  __device__ void load(int64_t k0, v8s* reg) const {
+    kr = 16 * w + (l >> 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t k = k0 + kr + 16 * i;
-      reg[i] = (cok && k < K) ? ld8(base + k * ld + col) : zero8();
+      int c = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
+      col[i] = r0 + 8 * c;
+      cok[i] = col[i] < rows;
     }
+  }
+  __device__ const bf16* src(int64_t k0, int i) const {
+    int64_t k = k0 + kr + 4 * i;
+    return (cok[i] && k < K) ? base + k * ld + col[i] : zchunk();
   }
 };
 
@@ -132,11 +140,11 @@ struct ConvFwdA {
   static constexpr bool KMAJ = true;
   const bf16* x; ConvGeom g; int64_t Ktot, rows;
   int64_t nb[4]; int ih0[4], iw0[4]; bool rok[4]; int ch;
-  __device__ void init(int64_t r0, int tid, int64_t) {
-    ch = tid & 7;
+  __device__ void init(int64_t r0, int w, int l, int64_t) {
+    ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + (tid >> 3) + 32 * i;
+      int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
       rok[i] = r < rows;
       int64_t rr = rok[i] ? r : 0;
       int ow = (int)(rr % g.OW);
@@ -148,18 +156,14 @@ struct ConvFwdA {
       iw0[i] = ow * g.sw - g.pw;
     }
   }
-  __device__ void load(int64_t k0, v8s* reg) const {
+  __device__ const bf16* src(int64_t k0, int i) const {
     int64_t k = k0 + ch * 8;
     int tap = (int)(k / g.C);
     int ci = (int)(k - (int64_t)tap * g.C);
     int kh = tap / g.KW, kw = tap - kh * g.KW;
-    bool kok = k < Ktot;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int ih = ih0[i] + kh, iw = iw0[i] + kw;
-      bool ok = kok && rok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-      reg[i] = ok ? ld8(x + ((nb[i] + ih) * g.W + iw) * g.C + ci) : zero8();
-    }
+    int ih = ih0[i] + kh, iw = iw0[i] + kw;
+    bool ok = k < Ktot && rok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+    return ok ? x + ((nb[i] + ih) * g.W + iw) * g.C + ci : zchunk();
   }
 };
 
@@ -168,11 +172,11 @@ struct ConvDgradA {
   static constexpr bool KMAJ = true;
   const bf16* dy; ConvGeom g; int64_t Ktot, rows;
   int64_t nb[4]; int ih[4], iw[4]; bool rok[4]; int ch;
-  __device__ void init(int64_t r0, int tid, int64_t) {
-    ch = tid & 7;
+  __device__ void init(int64_t r0, int w, int l, int64_t) {
+    ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + (tid >> 3) + 32 * i;
+      int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
       rok[i] = r < rows;
       int64_t rr = rok[i] ? r : 0;
       iw[i] = (int)(rr % g.W);
@@ -181,20 +185,16 @@ struct ConvDgradA {
       nb[i] = (t / g.H) * g.OH;
     }
   }
-  __device__ void load(int64_t k0, v8s* reg) const {
+  __device__ const bf16* src(int64_t k0, int i) const {
     int64_t k = k0 + ch * 8;
     int tap = (int)(k / g.K);
     int co = (int)(k - (int64_t)tap * g.K);
     int kh = tap / g.KW, kw = tap - kh * g.KW;
-    bool kok = k < Ktot;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int th = ih[i] + g.ph - kh, tw = iw[i] + g.pw - kw;
-      int oh = th / g.sh, ow = tw / g.sw;
-      bool ok = kok && rok[i] && th >= 0 && tw >= 0 && oh * g.sh == th && ow * g.sw == tw &&
-                oh < g.OH && ow < g.OW;
-      reg[i] = ok ? ld8(dy + ((nb[i] + oh) * g.OW + ow) * g.K + co) : zero8();
-    }
+    int th = ih[i] + g.ph - kh, tw = iw[i] + g.pw - kw;
+    int oh = th / g.sh, ow = tw / g.sw;
+    bool ok = k < Ktot && rok[i] && th >= 0 && tw >= 0 && oh * g.sh == th && ow * g.sw == tw &&
+              oh < g.OH && ow < g.OW;
+    return ok ? dy + ((nb[i] + oh) * g.OW + ow) * g.K + co : zchunk();
   }
 };
 
@@ -202,21 +202,21 @@ struct ConvDgradA {
 struct ConvDgradB {
   static constexpr bool KMAJ = false;
   const bf16* w; ConvGeom g; int64_t Ktot;
-  int col; bool cok; int kr;
-  __device__ void init(int64_t r0, int tid, int64_t) {
-    col = (int)r0 + (tid & 15) * 8;
-    cok = col < g.C;
-    kr = tid >> 4;
-  }
-  __device__ void load(int64_t k0, v8s* reg) const {
-    const int taps = g.KH * g.KW;
+  int col[4]; bool cok[4]; int kr;
+  __device__ void init(int64_t r0, int wv, int l, int64_t) {
+    kr = 16 * wv + (l >> 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t k = k0 + kr + 16 * i;
-      int tap = (int)(k / g.K);
-      int co = (int)(k - (int64_t)tap * g.K);
-      reg[i] = (cok && k < Ktot) ? ld8(w + ((int64_t)co * taps + tap) * g.C + col) : zero8();
+      int c = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
+      col[i] = (int)r0 + 8 * c;
+      cok[i] = col[i] < g.C;
     }
+  }
+  __device__ const bf16* src(int64_t k0, int i) const {
+    int64_t k = k0 + kr + 4 * i;
+    int tap = (int)(k / g.K);
+    int co = (int)(k - (int64_t)tap * g.K);
+    return (cok[i] && k < Ktot) ? w + ((int64_t)co * (g.KH * g.KW) + tap) * g.C + col[i] : zchunk();
   }
 };
 
@@ -224,28 +224,29 @@ struct ConvDgradB {
 struct ConvWgradB {
   static constexpr bool KMAJ = false;
   const bf16* x; ConvGeom g; int64_t P;  // P = N*OH*OW
-  int kh, kw, ci; bool cok; int kr;
-  __device__ void init(int64_t r0, int tid, int64_t) {
-    int col = (int)r0 + (tid & 15) * 8;
-    cok = col < g.KH * g.KW * g.C;
-    int tap = col / g.C;
-    ci = col - tap * g.C;
-    kh = tap / g.KW;
-    kw = tap - kh * g.KW;
-    kr = tid >> 4;
-  }
-  __device__ void load(int64_t k0, v8s* reg) const {
+  int kh[4], kw[4], ci[4]; bool cok[4]; int kr;
+  __device__ void init(int64_t r0, int w, int l, int64_t) {
+    kr = 16 * w + (l >> 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t p = k0 + kr + 16 * i;
-      int ow = (int)(p % g.OW);
-      int64_t t = p / g.OW;
-      int oh = (int)(t % g.OH);
-      int64_t n = t / g.OH;
-      int ih = oh * g.sh - g.ph + kh, iw = ow * g.sw - g.pw + kw;
-      bool ok = cok && p < P && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-      reg[i] = ok ? ld8(x + ((n * g.H + ih) * g.W + iw) * g.C + ci) : zero8();
+      int c = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
+      int col = (int)r0 + 8 * c;
+      cok[i] = col < g.KH * g.KW * g.C;
+      int tap = col / g.C;
+      ci[i] = col - tap * g.C;
+      kh[i] = tap / g.KW;
+      kw[i] = tap - kh[i] * g.KW;
     }
+  }
+  __device__ const bf16* src(int64_t k0, int i) const {
+    int64_t p = k0 + kr + 4 * i;
+    int ow = (int)(p % g.OW);
+    int64_t t = p / g.OW;
+    int oh = (int)(t % g.OH);
+    int64_t n = t / g.OH;
+    int ih = oh * g.sh - g.ph + kh[i], iw = ow * g.sw - g.pw + kw[i];
+    bool ok = cok[i] && p < P && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+    return ok ? x + ((n * g.H + ih) * g.W + iw) * g.C + ci[i] : zchunk();
   }
 };
 
@@ -288,8 +289,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   const int tn = (wg % per_group) / gsz;
 
   const int64_t batch = blockIdx.y;
-  la.init((int64_t)tm * BM, tid, batch);
-  lb.init((int64_t)tn * BN, tid, batch);
+  la.init((int64_t)tm * BM, wave, lane, batch);
+  lb.init((int64_t)tn * BN, wave, lane, batch);
 
   const int nkt = (int)((K + BK - 1) / BK);
   const int kt0 = blockIdx.z * ktps;
@@ -301,21 +302,23 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  v8s ra[4], rb[4];
-  if (kt0 < kt1) {
-    la.load((int64_t)kt0 * BK, ra);
-    lb.load((int64_t)kt0 * BK, rb);
-    lds_store<LA::KMAJ>(smem[0], ra, tid);
-    lds_store<LB::KMAJ>(smem[0] + TILE_BYTES, rb, tid);
-  }
+  // stage K-tile kt into LDS buffer b: 4 + 4 global_load_lds per wave
+  auto stage = [&](int kt, int b) {
+    char* As = smem[b] + 4096 * wave;
+    char* Bs = smem[b] + TILE_BYTES + 4096 * wave;
+    const int64_t k0 = (int64_t)kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(la.src(k0, i), As + 1024 * i);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(lb.src(k0, i), Bs + 1024 * i);
+  };
+
+  if (kt0 < kt1) stage(kt0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) {
-      la.load((int64_t)(kt + 1) * BK, ra);
-      lb.load((int64_t)(kt + 1) * BK, rb);
-    }
+    if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
     const char* As = smem[cur];
     const char* Bs = smem[cur] + TILE_BYTES;
 #pragma unroll
@@ -331,10 +334,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[j], mf[i], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      lds_store<LA::KMAJ>(smem[cur ^ 1], ra, tid);
-      lds_store<LB::KMAJ>(smem[cur ^ 1] + TILE_BYTES, rb, tid);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 

@@ -1,15 +1,14 @@
 #!/bin/bash
-# Experiment run: vendor vs autotuned conv bench, profile of the autotuned run,
-# and a small-table WDL (PS + HET cache) smoke bench.
+# Experiment run: GEMM/conv tests, autotuned ResNet-50 bench + profile, WDL (PS + HET cache) bench.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONPATH=$PWD${PYTHONPATH:+:$PYTHONPATH}
 export TMPDIR=/tmp
 echo "== build"; make -C csrc -j16 > gpurun_out/build.log 2>&1 || { tail -20 gpurun_out/build.log; exit 1; }
-echo "== bench vendor"
-HETU_CONV=vendor HETU_GEMM=vendor timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_vendor.json 2> gpurun_out/bench_vendor.err || { tail -20 gpurun_out/bench_vendor.err; exit 1; }
-cat gpurun_out/bench_vendor.json
+echo "== gemm tests"
+timeout -k 10 300 python -m pytest tests/test_gemm_gpu.py -q -x > gpurun_out/gemm_tests.log 2>&1 || { tail -30 gpurun_out/gemm_tests.log; exit 1; }
+tail -2 gpurun_out/gemm_tests.log
 echo "== bench auto"
 HETU_AUTOTUNE_DUMP=gpurun_out/autotune.txt timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_auto.json 2> gpurun_out/bench_auto.err || { tail -20 gpurun_out/bench_auto.err; exit 1; }
 cat gpurun_out/bench_auto.json

@@ -273,7 +273,10 @@ __device__ __forceinline__ float act_f(float v, int act) {
 template <class LA, class LB>
 __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                   int64_t K, int tiles_m, int tiles_n, int ktps) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2 * TILE_BYTES];
+  // dynamic LDS: 2 x 32 KiB double buffer, or one 32 KiB buffer when every block
+  // owns a single K-tile (short-K 1x1 convolutions: more resident blocks per CU)
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  char* smem[2] = {smem_raw, smem_raw + (ktps > 1 ? 2 * TILE_BYTES : 0)};
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
 
@@ -414,6 +417,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   }
 }
 
+static inline size_t lds_bytes(int ktps) { return (ktps > 1 ? 4 : 2) * TILE_BYTES; }
+
 // dst[m][n] (ld ldd, fp32 or bf16) (+)= sum_z slab[z][m][n]
 __global__ void splitk_reduce_k(const float* __restrict__ slab, int64_t stride, int nz,
                                 void* dst, int64_t M, int64_t N, int64_t ldd, int out_f32,
@@ -449,8 +454,8 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
   if (ep.slab && splitk > 1) {
     Epi e2 = ep;
     e2.slab_stride = M * N;
-    hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K, tiles_m,
-                       tiles_n, ktps);
+    hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), lds_bytes(ktps), st, la, lb, e2, M, N,
+                       K, tiles_m, tiles_n, ktps);
     int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, ep.slab, M * N, splitk, ep.C, M,
                        N, ep.ldc, ep.out_f32, ep.atomic);
@@ -459,8 +464,8 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
   Epi e1 = ep;
   e1.slab = nullptr;
   if (splitk > 1) e1.atomic = 1;
-  hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m,
-                     tiles_n, ktps);
+  hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), lds_bytes(ktps), st, la, lb, e1, M, N,
+                     K, tiles_m, tiles_n, ktps);
   return (int)hipGetLastError();
 }
 
@@ -524,13 +529,14 @@ HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const flo
   return launch(la, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M, K, Kt, 1, 1, st);
 }
 
-// dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[K,KH,KW,C]).  K % 8 == 0, C % 8 == 0.
-HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, int N, int H, int W,
-                                  int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-                                  hipStream_t st) {
+// dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[K,KH,KW,C]) (+ acc[N,H,W,C] when given:
+// the gradient joined at the conv input, added in the epilogue).  K % 8 == 0, C % 8 == 0.
+HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const void* acc,
+                                  int acc_f32, int N, int H, int W, int C, int K, int KH, int KW,
+                                  int sh, int sw, int ph, int pw, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t M = (int64_t)N * H * W, Kt = (int64_t)KH * KW * K;
-  Epi ep{dx, nullptr, nullptr, C, 0, 0, 0, 1.f, 0.f, 0, 0, 0, 0, 0, nullptr, 0};
+  Epi ep{dx, acc, nullptr, C, C, 0, 0, 1.f, acc ? 1.f : 0.f, 0, 0, acc_f32, 0, 0, nullptr, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(PlainK{(const bf16*)dy, K, M, K, 0}, PlainMN{(const bf16*)w, C, C, K, 0}, ep, M,
                   C, K, 1, 1, st);

@@ -7,6 +7,10 @@ Rewrites (in place, preserving the identity of the user-visible output node):
 These are the memory-bound op chains that dominate ResNet time outside the
 convolutions; the reference runs each as its own cuDNN/elementwise call.
 Only applied when the intermediate values have no other consumer.
+
+Backward (``fuse_backward``, run on the gradient graph):
+  sum(conv_dgrad(w, g), r, ...)   -> conv_dgrad accumulating r in its epilogue
+                                     (the residual-branch gradient join of ResNet)
 """
 from __future__ import annotations
 
@@ -66,3 +70,37 @@ def _become_bn(node, bn, relu, residual):
     node.running_mean = bn.running_mean
     node.running_var = bn.running_var
     node.fused_from = bn
+
+
+def fuse_backward(roots):
+    """Fold gradient fan-in sums into the data-gradient GEMM epilogue."""
+    if os.environ.get('HETU_FUSE', '1') == '0':
+        return 0
+    from .ops.reduce import SumOp
+    from .ops.nn import Conv2d_Gradient_of_DataOp
+    topo, cons = _consumers(roots)
+    root_set = set(roots)
+    fused = 0
+    for n in topo:
+        if not isinstance(n, SumOp) or len(n.inputs) < 2:
+            continue
+        for d in n.inputs:
+            if isinstance(d, Conv2d_Gradient_of_DataOp) and len(d.inputs) == 3 and \
+                    len(cons.get(d, [])) == 1 and d not in root_set:
+                rest = [i for i in n.inputs if i is not d]
+                if len(rest) > 1:
+                    other = SumOp(rest, ctx=n.raw_ctx)
+                    other.bw_of = getattr(n, 'bw_of', None)
+                else:
+                    other = rest[0]
+                keep_id, keep_name, bw = n.id, n.name, getattr(n, 'bw_of', None)
+                n.__class__ = Conv2d_Gradient_of_DataOp
+                n.__dict__.update({k: v for k, v in d.__dict__.items() if k not in ('id', 'name', 'inputs', 'bw_of')})
+                n.inputs = list(d.inputs) + [other]
+                n.op_type = 'Conv2d_Gradient_of_DataOp'
+                n.id, n.name = keep_id, keep_name
+                if bw is not None:
+                    n.bw_of = bw
+                fused += 1
+                break
+    return fused

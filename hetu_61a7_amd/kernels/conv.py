@@ -62,19 +62,30 @@ def conv2d(x, w, b, stride, padding):
     return y
 
 
-def conv2d_backward_data(g, w, x_shape, stride, padding):
+def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None):
+    """dx (+ acc when given: a gradient joined at the conv input, fused into the
+    epilogue on the HIP path)."""
     g, w = _match(g, w)
     if g.is_cuda:
         g = g.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
+        if acc is not None:
+            acc = acc.contiguous(memory_format=CL)
         from . import conv_igemm
-        return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding)),
-                     lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding),
-                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding))
-    return _vendor_dgrad(g, w, x_shape, stride, padding)
+        return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
+                     lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
+                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc))
+    return _vendor_dgrad(g, w, x_shape, stride, padding, acc)
 
 
-def _vendor_dgrad(g, w, x_shape, stride, padding):
+def _vendor_dgrad(g, w, x_shape, stride, padding, acc=None):
+    dx = _vendor_dgrad0(g, w, x_shape, stride, padding)
+    if acc is not None:
+        dx = dx + acc.to(dx.dtype)
+    return dx
+
+
+def _vendor_dgrad0(g, w, x_shape, stride, padding):
     xs = torch.empty(x_shape, dtype=g.dtype, device=g.device)
     if g.is_cuda:
         xs = xs.contiguous(memory_format=CL)

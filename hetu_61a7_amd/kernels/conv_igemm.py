@@ -48,15 +48,20 @@ def try_forward(x, w, stride, padding, bias=None, act=None):
     return y.permute(0, 3, 1, 2)
 
 
-def try_backward_data(g, w, x_shape, stride, padding):
+def try_backward_data(g, w, x_shape, stride, padding, acc=None):
     if not _ok(g, w, x_shape[1], w.shape[0]):
+        return None
+    if acc is not None and (tuple(acc.shape) != tuple(x_shape) or
+                            not acc.is_contiguous(memory_format=CL) or
+                            acc.dtype not in (torch.bfloat16, torch.float32)):
         return None
     N, C, H, W = x_shape
     K, _, KH, KW = w.shape
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
-    f = fn('hetu_conv_dgrad_bf16', [P, P, P] + _GEOM + [P])
-    check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
-            padding[0], padding[1], stream_ptr()), 'conv_dgrad')
+    f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [P])
+    check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
+            int(acc is not None and acc.dtype == torch.float32), N, H, W, C, K, KH, KW,
+            stride[0], stride[1], padding[0], padding[1], stream_ptr()), 'conv_dgrad')
     return dx.permute(0, 3, 1, 2)
 
 

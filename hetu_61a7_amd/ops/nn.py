@@ -75,8 +75,10 @@ class Conv2d_Gradient_of_DataOp(Op):
         self.padding, self.stride = _pair(padding), _pair(stride)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        w, g, xshape = input_vals
-        return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding)
+        # optional 4th input: a gradient to accumulate (fused fan-in sum, graph_opt)
+        w, g, xshape = input_vals[:3]
+        acc = input_vals[3] if len(input_vals) > 3 else None
+        return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc)
 
     def gradient(self, output_grad):
         raise NotImplementedError

@@ -64,6 +64,8 @@ class Optimizer(object):
             var_list = self.get_var_list(loss)
         self.params = var_list
         grads, self.backward2forward, self.forward2backward = gradients(loss, self.params, return_all=True)
+        from .graph_opt import fuse_backward
+        fuse_backward([g for g in grads if g is not None])
         return OptimizerOp(grads, self)
 
     def get_learning_rate(self):

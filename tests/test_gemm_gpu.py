@@ -76,6 +76,9 @@ def test_conv_passes(shape):
     ref.backward(dy.float())
     dx = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p))
     assert dx is not None and _rel(dx, xf.grad) < 1e-2
+    r = torch.randn_like(x)
+    dx2 = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p), acc=r)
+    assert dx2 is not None and _rel(dx2, xf.grad + r.float()) < 1e-2
     dw = CI.try_backward_filter(dy, x, w.shape, (s, s), (p, p))
     assert dw is not None and dw.dtype == torch.float32
     assert _rel(dw, wf.grad) < 1e-2

@@ -270,13 +270,13 @@ __device__ __forceinline__ float act_f(float v, int act) {
   return v;
 }
 
-template <class LA, class LB>
+template <class LA, class LB, bool DB>
 __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                   int64_t K, int tiles_m, int tiles_n, int ktps) {
-  // dynamic LDS: 2 x 32 KiB double buffer, or one 32 KiB buffer when every block
-  // owns a single K-tile (short-K 1x1 convolutions: more resident blocks per CU)
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  char* smem[2] = {smem_raw, smem_raw + (ktps > 1 ? 2 * TILE_BYTES : 0)};
+  // DB: 2 x 32 KiB double buffer; !DB: one 32 KiB buffer when every block owns a
+  // single K-tile (short-K 1x1 convolutions: more resident blocks per CU)
+  __shared__ __attribute__((aligned(16))) char smem_raw[(DB ? 2 : 1) * 2 * TILE_BYTES];
+  constexpr int buf_stride = DB ? 2 * TILE_BYTES : 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
 
@@ -307,8 +307,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
 
   // stage K-tile kt into LDS buffer b: 4 + 4 global_load_lds per wave
   auto stage = [&](int kt, int b) {
-    char* As = smem[b] + 4096 * wave;
-    char* Bs = smem[b] + TILE_BYTES + 4096 * wave;
+    char* As = smem_raw + b * buf_stride + 4096 * wave;
+    char* Bs = As + TILE_BYTES;
     const int64_t k0 = (int64_t)kt * BK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) glds16(la.src(k0, i), As + 1024 * i);
@@ -322,8 +322,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   for (int kt = kt0; kt < kt1; ++kt) {
     const int cur = (kt - kt0) & 1;
     if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
-    const char* As = smem[cur];
-    const char* Bs = smem[cur] + TILE_BYTES;
+    const char* As = smem_raw + cur * buf_stride;
+    const char* Bs = As + TILE_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       v8s mf[4], nf[4];
@@ -417,8 +417,6 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   }
 }
 
-static inline size_t lds_bytes(int ktps) { return (ktps > 1 ? 4 : 2) * TILE_BYTES; }
-
 // dst[m][n] (ld ldd, fp32 or bf16) (+)= sum_z slab[z][m][n]
 __global__ void splitk_reduce_k(const float* __restrict__ slab, int64_t stride, int nz,
                                 void* dst, int64_t M, int64_t N, int64_t ldd, int out_f32,
@@ -454,8 +452,12 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
   if (ep.slab && splitk > 1) {
     Epi e2 = ep;
     e2.slab_stride = M * N;
-    hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), lds_bytes(ktps), st, la, lb, e2, M, N,
-                       K, tiles_m, tiles_n, ktps);
+    if (ktps > 1)
+      hipLaunchKernelGGL((gemm_kernel<LA, LB, true>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K,
+                         tiles_m, tiles_n, ktps);
+    else
+      hipLaunchKernelGGL((gemm_kernel<LA, LB, false>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K,
+                         tiles_m, tiles_n, ktps);
     int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, ep.slab, M * N, splitk, ep.C, M,
                        N, ep.ldc, ep.out_f32, ep.atomic);
@@ -464,8 +466,12 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
   Epi e1 = ep;
   e1.slab = nullptr;
   if (splitk > 1) e1.atomic = 1;
-  hipLaunchKernelGGL((gemm_kernel<LA, LB>), grid, dim3(NT), lds_bytes(ktps), st, la, lb, e1, M, N,
-                     K, tiles_m, tiles_n, ktps);
+  if (ktps > 1)
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                       tiles_m, tiles_n, ktps);
+  else
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, false>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                       tiles_m, tiles_n, ktps);
   return (int)hipGetLastError();
 }
 

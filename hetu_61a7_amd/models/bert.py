@@ -1,0 +1,232 @@
+"""BERT (reference ``examples/nlp/bert/hetu_bert.py``, config ``bert_config.py``).
+
+Same architecture and parameter naming scheme as the reference (embeddings
+word/position/token-type + LayerNorm, N x [self-attention, add&LN, GELU FFN,
+add&LN], tanh pooler, MLM head tied to the word embedding, NSP head), written
+MI355X-first:
+
+* hidden states stay 2-D ``[B*S, H]`` between layers, so every projection is one
+  plain bf16 GEMM with the bias (and GELU) fused in the epilogue
+  (``linear_op(..., activation='gelu')``) instead of reshape->matmul->broadcast-add;
+* Q, K and V come from ONE fused [H, 3H] projection;
+* attention is the single ``attention_op`` (QK^T/PV on the MFMA batched GEMM,
+  masked softmax + recompute-dropout kernels);
+* the pretraining losses are sparse-label softmax-CE (one wave64 kernel, ignore
+  index -1) rather than softmax followed by cross-entropy.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import init
+from .. import ops as ht
+from .. import optimizer as optim
+
+
+class BertConfig(object):
+    def __init__(self, vocab_size=30522, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                 intermediate_size=3072, hidden_act='gelu', hidden_dropout_prob=0.1,
+                 attention_probs_dropout_prob=0.1, max_position_embeddings=512, type_vocab_size=2,
+                 initializer_range=0.02, batch_size=64, seq_len=128):
+        self.vocab_size = vocab_size
+        self.hidden_size = hidden_size
+        self.num_hidden_layers = num_hidden_layers
+        self.num_attention_heads = num_attention_heads
+        self.intermediate_size = intermediate_size
+        self.hidden_act = hidden_act
+        self.hidden_dropout_prob = hidden_dropout_prob
+        self.attention_probs_dropout_prob = attention_probs_dropout_prob
+        self.max_position_embeddings = max_position_embeddings
+        self.type_vocab_size = type_vocab_size
+        self.initializer_range = initializer_range
+        self.batch_size = batch_size
+        self.seq_len = seq_len
+
+    @classmethod
+    def base(cls, **kw):
+        return cls(**kw)
+
+    @classmethod
+    def large(cls, **kw):
+        d = dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16, intermediate_size=4096)
+        d.update(kw)
+        return cls(**d)
+
+
+def _w(name, shape, cfg):
+    return init.truncated_normal(shape, stddev=cfg.initializer_range, name=name)
+
+
+def _zeros(name, n):
+    return init.zeros((n,), name=name)
+
+
+def _ones(name, n):
+    return init.ones((n,), name=name)
+
+
+def _dense(x, din, dout, name, cfg, act=None):
+    W = _w(name + '_weight', (din, dout), cfg)
+    b = _zeros(name + '_bias', dout)
+    return ht.linear_op(x, W, b, activation=act)
+
+
+def _ln(x, h, name):
+    return ht.layer_normalization_op(x, _ones(name + '_scale', h), _zeros(name + '_bias', h), eps=1e-12)
+
+
+def _dropout(x, p):
+    return ht.dropout_op(x, 1.0 - p) if p > 0 else x
+
+
+class BertLayer(object):
+    def __init__(self, cfg, idx):
+        self.cfg, self.idx = cfg, idx
+
+    def __call__(self, h2d, mask):
+        c = self.cfg
+        B, S, H = c.batch_size, c.seq_len, c.hidden_size
+        nh, hd = c.num_attention_heads, H // c.num_attention_heads
+        p = 'layer%d_' % self.idx
+        qkv = _dense(h2d, H, 3 * H, p + 'attention_qkv', c)                  # [B*S, 3H]
+        qkv = ht.array_reshape_op(qkv, (B, S, 3, nh, hd))
+        qkv = ht.transpose_op(qkv, (2, 0, 3, 1, 4))                           # [3, B, nh, S, hd]
+        q = ht.slice_op(qkv, (0, 0, 0, 0, 0), (1, B, nh, S, hd))
+        k = ht.slice_op(qkv, (1, 0, 0, 0, 0), (1, B, nh, S, hd))
+        v = ht.slice_op(qkv, (2, 0, 0, 0, 0), (1, B, nh, S, hd))
+        q, k, v = [ht.array_reshape_op(t, (B, nh, S, hd)) for t in (q, k, v)]
+        ctxl = ht.attention_op(q, k, v, mask, dropout=c.attention_probs_dropout_prob)
+        ctxl = ht.array_reshape_op(ht.transpose_op(ctxl, (0, 2, 1, 3)), (B * S, H))
+        a = _dense(ctxl, H, H, p + 'attention_output', c)
+        a = _ln(_dropout(a, c.hidden_dropout_prob) + h2d, H, p + 'attention_LayerNorm')
+        f = _dense(a, H, c.intermediate_size, p + 'intermediate', c, act=c.hidden_act)
+        f = _dense(f, c.intermediate_size, H, p + 'output', c)
+        return _ln(_dropout(f, c.hidden_dropout_prob) + a, H, p + 'output_LayerNorm')
+
+
+class BertModel(object):
+    def __init__(self, cfg: BertConfig):
+        self.cfg = cfg
+        H = cfg.hidden_size
+        self.word_embeddings = _w('word_embeddings', (cfg.vocab_size, H), cfg)
+        self.position_embeddings = _w('position_embeddings', (cfg.max_position_embeddings, H), cfg)
+        self.token_type_embeddings = _w('token_type_embeddings', (cfg.type_vocab_size, H), cfg)
+        self.layers = [BertLayer(cfg, i) for i in range(cfg.num_hidden_layers)]
+
+    def __call__(self, input_ids, token_type_ids, attention_mask):
+        """input_ids / token_type_ids: [B, S] ints; attention_mask: [B, S] of {0,1}.
+        Returns (sequence_output [B*S, H], pooled_output [B, H])."""
+        c = self.cfg
+        B, S, H = c.batch_size, c.seq_len, c.hidden_size
+        pos = ht.Variable('position_ids', value=np.tile(np.arange(S, dtype=np.int64), (B, 1)), trainable=False)
+        e = ht.embedding_lookup_op(self.word_embeddings, input_ids) + \
+            ht.embedding_lookup_op(self.position_embeddings, pos) + \
+            ht.embedding_lookup_op(self.token_type_embeddings, token_type_ids)
+        e = ht.array_reshape_op(e, (B * S, H))
+        h = _dropout(_ln(e, H, 'embeddings_LayerNorm'), c.hidden_dropout_prob)
+        # extended additive mask [B, 1, 1, S]: 0 keep, -10000 masked
+        m = ht.array_reshape_op(attention_mask, (B, 1, 1, S))
+        m = ht.mul_byconst_op(ht.addbyconst_op(m, -1.0), 10000.0)
+        for layer in self.layers:
+            h = layer(h, m)
+        first = ht.array_reshape_op(ht.slice_op(ht.array_reshape_op(h, (B, S, H)), (0, 0, 0), (B, 1, H)), (B, H))
+        pooled = ht.tanh_op(_dense(first, H, H, 'pooler_dense', c))
+        return h, pooled
+
+
+class BertPreTrainingHeads(object):
+    def __init__(self, cfg, word_embeddings):
+        self.cfg, self.E = cfg, word_embeddings
+
+    def __call__(self, seq, pooled):
+        c = self.cfg
+        H = c.hidden_size
+        t = _dense(seq, H, H, 'cls_transform_dense', c, act=c.hidden_act)
+        t = _ln(t, H, 'cls_transform_LayerNorm')
+        bias = _zeros('cls_lm_bias', c.vocab_size)
+        scores = ht.linear_op(t, self.E, bias, trans_B=True)            # tied decoder: [B*S, V]
+        nsp = _dense(pooled, H, 2, 'cls_seq_relationship', c)
+        return scores, nsp
+
+
+class BertForPreTraining(object):
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.bert = BertModel(cfg)
+        self.cls = BertPreTrainingHeads(cfg, self.bert.word_embeddings)
+
+    def __call__(self, input_ids, token_type_ids, attention_mask, masked_lm_labels=None,
+                 next_sentence_label=None):
+        seq, pooled = self.bert(input_ids, token_type_ids, attention_mask)
+        scores, nsp = self.cls(seq, pooled)
+        out = [scores, nsp]
+        if masked_lm_labels is not None and next_sentence_label is not None:
+            mlm = ht.softmaxcrossentropy_sparse_op(scores, masked_lm_labels, ignored_index=-1)
+            ns = ht.softmaxcrossentropy_sparse_op(nsp, next_sentence_label, ignored_index=-1)
+            out += [mlm, ns]
+        return out
+
+
+class BertForMaskedLM(BertForPreTraining):
+    def __call__(self, input_ids, token_type_ids=None, attention_mask=None, masked_lm_labels=None):
+        seq, pooled = self.bert(input_ids, token_type_ids, attention_mask)
+        scores, _ = self.cls(seq, pooled)
+        if masked_lm_labels is None:
+            return [scores]
+        return [scores, ht.softmaxcrossentropy_sparse_op(scores, masked_lm_labels, ignored_index=-1)]
+
+
+class BertForNextSentencePrediction(BertForPreTraining):
+    def __call__(self, input_ids, token_type_ids=None, attention_mask=None, next_sentence_label=None):
+        seq, pooled = self.bert(input_ids, token_type_ids, attention_mask)
+        _, nsp = self.cls(seq, pooled)
+        if next_sentence_label is None:
+            return [nsp]
+        return [nsp, ht.softmaxcrossentropy_sparse_op(nsp, next_sentence_label, ignored_index=-1)]
+
+
+class BertForSequenceClassification(object):
+    """GLUE fine-tuning head (reference test_glue_hetu_bert.py)."""
+
+    def __init__(self, cfg, num_labels=2):
+        self.cfg, self.num_labels = cfg, num_labels
+        self.bert = BertModel(cfg)
+
+    def __call__(self, input_ids, token_type_ids, attention_mask, labels=None):
+        _, pooled = self.bert(input_ids, token_type_ids, attention_mask)
+        logits = _dense(_dropout(pooled, self.cfg.hidden_dropout_prob), self.cfg.hidden_size,
+                        self.num_labels, 'classifier', self.cfg)
+        if labels is None:
+            return [logits]
+        return [logits, ht.softmaxcrossentropy_sparse_op(logits, labels, ignored_index=-1)]
+
+
+def bert_pretrain_graph(cfg, lr=1e-5, optimizer=None):
+    """Placeholders + loss + train op for BERT pretraining (reference
+    train_hetu_bert.py: Adam lr 1e-5, loss = mean MLM + mean NSP)."""
+    input_ids = ht.Variable(name='input_ids', trainable=False)
+    token_type_ids = ht.Variable(name='token_type_ids', trainable=False)
+    attention_mask = ht.Variable(name='attention_mask', trainable=False)
+    mlm_labels = ht.Variable(name='masked_lm_labels', trainable=False)
+    nsp_labels = ht.Variable(name='next_sentence_label', trainable=False)
+    model = BertForPreTraining(cfg)
+    _, _, mlm, nsp = model(input_ids, token_type_ids, attention_mask, mlm_labels, nsp_labels)
+    loss = ht.reduce_mean_op(mlm, [0]) + ht.reduce_mean_op(nsp, [0])
+    opt = optimizer or optim.AdamOptimizer(learning_rate=lr)
+    train = opt.minimize(loss)
+    feeds = dict(input_ids=input_ids, token_type_ids=token_type_ids, attention_mask=attention_mask,
+                 masked_lm_labels=mlm_labels, next_sentence_label=nsp_labels)
+    return feeds, loss, train
+
+
+def synthetic_bert_batch(cfg, seed=0, mask_prob=0.15):
+    rng = np.random.default_rng(seed)
+    B, S = cfg.batch_size, cfg.seq_len
+    ids = rng.integers(1000, cfg.vocab_size, (B, S)).astype(np.int64)
+    types = np.zeros((B, S), np.int64)
+    types[:, S // 2:] = 1
+    mask = np.ones((B, S), np.float32)
+    mlm = np.where(rng.random((B, S)) < mask_prob, ids, -1).astype(np.int64)
+    nsp = rng.integers(0, 2, (B,)).astype(np.int64)
+    return dict(input_ids=ids, token_type_ids=types, attention_mask=mask, masked_lm_labels=mlm,
+                next_sentence_label=nsp)

@@ -179,7 +179,10 @@ class HetuConfig(object):
             self.context = ctx
             self.node_strategy = {}
             self.device_group = None
-        if pipeline is not None:
+        from ..parallel.lowering import lower_dispatch, PENDING_MESHES
+        lower_dispatch(list(eval_node_list))
+        self.spmd = bool(PENDING_MESHES)
+        if pipeline is not None or self.spmd:
             # one process per GPU: this rank's device is its own GPU ordinal
             self.context = ndarray.gpu(local) if torch.cuda.is_available() else ndarray.cpu(0)
             launch_mpi = launch_ps = False
@@ -193,6 +196,7 @@ class HetuConfig(object):
             elif world > 1 and dist_strategy is None and pipeline is None:
                 comm_mode = None
         self.comm_mode = comm_mode
+        self.cpu_only = not torch.cuda.is_available()
         if ndarray.is_gpu_ctx(self.context) and not torch.cuda.is_available():
             # CPU-only process (tests / gloo rehearsal of the distributed path)
             self.context = ndarray.cpu(0)
@@ -207,6 +211,9 @@ class HetuConfig(object):
             if world > 1:
                 from ..parallel import comm as C
                 self.comm = C.init_process_group(use_gpu=ndarray.is_gpu_ctx(self.context))
+                if self.spmd:
+                    from ..parallel.lowering import create_groups
+                    create_groups(PENDING_MESHES, world)
         if self.comm_mode in ('PS', 'Hybrid'):
             from ..ps import worker as psw
             self.ps_comm = psw.get_worker(self)

@@ -135,7 +135,8 @@ class Op(object):
 
     # hooks (reference Node.py:192-213) ------------------------------------------
     def forward_hook(self, config):
-        if getattr(config, 'pipeline', None) is not None:
+        if getattr(config, 'pipeline', None) is not None or getattr(config, 'spmd', False) or \
+                (getattr(config, 'cpu_only', False) and not isinstance(self.ctx, ndarray.DLContext)):
             # pipeline: each process computes only its own stage, on its own
             # device; cross-stage edges are p2p messages, not transfer ops
             self.ctx = config.context

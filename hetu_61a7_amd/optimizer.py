@@ -58,6 +58,8 @@ class Optimizer(object):
     def minimize(self, loss, var_list=None):
         from .ops.executor import gradients
         from .graph_opt import fuse_forward
+        from .parallel.lowering import lower_dispatch
+        lower_dispatch([loss])
         fuse_forward([loss])
         self.loss = loss
         if not var_list:

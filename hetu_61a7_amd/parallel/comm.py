@@ -66,8 +66,14 @@ def is_initialized() -> bool:
     return _WORLD is not None
 
 
-def new_group_comm(ranks: Optional[Sequence[int]] = None) -> 'Communicator':
-    """Cached sub-group communicator (every rank must call in the same order)."""
+def new_group_comm(ranks: Optional[Sequence[int]] = None, local_sync: bool = False) -> 'Communicator':
+    """Cached sub-group communicator.
+
+    By default every rank of the world must call in the same order (static
+    groups: TP/PP/DistGCN row and column groups).  ``local_sync=True`` creates
+    the group with only its members participating -- what partial-reduce needs,
+    whose partner sets are formed at run time (reference preduce.py:41-42 builds
+    an NCCL group unique id among the partners only)."""
     w = init_process_group()
     if ranks is None:
         return w
@@ -75,7 +81,7 @@ def new_group_comm(ranks: Optional[Sequence[int]] = None) -> 'Communicator':
     if len(key) == w.nrank:
         return w
     if key not in _GROUPS:
-        _GROUPS[key] = Communicator(key, use_gpu=w.use_gpu)
+        _GROUPS[key] = Communicator(key, use_gpu=w.use_gpu, local_sync=local_sync)
     return _GROUPS[key]
 
 
@@ -91,10 +97,15 @@ class Communicator(object):
     keeps flowing -- the overlap the reference gets from its nccl_stream).
     """
 
-    def __init__(self, ranks: Optional[Tuple[int, ...]], use_gpu: bool = True):
+    def __init__(self, ranks: Optional[Tuple[int, ...]], use_gpu: bool = True, local_sync: bool = False):
         self.use_gpu = use_gpu
         self.ranks = ranks
-        self.group = dist.new_group(list(ranks)) if ranks is not None else None
+        if ranks is None:
+            self.group = None
+        elif local_sync:
+            self.group = dist.new_group(list(ranks), use_local_synchronization=True)
+        else:
+            self.group = dist.new_group(list(ranks))
         self.rank = dist.get_rank(self.group) if (ranks is None or dist.get_rank() in ranks) else -1
         self.nrank = dist.get_world_size(self.group) if ranks is None or self.rank >= 0 else len(ranks)
         self.global_rank = dist.get_rank()

@@ -11,7 +11,7 @@ STEPS=${STEPS:-20}
 echo "== build" ; make -C csrc -j16 > gpurun_out/build.log 2>&1 || { echo build failed; tail -20 gpurun_out/build.log; exit 1; }
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   echo "== pytest -m gpu"
-  timeout -k 10 ${TEST_TIMEOUT:-420} python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-420} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
   rc=$?
   tail -25 gpurun_out/pytest_gpu.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi

@@ -36,6 +36,28 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = 128 * BK * 2;  // 16 KiB per operand tile
 
+// n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery): the implicit-GEMM
+// loaders decompose pixel / tap indices per lane per K-tile, where a hardware-less
+// 32-bit integer division would cost ~40 VALU ops each.
+struct FastDiv {
+  uint32_t d, m, l;
+  __host__ __device__ FastDiv() : d(1), m(1), l(0) {}
+  __host__ __device__ explicit FastDiv(uint32_t dv) : d(dv < 1 ? 1 : dv) {
+    l = 0;
+    while (l < 31 && (1u << l) < d) ++l;
+    m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> l; }
+};
+
+// Default per-block problem view: the whole M x K problem, rows stored linearly.
+// Loaders that split the problem into classes over blockIdx.y (strided dgrad)
+// override rows_eff / k_eff / out_row.
+#define HETU_LINEAR_ROWS                                             \
+  __device__ int64_t rows_eff(int64_t M_) const { return M_; }        \
+  __device__ int64_t k_eff(int64_t K_) const { return K_; }           \
+  __device__ int64_t out_row(int64_t m_) const { return m_; }
+
 
 
 
@@ -91,6 +113,7 @@ __device__ __forceinline__ const bf16* zchunk() { return g_zero_chunk; }
 
 // plain row-major operand with contiguous K: element (r, k) at base[r*ld + k]
 struct PlainK {
+  HETU_LINEAR_ROWS
   static constexpr bool KMAJ = true;
   const bf16* base; int64_t ld, rows, K, bstride;
   int64_t roff[4]; bool rok[4]; int ch;
@@ -112,6 +135,7 @@ struct PlainK {
 
 // plain operand stored [K][rows]: element (r, k) at base[k*ld + r]
 struct PlainMN {
+  HETU_LINEAR_ROWS
   static constexpr bool KMAJ = false;
   const bf16* base; int64_t ld, rows, K, bstride;
   int64_t col[4]; bool cok[4]; int kr;
@@ -133,95 +157,150 @@ struct PlainMN {
 
 struct ConvGeom {
   int N, H, W, C, K, KH, KW, sh, sw, ph, pw, OH, OW;  // C = in channels, K = out channels
+  FastDiv fOW, fOH, fC, fK, fKW;
 };
 
 // forward, M side: rows = output pixels, k = (kh, kw, ci), ci fastest
 struct ConvFwdA {
+  HETU_LINEAR_ROWS
   static constexpr bool KMAJ = true;
   const bf16* x; ConvGeom g; int64_t Ktot, rows;
-  int64_t nb[4]; int ih0[4], iw0[4]; bool rok[4]; int ch;
+  int nb[4]; int ih0[4], iw0[4]; bool rok[4]; int ch;
   __device__ void init(int64_t r0, int w, int l, int64_t) {
     ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
       rok[i] = r < rows;
-      int64_t rr = rok[i] ? r : 0;
-      int ow = (int)(rr % g.OW);
-      int64_t t = rr / g.OW;
-      int oh = (int)(t % g.OH);
-      int64_t n = t / g.OH;
-      nb[i] = n * g.H;
+      uint32_t rr = rok[i] ? (uint32_t)r : 0;
+      uint32_t t = g.fOW.div(rr);
+      int ow = (int)(rr - t * g.OW);
+      uint32_t n = g.fOH.div(t);
+      int oh = (int)(t - n * g.OH);
+      nb[i] = (int)n * g.H;
       ih0[i] = oh * g.sh - g.ph;
       iw0[i] = ow * g.sw - g.pw;
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    int64_t k = k0 + ch * 8;
-    int tap = (int)(k / g.C);
-    int ci = (int)(k - (int64_t)tap * g.C);
-    int kh = tap / g.KW, kw = tap - kh * g.KW;
-    int ih = ih0[i] + kh, iw = iw0[i] + kw;
+    uint32_t k = (uint32_t)k0 + ch * 8;
+    uint32_t tap = g.fC.div(k);
+    int ci = (int)(k - tap * g.C);
+    uint32_t kh = g.fKW.div(tap);
+    int kw = (int)(tap - kh * g.KW);
+    int ih = ih0[i] + (int)kh, iw = iw0[i] + kw;
     bool ok = k < Ktot && rok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-    return ok ? x + ((nb[i] + ih) * g.W + iw) * g.C + ci : zchunk();
+    return ok ? x + ((int64_t)(nb[i] + ih) * g.W + iw) * g.C + ci : zchunk();
   }
 };
 
-// data gradient, M side: rows = input pixels (n, ih, iw), k = (kh, kw, co)
+// Data gradient, split into sh*sw stride classes over blockIdx.y.  Class (a, b)
+// holds the input pixels with ih % sh == a, iw % sw == b; only the taps with
+// kh == (a + ph) mod sh (step sh), kw likewise, reach an output pixel, so each
+// class is a dense implicit GEMM over exactly its useful taps (no zero-filled
+// K-tiles, no divisibility tests).  Stride 1 is the single class (0, 0).
+struct DgradClass {
+  int a, b, kh0, kw0, nth, ntw, Hc, Wc;
+  FastDiv fWc, fHc, fntw;
+  __device__ void make(const ConvGeom& g, int cls) {
+    a = cls / g.sw;
+    b = cls - a * g.sw;
+    Hc = a < g.H ? (g.H - a + g.sh - 1) / g.sh : 0;
+    Wc = b < g.W ? (g.W - b + g.sw - 1) / g.sw : 0;
+    kh0 = (a + g.ph) % g.sh;
+    kw0 = (b + g.pw) % g.sw;
+    nth = kh0 < g.KH ? (g.KH - kh0 + g.sh - 1) / g.sh : 0;
+    ntw = kw0 < g.KW ? (g.KW - kw0 + g.sw - 1) / g.sw : 0;
+    fWc = FastDiv((uint32_t)Wc);
+    fHc = FastDiv((uint32_t)Hc);
+    fntw = FastDiv((uint32_t)ntw);
+  }
+};
+
+// data gradient, M side: rows = class pixels (n, i, j), k = (tap in class, co)
 struct ConvDgradA {
   static constexpr bool KMAJ = true;
-  const bf16* dy; ConvGeom g; int64_t Ktot, rows;
-  int64_t nb[4]; int ih[4], iw[4]; bool rok[4]; int ch;
-  __device__ void init(int64_t r0, int w, int l, int64_t) {
+  const bf16* dy; ConvGeom g;
+  DgradClass c;
+  int nb[4]; int ih[4], iw[4]; bool rok[4]; int ch;
+  int64_t mrows, kdim;
+  __device__ int64_t rows_eff(int64_t) const { return mrows; }
+  __device__ int64_t k_eff(int64_t) const { return kdim; }
+  __device__ int64_t out_row(int64_t m) const {
+    uint32_t t = c.fWc.div((uint32_t)m);
+    int j = (int)((uint32_t)m - t * c.Wc);
+    uint32_t n = c.fHc.div(t);
+    int i = (int)(t - n * c.Hc);
+    return ((int64_t)n * g.H + c.a + g.sh * i) * g.W + c.b + g.sw * j;
+  }
+  __device__ void init(int64_t r0, int w, int l, int64_t cls) {
+    c.make(g, (int)cls);
+    mrows = (int64_t)g.N * c.Hc * c.Wc;
+    kdim = (int64_t)c.nth * c.ntw * g.K;
     ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
-      rok[i] = r < rows;
-      int64_t rr = rok[i] ? r : 0;
-      iw[i] = (int)(rr % g.W);
-      int64_t t = rr / g.W;
-      ih[i] = (int)(t % g.H);
-      nb[i] = (t / g.H) * g.OH;
+      rok[i] = r < mrows;
+      uint32_t rr = rok[i] ? (uint32_t)r : 0;
+      uint32_t t = c.fWc.div(rr);
+      int j = (int)(rr - t * c.Wc);
+      uint32_t n = c.fHc.div(t);
+      int ii = (int)(t - n * c.Hc);
+      ih[i] = c.a + g.sh * ii;
+      iw[i] = c.b + g.sw * j;
+      nb[i] = (int)n * g.OH;
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    int64_t k = k0 + ch * 8;
-    int tap = (int)(k / g.K);
-    int co = (int)(k - (int64_t)tap * g.K);
-    int kh = tap / g.KW, kw = tap - kh * g.KW;
-    int th = ih[i] + g.ph - kh, tw = iw[i] + g.pw - kw;
-    int oh = th / g.sh, ow = tw / g.sw;
-    bool ok = k < Ktot && rok[i] && th >= 0 && tw >= 0 && oh * g.sh == th && ow * g.sw == tw &&
-              oh < g.OH && ow < g.OW;
-    return ok ? dy + ((nb[i] + oh) * g.OW + ow) * g.K + co : zchunk();
+    uint32_t k = (uint32_t)k0 + ch * 8;
+    uint32_t tap = g.fK.div(k);
+    int co = (int)(k - tap * g.K);
+    uint32_t th = c.fntw.div(tap);
+    int tw = (int)(tap - th * c.ntw);
+    int kh = c.kh0 + g.sh * (int)th, kw = c.kw0 + g.sw * tw;
+    int nh = ih[i] + g.ph - kh, nw = iw[i] + g.pw - kw;   // exact multiples of the stride
+    int oh = nh / g.sh, ow = nw / g.sw;
+    bool ok = (int64_t)k < kdim && rok[i] && nh >= 0 && nw >= 0 && oh < g.OH && ow < g.OW;
+    return ok ? dy + ((int64_t)(nb[i] + oh) * g.OW + ow) * g.K + co : zchunk();
   }
 };
 
-// data gradient, N side: cols = ci, k rows = (kh, kw, co): w[co][kh][kw][ci]
+// data gradient, N side: cols = ci, k rows = (tap in class, co): w[co][kh][kw][ci]
 struct ConvDgradB {
+  HETU_LINEAR_ROWS
   static constexpr bool KMAJ = false;
-  const bf16* w; ConvGeom g; int64_t Ktot;
+  const bf16* w; ConvGeom g;
+  DgradClass c;
+  int64_t kdim;
   int col[4]; bool cok[4]; int kr;
-  __device__ void init(int64_t r0, int wv, int l, int64_t) {
+  __device__ void init(int64_t r0, int wv, int l, int64_t cls) {
+    c.make(g, (int)cls);
+    kdim = (int64_t)c.nth * c.ntw * g.K;
     kr = 16 * wv + (l >> 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int c = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
-      col[i] = (int)r0 + 8 * c;
+      int cc = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
+      col[i] = (int)r0 + 8 * cc;
       cok[i] = col[i] < g.C;
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    int64_t k = k0 + kr + 4 * i;
-    int tap = (int)(k / g.K);
-    int co = (int)(k - (int64_t)tap * g.K);
-    return (cok[i] && k < Ktot) ? w + ((int64_t)co * (g.KH * g.KW) + tap) * g.C + col[i] : zchunk();
+    uint32_t k = (uint32_t)k0 + kr + 4 * i;
+    uint32_t tap = g.fK.div(k);
+    int co = (int)(k - tap * g.K);
+    uint32_t th = c.fntw.div(tap);
+    int tw = (int)(tap - th * c.ntw);
+    int kh = c.kh0 + g.sh * (int)th, kw = c.kw0 + g.sw * tw;
+    return (cok[i] && (int64_t)k < kdim)
+               ? w + ((int64_t)co * (g.KH * g.KW) + kh * g.KW + kw) * g.C + col[i]
+               : zchunk();
   }
 };
 
 // weight gradient, N side: cols = (kh, kw, ci), k rows = output pixels
 struct ConvWgradB {
+  HETU_LINEAR_ROWS
   static constexpr bool KMAJ = false;
   const bf16* x; ConvGeom g; int64_t P;  // P = N*OH*OW
   int kh[4], kw[4], ci[4]; bool cok[4]; int kr;
@@ -239,14 +318,14 @@ struct ConvWgradB {
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    int64_t p = k0 + kr + 4 * i;
-    int ow = (int)(p % g.OW);
-    int64_t t = p / g.OW;
-    int oh = (int)(t % g.OH);
-    int64_t n = t / g.OH;
+    uint32_t p = (uint32_t)k0 + kr + 4 * i;
+    uint32_t t = g.fOW.div(p);
+    int ow = (int)(p - t * g.OW);
+    uint32_t n = g.fOH.div(t);
+    int oh = (int)(t - n * g.OH);
     int ih = oh * g.sh - g.ph + kh[i], iw = ow * g.sw - g.pw + kw[i];
-    bool ok = cok[i] && p < P && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-    return ok ? x + ((n * g.H + ih) * g.W + iw) * g.C + ci[i] : zchunk();
+    bool ok = cok[i] && (int64_t)p < P && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+    return ok ? x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + ci[i] : zchunk();
   }
 };
 
@@ -275,7 +354,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
                                                   int64_t K, int tiles_m, int tiles_n, int ktps) {
   // DB: 2 x 32 KiB double buffer; !DB: one 32 KiB buffer when every block owns a
   // single K-tile (short-K 1x1 convolutions: more resident blocks per CU)
-  __shared__ __attribute__((aligned(16))) char smem_raw[(DB ? 2 : 1) * 2 * TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem_raw[DB ? 4 * TILE_BYTES : 64 * (BN + 4) * 4];
   constexpr int buf_stride = DB ? 2 * TILE_BYTES : 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
@@ -294,6 +373,10 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   const int64_t batch = blockIdx.y;
   la.init((int64_t)tm * BM, wave, lane, batch);
   lb.init((int64_t)tn * BN, wave, lane, batch);
+  // per-block problem view (a stride class of a strided dgrad may be smaller)
+  const int64_t Mb = la.rows_eff(M);
+  if ((int64_t)tm * BM >= Mb) return;  // block-uniform, before any barrier
+  K = la.k_eff(K);
 
   const int nkt = (int)((K + BK - 1) / BK);
   const int kt0 = blockIdx.z * ktps;
@@ -347,7 +430,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
-      if (m >= M) continue;
+      if (m >= Mb) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
@@ -367,10 +450,102 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   }
   char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
   const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
+  if (!ep.atomic) {
+    // Row-coalesced epilogue: the tile goes through LDS in two 64-row halves
+    // (fp32, rows padded by 4 floats so the 16-row MFMA write pattern spreads
+    // over the banks), then 16 lanes cover one 128-column row with 8 elements
+    // each: full 256-byte bf16 rows per instruction instead of 16 scattered
+    // 32-byte pieces, and the same for the Cin (residual / beta) read.
+    constexpr int SROW = BN + 4;
+    float* stg = reinterpret_cast<float*>(smem_raw);
+    const bool cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)Cb & 15) == 0)
+                                 : ((ep.ldc & 7) == 0 && ((uintptr_t)Cb & 15) == 0);
+    const bool ivec = Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)Cinb & 15) == 0)
+                                          : ((ep.ldcin & 7) == 0 && ((uintptr_t)Cinb & 15) == 0));
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (wm == half) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = i * 16 + (lane & 15), c = wn * 64 + j * 16 + 4 * (lane >> 4);
+            *reinterpret_cast<v4f*>(stg + r * SROW + c) = acc[i][j];
+          }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int pss = 0; pss < 4; ++pss) {
+        const int r = pss * 16 + (tid >> 4), c = (tid & 15) * 8;
+        const int64_t m = (int64_t)tm * BM + half * 64 + r;
+        const int64_t n = (int64_t)tn * BN + c;
+        if (m >= Mb || n >= N) continue;
+        const int64_t orow = la.out_row(m);
+        float v[8];
+        {
+          v4f a0 = *reinterpret_cast<const v4f*>(stg + r * SROW + c);
+          v4f a1 = *reinterpret_cast<const v4f*>(stg + r * SROW + c + 4);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
+        }
+        const bool full = n + 7 < N;
+        if (ep.bias) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            v[t] += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
+        }
+        if (Cinb) {
+          const int64_t o = orow * ep.ldcin + n;
+          float cv[8];
+          if (ivec && full) {
+            if (ep.cin_f32) {
+              float4 c0 = *reinterpret_cast<const float4*>((const float*)Cinb + o);
+              float4 c1 = *reinterpret_cast<const float4*>((const float*)Cinb + o + 4);
+              cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
+              cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
+            } else {
+              load_vec<bf16>((const bf16*)Cinb + o, cv);
+            }
+          } else {
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+              cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)Cinb)[o + t]
+                                              : to_f(((const bf16*)Cinb)[o + t])) : 0.f;
+          }
+#pragma unroll
+          for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
+        const int64_t o = orow * ep.ldc + n;
+        if (ep.out_f32) {
+          float* Cf = (float*)Cb + o;
+          if (cvec && full) {
+            *reinterpret_cast<float4*>(Cf) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(Cf + 4) = make_float4(v[4], v[5], v[6], v[7]);
+          } else {
+            for (int t = 0; t < 8; ++t)
+              if (n + t < N) Cf[t] = v[t];
+          }
+        } else {
+          bf16* Ch = (bf16*)Cb + o;
+          if (cvec && full) {
+            store_vec<bf16>(Ch, v);
+          } else {
+            for (int t = 0; t < 8; ++t)
+              if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
-    if (m >= M) continue;
+    if (m >= Mb) continue;
+    const int64_t orow = la.out_row(m);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
@@ -381,13 +556,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
         float x = acc[i][j][t] * ep.alpha;
         if (ep.bias) x += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
         if (Cinb && n + t < N) {
-          int64_t o = m * ep.ldcin + n + t;
+          int64_t o = orow * ep.ldcin + n + t;
           float c = ep.cin_f32 ? ((const float*)Cinb)[o] : to_f(((const bf16*)Cinb)[o]);
           x += ep.beta * c;
         }
         v[t] = act_f(x, ep.act);
       }
-      const int64_t o = m * ep.ldc + n;
+      const int64_t o = orow * ep.ldc + n;
       if (ep.atomic) {
         float* Cf = (float*)Cb;
 #pragma unroll
@@ -481,7 +656,7 @@ static int pick_splitk(int64_t M, int64_t N, int64_t K) {
   int64_t ktiles = (K + BK - 1) / BK;
   int64_t want = (512 + tiles - 1) / tiles;
   int64_t cap = std::max<int64_t>(1, ktiles / 8);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(want, cap), 64));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(want, cap), 512));
 }
 
 }  // namespace gemm
@@ -518,6 +693,11 @@ static ConvGeom geom(int N, int H, int W, int C, int K, int KH, int KW, int sh, 
   ConvGeom g{N, H, W, C, K, KH, KW, sh, sw, ph, pw, 0, 0};
   g.OH = (H + 2 * ph - KH) / sh + 1;
   g.OW = (W + 2 * pw - KW) / sw + 1;
+  g.fOW = FastDiv((uint32_t)g.OW);
+  g.fOH = FastDiv((uint32_t)g.OH);
+  g.fC = FastDiv((uint32_t)C);
+  g.fK = FastDiv((uint32_t)K);
+  g.fKW = FastDiv((uint32_t)KW);
   return g;
 }
 
@@ -531,7 +711,11 @@ HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const flo
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(PlainK{(const bf16*)x, C, M, C, 0}, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M,
                   K, Kt, 1, 1, st);
-  ConvFwdA la{(const bf16*)x, g, Kt, M};
+  ConvFwdA la{};
+  la.x = (const bf16*)x;
+  la.g = g;
+  la.Ktot = Kt;
+  la.rows = M;
   return launch(la, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M, K, Kt, 1, 1, st);
 }
 
@@ -541,14 +725,23 @@ HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const
                                   int acc_f32, int N, int H, int W, int C, int K, int KH, int KW,
                                   int sh, int sw, int ph, int pw, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  int64_t M = (int64_t)N * H * W, Kt = (int64_t)KH * KW * K;
   Epi ep{dx, acc, nullptr, C, C, 0, 0, 1.f, acc ? 1.f : 0.f, 0, 0, acc_f32, 0, 0, nullptr, 0};
-  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
+  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0) {
+    int64_t M = (int64_t)N * H * W;
     return launch(PlainK{(const bf16*)dy, K, M, K, 0}, PlainMN{(const bf16*)w, C, C, K, 0}, ep, M,
                   C, K, 1, 1, st);
-  ConvDgradA la{(const bf16*)dy, g, Kt, M};
-  ConvDgradB lb{(const bf16*)w, g, Kt};
-  return launch(la, lb, ep, M, C, Kt, 1, 1, st);
+  }
+  // one launch over the sh*sw stride classes (blockIdx.y); grid sized for the
+  // largest class, the others exit early per block
+  int64_t Mmax = (int64_t)N * ((H + sh - 1) / sh) * ((W + sw - 1) / sw);
+  int64_t Kmax = (int64_t)((KH + sh - 1) / sh) * ((KW + sw - 1) / sw) * K;
+  ConvDgradA la{};
+  la.dy = (const bf16*)dy;
+  la.g = g;
+  ConvDgradB lb{};
+  lb.w = (const bf16*)w;
+  lb.g = g;
+  return launch(la, lb, ep, Mmax, C, Kmax, sh * sw, 1, st);
 }
 
 HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }
@@ -564,6 +757,9 @@ HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int 
   PlainMN la{(const bf16*)dy, K, K, P, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(la, PlainMN{(const bf16*)x, C, C, P, 0}, ep, K, Nc, P, 1, splitk, st);
-  ConvWgradB lb{(const bf16*)x, g, P};
+  ConvWgradB lb{};
+  lb.x = (const bf16*)x;
+  lb.g = g;
+  lb.P = P;
   return launch(la, lb, ep, K, Nc, P, 1, splitk, st);
 }

@@ -58,7 +58,8 @@ def test_gemm_batched_and_splitk():
 
 CONV_SHAPES = [  # N, C, H, K, k, stride, pad
     (4, 64, 14, 64, 1, 1, 0), (4, 64, 14, 128, 3, 1, 1), (4, 128, 15, 64, 3, 2, 1),
-    (2, 256, 14, 128, 1, 2, 0), (2, 8, 32, 64, 7, 2, 3), (3, 72, 9, 40, 3, 1, 0)]
+    (2, 256, 14, 128, 1, 2, 0), (2, 8, 32, 64, 7, 2, 3), (3, 72, 9, 40, 3, 1, 0),
+    (2, 64, 16, 64, 3, 2, 1), (2, 32, 13, 64, 5, 2, 2), (2, 64, 11, 32, 3, 3, 1)]
 
 
 @pytest.mark.parametrize('shape', CONV_SHAPES)

@@ -35,7 +35,7 @@ static BnGeom bn_geom(int64_t M, int C, int vec) {
   return g;
 }
 
-// partial statistics: ws_mean/ws_m2 [chunks][C]; counts derivable on host side
+// partial statistics: ws_mean/ws_m2 [C][chunks] (raw sums); counts derivable on host side
 template <typename T>
 __global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x, int64_t M, int C,
                                                          int W, int RP, int64_t rows_per_chunk,
@@ -76,16 +76,17 @@ __global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x,
       Q += sh_q[tt * V + lane_i];
     }
     const int c = blockIdx.y * W * V + c_local;
-    if (c < C) {
-      ws_mean[(int64_t)blockIdx.x * C + c] = S;  // raw per-chunk sums; merged in fp64
-      ws_m2[(int64_t)blockIdx.x * C + c] = Q;
+    if (c < C) {  // [C][chunks]: the finalize wave reads one channel contiguously
+      ws_mean[(int64_t)c * gridDim.x + blockIdx.x] = S;  // raw per-chunk sums; merged in fp64
+      ws_m2[(int64_t)c * gridDim.x + blockIdx.x] = Q;
     }
   }
 }
 
 // Merge of the chunk sums in fp64 (mean = S/n, var = Q/n - mean^2); writes
 // save_mean/save_invstd, running stats and the folded affine a = scale*invstd,
-// b = bias - mean*a.  Block = 16 channels x 16 lanes, independent loads per lane.
+// b = bias - mean*a.  One wave per channel over its contiguous [chunks] row:
+// every lane issues all its loads up front (no serial latency chain).
 __global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict__ ws_s, const float* __restrict__ ws_q,
                                   int chunks, int64_t rows_per_chunk, int64_t M, int C,
                                   const float* __restrict__ scale, const float* __restrict__ bias,
@@ -93,22 +94,23 @@ __global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict
                                   float factor, float eps, float* __restrict__ save_mean,
                                   float* __restrict__ save_invstd, float* __restrict__ fold_a,
                                   float* __restrict__ fold_b) {
-  __shared__ double sh_s[256], sh_q[256];
-  const int cl = threadIdx.x & 15, lane = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float* ps = ws_s + (int64_t)c * chunks;
+  const float* pq = ws_q + (int64_t)c * chunks;
   double S = 0.0, Q = 0.0;
-  if (c < C) {
-#pragma unroll 4
-    for (int p = lane; p < chunks; p += 16) {
-      S += (double)ws_s[(int64_t)p * C + c];
-      Q += (double)ws_q[(int64_t)p * C + c];
-    }
+#pragma unroll 8
+  for (int p = lane; p < chunks; p += 64) {
+    S += (double)ps[p];
+    Q += (double)pq[p];
   }
-  sh_s[threadIdx.x] = S;
-  sh_q[threadIdx.x] = Q;
-  __syncthreads();
-  if (lane == 0 && c < C) {
-    for (int l = 1; l < 16; ++l) { S += sh_s[l * 16 + cl]; Q += sh_q[l * 16 + cl]; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    S += __shfl_xor(S, o, 64);
+    Q += __shfl_xor(Q, o, 64);
+  }
+  if (lane == 0) {
     const double n = (double)M;
     const double mean = S / n;
     double var = Q / n - mean * mean;
@@ -229,8 +231,8 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
     }
     const int c = blockIdx.y * W * V + t;
     if (c < C) {
-      ws_sdy[(int64_t)blockIdx.x * C + c] = S;
-      ws_sdyx[(int64_t)blockIdx.x * C + c] = Q;
+      ws_sdy[(int64_t)c * gridDim.x + blockIdx.x] = S;
+      ws_sdyx[(int64_t)c * gridDim.x + blockIdx.x] = Q;
     }
   }
 }
@@ -241,20 +243,20 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize(const float* __restrict__
                                 float* __restrict__ dscale, float* __restrict__ dbias,
                                 float* __restrict__ cA, float* __restrict__ cB,
                                 float* __restrict__ cC) {
-  __shared__ float s1[256], s2[256];
-  const int cl = threadIdx.x & 15, lane = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float* p1 = ws_sdy + (int64_t)c * chunks;
+  const float* p2 = ws_sdyx + (int64_t)c * chunks;
   float sdy = 0.f, sdyx = 0.f;
-  if (c < C) {
-    for (int p = lane; p < chunks; p += 16) {
-      sdy += ws_sdy[(int64_t)p * C + c];
-      sdyx += ws_sdyx[(int64_t)p * C + c];
-    }
+#pragma unroll 8
+  for (int p = lane; p < chunks; p += 64) {
+    sdy += p1[p];
+    sdyx += p2[p];
   }
-  s1[threadIdx.x] = sdy; s2[threadIdx.x] = sdyx;
-  __syncthreads();
-  if (lane == 0 && c < C) {
-    for (int l = 1; l < 16; ++l) { sdy += s1[l * 16 + cl]; sdyx += s2[l * 16 + cl]; }
+  sdy = wave_sum(sdy);
+  sdyx = wave_sum(sdyx);
+  if (lane == 0) {
     if (dscale) dscale[c] = sdyx;
     if (dbias) dbias[c] = sdy;
     const float invM = 1.f / (float)M;
@@ -327,7 +329,7 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
     float* wq = ws + (int64_t)g.chunks * C;
     hipLaunchKernelGGL(bn_stats_partial<T>, dim3(g.chunks, g.tiles), dim3(256), 0, st,
                        (const T*)x, M, C, g.W, g.RP, g.rows_per_chunk, wm, wq);
-    hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 15) / 16), dim3(256), 0, st, wm, wq,
+    hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 3) / 4), dim3(256), 0, st, wm, wq,
                        g.chunks, g.rows_per_chunk, M, C, scale, bias, run_mean, run_var, factor,
                        eps, save_mean, save_invstd, fa, fb);
   } else {
@@ -372,7 +374,7 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const T* x, 
   constexpr int V = Vec<T>::N;
   hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, x,
                      mean, invstd, fa, fb, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 15) / 16), dim3(256), 0, st, w1, w2, g.chunks, M,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 3) / 4), dim3(256), 0, st, w1, w2, g.chunks, M,
                      C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
   int64_t nvec = M * C / V;
   int grid = stream_grid(nvec, 256, 4);

@@ -297,7 +297,10 @@ class OptimizerOp(Op):
                               shadow=amp, device=self.ctx.torch_device if self.ctx else None)
         for p in dense:
             values[p] = self.flat.view(p, 'param')
-            if amp:
+            # 1-D parameters (biases, BN/LN affine) are consumed by fp32 epilogues and
+            # normalisation kernels: they read the fp32 master directly (no bf16 copy,
+            # no per-step cast kernels)
+            if amp and len(self.flat.offsets[p][2]) >= 2:
                 config.compute_values[p] = self.flat.view(p, 'shadow')
         for p in sparse:
             st = {}

@@ -76,6 +76,108 @@ __global__ void __launch_bounds__(256) maxpool_bwd_k(const T* __restrict__ dy, c
   }
 }
 
+
+// Vectorized channels-last variants: one thread owns V = 16/sizeof(T) channels of
+// one pixel (16-byte loads/stores, 8-byte winning-tap words); 32-bit index math.
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_fwd_vec(const T* __restrict__ x, T* __restrict__ y,
+                                                        uint8_t* __restrict__ idx, int N, int H, int W,
+                                                        int C, int Ho, int Wo, int kh, int kw, int sh,
+                                                        int sw, int ph, int pw) {
+  constexpr int V = Vec<T>::N;
+  const int cv = C / V;
+  const int total = N * Ho * Wo * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cg = i % cv;
+    int t = i / cv;
+    const int wo = t % Wo;
+    t /= Wo;
+    const int ho = t % Ho;
+    const int n = t / Ho;
+    float best[V];
+    uint8_t bi[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int a = 0; a < kh; ++a) {
+      const int h = ho * sh - ph + a;
+      if (h < 0 || h >= H) continue;
+      for (int b = 0; b < kw; ++b) {
+        const int w = wo * sw - pw + b;
+        if (w < 0 || w >= W) continue;
+        float v[V];
+        load_vec<T>(x + ((int64_t)(n * H + h) * W + w) * C + cg * V, v);
+        const uint8_t tap = (uint8_t)(a * kw + b);
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (v[k] > best[k]) { best[k] = v[k]; bi[k] = tap; }
+      }
+    }
+    store_vec<T>(y + (int64_t)i * V, best);
+    if (idx) {
+      if (V == 8) {
+        uint2 pk;
+        pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+        pk.y = bi[4 % V] | (bi[5 % V] << 8) | (bi[6 % V] << 16) | ((uint32_t)bi[7 % V] << 24);
+        *reinterpret_cast<uint2*>(idx + (int64_t)i * V) = pk;
+      } else {
+        *reinterpret_cast<uint32_t*>(idx + (int64_t)i * V) =
+            bi[0] | (bi[1 % V] << 8) | (bi[2 % V] << 16) | ((uint32_t)bi[3 % V] << 24);
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_bwd_vec(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                        T* __restrict__ dx, int N, int H, int W, int C,
+                                                        int Ho, int Wo, int kh, int kw, int sh, int sw,
+                                                        int ph, int pw) {
+  constexpr int V = Vec<T>::N;
+  const int cv = C / V;
+  const int total = N * H * W * cv;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cg = i % cv;
+    int t = i / cv;
+    const int w = t % W;
+    t /= W;
+    const int h = t % H;
+    const int n = t / H;
+    int ho0 = (h + ph - kh + sh) / sh; if (h + ph - kh + 1 < 0) ho0 = 0;
+    int ho1 = (h + ph) / sh; if (ho1 >= Ho) ho1 = Ho - 1;
+    int wo0 = (w + pw - kw + sw) / sw; if (w + pw - kw + 1 < 0) wo0 = 0;
+    int wo1 = (w + pw) / sw; if (wo1 >= Wo) wo1 = Wo - 1;
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+    for (int ho = ho0; ho <= ho1; ++ho) {
+      const int a = h + ph - ho * sh;
+      if (a < 0 || a >= kh) continue;
+      for (int wo = wo0; wo <= wo1; ++wo) {
+        const int b = w + pw - wo * sw;
+        if (b < 0 || b >= kw) continue;
+        const int64_t o = ((int64_t)(n * Ho + ho) * Wo + wo) * C + cg * V;
+        const uint8_t tap = (uint8_t)(a * kw + b);
+        uint8_t ix[V];
+        if (V == 8) {
+          uint2 pk = *reinterpret_cast<const uint2*>(idx + o);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { ix[k] = (pk.x >> (8 * k)) & 255; ix[(4 + k) % V] = (pk.y >> (8 * k)) & 255; }
+        } else {
+          uint32_t pk = *reinterpret_cast<const uint32_t*>(idx + o);
+#pragma unroll
+          for (int k = 0; k < V; ++k) ix[k] = (pk >> (8 * k)) & 255;
+        }
+        float g[V];
+        load_vec<T>(dy + o, g);
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (ix[k] == tap) acc[k] += g[k];
+      }
+    }
+    store_vec<T>(dx + (int64_t)i * V, acc);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N,
                                                       int H, int W, int C, int Ho, int Wo, int kh,
@@ -201,6 +303,15 @@ HETU_API int hetu_maxpool_fwd(const void* x, void* y, uint8_t* idx, int N, int H
                               int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw,
                               int is_bf16, hipStream_t st) {
   int64_t total = (int64_t)N * Ho * Wo * C;
+  const int V = is_bf16 ? 8 : 4;
+  if (C % V == 0 && total < (1LL << 31) && (int64_t)N * H * W * C < (1LL << 31)) {
+    int64_t nb = (total / V + 255) / 256;
+    int grid = (int)(nb < 65536 ? nb : 65536);
+    if (is_bf16) hipLaunchKernelGGL(maxpool_fwd_vec<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, idx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+    else hipLaunchKernelGGL(maxpool_fwd_vec<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, idx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+    HETU_LAUNCH_CHECK();
+    return 0;
+  }
   int grid = stream_grid(total, 256, 2);
   if (is_bf16) hipLaunchKernelGGL(maxpool_fwd_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, idx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
   else hipLaunchKernelGGL(maxpool_fwd_k<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, idx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
@@ -212,6 +323,15 @@ HETU_API int hetu_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int 
                               int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph,
                               int pw, int is_bf16, hipStream_t st) {
   int64_t total = (int64_t)N * H * W * C;
+  const int V = is_bf16 ? 8 : 4;
+  if (C % V == 0 && total < (1LL << 31)) {
+    int64_t nb = (total / V + 255) / 256;
+    int grid = (int)(nb < 65536 ? nb : 65536);
+    if (is_bf16) hipLaunchKernelGGL(maxpool_bwd_vec<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)dy, idx, (bf16*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+    else hipLaunchKernelGGL(maxpool_bwd_vec<float>, dim3(grid), dim3(256), 0, st, (const float*)dy, idx, (float*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+    HETU_LAUNCH_CHECK();
+    return 0;
+  }
   int grid = stream_grid(total, 256, 2);
   if (is_bf16) hipLaunchKernelGGL(maxpool_bwd_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)dy, idx, (bf16*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
   else hipLaunchKernelGGL(maxpool_bwd_k<float>, dim3(grid), dim3(256), 0, st, (const float*)dy, idx, (float*)dx, N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);

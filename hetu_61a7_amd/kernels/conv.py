@@ -94,16 +94,33 @@ def _vendor_dgrad0(g, w, x_shape, stride, padding):
     return dx
 
 
-def conv2d_backward_filter(g, x, w_shape, stride, padding):
+def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
+    """Weight gradient.  ``out`` (an fp32 channels-last view, e.g. the
+    optimizer's flat gradient slot) receives the result in place."""
     g, x = _match(g, x)
+    if out is not None and (out.dtype != torch.float32 or tuple(out.shape) != tuple(w_shape) or
+                            not out.is_contiguous(memory_format=CL)):
+        out = None
     if g.is_cuda:
         g = g.contiguous(memory_format=CL)
         x = x.contiguous(memory_format=CL)
         from . import conv_igemm
+
+        def vendor():
+            dw = _vendor_wgrad(g, x, w_shape, stride, padding)
+            if out is None:
+                return dw
+            out.copy_(dw)
+            return out
         return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
-                     lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding),
-                     lambda: _vendor_wgrad(g, x, w_shape, stride, padding))
-    return _vendor_wgrad(g, x, w_shape, stride, padding)
+                     lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
+                                                            accumulate=False),
+                     vendor)
+    dw = _vendor_wgrad(g, x, w_shape, stride, padding)
+    if out is not None:
+        out.copy_(dw)
+        return out
+    return dw
 
 
 def _vendor_wgrad(g, x, w_shape, stride, padding):

@@ -69,15 +69,17 @@ def _splitk(M, Nc, P_):
     return int(fn('hetu_gemm_pick_splitk', [I64, I64, I64])(M, Nc, P_))
 
 
-def try_backward_filter(g, x, w_shape, stride, padding, out=None):
-    """Returns the fp32 weight gradient (channels-last), accumulating into ``out``
-    when given (it must then be a zeroed / partial fp32 CL tensor)."""
+def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=None):
+    """Returns the fp32 weight gradient (channels-last) written into ``out`` when
+    given: accumulated onto its contents (default) or overwriting them
+    (``accumulate=False``)."""
     if not _ok(x, g, x.shape[1], g.shape[1]):
         return None
     N, C, H, W = x.shape
     K, _, KH, KW = w_shape
     OH, OW = g.shape[2], g.shape[3]
-    accumulate = out is not None
+    if accumulate is None:
+        accumulate = out is not None
     if out is None:
         dw = torch.empty((K, KH, KW, C), dtype=torch.float32, device=g.device)
     else:

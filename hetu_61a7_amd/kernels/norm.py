@@ -84,7 +84,8 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
     return y, mean.float(), invstd.float()
 
 
-def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=False, bias=None):
+def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=False, bias=None,
+                dscale_out=None, dbias_out=None):
     """Returns (dx, dscale, dbias, dres)."""
     C = x.shape[1]
     if native(x) and x.dtype in (torch.float32, torch.bfloat16):
@@ -101,8 +102,8 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
             M = x.numel() // C
             dx = _like_rows(x)
             dres = _like_rows(x) if want_dres else None
-            dscale = torch.empty(C, dtype=torch.float32, device=x.device)
-            dbias = torch.empty(C, dtype=torch.float32, device=x.device)
+            dscale = dscale_out if dscale_out is not None else torch.empty(C, dtype=torch.float32, device=x.device)
+            dbias = dbias_out if dbias_out is not None else torch.empty(C, dtype=torch.float32, device=x.device)
             ws = _ws(M, C, is_bf16(x), x.device)
             f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P])
             check(f(dy.data_ptr(), y.data_ptr() if relu else None, x.data_ptr(), dx.data_ptr(),

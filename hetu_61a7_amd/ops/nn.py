@@ -94,9 +94,16 @@ class Conv2d_Gradient_of_FilterOp(Op):
         super().__init__(Conv2d_Gradient_of_FilterOp, [x, grad, w_ref], ctx)
         self.padding, self.stride = _pair(padding), _pair(stride)
 
+    grad_dest = None  # set by the optimizer: this op's slot in the flat gradient buffer
+
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x, g, wshape = input_vals
-        return KC.conv2d_backward_filter(g, x, tuple(wshape), self.stride, self.padding)
+        return KC.conv2d_backward_filter(g, x, tuple(wshape), self.stride, self.padding,
+                                         out=self.grad_dest)
+
+    def set_grad_dest(self, dest):
+        self.grad_dest = dest
+        return True
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -306,8 +313,10 @@ class Batch_Normalization_GradientOp(Op):
         g, x, scale, (y, (mean, invstd)) = input_vals[:4]
         bias = input_vals[4] if len(input_vals) > 4 else None
         fw = self.forward_node
+        dests = getattr(self, 'grad_dests', {})
         dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
-                                                 relu=fw.relu, want_dres=fw.has_residual, bias=bias)
+                                                 relu=fw.relu, want_dres=fw.has_residual, bias=bias,
+                                                 dscale_out=dests.get(1), dbias_out=dests.get(2))
         return (dx, dscale, dbias, dres)
 
     def gradient(self, output_grad):
@@ -321,6 +330,18 @@ class BNGradSelectOp(Op):
     def __init__(self, g, index, ctx=None):
         super().__init__(BNGradSelectOp, [g], ctx)
         self.index = index
+
+    def set_grad_dest(self, dest):
+        """dscale / dbias are written by the fused BN-backward kernel straight into
+        the optimizer's flat gradient buffer."""
+        src = self.inputs[0]
+        if self.index in (1, 2) and isinstance(src, Batch_Normalization_GradientOp) and \
+                dest.dtype == torch.float32 and dest.is_contiguous():
+            if not hasattr(src, 'grad_dests'):
+                src.grad_dests = {}
+            src.grad_dests[self.index] = dest
+            return True
+        return False
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         return input_vals[0][self.index]

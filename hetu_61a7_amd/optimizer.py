@@ -295,6 +295,12 @@ class OptimizerOp(Op):
         amp = config.mixed_precision
         self.flat = FlatGroup(dense, values, opt.n_states, getattr(opt, 'state_init', (0.0, 0.0)),
                               shadow=amp, device=self.ctx.torch_device if self.ctx else None)
+        # ops that can write their gradient straight into the flat buffer get its view
+        grad_of = {pp: g for pp, g in zip(self.param_of_input, self.inputs)}
+        for p in dense:
+            g = grad_of.get(p)
+            if g is not None and hasattr(g, 'set_grad_dest') and not config.cpu_only:
+                g.set_grad_dest(self.flat.view(p, 'grad'))
         for p in dense:
             values[p] = self.flat.view(p, 'param')
             # 1-D parameters (biases, BN/LN affine) are consumed by fp32 epilogues and
@@ -359,9 +365,11 @@ class OptimizerOp(Op):
             self._pending_sparse.append((p, value))
             return
         dst = self.flat.view(p, 'grad')
-        if value.shape != dst.shape:
-            value = value.reshape(dst.shape)
-        dst.copy_(value)
+        if not (value.data_ptr() == dst.data_ptr() and value.dtype == dst.dtype and
+                value.stride() == dst.stride()):
+            if value.shape != dst.shape:
+                value = value.reshape(dst.shape)
+            dst.copy_(value)
         if self.dp:
             b = self.bucket_of.get(p)
             if b is not None:

@@ -276,7 +276,7 @@ def pinned_empty(shape, dtype=torch.float32) -> torch.Tensor:
 class ND_Sparse_Array(object):
     """CSR sparse matrix (reference ``ndarray.py:460-504``)."""
 
-    __slots__ = ('data', 'row', 'col', 'nrow', 'ncol', 'lazy')
+    __slots__ = ('data', 'row', 'col', 'nrow', 'ncol', 'lazy', 'cache')
 
     def __init__(self, data: NDArray, row: NDArray, col: NDArray, nrow: int, ncol: int):
         self.data = data
@@ -285,6 +285,7 @@ class ND_Sparse_Array(object):
         self.nrow = nrow
         self.ncol = ncol
         self.lazy = False
+        self.cache = {}  # device CSR parts / transposed CSR (kernels.spmm)
 
     @property
     def shape(self):

@@ -52,3 +52,4 @@ from .moe import (layout_transform_op, layout_transform_gradient_op, reverse_lay
                   sam_group_sum_op, sam_max_op, sammax_grad_op, group_topk_idx_op)
 from .executor import Executor, HetuConfig, gradients, find_topo_sort
 from .attention import attention_op, AttentionOp, AttentionGradientOp
+from .distgcn import distgcn_15d_op, DistGCN_15dOp, make_15d_groups, partition_15d

@@ -16,11 +16,23 @@ MI355X-first:
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 
 from .. import init
 from .. import ops as ht
 from .. import optimizer as optim
+from ..context import context as _context
+
+
+def _stage_ctx(placement, layer):
+    """Context of planner layer ``layer`` (0 = embeddings, 1..L = encoder
+    layers, L+1 = heads) under ``placement`` (a callable layer -> device group),
+    or a no-op when the model is not pipelined."""
+    if placement is None:
+        return contextlib.nullcontext()
+    return _context(placement(layer))
 
 
 class BertConfig(object):
@@ -105,12 +117,14 @@ class BertLayer(object):
 
 
 class BertModel(object):
-    def __init__(self, cfg: BertConfig):
+    def __init__(self, cfg: BertConfig, placement=None):
         self.cfg = cfg
+        self.placement = placement
         H = cfg.hidden_size
-        self.word_embeddings = _w('word_embeddings', (cfg.vocab_size, H), cfg)
-        self.position_embeddings = _w('position_embeddings', (cfg.max_position_embeddings, H), cfg)
-        self.token_type_embeddings = _w('token_type_embeddings', (cfg.type_vocab_size, H), cfg)
+        with _stage_ctx(placement, 0):
+            self.word_embeddings = _w('word_embeddings', (cfg.vocab_size, H), cfg)
+            self.position_embeddings = _w('position_embeddings', (cfg.max_position_embeddings, H), cfg)
+            self.token_type_embeddings = _w('token_type_embeddings', (cfg.type_vocab_size, H), cfg)
         self.layers = [BertLayer(cfg, i) for i in range(cfg.num_hidden_layers)]
 
     def __call__(self, input_ids, token_type_ids, attention_mask):
@@ -118,19 +132,27 @@ class BertModel(object):
         Returns (sequence_output [B*S, H], pooled_output [B, H])."""
         c = self.cfg
         B, S, H = c.batch_size, c.seq_len, c.hidden_size
-        pos = ht.Variable('position_ids', value=np.tile(np.arange(S, dtype=np.int64), (B, 1)), trainable=False)
-        e = ht.embedding_lookup_op(self.word_embeddings, input_ids) + \
-            ht.embedding_lookup_op(self.position_embeddings, pos) + \
-            ht.embedding_lookup_op(self.token_type_embeddings, token_type_ids)
-        e = ht.array_reshape_op(e, (B * S, H))
-        h = _dropout(_ln(e, H, 'embeddings_LayerNorm'), c.hidden_dropout_prob)
-        # extended additive mask [B, 1, 1, S]: 0 keep, -10000 masked
-        m = ht.array_reshape_op(attention_mask, (B, 1, 1, S))
-        m = ht.mul_byconst_op(ht.addbyconst_op(m, -1.0), 10000.0)
-        for layer in self.layers:
-            h = layer(h, m)
-        first = ht.array_reshape_op(ht.slice_op(ht.array_reshape_op(h, (B, S, H)), (0, 0, 0), (B, 1, H)), (B, H))
-        pooled = ht.tanh_op(_dense(first, H, H, 'pooler_dense', c))
+        pl = self.placement
+        with _stage_ctx(pl, 0):
+            pos = ht.Variable('position_ids', value=np.tile(np.arange(S, dtype=np.int64), (B, 1)),
+                              trainable=False)
+            e = ht.embedding_lookup_op(self.word_embeddings, input_ids) + \
+                ht.embedding_lookup_op(self.position_embeddings, pos) + \
+                ht.embedding_lookup_op(self.token_type_embeddings, token_type_ids)
+            e = ht.array_reshape_op(e, (B * S, H))
+            h = _dropout(_ln(e, H, 'embeddings_LayerNorm'), c.hidden_dropout_prob)
+        for i, layer in enumerate(self.layers):
+            with _stage_ctx(pl, i + 1):
+                # extended additive mask [B, 1, 1, S]: 0 keep, -10000 masked (built on
+                # every stage from the fed mask, so it never crosses a stage boundary)
+                if i == 0 or pl is not None and pl(i + 1) != pl(i):
+                    m = ht.array_reshape_op(attention_mask, (B, 1, 1, S))
+                    m = ht.mul_byconst_op(ht.addbyconst_op(m, -1.0), 10000.0)
+                h = layer(h, m)
+        with _stage_ctx(pl, len(self.layers) + 1):
+            first = ht.array_reshape_op(ht.slice_op(ht.array_reshape_op(h, (B, S, H)), (0, 0, 0), (B, 1, H)),
+                                        (B, H))
+            pooled = ht.tanh_op(_dense(first, H, H, 'pooler_dense', c))
         return h, pooled
 
 
@@ -150,20 +172,30 @@ class BertPreTrainingHeads(object):
 
 
 class BertForPreTraining(object):
-    def __init__(self, cfg):
+    def __init__(self, cfg, placement=None):
         self.cfg = cfg
-        self.bert = BertModel(cfg)
-        self.cls = BertPreTrainingHeads(cfg, self.bert.word_embeddings)
+        self.placement = placement
+        self.bert = BertModel(cfg, placement)
+        head = len(self.bert.layers) + 1
+        if placement is not None and placement(head) != placement(0):
+            # pipelined: the MLM decoder lives on the last stage, so it gets its own
+            # weight instead of shipping the tied 30522 x H table across stages
+            with _stage_ctx(placement, head):
+                E = _w('cls_decoder_weight', (cfg.vocab_size, cfg.hidden_size), cfg)
+        else:
+            E = self.bert.word_embeddings
+        self.cls = BertPreTrainingHeads(cfg, E)
 
     def __call__(self, input_ids, token_type_ids, attention_mask, masked_lm_labels=None,
                  next_sentence_label=None):
         seq, pooled = self.bert(input_ids, token_type_ids, attention_mask)
-        scores, nsp = self.cls(seq, pooled)
-        out = [scores, nsp]
-        if masked_lm_labels is not None and next_sentence_label is not None:
-            mlm = ht.softmaxcrossentropy_sparse_op(scores, masked_lm_labels, ignored_index=-1)
-            ns = ht.softmaxcrossentropy_sparse_op(nsp, next_sentence_label, ignored_index=-1)
-            out += [mlm, ns]
+        with _stage_ctx(self.placement, len(self.bert.layers) + 1):
+            scores, nsp = self.cls(seq, pooled)
+            out = [scores, nsp]
+            if masked_lm_labels is not None and next_sentence_label is not None:
+                mlm = ht.softmaxcrossentropy_sparse_op(scores, masked_lm_labels, ignored_index=-1)
+                ns = ht.softmaxcrossentropy_sparse_op(nsp, next_sentence_label, ignored_index=-1)
+                out += [mlm, ns]
         return out
 
 
@@ -201,19 +233,43 @@ class BertForSequenceClassification(object):
         return [logits, ht.softmaxcrossentropy_sparse_op(logits, labels, ignored_index=-1)]
 
 
-def bert_pretrain_graph(cfg, lr=1e-5, optimizer=None):
+def plan_placement(plan, ctx_of_ranks=None):
+    """layer -> device group of its pipeline stage under a Galvatron ``Plan``
+    (``parallel.galvatron``); ``ctx_of_ranks`` maps a rank list to a context
+    (default: the stage's GPUs)."""
+    def placement(layer):
+        s = next(i for i, (a, b) in enumerate(plan.stages) if a <= layer < b)
+        ranks = plan.stage_ranks(s)
+        if ctx_of_ranks is not None:
+            return ctx_of_ranks(ranks)
+        devs = plan.stage_devices(s)
+        return devs if len(devs) > 1 else devs[0]
+    return placement
+
+
+def bert_pretrain_graph(cfg, lr=1e-5, optimizer=None, plan=None, placement=None):
     """Placeholders + loss + train op for BERT pretraining (reference
-    train_hetu_bert.py: Adam lr 1e-5, loss = mean MLM + mean NSP)."""
-    input_ids = ht.Variable(name='input_ids', trainable=False)
-    token_type_ids = ht.Variable(name='token_type_ids', trainable=False)
-    attention_mask = ht.Variable(name='attention_mask', trainable=False)
-    mlm_labels = ht.Variable(name='masked_lm_labels', trainable=False)
-    nsp_labels = ht.Variable(name='next_sentence_label', trainable=False)
-    model = BertForPreTraining(cfg)
+    train_hetu_bert.py: Adam lr 1e-5, loss = mean MLM + mean NSP).
+
+    ``plan`` (a Galvatron ``Plan`` over the L+2 planner layers of
+    ``galvatron.bert_layers``) or an explicit ``placement`` puts every layer in
+    its pipeline stage's device context; run the result with
+    ``Executor(..., pipeline='gpipe' | 'pipedream')``."""
+    if plan is not None and placement is None and plan.pp > 1:
+        placement = plan_placement(plan)
+    with _stage_ctx(placement, 0):
+        input_ids = ht.Variable(name='input_ids', trainable=False)
+        token_type_ids = ht.Variable(name='token_type_ids', trainable=False)
+        attention_mask = ht.Variable(name='attention_mask', trainable=False)
+    with _stage_ctx(placement, cfg.num_hidden_layers + 1):
+        mlm_labels = ht.Variable(name='masked_lm_labels', trainable=False)
+        nsp_labels = ht.Variable(name='next_sentence_label', trainable=False)
+    model = BertForPreTraining(cfg, placement)
     _, _, mlm, nsp = model(input_ids, token_type_ids, attention_mask, mlm_labels, nsp_labels)
-    loss = ht.reduce_mean_op(mlm, [0]) + ht.reduce_mean_op(nsp, [0])
-    opt = optimizer or optim.AdamOptimizer(learning_rate=lr)
-    train = opt.minimize(loss)
+    with _stage_ctx(placement, cfg.num_hidden_layers + 1):
+        loss = ht.reduce_mean_op(mlm, [0]) + ht.reduce_mean_op(nsp, [0])
+        opt = optimizer or optim.AdamOptimizer(learning_rate=lr)
+        train = opt.minimize(loss)
     feeds = dict(input_ids=input_ids, token_type_ids=token_type_ids, attention_mask=attention_mask,
                  masked_lm_labels=mlm_labels, next_sentence_label=nsp_labels)
     return feeds, loss, train

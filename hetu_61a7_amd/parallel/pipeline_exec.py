@@ -323,8 +323,10 @@ class PipelineSubExecutor(object):
                         if v is None:
                             continue
                         if isinstance(v, ndarray.IndexedSlices):
-                            v = v.to_dense()
-                        acc[i] = v.float() if i not in acc else acc[i] + v.float()
+                            # sparse (embedding) grads stay sparse across micro-batches
+                            acc[i] = v if i not in acc else acc[i].merge(v)
+                        else:
+                            acc[i] = v.float() if i not in acc else acc[i] + v.float()
                 states[mb] = None
         self.p2p.flush()
         if self.opt is not None and acc:

@@ -80,13 +80,14 @@ class ThresholdMaskGradOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, x = input_vals
+        g = g.reshape(x.shape)
         return torch.where(x >= self.threshold, g, torch.zeros_like(g))
 
     def gradient(self, output_grad):
         raise NotImplementedError
 
     def infer_shape(self, input_shapes):
-        return input_shapes[0]
+        return input_shapes[1]
 
 
 def threshold_mask_op(x, threshold, ctx=None):

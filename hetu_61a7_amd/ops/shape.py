@@ -678,7 +678,8 @@ class IndexingGradOp(Op):
         return out
 
     def gradient(self, output_grad):
-        raise NotImplementedError
+        # scatter by a permutation: its adjoint is the gather with the same index
+        return [indexing_op(output_grad, self.inputs[1], ctx=self.raw_ctx), None]
 
     def infer_shape(self, input_shapes):
         return input_shapes[0]

@@ -1,0 +1,208 @@
+"""MoE layers on the CPU backend (reference examples/moe/test_moe_*.py): gate
+routing, dispatch/combine numerics against a dense torch reference, training
+progress for every gate family, and expert parallelism over a 2-rank gloo
+all-to-all."""
+import numpy as np
+import pytest
+import torch
+
+import hetu_61a7_amd as ht
+from hetu_61a7_amd.layers.moe import (TopKGate, KTop1Gate, HashGate, SAMGate, DenseToSparseGate,
+                                      BalanceAssignmentGate, Expert, MoELayer, HashLayer, SAMLayer,
+                                      KTop1Layer)
+from hetu_61a7_amd.kernels import moe as KM
+
+
+def _ref_topk_moe(X, Wg, bg, W1s, W2s, k):
+    """Dense reference: y_t = sum_j gate_tj * expert_{idx_tj}(x_t) (no drops)."""
+    x = torch.tensor(X)
+    g = torch.softmax(x @ torch.tensor(Wg) + torch.tensor(bg), -1)
+    v, i = torch.topk(g, k, -1)
+    y = torch.zeros_like(x)
+    for t in range(x.shape[0]):
+        for j in range(k):
+            e = int(i[t, j])
+            h = torch.relu(x[t] @ torch.tensor(W1s[e]))
+            y[t] += v[t, j] * (h @ torch.tensor(W2s[e]))
+    return y.numpy()
+
+
+def _params(ex):
+    return {n.name: ex.config.placeholder_to_arr_map[n].detach().float().cpu().numpy()
+            for n in ex.config.placeholder_to_arr_map}
+
+
+@pytest.mark.parametrize('k', [1, 2])
+def test_topk_moe_matches_dense_reference(k):
+    T, d, E = 24, 8, 4
+    rng = np.random.RandomState(k)
+    X = rng.randn(T, d).astype(np.float32)
+    x = ht.Variable(name='x')
+    gate = TopKGate(d, T, E, k=k, capacity_factor=float(E))   # capacity large enough: no drops
+    experts = [Expert(d, 12, activation='relu', name='expert_%d' % i) for i in range(E)]
+    y, l_aux = MoELayer(gate, experts, num_tokens=T, embed_dim=d)(x)
+    ex = ht.Executor([y, l_aux], ctx=ht.cpu(0))
+    got = ex.run(feed_dict={x: X}, convert_to_numpy_ret_vals=True)
+    p = _params(ex)
+    Wg, bg = p['TopK_Gate_linear_weight'], p['TopK_Gate_linear_bias']
+    W1s = [p['expert_%d_weight_1' % i] for i in range(E)]
+    W2s = [p['expert_%d_weight_2' % i] for i in range(E)]
+    ref = _ref_topk_moe(X, Wg, bg, W1s, W2s, k)
+    np.testing.assert_allclose(got[0], ref, rtol=1e-4, atol=1e-5)
+    assert np.isfinite(got[1]).all()
+
+
+def test_capacity_drops_overflow_tokens():
+    T, d, E, cap = 8, 4, 2, 3
+    x = torch.arange(T * d, dtype=torch.float32).reshape(T, d)
+    idx = torch.zeros(T, 1, dtype=torch.long)                 # everyone wants expert 0
+    loc = torch.arange(T).reshape(T, 1)
+    out = KM.layout_transform(x, idx, loc, cap, E)
+    assert out.shape == (E * cap, d)
+    np.testing.assert_array_equal(out[:cap].numpy(), x[:cap].numpy())
+    assert float(out[cap:].abs().sum()) == 0.0
+    y = KM.reverse_layout_transform(out, idx, loc, torch.ones(T, 1), cap)
+    np.testing.assert_array_equal(y[:cap].numpy(), x[:cap].numpy())
+    assert float(y[cap:].abs().sum()) == 0.0                 # dropped tokens contribute 0
+
+
+def _routing(rng, T, E, k, cap):
+    idx = torch.tensor(np.stack([rng.permutation(E)[:k] for _ in range(T)]))
+    loc = torch.zeros(T, k, dtype=torch.long)
+    counts = [0] * E
+    for j in range(k):
+        for t in range(T):
+            loc[t, j] = counts[idx[t, j]]
+            counts[idx[t, j]] += 1
+    return idx, loc
+
+
+def dispatch_combine_check(device, dtype, T=10, d=6, E=3, k=2, cap=5, seed=3, tol=1e-5):
+    """Dispatch -> tanh -> gated combine, forward and backward, vs autograd."""
+    rng = np.random.RandomState(seed)
+    x = torch.tensor(rng.randn(T, d).astype(np.float32), requires_grad=True)
+    idx, loc = _routing(rng, T, E, k, cap)
+    gates = torch.tensor(rng.rand(T, k).astype(np.float32), requires_grad=True)
+    slots = idx * cap + loc
+    valid = loc < cap
+    disp = torch.zeros(E * cap, d).index_put((slots[valid],), x.unsqueeze(1).expand(T, k, d)[valid])
+    yexp = torch.tanh(disp)
+    comb = (yexp[slots.clamp(max=E * cap - 1)] * (valid.unsqueeze(-1) * gates.unsqueeze(-1))).sum(1)
+    go = torch.tensor(rng.randn(T, d).astype(np.float32))
+    comb.backward(go)
+    dev = lambda t: t.detach().to(device)
+    xd, gd, god = dev(x).to(dtype), dev(gates), dev(go).to(dtype)
+    idd, lod = dev(idx), dev(loc)
+    d0 = KM.layout_transform(xd, idd, lod, cap, E)
+    y0 = torch.tanh(d0.float()).to(dtype)
+    out = KM.reverse_layout_transform(y0, idd, lod, gd, cap)
+    np.testing.assert_allclose(out.float().cpu().numpy(), comb.detach().numpy(), rtol=tol, atol=tol)
+    gy = KM.reverse_layout_transform_backward_data(god, idd, lod, gd, cap, E * cap)
+    gdisp = (gy.float() * (1 - y0.float() * y0.float())).to(dtype)
+    gx = KM.layout_transform_backward(gdisp, idd, lod, cap)
+    np.testing.assert_allclose(gx.float().cpu().numpy(), x.grad.numpy(), rtol=10 * tol, atol=10 * tol)
+    for j in range(k):
+        gg = KM.reverse_layout_transform_backward_gate(god, y0, idd[:, j:j + 1], lod[:, j:j + 1], cap)
+        np.testing.assert_allclose(gg.reshape(-1).float().cpu().numpy(), gates.grad[:, j].numpy(),
+                                   rtol=10 * tol, atol=10 * tol)
+
+
+def test_dispatch_combine_gradients_match_autograd():
+    dispatch_combine_check('cpu', torch.float32)
+    dispatch_combine_check('cpu', torch.float32, T=40, d=16, E=4, k=2, cap=6, seed=5)  # with drops
+
+
+def _train(layer_fn, feeds, steps=6, lr=0.05):
+    out = layer_fn()
+    if not isinstance(out, (tuple, list)):
+        out = (out,)
+    y, extra = out[0], list(out[1:])
+    loss = ht.reduce_mean_op(ht.mul_op(y, y), [0, 1])
+    for e in extra:
+        loss = ht.add_op(loss, ht.mul_byconst_op(e, 0.01))
+    train = ht.optim.SGDOptimizer(lr).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.cpu(0))
+    return [float(np.asarray(ex.run('train', feed_dict=feeds, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0])
+            for _ in range(steps)]
+
+
+@pytest.mark.parametrize('kind', ['topk', 'ktop1', 'hash', 'sam', 'dts', 'base'])
+def test_gate_family_trains(kind):
+    T, d, E = 32, 8, 4
+    rng = np.random.RandomState(0)
+    X = rng.randn(T, d).astype(np.float32)
+    x = ht.Variable(name='x')
+    experts = [Expert(d, 16, activation='relu', name='expert_%d' % i) for i in range(E)]
+    feeds = {x: X}
+    if kind == 'topk':
+        fn = lambda: MoELayer(TopKGate(d, T, E, k=2, capacity_factor=2.0), experts, T, d)(x)
+    elif kind == 'ktop1':
+        fn = lambda: KTop1Layer(KTop1Gate(d, T, E, k=2, capacity_factor=2.0), experts, T, d)(x)
+    elif kind == 'hash':
+        h = ht.Variable(name='h')
+        feeds[h] = (np.arange(T) % E).astype(np.float32).reshape(T, 1)
+        fn = lambda: HashLayer(HashGate(d, T, E, capacity_factor=2.0), experts, T, d)(x, h)
+    elif kind == 'sam':
+        fn = lambda: SAMLayer(SAMGate(d, T, E, k=1, capacity_factor=2.0, num_local_gpus=2), experts, T, d,
+                              num_local_gpus=2)(x)
+    elif kind == 'dts':
+        fn = lambda: MoELayer(DenseToSparseGate(d, T, E, k=2, capacity_factor=2.0), experts, T, d)(x)
+    else:
+        fn = lambda: MoELayer(BalanceAssignmentGate(d, T, E), experts, T, d, name='BalanceAssignmentLayer')(x)
+    losses = _train(fn, feeds)
+    assert np.isfinite(losses).all(), losses
+    assert losses[-1] < losses[0], losses
+
+
+def test_dts_temperature_anneals_to_sparse():
+    from hetu_61a7_amd.layers.moe import DTSTemperature
+    t = DTSTemperature(tau0=2.0, tau_min=0.3, decay=0.9)
+    vals = [t.step() for _ in range(50)]
+    assert vals[0] < 2.0 and vals[-1] == pytest.approx(0.3)
+    assert all(a >= b for a, b in zip(vals, vals[1:]))
+
+
+def _ep_worker(rank, world, port, q):
+    import os
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), HETU_USE_CONFIG='0')
+    import numpy as np
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.layers.moe import TopKGate, Expert, MoELayer
+    T, d, n_local = 16, 8, 2
+    E = n_local * world
+    rng = np.random.RandomState(100 + rank)
+    X = rng.randn(T, d).astype(np.float32)
+    x = ht.Variable(name='x')
+    experts = [Expert(d, 16, activation='relu', name='expert_%d' % (rank * n_local + i)) for i in range(n_local)]
+    y, l_aux = MoELayer(TopKGate(d, T, E, k=2, capacity_factor=float(E)), experts, T, d, all2all_size=world)(x)
+    loss = ht.add_op(ht.reduce_mean_op(ht.mul_op(y, y), [0, 1]), ht.mul_byconst_op(l_aux, 0.01))
+    train = ht.optim.SGDOptimizer(0.05).minimize(loss)
+    ex = ht.Executor({'train': [loss, y, train]}, comm_mode='AllReduce')
+    outs = []
+    for _ in range(4):
+        r = ex.run('train', feed_dict={x: X}, convert_to_numpy_ret_vals=True)
+        outs.append(float(np.asarray(r[0]).reshape(-1)[0]))
+    q.put((rank, outs))
+    from hetu_61a7_amd.parallel import comm
+    comm.destroy()
+
+
+def test_expert_parallel_two_ranks():
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ep_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert np.isfinite(res[r]).all() and res[r][-1] < res[r][0], res

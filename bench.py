@@ -8,8 +8,10 @@ bucketed RCCL all-reduce overlapped with backward.
         --master-addr 127.0.0.1 --master-port 29500 bench.py --gpus 8
 
 Prints ONE JSON line on rank 0.  ``value`` is whole-job samples/s (all ranks),
-``scaling`` is weak (fixed per-GPU batch).  ``--model wdl`` runs the
-Wide&Deep-Criteo-shape configuration instead (secondary metric).
+``scaling`` is weak (fixed per-GPU batch).  Secondary BASELINE configs:
+``--model wdl`` (Wide&Deep-Criteo, PS + HET cache), ``--model bert`` (BERT-base
+pretraining, Galvatron-planned DP), ``--model moe`` (top-2 MoE, expert
+all-to-all; ``--moe-gate dts`` for the dense-to-sparse gate).
 """
 from __future__ import annotations
 
@@ -30,7 +32,8 @@ def parse():
     p.add_argument('--batch', type=int, default=None, help='per-GPU batch (256 resnet50, 128 wdl)')
     p.add_argument('--criteo-rows', type=int, default=0, help='embedding rows (default: full Criteo 33762577)')
     p.add_argument('--cache', default='LFUOpt')
-    p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl'])
+    p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl', 'bert', 'moe'])
+    p.add_argument('--moe-gate', default='topk', choices=['topk', 'dts'])
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     p.add_argument('--bucket-mb', type=float, default=32)
     p.add_argument('--op-profile', default=None, help='write per-op-type GPU time (ms) to this file')
@@ -96,6 +99,12 @@ def main():
                'per_gpu_batch': B}
         step = lambda: ex.run('train', feed_dict=feed)
         samples_per_step = B * world
+    elif args.model == 'bert':
+        from hetu_61a7_amd.models.bert import bert_bench
+        step, samples_per_step, cfg, metric, finish = bert_bench(args, world, rank, local)
+    elif args.model == 'moe':
+        from hetu_61a7_amd.models.moe import moe_top_bench
+        step, samples_per_step, cfg, metric, finish = moe_top_bench(args, world, rank, local)
     else:
         from hetu_61a7_amd.models.ctr import wdl_criteo_bench
         step, samples_per_step, cfg, metric, finish = wdl_criteo_bench(args, world, rank, local)
@@ -130,7 +139,7 @@ def main():
         print('non-channels-last 4D outputs:', layout_report(), file=sys.stderr)
     value = samples_per_step * args.steps / dt_s
     if rank == 0:
-        out = {'metric': metric, 'value': round(value, 2), 'unit': 'samples/s', 'n_gpus': world,
+        out = {'metric': metric, 'value': round(value, 2), 'unit': 'tokens/s' if args.model == 'moe' else 'samples/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
                'dtype': args.dtype, 'data': 'synthetic (random-init weights)', 'config': cfg}

@@ -1,0 +1,401 @@
+// Mixture-of-Experts routing kernels for gfx950 (reference src/ops/LayoutTransform.cu,
+// TopKIdx.cu, TopKVal.cu, CumSum.cu).
+//
+// The reference dispatch scatters token rows with one thread per token and
+// combines with atomicAdd; its gate gradient is a 32-lane shuffle dot product.
+// Here every data-moving kernel is a *gather* (deterministic, no atomics) run as
+// one wave64 per output row with 16-byte vector accesses:
+//
+//   slot_map      slot_src[e*cap + loc] = t*k + j  for every routed (t, j) with loc < cap
+//   gather_slots  out[s, :] = w[slot_src[s]] * src[slot_src[s] / k, :]   (0 for empty slots)
+//                 -> dispatch forward (w = 1) and combine backward-data (w = gate)
+//   combine       out[t, :] = sum_j w[t, j] * y[slot(t, j), :]            (dropped -> 0)
+//                 -> combine forward (w = gate) and dispatch backward (w = 1)
+//   gate_grad     dgate[t, j] = <dout[t, :], y[slot(t, j), :]>            (wave64 dot)
+//
+// The gate itself is fused: `gate_topk` (softmax + top-k, one wave per token,
+// k rounds of wave arg-max, experts held in registers) and `locations` (slot of
+// every (token, choice) inside its expert's capacity, choice-major like the
+// reference's cumsum chain, one workgroup per expert using ballot/popcount
+// prefix sums; it also emits the per-expert load-balancing terms).  The gate
+// backward `gate_backward` folds the gate-value gradient and the balance-loss
+// gradient into one softmax backward per token.
+#include "common.h"
+
+namespace hetu {
+
+constexpr int kMaxEPL = 8;   // experts per lane (E <= 512)
+constexpr int kMaxK = 8;
+
+// ---------------------------------------------------------------------------
+// softmax + top-k per row
+template <typename T>
+__global__ void __launch_bounds__(256) gate_topk_k(const T* __restrict__ logits, float* __restrict__ probs,
+                                                    int64_t* __restrict__ idx, float* __restrict__ val,
+                                                    int rows, int E, int k, int do_softmax) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* x = logits + (int64_t)row * E;
+  float v[kMaxEPL];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < kMaxEPL; ++i) {
+    const int e = lane + 64 * i;
+    v[i] = (e < E) ? to_f(x[e]) : -INFINITY;
+    m = fmaxf(m, v[i]);
+  }
+  if (do_softmax) {
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i) {
+      const int e = lane + 64 * i;
+      v[i] = (e < E) ? __expf(v[i] - m) : 0.f;
+      s += v[i];
+    }
+    s = wave_sum(s);
+    const float inv = 1.f / s;
+#pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i) {
+      const int e = lane + 64 * i;
+      if (e < E) {
+        v[i] *= inv;
+        probs[(int64_t)row * E + e] = v[i];
+      } else {
+        v[i] = -INFINITY;
+      }
+    }
+  }
+  for (int j = 0; j < k; ++j) {
+    // lane-local best (lowest expert id on ties), then wave arg-max
+    float bv = -INFINITY;
+    int be = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i) {
+      const int e = lane + 64 * i;
+      if (e < E && (v[i] > bv || (v[i] == bv && e < be))) { bv = v[i]; be = e; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oe = __shfl_xor(be, o, 64);
+      if (ov > bv || (ov == bv && oe < be)) { bv = ov; be = oe; }
+    }
+    if (lane == 0) {
+      idx[(int64_t)row * k + j] = be;
+      val[(int64_t)row * k + j] = bv;
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i)
+      if (lane + 64 * i == be) v[i] = -INFINITY;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// capacity slots, choice-major: loc(t, j) = #{(t', j') before (t, j) in order
+// (j' < j) or (j' == j, t' < t) with idx == idx(t, j)}.  One workgroup per
+// expert; also counts[e] = routed (t, j) pairs (before drops) and
+// psum[e] = sum_t probs[t, e] (balance loss).
+__global__ void __launch_bounds__(256) locations_k(const int64_t* __restrict__ idx,
+                                                   const float* __restrict__ probs,
+                                                   int64_t* __restrict__ loc, int* __restrict__ counts,
+                                                   float* __restrict__ psum, int T, int k, int E) {
+  __shared__ int wsum[4];
+  __shared__ float fsum[4];
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int base = 0;
+  const int total = T * k;
+  for (int c0 = 0; c0 < total; c0 += 256) {
+    const int c = c0 + threadIdx.x;      // choice-major flat index: j * T + t
+    bool hit = false;
+    int t = 0, j = 0;
+    if (c < total) {
+      j = c / T;
+      t = c - j * T;
+      hit = idx[(int64_t)t * k + j] == e;
+    }
+    const unsigned long long b = __ballot(hit);
+    const int before = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(b);
+    __syncthreads();
+    int off = base;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    if (hit) loc[(int64_t)t * k + j] = off + before;
+    base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  float s = 0.f;
+  if (probs != nullptr)
+    for (int t = threadIdx.x; t < T; t += 256) s += probs[(int64_t)t * E + e];
+  s = wave_sum(s);
+  if (lane == 0) fsum[w] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    counts[e] = base;
+    if (psum != nullptr) psum[e] = fsum[0] + fsum[1] + fsum[2] + fsum[3];
+  }
+}
+
+// dlogits[t, :] = softmax_bwd(p, dp) with
+// dp[t, e] = sum_j [idx(t, j) == e] * dgate[t, j] + aux_coef[e]
+__global__ void __launch_bounds__(256) gate_backward_k(const float* __restrict__ probs,
+                                                       const int64_t* __restrict__ idx,
+                                                       const float* __restrict__ dgate,
+                                                       const float* __restrict__ aux_coef,
+                                                       float* __restrict__ dlogits, int rows, int E, int k) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  int ie[kMaxK];
+  float ig[kMaxK];
+#pragma unroll
+  for (int j = 0; j < kMaxK; ++j) {
+    ie[j] = (j < k) ? (int)idx[(int64_t)row * k + j] : -1;
+    ig[j] = (j < k && dgate != nullptr) ? dgate[(int64_t)row * k + j] : 0.f;
+  }
+  float p[kMaxEPL], dp[kMaxEPL];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxEPL; ++i) {
+    const int e = lane + 64 * i;
+    p[i] = 0.f; dp[i] = 0.f;
+    if (e < E) {
+      p[i] = probs[(int64_t)row * E + e];
+      float d = aux_coef != nullptr ? aux_coef[e] : 0.f;
+#pragma unroll
+      for (int j = 0; j < kMaxK; ++j) d += (ie[j] == e) ? ig[j] : 0.f;
+      dp[i] = d;
+      dot += p[i] * d;
+    }
+  }
+  dot = wave_sum(dot);
+#pragma unroll
+  for (int i = 0; i < kMaxEPL; ++i) {
+    const int e = lane + 64 * i;
+    if (e < E) dlogits[(int64_t)row * E + e] = p[i] * (dp[i] - dot);
+  }
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) slot_map_k(const int64_t* __restrict__ idx,
+                                                  const int64_t* __restrict__ loc, int* __restrict__ slot_src,
+                                                  int Tk, int cap, int nslots) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Tk) return;
+  const int64_t l = loc[i], e = idx[i];
+  if (l < cap && l >= 0 && e >= 0) {
+    const int64_t s = e * cap + l;
+    if (s < nslots) slot_src[s] = i;
+  }
+}
+
+// row copy helpers: one wave moves one row of d elements (vectorised when aligned)
+template <typename T>
+__device__ __forceinline__ void row_scale_copy(const T* __restrict__ src, T* __restrict__ dst, float w, int d,
+                                               int lane, bool vec) {
+  constexpr int N = Vec<T>::N;
+  if (vec) {
+    for (int c = lane * N; c < d; c += 64 * N) {
+      float v[N];
+      load_vec<T>(src + c, v);
+#pragma unroll
+      for (int q = 0; q < N; ++q) v[q] *= w;
+      store_vec<T>(dst + c, v);
+    }
+  } else {
+    for (int c = lane; c < d; c += 64) dst[c] = from_f<T>(w * to_f(src[c]));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gather_slots_k(const T* __restrict__ src, const int* __restrict__ slot_src,
+                                                      const float* __restrict__ w, T* __restrict__ out,
+                                                      int nslots, int d, int k, int vec) {
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslots) return;
+  const int si = slot_src[s];
+  T* o = out + (int64_t)s * d;
+  if (si < 0) {
+    constexpr int N = Vec<T>::N;
+    if (vec) {
+      float z[N];
+#pragma unroll
+      for (int q = 0; q < N; ++q) z[q] = 0.f;
+      for (int c = lane * N; c < d; c += 64 * N) store_vec<T>(o + c, z);
+    } else {
+      for (int c = lane; c < d; c += 64) o[c] = from_f<T>(0.f);
+    }
+    return;
+  }
+  const float ww = w != nullptr ? w[si] : 1.f;
+  row_scale_copy<T>(src + (int64_t)(si / k) * d, o, ww, d, lane, vec != 0);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) combine_k(const T* __restrict__ y, const int64_t* __restrict__ idx,
+                                                 const int64_t* __restrict__ loc, const float* __restrict__ w,
+                                                 T* __restrict__ out, int Tn, int k, int cap, int d, int vec) {
+  constexpr int N = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= Tn) return;
+  const T* rows[kMaxK];
+  float ws[kMaxK];
+  int nv = 0;
+  for (int j = 0; j < k && j < kMaxK; ++j) {
+    const int64_t l = loc[(int64_t)t * k + j];
+    if (l < cap && l >= 0) {
+      rows[nv] = y + ((int64_t)idx[(int64_t)t * k + j] * cap + l) * d;
+      ws[nv] = w != nullptr ? w[(int64_t)t * k + j] : 1.f;
+      ++nv;
+    }
+  }
+  T* o = out + (int64_t)t * d;
+  if (vec) {
+    for (int c = lane * N; c < d; c += 64 * N) {
+      float acc[N];
+#pragma unroll
+      for (int q = 0; q < N; ++q) acc[q] = 0.f;
+      for (int r = 0; r < nv; ++r) {
+        float v[N];
+        load_vec<T>(rows[r] + c, v);
+#pragma unroll
+        for (int q = 0; q < N; ++q) acc[q] += ws[r] * v[q];
+      }
+      store_vec<T>(o + c, acc);
+    }
+  } else {
+    for (int c = lane; c < d; c += 64) {
+      float acc = 0.f;
+      for (int r = 0; r < nv; ++r) acc += ws[r] * to_f(rows[r][c]);
+      o[c] = from_f<T>(acc);
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gate_grad_k(const T* __restrict__ g, const T* __restrict__ y,
+                                                   const int64_t* __restrict__ idx, const int64_t* __restrict__ loc,
+                                                   float* __restrict__ out, int Tk, int k, int cap, int d, int vec) {
+  constexpr int N = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= Tk) return;
+  const int64_t l = loc[i];
+  if (l >= cap || l < 0) {
+    if (lane == 0) out[i] = 0.f;
+    return;
+  }
+  const T* gr = g + (int64_t)(i / k) * d;
+  const T* yr = y + ((int64_t)idx[i] * cap + l) * d;
+  float s = 0.f;
+  if (vec) {
+    for (int c = lane * N; c < d; c += 64 * N) {
+      float a[N], b[N];
+      load_vec<T>(gr + c, a);
+      load_vec<T>(yr + c, b);
+#pragma unroll
+      for (int q = 0; q < N; ++q) s += a[q] * b[q];
+    }
+  } else {
+    for (int c = lane; c < d; c += 64) s += to_f(gr[c]) * to_f(yr[c]);
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[i] = s;
+}
+
+template <typename T>
+static bool vec_ok(const void* a, const void* b, int d) {
+  constexpr int N = Vec<T>::N;
+  return (d % N) == 0 && ((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0;
+}
+
+}  // namespace hetu
+
+using namespace hetu;
+
+HETU_API int hetu_moe_gate_topk(const void* logits, float* probs, int64_t* idx, float* val, int rows, int E,
+                                int k, int do_softmax, int bf16_in, hipStream_t s) {
+  if (E > 64 * kMaxEPL || k > kMaxK || k > E) return (int)hipErrorInvalidValue;
+  const int g = (rows + 3) / 4;
+  if (g == 0) return 0;
+  if (bf16_in)
+    gate_topk_k<bf16><<<g, 256, 0, s>>>((const bf16*)logits, probs, idx, val, rows, E, k, do_softmax);
+  else
+    gate_topk_k<float><<<g, 256, 0, s>>>((const float*)logits, probs, idx, val, rows, E, k, do_softmax);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_moe_locations(const int64_t* idx, const float* probs, int64_t* loc, int* counts, float* psum,
+                                int T, int k, int E, hipStream_t s) {
+  if (E <= 0) return 0;
+  locations_k<<<E, 256, 0, s>>>(idx, probs, loc, counts, psum, T, k, E);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_moe_gate_backward(const float* probs, const int64_t* idx, const float* dgate,
+                                    const float* aux_coef, float* dlogits, int rows, int E, int k, hipStream_t s) {
+  if (E > 64 * kMaxEPL || k > kMaxK) return (int)hipErrorInvalidValue;
+  const int g = (rows + 3) / 4;
+  if (g == 0) return 0;
+  gate_backward_k<<<g, 256, 0, s>>>(probs, idx, dgate, aux_coef, dlogits, rows, E, k);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_moe_slot_map(const int64_t* idx, const int64_t* loc, int* slot_src, int Tk, int cap,
+                               int nslots, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(slot_src, 0xff, (size_t)nslots * sizeof(int), s);
+  if (e != hipSuccess) return (int)e;
+  if (Tk > 0) slot_map_k<<<(Tk + 255) / 256, 256, 0, s>>>(idx, loc, slot_src, Tk, cap, nslots);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_moe_gather_slots(const void* src, const int* slot_src, const float* w, void* out, int nslots,
+                                   int d, int k, int bf16_io, hipStream_t s) {
+  const int g = (nslots + 3) / 4;
+  if (g == 0) return 0;
+  if (bf16_io)
+    gather_slots_k<bf16><<<g, 256, 0, s>>>((const bf16*)src, slot_src, w, (bf16*)out, nslots, d, k,
+                                           vec_ok<bf16>(src, out, d));
+  else
+    gather_slots_k<float><<<g, 256, 0, s>>>((const float*)src, slot_src, w, (float*)out, nslots, d, k,
+                                            vec_ok<float>(src, out, d));
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_moe_combine(const void* y, const int64_t* idx, const int64_t* loc, const float* w, void* out,
+                              int T, int k, int cap, int d, int bf16_io, hipStream_t s) {
+  if (k > kMaxK) return (int)hipErrorInvalidValue;
+  const int g = (T + 3) / 4;
+  if (g == 0) return 0;
+  if (bf16_io)
+    combine_k<bf16><<<g, 256, 0, s>>>((const bf16*)y, idx, loc, w, (bf16*)out, T, k, cap, d,
+                                      vec_ok<bf16>(y, out, d));
+  else
+    combine_k<float><<<g, 256, 0, s>>>((const float*)y, idx, loc, w, (float*)out, T, k, cap, d,
+                                       vec_ok<float>(y, out, d));
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_moe_gate_grad(const void* g, const void* y, const int64_t* idx, const int64_t* loc, float* out,
+                                int Tk, int k, int cap, int d, int bf16_io, hipStream_t s) {
+  const int gr = (Tk + 3) / 4;
+  if (gr == 0) return 0;
+  if (bf16_io)
+    gate_grad_k<bf16><<<gr, 256, 0, s>>>((const bf16*)g, (const bf16*)y, idx, loc, out, Tk, k, cap, d,
+                                         vec_ok<bf16>(g, y, d));
+  else
+    gate_grad_k<float><<<gr, 256, 0, s>>>((const float*)g, (const float*)y, idx, loc, out, Tk, k, cap, d,
+                                          vec_ok<float>(g, y, d));
+  HETU_LAUNCH_CHECK();
+  return 0;
+}

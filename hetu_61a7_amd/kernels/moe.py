@@ -5,7 +5,8 @@ Reference LayoutTransform.cu scatters token i into slot
 ``expert(i) * capacity + location(i)`` (dropped when location >= capacity) and
 combines with gate weights through atomicAdd; its gate-gradient uses a
 hard-coded 32-lane shuffle.  Here dispatch and combine are gathers keyed by a
-per-slot source index (deterministic, no atomics) with wave64 dot products.
+per-slot source index (deterministic, no atomics) with wave64 dot products, and
+the top-k gate is fused (softmax + top-k + capacity slots + balance terms).
 """
 from __future__ import annotations
 
@@ -14,32 +15,133 @@ import torch
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32
 
 
-def topk(x, k):
+def _ik(t, T):
+    return t.reshape(T, -1).long().contiguous()
+
+
+def _io_ok(*ts):
+    return native(ts[0]) and all(supported_float(t) for t in ts) and len({t.dtype for t in ts}) == 1
+
+
+def topk(x, k, softmax=False):
+    """(values, indices) of the k largest entries per row; ``softmax=True``
+    ranks softmax(x) and also returns the probabilities (wave-per-row kernel)."""
+    R, E = x.reshape(-1, x.shape[-1]).shape
+    if native(x) and supported_float(x) and E <= 512 and k <= min(8, E):
+        x2 = x.reshape(R, E).contiguous()
+        probs = torch.empty((R, E) if softmax else (1,), dtype=torch.float32, device=x.device)
+        idx = torch.empty((R, k), dtype=torch.int64, device=x.device)
+        val = torch.empty((R, k), dtype=torch.float32, device=x.device)
+        f = fn('hetu_moe_gate_topk', [P, P, P, P, I32, I32, I32, I32, I32, P])
+        check(f(x2.data_ptr(), probs.data_ptr(), idx.data_ptr(), val.data_ptr(), R, E, k, int(softmax),
+                is_bf16(x2), stream_ptr()), 'moe_gate_topk')
+        return (val, idx, probs) if softmax else (val, idx)
+    if softmax:
+        p = torch.softmax(x.reshape(R, E).float(), -1)
+        v, i = torch.topk(p, k, dim=-1)
+        return v, i, p
     v, i = torch.topk(x, k, dim=-1)
     return v, i
+
+
+def locations(idx, num_experts, probs=None):
+    """Slot of every (token, choice) inside its expert, choice-major (the
+    reference's cumsum chain, moe_layer.py / TopGate.py), plus per-expert routed
+    counts and column sums of ``probs`` (balance loss terms)."""
+    T, k = idx.shape
+    E = num_experts
+    if native(idx):
+        idx = idx.long().contiguous()
+        loc = torch.empty((T, k), dtype=torch.int64, device=idx.device)
+        counts = torch.empty((E,), dtype=torch.int32, device=idx.device)
+        psum = torch.empty((E,), dtype=torch.float32, device=idx.device) if probs is not None else None
+        f = fn('hetu_moe_locations', [P, P, P, P, P, I32, I32, I32, P])
+        check(f(idx.data_ptr(), probs.contiguous().data_ptr() if probs is not None else None, loc.data_ptr(),
+                counts.data_ptr(), psum.data_ptr() if psum is not None else None, T, k, E, stream_ptr()),
+              'moe_locations')
+        return loc, counts, psum
+    oh = torch.nn.functional.one_hot(idx.long().t().reshape(-1), E)          # [(j, t), E], choice-major
+    cum = torch.cumsum(oh, 0) - 1
+    loc = (cum * oh).sum(1).reshape(k, T).t().contiguous()
+    counts = oh.sum(0).int()
+    psum = probs.float().sum(0) if probs is not None else None
+    return loc, counts, psum
+
+
+def gate_backward(probs, idx, dgate, aux_coef):
+    """d logits of (gate values [T, k] = probs[t, idx], balance term sum_e c_e * sum_t probs[t, e])."""
+    T, E = probs.shape
+    k = idx.shape[1]
+    if native(probs) and E <= 512 and k <= 8:
+        out = torch.empty((T, E), dtype=torch.float32, device=probs.device)
+        dg = dgate.float().reshape(T, k).contiguous() if dgate is not None else None
+        ac = aux_coef.float().contiguous() if aux_coef is not None else None
+        f = fn('hetu_moe_gate_backward', [P, P, P, P, P, I32, I32, I32, P])
+        check(f(probs.contiguous().data_ptr(), idx.long().contiguous().data_ptr(), ptr_or_none(dg), ptr_or_none(ac),
+                out.data_ptr(), T, E, k, stream_ptr()), 'moe_gate_backward')
+        return out
+    dp = torch.zeros((T, E), dtype=torch.float32, device=probs.device)
+    if dgate is not None:
+        dp.scatter_add_(1, idx.long(), dgate.float().reshape(T, k))
+    if aux_coef is not None:
+        dp = dp + aux_coef.float().unsqueeze(0)
+    p = probs.float()
+    return p * (dp - (p * dp).sum(-1, keepdim=True))
+
+
+def ptr_or_none(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _slot_map(idx, loc, capacity, nslots):
+    Tk = idx.numel()
+    m = torch.empty((nslots,), dtype=torch.int32, device=idx.device)
+    f = fn('hetu_moe_slot_map', [P, P, P, I32, I32, I32, P])
+    check(f(idx.data_ptr(), loc.data_ptr(), m.data_ptr(), Tk, capacity, nslots, stream_ptr()), 'moe_slot_map')
+    return m
 
 
 def layout_transform(x, indices, locations, capacity, num_experts):
     """x [T, d]; indices/locations [T, k] -> out [E*capacity, d] (zero padded)."""
     T, d = x.shape
-    k = indices.shape[1] if indices.dim() == 2 else 1
-    idx = indices.reshape(T, k).long()
-    loc = locations.reshape(T, k).long()
-    out = torch.zeros((num_experts * capacity, d), dtype=x.dtype, device=x.device)
+    idx, loc = _ik(indices, T), _ik(locations, T)
+    k = idx.shape[1]
+    nslots = num_experts * capacity
+    if _io_ok(x):
+        x = x.contiguous()
+        smap = _slot_map(idx, loc, capacity, nslots)
+        out = torch.empty((nslots, d), dtype=x.dtype, device=x.device)
+        f = fn('hetu_moe_gather_slots', [P, P, P, P, I32, I32, I32, I32, P])
+        check(f(x.data_ptr(), smap.data_ptr(), None, out.data_ptr(), nslots, d, k, is_bf16(x), stream_ptr()),
+              'moe_gather_slots')
+        return out
+    out = torch.zeros((nslots, d), dtype=x.dtype, device=x.device)
     valid = loc < capacity
     slots = idx * capacity + loc
     tok = torch.arange(T, device=x.device).unsqueeze(1).expand(T, k)
-    s, t = slots[valid], tok[valid]
-    out[s] = x[t]
+    out[slots[valid]] = x[tok[valid]]
+    return out
+
+
+def _combine(y, idx, loc, w, capacity, T):
+    d = y.shape[-1]
+    k = idx.shape[1]
+    y = y.contiguous()
+    out = torch.empty((T, d), dtype=y.dtype, device=y.device)
+    wf = w.float().reshape(T, k).contiguous() if w is not None else None
+    f = fn('hetu_moe_combine', [P, P, P, P, P, I32, I32, I32, I32, I32, P])
+    check(f(y.data_ptr(), idx.data_ptr(), loc.data_ptr(), ptr_or_none(wf), out.data_ptr(), T, k, capacity, d,
+            is_bf16(y), stream_ptr()), 'moe_combine')
     return out
 
 
 def layout_transform_backward(g, indices, locations, capacity):
     """grad wrt x: sum over the k slots each token was written to."""
     T = indices.shape[0]
-    k = indices.shape[1] if indices.dim() == 2 else 1
-    idx = indices.reshape(T, k).long()
-    loc = locations.reshape(T, k).long()
+    idx, loc = _ik(indices, T), _ik(locations, T)
+    k = idx.shape[1]
+    if _io_ok(g) and k <= 8:
+        return _combine(g, idx, loc, None, capacity, T)
     valid = (loc < capacity)
     slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
     gathered = g[slots.reshape(-1)].reshape(T, k, -1) * valid.unsqueeze(-1).to(g.dtype)
@@ -49,9 +151,10 @@ def layout_transform_backward(g, indices, locations, capacity):
 def reverse_layout_transform(y, indices, locations, gates, capacity):
     """combine: out[t] = sum_j gates[t, j] * y[slot(t, j)] (dropped slots -> 0)."""
     T = indices.shape[0]
-    k = indices.shape[1] if indices.dim() == 2 else 1
-    idx = indices.reshape(T, k).long()
-    loc = locations.reshape(T, k).long()
+    idx, loc = _ik(indices, T), _ik(locations, T)
+    k = idx.shape[1]
+    if _io_ok(y) and k <= 8:
+        return _combine(y, idx, loc, gates, capacity, T)
     valid = loc < capacity
     slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
     rows = y[slots.reshape(-1)].reshape(T, k, -1).float()
@@ -61,29 +164,44 @@ def reverse_layout_transform(y, indices, locations, gates, capacity):
 
 def reverse_layout_transform_backward_data(g, indices, locations, gates, capacity, num_slots):
     T = indices.shape[0]
-    k = indices.shape[1] if indices.dim() == 2 else 1
-    idx = indices.reshape(T, k).long()
-    loc = locations.reshape(T, k).long()
+    idx, loc = _ik(indices, T), _ik(locations, T)
+    k = idx.shape[1]
+    d = g.shape[-1]
+    if _io_ok(g):
+        g = g.contiguous()
+        smap = _slot_map(idx, loc, capacity, num_slots)
+        wf = gates.float().reshape(T, k).contiguous() if gates is not None else None
+        out = torch.empty((num_slots, d), dtype=g.dtype, device=g.device)
+        f = fn('hetu_moe_gather_slots', [P, P, P, P, I32, I32, I32, I32, P])
+        check(f(g.data_ptr(), smap.data_ptr(), ptr_or_none(wf), out.data_ptr(), num_slots, d, k, is_bf16(g),
+                stream_ptr()), 'moe_gather_slots')
+        return out
     valid = loc < capacity
     slots = idx * capacity + loc
     w = (gates.reshape(T, k).float() * valid.float()) if gates is not None else valid.float()
-    out = torch.zeros((num_slots, g.shape[-1]), dtype=torch.float32, device=g.device)
+    out = torch.zeros((num_slots, d), dtype=torch.float32, device=g.device)
     contrib = g.float().unsqueeze(1) * w.unsqueeze(-1)
-    sv = slots[valid]
-    out.index_add_(0, sv, contrib[valid])
+    out.index_add_(0, slots[valid], contrib[valid])
     return out.to(g.dtype)
 
 
 def reverse_layout_transform_backward_gate(g, y, indices, locations, capacity):
     T = indices.shape[0]
-    k = indices.shape[1] if indices.dim() == 2 else 1
-    idx = indices.reshape(T, k).long()
-    loc = locations.reshape(T, k).long()
+    idx, loc = _ik(indices, T), _ik(locations, T)
+    k = idx.shape[1]
+    d = g.shape[-1]
+    if _io_ok(g, y):
+        g, y = g.contiguous(), y.contiguous()
+        out = torch.empty((T, k), dtype=torch.float32, device=g.device)
+        f = fn('hetu_moe_gate_grad', [P, P, P, P, P, I32, I32, I32, I32, I32, P])
+        check(f(g.data_ptr(), y.data_ptr(), idx.data_ptr(), loc.data_ptr(), out.data_ptr(), T * k, k, capacity, d,
+                is_bf16(g), stream_ptr()), 'moe_gate_grad')
+        return out.reshape(indices.shape)
     valid = loc < capacity
     slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
     rows = y[slots.reshape(-1)].reshape(T, k, -1).float()
-    d = (rows * g.float().unsqueeze(1)).sum(-1) * valid.float()
-    return d.reshape(indices.shape)
+    dd = (rows * g.float().unsqueeze(1)).sum(-1) * valid.float()
+    return dd.reshape(indices.shape)
 
 
 def balanced_assignment(scores, max_iterations=100):

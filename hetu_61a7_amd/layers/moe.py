@@ -40,9 +40,13 @@ def _locations(masks):
     return locs
 
 
-def topkgating(logits, k, capacity_factor, num_tokens, num_experts, embed_dim=None):
-    gates = O.softmax_op(logits)
+def topkgating(logits, k, capacity_factor, num_tokens, num_experts, embed_dim=None, fused=True):
     capacity = k * math.ceil((num_tokens / num_experts) * capacity_factor)
+    if fused and k <= 8 and num_experts <= 512:
+        from ..ops.moe import topk_gating_op
+        l_aux, idx, loc, gate_w = topk_gating_op(logits, k, capacity, num_experts)
+        return l_aux, [idx], [loc], [gate_w], capacity
+    gates = O.softmax_op(logits)
     topk_indices = O.topk_idx_op(gates, topk=k)
     indices_s = [O.split_op(topk_indices, axes=[1], indices=[i], splits=[k]) for i in range(k)]
     masks = [O.array_reshape_op(O.one_hot_op(ix, num_classes=num_experts), [-1, num_experts]) for ix in indices_s]
@@ -70,14 +74,19 @@ class _GateBase(BaseLayer):
 
 
 class TopKGate(_GateBase):
+    """``fused=True`` (default) runs the whole gate as the fused softmax/top-k/
+    slot kernels (``topk_gating_op``); ``fused=False`` builds the reference's
+    op-by-op graph (same values)."""
+
     def __init__(self, embed_dim, num_tokens, num_experts, k=1, capacity_factor=1.0,
-                 eval_capacity_factor=1.0, initializer=None, name='TopK_Gate'):
+                 eval_capacity_factor=1.0, initializer=None, name='TopK_Gate', fused=True):
         super().__init__(embed_dim, num_tokens, num_experts, k, capacity_factor, eval_capacity_factor,
                          initializer, name)
+        self.fused = fused
 
     def __call__(self, x):
         return topkgating(self._logits(x), self.top_k, self.capacity_factor, self.num_tokens,
-                          self.num_experts)
+                          self.num_experts, fused=self.fused)
 
 
 class KTop1Gate(_GateBase):

@@ -286,3 +286,40 @@ def synthetic_bert_batch(cfg, seed=0, mask_prob=0.15):
     nsp = rng.integers(0, 2, (B,)).astype(np.int64)
     return dict(input_ids=ids, token_type_ids=types, attention_mask=mask, masked_lm_labels=mlm,
                 next_sentence_label=nsp)
+
+
+def bert_bench(args, world, rank, local):
+    """Benchmark step for BASELINE config 4 (reference
+    examples/nlp/bert/scripts/train_hetu_bert_base_dp.sh: BERT-base, seq 128,
+    batch 64 per GPU, Adam lr 1e-5, MLM + NSP pretraining), bf16 compute,
+    synthetic token ids.  On N > 1 GPUs the Galvatron planner picks the
+    DP x PP layout for the node (``galvatron.plan_bert``); for BERT-base it
+    selects pure DP (the model fits every GPU; PP only adds a bubble), run with
+    the bucketed RCCL all-reduce.
+    Returns (step_fn, samples_per_step, config, metric, finish_fn)."""
+    import torch
+    import hetu_61a7_amd as H
+    from ..parallel.galvatron import GalvatronPlanner, Hardware, bert_layers
+    B = args.batch or 64
+    cfg = BertConfig.base(batch_size=B, seq_len=128)
+    specs = bert_layers(cfg.hidden_size, cfg.num_hidden_layers, cfg.seq_len, cfg.vocab_size)
+    plan = GalvatronPlanner(specs, hw=Hardware(gpus=world)).search(B * world)
+    if plan.pp > 1 or max(plan.tp) > 1:
+        raise NotImplementedError('bench: planner chose %s; only its DP layout is benchmarked' % plan.short())
+    feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-5)
+    kw = dict(mixed_precision=args.dtype, seed=1234, bucket_mb=getattr(args, 'bucket_mb', 32))
+    if world > 1:
+        ex = H.Executor({'train': [loss, train]}, dist_strategy=H.dist.DataParallel('allreduce'), **kw)
+    else:
+        ex = H.Executor({'train': [loss, train]}, ctx=H.gpu(local), **kw)
+    dev = torch.device('cuda', local)
+    batch = synthetic_bert_batch(cfg, seed=10 + rank)
+    fd = {feeds[k]: torch.from_numpy(v).to(dev) for k, v in batch.items()}
+
+    def step():
+        ex.run('train', feed_dict=fd)
+
+    conf = {'model': 'BERT-base (L12 H768 A12, MLM+NSP)', 'global_batch': B * world, 'seq_len': 128,
+            'parallelism': 'dp%d (galvatron plan: %s)' % (world, plan.short()), 'optimizer': 'adam',
+            'per_gpu_batch': B}
+    return step, B * world, conf, 'samples/sec (whole node) BERT-base pretraining', None

@@ -1,0 +1,95 @@
+"""MoE model family (reference examples/moe/test_moe_top.py:17-36, test_moe_hash.py,
+test_moe_ktop1.py, test_moe_sam.py, test_moe_base.py).
+
+``moe_top`` is the reference's top-k benchmark network: one MoE layer (TopK gate,
+``num_local_experts`` two-layer ReLU experts per GPU, expert-parallel over all
+ranks with RCCL all-to-all) followed by reduce-sum over the model dim, softmax
+over tokens and an NLL loss, plus the balance loss.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import ops as ht
+from ..layers.moe import (TopKGate, KTop1Gate, HashGate, SAMGate, DenseToSparseGate, BalanceAssignmentGate,
+                          Expert, MoELayer, KTop1Layer, HashLayer, SAMLayer)
+
+
+def moe_experts(model_dim, hidden_size, num_local_experts, rank=0, dropout_rate=0.1):
+    return [Expert(embed_dim=model_dim, ffn_dim=hidden_size, dropout_rate=dropout_rate, activation='relu',
+                   name='expert_%d' % (rank * num_local_experts + i)) for i in range(num_local_experts)]
+
+
+def moe_top(x, y_, batch_size, num_tokens, model_dim, hidden_size, num_local_experts, world=1, rank=0,
+            top=2, gate='topk', dropout_rate=0.1, hash_ids=None):
+    """Returns (loss, y).  ``x`` [B, T, d]; ``y_`` the NLL targets [B]."""
+    E = num_local_experts * world
+    ntok = batch_size * num_tokens
+    experts = moe_experts(model_dim, hidden_size, num_local_experts, rank, dropout_rate)
+    extra = []
+    if gate == 'topk':
+        out = MoELayer(TopKGate(model_dim, ntok, E, k=top), experts, num_tokens, model_dim, world, top=top)(x)
+    elif gate == 'dts':
+        out = MoELayer(DenseToSparseGate(model_dim, ntok, E, k=top), experts, num_tokens, model_dim, world)(x)
+    elif gate == 'ktop1':
+        out = KTop1Layer(KTop1Gate(model_dim, ntok, E, k=top), experts, num_tokens, model_dim, world, k=top)(x)
+    elif gate == 'sam':
+        out = SAMLayer(SAMGate(model_dim, ntok, E, k=top, num_local_gpus=max(world, 1)), experts, num_tokens,
+                       model_dim, world, k=top, num_local_gpus=max(world, 1))(x)
+    elif gate == 'hash':
+        out = (HashLayer(HashGate(model_dim, ntok, E), experts, num_tokens, model_dim, world)(x, hash_ids),)
+    elif gate == 'base':
+        out = (MoELayer(BalanceAssignmentGate(model_dim, ntok, E, device_id=rank), experts, num_tokens, model_dim,
+                        world, name='BalanceAssignmentLayer')(x),)
+    else:
+        raise ValueError(gate)
+    y, extra = out[0], list(out[1:])
+    y = ht.array_reshape_op(y, [-1, num_tokens, model_dim])
+    y = ht.reduce_sum_op(y, axes=2)
+    y = ht.softmax_op(y)
+    loss = ht.nll_loss_op(y, y_, num_tokens)
+    for e in extra:
+        loss = loss + e
+    return loss, y
+
+
+def moe_top_bench(args, world, rank, local):
+    """Benchmark step for BASELINE config 5 (reference test_moe_top.py defaults:
+    per GPU batch 16 x 1024 tokens, d_model = d_ffn = 2048, 2 experts per GPU,
+    top-2, expert dropout 0.1, SGD lr 0.125), bf16 compute.  Gate: top-k (default)
+    or the dense-to-sparse gate (``--moe-gate dts``).
+    Returns (step_fn, samples_per_step, config, metric, finish_fn); a "sample"
+    is one token."""
+    import torch
+    import hetu_61a7_amd as H
+    B, T, d, ffn, nle = args.batch or 16, 1024, 2048, 2048, 2
+    gate = getattr(args, 'moe_gate', 'topk')
+    x, y_ = H.Variable(name='x', trainable=False), H.Variable(name='y_', trainable=False)
+    loss, y = moe_top(x, y_, B, T, d, ffn, nle, world, rank, top=2, gate=gate)
+    train = H.optim.SGDOptimizer(learning_rate=0.125).minimize(loss)
+    kw = dict(mixed_precision=args.dtype, seed=1234)
+    if world > 1:
+        ex = H.Executor({'train': [loss, train]}, ctx=H.gpu(local), comm_mode='AllReduce', **kw)
+    else:
+        ex = H.Executor({'train': [loss, train]}, ctx=H.gpu(local), **kw)
+    dev = torch.device('cuda', local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000 + rank)
+    dt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    X = torch.randn((B, T, d), generator=g, device=dev).to(dt)
+    Y = torch.zeros((B,), dtype=torch.float32, device=dev)
+    feed = {x: X, y_: Y}
+
+    def step():
+        ex.run('train', feed_dict=feed)
+
+    cfg = {'model': 'MoE top-2 (examples/moe/test_moe_top.py: d=2048, ffn=2048, 2 experts/GPU)',
+           'global_batch': B * world, 'seq_len': T, 'parallelism': 'ep%d (all-to-all) + dp%d gate' % (world, world),
+           'gate': gate, 'experts': nle * world, 'optimizer': 'sgd', 'per_gpu_batch': B}
+    return step, B * T * world, cfg, 'tokens/sec (whole node) MoE %s gate, expert all-to-all' % gate, None
+
+
+def moe_random_batch(batch_size, num_tokens, model_dim, seed=0):
+    rng = np.random.RandomState(seed)
+    return (rng.normal(size=(batch_size, num_tokens, model_dim)).astype(np.float32),
+            np.zeros((batch_size,), np.float32))

@@ -16,6 +16,8 @@ from ..kernels import moe as KM
 
 
 def _stack(vals):
+    if len(vals) == 1 and vals[0].dim() == 2:
+        return vals[0]          # already [T, k] (fused gate output)
     return torch.stack([v.reshape(-1) for v in vals], 1)
 
 
@@ -143,8 +145,9 @@ class ReverseLayoutTransformGradientGateOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, y, idx, loc = input_vals
-        return KM.reverse_layout_transform_backward_gate(g, y, idx.reshape(-1, 1), loc.reshape(-1, 1),
-                                                         self.capacity).reshape(idx.shape)
+        if idx.dim() != 2:
+            idx, loc = idx.reshape(-1, 1), loc.reshape(-1, 1)
+        return KM.reverse_layout_transform_backward_gate(g, y, idx, loc, self.capacity).reshape(input_vals[2].shape)
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -327,3 +330,109 @@ class GroupTopKIdxOp(Op):
 
 def group_topk_idx_op(node_A, node_B, topk, num_local_gpus, ctx=None):
     return GroupTopKIdxOp(node_A, node_B, topk, num_local_gpus, ctx=ctx)
+
+
+# ---------------------------------------------------------------------------
+# Fused top-k gate (MI355X path of reference TopGate.py:7-79): softmax, top-k,
+# capacity slots and the balance-loss terms in two kernels instead of the
+# ~6k-node softmax/topk/one_hot/cumsum/reduce chain.
+class TopKGatingOp(Op):
+    """value: gate weights [T, k] (softmax prob of each chosen expert);
+    aux: (probs [T, E], indices [T, k] int64, locations [T, k] int64, l_aux)."""
+
+    def __init__(self, logits, k, capacity, num_experts, ctx=None):
+        super().__init__(TopKGatingOp, [logits], ctx)
+        self.k, self.capacity, self.num_experts = int(k), int(capacity), int(num_experts)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from .nn import AuxResult
+        logits = input_vals[0]
+        T, E = logits.shape
+        val, idx, probs = KM.topk(logits, self.k, softmax=True)
+        loc, counts, psum = KM.locations(idx, E, probs)
+        coef = counts.float() / float(T)                     # mean_t mask[t, e] summed over choices
+        l_aux = (psum / float(T) * coef).sum() * float(E)
+        return AuxResult(val, (probs, idx, loc, l_aux, coef))
+
+    def gradient(self, output_grad):
+        return [TopKGatingGradOp(output_grad, self, None, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return (input_shapes[0][0], self.k)
+
+
+class TopKGatingGradOp(Op):
+    """d logits from d gate weights (``grad`` [T, k]) or from d l_aux (scalar,
+    ``aux_grad``): one fused softmax backward per token."""
+    value_and_aux_inputs = (1,)
+
+    def __init__(self, grad, gating, aux_grad, ctx=None):
+        ins = [grad if grad is not None else aux_grad, gating]
+        super().__init__(TopKGatingGradOp, ins, ctx)
+        self.is_aux = grad is None
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        g, (val, (probs, idx, loc, l_aux, coef)) = input_vals
+        T, E = probs.shape
+        if self.is_aux:
+            # l_aux = E * sum_e coef_e * sum_t probs[t, e] / T
+            c = coef * (float(E) / float(T)) * g.float().reshape(-1)[0]
+            return KM.gate_backward(probs, idx, None, c)
+        return KM.gate_backward(probs, idx, g, None)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return None
+
+
+class GatingSelectOp(Op):
+    """indices / locations / l_aux of a fused gate."""
+    value_and_aux_inputs = (0,)
+    _slot = {'indices': 1, 'locations': 2, 'l_aux': 3}
+
+    def __init__(self, gating, what, ctx=None):
+        super().__init__(GatingSelectOp, [gating], ctx)
+        self.what = what
+        self.gating = gating
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        val, aux = input_vals[0]
+        r = aux[self._slot[self.what]]
+        return r.reshape(1) if self.what == 'l_aux' else r
+
+    def gradient(self, output_grad):
+        if self.what != 'l_aux':
+            return [None]
+        return [None]   # routed to the logits by TopKGatingAuxGrad (see topk_gating_op)
+
+    def infer_shape(self, input_shapes):
+        T, k = input_shapes[0]
+        return (1,) if self.what == 'l_aux' else (T, k)
+
+
+class AuxLossOp(Op):
+    """l_aux of a fused gate, differentiable wrt the gate logits."""
+    value_and_aux_inputs = (0,)
+
+    def __init__(self, gating, logits, ctx=None):
+        super().__init__(AuxLossOp, [gating, logits], ctx)
+        self.gating = gating
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        val, aux = input_vals[0]
+        return aux[3].reshape(1)
+
+    def gradient(self, output_grad):
+        return [None, TopKGatingGradOp(None, self.gating, output_grad, ctx=self.raw_ctx)]
+
+    def infer_shape(self, input_shapes):
+        return (1,)
+
+
+def topk_gating_op(logits, k, capacity, num_experts, ctx=None):
+    """Returns (l_aux, indices [T,k], locations [T,k], gates [T,k]) nodes."""
+    g = TopKGatingOp(logits, k, capacity, num_experts, ctx=ctx)
+    return (AuxLossOp(g, logits, ctx=ctx), GatingSelectOp(g, 'indices', ctx=ctx),
+            GatingSelectOp(g, 'locations', ctx=ctx), g)

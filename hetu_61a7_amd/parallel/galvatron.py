@@ -114,6 +114,10 @@ class Plan:
         t = self.tp[layer]
         return [ranks[i:i + t] for i in range(0, len(ranks), t)]
 
+    def short(self):
+        tps = sorted(set(self.tp))
+        return 'pp%d tp%s mb%d' % (self.pp, '/'.join(map(str, tps)), self.micro_batches)
+
     def describe(self):
         lines = ['pp=%d micro_batches=%d est %.2f ms/step, %.1f samples/s' %
                  (self.pp, self.micro_batches, self.time * 1e3, self.throughput)]

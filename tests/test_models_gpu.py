@@ -73,3 +73,38 @@ def test_hipgraph_mlp_matches_eager():
         ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, use_hipgraph=g)
         out.append([float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]) for _ in range(8)])
     np.testing.assert_allclose(out[0], out[1], rtol=1e-4, atol=1e-5)
+
+
+def _tiny_bert_losses(ctx, mp=None, steps=4):
+    from hetu_61a7_amd.models.bert import BertConfig, bert_pretrain_graph, synthetic_bert_batch
+    from hetu_61a7_amd.ops import node as _node
+    _node.G_NODE_ID = 0
+    cfg = BertConfig(vocab_size=1200, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                     intermediate_size=128, batch_size=4, seq_len=16, max_position_embeddings=16,
+                     hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-3)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ctx, seed=5, mixed_precision=mp)
+    fd = {feeds[k]: v for k, v in synthetic_bert_batch(cfg, seed=1).items()}
+    return [float(np.asarray(ex.run('train', feed_dict=fd, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0])
+            for _ in range(steps)]
+
+
+def test_tiny_bert_gpu_matches_cpu():
+    a = _tiny_bert_losses(ht.cpu(0))
+    b = _tiny_bert_losses(ht.gpu(0))
+    np.testing.assert_allclose(a, b, rtol=2e-3, atol=2e-3)
+    c = _tiny_bert_losses(ht.gpu(0), mp='bf16', steps=6)
+    assert np.isfinite(c).all() and c[-1] < c[0]
+
+
+def test_moe_top_bf16_step():
+    from hetu_61a7_amd.models.moe import moe_top, moe_random_batch
+    B, T, d = 2, 64, 128
+    x, y_ = ht.Variable(name='x', trainable=False), ht.Variable(name='y_', trainable=False)
+    loss, y = moe_top(x, y_, B, T, d, 256, 2, top=2)
+    train = ht.optim.SGDOptimizer(0.5).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3)
+    X, Y = moe_random_batch(B, T, d)
+    ls = [float(np.asarray(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0])
+          for _ in range(6)]
+    assert np.isfinite(ls).all() and ls[-1] < ls[0], ls

@@ -1,0 +1,47 @@
+"""MoE HIP kernels (moe.hip) vs the CPU/torch reference; fused-gate MoE layer
+on the GPU vs the op-by-op gate."""
+import numpy as np
+import pytest
+import torch
+
+import hetu_61a7_amd as ht
+from hetu_61a7_amd.kernels import moe as KM
+from test_moe_cpu import dispatch_combine_check, moe_fused_vs_graph
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('dt,tol', [(torch.float32, 1e-5), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize('shape', [(10, 6, 3, 2, 5), (64, 256, 8, 2, 12), (33, 130, 4, 1, 9)])
+def test_dispatch_combine(dt, tol, shape):
+    T, d, E, k, cap = shape
+    dispatch_combine_check('cuda', dt, T=T, d=d, E=E, k=k, cap=cap, seed=T, tol=tol)
+
+
+@pytest.mark.parametrize('E,k', [(4, 1), (16, 2), (100, 3), (512, 8)])
+def test_gate_topk_and_locations(E, k):
+    rng = np.random.RandomState(E)
+    T = 300
+    x = torch.tensor(rng.randn(T, E).astype(np.float32))
+    v, i, p = KM.topk(x.cuda(), k, softmax=True)
+    rv, ri, rp = KM.topk(x, k, softmax=True)
+    np.testing.assert_allclose(p.cpu().numpy(), rp.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(v.cpu().numpy(), rv.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(i.cpu().numpy(), ri.numpy())
+    loc, cnt, ps = KM.locations(i, E, p)
+    rloc, rcnt, rps = KM.locations(ri, E, rp)
+    np.testing.assert_array_equal(loc.cpu().numpy(), rloc.numpy())
+    np.testing.assert_array_equal(cnt.cpu().numpy(), rcnt.numpy())
+    np.testing.assert_allclose(ps.cpu().numpy(), rps.numpy(), rtol=1e-4, atol=1e-5)
+    dg = torch.tensor(rng.randn(T, k).astype(np.float32))
+    coef = torch.tensor(rng.rand(E).astype(np.float32))
+    got = KM.gate_backward(p, i, dg.cuda(), coef.cuda())
+    ref = KM.gate_backward(rp, ri, dg, coef)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-6)
+
+
+def test_fused_gate_layer_gpu_matches_graph_gate():
+    a, b = moe_fused_vs_graph(ht.gpu(0))
+    np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    c, _ = moe_fused_vs_graph(ht.cpu(0))
+    np.testing.assert_allclose(a, c, rtol=1e-3, atol=1e-4)

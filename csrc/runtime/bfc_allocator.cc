@@ -1,0 +1,401 @@
+// BFC allocator implementation + C ABI + PyTorch pluggable-allocator entry
+// points (see bfc_allocator.h for the design).
+#include "bfc_allocator.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace hetu {
+
+BFCAllocator::BFCAllocator(MemKind kind, int device, size_t limit_bytes, size_t first_region)
+    : kind_(kind), device_(device), limit_(limit_bytes), next_region_(first_region) {
+  st_.bytes_limit = (int64_t)limit_bytes;
+  if (next_region_ < (2u << 20)) next_region_ = 2u << 20;
+}
+
+BFCAllocator::~BFCAllocator() {
+  for (auto& r : regions_) {
+    Chunk* c = r.first;
+    while (c) {
+      Chunk* n = c->next;
+      delete c;
+      c = n;
+    }
+    sub_free(r.base);
+  }
+}
+
+int BFCAllocator::bin_of(size_t size) {
+  size_t q = size / kMinAlloc;
+  int b = 0;
+  while (q > 1 && b < kNumBins - 1) {
+    q >>= 1;
+    ++b;
+  }
+  return b;
+}
+
+void* BFCAllocator::sub_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (plain_host()) {
+    if (posix_memalign(&p, 4096, bytes) != 0) return nullptr;
+    return p;
+  }
+  int cur = 0;
+  hipGetDevice(&cur);
+  if (cur != device_) hipSetDevice(device_);
+  hipError_t e = kind_ == MemKind::kDevice ? hipMalloc(&p, bytes)
+                                            : hipHostMalloc(&p, bytes, hipHostMallocPortable);
+  if (cur != device_) hipSetDevice(cur);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void BFCAllocator::sub_free(void* p) {
+  if (plain_host()) {
+    free(p);
+    return;
+  }
+  if (kind_ == MemKind::kDevice) {
+    hipFree(p);
+  } else {
+    hipHostFree(p);
+  }
+}
+
+void BFCAllocator::insert_free(Chunk* c) {
+  bins_[c->stream].b[bin_of(c->size)].insert(c);
+  st_.num_free_chunks++;
+}
+
+void BFCAllocator::erase_free(Chunk* c) {
+  bins_[c->stream].b[bin_of(c->size)].erase(c);
+  st_.num_free_chunks--;
+}
+
+BFCAllocator::Chunk* BFCAllocator::take_from(Bins& bins, size_t size) {
+  Chunk key{nullptr, size, false, 0, nullptr, nullptr, nullptr};
+  for (int b = bin_of(size); b < kNumBins; ++b) {
+    auto it = bins.b[b].lower_bound(&key);
+    if (it != bins.b[b].end()) return *it;
+  }
+  return nullptr;
+}
+
+BFCAllocator::Chunk* BFCAllocator::find_chunk(size_t size, hipStream_t s) {
+  Chunk* c = nullptr;
+  auto it = bins_.find(s);
+  if (it != bins_.end()) c = take_from(it->second, size);
+  if (c == nullptr && s != nullptr) {
+    auto jt = bins_.find(nullptr);
+    if (jt != bins_.end()) c = take_from(jt->second, size);
+  }
+  if (c == nullptr) return nullptr;
+  erase_free(c);
+  if (c->size - size >= kMinAlloc) {   // split; the remainder stays free on the same stream
+    Chunk* r = new Chunk{c->ptr + size, c->size - size, false, c->region, c, c->next, c->stream};
+    if (c->next) c->next->prev = r;
+    c->next = r;
+    c->size = size;
+    insert_free(r);
+  }
+  return c;
+}
+
+bool BFCAllocator::grow(size_t min_bytes) {
+  size_t want = std::max(next_region_, min_bytes);
+  if (limit_ && (size_t)st_.bytes_reserved + want > limit_) want = min_bytes;
+  if (limit_ && (size_t)st_.bytes_reserved + want > limit_) return false;
+  void* p = sub_alloc(want);
+  if (p == nullptr && want > min_bytes) {
+    want = min_bytes;
+    p = sub_alloc(want);
+  }
+  if (p == nullptr) return false;
+  Chunk* c = new Chunk{(char*)p, want, false, (int)regions_.size(), nullptr, nullptr, nullptr};
+  regions_.push_back(Region{(char*)p, want, c});
+  st_.bytes_reserved += (int64_t)want;
+  st_.num_regions++;
+  next_region_ = std::min<size_t>(next_region_ * 2, (size_t)16 << 30);
+  insert_free(c);
+  return true;
+}
+
+void BFCAllocator::clean_streams() {
+  // wait for every stream that owns free chunks to pass "now", then move those
+  // chunks to the clean bins (coalescing with clean neighbours)
+  std::vector<Chunk*> moved;
+  for (auto& kv : bins_) {
+    if (kv.first == nullptr) continue;
+    bool any = false;
+    for (auto& bin : kv.second.b) any |= !bin.empty();
+    if (!any) continue;
+    if (kind_ == MemKind::kDevice) {
+      hipEvent_t ev;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+        hipEventRecord(ev, kv.first);
+        hipEventSynchronize(ev);
+        hipEventDestroy(ev);
+      } else {
+        hipStreamSynchronize(kv.first);
+      }
+    }
+    for (auto& bin : kv.second.b) {
+      for (Chunk* c : bin) moved.push_back(c);
+      st_.num_free_chunks -= (int64_t)bin.size();
+      bin.clear();
+    }
+  }
+  if (moved.empty()) return;
+  std::unordered_map<Chunk*, int> mv;
+  for (Chunk* c : moved) {
+    c->stream = nullptr;
+    mv[c] = 1;
+  }
+  // one pass per region: re-insert moved chunks in address order so each one
+  // coalesces with its (already re-listed) free predecessor
+  for (auto& r : regions_) {
+    Chunk* c = r.base ? r.first : nullptr;
+    while (c) {
+      if (mv.count(c)) {
+        Chunk* m = free_chunk(c);
+        c = m->next;
+      } else {
+        c = c->next;
+      }
+    }
+  }
+}
+
+BFCAllocator::Chunk* BFCAllocator::free_chunk(Chunk* c) {
+  // c is not in any bin here; merge with free neighbours of the same stream tag
+  // (a tagged chunk never swallows clean memory: that would force a clean on the
+  // next other-stream allocation)
+  c->in_use = false;
+  Chunk* p = c->prev;
+  if (p && !p->in_use && p->stream == c->stream) {
+    bool listed = bins_[p->stream].b[bin_of(p->size)].count(p) > 0;
+    if (listed) {
+      erase_free(p);
+      p->size += c->size;
+      p->next = c->next;
+      if (c->next) c->next->prev = p;
+      delete c;
+      c = p;
+    }
+  }
+  Chunk* n = c->next;
+  if (n && !n->in_use && n->stream == c->stream) {
+    bool listed = bins_[n->stream].b[bin_of(n->size)].count(n) > 0;
+    if (listed) {
+      erase_free(n);
+      c->size += n->size;
+      c->next = n->next;
+      if (n->next) n->next->prev = c;
+      delete n;
+    }
+  }
+  insert_free(c);
+  return c;
+}
+
+void* BFCAllocator::allocate(size_t bytes, hipStream_t stream) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!tagged()) stream = nullptr;
+  size_t size = round_up(bytes ? bytes : 1);
+  Chunk* c = find_chunk(size, stream);
+  if (c == nullptr) {
+    clean_streams();
+    c = find_chunk(size, stream);
+  }
+  if (c == nullptr && grow(size)) c = find_chunk(size, stream);
+  if (c == nullptr) {
+    // last resort: hand wholly free regions back to the driver and retry once
+    size_t freed = 0;
+    for (size_t i = 0; i < regions_.size(); ++i) {
+      Region& r = regions_[i];
+      Chunk* f = r.first;
+      if (f && !f->in_use && f->next == nullptr && f->size == r.size && r.base) {
+        erase_free(f);
+        delete f;
+        sub_free(r.base);
+        freed += r.size;
+        st_.bytes_reserved -= (int64_t)r.size;
+        st_.num_regions--;
+        r.base = nullptr;
+        r.first = nullptr;
+        r.size = 0;
+      }
+    }
+    if (freed && grow(size)) c = find_chunk(size, stream);
+    if (c == nullptr) return nullptr;
+  }
+  c->in_use = true;
+  c->stream = stream;
+  in_use_[c->ptr] = c;
+  st_.num_allocs++;
+  st_.bytes_in_use += (int64_t)c->size;
+  st_.peak_bytes_in_use = std::max(st_.peak_bytes_in_use, st_.bytes_in_use);
+  st_.largest_alloc_size = std::max(st_.largest_alloc_size, (int64_t)c->size);
+  return c->ptr;
+}
+
+void BFCAllocator::deallocate(void* p, hipStream_t stream) {
+  if (p == nullptr) return;
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = in_use_.find((char*)p);
+  if (it == in_use_.end()) {
+    fprintf(stderr, "hetu BFC: free of unknown pointer %p\n", p);
+    return;
+  }
+  Chunk* c = it->second;
+  in_use_.erase(it);
+  st_.bytes_in_use -= (int64_t)c->size;
+  if (tagged() && stream != nullptr) c->stream = stream;
+  if (!tagged()) c->stream = nullptr;
+  free_chunk(c);
+}
+
+size_t BFCAllocator::allocation_size(void* p) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = in_use_.find((char*)p);
+  return it == in_use_.end() ? 0 : it->second->size;
+}
+
+AllocatorStats BFCAllocator::stats() {
+  std::lock_guard<std::mutex> g(mu_);
+  return st_;
+}
+
+size_t BFCAllocator::release_free_regions() {
+  std::lock_guard<std::mutex> g(mu_);
+  clean_streams();
+  size_t freed = 0;
+  for (auto& r : regions_) {
+    Chunk* f = r.first;
+    if (r.base && f && !f->in_use && f->next == nullptr && f->size == r.size) {
+      erase_free(f);
+      delete f;
+      sub_free(r.base);
+      freed += r.size;
+      st_.bytes_reserved -= (int64_t)r.size;
+      st_.num_regions--;
+      r.base = nullptr;
+      r.first = nullptr;
+      r.size = 0;
+    }
+  }
+  return freed;
+}
+
+bool BFCAllocator::check_invariants() {
+  std::lock_guard<std::mutex> g(mu_);
+  int64_t used = 0, nfree = 0;
+  for (auto& r : regions_) {
+    if (!r.base) continue;
+    size_t total = 0;
+    char* expect = r.base;
+    for (Chunk* c = r.first; c; c = c->next) {
+      if (c->ptr != expect) return false;
+      if (c->next && c->next->prev != c) return false;
+      if (c->size % kMinAlloc) return false;
+      if (c->in_use) {
+        used += (int64_t)c->size;
+        if (!in_use_.count(c->ptr)) return false;
+      } else {
+        if (!bins_[c->stream].b[bin_of(c->size)].count(c)) return false;
+        ++nfree;
+        // no two adjacent free chunks with compatible streams may remain
+        if (c->next && !c->next->in_use && c->next->stream == c->stream) return false;
+      }
+      expect += c->size;
+      total += c->size;
+    }
+    if (total != r.size) return false;
+  }
+  return used == st_.bytes_in_use && nfree == st_.num_free_chunks;
+}
+
+}  // namespace hetu
+
+// ---------------------------------------------------------------------------
+// C ABI (ctypes) and torch.cuda.memory.CUDAPluggableAllocator entry points
+using hetu::BFCAllocator;
+using hetu::MemKind;
+
+#define HETU_RT_API extern "C" __attribute__((visibility("default")))
+
+HETU_RT_API void* hetu_bfc_create(int kind, int device, int64_t limit_bytes, int64_t first_region) {
+  return new BFCAllocator((MemKind)kind, device, (size_t)limit_bytes, (size_t)first_region);
+}
+HETU_RT_API void hetu_bfc_destroy(void* h) { delete (BFCAllocator*)h; }
+HETU_RT_API void* hetu_bfc_alloc(void* h, int64_t bytes, void* stream) {
+  return ((BFCAllocator*)h)->allocate((size_t)bytes, (hipStream_t)stream);
+}
+HETU_RT_API void hetu_bfc_free(void* h, void* p, void* stream) {
+  ((BFCAllocator*)h)->deallocate(p, (hipStream_t)stream);
+}
+HETU_RT_API int64_t hetu_bfc_size(void* h, void* p) { return (int64_t)((BFCAllocator*)h)->allocation_size(p); }
+HETU_RT_API int64_t hetu_bfc_release(void* h) { return (int64_t)((BFCAllocator*)h)->release_free_regions(); }
+HETU_RT_API int hetu_bfc_check(void* h) { return ((BFCAllocator*)h)->check_invariants() ? 1 : 0; }
+HETU_RT_API void hetu_bfc_stats(void* h, int64_t* out) {
+  hetu::AllocatorStats s = ((BFCAllocator*)h)->stats();
+  out[0] = s.num_allocs;
+  out[1] = s.bytes_in_use;
+  out[2] = s.peak_bytes_in_use;
+  out[3] = s.largest_alloc_size;
+  out[4] = s.bytes_reserved;
+  out[5] = s.bytes_limit;
+  out[6] = s.num_regions;
+  out[7] = s.num_free_chunks;
+}
+
+// One device allocator per GPU for torch's pluggable-allocator hook
+// (HETU_ALLOCATOR=bfc).  Limit: HETU_BFC_LIMIT_GB, default 95% of the device.
+static BFCAllocator* g_dev[64];
+static std::mutex g_dev_mu;
+
+static BFCAllocator* dev_alloc(int device) {
+  if (device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  if (!g_dev[device]) {
+    size_t limit = 0;
+    const char* env = getenv("HETU_BFC_LIMIT_GB");
+    if (env) {
+      limit = (size_t)(atof(env) * (double)(1ull << 30));
+    } else {
+      int cur = 0;
+      hipGetDevice(&cur);
+      hipSetDevice(device);
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess) limit = (size_t)(tot * 0.95);
+      hipSetDevice(cur);
+    }
+    const char* reg = getenv("HETU_BFC_REGION_MB");
+    size_t first = reg ? (size_t)atoll(reg) << 20 : (size_t)1 << 30;
+    g_dev[device] = new BFCAllocator(MemKind::kDevice, device, limit, first);
+  }
+  return g_dev[device];
+}
+
+HETU_RT_API void* hetu_torch_alloc(ssize_t size, int device, hipStream_t stream) {
+  BFCAllocator* a = dev_alloc(device);
+  return a ? a->allocate((size_t)size, stream) : nullptr;
+}
+
+HETU_RT_API void hetu_torch_free(void* ptr, ssize_t size, int device, hipStream_t stream) {
+  (void)size;
+  BFCAllocator* a = dev_alloc(device);
+  if (a) a->deallocate(ptr, stream);
+}
+
+HETU_RT_API void hetu_torch_stats(int device, int64_t* out) {
+  BFCAllocator* a = dev_alloc(device);
+  if (a) hetu_bfc_stats(a, out);
+}

@@ -11,9 +11,16 @@ framework with the capabilities and Python API of Hetu.
 Compute path: torch-ROCm tensors + hand-written HIP kernels for gfx950
 (``csrc/kernels``, loaded from ``hetu_61a7_amd/lib/libhetu_kernels.so``),
 RCCL over xGMI for collectives, a C++ host runtime for the parameter server,
-HET embedding cache and pinned-memory allocator.
+HET embedding cache, and a BFC allocator for HBM and pinned DRAM
+(``memory_pool``; ``HETU_ALLOCATOR=bfc`` makes it the process-wide device allocator).
 """
 from __future__ import annotations
+
+import os as _os
+
+if _os.environ.get('HETU_ALLOCATOR', '') == 'bfc':   # before any device allocation
+    from .memory_pool import enable_torch_bfc as _enable_bfc
+    _enable_bfc()
 
 from .ops import *  # noqa: F401,F403
 from .ops import Executor, HetuConfig, gradients, Variable, placeholder_op

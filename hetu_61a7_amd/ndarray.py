@@ -266,11 +266,15 @@ def numpyasdlarrayhandle(data: np.ndarray) -> NDArray:
 
 
 def pinned_empty(shape, dtype=torch.float32) -> torch.Tensor:
-    """Pinned host buffer (``hipHostMalloc``) used for async staging."""
-    t = torch.empty(tuple(shape), dtype=dtype)
+    """Pinned host buffer used for async staging: carved from the native
+    pinned-DRAM BFC pool (``memory_pool.pinned_pool``, hipHostMalloc regions),
+    or torch's pinned allocator when the pool library is not built."""
     if torch.cuda.is_available():
-        t = t.pin_memory()
-    return t
+        from . import memory_pool
+        if memory_pool.available():
+            return memory_pool.pinned_pool().tensor(tuple(shape), dtype)
+        return torch.empty(tuple(shape), dtype=dtype).pin_memory()
+    return torch.empty(tuple(shape), dtype=dtype)
 
 
 class ND_Sparse_Array(object):

@@ -21,10 +21,8 @@ from .worker import PARAM_DENSE, PARAM_SPARSE, PARAM_CACHE
 
 
 def _pinned(n, dtype=torch.float32):
-    t = torch.empty(n, dtype=dtype)
-    if torch.cuda.is_available():
-        t = t.pin_memory()
-    return t
+    from ..ndarray import pinned_empty
+    return pinned_empty((n,), dtype)
 
 
 class _Staging(object):

@@ -14,7 +14,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   grep -E "PASSED|FAILED|ERROR" gpurun_out/pytest_gpu.log | tail -60; tail -3 gpurun_out/pytest_gpu.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
 fi
-for m in ${BENCHES:-resnet50 bert moe wdl}; do
+for m in ${BENCHES-resnet50 bert moe wdl}; do
   echo "== bench $m"
   extra=""
   [ "$m" = "wdl" ] && extra="${WDL_ARGS:-}"

@@ -1,0 +1,90 @@
+"""Native BFC allocator (csrc/runtime/bfc_allocator.cc) bookkeeping on host
+memory: best fit, split/coalesce, stream-tagged reuse, region growth, limits,
+stats (reference src/memory_pool/BFC_allocator.h semantics)."""
+import random
+
+import pytest
+
+from hetu_61a7_amd import memory_pool as MP
+
+
+def test_split_coalesce_and_stats():
+    a = MP.BFCAllocator(MP.HOST, 0, 0, 4 << 20)
+    p1 = a.alloc(1000)
+    p2 = a.alloc(3000)
+    p3 = a.alloc(256)
+    assert p1 and p2 and p3 and len({p1, p2, p3}) == 3
+    assert a.size_of(p1) == 1024 and a.size_of(p2) == 3072
+    assert p1 % 256 == 0 and p2 == p1 + 1024          # carved from the same region in order
+    s = a.stats()
+    assert s['bytes_in_use'] == 1024 + 3072 + 256 and s['num_regions'] == 1
+    a.free(p2)
+    p4 = a.alloc(2048)                                # best fit re-uses the hole
+    assert p4 == p2
+    a.free(p1)
+    a.free(p4)
+    a.free(p3)
+    assert a.check()
+    s = a.stats()
+    assert s['bytes_in_use'] == 0 and s['num_free_chunks'] == 1   # everything coalesced back
+    assert s['peak_bytes_in_use'] == 1024 + 3072 + 256
+
+
+def test_growth_limit_and_release():
+    a = MP.BFCAllocator(MP.HOST, 0, 16 << 20, 2 << 20)
+    ps = [a.alloc(1 << 20) for _ in range(6)]          # needs a second region (2 MiB + 4 MiB ...)
+    assert all(ps) and a.stats()['num_regions'] >= 2
+    assert a.alloc(64 << 20) is None                   # above the limit
+    for p in ps:
+        a.free(p)
+    assert a.check()
+    assert a.release() > 0 and a.stats()['bytes_reserved'] == 0
+
+
+def test_stream_tagged_reuse():
+    a = MP.BFCAllocator(MP.HOST_TAGGED, 0, 0, 1 << 20)
+    s1, s2 = 0x1000, 0x2000                            # opaque stream tags
+    p = a.alloc(4096, s1)
+    a.free(p, s1)
+    assert a.alloc(4096, s1) == p                      # same stream: immediate reuse
+    a.free(p, s1)
+    q = a.alloc(4096, s2)                              # other stream: not the s1 chunk ...
+    assert q != p
+    big = a.alloc((1 << 20) - 8192, s2)                # ... until the pool must clean s1's chunks
+    assert big is not None
+    a.free(q, s2)
+    a.free(big, s2)
+    assert a.check()
+
+
+def test_random_stress_invariants():
+    rng = random.Random(0)
+    a = MP.BFCAllocator(MP.HOST_TAGGED, 0, 0, 1 << 20)
+    live = []
+    for i in range(3000):
+        if live and rng.random() < 0.45:
+            p, s = live.pop(rng.randrange(len(live)))
+            a.free(p, s)
+        else:
+            s = rng.choice([0, 0x10, 0x20])
+            p = a.alloc(rng.choice([1, 100, 256, 777, 4096, 65536, 300000]), s or None)
+            assert p
+            live.append((p, s or None))
+        if i % 250 == 0:
+            assert a.check()
+    for p, s in live:
+        a.free(p, s)
+    assert a.check() and a.stats()['bytes_in_use'] == 0
+
+
+def test_pool_backed_host_tensor():
+    import torch
+    a = MP.BFCAllocator(MP.HOST, 0, 0, 1 << 20)
+    t = a.tensor((16, 8), torch.float32)
+    t.fill_(3.0)
+    assert float(t.sum()) == 16 * 8 * 3.0
+    assert a.stats()['bytes_in_use'] == 512
+    del t
+    import gc
+    gc.collect()
+    assert a.stats()['bytes_in_use'] == 0

@@ -104,6 +104,281 @@ __global__ void __launch_bounds__(256) dropout_k(const T* __restrict__ x, T* __r
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Vectorised register-resident path (N % 4 == 0, N <= 2048): one wave per row
+// holds the whole row in registers (CPL chunks of 4 per lane), optionally
+// fused with "dropout(x) + residual" in front of the normalisation (BERT /
+// Transformer post-LN blocks: LN(dropout(sublayer) + h)).  Dropout uses the
+// same Philox counters as dropout_k (counter = flat element index / 4), so a
+// standalone dropout with the same seed reproduces the mask.
+template <typename T> struct IO4;
+template <> struct IO4<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
+    float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct IO4<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float (&v)[4]) {
+    uint2 x = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+    v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float (&v)[4]) {
+    uint2 x;
+    x.x = (unsigned)f_to_bf16_bits(v[0]) | ((unsigned)f_to_bf16_bits(v[1]) << 16);
+    x.y = (unsigned)f_to_bf16_bits(v[2]) | ((unsigned)f_to_bf16_bits(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = x;
+  }
+};
+
+__device__ __forceinline__ void drop4(float (&v)[4], uint64_t seed, uint64_t ctr, float keep) {
+  const uint4 r = Philox::gen(seed, ctr);
+  const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
+  const float inv = 1.f / keep;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = Philox::u01(rr[k]) < keep ? v[k] * inv : 0.f;
+}
+
+template <typename T, int CPL>
+__global__ void __launch_bounds__(256) ln_fwd4_k(const T* __restrict__ x, const T* __restrict__ res,
+                                                  const float* __restrict__ g, const float* __restrict__ b,
+                                                  T* __restrict__ y, T* __restrict__ sum_out,
+                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                  int64_t R, int N, float eps, float keep, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int nc = N >> 2;
+  const int64_t base = row * N;
+  float v[CPL][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nc) {
+      IO4<T>::load(x + base + 4 * c, v[i]);
+      if (keep < 1.f) drop4(v[i], seed, (uint64_t)(base >> 2) + c, keep);
+      if (res != nullptr) {
+        float r4[4];
+        IO4<T>::load(res + base + 4 * c, r4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] += r4[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += v[i][k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[i][k] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)N;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    if (lane + 64 * i < nc) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d = v[i][k] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)N + eps);
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nc) {
+      if (sum_out != nullptr) IO4<T>::store(sum_out + base + 4 * c, v[i]);
+      const float4 gg = *reinterpret_cast<const float4*>(g + 4 * c);
+      const float4 bb = *reinterpret_cast<const float4*>(b + 4 * c);
+      float o[4];
+      o[0] = (v[i][0] - mean) * rstd * gg.x + bb.x;
+      o[1] = (v[i][1] - mean) * rstd * gg.y + bb.y;
+      o[2] = (v[i][2] - mean) * rstd * gg.z + bb.z;
+      o[3] = (v[i][3] - mean) * rstd * gg.w + bb.w;
+      IO4<T>::store(y + base + 4 * c, o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Backward: dsum = LN'(dy) per row (wave per row, rows of one block strided
+// over its 4 waves); dx_drop = dropout-mask(dsum) when the forward fused a
+// dropout; dgamma/dbeta accumulate in registers, are folded across the 4
+// waves in LDS and written as one partial row per workgroup (col_reduce2_k
+// finishes them).  LDS: 4 * N floats (dynamic).
+template <typename T, int CPL>
+__global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const T* __restrict__ xs,
+                                                  const float* __restrict__ g, const float* __restrict__ mean,
+                                                  const float* __restrict__ rstd, T* __restrict__ dsum,
+                                                  T* __restrict__ dx_drop, float* __restrict__ pg,
+                                                  float* __restrict__ pb, int64_t R, int N, int rpb, float keep,
+                                                  uint64_t seed) {
+  extern __shared__ float lds[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nc = N >> 2;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
+  float gm[CPL][4], ag[CPL][4], ab[CPL][4];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nc) {
+      const float4 t = *reinterpret_cast<const float4*>(g + 4 * c);
+      gm[i][0] = t.x; gm[i][1] = t.y; gm[i][2] = t.z; gm[i][3] = t.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gm[i][k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { ag[i][k] = 0.f; ab[i][k] = 0.f; }
+  }
+  for (int64_t row = r0 + w; row < r1; row += 4) {
+    const int64_t base = row * N;
+    const float mu = mean[row], rs = rstd[row];
+    float d[CPL][4], xh[CPL][4];
+    float a = 0.f, cc = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
+        IO4<T>::load(dy + base + 4 * c, d[i]);
+        IO4<T>::load(xs + base + 4 * c, xh[i]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[i][k] = (xh[i][k] - mu) * rs;
+          const float dg = d[i][k] * gm[i][k];
+          a += dg;
+          cc += dg * xh[i][k];
+          ag[i][k] += d[i][k] * xh[i][k];
+          ab[i][k] += d[i][k];
+        }
+      }
+    }
+    a = wave_sum(a) / (float)N;
+    cc = wave_sum(cc) / (float)N;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = rs * (d[i][k] * gm[i][k] - a - xh[i][k] * cc);
+        if (dsum != nullptr) IO4<T>::store(dsum + base + 4 * c, o);
+        if (dx_drop != nullptr) {
+          drop4(o, seed, (uint64_t)(base >> 2) + c, keep);
+          IO4<T>::store(dx_drop + base + 4 * c, o);
+        }
+      }
+    }
+  }
+  // fold the 4 waves' partials (dgamma, then dbeta) through LDS
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lds[w * N + 4 * c + k] = pass == 0 ? ag[i][k] : ab[i][k];
+      }
+    }
+    __syncthreads();
+    float* out = (pass == 0 ? pg : pb) + (int64_t)blockIdx.x * N;
+    for (int j = threadIdx.x; j < N; j += 256) out[j] = lds[j] + lds[N + j] + lds[2 * N + j] + lds[3 * N + j];
+    __syncthreads();
+  }
+}
+
+// oa[j] = sum_r pa[r, j], ob[j] = sum_r pb[r, j]: 64 columns x 4 row groups per block
+__global__ void __launch_bounds__(256) col_reduce2_k(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                      float* __restrict__ oa, float* __restrict__ ob, int rows,
+                                                      int N) {
+  __shared__ float sa[4][64], sb[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float a = 0.f, b = 0.f;
+  if (col < N) {
+    float a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f, a3 = 0.f, b3 = 0.f;   // 4 loads in flight
+    int r = grp;
+    for (; r + 12 < rows; r += 16) {
+      a += pa[(int64_t)r * N + col];        b += pb[(int64_t)r * N + col];
+      a1 += pa[(int64_t)(r + 4) * N + col]; b1 += pb[(int64_t)(r + 4) * N + col];
+      a2 += pa[(int64_t)(r + 8) * N + col]; b2 += pb[(int64_t)(r + 8) * N + col];
+      a3 += pa[(int64_t)(r + 12) * N + col]; b3 += pb[(int64_t)(r + 12) * N + col];
+    }
+    for (; r < rows; r += 4) {
+      a += pa[(int64_t)r * N + col];
+      b += pb[(int64_t)r * N + col];
+    }
+    a += a1 + a2 + a3;
+    b += b1 + b2 + b3;
+  }
+  sa[grp][lane] = a;
+  sb[grp][lane] = b;
+  __syncthreads();
+  if (grp == 0 && col < N) {
+    oa[col] = sa[0][lane] + sa[1][lane] + sa[2][lane] + sa[3][lane];
+    ob[col] = sb[0][lane] + sb[1][lane] + sb[2][lane] + sb[3][lane];
+  }
+}
+
+template <typename T, int CPL>
+static void launch_fwd4(const void* x, const void* res, const float* g, const float* b, void* y, void* sum_out,
+                        float* mean, float* rstd, int64_t R, int N, float eps, float keep, uint64_t seed,
+                        hipStream_t st) {
+  hipLaunchKernelGGL((ln_fwd4_k<T, CPL>), dim3((unsigned)((R + 3) / 4)), dim3(256), 0, st, (const T*)x,
+                     (const T*)res, g, b, (T*)y, (T*)sum_out, mean, rstd, R, N, eps, keep, seed);
+}
+
+template <typename T, int CPL>
+static void launch_bwd4(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
+                        void* dsum, void* dxd, float* pg, float* pb, int64_t R, int N, int nblk, int rpb,
+                        float keep, uint64_t seed, hipStream_t st) {
+  hipLaunchKernelGGL((ln_bwd4_k<T, CPL>), dim3((unsigned)nblk), dim3(256), 4 * N * sizeof(float), st,
+                     (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed);
+}
+
+#define HETU_CPL_DISPATCH(CPL_NEEDED, FN, ...)                 \
+  do {                                                         \
+    const int cpl_ = (CPL_NEEDED);                             \
+    if (cpl_ <= 1) FN<1>(__VA_ARGS__);                         \
+    else if (cpl_ <= 2) FN<2>(__VA_ARGS__);                    \
+    else if (cpl_ <= 3) FN<3>(__VA_ARGS__);                    \
+    else if (cpl_ <= 4) FN<4>(__VA_ARGS__);                    \
+    else if (cpl_ <= 6) FN<6>(__VA_ARGS__);                    \
+    else FN<8>(__VA_ARGS__);                                   \
+  } while (0)
+
+template <int CPL> static void fwd4_bf16(const void* x, const void* res, const float* g, const float* b, void* y,
+                                         void* so, float* m, float* r, int64_t R, int N, float eps, float keep,
+                                         uint64_t seed, hipStream_t st) {
+  launch_fwd4<bf16, CPL>(x, res, g, b, y, so, m, r, R, N, eps, keep, seed, st);
+}
+template <int CPL> static void fwd4_f32(const void* x, const void* res, const float* g, const float* b, void* y,
+                                        void* so, float* m, float* r, int64_t R, int N, float eps, float keep,
+                                        uint64_t seed, hipStream_t st) {
+  launch_fwd4<float, CPL>(x, res, g, b, y, so, m, r, R, N, eps, keep, seed, st);
+}
+template <int CPL> static void bwd4_bf16(const void* dy, const void* xs, const float* g, const float* m,
+                                         const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
+                                         int N, int nblk, int rpb, float keep, uint64_t seed, hipStream_t st) {
+  launch_bwd4<bf16, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, st);
+}
+template <int CPL> static void bwd4_f32(const void* dy, const void* xs, const float* g, const float* m,
+                                        const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
+                                        int N, int nblk, int rpb, float keep, uint64_t seed, hipStream_t st) {
+  launch_bwd4<float, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, st);
+}
+
 }  // namespace hetu
 
 using namespace hetu;
@@ -127,7 +402,7 @@ HETU_API int hetu_layernorm_bwd(const void* dy, const void* x, const float* g, c
   float* wb = ws + (int64_t)nwaves * N;
   if (is_bf16) hipLaunchKernelGGL(ln_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, g, mean, rstd, (bf16*)dx, wg, wb, R, N, nwaves);
   else hipLaunchKernelGGL(ln_bwd_k<float>, grid, dim3(256), 0, st, (const float*)dy, (const float*)x, g, mean, rstd, (float*)dx, wg, wb, R, N, nwaves);
-  hipLaunchKernelGGL(col_sum2_k, dim3((N + 255) / 256), dim3(256), 0, st, wg, wb, dg, db, nwaves, N);
+  hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, wg, wb, dg, db, nwaves, N);
   HETU_LAUNCH_CHECK();
   return 0;
 }
@@ -137,6 +412,38 @@ HETU_API int hetu_dropout(const void* x, void* y, int64_t n, float keep, int64_t
   int grid = stream_grid((n + 3) / 4, 256, 1);
   if (is_bf16) hipLaunchKernelGGL(dropout_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n, keep, (uint64_t)seed);
   else hipLaunchKernelGGL(dropout_k<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, n, keep, (uint64_t)seed);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+// Fused [dropout(x) + residual ->] LayerNorm forward.  res / sum_out may be null;
+// keep >= 1 disables dropout.  Requires N % 4 == 0 and N <= 2048 (returns
+// hipErrorInvalidValue otherwise -- the caller falls back to hetu_layernorm_fwd).
+HETU_API int hetu_ln_fused_fwd(const void* x, const void* res, const float* g, const float* b, void* y,
+                               void* sum_out, float* mean, float* rstd, int64_t R, int N, float eps, float keep,
+                               int64_t seed, int is_bf16, hipStream_t st) {
+  if ((N & 3) || N > 2048 || R <= 0) return (int)hipErrorInvalidValue;
+  const int cpl = (N / 4 + 63) / 64;
+  if (is_bf16) HETU_CPL_DISPATCH(cpl, fwd4_bf16, x, res, g, b, y, sum_out, mean, rstd, R, N, eps, keep, (uint64_t)seed, st);
+  else HETU_CPL_DISPATCH(cpl, fwd4_f32, x, res, g, b, y, sum_out, mean, rstd, R, N, eps, keep, (uint64_t)seed, st);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward of the fused forward.  xs = the normalised input (x + res after
+// dropout, or x).  dsum (grad of xs / of the residual) and dx_drop (grad of x
+// through the dropout) may each be null.  ws: 2 * nblk * N floats.
+HETU_API int hetu_ln_fused_bwd(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
+                               void* dsum, void* dx_drop, float* dg, float* db, float* ws, int64_t R, int N,
+                               int nblk, float keep, int64_t seed, int is_bf16, hipStream_t st) {
+  if ((N & 3) || N > 2048 || R <= 0 || nblk <= 0) return (int)hipErrorInvalidValue;
+  const int cpl = (N / 4 + 63) / 64;
+  const int rpb = (int)((R + nblk - 1) / nblk);
+  float* pg = ws;
+  float* pb = ws + (int64_t)nblk * N;
+  if (is_bf16) HETU_CPL_DISPATCH(cpl, bwd4_bf16, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, st);
+  else HETU_CPL_DISPATCH(cpl, bwd4_f32, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, st);
+  hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, pg, pb, dg, db, nblk, N);
   HETU_LAUNCH_CHECK();
   return 0;
 }

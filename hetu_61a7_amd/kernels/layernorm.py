@@ -12,6 +12,9 @@ from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I
 def layer_norm(x, gamma, beta, eps):
     N = x.shape[-1]
     R = x.numel() // N
+    if _fused_ok(x):
+        y, _, mean, rstd = layer_norm_fused(x, None, gamma, beta, eps)
+        return y, mean, rstd
     if native(x) and supported_float(x):
         xc = x.contiguous()
         y = torch.empty_like(xc)
@@ -33,6 +36,9 @@ def layer_norm(x, gamma, beta, eps):
 def layer_norm_backward(dy, x, gamma, mean, rstd):
     N = x.shape[-1]
     R = x.numel() // N
+    if _fused_ok(x) and dy.dtype == x.dtype:
+        ds, _, dg, db = layer_norm_fused_backward(dy, x, gamma, mean, rstd, need_dx=False)
+        return ds, dg, db
     if native(x) and supported_float(x) and dy.dtype == x.dtype:
         xc, dyc = x.contiguous(), dy.contiguous()
         dx = torch.empty_like(xc)
@@ -53,3 +59,69 @@ def layer_norm_backward(dy, x, gamma, mean, rstd):
     gg = g * gamma.float()
     dx = rstd[:, None] * (gg - gg.mean(1, keepdim=True) - xhat * (gg * xhat).mean(1, keepdim=True))
     return dx.reshape(x.shape).to(x.dtype), dg, db
+
+
+def _fused_ok(x):
+    N = x.shape[-1]
+    return native(x) and supported_float(x) and N % 4 == 0 and N <= 2048
+
+
+def layer_norm_fused(x, residual, gamma, beta, eps, keep=1.0, seed=0):
+    """y = LN(dropout(x; keep, seed) + residual) in one pass (``residual`` may be
+    None, ``keep`` 1 disables dropout).  Returns (y, s, mean, rstd) where ``s``
+    is the normalised input (needed by the backward; ``x`` itself when there is
+    neither residual nor dropout)."""
+    N = x.shape[-1]
+    R = x.numel() // N
+    plain = residual is None and keep >= 1.0
+    if _fused_ok(x) and (residual is None or residual.dtype == x.dtype):
+        xc = x.contiguous()
+        rc = residual.contiguous() if residual is not None else None
+        y = torch.empty_like(xc)
+        s = xc if plain else torch.empty_like(xc)
+        mean = torch.empty(R, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        f = fn('hetu_ln_fused_fwd', [P, P, P, P, P, P, P, P, I64, I32, F32, F32, I64, I32, P])
+        check(f(xc.data_ptr(), rc.data_ptr() if rc is not None else None, gamma.float().contiguous().data_ptr(),
+                beta.float().contiguous().data_ptr(), y.data_ptr(), None if plain else s.data_ptr(),
+                mean.data_ptr(), rstd.data_ptr(), R, N, float(eps), float(keep), int(seed), is_bf16(x),
+                stream_ptr()), 'ln_fused_fwd')
+        return y, s, mean, rstd
+    from . import dropout as KD
+    s = x if keep >= 1.0 else KD.dropout(x, keep, seed)
+    if residual is not None:
+        s = (s.float() + residual.float()).to(x.dtype)
+    y, mean, rstd = layer_norm(s, gamma, beta, eps)
+    return y, s, mean, rstd
+
+
+def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_ds=True, need_dx=True):
+    """Backward of ``layer_norm_fused``: (ds, dx, dgamma, dbeta) with ds the grad
+    of the normalised input (= grad of the residual) and dx = dropout-mask(ds)
+    the grad of ``x`` (None when not requested)."""
+    N = s.shape[-1]
+    R = s.numel() // N
+    if _fused_ok(s) and dy.dtype == s.dtype:
+        dyc, sc = dy.contiguous(), s.contiguous()
+        ds = torch.empty_like(sc) if need_ds else None
+        dx = torch.empty_like(sc) if (need_dx and keep < 1.0) else None
+        if need_dx and keep >= 1.0 and not need_ds:
+            ds = torch.empty_like(sc)
+        nblk = max(1, min(512, (R + 7) // 8))
+        ws = torch.empty(2 * nblk * N, dtype=torch.float32, device=s.device)
+        dg = torch.empty(N, dtype=torch.float32, device=s.device)
+        db = torch.empty(N, dtype=torch.float32, device=s.device)
+        f = fn('hetu_ln_fused_bwd', [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, P])
+        check(f(dyc.data_ptr(), sc.data_ptr(), gamma.float().contiguous().data_ptr(), mean.data_ptr(),
+                rstd.data_ptr(), ds.data_ptr() if ds is not None else None,
+                dx.data_ptr() if dx is not None else None, dg.data_ptr(), db.data_ptr(), ws.data_ptr(), R, N, nblk,
+                float(keep), int(seed), is_bf16(s), stream_ptr()), 'ln_fused_bwd')
+        if need_dx and keep >= 1.0:
+            dx = ds
+        return ds, dx, dg, db
+    ds, dg, db = layer_norm_backward(dy, s, gamma, mean, rstd)
+    dx = None
+    if need_dx:
+        from . import dropout as KD
+        dx = ds if keep >= 1.0 else KD.dropout(ds, keep, seed)
+    return ds, dx, dg, db

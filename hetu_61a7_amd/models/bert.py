@@ -87,6 +87,12 @@ def _ln(x, h, name):
     return ht.layer_normalization_op(x, _ones(name + '_scale', h), _zeros(name + '_bias', h), eps=1e-12)
 
 
+def _drop_add_ln(x, res, h, name, p):
+    """LN(dropout(x) + res) as one fused kernel each way."""
+    return ht.dropout_add_layernorm_op(x, res, _ones(name + '_scale', h), _zeros(name + '_bias', h),
+                                       keep_prob=1.0 - p, eps=1e-12)
+
+
 def _dropout(x, p):
     return ht.dropout_op(x, 1.0 - p) if p > 0 else x
 
@@ -110,10 +116,10 @@ class BertLayer(object):
         ctxl = ht.attention_op(q, k, v, mask, dropout=c.attention_probs_dropout_prob)
         ctxl = ht.array_reshape_op(ht.transpose_op(ctxl, (0, 2, 1, 3)), (B * S, H))
         a = _dense(ctxl, H, H, p + 'attention_output', c)
-        a = _ln(_dropout(a, c.hidden_dropout_prob) + h2d, H, p + 'attention_LayerNorm')
+        a = _drop_add_ln(a, h2d, H, p + 'attention_LayerNorm', c.hidden_dropout_prob)
         f = _dense(a, H, c.intermediate_size, p + 'intermediate', c, act=c.hidden_act)
         f = _dense(f, c.intermediate_size, H, p + 'output', c)
-        return _ln(_dropout(f, c.hidden_dropout_prob) + a, H, p + 'output_LayerNorm')
+        return _drop_add_ln(f, a, H, p + 'output_LayerNorm', c.hidden_dropout_prob)
 
 
 class BertModel(object):

@@ -28,7 +28,7 @@ from .nn import (conv2d_op, conv2d_gradient_of_data_op, conv2d_gradient_of_filte
                  max_pool2d_gradient_op, batch_normalization_op, batch_normalization_gradient_op,
                  batch_normalization_gradient_of_data_op, batch_normalization_gradient_of_scale_op,
                  batch_normalization_gradient_of_bias_op, fused_bn_relu_op, fused_bn_add_relu_op,
-                 layer_normalization_op, layer_normalization_gradient_op,
+                 layer_normalization_op, layer_normalization_gradient_op, dropout_add_layernorm_op,
                  layer_normalization_gradient_of_data_op, layer_normalization_gradient_of_scale_op,
                  layer_normalization_gradient_of_bias_op, instance_normalization2d_op,
                  instance_normalization2d_gradient_op, dropout_op, dropout_gradient_op,

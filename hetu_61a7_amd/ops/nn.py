@@ -456,6 +456,68 @@ def layer_normalization_gradient_of_bias_op(ln_gradient, in_bias, ctx=None):
     return _sel(ln_gradient, 2, 'Layer_Normalization_Gradient_of_BiasOp', ctx)
 
 
+class DropoutAddLayerNormOp(Op):
+    """y = LayerNorm(dropout(x) + residual) as ONE kernel (MI355X fusion of the
+    post-LN transformer block tail, reference hetu_bert.py / hetu_transformer.py
+    ``layer_norm(dropout(h) + input)`` = 3 ops, 3 kernels each way).  The
+    backward regenerates the dropout mask from the seed (no mask tensor) and
+    emits dx, dresidual, dscale, dbias from one row pass + one column reduce."""
+
+    def __init__(self, x, residual, scale, bias, keep_prob=1.0, eps=1e-12, ctx=None):
+        ins = [x] + ([residual] if residual is not None else []) + [scale, bias]
+        super().__init__(DropoutAddLayerNormOp, ins, ctx)
+        self.has_res = residual is not None
+        self.keep_prob, self.eps = float(keep_prob), eps
+        self.inference = False
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        x = input_vals[0]
+        res = input_vals[1] if self.has_res else None
+        g, b = input_vals[-2], input_vals[-1]
+        keep = 1.0 if self.inference else self.keep_prob
+        seed = _next_seed() if keep < 1.0 else 0
+        if res is not None and res.dtype != x.dtype:
+            res = res.to(x.dtype)
+        y, sm, mean, rstd = KLN.layer_norm_fused(x, res, g, b, self.eps, keep, seed)
+        return AuxResult(y, (sm, mean, rstd, keep, seed))
+
+    def gradient(self, output_grad):
+        gn = DropoutAddLayerNormGradientOp(output_grad, self, ctx=self.raw_ctx)
+        grads = [_sel(gn, 0, 'DropoutAddLayerNorm_Gradient_of_DataOp', self.raw_ctx)]
+        if self.has_res:
+            grads.append(_sel(gn, 1, 'DropoutAddLayerNorm_Gradient_of_ResidualOp', self.raw_ctx))
+        grads += [_sel(gn, 2, 'DropoutAddLayerNorm_Gradient_of_ScaleOp', self.raw_ctx),
+                  _sel(gn, 3, 'DropoutAddLayerNorm_Gradient_of_BiasOp', self.raw_ctx)]
+        return grads
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+class DropoutAddLayerNormGradientOp(Op):
+    aux_inputs = (1,)
+
+    def __init__(self, out_gradient, forward_node, ctx=None):
+        super().__init__(DropoutAddLayerNormGradientOp, [out_gradient, forward_node, forward_node.inputs[-2]], ctx)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        dy, (sm, mean, rstd, keep, seed), g = input_vals
+        if dy.dtype != sm.dtype:
+            dy = dy.to(sm.dtype)
+        ds, dx, dg, db = KLN.layer_norm_fused_backward(dy, sm, g, mean, rstd, keep, seed)
+        return (dx, ds, dg, db)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return None
+
+
+def dropout_add_layernorm_op(x, residual, ln_scale, ln_bias, keep_prob=1.0, eps=1e-12, ctx=None):
+    return DropoutAddLayerNormOp(x, residual, ln_scale, ln_bias, keep_prob, eps, ctx=ctx)
+
+
 class Instance_Normalization2dOp(Op):
     def __init__(self, x, eps=1e-7, ctx=None):
         super().__init__(Instance_Normalization2dOp, [x], ctx)

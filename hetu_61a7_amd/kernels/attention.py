@@ -1,0 +1,99 @@
+"""Fused multi-head attention over a packed QKV projection (``attention.hip``).
+
+``qkv`` is the [B*S, 3H] output of the QKV linear layer (head h of Q/K/V at
+columns h*D, H + h*D, 2H + h*D); the context comes back as [B*S, H] and the
+gradient as one packed [B*S, 3H] tensor -- no head transposes, slices or
+concatenations around the kernel.  ``mask`` is an additive key mask [B, S].
+Dropout on the probabilities uses Philox(seed, flat index of P / 4), so the
+backward regenerates it.  GPU fast path: bf16, head dim 64, S % 32 == 0,
+S <= 128 (S <= 256 forward-only); elsewhere a torch reference with the same
+semantics (the CPU backend and the numerics oracle).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import fn, native, stream_ptr, check, P, I64, I32, F32
+
+
+def fused_ok(qkv, S, D, need_bwd=True):
+    return (native(qkv) and qkv.dtype == torch.bfloat16 and D == 64 and S % 32 == 0 and 0 < S <= (128 if need_bwd else 256)
+            and qkv.is_contiguous())
+
+
+def _heads(qkv, B, S, NH, D):
+    H = NH * D
+    x = qkv.reshape(B, S, 3, NH, D)
+    return x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+
+
+def _ref_probs(qkv, mask, B, S, NH, D, scale):
+    q, k, v = _heads(qkv.float(), B, S, NH, D)
+    s = q @ k.transpose(-1, -2) * scale
+    if mask is not None:
+        s = s + mask.float().reshape(B, 1, 1, S)
+    return torch.softmax(s, -1), v
+
+
+def _ref_dropmask(shape, keep, seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed) & 0x7FFFFFFF)
+    return (torch.rand(shape, generator=g, device=device) < keep).float() / keep
+
+
+def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
+    """-> (out [B*S, H], lse [B*NH*S] fp32 or probs (reference path))."""
+    H = qkv.shape[1] // 3
+    D = H // NH
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if fused_ok(qkv, S, D, need_bwd=False):
+        out = torch.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
+        m = mask.float().contiguous() if mask is not None else None
+        f = fn('hetu_attn_fwd', [P, P, P, I64, I64, I64, P, P, I64, P, I32, I32, I32, F32, F32, I64, P])
+        base = qkv.data_ptr()
+        es = qkv.element_size()
+        check(f(base, base + H * es, base + 2 * H * es, 3 * H, 3 * H, 3 * H, m.data_ptr() if m is not None else None,
+                out.data_ptr(), H, lse.data_ptr(), B, NH, S, float(scale), float(keep), int(seed), stream_ptr()),
+              'attn_fwd')
+        return out, lse
+    p, v = _ref_probs(qkv, mask, B, S, NH, D, scale)
+    pd = p * _ref_dropmask(p.shape, keep, seed, p.device) if keep < 1.0 else p
+    o = (pd @ v).transpose(1, 2).reshape(B * S, H)
+    return o.to(qkv.dtype), p
+
+
+def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale=None):
+    """-> dqkv [B*S, 3H] (same dtype as qkv)."""
+    H = qkv.shape[1] // 3
+    D = H // NH
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if fused_ok(qkv, S, D) and saved.dim() == 1:
+        dout = dout.to(qkv.dtype).contiguous()
+        dqkv = torch.empty_like(qkv)
+        m = mask.float().contiguous() if mask is not None else None
+        f = fn('hetu_attn_bwd', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
+                                 I32, I32, I32, F32, F32, I64, P])
+        es = qkv.element_size()
+        b, g = qkv.data_ptr(), dqkv.data_ptr()
+        check(f(b, b + H * es, b + 2 * H * es, 3 * H, 3 * H, 3 * H, m.data_ptr() if m is not None else None,
+                out.data_ptr(), H, saved.data_ptr(), dout.data_ptr(), H, g, g + H * es, g + 2 * H * es,
+                3 * H, 3 * H, 3 * H, B, NH, S, float(scale), float(keep), int(seed), stream_ptr()), 'attn_bwd')
+        return dqkv
+    if saved.dim() == 1:    # fused forward (S <= 256) but no fused backward: recompute probs
+        saved, _ = _ref_probs(qkv, mask, B, S, NH, D, scale)
+    p = saved
+    q, k, v = _heads(qkv.float(), B, S, NH, D)
+    do = dout.float().reshape(B, S, NH, D).transpose(1, 2)
+    dm = _ref_dropmask(p.shape, keep, seed, p.device) if keep < 1.0 else None
+    pd = p * dm if dm is not None else p
+    dv = pd.transpose(-1, -2) @ do
+    dpd = do @ v.transpose(-1, -2)
+    dp = dpd * dm if dm is not None else dpd
+    ds = p * (dp - (dp * p).sum(-1, keepdim=True)) * scale
+    dq = ds @ k
+    dk = ds.transpose(-1, -2) @ q
+    pack = torch.stack([dq, dk, dv], 2)               # [B, NH, 3, S, D]
+    return pack.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H).to(qkv.dtype)

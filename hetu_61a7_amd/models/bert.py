@@ -39,8 +39,9 @@ class BertConfig(object):
     def __init__(self, vocab_size=30522, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
                  intermediate_size=3072, hidden_act='gelu', hidden_dropout_prob=0.1,
                  attention_probs_dropout_prob=0.1, max_position_embeddings=512, type_vocab_size=2,
-                 initializer_range=0.02, batch_size=64, seq_len=128):
+                 initializer_range=0.02, batch_size=64, seq_len=128, fused_attention=True):
         self.vocab_size = vocab_size
+        self.fused_attention = fused_attention   # packed-QKV HIP attention (else op-by-op graph)
         self.hidden_size = hidden_size
         self.num_hidden_layers = num_hidden_layers
         self.num_attention_heads = num_attention_heads
@@ -107,6 +108,15 @@ class BertLayer(object):
         nh, hd = c.num_attention_heads, H // c.num_attention_heads
         p = 'layer%d_' % self.idx
         qkv = _dense(h2d, H, 3 * H, p + 'attention_qkv', c)                  # [B*S, 3H]
+        if c.fused_attention:
+            # one HIP kernel each way straight off the packed projection
+            ctxl = ht.packed_attention_op(qkv, mask, B, S, nh, dropout=c.attention_probs_dropout_prob)
+            a = _dense(ctxl, H, H, p + 'attention_output', c)
+            a = _drop_add_ln(a, h2d, H, p + 'attention_LayerNorm', c.hidden_dropout_prob)
+            f = _dense(a, H, c.intermediate_size, p + 'intermediate', c, act=c.hidden_act)
+            f = _dense(f, c.intermediate_size, H, p + 'output', c)
+            return _drop_add_ln(f, a, H, p + 'output_LayerNorm', c.hidden_dropout_prob)
+        mask = ht.array_reshape_op(mask, (B, 1, 1, S))
         qkv = ht.array_reshape_op(qkv, (B, S, 3, nh, hd))
         qkv = ht.transpose_op(qkv, (2, 0, 3, 1, 4))                           # [3, B, nh, S, hd]
         q = ht.slice_op(qkv, (0, 0, 0, 0, 0), (1, B, nh, S, hd))
@@ -149,10 +159,10 @@ class BertModel(object):
             h = _dropout(_ln(e, H, 'embeddings_LayerNorm'), c.hidden_dropout_prob)
         for i, layer in enumerate(self.layers):
             with _stage_ctx(pl, i + 1):
-                # extended additive mask [B, 1, 1, S]: 0 keep, -10000 masked (built on
+                # additive key mask [B, S]: 0 keep, -10000 masked (built on
                 # every stage from the fed mask, so it never crosses a stage boundary)
                 if i == 0 or pl is not None and pl(i + 1) != pl(i):
-                    m = ht.array_reshape_op(attention_mask, (B, 1, 1, S))
+                    m = ht.array_reshape_op(attention_mask, (B, S))
                     m = ht.mul_byconst_op(ht.addbyconst_op(m, -1.0), 10000.0)
                 h = layer(h, m)
         with _stage_ctx(pl, len(self.layers) + 1):

@@ -108,3 +108,64 @@ class AttentionGradientOp(Op):
 
 def attention_op(q, k, v, mask=None, dropout=0.0, causal=False, scale=None, ctx=None):
     return AttentionOp(q, k, v, mask, dropout, causal, scale, ctx=ctx)
+
+
+# ---------------------------------------------------------------------------
+# Packed-QKV fused attention (MI355X path for the BERT / Transformer encoder):
+# one HIP kernel forward, one backward, reading Q/K/V out of the QKV projection
+# and producing the gradient as one packed tensor.
+class PackedAttentionOp(Op):
+    """out [B*S, H] = MHA(qkv [B*S, 3H]); mask: additive key mask [B, S] (or None)."""
+
+    def __init__(self, qkv, mask, batch, seq_len, num_heads, dropout=0.0, scale=None, ctx=None):
+        super().__init__(PackedAttentionOp, [qkv] + ([mask] if mask is not None else []), ctx)
+        self.has_mask = mask is not None
+        self.B, self.S, self.NH = int(batch), int(seq_len), int(num_heads)
+        self.keep_prob = 1.0 - float(dropout)
+        self.scale = scale
+        self.seed = 0
+        self.inference = False
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels import attention as KA
+        qkv = input_vals[0]
+        mask = input_vals[1].reshape(self.B, self.S) if self.has_mask else None
+        keep = 1.0 if self.inference else self.keep_prob
+        seed = 0
+        if keep < 1.0:
+            self.seed += 1
+            seed = (self.id << 32) + self.seed
+        out, saved = KA.attention_fwd(qkv.contiguous(), mask, self.B, self.S, self.NH, keep, seed, self.scale)
+        return AuxResult(out, (saved, keep, seed))
+
+    def gradient(self, output_grad):
+        g = PackedAttentionGradientOp(output_grad, self, ctx=self.raw_ctx)
+        return [g] + ([None] if self.has_mask else [])
+
+    def infer_shape(self, input_shapes):
+        return (input_shapes[0][0], input_shapes[0][1] // 3)
+
+
+class PackedAttentionGradientOp(Op):
+    value_and_aux_inputs = (1,)
+
+    def __init__(self, dout, fwd, ctx=None):
+        super().__init__(PackedAttentionGradientOp, [dout, fwd] + fwd.inputs, ctx)
+        self.fwd = fwd
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels import attention as KA
+        f = self.fwd
+        dout, (out, (saved, keep, seed)), qkv = input_vals[:3]
+        mask = input_vals[3].reshape(f.B, f.S) if f.has_mask else None
+        return KA.attention_bwd(dout, qkv.contiguous(), out, saved, mask, f.B, f.S, f.NH, keep, seed, f.scale)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[2]
+
+
+def packed_attention_op(qkv, mask, batch, seq_len, num_heads, dropout=0.0, scale=None, ctx=None):
+    return PackedAttentionOp(qkv, mask, batch, seq_len, num_heads, dropout, scale, ctx=ctx)

@@ -43,3 +43,61 @@ def test_tiny_bert_pretraining_learns():
     losses = [float(ex.run('train', feed_dict=fd, convert_to_numpy_ret_vals=True)[0]) for _ in range(15)]
     assert np.isfinite(losses).all()
     assert losses[-1] < losses[0] * 0.8, losses
+
+
+def packed_attention_check(device, dtype, B=2, S=32, NH=2, D=64, keep=1.0, tol=1e-4, seed=9):
+    """Packed-QKV attention fwd/bwd vs torch autograd (fp32 reference)."""
+    from hetu_61a7_amd.kernels import attention as KA
+    rng = np.random.RandomState(B * S + NH)
+    H = NH * D
+    qkv = torch.tensor(rng.randn(B * S, 3 * H).astype(np.float32) * 0.5)
+    mask = torch.zeros(B, S)
+    mask[-1, -5:] = -10000.0
+    dout = torch.tensor(rng.randn(B * S, H).astype(np.float32))
+    out, saved = KA.attention_fwd(qkv.to(device, dtype), mask.to(device), B, S, NH, keep, seed)
+    # reference with the kernel's own dropout mask (flat P index -> Philox/generator bits)
+    t = qkv.clone().requires_grad_(True)
+    x = t.reshape(B, S, 3, NH, D)
+    q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    p = torch.softmax(q @ k.transpose(-1, -2) / np.sqrt(D) + mask.reshape(B, 1, 1, S), -1)
+    if keep < 1.0:
+        from hetu_61a7_amd.kernels import dropout as KD
+        if device == 'cpu':
+            dm = KA._ref_dropmask(p.shape, keep, seed, 'cpu')
+        else:   # kernel uses the standalone Philox dropout's counters over the flat P tensor
+            dm = KD.dropout(torch.ones(p.shape, device=device), keep, seed).float().cpu()
+        p = p * dm
+    o = (p @ v).transpose(1, 2).reshape(B * S, H)
+    o.backward(dout)
+    np.testing.assert_allclose(out.float().cpu().numpy(), o.detach().numpy(), rtol=tol, atol=tol)
+    dqkv = KA.attention_bwd(dout.to(device, dtype), qkv.to(device, dtype), out, saved, mask.to(device), B, S, NH,
+                            keep, seed)
+    np.testing.assert_allclose(dqkv.float().cpu().numpy(), t.grad.numpy(), rtol=10 * tol, atol=10 * tol)
+
+
+def test_packed_attention_reference_cpu():
+    packed_attention_check('cpu', torch.float32)
+    packed_attention_check('cpu', torch.float32, B=1, S=8, NH=3, D=4, keep=0.7)
+
+
+def test_bert_fused_vs_unfused_attention_graph():
+    from hetu_61a7_amd.models.bert import BertConfig, bert_pretrain_graph, synthetic_bert_batch
+    from hetu_61a7_amd.ops import node as _node
+    out, init = [], None
+    for fused in (False, True):
+        _node.G_NODE_ID = 0
+        cfg = BertConfig(vocab_size=1200, hidden_size=32, num_hidden_layers=2, num_attention_heads=4,
+                         intermediate_size=64, batch_size=4, seq_len=16, max_position_embeddings=16,
+                         hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0, fused_attention=fused)
+        feeds, loss, train = bert_pretrain_graph(cfg, lr=3e-3)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.cpu(0), seed=2)
+        pm = {n.name: t for n, t in ex.config.placeholder_to_arr_map.items() if n.trainable}
+        if init is None:
+            init = {k: v.detach().clone() for k, v in pm.items()}
+        else:
+            for k, v in pm.items():
+                v.copy_(init[k])
+        fd = {feeds[k]: v for k, v in synthetic_bert_batch(cfg, seed=1).items()}
+        out.append([float(np.asarray(ex.run('train', feed_dict=fd, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0])
+                    for _ in range(4)])
+    np.testing.assert_allclose(out[0], out[1], rtol=1e-4, atol=1e-5)

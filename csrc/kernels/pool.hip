@@ -259,6 +259,48 @@ __global__ void __launch_bounds__(256) reduce_mid_k(const T* __restrict__ x, flo
   }
 }
 
+// vectorised variant (C % VEC == 0, 16-byte aligned rows): each lane sums VEC
+// adjacent columns with 16-byte loads, so a wave streams 1 KiB (bf16) per row
+template <typename T>
+__global__ void __launch_bounds__(256) reduce_mid_vec_k(const T* __restrict__ x, float* __restrict__ part,
+                                                         int64_t B, int64_t R, int64_t C,
+                                                         int64_t rows_per_chunk) {
+  constexpr int VEC = Vec<T>::N;
+  __shared__ float sh[4][64 * VEC];
+  const int lane = threadIdx.x & 63, rsub = threadIdx.x >> 6;
+  const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * VEC;
+  const int64_t b = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.z * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > R) r1 = R;
+  float acc[VEC], acc2[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) { acc[k] = 0.f; acc2[k] = 0.f; }
+  if (c < C) {
+    int64_t r = r0 + rsub;
+    for (; r + 4 < r1; r += 8) {          // two rows in flight per lane
+      float v[VEC], w[VEC];
+      load_vec<T>(x + (b * R + r) * C + c, v);
+      load_vec<T>(x + (b * R + r + 4) * C + c, w);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) { acc[k] += v[k]; acc2[k] += w[k]; }
+    }
+    for (; r < r1; r += 4) {
+      float v[VEC];
+      load_vec<T>(x + (b * R + r) * C + c, v);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] += v[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) sh[rsub][lane * VEC + k] = acc[k] + acc2[k];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 64 * VEC; j += 256) {
+    const int64_t cc = (int64_t)blockIdx.x * 64 * VEC + j;
+    if (cc < C) part[((int64_t)blockIdx.z * B + b) * C + cc] = sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j];
+  }
+}
+
 template <typename TO>
 __global__ void reduce_mid_final_k(const float* __restrict__ part, TO* __restrict__ y, int64_t BC,
                                    int chunks, float scale) {
@@ -362,8 +404,13 @@ HETU_API int hetu_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int
 }
 
 // workspace: chunks * B * C floats; returns needed floats when ws == null
+static int64_t reduce_mid_cols_per_tile(int64_t C, int x_bf16) {
+  const int vec = x_bf16 ? 8 : 4;
+  return (C % vec == 0) ? 64 * vec : 64;
+}
+
 HETU_API int64_t hetu_reduce_mid_ws(int64_t B, int64_t R, int64_t C) {
-  int64_t ctiles = (C + 63) / 64;
+  int64_t ctiles = (C + 511) / 512;   // widest tile (bf16 vector path) -> most chunks
   int64_t blocks = ctiles * B;
   int64_t chunks = blocks >= 1024 ? 1 : (1024 + blocks - 1) / blocks;
   int64_t maxc = (R + 63) / 64;
@@ -374,16 +421,27 @@ HETU_API int64_t hetu_reduce_mid_ws(int64_t B, int64_t R, int64_t C) {
 
 HETU_API int hetu_reduce_mid(const void* x, void* y, int64_t B, int64_t R, int64_t C, float scale,
                              int x_bf16, int y_bf16, float* ws, hipStream_t st) {
-  int64_t ctiles = (C + 63) / 64;
+  const int64_t cpt = reduce_mid_cols_per_tile(C, x_bf16);
+  const bool vec = cpt > 64 && ((uintptr_t)x % 16) == 0;
+  int64_t ctiles = (C + (vec ? cpt : 64) - 1) / (vec ? cpt : 64);
   int64_t blocks = ctiles * B;
   int64_t chunks = blocks >= 1024 ? 1 : (1024 + blocks - 1) / blocks;
   int64_t maxc = (R + 63) / 64;
   if (chunks > maxc) chunks = maxc;
   if (chunks < 1) chunks = 1;
+  // never more chunks than the workspace sized by hetu_reduce_mid_ws holds
+  const int64_t ws_chunks = hetu_reduce_mid_ws(B, R, C) / (B * C);
+  if (chunks > ws_chunks) chunks = ws_chunks;
   int64_t rpc = (R + chunks - 1) / chunks;
   dim3 grid((unsigned)ctiles, (unsigned)B, (unsigned)chunks);
-  if (x_bf16) hipLaunchKernelGGL(reduce_mid_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ws, B, R, C, rpc);
-  else hipLaunchKernelGGL(reduce_mid_k<float>, grid, dim3(256), 0, st, (const float*)x, ws, B, R, C, rpc);
+  if (vec) {
+    if (x_bf16) hipLaunchKernelGGL(reduce_mid_vec_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ws, B, R, C, rpc);
+    else hipLaunchKernelGGL(reduce_mid_vec_k<float>, grid, dim3(256), 0, st, (const float*)x, ws, B, R, C, rpc);
+  } else if (x_bf16) {
+    hipLaunchKernelGGL(reduce_mid_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ws, B, R, C, rpc);
+  } else {
+    hipLaunchKernelGGL(reduce_mid_k<float>, grid, dim3(256), 0, st, (const float*)x, ws, B, R, C, rpc);
+  }
   int g2 = stream_grid(B * C, 256, 1);
   if (y_bf16) hipLaunchKernelGGL(reduce_mid_final_k<bf16>, dim3(g2), dim3(256), 0, st, ws, (bf16*)y, B * C, (int)chunks, scale);
   else hipLaunchKernelGGL(reduce_mid_final_k<float>, dim3(g2), dim3(256), 0, st, ws, (float*)y, B * C, (int)chunks, scale);

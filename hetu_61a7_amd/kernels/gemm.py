@@ -54,7 +54,12 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
 
 
 def _vendor(a, b, ta, tb, bias, activation):
-    y = torch.matmul(_tr(a, ta), _tr(b, tb))
+    A, B = _tr(a, ta), _tr(b, tb)
+    if bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
+        y = torch.addmm(bias.to(A.dtype), A, B)     # bias in the hipBLASLt epilogue
+        bias = None
+    else:
+        y = torch.matmul(A, B)
     if bias is not None or activation is not None:
         from .elementwise import binary, unary
         if bias is not None:
@@ -83,3 +88,27 @@ def bmm(a, b, ta=False, tb=False):
                 if y is not None:
                     return y
     return torch.matmul(_tr(a, ta), _tr(b, tb))
+
+
+def matmul_into(a, b, ta, tb, out):
+    """out (fp32, e.g. a slot of the flat gradient buffer) = op(a) @ op(b):
+    the MFMA kernel writes fp32 directly; the library path computes in the
+    input dtype and converts once.  Returns ``out``."""
+    a, b = _match(a, b)
+    if native(a) and a.dtype == torch.bfloat16 and _MFMA not in ('off', 'vendor'):
+        from . import gemm_mfma
+        from .autotune import choose
+
+        def hip():
+            return gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), out=out)
+
+        def vendor():
+            out.copy_(torch.matmul(_tr(a, ta), _tr(b, tb)))
+            return out
+        key = ('gemm_into', _sig(a), _sig(b), ta, tb)
+        if _MFMA == 'hip' or choose(key, {'hip': hip, 'vendor': vendor}) == 'hip':
+            if hip() is not None:
+                return out
+        return vendor()
+    out.copy_(torch.matmul(_tr(a, ta), _tr(b, tb)))
+    return out

@@ -6,20 +6,26 @@ import torch
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32, F32
 
 
-def reduce_mid(x3: torch.Tensor, scale: float = 1.0, out_dtype=None) -> torch.Tensor:
-    """x3 [B, R, C] contiguous -> [B, C] = scale * sum over R."""
+def reduce_mid(x3: torch.Tensor, scale: float = 1.0, out_dtype=None, out=None) -> torch.Tensor:
+    """x3 [B, R, C] contiguous -> [B, C] = scale * sum over R (into ``out`` if given)."""
     B, R, C = x3.shape
+    if out is not None:
+        out_dtype = out.dtype
     out_dtype = out_dtype or x3.dtype
     if native(x3) and supported_float(x3) and out_dtype in (torch.float32, torch.bfloat16):
         x3 = x3.contiguous()
         wsf = fn('hetu_reduce_mid_ws', [I64, I64, I64], restype=I64)
         ws = torch.empty(wsf(B, R, C), dtype=torch.float32, device=x3.device)
-        y = torch.empty((B, C), dtype=out_dtype, device=x3.device)
+        y = out if out is not None else torch.empty((B, C), dtype=out_dtype, device=x3.device)
         f = fn('hetu_reduce_mid', [P, P, I64, I64, I64, F32, I32, I32, P, P])
         check(f(x3.data_ptr(), y.data_ptr(), B, R, C, float(scale), is_bf16(x3),
                 1 if out_dtype == torch.bfloat16 else 0, ws.data_ptr(), stream_ptr()), 'reduce_mid')
         return y
-    return (x3.float().sum(1) * scale).to(out_dtype)
+    r = (x3.float().sum(1) * scale).to(out_dtype)
+    if out is not None:
+        out.copy_(r.reshape(out.shape))
+        return out
+    return r
 
 
 def reduce_last(x2: torch.Tensor, scale: float = 1.0, out_dtype=None) -> torch.Tensor:

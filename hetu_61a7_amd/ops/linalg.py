@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 
 from .node import Op
+from .nn import AuxResult
 from ..kernels import gemm as KG
 
 
@@ -23,8 +24,22 @@ class MatMulOp(Op):
         super().__init__(MatMulOp, [a, b], ctx)
         self.matmul_attr_trans_A, self.matmul_attr_trans_B = trans_A, trans_B
 
+    grad_dest = None  # fp32 slot in the optimizer's flat gradient buffer (weight grads)
+
+    def set_grad_dest(self, dest):
+        if dest.dtype == torch.float32 and dest.is_contiguous():
+            self.grad_dest = dest
+            return True
+        return False
+
     def compute(self, input_vals, output_val=None, stream_handle=None):
         a, b = input_vals
+        d = self.grad_dest
+        if d is not None and a.is_cuda and a.dim() == 2 and b.dim() == 2:
+            m = a.shape[1] if self.matmul_attr_trans_A else a.shape[0]
+            n = b.shape[0] if self.matmul_attr_trans_B else b.shape[1]
+            if d.numel() == m * n:
+                return KG.matmul_into(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, d.view(m, n))
         return KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B)
 
     def gradient(self, output_grad):
@@ -61,25 +76,50 @@ class LinearOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         a, b, bias = input_vals
+        if self.activation == 'gelu' and self.need_pre:
+            # keep the pre-activation for the backward (instead of re-running the GEMM)
+            from ..kernels.elementwise import unary
+            pre = KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias=bias)
+            return AuxResult(unary('gelu', pre), pre)
         return KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias=bias,
                          activation=self.activation)
 
+    need_pre = False
+
     def gradient(self, output_grad):
         from .reduce import reducesumaxiszero_op
-        from .basic import relu_gradient_op, gelu_gradient_op
+        from .basic import relu_gradient_op
         G = output_grad
         if self.activation == 'relu':
             G = relu_gradient_op(self, output_grad, ctx=self.raw_ctx)
         elif self.activation == 'gelu':
-            pre = LinearOp(self.inputs[0], self.inputs[1], self.inputs[2], self.matmul_attr_trans_A,
-                           self.matmul_attr_trans_B, None, ctx=self.raw_ctx)
-            G = gelu_gradient_op(pre, output_grad, ctx=self.raw_ctx)
+            self.need_pre = True
+            G = LinearGeluGradOp(output_grad, self, ctx=self.raw_ctx)
         mm = MatMulOp(self.inputs[0], self.inputs[1], self.matmul_attr_trans_A, self.matmul_attr_trans_B)
         ga, gb = mm.gradient(G)
         return [ga, gb, reducesumaxiszero_op(G, ctx=self.raw_ctx)]
 
     def infer_shape(self, input_shapes):
         return MatMulOp.infer_shape(self, input_shapes[:2])
+
+
+class LinearGeluGradOp(Op):
+    """gelu'(pre) * grad with the pre-activation saved by the forward LinearOp."""
+    value_and_aux_inputs = (1,)
+
+    def __init__(self, grad, fwd, ctx=None):
+        super().__init__(LinearGeluGradOp, [grad, fwd], ctx)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels.elementwise import binary
+        g, (y, pre) = input_vals
+        return binary('gelu_grad', pre.contiguous(), g.contiguous())
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
 
 
 def linear_op(node_A, node_B, bias, trans_A=False, trans_B=False, activation=None, ctx=None):

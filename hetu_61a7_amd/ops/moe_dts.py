@@ -21,7 +21,10 @@ class GumbelSoftmaxOp(Op):
         x = input_vals[0].float()
         tau = float(self.temperature.value)
         if not self.inference:
-            u = torch.rand_like(x).clamp_(1e-9, 1 - 1e-9)
+            from .nn import _next_seed
+            g = torch.Generator(device=x.device)
+            g.manual_seed(_next_seed() & 0x7FFFFFFFFFFF)
+            u = torch.rand(x.shape, generator=g, device=x.device).clamp_(1e-9, 1 - 1e-9)
             x = x - torch.log(-torch.log(u))
         y = torch.softmax(x / tau, -1)
         return AuxResult(y, tau)

@@ -117,11 +117,22 @@ def reduce_mean_op(node, axes=None, keepdims=False, ctx=None):
 
 
 class ReduceSumAxisZeroOp(Op):
+    grad_dest = None   # bias gradients: fp32 slot of the flat gradient buffer
+
     def __init__(self, node, ctx=None):
         super().__init__(ReduceSumAxisZeroOp, [node], ctx)
 
+    def set_grad_dest(self, dest):
+        if dest.dtype == torch.float32 and dest.is_contiguous():
+            self.grad_dest = dest
+            return True
+        return False
+
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x = input_vals[0].contiguous()
+        d = self.grad_dest
+        if d is not None and x.is_cuda and d.numel() == x[0].numel():
+            return KR.reduce_mid(x.reshape(1, x.shape[0], -1), out=d.view(1, -1)).reshape(x.shape[1:])
         return KR.reduce_mid(x.reshape(1, x.shape[0], -1)).reshape(x.shape[1:])
 
     def gradient(self, output_grad):

@@ -326,7 +326,9 @@ class PipelineSubExecutor(object):
                             # sparse (embedding) grads stay sparse across micro-batches
                             acc[i] = v if i not in acc else acc[i].merge(v)
                         else:
-                            acc[i] = v.float() if i not in acc else acc[i] + v.float()
+                            # clone: v may be a slot of the flat gradient buffer that the next
+                            # micro-batch overwrites in place
+                            acc[i] = v.float().clone() if i not in acc else acc[i] + v.float()
                 states[mb] = None
         self.p2p.flush()
         if self.opt is not None and acc:

@@ -312,6 +312,30 @@ __global__ void reduce_mid_final_k(const float* __restrict__ part, TO* __restric
   }
 }
 
+// final pass over the chunk partials: 64 columns x 4 chunk groups per block,
+// 4 independent accumulators per thread (loads in flight), LDS fold
+template <typename TO>
+__global__ void __launch_bounds__(256) reduce_mid_final2_k(const float* __restrict__ part, TO* __restrict__ y,
+                                                            int64_t BC, int chunks, float scale) {
+  __shared__ float sh[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < BC) {
+    int k = grp;
+    for (; k + 12 < chunks; k += 16) {
+      a0 += part[(int64_t)k * BC + i];
+      a1 += part[(int64_t)(k + 4) * BC + i];
+      a2 += part[(int64_t)(k + 8) * BC + i];
+      a3 += part[(int64_t)(k + 12) * BC + i];
+    }
+    for (; k < chunks; k += 4) a0 += part[(int64_t)k * BC + i];
+  }
+  sh[grp][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (grp == 0 && i < BC) y[i] = from_f<TO>((sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane]) * scale);
+}
+
 // y[r] = scale * sum_c x[r, c]  (one wave per row)
 template <typename T, typename TO>
 __global__ void __launch_bounds__(256) reduce_last_k(const T* __restrict__ x, TO* __restrict__ y, int64_t R,
@@ -442,9 +466,15 @@ HETU_API int hetu_reduce_mid(const void* x, void* y, int64_t B, int64_t R, int64
   } else {
     hipLaunchKernelGGL(reduce_mid_k<float>, grid, dim3(256), 0, st, (const float*)x, ws, B, R, C, rpc);
   }
-  int g2 = stream_grid(B * C, 256, 1);
-  if (y_bf16) hipLaunchKernelGGL(reduce_mid_final_k<bf16>, dim3(g2), dim3(256), 0, st, ws, (bf16*)y, B * C, (int)chunks, scale);
-  else hipLaunchKernelGGL(reduce_mid_final_k<float>, dim3(g2), dim3(256), 0, st, ws, (float*)y, B * C, (int)chunks, scale);
+  if (chunks >= 16) {
+    const unsigned g2 = (unsigned)((B * C + 63) / 64);
+    if (y_bf16) hipLaunchKernelGGL(reduce_mid_final2_k<bf16>, dim3(g2), dim3(256), 0, st, ws, (bf16*)y, B * C, (int)chunks, scale);
+    else hipLaunchKernelGGL(reduce_mid_final2_k<float>, dim3(g2), dim3(256), 0, st, ws, (float*)y, B * C, (int)chunks, scale);
+  } else {
+    int g2 = stream_grid(B * C, 256, 1);
+    if (y_bf16) hipLaunchKernelGGL(reduce_mid_final_k<bf16>, dim3(g2), dim3(256), 0, st, ws, (bf16*)y, B * C, (int)chunks, scale);
+    else hipLaunchKernelGGL(reduce_mid_final_k<float>, dim3(g2), dim3(256), 0, st, ws, (float*)y, B * C, (int)chunks, scale);
+  }
   HETU_LAUNCH_CHECK();
   return 0;
 }

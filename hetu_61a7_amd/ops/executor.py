@@ -514,6 +514,7 @@ class SubExecutor(object):
         for n, v in feed_dict.items():
             node = n
             vals[node] = self._feed_value(node, v)
+        self.last_feed_shapes = {n: tuple(vals[n].shape) for n in feed_dict if hasattr(vals[n], 'shape')}
         for n in self.feed_nodes:
             if n not in vals:
                 raise KeyError('placeholder %s not fed' % n.name)

@@ -269,8 +269,11 @@ class Batch_NormalizationOp(Op):
 
     def _init_running(self, C, device):
         if self.running_mean is None or self.running_mean.device != device:
-            self.running_mean = torch.zeros(C, dtype=torch.float32, device=device)
-            self.running_var = torch.ones(C, dtype=torch.float32, device=device)
+            rm0, rv0 = getattr(self, 'running_mean_init', None), getattr(self, 'running_var_init', None)
+            self.running_mean = torch.zeros(C, dtype=torch.float32, device=device) if rm0 is None else \
+                torch.as_tensor(rm0, dtype=torch.float32).to(device)
+            self.running_var = torch.ones(C, dtype=torch.float32, device=device) if rv0 is None else \
+                torch.as_tensor(rv0, dtype=torch.float32).to(device)
 
     def compute(self, input_vals, output_val=None, stream_handle=None, inference=None):
         x, scale, bias = input_vals[:3]

@@ -38,6 +38,7 @@ from . import layers
 from . import data
 from . import metrics
 from . import onnx
+from . import graphboard
 from .utils.profiler import HetuProfiler, NCCLProfiler
 from .launcher_api import (wrapped_mpi_nccl_init, worker_init, worker_finish, server_init,
                            server_finish, scheduler_init, scheduler_finish, get_worker_communicate)

@@ -79,6 +79,9 @@ def unary(op: str, x: torch.Tensor, c: float = 0.0, c2: float = 0.0, out=None) -
         check(f(U[op], x.data_ptr(), y.data_ptr(), x.numel(), is_bf16(x), float(c), float(c2),
                 stream_ptr()), 'unary:' + op)
         return y
+    from . import cpu_native
+    if op in cpu_native.UNARY and cpu_native.active(x) and out is None:
+        return cpu_native.unary(op, x)
     r = _ref_unary(op, x, c, c2)
     if out is not None:
         out.copy_(r)
@@ -150,6 +153,9 @@ def binary(op: str, a: torch.Tensor, b: torch.Tensor, c: float = 0.0, out=None) 
             return y
     if b.dtype != a.dtype and b.numel() <= a.numel():
         b = b.to(a.dtype)
+    from . import cpu_native
+    if op == 'relu_grad' and out is None and b.shape == a.shape and cpu_native.active(a, b):
+        return cpu_native.relu_grad(a, b)
     r = _ref_binary(op, a, b, c)
     if r.dtype != a.dtype and a.dtype.is_floating_point:
         r = r.to(a.dtype)

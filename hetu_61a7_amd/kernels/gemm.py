@@ -36,6 +36,10 @@ def _tr(t, f):
 
 def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     a, b = _match(a, b)
+    from . import cpu_native
+    if cpu_native.active(a, b, bias) and a.dim() == 2 and b.dim() == 2 and activation in (None, 'relu', 'gelu'):
+        y = cpu_native.gemm(_tr(a, ta), _tr(b, tb), bias)
+        return cpu_native.unary(activation, y) if activation else y
     if native(a) and _MFMA not in ('off', 'vendor'):
         from . import gemm_mfma
         hip = lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)

@@ -31,6 +31,12 @@ def optimizer_flat(mode, p, g, s1=None, s2=None, shadow=None, lr=0.01, l2=0.0, m
         return
     if dyn is not None:
         lr, beta1t, beta2t, gscale = [float(v) for v in dyn.tolist()]
+    from . import cpu_native
+    if mode != 'lamb' and cpu_native.active(p, g) and p.is_contiguous() and g.is_contiguous():
+        cpu_native.optimizer(mode, p, g, s1, s2, lr, l2, mu, beta1, beta2, beta1t, beta2t, eps, wd, gscale)
+        if shadow is not None:
+            shadow.copy_(p)
+        return
     gr = g * gscale + l2 * p if (gscale != 1.0 or l2) else g
     if mode == 'sgd':
         p.sub_(lr * gr)

@@ -21,6 +21,9 @@ def reduce_mid(x3: torch.Tensor, scale: float = 1.0, out_dtype=None, out=None) -
         check(f(x3.data_ptr(), y.data_ptr(), B, R, C, float(scale), is_bf16(x3),
                 1 if out_dtype == torch.bfloat16 else 0, ws.data_ptr(), stream_ptr()), 'reduce_mid')
         return y
+    from . import cpu_native
+    if B == 1 and out is None and out_dtype == torch.float32 and cpu_native.active(x3):
+        return cpu_native.reduce_rows(x3.reshape(R, C), scale).reshape(1, C)
     r = (x3.float().sum(1) * scale).to(out_dtype)
     if out is not None:
         out.copy_(r.reshape(out.shape))

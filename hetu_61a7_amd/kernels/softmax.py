@@ -48,6 +48,9 @@ def softmax_ce(logits: torch.Tensor, labels: torch.Tensor):
         check(f(x.data_ptr(), lab.data_ptr(), loss.data_ptr(), lse.data_ptr(), R, N,
                 is_bf16(x), is_bf16(lab), stream_ptr()), 'softmax_ce')
         return loss, lse
+    from . import cpu_native
+    if cpu_native.active(logits) and logits.dim() == 2:
+        return cpu_native.softmax_ce(logits, labels)
     xf = logits.float()
     lse = torch.logsumexp(xf, -1)
     loss = (labels.float() * (lse.unsqueeze(-1) - xf)).sum(-1)
@@ -68,6 +71,9 @@ def softmax_ce_backward(logits, labels, grad, lse=None):
                 lse.contiguous().data_ptr() if lse is not None else None, dx.data_ptr(), R, N,
                 is_bf16(x), is_bf16(lab), stream_ptr()), 'softmax_ce_bwd')
         return dx
+    from . import cpu_native
+    if cpu_native.active(logits) and logits.dim() == 2 and lse is not None:
+        return cpu_native.softmax_ce_backward(logits, labels, grad, lse)
     xf = logits.float()
     yl = labels.float()
     sm = torch.softmax(xf, -1)

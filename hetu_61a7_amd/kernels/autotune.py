@@ -15,7 +15,7 @@ import torch
 
 _decisions = {}
 _times = {}
-REPS = int(os.environ.get('HETU_AUTOTUNE_REPS', '3'))
+REPS = int(os.environ.get('HETU_AUTOTUNE_REPS', '10'))
 
 
 def choose(key, candidates):
@@ -30,6 +30,7 @@ def choose(key, candidates):
         f = candidates[n]
         if f() is None:  # unsupported shape
             continue
+        f()  # second warm call: first-use library heuristics / code-object loads
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(REPS):

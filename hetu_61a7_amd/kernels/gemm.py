@@ -50,16 +50,24 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
         elif a.dtype == torch.bfloat16:
             from .autotune import choose
             key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
-            if choose(key, {'hip': hip, 'vendor': lambda: _vendor(a, b, ta, tb, bias, activation)}) == 'hip':
+            cands = {'hip': hip, 'vendor': lambda: _vendor(a, b, ta, tb, bias, activation)}
+            if bias is not None:
+                # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
+                # plain GEMM + a separate bias pass: measure both
+                cands['vendor_nobias'] = lambda: _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
+            c = choose(key, cands)
+            if c == 'hip':
                 y = hip()
                 if y is not None:
                     return y
+            elif c == 'vendor_nobias':
+                return _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
     return _vendor(a, b, ta, tb, bias, activation)
 
 
-def _vendor(a, b, ta, tb, bias, activation):
+def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
     A, B = _tr(a, ta), _tr(b, tb)
-    if bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
+    if fuse_bias and bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
         y = torch.addmm(bias.to(A.dtype), A, B)     # bias in the hipBLASLt epilogue
         bias = None
     else:

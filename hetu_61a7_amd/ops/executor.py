@@ -352,6 +352,9 @@ class Executor(object):
     def clearTimer(self, name='default'):
         return self.subexecutor[name].clearTimer()
 
+    def export_chrome_trace(self, path, name='default'):
+        return self.subexecutor[name].export_chrome_trace(path)
+
     def recordLoads(self):
         if self.config.ps_comm is not None:
             self.config.ps_comm.record_loads()
@@ -601,6 +604,12 @@ class SubExecutor(object):
         if self.timer is None:
             return None
         return self.timer.log_out(path, log_level, clear)
+
+    def export_chrome_trace(self, path):
+        """Chrome/Perfetto trace of the timed steps (needs ``timing=``)."""
+        if self.timer is None:
+            raise RuntimeError('enable timing (Executor(..., timing="gpu"|"cpu")) to record a trace')
+        return self.timer.export_chrome_trace(path)
 
     def clearTimer(self):
         if self.timer is not None:

@@ -55,7 +55,15 @@ __global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x,
 #pragma unroll
   for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; }
   if (active) {
-    for (int64_t r = r0 + rsub; r < r1; r += RP) {
+    int64_t r = r0 + rsub;
+    for (; r + RP < r1; r += 2 * RP) {   // two rows in flight
+      float v[V], w[V];
+      load_vec<T>(x + r * C + (int64_t)vc * V, v);
+      load_vec<T>(x + (r + RP) * C + (int64_t)vc * V, w);
+#pragma unroll
+      for (int i = 0; i < V; ++i) { s[i] += v[i] + w[i]; q[i] += v[i] * v[i] + w[i] * w[i]; }
+    }
+    for (; r < r1; r += RP) {
       float v[V];
       load_vec<T>(x + r * C + (int64_t)vc * V, v);
 #pragma unroll
@@ -145,18 +153,43 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
                                                  const float* __restrict__ fa,
                                                  const float* __restrict__ fb, T* __restrict__ y,
                                                  int64_t nvec, int C) {
+  // channel-stationary threads: the grid stride is a multiple of C/V, so every
+  // thread keeps one channel group's folded affine in registers (no per-element
+  // parameter loads, no 64-bit modulo) and streams 2 vectors per iteration
   constexpr int V = Vec<T>::N;
   const int cv = C / V;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * V;
-    float v[V];
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  const int64_t stride = nth - nth % cv;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= stride) return;
+  const int c0 = (int)(tid % cv) * V;
+  float a[V], bb[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) { a[k] = fa[c0 + k]; bb[k] = fb[c0 + k]; }
+  int64_t i = tid;
+  for (; i + stride < nvec; i += 2 * stride) {
+    float v[V], w[V], r[V], r2[V];
     load_vec<T>(x + i * V, v);
-    float r[V];
+    load_vec<T>(x + (i + stride) * V, w);
+    if (RES) { load_vec<T>(res + i * V, r); load_vec<T>(res + (i + stride) * V, r2); }
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float o = v[k] * a[k] + bb[k], o2 = w[k] * a[k] + bb[k];
+      if (RES) { o += r[k]; o2 += r2[k]; }
+      if (RELU) { o = fmaxf(o, 0.f); o2 = fmaxf(o2, 0.f); }
+      v[k] = o;
+      w[k] = o2;
+    }
+    store_vec<T>(y + i * V, v);
+    store_vec<T>(y + (i + stride) * V, w);
+  }
+  if (i < nvec) {
+    float v[V], r[V];
+    load_vec<T>(x + i * V, v);
     if (RES) load_vec<T>(res + i * V, r);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      float o = v[k] * fa[c0 + k] + fb[c0 + k];
+      float o = v[k] * a[k] + bb[k];
       if (RES) o += r[k];
       if (RELU) o = fmaxf(o, 0.f);
       v[k] = o;
@@ -279,11 +312,22 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
                                                      const float* __restrict__ fb,
                                                      T* __restrict__ dx, T* __restrict__ dres,
                                                      int64_t nvec, int C) {
+  // channel-stationary threads (see bn_apply): per-channel coefficients live in
+  // registers for the whole grid-stride loop
   constexpr int V = Vec<T>::N;
   const int cv = C / V;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * V;
+  const int64_t nth = (int64_t)gridDim.x * blockDim.x;
+  const int64_t stride = nth - nth % cv;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= stride) return;
+  const int c0 = (int)(tid % cv) * V;
+  float A[V], Bc[V], Cc[V], ka[V], kb[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    A[k] = cA[c0 + k]; Bc[k] = cB[c0 + k]; Cc[k] = cC[c0 + k];
+    if (RELU == 2) { ka[k] = fa[c0 + k]; kb[k] = fb[c0 + k]; }
+  }
+  for (int64_t i = tid; i < nvec; i += stride) {
     float g[V], xv[V];
     load_vec<T>(dy + i * V, g);
     load_vec<T>(x + i * V, xv);
@@ -294,12 +338,12 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
       for (int k = 0; k < V; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
     } else if (RELU == 2) {
 #pragma unroll
-      for (int k = 0; k < V; ++k) g[k] = (xv[k] * fa[c0 + k] + fb[c0 + k]) > 0.f ? g[k] : 0.f;
+      for (int k = 0; k < V; ++k) g[k] = (xv[k] * ka[k] + kb[k]) > 0.f ? g[k] : 0.f;
     }
     if (DRES) store_vec<T>(dres + i * V, g);
     float o[V];
 #pragma unroll
-    for (int k = 0; k < V; ++k) o[k] = cA[c0 + k] * g[k] + cB[c0 + k] * xv[k] + cC[c0 + k];
+    for (int k = 0; k < V; ++k) o[k] = A[k] * g[k] + Bc[k] * xv[k] + Cc[k];
     store_vec<T>(dx + i * V, o);
   }
 }
@@ -338,6 +382,10 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
   }
   int64_t nvec = M * C / V;
   int grid = stream_grid(nvec, 256, 4);
+  {  // channel-stationary kernels need >= C/V threads
+    const int need = (int)((C / Vec<T>::N + 255) / 256);
+    if (grid < need) grid = need;
+  }
   const T* xr = (const T*)x;
   const T* rr = (const T*)res;
   T* yr = (T*)y;
@@ -378,6 +426,10 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const T* x, 
                      C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
   int64_t nvec = M * C / V;
   int grid = stream_grid(nvec, 256, 4);
+  {  // channel-stationary kernels need >= C/V threads
+    const int need = (int)((C / Vec<T>::N + 255) / 256);
+    if (grid < need) grid = need;
+  }
   if (dres)
     hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, fa, fb, dx, dres, nvec, C);
   else

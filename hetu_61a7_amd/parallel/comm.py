@@ -30,9 +30,18 @@ def backend_for_device(dev_is_gpu: bool) -> str:
     return 'nccl' if dev_is_gpu else 'gloo'
 
 
-def init_process_group(use_gpu: Optional[bool] = None, timeout_s: int = 1800) -> 'Communicator':
-    """Initialise the global communicator (idempotent)."""
+def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] = None) -> 'Communicator':
+    """Initialise the global communicator (idempotent).
+
+    Failure detection (SURVEY §5.3 "RCCL watchdog"): collectives time out after
+    ``timeout_s`` (env ``HETU_COMM_TIMEOUT``, default 1800 s) and RCCL async
+    errors are handled by the process-group watchdog, which aborts the
+    communicator and raises in this process -- the launcher then restarts the
+    job, which resumes from the last checkpoint (``utils.checkpoint``)."""
     global _WORLD
+    if timeout_s is None:
+        timeout_s = int(os.environ.get('HETU_COMM_TIMEOUT', '1800'))
+    os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '1')
     if _WORLD is not None:
         return _WORLD
     rank, world, local = dist_env()

@@ -80,6 +80,40 @@ class Hardware:
     def p2p(self, nbytes):
         return nbytes / (self.link_bw * self.eff) + self.latency
 
+    @classmethod
+    def calibrate(cls, gpus=None, gemm=(8192, 3072, 768), comm=None, sizes=(1 << 22, 1 << 24), **kw):
+        """Profile-driven hardware model: the achieved bf16 GEMM rate of this
+        device (a transformer-sized matmul, the HetuProfiler role) and, when a
+        multi-rank communicator is given, the measured all-reduce bus bandwidth
+        (NCCLProfiler.bandwidth_sweep) replacing the xGMI link defaults."""
+        import time
+        import torch
+        hw = cls(gpus=gpus or (comm.nrank if comm is not None else 1), **kw)
+        M, N, K = gemm
+        dev = 'cuda' if torch.cuda.is_available() else 'cpu'
+        dt = torch.bfloat16 if dev == 'cuda' else torch.float32
+        a = torch.randn(M, K, device=dev).to(dt)
+        b = torch.randn(K, N, device=dev).to(dt)
+        for _ in range(3):
+            a @ b
+        if dev == 'cuda':
+            torch.cuda.synchronize()
+        it = 20 if dev == 'cuda' else 2
+        t0 = time.perf_counter()
+        for _ in range(it):
+            a @ b
+        if dev == 'cuda':
+            torch.cuda.synchronize()
+        hw.flops = 2.0 * M * N * K * it / (time.perf_counter() - t0)
+        if comm is not None and comm.nrank > 1:
+            from ..utils.profiler import NCCLProfiler
+            sweep = NCCLProfiler(comm).bandwidth_sweep(sizes)
+            if sweep:
+                busbw = max(v['busbw_GBps'] for v in sweep.values()) * 1e9
+                hw.link_bw = busbw / max(1, min(comm.nrank - 1, hw.links))
+                hw.eff = 1.0
+        return hw
+
 
 @dataclass
 class Plan:

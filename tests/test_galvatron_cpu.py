@@ -122,3 +122,11 @@ def test_planned_bert_pipeline_runs_on_two_stages():
     last = [l for l in losses1 if l]                       # losses surface on the last stage
     assert last and all(np.isfinite(v).all() for v in last)
     assert np.mean(last[-1]) < np.mean(last[0])
+
+
+def test_calibrated_hardware_model():
+    from hetu_61a7_amd.parallel.galvatron import Hardware, GalvatronPlanner, bert_layers
+    hw = Hardware.calibrate(gpus=8, gemm=(256, 256, 256))
+    assert hw.flops > 1e8 and hw.gpus == 8
+    plan = GalvatronPlanner(bert_layers(64, 2, 16, 1000), hw=hw).search(32)
+    assert plan.pp >= 1 and plan.time > 0

@@ -393,7 +393,9 @@ class SubExecutor(object):
         self.eval_node_list = list(eval_node_list)
         self.config = config
         self.topo_order = find_topo_sort(self.eval_node_list)
-        self.inference = not any(isinstance(n, OptimizerOp) for n in self.topo_order)
+        # training mode when the set updates weights or evaluates any gradient node
+        self.inference = not any(isinstance(n, OptimizerOp) or getattr(n, 'bw_of', None) is not None
+                                 for n in self.topo_order)
         self.param_nodes, self.feed_nodes, self.dataloader_nodes, self.computing_nodes = [], [], [], []
         for n in self.topo_order:
             if isinstance(n, PlaceholderOp):
@@ -568,7 +570,9 @@ class SubExecutor(object):
                 for op, j in hooks:
                     op.on_grad_ready(j, r)
             for dead in self.release_after[i]:
-                vals.pop(dead, None)
+                v = vals.pop(dead, None)
+                if v is not None and dead not in shapes:   # later shape-only consumers
+                    shapes[dead] = _shape_of(v)
                 aux.pop(dead, None)
         self.step_count += 1
         return vals

@@ -1,0 +1,33 @@
+"""The examples/ entry points (reference examples/*) run end to end on the CPU
+backend with tiny settings."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+RUNS = [
+    ['examples/cnn/main.py', '--model', 'mlp', '--dataset', 'cifar10', '--gpu', '-1', '--num-epochs', '1',
+     '--max-steps', '3', '--synthetic', '--validate', '--timing'],
+    ['examples/cnn/main.py', '--model', 'lenet', '--dataset', 'mnist', '--gpu', '-1', '--num-epochs', '1',
+     '--max-steps', '2', '--synthetic', '--opt', 'adam', '--learning-rate', '0.001'],
+    ['examples/cnn/main.py', '--model', 'lstm', '--dataset', 'mnist', '--gpu', '-1', '--num-epochs', '1',
+     '--max-steps', '2', '--synthetic', '--opt', 'momentum'],
+    ['examples/ctr/run_hetu.py', '--model', 'wdl_criteo', '--gpu', '-1', '--nepoch', '1', '--steps', '3', '--val'],
+    ['examples/ctr/run_hetu.py', '--model', 'dfm_criteo', '--gpu', '-1', '--nepoch', '1', '--steps', '3'],
+    ['examples/nlp/train_hetu_bert.py', '--gpu', '-1', '--hidden_size', '64', '--num_hidden_layers', '2',
+     '--num_attention_heads', '2', '--seq_length', '32', '--train_batch_size', '4', '--vocab_size', '2000',
+     '--steps', '2', '--fp32'],
+    ['examples/moe/test_moe.py', '--gpu', '-1', '--batch_size', '2', '--num_tokens', '32', '--model_dim', '16',
+     '--hidden_size', '32', '--num_steps', '2', '--gate', 'top'],
+    ['examples/gnn/run_single.py', '--gpu', '-1', '--nodes', '500', '--epochs', '2'],
+]
+
+
+@pytest.mark.parametrize('cmd', RUNS, ids=[' '.join(c[:3]) for c in RUNS])
+def test_example_runs(cmd):
+    r = subprocess.run([sys.executable] + cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

@@ -36,6 +36,7 @@ def parse():
     p.add_argument('--moe-gate', default='topk', choices=['topk', 'dts'])
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     p.add_argument('--bucket-mb', type=float, default=32)
+    p.add_argument('--zero', type=int, default=0, help='1: ZeRO-1 sharded optimizer state over the DP group')
     p.add_argument('--op-profile', default=None, help='write per-op-type GPU time (ms) to this file')
     return p.parse_args()
 
@@ -79,7 +80,7 @@ def main():
         loss, logits = resnet50_imagenet(x, y_, 1000)
         opt = ht.optim.MomentumOptimizer(learning_rate=0.1 / max(world, 1), momentum=0.9)
         train_op = opt.minimize(loss)
-        kw = dict(mixed_precision=args.dtype, bucket_mb=args.bucket_mb, seed=1234,
+        kw = dict(mixed_precision=args.dtype, bucket_mb=args.bucket_mb, seed=1234, zero=args.zero,
                   timing='gpu' if args.op_profile else None)
         if world > 1:
             ex = ht.Executor({'train': [loss, train_op]}, dist_strategy=ht.dist.DataParallel('allreduce'), **kw)

@@ -11,6 +11,8 @@ Only applied when the intermediate values have no other consumer.
 Backward (``fuse_backward``, run on the gradient graph):
   sum(conv_dgrad(w, g), r, ...)   -> conv_dgrad accumulating r in its epilogue
                                      (the residual-branch gradient join of ResNet)
+  sum(matmul(g, w^T), r, ...)     -> matmul with r added in the GEMM epilogue
+                                     (beta = 1; the transformer residual-stream join)
 """
 from __future__ import annotations
 
@@ -78,11 +80,33 @@ def fuse_backward(roots):
         return 0
     from .ops.reduce import SumOp
     from .ops.nn import Conv2d_Gradient_of_DataOp
+    from .ops.linalg import MatMulOp
     topo, cons = _consumers(roots)
     root_set = set(roots)
     fused = 0
     for n in topo:
-        if not isinstance(n, SumOp) or len(n.inputs) < 2:
+        if not isinstance(n, SumOp) or len(n.inputs) < 2 or getattr(n, 'sparse', False):
+            continue
+        mm = [d for d in n.inputs if type(d) is MatMulOp and len(d.inputs) == 2 and len(cons.get(d, [])) == 1
+              and d not in root_set and getattr(d, 'raw_ctx', None) == getattr(n, 'raw_ctx', None)
+              and all(getattr(i, 'raw_ctx', None) == getattr(n, 'raw_ctx', None) for i in n.inputs)]
+        if mm:
+            d = mm[0]
+            rest = [i for i in n.inputs if i is not d]
+            if len(rest) > 1:
+                other = SumOp(rest, ctx=n.raw_ctx)
+                other.bw_of = getattr(n, 'bw_of', None)
+            else:
+                other = rest[0]
+            keep_id, keep_name, bw = n.id, n.name, getattr(n, 'bw_of', None)
+            n.__class__ = MatMulOp
+            n.__dict__.update({k: v for k, v in d.__dict__.items() if k not in ('id', 'name', 'inputs', 'bw_of')})
+            n.inputs = list(d.inputs) + [other]
+            n.op_type = 'MatMulOp'
+            n.id, n.name = keep_id, keep_name
+            if bw is not None:
+                n.bw_of = bw
+            fused += 1
             continue
         for d in n.inputs:
             if isinstance(d, Conv2d_Gradient_of_DataOp) and len(d.inputs) == 3 and \

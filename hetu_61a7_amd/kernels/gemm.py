@@ -102,6 +102,24 @@ def bmm(a, b, ta=False, tb=False):
     return torch.matmul(_tr(a, ta), _tr(b, tb))
 
 
+_MM_DTYPE_OK = [None]   # aten::mm.dtype (bf16 x bf16 -> fp32 in the hipBLASLt epilogue) usable?
+
+
+def _vendor_into(A, B, out):
+    """out (fp32) = A @ B on the library GEMM, writing fp32 directly when the
+    bf16->fp32 ``mm.dtype`` overload is available (no bf16 round trip + copy)."""
+    if _MM_DTYPE_OK[0] is not False and A.is_cuda and A.dtype == torch.bfloat16 and A.dim() == 2 \
+            and out.is_contiguous():
+        try:
+            torch.mm(A, B, out_dtype=torch.float32, out=out)
+            _MM_DTYPE_OK[0] = True
+            return out
+        except (RuntimeError, TypeError):
+            _MM_DTYPE_OK[0] = False
+    out.copy_(torch.matmul(A, B))
+    return out
+
+
 def matmul_into(a, b, ta, tb, out):
     """out (fp32, e.g. a slot of the flat gradient buffer) = op(a) @ op(b):
     the MFMA kernel writes fp32 directly; the library path computes in the
@@ -115,12 +133,34 @@ def matmul_into(a, b, ta, tb, out):
             return gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), out=out)
 
         def vendor():
-            out.copy_(torch.matmul(_tr(a, ta), _tr(b, tb)))
-            return out
+            return _vendor_into(_tr(a, ta), _tr(b, tb), out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
         if _MFMA == 'hip' or choose(key, {'hip': hip, 'vendor': vendor}) == 'hip':
             if hip() is not None:
                 return out
         return vendor()
-    out.copy_(torch.matmul(_tr(a, ta), _tr(b, tb)))
-    return out
+    return _vendor_into(_tr(a, ta), _tr(b, tb), out)
+
+
+def matmul_acc(a, b, ta, tb, acc):
+    """op(a) @ op(b) + acc with the addition in the GEMM epilogue (beta = 1):
+    the MFMA kernel reads ``acc`` as Cin, hipBLASLt runs it as addmm."""
+    a, b = _match(a, b)
+    A, B = _tr(a, ta), _tr(b, tb)
+    if native(a) and a.dtype == torch.bfloat16 and A.dim() == 2 and tuple(acc.shape) == (A.shape[0], B.shape[1]) \
+            and _MFMA not in ('off', 'vendor'):
+        from . import gemm_mfma
+        from .autotune import choose
+        c = acc.to(a.dtype) if acc.dtype != a.dtype else acc
+        hip = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0)
+        vendor = lambda: torch.addmm(c, A, B)
+        key = ('gemm_acc', _sig(a), _sig(b), ta, tb)
+        if _MFMA == 'hip' or choose(key, {'hip': hip, 'vendor': vendor}) == 'hip':
+            y = hip()
+            if y is not None:
+                return y
+        return vendor()
+    if A.dim() == 2 and acc.dim() == 2 and acc.dtype == A.dtype:
+        return torch.addmm(acc, A, B)
+    y = torch.matmul(A, B)
+    return y + acc.to(y.dtype)

@@ -323,7 +323,8 @@ def bert_bench(args, world, rank, local):
     if plan.pp > 1 or max(plan.tp) > 1:
         raise NotImplementedError('bench: planner chose %s; only its DP layout is benchmarked' % plan.short())
     feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-5)
-    kw = dict(mixed_precision=args.dtype, seed=1234, bucket_mb=getattr(args, 'bucket_mb', 32))
+    kw = dict(mixed_precision=args.dtype, seed=1234, bucket_mb=getattr(args, 'bucket_mb', 32),
+              zero=getattr(args, 'zero', 0))
     if world > 1:
         ex = H.Executor({'train': [loss, train]}, dist_strategy=H.dist.DataParallel('allreduce'), **kw)
     else:

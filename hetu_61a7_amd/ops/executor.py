@@ -131,7 +131,7 @@ class HetuConfig(object):
                  cstable_policy=None, bsp=-1, prefetch=True, enable_lazy=False, cache_bound=100,
                  log_path=None, pipeline=None, dist_strategy=None, use_preduce=False, overlap=True,
                  use_nccl_collectives=True, mixed_precision=None, bucket_mb=32, use_hipgraph=False,
-                 timing=None, **kwargs):
+                 timing=None, zero=0, **kwargs):
         self.eval_node_list = eval_node_list
         self.seed = seed if seed is not None else int(os.environ.get('HETU_SEED', 0) or 0) or int(time.time())
         if seed is None and os.environ.get('HETU_SEED') is None:
@@ -144,6 +144,7 @@ class HetuConfig(object):
         self.use_preduce, self.overlap, self.use_nccl_collectives = use_preduce, overlap, use_nccl_collectives
         self.mixed_precision = mixed_precision in ('bf16', 'bfloat16', True)
         self.bucket_mb = bucket_mb
+        self.zero = int(zero)   # 1: ZeRO-1 sharded optimizer state (optimizer.py _make_zero_buckets)
         self.use_hipgraph = use_hipgraph
         self.timing = timing
         self.h2d_ops, self.d2h_ops = {}, {}

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import torch
 
+from .. import ndarray
 from .node import Op
 from .nn import AuxResult
 from ..kernels import gemm as KG
@@ -33,7 +34,16 @@ class MatMulOp(Op):
         return False
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        a, b = input_vals
+        a, b = input_vals[:2]
+        if len(input_vals) == 3:   # fused gradient join (graph_opt.fuse_backward): op(a) @ op(b) + acc
+            acc = input_vals[2]
+            if self.grad_dest is None and not isinstance(acc, ndarray.IndexedSlices):
+                return KG.matmul_acc(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, acc)
+            y = self.compute([a, b])
+            if not (self.grad_dest is not None and y.data_ptr() == self.grad_dest.data_ptr()):
+                y = y.float() if self.grad_dest is not None else y.clone()
+            y.add_((acc.to_dense() if isinstance(acc, ndarray.IndexedSlices) else acc).to(y.dtype))
+            return y
         d = self.grad_dest
         if d is not None and a.is_cuda and a.dim() == 2 and b.dim() == 2:
             m = a.shape[1] if self.matmul_attr_trans_A else a.shape[0]
@@ -55,7 +65,7 @@ class MatMulOp(Op):
         return [matmul_op(B, G, True, True, ctx=c), matmul_op(G, A, True, True, ctx=c)]
 
     def infer_shape(self, input_shapes):
-        a, b = input_shapes
+        a, b = input_shapes[:2]
         m = a[1] if self.matmul_attr_trans_A else a[0]
         n = b[0] if self.matmul_attr_trans_B else b[1]
         return (m, n)

@@ -179,7 +179,8 @@ class FlatGroup(object):
     """Flat fp32 storage for a set of dense parameters (one per device)."""
 
     def __init__(self, params: List[Op], values: Dict[Op, torch.Tensor], n_states: int,
-                 state_init=(0.0, 0.0), shadow: bool = False, device=None):
+                 state_init=(0.0, 0.0), shadow: bool = False, device=None, pad_to: int = 1,
+                 state_numel: Optional[int] = None):
         self.params = params
         self.offsets = {}
         off = 0
@@ -187,13 +188,16 @@ class FlatGroup(object):
             self.offsets[p] = (off, values[p].numel(), tuple(values[p].shape))
             off += values[p].numel()
         self.numel = off
+        # ZeRO-1 pads the buffers so every bucket splits evenly over the ranks
+        self.padded = max(-(-off // pad_to) * pad_to, 1)
         dev = device
-        self.param = torch.empty(max(off, 1), dtype=torch.float32, device=dev)
+        self.param = torch.zeros(self.padded, dtype=torch.float32, device=dev)
         for p in params:
             self.view(p, 'param').copy_(values[p].float())
         self.grad = torch.zeros_like(self.param)
-        self.s1 = torch.full_like(self.param, state_init[0]) if n_states >= 1 else None
-        self.s2 = torch.full_like(self.param, state_init[1]) if n_states >= 2 else None
+        ns = self.padded if state_numel is None else state_numel   # ZeRO-1: this rank's shard only
+        self.s1 = torch.full((ns,), state_init[0], dtype=torch.float32, device=dev) if n_states >= 1 else None
+        self.s2 = torch.full((ns,), state_init[1], dtype=torch.float32, device=dev) if n_states >= 2 else None
         self.shadow = None
         if shadow:
             self.shadow = self.param.to(torch.bfloat16)  # same (channels-last) layout
@@ -217,12 +221,13 @@ class FlatGroup(object):
 
 
 class Bucket(object):
-    __slots__ = ('start', 'end', 'pending', 'total', 'work')
+    __slots__ = ('start', 'end', 'pending', 'total', 'work', 'own', 'zoff')
 
     def __init__(self, start, end, total):
         self.start, self.end, self.total = start, end, total
         self.pending = total
         self.work = None
+        self.own, self.zoff = None, 0
 
 
 class OptimizerOp(Op):
@@ -242,6 +247,7 @@ class OptimizerOp(Op):
         self.bucket_bytes = 32 << 20
         self.allreduce_mode = 'sum'
         self.ps_params = set()
+        self.zero = False
 
     # ----------------------------------------------------------------------------
     def gradient(self, output_grad):
@@ -293,8 +299,18 @@ class OptimizerOp(Op):
             else:
                 dense.append(p)
         amp = config.mixed_precision
+        self.zero = bool(getattr(config, 'zero', 0)) and self.dp and opt.mode != 'lamb' \
+            and not any(self.excluded_from_dp(p) for p in dense)
+        pad_to, state_numel = 1, None
+        if self.zero:
+            P = self.comm.nrank
+            self.zero_unit = P * 64                       # every bucket splits into 64-aligned shards
+            pad_to = self.zero_unit
+            total = -(-sum(values[p].numel() for p in dense) // pad_to) * pad_to
+            state_numel = max(total // P, 1)
         self.flat = FlatGroup(dense, values, opt.n_states, getattr(opt, 'state_init', (0.0, 0.0)),
-                              shadow=amp, device=self.ctx.torch_device if self.ctx else None)
+                              shadow=amp, device=self.ctx.torch_device if self.ctx else None,
+                              pad_to=pad_to, state_numel=state_numel)
         # ops that can write their gradient straight into the flat buffer get its view
         grad_of = {pp: g for pp, g in zip(self.param_of_input, self.inputs)}
         for p in dense:
@@ -320,7 +336,9 @@ class OptimizerOp(Op):
         self.slot = {}
         for i, p in enumerate(self.param_of_input):
             self.slot[i] = p
-        if self.dp:
+        if self.zero:
+            self._make_zero_buckets(dense)
+        elif self.dp:
             self._make_buckets(dense)
         if self.ps_dense_wanted and self.flat.numel > 0:
             from .ps.table import PSDense
@@ -344,6 +362,67 @@ class OptimizerOp(Op):
             cur_n += n
         if members:
             self._close_bucket(cur_start, cur_n, members)
+
+    def _make_zero_buckets(self, dense):
+        """ZeRO-1 (absent in the reference): fixed-size buckets
+        over the padded flat buffer.  Each bucket is reduce-scattered as soon as
+        every parameter overlapping it has its gradient (same overlap with the
+        backward pass as the all-reduce buckets); rank r owns the r-th 1/P of
+        every bucket, keeps optimizer state for that shard only, updates it, and
+        all-gathers the fp32 weights.  Same bytes on the wire as an all-reduce,
+        optimizer state memory / P."""
+        P, r = self.comm.nrank, self.comm.rank
+        unit = self.zero_unit
+        cap = max(self.bucket_bytes // 4 // unit, 1) * unit
+        total = self.flat.padded
+        self.buckets, self.bucket_of = [], {}
+        zoff = 0
+        for s in range(0, total, cap):
+            e = min(s + cap, total)
+            b = Bucket(s, e, 0)
+            n = (e - s) // P
+            b.own, b.zoff = (s + r * n, s + (r + 1) * n), zoff
+            zoff += n
+            self.buckets.append(b)
+        assert zoff == self.flat.s1.numel() if self.flat.s1 is not None else True
+        self.flat.zgrad = torch.zeros(max(zoff, 1), dtype=torch.float32, device=self.flat.param.device)
+        for p in dense:
+            o, n, _ = self.flat.offsets[p]
+            bs = self.buckets[o // cap:(o + n - 1) // cap + 1]
+            self.bucket_of[p] = bs
+            for b in bs:
+                b.total += 1
+        for b in self.buckets:
+            b.pending = b.total
+
+    def _reduce_bucket(self, b, async_op=True):
+        if not self.zero:
+            return self.comm.all_reduce(self.flat.grad[b.start:b.end], self.allreduce_mode, async_op=async_op)
+        lo, hi = b.own
+        return self.comm.reduce_scatter(self.flat.zgrad[b.zoff:b.zoff + hi - lo], self.flat.grad[b.start:b.end],
+                                        self.allreduce_mode, async_op=async_op)
+
+    def _zero_step(self):
+        f, opt = self.flat, self.optimizer
+        h = opt.hyper(self.step)
+        dyn = getattr(self, 'dyn', None)
+        gathers = []
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()
+            else:
+                self._reduce_bucket(b, async_op=False)
+            lo, hi = b.own
+            sl = slice(b.zoff, b.zoff + hi - lo)
+            KO.optimizer_flat(opt.mode, f.param[lo:hi], f.zgrad[sl], f.s1[sl] if f.s1 is not None else None,
+                              f.s2[sl] if f.s2 is not None else None, None, gscale=f.gscale, dyn=dyn, **h)
+            # the gather of this bucket overlaps the update of the next one
+            gathers.append(self.comm.all_gather(f.param[b.start:b.end], f.param[lo:hi].clone(), async_op=True))
+        for w in gathers:
+            if w is not None:
+                w.wait()
+        if f.shadow is not None:
+            f.shadow.copy_(f.param)
 
     def _close_bucket(self, start, n, members):
         b = Bucket(start, start + n, len(members))
@@ -371,12 +450,12 @@ class OptimizerOp(Op):
                 value = value.reshape(dst.shape)
             dst.copy_(value)
         if self.dp:
-            b = self.bucket_of.get(p)
-            if b is not None:
-                b.pending -= 1
-                if b.pending == 0:
-                    b.work = self.comm.all_reduce(self.flat.grad[b.start:b.end], self.allreduce_mode,
-                                                  async_op=True)
+            bs = self.bucket_of.get(p)
+            if bs is not None:
+                for b in (bs if self.zero else (bs,)):
+                    b.pending -= 1
+                    if b.pending == 0:
+                        b.work = self._reduce_bucket(b)
 
     def begin_step(self):
         self._pending_sparse = []
@@ -387,13 +466,17 @@ class OptimizerOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         self.step += 1
-        for b in self.buckets:
+        if self.zero:
+            self._zero_step()
+        for b in self.buckets if not self.zero else ():
             if b.work is not None:
                 b.work.wait()
             elif self.dp:
                 # a bucket whose grads never arrived this step (should not happen)
                 self.comm.all_reduce(self.flat.grad[b.start:b.end], self.allreduce_mode)
-        if self.ps_dense is not None:
+        if self.zero:
+            pass
+        elif self.ps_dense is not None:
             self.ps_dense.step(self.optimizer.get_learning_rate())
         elif self.flat is not None and self.flat.numel > 0:
             self.optimizer.dense_update(self.flat, self.step, getattr(self, 'dyn', None))

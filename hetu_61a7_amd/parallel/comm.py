@@ -145,6 +145,13 @@ class Communicator(object):
         return dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group, async_op=async_op)
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = 'sum', async_op: bool = False):
+        """out = this rank's 1/P chunk (dim 0) of the reduction of ``inp``."""
+        if not self.use_gpu:
+            # gloo has no reduce-scatter: all-reduce a copy and keep our chunk
+            t = inp.contiguous().clone()
+            dist.all_reduce(t, _RED.get(op, dist.ReduceOp.SUM), group=self.group)
+            out.copy_(t.reshape(self.nrank, -1)[self.rank].reshape(out.shape))
+            return _Done() if async_op else None
         return dist.reduce_scatter_tensor(out, inp.contiguous(), _RED.get(op, dist.ReduceOp.SUM),
                                           group=self.group, async_op=async_op)
 
@@ -181,6 +188,11 @@ class Communicator(object):
 
     def __repr__(self):
         return 'Communicator(rank=%d, nrank=%d, ranks=%s)' % (self.rank, self.nrank, self.ranks)
+
+
+class _Done(object):
+    def wait(self):
+        return True
 
 
 class _PostDiv(object):

@@ -2,7 +2,9 @@
 
 Parallel-equivalence pattern of the reference (examples/runner/parallel/
 validate_results.py): DP with SUM all-reduce and lr/N must reproduce the
-single-process baseline on the concatenated batch.
+single-process baseline on the concatenated batch.  The ZeRO-1 variant
+(reduce-scatter, sharded optimizer state, all-gather of the weights) must
+reproduce it too.
 """
 import os
 import socket
@@ -21,7 +23,7 @@ def _free_port():
     return p
 
 
-def _mlp_losses(X, Y, lr, steps, dp=False, bucket_mb=32):
+def _mlp_losses(X, Y, lr, steps, dp=False, bucket_mb=32, opt='momentum', zero=0):
     import hetu_61a7_amd as ht
     rng = np.random.RandomState(11)
     w1 = (rng.randn(20, 32) * 0.3).astype(np.float32)
@@ -32,8 +34,11 @@ def _mlp_losses(X, Y, lr, steps, dp=False, bucket_mb=32):
     W2 = ht.Variable(name='w2', value=w2)
     h = ht.relu_op(ht.linear_op(x, W1, B1))
     loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(h, W2), y_), [0])
-    train = ht.optim.MomentumOptimizer(lr, 0.9).minimize(loss)
+    o = ht.optim.MomentumOptimizer(lr, 0.9) if opt == 'momentum' else ht.optim.AdamOptimizer(lr)
+    train = o.minimize(loss)
     kw = dict(bucket_mb=bucket_mb)
+    if zero:
+        kw['zero'] = zero
     if dp:
         ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'), **kw)
     else:
@@ -42,40 +47,68 @@ def _mlp_losses(X, Y, lr, steps, dp=False, bucket_mb=32):
     for _ in range(steps):
         out.append(float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]))
     params = {n.name: v.numpy().copy() for n, v in ex.config.placeholder_to_arr_map.items() if n.trainable}
-    return out, params
+    info = {}
+    if train.flat is not None:
+        info = dict(zero=train.zero, padded=train.flat.padded,
+                    state=train.flat.s1.numel() if train.flat.s1 is not None else 0, buckets=len(train.buckets))
+    return out, params, info
 
 
-def _worker(rank, world, port, X, Y, q):
+def _worker(rank, world, port, X, Y, q, opt, zero):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), HETU_USE_CONFIG='0')
     n = X.shape[0] // world
     sl = slice(rank * n, (rank + 1) * n)
+    lr = 0.1 / world if opt == 'momentum' else 0.01
     # tiny bucket so several buckets are exercised
-    losses, params = _mlp_losses(X[sl], Y[sl], 0.1 / world, 5, dp=True, bucket_mb=0.001)
-    q.put((rank, losses, params))
+    losses, params, info = _mlp_losses(X[sl], Y[sl], lr, 5, dp=True, bucket_mb=0.001, opt=opt, zero=zero)
+    q.put((rank, losses, params, info))
     from hetu_61a7_amd.parallel import comm
     comm.destroy()
 
 
-def test_dp_allreduce_matches_single_process():
-    rng = np.random.RandomState(0)
-    X = rng.randn(32, 20).astype(np.float32)
-    Y = np.eye(4, dtype=np.float32)[rng.randint(0, 4, 32)]
-    # baseline: one process on the full batch (mean loss), lr 0.1
-    _, base_params = _mlp_losses(X, Y, 0.1, 5)
-    world = 2
+def _run_dp(X, Y, opt, zero, world=2):
     port = _free_port()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, X, Y, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, X, Y, q, opt, zero)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    res.sort()
+    res.sort(key=lambda t: t[0])
+    return res
+
+
+def _data():
+    rng = np.random.RandomState(0)
+    X = rng.randn(32, 20).astype(np.float32)
+    Y = np.eye(4, dtype=np.float32)[rng.randint(0, 4, 32)]
+    return X, Y
+
+
+def test_dp_allreduce_matches_single_process():
+    X, Y = _data()
+    # baseline: one process on the full batch (mean loss), lr 0.1
+    _, base_params, _ = _mlp_losses(X, Y, 0.1, 5)
+    res = _run_dp(X, Y, 'momentum', 0)
     # SUM all-reduce of per-shard mean-loss grads with lr/N == full-batch mean with lr
     for name, v in base_params.items():
         np.testing.assert_allclose(res[0][2][name], v, rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(res[1][2][name], v, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize('opt', ['momentum', 'adam'])
+def test_zero1_matches_single_process(opt):
+    X, Y = _data()
+    # Adam is invariant to the gradient scale (SUM of 2 shard means = 2 x full mean)
+    _, base_params, _ = _mlp_losses(X, Y, 0.1 if opt == 'momentum' else 0.01, 5, opt=opt)
+    res = _run_dp(X, Y, opt, 1)
+    for rank, _, params, info in res:
+        assert info['zero'] and info['buckets'] > 1
+        if opt == 'adam':
+            assert info['state'] == info['padded'] // 2     # optimizer state sharded over 2 ranks
+        for name, v in base_params.items():
+            np.testing.assert_allclose(params[name], v, rtol=2e-4, atol=2e-5)

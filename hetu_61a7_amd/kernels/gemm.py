@@ -120,6 +120,25 @@ def _vendor_into(A, B, out):
     return out
 
 
+def _vendor_splitk_into(A, B, out, s=4):
+    """out = A @ B with K split into ``s`` batched hipBLASLt GEMMs (fp32 partials)
+    and one reduction -- s x more workgroups for long-K / small-MN products."""
+    M, K = A.shape
+    N = B.shape[1]
+    if K % s or not A.is_cuda:
+        return None
+    kc = K // s
+    # [M, K] -> [s, M, kc] and [K, N] -> [s, kc, N] as strided views (no copies)
+    Av = A.as_strided((s, M, kc), (kc * A.stride(1), A.stride(0), A.stride(1)))
+    Bv = B.as_strided((s, kc, N), (kc * B.stride(0), B.stride(0), B.stride(1)))
+    try:
+        part = torch.bmm(Av, Bv, out_dtype=torch.float32)
+    except (RuntimeError, TypeError):
+        return None
+    torch.sum(part, 0, out=out)
+    return out
+
+
 def matmul_into(a, b, ta, tb, out):
     """out (fp32, e.g. a slot of the flat gradient buffer) = op(a) @ op(b):
     the MFMA kernel writes fp32 directly; the library path computes in the
@@ -134,10 +153,22 @@ def matmul_into(a, b, ta, tb, out):
 
         def vendor():
             return _vendor_into(_tr(a, ta), _tr(b, tb), out)
+        cands = {'hip': hip, 'vendor': vendor}
+        # weight gradients: small M x N output, long K (= tokens): too few 128x128
+        # tiles to fill 256 CUs -> split K over more workgroups (fp32 slab + reduce)
+        A, B = _tr(a, ta), _tr(b, tb)
+        if A.dim() == 2:
+            M, K, N = A.shape[0], A.shape[1], B.shape[1]
+            tiles = -(-M // 128) * -(-N // 128)
+            for s in (2, 4, 8):
+                if tiles * s <= 1536 and K // s >= 512:
+                    cands['hip_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s))
+            if K >= 2048:
+                cands['vendor_sk'] = lambda: _vendor_splitk_into(A, B, out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
-        if _MFMA == 'hip' or choose(key, {'hip': hip, 'vendor': vendor}) == 'hip':
-            if hip() is not None:
-                return out
+        c = 'hip' if _MFMA == 'hip' else choose(key, cands)
+        if c != 'vendor' and cands[c]() is not None:
+            return out
         return vendor()
     return _vendor_into(_tr(a, ta), _tr(b, tb), out)
 

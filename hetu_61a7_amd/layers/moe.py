@@ -40,6 +40,13 @@ def _locations(masks):
     return locs
 
 
+def _fused_locations(topk_indices, k, num_experts):
+    """Same slots as ``_locations`` from the [T, k] index node in one native pass."""
+    from ..ops.moe import topk_locations_op
+    loc = topk_locations_op(topk_indices, num_experts)
+    return [O.split_op(loc, axes=[1], indices=[i], splits=[k]) for i in range(k)]
+
+
 def topkgating(logits, k, capacity_factor, num_tokens, num_experts, embed_dim=None, fused=True):
     capacity = k * math.ceil((num_tokens / num_experts) * capacity_factor)
     if fused and k <= 8 and num_experts <= 512:
@@ -152,7 +159,7 @@ class SAMGate(_GateBase):
             l_aux = O.add_op(l_aux, balance_loss(gates, masks[i], E))
         tmp = O.sam_max_op(gates, top1_group, indices_s[k - 1], E // G)
         l_align = O.reduce_sum_op(O.reduce_sum_op(tmp, axes=0), axes=0)
-        location_s = _locations(masks)
+        location_s = _fused_locations(topk_indices, k, E)
         gates_s = [O.reduce_sum_op(O.mul_op(gates, m), axes=1) for m in masks]
         return l_aux, l_align, indices_s, location_s, gates_s, capacity
 
@@ -230,7 +237,7 @@ class DenseToSparseGate(_GateBase):
         indices_s = [O.split_op(topk_indices, axes=[1], indices=[i], splits=[k]) for i in range(k)]
         masks = [O.array_reshape_op(O.one_hot_op(ix, num_classes=E), [-1, E]) for ix in indices_s]
         l_aux = balance_loss(gates, masks[0], E)
-        location_s = _locations(masks)
+        location_s = _fused_locations(topk_indices, k, E)
         gates_s = [threshold_mask_op(O.reduce_sum_op(O.mul_op(gates, m), axes=1), self.threshold) for m in masks]
         return l_aux, indices_s, location_s, gates_s, capacity
 

@@ -436,3 +436,29 @@ def topk_gating_op(logits, k, capacity, num_experts, ctx=None):
     g = TopKGatingOp(logits, k, capacity, num_experts, ctx=ctx)
     return (AuxLossOp(g, logits, ctx=ctx), GatingSelectOp(g, 'indices', ctx=ctx),
             GatingSelectOp(g, 'locations', ctx=ctx), g)
+
+
+class TopKLocationsOp(Op):
+    """Slot of every (token, choice) inside its expert's capacity from top-k
+    indices [T, k] (choice-major, as the reference's one_hot/cumsum/mul/reduce
+    chain of TopGate.py): one native counting pass instead of a column scan."""
+
+    def __init__(self, indices, num_experts, ctx=None):
+        super().__init__(TopKLocationsOp, [indices], ctx)
+        self.num_experts = int(num_experts)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        idx = input_vals[0]
+        idx = idx.reshape(idx.shape[0], -1)
+        loc, _, _ = KM.locations(idx, self.num_experts)
+        return loc
+
+    def gradient(self, output_grad):
+        return [None]
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+def topk_locations_op(indices, num_experts, ctx=None):
+    return TopKLocationsOp(indices, num_experts, ctx=ctx)

@@ -323,8 +323,13 @@ class CumsumOp(Op):
         self.bias, self.dim = bias, dim
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        x = input_vals[0]
-        return torch.cumsum(x.float(), self.dim) + self.bias
+        x = input_vals[0].float()
+        d = self.dim % x.dim()
+        if x.is_cuda and d != x.dim() - 1 and x.shape[d] > 4 * x.numel() // max(x.shape[d], 1):
+            # long scan over few columns: an outer-dim scan runs one serial thread
+            # per column -- scan the innermost dim of the transposed copy instead
+            return torch.cumsum(x.transpose(d, -1).contiguous(), -1).transpose(d, -1) + self.bias
+        return torch.cumsum(x, self.dim) + self.bias
 
     def gradient(self, output_grad):
         return [None]

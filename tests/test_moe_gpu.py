@@ -45,3 +45,12 @@ def test_fused_gate_layer_gpu_matches_graph_gate():
     np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
     c, _ = moe_fused_vs_graph(ht.cpu(0))
     np.testing.assert_allclose(a, c, rtol=1e-3, atol=1e-4)
+
+
+def test_cumsum_long_column_scan_matches_cpu():
+    import hetu_61a7_amd as ht
+    x = ht.Variable(name='x')
+    y = ht.cumsum_with_bias_op(x, bias=-1, dim=0)
+    X = (np.random.RandomState(0).rand(16384, 2) > 0.5).astype(np.float32)
+    got = ht.Executor([y], ctx=ht.gpu(0)).run(feed_dict={x: X}, convert_to_numpy_ret_vals=True)[0]
+    np.testing.assert_array_equal(got, np.cumsum(X, 0) - 1)

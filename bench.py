@@ -32,6 +32,8 @@ def parse():
     p.add_argument('--batch', type=int, default=None, help='per-GPU batch (256 resnet50, 128 wdl)')
     p.add_argument('--criteo-rows', type=int, default=0, help='embedding rows (default: full Criteo 33762577)')
     p.add_argument('--cache', default='LFUOpt')
+    p.add_argument('--no-prefetch', dest='prefetch', action='store_false',
+                   help='wdl: do not prefetch the next batch rows with the push')
     p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl', 'bert', 'moe'])
     p.add_argument('--moe-gate', default='topk', choices=['topk', 'dts'])
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])

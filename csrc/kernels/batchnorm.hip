@@ -229,7 +229,37 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
       mu[i] = mean[vc * V + i]; is[i] = invstd[vc * V + i];
       if (RELU == 2) { ka[i] = fa[vc * V + i]; kb[i] = fb[vc * V + i]; }
     }
-    for (int64_t r = r0 + rsub; r < r1; r += RP) {
+    // two rows in flight per iteration (all loads issued before any use)
+    int64_t r = r0 + rsub;
+    for (; r + RP < r1; r += 2 * RP) {
+      const int64_t off = r * C + (int64_t)vc * V, off2 = off + (int64_t)RP * C;
+      float g[V], xv[V], g2[V], xv2[V], yv[V], yv2[V];
+      load_vec<T>(dy + off, g);
+      load_vec<T>(x + off, xv);
+      load_vec<T>(dy + off2, g2);
+      load_vec<T>(x + off2, xv2);
+      if (RELU == 1) {
+        load_vec<T>(y + off, yv);
+        load_vec<T>(y + off2, yv2);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          g[i] = yv[i] > 0.f ? g[i] : 0.f;
+          g2[i] = yv2[i] > 0.f ? g2[i] : 0.f;
+        }
+      } else if (RELU == 2) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          g[i] = (xv[i] * ka[i] + kb[i]) > 0.f ? g[i] : 0.f;
+          g2[i] = (xv2[i] * ka[i] + kb[i]) > 0.f ? g2[i] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        s[i] += g[i] + g2[i];
+        q[i] += (g[i] * (xv[i] - mu[i]) + g2[i] * (xv2[i] - mu[i])) * is[i];
+      }
+    }
+    for (; r < r1; r += RP) {
       const int64_t off = r * C + (int64_t)vc * V;
       float g[V], xv[V];
       load_vec<T>(dy + off, g);
@@ -327,7 +357,43 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
     A[k] = cA[c0 + k]; Bc[k] = cB[c0 + k]; Cc[k] = cC[c0 + k];
     if (RELU == 2) { ka[k] = fa[c0 + k]; kb[k] = fb[c0 + k]; }
   }
-  for (int64_t i = tid; i < nvec; i += stride) {
+  int64_t i = tid;
+  for (; i + stride < nvec; i += 2 * stride) {   // two vectors in flight
+    const int64_t j = i + stride;
+    float g[V], xv[V], g2[V], xv2[V], yv[V], yv2[V];
+    load_vec<T>(dy + i * V, g);
+    load_vec<T>(x + i * V, xv);
+    load_vec<T>(dy + j * V, g2);
+    load_vec<T>(x + j * V, xv2);
+    if (RELU == 1) {
+      load_vec<T>(y + i * V, yv);
+      load_vec<T>(y + j * V, yv2);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        g[k] = yv[k] > 0.f ? g[k] : 0.f;
+        g2[k] = yv2[k] > 0.f ? g2[k] : 0.f;
+      }
+    } else if (RELU == 2) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        g[k] = (xv[k] * ka[k] + kb[k]) > 0.f ? g[k] : 0.f;
+        g2[k] = (xv2[k] * ka[k] + kb[k]) > 0.f ? g2[k] : 0.f;
+      }
+    }
+    if (DRES) {
+      store_vec<T>(dres + i * V, g);
+      store_vec<T>(dres + j * V, g2);
+    }
+    float o[V], o2[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      o[k] = A[k] * g[k] + Bc[k] * xv[k] + Cc[k];
+      o2[k] = A[k] * g2[k] + Bc[k] * xv2[k] + Cc[k];
+    }
+    store_vec<T>(dx + i * V, o);
+    store_vec<T>(dx + j * V, o2);
+  }
+  for (; i < nvec; i += stride) {
     float g[V], xv[V];
     load_vec<T>(dy + i * V, g);
     load_vec<T>(x + i * V, xv);

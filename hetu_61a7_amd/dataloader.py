@@ -131,6 +131,13 @@ class Dataloader(object):
     def get_next_arr(self):
         return self.get_arr()
 
+    def peek_next_arr(self):
+        """The batch the next ``get_arr`` will return (already staged), without
+        advancing; None before the first batch."""
+        if not self.initialized or self._pending is None:
+            return None
+        return self._pending[2] if len(self._pending) > 2 else self._pending[0]
+
     def get_cur_shape(self):
         return self.shape
 
@@ -177,6 +184,10 @@ class DataloaderOp(Op):
 
     def get_next_arr(self, name):
         return self.get_arr(name)
+
+    def peek_next_arr(self, name):
+        dl = self.dataloaders.get(name)
+        return None if dl is None else dl.peek_next_arr()
 
     def get_cur_shape(self, name):
         return self.dataloaders[name].get_cur_shape()

@@ -180,24 +180,20 @@ def wdl_criteo_bench(args, world, rank, local):
     import hetu_61a7_amd as ht
     rows = int(getattr(args, 'criteo_rows', 0) or CRITEO_ROWS)
     B = args.batch or 128
-    xd, xs, y_ = ht.Variable(name='dense_input'), ht.Variable(name='sparse_input'), ht.Variable(name='y_')
+    nb = 64
+    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + rank)
+    # dataloader-fed inputs, as the reference's run_hetu.py: the executor knows the
+    # next batch's sparse ids and prefetches their rows with this step's push
+    xd = ht.dataloader_op([ht.Dataloader(dense, B, 'train')])
+    xs = ht.dataloader_op([ht.Dataloader(sparse, B, 'train')])
+    y_ = ht.dataloader_op([ht.Dataloader(labels, B, 'train')])
     loss, y, _, train = wdl_criteo(xd, xs, y_, feature_dimension=rows, embedding_size=128, learning_rate=0.01)
     ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(local), comm_mode='Hybrid',
                      cstable_policy=getattr(args, 'cache', 'LFUOpt'), cache_bound=3, bsp=-1,
-                     mixed_precision=args.dtype, seed=1234)
-    nb = 64
-    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + rank)
-    dev = torch.device('cuda', local)
-    D = torch.from_numpy(dense).to(dev)
-    L = torch.from_numpy(labels).to(dev)
-    S = torch.from_numpy(sparse)
-    it = [0]
+                     mixed_precision=args.dtype, seed=1234, prefetch=getattr(args, 'prefetch', True))
 
     def step():
-        i = it[0] % nb
-        it[0] += 1
-        sl = slice(i * B, (i + 1) * B)
-        ex.run('train', feed_dict={xd: D[sl], xs: S[sl], y_: L[sl]})
+        ex.run('train')
 
     def finish():
         from ..ps import worker

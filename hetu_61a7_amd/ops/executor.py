@@ -411,6 +411,15 @@ class SubExecutor(object):
         for p in self.param_nodes:
             config.init_param(p)
         self.opt_ops = [n for n in self.computing_nodes if isinstance(n, OptimizerOp)]
+        # PS tables looked up with dataloader-fed ids: prefetch the next batch's rows
+        self.ps_prefetch = []
+        if getattr(config, 'prefetch', False):
+            from .embedding import EmbeddingLookUp
+            for n in self.computing_nodes:
+                if isinstance(n, EmbeddingLookUp) and isinstance(n.inputs[1], DataloaderOp):
+                    t = config.placeholder_to_arr_map.get(n.inputs[0])
+                    if t is not None and hasattr(t, 'next_ids_fn'):
+                        self.ps_prefetch.append((t, n.inputs[1]))
         self.mode_nodes = [n for n in self.topo_order if hasattr(n, 'inference')]
         self._build_plan()
         self.timer = None
@@ -526,6 +535,8 @@ class SubExecutor(object):
                 raise KeyError('placeholder %s not fed' % n.name)
         for d in self.dataloader_nodes:
             vals[d] = d.get_arr(self.name, cfg)
+        for t, d in self.ps_prefetch:
+            t.next_ids_fn = (lambda d=d, nm=self.name: d.peek_next_arr(nm))
         return vals
 
     def _run_eager(self, feed_dict, vals=None):

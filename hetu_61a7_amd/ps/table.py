@@ -87,6 +87,17 @@ class PSTable(object):
         self.pending = None
         self.pending_push = None
         self.version = 0
+        # prefetch (reference executor.py:531-536, HetuConfig(prefetch=True)): when the
+        # ids of the NEXT batch are known (dataloader-fed lookups) and training is
+        # asynchronous (bsp=-1), the cache lookup of batch i+1 is queued right after
+        # the lookup of batch i, so it runs on the cache thread while the GPU computes
+        # step i.  Rows batch i+1 shares with batch i then miss step i's own update
+        # (staleness 1, inside the HET cache's pull bound); BSP/SSP never prefetch.
+        self.next_ids_fn = None
+        self.pf_stages = (_Staging(), _Staging())
+        self.pf_flip = 0
+        self.prefetched = None
+        self.prefetch_hits = 0
 
     # tensor-like attributes the graph code may query
     @property
@@ -105,21 +116,49 @@ class PSTable(object):
             self.pending = None
             self.pending_push = None
 
+    def _take_prefetched(self, ids):
+        pf, self.prefetched = self.prefetched, None
+        if pf is None:
+            return None, None
+        pids, dest, ticket, stage = pf
+        self.cache.wait(ticket)
+        if pids.numel() != ids.numel() or not torch.equal(pids, ids):
+            return None, None
+        self.prefetch_hits += 1
+        return dest, stage
+
+    def _prefetch_next(self):
+        if self.next_ids_fn is None or self.cache is None or self.bsp is None or self.bsp >= 0:
+            return
+        nxt = self.next_ids_fn()
+        if nxt is None:
+            return
+        nxt = nxt.reshape(-1).long().contiguous()
+        stage = self.pf_stages[self.pf_flip]
+        self.pf_flip ^= 1
+        dest = stage.get(nxt.numel() * self.width).view(-1, self.width)
+        t = self.cache.embedding_lookup(nxt, dest)
+        self.prefetched = (nxt, dest, t, stage)
+
     def lookup(self, idx, out_dtype=None):
         ids = idx.reshape(-1)
         if ids.is_cuda:
             ids = ids.cpu()
         ids = ids.long().contiguous()
-        self._wait_push()
-        dest = self.out_stage.get(ids.numel() * self.width).view(-1, self.width)
-        if self.cache is not None:
-            self.cache.embedding_lookup(ids, dest, sync=True)
-        else:
-            t = self.agent.SparsePull(self.key, ids, dest)
-            self.agent.WaitTicket(t)
+        dest, stage = self._take_prefetched(ids)
+        if dest is None:
+            self._wait_push()      # on-demand pull sees every push issued so far
+            stage = self.out_stage
+            dest = stage.get(ids.numel() * self.width).view(-1, self.width)
+            if self.cache is not None:
+                self.cache.embedding_lookup(ids, dest, sync=True)
+            else:
+                t = self.agent.SparsePull(self.key, ids, dest)
+                self.agent.WaitTicket(t)
+        self._prefetch_next()
         if self.device.type == 'cuda':
             out = dest.to(self.device, non_blocking=True)
-            self.out_stage.guard()
+            stage.guard()
             if out_dtype is not None and out_dtype != out.dtype:
                 out = out.to(out_dtype)
         else:
@@ -129,6 +168,7 @@ class PSTable(object):
     def stage_grad(self, slices, lr):
         """Scale by -lr on the device and start the D2H copy (called as soon as the
         gradient exists, so it overlaps the rest of backward)."""
+        self._wait_push()          # the last push may still read the staging buffer
         ids = slices.indices.reshape(-1)
         if ids.is_cuda:
             ids = ids.cpu()

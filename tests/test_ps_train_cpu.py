@@ -156,22 +156,33 @@ def _worker_dl(rank, env, q, prefetch, steps):
     comm.destroy()
 
 
-def _run_dl(prefetch, steps):
-    env = dict(DMLC_PS_ROOT_PORT=str(20000 + uuid.uuid4().int % 30000), DMLC_NUM_WORKER='1',
-               DMLC_NUM_SERVER='1', HETU_PS_HEAP_GB='0.1', WORLD_SIZE='1',
+def _run_dl(prefetch, steps, nw=1):
+    env = dict(DMLC_PS_ROOT_PORT=str(20000 + uuid.uuid4().int % 30000), DMLC_NUM_WORKER=str(nw),
+               DMLC_NUM_SERVER='1', HETU_PS_HEAP_GB='0.1', WORLD_SIZE=str(nw),
                MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()), HETU_USE_CONFIG='0')
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     srv = ctx.Process(target=_server, args=(env,))
     srv.start()
-    w = ctx.Process(target=_worker_dl, args=(0, env, q, prefetch, steps))
-    w.start()
-    res = q.get(timeout=180)
-    w.join(60)
-    assert w.exitcode == 0
+    ws = [ctx.Process(target=_worker_dl, args=(r, env, q, prefetch, steps)) for r in range(nw)]
+    for w in ws:
+        w.start()
+    res = sorted([q.get(timeout=180) for _ in ws], key=lambda r: r[0])
+    for w in ws:
+        w.join(60)
+        assert w.exitcode == 0
     srv.join(60)
     assert srv.exitcode == 0
-    return res
+    return res[0] if nw == 1 else res
+
+
+def test_prefetch_two_workers_hybrid():
+    """Two dataloader-fed workers (data sharded per rank, dense grads all-reduced
+    over gloo) with prefetch on: each serves its later lookups from the prefetch."""
+    res = _run_dl(True, 5, nw=2)
+    for rank, losses, table, (n_pf, hits) in res:
+        assert n_pf == 1 and hits == 4
+        assert np.all(np.isfinite(losses))
 
 
 def test_prefetch_next_batch_rows():

@@ -26,6 +26,15 @@ _GROUPS: Dict[Tuple[int, ...], 'Communicator'] = {}
 _WORLD: Optional['Communicator'] = None
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def backend_for_device(dev_is_gpu: bool) -> str:
     return 'nccl' if dev_is_gpu else 'gloo'
 
@@ -51,7 +60,9 @@ def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] 
         torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
     if not dist.is_initialized():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        os.environ.setdefault('MASTER_PORT', '29517')
+        if 'MASTER_PORT' not in os.environ:
+            # a lone process picks a free port so concurrent single-rank jobs don't collide
+            os.environ['MASTER_PORT'] = str(_free_port()) if world == 1 else '29517'
         os.environ.setdefault('RANK', str(rank))
         os.environ.setdefault('WORLD_SIZE', str(world))
         kw = dict(backend=backend_for_device(use_gpu), rank=rank, world_size=world,

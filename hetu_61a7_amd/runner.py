@@ -4,6 +4,16 @@
     heturun -w 8 python train.py ...            # 8 GPU workers (one process per GPU)
     heturun -w 8 -s 1 python run_ctr.py ...     # + 1 PS server (Hybrid / PS jobs)
     heturun -c cluster.yml python train.py      # counts from a YAML spec
+    heturun -w 8 --max-restarts 3 python train.py   # elastic: restart the group
+                                                    # on a worker failure
+
+Elastic recovery (SURVEY §5.3 "abort and restart from checkpoint", not
+present in the reference): when a worker exits non-zero (an RCCL watchdog
+abort, ``HETU_COMM_TIMEOUT``, a crash), every process of the group is stopped
+and the whole group is relaunched on a fresh rendezvous port, up to
+``max_restarts`` times.  Each attempt sees ``HETU_RESTART_COUNT``; the training
+script resumes with ``utils.checkpoint.resume(ex, dir)`` from the last
+atomically committed ``utils.checkpoint.save_resumable`` snapshot.
 
 The reference wrapped ``mpirun`` and ssh; on one MI355X node every worker is a
 local process with the torch.distributed environment (RANK, LOCAL_RANK,
@@ -51,9 +61,29 @@ def parse_config(path):
     return workers, servers, {str(k): str(v) for k, v in (spec.get('shared') or {}).items()}
 
 
-def launch(command, workers, servers=0, shared=None, env=None, poll=0.2):
-    """Start servers then workers; returns the first non-zero worker exit code."""
+def launch(command, workers, servers=0, shared=None, env=None, poll=0.2, max_restarts=0):
+    """Start servers then workers; returns the first non-zero worker exit code.
+
+    With ``max_restarts > 0`` a failed group is torn down and relaunched (new
+    MASTER_PORT / PS root port, ``HETU_RESTART_COUNT`` incremented) until it
+    succeeds or the restarts are used up."""
     base = dict(os.environ if env is None else env)
+    rc = 0
+    for attempt in range(max_restarts + 1):
+        e = dict(base, HETU_RESTART_COUNT=str(attempt))
+        if attempt:
+            e.pop('MASTER_PORT', None)
+            e.pop('DMLC_PS_ROOT_PORT', None)
+            print('heturun: worker group failed (rc=%d); restart %d/%d' % (rc, attempt, max_restarts),
+                  file=sys.stderr, flush=True)
+        rc = _launch_once(command, workers, servers, shared, e, poll)
+        if rc == 0 or rc == 130:
+            return rc
+    return rc
+
+
+def _launch_once(command, workers, servers, shared, base, poll):
+    base = dict(base)
     base.update(shared or {})
     port = int(base.get('MASTER_PORT') or _free_port())
     base.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(workers),
@@ -99,6 +129,8 @@ def main(argv=None):
     ap.add_argument('-c', '--config', default=None, help='YAML cluster spec')
     ap.add_argument('-w', '--workers', type=int, default=0)
     ap.add_argument('-s', '--servers', type=int, default=0)
+    ap.add_argument('--max-restarts', type=int, default=int(os.environ.get('HETU_MAX_RESTARTS', '0')),
+                    help='relaunch the worker group this many times after a failure')
     ap.add_argument('command', nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     shared = {}
@@ -108,7 +140,7 @@ def main(argv=None):
         w, s = w or cw, s or cs
     if not a.command:
         ap.error('no command given')
-    return launch(a.command, max(w, 1), s, shared)
+    return launch(a.command, max(w, 1), s, shared, max_restarts=a.max_restarts)
 
 
 if __name__ == '__main__':

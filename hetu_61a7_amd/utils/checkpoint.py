@@ -110,3 +110,55 @@ def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
                     dev = cfg.device
                     n.running_mean = torch.from_numpy(m).to(dev)
                     n.running_var = torch.from_numpy(v).to(dev)
+
+
+# ---------------------------------------------------------------------------
+# Resumable snapshots for elastic restarts (heturun --max-restarts).
+# A snapshot is a directory ``<dir>/step_<N>/`` holding the reference-format
+# pickle plus the ``.ext`` optimizer/BN/scheduler state; it becomes visible
+# only when ``<dir>/latest`` (a one-line text file, replaced by an atomic
+# rename) names it, so a worker killed mid-write never leaves a torn
+# checkpoint behind.  Rank 0 writes; every rank reads.
+
+def save_resumable(ex, ckpt_dir, step, keep=2):
+    """Commit a full snapshot (weights + optimizer state) taken after ``step``
+    completed steps.  Returns the snapshot path on the writing rank."""
+    cfg = ex.config
+    sub = os.path.join(ckpt_dir, 'step_%d' % step)
+    path = save(ex, sub, save_optimizer=True)
+    if path is not None:
+        tmp = os.path.join(ckpt_dir, '.latest.%d' % os.getpid())
+        with open(tmp, 'w') as f:
+            f.write('step_%d\n' % step)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, os.path.join(ckpt_dir, 'latest'))
+        snaps = sorted((d for d in os.listdir(ckpt_dir) if d.startswith('step_')),
+                       key=lambda d: int(d[5:]))
+        for d in snaps[:-keep] if keep else []:
+            if d != 'step_%d' % step:
+                import shutil
+                shutil.rmtree(os.path.join(ckpt_dir, d), ignore_errors=True)
+    if cfg.nrank > 1 and cfg.comm_mode in ('AllReduce', 'Hybrid'):
+        from ..parallel import comm
+        comm.world().barrier()
+    return path
+
+
+def latest_step(ckpt_dir):
+    """Step count of the last committed snapshot, or 0 if there is none."""
+    try:
+        with open(os.path.join(ckpt_dir, 'latest')) as f:
+            name = f.read().strip()
+    except FileNotFoundError:
+        return 0
+    return int(name[5:]) if name.startswith('step_') else 0
+
+
+def resume(ex, ckpt_dir):
+    """Load the last committed snapshot into ``ex``; returns the number of
+    completed steps it holds (0: nothing to resume, ``ex`` untouched)."""
+    step = latest_step(ckpt_dir)
+    if step:
+        load(ex, os.path.join(ckpt_dir, 'step_%d' % step))
+    return step

@@ -1,0 +1,77 @@
+"""Elastic recovery: heturun --max-restarts relaunches a failed
+2-worker DP group; the workers resume from the last atomically committed
+snapshot (weights + momentum state + step counter) and finish with exactly
+the parameters of an uninterrupted run.  Fault injection: rank 1 exits with
+status 3 after step 7 on the first attempt only (HETU_RESTART_COUNT=0)."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+JOB = textwrap.dedent('''
+    import os, sys
+    import numpy as np
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.utils import checkpoint
+    from hetu_61a7_amd.parallel import comm
+    ckpt, out, crash_at = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    attempt = int(os.environ.get('HETU_RESTART_COUNT', '0'))
+    rng = np.random.RandomState(5)
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    W1 = ht.Variable(name='w1', value=(rng.randn(12, 16) * 0.3).astype(np.float32))
+    W2 = ht.Variable(name='w2', value=(rng.randn(16, 3) * 0.3).astype(np.float32))
+    loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(
+        ht.matmul_op(ht.relu_op(ht.matmul_op(x, W1)), W2), y_), [0])
+    train = ht.optim.MomentumOptimizer(0.05, 0.9).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'))
+    start = checkpoint.resume(ex, ckpt)
+    for step in range(start, 10):
+        r = np.random.RandomState(1000 + step * world + rank)   # data keyed by (step, rank)
+        X = r.randn(8, 12).astype(np.float32)
+        Y = np.eye(3, dtype=np.float32)[r.randint(0, 3, 8)]
+        ex.run('train', feed_dict={x: X, y_: Y})
+        if (step + 1) % 3 == 0:
+            checkpoint.save_resumable(ex, ckpt, step + 1)
+        if attempt == 0 and rank == 1 and step + 1 == crash_at:
+            os._exit(3)
+    if rank == 0:
+        np.savez(out, start=start, **checkpoint.state_dict(ex))
+    comm.destroy()
+''')
+
+
+def _run(tmp_path, tag, crash_at, restarts):
+    script = tmp_path / 'job.py'
+    script.write_text(JOB)
+    ckpt, out = tmp_path / ('ckpt_' + tag), tmp_path / (tag + '.npz')
+    env = dict(os.environ, PYTHONPATH=ROOT, HETU_USE_CONFIG='0')
+    env.pop('MASTER_PORT', None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bin', 'heturun'), '-w', '2',
+                        '--max-restarts', str(restarts), sys.executable, str(script),
+                        str(ckpt), str(out), str(crash_at)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    return r, out, ckpt
+
+
+def test_restart_resumes_from_last_snapshot(tmp_path):
+    ref, ref_out, _ = _run(tmp_path, 'ref', crash_at=-1, restarts=0)
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    r, out, ckpt = _run(tmp_path, 'elastic', crash_at=7, restarts=2)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert 'restart 1/2' in r.stderr
+    a, b = np.load(ref_out), np.load(out)
+    assert int(a['start']) == 0 and int(b['start']) == 6   # resumed after step 6's snapshot
+    for k in ('w1', 'w2'):
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6)
+    # keep=2: only the two newest snapshots survive, `latest` names the last one
+    assert sorted(os.listdir(ckpt)) == ['latest', 'step_6', 'step_9']
+
+
+def test_no_restart_propagates_failure(tmp_path):
+    r, _, _ = _run(tmp_path, 'fail', crash_at=4, restarts=0)
+    assert r.returncode == 3

@@ -97,3 +97,50 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
     dk = ds.transpose(-1, -2) @ q
     pack = torch.stack([dq, dk, dv], 2)               # [B, NH, 3, S, D]
     return pack.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H).to(qkv.dtype)
+
+
+# ---------------------------------------------------------------------------
+# Separate (strided) Q / K / V operands: the kernels take one pointer and row
+# stride per operand, so a query block and a key/value block that live in
+# different buffers (ring attention, ``parallel/ring_attention.py``) run
+# through the same MFMA kernels without packing.  All operands are 2-D
+# [B*S, H]-shaped row-major views (stride(1) == 1); lse is [B*NH*S] fp32.
+
+def blocks_fused_ok(q, k, v, S, D):
+    return (all(native(t) and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1
+                for t in (q, k, v)) and D == 64 and S % 32 == 0 and 0 < S <= 128)
+
+
+def attention_fwd_blocks(q, k, v, mask, B, S, NH, scale):
+    """-> (out [B*S, H] bf16, lse [B*NH*S] fp32) of softmax(q k^T * scale + mask) v."""
+    H = q.shape[1]
+    out = torch.empty((B * S, H), dtype=q.dtype, device=q.device)
+    lse = torch.empty((B * NH * S,), dtype=torch.float32, device=q.device)
+    m = mask.float().contiguous() if mask is not None else None
+    f = fn('hetu_attn_fwd', [P, P, P, I64, I64, I64, P, P, I64, P, I32, I32, I32, F32, F32, I64, P])
+    check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
+            m.data_ptr() if m is not None else None, out.data_ptr(), H, lse.data_ptr(), B, NH, S,
+            float(scale), 1.0, 0, stream_ptr()), 'attn_fwd')
+    return out, lse
+
+
+def attention_bwd_blocks(dout, q, k, v, out, lse, mask, B, S, NH, scale):
+    """Gradient of one (query block, key block) pair given the GLOBAL softmax
+    statistics: ``out`` and ``lse`` are the final merged output and row
+    log-sum-exp of the query block, so P = exp(s - lse) and
+    D = rowsum(dout * out) are the exact global terms and the returned
+    (dq, dk, dv) [B*S, H] are this key block's exact contributions."""
+    H = q.shape[1]
+    dout = dout.to(q.dtype).contiguous()
+    out = out.to(q.dtype).contiguous()
+    dq = torch.empty((B * S, H), dtype=q.dtype, device=q.device)
+    dk = torch.empty_like(dq)
+    dv = torch.empty_like(dq)
+    m = mask.float().contiguous() if mask is not None else None
+    f = fn('hetu_attn_bwd', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
+                             I32, I32, I32, F32, F32, I64, P])
+    check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
+            m.data_ptr() if m is not None else None, out.data_ptr(), H, lse.contiguous().data_ptr(),
+            dout.data_ptr(), H, dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), H, H, H, B, NH, S,
+            float(scale), 1.0, 0, stream_ptr()), 'attn_bwd')
+    return dq, dk, dv

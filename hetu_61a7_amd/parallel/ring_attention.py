@@ -11,7 +11,12 @@ rank (r - s) mod P while the next block is already in flight from rank r-1
 point-to-point link per step and the transfer hides behind the block's
 matmuls).  Partial results are merged with the online-softmax rule, so no
 rank ever holds more than an [S/P, S/P] score tile per head, and the saved
-state for backward is just O and the row log-sum-exp.
+state for backward is just O and the row log-sum-exp.  Each non-causal block
+pair runs through the fused MFMA attention kernels (``kernels/attention.py``
+``attention_{fwd,bwd}_blocks``: bf16, head dim 64, S/P <= 128) with Q and the
+travelling K/V block as separate strided operands; the block's (out, lse)
+is merged in fp32 with ``logaddexp``.  The backward kernel is handed the
+GLOBAL out and lse, which makes its dQ/dK/dV the exact per-block terms.
 
 Backward re-runs the ring: the K/V block travels together with an fp32 dK/dV
 accumulator; every rank adds its queries' contribution to the block it holds,
@@ -33,9 +38,15 @@ from ..ops.node import Op
 from ..ops.nn import AuxResult
 
 
-def _split(qkv, B, S_l, NH, D):
-    x = qkv.reshape(B, S_l, 3, NH, D).permute(2, 0, 3, 1, 4)     # [3, B, NH, S_l, D]
-    return x[0], x[1:].contiguous()
+def _heads(x, B, S_l, NH, D):
+    """[B*S_l, NH*D] row view -> [B, NH, S_l, D]"""
+    return x.reshape(B, S_l, NH, D).transpose(1, 2)
+
+
+def _rows(x):
+    """[B, NH, S_l, D] -> [B*S_l, NH*D]"""
+    B, NH, S_l, D = x.shape
+    return x.transpose(1, 2).reshape(B * S_l, NH * D)
 
 
 def _rotate(comm, tensors):
@@ -59,55 +70,95 @@ def _scores(q, k, kmask, scale, causal_diag):
     return s
 
 
-def ring_attention_fwd(q, kv, kmask, comm, causal=False, scale=None):
-    """q [B, NH, S_l, D]; kv [2, B, NH, S_l, D]; kmask [B, S_l] or None.
-    Returns (out [B, NH, S_l, D] in q's dtype, lse [B, NH, S_l, 1] fp32)."""
+def _use_fused(q, k, v, S_l, D, diag):
+    if diag:                     # the MFMA kernel has no causal mask: diagonal block on the torch path
+        return False
+    from ..kernels import attention as KA
+    return KA.blocks_fused_ok(q, k, v, S_l, D)
+
+
+def _block_fwd(q, k, v, kmask, B, S_l, NH, D, scale, diag):
+    """One (query block, key block) pair -> (out [B, S_l, NH, D], lse [B, NH, S_l] fp32)."""
+    if _use_fused(q, k, v, S_l, D, diag):
+        from ..kernels import attention as KA
+        o, lse = KA.attention_fwd_blocks(q, k, v, kmask, B, S_l, NH, scale)
+        return o.reshape(B, S_l, NH, D), lse.reshape(B, NH, S_l)
+    sc = _scores(_heads(q, B, S_l, NH, D), _heads(k, B, S_l, NH, D), kmask, scale, diag)
+    m = sc.amax(-1, keepdim=True)
+    p = torch.exp(sc - m)
+    l = p.sum(-1, keepdim=True)
+    vh = _heads(v, B, S_l, NH, D)
+    o = torch.matmul(p.to(vh.dtype), vh).float() / l
+    return o.transpose(1, 2), (m + torch.log(l)).squeeze(-1)
+
+
+def _block_bwd(dout, q, k, v, out, lse, kmask, B, S_l, NH, D, scale, diag):
+    """Exact contribution of one key block given the global (out, lse) -> (dq, dk, dv) [B*S_l, H]."""
+    if _use_fused(q, k, v, S_l, D, diag):
+        from ..kernels import attention as KA
+        return KA.attention_bwd_blocks(dout, q, k, v, out, lse, kmask, B, S_l, NH, scale)
+    qh, kh, vh = _heads(q, B, S_l, NH, D), _heads(k, B, S_l, NH, D), _heads(v, B, S_l, NH, D)
+    doh = _heads(dout, B, S_l, NH, D).to(q.dtype)
+    delta = (doh.float() * _heads(out, B, S_l, NH, D).float()).sum(-1, keepdim=True)
+    p = torch.exp(_scores(qh, kh, kmask, scale, diag) - lse.reshape(B, NH, S_l, 1))
+    dv = torch.matmul(p.transpose(-1, -2).to(doh.dtype), doh)
+    dp = torch.matmul(doh, vh.transpose(-1, -2)).float()
+    ds = (p * (dp - delta) * scale).to(q.dtype)
+    return _rows(torch.matmul(ds, kh)), _rows(torch.matmul(ds.transpose(-1, -2), qh)), _rows(dv)
+
+
+def ring_attention_fwd(qkv, kmask, comm, B, S_l, NH, causal=False, scale=None):
+    """qkv [B*S_l, 3H] (this rank's tokens), kmask [B, S_l] or None.
+    Returns (out [B*S_l, H] in qkv's dtype, lse [B, NH, S_l] fp32)."""
     P, r = comm.nrank, comm.rank
-    scale = scale or 1.0 / math.sqrt(q.shape[-1])
-    B, NH, S_l, D = q.shape
-    o = torch.zeros((B, NH, S_l, D), dtype=torch.float32, device=q.device)
-    m = torch.full((B, NH, S_l, 1), float('-inf'), dtype=torch.float32, device=q.device)
-    l = torch.zeros_like(m)
-    cur = [kv] + ([kmask.contiguous()] if kmask is not None else [])
+    H = qkv.shape[1] // 3
+    D = H // NH
+    scale = scale or 1.0 / math.sqrt(D)
+    q = qkv[:, :H]
+    o = torch.zeros((B, S_l, NH, D), dtype=torch.float32, device=qkv.device)
+    lse = torch.full((B, NH, S_l), float('-inf'), dtype=torch.float32, device=qkv.device)
+    cur = [qkv[:, H:].contiguous()] + ([kmask.contiguous()] if kmask is not None else [])
     for s in range(P):
         j = (r - s) % P
         nxt, reqs = _rotate(comm, cur) if s < P - 1 else (None, [])
         if not (causal and j > r):
-            k, v = cur[0][0], cur[0][1]
-            sc = _scores(q, k, cur[1] if kmask is not None else None, scale, causal and j == r)
-            m_new = torch.maximum(m, sc.amax(-1, keepdim=True))
-            p = torch.exp(sc - m_new)
-            alpha = torch.exp(m - m_new)
-            l = l * alpha + p.sum(-1, keepdim=True)
-            o = o * alpha + torch.matmul(p.to(v.dtype), v).float()
-            m = m_new
+            kv = cur[0]
+            ob, lb = _block_fwd(q, kv[:, :H], kv[:, H:], cur[1] if kmask is not None else None,
+                                B, S_l, NH, D, scale, causal and j == r)
+            new = torch.logaddexp(lse, lb)
+            wa = torch.exp(lse - new).transpose(1, 2).unsqueeze(-1)     # [B, S_l, NH, 1]
+            wb = torch.exp(lb - new).transpose(1, 2).unsqueeze(-1)
+            o = o * wa + ob.float() * wb
+            lse = new
         for w in reqs:
             w.wait()
         if nxt is not None:
             cur = nxt
-    out = (o / l).to(q.dtype)
-    return out, m + torch.log(l)
+    return o.reshape(B * S_l, H).to(qkv.dtype), lse
 
 
-def ring_attention_bwd(dout, q, kv, kmask, out, lse, comm, causal=False, scale=None):
-    """Returns (dq [B, NH, S_l, D], dkv [2, B, NH, S_l, D]) in fp32."""
+def ring_attention_bwd(dout, qkv, kmask, out, lse, comm, B, S_l, NH, causal=False, scale=None):
+    """Returns dqkv [B*S_l, 3H] in qkv's dtype."""
     P, r = comm.nrank, comm.rank
-    scale = scale or 1.0 / math.sqrt(q.shape[-1])
-    dout = dout.to(q.dtype)
-    delta = (dout.float() * out.float()).sum(-1, keepdim=True)      # rowsum(dO * O)
-    dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
-    dkv = torch.zeros(kv.shape, dtype=torch.float32, device=q.device)
-    cur = [kv] + ([kmask.contiguous()] if kmask is not None else [])
+    H = qkv.shape[1] // 3
+    D = H // NH
+    scale = scale or 1.0 / math.sqrt(D)
+    q = qkv[:, :H]
+    dout = dout.to(qkv.dtype).contiguous()
+    dq = torch.zeros((B * S_l, H), dtype=torch.float32, device=qkv.device)
+    dkv = torch.zeros((B * S_l, 2 * H), dtype=torch.float32, device=qkv.device)
+    cur = [qkv[:, H:].contiguous()] + ([kmask.contiguous()] if kmask is not None else [])
     for s in range(P):
         j = (r - s) % P
         if not (causal and j > r):
-            k, v = cur[0][0], cur[0][1]
-            p = torch.exp(_scores(q, k, cur[1] if kmask is not None else None, scale, causal and j == r) - lse)
-            dkv[1] += torch.matmul(p.transpose(-1, -2).to(dout.dtype), dout).float()
-            dp = torch.matmul(dout, v.transpose(-1, -2)).float()
-            ds = (p * (dp - delta) * scale).to(q.dtype)
-            dq += torch.matmul(ds, k).float()
-            dkv[0] += torch.matmul(ds.transpose(-1, -2), q).float()
+            kv = cur[0]
+            gq, gk, gv = _block_bwd(dout, q, kv[:, :H], kv[:, H:], out, lse, cur[1] if kmask is not None else None,
+                                    B, S_l, NH, D, scale, causal and j == r)
+            dq += gq.float()
+            dkv[:, :H] += gk.float()
+            dkv[:, H:] += gv.float()
+        if P == 1:
+            break
         # the K/V block moves on with its gradient; the last hop only returns dK/dV to the owner
         (nxt, reqs) = _rotate(comm, ([dkv] + cur) if s < P - 1 else [dkv])
         for w in reqs:
@@ -115,7 +166,7 @@ def ring_attention_bwd(dout, q, kv, kmask, out, lse, comm, causal=False, scale=N
         dkv = nxt[0]
         if s < P - 1:
             cur = nxt[1:]
-    return dq, dkv
+    return torch.cat([dq, dkv], 1).to(qkv.dtype)
 
 
 class RingAttentionOp(Op):
@@ -141,11 +192,9 @@ class RingAttentionOp(Op):
         H = qkv.shape[1] // 3
         D = H // self.NH
         assert qkv.shape[0] == self.B * self.S_l, (qkv.shape, self.B, self.S_l)
-        q, kv = _split(qkv, self.B, self.S_l, self.NH, D)
         kmask = input_vals[1].reshape(self.B, self.S_l) if self.has_mask else None
-        out, lse = ring_attention_fwd(q, kv, kmask, comm, self.causal, self.scale)
-        flat = out.permute(0, 2, 1, 3).reshape(self.B * self.S_l, H)
-        return AuxResult(flat, (q, kv, kmask, out, lse))
+        out, lse = ring_attention_fwd(qkv, kmask, comm, self.B, self.S_l, self.NH, self.causal, self.scale)
+        return AuxResult(out, (qkv, kmask, lse))
 
     def gradient(self, output_grad):
         return [RingAttentionGradientOp(output_grad, self, ctx=self.raw_ctx)] + ([None] if self.has_mask else [])
@@ -163,12 +212,8 @@ class RingAttentionGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         f = self.fwd
-        dflat, (_, (q, kv, kmask, out, lse)) = input_vals
-        B, NH, S_l, D = q.shape
-        dout = dflat.reshape(B, S_l, NH, D).permute(0, 2, 1, 3)
-        dq, dkv = ring_attention_bwd(dout, q, kv, kmask, out, lse, f.comm, f.causal, f.scale)
-        d = torch.cat([dq.unsqueeze(0), dkv], 0)                        # [3, B, NH, S_l, D]
-        return d.permute(1, 3, 0, 2, 4).reshape(B * S_l, 3 * NH * D).to(dflat.dtype)
+        dout, (out, (qkv, kmask, lse)) = input_vals
+        return ring_attention_bwd(dout, qkv, kmask, out, lse, f.comm, f.B, f.S_l, f.NH, f.causal, f.scale)
 
     def gradient(self, output_grad):
         raise NotImplementedError

@@ -23,6 +23,13 @@ RUNS = [
     ['examples/moe/test_moe.py', '--gpu', '-1', '--batch_size', '2', '--num_tokens', '32', '--model_dim', '16',
      '--hidden_size', '32', '--num_steps', '2', '--gate', 'top'],
     ['examples/gnn/run_single.py', '--gpu', '-1', '--nodes', '500', '--epochs', '2'],
+    ['examples/rec/run_hetu.py', '--gpu', '-1', '--nepoch', '1', '--steps', '3', '--batch-size', '256', '--val'],
+    ['examples/nlp/train_hetu_transformer.py', '--gpu', '-1', '--vocab_size', '200', '--d_model', '32', '--d_ff',
+     '64', '--num_blocks', '1', '--num_heads', '4', '--maxlen1', '8', '--maxlen2', '9', '--batch_size', '4',
+     '--steps', '2'],
+    ['examples/runner/run_mlp.py', '--gpu', '-1', '--steps', '5'],
+    ['bin/heturun', '-w', '2', sys.executable, 'examples/runner/run_mlp.py', '--comm-mode', 'AllReduce',
+     '--steps', '5'],
 ]
 
 

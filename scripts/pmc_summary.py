@@ -1,0 +1,74 @@
+"""Summarise rocprofv3 --pmc passes (scripts/gpu_pmc.sh) per kernel family.
+
+    python scripts/pmc_summary.py gpurun_out/pmc_sq gpurun_out/pmc_mem gpurun_out/pmc_wr > profiles/x.txt
+
+Per kernel family (template arguments and parameter lists stripped) it sums the
+counters over every dispatch and derives:
+  ms       = summed dispatch time (the --pmc run serialises dispatches)
+  clk_GHz  = GRBM_GUI_ACTIVE / 8 / time (GRBM is summed over the 8 XCDs)
+  mfma_pk  = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * GRBM_GUI_ACTIVE / 8): the
+             fraction of the chip's matrix-pipe cycles that were busy, i.e. the
+             fraction of dense bf16 MFMA peak at the running clock
+  wait     = SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt/barrier)
+  lds_cf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+  rd_TB/s  = 2 * FETCH_SIZE KB / time (FETCH_SIZE reads 1/2 of a wide coalesced
+             stream on gfx950, MI355X_MICROARCH.md); wr_TB/s = WRITE_SIZE KB / time
+"""
+import collections
+import csv
+import glob
+import os
+import re
+import sys
+
+
+def family(name):
+    n = re.sub(r'\(.*', '', name)
+    n = re.sub(r'^void ', '', n)
+    if n.startswith('igemm_'):
+        return n.split('_gtcx')[0] + ' (MIOpen)'
+    return n[:90]
+
+
+def load(d):
+    """-> ({family: {counter: sum}}, {family: n_dispatches}, {family: summed dispatch ns})"""
+    files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    seen = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            k = family(r['Kernel_Name'])
+            agg[k][r['Counter_Name']] += float(r['Counter_Value'])
+            seen[r['Dispatch_Id']] = (k, int(r['End_Timestamp']) - int(r['Start_Timestamp']))
+    calls, ns = collections.Counter(), collections.defaultdict(float)
+    for k, t in seen.values():
+        calls[k] += 1
+        ns[k] += t
+    return agg, calls, ns
+
+
+def main(dirs):
+    sq, calls, ns = load(dirs[0])
+    mem = load(dirs[1]) if len(dirs) > 1 else ({}, {}, {})
+    wr = load(dirs[2]) if len(dirs) > 2 else ({}, {}, {})
+    rows = sorted(sq.items(), key=lambda kv: -ns[kv[0]])
+    print('%-64s %6s %8s %8s %8s %8s %8s %8s %7s' % ('kernel family', 'calls', 'ms', 'clk_GHz', 'mfma_pk',
+                                                     'wait', 'lds_cf', 'rd_TB/s', 'wr_TB/s'))
+    for k, c in rows[:40]:
+        t = ns[k] * 1e-9
+        cyc = c.get('GRBM_GUI_ACTIVE', 0) / 8.0                      # summed over 8 XCDs
+        clk = cyc / t / 1e9 if t else float('nan')
+        mf = c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / (1024.0 * cyc) if cyc else float('nan')
+        wc = c.get('SQ_WAVE_CYCLES', 0)
+        wait = c.get('SQ_WAIT_ANY', 0) / wc if wc else float('nan')
+        lds = mem[0].get(k, {}).get('SQ_LDS_IDX_ACTIVE', 0)
+        lc = c.get('SQ_LDS_BANK_CONFLICT', 0) / lds if lds else float('nan')
+        tm = mem[2].get(k, 0) * 1e-9
+        rd = 2 * mem[0].get(k, {}).get('FETCH_SIZE', 0) * 1024 / tm / 1e12 if tm else float('nan')
+        tw = wr[2].get(k, 0) * 1e-9
+        w = wr[0].get(k, {}).get('WRITE_SIZE', 0) * 1024 / tw / 1e12 if tw else float('nan')
+        print('%-64s %6d %8.2f %8.2f %8.3f %8.3f %8.3f %8.2f %7.2f' % (k[:64], calls[k], t * 1e3, clk, mf, wait, lc, rd, w))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1:])

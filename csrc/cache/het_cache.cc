@@ -135,7 +135,7 @@ class Cache {
   Cache(int policy, int64_t limit, int64_t rows, int64_t width, int key, int64_t pull_bound,
         int64_t push_bound)
       : limit_(limit), rows_(rows), width_(width), key_(key), pull_bound_(pull_bound),
-        push_bound_(push_bound) {
+        push_bound_(push_bound), policy_(policy) {
     if (policy == 0) pol_.reset(new LRU());
     else pol_.reset(new LFU(policy == 2));
   }
@@ -246,6 +246,14 @@ class Cache {
     std::lock_guard<std::mutex> g(mu_);
     return (int64_t)pol_->size();
   }
+  // drop every cached line without pushing (after the server's table was
+  // replaced, e.g. a checkpoint load): the next lookup re-pulls all rows
+  void clear() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (policy_ == 0) pol_.reset(new LRU());
+    else pol_.reset(new LFU(policy_ == 2));
+    live_.clear();
+  }
   void set_bounds(int64_t pull, int64_t push) { pull_bound_ = pull; push_bound_ = push; }
   void set_bypass(bool b) { bypass_ = b; }
   void set_perf(bool b) { perf_ = b; }
@@ -300,6 +308,7 @@ class Cache {
   int64_t limit_, rows_, width_;
   int key_;
   int64_t pull_bound_, push_bound_;
+  int policy_;
   bool bypass_ = false, perf_ = false;
   std::unique_ptr<Policy> pol_;
   std::unordered_map<int64_t, LineP> live_;
@@ -441,6 +450,12 @@ int hc_flush(int h) {
   Cache* c = get(h);
   if (!c) return -1;
   c->flush_all();
+  return 0;
+}
+int hc_clear(int h) {
+  Cache* c = get(h);
+  if (!c) return -1;
+  c->clear();
   return 0;
 }
 int64_t hc_size(int h) {

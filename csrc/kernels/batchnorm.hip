@@ -73,10 +73,12 @@ __global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x,
 #pragma unroll
   for (int i = 0; i < V; ++i) { sh_s[t * V + i] = s[i]; sh_q[t * V + i] = q[i]; }
   __syncthreads();
-  // one thread per channel of the tile folds the RP row-partials
+  // fold the RP row-partials per channel of the tile; a tile holds W*V channels
+  // (up to 512 for bf16), more than the 256 threads, so each thread folds
+  // every 256th channel
   const int nch = W * V;
-  if (t < nch) {
-    const int c_local = t, colw = c_local / V, lane_i = c_local % V;
+  for (int c_local = t; c_local < nch; c_local += 256) {
+    const int colw = c_local / V, lane_i = c_local % V;
     float S = 0.f, Q = 0.f;
     for (int rr = 0; rr < RP; ++rr) {
       int tt = rr * W + colw;
@@ -283,16 +285,16 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
 #pragma unroll
   for (int i = 0; i < V; ++i) { sh_s[t * V + i] = s[i]; sh_q[t * V + i] = q[i]; }
   __syncthreads();
-  const int nch = W * V;
-  if (t < nch) {
-    const int colw = t / V, lane_i = t % V;
+  const int nch = W * V;   // up to 512 channels per tile (bf16): 2 per thread
+  for (int c_local = t; c_local < nch; c_local += 256) {
+    const int colw = c_local / V, lane_i = c_local % V;
     float S = 0.f, Q = 0.f;
     for (int rr = 0; rr < RP; ++rr) {
       int tt = rr * W + colw;
       S += sh_s[tt * V + lane_i];
       Q += sh_q[tt * V + lane_i];
     }
-    const int c = blockIdx.y * W * V + t;
+    const int c = blockIdx.y * W * V + c_local;
     if (c < C) {
       ws_sdy[(int64_t)c * gridDim.x + blockIdx.x] = S;
       ws_sdyx[(int64_t)c * gridDim.x + blockIdx.x] = Q;

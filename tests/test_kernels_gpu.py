@@ -46,8 +46,10 @@ def test_binary_modes(op, dt):
 
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('relu,res', [(False, False), (True, False), (True, True)])
-def test_batchnorm_nhwc(dt, relu, res):
-    N, C, H, W = 8, 64, 14, 14
+@pytest.mark.parametrize('N,C,H,W', [(8, 64, 14, 14), (2, 512, 28, 28), (2, 1024, 14, 14), (2, 2048, 7, 7)])
+def test_batchnorm_nhwc(dt, relu, res, N, C, H, W):
+    # C >= 512 in bf16 puts 512 channels in one stats tile (more than the 256
+    # threads that fold it): the ResNet-50 stage 2-4 shapes
     x = torch.randn(N, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
     r = torch.randn(N, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last) if res else None
     scale = torch.rand(C, device=DEV) + 0.5

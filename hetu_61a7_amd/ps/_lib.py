@@ -60,6 +60,7 @@ _SIGS = {
     'hc_async_push_pull': ([I32, P, I64, P, P, I64, P], I64),
     'hc_wait': ([I64], I32),
     'hc_flush': ([I32], I32),
+    'hc_clear': ([I32], I32),
     'hc_size': ([I32], I64),
     'hc_set_bounds': ([I32, I64, I64], I32),
     'hc_set_bypass': ([I32, I32], I32),

@@ -74,6 +74,11 @@ class CacheSparseTable(object):
     def size(self):
         return lib('hc_size')(self.handle)
 
+    def clear(self):
+        """Drop every cached line without pushing it (the server's table was
+        replaced, e.g. by a checkpoint load); later lookups re-pull."""
+        lib('hc_clear')(self.handle)
+
     def bypass(self, on=True):
         lib('hc_set_bypass')(self.handle, int(on))
 

@@ -207,6 +207,16 @@ class PSTable(object):
         if self.cache is not None:
             self.cache.flush()
 
+    def invalidate(self):
+        """Forget every worker-side copy of the table's rows (after the server
+        loaded a checkpoint): pending pushes are drained first by ``close``."""
+        self.close()
+        if self.prefetched is not None:
+            self.cache.wait(self.prefetched[2])
+            self.prefetched = None
+        if self.cache is not None:
+            self.cache.clear()
+
     def to_dense(self):
         """Full table (host) -- checkpointing / tests."""
         self._wait_push()
@@ -241,6 +251,10 @@ class PSDense(object):
         if self.bsp and self.bsp > 0:
             self.agent.ssp_init(key, self.agent.nrank(), self.bsp)
         self.version = 0
+
+    def repull(self):
+        """Reload the worker's copy from the server (after a checkpoint load)."""
+        self._pull_into_device()
 
     def _pull_into_device(self):
         t = self.agent.Pull(self.key, self.pull_buf)

@@ -1,17 +1,31 @@
 """Checkpoint / resume.
 
 Format-compatible with the reference (``executor.py:457-537``): a pickle of
-``{param.name: np.float32 ndarray}`` written by rank 0; PS-held parameters are
-written by the servers as raw float32 ``<dir>/<node_id>_<partition>.dat``.
+``{param.name: np.float32 ndarray}`` written by rank 0 for every parameter the
+worker holds; PS-held parameters (embedding tables in PS/Hybrid mode, the flat
+dense buffer in pure PS mode) are written by the server as raw float32
+``<dir>/<node_id>_<partition>.dat`` (reference ``PSAgent.h:447-476``,
+``PSFHandle.h:389-427``): workers drain their pending pushes, meet at a
+worker barrier, worker 0 issues SaveParam/LoadParam per PS key, and a second
+barrier releases everyone.  After a load every HET cache is invalidated and
+PS-held dense parameters are re-pulled.
 
 Extension (opt-in, ``save_optimizer=True``): ``<file>.ext`` holds optimizer
-states (flat m/v/velocity), step counters, BN running statistics and LR
-scheduler state -- none of which the reference saves.
-Loading never unpickles foreign files with code execution beyond plain numpy
-arrays (``numpy`` arrays inside a dict; use trusted checkpoints only).
+states (flat m/v/velocity, per-table sparse states), step counters, BN running
+statistics and LR-scheduler state -- none of which the reference saves
+(SURVEY §5.4).  With ZeRO-1 each rank owns a 1/P shard of the flat optimizer
+state; it is written by that rank to ``<file>.ext.rank<r>`` and read back by
+the same rank.
+
+Loading uses a restricted unpickler that only reconstructs numpy arrays and
+builtin containers/scalars, so a foreign checkpoint cannot run code.
+Every file is fsynced before it becomes reachable, and resumable snapshots
+are published by an atomic rename of ``<dir>/latest`` followed by a
+directory fsync.
 """
 from __future__ import annotations
 
+import io
 import os
 import pickle
 
@@ -19,59 +33,204 @@ import numpy as np
 import torch
 
 
+# ---------------------------------------------------------------------------
+# safe (de)serialisation
+
+_SAFE_GLOBALS = {
+    ('builtins', n) for n in ('dict', 'list', 'tuple', 'set', 'frozenset', 'int', 'float', 'bool',
+                              'str', 'bytes', 'bytearray', 'complex', 'slice', 'range')
+} | {
+    ('collections', 'OrderedDict'),
+    ('_codecs', 'encode'),             # protocol-2 pickles spell bytes this way
+    ('numpy', 'ndarray'), ('numpy', 'dtype'),
+    ('numpy.core.multiarray', '_reconstruct'), ('numpy.core.multiarray', 'scalar'),
+    ('numpy._core.multiarray', '_reconstruct'), ('numpy._core.multiarray', 'scalar'),
+    ('numpy.core.numeric', '_frombuffer'), ('numpy._core.numeric', '_frombuffer'),   # protocol 5
+}
+
+
+class _SafeUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        if (module, name) in _SAFE_GLOBALS:
+            return super().find_class(module, name)
+        if module == 'numpy' and name.endswith('DType'):
+            return super().find_class(module, name)
+        if module in ('numpy.dtypes',) and name.endswith('DType'):
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError('checkpoint refers to %s.%s, which a checkpoint may not '
+                                     'contain (only numpy arrays and builtin values)' % (module, name))
+
+
+def safe_load(f):
+    """Unpickle ``f`` allowing only numpy arrays and builtin values."""
+    return _SafeUnpickler(f).load()
+
+
+def _fsync_dir(path):
+    try:
+        fd = os.open(path, os.O_RDONLY)
+    except OSError:
+        return
+    try:
+        os.fsync(fd)
+    except OSError:
+        pass
+    finally:
+        os.close(fd)
+
+
+def _write_durable(path, obj):
+    """Pickle ``obj`` to ``path`` via a temporary file: written, fsynced, renamed."""
+    tmp = '%s.tmp.%d' % (path, os.getpid())
+    with open(tmp, 'wb') as f:
+        pickle.dump(obj, f, protocol=4)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+def _read(path):
+    with open(path, 'rb') as f:
+        return safe_load(io.BufferedReader(f))
+
+
+# ---------------------------------------------------------------------------
+# parameter views
+
 def _params(ex):
     from ..ops.variable import PlaceholderOp
     return [n for n in ex.config.placeholder_to_arr_map if isinstance(n, PlaceholderOp) and n.trainable]
 
 
+def _ps_tables(ex):
+    from ..ps.table import PSTable
+    return [(n, t) for n, t in ex.config.placeholder_to_arr_map.items() if isinstance(t, PSTable)]
+
+
+def _opt_ops(ex):
+    return [op for sub in ex.subexecutor.values() for op in getattr(sub, 'opt_ops', [])]
+
+
+def _ps_dense(ex):
+    return [op.ps_dense for op in _opt_ops(ex) if getattr(op, 'ps_dense', None) is not None]
+
+
 def state_dict(ex):
+    """``{name: float32 ndarray}`` of every worker-held trainable parameter (PS
+    tables are saved by the server, not here)."""
     out = {}
     for n in _params(ex):
         t = ex.config.placeholder_to_arr_map[n]
+        if not isinstance(t, torch.Tensor):
+            continue
         out[n.name] = t.detach().float().cpu().numpy().astype(np.float32)
     return out
 
 
+def _zero_rank(ex):
+    for op in _opt_ops(ex):
+        if getattr(op, 'zero', False) and op.comm is not None:
+            return op.comm.rank
+    return None
+
+
+# ---------------------------------------------------------------------------
+# save
+
+def _ps_save(ex, file_path):
+    """Reference executor.py:465-481: drain, barrier, worker 0 -> SaveParam per
+    PS key, barrier."""
+    agent = ex.config.ps_comm
+    tables = _ps_tables(ex)
+    for _, t in tables:
+        t.close()                      # flush staged grads, wait pushes, flush cache lines
+    agent.BarrierWorker()
+    if agent.rank() == 0:
+        os.makedirs(file_path, exist_ok=True)
+        for _, t in tables:
+            agent.SaveParam(t.key, file_path)
+        for d in _ps_dense(ex):
+            agent.SaveParam(d.key, file_path)
+        for name in os.listdir(file_path):
+            if name.endswith('.dat'):
+                with open(os.path.join(file_path, name), 'rb') as f:
+                    os.fsync(f.fileno())
+        _fsync_dir(file_path)
+    agent.BarrierWorker()
+
+
+def _ext_state(ex, zero_rank):
+    ext = {'optimizers': [], 'bn': {}}
+    for op in _opt_ops(ex):
+        fl = op.flat
+        d = {'step': op.step, 'name': op.name, 'zero': bool(getattr(op, 'zero', False))}
+        if fl is not None:
+            d['order'] = [p.name for p in fl.params]
+            if not d['zero']:   # ZeRO shards go to the per-rank file
+                d['s1'] = fl.s1.cpu().numpy() if fl.s1 is not None else None
+                d['s2'] = fl.s2.cpu().numpy() if fl.s2 is not None else None
+        d['sparse'] = {p.name: {k: v.detach().float().cpu().numpy() for k, v in st.items()}
+                       for p, st in op.sparse_state.items()}
+        lr = op.optimizer.learning_rate
+        if hasattr(lr, 'state_dict'):
+            d['lr_sched'] = lr.state_dict()
+        ext['optimizers'].append(d)
+    for sub in ex.subexecutor.values():
+        for n in sub.topo_order:
+            if getattr(n, 'running_mean', None) is not None:
+                ext['bn'][n.name] = (n.running_mean.cpu().numpy(), n.running_var.cpu().numpy())
+    return ext
+
+
+def _zero_shards(ex):
+    out = []
+    for op in _opt_ops(ex):
+        fl = op.flat
+        if not getattr(op, 'zero', False) or fl is None:
+            out.append(None)
+            continue
+        out.append({'s1': fl.s1.cpu().numpy() if fl.s1 is not None else None,
+                    's2': fl.s2.cpu().numpy() if fl.s2 is not None else None,
+                    'nrank': op.comm.nrank, 'rank': op.comm.rank})
+    return out
+
+
 def save(ex, file_path, file_name='checkpoint.pkl', save_optimizer=False):
+    """Write the checkpoint; every rank must call it (PS barriers, ZeRO shards).
+    Returns the pickle path on the rank that wrote it, else None."""
     cfg = ex.config
     if cfg.ps_comm is not None:
-        cfg.ps_comm.save_params(file_path)
-    if cfg.nrank > 1 and cfg.rank != 0 and cfg.comm_mode in ('AllReduce', 'Hybrid'):
+        _ps_save(ex, file_path)
+    path = os.path.join(file_path, file_name)
+    zr = _zero_rank(ex) if save_optimizer else None
+    if zr is not None:
+        os.makedirs(file_path, exist_ok=True)
+        _write_durable('%s.ext.rank%d' % (path, zr), _zero_shards(ex))
+    writer = not (cfg.nrank > 1 and cfg.rank != 0 and cfg.comm_mode in ('AllReduce', 'Hybrid'))
+    if cfg.ps_comm is not None and cfg.comm_mode == 'PS':
+        writer = cfg.ps_comm.rank() == 0
+    if not writer:
         return None
     os.makedirs(file_path, exist_ok=True)
-    st = state_dict(ex)
-    path = os.path.join(file_path, file_name)
-    with open(path, 'wb') as f:
-        pickle.dump(st, f)
+    _write_durable(path, state_dict(ex))
     if save_optimizer:
-        ext = {'optimizers': [], 'bn': {}}
-        for sub in ex.subexecutor.values():
-            for op in getattr(sub, 'opt_ops', []):
-                fl = op.flat
-                d = {'step': op.step, 'name': op.name}
-                if fl is not None:
-                    d['order'] = [p.name for p in fl.params]
-                    d['s1'] = fl.s1.cpu().numpy() if fl.s1 is not None else None
-                    d['s2'] = fl.s2.cpu().numpy() if fl.s2 is not None else None
-                lr = op.optimizer.learning_rate
-                if hasattr(lr, 'state_dict'):
-                    d['lr_sched'] = lr.state_dict()
-                ext['optimizers'].append(d)
-            for n in sub.topo_order:
-                if getattr(n, 'running_mean', None) is not None:
-                    ext['bn'][n.name] = (n.running_mean.cpu().numpy(), n.running_var.cpu().numpy())
-        with open(path + '.ext', 'wb') as f:
-            pickle.dump(ext, f)
+        _write_durable(path + '.ext', _ext_state(ex, zr))
+    _fsync_dir(file_path)
     return path
 
+
+# ---------------------------------------------------------------------------
+# load
 
 def load_dict(ex, state, consider_splits=False):
     cfg = ex.config
     for n in _params(ex):
         if n.name not in state:
             continue
-        v = np.asarray(state[n.name], dtype=np.float32)
         t = cfg.placeholder_to_arr_map[n]
+        if not isinstance(t, torch.Tensor):
+            continue
+        v = np.asarray(state[n.name], dtype=np.float32)
         src = torch.from_numpy(v)
         if consider_splits and n.mp_split is not None:
             src = n.mp_split.slice_tensor(src)
@@ -79,37 +238,74 @@ def load_dict(ex, state, consider_splits=False):
         cv = cfg.compute_values.get(n)
         if cv is not None:
             cv.copy_(t)
+    for op in _opt_ops(ex):   # refresh the bf16 shadow of the flat master
+        if op.flat is not None and op.flat.shadow is not None:
+            op.flat.shadow.copy_(op.flat.param)
+
+
+def _ps_load(ex, file_path):
+    agent = ex.config.ps_comm
+    tables = _ps_tables(ex)
+    for _, t in tables:
+        t.close()
+    agent.BarrierWorker()
+    if agent.rank() == 0:
+        for _, t in tables:
+            agent.LoadParam(t.key, file_path)
+        for d in _ps_dense(ex):
+            agent.LoadParam(d.key, file_path)
+    agent.BarrierWorker()
+    for _, t in tables:
+        t.invalidate()
+    for d in _ps_dense(ex):
+        d.repull()
 
 
 def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
     cfg = ex.config
     path = os.path.join(file_path, file_name)
-    with open(path, 'rb') as f:
-        st = pickle.load(f)
-    load_dict(ex, st, consider_splits)
+    load_dict(ex, _read(path), consider_splits)
     if cfg.ps_comm is not None:
-        cfg.ps_comm.load_params(file_path)
+        _ps_load(ex, file_path)
     ext_path = path + '.ext'
-    if os.path.exists(ext_path):
-        with open(ext_path, 'rb') as f:
-            ext = pickle.load(f)
-        ops = [op for sub in ex.subexecutor.values() for op in getattr(sub, 'opt_ops', [])]
-        for op, d in zip(ops, ext.get('optimizers', [])):
-            op.step = d['step']
-            if op.flat is not None and d.get('s1') is not None and op.flat.s1 is not None:
-                op.flat.s1.copy_(torch.from_numpy(d['s1']))
-            if op.flat is not None and d.get('s2') is not None and op.flat.s2 is not None:
-                op.flat.s2.copy_(torch.from_numpy(d['s2']))
-            lr = op.optimizer.learning_rate
-            if 'lr_sched' in d and hasattr(lr, 'load_state_dict'):
-                lr.load_state_dict(d['lr_sched'])
-        for sub in ex.subexecutor.values():
-            for n in sub.topo_order:
-                if n.name in ext.get('bn', {}):
-                    m, v = ext['bn'][n.name]
-                    dev = cfg.device
-                    n.running_mean = torch.from_numpy(m).to(dev)
-                    n.running_var = torch.from_numpy(v).to(dev)
+    if not os.path.exists(ext_path):
+        return
+    ext = _read(ext_path)
+    ops = _opt_ops(ex)
+    zr = _zero_rank(ex)
+    shards = None
+    if zr is not None and os.path.exists('%s.ext.rank%d' % (path, zr)):
+        shards = _read('%s.ext.rank%d' % (path, zr))
+    for i, (op, d) in enumerate(zip(ops, ext.get('optimizers', []))):
+        op.step = d['step']
+        fl = op.flat
+        src = d
+        if getattr(op, 'zero', False):
+            src = shards[i] if shards is not None and i < len(shards) and shards[i] is not None else {}
+            if src and src.get('nrank') != op.comm.nrank:
+                raise ValueError('ZeRO checkpoint was written with %s ranks, resuming with %d'
+                                 % (src.get('nrank'), op.comm.nrank))
+        if fl is not None:
+            for k in ('s1', 's2'):
+                buf = getattr(fl, k)
+                if src.get(k) is not None and buf is not None:
+                    buf.copy_(torch.from_numpy(src[k]).to(buf.device))
+        by_name = {p.name: st for p, st in op.sparse_state.items()}
+        for name, st in d.get('sparse', {}).items():
+            if name in by_name:
+                for k, v in st.items():
+                    if k in by_name[name]:
+                        by_name[name][k].copy_(torch.from_numpy(v).to(by_name[name][k].device))
+        lr = op.optimizer.learning_rate
+        if 'lr_sched' in d and hasattr(lr, 'load_state_dict'):
+            lr.load_state_dict(d['lr_sched'])
+    for sub in ex.subexecutor.values():
+        for n in sub.topo_order:
+            if n.name in ext.get('bn', {}):
+                m, v = ext['bn'][n.name]
+                dev = cfg.device
+                n.running_mean = torch.from_numpy(m).to(dev)
+                n.running_var = torch.from_numpy(v).to(dev)
 
 
 # ---------------------------------------------------------------------------
@@ -117,31 +313,41 @@ def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
 # A snapshot is a directory ``<dir>/step_<N>/`` holding the reference-format
 # pickle plus the ``.ext`` optimizer/BN/scheduler state; it becomes visible
 # only when ``<dir>/latest`` (a one-line text file, replaced by an atomic
-# rename) names it, so a worker killed mid-write never leaves a torn
-# checkpoint behind.  Rank 0 writes; every rank reads.
+# rename) names it.  Every snapshot file and the snapshot directory are
+# fsynced before ``latest`` moves, and ``<dir>`` is fsynced after, so a crash
+# never leaves ``latest`` naming a torn snapshot.  Every rank calls it.
+
+def _barrier(ex):
+    cfg = ex.config
+    if cfg.nrank > 1 and cfg.comm_mode in ('AllReduce', 'Hybrid'):
+        from ..parallel import comm
+        comm.world().barrier()
+    elif cfg.ps_comm is not None:
+        cfg.ps_comm.BarrierWorker()
+
 
 def save_resumable(ex, ckpt_dir, step, keep=2):
     """Commit a full snapshot (weights + optimizer state) taken after ``step``
     completed steps.  Returns the snapshot path on the writing rank."""
-    cfg = ex.config
     sub = os.path.join(ckpt_dir, 'step_%d' % step)
     path = save(ex, sub, save_optimizer=True)
+    _barrier(ex)                      # every rank's ZeRO shard is durable
     if path is not None:
+        _fsync_dir(sub)
         tmp = os.path.join(ckpt_dir, '.latest.%d' % os.getpid())
         with open(tmp, 'w') as f:
             f.write('step_%d\n' % step)
             f.flush()
             os.fsync(f.fileno())
         os.replace(tmp, os.path.join(ckpt_dir, 'latest'))
+        _fsync_dir(ckpt_dir)
         snaps = sorted((d for d in os.listdir(ckpt_dir) if d.startswith('step_')),
                        key=lambda d: int(d[5:]))
         for d in snaps[:-keep] if keep else []:
             if d != 'step_%d' % step:
                 import shutil
                 shutil.rmtree(os.path.join(ckpt_dir, d), ignore_errors=True)
-    if cfg.nrank > 1 and cfg.comm_mode in ('AllReduce', 'Hybrid'):
-        from ..parallel import comm
-        comm.world().barrier()
+    _barrier(ex)
     return path
 
 

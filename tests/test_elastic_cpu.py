@@ -19,6 +19,7 @@ JOB = textwrap.dedent('''
     from hetu_61a7_amd.utils import checkpoint
     from hetu_61a7_amd.parallel import comm
     ckpt, out, crash_at = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    zero = len(sys.argv) > 4 and sys.argv[4] == 'zero'
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     attempt = int(os.environ.get('HETU_RESTART_COUNT', '0'))
     rng = np.random.RandomState(5)
@@ -27,8 +28,14 @@ JOB = textwrap.dedent('''
     W2 = ht.Variable(name='w2', value=(rng.randn(16, 3) * 0.3).astype(np.float32))
     loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(
         ht.matmul_op(ht.relu_op(ht.matmul_op(x, W1)), W2), y_), [0])
-    train = ht.optim.MomentumOptimizer(0.05, 0.9).minimize(loss)
-    ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'))
+    if zero:   # ZeRO-1: every rank owns half of the Adam moments
+        train = ht.optim.AdamOptimizer(0.01).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'),
+                         zero=1, bucket_mb=0.001)
+        assert train.zero
+    else:
+        train = ht.optim.MomentumOptimizer(0.05, 0.9).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'))
     start = checkpoint.resume(ex, ckpt)
     for step in range(start, 10):
         r = np.random.RandomState(1000 + step * world + rank)   # data keyed by (step, rank)
@@ -45,7 +52,7 @@ JOB = textwrap.dedent('''
 ''')
 
 
-def _run(tmp_path, tag, crash_at, restarts):
+def _run(tmp_path, tag, crash_at, restarts, extra=()):
     script = tmp_path / 'job.py'
     script.write_text(JOB)
     ckpt, out = tmp_path / ('ckpt_' + tag), tmp_path / (tag + '.npz')
@@ -53,7 +60,7 @@ def _run(tmp_path, tag, crash_at, restarts):
     env.pop('MASTER_PORT', None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'bin', 'heturun'), '-w', '2',
                         '--max-restarts', str(restarts), sys.executable, str(script),
-                        str(ckpt), str(out), str(crash_at)],
+                        str(ckpt), str(out), str(crash_at)] + list(extra),
                        env=env, capture_output=True, text=True, timeout=240)
     return r, out, ckpt
 
@@ -75,3 +82,20 @@ def test_restart_resumes_from_last_snapshot(tmp_path):
 def test_no_restart_propagates_failure(tmp_path):
     r, _, _ = _run(tmp_path, 'fail', crash_at=4, restarts=0)
     assert r.returncode == 3
+
+
+def test_zero1_restart_restores_every_rank_shard(tmp_path):
+    """ZeRO-1 + Adam: each rank's 1/P moment shard is written to its own
+    ``.ext.rank<r>`` file and read back by that rank, so the resumed run ends
+    exactly where the uninterrupted one does (a rank restored from another
+    rank's shard would drift)."""
+    ref, ref_out, _ = _run(tmp_path, 'zref', crash_at=-1, restarts=0, extra=['zero'])
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    r, out, ckpt = _run(tmp_path, 'zel', crash_at=7, restarts=1, extra=['zero'])
+    assert r.returncode == 0, r.stderr[-2000:]
+    a, b = np.load(ref_out), np.load(out)
+    assert int(b['start']) == 6
+    for k in ('w1', 'w2'):
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6)
+    snap = os.listdir(os.path.join(ckpt, 'step_9'))
+    assert 'checkpoint.pkl.ext.rank0' in snap and 'checkpoint.pkl.ext.rank1' in snap

@@ -145,3 +145,42 @@ def test_moe_top_bf16_step():
     l2 = [float(np.asarray(ex2.run('train', feed_dict={x2: X2}, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0])
           for _ in range(8)]
     assert np.isfinite(l2).all() and l2[-1] < l2[0], l2
+
+
+def test_bert_base_width_bf16_forward_matches_fp32():
+    """BERT-base widths (hidden 768, 12 heads, FFN 3072, seq 128) with two layers:
+    the bf16 forward (fused attention, fused LayerNorm tails, MFMA GEMMs) stays
+    close to the fp32 forward on identical weights."""
+    from hetu_61a7_amd.models.bert import BertConfig, bert_pretrain_graph, synthetic_bert_batch
+    from hetu_61a7_amd.ops import node as _node
+    cfg = BertConfig(num_hidden_layers=2, batch_size=4, seq_len=128, hidden_dropout_prob=0.0,
+                     attention_probs_dropout_prob=0.0)
+    out = []
+    for mp in (None, 'bf16'):
+        _node.G_NODE_ID = 0
+        feeds, loss, train = bert_pretrain_graph(cfg, lr=0.0)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=5, mixed_precision=mp)
+        fd = {feeds[k]: v for k, v in synthetic_bert_batch(cfg, seed=1).items()}
+        out.append(float(np.asarray(ex.run('train', feed_dict=fd, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0]))
+    assert np.isfinite(out).all(), out
+    assert abs(out[1] - out[0]) < 0.02 * abs(out[0]), out
+
+
+def test_moe_d2048_bf16_forward_matches_fp32():
+    """The bench MoE shape class (d_model 2048, top-2, 4 experts): bf16 loss
+    tracks fp32 on identical weights and batch."""
+    from hetu_61a7_amd.models.moe import moe_top, moe_random_batch
+    from hetu_61a7_amd.ops import node as _node
+    B, T, d = 2, 256, 2048
+    X, Y = moe_random_batch(B, T, d)
+    out = []
+    for mp in (None, 'bf16'):
+        _node.G_NODE_ID = 0
+        x, y_ = ht.Variable(name='x', trainable=False), ht.Variable(name='y_', trainable=False)
+        loss, _ = moe_top(x, y_, B, T, d, 2048, 4, top=2)
+        train = ht.optim.SGDOptimizer(0.0).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision=mp, seed=3)
+        out.append(float(np.asarray(ex.run('train', feed_dict={x: X, y_: Y},
+                                           convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0]))
+    assert np.isfinite(out).all(), out
+    assert abs(out[1] - out[0]) < 0.03 * abs(out[0]) + 1e-3, out

@@ -20,19 +20,58 @@ CL = torch.channels_last
 MODE = os.environ.get('HETU_CONV', 'auto')  # hip | vendor | auto (per-shape measured choice)
 
 
-def _pick(key, hip, vendor):
+def _pick(key, hip, vendor, blas=None):
+    """hip: hand-written implicit GEMM; vendor: MIOpen; blas: a 1x1 convolution
+    run as the plain library GEMM it is (hipBLASLt), where applicable."""
     if MODE == 'hip':
         r = hip()
         return r if r is not None else vendor()
     if MODE == 'vendor':
         return vendor()
     from .autotune import choose
-    c = choose(key, {'hip': hip, 'vendor': vendor})
+    cands = {'hip': hip, 'vendor': vendor}
+    if blas is not None:
+        cands.update(blas)
+    c = choose(key, cands)
+    if c not in ('hip', 'vendor'):
+        r = cands[c]()
+        if r is not None:
+            return r
     if c == 'hip':
         r = hip()
         if r is not None:
             return r
     return vendor()
+
+
+def _plain_1x1(ts, w_shape, stride, padding):
+    """1x1 / stride 1 / no padding on channels-last bf16 tensors ``ts``: the
+    convolution is a plain GEMM over [pixels, channels] views (no copies)."""
+    return (w_shape[2] == 1 and w_shape[3] == 1 and tuple(stride) == (1, 1) and
+            tuple(padding) == (0, 0) and
+            all(t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous(memory_format=CL) for t in ts))
+
+
+def _pad_c(t):
+    """Zero-pad dim 1 (channels) of a channels-last bf16 tensor to a multiple of 8
+    so the implicit-GEMM kernels (16-byte channel chunks) accept it -- the
+    3-channel ResNet stem."""
+    n, c, h, w = t.shape
+    cp = -(-c // 8) * 8
+    buf = torch.zeros((n, h, w, cp), dtype=t.dtype, device=t.device)
+    buf[..., :c].copy_(t.permute(0, 2, 3, 1))
+    return buf.permute(0, 3, 1, 2)
+
+
+def _needs_pad(x, w):
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] % 8 != 0
+            and w.shape[0] % 8 == 0)
+
+
+def _rows(t):
+    """channels-last [N, C, H, W] -> [N*H*W, C] view"""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
 
 
 def _match(x, w):
@@ -50,9 +89,19 @@ def conv2d(x, w, b, stride, padding):
         x = x.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
         from . import conv_igemm
+        blas = None
+        if _plain_1x1((x, w), w.shape, stride, padding):
+            n, _, h, ww_ = x.shape
+            co = w.shape[0]
+
+            def blas_fwd():
+                return torch.mm(_rows(x), w.reshape(co, -1).t()).view(n, h, ww_, co).permute(0, 3, 1, 2)
+            blas = {'blas': blas_fwd}
+        elif _needs_pad(x, w):
+            blas = {'hip_pad': lambda: conv_igemm.try_forward(_pad_c(x), _pad_c(w), stride, padding)}
         y = _pick(('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding)),
                   lambda: conv_igemm.try_forward(x, w, stride, padding),
-                  lambda: F.conv2d(x, w, None, stride, padding))
+                  lambda: F.conv2d(x, w, None, stride, padding), blas)
         if b is not None:
             from .elementwise import binary
             n, c, h, ww = y.shape
@@ -72,9 +121,27 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None):
         if acc is not None:
             acc = acc.contiguous(memory_format=CL)
         from . import conv_igemm
+        blas = None
+        if _plain_1x1((g, w), w.shape, stride, padding) and (acc is None or acc.dtype == torch.bfloat16):
+            n, ci, h, ww_ = x_shape
+            co = w.shape[0]
+
+            def blas_dgrad():
+                w2 = w.reshape(co, ci)
+                d = torch.mm(_rows(g), w2) if acc is None else torch.addmm(_rows(acc), _rows(g), w2)
+                return d.view(n, h, ww_, ci).permute(0, 3, 1, 2)
+            blas = {'blas': blas_dgrad}
+        elif _needs_pad(torch.empty(0, x_shape[1], 1, 1, dtype=g.dtype, device=g.device), w) and acc is None:
+            n, ci, h, ww_ = x_shape
+            cp = -(-ci // 8) * 8
+
+            def pad_dgrad():
+                d = conv_igemm.try_backward_data(g, _pad_c(w), (n, cp, h, ww_), stride, padding)
+                return None if d is None else d[:, :ci]
+            blas = {'hip_pad': pad_dgrad}
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
                      lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
-                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc))
+                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas)
     return _vendor_dgrad(g, w, x_shape, stride, padding, acc)
 
 
@@ -112,10 +179,41 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                 return dw
             out.copy_(dw)
             return out
+        blas = None
+        if _plain_1x1((g, x), w_shape, stride, padding):
+            from .gemm import _vendor_into, _vendor_splitk_into
+            co, ci = w_shape[0], w_shape[1]
+
+            def dest():
+                if out is not None:
+                    return out.reshape(co, ci)
+                return torch.empty((co, ci), dtype=torch.float32, device=g.device)
+
+            def wrap(d):
+                return None if d is None else d.view(co, ci, 1, 1)
+            A, B = _rows(g).t(), _rows(x)
+            blas = {'blas': lambda: wrap(_vendor_into(A, B, dest()))}
+            for sk in (4, 16):
+                if A.shape[1] % sk == 0 and A.shape[1] // sk >= 2048:
+                    blas['blas_sk%d' % sk] = (lambda sk=sk: wrap(_vendor_splitk_into(A, B, dest(), sk)))
+        elif _needs_pad(x, g.new_empty((g.shape[1], 1, 1, 1))):
+            co, ci, kh, kw = w_shape
+            cp = -(-ci // 8) * 8
+
+            def pad_wgrad():
+                d = conv_igemm.try_backward_filter(g, _pad_c(x), (co, cp, kh, kw), stride, padding,
+                                                   accumulate=False)
+                if d is None:
+                    return None
+                if out is None:
+                    return d[:, :ci]
+                out.copy_(d[:, :ci])
+                return out
+            blas = {'hip_pad': pad_wgrad}
         return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
                      lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                             accumulate=False),
-                     vendor)
+                     vendor, blas)
     dw = _vendor_wgrad(g, x, w_shape, stride, padding)
     if out is not None:
         out.copy_(dw)

@@ -190,7 +190,9 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                 return torch.empty((co, ci), dtype=torch.float32, device=g.device)
 
             def wrap(d):
-                return None if d is None else d.view(co, ci, 1, 1)
+                if d is None:
+                    return None
+                return out if out is not None else d.view(co, ci, 1, 1)   # the caller's exact view
             A, B = _rows(g).t(), _rows(x)
             blas = {'blas': lambda: wrap(_vendor_into(A, B, dest()))}
             for sk in (4, 16):

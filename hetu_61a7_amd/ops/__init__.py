@@ -51,6 +51,8 @@ from .moe import (layout_transform_op, layout_transform_gradient_op, reverse_lay
                   reverse_layout_transform_no_gate_gradient_op, balance_assignment_op,
                   sam_group_sum_op, sam_max_op, sammax_grad_op, group_topk_idx_op, topk_gating_op,
                   topk_locations_op)
+from .ps_ops import (parameterServerCommunicate_op, parameterServerSparsePull_op,
+                     ParameterServerCommunicateOp, ParameterServerSparsePullOp)
 from .executor import Executor, HetuConfig, gradients, find_topo_sort
 from .attention import attention_op, AttentionOp, AttentionGradientOp, packed_attention_op
 from .distgcn import distgcn_15d_op, DistGCN_15dOp, make_15d_groups, partition_15d

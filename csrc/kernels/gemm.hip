@@ -111,18 +111,40 @@ __device__ __forceinline__ v8s lds_frag(const char* lds, int rb, int s, int lane
 
 __device__ __forceinline__ const bf16* zchunk() { return g_zero_chunk; }
 
+// Which slot of the staged tile load i of wave w, lane l fills.  `map`:
+//  0  128x128 kernel (4 waves): one 128-row image per operand, 4 loads per wave.
+//  1  256x256 kernel, A operand (2 wave rows x 128 rows, sub-tiles of 64 rows)
+//  2  256x256 kernel, B operand (4 wave columns x 64, sub-tiles of 32)
+//  For 1/2 each operand is staged as two 128-row "half-tile" images (2 loads per wave
+//  each); half h holds the rows every wave reads in ITS h-th sub-tile, so a half can be
+//  restaged as soon as the phase that reads it has passed (gemm_big_kernel).
+__device__ __forceinline__ int half_to_rel(int map, int h, int x) {
+  return map == 1 ? (x >> 6) * 128 + h * 64 + (x & 63) : (x >> 5) * 64 + h * 32 + (x & 31);
+}
+// K-major: returns the operand row (relative to the tile) of the lane's 16-B chunk.
+__device__ __forceinline__ int kmaj_row(int map, int w, int i, int l) {
+  if (map == 0) return 32 * w + 8 * i + (l >> 3);
+  return half_to_rel(map, i >> 1, 16 * w + 8 * (i & 1) + (l >> 3));
+}
+// MN-major: k row of the image and operand column (relative) of the lane's chunk.
+__device__ __forceinline__ void mn_slot(int map, int w, int i, int l, int& k, int& col) {
+  k = map ? 8 * w + 4 * (i & 1) + (l >> 4) : 16 * w + 4 * i + (l >> 4);
+  const int c = (l & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3));  // T10 image, logical chunk
+  col = map ? half_to_rel(map, i >> 1, 8 * c) : 8 * c;
+}
+
 // plain row-major operand with contiguous K: element (r, k) at base[r*ld + k]
 struct PlainK {
   HETU_LINEAR_ROWS
   static constexpr bool KMAJ = true;
   const bf16* base; int64_t ld, rows, K, bstride;
   int64_t roff[4]; bool rok[4]; int ch;
-  __device__ void init(int64_t r0, int w, int l, int64_t batch) {
+  __device__ void init(int64_t r0, int w, int l, int64_t batch, int big) {
     base += batch * bstride;
     ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
+      int64_t r = r0 + kmaj_row(big, w, i, l);
       rok[i] = r < rows;
       roff[i] = r * ld;
     }
@@ -138,19 +160,19 @@ struct PlainMN {
   HETU_LINEAR_ROWS
   static constexpr bool KMAJ = false;
   const bf16* base; int64_t ld, rows, K, bstride;
-  int64_t col[4]; bool cok[4]; int kr;
-  __device__ void init(int64_t r0, int w, int l, int64_t batch) {
+  int64_t col[4]; bool cok[4]; int kk[4];
+  __device__ void init(int64_t r0, int w, int l, int64_t batch, int big) {
     base += batch * bstride;
-    kr = 16 * w + (l >> 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int c = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
-      col[i] = r0 + 8 * c;
+      int c;
+      mn_slot(big, w, i, l, kk[i], c);
+      col[i] = r0 + c;
       cok[i] = col[i] < rows;
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    int64_t k = k0 + kr + 4 * i;
+    int64_t k = k0 + kk[i];
     return (cok[i] && k < K) ? base + k * ld + col[i] : zchunk();
   }
 };
@@ -158,6 +180,10 @@ struct PlainMN {
 struct ConvGeom {
   int N, H, W, C, K, KH, KW, sh, sw, ph, pw, OH, OW;  // C = in channels, K = out channels
   FastDiv fOW, fOH, fC, fK, fKW;
+  // reduction channels (C forward, K data-gradient) a multiple of the 64-wide
+  // K-tile: every K-tile lies inside ONE filter tap, so the tap decomposition is
+  // wave-uniform (scalar ALU, once per tile) and each lane only adds offsets
+  int ctap;
 };
 
 // forward, M side: rows = output pixels, k = (kh, kw, ci), ci fastest
@@ -166,11 +192,12 @@ struct ConvFwdA {
   static constexpr bool KMAJ = true;
   const bf16* x; ConvGeom g; int64_t Ktot, rows;
   int nb[4]; int ih0[4], iw0[4]; bool rok[4]; int ch;
-  __device__ void init(int64_t r0, int w, int l, int64_t) {
+  int64_t pix[4];  // element offset of (n, ih0, iw0, 0); dereferenced only in bounds
+  __device__ void init(int64_t r0, int w, int l, int64_t, int big) {
     ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
+      int64_t r = r0 + kmaj_row(big, w, i, l);
       rok[i] = r < rows;
       uint32_t rr = rok[i] ? (uint32_t)r : 0;
       uint32_t t = g.fOW.div(rr);
@@ -180,9 +207,20 @@ struct ConvFwdA {
       nb[i] = (int)n * g.H;
       ih0[i] = oh * g.sh - g.ph;
       iw0[i] = ow * g.sw - g.pw;
+      pix[i] = ((int64_t)(nb[i] + ih0[i]) * g.W + iw0[i]) * g.C;
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
+    if (g.ctap) {
+      // tap, kh, kw uniform over the tile (k0 is wave-uniform)
+      const uint32_t tap = g.fC.div((uint32_t)k0);
+      const int ci = (int)((uint32_t)k0 - tap * g.C) + ch * 8;
+      const uint32_t kh = g.fKW.div(tap);
+      const int kw = (int)(tap - kh * g.KW);
+      const int ih = ih0[i] + (int)kh, iw = iw0[i] + kw;
+      const bool ok = k0 < Ktot && rok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      return ok ? x + pix[i] + ((int64_t)kh * g.W + kw) * g.C + ci : zchunk();
+    }
     uint32_t k = (uint32_t)k0 + ch * 8;
     uint32_t tap = g.fC.div(k);
     int ci = (int)(k - tap * g.C);
@@ -200,7 +238,7 @@ struct ConvFwdA {
 // class is a dense implicit GEMM over exactly its useful taps (no zero-filled
 // K-tiles, no divisibility tests).  Stride 1 is the single class (0, 0).
 struct DgradClass {
-  int a, b, kh0, kw0, nth, ntw, Hc, Wc;
+  int a, b, kh0, kw0, nth, ntw, Hc, Wc, cbh, cbw;
   FastDiv fWc, fHc, fntw;
   __device__ void make(const ConvGeom& g, int cls) {
     a = cls / g.sw;
@@ -211,6 +249,10 @@ struct DgradClass {
     kw0 = (b + g.pw) % g.sw;
     nth = kh0 < g.KH ? (g.KH - kh0 + g.sh - 1) / g.sh : 0;
     ntw = kw0 < g.KW ? (g.KW - kw0 + g.sw - 1) / g.sw : 0;
+    // (a + ph - kh0) is a multiple of sh: output row of class row i and class tap th
+    // is oh = i + cbh - th exactly (no per-lane division by the stride)
+    cbh = (a + g.ph) / g.sh;
+    cbw = (b + g.pw) / g.sw;
     fWc = FastDiv((uint32_t)Wc);
     fHc = FastDiv((uint32_t)Hc);
     fntw = FastDiv((uint32_t)ntw);
@@ -222,7 +264,7 @@ struct ConvDgradA {
   static constexpr bool KMAJ = true;
   const bf16* dy; ConvGeom g;
   DgradClass c;
-  int nb[4]; int ih[4], iw[4]; bool rok[4]; int ch;
+  int nb[4]; int ii[4], jj[4]; bool rok[4]; int ch;
   int64_t mrows, kdim;
   __device__ int64_t rows_eff(int64_t) const { return mrows; }
   __device__ int64_t k_eff(int64_t) const { return kdim; }
@@ -233,35 +275,39 @@ struct ConvDgradA {
     int i = (int)(t - n * c.Hc);
     return ((int64_t)n * g.H + c.a + g.sh * i) * g.W + c.b + g.sw * j;
   }
-  __device__ void init(int64_t r0, int w, int l, int64_t cls) {
+  __device__ void init(int64_t r0, int w, int l, int64_t cls, int big) {
     c.make(g, (int)cls);
     mrows = (int64_t)g.N * c.Hc * c.Wc;
     kdim = (int64_t)c.nth * c.ntw * g.K;
     ch = (l & 7) ^ (l >> 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + 32 * w + 8 * i + (l >> 3);
+      int64_t r = r0 + kmaj_row(big, w, i, l);
       rok[i] = r < mrows;
       uint32_t rr = rok[i] ? (uint32_t)r : 0;
       uint32_t t = c.fWc.div(rr);
       int j = (int)(rr - t * c.Wc);
       uint32_t n = c.fHc.div(t);
-      int ii = (int)(t - n * c.Hc);
-      ih[i] = c.a + g.sh * ii;
-      iw[i] = c.b + g.sw * j;
+      ii[i] = (int)(t - n * c.Hc) + c.cbh;
+      jj[i] = j + c.cbw;
       nb[i] = (int)n * g.OH;
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    uint32_t k = (uint32_t)k0 + ch * 8;
-    uint32_t tap = g.fK.div(k);
-    int co = (int)(k - tap * g.K);
+    uint32_t tap, co;
+    if (g.ctap) {                     // K % 64 == 0: one tap per K-tile (scalar)
+      tap = g.fK.div((uint32_t)k0);
+      co = (uint32_t)k0 - tap * g.K + ch * 8;
+    } else {
+      uint32_t k = (uint32_t)k0 + ch * 8;
+      tap = g.fK.div(k);
+      co = k - tap * g.K;
+    }
     uint32_t th = c.fntw.div(tap);
     int tw = (int)(tap - th * c.ntw);
-    int kh = c.kh0 + g.sh * (int)th, kw = c.kw0 + g.sw * tw;
-    int nh = ih[i] + g.ph - kh, nw = iw[i] + g.pw - kw;   // exact multiples of the stride
-    int oh = nh / g.sh, ow = nw / g.sw;
-    bool ok = (int64_t)k < kdim && rok[i] && nh >= 0 && nw >= 0 && oh < g.OH && ow < g.OW;
+    int oh = ii[i] - (int)th, ow = jj[i] - tw;
+    bool ok = (int64_t)k0 + (g.ctap ? 0 : ch * 8) < kdim && rok[i] && (unsigned)oh < (unsigned)g.OH &&
+              (unsigned)ow < (unsigned)g.OW;
     return ok ? dy + ((int64_t)(nb[i] + oh) * g.OW + ow) * g.K + co : zchunk();
   }
 };
@@ -273,22 +319,29 @@ struct ConvDgradB {
   const bf16* w; ConvGeom g;
   DgradClass c;
   int64_t kdim;
-  int col[4]; bool cok[4]; int kr;
-  __device__ void init(int64_t r0, int wv, int l, int64_t cls) {
+  int col[4]; bool cok[4]; int kk[4];
+  __device__ void init(int64_t r0, int wv, int l, int64_t cls, int big) {
     c.make(g, (int)cls);
     kdim = (int64_t)c.nth * c.ntw * g.K;
-    kr = 16 * wv + (l >> 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int cc = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
-      col[i] = (int)r0 + 8 * cc;
+      int cc;
+      mn_slot(big, wv, i, l, kk[i], cc);
+      col[i] = (int)r0 + cc;
       cok[i] = col[i] < g.C;
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    uint32_t k = (uint32_t)k0 + kr + 4 * i;
-    uint32_t tap = g.fK.div(k);
-    int co = (int)(k - tap * g.K);
+    uint32_t k = (uint32_t)k0 + kk[i];
+    uint32_t tap;
+    int co;
+    if (g.ctap) {                     // tap uniform over the K-tile
+      tap = g.fK.div((uint32_t)k0);
+      co = (int)(k - tap * g.K);
+    } else {
+      tap = g.fK.div(k);
+      co = (int)(k - tap * g.K);
+    }
     uint32_t th = c.fntw.div(tap);
     int tw = (int)(tap - th * c.ntw);
     int kh = c.kh0 + g.sh * (int)th, kw = c.kw0 + g.sw * tw;
@@ -303,13 +356,13 @@ struct ConvWgradB {
   HETU_LINEAR_ROWS
   static constexpr bool KMAJ = false;
   const bf16* x; ConvGeom g; int64_t P;  // P = N*OH*OW
-  int kh[4], kw[4], ci[4]; bool cok[4]; int kr;
-  __device__ void init(int64_t r0, int w, int l, int64_t) {
-    kr = 16 * w + (l >> 4);
+  int kh[4], kw[4], ci[4]; bool cok[4]; int kk[4];
+  __device__ void init(int64_t r0, int w, int l, int64_t, int big) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int c = (l & 15) ^ ((((l >> 4) & 3) << 2) | i);
-      int col = (int)r0 + 8 * c;
+      int c;
+      mn_slot(big, w, i, l, kk[i], c);
+      int col = (int)r0 + c;
       cok[i] = col < g.KH * g.KW * g.C;
       int tap = col / g.C;
       ci[i] = col - tap * g.C;
@@ -318,7 +371,7 @@ struct ConvWgradB {
     }
   }
   __device__ const bf16* src(int64_t k0, int i) const {
-    uint32_t p = (uint32_t)k0 + kr + 4 * i;
+    uint32_t p = (uint32_t)k0 + kk[i];
     uint32_t t = g.fOW.div(p);
     int ow = (int)(p - t * g.OW);
     uint32_t n = g.fOH.div(t);
@@ -371,8 +424,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   const int tn = (wg % per_group) / gsz;
 
   const int64_t batch = blockIdx.y;
-  la.init((int64_t)tm * BM, wave, lane, batch);
-  lb.init((int64_t)tn * BN, wave, lane, batch);
+  la.init((int64_t)tm * BM, wave, lane, batch, 0);
+  lb.init((int64_t)tn * BN, wave, lane, batch, 0);
   // per-block problem view (a stride class of a strided dgrad may be smaller)
   const int64_t Mb = la.rows_eff(M);
   if ((int64_t)tm * BM >= Mb) return;  // block-uniform, before any barrier
@@ -592,6 +645,295 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   }
 }
 
+// ---- 256x256 tile, 8 waves, phase-interleaved K loop -----------------------------------
+// Block tile 256x256x64, 512 threads = 8 waves as 2 (M) x 4 (N); wave tile 128x64 =
+// 8 x 4 mfma_f32_16x16x32_bf16 tiles (128 fp32 accumulators per lane).  LDS = 2 K-tile
+// buffers x 4 half-tile images of 16 KiB (A rows / B columns each wave reads in its
+// sub-tile 0 or 1; kmaj_row / mn_slot) = 128 KiB, one block per CU, 2 waves per SIMD.
+// Every K-tile runs as 4 phases; each phase reads one register sub-tile from LDS,
+// stages ONE half-tile (2 global_load_lds per thread) 7 half-tiles ahead, and runs the
+// 16 MFMAs of one 64x32 quadrant of the wave tile between two raw s_barriers.  The DMA
+// stays in flight across the barriers (counted vmcnt, never 0 in the loop): the
+// buffer for K-tile t+1 is retired by the wait in the last phase of K-tile t.
+//   phase 0: read A-sub0 + B-sub0, MMA (A0,B0)     restage (K-tile t+2, same buffer):
+//   phase 1: read B-sub1,          MMA (A0,B1)       A-half0 in phase 1, B-half1 in 2,
+//   phase 2: read A-sub1,          MMA (A1,B1)       A-half1 in 3, B-half0 in phase 0
+//   phase 3: read B-sub0,          MMA (A1,B0)       of t+1: one phase after last read
+constexpr int BIG = 256, BIG_NT = 512;
+constexpr int HALF_BYTES = 128 * BK * 2;       // 16 KiB
+constexpr int BUF_BYTES = 4 * HALF_BYTES;       // A-h0, A-h1, B-h0, B-h1
+
+__device__ __forceinline__ void vm_wait_halves(int n) {
+  // wait until at most n half-tiles (2 DMA each) of this wave are still in flight
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+// ablation knobs for profiling (hetu_gemm_big_variant; 0 in production):
+//  1 no wave-group stagger, 4 no s_setprio, 8 skip the DMA issue, 16 skip the MFMAs
+static int g_big_variant = 0;
+
+template <class LA, class LB>
+__global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
+                                                             int64_t K, int tiles_m, int tiles_n, int ktps,
+                                                             int var) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int gid = wg / per_group, first_m = gid * GROUP;
+  const int gsz = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+
+  const int64_t batch = blockIdx.y;
+  la.init((int64_t)tm * BIG, wave, lane, batch, 1);
+  lb.init((int64_t)tn * BIG, wave, lane, batch, 2);
+  const int64_t Mb = la.rows_eff(M);
+  if ((int64_t)tm * BIG >= Mb) return;  // block-uniform, before any barrier
+  K = la.k_eff(K);
+  const int nkt = (int)((K + BK - 1) / BK);
+  const int kt0 = blockIdx.z * ktps;
+  const int nk = max(0, min(kt0 + ktps, nkt) - kt0);
+  const int nh = 4 * nk;                 // half-tiles to stage
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile j: K-tile j>>2, staging order A-h0, B-h1, A-h1, B-h0 (the order the
+  // phases of the previous use of the buffer finish reading them, see below)
+  auto issue = [&](int j) {
+    if (j >= nh || (var & 8)) return;
+    const int t = j >> 2, which = j & 3;
+    const int64_t k0 = (int64_t)(kt0 + t) * BK;
+    char* buf = smem + (t & 1) * BUF_BYTES;
+    const bool isA = (which & 1) == 0;
+    const int h = isA ? (which >> 1) : (which == 1 ? 1 : 0);
+    char* dst = buf + (isA ? 0 : 2 * HALF_BYTES) + h * HALF_BYTES + 2048 * wave;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const bf16* src = isA ? la.src(k0, 2 * h + ii) : lb.src(k0, 2 * h + ii);
+      glds16(src, dst + 1024 * ii);
+    }
+  };
+  // half-tiles issued after the last half of K-tile t (at most 3 in flight)
+  auto younger_than_tile = [&](int t, int issued) { return max(0, min(3, issued - 4 * (t + 1))); };
+
+#pragma clang loop unroll(full)
+  for (int j = 0; j < 7; ++j) issue(j);   // unrolled: loader arrays stay in registers
+  int issued = min(7, nh);
+  vm_wait_halves(younger_than_tile(0, issued));
+  raw_barrier();
+  // Ping-pong: the wave-row-1 group runs one barrier behind the wave-row-0 group, so on
+  // every SIMD (one wave of each group) one wave's 16 MFMAs overlap the other wave's
+  // LDS reads / DMA issue / waits.  Each phase ends its reads with lgkmcnt(0) BEFORE its
+  // first barrier, so a half is restaged one phase after the phase that last read it.
+  if (wr == 1 && !(var & 1)) raw_barrier();
+
+  v8s fa[2][4][2], fb[2][2][2];   // [sub][row/col block][k-step]
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF_BYTES;
+    const char* Ah[2] = {buf, buf + HALF_BYTES};
+    const char* Bh[2] = {buf + 2 * HALF_BYTES, buf + 3 * HALF_BYTES};
+#pragma clang loop unroll(full)
+    for (int p = 0; p < 4; ++p) {
+      // phase p reads: 0: B-sub0 + A-sub0, 1: B-sub1, 2: A-sub1, 3: B-sub0 again
+      if (p == 0 || p == 3) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fb[0][jj][s2] = lds_frag<LB::KMAJ>(Bh[0], wc * 2 + jj, s2, lane);
+      }
+      if (p == 0) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fa[0][ii][s2] = lds_frag<LA::KMAJ>(Ah[0], wr * 4 + ii, s2, lane);
+      } else if (p == 1) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fb[1][jj][s2] = lds_frag<LB::KMAJ>(Bh[1], wc * 2 + jj, s2, lane);
+      } else if (p == 2) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) fa[1][ii][s2] = lds_frag<LA::KMAJ>(Ah[1], wr * 4 + ii, s2, lane);
+      }
+      issue(4 * t + p + 7);
+      if (p == 3) {
+        issued = min(4 * t + 11, nh);
+        vm_wait_halves(younger_than_tile(t + 1, issued));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      raw_barrier();
+      const int sa = (p < 2) ? 0 : 1;
+      const int sb = (p == 0 || p == 3) ? 0 : 1;
+      if (!(var & 4)) __builtin_amdgcn_s_setprio(1);
+      if (!(var & 16)) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+              acc[sa * 4 + ii][sb * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  fb[sb][jj][s2], fa[sa][ii][s2], acc[sa * 4 + ii][sb * 2 + jj], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            asm volatile("" :: "v"(fa[sa][ii][0]), "v"(fa[sa][ii][1]), "v"(fb[sb][jj][0]), "v"(fb[sb][jj][1]));
+      }
+      __builtin_amdgcn_s_setprio(0);
+      raw_barrier();
+    }
+  }
+  if (wr == 0 && !(var & 1)) raw_barrier();   // re-align the two groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: lane holds C[m][n..n+3] of acc[i][j],
+  //   m = tm*256 + wr*128 + 16i + (lane&15), n = tn*256 + wc*64 + 16j + 4(lane>>4)
+  if (ep.slab || ep.atomic) {
+    float* S = ep.slab ? ep.slab + blockIdx.z * ep.slab_stride : nullptr;
+    char* Cb = (char*)ep.C + batch * ep.sC * 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t m = (int64_t)tm * BIG + wr * 128 + i * 16 + (lane & 15);
+      if (m >= Mb) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = (int64_t)tn * BIG + wc * 64 + j * 16 + 4 * (lane >> 4);
+        if (n >= N) continue;
+        if (S) {
+          float* d = S + m * N + n;
+          if (n + 3 < N && (N & 3) == 0) {
+            *reinterpret_cast<float4*>(d) = make_float4(acc[i][j][0] * ep.alpha, acc[i][j][1] * ep.alpha,
+                                                        acc[i][j][2] * ep.alpha, acc[i][j][3] * ep.alpha);
+          } else {
+            for (int t = 0; t < 4; ++t)
+              if (n + t < N) d[t] = acc[i][j][t] * ep.alpha;
+          }
+        } else {
+          float* Cf = (float*)Cb + la.out_row(m) * ep.ldc + n;
+          for (int t = 0; t < 4; ++t)
+            if (n + t < N) unsafeAtomicAdd(Cf + t, acc[i][j][t] * ep.alpha);
+        }
+      }
+    }
+    return;
+  }
+  char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
+  const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
+  constexpr int SROW = BIG + 4;
+  float* stg = reinterpret_cast<float*>(smem);
+  const bool cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)Cb & 15) == 0)
+                               : ((ep.ldc & 7) == 0 && ((uintptr_t)Cb & 15) == 0);
+  const bool ivec = Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)Cinb & 15) == 0)
+                                        : ((ep.ldcin & 7) == 0 && ((uintptr_t)Cinb & 15) == 0));
+  // 4 passes of 64 rows through LDS (64 x 260 fp32 = 66.5 KiB), full-row stores
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    if (wr == (pass >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = (pass & 1) * 4 + ii;
+          const int rr = ii * 16 + (lane & 15), c = wc * 64 + j * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<v4f*>(stg + rr * SROW + c) = acc[i][j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sp = 0; sp < 4; ++sp) {
+      const int rr = sp * 16 + (tid >> 5), c = (tid & 31) * 8;
+      const int64_t m = (int64_t)tm * BIG + pass * 64 + rr;
+      const int64_t n = (int64_t)tn * BIG + c;
+      if (m >= Mb || n >= N) continue;
+      const int64_t orow = la.out_row(m);
+      float v[8];
+      {
+        v4f a0 = *reinterpret_cast<const v4f*>(stg + rr * SROW + c);
+        v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + c + 4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
+      }
+      const bool full = n + 7 < N;
+      if (ep.bias) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          v[t] += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
+      }
+      if (Cinb) {
+        const int64_t o = orow * ep.ldcin + n;
+        float cv[8];
+        if (ivec && full) {
+          if (ep.cin_f32) {
+            float4 c0 = *reinterpret_cast<const float4*>((const float*)Cinb + o);
+            float4 c1 = *reinterpret_cast<const float4*>((const float*)Cinb + o + 4);
+            cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
+            cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
+          } else {
+            load_vec<bf16>((const bf16*)Cinb + o, cv);
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)Cinb)[o + t] : to_f(((const bf16*)Cinb)[o + t])) : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
+      const int64_t o = orow * ep.ldc + n;
+      if (ep.out_f32) {
+        float* Cf = (float*)Cb + o;
+        if (cvec && full) {
+          *reinterpret_cast<float4*>(Cf) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(Cf + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+          for (int t = 0; t < 8; ++t)
+            if (n + t < N) Cf[t] = v[t];
+        }
+      } else {
+        bf16* Ch = (bf16*)Cb + o;
+        if (cvec && full) {
+          store_vec<bf16>(Ch, v);
+        } else {
+          for (int t = 0; t < 8; ++t)
+            if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // dst[m][n] (ld ldd, fp32 or bf16) (+)= sum_z slab[z][m][n]
 __global__ void splitk_reduce_k(const float* __restrict__ slab, int64_t stride, int nz,
                                 void* dst, int64_t M, int64_t N, int64_t ldd, int out_f32,
@@ -614,8 +956,38 @@ __global__ void splitk_reduce_k(const float* __restrict__ slab, int64_t stride, 
 }
 
 template <class LA, class LB>
+static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
+                      int batch, int splitk, hipStream_t st) {
+  int tiles_m = (int)((M + BIG - 1) / BIG), tiles_n = (int)((N + BIG - 1) / BIG);
+  int nkt = (int)((K + BK - 1) / BK);
+  if (splitk < 1) splitk = 1;
+  if (splitk > nkt) splitk = nkt > 0 ? nkt : 1;
+  int ktps = (nkt + splitk - 1) / splitk;
+  splitk = (nkt + ktps - 1) / ktps;
+  if (splitk < 1) splitk = 1;
+  dim3 grid(tiles_m * tiles_n, batch, splitk);
+  Epi e1 = ep;
+  if (ep.slab && splitk > 1) {
+    e1.slab_stride = M * N;
+    hipLaunchKernelGGL((gemm_big_kernel<LA, LB>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                       tiles_n, ktps, g_big_variant);
+    int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, ep.slab, M * N, splitk, ep.C, M, N,
+                       ep.ldc, ep.out_f32, ep.atomic);
+    return (int)hipGetLastError();
+  }
+  e1.slab = nullptr;
+  if (splitk > 1) e1.atomic = 1;
+  hipLaunchKernelGGL((gemm_big_kernel<LA, LB>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                     tiles_n, ktps, g_big_variant);
+  return (int)hipGetLastError();
+}
+
+// tile: 0 = 128x128 (4 waves, 2-3 blocks per CU), 1 = 256x256 (8 waves, 1 block per CU)
+template <class LA, class LB>
 static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
-                  int batch, int splitk, hipStream_t st) {
+                  int batch, int splitk, hipStream_t st, int tile = 0) {
+  if (tile == 1) return launch_big(la, lb, ep, M, N, K, batch, splitk, st);
   int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
   int nkt = (int)((K + BK - 1) / BK);
   if (splitk < 1) splitk = 1;
@@ -674,23 +1046,24 @@ HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* C
                             int64_t ldb, int64_t ldc, int64_t ldcin, int a_kmaj, int b_kmaj,
                             int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
                             float alpha, float beta, int act, int out_f32, int cin_f32,
-                            int bias_on_m, int splitk, int atomic, float* ws, hipStream_t st) {
+                            int bias_on_m, int splitk, int atomic, float* ws, int tile, hipStream_t st) {
   Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32, atomic,
          bias_on_m, ws, 0};
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   if (a_kmaj && b_kmaj)
-    return launch(PlainK{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
+    return launch(PlainK{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
   if (a_kmaj && !b_kmaj)
-    return launch(PlainK{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
+    return launch(PlainK{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
   if (!a_kmaj && b_kmaj)
-    return launch(PlainMN{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
-  return launch(PlainMN{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st);
+    return launch(PlainMN{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
+  return launch(PlainMN{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
 }
 
 static ConvGeom geom(int N, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
                      int pw) {
   ConvGeom g{N, H, W, C, K, KH, KW, sh, sw, ph, pw, 0, 0};
+  g.ctap = 0;
   g.OH = (H + 2 * ph - KH) / sh + 1;
   g.OW = (W + 2 * pw - KW) / sw + 1;
   g.fOW = FastDiv((uint32_t)g.OW);
@@ -704,62 +1077,80 @@ static ConvGeom geom(int N, int H, int W, int C, int K, int KH, int KW, int sh, 
 // y[N,OH,OW,K] (NHWC) = conv(x[N,H,W,C] NHWC, w[K,KH,KW,C]) (+bias[K]) -> act.  C % 8 == 0.
 HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const float* bias, int N,
                                 int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
-                                int pw, int act, hipStream_t st) {
+                                int pw, int act, int tile, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t M = (int64_t)N * g.OH * g.OW, Kt = (int64_t)KH * KW * C;
   Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0, nullptr, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(PlainK{(const bf16*)x, C, M, C, 0}, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M,
-                  K, Kt, 1, 1, st);
+                  K, Kt, 1, 1, st, tile);
   ConvFwdA la{};
   la.x = (const bf16*)x;
+  g.ctap = C % BK == 0;
   la.g = g;
   la.Ktot = Kt;
   la.rows = M;
-  return launch(la, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M, K, Kt, 1, 1, st);
+  return launch(la, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M, K, Kt, 1, 1, st, tile);
 }
 
 // dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[K,KH,KW,C]) (+ acc[N,H,W,C] when given:
 // the gradient joined at the conv input, added in the epilogue).  K % 8 == 0, C % 8 == 0.
 HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const void* acc,
                                   int acc_f32, int N, int H, int W, int C, int K, int KH, int KW,
-                                  int sh, int sw, int ph, int pw, hipStream_t st) {
+                                  int sh, int sw, int ph, int pw, int tile, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   Epi ep{dx, acc, nullptr, C, C, 0, 0, 1.f, acc ? 1.f : 0.f, 0, 0, acc_f32, 0, 0, nullptr, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0) {
     int64_t M = (int64_t)N * H * W;
     return launch(PlainK{(const bf16*)dy, K, M, K, 0}, PlainMN{(const bf16*)w, C, C, K, 0}, ep, M,
-                  C, K, 1, 1, st);
+                  C, K, 1, 1, st, tile);
   }
   // one launch over the sh*sw stride classes (blockIdx.y); grid sized for the
   // largest class, the others exit early per block
   int64_t Mmax = (int64_t)N * ((H + sh - 1) / sh) * ((W + sw - 1) / sw);
   int64_t Kmax = (int64_t)((KH + sh - 1) / sh) * ((KW + sw - 1) / sw) * K;
+  g.ctap = K % BK == 0;
   ConvDgradA la{};
   la.dy = (const bf16*)dy;
   la.g = g;
   ConvDgradB lb{};
   lb.w = (const bf16*)w;
   lb.g = g;
-  return launch(la, lb, ep, Mmax, C, Kmax, sh * sw, 1, st);
+  return launch(la, lb, ep, Mmax, C, Kmax, sh * sw, 1, st, tile);
 }
 
 HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }
+
+// profiling ablations of the 256x256 kernel (see g_big_variant); returns the previous value
+HETU_API int hetu_gemm_big_variant(int v) {
+  int old = g_big_variant;
+  g_big_variant = v;
+  return old;
+}
+
+// split count for the 256x256 kernel: about one block per CU, slices of >= 8 K-tiles
+HETU_API int hetu_gemm_pick_splitk_big(int64_t M, int64_t N, int64_t K) {
+  int64_t tiles = ((M + BIG - 1) / BIG) * ((N + BIG - 1) / BIG);
+  int64_t ktiles = (K + BK - 1) / BK;
+  int64_t want = (256 + tiles - 1) / tiles;
+  int64_t cap = std::max<int64_t>(1, ktiles / 8);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(want, cap), 512));
+}
 
 // dw[K, KH*KW*C] fp32 (+)= sum over output pixels dy^T x_im2col.  Split-K over
 // the pixel axis into fp32 slabs (ws: splitk*K*KH*KW*C floats) + one reduce; no atomics.
 HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int N, int H, int W,
                                   int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-                                  int splitk, int accumulate, float* ws, hipStream_t st) {
+                                  int splitk, int accumulate, float* ws, int tile, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t P = (int64_t)N * g.OH * g.OW, Nc = (int64_t)KH * KW * C;
   Epi ep{dw, nullptr, nullptr, Nc, 0, 0, 0, 1.f, 0.f, 0, 1, 0, accumulate, 0, splitk > 1 ? ws : nullptr, 0};
   PlainMN la{(const bf16*)dy, K, K, P, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
-    return launch(la, PlainMN{(const bf16*)x, C, C, P, 0}, ep, K, Nc, P, 1, splitk, st);
+    return launch(la, PlainMN{(const bf16*)x, C, C, P, 0}, ep, K, Nc, P, 1, splitk, st, tile);
   ConvWgradB lb{};
   lb.x = (const bf16*)x;
   lb.g = g;
   lb.P = P;
-  return launch(la, lb, ep, K, Nc, P, 1, splitk, st);
+  return launch(la, lb, ep, K, Nc, P, 1, splitk, st, tile);
 }

@@ -1,8 +1,9 @@
 """2-D convolution (logical NCHW, physical channels-last on the GPU).
 
 The forward/backward-data/backward-filter entry points dispatch per shape to
-the hand-written implicit-GEMM MFMA kernel (``gemm.hip`` via ``conv_igemm``)
-or to the vendor convolution (MIOpen through torch).  ``HETU_CONV=auto``
+the hand-written implicit-GEMM MFMA kernels (``gemm.hip`` via ``conv_igemm``:
+the 128x128-tile kernel, ``hip``, and the 256x256-tile phase-interleaved kernel,
+``hip256``) or to the vendor convolution (MIOpen through torch).  ``HETU_CONV=auto``
 (default) selects per shape by measurement (``autotune.choose``), so the
 hand-written kernel runs exactly where it is at least as fast; ``hip`` /
 ``vendor`` force one side.
@@ -99,6 +100,9 @@ def conv2d(x, w, b, stride, padding):
             blas = {'blas': blas_fwd}
         elif _needs_pad(x, w):
             blas = {'hip_pad': lambda: conv_igemm.try_forward(_pad_c(x), _pad_c(w), stride, padding)}
+        if w.shape[0] >= 128:   # 256x256-tile kernel: only with >= half a tile of output channels
+            blas = dict(blas or {})
+            blas['hip256'] = lambda: conv_igemm.try_forward(x, w, stride, padding, tile=1)
         y = _pick(('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding)),
                   lambda: conv_igemm.try_forward(x, w, stride, padding),
                   lambda: F.conv2d(x, w, None, stride, padding), blas)
@@ -139,6 +143,9 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None):
                 d = conv_igemm.try_backward_data(g, _pad_c(w), (n, cp, h, ww_), stride, padding)
                 return None if d is None else d[:, :ci]
             blas = {'hip_pad': pad_dgrad}
+        if x_shape[1] >= 128:
+            blas = dict(blas or {})
+            blas['hip256'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=1)
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
                      lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
                      lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas)
@@ -212,6 +219,10 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                 out.copy_(d[:, :ci])
                 return out
             blas = {'hip_pad': pad_wgrad}
+        if w_shape[0] >= 128:
+            blas = dict(blas or {})
+            blas['hip256'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
+                                                                    accumulate=False, tile=1)
         return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
                      lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                             accumulate=False),

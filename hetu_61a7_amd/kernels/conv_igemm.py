@@ -33,22 +33,22 @@ def _out_hw(H, W, KH, KW, stride, padding):
     return (H + 2 * padding[0] - KH) // stride[0] + 1, (W + 2 * padding[1] - KW) // stride[1] + 1
 
 
-def try_forward(x, w, stride, padding, bias=None, act=None):
+def try_forward(x, w, stride, padding, bias=None, act=None, tile=0):
     if not _ok(x, w, x.shape[1], w.shape[0]):
         return None
     N, C, H, W = x.shape
     K, _, KH, KW = w.shape
     OH, OW = _out_hw(H, W, KH, KW, stride, padding)
     y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
-    f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, P])
+    f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, I32, P])
     check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(),
             bias.float().contiguous().data_ptr() if bias is not None else None,
             N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
-            {None: 0, 'relu': 1}[act], stream_ptr()), 'conv_fwd')
+            {None: 0, 'relu': 1}[act], int(tile), stream_ptr()), 'conv_fwd')
     return y.permute(0, 3, 1, 2)
 
 
-def try_backward_data(g, w, x_shape, stride, padding, acc=None):
+def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0):
     if not _ok(g, w, x_shape[1], w.shape[0]):
         return None
     if acc is not None and (tuple(acc.shape) != tuple(x_shape) or
@@ -58,18 +58,19 @@ def try_backward_data(g, w, x_shape, stride, padding, acc=None):
     N, C, H, W = x_shape
     K, _, KH, KW = w.shape
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
-    f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [P])
+    f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [I32, P])
     check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
             int(acc is not None and acc.dtype == torch.float32), N, H, W, C, K, KH, KW,
-            stride[0], stride[1], padding[0], padding[1], stream_ptr()), 'conv_dgrad')
+            stride[0], stride[1], padding[0], padding[1], int(tile), stream_ptr()), 'conv_dgrad')
     return dx.permute(0, 3, 1, 2)
 
 
-def _splitk(M, Nc, P_):
-    return int(fn('hetu_gemm_pick_splitk', [I64, I64, I64])(M, Nc, P_))
+def _splitk(M, Nc, P_, tile=0):
+    name = 'hetu_gemm_pick_splitk_big' if tile == 1 else 'hetu_gemm_pick_splitk'
+    return int(fn(name, [I64, I64, I64])(M, Nc, P_))
 
 
-def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=None):
+def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=None, tile=0):
     """Returns the fp32 weight gradient (channels-last) written into ``out`` when
     given: accumulated onto its contents (default) or overwriting them
     (``accumulate=False``)."""
@@ -86,13 +87,13 @@ def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=Non
         dw = out.permute(0, 2, 3, 1)
         assert dw.is_contiguous() and dw.dtype == torch.float32
     Nc = KH * KW * C
-    sk = _splitk(K, Nc, N * OH * OW)
+    sk = _splitk(K, Nc, N * OH * OW, tile)
     ws = torch.empty(sk * K * Nc, dtype=torch.float32, device=g.device) if sk > 1 else None
     if sk == 1 and not accumulate:
         dw.zero_()
         accumulate = True  # single slice accumulates straight into dw
-    f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, I32, P, P])
+    f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, I32, P, I32, P])
     check(f(g.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
             padding[0], padding[1], sk, int(accumulate), ws.data_ptr() if ws is not None else None,
-            stream_ptr()), 'conv_wgrad')
+            int(tile), stream_ptr()), 'conv_wgrad')
     return dw.permute(0, 3, 1, 2)

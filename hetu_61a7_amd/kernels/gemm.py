@@ -51,18 +51,26 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
             from .autotune import choose
             key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
             cands = {'hip': hip, 'vendor': lambda: _vendor(a, b, ta, tb, bias, activation)}
+            if _big_ok(a, b, ta, tb):
+                cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
             if bias is not None:
                 # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
                 # plain GEMM + a separate bias pass: measure both
                 cands['vendor_nobias'] = lambda: _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
             c = choose(key, cands)
-            if c == 'hip':
-                y = hip()
+            if c in ('hip', 'hip256'):
+                y = cands[c]()
                 if y is not None:
                     return y
             elif c == 'vendor_nobias':
                 return _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
     return _vendor(a, b, ta, tb, bias, activation)
+
+
+def _big_ok(a, b, ta, tb):
+    """the 256x256-tile kernel is a candidate once both output dims fill a tile"""
+    A, B = _tr(a, ta), _tr(b, tb)
+    return A.dim() == 2 and B.dim() == 2 and A.shape[0] >= 256 and B.shape[1] >= 256
 
 
 def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
@@ -163,6 +171,12 @@ def matmul_into(a, b, ta, tb, out):
             for s in (2, 4, 8):
                 if tiles * s <= 1536 and K // s >= 512:
                     cands['hip_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s))
+            if M >= 256 and N >= 256:
+                cands['hip256'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=1)
+                t256 = -(-M // 256) * -(-N // 256)
+                for s in (2, 4, 8):
+                    if t256 * s <= 512 and K // s >= 1024:
+                        cands['hip256_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=1))
             if K >= 2048:
                 cands['vendor_sk'] = lambda: _vendor_splitk_into(A, B, out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
@@ -186,8 +200,12 @@ def matmul_acc(a, b, ta, tb, acc):
         hip = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0)
         vendor = lambda: torch.addmm(c, A, B)
         key = ('gemm_acc', _sig(a), _sig(b), ta, tb)
-        if _MFMA == 'hip' or choose(key, {'hip': hip, 'vendor': vendor}) == 'hip':
-            y = hip()
+        cands = {'hip': hip, 'vendor': vendor}
+        if A.shape[0] >= 256 and B.shape[1] >= 256:
+            cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=1)
+        ch = 'hip' if _MFMA == 'hip' else choose(key, cands)
+        if ch != 'vendor':
+            y = cands[ch]()
             if y is not None:
                 return y
         return vendor()

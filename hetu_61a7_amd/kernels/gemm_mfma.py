@@ -16,7 +16,10 @@ from . import fn, stream_ptr, check, P, I64, I32, F32
 
 _ACT = {None: 0, 'relu': 1, 'gelu': 2}
 _ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64, I64,
-         F32, F32, I32, I32, I32, I32, I32, I32, P, P]
+         F32, F32, I32, I32, I32, I32, I32, I32, P, I32, P]
+# tile configurations of the kernel (gemm.hip launch): 0 = 128x128 tile, 4 waves;
+# 1 = 256x256 tile, 8 waves, phase-interleaved K loop (one block per CU)
+TILES = (0, 1)
 MODE = os.environ.get('HETU_GEMM', 'auto')
 
 
@@ -44,7 +47,7 @@ def _aligned(*ts):
 
 
 def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None,
-         accumulate=False, splitk=1, bias_on_m=False):
+         accumulate=False, splitk=1, bias_on_m=False, tile=0):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+beta*cin) (+bias) -> act, a/b arbitrary
     strided views (batched 3-D allowed).  Returns None if unsupported."""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
@@ -93,7 +96,8 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
             int(da[0]), int(db[0]), batch, da[2], db[2], sC, sCin, float(alpha), float(beta),
             _ACT[act], int(out.dtype == torch.float32),
             int(cin_t is not None and cin_t.dtype == torch.float32), int(bias_on_m), int(splitk),
-            int(accumulate), ws.data_ptr() if ws is not None else None, stream_ptr()), 'gemm_bf16')
+            int(accumulate), ws.data_ptr() if ws is not None else None, int(tile), stream_ptr()),
+          'gemm_bf16')
     return out
 
 

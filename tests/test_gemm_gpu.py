@@ -15,27 +15,30 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
 
 
+@pytest.mark.parametrize('tile', G.TILES)
 @pytest.mark.parametrize('ta', [False, True])
 @pytest.mark.parametrize('tb', [False, True])
-@pytest.mark.parametrize('mnk', [(256, 256, 256), (200, 136, 72), (1000, 8, 520), (64, 1032, 4096)])
-def test_gemm_modes(ta, tb, mnk):
+@pytest.mark.parametrize('mnk', [(256, 256, 256), (200, 136, 72), (1000, 8, 520), (64, 1032, 4096),
+                                 (520, 776, 1000), (768, 512, 64)])
+def test_gemm_modes(ta, tb, mnk, tile):
     M, N, K = mnk
     a = torch.randn(K, M, device=DEV).bfloat16().t() if ta else torch.randn(M, K, device=DEV).bfloat16()
     b = torch.randn(N, K, device=DEV).bfloat16().t() if tb else torch.randn(K, N, device=DEV).bfloat16()
-    y = G.gemm(a, b)
+    y = G.gemm(a, b, tile=tile)
     assert y is not None
     ref = a.float() @ b.float()
     assert _rel(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize('tile', G.TILES)
 @pytest.mark.parametrize('act', [None, 'relu', 'gelu'])
-def test_gemm_epilogue(act):
+def test_gemm_epilogue(act, tile):
     M, N, K = 384, 264, 128
     a = torch.randn(M, K, device=DEV).bfloat16()
     b = torch.randn(K, N, device=DEV).bfloat16()
     bias = torch.randn(N, device=DEV)
     cin = torch.randn(M, N, device=DEV)
-    y = G.gemm(a, b, bias=bias, act=act, alpha=0.5, beta=2.0, cin=cin, out_dtype=torch.float32)
+    y = G.gemm(a, b, bias=bias, act=act, alpha=0.5, beta=2.0, cin=cin, out_dtype=torch.float32, tile=tile)
     ref = 0.5 * (a.float() @ b.float()) + bias + 2.0 * cin
     if act == 'relu':
         ref = torch.relu(ref)
@@ -44,30 +47,36 @@ def test_gemm_epilogue(act):
     assert _rel(y, ref) < 1e-2
 
 
-def test_gemm_batched_and_splitk():
+@pytest.mark.parametrize('tile', G.TILES)
+def test_gemm_batched_and_splitk(tile):
     a = torch.randn(6, 128, 64, device=DEV).bfloat16()
     b = torch.randn(6, 128, 64, device=DEV).bfloat16().transpose(1, 2)  # [6, 64, 128]
-    y = G.try_bmm(a, b, False, False)
+    y = G.gemm(a, b, tile=tile)
     assert _rel(y, a.float() @ b.float()) < 1e-2
     x = torch.randn(8192, 96, device=DEV).bfloat16()
     g = torch.randn(8192, 136, device=DEV).bfloat16()
     out = torch.zeros(96, 136, device=DEV)
-    G.gemm(x.t(), g, out=out, accumulate=True, splitk=16)
+    G.gemm(x.t(), g, out=out, accumulate=True, splitk=16, tile=tile)
     assert _rel(out, x.float().t() @ g.float()) < 1e-2
+    # split-K through fp32 slabs + reduce (bf16 output)
+    y2 = G.gemm(x.t(), g, splitk=4, tile=tile)
+    assert _rel(y2, x.float().t() @ g.float()) < 1e-2
 
 
 CONV_SHAPES = [  # N, C, H, K, k, stride, pad
     (4, 64, 14, 64, 1, 1, 0), (4, 64, 14, 128, 3, 1, 1), (4, 128, 15, 64, 3, 2, 1),
     (2, 256, 14, 128, 1, 2, 0), (2, 8, 32, 64, 7, 2, 3), (3, 72, 9, 40, 3, 1, 0),
-    (2, 64, 16, 64, 3, 2, 1), (2, 32, 13, 64, 5, 2, 2), (2, 64, 11, 32, 3, 3, 1)]
+    (2, 64, 16, 64, 3, 2, 1), (2, 32, 13, 64, 5, 2, 2), (2, 64, 11, 32, 3, 3, 1),
+    (2, 64, 13, 128, 3, 2, 1), (2, 192, 9, 64, 3, 1, 1), (2, 128, 7, 192, 3, 1, 1)]
 
 
+@pytest.mark.parametrize('tile', G.TILES)
 @pytest.mark.parametrize('shape', CONV_SHAPES)
-def test_conv_passes(shape):
+def test_conv_passes(shape, tile):
     N, C, H, K, k, s, p = shape
     x = torch.randn(N, C, H, H, device=DEV).bfloat16().contiguous(memory_format=CL)
     w = (torch.randn(K, C, k, k, device=DEV) * 0.1).bfloat16().contiguous(memory_format=CL)
-    y = CI.try_forward(x, w, (s, s), (p, p))
+    y = CI.try_forward(x, w, (s, s), (p, p), tile=tile)
     xf = x.float().requires_grad_(True)
     wf = w.float().requires_grad_(True)
     ref = F.conv2d(xf, wf, None, s, p)
@@ -75,11 +84,11 @@ def test_conv_passes(shape):
     assert _rel(y, ref) < 1e-2
     dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
     ref.backward(dy.float())
-    dx = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p))
+    dx = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p), tile=tile)
     assert dx is not None and _rel(dx, xf.grad) < 1e-2
     r = torch.randn_like(x)
-    dx2 = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p), acc=r)
+    dx2 = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p), acc=r, tile=tile)
     assert dx2 is not None and _rel(dx2, xf.grad + r.float()) < 1e-2
-    dw = CI.try_backward_filter(dy, x, w.shape, (s, s), (p, p))
+    dw = CI.try_backward_filter(dy, x, w.shape, (s, s), (p, p), tile=tile)
     assert dw is not None and dw.dtype == torch.float32
     assert _rel(dw, wf.grad) < 1e-2

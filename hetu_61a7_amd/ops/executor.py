@@ -39,7 +39,11 @@ from ..stream import Stream, Event
 # ---------------------------------------------------------------------------
 # graph utilities
 def find_topo_sort(node_list) -> List[Op]:
-    """Iterative post-order DFS (no recursion limit on deep nets)."""
+    """Iterative post-order DFS (no recursion limit on deep nets).
+
+    A node may set ``topo_input_order`` (a permutation of its input indices) to
+    change the order its inputs are visited in; the optimizer uses it to order the
+    weight-gradient computations (see ``OptimizerOp.backward_hook``)."""
     visited = set()
     order = []
     for root in node_list:
@@ -53,7 +57,8 @@ def find_topo_sort(node_list) -> List[Op]:
                     continue
             if i < len(node.inputs):
                 stack.append((node, i + 1))
-                child = node.inputs[i]
+                perm = getattr(node, 'topo_input_order', None)
+                child = node.inputs[perm[i] if perm is not None else i]
                 if child is not None and child not in visited:
                     stack.append((child, 0))
             else:

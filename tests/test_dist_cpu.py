@@ -112,3 +112,49 @@ def test_zero1_matches_single_process(opt):
             assert info['state'] == info['padded'] // 2     # optimizer state sharded over 2 ranks
         for name, v in base_params.items():
             np.testing.assert_allclose(params[name], v, rtol=2e-4, atol=2e-5)
+
+
+def _resnet_worker(rank, world, port, q):
+    """bench.py's ResNet-50 data-parallel path (DataParallel('allreduce'), bucketed
+    SUM all-reduce, momentum SGD with lr/N) on gloo, 1 image per rank."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), HETU_USE_CONFIG='0')
+    torch.set_num_threads(2)
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.models import resnet50_imagenet
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    loss, _ = resnet50_imagenet(x, y_, 10)
+    train = ht.optim.MomentumOptimizer(learning_rate=0.1 / world, momentum=0.9).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'),
+                     mixed_precision='bf16', bucket_mb=8, seed=1234)
+    rng = np.random.RandomState(100 + rank)
+    X = rng.randn(1, 3, 224, 224).astype(np.float32)
+    Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 1)]
+    losses = [float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0])
+              for _ in range(2)]
+    params = {n.name: v.numpy().copy() for n, v in ex.config.placeholder_to_arr_map.items()
+              if n.trainable and ('fc' in n.name or n.name.startswith('stem'))}
+    q.put((rank, losses, params, len(train.buckets)))
+    from hetu_61a7_amd.parallel import comm
+    comm.destroy()
+
+
+def test_resnet50_dp_bench_path_keeps_replicas_identical():
+    """Rehearsal of the driver's N-GPU bench: every rank must hold identical weights
+    after each all-reduced step (per-rank data differs)."""
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_resnet_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (_, l0, p0, nb0), (_, l1, p1, nb1) = res
+    assert np.all(np.isfinite(l0 + l1)) and l0 != l1        # different data per rank
+    assert nb0 == nb1 and nb0 > 1                            # several buckets exercised
+    assert p0.keys() == p1.keys() and len(p0) >= 3
+    for k in p0:
+        np.testing.assert_array_equal(p0[k], p1[k])

@@ -139,6 +139,55 @@ __global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict
   }
 }
 
+// Same merge from per-channel totals (sum, sum of squares) accumulated elsewhere: by
+// the convolution epilogue that produced x (gemm.hip colstats) or by bn_sums_merge.
+__global__ void __launch_bounds__(256) bn_sums_finalize(const float* __restrict__ sums, int64_t M, int C,
+                                 const float* __restrict__ scale, const float* __restrict__ bias,
+                                 float* __restrict__ run_mean, float* __restrict__ run_var,
+                                 float factor, float eps, float* __restrict__ save_mean,
+                                 float* __restrict__ save_invstd, float* __restrict__ fold_a,
+                                 float* __restrict__ fold_b) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double n = (double)M;
+  const double mean = (double)sums[c] / n;
+  double var = (double)sums[C + c] / n - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = rsqrtf((float)var + eps);
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  if (run_mean != nullptr) {
+    const float unb = n > 1.0 ? (float)(var * n / (n - 1.0)) : (float)var;
+    run_mean[c] = (1.f - factor) * run_mean[c] + factor * (float)mean;
+    run_var[c] = (1.f - factor) * run_var[c] + factor * unb;
+  }
+  const float aa = scale[c] * invstd;
+  fold_a[c] = aa;
+  fold_b[c] = bias[c] - (float)mean * aa;
+}
+
+// per-channel totals from the [C][chunks] partials of bn_stats_partial
+__global__ void __launch_bounds__(256) bn_sums_merge(const float* __restrict__ ws_s, const float* __restrict__ ws_q,
+                                                      int chunks, int C, float* __restrict__ sums) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  double S = 0.0, Q = 0.0;
+  for (int p = lane; p < chunks; p += 64) {
+    S += (double)ws_s[(int64_t)c * chunks + p];
+    Q += (double)ws_q[(int64_t)c * chunks + p];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    S += __shfl_xor(S, o, 64);
+    Q += __shfl_xor(Q, o, 64);
+  }
+  if (lane == 0) {
+    sums[c] = (float)S;
+    sums[C + c] = (float)Q;
+  }
+}
+
 // inference: fold running stats
 __global__ void bn_infer_fold(const float* __restrict__ run_mean, const float* __restrict__ run_var,
                               const float* __restrict__ scale, const float* __restrict__ bias, int C,
@@ -430,13 +479,16 @@ template <typename T>
 static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                        const float* bias, float* run_mean, float* run_var, float factor, float eps,
                        float* save_mean, float* save_invstd, float* ws, int relu, int training,
-                       hipStream_t st) {
+                       const float* sums, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
   float* fa = ws + 2 * (int64_t)g.chunks * C;
   float* fb = fa + C;
-  if (training) {
+  if (training && sums) {   // statistics already reduced (fused into the producer)
+    hipLaunchKernelGGL(bn_sums_finalize, dim3((C + 255) / 256), dim3(256), 0, st, sums, M, C, scale,
+                       bias, run_mean, run_var, factor, eps, save_mean, save_invstd, fa, fb);
+  } else if (training) {
     float* wm = ws;
     float* wq = ws + (int64_t)g.chunks * C;
     hipLaunchKernelGGL(bn_stats_partial<T>, dim3(g.chunks, g.tiles), dim3(256), 0, st,
@@ -473,12 +525,31 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
 HETU_API int hetu_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int is_bf16,
                          const float* scale, const float* bias, float* run_mean, float* run_var,
                          float factor, float eps, float* save_mean, float* save_invstd, float* ws,
-                         int relu, int training, hipStream_t st) {
+                         int relu, int training, const float* sums, hipStream_t st) {
   if (is_bf16)
     return bn_fwd_impl<bf16>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
-                             save_mean, save_invstd, ws, relu, training, st);
+                             save_mean, save_invstd, ws, relu, training, sums, st);
   return bn_fwd_impl<float>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
-                            save_mean, save_invstd, ws, relu, training, st);
+                            save_mean, save_invstd, ws, relu, training, sums, st);
+}
+
+// sums[0..C) / sums[C..2C) = per-channel sum / sum of squares of x [M, C] (fp64 merge)
+HETU_API int hetu_col_sums(const void* x, int64_t M, int C, int is_bf16, float* ws, float* sums,
+                           hipStream_t st) {
+  const int V = is_bf16 ? 8 : 4;
+  if (C % V != 0) return (int)hipErrorInvalidValue;
+  BnGeom g = bn_geom(M, C, V);
+  float* wm = ws;
+  float* wq = ws + (int64_t)g.chunks * C;
+  if (is_bf16)
+    hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(g.chunks, g.tiles), dim3(256), 0, st, (const bf16*)x,
+                       M, C, g.W, g.RP, g.rows_per_chunk, wm, wq);
+  else
+    hipLaunchKernelGGL(bn_stats_partial<float>, dim3(g.chunks, g.tiles), dim3(256), 0, st, (const float*)x,
+                       M, C, g.W, g.RP, g.rows_per_chunk, wm, wq);
+  hipLaunchKernelGGL(bn_sums_merge, dim3((C + 3) / 4), dim3(256), 0, st, wm, wq, g.chunks, C, sums);
+  HETU_LAUNCH_CHECK();
+  return 0;
 }
 
 template <typename T, int RELU>

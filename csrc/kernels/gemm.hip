@@ -394,7 +394,51 @@ struct Epi {
   int bias_on_m;  // bias indexed by m instead of n
   float* slab;    // split-K: fp32 partial tiles, slab z at slab + z*slab_stride (ld = N)
   int64_t slab_stride;
+  // per-column sum / sum of squares of the stored outputs (fp32 atomics into
+  // colstats[0..N) and colstats[N..2N), pre-zeroed): the BatchNorm statistics of a
+  // convolution output, fused into the epilogue that already holds the values
+  float* colstats;
 };
+
+// column statistics of one epilogue: each thread holds sums of its 8 columns over
+// its rows; threads sharing columns are folded by lane shuffles (lanes l ^ 16k within
+// a wave), then across waves through LDS, one atomic per column per block.
+//   groups: threads per row (16 for the 128-wide tile, 32 for the 256-wide tile)
+template <int GROUPS, int NWAVES>
+__device__ __forceinline__ void epilogue_colstats(float (&cs)[8], float (&cq)[8], float* lds, int tid,
+                                                  int64_t n0, int64_t N, float* colstats) {
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+#pragma unroll
+    for (int o = GROUPS; o < 64; o <<= 1) {
+      cs[t] += __shfl_xor(cs[t], o, 64);
+      cq[t] += __shfl_xor(cq[t], o, 64);
+    }
+  }
+  __syncthreads();   // the staging area is free again
+  if (lane < GROUPS) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      lds[(wave * GROUPS + lane) * 8 + t] = cs[t];
+      lds[NWAVES * GROUPS * 8 + (wave * GROUPS + lane) * 8 + t] = cq[t];
+    }
+  }
+  __syncthreads();
+  if (tid < GROUPS * 8) {
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWAVES; ++w) {
+      S += lds[w * GROUPS * 8 + tid];
+      Q += lds[NWAVES * GROUPS * 8 + w * GROUPS * 8 + tid];
+    }
+    const int64_t n = n0 + tid;
+    if (n < N) {
+      unsafeAtomicAdd(colstats + n, S);
+      unsafeAtomicAdd(colstats + N + n, Q);
+    }
+  }
+}
 
 __device__ __forceinline__ float act_f(float v, int act) {
   if (act == 1) return v > 0.f ? v : 0.f;
@@ -504,6 +548,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
   const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
   if (!ep.atomic) {
+    float cs[8], cq[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { cs[t] = 0.f; cq[t] = 0.f; }
     // Row-coalesced epilogue: the tile goes through LDS in two 64-row halves
     // (fp32, rows padded by 4 floats so the 16-row MFMA write pattern spreads
     // over the banks), then 16 lanes cover one 128-column row with 8 elements
@@ -589,9 +636,19 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
               if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
           }
         }
+        if (ep.colstats) {   // statistics of the values as stored
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));
+            cs[t] += sv;
+            cq[t] += sv * sv;
+          }
+        }
       }
       __syncthreads();
     }
+    if (ep.colstats)
+      epilogue_colstats<16, 4>(cs, cq, stg, tid, (int64_t)tn * BN, N, ep.colstats);
     return;
   }
 #pragma unroll
@@ -854,6 +911,9 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
                                : ((ep.ldc & 7) == 0 && ((uintptr_t)Cb & 15) == 0);
   const bool ivec = Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)Cinb & 15) == 0)
                                         : ((ep.ldcin & 7) == 0 && ((uintptr_t)Cinb & 15) == 0));
+  float cs[8], cq[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) { cs[t] = 0.f; cq[t] = 0.f; }
   // 4 passes of 64 rows through LDS (64 x 260 fp32 = 66.5 KiB), full-row stores
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
@@ -929,9 +989,18 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
             if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
         }
       }
+      if (ep.colstats) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));
+          cs[t] += sv;
+          cq[t] += sv * sv;
+        }
+      }
     }
     __syncthreads();
   }
+  if (ep.colstats) epilogue_colstats<32, 8>(cs, cq, stg, tid, (int64_t)tn * BIG, N, ep.colstats);
 }
 
 // dst[m][n] (ld ldd, fp32 or bf16) (+)= sum_z slab[z][m][n]
@@ -1075,12 +1144,14 @@ static ConvGeom geom(int N, int H, int W, int C, int K, int KH, int KW, int sh, 
 }
 
 // y[N,OH,OW,K] (NHWC) = conv(x[N,H,W,C] NHWC, w[K,KH,KW,C]) (+bias[K]) -> act.  C % 8 == 0.
+// colstats (optional, 2*K floats, zeroed by the caller) += per-channel sum and sum of
+// squares of the stored y: the statistics a training-mode BatchNorm on y needs.
 HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const float* bias, int N,
                                 int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
-                                int pw, int act, int tile, hipStream_t st) {
+                                int pw, int act, float* colstats, int tile, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t M = (int64_t)N * g.OH * g.OW, Kt = (int64_t)KH * KW * C;
-  Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0, nullptr, 0};
+  Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0, nullptr, 0, colstats};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
     return launch(PlainK{(const bf16*)x, C, M, C, 0}, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M,
                   K, Kt, 1, 1, st, tile);

@@ -84,6 +84,55 @@ def _match(x, w):
     return x, w
 
 
+def conv2d_with_stats(x, w, stride, padding):
+    """(y, sums): the convolution (no bias) and the [2*Cout] per-channel sum / sum of
+    squares of y that a following training-mode BatchNorm needs.  Every candidate
+    delivers both, so the per-shape choice prices the statistics pass in: the
+    hand-written kernels fuse it into their epilogue, the library convolutions pay a
+    separate column-statistics pass."""
+    x, w = _match(x, w)
+    if not (x.is_cuda and x.dtype == torch.bfloat16):
+        return conv2d(x, w, None, stride, padding), None
+    from . import conv_igemm
+    from .norm import col_sums
+    x = x.contiguous(memory_format=CL)
+    w = w.contiguous(memory_format=CL)
+    co = w.shape[0]
+
+    def fused(run):
+        def f():
+            s = torch.zeros(2 * co, dtype=torch.float32, device=x.device)
+            y = run(s)
+            return None if y is None else (y, s)
+        return f
+
+    def separate(run):
+        def f():
+            y = run()
+            return None if y is None else (y, col_sums(y))
+        return f
+    cands = {'hip': fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, colstats=s)),
+             'vendor': separate(lambda: F.conv2d(x, w, None, stride, padding))}
+    if co >= 128:
+        cands['hip256'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=1, colstats=s))
+    if _plain_1x1((x, w), w.shape, stride, padding):
+        n, _, h, ww_ = x.shape
+        cands['blas'] = separate(lambda: torch.mm(_rows(x), w.reshape(co, -1).t()).view(n, h, ww_, co)
+                                 .permute(0, 3, 1, 2))
+    elif _needs_pad(x, w):
+        cands['hip_pad'] = fused(lambda s: conv_igemm.try_forward(_pad_c(x), _pad_c(w), stride, padding,
+                                                                   colstats=s))
+    key = ('fwd_stats', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding))
+    if MODE == 'vendor':
+        return cands['vendor']()
+    from .autotune import choose
+    c = 'hip' if MODE == 'hip' else choose(key, cands)
+    r = cands[c]()
+    if r is None:
+        r = cands['vendor']()
+    return r
+
+
 def conv2d(x, w, b, stride, padding):
     x, w = _match(x, w)
     if x.is_cuda:

@@ -33,18 +33,21 @@ def _out_hw(H, W, KH, KW, stride, padding):
     return (H + 2 * padding[0] - KH) // stride[0] + 1, (W + 2 * padding[1] - KW) // stride[1] + 1
 
 
-def try_forward(x, w, stride, padding, bias=None, act=None, tile=0):
+def try_forward(x, w, stride, padding, bias=None, act=None, tile=0, colstats=None):
+    """``colstats`` ([2*Cout] fp32, zeroed): receives the per-channel sum and sum of
+    squares of the stored output (BatchNorm statistics fused into the epilogue)."""
     if not _ok(x, w, x.shape[1], w.shape[0]):
         return None
     N, C, H, W = x.shape
     K, _, KH, KW = w.shape
     OH, OW = _out_hw(H, W, KH, KW, stride, padding)
     y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
-    f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, I32, P])
+    f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, P, I32, P])
     check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(),
             bias.float().contiguous().data_ptr() if bias is not None else None,
             N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
-            {None: 0, 'relu': 1}[act], int(tile), stream_ptr()), 'conv_fwd')
+            {None: 0, 'relu': 1}[act], colstats.data_ptr() if colstats is not None else None, int(tile),
+            stream_ptr()), 'conv_fwd')
     return y.permute(0, 3, 1, 2)
 
 

@@ -31,10 +31,28 @@ def _ws(M, C, bf, device):
     return torch.empty(n, dtype=torch.float32, device=device)
 
 
+def col_sums(x):
+    """[2, C] fp32: per-channel sum and sum of squares of a channels-last activation
+    (the BatchNorm statistics inputs), or None where the native path does not apply."""
+    rows = _as_rows(x) if native(x) and x.dtype in (torch.float32, torch.bfloat16) else None
+    C = x.shape[1]
+    if rows is None or C % (8 if x.dtype == torch.bfloat16 else 4):
+        return None
+    xr, _ = rows
+    M = xr.shape[0]
+    sums = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    ws = _ws(M, C, is_bf16(x), x.device)
+    f = fn('hetu_col_sums', [P, I64, I32, I32, P, P, P])
+    check(f(xr.data_ptr(), M, C, is_bf16(x), ws.data_ptr(), sums.data_ptr(), stream_ptr()), 'col_sums')
+    return sums
+
+
 def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
-               relu=False, residual=None):
+               relu=False, residual=None, sums=None):
     """Returns (y, save_mean, save_invstd).  ``factor`` = weight of the new batch
-    statistics in the running average."""
+    statistics in the running average.  ``sums`` ([2C] fp32 per-channel sum and sum
+    of squares of x, e.g. from the convolution epilogue that produced x) skips the
+    statistics pass."""
     C = x.shape[1]
     if native(x) and x.dtype in (torch.float32, torch.bfloat16):
         if x.dim() == 4 and not x.is_contiguous(memory_format=torch.channels_last):
@@ -50,13 +68,14 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
             save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
             save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
             ws = _ws(M, C, is_bf16(x), x.device)
-            f = fn('hetu_bn_fwd', [P, P, P, I64, I32, I32, P, P, P, P, F32, F32, P, P, P, I32, I32, P])
+            f = fn('hetu_bn_fwd', [P, P, P, I64, I32, I32, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P])
             check(f(x.data_ptr(), residual.data_ptr() if residual is not None else None, y.data_ptr(),
                     M, C, is_bf16(x), scale.data_ptr(), bias.data_ptr(),
                     running_mean.data_ptr() if running_mean is not None else None,
                     running_var.data_ptr() if running_var is not None else None,
                     float(factor), float(eps), save_mean.data_ptr(), save_invstd.data_ptr(),
-                    ws.data_ptr(), int(relu), int(training), stream_ptr()), 'bn_fwd')
+                    ws.data_ptr(), int(relu), int(training),
+                    sums.data_ptr() if (sums is not None and training) else None, stream_ptr()), 'bn_fwd')
             return y, save_mean, save_invstd
     # torch reference (CPU backend / unsupported layouts)
     xf = x.float()

@@ -60,6 +60,7 @@ def _worker(rank, env, q, pull):
     table = cfg.placeholder_to_arr_map[E]
     E0 = table.to_dense().numpy().copy()
     W0 = cfg.placeholder_to_arr_map[W].numpy().copy()
+    cfg.ps_comm.BarrierWorker()   # both workers read the initial table before any push
     l0 = float(ex.run('train', feed_dict={xs: ids, y_: lab}, convert_to_numpy_ret_vals=True)[0])
     cfg.ps_comm.BarrierWorker()
     E1 = table.to_dense().numpy().copy()

@@ -16,8 +16,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -33,96 +35,261 @@
 
 namespace hc {
 
+// A cached row: header + its data and pending-gradient vectors live in one pooled
+// record (no per-line heap allocations); policy lists are intrusive.
+struct FreqNode;
 struct Line {
   int64_t key;
   int64_t ver;      // server version this line reflects
   int64_t updates;  // local updates not yet pushed
   int64_t freq;
-  std::vector<float> data;
-  std::vector<float> grad;
+  Line* prev;
+  Line* next;
+  FreqNode* fnode;  // LFU bucket
+  bool cached;
+  float* data;
+  float* grad;
 };
-using LineP = std::shared_ptr<Line>;
+
+struct DList {  // intrusive doubly-linked list of lines, most recent at head
+  Line* head = nullptr;
+  Line* tail = nullptr;
+  bool empty() const { return head == nullptr; }
+  void push_front(Line* l) {
+    l->prev = nullptr;
+    l->next = head;
+    if (head) head->prev = l;
+    head = l;
+    if (!tail) tail = l;
+  }
+  void remove(Line* l) {
+    if (l->prev) l->prev->next = l->next; else head = l->next;
+    if (l->next) l->next->prev = l->prev; else tail = l->prev;
+    l->prev = l->next = nullptr;
+  }
+};
+
+// open-addressing int64 -> Line* map (linear probing, backward-shift deletion)
+class KeyMap {
+ public:
+  KeyMap() { rehash(1024); }
+  Line* find(int64_t k) const {
+    for (size_t i = slot(k);; i = (i + 1) & mask_) {
+      if (keys_[i] == kEmpty) return nullptr;
+      if (keys_[i] == k) return vals_[i];
+    }
+  }
+  void insert(int64_t k, Line* v) {
+    if ((size_ + 1) * 2 > keys_.size()) rehash(keys_.size() * 2);
+    size_t i = slot(k);
+    while (keys_[i] != kEmpty && keys_[i] != k) i = (i + 1) & mask_;
+    if (keys_[i] == kEmpty) ++size_;
+    keys_[i] = k;
+    vals_[i] = v;
+  }
+  void erase(int64_t k) {
+    size_t i = slot(k);
+    while (keys_[i] != k) {
+      if (keys_[i] == kEmpty) return;
+      i = (i + 1) & mask_;
+    }
+    // backward shift: move later entries of the probe run into the hole
+    size_t j = i;
+    for (;;) {
+      j = (j + 1) & mask_;
+      if (keys_[j] == kEmpty) break;
+      size_t h = slot(keys_[j]);
+      const bool between = (i <= j) ? (i < h && h <= j) : (i < h || h <= j);
+      if (!between) {
+        keys_[i] = keys_[j];
+        vals_[i] = vals_[j];
+        i = j;
+      }
+    }
+    keys_[i] = kEmpty;
+    --size_;
+  }
+  size_t size() const { return size_; }
+  template <class F> void for_each(F f) const {
+    for (size_t i = 0; i < keys_.size(); ++i)
+      if (keys_[i] != kEmpty) f(vals_[i]);
+  }
+  void clear() {
+    keys_.assign(1024, kEmpty);
+    vals_.assign(1024, nullptr);
+    mask_ = 1023;
+    size_ = 0;
+  }
+
+ private:
+  static constexpr int64_t kEmpty = INT64_MIN;
+  size_t slot(int64_t k) const {
+    uint64_t x = (uint64_t)k + 0x9e3779b97f4a7c15ull;   // splitmix64 finaliser
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return (size_t)(x ^ (x >> 31)) & mask_;
+  }
+  void rehash(size_t cap) {
+    std::vector<int64_t> ok;
+    std::vector<Line*> ov;
+    ok.swap(keys_);
+    ov.swap(vals_);
+    keys_.assign(cap, kEmpty);
+    vals_.assign(cap, nullptr);
+    mask_ = cap - 1;
+    size_ = 0;
+    for (size_t i = 0; i < ok.size(); ++i)
+      if (ok[i] != kEmpty) insert(ok[i], ov[i]);
+  }
+  std::vector<int64_t> keys_;
+  std::vector<Line*> vals_;
+  size_t mask_ = 0, size_ = 0;
+};
+
+// fixed-size record pool: Line header + 2*width floats per record
+class LinePool {
+ public:
+  explicit LinePool(int64_t width) : width_(width) {}
+  Line* get() {
+    if (free_.empty()) grow();
+    Line* l = free_.back();
+    free_.pop_back();
+    return l;
+  }
+  void put(Line* l) { free_.push_back(l); }
+  void reset() {
+    free_.clear();
+    chunks_.clear();
+  }
+
+ private:
+  void grow() {
+    const size_t rec = sizeof(Line) + 2 * (size_t)width_ * sizeof(float);
+    const size_t recr = (rec + 63) & ~(size_t)63;
+    const size_t n = 4096;
+    chunks_.emplace_back(new char[recr * n + 64]);
+    char* base = (char*)(((uintptr_t)chunks_.back().get() + 63) & ~(uintptr_t)63);
+    for (size_t i = 0; i < n; ++i) {
+      Line* l = reinterpret_cast<Line*>(base + i * recr);
+      l->data = reinterpret_cast<float*>((char*)l + sizeof(Line));
+      l->grad = l->data + width_;
+      free_.push_back(l);
+    }
+  }
+  int64_t width_;
+  std::vector<Line*> free_;
+  std::vector<std::unique_ptr<char[]>> chunks_;
+};
 
 class Policy {
  public:
   virtual ~Policy() {}
-  virtual LineP find(int64_t k) = 0;
-  virtual void touch(const LineP& l) = 0;
-  virtual void insert(const LineP& l) = 0;
-  virtual LineP evict() = 0;  // removes and returns the victim
-  virtual size_t size() const = 0;
+  virtual void touch(Line* l) = 0;
+  virtual void insert(Line* l) = 0;
+  virtual Line* evict() = 0;  // unlinks and returns the victim
+  virtual void reset() = 0;
 };
 
 class LRU : public Policy {
  public:
-  LineP find(int64_t k) override {
-    auto it = map_.find(k);
-    return it == map_.end() ? nullptr : *it->second;
-  }
-  void touch(const LineP& l) override {
-    auto it = map_.find(l->key);
-    lst_.splice(lst_.begin(), lst_, it->second);
-  }
-  void insert(const LineP& l) override {
+  void touch(Line* l) override {
+    lst_.remove(l);
     lst_.push_front(l);
-    map_[l->key] = lst_.begin();
   }
-  LineP evict() override {
-    LineP v = lst_.back();
-    map_.erase(v->key);
-    lst_.pop_back();
+  void insert(Line* l) override { lst_.push_front(l); }
+  Line* evict() override {
+    Line* v = lst_.tail;
+    if (v) lst_.remove(v);
     return v;
   }
-  size_t size() const override { return map_.size(); }
+  void reset() override { lst_ = DList(); }
 
  private:
-  std::list<LineP> lst_;
-  std::unordered_map<int64_t, std::list<LineP>::iterator> map_;
+  DList lst_;
+};
+
+// O(1) LFU: an ascending list of frequency buckets, each an intrusive list of lines
+// (most recently touched first); eviction takes the oldest line of the lowest bucket.
+struct FreqNode {
+  int64_t freq;
+  DList lines;
+  FreqNode* prev;
+  FreqNode* next;
 };
 
 class LFU : public Policy {
  public:
   explicit LFU(bool opt) : opt_(opt) {}
-  LineP find(int64_t k) override {
-    auto it = map_.find(k);
-    return it == map_.end() ? nullptr : it->second.line;
+  ~LFU() override { reset(); }
+  void touch(Line* l) override {
+    FreqNode* f = l->fnode;
+    const int64_t nf = f->freq + 1;
+    FreqNode* g = f->next;
+    if (!g || g->freq != nf) g = link_after(f, nf);
+    f->lines.remove(l);
+    g->lines.push_front(l);
+    l->fnode = g;
+    l->freq = nf;
+    if (f->lines.empty()) unlink(f);
   }
-  void touch(const LineP& l) override {
-    auto& ent = map_[l->key];
-    auto& bucket = buckets_[l->freq];
-    bucket.erase(ent.it);
-    if (bucket.empty()) buckets_.erase(l->freq);
-    l->freq += 1;
-    auto& nb = buckets_[l->freq];
-    nb.push_front(l);
-    ent.it = nb.begin();
-  }
-  void insert(const LineP& l) override {
+  void insert(Line* l) override {
     // LFUOpt: a new line enters at the minimum live frequency instead of 1, so a
     // burst of new keys does not immediately evict each other
-    if (opt_ && !buckets_.empty()) l->freq = std::max<int64_t>(l->freq, buckets_.begin()->first);
-    auto& b = buckets_[l->freq];
-    b.push_front(l);
-    map_[l->key] = Ent{l, b.begin()};
+    int64_t f0 = l->freq;
+    if (opt_ && head_) f0 = std::max<int64_t>(f0, head_->freq);
+    FreqNode* g = head_;
+    if (!g || g->freq != f0) {
+      // f0 <= every live frequency (plain LFU inserts at 1, LFUOpt at the minimum)
+      g = link_after(nullptr, f0);
+    }
+    g->lines.push_front(l);
+    l->fnode = g;
+    l->freq = f0;
   }
-  LineP evict() override {
-    auto bit = buckets_.begin();
-    LineP v = bit->second.back();
-    bit->second.pop_back();
-    if (bit->second.empty()) buckets_.erase(bit);
-    map_.erase(v->key);
+  Line* evict() override {
+    FreqNode* h = head_;
+    if (!h) return nullptr;
+    Line* v = h->lines.tail;
+    h->lines.remove(v);
+    if (h->lines.empty()) unlink(h);
     return v;
   }
-  size_t size() const override { return map_.size(); }
+  void reset() override {
+    for (FreqNode* f = head_; f;) {
+      FreqNode* n = f->next;
+      delete f;
+      f = n;
+    }
+    head_ = nullptr;
+    for (FreqNode* f : spare_) delete f;
+    spare_.clear();
+  }
 
  private:
-  struct Ent {
-    LineP line;
-    std::list<LineP>::iterator it;
-  };
+  FreqNode* link_after(FreqNode* f, int64_t freq) {
+    FreqNode* g;
+    if (!spare_.empty()) {
+      g = spare_.back();
+      spare_.pop_back();
+    } else {
+      g = new FreqNode();
+    }
+    g->freq = freq;
+    g->lines = DList();
+    g->prev = f;
+    g->next = f ? f->next : head_;
+    if (g->next) g->next->prev = g;
+    if (f) f->next = g; else head_ = g;
+    return g;
+  }
+  void unlink(FreqNode* f) {
+    if (f->prev) f->prev->next = f->next; else head_ = f->next;
+    if (f->next) f->next->prev = f->prev;
+    spare_.push_back(f);
+  }
   bool opt_;
-  std::map<int64_t, std::list<LineP>> buckets_;
-  std::unordered_map<int64_t, Ent> map_;
+  FreqNode* head_ = nullptr;
+  std::vector<FreqNode*> spare_;
 };
 
 struct Perf {
@@ -130,67 +297,200 @@ struct Perf {
   double t_unique = 0, t_sync = 0, t_copy = 0, t_push = 0;
 };
 
+// Small persistent fork-join pool for the cache's row-copy / gradient loops, which
+// are host-memory-bandwidth bound on one thread (HETU_CACHE_THREADS, default 4).
+class ParallelFor {
+ public:
+  ParallelFor() {
+    int n = 4;
+    if (const char* e = getenv("HETU_CACHE_THREADS")) n = atoi(e);
+    n = std::max(1, std::min(n, 64));
+    for (int i = 1; i < n; ++i) th_.emplace_back([this] { worker(); });
+    nthreads_ = n;
+  }
+  ~ParallelFor() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // fn(begin, end) over [0, n) in chunks; runs inline when small or single-threaded
+  void run(int64_t n, int64_t min_chunk, const std::function<void(int64_t, int64_t)>& fn) {
+    if (nthreads_ == 1 || n < 2 * min_chunk) {
+      fn(0, n);
+      return;
+    }
+    std::lock_guard<std::mutex> call(call_mu_);   // one parallel region at a time
+    const int64_t parts = std::min<int64_t>(nthreads_, n / min_chunk);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fn_ = &fn;
+      n_ = n;
+      parts_ = parts;
+      next_.store(0);
+      done_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return done_ == parts_; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const int64_t p = next_.fetch_add(1);
+      if (p >= parts_) return;
+      const int64_t b = n_ * p / parts_, e = n_ * (p + 1) / parts_;
+      (*fn_)(b, e);
+      std::lock_guard<std::mutex> g(mu_);
+      if (++done_ == parts_) done_cv_.notify_all();
+    }
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        if (!fn_) continue;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> th_;
+  int nthreads_ = 1;
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int64_t, int64_t)>* fn_ = nullptr;
+  int64_t n_ = 0, parts_ = 0, done_ = 0;
+  std::atomic<int64_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+static ParallelFor& pool() {
+  static ParallelFor p;
+  return p;
+}
+
+// De-duplication of a batch of keys in O(n): an open-addressing scratch table
+// (reused across calls, cleared by generation stamps) maps each key to its first
+// occurrence.  uniq = distinct keys in first-seen order, pos[r] = index of keys[r].
+class Dedup {
+ public:
+  void run(const int64_t* keys, int64_t n, std::vector<int64_t>& uniq, std::vector<int32_t>& pos) {
+    size_t cap = 64;
+    while (cap < (size_t)n * 2) cap <<= 1;
+    if (cap > tkey_.size()) {
+      tkey_.assign(cap, 0);
+      tidx_.assign(cap, 0);
+      tgen_.assign(cap, 0);
+      gen_ = 0;
+    }
+    const size_t mask = cap - 1;
+    if (++gen_ == 0) {               // stamp wrap-around: clear once
+      std::fill(tgen_.begin(), tgen_.end(), 0);
+      gen_ = 1;
+    }
+    uniq.clear();
+    pos.resize(n);
+    for (int64_t r = 0; r < n; ++r) {
+      const int64_t k = keys[r];
+      uint64_t x = (uint64_t)k * 0x9e3779b97f4a7c15ull;
+      size_t i = (size_t)(x >> 32) & mask;
+      for (;; i = (i + 1) & mask) {
+        if (tgen_[i] != gen_) {
+          tgen_[i] = gen_;
+          tkey_[i] = k;
+          tidx_[i] = (int32_t)uniq.size();
+          uniq.push_back(k);
+          break;
+        }
+        if (tkey_[i] == k) break;
+      }
+      pos[r] = tidx_[i];
+    }
+  }
+
+ private:
+  std::vector<int64_t> tkey_;
+  std::vector<int32_t> tidx_;
+  std::vector<uint32_t> tgen_;
+  uint32_t gen_ = 0;
+};
+
 class Cache {
  public:
   Cache(int policy, int64_t limit, int64_t rows, int64_t width, int key, int64_t pull_bound,
         int64_t push_bound)
       : limit_(limit), rows_(rows), width_(width), key_(key), pull_bound_(pull_bound),
-        push_bound_(push_bound), policy_(policy) {
-    if (policy == 0) pol_.reset(new LRU());
-    else pol_.reset(new LFU(policy == 2));
+        push_bound_(push_bound), policy_(policy), pool_(width) {
+    make_policy();
   }
+  ~Cache() { pol_.reset(); }
 
   void lookup(const int64_t* keys, int64_t n, float* dest) {
     std::lock_guard<std::mutex> g(mu_);
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<int64_t> uniq(keys, keys + n);
-    std::sort(uniq.begin(), uniq.end());
-    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    dedup_.run(keys, n, uniq_, pos_);
     auto t1 = std::chrono::steady_clock::now();
-    const int64_t u = (int64_t)uniq.size();
-    std::vector<int64_t> vers(u);
-    std::vector<LineP> lines(u);
+    const int64_t u = (int64_t)uniq_.size();
+    vers_.resize(u);
+    lines_.resize(u);
     int64_t miss = 0;
     for (int64_t i = 0; i < u; ++i) {
-      lines[i] = pol_->find(uniq[i]);
-      vers[i] = lines[i] ? lines[i]->ver : -1;
-      if (!lines[i]) ++miss;
+      Line* l = map_.find(uniq_[i]);
+      lines_[i] = l;
+      vers_[i] = (l && !bypass_) ? l->ver : -1;
+      miss += l == nullptr;
     }
-    if (bypass_) std::fill(vers.begin(), vers.end(), -1);
-    std::vector<int64_t> idx(u), nver(u);
-    std::vector<float> data((size_t)u * width_);
-    int64_t cnt = hps_sync_embedding(key_, uniq.data(), u, vers.data(), pull_bound_, idx.data(),
-                                     nver.data(), data.data());
+    idx_.resize(u);
+    nver_.resize(u);
+    if ((int64_t)sync_data_.size() < u * width_) sync_data_.resize((size_t)u * width_);
+    int64_t cnt = hps_sync_embedding(key_, uniq_.data(), u, vers_.data(), pull_bound_, idx_.data(),
+                                     nver_.data(), sync_data_.data());
     auto t2 = std::chrono::steady_clock::now();
     for (int64_t c = 0; c < std::max<int64_t>(cnt, 0); ++c) {
-      int64_t i = idx[c];
-      LineP& l = lines[i];
-      const float* src = data.data() + c * width_;
+      const int64_t i = idx_[c];
+      const float* src = sync_data_.data() + c * width_;
+      Line* l = lines_[i];
       if (!l) {
-        l = std::make_shared<Line>();
-        l->key = uniq[i];
+        l = pool_.get();
+        l->key = uniq_[i];
         l->updates = 0;
         l->freq = 1;
-        l->data.assign(src, src + width_);
-        l->grad.assign(width_, 0.f);
-        l->ver = nver[c];
+        l->prev = l->next = nullptr;
+        l->fnode = nullptr;
+        memcpy(l->data, src, width_ * sizeof(float));
+        memset(l->grad, 0, width_ * sizeof(float));
+        l->ver = nver_[c];
         admit(l);
+        lines_[i] = l;
       } else {
         // server copy + our pending (unpushed) gradient
         for (int64_t j = 0; j < width_; ++j) l->data[j] = src[j] + l->grad[j];
-        l->ver = nver[c];
+        l->ver = nver_[c];
       }
     }
     for (int64_t i = 0; i < u; ++i)
-      if (lines[i] && pol_->find(uniq[i])) pol_->touch(lines[i]);
-    std::unordered_map<int64_t, int64_t> pos;
-    pos.reserve(u * 2);
-    for (int64_t i = 0; i < u; ++i) pos[uniq[i]] = i;
-    for (int64_t r = 0; r < n; ++r) {
-      const LineP& l = lines[pos[keys[r]]];
-      if (l) memcpy(dest + r * width_, l->data.data(), width_ * sizeof(float));
-      else memset(dest + r * width_, 0, width_ * sizeof(float));
-    }
+      if (lines_[i] && lines_[i]->cached) pol_->touch(lines_[i]);
+    pool().run(n, 256, [&](int64_t b, int64_t e) {
+      for (int64_t r = b; r < e; ++r) {
+        const Line* l = lines_[pos_[r]];
+        if (l) memcpy(dest + r * width_, l->data, width_ * sizeof(float));
+        else memset(dest + r * width_, 0, width_ * sizeof(float));
+      }
+    });
+    flush_pending();   // gradients of dirty lines evicted by this batch's admissions
+    release_evicted();
     auto t3 = std::chrono::steady_clock::now();
     if (perf_) {
       perf_rec_.calls++;
@@ -205,54 +505,81 @@ class Cache {
 
   void update(const int64_t* keys, int64_t n, const float* grads) {
     std::lock_guard<std::mutex> g(mu_);
-    std::unordered_map<int64_t, std::vector<float>> acc;
-    acc.reserve(n * 2);
-    for (int64_t r = 0; r < n; ++r) {
-      auto& v = acc[keys[r]];
-      if (v.empty()) v.assign(width_, 0.f);
-      const float* gr = grads + r * width_;
-      for (int64_t j = 0; j < width_; ++j) v[j] += gr[j];
+    dedup_.run(keys, n, ukeys_, pos_);
+    const int64_t u = (int64_t)ukeys_.size();
+    // cached rows take their gradient rows directly (no accumulation pass); rows
+    // the cache does not hold are summed per key and pushed straight through
+    ulines_.resize(u);
+    slot_.assign(u, -1);
+    int64_t nacc = 0;
+    for (int64_t i = 0; i < u; ++i) {
+      Line* l = bypass_ ? nullptr : map_.find(ukeys_[i]);
+      ulines_[i] = l;
+      if (!l) slot_[i] = nacc++;
     }
-    std::vector<int64_t> prow, pupd;
-    std::vector<float> pdata;
-    for (auto& kv : acc) {
-      LineP l = pol_->find(kv.first);
-      if (!l || bypass_) {
-        // not cached: push straight through
-        prow.push_back(kv.first);
-        pupd.push_back(1);
-        pdata.insert(pdata.end(), kv.second.begin(), kv.second.end());
+    acc_.assign((size_t)nacc * width_, 0.f);
+    // rows grouped by key (counting sort), then keys split over threads: every key's
+    // rows are applied by one thread, so lines and accumulators need no locks
+    start_.assign(u + 1, 0);
+    for (int64_t r = 0; r < n; ++r) ++start_[pos_[r] + 1];
+    for (int64_t i = 0; i < u; ++i) start_[i + 1] += start_[i];
+    order_.resize(n);
+    fill_ = start_;
+    for (int64_t r = 0; r < n; ++r) order_[fill_[pos_[r]]++] = r;
+    pool().run(u, 64, [&](int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; ++i) {
+        Line* l = ulines_[i];
+        float* __restrict__ d = l ? l->data : acc_.data() + slot_[i] * width_;
+        float* __restrict__ gg = l ? l->grad : nullptr;
+        const int64_t w = width_;
+        for (int64_t q = start_[i]; q < start_[i + 1]; ++q) {
+          const float* __restrict__ gr = grads + order_[q] * w;
+          if (gg) {
+            for (int64_t j = 0; j < w; ++j) {
+              d[j] += gr[j];
+              gg[j] += gr[j];
+            }
+          } else {
+            for (int64_t j = 0; j < w; ++j) d[j] += gr[j];
+          }
+        }
+      }
+    });
+    for (int64_t i = 0; i < u; ++i) {
+      Line* l = ulines_[i];
+      if (!l) {
+        const float* a = acc_.data() + slot_[i] * width_;
+        prow_.push_back(ukeys_[i]);
+        pupd_.push_back(1);
+        pdata_.insert(pdata_.end(), a, a + width_);
         continue;
       }
-      for (int64_t j = 0; j < width_; ++j) {
-        l->data[j] += kv.second[j];
-        l->grad[j] += kv.second[j];
-      }
       l->updates += 1;
-      if (l->updates > push_bound_) stage_push(l, prow, pupd, pdata);
+      if (l->updates > push_bound_) stage_push(l);
     }
-    flush(prow, pupd, pdata);
+    flush_pending();
   }
 
   void flush_all() {
     std::lock_guard<std::mutex> g(mu_);
-    std::vector<int64_t> prow, pupd;
-    std::vector<float> pdata;
-    for (auto& l : all_lines()) if (l->updates > 0) stage_push(l, prow, pupd, pdata);
-    flush(prow, pupd, pdata);
+    map_.for_each([&](Line* l) {
+      if (l->updates > 0) stage_push(l);
+    });
+    flush_pending();
   }
 
   int64_t size() {
     std::lock_guard<std::mutex> g(mu_);
-    return (int64_t)pol_->size();
+    return (int64_t)map_.size();
   }
   // drop every cached line without pushing (after the server's table was
   // replaced, e.g. a checkpoint load): the next lookup re-pulls all rows
   void clear() {
     std::lock_guard<std::mutex> g(mu_);
-    if (policy_ == 0) pol_.reset(new LRU());
-    else pol_.reset(new LFU(policy_ == 2));
-    live_.clear();
+    make_policy();
+    map_.clear();
+    pool_.reset();
+    evicted_.clear();
   }
   void set_bounds(int64_t pull, int64_t push) { pull_bound_ = pull; push_bound_ = push; }
   void set_bypass(bool b) { bypass_ = b; }
@@ -265,44 +592,45 @@ class Cache {
   }
 
  private:
-  void admit(const LineP& l) {
-    while ((int64_t)pol_->size() >= limit_ && pol_->size() > 0) {
-      LineP v = pol_->evict();
+  void make_policy() {
+    if (policy_ == 0) pol_.reset(new LRU());
+    else pol_.reset(new LFU(policy_ == 2));
+  }
+  void admit(Line* l) {
+    while ((int64_t)map_.size() >= limit_ && map_.size() > 0) {
+      Line* v = pol_->evict();
+      if (!v) break;
       perf_rec_.evict++;
-      if (v->updates > 0) {
-        std::vector<int64_t> prow, pupd;
-        std::vector<float> pdata;
-        stage_push(v, prow, pupd, pdata);
-        flush(prow, pupd, pdata);
-      }
-      live_.erase(v->key);
+      if (v->updates > 0) stage_push(v);
+      map_.erase(v->key);
+      v->cached = false;
+      evicted_.push_back(v);   // freed after this call: lines_ may still point to it
     }
     pol_->insert(l);
-    live_[l->key] = l;
+    map_.insert(l->key, l);
+    l->cached = true;
   }
-  std::vector<LineP> all_lines() {
-    std::vector<LineP> out;
-    for (auto& kv : live_) out.push_back(kv.second);
-    return out;
+  void release_evicted() {
+    for (Line* v : evicted_) pool_.put(v);
+    evicted_.clear();
   }
-  void stage_push(const LineP& l, std::vector<int64_t>& prow, std::vector<int64_t>& pupd,
-                  std::vector<float>& pdata) {
-    prow.push_back(l->key);
-    pupd.push_back(l->updates);
-    pdata.insert(pdata.end(), l->grad.begin(), l->grad.end());
+  void stage_push(Line* l) {
+    prow_.push_back(l->key);
+    pupd_.push_back(l->updates);
+    pdata_.insert(pdata_.end(), l->grad, l->grad + width_);
     l->ver += l->updates;
     l->updates = 0;
-    std::fill(l->grad.begin(), l->grad.end(), 0.f);
+    memset(l->grad, 0, width_ * sizeof(float));
   }
-  void flush(std::vector<int64_t>& prow, std::vector<int64_t>& pupd, std::vector<float>& pdata) {
-    if (prow.empty()) return;
+  void flush_pending() {
+    if (prow_.empty()) return;
     auto t0 = std::chrono::steady_clock::now();
-    hps_push_embedding(key_, prow.data(), (int64_t)prow.size(), pdata.data(), pupd.data());
-    perf_rec_.pushed += (int64_t)prow.size();
+    hps_push_embedding(key_, prow_.data(), (int64_t)prow_.size(), pdata_.data(), pupd_.data());
+    perf_rec_.pushed += (int64_t)prow_.size();
     perf_rec_.t_push += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    prow.clear();
-    pupd.clear();
-    pdata.clear();
+    prow_.clear();
+    pupd_.clear();
+    pdata_.clear();
   }
 
   int64_t limit_, rows_, width_;
@@ -310,8 +638,17 @@ class Cache {
   int64_t pull_bound_, push_bound_;
   int policy_;
   bool bypass_ = false, perf_ = false;
+  LinePool pool_;
   std::unique_ptr<Policy> pol_;
-  std::unordered_map<int64_t, LineP> live_;
+  KeyMap map_;
+  std::vector<Line*> evicted_;
+  // per-call scratch, kept to avoid reallocation
+  std::vector<int64_t> uniq_, vers_, idx_, nver_, ukeys_, prow_, pupd_;
+  std::vector<int32_t> pos_;
+  std::vector<int64_t> slot_, start_, fill_, order_;
+  Dedup dedup_;
+  std::vector<Line*> lines_, ulines_;
+  std::vector<float> sync_data_, acc_, pdata_;
   std::mutex mu_;
   Perf perf_rec_;
 };

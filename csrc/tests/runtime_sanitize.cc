@@ -124,6 +124,21 @@ static void worker_main(const char* name) {
   }
   for (auto& x : th) x.join();
   CHECK(hc_flush(h) == 0);
+  // large batches (> the cache's parallel-loop threshold): the row copy and the
+  // gradient application run on the cache's worker threads, with evictions
+  int h2 = hc_create(1, 300, 1000, 8, 3, 3, 3);
+  CHECK(h2 >= 0);
+  {
+    std::mt19937 rng(91 + r);
+    std::vector<int64_t> k(2048);
+    std::vector<float> d(2048 * 8), gr(2048 * 8, 0.01f);
+    for (int it = 0; it < 20; ++it) {
+      for (auto& x : k) x = rng() % 1000;
+      CHECK(hc_lookup(h2, k.data(), 2048, d.data()) == 0);
+      CHECK(hc_update(h2, k.data(), 2048, gr.data()) == 0);
+    }
+    CHECK(hc_flush(h2) == 0);
+  }
   hps_barrier_worker();
   CHECK(hps_finalize() == 0);
 }

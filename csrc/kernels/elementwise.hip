@@ -101,7 +101,8 @@ template <typename T, int OP>
 __global__ void __launch_bounds__(256) unary_k(const T* __restrict__ x, T* __restrict__ y, int64_t n,
                                                 float c, float c2) {
   constexpr int V = Vec<T>::N;
-  const int64_t nv = n / V;
+  // 16-byte vectors only on 16-byte aligned bases (offset views go scalar)
+  const int64_t nv = (((uintptr_t)x | (uintptr_t)y) % 16 == 0) ? n / V : 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
     float v[V];
@@ -122,8 +123,12 @@ __global__ void __launch_bounds__(256) binary_k(const T* __restrict__ a, const T
                                                  int64_t inner, float c) {
   constexpr int V = Vec<T>::N;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const bool vec_ok = (b_mode == 0 && sizeof(T) == sizeof(TB)) || (b_mode == 1 && inner % V == 0) ||
-                      b_mode == 2;
+  // 16-byte vector path only on 16-byte aligned bases (views with an element offset
+  // take the scalar path)
+  const uintptr_t al = (uintptr_t)a | (uintptr_t)y | (b_mode == 0 ? (uintptr_t)b : (uintptr_t)0);
+  const bool vec_ok = (al % 16 == 0) &&
+                      ((b_mode == 0 && sizeof(T) == sizeof(TB)) || (b_mode == 1 && inner % V == 0) ||
+                       b_mode == 2);
   if (vec_ok) {
     const int64_t nv = n / V;
     const float bs = b_mode == 2 ? to_f(b[0]) : 0.f;

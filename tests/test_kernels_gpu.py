@@ -210,3 +210,19 @@ def test_csr_spmm_spmv(dt):
                                dense[:, 50:120] @ bw.float(), **tol)
     x = torch.randn(200, device=DEV).to(dt)
     torch.testing.assert_close(KSPM.csrmv(a, x).float(), dense @ x.float(), **tol)
+
+
+def test_elementwise_offset_views_take_the_scalar_path():
+    """Contiguous views at an element offset (not 16-byte aligned) through the
+    unary / binary kernels (vector path needs aligned bases)."""
+    from hetu_61a7_amd.kernels import elementwise as E
+    for dt in (torch.float32, torch.bfloat16):
+        base = torch.randn(1 + 4 * 1000, device='cuda').to(dt)
+        x = base[1:]                      # 2- or 4-byte aligned only
+        assert x.data_ptr() % 16 != 0
+        y = E.unary('relu', x)
+        assert torch.equal(y.float(), torch.relu(x.float()).to(dt).float())
+        b = torch.randn(4, device='cuda').to(dt)
+        z = E.binary('add', x.view(1000, 4), b)
+        ref = (x.float().view(1000, 4) + b.float()).to(dt).float()
+        assert torch.allclose(z.float(), ref, atol=1e-2)

@@ -7,6 +7,7 @@
 // the reference.  Sparse updates run on de-duplicated rows (unique ids), so
 // every row is owned by exactly one wave: no atomics, deterministic.
 #include "common.h"
+#include <algorithm>
 
 namespace hetu {
 
@@ -49,8 +50,29 @@ __global__ void __launch_bounds__(256) scatter_add_rows_k(float* __restrict__ ds
   }
 }
 
-// segment sum by inverse map: out[inv[r], :] += src[r, :] into fp32 out (dedup)
-// identical to scatter_add but kept separate for clarity of intent.
+// Deterministic scatter-add (Executor(deterministic=True)): the
+// rows are pre-sorted by destination (stable), segment s = rows perm[off[s]..off[s+1])
+// all go to dst row seg_row[s]; one wave owns a segment and sums its rows in order,
+// so every destination row is written once, by one wave: bitwise reproducible.
+template <typename T>
+__global__ void __launch_bounds__(256) segment_sum_rows_k(float* __restrict__ dst,
+                                                           const int64_t* __restrict__ seg_row,
+                                                           const int64_t* __restrict__ off,
+                                                           const int64_t* __restrict__ perm,
+                                                           const T* __restrict__ src, int64_t nseg,
+                                                           int64_t dim, int64_t nrows) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t sg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); sg < nseg; sg += (int64_t)gridDim.x * 4) {
+    const int64_t id = seg_row[sg];
+    if (id < 0 || id >= nrows) continue;
+    const int64_t q0 = off[sg], q1 = off[sg + 1];
+    for (int64_t j = lane; j < dim; j += 64) {
+      float acc = dst[id * dim + j];
+      for (int64_t q = q0; q < q1; ++q) acc += to_f(src[perm[q] * dim + j]);
+      dst[id * dim + j] = acc;
+    }
+  }
+}
 
 enum { SP_SGD = 0, SP_MOMENTUM = 1, SP_NESTEROV = 2, SP_ADAGRAD = 3, SP_ADAM = 4, SP_ADAMW = 5 };
 
@@ -122,6 +144,21 @@ HETU_API int hetu_scatter_add_rows(float* dst, const int64_t* ids, const void* s
   if (n <= 0) return 0;
   if (src_bf16) hipLaunchKernelGGL(scatter_add_rows_k<bf16>, dim3(rows_blocks(n)), dim3(256), 0, st, dst, ids, (const bf16*)src, n, dim, nrows);
   else hipLaunchKernelGGL(scatter_add_rows_k<float>, dim3(rows_blocks(n)), dim3(256), 0, st, dst, ids, (const float*)src, n, dim, nrows);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+HETU_API int hetu_segment_sum_rows(float* dst, const int64_t* seg_row, const int64_t* off,
+                                   const int64_t* perm, const void* src, int64_t nseg, int64_t dim,
+                                   int64_t nrows, int src_bf16, hipStream_t st) {
+  if (nseg <= 0) return 0;
+  int grid = (int)std::min<int64_t>((nseg + 3) / 4, 65535);
+  if (src_bf16)
+    hipLaunchKernelGGL(segment_sum_rows_k<bf16>, dim3(grid), dim3(256), 0, st, dst, seg_row, off, perm,
+                       (const bf16*)src, nseg, dim, nrows);
+  else
+    hipLaunchKernelGGL(segment_sum_rows_k<float>, dim3(grid), dim3(256), 0, st, dst, seg_row, off, perm,
+                       (const float*)src, nseg, dim, nrows);
   HETU_LAUNCH_CHECK();
   return 0;
 }

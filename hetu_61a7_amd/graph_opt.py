@@ -64,7 +64,8 @@ def fuse_forward(roots):
     # opt-in: measured neutral on ResNet-50 bs256 (8082-8091 img/s with, 8106-8145
     # without, same box): the per-column atomics and the zero-fill cost about what
     # the skipped statistics pass saved (profiles/bn_stats_fusion_r2p.md)
-    if os.environ.get('HETU_FUSE_BN_STATS', '0') != '1':
+    from .kernels import deterministic
+    if os.environ.get('HETU_FUSE_BN_STATS', '0') != '1' or deterministic():   # fp32 atomics
         return fused
     from .ops.nn import Conv2dOp
     topo, cons = _consumers(roots)

@@ -26,6 +26,23 @@ F32 = ctypes.c_float
 
 _NATIVE_DISABLED = os.environ.get('HETU_NATIVE', '1') == '0'
 _cache = {}
+_DETERMINISTIC = [os.environ.get('HETU_DETERMINISTIC', '0') == '1']
+
+
+def deterministic() -> bool:
+    """Bitwise-reproducible mode (``Executor(deterministic=True)`` or
+    ``HETU_DETERMINISTIC=1``): scatter-adds become sorted segment sums, LAMB norms
+    ordered reductions, every per-shape kernel choice is fixed (no timing-based
+    autotune, whose winner may differ between runs and with it the rounding), and
+    the library paths run their deterministic algorithms."""
+    return _DETERMINISTIC[0]
+
+
+def set_deterministic(on: bool = True):
+    _DETERMINISTIC[0] = bool(on)
+    torch.use_deterministic_algorithms(bool(on), warn_only=True)
+    torch.backends.cudnn.deterministic = bool(on)
+    torch.backends.cudnn.benchmark = not on
 
 
 def fn(name, argtypes, restype=ctypes.c_int):

@@ -17,7 +17,10 @@ def optimizer_flat(mode, p, g, s1=None, s2=None, shadow=None, lr=0.01, l2=0.0, m
     (bf16, same numel) receives the updated weights for mixed precision.
     """
     m = MODES[mode]
-    if native(p):
+    from . import deterministic
+    # deterministic LAMB: the per-tensor norms as ordered torch reductions below
+    # instead of the fused kernel's cross-block atomics
+    if native(p) and not (mode == 'lamb' and deterministic()):
         f = fn('hetu_optimizer_flat', [I32, P, P, P, P, P, I64, F32, F32, F32, F32, F32, F32, F32,
                                        F32, F32, F32, P, I32, P, P, P])
         nseg = (seg_off.numel() - 1) if seg_off is not None else 0

@@ -25,10 +25,24 @@ def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
 
 
 def scatter_add_rows(dst: torch.Tensor, ids: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
-    """dst[ids[r], :] += src[r, :] (fp32 dst)."""
+    """dst[ids[r], :] += src[r, :] (fp32 dst).  Deterministic mode: rows sorted by
+    destination (stable) and summed per destination in order by one wave."""
     dim = dst.shape[-1]
     idx = ids.reshape(-1).long()
     src2 = src.reshape(-1, dim)
+    from . import deterministic
+    if native(dst) and dst.dtype == torch.float32 and supported_float(src2) and dst.is_contiguous() \
+            and deterministic():
+        idx = idx.contiguous()
+        src2 = src2.contiguous()
+        sidx, perm = torch.sort(idx, stable=True)
+        seg_row, counts = torch.unique_consecutive(sidx, return_counts=True)
+        off = torch.zeros(seg_row.numel() + 1, dtype=torch.int64, device=idx.device)
+        torch.cumsum(counts, 0, out=off[1:])
+        f = fn('hetu_segment_sum_rows', [P, P, P, P, P, I64, I64, I64, I32, P])
+        check(f(dst.data_ptr(), seg_row.data_ptr(), off.data_ptr(), perm.data_ptr(), src2.data_ptr(),
+                seg_row.numel(), dim, dst.shape[0], is_bf16(src2), stream_ptr()), 'segment_sum_rows')
+        return dst
     if native(dst) and dst.dtype == torch.float32 and supported_float(src2) and dst.is_contiguous():
         idx = idx.contiguous()
         src2 = src2.contiguous()

@@ -136,8 +136,12 @@ class HetuConfig(object):
                  cstable_policy=None, bsp=-1, prefetch=True, enable_lazy=False, cache_bound=100,
                  log_path=None, pipeline=None, dist_strategy=None, use_preduce=False, overlap=True,
                  use_nccl_collectives=True, mixed_precision=None, bucket_mb=32, use_hipgraph=False,
-                 timing=None, zero=0, **kwargs):
+                 timing=None, zero=0, deterministic=None, **kwargs):
         self.eval_node_list = eval_node_list
+        if deterministic is not None:
+            # bitwise-reproducible kernels (kernels.deterministic); process-wide
+            from ..kernels import set_deterministic
+            set_deterministic(deterministic)
         self.seed = seed if seed is not None else int(os.environ.get('HETU_SEED', 0) or 0) or int(time.time())
         if seed is None and os.environ.get('HETU_SEED') is None:
             # identical seeds on every data-parallel rank keep parameters identical

@@ -159,3 +159,16 @@ def test_timer_log_and_chrome_trace(tmp_path):
     assert any(e['cat'] == 'MatMulOp' for e in tr)
     by_type = ex.logOut(log_level='type')
     assert 'MatMulOp' in by_type or any('MatMul' in k for k in by_type)
+
+
+def test_deterministic_flag_toggles_fixed_kernel_choice():
+    from hetu_61a7_amd import kernels as K
+    from hetu_61a7_amd.kernels import autotune
+    import torch
+    K.set_deterministic(True)
+    try:
+        assert K.deterministic() and torch.are_deterministic_algorithms_enabled()
+        assert autotune.choose(('det-test',), {'hip': lambda: 1, 'vendor': lambda: 2}) == 'hip'
+    finally:
+        K.set_deterministic(False)
+    assert not K.deterministic() and not torch.are_deterministic_algorithms_enabled()

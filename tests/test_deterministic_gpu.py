@@ -36,9 +36,11 @@ def _train(det):
     dense = rng.randn(64, 16).astype(np.float32)
     lab = np.eye(4, dtype=np.float32)[rng.randint(0, 4, 64)]
     xi, xd, y_ = ht.Variable(name='ids'), ht.Variable(name='dense'), ht.Variable(name='y_')
-    E = ht.init.random_normal([300, 32], stddev=0.1, name='E')
-    W = ht.init.random_normal([6 * 32 + 16, 64], stddev=0.1, name='W')
-    W2 = ht.init.random_normal([64, 4], stddev=0.1, name='W2')
+    # explicit initial values: random initializers seed by node id, which differs
+    # between two graphs built in one process
+    E = ht.Variable(name='E', value=(rng.randn(300, 32) * 0.1).astype(np.float32))
+    W = ht.Variable(name='W', value=(rng.randn(6 * 32 + 16, 64) * 0.1).astype(np.float32))
+    W2 = ht.Variable(name='W2', value=(rng.randn(64, 4) * 0.1).astype(np.float32))
     h = ht.concat_op(ht.array_reshape_op(ht.embedding_lookup_op(E, xi), (-1, 6 * 32)), xd, axis=1)
     h = ht.relu_op(ht.matmul_op(h, W))
     loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(h, W2), y_), [0])

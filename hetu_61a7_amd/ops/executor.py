@@ -154,7 +154,7 @@ class HetuConfig(object):
         self.mixed_precision = mixed_precision in ('bf16', 'bfloat16', True)
         self.bucket_mb = bucket_mb
         self.zero = int(zero)   # 1: ZeRO-1 sharded optimizer state (optimizer.py _make_zero_buckets)
-        self.use_hipgraph = use_hipgraph
+        self.use_hipgraph = use_hipgraph or os.environ.get('HETU_HIPGRAPH', '0') == '1'
         self.timing = timing
         self.h2d_ops, self.d2h_ops = {}, {}
         self.placeholder_to_arr_map: Dict[Op, torch.Tensor] = {}

@@ -38,3 +38,26 @@ def test_example_runs(cmd):
     r = subprocess.run([sys.executable] + cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, PYTHONPATH=ROOT))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+def test_parallel_equivalence_examples(tmp_path):
+    """examples/runner/parallel: pipeline (GPipe, 1F1B), data+pipeline and the three
+    model-parallel splits reproduce the single-process losses (validate_results)."""
+    import subprocess
+    d = os.path.join(ROOT, 'examples', 'runner', 'parallel')
+    out = str(tmp_path / 'results')
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    heturun = [sys.executable, os.path.join(ROOT, 'bin', 'heturun')]
+    script = os.path.join(d, 'mlp_parallel.py')
+    runs = [[sys.executable, script, '--mode', 'base', '--cpu'],
+            heturun + ['-w', '2', sys.executable, script, '--mode', 'pp', '--schedule', 'gpipe'],
+            heturun + ['-w', '3', sys.executable, script, '--mode', 'pp', '--schedule', 'pipedream'],
+            heturun + ['-w', '4', sys.executable, script, '--mode', 'dp_pp', '--replicas', '2'],
+            heturun + ['-w', '2', sys.executable, script, '--mode', 'mp', '--split', 'right']]
+    for cmd in runs:
+        r = subprocess.run(cmd + ['--out', out, '--steps', '3'], env=env, cwd=ROOT, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    r = subprocess.run([sys.executable, os.path.join(d, 'validate_results.py'), out], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.count(' ok') == 4, r.stdout

@@ -251,13 +251,15 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
 
 // ---------------------------------------------------------------------------
 // backward
+// RELU == 2: the ReLU mask is recomputed from x and the forward affine
+// a = scale*invstd, b = bias - mean*a (folded per thread, no separate fold launch)
 template <typename T, int RELU>
 __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ y,
                                                        const T* __restrict__ x,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
-                                                       const float* __restrict__ fa,
-                                                       const float* __restrict__ fb, int64_t M,
+                                                       const float* __restrict__ fscale,
+                                                       const float* __restrict__ fbias, int64_t M,
                                                        int C, int W, int RP, int64_t rows_per_chunk,
                                                        float* __restrict__ ws_sdy,
                                                        float* __restrict__ ws_sdyx) {
@@ -278,7 +280,7 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
 #pragma unroll
     for (int i = 0; i < V; ++i) {
       mu[i] = mean[vc * V + i]; is[i] = invstd[vc * V + i];
-      if (RELU == 2) { ka[i] = fa[vc * V + i]; kb[i] = fb[vc * V + i]; }
+      if (RELU == 2) { ka[i] = fscale[vc * V + i] * is[i]; kb[i] = fbias[vc * V + i] - mu[i] * ka[i]; }
     }
     // two rows in flight per iteration (all loads issued before any use)
     int64_t r = r0 + rsub;
@@ -389,8 +391,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
                                                      const float* __restrict__ cA,
                                                      const float* __restrict__ cB,
                                                      const float* __restrict__ cC,
-                                                     const float* __restrict__ fa,
-                                                     const float* __restrict__ fb,
+                                                     const float* __restrict__ fscale,
+                                                     const float* __restrict__ fbias,
+                                                     const float* __restrict__ fmean,
+                                                     const float* __restrict__ finvstd,
                                                      T* __restrict__ dx, T* __restrict__ dres,
                                                      int64_t nvec, int C) {
   // channel-stationary threads (see bn_apply): per-channel coefficients live in
@@ -406,7 +410,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     A[k] = cA[c0 + k]; Bc[k] = cB[c0 + k]; Cc[k] = cC[c0 + k];
-    if (RELU == 2) { ka[k] = fa[c0 + k]; kb[k] = fb[c0 + k]; }
+    if (RELU == 2) {
+      ka[k] = fscale[c0 + k] * finvstd[c0 + k];
+      kb[k] = fbias[c0 + k] - fmean[c0 + k] * ka[k];
+    }
   }
   int64_t i = tid;
   for (; i + stride < nvec; i += 2 * stride) {   // two vectors in flight
@@ -555,12 +562,12 @@ HETU_API int hetu_col_sums(const void* x, int64_t M, int C, int is_bf16, float* 
 template <typename T, int RELU>
 static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const T* x, T* dx, T* dres,
                           int64_t M, int C, const float* mean, const float* invstd,
-                          const float* fa, const float* fb, float* w1, float* w2, float* cA,
+                          const float* bias, float* w1, float* w2, float* cA,
                           float* cB, float* cC, const float* scale, float* dscale, float* dbias,
                           hipStream_t st) {
   constexpr int V = Vec<T>::N;
   hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, x,
-                     mean, invstd, fa, fb, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
+                     mean, invstd, scale, bias, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 3) / 4), dim3(256), 0, st, w1, w2, g.chunks, M,
                      C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
   int64_t nvec = M * C / V;
@@ -570,19 +577,11 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const T* x, 
     if (grid < need) grid = need;
   }
   if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, fa, fb, dx, dres, nvec, C);
+    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, scale,
+                       bias, mean, invstd, dx, dres, nvec, C);
   else
-    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, fa, fb, dx, dres, nvec, C);
-}
-
-__global__ void bn_fold_k(const float* __restrict__ scale, const float* __restrict__ bias,
-                          const float* __restrict__ mean, const float* __restrict__ invstd, int C,
-                          float* __restrict__ fa, float* __restrict__ fb) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = scale[c] * invstd[c];
-  fa[c] = a;
-  fb[c] = bias[c] - mean[c] * a;
+    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, scale,
+                       bias, mean, invstd, dx, dres, nvec, C);
 }
 
 template <typename T>
@@ -598,18 +597,14 @@ static int bn_bwd_impl(const void* dy, const void* y, const void* x, void* dx, v
   float* cA = ws + 2 * (int64_t)g.chunks * C;
   float* cB = cA + C;
   float* cC = cB + C;
-  float* fa = cC + C;
-  float* fb = fa + C;
   const T *dyr = (const T*)dy, *yr = (const T*)y, *xr = (const T*)x;
   T *dxr = (T*)dx, *drr = (T*)dres;
   // mask source: the saved output y when a residual was added (mask depends on it),
-  // otherwise recomputed from x (one less stream to read)
+  // otherwise recomputed from x and the folded forward affine (one less stream)
   int mode = !relu ? 0 : ((dres || !bias) ? 1 : 2);
-  if (mode == 2)
-    hipLaunchKernelGGL(bn_fold_k, dim3((C + 255) / 256), dim3(256), 0, st, scale, bias, mean, invstd, C, fa, fb);
-  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, fa, fb, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
-  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, fa, fb, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
-  else bn_bwd_launch<T, 2>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, fa, fb, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  else bn_bwd_launch<T, 2>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
   HETU_LAUNCH_CHECK();
   return 0;
 }

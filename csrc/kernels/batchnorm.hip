@@ -20,13 +20,26 @@ struct BnGeom {
   int64_t rows_per_chunk;
 };
 
+// launch-shape tunables (hetu_bn_tune; scripts/bench_bn.py sweeps them): target
+// partial-statistics blocks per launch, and the block cap of the streaming kernels
+static int g_bn_chunk_target = 1024;
+static int g_bn_apply_blocks = 2048;
+
+static int bn_apply_grid(int64_t nvec, int C, int V) {
+  int64_t b = (nvec + 1023) / 1024;
+  if (b > g_bn_apply_blocks) b = g_bn_apply_blocks;
+  if (b < 1) b = 1;
+  const int need = (int)((C / V + 255) / 256);   // channel-stationary kernels need >= C/V threads
+  return b < need ? need : (int)b;
+}
+
 static BnGeom bn_geom(int64_t M, int C, int vec) {
   BnGeom g;
   int cv = C / vec;
   g.W = cv < 64 ? cv : 64;
   g.RP = 256 / g.W;
   g.tiles = (cv + g.W - 1) / g.W;
-  int want = (int)((1024 + g.tiles - 1) / g.tiles);
+  int want = (int)((g_bn_chunk_target + g.tiles - 1) / g.tiles);
   int64_t max_chunks = (M + g.RP - 1) / g.RP;
   if (want > max_chunks) want = (int)max_chunks;
   if (want < 1) want = 1;
@@ -199,11 +212,22 @@ __global__ void bn_infer_fold(const float* __restrict__ run_mean, const float* _
   fold_b[c] = bias[c] - run_mean[c] * a;
 }
 
-template <typename T, bool RELU, bool RES>
+// ReLU keep-bit of each lane of a vector, packed into one byte (bit k = lane k)
+template <int V>
+__device__ __forceinline__ uint8_t relu_bits(const float (&o)[V]) {
+  unsigned m = 0;
+#pragma unroll
+  for (int k = 0; k < V; ++k) m |= (o[k] > 0.f ? 1u : 0u) << k;
+  return (uint8_t)m;
+}
+
+// MASK: also store the ReLU keep-bits (1 byte per 16-byte vector, 1/16 of y) so the
+// backward of a fused add+ReLU reads them instead of re-reading y
+template <typename T, bool RELU, bool RES, bool MASK = false>
 __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T* __restrict__ res,
                                                  const float* __restrict__ fa,
                                                  const float* __restrict__ fb, T* __restrict__ y,
-                                                 int64_t nvec, int C) {
+                                                 int64_t nvec, int C, uint8_t* __restrict__ mask) {
   // channel-stationary threads: the grid stride is a multiple of C/V, so every
   // thread keeps one channel group's folded affine in registers (no per-element
   // parameter loads, no 64-bit modulo) and streams 2 vectors per iteration
@@ -233,6 +257,7 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
     }
     store_vec<T>(y + i * V, v);
     store_vec<T>(y + (i + stride) * V, w);
+    if (MASK) { mask[i] = relu_bits<V>(v); mask[i + stride] = relu_bits<V>(w); }
   }
   if (i < nvec) {
     float v[V], r[V];
@@ -246,6 +271,7 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
       v[k] = o;
     }
     store_vec<T>(y + i * V, v);
+    if (MASK) mask[i] = relu_bits<V>(v);
   }
 }
 
@@ -253,8 +279,10 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
 // backward
 // RELU == 2: the ReLU mask is recomputed from x and the forward affine
 // a = scale*invstd, b = bias - mean*a (folded per thread, no separate fold launch)
+// RELU == 3: the ReLU mask is the forward's keep-bit byte per vector (``mask``)
 template <typename T, int RELU>
 __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ y,
+                                                       const uint8_t* __restrict__ mask,
                                                        const T* __restrict__ x,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
@@ -305,6 +333,13 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
           g[i] = (xv[i] * ka[i] + kb[i]) > 0.f ? g[i] : 0.f;
           g2[i] = (xv2[i] * ka[i] + kb[i]) > 0.f ? g2[i] : 0.f;
         }
+      } else if (RELU == 3) {
+        const unsigned m1 = mask[off / V], m2 = mask[off2 / V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          g[i] = (m1 >> i) & 1u ? g[i] : 0.f;
+          g2[i] = (m2 >> i) & 1u ? g2[i] : 0.f;
+        }
       }
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -325,6 +360,10 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
       } else if (RELU == 2) {
 #pragma unroll
         for (int i = 0; i < V; ++i) g[i] = (xv[i] * ka[i] + kb[i]) > 0.f ? g[i] : 0.f;
+      } else if (RELU == 3) {
+        const unsigned m1 = mask[off / V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) g[i] = (m1 >> i) & 1u ? g[i] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -387,6 +426,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize(const float* __restrict__
 
 template <typename T, int RELU, bool DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ y,
+                                                     const uint8_t* __restrict__ mask,
                                                      const T* __restrict__ x,
                                                      const float* __restrict__ cA,
                                                      const float* __restrict__ cB,
@@ -437,6 +477,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
         g[k] = (xv[k] * ka[k] + kb[k]) > 0.f ? g[k] : 0.f;
         g2[k] = (xv2[k] * ka[k] + kb[k]) > 0.f ? g2[k] : 0.f;
       }
+    } else if (RELU == 3) {
+      const unsigned m1 = mask[i], m2 = mask[j];
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        g[k] = (m1 >> k) & 1u ? g[k] : 0.f;
+        g2[k] = (m2 >> k) & 1u ? g2[k] : 0.f;
+      }
     }
     if (DRES) {
       store_vec<T>(dres + i * V, g);
@@ -463,6 +510,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
     } else if (RELU == 2) {
 #pragma unroll
       for (int k = 0; k < V; ++k) g[k] = (xv[k] * ka[k] + kb[k]) > 0.f ? g[k] : 0.f;
+    } else if (RELU == 3) {
+      const unsigned m1 = mask[i];
+#pragma unroll
+      for (int k = 0; k < V; ++k) g[k] = (m1 >> k) & 1u ? g[k] : 0.f;
     }
     if (DRES) store_vec<T>(dres + i * V, g);
     float o[V];
@@ -476,6 +527,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
 
 using namespace hetu;
 
+HETU_API void hetu_bn_tune(int chunk_target, int apply_blocks) {
+  if (chunk_target > 0) g_bn_chunk_target = chunk_target;
+  if (apply_blocks > 0) g_bn_apply_blocks = apply_blocks;
+}
+
 // workspace floats needed: 2 * chunks * C + 5 * C  (partials + fold/bwd coefficients)
 HETU_API int64_t hetu_bn_workspace_floats(int64_t M, int C, int is_bf16) {
   BnGeom g = bn_geom(M, C, is_bf16 ? 8 : 4);
@@ -486,7 +542,7 @@ template <typename T>
 static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                        const float* bias, float* run_mean, float* run_var, float factor, float eps,
                        float* save_mean, float* save_invstd, float* ws, int relu, int training,
-                       const float* sums, hipStream_t st) {
+                       const float* sums, uint8_t* mask, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
@@ -508,36 +564,37 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
                        scale, bias, C, eps, fa, fb);
   }
   int64_t nvec = M * C / V;
-  int grid = stream_grid(nvec, 256, 4);
-  {  // channel-stationary kernels need >= C/V threads
-    const int need = (int)((C / Vec<T>::N + 255) / 256);
-    if (grid < need) grid = need;
-  }
+  const int grid = bn_apply_grid(nvec, C, V);
   const T* xr = (const T*)x;
   const T* rr = (const T*)res;
   T* yr = (T*)y;
-  if (relu && res)
-    hipLaunchKernelGGL((bn_apply<T, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+  if (relu && res && mask)
+    hipLaunchKernelGGL((bn_apply<T, true, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+  else if (relu && res)
+    hipLaunchKernelGGL((bn_apply<T, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+  else if (relu && mask)
+    hipLaunchKernelGGL((bn_apply<T, true, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
   else if (relu)
-    hipLaunchKernelGGL((bn_apply<T, true, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+    hipLaunchKernelGGL((bn_apply<T, true, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
   else if (res)
-    hipLaunchKernelGGL((bn_apply<T, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+    hipLaunchKernelGGL((bn_apply<T, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
   else
-    hipLaunchKernelGGL((bn_apply<T, false, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C);
+    hipLaunchKernelGGL((bn_apply<T, false, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
   HETU_LAUNCH_CHECK();
   return 0;
 }
 
-// x,y,res: [M,C] channels-last; res may be null; run_* may be null (no update)
+// x,y,res: [M,C] channels-last; res may be null; run_* may be null (no update);
+// mask (relu only, may be null): [M*C/V] bytes of ReLU keep-bits (V = 8 bf16 / 4 fp32)
 HETU_API int hetu_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int is_bf16,
                          const float* scale, const float* bias, float* run_mean, float* run_var,
                          float factor, float eps, float* save_mean, float* save_invstd, float* ws,
-                         int relu, int training, const float* sums, hipStream_t st) {
+                         int relu, int training, const float* sums, uint8_t* mask, hipStream_t st) {
   if (is_bf16)
     return bn_fwd_impl<bf16>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
-                             save_mean, save_invstd, ws, relu, training, sums, st);
+                             save_mean, save_invstd, ws, relu, training, sums, mask, st);
   return bn_fwd_impl<float>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
-                            save_mean, save_invstd, ws, relu, training, sums, st);
+                            save_mean, save_invstd, ws, relu, training, sums, mask, st);
 }
 
 // sums[0..C) / sums[C..2C) = per-channel sum / sum of squares of x [M, C] (fp64 merge)
@@ -560,33 +617,29 @@ HETU_API int hetu_col_sums(const void* x, int64_t M, int C, int is_bf16, float* 
 }
 
 template <typename T, int RELU>
-static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const T* x, T* dx, T* dres,
+static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const uint8_t* mask, const T* x, T* dx, T* dres,
                           int64_t M, int C, const float* mean, const float* invstd,
                           const float* bias, float* w1, float* w2, float* cA,
                           float* cB, float* cC, const float* scale, float* dscale, float* dbias,
                           hipStream_t st) {
   constexpr int V = Vec<T>::N;
-  hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, x,
+  hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, mask, x,
                      mean, invstd, scale, bias, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 3) / 4), dim3(256), 0, st, w1, w2, g.chunks, M,
                      C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
   int64_t nvec = M * C / V;
-  int grid = stream_grid(nvec, 256, 4);
-  {  // channel-stationary kernels need >= C/V threads
-    const int need = (int)((C / Vec<T>::N + 255) / 256);
-    if (grid < need) grid = need;
-  }
+  const int grid = bn_apply_grid(nvec, C, V);
   if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, scale,
+    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB, cC, scale,
                        bias, mean, invstd, dx, dres, nvec, C);
   else
-    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false>), dim3(grid), dim3(256), 0, st, dy, y, x, cA, cB, cC, scale,
+    hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB, cC, scale,
                        bias, mean, invstd, dx, dres, nvec, C);
 }
 
 template <typename T>
-static int bn_bwd_impl(const void* dy, const void* y, const void* x, void* dx, void* dres, int64_t M,
-                       int C, const float* scale, const float* bias, const float* mean,
+static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
+                       int64_t M, int C, const float* scale, const float* bias, const float* mean,
                        const float* invstd, float* dscale, float* dbias, float* ws, int relu,
                        hipStream_t st) {
   constexpr int V = Vec<T>::N;
@@ -601,21 +654,23 @@ static int bn_bwd_impl(const void* dy, const void* y, const void* x, void* dx, v
   T *dxr = (T*)dx, *drr = (T*)dres;
   // mask source: the saved output y when a residual was added (mask depends on it),
   // otherwise recomputed from x and the folded forward affine (one less stream)
-  int mode = !relu ? 0 : ((dres || !bias) ? 1 : 2);
-  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
-  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
-  else bn_bwd_launch<T, 2>(g, dyr, yr, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  // (or, with the forward's keep-bit mask, from that: 1/16 of the bytes of y)
+  int mode = !relu ? 0 : (mask ? 3 : ((dres || !bias) ? 1 : 2));
+  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  else if (mode == 2) bn_bwd_launch<T, 2>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  else bn_bwd_launch<T, 3>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
   HETU_LAUNCH_CHECK();
   return 0;
 }
 
-// dy,y,x,dx,dres: [M,C]; y only read when relu; dres may be null
-// bias may be null (then the ReLU mask is read from y)
+// dy,y,x,dx,dres: [M,C]; y only read when relu (and no mask); dres may be null
+// bias may be null (then the ReLU mask is read from y); mask: hetu_bn_fwd's keep-bits
 HETU_API int hetu_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres,
                          int64_t M, int C, int is_bf16, const float* scale, const float* bias,
                          const float* mean, const float* invstd, float* dscale, float* dbias,
-                         float* ws, int relu, hipStream_t st) {
+                         float* ws, int relu, const uint8_t* mask, hipStream_t st) {
   if (is_bf16)
-    return bn_bwd_impl<bf16>(dy, y, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
-  return bn_bwd_impl<float>(dy, y, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
+    return bn_bwd_impl<bf16>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
+  return bn_bwd_impl<float>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
 }

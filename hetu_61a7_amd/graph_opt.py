@@ -94,6 +94,10 @@ def _become_bn(node, bn, relu, residual):
     node.fused_from = bn
 
 
+# gradient ops whose value is always a new tensor (never a view of an input)
+_FRESH_OUTPUT = ('BNGradSelectOp', 'Conv2d_Gradient_of_DataOp', 'SumOp')
+
+
 def fuse_backward(roots):
     """Fold gradient fan-in sums into the data-gradient GEMM epilogue."""
     if os.environ.get('HETU_FUSE', '1') == '0':
@@ -141,6 +145,12 @@ def fuse_backward(roots):
                 n.__class__ = Conv2d_Gradient_of_DataOp
                 n.__dict__.update({k: v for k, v in d.__dict__.items() if k not in ('id', 'name', 'inputs', 'bw_of')})
                 n.inputs = list(d.inputs) + [other]
+                # the accumulated gradient may be overwritten in place (the library
+                # GEMM then accumulates into it: beta = 1, C == D, no copy of it into
+                # a fresh output) when this join is its only consumer and its op
+                # always hands out a freshly allocated tensor
+                n.acc_inplace = other not in root_set and \
+                    (len(rest) > 1 or (len(cons.get(other, [])) == 1 and type(other).__name__ in _FRESH_OUTPUT))
                 n.op_type = 'Conv2d_Gradient_of_DataOp'
                 n.id, n.name = keep_id, keep_name
                 if bw is not None:

@@ -21,9 +21,11 @@ CL = torch.channels_last
 MODE = os.environ.get('HETU_CONV', 'auto')  # hip | vendor | auto (per-shape measured choice)
 
 
-def _pick(key, hip, vendor, blas=None):
+def _pick(key, hip, vendor, blas=None, tuned=None):
     """hip: hand-written implicit GEMM; vendor: MIOpen; blas: a 1x1 convolution
-    run as the plain library GEMM it is (hipBLASLt), where applicable."""
+    run as the plain library GEMM it is (hipBLASLt), where applicable.
+    ``tuned()`` runs once the choice is made, before the call that produces the
+    result (candidates that write in place time against scratch until then)."""
     if MODE == 'hip':
         r = hip()
         return r if r is not None else vendor()
@@ -34,6 +36,8 @@ def _pick(key, hip, vendor, blas=None):
     if blas is not None:
         cands.update(blas)
     c = choose(key, cands)
+    if tuned is not None:
+        tuned()
     if c not in ('hip', 'vendor'):
         r = cands[c]()
         if r is not None:
@@ -164,9 +168,10 @@ def conv2d(x, w, b, stride, padding):
     return y
 
 
-def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None):
+def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=False):
     """dx (+ acc when given: a gradient joined at the conv input, fused into the
-    epilogue on the HIP path)."""
+    epilogue on the HIP path).  ``acc_inplace``: acc is dead after this call and
+    may receive the result (the library GEMM accumulates into it, C == D)."""
     g, w = _match(g, w)
     if g.is_cuda:
         g = g.contiguous(memory_format=CL)
@@ -175,15 +180,30 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None):
             acc = acc.contiguous(memory_format=CL)
         from . import conv_igemm
         blas = None
+        tuned = None
         if _plain_1x1((g, w), w.shape, stride, padding) and (acc is None or acc.dtype == torch.bfloat16):
             n, ci, h, ww_ = x_shape
             co = w.shape[0]
+            key = ('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None)
+            inplace = acc is not None and acc_inplace and acc.is_contiguous(memory_format=CL)
+            from .autotune import _decisions
+            # while the shape is being timed, the in-place candidate accumulates into scratch
+            dst = [acc.clone(memory_format=CL) if inplace and key not in _decisions else acc]
 
             def blas_dgrad():
                 w2 = w.reshape(co, ci)
-                d = torch.mm(_rows(g), w2) if acc is None else torch.addmm(_rows(acc), _rows(g), w2)
+                if acc is None:
+                    d = torch.mm(_rows(g), w2)
+                elif inplace:     # hipBLASLt beta = 1 into the dead join operand: no copy of it
+                    _rows(dst[0]).addmm_(_rows(g), w2)
+                    return dst[0]
+                else:
+                    d = torch.addmm(_rows(acc), _rows(g), w2)
                 return d.view(n, h, ww_, ci).permute(0, 3, 1, 2)
             blas = {'blas': blas_dgrad}
+
+            def tuned():
+                dst[0] = acc
         elif _needs_pad(torch.empty(0, x_shape[1], 1, 1, dtype=g.dtype, device=g.device), w) and acc is None:
             n, ci, h, ww_ = x_shape
             cp = -(-ci // 8) * 8
@@ -197,7 +217,7 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None):
             blas['hip256'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=1)
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
                      lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
-                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas)
+                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas, tuned)
     return _vendor_dgrad(g, w, x_shape, stride, padding, acc)
 
 
@@ -209,9 +229,10 @@ def _vendor_dgrad(g, w, x_shape, stride, padding, acc=None):
 
 
 def _vendor_dgrad0(g, w, x_shape, stride, padding):
-    xs = torch.empty(x_shape, dtype=g.dtype, device=g.device)
-    if g.is_cuda:
-        xs = xs.contiguous(memory_format=CL)
+    # MIOpen only reads x's shape + layout: allocate it channels-last directly
+    # (``empty(...).contiguous(CL)`` was a full-size copy of garbage per call)
+    xs = torch.empty(x_shape, dtype=g.dtype, device=g.device,
+                     memory_format=CL if g.is_cuda else torch.contiguous_format)
     dx, _, _ = torch.ops.aten.convolution_backward(
         g, xs, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [True, False, False])
     return dx
@@ -284,9 +305,8 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
 
 
 def _vendor_wgrad(g, x, w_shape, stride, padding):
-    ws = torch.empty(w_shape, dtype=g.dtype, device=g.device)
-    if g.is_cuda:
-        ws = ws.contiguous(memory_format=CL)
+    ws = torch.empty(w_shape, dtype=g.dtype, device=g.device,
+                     memory_format=CL if g.is_cuda else torch.contiguous_format)
     _, dw, _ = torch.ops.aten.convolution_backward(
         g, x, ws, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [False, True, False])
     return dw

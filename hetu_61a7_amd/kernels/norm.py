@@ -47,12 +47,19 @@ def col_sums(x):
     return sums
 
 
+def relu_mask_bytes(x):
+    """Size of the ReLU keep-bit mask ``bn_forward(mask=...)`` writes: one byte per
+    16-byte vector of x (8 bf16 / 4 fp32 channels)."""
+    return x.numel() // (8 if x.dtype == torch.bfloat16 else 4)
+
+
 def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
-               relu=False, residual=None, sums=None):
+               relu=False, residual=None, sums=None, mask=None):
     """Returns (y, save_mean, save_invstd).  ``factor`` = weight of the new batch
     statistics in the running average.  ``sums`` ([2C] fp32 per-channel sum and sum
     of squares of x, e.g. from the convolution epilogue that produced x) skips the
-    statistics pass."""
+    statistics pass.  ``mask`` (uint8 [relu_mask_bytes(x)], ReLU only): receives the
+    ReLU keep-bits, which ``bn_backward(mask=...)`` reads instead of y."""
     C = x.shape[1]
     if native(x) and x.dtype in (torch.float32, torch.bfloat16):
         if x.dim() == 4 and not x.is_contiguous(memory_format=torch.channels_last):
@@ -68,14 +75,17 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
             save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
             save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
             ws = _ws(M, C, is_bf16(x), x.device)
-            f = fn('hetu_bn_fwd', [P, P, P, I64, I32, I32, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P])
+            if mask is not None:
+                assert relu and mask.dtype == torch.uint8 and mask.numel() == relu_mask_bytes(x) and mask.is_cuda
+            f = fn('hetu_bn_fwd', [P, P, P, I64, I32, I32, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P, P])
             check(f(x.data_ptr(), residual.data_ptr() if residual is not None else None, y.data_ptr(),
                     M, C, is_bf16(x), scale.data_ptr(), bias.data_ptr(),
                     running_mean.data_ptr() if running_mean is not None else None,
                     running_var.data_ptr() if running_var is not None else None,
                     float(factor), float(eps), save_mean.data_ptr(), save_invstd.data_ptr(),
                     ws.data_ptr(), int(relu), int(training),
-                    sums.data_ptr() if (sums is not None and training) else None, stream_ptr()), 'bn_fwd')
+                    sums.data_ptr() if (sums is not None and training) else None,
+                    mask.data_ptr() if mask is not None else None, stream_ptr()), 'bn_fwd')
             return y, save_mean, save_invstd
     # torch reference (CPU backend / unsupported layouts)
     xf = x.float()
@@ -104,15 +114,16 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
 
 
 def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=False, bias=None,
-                dscale_out=None, dbias_out=None):
-    """Returns (dx, dscale, dbias, dres)."""
+                dscale_out=None, dbias_out=None, mask=None):
+    """Returns (dx, dscale, dbias, dres).  ``mask``: the forward's ReLU keep-bits
+    (native path only; y is then not read)."""
     C = x.shape[1]
     if native(x) and x.dtype in (torch.float32, torch.bfloat16):
         cl = torch.channels_last
         if x.dim() == 4:
             x = x.contiguous(memory_format=cl)
             dy = dy.contiguous(memory_format=cl)
-            if relu:
+            if relu and mask is None:
                 y = y.contiguous(memory_format=cl)
         else:
             dy = dy.contiguous()
@@ -124,12 +135,15 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
             dscale = dscale_out if dscale_out is not None else torch.empty(C, dtype=torch.float32, device=x.device)
             dbias = dbias_out if dbias_out is not None else torch.empty(C, dtype=torch.float32, device=x.device)
             ws = _ws(M, C, is_bf16(x), x.device)
-            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P])
-            check(f(dy.data_ptr(), y.data_ptr() if relu else None, x.data_ptr(), dx.data_ptr(),
-                    dres.data_ptr() if dres is not None else None, M, C, is_bf16(x),
+            if mask is not None:
+                assert relu and mask.dtype == torch.uint8 and mask.numel() == relu_mask_bytes(x)
+            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P, P])
+            check(f(dy.data_ptr(), y.data_ptr() if (relu and mask is None) else None, x.data_ptr(),
+                    dx.data_ptr(), dres.data_ptr() if dres is not None else None, M, C, is_bf16(x),
                     scale.data_ptr(), bias.float().contiguous().data_ptr() if bias is not None else None,
                     save_mean.data_ptr(), save_invstd.data_ptr(),
-                    dscale.data_ptr(), dbias.data_ptr(), ws.data_ptr(), int(relu), stream_ptr()),
+                    dscale.data_ptr(), dbias.data_ptr(), ws.data_ptr(), int(relu),
+                    mask.data_ptr() if mask is not None else None, stream_ptr()),
                   'bn_bwd')
             return dx, dscale, dbias, dres
     dims = [0] + list(range(2, x.dim()))
@@ -142,7 +156,7 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
     dbias = g.sum(dims)
     dscale = (g * xhat).sum(dims)
     dx = (scale.float() * save_invstd).view(shape) * (g - dbias.view(shape) / M - xhat * dscale.view(shape) / M)
-    dres = g.to(x.dtype) if want_dres else None
+    dres = g.to(x.dtype, copy=True) if want_dres else None   # never an alias of dy
     dx = dx.to(x.dtype)
     if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
         dx = dx.contiguous(memory_format=torch.channels_last)

@@ -28,6 +28,7 @@ from ..kernels import norm as KN
 from ..kernels import pool as KP
 from ..kernels import conv as KC
 from ..kernels import layernorm as KLN
+from ..kernels import native
 from ..kernels import dropout as KD
 
 
@@ -85,7 +86,8 @@ class Conv2d_Gradient_of_DataOp(Op):
         # optional 4th input: a gradient to accumulate (fused fan-in sum, graph_opt)
         w, g, xshape = input_vals[:3]
         acc = input_vals[3] if len(input_vals) > 3 else None
-        return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc)
+        return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,
+                                       acc_inplace=getattr(self, 'acc_inplace', False))
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -288,12 +290,18 @@ class Batch_NormalizationOp(Op):
         self._init_running(x.shape[1], x.device)
         training = not (self.inference if inference is None else inference)
         sums = getattr(x, 'hetu_bn_sums', None) if training else None
+        # fused add+ReLU: the backward needs the ReLU mask, which then depends on the
+        # residual too; keep it as bits (1/16 of y's bytes) instead of re-reading y
+        mask = None
+        if training and self.relu and self.has_residual and x.is_cuda and native(x) and \
+                x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % (8 if x.dtype == torch.bfloat16 else 4) == 0:
+            mask = torch.empty(KN.relu_mask_bytes(x), dtype=torch.uint8, device=x.device)
         y, mean, invstd = KN.bn_forward(x, scale.float(), bias.float(), self.running_mean,
                                         self.running_var, self.momentum, self.eps, training,
-                                        relu=self.relu, residual=res, sums=sums)
+                                        relu=self.relu, residual=res, sums=sums, mask=mask)
         if not training:
             return y
-        return AuxResult(y, (mean, invstd))
+        return AuxResult(y, (mean, invstd) if mask is None else (mean, invstd, mask))
 
     def gradient(self, output_grad):
         g = Batch_Normalization_GradientOp(output_grad, self.inputs[0], self.inputs[1], self,
@@ -321,13 +329,15 @@ class Batch_Normalization_GradientOp(Op):
         self.eps = eps
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        g, x, scale, (y, (mean, invstd)) = input_vals[:4]
+        g, x, scale, (y, aux) = input_vals[:4]
+        mean, invstd = aux[:2]
+        mask = aux[2] if len(aux) > 2 else None
         bias = input_vals[4] if len(input_vals) > 4 else None
         fw = self.forward_node
         dests = getattr(self, 'grad_dests', {})
         dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
                                                  relu=fw.relu, want_dres=fw.has_residual, bias=bias,
-                                                 dscale_out=dests.get(1), dbias_out=dests.get(2))
+                                                 dscale_out=dests.get(1), dbias_out=dests.get(2), mask=mask)
         return (dx, dscale, dbias, dres)
 
     def gradient(self, output_grad):

@@ -40,6 +40,8 @@ def main():
     ap.add_argument('--last', type=int, default=3)
     ap.add_argument('--marker', default='opt_flat_k')
     ap.add_argument('--top', type=int, default=40)
+    ap.add_argument('--context', action='append', default=[],
+                    help='category substring: list each launch of it in the last step with its neighbours')
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
@@ -62,6 +64,15 @@ def main():
     print('%-52s %9s %7s %6s' % ('category', 'ms/step', 'calls', '%'))
     for c, t in sorted(cat.items(), key=lambda kv: -kv[1])[:a.top]:
         print('%-52s %9.3f %7.1f %6.1f' % (c, t / a.last, cnt[c] / a.last, 100 * t / busy))
+    last = rows[ends[-2] + 1:ends[-1] + 1]
+    for want in a.context:
+        print('\n# launches of %r in the last step (prev | this | next)' % want)
+        for i, r in enumerate(last):
+            if want in classify(r['Kernel_Name']):
+                dur = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
+                nb = lambda j: classify(last[j]['Kernel_Name']) if 0 <= j < len(last) else '-'
+                print('%4d  %-40s | %-30s %7.1f us | %s' % (i, nb(i - 1)[:40], classify(r['Kernel_Name'])[:30],
+                                                         dur, nb(i + 1)[:40]))
 
 
 if __name__ == '__main__':

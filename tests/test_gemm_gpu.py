@@ -127,3 +127,27 @@ def test_bn_from_fused_statistics_matches_plain_bn():
     assert _rel(b, a) < 1e-2
     s2 = KN.col_sums(y)
     assert _rel(s2, sums) < 1e-4
+
+
+def test_dgrad_join_accumulates_in_place():
+    """1x1 data gradient with a fused gradient join (acc): autotuning times the
+    in-place library candidate against scratch, and once chosen it accumulates
+    into acc itself (no copy of acc into a new output)."""
+    from hetu_61a7_amd.kernels import conv as KC, autotune
+    g = torch.randn(4, 64, 14, 14, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(64, 32, 1, 1, device=DEV) * 0.1).bfloat16().contiguous(memory_format=CL)
+    acc = torch.randn(4, 32, 14, 14, device=DEV).bfloat16().contiguous(memory_format=CL)
+    ref = torch.einsum('nkhw,kc->nchw', g.float(), w.float().view(64, 32)) + acc.float()
+    key = ('dgrad', tuple(g.shape), tuple(w.shape), (1, 1), (0, 0), True)
+    for forced in (None, 'blas'):
+        autotune._decisions.pop(key, None)
+        if forced:
+            autotune._decisions[key] = forced
+        a = acc.clone(memory_format=CL)
+        dx = KC.conv2d_backward_data(g, w, (4, 32, 14, 14), (1, 1), (0, 0), acc=a, acc_inplace=True)
+        assert _rel(dx, ref) < 1e-2
+        if forced == 'blas':
+            assert dx.data_ptr() == a.data_ptr() and dx.is_contiguous(memory_format=CL)
+        elif autotune._decisions[key] != 'blas':
+            assert torch.equal(a, acc)     # timing trials never touched the live operand
+    autotune._decisions.pop(key, None)

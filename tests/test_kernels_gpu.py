@@ -81,6 +81,31 @@ def test_batchnorm_nhwc(dt, relu, res, N, C, H, W):
 
 
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('res', [False, True])
+@pytest.mark.parametrize('N,C,H,W', [(8, 64, 14, 14), (2, 2048, 7, 7), (3, 24, 5, 7)])
+def test_batchnorm_relu_keep_bits(dt, res, N, C, H, W):
+    """The forward's packed ReLU keep-bits drive the backward exactly as re-reading y does."""
+    x = torch.randn(N, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(x) if res else None
+    scale, bias = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mask = torch.full((KN.relu_mask_bytes(x),), 0xAA, dtype=torch.uint8, device=DEV)
+    y, mean, invstd = KN.bn_forward(x, scale, bias, rm, rv, 0.1, 1e-5, True, relu=True, residual=r, mask=mask)
+    y0, _, _ = KN.bn_forward(x, scale, bias, rm.clone(), rv.clone(), 0.1, 1e-5, True, relu=True, residual=r)
+    assert torch.equal(y, y0)
+    V = 8 if dt == torch.bfloat16 else 4
+    keep = (y.permute(0, 2, 3, 1).reshape(-1, V) > 0).to(torch.int32)
+    bits = (keep << torch.arange(V, device=DEV, dtype=torch.int32)).sum(1)
+    assert torch.equal(bits.to(torch.uint8), mask)
+    dy = torch.randn_like(x)
+    a = KN.bn_backward(dy, y, x, scale, mean, invstd, relu=True, want_dres=res, bias=bias, mask=mask)
+    b = KN.bn_backward(dy, y, x, scale, mean, invstd, relu=True, want_dres=res, bias=None)   # mask from y
+    for u, v in zip(a, b):
+        if u is not None:
+            torch.testing.assert_close(u.float(), v.float(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
 def test_softmax_and_ce(dt):
     x = torch.randn(300, 1000, device=DEV).to(dt)
     lab = F.one_hot(torch.randint(0, 1000, (300,), device=DEV), 1000).float()

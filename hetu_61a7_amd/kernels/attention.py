@@ -12,6 +12,7 @@ semantics (the CPU backend and the numerics oracle).
 from __future__ import annotations
 
 import math
+import weakref
 
 import torch
 
@@ -43,6 +44,32 @@ def _ref_dropmask(shape, keep, seed, device):
     return (torch.rand(shape, generator=g, device=device) < keep).float() / keep
 
 
+_mask_memo = {}
+
+
+def _mask_f32(mask):
+    """fp32 contiguous copy of the attention mask, made once per mask tensor: every
+    layer's forward and backward of a step receives the same (bf16 in mixed
+    precision) mask (views of one tensor).  Keyed on that tensor, the view and the
+    version counter; never
+    memoised inside a hipGraph capture (a replay must re-read its fed buffer)."""
+    if mask is None:
+        return None
+    if mask.dtype == torch.float32 and mask.is_contiguous():
+        return mask
+    if mask.is_cuda and torch.cuda.is_current_stream_capturing():
+        return mask.float().contiguous()
+    root = mask._base if mask._base is not None else mask     # ops hand in fresh views of it
+    sig = (mask.data_ptr(), tuple(mask.shape), mask.stride(), mask._version)
+    ent = _mask_memo.get(id(root))
+    if ent is not None and ent[0]() is root and ent[1] == sig:
+        return ent[2]
+    m = mask.float().contiguous()
+    _mask_memo.clear()
+    _mask_memo[id(root)] = (weakref.ref(root), sig, m)
+    return m
+
+
 def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
     """-> (out [B*S, H], lse [B*NH*S] fp32 or probs (reference path))."""
     H = qkv.shape[1] // 3
@@ -51,7 +78,7 @@ def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
     if fused_ok(qkv, S, D, need_bwd=False):
         out = torch.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
-        m = mask.float().contiguous() if mask is not None else None
+        m = _mask_f32(mask)
         f = fn('hetu_attn_fwd', [P, P, P, I64, I64, I64, P, P, I64, P, I32, I32, I32, F32, F32, I64, P])
         base = qkv.data_ptr()
         es = qkv.element_size()
@@ -73,7 +100,7 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
     if fused_ok(qkv, S, D) and saved.dim() == 1:
         dout = dout.to(qkv.dtype).contiguous()
         dqkv = torch.empty_like(qkv)
-        m = mask.float().contiguous() if mask is not None else None
+        m = _mask_f32(mask)
         f = fn('hetu_attn_bwd', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
                                  I32, I32, I32, F32, F32, I64, P])
         es = qkv.element_size()
@@ -116,7 +143,7 @@ def attention_fwd_blocks(q, k, v, mask, B, S, NH, scale):
     H = q.shape[1]
     out = torch.empty((B * S, H), dtype=q.dtype, device=q.device)
     lse = torch.empty((B * NH * S,), dtype=torch.float32, device=q.device)
-    m = mask.float().contiguous() if mask is not None else None
+    m = _mask_f32(mask)
     f = fn('hetu_attn_fwd', [P, P, P, I64, I64, I64, P, P, I64, P, I32, I32, I32, F32, F32, I64, P])
     check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
             m.data_ptr() if m is not None else None, out.data_ptr(), H, lse.data_ptr(), B, NH, S,
@@ -136,7 +163,7 @@ def attention_bwd_blocks(dout, q, k, v, out, lse, mask, B, S, NH, scale):
     dq = torch.empty((B * S, H), dtype=q.dtype, device=q.device)
     dk = torch.empty_like(dq)
     dv = torch.empty_like(dq)
-    m = mask.float().contiguous() if mask is not None else None
+    m = _mask_f32(mask)
     f = fn('hetu_attn_bwd', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
                              I32, I32, I32, F32, F32, I64, P])
     check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),

@@ -73,10 +73,21 @@ def _big_ok(a, b, ta, tb):
     return A.dim() == 2 and B.dim() == 2 and A.shape[0] >= 256 and B.shape[1] >= 256
 
 
+def _as_dtype(t, dt):
+    """t in dtype dt; an fp32 master parameter carries its bf16 compute copy (the
+    optimizer's shadow, refreshed by the fused update) as ``hetu_bf16``."""
+    if t.dtype == dt:
+        return t
+    sh = getattr(t, 'hetu_bf16', None)
+    if sh is not None and sh.dtype == dt:
+        return sh
+    return t.to(dt)
+
+
 def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
     A, B = _tr(a, ta), _tr(b, tb)
     if fuse_bias and bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
-        y = torch.addmm(bias.to(A.dtype), A, B)     # bias in the hipBLASLt epilogue
+        y = torch.addmm(_as_dtype(bias, A.dtype), A, B)     # bias in the hipBLASLt epilogue
         bias = None
     else:
         y = torch.matmul(A, B)

@@ -33,19 +33,28 @@ def layer_norm(x, gamma, beta, eps):
     return y.reshape(x.shape).to(x.dtype), mean, rstd
 
 
-def layer_norm_backward(dy, x, gamma, mean, rstd):
+def _dest(out, N, dev):
+    """fp32 [N] result buffer: the caller's (e.g. the optimizer's flat gradient slot) or new"""
+    if out is not None and out.dtype == torch.float32 and out.is_contiguous() and out.numel() == N:
+        return out
+    return torch.empty(N, dtype=torch.float32, device=dev)
+
+
+def layer_norm_backward(dy, x, gamma, mean, rstd, dg_out=None, db_out=None):
+    """(dx, dgamma, dbeta); ``dg_out`` / ``db_out``: fp32 buffers that receive
+    dgamma / dbeta (the optimizer's flat gradient slots)."""
     N = x.shape[-1]
     R = x.numel() // N
     if _fused_ok(x) and dy.dtype == x.dtype:
-        ds, _, dg, db = layer_norm_fused_backward(dy, x, gamma, mean, rstd, need_dx=False)
+        ds, _, dg, db = layer_norm_fused_backward(dy, x, gamma, mean, rstd, need_dx=False,
+                                                  dg_out=dg_out, db_out=db_out)
         return ds, dg, db
     if native(x) and supported_float(x) and dy.dtype == x.dtype:
         xc, dyc = x.contiguous(), dy.contiguous()
         dx = torch.empty_like(xc)
         ws_rows = min(R, 1024)
         ws = torch.empty(2 * ws_rows * N, dtype=torch.float32, device=x.device)
-        dg = torch.empty(N, dtype=torch.float32, device=x.device)
-        db = torch.empty(N, dtype=torch.float32, device=x.device)
+        dg, db = _dest(dg_out, N, x.device), _dest(db_out, N, x.device)
         f = fn('hetu_layernorm_bwd', [P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, P])
         check(f(dyc.data_ptr(), xc.data_ptr(), gamma.float().contiguous().data_ptr(), mean.data_ptr(),
                 rstd.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), ws.data_ptr(), R, N,
@@ -95,7 +104,8 @@ def layer_norm_fused(x, residual, gamma, beta, eps, keep=1.0, seed=0):
     return y, s, mean, rstd
 
 
-def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_ds=True, need_dx=True):
+def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_ds=True, need_dx=True,
+                              dg_out=None, db_out=None):
     """Backward of ``layer_norm_fused``: (ds, dx, dgamma, dbeta) with ds the grad
     of the normalised input (= grad of the residual) and dx = dropout-mask(ds)
     the grad of ``x`` (None when not requested)."""
@@ -109,8 +119,7 @@ def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_d
             ds = torch.empty_like(sc)
         nblk = max(1, min(512, (R + 7) // 8))
         ws = torch.empty(2 * nblk * N, dtype=torch.float32, device=s.device)
-        dg = torch.empty(N, dtype=torch.float32, device=s.device)
-        db = torch.empty(N, dtype=torch.float32, device=s.device)
+        dg, db = _dest(dg_out, N, s.device), _dest(db_out, N, s.device)
         f = fn('hetu_ln_fused_bwd', [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, P])
         check(f(dyc.data_ptr(), sc.data_ptr(), gamma.float().contiguous().data_ptr(), mean.data_ptr(),
                 rstd.data_ptr(), ds.data_ptr() if ds is not None else None,

@@ -319,6 +319,7 @@ class Batch_NormalizationOp(Op):
 
 class Batch_Normalization_GradientOp(Op):
     """Computes (dx, dscale, dbias[, dresidual]) in one fused kernel pass."""
+    grad_dest_slots = (1, 2)
     aux_inputs = (3,)
     value_and_aux_inputs = (3,)
 
@@ -353,10 +354,10 @@ class BNGradSelectOp(Op):
         self.index = index
 
     def set_grad_dest(self, dest):
-        """dscale / dbias are written by the fused BN-backward kernel straight into
-        the optimizer's flat gradient buffer."""
+        """dscale / dbias (BN, LayerNorm) are written by the fused backward kernel
+        straight into the optimizer's flat gradient buffer."""
         src = self.inputs[0]
-        if self.index in (1, 2) and isinstance(src, Batch_Normalization_GradientOp) and \
+        if self.index in getattr(src, 'grad_dest_slots', ()) and \
                 dest.dtype == torch.float32 and dest.is_contiguous():
             if not hasattr(src, 'grad_dests'):
                 src.grad_dests = {}
@@ -435,6 +436,7 @@ class Layer_NormalizationOp(Op):
 
 class Layer_Normalization_GradientOp(Op):
     aux_inputs = (3,)
+    grad_dest_slots = (1, 2)
 
     def __init__(self, out_gradient, x, scale, forward_node, eps, ctx=None):
         super().__init__(Layer_Normalization_GradientOp, [out_gradient, x, scale, forward_node], ctx)
@@ -442,7 +444,8 @@ class Layer_Normalization_GradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         dy, x, g, (mean, rstd) = input_vals
-        return KLN.layer_norm_backward(dy, x, g, mean, rstd)
+        dests = getattr(self, 'grad_dests', {})
+        return KLN.layer_norm_backward(dy, x, g, mean, rstd, dg_out=dests.get(1), db_out=dests.get(2))
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -517,6 +520,7 @@ class DropoutAddLayerNormOp(Op):
 
 class DropoutAddLayerNormGradientOp(Op):
     aux_inputs = (1,)
+    grad_dest_slots = (2, 3)
 
     def __init__(self, out_gradient, forward_node, ctx=None):
         super().__init__(DropoutAddLayerNormGradientOp, [out_gradient, forward_node, forward_node.inputs[-2]], ctx)
@@ -525,7 +529,9 @@ class DropoutAddLayerNormGradientOp(Op):
         dy, (sm, mean, rstd, keep, seed), g = input_vals
         if dy.dtype != sm.dtype:
             dy = dy.to(sm.dtype)
-        ds, dx, dg, db = KLN.layer_norm_fused_backward(dy, sm, g, mean, rstd, keep, seed)
+        dests = getattr(self, 'grad_dests', {})
+        ds, dx, dg, db = KLN.layer_norm_fused_backward(dy, sm, g, mean, rstd, keep, seed,
+                                                       dg_out=dests.get(2), db_out=dests.get(3))
         return (dx, ds, dg, db)
 
     def gradient(self, output_grad):

@@ -346,6 +346,8 @@ class OptimizerOp(Op):
             # no per-step cast kernels)
             if amp and len(self.flat.offsets[p][2]) >= 2:
                 config.compute_values[p] = self.flat.view(p, 'shadow')
+            elif amp:   # library GEMM bias epilogues take bf16: hand them the shadow (no cast)
+                values[p].hetu_bf16 = self.flat.view(p, 'shadow')
         for p in sparse:
             st = {}
             t = values[p]

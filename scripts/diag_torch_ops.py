@@ -1,8 +1,8 @@
 """List the aten ops (i.e. everything NOT launched through our own HIP kernels)
-that one steady-state ResNet-50 training step issues, grouped by op + the
+that one steady-state training step (ResNet-50 / BERT / MoE bench) issues, grouped by op + the
 framework source line that called it.  Finds stray layout copies / casts.
 
-    python scripts/diag_torch_ops.py [batch]
+    python scripts/diag_torch_ops.py [batch|0] [resnet50|bert|moe]
 """
 import collections
 import os
@@ -16,7 +16,7 @@ from torch.utils._python_dispatch import TorchDispatchMode
 import hetu_61a7_amd as ht
 from hetu_61a7_amd.models import resnet50_imagenet
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 PKG = os.sep + 'hetu_61a7_amd' + os.sep
 SKIP = {'aten.empty.memory_format', 'aten.empty_strided.default', 'aten.view.default', 'aten.t.default',
         'aten.permute.default', 'aten.reshape.default', 'aten._unsafe_view.default', 'aten.as_strided.default',
@@ -57,20 +57,34 @@ class Log(TorchDispatchMode):
         return out
 
 
-x = ht.Variable(name='x')
-y_ = ht.Variable(name='y_')
-loss, _ = resnet50_imagenet(x, y_, 1000)
-opt = ht.optim.MomentumOptimizer(learning_rate=0.1, momentum=0.9)
-train_op = opt.minimize(loss)
-ex = ht.Executor({'train': [loss, train_op]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=1234)
-X = torch.randn((B, 3, 224, 224), device='cuda').bfloat16().contiguous(memory_format=torch.channels_last)
-Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda'), 1000).bfloat16()
+MODEL = sys.argv[2] if len(sys.argv) > 2 else 'resnet50'
+if MODEL == 'resnet50':
+    x = ht.Variable(name='x')
+    y_ = ht.Variable(name='y_')
+    loss, _ = resnet50_imagenet(x, y_, 1000)
+    opt = ht.optim.MomentumOptimizer(learning_rate=0.1, momentum=0.9)
+    train_op = opt.minimize(loss)
+    ex = ht.Executor({'train': [loss, train_op]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=1234)
+    B = B or 256
+    X = torch.randn((B, 3, 224, 224), device='cuda').bfloat16().contiguous(memory_format=torch.channels_last)
+    Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda'), 1000).bfloat16()
+
+    def step():
+        ex.run('train', feed_dict={x: X, y_: Y})
+else:   # the bench.py step of another model (its default batch unless given)
+    import bench
+    sys.argv = ['bench.py', '--model', MODEL] + (['--batch', str(B)] if B else [])
+    if MODEL == 'bert':
+        from hetu_61a7_amd.models.bert import bert_bench as build
+    else:
+        from hetu_61a7_amd.models.moe import moe_top_bench as build
+    step, *_ = build(bench.parse(), 1, 0, 0)
 for _ in range(4):
-    ex.run('train', feed_dict={x: X, y_: Y})
+    step()
 torch.cuda.synchronize()
 log = Log()
 with log:
-    ex.run('train', feed_dict={x: X, y_: Y})
+    step()
 torch.cuda.synchronize()
 print('aten ops in one steady-state step (count, op, call site, first example):')
 for (name, site), n in sorted(log.rows.items(), key=lambda kv: -kv[1]):

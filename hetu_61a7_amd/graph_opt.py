@@ -98,6 +98,15 @@ def _become_bn(node, bn, relu, residual):
 _FRESH_OUTPUT = ('BNGradSelectOp', 'Conv2d_Gradient_of_DataOp', 'SumOp')
 
 
+def _dead_join_operand(other, rest, cons, root_set):
+    """True when the join operand may be overwritten in place (the library GEMM then
+    accumulates into it: beta = 1, C == D, no copy into a fresh output): this join
+    is its only consumer and its op always hands out a freshly allocated tensor."""
+    if other in root_set:
+        return False
+    return len(rest) > 1 or (len(cons.get(other, [])) == 1 and type(other).__name__ in _FRESH_OUTPUT)
+
+
 def fuse_backward(roots):
     """Fold gradient fan-in sums into the data-gradient GEMM epilogue."""
     if os.environ.get('HETU_FUSE', '1') == '0':
@@ -127,6 +136,7 @@ def fuse_backward(roots):
             n.__dict__.update({k: v for k, v in d.__dict__.items() if k not in ('id', 'name', 'inputs', 'bw_of')})
             n.inputs = list(d.inputs) + [other]
             n.op_type = 'MatMulOp'
+            n.acc_inplace = _dead_join_operand(other, rest, cons, root_set)
             n.id, n.name = keep_id, keep_name
             if bw is not None:
                 n.bw_of = bw
@@ -145,12 +155,7 @@ def fuse_backward(roots):
                 n.__class__ = Conv2d_Gradient_of_DataOp
                 n.__dict__.update({k: v for k, v in d.__dict__.items() if k not in ('id', 'name', 'inputs', 'bw_of')})
                 n.inputs = list(d.inputs) + [other]
-                # the accumulated gradient may be overwritten in place (the library
-                # GEMM then accumulates into it: beta = 1, C == D, no copy of it into
-                # a fresh output) when this join is its only consumer and its op
-                # always hands out a freshly allocated tensor
-                n.acc_inplace = other not in root_set and \
-                    (len(rest) > 1 or (len(cons.get(other, [])) == 1 and type(other).__name__ in _FRESH_OUTPUT))
+                n.acc_inplace = _dead_join_operand(other, rest, cons, root_set)
                 n.op_type = 'Conv2d_Gradient_of_DataOp'
                 n.id, n.name = keep_id, keep_name
                 if bw is not None:

@@ -198,23 +198,29 @@ def matmul_into(a, b, ta, tb, out):
     return _vendor_into(_tr(a, ta), _tr(b, tb), out)
 
 
-def matmul_acc(a, b, ta, tb, acc):
+def matmul_acc(a, b, ta, tb, acc, inplace=False):
     """op(a) @ op(b) + acc with the addition in the GEMM epilogue (beta = 1):
-    the MFMA kernel reads ``acc`` as Cin, hipBLASLt runs it as addmm."""
+    the MFMA kernel reads ``acc`` as Cin, hipBLASLt runs it as addmm.
+    ``inplace``: acc is dead after this call, so the library GEMM accumulates
+    into it (C == D) instead of first copying it into a new output."""
     a, b = _match(a, b)
     A, B = _tr(a, ta), _tr(b, tb)
     if native(a) and a.dtype == torch.bfloat16 and A.dim() == 2 and tuple(acc.shape) == (A.shape[0], B.shape[1]) \
             and _MFMA not in ('off', 'vendor'):
         from . import gemm_mfma
-        from .autotune import choose
+        from .autotune import choose, _decisions
         c = acc.to(a.dtype) if acc.dtype != a.dtype else acc
-        hip = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0)
-        vendor = lambda: torch.addmm(c, A, B)
         key = ('gemm_acc', _sig(a), _sig(b), ta, tb)
+        inplace = inplace and c is acc and c.is_contiguous()
+        # while the shape is timed, the in-place candidate accumulates into scratch
+        dst = [c.clone() if inplace and key not in _decisions and _MFMA != 'hip' else c]
+        hip = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0)
+        vendor = (lambda: dst[0].addmm_(A, B)) if inplace else (lambda: torch.addmm(c, A, B))
         cands = {'hip': hip, 'vendor': vendor}
         if A.shape[0] >= 256 and B.shape[1] >= 256:
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=1)
         ch = 'hip' if _MFMA == 'hip' else choose(key, cands)
+        dst[0] = c
         if ch != 'vendor':
             y = cands[ch]()
             if y is not None:

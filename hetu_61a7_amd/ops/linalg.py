@@ -12,7 +12,7 @@ import torch
 
 from .. import ndarray
 from .node import Op
-from .nn import AuxResult
+from .nn import AuxResult, _may_overwrite
 from ..kernels import gemm as KG
 
 
@@ -38,7 +38,8 @@ class MatMulOp(Op):
         if len(input_vals) == 3:   # fused gradient join (graph_opt.fuse_backward): op(a) @ op(b) + acc
             acc = input_vals[2]
             if self.grad_dest is None and not isinstance(acc, ndarray.IndexedSlices):
-                return KG.matmul_acc(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, acc)
+                return KG.matmul_acc(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, acc,
+                                     inplace=_may_overwrite(self, acc))
             y = self.compute([a, b])
             if not (self.grad_dest is not None and y.data_ptr() == self.grad_dest.data_ptr()):
                 y = y.float() if self.grad_dest is not None else y.clone()

@@ -75,6 +75,12 @@ class Conv2dOp(Op):
         return (n, f, ho, wo)
 
 
+def _may_overwrite(op, acc):
+    """graph_opt marked the fused join operand dead after this op, and at run time it
+    is not an alias of another live output"""
+    return bool(getattr(op, 'acc_inplace', False)) and acc is not None and not getattr(acc, 'hetu_shared', False)
+
+
 class Conv2d_Gradient_of_DataOp(Op):
     shape_only_inputs = (2,)
 
@@ -87,7 +93,7 @@ class Conv2d_Gradient_of_DataOp(Op):
         w, g, xshape = input_vals[:3]
         acc = input_vals[3] if len(input_vals) > 3 else None
         return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,
-                                       acc_inplace=getattr(self, 'acc_inplace', False))
+                                       acc_inplace=_may_overwrite(self, acc))
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -366,7 +372,12 @@ class BNGradSelectOp(Op):
         return False
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        return input_vals[0][self.index]
+        tup = input_vals[0]
+        v = tup[self.index]
+        if isinstance(v, torch.Tensor) and v.numel() and \
+                sum(1 for o in tup if isinstance(o, torch.Tensor) and o.data_ptr() == v.data_ptr()) > 1:
+            v.hetu_shared = True    # aliases another output (e.g. LN dx is ds without dropout): never overwrite
+        return v
 
     def gradient(self, output_grad):
         raise NotImplementedError

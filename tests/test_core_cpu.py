@@ -172,3 +172,21 @@ def test_deterministic_flag_toggles_fixed_kernel_choice():
     finally:
         K.set_deterministic(False)
     assert not K.deterministic() and not torch.are_deterministic_algorithms_enabled()
+
+
+def test_gradient_select_flags_aliased_outputs():
+    """A fused backward that returns one tensor in two slots (LayerNorm dx == ds
+    without dropout) marks it shared, so no fused join overwrites it in place."""
+    import torch
+    from hetu_61a7_amd.ops.nn import BNGradSelectOp, _may_overwrite
+    t, u = torch.ones(4, 4), torch.zeros(4, 4)
+    sel = BNGradSelectOp.__new__(BNGradSelectOp)
+    sel.index = 1
+    v = sel.compute([(t, t, torch.ones(4), torch.ones(4))])
+    assert v is t and getattr(t, 'hetu_shared', False)
+    w = sel.compute([(torch.ones(2), u, torch.ones(4), torch.ones(4))])
+    assert w is u and not getattr(u, 'hetu_shared', False)
+
+    class _J:
+        acc_inplace = True
+    assert _may_overwrite(_J(), u) and not _may_overwrite(_J(), t)

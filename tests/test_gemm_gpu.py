@@ -151,3 +151,24 @@ def test_dgrad_join_accumulates_in_place():
         elif autotune._decisions[key] != 'blas':
             assert torch.equal(a, acc)     # timing trials never touched the live operand
     autotune._decisions.pop(key, None)
+
+
+def test_matmul_join_accumulates_in_place():
+    from hetu_61a7_amd.kernels import gemm as KG, autotune
+    a = torch.randn(512, 256, device=DEV).bfloat16()
+    b = torch.randn(384, 256, device=DEV).bfloat16()
+    acc = torch.randn(512, 384, device=DEV).bfloat16()
+    ref = a.float() @ b.float().t() + acc.float()
+    key = ('gemm_acc', KG._sig(a), KG._sig(b), False, True)
+    for forced in (None, 'vendor'):
+        autotune._decisions.pop(key, None)
+        if forced:
+            autotune._decisions[key] = forced
+        c = acc.clone()
+        y = KG.matmul_acc(a, b, False, True, c, inplace=True)
+        assert _rel(y, ref) < 1e-2
+        if forced == 'vendor':
+            assert y.data_ptr() == c.data_ptr()
+        elif autotune._decisions[key] != 'vendor':
+            assert torch.equal(c, acc)
+    autotune._decisions.pop(key, None)

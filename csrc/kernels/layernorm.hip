@@ -221,7 +221,8 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
                                                   const float* __restrict__ rstd, T* __restrict__ dsum,
                                                   T* __restrict__ dx_drop, float* __restrict__ pg,
                                                   float* __restrict__ pb, int64_t R, int N, int rpb, float keep,
-                                                  uint64_t seed) {
+                                                  uint64_t seed, float* __restrict__ zero_a,
+                                                  float* __restrict__ zero_b) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nc = N >> 2;
@@ -241,17 +242,32 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
 #pragma unroll
     for (int k = 0; k < 4; ++k) { ag[i][k] = 0.f; ab[i][k] = 0.f; }
   }
+  if (zero_a != nullptr && blockIdx.x == 0)   // col_reduce2_k accumulates its row slices into these
+    for (int j = threadIdx.x; j < N; j += 256) { zero_a[j] = 0.f; zero_b[j] = 0.f; }
+  // software-pipelined over this wave's rows: the next row's loads are in flight
+  // while the current row is reduced and written
+  float d[CPL][4], xh[CPL][4];
+  auto load_row = [&](int64_t rw, float (&dd)[CPL][4], float (&xx)[CPL][4]) {
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
+        IO4<T>::load(dy + rw * N + 4 * c, dd[i]);
+        IO4<T>::load(xs + rw * N + 4 * c, xx[i]);
+      }
+    }
+  };
+  if (r0 + w < r1) load_row(r0 + w, d, xh);
   for (int64_t row = r0 + w; row < r1; row += 4) {
     const int64_t base = row * N;
     const float mu = mean[row], rs = rstd[row];
-    float d[CPL][4], xh[CPL][4];
+    float dn[CPL][4], xn[CPL][4];
+    if (row + 4 < r1) load_row(row + 4, dn, xn);
     float a = 0.f, cc = 0.f;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
       const int c = lane + 64 * i;
       if (c < nc) {
-        IO4<T>::load(dy + base + 4 * c, d[i]);
-        IO4<T>::load(xs + base + 4 * c, xh[i]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           xh[i][k] = (xh[i][k] - mu) * rs;
@@ -279,6 +295,10 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
         }
       }
     }
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { d[i][k] = dn[i][k]; xh[i][k] = xn[i][k]; }
   }
   // fold the 4 waves' partials (dgamma, then dbeta) through LDS
 #pragma unroll
@@ -298,24 +318,31 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
   }
 }
 
-// oa[j] = sum_r pa[r, j], ob[j] = sum_r pb[r, j]: 64 columns x 4 row groups per block
+// oa[j] = sum_r pa[r, j], ob[j] = sum_r pb[r, j]: 64 columns x 4 row groups per block.
+// gridDim.y > 1 splits the rows into slices whose sums are atomically added into
+// oa / ob (zeroed beforehand by the producer kernel): the few hundred partial rows
+// are otherwise reduced by only N/64 blocks, latency-bound.  gridDim.y == 1 stores
+// (fixed summation order: deterministic mode).
 __global__ void __launch_bounds__(256) col_reduce2_k(const float* __restrict__ pa, const float* __restrict__ pb,
                                                       float* __restrict__ oa, float* __restrict__ ob, int rows,
                                                       int N) {
   __shared__ float sa[4][64], sb[4][64];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
+  const int per = (rows + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int rlo = (int)blockIdx.y * per;
+  const int rhi = rlo + per < rows ? rlo + per : rows;
   float a = 0.f, b = 0.f;
   if (col < N) {
     float a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f, a3 = 0.f, b3 = 0.f;   // 4 loads in flight
-    int r = grp;
-    for (; r + 12 < rows; r += 16) {
+    int r = rlo + grp;
+    for (; r + 12 < rhi; r += 16) {
       a += pa[(int64_t)r * N + col];        b += pb[(int64_t)r * N + col];
       a1 += pa[(int64_t)(r + 4) * N + col]; b1 += pb[(int64_t)(r + 4) * N + col];
       a2 += pa[(int64_t)(r + 8) * N + col]; b2 += pb[(int64_t)(r + 8) * N + col];
       a3 += pa[(int64_t)(r + 12) * N + col]; b3 += pb[(int64_t)(r + 12) * N + col];
     }
-    for (; r < rows; r += 4) {
+    for (; r < rhi; r += 4) {
       a += pa[(int64_t)r * N + col];
       b += pb[(int64_t)r * N + col];
     }
@@ -326,8 +353,15 @@ __global__ void __launch_bounds__(256) col_reduce2_k(const float* __restrict__ p
   sb[grp][lane] = b;
   __syncthreads();
   if (grp == 0 && col < N) {
-    oa[col] = sa[0][lane] + sa[1][lane] + sa[2][lane] + sa[3][lane];
-    ob[col] = sb[0][lane] + sb[1][lane] + sb[2][lane] + sb[3][lane];
+    const float ta = sa[0][lane] + sa[1][lane] + sa[2][lane] + sa[3][lane];
+    const float tb = sb[0][lane] + sb[1][lane] + sb[2][lane] + sb[3][lane];
+    if (gridDim.y == 1) {
+      oa[col] = ta;
+      ob[col] = tb;
+    } else {
+      unsafeAtomicAdd(oa + col, ta);
+      unsafeAtomicAdd(ob + col, tb);
+    }
   }
 }
 
@@ -342,9 +376,10 @@ static void launch_fwd4(const void* x, const void* res, const float* g, const fl
 template <typename T, int CPL>
 static void launch_bwd4(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
                         void* dsum, void* dxd, float* pg, float* pb, int64_t R, int N, int nblk, int rpb,
-                        float keep, uint64_t seed, hipStream_t st) {
+                        float keep, uint64_t seed, float* za, float* zb, hipStream_t st) {
   hipLaunchKernelGGL((ln_bwd4_k<T, CPL>), dim3((unsigned)nblk), dim3(256), 4 * N * sizeof(float), st,
-                     (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed);
+                     (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed,
+                     za, zb);
 }
 
 #define HETU_CPL_DISPATCH(CPL_NEEDED, FN, ...)                 \
@@ -370,13 +405,15 @@ template <int CPL> static void fwd4_f32(const void* x, const void* res, const fl
 }
 template <int CPL> static void bwd4_bf16(const void* dy, const void* xs, const float* g, const float* m,
                                          const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
-                                         int N, int nblk, int rpb, float keep, uint64_t seed, hipStream_t st) {
-  launch_bwd4<bf16, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, st);
+                                         int N, int nblk, int rpb, float keep, uint64_t seed, float* za,
+                                         float* zb, hipStream_t st) {
+  launch_bwd4<bf16, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, st);
 }
 template <int CPL> static void bwd4_f32(const void* dy, const void* xs, const float* g, const float* m,
                                         const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
-                                        int N, int nblk, int rpb, float keep, uint64_t seed, hipStream_t st) {
-  launch_bwd4<float, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, st);
+                                        int N, int nblk, int rpb, float keep, uint64_t seed, float* za,
+                                        float* zb, hipStream_t st) {
+  launch_bwd4<float, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, st);
 }
 
 }  // namespace hetu
@@ -433,17 +470,23 @@ HETU_API int hetu_ln_fused_fwd(const void* x, const void* res, const float* g, c
 // Backward of the fused forward.  xs = the normalised input (x + res after
 // dropout, or x).  dsum (grad of xs / of the residual) and dx_drop (grad of x
 // through the dropout) may each be null.  ws: 2 * nblk * N floats.
+// deterministic != 0: the dgamma/dbeta partial rows are summed in a fixed order
+// (one block per 64 columns) instead of by row slices with fp32 atomics.
 HETU_API int hetu_ln_fused_bwd(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
                                void* dsum, void* dx_drop, float* dg, float* db, float* ws, int64_t R, int N,
-                               int nblk, float keep, int64_t seed, int is_bf16, hipStream_t st) {
+                               int nblk, float keep, int64_t seed, int is_bf16, int deterministic, hipStream_t st) {
   if ((N & 3) || N > 2048 || R <= 0 || nblk <= 0) return (int)hipErrorInvalidValue;
   const int cpl = (N / 4 + 63) / 64;
   const int rpb = (int)((R + nblk - 1) / nblk);
   float* pg = ws;
   float* pb = ws + (int64_t)nblk * N;
-  if (is_bf16) HETU_CPL_DISPATCH(cpl, bwd4_bf16, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, st);
-  else HETU_CPL_DISPATCH(cpl, bwd4_f32, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, st);
-  hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, pg, pb, dg, db, nblk, N);
+  const int slices = deterministic ? 1 : (nblk >= 256 ? 8 : (nblk >= 64 ? 4 : 1));
+  float* za = slices > 1 ? dg : nullptr;
+  float* zb = slices > 1 ? db : nullptr;
+  if (is_bf16) HETU_CPL_DISPATCH(cpl, bwd4_bf16, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, st);
+  else HETU_CPL_DISPATCH(cpl, bwd4_f32, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, st);
+  hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64), (unsigned)slices), dim3(256), 0, st, pg, pb, dg,
+                     db, nblk, N);
   HETU_LAUNCH_CHECK();
   return 0;
 }

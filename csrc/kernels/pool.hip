@@ -249,8 +249,18 @@ __global__ void __launch_bounds__(256) reduce_mid_k(const T* __restrict__ x, flo
   if (r1 > R) r1 = R;
   __shared__ float sh[256];
   float s = 0.f;
-  if (c < C)
-    for (int64_t r = r0 + rsub; r < r1; r += 4) s += to_f(x[(b * R + r) * C + c]);
+  if (c < C) {   // 4 rows in flight per lane (one element per load: latency-bound otherwise)
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = r0 + rsub;
+    for (; r + 12 < r1; r += 16) {
+      s += to_f(x[(b * R + r) * C + c]);
+      s1 += to_f(x[(b * R + r + 4) * C + c]);
+      s2 += to_f(x[(b * R + r + 8) * C + c]);
+      s3 += to_f(x[(b * R + r + 12) * C + c]);
+    }
+    for (; r < r1; r += 4) s += to_f(x[(b * R + r) * C + c]);
+    s += s1 + s2 + s3;
+  }
   sh[threadIdx.x] = s;
   __syncthreads();
   if (rsub == 0 && c < C) {
@@ -449,7 +459,8 @@ HETU_API int hetu_reduce_mid(const void* x, void* y, int64_t B, int64_t R, int64
   const bool vec = cpt > 64 && ((uintptr_t)x % 16) == 0;
   int64_t ctiles = (C + (vec ? cpt : 64) - 1) / (vec ? cpt : 64);
   int64_t blocks = ctiles * B;
-  int64_t chunks = blocks >= 1024 ? 1 : (1024 + blocks - 1) / blocks;
+  const int64_t target = vec ? 1024 : 2048;   // the scalar path moves 4x fewer bytes per block
+  int64_t chunks = blocks >= target ? 1 : (target + blocks - 1) / blocks;
   int64_t maxc = (R + 63) / 64;
   if (chunks > maxc) chunks = maxc;
   if (chunks < 1) chunks = 1;

@@ -120,11 +120,12 @@ def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_d
         nblk = max(1, min(512, (R + 7) // 8))
         ws = torch.empty(2 * nblk * N, dtype=torch.float32, device=s.device)
         dg, db = _dest(dg_out, N, s.device), _dest(db_out, N, s.device)
-        f = fn('hetu_ln_fused_bwd', [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, P])
+        from . import deterministic
+        f = fn('hetu_ln_fused_bwd', [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, I32, P])
         check(f(dyc.data_ptr(), sc.data_ptr(), gamma.float().contiguous().data_ptr(), mean.data_ptr(),
                 rstd.data_ptr(), ds.data_ptr() if ds is not None else None,
                 dx.data_ptr() if dx is not None else None, dg.data_ptr(), db.data_ptr(), ws.data_ptr(), R, N, nblk,
-                float(keep), int(seed), is_bf16(s), stream_ptr()), 'ln_fused_bwd')
+                float(keep), int(seed), is_bf16(s), int(deterministic()), stream_ptr()), 'ln_fused_bwd')
         if need_dx and keep >= 1.0:
             dx = ds
         return ds, dx, dg, db

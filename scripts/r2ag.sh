@@ -1,0 +1,8 @@
+# same-box A/B: ab_old = previous commit, . = working tree (alternating runs)
+export TMPDIR=/tmp
+S=scripts/gpu_step.sh
+for i in 1 2; do
+  (cd ab_old && PYTHONPATH=$PWD timeout -k 10 200 python bench.py --model bert --steps 30 --warmup 5 > ../gpurun_out/ab_old_$i.log 2>&1) || exit 1
+  PYTHONPATH=$PWD timeout -k 10 200 python bench.py --model bert --steps 30 --warmup 5 > gpurun_out/ab_new_$i.log 2>&1 || exit 1
+done
+grep -h value gpurun_out/ab_old_*.log gpurun_out/ab_new_*.log | cut -c1-140

@@ -34,6 +34,73 @@ __device__ __forceinline__ void row_max_sum(const T* x, int N, int lane, float& 
   }
 }
 
+// Long rows (the MLM vocabulary, N ~ 30k) split into an unaligned scalar head,
+// a 16-byte vector body (8 bf16 / 4 fp32 per lane: one max + one rescale per
+// vector) and a scalar tail; the row start is only element-aligned in general.
+template <typename T>
+__device__ __forceinline__ int row_head(const T* x, int N) {
+  const int h = (int)(((16 - ((uintptr_t)x & 15)) & 15) / sizeof(T));
+  return h < N ? h : N;
+}
+
+template <typename T>
+__device__ __forceinline__ void online_merge(float& m, float& s, float v) {
+  const float nm = fmaxf(m, v);
+  s = s * __expf(m - nm) + __expf(v - nm);
+  m = nm;
+}
+
+template <typename T>
+__device__ __forceinline__ void row_max_sum_vec(const T* x, int N, int lane, float& m, float& s) {
+  constexpr int V = Vec<T>::N;
+  m = -INFINITY;
+  s = 0.f;
+  const int h = row_head(x, N);
+  if (lane < h) online_merge<T>(m, s, to_f(x[lane]));
+  const int nv = (N - h) / V;
+  const T* xb = x + h;
+  int j = lane;
+  for (; j + 64 < nv; j += 128) {          // two vectors in flight
+    float v[V], w[V];
+    load_vec<T>(xb + (int64_t)j * V, v);
+    load_vec<T>(xb + (int64_t)(j + 64) * V, w);
+    float vm = v[0];
+#pragma unroll
+    for (int k = 1; k < V; ++k) vm = fmaxf(vm, v[k]);
+#pragma unroll
+    for (int k = 0; k < V; ++k) vm = fmaxf(vm, w[k]);
+    const float nm = fmaxf(m, vm);
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) t += __expf(v[k] - nm) + __expf(w[k] - nm);
+    s = s * __expf(m - nm) + t;
+    m = nm;
+  }
+  for (; j < nv; j += 64) {
+    float v[V];
+    load_vec<T>(xb + (int64_t)j * V, v);
+    float vm = v[0];
+#pragma unroll
+    for (int k = 1; k < V; ++k) vm = fmaxf(vm, v[k]);
+    const float nm = fmaxf(m, vm);
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) t += __expf(v[k] - nm);
+    s = s * __expf(m - nm) + t;
+    m = nm;
+  }
+  for (int t = h + nv * V + lane; t < N; t += 64) online_merge<T>(m, s, to_f(x[t]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    float nm = fmaxf(m, om);
+    float a = (m == -INFINITY) ? 0.f : s * __expf(m - nm);
+    float b = (om == -INFINITY) ? 0.f : os * __expf(om - nm);
+    m = nm;
+    s = a + b;
+  }
+}
+
 template <typename T, bool LOG>
 __global__ void __launch_bounds__(256) softmax_fwd_k(const T* __restrict__ x, T* __restrict__ y,
                                                       int64_t R, int N) {
@@ -130,7 +197,7 @@ __global__ void __launch_bounds__(256) sce_sparse_fwd_k(const T* __restrict__ x,
   if (row >= R) return;
   const T* xr = x + row * N;
   float m, s;
-  row_max_sum(xr, N, lane, m, s);
+  row_max_sum_vec(xr, N, lane, m, s);
   const float lse = m + __logf(s);
   if (lane == 0) {
     const int64_t c = lab[row];
@@ -157,12 +224,32 @@ __global__ void __launch_bounds__(256) sce_sparse_bwd_k(const T* __restrict__ x,
     lse = lse_in[row];
   } else {
     float m, s;
-    row_max_sum(xr, N, lane, m, s);
+    row_max_sum_vec(xr, N, lane, m, s);
     lse = m + __logf(s);
   }
   const float gr = ign ? 0.f : (g_scalar ? g[0] : g[row]);
-  for (int j = lane; j < N; j += 64)
-    dx[row * N + j] = from_f<T>(gr * (__expf(ld(xr, j) - lse) - (j == c ? 1.f : 0.f)));
+  T* dr = dx + row * N;
+  constexpr int V = Vec<T>::N;
+  // x and dx share the row pitch; vector body only when their rows align alike
+  const int h = row_head(xr, N);
+  const bool vec = ((uintptr_t)xr & 15) == ((uintptr_t)dr & 15);
+  if (!vec) {
+    for (int j = lane; j < N; j += 64)
+      dr[j] = from_f<T>(gr * (__expf(ld(xr, j) - lse) - (j == c ? 1.f : 0.f)));
+    return;
+  }
+  if (lane < h) dr[lane] = from_f<T>(gr * (__expf(ld(xr, lane) - lse) - (lane == c ? 1.f : 0.f)));
+  const int nv = (N - h) / V;
+  for (int j = lane; j < nv; j += 64) {
+    const int64_t e0 = h + (int64_t)j * V;
+    float v[V];
+    load_vec<T>(xr + e0, v);
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = gr * (__expf(v[k] - lse) - (e0 + k == c ? 1.f : 0.f));
+    store_vec<T>(dr + e0, v);
+  }
+  for (int t = h + nv * V + lane; t < N; t += 64)
+    dr[t] = from_f<T>(gr * (__expf(ld(xr, t) - lse) - (t == c ? 1.f : 0.f)));
 }
 
 }  // namespace hetu

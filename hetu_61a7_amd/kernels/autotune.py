@@ -1,7 +1,8 @@
 """Per-shape kernel selection by measurement.
 
 ``choose(key, {name: fn})`` times every candidate once per key (events on the
-current stream, a few repetitions after a warm call) and caches the fastest.
+current stream; after two warm calls, interleaved rounds of a few repetitions,
+best round per candidate) and caches the fastest.
 Used to pick, per convolution / GEMM shape, between the hand-written MFMA
 kernels and the vendor library, so a hand-written kernel runs exactly where it
 is at least as fast.  Never measures inside a hipGraph capture (returns the
@@ -15,7 +16,8 @@ import torch
 
 _decisions = {}
 _times = {}
-REPS = int(os.environ.get('HETU_AUTOTUNE_REPS', '10'))
+REPS = int(os.environ.get('HETU_AUTOTUNE_REPS', '5'))
+ROUNDS = int(os.environ.get('HETU_AUTOTUNE_ROUNDS', '3'))
 
 
 def choose(key, candidates):
@@ -28,19 +30,28 @@ def choose(key, candidates):
         return names[0]       # fixed choice: the hand-written kernel every call site lists first
     if len(names) == 1 or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
         return names[0]
-    times = {}
+    live = []
     for n in names:
         f = candidates[n]
         if f() is None:  # unsupported shape
             continue
         f()  # second warm call: first-use library heuristics / code-object loads
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(REPS):
-            f()
-        e.record()
-        e.synchronize()
-        times[n] = s.elapsed_time(e) / REPS
+        live.append(n)
+    # ROUNDS interleaved rounds (a, b, c, a, b, c, ...) of REPS calls each; a
+    # candidate's time is its best round, so a clock / co-tenant dip during one
+    # candidate's window does not decide the choice
+    times = {}
+    for _ in range(ROUNDS):
+        for n in live:
+            f = candidates[n]
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(REPS):
+                f()
+            e.record()
+            e.synchronize()
+            t = s.elapsed_time(e) / REPS
+            times[n] = min(times.get(n, t), t)
     best = min(times, key=times.get) if times else names[-1]
     _decisions[key] = best
     _times[key] = times

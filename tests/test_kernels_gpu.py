@@ -125,6 +125,26 @@ def test_softmax_and_ce(dt):
     torch.testing.assert_close(ls, refs, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('N', [30522, 1001, 7, 520])
+def test_sparse_softmax_ce_unaligned_rows(dt, N):
+    """Vocabulary-wide rows whose starts are not 16-byte aligned (scalar head,
+    vector body, scalar tail), forward loss and backward gradient."""
+    R = 67
+    x = (torch.randn(R, N, device=DEV) * 3).to(dt)
+    ids = torch.randint(0, N, (R,), device=DEV)
+    ids[::5] = -1
+    valid = ids >= 0
+    ls, lse = KS.softmax_ce_sparse(x, ids, -1)
+    ref = torch.where(valid, F.cross_entropy(x.float(), ids.clamp_min(0), reduction='none'), torch.zeros(R, device=DEV))
+    torch.testing.assert_close(ls, ref, rtol=1e-4, atol=1e-4)
+    g = torch.rand(R, device=DEV)
+    for l in (lse, None):
+        dx = KS.softmax_ce_sparse_backward(x, ids, g, l, -1)
+        refd = (g * valid.float())[:, None] * (torch.softmax(x.float(), -1) - F.one_hot(ids.clamp_min(0), N).float())
+        torch.testing.assert_close(dx.float(), refd, **_tol(dt))
+
+
 @pytest.mark.parametrize('mode', ['sgd', 'momentum', 'nesterov', 'adagrad', 'adam', 'adamw', 'lamb'])
 def test_flat_optimizer(mode):
     n = 100003

@@ -22,8 +22,12 @@ struct BnGeom {
 
 // launch-shape tunables (hetu_bn_tune; scripts/bench_bn.py sweeps them): target
 // partial-statistics blocks per launch, and the block cap of the streaming kernels
-static int g_bn_chunk_target = 1024;
+static int g_bn_chunk_target = 512;
 static int g_bn_apply_blocks = 2048;
+// at least this many row passes per thread in the partial kernels: small layers
+// (14x14, 7x7) otherwise spread over ~1024 blocks of a dozen rows each, writing
+// as many partial sums as they read activations
+static int g_bn_min_passes = 16;
 
 static int bn_apply_grid(int64_t nvec, int C, int V) {
   int64_t b = (nvec + 1023) / 1024;
@@ -41,6 +45,8 @@ static BnGeom bn_geom(int64_t M, int C, int vec) {
   g.tiles = (cv + g.W - 1) / g.W;
   int want = (int)((g_bn_chunk_target + g.tiles - 1) / g.tiles);
   int64_t max_chunks = (M + g.RP - 1) / g.RP;
+  const int64_t pass_cap = M / ((int64_t)g.RP * g_bn_min_passes);
+  if (max_chunks > pass_cap) max_chunks = pass_cap;
   if (want > max_chunks) want = (int)max_chunks;
   if (want < 1) want = 1;
   g.chunks = want;
@@ -527,9 +533,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
 
 using namespace hetu;
 
-HETU_API void hetu_bn_tune(int chunk_target, int apply_blocks) {
+HETU_API void hetu_bn_tune(int chunk_target, int apply_blocks, int min_passes) {
   if (chunk_target > 0) g_bn_chunk_target = chunk_target;
   if (apply_blocks > 0) g_bn_apply_blocks = apply_blocks;
+  if (min_passes > 0) g_bn_min_passes = min_passes;
 }
 
 // workspace floats needed: 2 * chunks * C + 5 * C  (partials + fold/bwd coefficients)

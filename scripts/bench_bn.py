@@ -1,7 +1,7 @@
 """BatchNorm kernel bandwidth over the ResNet-50 (bs 256, bf16, channels-last)
 BN shapes, against a plain device copy of the same tensor, with a sweep of the
 launch-shape tunables (hetu_bn_tune: partial-statistics block target, streaming
-block cap).  GB/s counts the compulsory HBM bytes of each op:
+block cap, minimum row passes per thread).  GB/s counts the compulsory HBM bytes of each op:
   stats  = read x                      (col_sums: partial + merge)
   fwd    = read x (stats) + read x + write y   (bn_forward, ReLU)
   bwd    = read dy,x (partial) + read dy,x + write dx   (bn_backward, ReLU mode 2)
@@ -22,7 +22,7 @@ SHAPES = [(64, 112), (64, 56), (256, 56), (128, 56), (128, 28), (512, 28), (256,
           (1024, 14), (512, 14), (512, 7), (2048, 7)]
 out_path = sys.argv[1] if len(sys.argv) > 1 else None
 lines = []
-tune = fn('hetu_bn_tune', [I32, I32])
+tune = fn('hetu_bn_tune', [I32, I32, I32])
 
 
 def emit(s):
@@ -67,11 +67,11 @@ def run(label):
     emit('total ms (one BN per shape): ' + ' '.join('%s %.3f' % kv for kv in tot.items()))
 
 
-run('defaults (chunk target 1024, apply cap 2048)')
-for ct, cap in [(2048, 2048), (512, 2048), (1024, 4096), (2048, 8192), (1024, 1024)]:
-    tune(ct, cap)
-    run('chunk target %d, apply cap %d' % (ct, cap))
-tune(1024, 2048)
+run('defaults (chunk target 512, apply cap 2048, min passes 16)')
+for ct, cap, mp in [(1024, 2048, 1), (1024, 2048, 8), (1024, 2048, 16), (1024, 2048, 32), (2048, 2048, 16)]:
+    tune(ct, cap, mp)
+    run('chunk target %d, apply cap %d, min passes %d' % (ct, cap, mp))
+tune(512, 2048, 16)
 if out_path:
     with open(out_path, 'w') as f:
         f.write('\n'.join(lines) + '\n')

@@ -370,22 +370,31 @@ class OptimizerOp(Op):
             self.ps_dense = PSDense(self.flat, (1 << 20) + self.id, config)
 
     def _make_buckets(self, dense):
-        cap = max(self.bucket_bytes // 4, 1)
-        cur_start, cur_n, members = 0, 0, []
-        self.buckets = []
-        for p in dense:
-            if self.excluded_from_dp(p):
-                continue
+        """Contiguous buckets over the flat gradient, built from the END of the
+        arrival order with growing caps (bucket_bytes/8, /4, /2, then full): the
+        all-reduce that can only start once the last gradient has arrived -- the
+        one the backward pass cannot hide -- is the smallest, while the early
+        buckets stay large (few, big RCCL calls over the xGMI ring)."""
+        full = max(self.bucket_bytes // 4, 1)
+        cap = max(full // 8, 1)
+        groups, cur, cur_n, nxt = [], [], 0, None
+        for p in reversed([p for p in dense if not self.excluded_from_dp(p)]):
             o, n, _ = self.flat.offsets[p]
-            if members and (o != cur_start + cur_n or cur_n + n > cap):
-                self._close_bucket(cur_start, cur_n, members)
-                cur_start, cur_n, members = o, 0, []
-            if not members:
-                cur_start = o
-            members.append(p)
+            # members must stay contiguous in the flat buffer (o + n == start of the next)
+            if cur and (o + n != nxt or cur_n + n > cap):
+                groups.append(cur)
+                cur, cur_n = [], 0
+                cap = min(cap * 2, full)
+            cur.append(p)
             cur_n += n
-        if members:
-            self._close_bucket(cur_start, cur_n, members)
+            nxt = o
+        if cur:
+            groups.append(cur)
+        self.buckets = []
+        for members in reversed(groups):
+            members = members[::-1]
+            start = self.flat.offsets[members[0]][0]
+            self._close_bucket(start, sum(self.flat.offsets[p][1] for p in members), members)
 
     def _make_zero_buckets(self, dense):
         """ZeRO-1 (absent in the reference): fixed-size buckets

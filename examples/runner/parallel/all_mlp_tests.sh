@@ -12,4 +12,5 @@ $R -w 2 python $S --mode pp --schedule gpipe
 $R -w 4 python $S --mode pp --schedule pipedream
 $R -w 4 python $S --mode dp_pp --replicas 2 --schedule gpipe
 for s in left right middle; do $R -w 2 python $S --mode mp --split $s; done
+$R -w 4 python complex_pipeline_mlp.py
 python validate_results.py

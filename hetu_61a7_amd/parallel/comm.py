@@ -36,6 +36,13 @@ def _free_port():
 
 
 def backend_for_device(dev_is_gpu: bool) -> str:
+    """RCCL ('nccl' on ROCm) for GPU tensors, gloo for host tensors.
+    ``HETU_DIST_BACKEND=gloo`` forces gloo for GPU tensors too: several ranks
+    can then share one GPU (RCCL refuses duplicate devices), which rehearses
+    the multi-rank GPU path on a one-GPU box."""
+    forced = os.environ.get('HETU_DIST_BACKEND')
+    if forced:
+        return forced
     return 'nccl' if dev_is_gpu else 'gloo'
 
 
@@ -67,7 +74,7 @@ def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] 
         os.environ.setdefault('WORLD_SIZE', str(world))
         kw = dict(backend=backend_for_device(use_gpu), rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu:
+        if use_gpu and kw['backend'] == 'nccl':
             kw['device_id'] = torch.device('cuda', torch.cuda.current_device())
         try:
             dist.init_process_group(**kw)
@@ -109,6 +116,13 @@ _RED = {'sum': dist.ReduceOp.SUM, 'max': dist.ReduceOp.MAX, 'min': dist.ReduceOp
         'prod': dist.ReduceOp.PRODUCT}
 
 
+class _CInt(object):
+    __slots__ = ('value',)
+
+    def __init__(self, v):
+        self.value = int(v)
+
+
 class Communicator(object):
     """A (sub-)group of ranks: collectives on the calling stream.
 
@@ -131,6 +145,24 @@ class Communicator(object):
         self.global_rank = dist.get_rank()
         self.local_rank = dist_env()[2]
         self.device_id = self.local_rank
+
+    # reference MPI_NCCL_Communicator fields (ctypes c_int: read through .value),
+    # used by manual-pipeline scripts (examples/runner/parallel/complex_pipeline_mlp.py)
+    @property
+    def myRank(self):
+        return _CInt(self.rank)
+
+    @property
+    def nRanks(self):
+        return _CInt(self.nrank)
+
+    @property
+    def localRank(self):
+        return _CInt(self.local_rank)
+
+    @property
+    def dev_id(self):
+        return _CInt(self.device_id)
 
     # -- helpers ------------------------------------------------------------------
     def _g(self, r):
@@ -192,7 +224,7 @@ class Communicator(object):
         return dist.batch_isend_irecv(p2p)
 
     def barrier(self):
-        if self.use_gpu:
+        if self.use_gpu and dist.get_backend(self.group) == 'nccl':
             dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier(group=self.group)

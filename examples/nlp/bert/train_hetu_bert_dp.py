@@ -1,0 +1,10 @@
+"""Reference entry point examples/nlp/bert/train_hetu_bert_dp.py: BERT pretraining (MLM + NSP), data parallel over all ranks (RCCL all-reduce; launch with heturun -w N / torchrun).
+Same flags as examples/nlp/train_hetu_bert.py."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+from train_hetu_bert import main  # noqa: E402
+
+if __name__ == '__main__':
+    main(['--dp'] + sys.argv[1:])

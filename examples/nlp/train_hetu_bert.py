@@ -37,6 +37,8 @@ def main(argv=None):
     p.add_argument('--steps', type=int, default=20, help='steps per epoch')
     p.add_argument('--gpu', type=int, default=0, help='-1 = CPU')
     p.add_argument('--dp', action='store_true', help='data parallel over all ranks (RCCL)')
+    p.add_argument('--ps', action='store_true', help='data parallel through the parameter server '
+                   '(DataParallel(aggregate="PS"); launch with heturun -s 1 -w N)')
     p.add_argument('--galvatron', action='store_true', help='DP x PP layout from the planner')
     p.add_argument('--fp32', action='store_true')
     a = p.parse_args(argv)
@@ -59,6 +61,8 @@ def main(argv=None):
     feeds, loss, train = bert_pretrain_graph(cfg, optimizer=opt, plan=plan)
     if plan is not None and plan.pp > 1:
         ex = ht.Executor({'train': [loss, train]}, pipeline='gpipe', **kw)
+    elif a.ps:
+        ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel(aggregate='PS'), **kw)
     elif a.dp or plan is not None:
         ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'), **kw)
     else:

@@ -245,8 +245,10 @@ class BertForSequenceClassification(object):
         logits = _dense(_dropout(pooled, self.cfg.hidden_dropout_prob), self.cfg.hidden_size,
                         self.num_labels, 'classifier', self.cfg)
         if labels is None:
-            return [logits]
-        return [logits, ht.softmaxcrossentropy_sparse_op(logits, labels, ignored_index=-1)]
+            return logits
+        # (loss, logits) like the reference (hetu_bert.py:853-865); the fused
+        # sparse softmax-CE kernel replaces its softmax_op -> crossentropy_sparse_op
+        return ht.softmaxcrossentropy_sparse_op(logits, labels, ignored_index=-1), logits
 
 
 def plan_placement(plan, ctx_of_ranks=None):

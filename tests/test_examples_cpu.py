@@ -4,6 +4,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,6 +23,11 @@ RUNS = [
      '--steps', '2', '--fp32'],
     ['examples/moe/test_moe.py', '--gpu', '-1', '--batch_size', '2', '--num_tokens', '32', '--model_dim', '16',
      '--hidden_size', '32', '--num_steps', '2', '--gate', 'top'],
+    ['examples/moe/test_moe_sam.py', '--gpu', '-1', '--batch_size', '2', '--num_tokens', '32', '--model_dim', '16',
+     '--hidden_size', '32', '--num_steps', '2'],
+    ['bin/heturun', '-w', '2', '-s', '1', sys.executable, 'examples/nlp/bert/train_hetu_bert_ps.py', '--gpu', '-1',
+     '--hidden_size', '64', '--num_hidden_layers', '2', '--num_attention_heads', '2', '--seq_length', '32',
+     '--train_batch_size', '4', '--vocab_size', '2000', '--steps', '2', '--fp32'],
     ['examples/gnn/run_single.py', '--gpu', '-1', '--nodes', '500', '--epochs', '2'],
     ['examples/rec/run_hetu.py', '--gpu', '-1', '--nepoch', '1', '--steps', '3', '--batch-size', '256', '--val'],
     ['examples/nlp/train_hetu_transformer.py', '--gpu', '-1', '--vocab_size', '200', '--d_model', '32', '--d_ff',
@@ -64,3 +70,14 @@ def test_parallel_equivalence_examples(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(d, 'validate_results.py'), out], capture_output=True,
                        text=True, timeout=60)
     assert r.returncode == 0 and r.stdout.count(' ok') == 5, r.stdout
+
+
+def test_glue_finetune_learns():
+    """examples/nlp/bert/test_glue_hetu_bert.py: the sequence-classification head
+    fine-tunes (3-label MNLI-shaped batches whose label is marked in the tokens)."""
+    sys.path.insert(0, os.path.join(ROOT, 'examples', 'nlp', 'bert'))
+    import test_glue_hetu_bert as G
+    accs = G.main(['--gpu_id', '-1', '--hidden_size', '64', '--num_hidden_layers', '2', '-a', '2', '-s', '16',
+                   '--train_batch_size', '32', '--vocab_size', '1100', '-e', '3', '--batches', '20', '--lr', '1e-3',
+                   '--dropout_prob', '0', '--task_name', 'mnli'])
+    assert np.mean(accs[:5]) < 0.5 and np.mean(accs[-5:]) > 0.6, accs

@@ -70,6 +70,8 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     assert world == args.gpus or world == 1, 'launch with --nproc-per-node == --gpus'
+    if os.environ.get('HETU_DIST_BACKEND') == 'gloo':
+        local = local % torch.cuda.device_count()     # multi-rank rehearsal on one GPU
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 

@@ -223,7 +223,8 @@ class GNNDataLoaderOp(Op):
     """Graph-sampling source (GraphMix hook in the reference; GraphMix itself is
     not shipped).  Feeds batches produced by a user ``handler``."""
 
-    graph = None
+    graph = None        # the sampled graph this step trains on
+    nxt_graph = None    # the one after it (prefetchable)
 
     def __init__(self, handler, ctx=None):
         super().__init__(GNNDataLoaderOp, [], ctx or ndarray.cpu(0))
@@ -235,6 +236,12 @@ class GNNDataLoaderOp(Op):
     def get_arr(self, name, config=None):
         return self.handler(GNNDataLoaderOp.graph)
 
+    def get_next_arr(self, name):
+        return self.handler(GNNDataLoaderOp.nxt_graph)
+
+    def get_cur_shape(self, name):
+        return self.handler(GNNDataLoaderOp.graph).shape
+
     def gradient(self, output_grad):
         return None
 
@@ -243,4 +250,8 @@ class GNNDataLoaderOp(Op):
 
     @classmethod
     def step(cls, graph):
-        cls.graph = graph
+        """Two-deep queue (reference dataloader.py:180-183): the graph given now
+        is trained on one step later, so its sampling overlaps the current step.
+        Call it twice before the first run."""
+        cls.graph = cls.nxt_graph
+        cls.nxt_graph = graph

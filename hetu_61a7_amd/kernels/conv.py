@@ -221,6 +221,11 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     return _vendor_dgrad(g, w, x_shape, stride, padding, acc)
 
 
+def _layout_of(t):
+    """channels-last for channels-last GPU tensors, else NCHW (one layout per vendor call)"""
+    return CL if t.is_cuda and t.is_contiguous(memory_format=CL) else torch.contiguous_format
+
+
 def _vendor_dgrad(g, w, x_shape, stride, padding, acc=None):
     dx = _vendor_dgrad0(g, w, x_shape, stride, padding)
     if acc is not None:
@@ -229,10 +234,11 @@ def _vendor_dgrad(g, w, x_shape, stride, padding, acc=None):
 
 
 def _vendor_dgrad0(g, w, x_shape, stride, padding):
-    # MIOpen only reads x's shape + layout: allocate it channels-last directly
-    # (``empty(...).contiguous(CL)`` was a full-size copy of garbage per call)
-    xs = torch.empty(x_shape, dtype=g.dtype, device=g.device,
-                     memory_format=CL if g.is_cuda else torch.contiguous_format)
+    # MIOpen only reads x's shape + layout: allocate it directly (``empty(...)
+    # .contiguous(CL)`` was a full-size copy of garbage per call) in g's layout --
+    # a channels-last x with an NCHW g (the fp32 3-channel differential test)
+    # mixes layouts in one MIOpen call, which aborted intermittently
+    xs = torch.empty(x_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
     dx, _, _ = torch.ops.aten.convolution_backward(
         g, xs, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [True, False, False])
     return dx
@@ -305,8 +311,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
 
 
 def _vendor_wgrad(g, x, w_shape, stride, padding):
-    ws = torch.empty(w_shape, dtype=g.dtype, device=g.device,
-                     memory_format=CL if g.is_cuda else torch.contiguous_format)
+    ws = torch.empty(w_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
     _, dw, _ = torch.ops.aten.convolution_backward(
         g, x, ws, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [False, True, False])
     return dw

@@ -214,6 +214,10 @@ class HetuConfig(object):
                 if ndarray.is_gpu_ctx(n.ctx):
                     n.ctx = self.context
         if self.context is not None and ndarray.is_gpu_ctx(self.context) and torch.cuda.is_available():
+            n_dev = torch.cuda.device_count()
+            if self.context.device_id >= n_dev and os.environ.get('HETU_DIST_BACKEND') == 'gloo':
+                # multi-rank rehearsal on a box with fewer GPUs than ranks (gloo only)
+                self.context = ndarray.gpu(self.context.device_id % n_dev)
             torch.cuda.set_device(self.context.device_id)
 
         # ---- communicators ------------------------------------------------------------
@@ -398,7 +402,7 @@ class SubExecutor(object):
 
     def __init__(self, name, eval_node_list, config: HetuConfig):
         from ..optimizer import OptimizerOp
-        from ..dataloader import DataloaderOp
+        from ..dataloader import DataloaderOp, GNNDataLoaderOp
         self.name = name
         self.eval_node_list = list(eval_node_list)
         self.config = config
@@ -413,7 +417,7 @@ class SubExecutor(object):
                     self.param_nodes.append(n)
                 else:
                     self.feed_nodes.append(n)
-            elif isinstance(n, DataloaderOp):
+            elif isinstance(n, (DataloaderOp, GNNDataLoaderOp)):
                 self.dataloader_nodes.append(n)
             else:
                 self.computing_nodes.append(n)
@@ -543,7 +547,9 @@ class SubExecutor(object):
             if n not in vals:
                 raise KeyError('placeholder %s not fed' % n.name)
         for d in self.dataloader_nodes:
-            vals[d] = d.get_arr(self.name, cfg)
+            v = d.get_arr(self.name, cfg)
+            # GNN sampling handlers return host arrays: place them like a feed
+            vals[d] = v if isinstance(v, torch.Tensor) else self._feed_value(d, v)
         for t, d in self.ps_prefetch:
             t.next_ids_fn = (lambda d=d, nm=self.name: d.peek_next_arr(nm))
         return vals

@@ -216,7 +216,20 @@ class DataloaderOp(Op):
 
 
 def dataloader_op(dataloaders):
-    return DataloaderOp(dataloaders)
+    """``dataloaders``: Dataloader objects, or their constructor arguments as
+    ``[data, batch_size, name, ...]`` lists or keyword dicts (reference
+    dataloader.py:243-257)."""
+    dls = []
+    for dl in dataloaders:
+        if isinstance(dl, Dataloader):
+            dls.append(dl)
+        elif isinstance(dl, (list, tuple)):
+            dls.append(Dataloader(*dl))
+        elif isinstance(dl, dict):
+            dls.append(Dataloader(**dl))
+        else:
+            raise TypeError('dataloader_op: expected Dataloader, list or dict, got %r' % type(dl))
+    return DataloaderOp(dls)
 
 
 class GNNDataLoaderOp(Op):

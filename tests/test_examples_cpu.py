@@ -38,6 +38,9 @@ RUNS = [
      '64', '--num_blocks', '1', '--num_heads', '4', '--maxlen1', '8', '--maxlen2', '9', '--batch_size', '4',
      '--steps', '2'],
     ['examples/runner/run_mlp.py', '--gpu', '-1', '--steps', '5'],
+    ['examples/runner/run_wdl.py', '--config', 'local', '--nepoch', '2', '--val'],
+    ['bin/heturun', '-w', '2', '-s', '1', sys.executable, 'examples/runner/run_wdl.py', '--config', 'lhy', '--cache',
+     'lfuopt', '--nepoch', '1', '--val'],
     ['bin/heturun', '-w', '2', sys.executable, 'examples/runner/run_mlp.py', '--comm-mode', 'AllReduce',
      '--steps', '5'],
 ]

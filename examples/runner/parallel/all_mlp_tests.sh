@@ -13,4 +13,6 @@ $R -w 4 python $S --mode pp --schedule pipedream
 $R -w 4 python $S --mode dp_pp --replicas 2 --schedule gpipe
 for s in left right middle; do $R -w 2 python $S --mode mp --split $s; done
 $R -w 4 python complex_pipeline_mlp.py
+$R -w 2 -s 1 python $S --mode pp --schedule hetpipe
+$R -w 4 -s 1 python $S --mode dp_pp --replicas 2 --schedule hetpipe
 python validate_results.py

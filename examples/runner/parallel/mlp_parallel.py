@@ -110,7 +110,8 @@ def main(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--mode', default='base', choices=['base', 'pp', 'mp', 'dp_pp'])
     p.add_argument('--split', default='middle', choices=sorted(SPLITS))
-    p.add_argument('--schedule', default='gpipe', choices=['gpipe', 'pipedream'])
+    p.add_argument('--schedule', default='gpipe', choices=['gpipe', 'pipedream', 'hetpipe'],
+                   help='hetpipe: 1F1B with each stage\'s weights synced through the PS (heturun -s 1)')
     p.add_argument('--micro-batches', type=int, default=4)
     p.add_argument('--replicas', type=int, default=2)
     p.add_argument('--batch-size', type=int, default=64)
@@ -130,7 +131,9 @@ def main(argv=None):
         M = a.micro_batches
         rep = a.replicas if a.mode == 'dp_pp' else 1
         train.optimizer.learning_rate = a.lr / (M * rep)
-        ex = ht.Executor({'train': [loss, train]}, pipeline=a.schedule)
+        # HetPipe in BSP mode (bsp=0): replicas push, barrier, pull -> same weights everywhere
+        kw = {'comm_mode': 'PS', 'bsp': 0} if a.schedule == 'hetpipe' else {}
+        ex = ht.Executor({'train': [loss, train]}, pipeline=a.schedule, **kw)
         r = ex.subexecutor['train'].replica
         n = a.batch_size // rep
         sl = slice(r * n, (r + 1) * n)

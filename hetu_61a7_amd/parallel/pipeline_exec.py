@@ -233,14 +233,16 @@ class PipelineSubExecutor(object):
         op.bucket_bytes = int(getattr(self.config, 'bucket_mb', 32) * (1 << 20))
         op.ps_dense = None
         op.ps_dense_wanted = False
-        if self.nreplica > 1:
+        # HetPipe: the PS aggregates the replicas' gradients, so no replica all-reduce
+        ps_sync = self.kind == 'hetpipe' and self.config.ps_comm is not None
+        if self.nreplica > 1 and not ps_sync:
             op.comm = self.replica_comms[self.stage]
             op.dp = True
         op.setup(self.config, list(range(len(local))))
         self.opt = op
-        if self.kind == 'hetpipe' and self.config.ps_comm is not None:
+        if ps_sync:
             from ..ps.table import PSDense
-            op.ps_dense = PSDense(op.flat, (1 << 21) + self.stage, self.config)
+            op.ps_dense = PSDense(op.flat, (1 << 21) + self.stage, self.config, publish=self.replica == 0)
 
     # ---------------------------------------------------------------------------------------
     def _compute(self, nodes, vals, aux):

@@ -232,15 +232,18 @@ class PSTable(object):
 class PSDense(object):
     """Flat dense parameters held by the PS (pure PS mode)."""
 
-    def __init__(self, flat, key, config):
+    def __init__(self, flat, key, config, publish=None):
         self.flat = flat
         self.key = key
         self.agent = psw.get_agent()
         self.bsp = config.bsp
         n = flat.numel
         self.agent.InitTensor(key, PARAM_DENSE, n, 1, 0, 0.0, 0.0, 0)
-        # worker 0 publishes its initial values; everyone starts from them
-        if self.agent.rank() == 0:
+        # one worker publishes its initial values (worker 0 by default; a
+        # pipeline stage's first replica for a per-stage key); everyone starts from them
+        if publish is None:
+            publish = self.agent.rank() == 0
+        if publish:
             host = flat.param.detach().float().cpu().contiguous()
             t = self.agent.Push(key, host)
             self.agent.WaitTicket(t)

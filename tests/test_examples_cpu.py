@@ -55,8 +55,9 @@ def test_example_runs(cmd):
 
 def test_parallel_equivalence_examples(tmp_path):
     """examples/runner/parallel: pipeline (GPipe, 1F1B), data+pipeline, a
-    model-parallel split and the hand-wired send/recv pipeline
-    (complex_pipeline_mlp) reproduce the single-process losses
+    model-parallel split, the hand-wired send/recv pipeline (complex_pipeline_mlp,
+    SURVEY §2.3 S9) and HetPipe with replicated stages synced through the PS
+    (S8) reproduce the single-process losses
     (validate_results)."""
     import subprocess
     d = os.path.join(ROOT, 'examples', 'runner', 'parallel')
@@ -69,14 +70,16 @@ def test_parallel_equivalence_examples(tmp_path):
             heturun + ['-w', '3', sys.executable, script, '--mode', 'pp', '--schedule', 'pipedream'],
             heturun + ['-w', '4', sys.executable, script, '--mode', 'dp_pp', '--replicas', '2'],
             heturun + ['-w', '2', sys.executable, script, '--mode', 'mp', '--split', 'right'],
-            heturun + ['-w', '3', sys.executable, os.path.join(d, 'complex_pipeline_mlp.py')]]
+            heturun + ['-w', '3', sys.executable, os.path.join(d, 'complex_pipeline_mlp.py')],
+            heturun + ['-w', '4', '-s', '1', sys.executable, script, '--mode', 'dp_pp', '--replicas', '2',
+                       '--schedule', 'hetpipe']]
     for cmd in runs:
         r = subprocess.run(cmd + ['--out', out, '--steps', '3'], env=env, cwd=ROOT, capture_output=True,
                            text=True, timeout=240)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     r = subprocess.run([sys.executable, os.path.join(d, 'validate_results.py'), out], capture_output=True,
                        text=True, timeout=60)
-    assert r.returncode == 0 and r.stdout.count(' ok') == 5, r.stdout
+    assert r.returncode == 0 and r.stdout.count(' ok') == 6, r.stdout
 
 
 def test_glue_finetune_learns():

@@ -75,12 +75,17 @@ __global__ void __launch_bounds__(256) bn_stats_partial(const T* __restrict__ x,
   for (int i = 0; i < V; ++i) { s[i] = 0.f; q[i] = 0.f; }
   if (active) {
     int64_t r = r0 + rsub;
-    for (; r + RP < r1; r += 2 * RP) {   // two rows in flight
-      float v[V], w[V];
-      load_vec<T>(x + r * C + (int64_t)vc * V, v);
-      load_vec<T>(x + (r + RP) * C + (int64_t)vc * V, w);
+    // four rows in flight: a read-only stream needs more bytes outstanding per
+    // lane than the two-tensor backward partial; the small 14x14 / 7x7 layers
+    // are bound by this latency chain (>= 16 row passes per thread)
+    for (; r + 3 * RP < r1; r += 4 * RP) {
+      float v[4][V];
 #pragma unroll
-      for (int i = 0; i < V; ++i) { s[i] += v[i] + w[i]; q[i] += v[i] * v[i] + w[i] * w[i]; }
+      for (int u = 0; u < 4; ++u) load_vec<T>(x + (r + u * RP) * C + (int64_t)vc * V, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < V; ++i) { s[i] += v[u][i]; q[i] += v[u][i] * v[u][i]; }
     }
     for (; r < r1; r += RP) {
       float v[V];
@@ -236,7 +241,7 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
                                                  int64_t nvec, int C, uint8_t* __restrict__ mask) {
   // channel-stationary threads: the grid stride is a multiple of C/V, so every
   // thread keeps one channel group's folded affine in registers (no per-element
-  // parameter loads, no 64-bit modulo) and streams 2 vectors per iteration
+  // parameter loads, no 64-bit modulo) and streams U vectors per iteration
   constexpr int V = Vec<T>::N;
   const int cv = C / V;
   const int64_t nth = (int64_t)gridDim.x * blockDim.x;
@@ -247,25 +252,31 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
   float a[V], bb[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) { a[k] = fa[c0 + k]; bb[k] = fb[c0 + k]; }
+  // U vectors in flight per lane: 4 without a residual stream, 2 with one (4 loads either way)
+  constexpr int U = RES ? 2 : 4;
   int64_t i = tid;
-  for (; i + stride < nvec; i += 2 * stride) {
-    float v[V], w[V], r[V], r2[V];
-    load_vec<T>(x + i * V, v);
-    load_vec<T>(x + (i + stride) * V, w);
-    if (RES) { load_vec<T>(res + i * V, r); load_vec<T>(res + (i + stride) * V, r2); }
+  for (; i + (U - 1) * stride < nvec; i += U * stride) {
+    float v[U][V], r[U][V];
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      float o = v[k] * a[k] + bb[k], o2 = w[k] * a[k] + bb[k];
-      if (RES) { o += r[k]; o2 += r2[k]; }
-      if (RELU) { o = fmaxf(o, 0.f); o2 = fmaxf(o2, 0.f); }
-      v[k] = o;
-      w[k] = o2;
+    for (int u = 0; u < U; ++u) load_vec<T>(x + (i + u * stride) * V, v[u]);
+    if (RES) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_vec<T>(res + (i + u * stride) * V, r[u]);
     }
-    store_vec<T>(y + i * V, v);
-    store_vec<T>(y + (i + stride) * V, w);
-    if (MASK) { mask[i] = relu_bits<V>(v); mask[i + stride] = relu_bits<V>(w); }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        float o = v[u][k] * a[k] + bb[k];
+        if (RES) o += r[u][k];
+        if (RELU) o = fmaxf(o, 0.f);
+        v[u][k] = o;
+      }
+      store_vec<T>(y + (i + u * stride) * V, v[u]);
+      if (MASK) mask[i + u * stride] = relu_bits<V>(v[u]);
+    }
   }
-  if (i < nvec) {
+  for (; i < nvec; i += stride) {
     float v[V], r[V];
     load_vec<T>(x + i * V, v);
     if (RES) load_vec<T>(res + i * V, r);
@@ -316,7 +327,7 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
       mu[i] = mean[vc * V + i]; is[i] = invstd[vc * V + i];
       if (RELU == 2) { ka[i] = fscale[vc * V + i] * is[i]; kb[i] = fbias[vc * V + i] - mu[i] * ka[i]; }
     }
-    // two rows in flight per iteration (all loads issued before any use)
+    // two rows (four vectors) in flight per iteration (all loads issued before any use)
     int64_t r = r0 + rsub;
     for (; r + RP < r1; r += 2 * RP) {
       const int64_t off = r * C + (int64_t)vc * V, off2 = off + (int64_t)RP * C;

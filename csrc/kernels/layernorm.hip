@@ -222,13 +222,16 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
                                                   T* __restrict__ dx_drop, float* __restrict__ pg,
                                                   float* __restrict__ pb, int64_t R, int N, int rpb, float keep,
                                                   uint64_t seed, float* __restrict__ zero_a,
-                                                  float* __restrict__ zero_b) {
+                                                  float* __restrict__ zero_b, float* __restrict__ pd,
+                                                  float* __restrict__ zero_d) {
   extern __shared__ float lds[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nc = N >> 2;
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
-  float gm[CPL][4], ag[CPL][4], ab[CPL][4];
+  // ad: column sums of the x-gradient (after the dropout mask) -- the bias
+  // gradient of the linear layer that produced x, when pd != nullptr
+  float gm[CPL][4], ag[CPL][4], ab[CPL][4], ad[CPL][4];
 #pragma unroll
   for (int i = 0; i < CPL; ++i) {
     const int c = lane + 64 * i;
@@ -240,10 +243,14 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
       for (int k = 0; k < 4; ++k) gm[i][k] = 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { ag[i][k] = 0.f; ab[i][k] = 0.f; }
+    for (int k = 0; k < 4; ++k) { ag[i][k] = 0.f; ab[i][k] = 0.f; ad[i][k] = 0.f; }
   }
   if (zero_a != nullptr && blockIdx.x == 0)   // col_reduce2_k accumulates its row slices into these
-    for (int j = threadIdx.x; j < N; j += 256) { zero_a[j] = 0.f; zero_b[j] = 0.f; }
+    for (int j = threadIdx.x; j < N; j += 256) {
+      zero_a[j] = 0.f;
+      zero_b[j] = 0.f;
+      if (zero_d != nullptr) zero_d[j] = 0.f;
+    }
   // software-pipelined over this wave's rows: the next row's loads are in flight
   // while the current row is reduced and written
   float d[CPL][4], xh[CPL][4];
@@ -293,6 +300,10 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
           drop4(o, seed, (uint64_t)(base >> 2) + c, keep);
           IO4<T>::store(dx_drop + base + 4 * c, o);
         }
+        if (pd != nullptr) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ad[i][k] += o[k];
+        }
       }
     }
 #pragma unroll
@@ -300,67 +311,73 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
 #pragma unroll
       for (int k = 0; k < 4; ++k) { d[i][k] = dn[i][k]; xh[i][k] = xn[i][k]; }
   }
-  // fold the 4 waves' partials (dgamma, then dbeta) through LDS
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+  // fold the 4 waves' partials (dgamma, dbeta, then the x-gradient column sums) through LDS
+  const int npass = pd != nullptr ? 3 : 2;
+  for (int pass = 0; pass < npass; ++pass) {
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
       const int c = lane + 64 * i;
       if (c < nc) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) lds[w * N + 4 * c + k] = pass == 0 ? ag[i][k] : ab[i][k];
+        for (int k = 0; k < 4; ++k) lds[w * N + 4 * c + k] = pass == 0 ? ag[i][k] : (pass == 1 ? ab[i][k] : ad[i][k]);
       }
     }
     __syncthreads();
-    float* out = (pass == 0 ? pg : pb) + (int64_t)blockIdx.x * N;
+    float* out = (pass == 0 ? pg : (pass == 1 ? pb : pd)) + (int64_t)blockIdx.x * N;
     for (int j = threadIdx.x; j < N; j += 256) out[j] = lds[j] + lds[N + j] + lds[2 * N + j] + lds[3 * N + j];
     __syncthreads();
   }
 }
 
-// oa[j] = sum_r pa[r, j], ob[j] = sum_r pb[r, j]: 64 columns x 4 row groups per block.
+// oa[j] = sum_r pa[r, j], ob[j] = sum_r pb[r, j] (and oc[j] = sum_r pc[r, j] when pc
+// is given; pb may be null): 64 columns x 4 row groups per block.
 // gridDim.y > 1 splits the rows into slices whose sums are atomically added into
-// oa / ob (zeroed beforehand by the producer kernel): the few hundred partial rows
-// are otherwise reduced by only N/64 blocks, latency-bound.  gridDim.y == 1 stores
-// (fixed summation order: deterministic mode).
+// oa / ob / oc (zeroed beforehand by the producer kernel): the few hundred partial
+// rows are otherwise reduced by only N/64 blocks, latency-bound.  gridDim.y == 1
+// stores (fixed summation order: deterministic mode).
 __global__ void __launch_bounds__(256) col_reduce2_k(const float* __restrict__ pa, const float* __restrict__ pb,
                                                       float* __restrict__ oa, float* __restrict__ ob, int rows,
-                                                      int N) {
-  __shared__ float sa[4][64], sb[4][64];
+                                                      int N, const float* __restrict__ pc = nullptr,
+                                                      float* __restrict__ oc = nullptr) {
+  __shared__ float sm[3][4][64];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
   const int per = (rows + (int)gridDim.y - 1) / (int)gridDim.y;
   const int rlo = (int)blockIdx.y * per;
   const int rhi = rlo + per < rows ? rlo + per : rows;
-  float a = 0.f, b = 0.f;
+  const float* src[3] = {pa, pb, pc};
+  float* dst[3] = {oa, ob, oc};
+  // all arrays in one loop, 4 rows each in flight (null arrays are skipped uniformly)
+  float t[3][4];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[a][u] = 0.f;
   if (col < N) {
-    float a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f, a3 = 0.f, b3 = 0.f;   // 4 loads in flight
     int r = rlo + grp;
     for (; r + 12 < rhi; r += 16) {
-      a += pa[(int64_t)r * N + col];        b += pb[(int64_t)r * N + col];
-      a1 += pa[(int64_t)(r + 4) * N + col]; b1 += pb[(int64_t)(r + 4) * N + col];
-      a2 += pa[(int64_t)(r + 8) * N + col]; b2 += pb[(int64_t)(r + 8) * N + col];
-      a3 += pa[(int64_t)(r + 12) * N + col]; b3 += pb[(int64_t)(r + 12) * N + col];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        if (src[a] == nullptr) continue;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[a][u] += src[a][(int64_t)(r + 4 * u) * N + col];
+      }
     }
     for (; r < rhi; r += 4) {
-      a += pa[(int64_t)r * N + col];
-      b += pb[(int64_t)r * N + col];
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+        if (src[a] != nullptr) t[a][0] += src[a][(int64_t)r * N + col];
     }
-    a += a1 + a2 + a3;
-    b += b1 + b2 + b3;
   }
-  sa[grp][lane] = a;
-  sb[grp][lane] = b;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) sm[a][grp][lane] = t[a][0] + t[a][1] + t[a][2] + t[a][3];
   __syncthreads();
   if (grp == 0 && col < N) {
-    const float ta = sa[0][lane] + sa[1][lane] + sa[2][lane] + sa[3][lane];
-    const float tb = sb[0][lane] + sb[1][lane] + sb[2][lane] + sb[3][lane];
-    if (gridDim.y == 1) {
-      oa[col] = ta;
-      ob[col] = tb;
-    } else {
-      unsafeAtomicAdd(oa + col, ta);
-      unsafeAtomicAdd(ob + col, tb);
+    for (int a = 0; a < 3; ++a) {
+      if (src[a] == nullptr) continue;
+      const float t = sm[a][0][lane] + sm[a][1][lane] + sm[a][2][lane] + sm[a][3][lane];
+      if (gridDim.y == 1) dst[a][col] = t;
+      else unsafeAtomicAdd(dst[a] + col, t);
     }
   }
 }
@@ -376,10 +393,10 @@ static void launch_fwd4(const void* x, const void* res, const float* g, const fl
 template <typename T, int CPL>
 static void launch_bwd4(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
                         void* dsum, void* dxd, float* pg, float* pb, int64_t R, int N, int nblk, int rpb,
-                        float keep, uint64_t seed, float* za, float* zb, hipStream_t st) {
+                        float keep, uint64_t seed, float* za, float* zb, float* pd, float* zd, hipStream_t st) {
   hipLaunchKernelGGL((ln_bwd4_k<T, CPL>), dim3((unsigned)nblk), dim3(256), 4 * N * sizeof(float), st,
                      (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed,
-                     za, zb);
+                     za, zb, pd, zd);
 }
 
 #define HETU_CPL_DISPATCH(CPL_NEEDED, FN, ...)                 \
@@ -406,14 +423,14 @@ template <int CPL> static void fwd4_f32(const void* x, const void* res, const fl
 template <int CPL> static void bwd4_bf16(const void* dy, const void* xs, const float* g, const float* m,
                                          const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
                                          int N, int nblk, int rpb, float keep, uint64_t seed, float* za,
-                                         float* zb, hipStream_t st) {
-  launch_bwd4<bf16, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, st);
+                                         float* zb, float* pd, float* zd, hipStream_t st) {
+  launch_bwd4<bf16, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, pd, zd, st);
 }
 template <int CPL> static void bwd4_f32(const void* dy, const void* xs, const float* g, const float* m,
                                         const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
                                         int N, int nblk, int rpb, float keep, uint64_t seed, float* za,
-                                        float* zb, hipStream_t st) {
-  launch_bwd4<float, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, st);
+                                        float* zb, float* pd, float* zd, hipStream_t st) {
+  launch_bwd4<float, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, pd, zd, st);
 }
 
 }  // namespace hetu
@@ -439,7 +456,8 @@ HETU_API int hetu_layernorm_bwd(const void* dy, const void* x, const float* g, c
   float* wb = ws + (int64_t)nwaves * N;
   if (is_bf16) hipLaunchKernelGGL(ln_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, g, mean, rstd, (bf16*)dx, wg, wb, R, N, nwaves);
   else hipLaunchKernelGGL(ln_bwd_k<float>, grid, dim3(256), 0, st, (const float*)dy, (const float*)x, g, mean, rstd, (float*)dx, wg, wb, R, N, nwaves);
-  hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, wg, wb, dg, db, nwaves, N);
+  hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, st, wg, wb, dg, db, nwaves, N,
+                     (const float*)nullptr, (float*)nullptr);
   HETU_LAUNCH_CHECK();
   return 0;
 }
@@ -472,21 +490,34 @@ HETU_API int hetu_ln_fused_fwd(const void* x, const void* res, const float* g, c
 // through the dropout) may each be null.  ws: 2 * nblk * N floats.
 // deterministic != 0: the dgamma/dbeta partial rows are summed in a fixed order
 // (one block per 64 columns) instead of by row slices with fp32 atomics.
-HETU_API int hetu_ln_fused_bwd(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
-                               void* dsum, void* dx_drop, float* dg, float* db, float* ws, int64_t R, int N,
-                               int nblk, float keep, int64_t seed, int is_bf16, int deterministic, hipStream_t st) {
+// dlin (may be null): also the column sums of the x-gradient (dx_drop, or dsum
+// without dropout) -- the bias gradient of the linear layer that produced x --
+// from the same row pass.  ws: (2 + (dlin != null)) * nblk * N floats.
+HETU_API int hetu_ln_fused_bwd2(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
+                                void* dsum, void* dx_drop, float* dg, float* db, float* dlin, float* ws, int64_t R,
+                                int N, int nblk, float keep, int64_t seed, int is_bf16, int deterministic,
+                                hipStream_t st) {
   if ((N & 3) || N > 2048 || R <= 0 || nblk <= 0) return (int)hipErrorInvalidValue;
   const int cpl = (N / 4 + 63) / 64;
   const int rpb = (int)((R + nblk - 1) / nblk);
   float* pg = ws;
   float* pb = ws + (int64_t)nblk * N;
+  float* pd = dlin != nullptr ? ws + 2 * (int64_t)nblk * N : nullptr;
   const int slices = deterministic ? 1 : (nblk >= 256 ? 8 : (nblk >= 64 ? 4 : 1));
   float* za = slices > 1 ? dg : nullptr;
   float* zb = slices > 1 ? db : nullptr;
-  if (is_bf16) HETU_CPL_DISPATCH(cpl, bwd4_bf16, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, st);
-  else HETU_CPL_DISPATCH(cpl, bwd4_f32, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, st);
+  float* zd = slices > 1 ? dlin : nullptr;
+  if (is_bf16) HETU_CPL_DISPATCH(cpl, bwd4_bf16, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, pd, zd, st);
+  else HETU_CPL_DISPATCH(cpl, bwd4_f32, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, pd, zd, st);
   hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64), (unsigned)slices), dim3(256), 0, st, pg, pb, dg,
-                     db, nblk, N);
+                     db, nblk, N, (const float*)pd, dlin);
   HETU_LAUNCH_CHECK();
   return 0;
+}
+
+HETU_API int hetu_ln_fused_bwd(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
+                               void* dsum, void* dx_drop, float* dg, float* db, float* ws, int64_t R, int N,
+                               int nblk, float keep, int64_t seed, int is_bf16, int deterministic, hipStream_t st) {
+  return hetu_ln_fused_bwd2(dy, xs, g, mean, rstd, dsum, dx_drop, dg, db, nullptr, ws, R, N, nblk, keep, seed,
+                            is_bf16, deterministic, st);
 }

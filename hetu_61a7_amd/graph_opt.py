@@ -17,6 +17,9 @@ Backward (``fuse_backward``, run on the gradient graph):
                                      (the residual-branch gradient join of ResNet)
   sum(matmul(g, w^T), r, ...)     -> matmul with r added in the GEMM epilogue
                                      (beta = 1; the transformer residual-stream join)
+  reduce_sum_axis0(d x) where x feeds a fused dropout+add+LayerNorm
+                                  -> the LayerNorm backward kernel emits that bias
+                                     gradient of the producing linear layer
 """
 from __future__ import annotations
 
@@ -111,12 +114,31 @@ def fuse_backward(roots):
     """Fold gradient fan-in sums into the data-gradient GEMM epilogue."""
     if os.environ.get('HETU_FUSE', '1') == '0':
         return 0
-    from .ops.reduce import SumOp
-    from .ops.nn import Conv2d_Gradient_of_DataOp
+    from .ops.reduce import SumOp, ReduceSumAxisZeroOp
+    from .ops.nn import Conv2d_Gradient_of_DataOp, DropoutAddLayerNormGradientOp, BNGradSelectOp
     from .ops.linalg import MatMulOp
     topo, cons = _consumers(roots)
     root_set = set(roots)
     fused = 0
+    # linear bias gradient = row sum of the x-gradient of a fused dropout+add+LayerNorm:
+    # the LayerNorm backward kernel sums it in its own row pass (no reduction over dx)
+    for n in topo:
+        if type(n) is not ReduceSumAxisZeroOp or len(n.inputs) != 1:
+            continue
+        s = n.inputs[0]
+        if type(s) is BNGradSelectOp and s.index == 0 and \
+                type(s.inputs[0]) is DropoutAddLayerNormGradientOp and not s.inputs[0].emit_lin_bias:
+            gn = s.inputs[0]
+            gn.emit_lin_bias = True
+            keep_id, keep_name, bw = n.id, n.name, getattr(n, 'bw_of', None)
+            n.__class__ = BNGradSelectOp
+            n.inputs = [gn]
+            n.index = 4
+            n.op_type = 'DropoutAddLayerNorm_Gradient_of_LinearBiasOp'
+            n.id, n.name = keep_id, keep_name
+            if bw is not None:
+                n.bw_of = bw
+            fused += 1
     for n in topo:
         if not isinstance(n, SumOp) or len(n.inputs) < 2 or getattr(n, 'sparse', False):
             continue

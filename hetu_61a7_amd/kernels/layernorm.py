@@ -105,10 +105,12 @@ def layer_norm_fused(x, residual, gamma, beta, eps, keep=1.0, seed=0):
 
 
 def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_ds=True, need_dx=True,
-                              dg_out=None, db_out=None):
+                              dg_out=None, db_out=None, want_dlin=False, dlin_out=None):
     """Backward of ``layer_norm_fused``: (ds, dx, dgamma, dbeta) with ds the grad
     of the normalised input (= grad of the residual) and dx = dropout-mask(ds)
-    the grad of ``x`` (None when not requested)."""
+    the grad of ``x`` (None when not requested).  ``want_dlin`` appends the
+    column sums of dx over all rows -- the bias gradient of the linear layer that
+    produced x -- computed in the same row pass (into ``dlin_out`` when given)."""
     N = s.shape[-1]
     R = s.numel() // N
     if _fused_ok(s) and dy.dtype == s.dtype:
@@ -118,20 +120,28 @@ def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_d
         if need_dx and keep >= 1.0 and not need_ds:
             ds = torch.empty_like(sc)
         nblk = max(1, min(512, (R + 7) // 8))
-        ws = torch.empty(2 * nblk * N, dtype=torch.float32, device=s.device)
+        ws = torch.empty((3 if want_dlin else 2) * nblk * N, dtype=torch.float32, device=s.device)
         dg, db = _dest(dg_out, N, s.device), _dest(db_out, N, s.device)
+        dlin = _dest(dlin_out, N, s.device) if want_dlin else None
         from . import deterministic
-        f = fn('hetu_ln_fused_bwd', [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, I32, P])
+        f = fn('hetu_ln_fused_bwd2', [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, I32, P])
         check(f(dyc.data_ptr(), sc.data_ptr(), gamma.float().contiguous().data_ptr(), mean.data_ptr(),
                 rstd.data_ptr(), ds.data_ptr() if ds is not None else None,
-                dx.data_ptr() if dx is not None else None, dg.data_ptr(), db.data_ptr(), ws.data_ptr(), R, N, nblk,
+                dx.data_ptr() if dx is not None else None, dg.data_ptr(), db.data_ptr(),
+                dlin.data_ptr() if dlin is not None else None, ws.data_ptr(), R, N, nblk,
                 float(keep), int(seed), is_bf16(s), int(deterministic()), stream_ptr()), 'ln_fused_bwd')
         if need_dx and keep >= 1.0:
             dx = ds
-        return ds, dx, dg, db
+        return (ds, dx, dg, db, dlin) if want_dlin else (ds, dx, dg, db)
     ds, dg, db = layer_norm_backward(dy, s, gamma, mean, rstd)
     dx = None
-    if need_dx:
+    if need_dx or want_dlin:
         from . import dropout as KD
         dx = ds if keep >= 1.0 else KD.dropout(ds, keep, seed)
+    if want_dlin:
+        dlin = dx.reshape(-1, N).float().sum(0)
+        if dlin_out is not None:
+            dlin_out.view(-1).copy_(dlin)
+            dlin = dlin_out
+        return ds, dx, dg, db, dlin
     return ds, dx, dg, db

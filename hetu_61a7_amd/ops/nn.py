@@ -530,8 +530,13 @@ class DropoutAddLayerNormOp(Op):
 
 
 class DropoutAddLayerNormGradientOp(Op):
+    """Outputs (dx, dresidual, dscale, dbias[, dlinear_bias]).  ``emit_lin_bias``
+    (set by graph_opt.fuse_backward when x comes from a linear layer whose bias
+    gradient is the row sum of dx) adds output 4: that bias gradient, summed in the
+    same kernel pass instead of a separate reduction over dx."""
     aux_inputs = (1,)
-    grad_dest_slots = (2, 3)
+    grad_dest_slots = (2, 3, 4)
+    emit_lin_bias = False
 
     def __init__(self, out_gradient, forward_node, ctx=None):
         super().__init__(DropoutAddLayerNormGradientOp, [out_gradient, forward_node, forward_node.inputs[-2]], ctx)
@@ -541,9 +546,24 @@ class DropoutAddLayerNormGradientOp(Op):
         if dy.dtype != sm.dtype:
             dy = dy.to(sm.dtype)
         dests = getattr(self, 'grad_dests', {})
-        ds, dx, dg, db = KLN.layer_norm_fused_backward(dy, sm, g, mean, rstd, keep, seed,
-                                                       dg_out=dests.get(2), db_out=dests.get(3))
-        return (dx, ds, dg, db)
+        if not self.emit_lin_bias:
+            ds, dx, dg, db = KLN.layer_norm_fused_backward(dy, sm, g, mean, rstd, keep, seed,
+                                                           dg_out=dests.get(2), db_out=dests.get(3))
+            return (dx, ds, dg, db)
+        if sm.dim() == 2:
+            ds, dx, dg, db, dl = KLN.layer_norm_fused_backward(dy, sm, g, mean, rstd, keep, seed,
+                                                               dg_out=dests.get(2), db_out=dests.get(3),
+                                                               want_dlin=True, dlin_out=dests.get(4))
+        else:   # the replaced node summed over axis 0 only
+            from ..kernels import reduce as KR
+            ds, dx, dg, db = KLN.layer_norm_fused_backward(dy, sm, g, mean, rstd, keep, seed,
+                                                           dg_out=dests.get(2), db_out=dests.get(3))
+            dl = KR.reduce_mid(dx.contiguous().reshape(1, dx.shape[0], -1)).reshape(dx.shape[1:])
+            d = dests.get(4)
+            if d is not None and d.numel() == dl.numel():
+                d.view(dl.shape).copy_(dl)
+                dl = d.view(dl.shape)
+        return (dx, ds, dg, db, dl)
 
     def gradient(self, output_grad):
         raise NotImplementedError

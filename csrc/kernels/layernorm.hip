@@ -382,6 +382,83 @@ __global__ void __launch_bounds__(256) col_reduce2_k(const float* __restrict__ p
   }
 }
 
+// g = dy * gelu'(pre) (erf form) for a [R, N] activation, plus the column sums
+// of g: the bias gradient of the linear layer whose output went through the
+// GELU (transformer FFN1).  Geometry as the BatchNorm partial kernels: a block
+// covers W vector-columns x RP rows per pass over its chunk of rows; each block
+// writes one partial row part[blockIdx.x][N] (reduced by col_reduce2_k).  Blocks
+// with blockIdx.x == 0 zero ``zero_out`` for the atomic row-slice reduce.
+__device__ __forceinline__ float gelu_erf_grad_f(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118f));
+  const float pdf = 0.39894228040f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gelu_grad_colsum_k(const T* __restrict__ pre, const T* __restrict__ dy,
+                                                           T* __restrict__ g, int64_t R, int N, int W, int RP,
+                                                           int64_t rows_per_chunk, float* __restrict__ part,
+                                                           float* __restrict__ zero_out) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float sh[256 * V];
+  const int t = threadIdx.x;
+  const int col = t % W, rsub = t / W;
+  const int vc = blockIdx.y * W + col;
+  const bool active = (rsub < RP) && (vc * V < N);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > R) r1 = R;
+  if (zero_out != nullptr && blockIdx.x == 0 && rsub == 0 && vc * V < N) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) zero_out[vc * V + k] = 0.f;
+  }
+  float s[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) s[k] = 0.f;
+  if (active) {
+    int64_t r = r0 + rsub;
+    for (; r + RP < r1; r += 2 * RP) {   // two rows (four vectors) in flight
+      const int64_t o1 = r * N + (int64_t)vc * V, o2 = o1 + (int64_t)RP * N;
+      float a1[V], b1[V], a2[V], b2[V];
+      load_vec<T>(pre + o1, a1);
+      load_vec<T>(dy + o1, b1);
+      load_vec<T>(pre + o2, a2);
+      load_vec<T>(dy + o2, b2);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        b1[k] *= gelu_erf_grad_f(a1[k]);
+        b2[k] *= gelu_erf_grad_f(a2[k]);
+        s[k] += b1[k] + b2[k];
+      }
+      store_vec<T>(g + o1, b1);
+      store_vec<T>(g + o2, b2);
+    }
+    for (; r < r1; r += RP) {
+      const int64_t o1 = r * N + (int64_t)vc * V;
+      float a1[V], b1[V];
+      load_vec<T>(pre + o1, a1);
+      load_vec<T>(dy + o1, b1);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        b1[k] *= gelu_erf_grad_f(a1[k]);
+        s[k] += b1[k];
+      }
+      store_vec<T>(g + o1, b1);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) sh[t * V + k] = s[k];
+  __syncthreads();
+  const int nch = W * V;
+  for (int c_local = t; c_local < nch; c_local += 256) {
+    const int colw = c_local / V, lane_i = c_local % V;
+    float S = 0.f;
+    for (int rr = 0; rr < RP; ++rr) S += sh[(rr * W + colw) * V + lane_i];
+    const int c = blockIdx.y * W * V + c_local;
+    if (c < N) part[(int64_t)blockIdx.x * N + c] = S;
+  }
+}
+
 template <typename T, int CPL>
 static void launch_fwd4(const void* x, const void* res, const float* g, const float* b, void* y, void* sum_out,
                         float* mean, float* rstd, int64_t R, int N, float eps, float keep, uint64_t seed,
@@ -520,4 +597,30 @@ HETU_API int hetu_ln_fused_bwd(const void* dy, const void* xs, const float* g, c
                                int nblk, float keep, int64_t seed, int is_bf16, int deterministic, hipStream_t st) {
   return hetu_ln_fused_bwd2(dy, xs, g, mean, rstd, dsum, dx_drop, dg, db, nullptr, ws, R, N, nblk, keep, seed,
                             is_bf16, deterministic, st);
+}
+
+// g = dy * gelu'(pre) and out[N] = column sums of g (the FFN1 bias gradient).
+// Requires N % (16 / sizeof(T)) == 0 and 16-byte aligned rows; ``chunks`` partial
+// rows in ws (chunks * N floats).
+HETU_API int hetu_gelu_grad_colsum(const void* pre, const void* dy, void* g, float* out, float* ws, int64_t R,
+                                   int N, int chunks, int is_bf16, int deterministic, hipStream_t st) {
+  const int V = is_bf16 ? 8 : 4;
+  if (N % V || R <= 0 || chunks <= 0) return (int)hipErrorInvalidValue;
+  const int cv = N / V;
+  const int W = cv < 64 ? cv : 64;
+  const int RP = 256 / W;
+  const int tiles = (cv + W - 1) / W;
+  const int64_t rpc = (R + chunks - 1) / chunks;
+  const int slices = deterministic ? 1 : (chunks >= 256 ? 8 : (chunks >= 64 ? 4 : 1));
+  float* zo = slices > 1 ? out : nullptr;
+  if (is_bf16)
+    hipLaunchKernelGGL(gelu_grad_colsum_k<bf16>, dim3((unsigned)chunks, (unsigned)tiles), dim3(256), 0, st,
+                       (const bf16*)pre, (const bf16*)dy, (bf16*)g, R, N, W, RP, rpc, ws, zo);
+  else
+    hipLaunchKernelGGL(gelu_grad_colsum_k<float>, dim3((unsigned)chunks, (unsigned)tiles), dim3(256), 0, st,
+                       (const float*)pre, (const float*)dy, (float*)g, R, N, W, RP, rpc, ws, zo);
+  hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64), (unsigned)slices), dim3(256), 0, st, ws,
+                     (const float*)nullptr, out, (float*)nullptr, chunks, N, (const float*)nullptr, (float*)nullptr);
+  HETU_LAUNCH_CHECK();
+  return 0;
 }

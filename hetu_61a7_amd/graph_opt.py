@@ -17,6 +17,8 @@ Backward (``fuse_backward``, run on the gradient graph):
                                      (the residual-branch gradient join of ResNet)
   sum(matmul(g, w^T), r, ...)     -> matmul with r added in the GEMM epilogue
                                      (beta = 1; the transformer residual-stream join)
+  reduce_sum_axis0(gelu_grad(...))  -> the GELU-gradient kernel also emits the
+                                     bias gradient (column sums) of the GELU linear
   reduce_sum_axis0(d x) where x feeds a fused dropout+add+LayerNorm
                                   -> the LayerNorm backward kernel emits that bias
                                      gradient of the producing linear layer
@@ -116,10 +118,25 @@ def fuse_backward(roots):
         return 0
     from .ops.reduce import SumOp, ReduceSumAxisZeroOp
     from .ops.nn import Conv2d_Gradient_of_DataOp, DropoutAddLayerNormGradientOp, BNGradSelectOp
-    from .ops.linalg import MatMulOp
+    from .ops.linalg import MatMulOp, LinearGeluGradOp, LinearGeluBiasGradOp
     topo, cons = _consumers(roots)
     root_set = set(roots)
     fused = 0
+    # bias gradient of a GELU linear layer = row sum of its GELU gradient: summed by
+    # the GELU-gradient kernel itself
+    for n in topo:
+        if type(n) is ReduceSumAxisZeroOp and len(n.inputs) == 1 and type(n.inputs[0]) is LinearGeluGradOp \
+                and not n.inputs[0].emit_colsum:
+            lg = n.inputs[0]
+            lg.emit_colsum = True
+            keep_id, keep_name, bw = n.id, n.name, getattr(n, 'bw_of', None)
+            n.__class__ = LinearGeluBiasGradOp
+            n.inputs = [lg]
+            n.op_type = 'LinearGeluBiasGradOp'
+            n.id, n.name = keep_id, keep_name
+            if bw is not None:
+                n.bw_of = bw
+            fused += 1
     # linear bias gradient = row sum of the x-gradient of a fused dropout+add+LayerNorm:
     # the LayerNorm backward kernel sums it in its own row pass (no reduction over dx)
     for n in topo:

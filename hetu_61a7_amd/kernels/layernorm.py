@@ -145,3 +145,39 @@ def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_d
             dlin = dlin_out
         return ds, dx, dg, db, dlin
     return ds, dx, dg, db
+
+
+def gelu_grad_colsum(pre, dy, out=None):
+    """(g, colsum) with g = dy * gelu'(pre) (erf form) and colsum = g summed over
+    rows -- the transformer FFN1 bias gradient -- from one pass over pre and dy
+    (``hetu_gelu_grad_colsum``).  ``out``: fp32 [N] destination (e.g. the
+    optimizer's flat gradient slot).  2-D inputs; other layouts take the generic
+    elementwise kernel + reduction."""
+    N = pre.shape[-1]
+    dt = pre.dtype
+    V = 8 if dt == torch.bfloat16 else 4
+    if not (pre.is_cuda and pre.dim() == 2 and dy.dtype == dt and dt in (torch.bfloat16, torch.float32)
+            and N % V == 0):
+        from .elementwise import binary
+        from . import reduce as KR
+        g = binary('gelu_grad', pre.contiguous(), dy.contiguous())
+        cs = KR.reduce_mid(g.reshape(1, g.shape[0], -1)).reshape(g.shape[1:])
+        if out is not None and out.numel() == cs.numel():
+            out.view(cs.shape).copy_(cs)
+            cs = out.view(cs.shape)
+        return g, cs
+    pre, dy = pre.contiguous(), dy.contiguous()
+    R = pre.shape[0]
+    g = torch.empty_like(pre)
+    cv = N // V
+    W = min(cv, 64)
+    RP = 256 // W
+    tiles = -(-cv // W)
+    chunks = max(1, min(max(1, 2048 // tiles), R // (RP * 4)))   # ~2048 blocks: 8 waves per CU
+    ws = torch.empty(chunks * N, dtype=torch.float32, device=pre.device)
+    cs = _dest(out, N, pre.device)
+    from . import deterministic
+    f = fn('hetu_gelu_grad_colsum', [P, P, P, P, P, I64, I32, I32, I32, I32, P])
+    check(f(pre.data_ptr(), dy.data_ptr(), g.data_ptr(), cs.data_ptr(), ws.data_ptr(), R, N, chunks,
+            is_bf16(pre), int(deterministic()), stream_ptr()), 'gelu_grad_colsum')
+    return g, cs

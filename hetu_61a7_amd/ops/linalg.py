@@ -121,8 +121,13 @@ class LinearOp(Op):
 
 
 class LinearGeluGradOp(Op):
-    """gelu'(pre) * grad with the pre-activation saved by the forward LinearOp."""
+    """gelu'(pre) * grad with the pre-activation saved by the forward LinearOp.
+    ``emit_colsum`` (graph_opt.fuse_backward): also the row sum of the result --
+    the layer's bias gradient -- from the same kernel pass, as the aux value read
+    by a LinearGeluBiasGradOp."""
     value_and_aux_inputs = (1,)
+    emit_colsum = False
+    colsum_dest = None
 
     def __init__(self, grad, fwd, ctx=None):
         super().__init__(LinearGeluGradOp, [grad, fwd], ctx)
@@ -130,6 +135,12 @@ class LinearGeluGradOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         from ..kernels.elementwise import binary
         g, (y, pre) = input_vals
+        if self.emit_colsum:
+            from ..kernels.layernorm import gelu_grad_colsum
+            if g.dtype != pre.dtype:
+                g = g.to(pre.dtype)
+            out, cs = gelu_grad_colsum(pre, g, out=self.colsum_dest)
+            return AuxResult(out, cs)
         return binary('gelu_grad', pre.contiguous(), g.contiguous())
 
     def gradient(self, output_grad):
@@ -137,6 +148,30 @@ class LinearGeluGradOp(Op):
 
     def infer_shape(self, input_shapes):
         return input_shapes[0]
+
+
+class LinearGeluBiasGradOp(Op):
+    """Bias gradient of a GELU linear layer, taken from its LinearGeluGradOp's
+    fused column sums (replaces ``reducesumaxiszero_op`` of the GELU gradient)."""
+    aux_inputs = (0,)
+
+    def __init__(self, gelu_grad, ctx=None):
+        super().__init__(LinearGeluBiasGradOp, [gelu_grad], ctx)
+
+    def set_grad_dest(self, dest):
+        if dest.dtype == torch.float32 and dest.is_contiguous():
+            self.inputs[0].colsum_dest = dest
+            return True
+        return False
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        return input_vals[0]
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return tuple(input_shapes[0][1:])
 
 
 def linear_op(node_A, node_B, bias, trans_A=False, trans_B=False, activation=None, ctx=None):

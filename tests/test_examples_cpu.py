@@ -84,14 +84,18 @@ def test_parallel_equivalence_examples(tmp_path):
 
 def test_glue_finetune_learns():
     """examples/nlp/bert/test_glue_hetu_bert.py: the sequence-classification head
-    fine-tunes (3-label MNLI-shaped batches whose label is marked in the tokens)."""
-    sys.path.insert(0, os.path.join(ROOT, 'examples', 'nlp', 'bert'))
-    import test_glue_hetu_bert as G
-    accs = G.main(['--gpu_id', '-1', '--hidden_size', '64', '--num_hidden_layers', '2', '-a', '2', '-s', '16',
-                   '--train_batch_size', '32', '--vocab_size', '1100', '-e', '6', '--batches', '20', '--lr', '1e-3',
-                   '--dropout_prob', '0', '--task_name', 'mnli'])
-    # initial weights follow seed + node id (reference semantics), so they depend on
-    # how many ops this process built before: 120 steps learn from any of them
+    fine-tunes (3-label MNLI-shaped batches whose label is marked in the tokens).
+    Runs in a fresh process: initial weights follow seed + node id (reference
+    semantics), so in a long-lived process they depend on the ops built before."""
+    import re
+    cmd = [sys.executable, 'examples/nlp/bert/test_glue_hetu_bert.py', '--gpu_id', '-1', '--hidden_size', '64',
+           '--num_hidden_layers', '2', '-a', '2', '-s', '16', '--train_batch_size', '32', '--vocab_size', '1100',
+           '-e', '6', '--batches', '20', '--lr', '1e-3', '--dropout_prob', '0', '--task_name', 'mnli']
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    accs = [float(a) for a in re.findall(r'Accuracy = ([0-9.]+)', r.stdout)]
+    assert len(accs) == 120
     assert np.mean(accs[:5]) < 0.5 and np.mean(accs[-10:]) > 0.55, accs
 
 

@@ -75,3 +75,21 @@ def test_ln_backward_emits_linear_bias_grad(dt, keep, R, N):
     torch.testing.assert_close(dl, ref, rtol=tol, atol=tol * (R ** 0.5))
     torch.testing.assert_close(dg, dg0, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(db, db0, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('R,N', [(8192, 3072), (100, 40), (3, 1024)])
+def test_gelu_grad_colsum_matches_torch(dt, R, N):
+    """hetu_gelu_grad_colsum: g = dy * gelu'(pre) and its column sums vs torch fp32."""
+    from hetu_61a7_amd.kernels.layernorm import gelu_grad_colsum
+    torch.manual_seed(0)
+    pre = torch.randn(R, N, device='cuda').to(dt)
+    dy = torch.randn(R, N, device='cuda').to(dt)
+    g, cs = gelu_grad_colsum(pre, dy)
+    x = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(dy.float())
+    ref = x.grad
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(g.float(), ref, rtol=tol, atol=tol)
+    torch.testing.assert_close(cs, ref.sum(0), rtol=tol, atol=tol * (R ** 0.5) * 4)

@@ -15,6 +15,9 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   grep -E "FAILED|ERROR" gpurun_out/pytest_gpu.log | tail -20; tail -2 gpurun_out/pytest_gpu.log
   [ $rc -ne 0 ] && { echo "pytest rc=$rc"; exit $rc; }
 fi
+echo "== smoke"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
 for m in ${BENCHES-resnet50 bert}; do
   echo "== bench $m"
   timeout -k 10 300 python bench.py --model $m --steps 20 --warmup 5 > gpurun_out/bench_$m.json 2> gpurun_out/bench_$m.err

@@ -56,8 +56,22 @@ def scatter_add_rows(dst: torch.Tensor, ids: torch.Tensor, src: torch.Tensor) ->
 
 
 def dedup_rows(idx: torch.Tensor, vals: torch.Tensor):
-    """Unique ids and the per-unique-id sum of their rows (fp32)."""
+    """Unique ids and the per-unique-id sum of their rows (fp32).
+
+    Heavily duplicated ids (BERT's token-type embedding: 8192 rows onto 2; the
+    position embedding: onto 128) would serialise thousands of fp32 atomics on
+    each destination element.  Rows are then spread over K private replicas of
+    the destination (row r -> replica r % K, at most ~16 rows per replica row),
+    scattered with little contention, and the replicas summed."""
     uniq, inv = torch.unique(idx, sorted=True, return_inverse=True)
-    merged = torch.zeros((uniq.numel(), vals.shape[-1]), dtype=torch.float32, device=vals.device)
+    nu, n, dim = uniq.numel(), inv.numel(), vals.shape[-1]
+    from . import deterministic
+    K = min(64, n // max(nu * 16, 1))
+    if K > 1 and vals.is_cuda and not deterministic():
+        rep = torch.arange(n, device=inv.device) % K
+        scratch = torch.zeros((K * nu, dim), dtype=torch.float32, device=vals.device)
+        scatter_add_rows(scratch, inv.reshape(-1) + rep * nu, vals.reshape(n, dim))
+        return uniq, scratch.view(K, nu, dim).sum(0)
+    merged = torch.zeros((nu, dim), dtype=torch.float32, device=vals.device)
     scatter_add_rows(merged, inv, vals)
     return uniq, merged

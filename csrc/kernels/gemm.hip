@@ -1024,6 +1024,49 @@ __global__ void splitk_reduce_k(const float* __restrict__ slab, int64_t stride, 
   }
 }
 
+// Vector form of splitk_reduce_k for fp32 outputs with N % 4 == 0, ldd % 4 == 0
+// and 16-byte aligned slab / dst: 4 columns per lane, the slices' loads in flight.
+__global__ void __launch_bounds__(256) splitk_reduce_vec_k(const float* __restrict__ slab, int64_t stride, int nz,
+                                                            float* __restrict__ dst, int64_t M, int64_t N,
+                                                            int64_t ldd, int accumulate) {
+  const int64_t n4 = N / 4, total4 = M * n4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / n4, c = (i - m * n4) * 4;
+    float4 acc = *reinterpret_cast<const float4*>(slab + m * N + c);
+    int z = 1;
+    for (; z + 1 < nz; z += 2) {
+      const float4 a = *reinterpret_cast<const float4*>(slab + z * stride + m * N + c);
+      const float4 b = *reinterpret_cast<const float4*>(slab + (z + 1) * stride + m * N + c);
+      acc.x += a.x + b.x; acc.y += a.y + b.y; acc.z += a.z + b.z; acc.w += a.w + b.w;
+    }
+    if (z < nz) {
+      const float4 a = *reinterpret_cast<const float4*>(slab + z * stride + m * N + c);
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    float4* d = reinterpret_cast<float4*>(dst + m * ldd + c);
+    if (accumulate) {
+      const float4 o = *d;
+      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    }
+    *d = acc;
+  }
+}
+
+static void launch_splitk_reduce(const float* slab, int splitk, void* C, int64_t M, int64_t N, int64_t ldc,
+                                 int out_f32, int atomic, hipStream_t st) {
+  if (out_f32 && (N % 4) == 0 && (ldc % 4) == 0 && ((((uintptr_t)slab) | ((uintptr_t)C)) & 15) == 0) {
+    int nb = (int)std::min<int64_t>((M * N / 4 + 255) / 256, 4096);
+    if (nb < 1) nb = 1;
+    hipLaunchKernelGGL(splitk_reduce_vec_k, dim3(nb), dim3(256), 0, st, slab, M * N, splitk, (float*)C, M, N,
+                       ldc, atomic);
+    return;
+  }
+  int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, slab, M * N, splitk, C, M, N, ldc, out_f32,
+                     atomic);
+}
+
 template <class LA, class LB>
 static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
                       int batch, int splitk, hipStream_t st) {
@@ -1040,9 +1083,7 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
     e1.slab_stride = M * N;
     hipLaunchKernelGGL((gemm_big_kernel<LA, LB>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
                        tiles_n, ktps, g_big_variant);
-    int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, ep.slab, M * N, splitk, ep.C, M, N,
-                       ep.ldc, ep.out_f32, ep.atomic);
+    launch_splitk_reduce(ep.slab, splitk, ep.C, M, N, ep.ldc, ep.out_f32, ep.atomic, st);
     return (int)hipGetLastError();
   }
   e1.slab = nullptr;
@@ -1074,9 +1115,7 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
     else
       hipLaunchKernelGGL((gemm_kernel<LA, LB, false>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K,
                          tiles_m, tiles_n, ktps);
-    int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, ep.slab, M * N, splitk, ep.C, M,
-                       N, ep.ldc, ep.out_f32, ep.atomic);
+    launch_splitk_reduce(ep.slab, splitk, ep.C, M, N, ep.ldc, ep.out_f32, ep.atomic, st);
     return (int)hipGetLastError();
   }
   Epi e1 = ep;
@@ -1224,4 +1263,31 @@ HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int 
   lb.g = g;
   lb.P = P;
   return launch(la, lb, ep, K, Nc, P, 1, splitk, st, tile);
+}
+
+// out[i] = sum_z slab[z * n + i] (fp32; the partials of a split-K library GEMM):
+// 16-byte vectors, every slab's load issued before the adds, grid-stride.
+__global__ void __launch_bounds__(256) splitk_sum_vec_k(const float4* __restrict__ slab, int64_t n4, int nz,
+                                                         float4* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 acc = slab[i];
+    float4 v[7];
+#pragma unroll
+    for (int z = 1; z < 8; ++z)
+      if (z < nz) v[z - 1] = slab[z * n4 + i];
+#pragma unroll
+    for (int z = 1; z < 8; ++z)
+      if (z < nz) { acc.x += v[z - 1].x; acc.y += v[z - 1].y; acc.z += v[z - 1].z; acc.w += v[z - 1].w; }
+    out[i] = acc;
+  }
+}
+
+HETU_API int hetu_splitk_sum_f32(const float* slab, int nz, float* out, int64_t n, hipStream_t st) {
+  if (nz < 1 || nz > 8 || (n & 3) || (((uintptr_t)slab | (uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  int64_t nb = (n4 + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(splitk_sum_vec_k, dim3((unsigned)nb), dim3(256), 0, st, (const float4*)slab, n4, nz, (float4*)out);
+  return (int)hipGetLastError();
 }

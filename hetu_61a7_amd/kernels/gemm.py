@@ -154,6 +154,22 @@ def _vendor_splitk_into(A, B, out, s=4):
         part = torch.bmm(Av, Bv, out_dtype=torch.float32)
     except (RuntimeError, TypeError):
         return None
+    _splitk_sum(part, out)
+    return out
+
+
+def _splitk_sum(part, out):
+    """out = part.sum(0) for the [s, M, N] fp32 split-K partials: the vectorised
+    ``hetu_splitk_sum_f32`` (all s loads in flight per lane) when ``out`` is a
+    contiguous aligned fp32 buffer, else torch."""
+    s = part.shape[0]
+    n = out.numel()
+    if part.is_contiguous() and out.is_contiguous() and out.dtype == torch.float32 and s <= 8 and n % 4 == 0 \
+            and part.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0 and part[0].numel() == n:
+        from . import fn, check, P, I32, I64, stream_ptr
+        f = fn('hetu_splitk_sum_f32', [P, I32, P, I64, P])
+        check(f(part.data_ptr(), s, out.data_ptr(), n, stream_ptr()), 'splitk_sum')
+        return out
     torch.sum(part, 0, out=out)
     return out
 

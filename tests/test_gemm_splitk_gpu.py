@@ -31,3 +31,28 @@ def test_weight_grad_paths_match_fp32(M, N, K):
     for name, o in outs.items():
         err = (o - ref).abs().max().item() / scale
         assert err < 2e-2, (name, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('s,M,N', [(4, 768, 3072), (2, 64, 36), (8, 30522, 768), (3, 5, 4)])
+def test_splitk_partial_sum_matches_torch(s, M, N):
+    """kernels.gemm._splitk_sum (vectorised fp32 sum of split-K partials) == torch.sum."""
+    from hetu_61a7_amd.kernels.gemm import _splitk_sum
+    torch.manual_seed(0)
+    part = torch.randn(s, M, N, device='cuda')
+    out = torch.empty(M, N, device='cuda')
+    _splitk_sum(part, out)
+    torch.testing.assert_close(out, part.sum(0), rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_vendor_splitk_gemm_matches_matmul():
+    from hetu_61a7_amd.kernels.gemm import _vendor_splitk_into
+    torch.manual_seed(0)
+    A = torch.randn(768, 8192, device='cuda').to(torch.bfloat16)
+    B = torch.randn(8192, 1024, device='cuda').to(torch.bfloat16)
+    out = torch.empty(768, 1024, device='cuda')
+    r = _vendor_splitk_into(A, B, out)
+    if r is None:
+        pytest.skip('bmm out_dtype unsupported')
+    torch.testing.assert_close(out, A.float() @ B.float(), rtol=2e-2, atol=0.5)

@@ -1266,24 +1266,26 @@ HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int 
 }
 
 // out[i] = sum_z slab[z * n + i] (fp32; the partials of a split-K library GEMM):
-// 16-byte vectors, every slab's load issued before the adds, grid-stride.
+// 16-byte vectors, the slabs' loads issued 8 at a time before the adds, grid-stride.
 __global__ void __launch_bounds__(256) splitk_sum_vec_k(const float4* __restrict__ slab, int64_t n4, int nz,
                                                          float4* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 acc = slab[i];
-    float4 v[7];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z0 = 0; z0 < nz; z0 += 8) {
+      float4 v[8];
 #pragma unroll
-    for (int z = 1; z < 8; ++z)
-      if (z < nz) v[z - 1] = slab[z * n4 + i];
+      for (int z = 0; z < 8; ++z)
+        if (z0 + z < nz) v[z] = slab[(z0 + z) * n4 + i];
 #pragma unroll
-    for (int z = 1; z < 8; ++z)
-      if (z < nz) { acc.x += v[z - 1].x; acc.y += v[z - 1].y; acc.z += v[z - 1].z; acc.w += v[z - 1].w; }
+      for (int z = 0; z < 8; ++z)
+        if (z0 + z < nz) { acc.x += v[z].x; acc.y += v[z].y; acc.z += v[z].z; acc.w += v[z].w; }
+    }
     out[i] = acc;
   }
 }
 
 HETU_API int hetu_splitk_sum_f32(const float* slab, int nz, float* out, int64_t n, hipStream_t st) {
-  if (nz < 1 || nz > 8 || (n & 3) || (((uintptr_t)slab | (uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
+  if (nz < 1 || nz > 64 || (n & 3) || (((uintptr_t)slab | (uintptr_t)out) & 15)) return (int)hipErrorInvalidValue;
   const int64_t n4 = n / 4;
   int64_t nb = (n4 + 255) / 256;
   if (nb > 4096) nb = 4096;

@@ -164,7 +164,7 @@ def _splitk_sum(part, out):
     contiguous aligned fp32 buffer, else torch."""
     s = part.shape[0]
     n = out.numel()
-    if part.is_contiguous() and out.is_contiguous() and out.dtype == torch.float32 and s <= 8 and n % 4 == 0 \
+    if part.is_contiguous() and out.is_contiguous() and out.dtype == torch.float32 and s <= 64 and n % 4 == 0 \
             and part.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0 and part[0].numel() == n:
         from . import fn, check, P, I32, I64, stream_ptr
         f = fn('hetu_splitk_sum_f32', [P, I32, P, I64, P])

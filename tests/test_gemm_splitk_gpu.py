@@ -34,7 +34,7 @@ def test_weight_grad_paths_match_fp32(M, N, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('s,M,N', [(4, 768, 3072), (2, 64, 36), (8, 30522, 768), (3, 5, 4)])
+@pytest.mark.parametrize('s,M,N', [(4, 768, 3072), (2, 64, 36), (8, 30522, 768), (3, 5, 4), (16, 256, 576), (11, 8, 12)])
 def test_splitk_partial_sum_matches_torch(s, M, N):
     """kernels.gemm._splitk_sum (vectorised fp32 sum of split-K partials) == torch.sum."""
     from hetu_61a7_amd.kernels.gemm import _splitk_sum

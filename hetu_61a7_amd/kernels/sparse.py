@@ -75,3 +75,28 @@ def dedup_rows(idx: torch.Tensor, vals: torch.Tensor):
     merged = torch.zeros((nu, dim), dtype=torch.float32, device=vals.device)
     scatter_add_rows(merged, inv, vals)
     return uniq, merged
+
+
+def dedup_rows_dense(idx: torch.Tensor, vals: torch.Tensor, nrows: int):
+    """Sync-free dedup for a small table: (ids, merged) over ALL ``nrows`` rows --
+    merged[r] = sum of the rows with id r, ids[r] = r where some row hit r, else
+    -1 (the row-sparse optimizer kernel skips those, so untouched rows keep
+    exact sparse-update semantics).  Unlike ``dedup_rows`` nothing depends on
+    the number of distinct ids, so the host never waits for the GPU (BERT's
+    position and token-type embeddings).  Duplicates are spread over private
+    replicas as in ``dedup_rows``; out-of-range ids are dropped."""
+    n, dim = idx.numel(), vals.shape[-1]
+    idx = idx.reshape(-1).long()
+    valid = (idx >= 0) & (idx < nrows)
+    from . import deterministic
+    K = 1 if deterministic() else max(1, min(64, n // max(nrows * 16, 1)))
+    tgt = idx if K == 1 else idx + (torch.arange(n, device=idx.device) % K) * nrows
+    tgt = torch.where(valid, tgt, torch.full_like(tgt, -1))
+    scratch = torch.zeros((K * nrows, dim), dtype=torch.float32, device=vals.device)
+    scatter_add_rows(scratch, tgt, vals.reshape(n, dim))
+    merged = scratch if K == 1 else scratch.view(K, nrows, dim).sum(0)
+    hit = torch.zeros(nrows + 1, dtype=torch.int64, device=idx.device)
+    hit.scatter_(0, torch.where(valid, idx, torch.full_like(idx, nrows)), 1)
+    rows = torch.arange(nrows, device=idx.device)
+    ids = torch.where(hit[:nrows] > 0, rows, torch.full_like(rows, -1))
+    return ids, merged

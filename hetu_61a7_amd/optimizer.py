@@ -518,7 +518,15 @@ class OptimizerOp(Op):
         self._pending_ps = []
         for p, sl in self._pending_sparse:
             table = self.config.placeholder_to_arr_map[p]
-            uniq, merged = sl.deduplicate().indices, sl.values
+            nrows = table.shape[0] if isinstance(table, torch.Tensor) else 0
+            if nrows and table.is_cuda and nrows <= 65536 and nrows * 4 <= sl._t(sl.indices).numel() * 64:
+                # small table: all-rows dedup with -1 for untouched rows (no host sync
+                # on the number of distinct ids; the sparse kernel skips -1 rows)
+                from .kernels import sparse as ksparse
+                w = sl.dense_shape[-1]
+                uniq, merged = ksparse.dedup_rows_dense(sl._t(sl.indices), sl._t(sl.values).reshape(-1, w), nrows)
+            else:
+                uniq, merged = sl.deduplicate().indices, sl.values
             if self.optimizer.mode == 'lamb':
                 pass
             self.optimizer.sparse_update(table, self.sparse_state.get(p, {}), uniq, merged, self.step)

@@ -288,3 +288,31 @@ def test_dedup_rows_heavy_duplication(n, nu, dim, dt):
     ref = torch.zeros(ru.numel(), dim, device='cuda').index_add_(0, inv, vals.float())
     assert torch.equal(uniq, ru)
     torch.testing.assert_close(merged, ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('n,nrows,dim', [(8192, 2, 768), (8192, 512, 768), (100, 4000, 64)])
+def test_dedup_rows_dense_matches_sparse_update(n, nrows, dim):
+    """kernels.sparse.dedup_rows_dense (no host sync): summed rows for every hit id,
+    -1 for untouched rows, out-of-range ids dropped; an Adam sparse update through
+    it equals the update through the unique-id dedup."""
+    from hetu_61a7_amd.kernels.sparse import dedup_rows_dense, dedup_rows
+    from hetu_61a7_amd.kernels import optim as KO
+    torch.manual_seed(0)
+    idx = torch.randint(-1, min(nrows, 128), (n,), device='cuda')
+    vals = torch.randn(n, dim, device='cuda').to(torch.bfloat16)
+    ids, merged = dedup_rows_dense(idx, vals, nrows)
+    valid = idx >= 0
+    ref = torch.zeros(nrows, dim, device='cuda').index_add_(0, idx[valid], vals[valid].float())
+    hit = torch.zeros(nrows, dtype=torch.bool, device='cuda')
+    hit[idx[valid]] = True
+    assert torch.equal(ids >= 0, hit)
+    torch.testing.assert_close(merged[hit], ref[hit], rtol=1e-4, atol=1e-3)
+    tabs = [torch.randn(nrows, dim, device='cuda') for _ in range(2)]
+    tabs[1].copy_(tabs[0])
+    st = [(torch.zeros(nrows, dim, device='cuda'), torch.zeros(nrows, dim, device='cuda')) for _ in range(2)]
+    u, m = dedup_rows(idx[valid], vals[valid])
+    KO.sparse_update('adam', tabs[0], u, m, st[0][0], st[0][1], lr=0.01, beta1t=0.9, beta2t=0.999)
+    KO.sparse_update('adam', tabs[1], ids, merged, st[1][0], st[1][1], lr=0.01, beta1t=0.9, beta2t=0.999)
+    torch.testing.assert_close(tabs[1], tabs[0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(st[1][1], st[0][1], rtol=1e-5, atol=1e-6)

@@ -299,6 +299,12 @@ struct Perf {
 
 // Small persistent fork-join pool for the cache's row-copy / gradient loops, which
 // are host-memory-bandwidth bound on one thread (HETU_CACHE_THREADS, default 4).
+// Every run() publishes its own Job (range, part count, callable, chunk counter,
+// completion count).  A worker copies the job pointer under the mutex and only ever
+// takes chunks from THAT job's counter, so a worker woken for an earlier run that is
+// descheduled between wake-up and fetch_add cannot execute a chunk of a later run
+// (it finds its old job exhausted), and run() returns only after every chunk of its
+// own job has finished.
 class ParallelFor {
  public:
   ParallelFor() {
@@ -324,54 +330,60 @@ class ParallelFor {
       return;
     }
     std::lock_guard<std::mutex> call(call_mu_);   // one parallel region at a time
-    const int64_t parts = std::min<int64_t>(nthreads_, n / min_chunk);
+    auto job = std::make_shared<Job>();
+    job->n = n;
+    job->parts = std::min<int64_t>(nthreads_, n / min_chunk);
+    job->fn = &fn;
     {
       std::lock_guard<std::mutex> g(mu_);
-      fn_ = &fn;
-      n_ = n;
-      parts_ = parts;
-      next_.store(0);
-      done_ = 0;
+      job_ = job;
       ++gen_;
     }
     cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> g(mu_);
-    done_cv_.wait(g, [&] { return done_ == parts_; });
-    fn_ = nullptr;
+    work(*job);
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      done_cv_.wait(g, [&] { return job->done == job->parts; });
+      job_.reset();   // workers still holding `job` see it exhausted
+    }
   }
 
  private:
-  void work() {
+  struct Job {
+    int64_t n = 0, parts = 0;
+    const std::function<void(int64_t, int64_t)>* fn = nullptr;
+    std::atomic<int64_t> next{0};
+    int64_t done = 0;   // guarded by mu_
+  };
+  void work(Job& j) {
     for (;;) {
-      const int64_t p = next_.fetch_add(1);
-      if (p >= parts_) return;
-      const int64_t b = n_ * p / parts_, e = n_ * (p + 1) / parts_;
-      (*fn_)(b, e);
+      const int64_t p = j.next.fetch_add(1);
+      if (p >= j.parts) return;
+      const int64_t b = j.n * p / j.parts, e = j.n * (p + 1) / j.parts;
+      (*j.fn)(b, e);
       std::lock_guard<std::mutex> g(mu_);
-      if (++done_ == parts_) done_cv_.notify_all();
+      if (++j.done == j.parts) done_cv_.notify_all();
     }
   }
   void worker() {
     uint64_t seen = 0;
     for (;;) {
+      std::shared_ptr<Job> job;
       {
         std::unique_lock<std::mutex> g(mu_);
         cv_.wait(g, [&] { return stop_ || gen_ != seen; });
         if (stop_) return;
         seen = gen_;
-        if (!fn_) continue;
+        job = job_;
       }
-      work();
+      if (job) work(*job);
     }
   }
   std::vector<std::thread> th_;
   int nthreads_ = 1;
   std::mutex mu_, call_mu_;
   std::condition_variable cv_, done_cv_;
-  const std::function<void(int64_t, int64_t)>* fn_ = nullptr;
-  int64_t n_ = 0, parts_ = 0, done_ = 0;
-  std::atomic<int64_t> next_{0};
+  std::shared_ptr<Job> job_;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
@@ -731,6 +743,24 @@ static Exec* exec() {
 using namespace hc;
 
 extern "C" {
+
+// Self-test of the fork-join pool: alternating parallel regions of
+// different sizes, each element must be visited exactly once per region.  Returns
+// the number of mis-visited elements (0 = OK).  Driven by the TSan binary
+// (csrc/tests/runtime_sanitize.cc) and tests/test_sanitizers_cpu.py.
+int64_t hc_parallel_for_selftest(int iters) {
+  int64_t bad = 0;
+  std::vector<std::atomic<int>> hits(1 << 16);
+  for (int it = 0; it < iters; ++it) {
+    const int64_t n = (it & 1) ? 4096 + (it % 7) * 1531 : 1024 + (it % 5) * 377;
+    for (int64_t i = 0; i < n; ++i) hits[i].store(0, std::memory_order_relaxed);
+    pool().run(n, 256, [&](int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; ++i) hits[i].fetch_add(1, std::memory_order_relaxed);
+    });
+    for (int64_t i = 0; i < n; ++i) bad += hits[i].load(std::memory_order_relaxed) != 1;
+  }
+  return bad;
+}
 
 // wait for every queued cache operation (called by hps_finalize before the PS
 // segment is unmapped, so no cache thread can touch it afterwards)

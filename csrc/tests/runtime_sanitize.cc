@@ -42,6 +42,7 @@ int hc_create(int policy, int64_t limit, int64_t rows, int64_t width, int key, i
 int hc_lookup(int h, const int64_t* keys, int64_t n, float* dest);
 int hc_update(int h, const int64_t* keys, int64_t n, const float* grads);
 int hc_flush(int h);
+int64_t hc_parallel_for_selftest(int iters);
 }
 
 #define CHECK(c)                                                          \
@@ -178,6 +179,9 @@ int main() {
   if (rc) return rc;
   rc = test_ps();
   if (rc) return rc;
+  // cache fork-join pool (after the forks: it starts threads): regions of
+  // alternating sizes, every element exactly once
+  CHECK(hc_parallel_for_selftest(400) == 0);
   printf("runtime sanitize test: OK\n");
   return 0;
 }

@@ -90,6 +90,11 @@ def sparse_update(mode, table, ids, grads, s1=None, s2=None, lr=0.01, l2=0.0, mu
                 ids.numel(), dim, table.shape[0], lr, l2, mu, beta1, beta2, beta1t, beta2t, eps,
                 wd, stream_ptr()), 'sparse_opt')
         return
+    # ids < 0 mark rows the dense de-duplication left untouched (optimizer.py);
+    # the native kernel skips them, the torch path must too (table[-1] is a real row)
+    keep = ids >= 0
+    if not bool(keep.all()):
+        ids, g = ids[keep], g[keep]
     p = table[ids]
     gr = g + l2 * p if l2 else g
     if mode == 'sgd':

@@ -27,6 +27,7 @@ import torch
 
 from .node import Op
 from .. import ndarray
+from ..ps import PS_KEY_DENSE_COMM
 
 
 def _lr_of(optimizer):
@@ -37,7 +38,7 @@ def _lr_of(optimizer):
 
 class ParameterServerCommunicateOp(Op):
     # dense-key namespace above node ids (< 2^20) and the optimizers' flat keys
-    DENSE_KEY_BASE = 1 << 21
+    DENSE_KEY_BASE = PS_KEY_DENSE_COMM
 
     def __init__(self, node, parameter, optimizer):
         super().__init__(ParameterServerCommunicateOp, [node], node.raw_ctx)

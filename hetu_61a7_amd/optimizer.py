@@ -366,8 +366,9 @@ class OptimizerOp(Op):
             self._make_buckets(dense)
         if self.ps_dense_wanted and self.flat.numel > 0:
             from .ps.table import PSDense
+            from .ps import PS_KEY_OPT_FLAT
             # key space: node ids are < 2^20; the flat dense key sits above them
-            self.ps_dense = PSDense(self.flat, (1 << 20) + self.id, config)
+            self.ps_dense = PSDense(self.flat, PS_KEY_OPT_FLAT + self.id, config)
 
     def _make_buckets(self, dense):
         """Contiguous buckets over the flat gradient, built from the END of the

@@ -33,6 +33,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ndarray
+from ..ps import PS_KEY_HETPIPE_STAGE
 from ..ops.node import Op
 from ..ops.variable import PlaceholderOp
 from ..ops.executor import find_topo_sort, AuxResult, _shape_of
@@ -242,7 +243,7 @@ class PipelineSubExecutor(object):
         self.opt = op
         if ps_sync:
             from ..ps.table import PSDense
-            op.ps_dense = PSDense(op.flat, (1 << 21) + self.stage, self.config, publish=self.replica == 0)
+            op.ps_dense = PSDense(op.flat, PS_KEY_HETPIPE_STAGE + self.stage, self.config, publish=self.replica == 0)
 
     # ---------------------------------------------------------------------------------------
     def _compute(self, nodes, vals, aux):

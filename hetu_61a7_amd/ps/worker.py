@@ -41,6 +41,7 @@ class PSAgent(object):
         check(lib('hps_init')(2, shm_name().encode(), nw, ns, 0), 'init')
         self.pending = {}
         self.keepalive = {}
+        self.keys = []   # node ids this worker registered (save_params / load_params)
 
     # ---- identity --------------------------------------------------------------------
     def rank(self):
@@ -56,6 +57,7 @@ class PSAgent(object):
             rows, width = length, 1
         check(lib('hps_param_init')(int(node_id), int(ptype), int(rows), int(width), int(init_type),
                                     float(init_a), float(init_b), int(seed)), 'ParamInit')
+        self._register(node_id)
 
     def init_tensor(self, node_id, param_type, shape, initializer, seed, opt=None):
         name = type(initializer).__name__
@@ -73,6 +75,11 @@ class PSAgent(object):
             length, width = int(shape[0]), int(np.prod(shape[1:]))
         check(lib('hps_param_init')(int(node_id), int(param_type), length, width, it, float(a),
                                     float(b), int(seed)), 'ParamInit')
+        self._register(node_id)
+
+    def _register(self, node_id):
+        if int(node_id) not in self.keys:
+            self.keys.append(int(node_id))
 
     def Clear(self, node_id):
         check(lib('hps_param_clear')(int(node_id)), 'Clear')
@@ -185,11 +192,24 @@ class PSAgent(object):
         with open(os.path.join(d, 'loads_%d.txt' % self.rank()), 'a') as f:
             f.write(repr(loads) + '\n')
 
-    def save_params(self, path):
-        pass
+    def save_params(self, path, keys=None):
+        """SaveParam for every table this worker registered (or ``keys``): one
+        ``<key>_<part>.dat`` per server partition under ``path``."""
+        keys = self.keys if keys is None else keys
+        if not keys:
+            raise ValueError('save_params: no PS tables registered on this worker')
+        for k in keys:
+            self.SaveParam(k, path)
+        return list(keys)
 
-    def load_params(self, path):
-        pass
+    def load_params(self, path, keys=None):
+        """LoadParam counterpart of :meth:`save_params`."""
+        keys = self.keys if keys is None else keys
+        if not keys:
+            raise ValueError('load_params: no PS tables registered on this worker')
+        for k in keys:
+            self.LoadParam(k, path)
+        return list(keys)
 
     def finalize(self):
         lib('hps_finalize')()

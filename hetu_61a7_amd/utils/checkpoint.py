@@ -281,8 +281,13 @@ def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
         fl = op.flat
         src = d
         if getattr(op, 'zero', False):
-            src = shards[i] if shards is not None and i < len(shards) and shards[i] is not None else {}
-            if src and src.get('nrank') != op.comm.nrank:
+            if shards is None or i >= len(shards) or shards[i] is None:
+                # a ZeRO-1 resume without this rank's moments would keep the restored
+                # step count with zeroed state (Adam bias correction off): refuse
+                raise FileNotFoundError('ZeRO-1 optimizer shard %s.ext.rank%s (optimizer %d) missing'
+                                        % (path, zr, i))
+            src = shards[i]
+            if src.get('nrank') != op.comm.nrank:
                 raise ValueError('ZeRO checkpoint was written with %s ranks, resuming with %d'
                                  % (src.get('nrank'), op.comm.nrank))
         if fl is not None:

@@ -89,6 +89,13 @@ def _worker(env, q, tmpdir):
     ag.SparsePull(2, torch.tensor([10], dtype=torch.int64), got2)
     ag.Wait(2)
     out['reloaded'] = float(got2[0, 0])
+    # save_params / load_params: every table this worker registered
+    d2 = os.path.join(tmpdir, 'all_%d' % r)
+    out['saved_keys'] = ag.save_params(d2)
+    out['saved_files'] = sorted(os.listdir(d2))
+    ag.BarrierWorker()
+    out['loaded_keys'] = ag.load_params(d2)
+    ag.BarrierWorker()
     out['loads'] = ag.getLoads()
     q.put((r, out))
     worker.worker_finish()
@@ -119,5 +126,7 @@ def test_ps_roles_and_psfs(tmp_path):
         assert o['ddpp_min'] >= nw + 1
         assert o['partners'] == list(range(nw))
         assert o['reloaded'] == pytest.approx(3.0)
+        assert o['saved_keys'] == [1, 2, 3] and o['loaded_keys'] == [1, 2, 3]
+        assert all(any(f.startswith('%d_' % k) for f in o['saved_files']) for k in (1, 2, 3))
         # each worker: 3 updates of +1 on row 5 -> 2*3 = 6 on the server
         assert o['cache_row5'] == pytest.approx(2 * 3.0)

@@ -40,6 +40,10 @@ def parse():
     p.add_argument('--bucket-mb', type=float, default=32)
     p.add_argument('--zero', type=int, default=0, help='1: ZeRO-1 sharded optimizer state over the DP group')
     p.add_argument('--op-profile', default=None, help='write per-op-type GPU time (ms) to this file')
+    p.add_argument('--grad-wire', default=os.environ.get('HETU_GRAD_WIRE', 'fp32'), choices=['fp32', 'bf16'],
+                   help='DP gradient all-reduce wire format (bf16: fp32 accumulation)')
+    p.add_argument('--comm-trace', action='store_true',
+                   help='report the last step\'s all-reduce bucket timeline in the JSON config')
     return p.parse_args()
 
 
@@ -57,9 +61,27 @@ def start_ps_server(world, local):
     return subprocess.Popen([sys.executable, '-m', 'hetu_61a7_amd.ps'], env=env)
 
 
+def _progress(rank, world, msg):
+    """per-rank progress on stderr for multi-rank runs (a stalled rank is then visible
+    by its last line, and faulthandler dumps every rank's stack if it stalls)"""
+    if world > 1:
+        print('[bench rank %d/%d %.1fs] %s' % (rank, world, time.perf_counter() - _T0, msg), file=sys.stderr,
+              flush=True)
+
+
+_T0 = time.perf_counter()
+
+
 def main():
     args = parse()
+    if args.comm_trace:
+        os.environ['HETU_COMM_TRACE'] = '1'
+    os.environ['HETU_GRAD_WIRE'] = args.grad_wire
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world > 1:
+        import faulthandler
+        # a rank silent for 240 s prints all its threads' stacks (then keeps running)
+        faulthandler.dump_traceback_later(240, repeat=True, file=sys.stderr)
     local = int(os.environ.get('LOCAL_RANK', '0'))
     server = start_ps_server(world, local) if args.model == 'wdl' else None
     import torch
@@ -118,9 +140,12 @@ def main():
         if world > 1:
             C.world().barrier()
 
-    for _ in range(args.warmup):
+    _progress(rank, world, 'graph built, comm=%s' % (C.world().backend if C.world() is not None else 'none'))
+    for i in range(args.warmup):
         step()
+        _progress(rank, world, 'warmup step %d issued' % i)
     torch.cuda.synchronize()
+    _progress(rank, world, 'warmup done')
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -143,6 +168,14 @@ def main():
         from hetu_61a7_amd.ops.executor import layout_report
         print('non-channels-last 4D outputs:', layout_report(), file=sys.stderr)
     value = samples_per_step * args.steps / dt_s
+    _progress(rank, world, 'timed steps done')
+    if world > 1 or args.comm_trace:
+        cfg = dict(cfg)
+        cfg['comm'] = C.world().backend if C.world() is not None else 'none'
+        cfg['grad_wire'] = args.grad_wire
+        if args.comm_trace and args.model == 'resnet50':
+            tr = [op.comm_trace() for op in ex.optimizer_ops('train')] if hasattr(ex, 'optimizer_ops') else []
+            cfg['comm_trace_last_step'] = tr[0] if tr else []
     if rank == 0:
         out = {'metric': metric, 'value': round(value, 2), 'unit': 'tokens/s' if args.model == 'moe' else 'samples/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),

@@ -1,0 +1,79 @@
+// Implicit-GEMM convolution (NHWC, bf16 operands, fp32 accumulate) on the MFMA
+// kernels of gemm_core.h: forward, data gradient (split into stride classes) and
+// weight gradient (split-K over output pixels).  1x1 / stride-1 convolutions are
+// plain GEMMs and go through the buffer-descriptor loaders.
+//
+// Replaces cuDNN convolution (reference src/ops/CudnnConv2d.cu:54-245,
+// CudnnConv2dAddBias.cu:93), SURVEY.md §2.7.
+#include "gemm_core.h"
+
+using namespace hetu;
+using namespace hetu::gemm;
+
+// y[N,OH,OW,K] (NHWC) = conv(x[N,H,W,C] NHWC, w[K,KH,KW,C]) (+bias[K]) -> act.  C % 8 == 0.
+// colstats (optional, 2*K floats, zeroed by the caller) += per-channel sum and sum of
+// squares of the stored y: the statistics a training-mode BatchNorm on y needs.
+HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const float* bias, int N,
+                                int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
+                                int pw, int act, float* colstats, int tile, hipStream_t st) {
+  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  int64_t M = (int64_t)N * g.OH * g.OW, Kt = (int64_t)KH * KW * C;
+  Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0, nullptr, 0, colstats};
+  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && buf_ok(M * C * 2, (int64_t)K * C * 2))
+    return C % BK == 0 ? launch_buf<true>((const bf16*)x, (const bf16*)w, 1, 1, C, C, 0, 0, ep, M, K, C, 1, 1, st, tile)
+                       : launch_buf<false>((const bf16*)x, (const bf16*)w, 1, 1, C, C, 0, 0, ep, M, K, C, 1, 1, st, tile);
+  ConvFwdA la{};
+  la.x = (const bf16*)x;
+  g.ctap = C % BK == 0;
+  la.g = g;
+  la.Ktot = Kt;
+  la.rows = M;
+  return launch(la, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M, K, Kt, 1, 1, st, tile);
+}
+
+// dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[K,KH,KW,C]) (+ acc[N,H,W,C] when given:
+// the gradient joined at the conv input, added in the epilogue).  K % 8 == 0, C % 8 == 0.
+HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const void* acc,
+                                  int acc_f32, int N, int H, int W, int C, int K, int KH, int KW,
+                                  int sh, int sw, int ph, int pw, int tile, hipStream_t st) {
+  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  Epi ep{dx, acc, nullptr, C, C, 0, 0, 1.f, acc ? 1.f : 0.f, 0, 0, acc_f32, 0, 0, nullptr, 0};
+  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 &&
+      buf_ok((int64_t)N * H * W * K * 2, (int64_t)K * C * 2)) {
+    int64_t M = (int64_t)N * H * W;
+    return K % BK == 0 ? launch_buf<true>((const bf16*)dy, (const bf16*)w, 1, 0, K, C, 0, 0, ep, M, C, K, 1, 1, st, tile)
+                       : launch_buf<false>((const bf16*)dy, (const bf16*)w, 1, 0, K, C, 0, 0, ep, M, C, K, 1, 1, st, tile);
+  }
+  // one launch over the sh*sw stride classes (blockIdx.y); grid sized for the
+  // largest class, the others exit early per block
+  int64_t Mmax = (int64_t)N * ((H + sh - 1) / sh) * ((W + sw - 1) / sw);
+  int64_t Kmax = (int64_t)((KH + sh - 1) / sh) * ((KW + sw - 1) / sw) * K;
+  g.ctap = K % BK == 0;
+  ConvDgradA la{};
+  la.dy = (const bf16*)dy;
+  la.g = g;
+  ConvDgradB lb{};
+  lb.w = (const bf16*)w;
+  lb.g = g;
+  return launch(la, lb, ep, Mmax, C, Kmax, sh * sw, 1, st, tile);
+}
+
+// dw[K, KH*KW*C] fp32 (+)= sum over output pixels dy^T x_im2col.  Split-K over
+// the pixel axis into fp32 slabs (ws: splitk*K*KH*KW*C floats) + one reduce; no atomics.
+HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int N, int H, int W,
+                                  int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
+                                  int splitk, int accumulate, float* ws, int tile, hipStream_t st) {
+  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
+  int64_t P = (int64_t)N * g.OH * g.OW, Nc = (int64_t)KH * KW * C;
+  Epi ep{dw, nullptr, nullptr, Nc, 0, 0, 0, 1.f, 0.f, 0, 1, 0, accumulate, 0, splitk > 1 ? ws : nullptr, 0};
+  PlainMN la{(const bf16*)dy, K, K, P, 0};
+  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && buf_ok(P * K * 2, P * C * 2))
+    return P % BK == 0 ? launch_buf<true>((const bf16*)dy, (const bf16*)x, 0, 0, K, C, 0, 0, ep, K, Nc, P, 1, splitk, st, tile)
+                       : launch_buf<false>((const bf16*)dy, (const bf16*)x, 0, 0, K, C, 0, 0, ep, K, Nc, P, 1, splitk, st, tile);
+  ConvWgradB lb{};
+  lb.x = (const bf16*)x;
+  lb.g = g;
+  lb.P = P;
+  return launch(la, lb, ep, K, Nc, P, 1, splitk, st, tile);
+}
+

@@ -1,1144 +1,17 @@
-// bf16 MFMA GEMM and implicit-GEMM convolution for gfx950 (CDNA4).
+// bf16 MFMA GEMM for gfx950 (CDNA4): the plain-operand C API (all four transpose
+// modes, batched, beta / bias / activation epilogues, split-K) over the kernels of
+// gemm_core.h, and the split-K slab reducers.
 //
 // Replaces the reference's cuBLAS Sgemm / SgemmStridedBatched call sites
 // (src/ops/MatrixMult.cu:22-26, BatchMatrixMult.cu:31-36, Linear.cu:50-55,
-// Addmm.cu:29, Baddbmm.cu:37) and cuDNN convolution (CudnnConv2d.cu:54-245,
-// CudnnConv2dAddBias.cu:93), SURVEY.md §2.7.
-//
-// One kernel template, operand "loaders" as policies:
-//   C[M,N] = alpha * sum_k  Am[m,k] * Bn[n,k]  (+ beta*Cin) (+ bias) -> act
-// Each operand is either K-contiguous ("KMAJ", LDS image [rows][64] with a
-// 16-byte-chunk XOR swizzle, fragments via ds_read_b128) or MN-contiguous
-// (LDS image [64 k][128 rows], 256-byte rows with the T10 XOR, fragments via
-// ds_read_b64_tr_b16 -- the hardware transpose read), so all four transpose
-// modes and the three conv passes use the same main loop with no transpose
-// pass over memory.
-//
-// Geometry: 128x128x64 block tile, 256 threads = 4 waves (2 M x 2 N), each wave
-// 64x64 = 4x4 mfma_f32_16x16x32_bf16 tiles; LDS double buffer (2 x 32 KiB)
-// filled by global_load_lds (16 B/lane, swizzle applied on the source address),
-// tile k+1 in flight during the MFMAs of tile k, one barrier per K-tile.  Operand roles are swapped (A_op = N side, B_op = M side) so the
-// accumulator holds 4 consecutive N columns per lane -> 8/16-byte stores.
-// Block ids are remapped so that consecutive tiles share an XCD's L2, then
-// grouped 8 tiles along M for operand reuse.  Split-K over gridDim.z with
-// fp32 atomics for the long-K weight-gradient GEMMs.
-#include "common.h"
-#include <algorithm>
+// Addmm.cu:29, Baddbmm.cu:37), SURVEY.md §2.7.  This unit instantiates the
+// K % 64 == 0 kernels; gemm_ktail.hip the ragged-K ones.
+#include "gemm_core.h"
 
 namespace hetu {
 namespace gemm {
-
-typedef short v4s __attribute__((ext_vector_type(4)));
-typedef short v8s __attribute__((ext_vector_type(8)));
-typedef float v4f __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4s lds_v4s;
-
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_BYTES = 128 * BK * 2;  // 16 KiB per operand tile
-
-// n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery): the implicit-GEMM
-// loaders decompose pixel / tap indices per lane per K-tile, where a hardware-less
-// 32-bit integer division would cost ~40 VALU ops each.
-struct FastDiv {
-  uint32_t d, m, l;
-  __host__ __device__ FastDiv() : d(1), m(1), l(0) {}
-  __host__ __device__ explicit FastDiv(uint32_t dv) : d(dv < 1 ? 1 : dv) {
-    l = 0;
-    while (l < 31 && (1u << l) < d) ++l;
-    m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
-  }
-  __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> l; }
-};
-
-// Default per-block problem view: the whole M x K problem, rows stored linearly.
-// Loaders that split the problem into classes over blockIdx.y (strided dgrad)
-// override rows_eff / k_eff / out_row.
-#define HETU_LINEAR_ROWS                                             \
-  __device__ int64_t rows_eff(int64_t M_) const { return M_; }        \
-  __device__ int64_t k_eff(int64_t K_) const { return K_; }           \
-  __device__ int64_t out_row(int64_t m_) const { return m_; }
-
-
-
-
-// ---- LDS images -------------------------------------------------------------------------
-// K-major: [128 rows][64 k] bf16, 128-B rows, chunk c (0..7) of row r at ((c ^ (r&7)) << 4)
-__device__ __forceinline__ int offk(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
-// MN-major: [64 k][128 cols] bf16, 256-B rows, chunk c (0..15), T10 image (b)
-__device__ __forceinline__ int offmn(int k, int c) {
-  return k * 256 + ((c ^ (((k & 3) << 2) | ((k >> 2) & 3))) << 4);
-}
-
-// Zero chunk that out-of-range / padding lanes stage from (global_load_lds has no
-// per-lane predicate: the lane still writes its LDS slot, so it reads zeros).
-__device__ __attribute__((aligned(64))) bf16 g_zero_chunk[32];
-
-__device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
-// fragment of 16 rows (row block rb) x 32 k (k-step s): lane holds row (lane&15),
-// k = 32s + 8(lane>>4) + j, j = 0..7
-template <bool KMAJ>
-__device__ __forceinline__ v8s lds_frag(const char* lds, int rb, int s, int lane) {
-  if constexpr (KMAJ) {
-    int r = rb * 16 + (lane & 15);
-    int c = s * 4 + (lane >> 4);
-    return *reinterpret_cast<const v8s*>(lds + offk(r, c));
-  } else {
-    int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    int c = rb * 2 + (p >> 1);
-    int k1 = s * 32 + 8 * g + q;
-    const char* a1 = lds + offmn(k1, c) + 8 * (p & 1);
-    const char* a2 = lds + offmn(k1 + 4, c) + 8 * (p & 1);
-    v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
-    v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
-    return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
-  }
-}
-
-// ---- operand loaders ------------------------------------------------------------------
-// The 128x64 tile is staged by 16 global_load_lds instructions (4 per wave), each
-// filling 1 KiB of LDS lane-linearly: instruction i of wave w covers LDS bytes
-// [4096w + 1024i, +1024).  The swizzle is applied on the SOURCE side: lane l of
-// that instruction fetches the logical chunk that belongs at its physical slot.
-//   KMAJ: row r = 32w + 8i + (l>>3), physical chunk l&7, logical c = (l&7) ^ (l>>3)
-//   MN  : k   = 16w + 4i + (l>>4), physical chunk l&15, logical
-//         c = (l&15) ^ (((l>>4)&3)<<2 | i)
-// Loaders return, per instruction i, the global address of that chunk (or the
-// zero chunk).
-
-__device__ __forceinline__ const bf16* zchunk() { return g_zero_chunk; }
-
-// Which slot of the staged tile load i of wave w, lane l fills.  `map`:
-//  0  128x128 kernel (4 waves): one 128-row image per operand, 4 loads per wave.
-//  1  256x256 kernel, A operand (2 wave rows x 128 rows, sub-tiles of 64 rows)
-//  2  256x256 kernel, B operand (4 wave columns x 64, sub-tiles of 32)
-//  For 1/2 each operand is staged as two 128-row "half-tile" images (2 loads per wave
-//  each); half h holds the rows every wave reads in ITS h-th sub-tile, so a half can be
-//  restaged as soon as the phase that reads it has passed (gemm_big_kernel).
-__device__ __forceinline__ int half_to_rel(int map, int h, int x) {
-  return map == 1 ? (x >> 6) * 128 + h * 64 + (x & 63) : (x >> 5) * 64 + h * 32 + (x & 31);
-}
-// K-major: returns the operand row (relative to the tile) of the lane's 16-B chunk.
-__device__ __forceinline__ int kmaj_row(int map, int w, int i, int l) {
-  if (map == 0) return 32 * w + 8 * i + (l >> 3);
-  return half_to_rel(map, i >> 1, 16 * w + 8 * (i & 1) + (l >> 3));
-}
-// MN-major: k row of the image and operand column (relative) of the lane's chunk.
-__device__ __forceinline__ void mn_slot(int map, int w, int i, int l, int& k, int& col) {
-  k = map ? 8 * w + 4 * (i & 1) + (l >> 4) : 16 * w + 4 * i + (l >> 4);
-  const int c = (l & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3));  // T10 image, logical chunk
-  col = map ? half_to_rel(map, i >> 1, 8 * c) : 8 * c;
-}
-
-// plain row-major operand with contiguous K: element (r, k) at base[r*ld + k]
-struct PlainK {
-  HETU_LINEAR_ROWS
-  static constexpr bool KMAJ = true;
-  const bf16* base; int64_t ld, rows, K, bstride;
-  int64_t roff[4]; bool rok[4]; int ch;
-  __device__ void init(int64_t r0, int w, int l, int64_t batch, int big) {
-    base += batch * bstride;
-    ch = (l & 7) ^ (l >> 3);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + kmaj_row(big, w, i, l);
-      rok[i] = r < rows;
-      roff[i] = r * ld;
-    }
-  }
-  __device__ const bf16* src(int64_t k0, int i) const {
-    int64_t k = k0 + ch * 8;
-    return (rok[i] && k < K) ? base + roff[i] + k : zchunk();
-  }
-};
-
-// plain operand stored [K][rows]: element (r, k) at base[k*ld + r]
-struct PlainMN {
-  HETU_LINEAR_ROWS
-  static constexpr bool KMAJ = false;
-  const bf16* base; int64_t ld, rows, K, bstride;
-  int64_t col[4]; bool cok[4]; int kk[4];
-  __device__ void init(int64_t r0, int w, int l, int64_t batch, int big) {
-    base += batch * bstride;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int c;
-      mn_slot(big, w, i, l, kk[i], c);
-      col[i] = r0 + c;
-      cok[i] = col[i] < rows;
-    }
-  }
-  __device__ const bf16* src(int64_t k0, int i) const {
-    int64_t k = k0 + kk[i];
-    return (cok[i] && k < K) ? base + k * ld + col[i] : zchunk();
-  }
-};
-
-struct ConvGeom {
-  int N, H, W, C, K, KH, KW, sh, sw, ph, pw, OH, OW;  // C = in channels, K = out channels
-  FastDiv fOW, fOH, fC, fK, fKW;
-  // reduction channels (C forward, K data-gradient) a multiple of the 64-wide
-  // K-tile: every K-tile lies inside ONE filter tap, so the tap decomposition is
-  // wave-uniform (scalar ALU, once per tile) and each lane only adds offsets
-  int ctap;
-};
-
-// forward, M side: rows = output pixels, k = (kh, kw, ci), ci fastest
-struct ConvFwdA {
-  HETU_LINEAR_ROWS
-  static constexpr bool KMAJ = true;
-  const bf16* x; ConvGeom g; int64_t Ktot, rows;
-  int nb[4]; int ih0[4], iw0[4]; bool rok[4]; int ch;
-  int64_t pix[4];  // element offset of (n, ih0, iw0, 0); dereferenced only in bounds
-  __device__ void init(int64_t r0, int w, int l, int64_t, int big) {
-    ch = (l & 7) ^ (l >> 3);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + kmaj_row(big, w, i, l);
-      rok[i] = r < rows;
-      uint32_t rr = rok[i] ? (uint32_t)r : 0;
-      uint32_t t = g.fOW.div(rr);
-      int ow = (int)(rr - t * g.OW);
-      uint32_t n = g.fOH.div(t);
-      int oh = (int)(t - n * g.OH);
-      nb[i] = (int)n * g.H;
-      ih0[i] = oh * g.sh - g.ph;
-      iw0[i] = ow * g.sw - g.pw;
-      pix[i] = ((int64_t)(nb[i] + ih0[i]) * g.W + iw0[i]) * g.C;
-    }
-  }
-  __device__ const bf16* src(int64_t k0, int i) const {
-    if (g.ctap) {
-      // tap, kh, kw uniform over the tile (k0 is wave-uniform)
-      const uint32_t tap = g.fC.div((uint32_t)k0);
-      const int ci = (int)((uint32_t)k0 - tap * g.C) + ch * 8;
-      const uint32_t kh = g.fKW.div(tap);
-      const int kw = (int)(tap - kh * g.KW);
-      const int ih = ih0[i] + (int)kh, iw = iw0[i] + kw;
-      const bool ok = k0 < Ktot && rok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      return ok ? x + pix[i] + ((int64_t)kh * g.W + kw) * g.C + ci : zchunk();
-    }
-    uint32_t k = (uint32_t)k0 + ch * 8;
-    uint32_t tap = g.fC.div(k);
-    int ci = (int)(k - tap * g.C);
-    uint32_t kh = g.fKW.div(tap);
-    int kw = (int)(tap - kh * g.KW);
-    int ih = ih0[i] + (int)kh, iw = iw0[i] + kw;
-    bool ok = k < Ktot && rok[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-    return ok ? x + ((int64_t)(nb[i] + ih) * g.W + iw) * g.C + ci : zchunk();
-  }
-};
-
-// Data gradient, split into sh*sw stride classes over blockIdx.y.  Class (a, b)
-// holds the input pixels with ih % sh == a, iw % sw == b; only the taps with
-// kh == (a + ph) mod sh (step sh), kw likewise, reach an output pixel, so each
-// class is a dense implicit GEMM over exactly its useful taps (no zero-filled
-// K-tiles, no divisibility tests).  Stride 1 is the single class (0, 0).
-struct DgradClass {
-  int a, b, kh0, kw0, nth, ntw, Hc, Wc, cbh, cbw;
-  FastDiv fWc, fHc, fntw;
-  __device__ void make(const ConvGeom& g, int cls) {
-    a = cls / g.sw;
-    b = cls - a * g.sw;
-    Hc = a < g.H ? (g.H - a + g.sh - 1) / g.sh : 0;
-    Wc = b < g.W ? (g.W - b + g.sw - 1) / g.sw : 0;
-    kh0 = (a + g.ph) % g.sh;
-    kw0 = (b + g.pw) % g.sw;
-    nth = kh0 < g.KH ? (g.KH - kh0 + g.sh - 1) / g.sh : 0;
-    ntw = kw0 < g.KW ? (g.KW - kw0 + g.sw - 1) / g.sw : 0;
-    // (a + ph - kh0) is a multiple of sh: output row of class row i and class tap th
-    // is oh = i + cbh - th exactly (no per-lane division by the stride)
-    cbh = (a + g.ph) / g.sh;
-    cbw = (b + g.pw) / g.sw;
-    fWc = FastDiv((uint32_t)Wc);
-    fHc = FastDiv((uint32_t)Hc);
-    fntw = FastDiv((uint32_t)ntw);
-  }
-};
-
-// data gradient, M side: rows = class pixels (n, i, j), k = (tap in class, co)
-struct ConvDgradA {
-  static constexpr bool KMAJ = true;
-  const bf16* dy; ConvGeom g;
-  DgradClass c;
-  int nb[4]; int ii[4], jj[4]; bool rok[4]; int ch;
-  int64_t mrows, kdim;
-  __device__ int64_t rows_eff(int64_t) const { return mrows; }
-  __device__ int64_t k_eff(int64_t) const { return kdim; }
-  __device__ int64_t out_row(int64_t m) const {
-    uint32_t t = c.fWc.div((uint32_t)m);
-    int j = (int)((uint32_t)m - t * c.Wc);
-    uint32_t n = c.fHc.div(t);
-    int i = (int)(t - n * c.Hc);
-    return ((int64_t)n * g.H + c.a + g.sh * i) * g.W + c.b + g.sw * j;
-  }
-  __device__ void init(int64_t r0, int w, int l, int64_t cls, int big) {
-    c.make(g, (int)cls);
-    mrows = (int64_t)g.N * c.Hc * c.Wc;
-    kdim = (int64_t)c.nth * c.ntw * g.K;
-    ch = (l & 7) ^ (l >> 3);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t r = r0 + kmaj_row(big, w, i, l);
-      rok[i] = r < mrows;
-      uint32_t rr = rok[i] ? (uint32_t)r : 0;
-      uint32_t t = c.fWc.div(rr);
-      int j = (int)(rr - t * c.Wc);
-      uint32_t n = c.fHc.div(t);
-      ii[i] = (int)(t - n * c.Hc) + c.cbh;
-      jj[i] = j + c.cbw;
-      nb[i] = (int)n * g.OH;
-    }
-  }
-  __device__ const bf16* src(int64_t k0, int i) const {
-    uint32_t tap, co;
-    if (g.ctap) {                     // K % 64 == 0: one tap per K-tile (scalar)
-      tap = g.fK.div((uint32_t)k0);
-      co = (uint32_t)k0 - tap * g.K + ch * 8;
-    } else {
-      uint32_t k = (uint32_t)k0 + ch * 8;
-      tap = g.fK.div(k);
-      co = k - tap * g.K;
-    }
-    uint32_t th = c.fntw.div(tap);
-    int tw = (int)(tap - th * c.ntw);
-    int oh = ii[i] - (int)th, ow = jj[i] - tw;
-    bool ok = (int64_t)k0 + (g.ctap ? 0 : ch * 8) < kdim && rok[i] && (unsigned)oh < (unsigned)g.OH &&
-              (unsigned)ow < (unsigned)g.OW;
-    return ok ? dy + ((int64_t)(nb[i] + oh) * g.OW + ow) * g.K + co : zchunk();
-  }
-};
-
-// data gradient, N side: cols = ci, k rows = (tap in class, co): w[co][kh][kw][ci]
-struct ConvDgradB {
-  HETU_LINEAR_ROWS
-  static constexpr bool KMAJ = false;
-  const bf16* w; ConvGeom g;
-  DgradClass c;
-  int64_t kdim;
-  int col[4]; bool cok[4]; int kk[4];
-  __device__ void init(int64_t r0, int wv, int l, int64_t cls, int big) {
-    c.make(g, (int)cls);
-    kdim = (int64_t)c.nth * c.ntw * g.K;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int cc;
-      mn_slot(big, wv, i, l, kk[i], cc);
-      col[i] = (int)r0 + cc;
-      cok[i] = col[i] < g.C;
-    }
-  }
-  __device__ const bf16* src(int64_t k0, int i) const {
-    uint32_t k = (uint32_t)k0 + kk[i];
-    uint32_t tap;
-    int co;
-    if (g.ctap) {                     // tap uniform over the K-tile
-      tap = g.fK.div((uint32_t)k0);
-      co = (int)(k - tap * g.K);
-    } else {
-      tap = g.fK.div(k);
-      co = (int)(k - tap * g.K);
-    }
-    uint32_t th = c.fntw.div(tap);
-    int tw = (int)(tap - th * c.ntw);
-    int kh = c.kh0 + g.sh * (int)th, kw = c.kw0 + g.sw * tw;
-    return (cok[i] && (int64_t)k < kdim)
-               ? w + ((int64_t)co * (g.KH * g.KW) + kh * g.KW + kw) * g.C + col[i]
-               : zchunk();
-  }
-};
-
-// weight gradient, N side: cols = (kh, kw, ci), k rows = output pixels
-struct ConvWgradB {
-  HETU_LINEAR_ROWS
-  static constexpr bool KMAJ = false;
-  const bf16* x; ConvGeom g; int64_t P;  // P = N*OH*OW
-  int kh[4], kw[4], ci[4]; bool cok[4]; int kk[4];
-  __device__ void init(int64_t r0, int w, int l, int64_t, int big) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int c;
-      mn_slot(big, w, i, l, kk[i], c);
-      int col = (int)r0 + c;
-      cok[i] = col < g.KH * g.KW * g.C;
-      int tap = col / g.C;
-      ci[i] = col - tap * g.C;
-      kh[i] = tap / g.KW;
-      kw[i] = tap - kh[i] * g.KW;
-    }
-  }
-  __device__ const bf16* src(int64_t k0, int i) const {
-    uint32_t p = (uint32_t)k0 + kk[i];
-    uint32_t t = g.fOW.div(p);
-    int ow = (int)(p - t * g.OW);
-    uint32_t n = g.fOH.div(t);
-    int oh = (int)(t - n * g.OH);
-    int ih = oh * g.sh - g.ph + kh[i], iw = ow * g.sw - g.pw + kw[i];
-    bool ok = cok[i] && (int64_t)p < P && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-    return ok ? x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + ci[i] : zchunk();
-  }
-};
-
-// ---- epilogue ------------------------------------------------------------------------
-struct Epi {
-  void* C; const void* Cin; const float* bias;
-  int64_t ldc, ldcin, sC, sCin;
-  float alpha, beta;
-  int act;        // 0 none, 1 relu, 2 gelu(erf)
-  int out_f32;    // C dtype
-  int cin_f32;    // Cin dtype
-  int atomic;     // fp32 atomicAdd into C (split-K / accumulate)
-  int bias_on_m;  // bias indexed by m instead of n
-  float* slab;    // split-K: fp32 partial tiles, slab z at slab + z*slab_stride (ld = N)
-  int64_t slab_stride;
-  // per-column sum / sum of squares of the stored outputs (fp32 atomics into
-  // colstats[0..N) and colstats[N..2N), pre-zeroed): the BatchNorm statistics of a
-  // convolution output, fused into the epilogue that already holds the values
-  float* colstats;
-};
-
-// column statistics of one epilogue: each thread holds sums of its 8 columns over
-// its rows; threads sharing columns are folded by lane shuffles (lanes l ^ 16k within
-// a wave), then across waves through LDS, one atomic per column per block.
-//   groups: threads per row (16 for the 128-wide tile, 32 for the 256-wide tile)
-template <int GROUPS, int NWAVES>
-__device__ __forceinline__ void epilogue_colstats(float (&cs)[8], float (&cq)[8], float* lds, int tid,
-                                                  int64_t n0, int64_t N, float* colstats) {
-  const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-#pragma unroll
-    for (int o = GROUPS; o < 64; o <<= 1) {
-      cs[t] += __shfl_xor(cs[t], o, 64);
-      cq[t] += __shfl_xor(cq[t], o, 64);
-    }
-  }
-  __syncthreads();   // the staging area is free again
-  if (lane < GROUPS) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      lds[(wave * GROUPS + lane) * 8 + t] = cs[t];
-      lds[NWAVES * GROUPS * 8 + (wave * GROUPS + lane) * 8 + t] = cq[t];
-    }
-  }
-  __syncthreads();
-  if (tid < GROUPS * 8) {
-    float S = 0.f, Q = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWAVES; ++w) {
-      S += lds[w * GROUPS * 8 + tid];
-      Q += lds[NWAVES * GROUPS * 8 + w * GROUPS * 8 + tid];
-    }
-    const int64_t n = n0 + tid;
-    if (n < N) {
-      unsafeAtomicAdd(colstats + n, S);
-      unsafeAtomicAdd(colstats + N + n, Q);
-    }
-  }
-}
-
-__device__ __forceinline__ float act_f(float v, int act) {
-  if (act == 1) return v > 0.f ? v : 0.f;
-  if (act == 2) return 0.5f * v * (1.f + erff(v * 0.70710678118f));
-  return v;
-}
-
-template <class LA, class LB, bool DB>
-__global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
-                                                  int64_t K, int tiles_m, int tiles_n, int ktps) {
-  // DB: 2 x 32 KiB double buffer; !DB: one 32 KiB buffer when every block owns a
-  // single K-tile (short-K 1x1 convolutions: more resident blocks per CU)
-  __shared__ __attribute__((aligned(16))) char smem_raw[DB ? 4 * TILE_BYTES : 64 * (BN + 4) * 4];
-  constexpr int buf_stride = DB ? 2 * TILE_BYTES : 0;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
-
-  // XCD-aware bijective remap, then group-of-8 along M for L2 reuse
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int GROUP = 8;
-  const int per_group = GROUP * tiles_n;
-  const int gid = wg / per_group, first_m = gid * GROUP;
-  const int gsz = min(tiles_m - first_m, GROUP);
-  const int tm = first_m + (wg % per_group) % gsz;
-  const int tn = (wg % per_group) / gsz;
-
-  const int64_t batch = blockIdx.y;
-  la.init((int64_t)tm * BM, wave, lane, batch, 0);
-  lb.init((int64_t)tn * BN, wave, lane, batch, 0);
-  // per-block problem view (a stride class of a strided dgrad may be smaller)
-  const int64_t Mb = la.rows_eff(M);
-  if ((int64_t)tm * BM >= Mb) return;  // block-uniform, before any barrier
-  K = la.k_eff(K);
-
-  const int nkt = (int)((K + BK - 1) / BK);
-  const int kt0 = blockIdx.z * ktps;
-  const int kt1 = min(kt0 + ktps, nkt);
-
-  v4f acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  // stage K-tile kt into LDS buffer b: 4 + 4 global_load_lds per wave
-  auto stage = [&](int kt, int b) {
-    char* As = smem_raw + b * buf_stride + 4096 * wave;
-    char* Bs = As + TILE_BYTES;
-    const int64_t k0 = (int64_t)kt * BK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(la.src(k0, i), As + 1024 * i);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(lb.src(k0, i), Bs + 1024 * i);
-  };
-
-  if (kt0 < kt1) stage(kt0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
-    const char* As = smem_raw + cur * buf_stride;
-    const char* Bs = As + TILE_BYTES;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      v8s mf[4], nf[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) mf[i] = lds_frag<LA::KMAJ>(As, wm * 4 + i, s, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nf[j] = lds_frag<LB::KMAJ>(Bs, wn * 4 + j, s, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[j], mf[i], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  // epilogue: lane holds C[m][n..n+3]
-  if (ep.slab) {  // split-K partial: plain fp32 stores into this slice's slab
-    float* S = ep.slab + blockIdx.z * ep.slab_stride;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
-      if (m >= Mb) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
-        if (n >= N) continue;
-        float* d = S + m * N + n;
-        if (n + 3 < N && (N & 3) == 0) {
-          *reinterpret_cast<float4*>(d) =
-              make_float4(acc[i][j][0] * ep.alpha, acc[i][j][1] * ep.alpha, acc[i][j][2] * ep.alpha,
-                          acc[i][j][3] * ep.alpha);
-        } else {
-          for (int t = 0; t < 4; ++t)
-            if (n + t < N) d[t] = acc[i][j][t] * ep.alpha;
-        }
-      }
-    }
-    return;
-  }
-  char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
-  const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
-  if (!ep.atomic) {
-    float cs[8], cq[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) { cs[t] = 0.f; cq[t] = 0.f; }
-    // Row-coalesced epilogue: the tile goes through LDS in two 64-row halves
-    // (fp32, rows padded by 4 floats so the 16-row MFMA write pattern spreads
-    // over the banks), then 16 lanes cover one 128-column row with 8 elements
-    // each: full 256-byte bf16 rows per instruction instead of 16 scattered
-    // 32-byte pieces, and the same for the Cin (residual / beta) read.
-    constexpr int SROW = BN + 4;
-    float* stg = reinterpret_cast<float*>(smem_raw);
-    const bool cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)Cb & 15) == 0)
-                                 : ((ep.ldc & 7) == 0 && ((uintptr_t)Cb & 15) == 0);
-    const bool ivec = Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)Cinb & 15) == 0)
-                                          : ((ep.ldcin & 7) == 0 && ((uintptr_t)Cinb & 15) == 0));
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (wm == half) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = i * 16 + (lane & 15), c = wn * 64 + j * 16 + 4 * (lane >> 4);
-            *reinterpret_cast<v4f*>(stg + r * SROW + c) = acc[i][j];
-          }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int pss = 0; pss < 4; ++pss) {
-        const int r = pss * 16 + (tid >> 4), c = (tid & 15) * 8;
-        const int64_t m = (int64_t)tm * BM + half * 64 + r;
-        const int64_t n = (int64_t)tn * BN + c;
-        if (m >= Mb || n >= N) continue;
-        const int64_t orow = la.out_row(m);
-        float v[8];
-        {
-          v4f a0 = *reinterpret_cast<const v4f*>(stg + r * SROW + c);
-          v4f a1 = *reinterpret_cast<const v4f*>(stg + r * SROW + c + 4);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
-        }
-        const bool full = n + 7 < N;
-        if (ep.bias) {
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            v[t] += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
-        }
-        if (Cinb) {
-          const int64_t o = orow * ep.ldcin + n;
-          float cv[8];
-          if (ivec && full) {
-            if (ep.cin_f32) {
-              float4 c0 = *reinterpret_cast<const float4*>((const float*)Cinb + o);
-              float4 c1 = *reinterpret_cast<const float4*>((const float*)Cinb + o + 4);
-              cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
-              cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
-            } else {
-              load_vec<bf16>((const bf16*)Cinb + o, cv);
-            }
-          } else {
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-              cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)Cinb)[o + t]
-                                              : to_f(((const bf16*)Cinb)[o + t])) : 0.f;
-          }
-#pragma unroll
-          for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
-        const int64_t o = orow * ep.ldc + n;
-        if (ep.out_f32) {
-          float* Cf = (float*)Cb + o;
-          if (cvec && full) {
-            *reinterpret_cast<float4*>(Cf) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<float4*>(Cf + 4) = make_float4(v[4], v[5], v[6], v[7]);
-          } else {
-            for (int t = 0; t < 8; ++t)
-              if (n + t < N) Cf[t] = v[t];
-          }
-        } else {
-          bf16* Ch = (bf16*)Cb + o;
-          if (cvec && full) {
-            store_vec<bf16>(Ch, v);
-          } else {
-            for (int t = 0; t < 8; ++t)
-              if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
-          }
-        }
-        if (ep.colstats) {   // statistics of the values as stored
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));
-            cs[t] += sv;
-            cq[t] += sv * sv;
-          }
-        }
-      }
-      __syncthreads();
-    }
-    if (ep.colstats)
-      epilogue_colstats<16, 4>(cs, cq, stg, tid, (int64_t)tn * BN, N, ep.colstats);
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
-    if (m >= Mb) continue;
-    const int64_t orow = la.out_row(m);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= N) continue;
-      float v[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        float x = acc[i][j][t] * ep.alpha;
-        if (ep.bias) x += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
-        if (Cinb && n + t < N) {
-          int64_t o = orow * ep.ldcin + n + t;
-          float c = ep.cin_f32 ? ((const float*)Cinb)[o] : to_f(((const bf16*)Cinb)[o]);
-          x += ep.beta * c;
-        }
-        v[t] = act_f(x, ep.act);
-      }
-      const int64_t o = orow * ep.ldc + n;
-      if (ep.atomic) {
-        float* Cf = (float*)Cb;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (n + t < N) unsafeAtomicAdd(Cf + o + t, v[t]);
-      } else if (ep.out_f32) {
-        float* Cf = (float*)Cb;
-        if (n + 3 < N && (o & 3) == 0) {
-          *reinterpret_cast<float4*>(Cf + o) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-          for (int t = 0; t < 4; ++t)
-            if (n + t < N) Cf[o + t] = v[t];
-        }
-      } else {
-        unsigned short* Ch = (unsigned short*)Cb;
-        if (n + 3 < N && (o & 3) == 0) {
-          uint2 pk;
-          pk.x = (uint32_t)f_to_bf16_bits(v[0]) | ((uint32_t)f_to_bf16_bits(v[1]) << 16);
-          pk.y = (uint32_t)f_to_bf16_bits(v[2]) | ((uint32_t)f_to_bf16_bits(v[3]) << 16);
-          *reinterpret_cast<uint2*>(Ch + o) = pk;
-        } else {
-          for (int t = 0; t < 4; ++t)
-            if (n + t < N) Ch[o + t] = f_to_bf16_bits(v[t]);
-        }
-      }
-    }
-  }
-}
-
-// ---- 256x256 tile, 8 waves, phase-interleaved K loop -----------------------------------
-// Block tile 256x256x64, 512 threads = 8 waves as 2 (M) x 4 (N); wave tile 128x64 =
-// 8 x 4 mfma_f32_16x16x32_bf16 tiles (128 fp32 accumulators per lane).  LDS = 2 K-tile
-// buffers x 4 half-tile images of 16 KiB (A rows / B columns each wave reads in its
-// sub-tile 0 or 1; kmaj_row / mn_slot) = 128 KiB, one block per CU, 2 waves per SIMD.
-// Every K-tile runs as 4 phases; each phase reads one register sub-tile from LDS,
-// stages ONE half-tile (2 global_load_lds per thread) 7 half-tiles ahead, and runs the
-// 16 MFMAs of one 64x32 quadrant of the wave tile between two raw s_barriers.  The DMA
-// stays in flight across the barriers (counted vmcnt, never 0 in the loop): the
-// buffer for K-tile t+1 is retired by the wait in the last phase of K-tile t.
-//   phase 0: read A-sub0 + B-sub0, MMA (A0,B0)     restage (K-tile t+2, same buffer):
-//   phase 1: read B-sub1,          MMA (A0,B1)       A-half0 in phase 1, B-half1 in 2,
-//   phase 2: read A-sub1,          MMA (A1,B1)       A-half1 in 3, B-half0 in phase 0
-//   phase 3: read B-sub0,          MMA (A1,B0)       of t+1: one phase after last read
-constexpr int BIG = 256, BIG_NT = 512;
-constexpr int HALF_BYTES = 128 * BK * 2;       // 16 KiB
-constexpr int BUF_BYTES = 4 * HALF_BYTES;       // A-h0, A-h1, B-h0, B-h1
-
-__device__ __forceinline__ void vm_wait_halves(int n) {
-  // wait until at most n half-tiles (2 DMA each) of this wave are still in flight
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-  }
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("" ::: "memory");
-}
-
-// ablation knobs for profiling (hetu_gemm_big_variant; 0 in production):
-//  1 no wave-group stagger, 4 no s_setprio, 8 skip the DMA issue, 16 skip the MFMAs
-static int g_big_variant = 0;
-
-template <class LA, class LB>
-__global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
-                                                             int64_t K, int tiles_m, int tiles_n, int ktps,
-                                                             int var) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int GROUP = 8;
-  const int per_group = GROUP * tiles_n;
-  const int gid = wg / per_group, first_m = gid * GROUP;
-  const int gsz = min(tiles_m - first_m, GROUP);
-  const int tm = first_m + (wg % per_group) % gsz;
-  const int tn = (wg % per_group) / gsz;
-
-  const int64_t batch = blockIdx.y;
-  la.init((int64_t)tm * BIG, wave, lane, batch, 1);
-  lb.init((int64_t)tn * BIG, wave, lane, batch, 2);
-  const int64_t Mb = la.rows_eff(M);
-  if ((int64_t)tm * BIG >= Mb) return;  // block-uniform, before any barrier
-  K = la.k_eff(K);
-  const int nkt = (int)((K + BK - 1) / BK);
-  const int kt0 = blockIdx.z * ktps;
-  const int nk = max(0, min(kt0 + ktps, nkt) - kt0);
-  const int nh = 4 * nk;                 // half-tiles to stage
-
-  v4f acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  // half-tile j: K-tile j>>2, staging order A-h0, B-h1, A-h1, B-h0 (the order the
-  // phases of the previous use of the buffer finish reading them, see below)
-  auto issue = [&](int j) {
-    if (j >= nh || (var & 8)) return;
-    const int t = j >> 2, which = j & 3;
-    const int64_t k0 = (int64_t)(kt0 + t) * BK;
-    char* buf = smem + (t & 1) * BUF_BYTES;
-    const bool isA = (which & 1) == 0;
-    const int h = isA ? (which >> 1) : (which == 1 ? 1 : 0);
-    char* dst = buf + (isA ? 0 : 2 * HALF_BYTES) + h * HALF_BYTES + 2048 * wave;
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
-      const bf16* src = isA ? la.src(k0, 2 * h + ii) : lb.src(k0, 2 * h + ii);
-      glds16(src, dst + 1024 * ii);
-    }
-  };
-  // half-tiles issued after the last half of K-tile t (at most 3 in flight)
-  auto younger_than_tile = [&](int t, int issued) { return max(0, min(3, issued - 4 * (t + 1))); };
-
-#pragma clang loop unroll(full)
-  for (int j = 0; j < 7; ++j) issue(j);   // unrolled: loader arrays stay in registers
-  int issued = min(7, nh);
-  vm_wait_halves(younger_than_tile(0, issued));
-  raw_barrier();
-  // Ping-pong: the wave-row-1 group runs one barrier behind the wave-row-0 group, so on
-  // every SIMD (one wave of each group) one wave's 16 MFMAs overlap the other wave's
-  // LDS reads / DMA issue / waits.  Each phase ends its reads with lgkmcnt(0) BEFORE its
-  // first barrier, so a half is restaged one phase after the phase that last read it.
-  if (wr == 1 && !(var & 1)) raw_barrier();
-
-  v8s fa[2][4][2], fb[2][2][2];   // [sub][row/col block][k-step]
-#pragma unroll 1
-  for (int t = 0; t < nk; ++t) {
-    const char* buf = smem + (t & 1) * BUF_BYTES;
-    const char* Ah[2] = {buf, buf + HALF_BYTES};
-    const char* Bh[2] = {buf + 2 * HALF_BYTES, buf + 3 * HALF_BYTES};
-#pragma clang loop unroll(full)
-    for (int p = 0; p < 4; ++p) {
-      // phase p reads: 0: B-sub0 + A-sub0, 1: B-sub1, 2: A-sub1, 3: B-sub0 again
-      if (p == 0 || p == 3) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fb[0][jj][s2] = lds_frag<LB::KMAJ>(Bh[0], wc * 2 + jj, s2, lane);
-      }
-      if (p == 0) {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fa[0][ii][s2] = lds_frag<LA::KMAJ>(Ah[0], wr * 4 + ii, s2, lane);
-      } else if (p == 1) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fb[1][jj][s2] = lds_frag<LB::KMAJ>(Bh[1], wc * 2 + jj, s2, lane);
-      } else if (p == 2) {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) fa[1][ii][s2] = lds_frag<LA::KMAJ>(Ah[1], wr * 4 + ii, s2, lane);
-      }
-      issue(4 * t + p + 7);
-      if (p == 3) {
-        issued = min(4 * t + 11, nh);
-        vm_wait_halves(younger_than_tile(t + 1, issued));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      raw_barrier();
-      const int sa = (p < 2) ? 0 : 1;
-      const int sb = (p == 0 || p == 3) ? 0 : 1;
-      if (!(var & 4)) __builtin_amdgcn_s_setprio(1);
-      if (!(var & 16)) {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-              acc[sa * 4 + ii][sb * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  fb[sb][jj][s2], fa[sa][ii][s2], acc[sa * 4 + ii][sb * 2 + jj], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            asm volatile("" :: "v"(fa[sa][ii][0]), "v"(fa[sa][ii][1]), "v"(fb[sb][jj][0]), "v"(fb[sb][jj][1]));
-      }
-      __builtin_amdgcn_s_setprio(0);
-      raw_barrier();
-    }
-  }
-  if (wr == 0 && !(var & 1)) raw_barrier();   // re-align the two groups
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // epilogue: lane holds C[m][n..n+3] of acc[i][j],
-  //   m = tm*256 + wr*128 + 16i + (lane&15), n = tn*256 + wc*64 + 16j + 4(lane>>4)
-  if (ep.slab || ep.atomic) {
-    float* S = ep.slab ? ep.slab + blockIdx.z * ep.slab_stride : nullptr;
-    char* Cb = (char*)ep.C + batch * ep.sC * 4;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t m = (int64_t)tm * BIG + wr * 128 + i * 16 + (lane & 15);
-      if (m >= Mb) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = (int64_t)tn * BIG + wc * 64 + j * 16 + 4 * (lane >> 4);
-        if (n >= N) continue;
-        if (S) {
-          float* d = S + m * N + n;
-          if (n + 3 < N && (N & 3) == 0) {
-            *reinterpret_cast<float4*>(d) = make_float4(acc[i][j][0] * ep.alpha, acc[i][j][1] * ep.alpha,
-                                                        acc[i][j][2] * ep.alpha, acc[i][j][3] * ep.alpha);
-          } else {
-            for (int t = 0; t < 4; ++t)
-              if (n + t < N) d[t] = acc[i][j][t] * ep.alpha;
-          }
-        } else {
-          float* Cf = (float*)Cb + la.out_row(m) * ep.ldc + n;
-          for (int t = 0; t < 4; ++t)
-            if (n + t < N) unsafeAtomicAdd(Cf + t, acc[i][j][t] * ep.alpha);
-        }
-      }
-    }
-    return;
-  }
-  char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
-  const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
-  constexpr int SROW = BIG + 4;
-  float* stg = reinterpret_cast<float*>(smem);
-  const bool cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)Cb & 15) == 0)
-                               : ((ep.ldc & 7) == 0 && ((uintptr_t)Cb & 15) == 0);
-  const bool ivec = Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)Cinb & 15) == 0)
-                                        : ((ep.ldcin & 7) == 0 && ((uintptr_t)Cinb & 15) == 0));
-  float cs[8], cq[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) { cs[t] = 0.f; cq[t] = 0.f; }
-  // 4 passes of 64 rows through LDS (64 x 260 fp32 = 66.5 KiB), full-row stores
-#pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
-    if (wr == (pass >> 1)) {
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = (pass & 1) * 4 + ii;
-          const int rr = ii * 16 + (lane & 15), c = wc * 64 + j * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<v4f*>(stg + rr * SROW + c) = acc[i][j];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int sp = 0; sp < 4; ++sp) {
-      const int rr = sp * 16 + (tid >> 5), c = (tid & 31) * 8;
-      const int64_t m = (int64_t)tm * BIG + pass * 64 + rr;
-      const int64_t n = (int64_t)tn * BIG + c;
-      if (m >= Mb || n >= N) continue;
-      const int64_t orow = la.out_row(m);
-      float v[8];
-      {
-        v4f a0 = *reinterpret_cast<const v4f*>(stg + rr * SROW + c);
-        v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + c + 4);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
-      }
-      const bool full = n + 7 < N;
-      if (ep.bias) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-          v[t] += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
-      }
-      if (Cinb) {
-        const int64_t o = orow * ep.ldcin + n;
-        float cv[8];
-        if (ivec && full) {
-          if (ep.cin_f32) {
-            float4 c0 = *reinterpret_cast<const float4*>((const float*)Cinb + o);
-            float4 c1 = *reinterpret_cast<const float4*>((const float*)Cinb + o + 4);
-            cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
-            cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
-          } else {
-            load_vec<bf16>((const bf16*)Cinb + o, cv);
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)Cinb)[o + t] : to_f(((const bf16*)Cinb)[o + t])) : 0.f;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
-      }
-#pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
-      const int64_t o = orow * ep.ldc + n;
-      if (ep.out_f32) {
-        float* Cf = (float*)Cb + o;
-        if (cvec && full) {
-          *reinterpret_cast<float4*>(Cf) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(Cf + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        } else {
-          for (int t = 0; t < 8; ++t)
-            if (n + t < N) Cf[t] = v[t];
-        }
-      } else {
-        bf16* Ch = (bf16*)Cb + o;
-        if (cvec && full) {
-          store_vec<bf16>(Ch, v);
-        } else {
-          for (int t = 0; t < 8; ++t)
-            if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
-        }
-      }
-      if (ep.colstats) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));
-          cs[t] += sv;
-          cq[t] += sv * sv;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (ep.colstats) epilogue_colstats<32, 8>(cs, cq, stg, tid, (int64_t)tn * BIG, N, ep.colstats);
-}
-
-// dst[m][n] (ld ldd, fp32 or bf16) (+)= sum_z slab[z][m][n]
-__global__ void splitk_reduce_k(const float* __restrict__ slab, int64_t stride, int nz,
-                                void* dst, int64_t M, int64_t N, int64_t ldd, int out_f32,
-                                int accumulate) {
-  const int64_t total = M * N;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int z = 0; z < nz; ++z) v += slab[z * stride + i];
-    const int64_t m = i / N, n = i - m * N;
-    const int64_t o = m * ldd + n;
-    if (out_f32) {
-      float* d = (float*)dst;
-      d[o] = accumulate ? d[o] + v : v;
-    } else {
-      unsigned short* d = (unsigned short*)dst;
-      d[o] = f_to_bf16_bits(accumulate ? bf16_bits_to_f(d[o]) + v : v);
-    }
-  }
-}
-
-// Vector form of splitk_reduce_k for fp32 outputs with N % 4 == 0, ldd % 4 == 0
-// and 16-byte aligned slab / dst: 4 columns per lane, the slices' loads in flight.
-__global__ void __launch_bounds__(256) splitk_reduce_vec_k(const float* __restrict__ slab, int64_t stride, int nz,
-                                                            float* __restrict__ dst, int64_t M, int64_t N,
-                                                            int64_t ldd, int accumulate) {
-  const int64_t n4 = N / 4, total4 = M * n4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / n4, c = (i - m * n4) * 4;
-    float4 acc = *reinterpret_cast<const float4*>(slab + m * N + c);
-    int z = 1;
-    for (; z + 1 < nz; z += 2) {
-      const float4 a = *reinterpret_cast<const float4*>(slab + z * stride + m * N + c);
-      const float4 b = *reinterpret_cast<const float4*>(slab + (z + 1) * stride + m * N + c);
-      acc.x += a.x + b.x; acc.y += a.y + b.y; acc.z += a.z + b.z; acc.w += a.w + b.w;
-    }
-    if (z < nz) {
-      const float4 a = *reinterpret_cast<const float4*>(slab + z * stride + m * N + c);
-      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
-    }
-    float4* d = reinterpret_cast<float4*>(dst + m * ldd + c);
-    if (accumulate) {
-      const float4 o = *d;
-      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
-    }
-    *d = acc;
-  }
-}
-
-static void launch_splitk_reduce(const float* slab, int splitk, void* C, int64_t M, int64_t N, int64_t ldc,
-                                 int out_f32, int atomic, hipStream_t st) {
-  if (out_f32 && (N % 4) == 0 && (ldc % 4) == 0 && ((((uintptr_t)slab) | ((uintptr_t)C)) & 15) == 0) {
-    int nb = (int)std::min<int64_t>((M * N / 4 + 255) / 256, 4096);
-    if (nb < 1) nb = 1;
-    hipLaunchKernelGGL(splitk_reduce_vec_k, dim3(nb), dim3(256), 0, st, slab, M * N, splitk, (float*)C, M, N,
-                       ldc, atomic);
-    return;
-  }
-  int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
-  hipLaunchKernelGGL(splitk_reduce_k, dim3(nb), dim3(256), 0, st, slab, M * N, splitk, C, M, N, ldc, out_f32,
-                     atomic);
-}
-
-template <class LA, class LB>
-static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
-                      int batch, int splitk, hipStream_t st) {
-  int tiles_m = (int)((M + BIG - 1) / BIG), tiles_n = (int)((N + BIG - 1) / BIG);
-  int nkt = (int)((K + BK - 1) / BK);
-  if (splitk < 1) splitk = 1;
-  if (splitk > nkt) splitk = nkt > 0 ? nkt : 1;
-  int ktps = (nkt + splitk - 1) / splitk;
-  splitk = (nkt + ktps - 1) / ktps;
-  if (splitk < 1) splitk = 1;
-  dim3 grid(tiles_m * tiles_n, batch, splitk);
-  Epi e1 = ep;
-  if (ep.slab && splitk > 1) {
-    e1.slab_stride = M * N;
-    hipLaunchKernelGGL((gemm_big_kernel<LA, LB>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
-                       tiles_n, ktps, g_big_variant);
-    launch_splitk_reduce(ep.slab, splitk, ep.C, M, N, ep.ldc, ep.out_f32, ep.atomic, st);
-    return (int)hipGetLastError();
-  }
-  e1.slab = nullptr;
-  if (splitk > 1) e1.atomic = 1;
-  hipLaunchKernelGGL((gemm_big_kernel<LA, LB>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
-                     tiles_n, ktps, g_big_variant);
-  return (int)hipGetLastError();
-}
-
-// tile: 0 = 128x128 (4 waves, 2-3 blocks per CU), 1 = 256x256 (8 waves, 1 block per CU)
-template <class LA, class LB>
-static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
-                  int batch, int splitk, hipStream_t st, int tile = 0) {
-  if (tile == 1) return launch_big(la, lb, ep, M, N, K, batch, splitk, st);
-  int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
-  int nkt = (int)((K + BK - 1) / BK);
-  if (splitk < 1) splitk = 1;
-  if (splitk > nkt) splitk = nkt > 0 ? nkt : 1;
-  int ktps = (nkt + splitk - 1) / splitk;
-  splitk = (nkt + ktps - 1) / ktps;
-  if (splitk < 1) splitk = 1;
-  dim3 grid(tiles_m * tiles_n, batch, splitk);
-  if (ep.slab && splitk > 1) {
-    Epi e2 = ep;
-    e2.slab_stride = M * N;
-    if (ktps > 1)
-      hipLaunchKernelGGL((gemm_kernel<LA, LB, true>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K,
-                         tiles_m, tiles_n, ktps);
-    else
-      hipLaunchKernelGGL((gemm_kernel<LA, LB, false>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K,
-                         tiles_m, tiles_n, ktps);
-    launch_splitk_reduce(ep.slab, splitk, ep.C, M, N, ep.ldc, ep.out_f32, ep.atomic, st);
-    return (int)hipGetLastError();
-  }
-  Epi e1 = ep;
-  e1.slab = nullptr;
-  if (splitk > 1) e1.atomic = 1;
-  if (ktps > 1)
-    hipLaunchKernelGGL((gemm_kernel<LA, LB, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
-                       tiles_m, tiles_n, ktps);
-  else
-    hipLaunchKernelGGL((gemm_kernel<LA, LB, false>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
-                       tiles_m, tiles_n, ktps);
-  return (int)hipGetLastError();
-}
-
-// split count: ~2 blocks per CU in flight, each slice at least 8 K-tiles
-static int pick_splitk(int64_t M, int64_t N, int64_t K) {
-  int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  int64_t ktiles = (K + BK - 1) / BK;
-  int64_t want = (512 + tiles - 1) / tiles;
-  int64_t cap = std::max<int64_t>(1, ktiles / 8);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(want, cap), 512));
-}
-
+template int launch_buf<true>(const bf16*, const bf16*, int, int, int64_t, int64_t, int64_t, int64_t, const Epi&,
+                              int64_t, int64_t, int64_t, int, int, hipStream_t, int);
 }  // namespace gemm
 }  // namespace hetu
 
@@ -1159,84 +32,33 @@ HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* C
          bias_on_m, ws, 0};
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
-  if (a_kmaj && b_kmaj)
-    return launch(PlainK{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
-  if (a_kmaj && !b_kmaj)
-    return launch(PlainK{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
-  if (!a_kmaj && b_kmaj)
-    return launch(PlainMN{a, lda, M, K, sA}, PlainK{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
-  return launch(PlainMN{a, lda, M, K, sA}, PlainMN{b, ldb, N, K, sB}, ep, M, N, K, batch, splitk, st, tile);
-}
-
-static ConvGeom geom(int N, int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
-                     int pw) {
-  ConvGeom g{N, H, W, C, K, KH, KW, sh, sw, ph, pw, 0, 0};
-  g.ctap = 0;
-  g.OH = (H + 2 * ph - KH) / sh + 1;
-  g.OW = (W + 2 * pw - KW) / sw + 1;
-  g.fOW = FastDiv((uint32_t)g.OW);
-  g.fOH = FastDiv((uint32_t)g.OH);
-  g.fC = FastDiv((uint32_t)C);
-  g.fK = FastDiv((uint32_t)K);
-  g.fKW = FastDiv((uint32_t)KW);
-  return g;
-}
-
-// y[N,OH,OW,K] (NHWC) = conv(x[N,H,W,C] NHWC, w[K,KH,KW,C]) (+bias[K]) -> act.  C % 8 == 0.
-// colstats (optional, 2*K floats, zeroed by the caller) += per-channel sum and sum of
-// squares of the stored y: the statistics a training-mode BatchNorm on y needs.
-HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const float* bias, int N,
-                                int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
-                                int pw, int act, float* colstats, int tile, hipStream_t st) {
-  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  int64_t M = (int64_t)N * g.OH * g.OW, Kt = (int64_t)KH * KW * C;
-  Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0, nullptr, 0, colstats};
-  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
-    return launch(PlainK{(const bf16*)x, C, M, C, 0}, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M,
-                  K, Kt, 1, 1, st, tile);
-  ConvFwdA la{};
-  la.x = (const bf16*)x;
-  g.ctap = C % BK == 0;
-  la.g = g;
-  la.Ktot = Kt;
-  la.rows = M;
-  return launch(la, PlainK{(const bf16*)w, Kt, K, Kt, 0}, ep, M, K, Kt, 1, 1, st, tile);
-}
-
-// dx[N,H,W,C] = conv_transpose(dy[N,OH,OW,K], w[K,KH,KW,C]) (+ acc[N,H,W,C] when given:
-// the gradient joined at the conv input, added in the epilogue).  K % 8 == 0, C % 8 == 0.
-HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const void* acc,
-                                  int acc_f32, int N, int H, int W, int C, int K, int KH, int KW,
-                                  int sh, int sw, int ph, int pw, int tile, hipStream_t st) {
-  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  Epi ep{dx, acc, nullptr, C, C, 0, 0, 1.f, acc ? 1.f : 0.f, 0, 0, acc_f32, 0, 0, nullptr, 0};
-  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0) {
-    int64_t M = (int64_t)N * H * W;
-    return launch(PlainK{(const bf16*)dy, K, M, K, 0}, PlainMN{(const bf16*)w, C, C, K, 0}, ep, M,
-                  C, K, 1, 1, st, tile);
+  if (M <= 0 || N <= 0) return 0;
+  // buffer-descriptor loaders address each operand slice with 32-bit offsets (< 2 GiB);
+  // a larger K-major A is processed in row chunks (A, C, Cin and a per-row bias advance)
+  const int64_t bbytes = (b_kmaj ? (N - 1) * ldb + K : (K - 1) * ldb + N) * 2;
+  const int64_t abytes = (a_kmaj ? (M - 1) * lda + K : (K - 1) * lda + M) * 2;
+  if (bbytes >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  if (abytes >= (1ll << 31)) {
+    if (!a_kmaj || batch != 1 || ep.slab || splitk > 1) return (int)hipErrorInvalidValue;
+    const int64_t rows = std::max<int64_t>(BIG, ((((1ll << 30) / (lda * 2)) / BIG) * BIG));
+    for (int64_t m0 = 0; m0 < M; m0 += rows) {
+      const int64_t mc = std::min(rows, M - m0);
+      Epi e = ep;
+      e.C = (char*)ep.C + m0 * ep.ldc * (ep.out_f32 ? 4 : 2);
+      if (ep.Cin) e.Cin = (const char*)ep.Cin + m0 * ep.ldcin * (ep.cin_f32 ? 4 : 2);
+      if (ep.bias && ep.bias_on_m) e.bias = ep.bias + m0;
+      const int rc = K % BK == 0 ? launch_buf<true>(a + m0 * lda, b, 1, b_kmaj, lda, ldb, 0, sB, e, mc, N, K, 1, 1, st, tile)
+                                 : launch_buf<false>(a + m0 * lda, b, 1, b_kmaj, lda, ldb, 0, sB, e, mc, N, K, 1, 1, st, tile);
+      if (rc) return rc;
+    }
+    return 0;
   }
-  // one launch over the sh*sw stride classes (blockIdx.y); grid sized for the
-  // largest class, the others exit early per block
-  int64_t Mmax = (int64_t)N * ((H + sh - 1) / sh) * ((W + sw - 1) / sw);
-  int64_t Kmax = (int64_t)((KH + sh - 1) / sh) * ((KW + sw - 1) / sw) * K;
-  g.ctap = K % BK == 0;
-  ConvDgradA la{};
-  la.dy = (const bf16*)dy;
-  la.g = g;
-  ConvDgradB lb{};
-  lb.w = (const bf16*)w;
-  lb.g = g;
-  return launch(la, lb, ep, Mmax, C, Kmax, sh * sw, 1, st, tile);
+  if (K % BK == 0) return launch_buf<true>(a, b, a_kmaj, b_kmaj, lda, ldb, sA, sB, ep, M, N, K, batch, splitk, st, tile);
+  return launch_buf<false>(a, b, a_kmaj, b_kmaj, lda, ldb, sA, sB, ep, M, N, K, batch, splitk, st, tile);
 }
 
 HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }
 
-// profiling ablations of the 256x256 kernel (see g_big_variant); returns the previous value
-HETU_API int hetu_gemm_big_variant(int v) {
-  int old = g_big_variant;
-  g_big_variant = v;
-  return old;
-}
 
 // split count for the 256x256 kernel: about one block per CU, slices of >= 8 K-tiles
 HETU_API int hetu_gemm_pick_splitk_big(int64_t M, int64_t N, int64_t K) {
@@ -1245,24 +67,6 @@ HETU_API int hetu_gemm_pick_splitk_big(int64_t M, int64_t N, int64_t K) {
   int64_t want = (256 + tiles - 1) / tiles;
   int64_t cap = std::max<int64_t>(1, ktiles / 8);
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(want, cap), 512));
-}
-
-// dw[K, KH*KW*C] fp32 (+)= sum over output pixels dy^T x_im2col.  Split-K over
-// the pixel axis into fp32 slabs (ws: splitk*K*KH*KW*C floats) + one reduce; no atomics.
-HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int N, int H, int W,
-                                  int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
-                                  int splitk, int accumulate, float* ws, int tile, hipStream_t st) {
-  ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
-  int64_t P = (int64_t)N * g.OH * g.OW, Nc = (int64_t)KH * KW * C;
-  Epi ep{dw, nullptr, nullptr, Nc, 0, 0, 0, 1.f, 0.f, 0, 1, 0, accumulate, 0, splitk > 1 ? ws : nullptr, 0};
-  PlainMN la{(const bf16*)dy, K, K, P, 0};
-  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0)
-    return launch(la, PlainMN{(const bf16*)x, C, C, P, 0}, ep, K, Nc, P, 1, splitk, st, tile);
-  ConvWgradB lb{};
-  lb.x = (const bf16*)x;
-  lb.g = g;
-  lb.P = P;
-  return launch(la, lb, ep, K, Nc, P, 1, splitk, st, tile);
 }
 
 // out[i] = sum_z slab[z * n + i] (fp32; the partials of a split-K library GEMM):
@@ -1293,3 +97,4 @@ HETU_API int hetu_splitk_sum_f32(const float* slab, int nz, float* out, int64_t 
   hipLaunchKernelGGL(splitk_sum_vec_k, dim3((unsigned)nb), dim3(256), 0, st, (const float4*)slab, n4, nz, (float4*)out);
   return (int)hipGetLastError();
 }
+

@@ -17,7 +17,7 @@ lowering pass); here they lower to RCCL (GPU) / gloo (CPU)
 collectives and send/recv.  Synthetic MNIST-shaped data.
 
     python bin/heturun -w 1 python examples/runner/parallel/mlp_parallel.py --mode base
-    python bin/heturun -w 4 python examples/runner/parallel/mlp_parallel.py --mode pp --schedule pipedream
+    python bin/heturun -w 4 python examples/runner/parallel/mlp_parallel.py --mode pp --schedule pipedream_flush
     python bin/heturun -w 2 python examples/runner/parallel/mlp_parallel.py --mode mp --split middle
     python examples/runner/parallel/validate_results.py
 """
@@ -110,7 +110,7 @@ def main(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--mode', default='base', choices=['base', 'pp', 'mp', 'dp_pp'])
     p.add_argument('--split', default='middle', choices=sorted(SPLITS))
-    p.add_argument('--schedule', default='gpipe', choices=['gpipe', 'pipedream', 'hetpipe'],
+    p.add_argument('--schedule', default='gpipe', choices=['gpipe', 'pipedream', 'pipedream_flush', 'hetpipe'],
                    help='hetpipe: 1F1B with each stage\'s weights synced through the PS (heturun -s 1)')
     p.add_argument('--micro-batches', type=int, default=4)
     p.add_argument('--replicas', type=int, default=2)

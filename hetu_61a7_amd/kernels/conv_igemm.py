@@ -29,6 +29,63 @@ def _ok(a, b, *channels):
             b.data_ptr() % 16 == 0)
 
 
+def _ok32(a, b, *channels):
+    """fp32 operands for the exact-fp32 MFMA convolution (gemm_f32.hip): channels-last,
+    16-byte aligned, channel counts multiples of 4 (16-byte chunks of 4 floats)."""
+    return (MODE != 'vendor' and a.dtype == torch.float32 and b.dtype == torch.float32 and
+            a.is_contiguous(memory_format=CL) and b.is_contiguous(memory_format=CL) and
+            all(c % 4 == 0 for c in channels) and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def forward_f32(x, w, stride, padding, bias=None, act=None):
+    """fp32 forward on the 16x16x4-f32 MFMA kernel; None when unsupported."""
+    if not _ok32(x, w, x.shape[1], w.shape[0]):
+        return None
+    N, C, H, W = x.shape
+    K, _, KH, KW = w.shape
+    OH, OW = _out_hw(H, W, KH, KW, stride, padding)
+    y = torch.empty((N, OH, OW, K), dtype=torch.float32, device=x.device)
+    f = fn('hetu_conv_fwd_f32', [P, P, P, P] + _GEOM + [I32, P])
+    check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), bias.float().contiguous().data_ptr() if bias is not None
+            else None, N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
+            {None: 0, 'relu': 1}[act], stream_ptr()), 'conv_fwd_f32')
+    return y.permute(0, 3, 1, 2)
+
+
+def backward_data_f32(g, w, x_shape, stride, padding, acc=None):
+    if not _ok32(g, w, x_shape[1], w.shape[0]):
+        return None
+    if acc is not None and (tuple(acc.shape) != tuple(x_shape) or acc.dtype != torch.float32 or
+                            not acc.is_contiguous(memory_format=CL)):
+        return None
+    N, C, H, W = x_shape
+    K, _, KH, KW = w.shape
+    dx = torch.empty((N, H, W, C), dtype=torch.float32, device=g.device)
+    f = fn('hetu_conv_dgrad_f32', [P, P, P, P] + _GEOM + [P])
+    check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
+            N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1], stream_ptr()), 'conv_dgrad_f32')
+    return dx.permute(0, 3, 1, 2)
+
+
+def backward_filter_f32(g, x, w_shape, stride, padding, out=None, accumulate=None):
+    if not _ok32(x, g, x.shape[1], g.shape[1]):
+        return None
+    N, C, H, W = x.shape
+    K, _, KH, KW = w_shape
+    if accumulate is None:
+        accumulate = out is not None
+    if out is None:
+        dw = torch.empty((K, KH, KW, C), dtype=torch.float32, device=g.device)
+    else:
+        dw = out.permute(0, 2, 3, 1)
+        if not dw.is_contiguous() or dw.dtype != torch.float32:
+            return None
+    f = fn('hetu_conv_wgrad_f32', [P, P, P] + _GEOM + [I32, P])
+    check(f(g.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
+            padding[0], padding[1], int(bool(accumulate)), stream_ptr()), 'conv_wgrad_f32')
+    return dw.permute(0, 3, 1, 2)
+
+
 def _out_hw(H, W, KH, KW, stride, padding):
     return (H + 2 * padding[0] - KH) // stride[0] + 1, (W + 2 * padding[1] - KW) // stride[1] + 1
 

@@ -23,20 +23,22 @@ TILES = (0, 1)
 MODE = os.environ.get('HETU_GEMM', 'auto')
 
 
-def _operand(t, rows_dim_last):
+def _operand(t, rows_dim_last, q=8):
     """Describe a 2-D (or batched 3-D) operand view.  ``t`` is viewed as
-    [..., R, K] (rows first) -> returns (kmaj, ld, batch_stride) or None."""
+    [..., R, K] (rows first) -> returns (kmaj, ld, batch_stride) or None.
+    ``q``: elements per 16-byte staging chunk (8 bf16, 4 fp32) -- the contiguous
+    extent and the leading dimension must be multiples of it."""
     sr, sk = t.stride(-2), t.stride(-1)
     R, K = t.shape[-2], t.shape[-1]
     bs = t.stride(0) if t.dim() == 3 else 0
     if sk == 1 or K == 1:
-        ld = sr if R > 1 else max(K, 8)
-        if K % 8 or ld % 8:
+        ld = sr if R > 1 else max(K, q)
+        if K % q or ld % q:
             return None
         return True, ld, bs
     if sr == 1 or R == 1:
-        ld = sk if K > 1 else max(R, 8)
-        if R % 8 or ld % 8:
+        ld = sk if K > 1 else max(R, q)
+        if R % q or ld % q:
             return None
         return False, ld, bs
     return None
@@ -46,10 +48,58 @@ def _aligned(*ts):
     return all(t.data_ptr() % 16 == 0 for t in ts)
 
 
+_F32_ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64, I64,
+             F32, F32, I32, I32, I32, P]
+
+
+def gemm_f32(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, accumulate=False,
+             bias_on_m=False):
+    """fp32 product on the exact-fp32 MFMA kernel (``gemm_f32.hip``, 16x16x4 f32):
+    the parity-mode GEMM.  Same view rules as :func:`gemm` with 4-element chunks."""
+    if a.dtype != torch.float32 or b.dtype != torch.float32 or a.dim() != b.dim() or a.dim() not in (2, 3):
+        return None
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    if b.shape[-2] != K:
+        raise ValueError('gemm shape mismatch %s @ %s' % (tuple(a.shape), tuple(b.shape)))
+    batch = a.shape[0] if a.dim() == 3 else 1
+    if a.dim() == 3 and b.shape[0] != batch:
+        return None
+    da = _operand(a, False, 4)
+    db = _operand(b.transpose(-1, -2), False, 4)
+    if da is None or db is None or not _aligned(a, b):
+        return None
+    if out is None:
+        shape = (batch, M, N) if a.dim() == 3 else (M, N)
+        out = (torch.zeros if accumulate else torch.empty)(shape, dtype=torch.float32, device=a.device)
+    if out.dtype != torch.float32 or out.stride(-1) != 1 or (out.dim() == 3 and out.dim() != a.dim()):
+        return None
+    ldc = out.stride(-2) if M > 1 else N
+    sC = out.stride(0) if out.dim() == 3 else 0
+    cin_t, ldcin, sCin = None, 0, 0
+    if cin is not None and beta != 0.0:
+        cin_t = cin.expand_as(out) if cin.shape != out.shape else cin
+        if cin_t.dtype != torch.float32 or cin_t.stride(-1) != 1:
+            cin_t = cin_t.float().contiguous()
+        ldcin = cin_t.stride(-2)
+        sCin = cin_t.stride(0) if cin_t.dim() == 3 else 0
+    bias_t = bias.float().contiguous() if bias is not None else None
+    f = fn('hetu_gemm_f32', _F32_ARGS)
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), cin_t.data_ptr() if cin_t is not None else None,
+            bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, ldcin,
+            int(da[0]), int(db[0]), batch, da[2], db[2], sC, sCin, float(alpha), float(beta), _ACT[act],
+            int(bias_on_m), int(accumulate), stream_ptr()), 'gemm_f32')
+    return out
+
+
 def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None,
          accumulate=False, splitk=1, bias_on_m=False, tile=0):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+beta*cin) (+bias) -> act, a/b arbitrary
     strided views (batched 3-D allowed).  Returns None if unsupported."""
+    if a.dtype == torch.float32 and b.dtype == torch.float32 and (out is None or out.dtype == torch.float32) \
+            and splitk == 1:
+        return gemm_f32(a, b, out=out, bias=bias, act=act, alpha=alpha, beta=beta, cin=cin,
+                        accumulate=accumulate, bias_on_m=bias_on_m)
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         return None
     if a.dim() != b.dim() or a.dim() not in (2, 3):

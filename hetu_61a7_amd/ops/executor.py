@@ -369,6 +369,10 @@ class Executor(object):
     def export_chrome_trace(self, path, name='default'):
         return self.subexecutor[name].export_chrome_trace(path)
 
+    def optimizer_ops(self, name='default'):
+        """The OptimizerOps of one named sub-graph (DP buckets, comm_trace())."""
+        return list(getattr(self.subexecutor[name], 'opt_ops', []))
+
     def recordLoads(self):
         if self.config.ps_comm is not None:
             self.config.ps_comm.record_loads()

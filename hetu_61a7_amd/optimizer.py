@@ -250,6 +250,13 @@ class OptimizerOp(Op):
         self.allreduce_mode = 'sum'
         self.ps_params = set()
         self.zero = False
+        # gradient wire format of the DP all-reduce: 'fp32', or 'bf16' (half the bytes,
+        # fp32 accumulation: Communicator.all_reduce_bf16)
+        self.grad_wire = os.environ.get('HETU_GRAD_WIRE', 'fp32')
+        # per-step bucket timeline (HETU_COMM_TRACE=1): host launch times relative to
+        # the end of the backward pass, and device events on GPUs (comm_trace())
+        self.trace = os.environ.get('HETU_COMM_TRACE', '0') == '1'
+        self._trace = []
 
     # ----------------------------------------------------------------------------
     def gradient(self, output_grad):
@@ -265,6 +272,7 @@ class OptimizerOp(Op):
             self.dp = True
             self.comm = config.comm
         self.bucket_bytes = int(getattr(config, 'bucket_mb', 32) * (1 << 20))
+        self.grad_wire = getattr(config, 'grad_wire', None) or self.grad_wire
         # PS placement (reference optimizer.py:145-163, Variable.py:55-81): embedding
         # tables (row-sparse grads) live on the PS in PS and Hybrid modes; in pure PS
         # mode the dense parameters are held there too (one flat key).
@@ -430,8 +438,17 @@ class OptimizerOp(Op):
             b.pending = b.total
 
     def _reduce_bucket(self, b, async_op=True):
+        if self.trace:
+            self._trace_launch(b)
         if not self.zero:
-            return self.comm.all_reduce(self.flat.grad[b.start:b.end], self.allreduce_mode, async_op=async_op)
+            g = self.flat.grad[b.start:b.end]
+            if self.grad_wire == 'bf16' and self.allreduce_mode == 'sum':
+                w = self.comm.all_reduce_bf16(g, async_op=async_op)
+            else:
+                w = self.comm.all_reduce(g, self.allreduce_mode, async_op=async_op)
+            if self.trace and w is not None:
+                self._trace[-1]['work'] = w
+            return w
         lo, hi = b.own
         return self.comm.reduce_scatter(self.flat.zgrad[b.zoff:b.zoff + hi - lo], self.flat.grad[b.start:b.end],
                                         self.allreduce_mode, async_op=async_op)
@@ -491,7 +508,41 @@ class OptimizerOp(Op):
                     if b.pending == 0:
                         b.work = self._reduce_bucket(b)
 
+    # ---- communication timeline (bench.py --comm-trace / HETU_COMM_TRACE=1) ------------
+    def _trace_launch(self, b):
+        import time
+        rec = {'bytes': (b.end - b.start) * 4, 't_host': time.perf_counter(), 'ev': None}
+        if self.flat is not None and self.flat.grad.is_cuda:
+            rec['ev'] = torch.cuda.Event(enable_timing=True)
+            rec['ev'].record()
+        self._trace.append(rec)
+
+    def comm_trace(self):
+        """Bucket timeline of the last step: per bucket its size, the host-side launch
+        time relative to the end of the backward pass (negative = launched while the
+        backward was still running), and on GPUs the device-side launch / completion
+        times relative to the same point (ms)."""
+        out = []
+        end = getattr(self, '_bwd_end', None)
+        if end is None:
+            return out
+        for r in self._trace:
+            e = {'bytes': r['bytes'], 'launch_host_ms': round((r['t_host'] - end[0]) * 1e3, 3)}
+            if r['ev'] is not None and end[1] is not None:
+                end[1].synchronize()
+                e['launch_dev_ms'] = round(-r['ev'].elapsed_time(end[1]), 3)
+                ev = getattr(r.get('work'), 'event', None)
+                if ev is not None:
+                    try:
+                        ev.synchronize()
+                        e['done_dev_ms'] = round(-ev.elapsed_time(end[1]), 3)
+                    except RuntimeError:   # event without timing
+                        pass
+            out.append(e)
+        return out
+
     def begin_step(self):
+        self._trace = []
         self._pending_sparse = []
         self._pending_ps = []
         for b in self.buckets:
@@ -500,6 +551,13 @@ class OptimizerOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         self.step += 1
+        if self.trace:
+            import time
+            ev = None
+            if self.flat is not None and self.flat.grad.is_cuda:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+            self._bwd_end = (time.perf_counter(), ev)
         if self.zero:
             self._zero_step()
         for b in self.buckets if not self.zero else ():

@@ -145,6 +145,16 @@ class Communicator(object):
         self.global_rank = dist.get_rank()
         self.local_rank = dist_env()[2]
         self.device_id = self.local_rank
+        # GPU collectives: the in-house RCCL communicator (csrc/comm/hetu_comm.cc) unless
+        # HETU_COMM=torch; torch.distributed stays the bootstrap / host-tensor path
+        self.native = None
+        if use_gpu and self.rank >= 0 and os.environ.get('HETU_COMM', 'native') != 'torch' \
+                and dist.get_backend(self.group) == 'nccl':
+            from . import rccl
+            if rccl.available():
+                self.native = rccl.world_from_dist(self.group)
+        self.backend = 'hetu-rccl' if self.native is not None else \
+            (dist.get_backend(self.group) if self.rank >= 0 else 'non-member')
 
     # reference MPI_NCCL_Communicator fields (ctypes c_int: read through .value),
     # used by manual-pipeline scripts (examples/runner/parallel/complex_pipeline_mlp.py)
@@ -175,6 +185,8 @@ class Communicator(object):
 
     # -- collectives ------------------------------------------------------------------
     def all_reduce(self, t: torch.Tensor, op: str = 'sum', async_op: bool = False):
+        if self.native is not None and t.is_cuda and t.is_contiguous():
+            return self.native.all_reduce(t, op, async_op=async_op)
         if op == 'mean':
             w = dist.all_reduce(t, dist.ReduceOp.SUM, group=self.group, async_op=async_op)
             if async_op:
@@ -185,10 +197,14 @@ class Communicator(object):
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
         """out = concat over ranks along dim 0."""
+        if self.native is not None and out.is_cuda and out.is_contiguous():
+            return self.native.all_gather(out, inp, async_op=async_op)
         return dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group, async_op=async_op)
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = 'sum', async_op: bool = False):
         """out = this rank's 1/P chunk (dim 0) of the reduction of ``inp``."""
+        if self.native is not None and out.is_cuda and out.is_contiguous():
+            return self.native.reduce_scatter(out, inp, op, async_op=async_op)
         if not self.use_gpu:
             # gloo has no reduce-scatter: all-reduce a copy and keep our chunk
             t = inp.contiguous().clone()
@@ -199,26 +215,46 @@ class Communicator(object):
                                           group=self.group, async_op=async_op)
 
     def broadcast(self, t: torch.Tensor, root: int = 0, async_op: bool = False):
+        if self.native is not None and t.is_cuda and t.is_contiguous():
+            return self.native.broadcast(t, root, async_op=async_op)
         return dist.broadcast(t, self._g(root), group=self.group, async_op=async_op)
 
     def reduce(self, t: torch.Tensor, root: int = 0, op: str = 'sum', async_op: bool = False):
+        if self.native is not None and t.is_cuda and t.is_contiguous():
+            return self.native.reduce(t, root, op, async_op=async_op)
         return dist.reduce(t, self._g(root), _RED[op], group=self.group, async_op=async_op)
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
         """Equal ``numel/nranks`` chunks along dim 0 (reference AllToAll semantics)."""
+        if self.native is not None and out.is_cuda and out.is_contiguous():
+            return self.native.all_to_all(out, inp, async_op=async_op)
         return dist.all_to_all_single(out, inp.contiguous(), group=self.group, async_op=async_op)
 
     def send(self, t: torch.Tensor, dst: int):
+        if self.native is not None and t.is_cuda:
+            return self.native.p2p([('send', t.contiguous(), dst)])
         return dist.isend(t.contiguous(), self._g(dst), group=self.group)
 
     def recv(self, t: torch.Tensor, src: int):
+        if self.native is not None and t.is_cuda and t.is_contiguous():
+            return self.native.p2p([('recv', t, src)])
         return dist.irecv(t, self._g(src), group=self.group)
+
+    def all_reduce_bf16(self, t: torch.Tensor, async_op: bool = False):
+        """SUM of an fp32 tensor with bf16 on the wire and fp32 accumulation (native
+        RCCL path, 16-byte aligned tensor).  Elsewhere a plain fp32 all-reduce."""
+        if self.native is not None and t.is_cuda and t.is_contiguous() and t.dtype == torch.float32 \
+                and t.data_ptr() % 16 == 0:
+            return self.native.all_reduce_bf16(t, async_op=async_op)
+        return self.all_reduce(t, 'sum', async_op=async_op)
 
     def batch_p2p(self, ops):
         """ops: list of ('send'|'recv', tensor, peer) issued as one RCCL group
         (reference GroupStart/GroupEnd around pipeline send/recv)."""
         if not ops:
             return []
+        if self.native is not None and all(t.is_cuda and t.is_contiguous() for _, t, _ in ops):
+            return [self.native.p2p(ops)]
         p2p = [dist.P2POp(dist.isend if k == 'send' else dist.irecv, t, self._g(p), group=self.group)
                for k, t, p in ops]
         return dist.batch_isend_irecv(p2p)
@@ -229,8 +265,14 @@ class Communicator(object):
         else:
             dist.barrier(group=self.group)
 
+    def health(self):
+        """RCCL watchdog probe: 0 when healthy, else the communicator's
+        asynchronous error code."""
+        return self.native.async_error() if self.native is not None else 0
+
     def __repr__(self):
-        return 'Communicator(rank=%d, nrank=%d, ranks=%s)' % (self.rank, self.nrank, self.ranks)
+        return 'Communicator(rank=%d, nrank=%d, ranks=%s, backend=%s)' % (self.rank, self.nrank, self.ranks,
+                                                                          self.backend)
 
 
 class _Done(object):
@@ -249,6 +291,11 @@ class _PostDiv(object):
 
 def destroy():
     global _WORLD
+    for c in list(_GROUPS.values()) + ([_WORLD] if _WORLD is not None else []):
+        if getattr(c, 'native', None) is not None:
+            torch.cuda.synchronize()
+            c.native.destroy()
+            c.native = None
     _GROUPS.clear()
     _WORLD = None
     if dist.is_initialized():

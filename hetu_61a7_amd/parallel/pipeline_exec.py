@@ -19,10 +19,15 @@ MI355X design
   are asynchronous, receives block, so any schedule in which each stage
   processes micro-batches in the same order is deadlock-free.
 * Schedules: ``gpipe`` (F0..Fm-1, B0..Bm-1), ``pipedream`` (1F1B: warm-up of
-  ``stages - s - 1`` forwards then alternate, cooldown), ``hetpipe`` (1F1B plus
-  a PS sync of the stage's dense parameters each step).  Gradients of a step
-  are accumulated over micro-batches and applied once (pipeline flush), which
-  keeps the step semantics of the non-pipelined model.
+  ``stages - s - 1`` forwards then alternate, cooldown), ``pipedream_flush``
+  (the same order, gradients accumulated and applied once per step) and
+  ``hetpipe`` (1F1B plus a PS sync of the stage's dense parameters each step).
+* ``pipedream`` is asynchronous PipeDream with weight stashing: every micro-batch
+  snapshots the stage's current weights at its forward, its backward runs
+  against that snapshot, and its gradient is applied to the latest weights
+  right after the backward (reference ``pipedream_subexecutor.py:90-147``).
+  GPipe / PipeDream-flush / HetPipe accumulate over the micro-batches of a step
+  and apply once (pipeline flush), the step semantics of the unpipelined model.
 """
 from __future__ import annotations
 
@@ -56,29 +61,76 @@ def _group_key(raw_ctx):
 
 
 class _P2P(object):
-    """Async tensor send (header + payload) / blocking receive over torch.distributed."""
+    """Point-to-point tensor messages between pipeline stages (RCCL send/recv over xGMI
+    through ``Communicator``; gloo on CPU).
 
-    def __init__(self, device):
+    Shape protocol (reference executor.py:774-833 exchanges shapes once per
+    (re)allocation): the first message of each key (a cross-stage edge) in a step
+    carries a small header (ndim, dtype, shape); the receiver reads it -- the one host
+    synchronisation -- and caches it, and every later micro-batch of the step sends the
+    payload alone, received into a buffer of the cached shape.  All payload sends of a
+    phase go out as one RCCL group (batch_isend_irecv), so do all payload receives whose
+    shapes are known.  ``hdr_syncs`` counts the header reads (tests)."""
+
+    def __init__(self, device, comm=None):
         self.device = device
+        self.comm = comm
         self.pending = []
+        self.shapes = {}        # key -> (shape, dtype) known for this step
+        self.hdr_syncs = 0
 
-    def send(self, t, dst):
-        t = t.contiguous()
-        hdr = torch.zeros(HDR, dtype=torch.int64)
-        hdr[0] = t.dim()
-        hdr[1] = _DT_INV[t.dtype]
-        hdr[2:2 + t.dim()] = torch.tensor(list(t.shape), dtype=torch.int64)
-        hdr = hdr.to(t.device)
-        self.pending.append((dist.isend(hdr, dst), hdr))
-        self.pending.append((dist.isend(t, dst), t))
+    def new_step(self):
+        self.shapes = {}
 
-    def recv(self, src):
-        hdr = torch.zeros(HDR, dtype=torch.int64, device=self.device)
-        dist.irecv(hdr, src).wait()
-        h = hdr.tolist()
-        nd, dt = int(h[0]), _DT[int(h[1])]
-        out = torch.empty(tuple(int(x) for x in h[2:2 + nd]), dtype=dt, device=self.device)
-        dist.irecv(out, src).wait()
+    def _batch(self, ops):
+        if self.comm is not None:
+            return self.comm.batch_p2p(ops)
+        return dist.batch_isend_irecv([dist.P2POp(dist.isend if k == 'send' else dist.irecv, t, p)
+                                       for k, t, p in ops]) if ops else []
+
+    def send_many(self, items):
+        """items: [(key, tensor, dst)] -- one group (plus headers of new keys)."""
+        hdrs, ops = [], []
+        for key, t, dst in items:
+            t = t.contiguous()
+            if self.shapes.get(key) != (tuple(t.shape), t.dtype):
+                hdr = torch.zeros(HDR, dtype=torch.int64)
+                hdr[0] = t.dim()
+                hdr[1] = _DT_INV[t.dtype]
+                hdr[2:2 + t.dim()] = torch.tensor(list(t.shape), dtype=torch.int64)
+                hdr = hdr.to(t.device)
+                hdrs.append(('send', hdr, dst))
+                self.shapes[key] = (tuple(t.shape), t.dtype)
+            ops.append(('send', t, dst))
+        for w in self._batch(hdrs):
+            self.pending.append((w, hdrs))
+        for w in self._batch(ops):
+            self.pending.append((w, ops))
+
+    def recv_many(self, items):
+        """items: [(key, src)] -> tensors in the same order."""
+        out = [None] * len(items)
+        hdr_ops, need = [], []
+        for j, (key, src) in enumerate(items):
+            if key not in self.shapes:
+                hdr = torch.zeros(HDR, dtype=torch.int64, device=self.device)
+                hdr_ops.append(('recv', hdr, src))
+                need.append((j, key, hdr))
+        if hdr_ops:
+            for w in self._batch(hdr_ops):
+                w.wait()
+            for j, key, hdr in need:
+                h = hdr.tolist()          # the host sync, once per key per step
+                self.hdr_syncs += 1
+                nd = int(h[0])
+                self.shapes[key] = (tuple(int(x) for x in h[2:2 + nd]), _DT[int(h[1])])
+        ops = []
+        for j, (key, src) in enumerate(items):
+            shape, dt = self.shapes[key]
+            out[j] = torch.empty(shape, dtype=dt, device=self.device)
+            ops.append(('recv', out[j], src))
+        for w in self._batch(ops):
+            w.wait()
         return out
 
     def flush(self):
@@ -108,7 +160,7 @@ def gpipe_schedule(stage, nstages, m):
 class PipelineSubExecutor(object):
     def __init__(self, kind, name, eval_node_list, config):
         from ..optimizer import OptimizerOp
-        assert kind in ('gpipe', 'pipedream', 'hetpipe'), kind
+        assert kind in ('gpipe', 'pipedream', 'pipedream_flush', 'hetpipe'), kind
         self.kind, self.name, self.config = kind, name, config
         self.eval_node_list = list(eval_node_list)
         topo = find_topo_sort(self.eval_node_list)
@@ -213,7 +265,7 @@ class PipelineSubExecutor(object):
         self.opt = None
         if self.opt_nodes:
             self._build_local_optimizer()
-        self.p2p = _P2P(config.device)
+        self.p2p = _P2P(config.device, getattr(config, 'comm', None) if dist.is_initialized() else None)
         self.step_count = 0
 
     # ---------------------------------------------------------------------------------------
@@ -272,14 +324,20 @@ class PipelineSubExecutor(object):
 
     def _phase(self, ph, mb, state):
         vals, aux = state
-        for _, src, node in self.recv_msgs[ph]:
-            vals[node] = self.p2p.recv(self._peer(src))
+        msgs = self.recv_msgs[ph]
+        if msgs:
+            got = self.p2p.recv_many([((nid, src), self._peer(src)) for nid, src, _ in msgs])
+            for (_, _, node), v in zip(msgs, got):
+                vals[node] = v
         self._compute(self.fwd if ph == 'F' else self.bwd, vals, aux)
-        for dst, _, node in self.send_msgs[ph]:
+        items = []
+        for dst, nid, node in self.send_msgs[ph]:
             v = vals[node]
             if isinstance(v, ndarray.IndexedSlices):
                 v = v.to_dense()
-            self.p2p.send(v, self._peer(dst))
+            items.append(((nid, self.stage), v, self._peer(dst)))
+        if items:
+            self.p2p.send_many(items)
 
     def run(self, eval_node_list=None, feed_dict=None, convert_to_numpy_ret_vals=False, batch_num=None, **kw):
         cfg = self.config
@@ -312,26 +370,42 @@ class PipelineSubExecutor(object):
             sched = pipedream_schedule(self.stage, self.nstages, m)
         acc = {}
         results = [None] * m
+        self.p2p.new_step()
+        stash = self.kind == 'pipedream' and not self.inference and self.opt is not None
         for ph, mb in sched:
             vals, aux = states[mb]
             if ph == 'F':
                 for d in self.loaders:
                     vals[d] = d.get_arr(self.name, cfg)
+                if stash:
+                    # weight stashing (reference pipedream_subexecutor.py:90-128): this
+                    # micro-batch's forward AND backward use the weights current at its
+                    # forward; updates of earlier micro-batches land in the live copy
+                    for p in self.params:
+                        vals[p] = cfg.compute_value(p).clone()
             self._phase(ph, mb, states[mb])
             if ph == 'B' or self.inference:
                 results[mb] = self._outputs(vals, convert_to_numpy_ret_vals)
                 if self.opt is not None:
+                    grads = {}
                     for g, i in self.local_grads.items():
                         v = vals.get(g)
                         if v is None:
                             continue
-                        if isinstance(v, ndarray.IndexedSlices):
+                        if stash:
+                            grads[i] = v
+                        elif isinstance(v, ndarray.IndexedSlices):
                             # sparse (embedding) grads stay sparse across micro-batches
                             acc[i] = v if i not in acc else acc[i].merge(v)
                         else:
                             # clone: v may be a slot of the flat gradient buffer that the next
                             # micro-batch overwrites in place
                             acc[i] = v.float().clone() if i not in acc else acc[i] + v.float()
+                    if stash and grads:
+                        # PipeDream: apply this micro-batch's gradient to the LATEST weights
+                        # right after its backward (reference copy_latest_weight :130-147 +
+                        # OptimizerOp per backward) -- no pipeline flush
+                        self._apply(grads)
                 states[mb] = None
         self.p2p.flush()
         if self.opt is not None and acc:
@@ -343,6 +417,14 @@ class PipelineSubExecutor(object):
             op.compute([])
         self.step_count += 1
         return results
+
+    def _apply(self, grads):
+        op = self.opt
+        op.begin_step()
+        for i in range(len(op.inputs)):
+            if i in grads:
+                op.on_grad_ready(i, grads[i])
+        op.compute([])
 
     def _outputs(self, vals, convert):
         out = []

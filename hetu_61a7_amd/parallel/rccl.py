@@ -1,0 +1,300 @@
+"""Python side of the in-house RCCL communicator (``csrc/comm/hetu_comm.cc``,
+``libhetu_comm.so``): the GPU collectives of :class:`parallel.comm.Communicator`.
+
+Reference: ``communicator/mpi_nccl_comm.py:164-342`` (NCCL_Communicator) over
+``src/communication/mpi_nccl_communication.cu``.  MI355X design:
+
+* rendezvous through the job's TCP store (torchrun / heturun ``MASTER_ADDR``), no MPI;
+* the collective runs on a per-communicator high-priority comm stream ordered after
+  the producer with a stream edge (``wait_stream``), and an async op returns a handle
+  whose ``wait()`` is another stream edge back onto the consumer's stream -- no host
+  synchronisation anywhere (the reference host-syncs every comm op's event,
+  ``executor.py:1034-1036``);
+* tensors used on the comm stream are ``record_stream``-ed so the caching allocator
+  does not recycle them while the collective is in flight;
+* ``reduce_scatter_bf16`` / ``all_reduce_bf16``: the gradient crosses the wire in bf16
+  (half the bytes) but is summed in fp32 -- a direct all-to-all reduce-scatter over
+  the xGMI full mesh (every peer pair has its own link) followed by an fp32 local sum
+  kernel and a bf16 all-gather ("bf16/fp32 gradient buckets").
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_LIB = None
+_NCCL_DT = {torch.float32: 7, torch.float16: 6, torch.bfloat16: 9, torch.int32: 2, torch.int64: 4,
+            torch.uint8: 1, torch.int8: 0, torch.float64: 8}
+_NCCL_OP = {'sum': 0, 'prod': 1, 'max': 2, 'min': 3, 'mean': 4, 'avg': 4}
+_TIMING = os.environ.get('HETU_COMM_TRACE', '0') == '1'   # timed completion events (bucket timeline)
+
+
+class RCCLError(RuntimeError):
+    pass
+
+
+def _rccl_path():
+    import glob
+    d = os.path.join(os.path.dirname(torch.__file__), 'lib')
+    cands = glob.glob(os.path.join(d, 'librccl.so*')) + ['/opt/rocm/lib/librccl.so.1']
+    return os.environ.get('HETU_RCCL_LIB', cands[0] if cands else 'librccl.so.1')
+
+
+def lib():
+    """libhetu_comm.so with RCCL loaded, or None (no library / no RCCL)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB or None
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'lib', 'libhetu_comm.so')
+    try:
+        L = ctypes.CDLL(path)
+    except OSError:
+        _LIB = False
+        return None
+    P, I, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    sig = {
+        'hcomm_load': ([ctypes.c_char_p], I), 'hcomm_loaded': ([], I), 'hcomm_version': ([], I),
+        'hcomm_error_string': ([I], ctypes.c_char_p), 'hcomm_set_channels': ([I, I], None),
+        'hcomm_unique_id': ([ctypes.c_char_p], I), 'hcomm_unique_id_bytes': ([], I),
+        'hcomm_init': ([ctypes.c_char_p, I, I, ctypes.POINTER(P)], I),
+        'hcomm_split': ([P, I, I, ctypes.POINTER(P)], I), 'hcomm_destroy': ([P], I), 'hcomm_abort': ([P], I),
+        'hcomm_async_error': ([P], I), 'hcomm_count': ([P], I), 'hcomm_user_rank': ([P], I),
+        'hcomm_all_reduce': ([P, P, P, SZ, I, I, P], I), 'hcomm_reduce_scatter': ([P, P, P, SZ, I, I, P], I),
+        'hcomm_all_gather': ([P, P, P, SZ, I, P], I), 'hcomm_broadcast': ([P, P, P, SZ, I, I, P], I),
+        'hcomm_reduce': ([P, P, P, SZ, I, I, I, P], I), 'hcomm_send': ([P, P, SZ, I, I, P], I),
+        'hcomm_recv': ([P, P, SZ, I, I, P], I), 'hcomm_group_start': ([], I), 'hcomm_group_end': ([], I),
+        'hcomm_all_to_all': ([P, P, P, SZ, I, P], I),
+        'hcomm_all_to_all_v': ([P, P, P, P, P, P, P, I, P], I),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes, f.restype = args, res
+    if L.hcomm_load(_rccl_path().encode()) != 0:
+        _LIB = False
+        return None
+    _LIB = L
+    return L
+
+
+def available() -> bool:
+    return torch.cuda.is_available() and lib() is not None
+
+
+def _check(r, what):
+    if r != 0:
+        L = lib()
+        msg = L.hcomm_error_string(r).decode() if L is not None and r > 0 else 'error %d' % r
+        raise RCCLError('RCCL %s failed: %s' % (what, msg))
+
+
+class Work(object):
+    """Handle of an async collective: ``wait()`` orders the caller's current stream
+    after it (no host sync); ``synchronize()`` blocks the host."""
+    __slots__ = ('event', 'post')
+
+    def __init__(self, event, post=None):
+        self.event, self.post = event, post
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+        if self.post is not None:
+            self.post()
+            self.post = None
+        return True
+
+    def is_completed(self):
+        return self.event.query()
+
+    def synchronize(self):
+        self.event.synchronize()
+
+
+class NativeComm(object):
+    """One RCCL communicator (a group of ``nrank`` ranks, this process = ``rank``)."""
+
+    _store_seq = {}
+
+    def __init__(self, handle, rank, nrank):
+        self.handle = ctypes.c_void_p(handle) if not isinstance(handle, ctypes.c_void_p) else handle
+        self.rank, self.nrank = rank, nrank
+        self.stream = torch.cuda.Stream(priority=-1)
+        self._bf16_ws = {}
+
+    # ---- construction -----------------------------------------------------------
+    @classmethod
+    def from_store(cls, store, key, rank, nrank, channels=None):
+        """Rendezvous: group rank 0 creates the unique id and publishes it in the TCP
+        store under ``key``; everyone initialises its rank.  All members call."""
+        L = lib()
+        if L is None:
+            raise RCCLError('libhetu_comm / RCCL unavailable')
+        if channels:
+            L.hcomm_set_channels(int(channels[0]), int(channels[1]))
+        nb = L.hcomm_unique_id_bytes()
+        if rank == 0:
+            buf = ctypes.create_string_buffer(nb)
+            _check(L.hcomm_unique_id(buf), 'get_unique_id')
+            store.set(key, buf.raw)
+            uid = buf.raw
+        else:
+            uid = bytes(store.get(key))
+        h = ctypes.c_void_p()
+        _check(L.hcomm_init(uid, int(nrank), int(rank), ctypes.byref(h)), 'comm_init_rank')
+        return cls(h, rank, nrank)
+
+    def split(self, color, key):
+        """ncclCommSplit: every rank of this communicator calls; ``color < 0`` opts out."""
+        h = ctypes.c_void_p()
+        _check(lib().hcomm_split(self.handle, int(color), int(key), ctypes.byref(h)), 'comm_split')
+        if color < 0 or not h.value:
+            return None
+        L = lib()
+        return NativeComm(h, L.hcomm_user_rank(h), L.hcomm_count(h))
+
+    def destroy(self):
+        if self.handle and self.handle.value:
+            lib().hcomm_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def abort(self):
+        if self.handle and self.handle.value:
+            lib().hcomm_abort(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def async_error(self):
+        return lib().hcomm_async_error(self.handle)
+
+    # ---- stream plumbing --------------------------------------------------------
+    def _run(self, fn, tensors, async_op, post=None):
+        """Run ``fn(stream_ptr)``: on the comm stream after the current stream's work
+        (async), or on the current stream itself (sync)."""
+        cur = torch.cuda.current_stream()
+        if not async_op:
+            fn(cur.cuda_stream)
+            if post is not None:
+                post()
+            return None
+        s = self.stream
+        s.wait_stream(cur)
+        fn(s.cuda_stream)
+        for t in tensors:
+            if t is not None and t.is_cuda:
+                t.record_stream(s)
+        ev = torch.cuda.Event(enable_timing=_TIMING)
+        ev.record(s)
+        return Work(ev, post)
+
+    # ---- collectives ------------------------------------------------------------
+    def all_reduce(self, t, op='sum', async_op=False):
+        assert t.is_contiguous()
+        L = lib()
+        nop = _NCCL_OP[op]
+        return self._run(lambda st: _check(L.hcomm_all_reduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
+                                                              _NCCL_DT[t.dtype], nop, st), 'all_reduce'),
+                         (t,), async_op)
+
+    def reduce_scatter(self, out, inp, op='sum', async_op=False):
+        inp = inp.contiguous()
+        assert out.is_contiguous() and out.numel() * self.nrank == inp.numel()
+        L = lib()
+        return self._run(lambda st: _check(L.hcomm_reduce_scatter(self.handle, inp.data_ptr(), out.data_ptr(),
+                                                                  out.numel(), _NCCL_DT[inp.dtype], _NCCL_OP[op],
+                                                                  st), 'reduce_scatter'),
+                         (out, inp), async_op)
+
+    def all_gather(self, out, inp, async_op=False):
+        inp = inp.contiguous()
+        assert out.is_contiguous() and out.numel() == inp.numel() * self.nrank
+        L = lib()
+        return self._run(lambda st: _check(L.hcomm_all_gather(self.handle, inp.data_ptr(), out.data_ptr(),
+                                                              inp.numel(), _NCCL_DT[inp.dtype], st), 'all_gather'),
+                         (out, inp), async_op)
+
+    def broadcast(self, t, root=0, async_op=False):
+        assert t.is_contiguous()
+        L = lib()
+        return self._run(lambda st: _check(L.hcomm_broadcast(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
+                                                             _NCCL_DT[t.dtype], int(root), st), 'broadcast'),
+                         (t,), async_op)
+
+    def reduce(self, t, root=0, op='sum', async_op=False):
+        assert t.is_contiguous()
+        L = lib()
+        return self._run(lambda st: _check(L.hcomm_reduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
+                                                          _NCCL_DT[t.dtype], _NCCL_OP[op], int(root), st),
+                                           'reduce'), (t,), async_op)
+
+    def all_to_all(self, out, inp, async_op=False):
+        inp = inp.contiguous()
+        assert out.is_contiguous() and out.numel() == inp.numel() and inp.numel() % self.nrank == 0
+        L = lib()
+        chunk = inp.numel() // self.nrank
+        return self._run(lambda st: _check(L.hcomm_all_to_all(self.handle, inp.data_ptr(), out.data_ptr(), chunk,
+                                                              _NCCL_DT[inp.dtype], st), 'all_to_all'),
+                         (out, inp), async_op)
+
+    def p2p(self, ops, async_op=True):
+        """ops: [('send'|'recv', tensor, peer)] as one RCCL group."""
+        L = lib()
+
+        def run(st):
+            _check(L.hcomm_group_start(), 'group_start')
+            for kind, t, peer in ops:
+                f = L.hcomm_send if kind == 'send' else L.hcomm_recv
+                _check(f(self.handle, t.data_ptr(), t.numel(), _NCCL_DT[t.dtype], int(peer), st), kind)
+            _check(L.hcomm_group_end(), 'group_end')
+        return self._run(run, [t for _, t, _ in ops], async_op)
+
+    # ---- bf16 wire, fp32 accumulation --------------------------------------------
+    def _ws(self, n, dtype, tag):
+        k = (tag, dtype)
+        b = self._bf16_ws.get(k)
+        if b is None or b.numel() < n:
+            b = torch.empty(max(n, 1), dtype=dtype, device='cuda')
+            self._bf16_ws[k] = b
+        return b[:n]
+
+    def all_reduce_bf16(self, t, async_op=False):
+        """fp32 ``t`` summed across ranks with bf16 on the wire: bf16 all-to-all (=
+        reduce-scatter traffic, padded to P chunks of a multiple of 8), fp32 sum of the
+        P received chunks, bf16 all-gather of the reduced chunk, fp32 result in place."""
+        from ..kernels import comm as KC
+        P, n = self.nrank, t.numel()
+        assert t.dtype == torch.float32 and t.is_contiguous()
+        c = -(-n // (8 * P)) * 8
+        send = self._ws(c * P, torch.bfloat16, 'send')
+        recv = self._ws(c * P, torch.bfloat16, 'recv')
+        red = self._ws(c, torch.bfloat16, 'red')
+        L = lib()
+
+        def run(st):
+            KC.cast_f32_bf16(t, send, st)
+            _check(L.hcomm_all_to_all(self.handle, send.data_ptr(), recv.data_ptr(), c, 9, st), 'all_to_all')
+            KC.sum_chunks_bf16(recv, P, c, red, st)           # fp32 accumulate, bf16 out
+            _check(L.hcomm_all_gather(self.handle, red.data_ptr(), send.data_ptr(), c, 9, st), 'all_gather')
+            KC.cast_bf16_f32(send, t, st)
+        return self._run(run, (t, send, recv, red), async_op)
+
+    def __repr__(self):
+        return 'NativeComm(rank=%d, nrank=%d)' % (self.rank, self.nrank)
+
+
+def world_from_dist(group=None, key_prefix='hetu_rccl') -> Optional[NativeComm]:
+    """Native communicator over the ranks of an initialised torch.distributed group
+    (its store carries the unique id).  Every member calls."""
+    import torch.distributed as dist
+    if not available() or not dist.is_initialized():
+        return None
+    store = dist.distributed_c10d._get_default_store()
+    ranks = None if group is None else dist.get_process_group_ranks(group)
+    rank = dist.get_rank(group)
+    nrank = dist.get_world_size(group)
+    name = 'world' if ranks is None else '_'.join(map(str, ranks))
+    seq = NativeComm._store_seq[name] = NativeComm._store_seq.get(name, 0) + 1   # same order on every member
+    key = '%s/%s/%d' % (key_prefix, name, seq)
+    ch = os.environ.get('HETU_RCCL_CHANNELS')
+    channels = tuple(int(x) for x in ch.split(',')) if ch else None
+    return NativeComm.from_store(store, key, rank, nrank, channels)

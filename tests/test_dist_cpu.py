@@ -158,3 +158,49 @@ def test_resnet50_dp_bench_path_keeps_replicas_identical():
     assert p0.keys() == p1.keys() and len(p0) >= 3
     for k in p0:
         np.testing.assert_array_equal(p0[k], p1[k])
+
+
+def _trace_worker(rank, world, port, q, order):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR='127.0.0.1',
+                      MASTER_PORT=str(port), HETU_USE_CONFIG='0', HETU_COMM_TRACE='1', HETU_GRAD_ORDER=order)
+    import hetu_61a7_amd as ht
+    rng = np.random.RandomState(3)
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    h = x
+    dims = [64, 256, 256, 256, 256, 8]
+    for i in range(len(dims) - 1):
+        W = ht.Variable(name='w%d' % i, value=(rng.randn(dims[i], dims[i + 1]) * 0.1).astype(np.float32))
+        h = ht.matmul_op(h, W)
+        if i < len(dims) - 2:
+            h = ht.relu_op(h)
+    loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(h, y_), [0])
+    train = ht.optim.SGDOptimizer(0.01).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'), bucket_mb=0.25)
+    X = rng.randn(64, 64).astype(np.float32)
+    Y = np.eye(8, dtype=np.float32)[rng.randint(0, 8, 64)]
+    for _ in range(2):
+        ex.run('train', feed_dict={x: X, y_: Y})
+    q.put((rank, train.comm_trace()))
+    from hetu_61a7_amd.parallel import comm
+    comm.destroy()
+
+
+@pytest.mark.parametrize('order', ['forward', 'reverse'])
+def test_buckets_launch_before_backward_ends(order):
+    """Overlap of the bucketed all-reduce with the backward pass:
+    every bucket but the last is launched while gradients are still being
+    produced, i.e. before the optimizer step that closes the backward."""
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_trace_worker, args=(r, 2, port, q, order)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, tr in res:
+        assert len(tr) >= 3, tr
+        early = [b for b in tr if b['launch_host_ms'] < 0]
+        assert len(early) >= len(tr) - 1, tr

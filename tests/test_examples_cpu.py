@@ -67,7 +67,7 @@ def test_parallel_equivalence_examples(tmp_path):
     script = os.path.join(d, 'mlp_parallel.py')
     runs = [[sys.executable, script, '--mode', 'base', '--cpu'],
             heturun + ['-w', '2', sys.executable, script, '--mode', 'pp', '--schedule', 'gpipe'],
-            heturun + ['-w', '3', sys.executable, script, '--mode', 'pp', '--schedule', 'pipedream'],
+            heturun + ['-w', '3', sys.executable, script, '--mode', 'pp', '--schedule', 'pipedream_flush'],
             heturun + ['-w', '4', sys.executable, script, '--mode', 'dp_pp', '--replicas', '2'],
             heturun + ['-w', '2', sys.executable, script, '--mode', 'mp', '--split', 'right'],
             heturun + ['-w', '3', sys.executable, os.path.join(d, 'complex_pipeline_mlp.py')],

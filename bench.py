@@ -39,6 +39,7 @@ def parse():
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     p.add_argument('--bucket-mb', type=float, default=32)
     p.add_argument('--zero', type=int, default=0, help='1: ZeRO-1 sharded optimizer state over the DP group')
+    p.add_argument('--pp', type=int, default=None, help='bert: force the Galvatron pipeline degree')
     p.add_argument('--op-profile', default=None, help='write per-op-type GPU time (ms) to this file')
     p.add_argument('--grad-wire', default=os.environ.get('HETU_GRAD_WIRE', 'fp32'), choices=['fp32', 'bf16'],
                    help='DP gradient all-reduce wire format (bf16: fp32 accumulation)')

@@ -161,9 +161,14 @@ class BertModel(object):
             with _stage_ctx(pl, i + 1):
                 # additive key mask [B, S]: 0 keep, -10000 masked (built on
                 # every stage from the fed mask, so it never crosses a stage boundary)
-                if i == 0 or pl is not None and pl(i + 1) != pl(i):
+                if i == 0:
                     m = ht.array_reshape_op(attention_mask, (B, S))
                     m = ht.mul_byconst_op(ht.addbyconst_op(m, -1.0), 10000.0)
+                elif pl is not None and pl(i + 1) != pl(i):
+                    from ..ops.node import shadow_ids
+                    with shadow_ids():
+                        m = ht.array_reshape_op(attention_mask, (B, S))
+                        m = ht.mul_byconst_op(ht.addbyconst_op(m, -1.0), 10000.0)
                 h = layer(h, m)
         with _stage_ctx(pl, len(self.layers) + 1):
             first = ht.array_reshape_op(ht.slice_op(ht.array_reshape_op(h, (B, S, H)), (0, 0, 0), (B, 1, H)),
@@ -194,10 +199,14 @@ class BertForPreTraining(object):
         self.bert = BertModel(cfg, placement)
         head = len(self.bert.layers) + 1
         if placement is not None and placement(head) != placement(0):
-            # pipelined: the MLM decoder lives on the last stage, so it gets its own
-            # weight instead of shipping the tied 30522 x H table across stages
-            with _stage_ctx(placement, head):
+            # pipelined: the MLM decoder lives on the last stage, so it holds its own copy
+            # of the tied 30522 x H table instead of shipping it across stages every step;
+            # ``tied_to`` keeps the copies equal (same initial values, gradients summed
+            # between the two stages each step: pipeline_exec ties)
+            from ..ops.node import shadow_ids
+            with _stage_ctx(placement, head), shadow_ids():
                 E = _w('cls_decoder_weight', (cfg.vocab_size, cfg.hidden_size), cfg)
+            E.tied_to = self.bert.word_embeddings
         else:
             E = self.bert.word_embeddings
         self.cls = BertPreTrainingHeads(cfg, E)
@@ -296,7 +305,7 @@ def bert_pretrain_graph(cfg, lr=1e-5, optimizer=None, plan=None, placement=None)
 def synthetic_bert_batch(cfg, seed=0, mask_prob=0.15):
     rng = np.random.default_rng(seed)
     B, S = cfg.batch_size, cfg.seq_len
-    ids = rng.integers(1000, cfg.vocab_size, (B, S)).astype(np.int64)
+    ids = rng.integers(min(1000, cfg.vocab_size // 2), cfg.vocab_size, (B, S)).astype(np.int64)
     types = np.zeros((B, S), np.int64)
     types[:, S // 2:] = 1
     mask = np.ones((B, S), np.float32)
@@ -310,35 +319,71 @@ def bert_bench(args, world, rank, local):
     """Benchmark step for BASELINE config 4 (reference
     examples/nlp/bert/scripts/train_hetu_bert_base_dp.sh: BERT-base, seq 128,
     batch 64 per GPU, Adam lr 1e-5, MLM + NSP pretraining), bf16 compute,
-    synthetic token ids.  On N > 1 GPUs the Galvatron planner picks the
-    DP x PP layout for the node (``galvatron.plan_bert``); for BERT-base it
-    selects pure DP (the model fits every GPU; PP only adds a bubble), run with
-    the bucketed RCCL all-reduce.
+    synthetic token ids.  On N > 1 GPUs the Galvatron planner picks the DP x PP
+    layout for the node (``galvatron.plan_bert``; ``args.pp`` forces the pipeline
+    degree) and the step runs EXACTLY that plan:
+
+    * pp = 1: data parallel, bucketed RCCL all-reduce;
+    * pp > 1: every planner layer goes to its stage's device group
+      (``plan_placement``), the stages run the GPipe schedule over the plan's
+      micro-batches, each stage is data parallel over its ``N / pp`` replicas
+      (replica r of stage s talks to replica r of stage s+1) and all-reduces its
+      gradients over the replica group.
+
+    Tensor parallelism inside a layer is left to the dispatch lowering
+    (``parallel.lowering``); the bench caps the planner at tp = 1
+    (``HETU_GALVATRON_MAX_TP`` raises it).  Weak scaling: the global batch is
+    ``batch * N`` in every layout.  ``args.bert_config`` (tests) replaces BERT-base.
     Returns (step_fn, samples_per_step, config, metric, finish_fn)."""
+    import os
     import torch
     import hetu_61a7_amd as H
     from ..parallel.galvatron import GalvatronPlanner, Hardware, bert_layers
     B = args.batch or 64
-    cfg = BertConfig.base(batch_size=B, seq_len=128)
+    cfg = getattr(args, 'bert_config', None) or BertConfig.base(batch_size=B, seq_len=128)
+    cfg.batch_size = B
     specs = bert_layers(cfg.hidden_size, cfg.num_hidden_layers, cfg.seq_len, cfg.vocab_size)
-    plan = GalvatronPlanner(specs, hw=Hardware(gpus=world)).search(B * world)
-    if plan.pp > 1 or max(plan.tp) > 1:
-        raise NotImplementedError('bench: planner chose %s; only its DP layout is benchmarked' % plan.short())
-    feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-5)
-    kw = dict(mixed_precision=args.dtype, seed=1234, bucket_mb=getattr(args, 'bucket_mb', 32),
-              zero=getattr(args, 'zero', 0))
-    if world > 1:
-        ex = H.Executor({'train': [loss, train]}, dist_strategy=H.dist.DataParallel('allreduce'), **kw)
+    planner = GalvatronPlanner(specs, hw=Hardware(gpus=world), max_tp=int(os.environ.get('HETU_GALVATRON_MAX_TP', '1')))
+    force_pp = getattr(args, 'pp', None)
+    plan = planner.search(B * world, pp_options=[force_pp] if force_pp else None)
+    if max(plan.tp) > 1:
+        raise NotImplementedError('bench: tensor-parallel layers (planner chose %s) are not wired into the '
+                                  'BERT bench graph' % plan.short())
+    on_gpu = torch.cuda.is_available()
+    dev = torch.device('cuda', local) if on_gpu else torch.device('cpu')
+    kw = dict(mixed_precision=args.dtype if on_gpu else None, seed=1234,
+              bucket_mb=getattr(args, 'bucket_mb', 32), zero=getattr(args, 'zero', 0))
+    opt = None
+    if getattr(args, 'optimizer', None) == 'sgd':          # tests: gradient-exact comparisons
+        opt = optim.SGDOptimizer(learning_rate=getattr(args, 'lr', 1e-2))
+    if plan.pp > 1:
+        kw.pop('zero')
+        cfg.batch_size = B * plan.pp                 # one replica's batch: global / (N / pp)
+        feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-5, plan=plan, optimizer=opt)
+        ex = H.Executor({'train': [loss, train]}, pipeline='gpipe', **kw)
+        sub = ex.subexecutor['train']
+        replica, m = sub.replica, plan.micro_batches
+        parallelism = 'pp%d x dp%d (galvatron plan: %s)' % (plan.pp, world // plan.pp, plan.short())
     else:
-        ex = H.Executor({'train': [loss, train]}, ctx=H.gpu(local), **kw)
-    dev = torch.device('cuda', local)
-    batch = synthetic_bert_batch(cfg, seed=10 + rank)
+        feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-5, optimizer=opt)
+        if world > 1:
+            ex = H.Executor({'train': [loss, train]}, dist_strategy=H.dist.DataParallel('allreduce'), **kw)
+        else:
+            ex = H.Executor({'train': [loss, train]}, ctx=H.gpu(local) if on_gpu else H.cpu(0), **kw)
+        replica, m = rank, None
+        parallelism = 'dp%d (galvatron plan: %s)' % (world, plan.short())
+    batch = synthetic_bert_batch(cfg, seed=10 + replica)
     fd = {feeds[k]: torch.from_numpy(v).to(dev) for k, v in batch.items()}
 
     def step():
-        ex.run('train', feed_dict=fd)
+        if m is None:
+            return ex.run('train', feed_dict=fd)
+        return ex.run('train', feed_dict=fd, batch_num=m)
 
-    conf = {'model': 'BERT-base (L12 H768 A12, MLM+NSP)', 'global_batch': B * world, 'seq_len': 128,
-            'parallelism': 'dp%d (galvatron plan: %s)' % (world, plan.short()), 'optimizer': 'adam',
-            'per_gpu_batch': B}
+    conf = {'model': 'BERT-base (L12 H768 A12, MLM+NSP)', 'global_batch': B * world, 'seq_len': cfg.seq_len,
+            'parallelism': parallelism, 'optimizer': 'adam', 'per_gpu_batch': B,
+            'plan': {'pp': plan.pp, 'micro_batches': plan.micro_batches, 'stages': plan.stages,
+                     'est_ms': round(plan.time * 1e3, 3)}}
+    step.executor = ex
+    step.plan = plan
     return step, B * world, conf, 'samples/sec (whole node) BERT-base pretraining', None

@@ -30,11 +30,48 @@ from .. import ndarray
 G_NODE_ID = 0
 
 
+_SHADOW_DEPTH = [0]
+
+
 def _next_id():
-    global G_NODE_ID
+    global G_NODE_ID, G_SHADOW_ID
+    if _SHADOW_DEPTH[0]:
+        i = G_SHADOW_ID
+        G_SHADOW_ID += 1
+        return i
     i = G_NODE_ID
     G_NODE_ID += 1
     return i
+
+
+class shadow_ids(object):
+    """``with shadow_ids():`` nodes created inside take ids from the shadow range:
+    placement-only additions (per-stage copies of a tied weight or of a mask
+    computation) then leave the ids of the rest of the graph as in the unplaced model."""
+
+    def __enter__(self):
+        _SHADOW_DEPTH[0] += 1
+        return self
+
+    def __exit__(self, *a):
+        _SHADOW_DEPTH[0] -= 1
+
+
+# ids of "shadow" nodes (the pipeline-stage copy of a tied weight): a separate range
+# below the PS key space (< 2^20) that does not advance the main counter, so adding
+# such a copy leaves every other node's id -- and with it its ``seed + id`` initial
+# value (reference initializers.py:13-16) -- unchanged
+G_SHADOW_ID = 900000
+
+
+def reassign_shadow_id(node):
+    """Move ``node`` (just created) out of the main id sequence."""
+    global G_NODE_ID, G_SHADOW_ID
+    if node.id == G_NODE_ID - 1:
+        G_NODE_ID -= 1
+    node.id = G_SHADOW_ID
+    G_SHADOW_ID += 1
+    return node
 
 
 class Op(object):

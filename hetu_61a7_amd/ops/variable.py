@@ -73,7 +73,10 @@ class PlaceholderOp(Op):
                 t = t.float()
             t = t.to(device)
         else:
-            t = self.initializer(self, seed, device=device)
+            # a parameter tied to another (``tied_to``: the pipeline-stage copy of a shared
+            # weight) draws exactly its source's initial values (seed + source id)
+            src = getattr(self, 'tied_to', None)
+            t = self.initializer(src if src is not None else self, seed, device=device)
         if self.mp_split is not None:
             t = self.mp_split.slice_tensor(t)
         return t

@@ -324,7 +324,7 @@ class OptimizerOp(Op):
             g = self.inputs[i]
             if p in self.ps_params:
                 continue
-            if g.use_indexed_slices or getattr(p, 'is_embed', False) and g.use_indexed_slices:
+            if g.use_indexed_slices and not getattr(p, 'force_dense_grad', False):
                 sparse.append(p)
             else:
                 dense.append(p)
@@ -495,6 +495,8 @@ class OptimizerOp(Op):
             self._pending_sparse.append((p, value))
             return
         dst = self.flat.view(p, 'grad')
+        if isinstance(value, ndarray.IndexedSlices):      # dense-updated sparse gradient
+            value = value.to_dense()
         if not (value.data_ptr() == dst.data_ptr() and value.dtype == dst.dtype and
                 value.stride() == dst.stride()):
             if value.shape != dst.shape:

@@ -259,6 +259,32 @@ class PipelineSubExecutor(object):
                 if len(ranks) > 1:
                     self.replica_comms[s] = C.new_group_comm(ranks)
 
+        # tied parameters across stages (``p.tied_to = q``, e.g. BERT's MLM decoder on the
+        # last stage and the word embeddings on the first): replica r of each of the two
+        # stages sums the pair's gradients over a 2-rank group before every update, so
+        # the copies (identical at init) stay identical -- Megatron's embedding tie.
+        # Groups are created collectively, in topo order, by every rank.
+        self.ties = {}
+        pairs = []
+        for n in topo:
+            t = getattr(n, 'tied_to', None)
+            if isinstance(n, PlaceholderOp) and t is not None and n in stage_of and t in stage_of \
+                    and stage_of[n] != stage_of[t]:
+                pairs.append((n, t))
+        if pairs and dist.is_initialized():
+            from . import comm as C
+            for a, b in pairs:
+                sa, sb = stage_of[a], stage_of[b]
+                for r in range(min(self._nrep(sa), self._nrep(sb))):
+                    g = C.new_group_comm([self.rank_of(sa, r), self.rank_of(sb, r)])
+                    if self.replica == r and self.stage in (sa, sb):
+                        mine = a if self.stage == sa else b
+                        self.ties[mine] = g
+                        # the pair's summed gradient is dense (the decoder's is), so the
+                        # copy whose own gradient is row-sparse (the embedding lookup's)
+                        # takes the dense update, exactly like the untied single graph
+                        mine.force_dense_grad = True
+
         # ---- parameters, local optimizer ----------------------------------------------------
         for p in self.params:
             config.init_param(p)
@@ -298,6 +324,24 @@ class PipelineSubExecutor(object):
             op.ps_dense = PSDense(op.flat, PS_KEY_HETPIPE_STAGE + self.stage, self.config, publish=self.replica == 0)
 
     # ---------------------------------------------------------------------------------------
+    def _nrep(self, s):
+        return len([d for d in self.stage_keys[s] if d[1] == 'gpu'])
+
+    def _sum_ties(self, grads):
+        """grads: {local optimizer index: tensor} -- sum the tied parameters' gradients
+        with the other stage's copy (in place; dense gradients only)."""
+        if not self.ties:
+            return grads
+        for i, g in list(grads.items()):
+            c = self.ties.get(self.opt.param_of_input[i])
+            if c is not None:
+                if isinstance(g, ndarray.IndexedSlices):
+                    g = g.to_dense()
+                g = g.float().contiguous().clone()
+                c.all_reduce(g, 'sum')
+                grads[i] = g
+        return grads
+
     def _compute(self, nodes, vals, aux):
         for n in nodes:
             args = []
@@ -409,6 +453,7 @@ class PipelineSubExecutor(object):
                 states[mb] = None
         self.p2p.flush()
         if self.opt is not None and acc:
+            acc = self._sum_ties(acc)
             op = self.opt
             op.begin_step()
             for i in range(len(op.inputs)):
@@ -419,6 +464,7 @@ class PipelineSubExecutor(object):
         return results
 
     def _apply(self, grads):
+        grads = self._sum_ties(grads)
         op = self.opt
         op.begin_step()
         for i in range(len(op.inputs)):

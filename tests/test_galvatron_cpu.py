@@ -130,3 +130,83 @@ def test_calibrated_hardware_model():
     assert hw.flops > 1e8 and hw.gpus == 8
     plan = GalvatronPlanner(bert_layers(64, 2, 16, 1000), hw=hw).search(32)
     assert plan.pp >= 1 and plan.time > 0
+
+
+def _floats(r):
+    import numpy as np
+    if r is None:
+        return None
+    if isinstance(r, (list, tuple)):
+        return [_floats(x) for x in r]
+    if hasattr(r, 'asnumpy'):
+        r = r.asnumpy()
+    if hasattr(r, 'detach'):
+        r = r.detach().cpu().numpy()
+    return float(np.asarray(r, dtype=np.float64).mean())
+
+
+def _bench_worker(rank, world, port, pp, q, batch):
+    import os
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR='127.0.0.1',
+                      MASTER_PORT=str(port), HETU_USE_CONFIG='0')
+    import types
+    import numpy as np
+    from hetu_61a7_amd.models.bert import BertConfig, bert_bench
+    cfg = BertConfig(vocab_size=512, hidden_size=32, num_hidden_layers=4, num_attention_heads=2,
+                     intermediate_size=64, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
+                     max_position_embeddings=32, seq_len=16, batch_size=4)
+    args = types.SimpleNamespace(batch=batch, dtype='fp32', bucket_mb=1, zero=0, pp=pp, bert_config=cfg,
+                                 optimizer=os.environ.get('HETU_TEST_OPT'), lr=0.5)
+    step, samples, conf, _, _ = bert_bench(args, world, rank, rank)
+    losses = []
+    for _ in range(int(os.environ.get('HETU_TEST_STEPS', '2'))):
+        r = step()
+        losses.append(_floats(r))
+    ex = step.executor
+    params = {n.name: v.detach().cpu().numpy().copy() for n, v in ex.config.placeholder_to_arr_map.items()
+              if getattr(n, 'trainable', False) and hasattr(v, 'detach')}
+    q.put((rank, conf, samples, params, losses))
+    if world > 1:
+        from hetu_61a7_amd.parallel import comm
+        comm.destroy()
+
+
+def _spawn(world, pp, batch):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, pp, q, batch)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda t: t[0])
+
+
+def test_bert_bench_runs_forced_pp2_plan_like_single_process():
+    """bench.py --model bert with a forced pp=2 Galvatron plan: the two stages (one GPU
+    each, GPipe over the plan's micro-batches) train the same model as one process on
+    the same global batch -- Adam is invariant to the micro-batch gradient sum."""
+    import numpy as np
+    ref = _spawn(1, None, 8)[0]
+    res = _spawn(2, 2, 4)
+    assert res[0][1]['plan']['pp'] == 2 and res[0][1]['parallelism'].startswith('pp2')
+    assert res[0][2] == ref[2] == 8                              # global batch 4 x 2 GPUs
+    merged = {}
+    for _, _, _, params, _ in res:
+        assert not set(params) & set(merged)
+        merged.update(params)
+    # the last stage holds its own copy of the tied MLM decoder / word-embedding table
+    dec = merged.pop('cls_decoder_weight')
+    emb = [k for k in merged if k.endswith('word_embeddings')][0]
+    np.testing.assert_array_equal(dec, merged[emb])            # copies kept identical
+    assert set(merged) == set(ref[3]), (sorted(set(merged) ^ set(ref[3])))
+    for k, v in ref[3].items():
+        np.testing.assert_allclose(merged[k], v, rtol=2e-3, atol=2e-6, err_msg=k)

@@ -93,4 +93,29 @@ def available() -> bool:
     return has_kernels()
 
 
+# ---- dispatch accounting ---------------------------------------------------------------
+# Every op that COULD run a hand-written kernel but takes a library / aten path for a
+# GPU tensor records it here (op name -> count), so a test or a bench can assert that a
+# steady-state step never leaves the native path.  ``HETU_STRICT_NATIVE=1`` turns such a
+# fallback into an error.
+FALLBACKS = {}
+NATIVE_CALLS = {}
+_STRICT = os.environ.get('HETU_STRICT_NATIVE', '0') == '1'
+
+
+def record_fallback(name, reason=''):
+    FALLBACKS[name] = FALLBACKS.get(name, 0) + 1
+    if _STRICT:
+        raise RuntimeError('HETU_STRICT_NATIVE: %s left the hand-written kernel path (%s)' % (name, reason))
+
+
+def record_native(name):
+    NATIVE_CALLS[name] = NATIVE_CALLS.get(name, 0) + 1
+
+
+def reset_dispatch_stats():
+    FALLBACKS.clear()
+    NATIVE_CALLS.clear()
+
+
 from . import elementwise, norm, softmax, optim, pool, sparse, reduce  # noqa: E402,F401

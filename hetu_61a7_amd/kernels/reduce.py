@@ -44,6 +44,27 @@ def reduce_last(x2: torch.Tensor, scale: float = 1.0, out_dtype=None) -> torch.T
     return (x2.float().sum(1) * scale).to(out_dtype)
 
 
+def reduce_sum(x: torch.Tensor, dims, keepdim: bool = False) -> torch.Tensor:
+    """Sum over ``dims`` (any set) with the native middle-axis reduction, one pass per
+    reduced dim (fp32 result)."""
+    dims = sorted({d % x.dim() for d in dims}, reverse=True)
+    y = x.contiguous()
+    shape = list(x.shape)
+    for d in dims:
+        outer = 1
+        for s_ in shape[:d]:
+            outer *= s_
+        inner = 1
+        for s_ in shape[d + 1:]:
+            inner *= s_
+        y = reduce_mid(y.reshape(outer, shape[d], inner), out_dtype=torch.float32)
+        shape[d] = 1
+        y = y.reshape(shape)
+    if not keepdim:
+        y = y.reshape([s_ for i, s_ in enumerate(shape) if i not in dims])
+    return y
+
+
 def sum_to_shape(g: torch.Tensor, shape) -> torch.Tensor:
     """Reduce a broadcast gradient back to ``shape`` (numpy broadcasting rules)."""
     shape = tuple(shape)

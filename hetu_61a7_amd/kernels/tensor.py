@@ -1,0 +1,328 @@
+"""Bindings of ``csrc/kernels/tensor_ops.hip`` and ``losses.hip``: the layout,
+indexing, scan, sort and loss kernels of the op long tail (concat / pad / roll /
+repeat / gather / scatter-add / cumsum / argmax / argsort / p-norm / CE / BCE / NLL).
+
+Each function takes torch tensors on the GPU and runs on the current HIP stream;
+the op modules call them for GPU tensors (``kernels.native``) and keep their torch
+reference path for the CPU backend.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import fn, check, stream_ptr, P, I32, I64, F32, record_native
+
+_ELEM = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.int64: 8, torch.int32: 4, torch.uint8: 1,
+         torch.int8: 1, torch.bool: 1, torch.float64: 8, torch.int16: 2}
+_ARR = ctypes.c_int64 * 8
+
+
+def _arr(v):
+    a = _ARR()
+    for i, x in enumerate(v):
+        a[i] = int(x)
+    return a
+
+
+def _bf(t):
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError('kernel takes fp32 / bf16, got %s' % t.dtype)
+
+
+def _dims(shape, dim):
+    dim = dim % len(shape) if len(shape) else 0
+    outer = 1
+    for s in shape[:dim]:
+        outer *= int(s)
+    inner = 1
+    for s in shape[dim + 1:]:
+        inner *= int(s)
+    return outer, int(shape[dim]) if len(shape) else 1, inner
+
+
+# ---- strided copies --------------------------------------------------------------------
+def nd_copy(src, dst, shift=None, imod=None):
+    """dst[c] = src[(c + shift) % imod] elementwise over dst's shape (both strided views
+    of the same dtype; src's shape may differ where imod wraps)."""
+    assert src.dtype == dst.dtype and src.is_cuda and dst.is_cuda
+    nd = dst.dim()
+    if nd == 0:
+        dst.copy_(src)
+        return dst
+    if nd > 8:
+        raise ValueError('nd_copy: at most 8 dims')
+    f = fn('hetu_nd_copy', [P, P, I32, I32, P, P, P, P, P, P])
+    check(f(src.data_ptr(), dst.data_ptr(), _ELEM[dst.dtype], nd, _arr(dst.shape), _arr(dst.stride()),
+            _arr(src.stride()), _arr(shift) if shift is not None else None,
+            _arr(imod) if imod is not None else None, stream_ptr()), 'nd_copy')
+    record_native('nd_copy')
+    return dst
+
+
+def fill_(t, value):
+    """t (contiguous) = value."""
+    assert t.is_contiguous()
+    bits = torch.tensor([value], dtype=t.dtype).view({1: torch.uint8, 2: torch.int16, 4: torch.int32,
+                                                      8: torch.int64}[_ELEM[t.dtype]]).item()
+    f = fn('hetu_fill', [P, I32, I64, ctypes.c_uint64, P])
+    check(f(t.data_ptr(), _ELEM[t.dtype], t.numel(), bits & ((1 << (8 * _ELEM[t.dtype])) - 1), stream_ptr()), 'fill')
+    return t
+
+
+def concat(tensors, axis):
+    dt = tensors[0].dtype
+    shape = list(tensors[0].shape)
+    axis = axis % len(shape)
+    shape[axis] = sum(int(t.shape[axis]) for t in tensors)
+    out = torch.empty(shape, dtype=dt, device=tensors[0].device)
+    off = 0
+    for t in tensors:
+        n = int(t.shape[axis])
+        if n:
+            nd_copy(t.to(dt), out.narrow(axis, off, n))
+        off += n
+    return out
+
+
+def pad_constant(x, pads, value):
+    """pads: [(before, after)] per dim (all dims)."""
+    shape = [int(s) + a + b for s, (a, b) in zip(x.shape, pads)]
+    out = torch.empty(shape, dtype=x.dtype, device=x.device)
+    fill_(out, value)
+    view = out
+    for d, (a, _) in enumerate(pads):
+        view = view.narrow(d, a, int(x.shape[d]))
+    nd_copy(x, view)
+    return out
+
+
+def unpad(g, pads):
+    """gradient of a constant pad: the interior view of g, contiguous."""
+    view = g
+    for d, (a, b) in enumerate(pads):
+        view = view.narrow(d, a, int(g.shape[d]) - a - b)
+    out = torch.empty(view.shape, dtype=g.dtype, device=g.device)
+    return nd_copy(view, out)
+
+
+def roll(x, shifts, dims):
+    out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    sh = [0] * x.dim()
+    md = [0] * x.dim()
+    for s, d in zip(shifts, dims):
+        d = d % x.dim()
+        n = int(x.shape[d])
+        if n:
+            sh[d] = (n - (s % n)) % n
+            md[d] = n
+    return nd_copy(x, out, sh, md)
+
+
+def repeat(x, reps):
+    """torch.Tensor.repeat semantics (reps may add leading dims)."""
+    reps = list(reps)
+    xs = [1] * (len(reps) - x.dim()) + list(x.shape)
+    xv = x.reshape(xs)
+    out = torch.empty([a * b for a, b in zip(xs, reps)], dtype=x.dtype, device=x.device)
+    return nd_copy(xv, out, [0] * len(xs), xs)
+
+
+# ---- gather / scatter-add ----------------------------------------------------------------
+def gather(x, dim, idx):
+    x = x.contiguous()
+    idx = idx.long().contiguous()
+    dim = dim % x.dim()
+    outer, nsrc, inner = _dims(x.shape, dim)
+    oi, nidx, ii = _dims(idx.shape, dim)
+    if oi != outer or ii != inner:
+        raise ValueError('gather: index must match the input outside dim')
+    out = torch.empty(idx.shape, dtype=x.dtype, device=x.device)
+    f = fn('hetu_gather_dim', [P, P, P, I64, I64, I64, I64, I32, P])
+    check(f(x.data_ptr(), idx.data_ptr(), out.data_ptr(), outer, nidx, nsrc, inner, _bf(x), stream_ptr()), 'gather')
+    record_native('gather')
+    return out
+
+
+def scatter_add(g, dim, idx, shape):
+    """dx (fp32, ``shape``) with dx[..idx..] += g (the gather gradient)."""
+    g = g.contiguous()
+    idx = idx.long().contiguous()
+    dim = dim % len(shape)
+    outer, nsrc, inner = _dims(shape, dim)
+    _, nidx, _ = _dims(idx.shape, dim)
+    dx = torch.zeros(shape, dtype=torch.float32, device=g.device)
+    f = fn('hetu_scatter_add_dim', [P, P, P, I64, I64, I64, I64, I32, P])
+    check(f(g.data_ptr(), idx.data_ptr(), dx.data_ptr(), outer, nidx, nsrc, inner, _bf(g), stream_ptr()),
+          'scatter_add')
+    record_native('scatter_add')
+    return dx
+
+
+# ---- scan / arg-reductions / sort / norm -------------------------------------------------------
+def cumsum(x, dim, bias=0.0):
+    x = x.contiguous()
+    outer, n, inner = _dims(x.shape, dim)
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    f = fn('hetu_scan_dim', [P, P, I64, I64, I64, F32, I32, P])
+    check(f(x.data_ptr(), y.data_ptr(), outer, n, inner, float(bias), _bf(x), stream_ptr()), 'scan')
+    record_native('cumsum')
+    return y
+
+
+def argmax(x, dim):
+    x = x.contiguous()
+    dim = dim % x.dim()
+    outer, n, inner = _dims(x.shape, dim)
+    shape = list(x.shape)
+    shape.pop(dim)
+    out = torch.empty(shape, dtype=torch.int64, device=x.device)
+    f = fn('hetu_argmax_dim', [P, P, I64, I64, I64, I32, P])
+    check(f(x.data_ptr(), out.data_ptr(), outer, n, inner, _bf(x), stream_ptr()), 'argmax')
+    record_native('argmax')
+    return out
+
+
+ARGSORT_MAX = 8192
+
+
+def argsort(x, dim=-1, descending=False):
+    """Per-row LDS bitonic sort (rows up to 8192 long); ties keep index order."""
+    dim = dim % x.dim()
+    xt = x.transpose(dim, -1).contiguous() if dim != x.dim() - 1 else x.contiguous()
+    n = int(xt.shape[-1])
+    if n > ARGSORT_MAX:
+        return None
+    rows = xt.numel() // max(n, 1)
+    out = torch.empty(xt.shape, dtype=torch.int64, device=x.device)
+    f = fn('hetu_argsort_rows', [P, P, I64, I64, I32, I32, P])
+    check(f(xt.data_ptr(), out.data_ptr(), rows, n, int(bool(descending)), _bf(xt), stream_ptr()), 'argsort')
+    record_native('argsort')
+    return out.transpose(dim, -1) if dim != x.dim() - 1 else out
+
+
+def pnorm(x, dim, p=2.0, keepdim=True):
+    x = x.contiguous()
+    dim = dim % x.dim()
+    outer, n, inner = _dims(x.shape, dim)
+    shape = list(x.shape)
+    shape[dim] = 1
+    y = torch.empty(shape, dtype=x.dtype, device=x.device)
+    f = fn('hetu_pnorm_dim', [P, P, I64, I64, I64, F32, I32, P])
+    check(f(x.data_ptr(), y.data_ptr(), outer, n, inner, float(p), _bf(x), stream_ptr()), 'pnorm')
+    record_native('norm')
+    return y if keepdim else y.squeeze(dim)
+
+
+def pnorm_grad(x, y, g, dim, p=2.0):
+    """y, g: the norm and its gradient with the reduced dim kept (size 1)."""
+    x = x.contiguous()
+    dim = dim % x.dim()
+    outer, n, inner = _dims(x.shape, dim)
+    y = y.to(x.dtype).contiguous()
+    g = g.to(x.dtype).contiguous()
+    dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    f = fn('hetu_pnorm_grad_dim', [P, P, P, P, I64, I64, I64, F32, I32, P])
+    check(f(x.data_ptr(), y.data_ptr(), g.data_ptr(), dx.data_ptr(), outer, n, inner, float(p), _bf(x),
+            stream_ptr()), 'pnorm_grad')
+    record_native('norm_grad')
+    return dx
+
+
+# ---- losses ------------------------------------------------------------------------------
+def _rows(y):
+    cols = int(y.shape[-1])
+    return y.numel() // max(cols, 1), cols
+
+
+def _g(g, rows):
+    g = g.float().contiguous()
+    return g, int(g.numel() == 1 and rows != 1)
+
+
+def ce_dense(y, lab):
+    y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
+    rows, cols = _rows(y)
+    out = torch.empty(y.shape[:-1], dtype=torch.float32, device=y.device)
+    check(fn('hetu_ce_dense', [P, P, P, I64, I64, I32, P])(y.data_ptr(), lab.data_ptr(), out.data_ptr(), rows,
+                                                            cols, _bf(y), stream_ptr()), 'ce_dense')
+    record_native('crossentropy')
+    return out
+
+
+def ce_dense_grad(g, y, lab):
+    y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
+    rows, cols = _rows(y)
+    g, gs = _g(g, rows)
+    dy = torch.empty(y.shape, dtype=y.dtype, device=y.device)
+    check(fn('hetu_ce_dense_grad', [P, P, P, P, I64, I64, I32, I32, P])(
+        g.data_ptr(), y.data_ptr(), lab.data_ptr(), dy.data_ptr(), rows, cols, gs, _bf(y), stream_ptr()),
+        'ce_dense_grad')
+    return dy
+
+
+def ce_sparse(y, lab, ignore=-1):
+    y = y.contiguous()
+    rows, cols = _rows(y)
+    lab = lab.long().reshape(-1).contiguous()
+    out = torch.empty(y.shape[:-1], dtype=torch.float32, device=y.device)
+    check(fn('hetu_ce_sparse', [P, P, P, I64, I64, I64, I32, P])(y.data_ptr(), lab.data_ptr(), out.data_ptr(),
+                                                                  rows, cols, int(ignore), _bf(y), stream_ptr()),
+          'ce_sparse')
+    record_native('crossentropy_sparse')
+    return out
+
+
+def ce_sparse_grad(g, y, lab, ignore=-1):
+    y = y.contiguous()
+    rows, cols = _rows(y)
+    lab = lab.long().reshape(-1).contiguous()
+    g, gs = _g(g, rows)
+    dy = torch.empty(y.shape, dtype=y.dtype, device=y.device)
+    check(fn('hetu_ce_sparse_grad', [P, P, P, P, I64, I64, I64, I32, I32, P])(
+        g.data_ptr(), y.data_ptr(), lab.data_ptr(), dy.data_ptr(), rows, cols, int(ignore), gs, _bf(y),
+        stream_ptr()), 'ce_sparse_grad')
+    return dy
+
+
+def bce(y, lab):
+    y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
+    out = torch.empty(y.shape, dtype=torch.float32, device=y.device)
+    check(fn('hetu_bce', [P, P, P, I64, I32, P])(y.data_ptr(), lab.data_ptr(), out.data_ptr(), y.numel(), _bf(y),
+                                                  stream_ptr()), 'bce')
+    record_native('bce')
+    return out
+
+
+def bce_grad(y, lab, g):
+    y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
+    g = g.float().expand(y.shape).contiguous() if g.numel() not in (1, y.numel()) else g.float().contiguous()
+    gs = int(g.numel() == 1 and y.numel() != 1)
+    dy = torch.empty(y.shape, dtype=y.dtype, device=y.device)
+    check(fn('hetu_bce_grad', [P, P, P, P, I64, I32, I32, P])(y.data_ptr(), lab.data_ptr(), g.data_ptr(),
+                                                               dy.data_ptr(), y.numel(), gs, _bf(y), stream_ptr()),
+          'bce_grad')
+    return dy
+
+
+def nll(x, t, cols):
+    x = x.reshape(-1, cols).contiguous()
+    t = t.long().reshape(-1).contiguous()
+    out = torch.zeros(1, dtype=torch.float32, device=x.device)
+    check(fn('hetu_nll', [P, P, P, I64, I64, I32, P])(x.data_ptr(), t.data_ptr(), out.data_ptr(), x.shape[0], cols,
+                                                       _bf(x), stream_ptr()), 'nll')
+    record_native('nll')
+    return out
+
+
+def nll_grad(g, t, cols):
+    t = t.long().reshape(-1).contiguous()
+    g = g.float().reshape(-1)[:1].contiguous()
+    dx = torch.empty((t.numel(), cols), dtype=torch.float32, device=t.device)
+    check(fn('hetu_nll_grad', [P, P, P, I64, I64, P])(g.data_ptr(), t.data_ptr(), dx.data_ptr(), t.numel(), cols,
+                                                       stream_ptr()), 'nll_grad')
+    return dx

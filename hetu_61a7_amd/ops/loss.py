@@ -22,6 +22,14 @@ def softmax_func(y):
     return e / np.sum(e, axis=-1, keepdims=True)
 
 
+from ..kernels import native as _native
+from ..kernels import tensor as KT
+
+
+def _gpu(t):
+    return isinstance(t, torch.Tensor) and _native(t) and t.dtype in (torch.float32, torch.bfloat16)
+
+
 class SoftmaxOp(Op):
     def __init__(self, x, ctx=None):
         super().__init__(SoftmaxOp, [x], ctx)
@@ -156,6 +164,8 @@ class CrossEntropyOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         y, lab = input_vals
+        if _gpu(y):
+            return KT.ce_dense(y, lab)
         return -(lab.float() * torch.log(y.float())).sum(-1)
 
     def gradient(self, output_grad):
@@ -171,6 +181,8 @@ class CrossEntropyGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, y, lab = input_vals
+        if _gpu(y):
+            return KT.ce_dense_grad(g, y, lab)
         gg = g.float().unsqueeze(-1) if g.numel() > 1 else g.float()
         return (-gg * lab.float() / y.float()).to(y.dtype)
 
@@ -196,6 +208,8 @@ class CrossEntropySparseOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         y, lab = input_vals
+        if _gpu(y):
+            return KT.ce_sparse(y, lab, self.ignored_index)
         lab = lab.long().reshape(y.shape[:-1])
         valid = lab != self.ignored_index
         safe = torch.where(valid, lab, torch.zeros_like(lab))
@@ -216,6 +230,8 @@ class CrossEntropySparseGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, y, lab = input_vals
+        if _gpu(y):
+            return KT.ce_sparse_grad(g, y, lab, self.ignored_index)
         lab = lab.long().reshape(y.shape[:-1])
         valid = lab != self.ignored_index
         safe = torch.where(valid, lab, torch.zeros_like(lab))
@@ -249,6 +265,8 @@ class BinaryCrossEntropyOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         y, lab = input_vals
+        if _gpu(y) and lab.shape == y.shape:
+            return KT.bce(y, lab)
         yf = y.float().clamp(1e-12, 1 - 1e-7)
         lf = lab.float()
         return -lf * torch.log(yf) - (1 - lf) * torch.log(1 - yf)
@@ -266,6 +284,8 @@ class BinaryCrossEntropyGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         y, lab, g = input_vals
+        if _gpu(y) and lab.shape == y.shape:
+            return KT.bce_grad(y, lab, g)
         yf = y.float().clamp(1e-12, 1 - 1e-7)
         lf = lab.float()
         return (g.float() * (-lf / yf + (1 - lf) / (1 - yf))).to(y.dtype)
@@ -294,6 +314,8 @@ class NllLossOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x, t = input_vals
+        if _gpu(x):
+            return KT.nll(x, t, self.cols)
         picked = torch.gather(x.float().reshape(-1, self.cols), 1, t.long().reshape(-1, 1))
         return -picked.mean().reshape(1)
 
@@ -311,6 +333,8 @@ class NllLossGradOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, t = input_vals
+        if _gpu(g):
+            return KT.nll_grad(g, t, self.cols)
         t = t.long().reshape(-1)
         out = torch.zeros((t.numel(), self.cols), dtype=torch.float32, device=t.device)
         out.scatter_(1, t.reshape(-1, 1), -(g.float().reshape(1, 1).expand(t.numel(), 1)) / t.numel())

@@ -44,6 +44,19 @@ def _reduce_sum(x, axes, keepdims, scale=1.0):
     return r.to(x.dtype)
 
 
+from ..kernels import native as _native, record_fallback as _record_fallback
+from ..kernels import tensor as KT
+
+
+def _gpu(t):
+    return isinstance(t, torch.Tensor) and _native(t) and t.dtype in (torch.float32, torch.bfloat16)
+
+
+def _fallback(name, t):
+    if isinstance(t, torch.Tensor) and t.is_cuda:
+        _record_fallback(name)
+
+
 class ReduceSumOp(Op):
     def __init__(self, node, axes=None, keepdims=False, ctx=None):
         super().__init__(ReduceSumOp, [node], ctx)
@@ -193,6 +206,8 @@ class NormOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x = input_vals[0]
+        if _gpu(x) and isinstance(self.axis, int):
+            return KT.pnorm(x, self.axis, self.p, self.keepdims)
         return torch.linalg.vector_norm(x.float(), self.p, dim=self.axis, keepdim=self.keepdims).to(x.dtype)
 
     def gradient(self, output_grad):
@@ -216,6 +231,8 @@ class NormGradientOp(Op):
         x, y, g = input_vals
         if not self.keepdims:
             y, g = y.unsqueeze(self.axis), g.unsqueeze(self.axis)
+        if _gpu(x) and isinstance(self.axis, int):
+            return KT.pnorm_grad(x, y, g, self.axis, self.p)
         xf = x.float()
         d = torch.sign(xf) * torch.abs(xf) ** (self.p - 1) / (y.float() ** (self.p - 1)).clamp_min(1e-12)
         return (d * g.float()).to(x.dtype)
@@ -241,6 +258,8 @@ class ArgmaxOp(Op):
         self.dim = dim
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        if _gpu(input_vals[0]):
+            return KT.argmax(input_vals[0], self.dim)
         return torch.argmax(input_vals[0], self.dim)
 
     def gradient(self, output_grad):
@@ -262,7 +281,13 @@ class ArgsortOp(Op):
         self.dim, self.descending = dim, descending
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        return torch.argsort(input_vals[0], dim=self.dim, descending=self.descending)
+        x = input_vals[0]
+        if _gpu(x):
+            r = KT.argsort(x, self.dim, self.descending)
+            if r is not None:
+                return r
+            _fallback('argsort', x)
+        return torch.argsort(x, dim=self.dim, descending=self.descending)
 
     def gradient(self, output_grad):
         return [None]
@@ -303,6 +328,8 @@ class TopKValOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         v, i = input_vals
+        if _gpu(v):
+            return KT.gather(v, -1, i)
         return torch.gather(v, -1, i.long())
 
     def gradient(self, output_grad):
@@ -323,6 +350,8 @@ class CumsumOp(Op):
         self.bias, self.dim = bias, dim
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        if _gpu(input_vals[0]):
+            return KT.cumsum(input_vals[0], self.dim, self.bias)
         x = input_vals[0].float()
         d = self.dim % x.dim()
         if x.is_cuda and d != x.dim() - 1 and x.shape[d] > 4 * x.numel() // max(x.shape[d], 1):

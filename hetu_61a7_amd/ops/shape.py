@@ -16,6 +16,19 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from ..kernels import native as _native, record_fallback as _record_fallback
+from ..kernels import tensor as KT
+
+
+def _gpu(t):
+    """hand-written kernel path for a GPU tensor (kernels.native)"""
+    return isinstance(t, torch.Tensor) and _native(t)
+
+
+def _fallback(name, t):
+    if isinstance(t, torch.Tensor) and t.is_cuda:
+        _record_fallback(name)
+
 from .node import Op
 from .basic import reduce_to_shape_op, _shape_bcast
 from ..kernels import reduce as KR
@@ -373,6 +386,8 @@ class ConcatenateOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         dt = input_vals[0].dtype
+        if _gpu(input_vals[0]):
+            return KT.concat([v.to(dt) for v in input_vals], self.axis)
         return torch.cat([v.to(dt) for v in input_vals], self.axis)
 
     def gradient(self, output_grad):
@@ -443,7 +458,10 @@ class PadOp(Op):
         for p in reversed(padl):
             pads += [p[0], p[1]]
         if self.mode == 'constant':
+            if _gpu(x):
+                return KT.pad_constant(x, padl, self.constant_values)
             return F.pad(x, pads, 'constant', self.constant_values)
+        _fallback('pad_' + self.mode, x)
         return F.pad(x, pads, self.mode)
 
     def gradient(self, output_grad):
@@ -465,6 +483,8 @@ class PadGradientOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g = input_vals[0]
         off = g.dim() - len(self.paddings)
+        if _gpu(g):
+            return KT.unpad(g, [[0, 0]] * off + self.paddings)
         sl = [slice(None)] * off + [slice(p[0], g.shape[off + i] - p[1]) for i, p in enumerate(self.paddings)]
         return g[tuple(sl)]
 
@@ -493,6 +513,8 @@ class RepeatOp(Op):
         self.reps = tuple(reps)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        if _gpu(input_vals[0]):
+            return KT.repeat(input_vals[0], self.reps)
         return input_vals[0].repeat(*self.reps)
 
     def gradient(self, output_grad):
@@ -518,6 +540,12 @@ class RepeatGradientOp(Op):
         inter = []
         for r, s in zip(self.reps, full):
             inter += [r, s]
+        if _gpu(g):
+            # sum over the tile axes: the interleaved [r0, s0, r1, s1, ...] view reduced
+            # over the r axes by the native column reduction
+            from ..kernels import reduce as KR
+            r = KR.reduce_sum(g.reshape(inter), tuple(range(0, 2 * len(full), 2)))
+            return r.reshape(shape).to(g.dtype)
         r = g.reshape(inter).float().sum(dim=tuple(range(0, 2 * len(full), 2)))
         return r.reshape(shape).to(g.dtype)
 
@@ -542,7 +570,14 @@ class RollOp(Op):
         self.shift, self.axis = shift, axis
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        return torch.roll(input_vals[0], self.shift, self.axis)
+        x = input_vals[0]
+        if _gpu(x):
+            if self.axis is None:
+                return KT.roll(x.reshape(-1), [self.shift], [0]).reshape(x.shape)
+            sh = list(self.shift) if isinstance(self.shift, (list, tuple)) else [self.shift]
+            ax = list(self.axis) if isinstance(self.axis, (list, tuple)) else [self.axis]
+            return KT.roll(x, sh, ax)
+        return torch.roll(x, self.shift, self.axis)
 
     def gradient(self, output_grad):
         neg = [-s for s in self.shift] if isinstance(self.shift, (list, tuple)) else -self.shift
@@ -613,6 +648,8 @@ class GatherOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x, idx = input_vals
+        if _gpu(x) and x.dtype in (torch.float32, torch.bfloat16):
+            return KT.gather(x, self.dim, idx)
         return torch.gather(x, self.dim, idx.long())
 
     def gradient(self, output_grad):
@@ -631,6 +668,8 @@ class GatherGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         shape, g, idx = input_vals
+        if _gpu(g) and g.dtype in (torch.float32, torch.bfloat16):
+            return KT.scatter_add(g, self.dim, idx, tuple(shape)).to(g.dtype)
         out = torch.zeros(tuple(shape), dtype=torch.float32, device=g.device)
         out.scatter_add_(self.dim, idx.long(), g.float())
         return out.to(g.dtype)

@@ -1,0 +1,115 @@
+"""Long-tail HIP kernels (csrc/kernels/tensor_ops.hip, losses.hip) against plain
+PyTorch fp32 references of the same ops, through the graph ops that route to them
+(reference tests/test_gpu_op.py pattern: kernel vs numpy).  Each test also checks
+that the native kernel ran (kernels.NATIVE_CALLS) and nothing fell back."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import hetu_61a7_amd as ht
+from hetu_61a7_amd import kernels as K
+from hetu_61a7_amd.kernels import tensor as KT
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(node_fn, *arrays):
+    xs = [ht.Variable(name='in%d' % i, trainable=False) for i in range(len(arrays))]
+    out = node_fn(*xs)
+    ex = ht.Executor([out], ctx=ht.gpu(0))
+    return ex.run(feed_dict={x: a for x, a in zip(xs, arrays)}, convert_to_numpy_ret_vals=True)[0]
+
+
+@pytest.fixture(autouse=True)
+def _stats():
+    K.reset_dispatch_stats()
+    yield
+    assert not K.FALLBACKS, K.FALLBACKS
+
+
+def _close(a, b, tol=1e-5):
+    np.testing.assert_allclose(np.asarray(a, np.float64), np.asarray(b, np.float64), rtol=tol, atol=tol)
+
+
+def test_concat_pad_roll_repeat():
+    rng = np.random.RandomState(0)
+    a, b, c = rng.randn(3, 4, 5).astype(np.float32), rng.randn(3, 2, 5).astype(np.float32), \
+        rng.randn(3, 7, 5).astype(np.float32)
+    _close(_run(lambda x, y, z: ht.concatenate_op([x, y, z], axis=1), a, b, c), np.concatenate([a, b, c], 1))
+    _close(_run(lambda x: ht.pad_op(x, [[1, 2], [0, 3]], constant_values=0.5), a),
+           F.pad(torch.from_numpy(a), [0, 3, 1, 2], value=0.5).numpy())
+    _close(_run(lambda x: ht.roll_op(x, 2, 1), a), np.roll(a, 2, 1))
+    _close(_run(lambda x: ht.roll_op(x, -3, None), a), np.roll(a, -3))
+    _close(_run(lambda x: ht.repeat_op(x, (2, 1, 3)), a), torch.from_numpy(a).repeat(2, 1, 3).numpy())
+    _close(_run(lambda x: ht.repeat_op(x, (2, 2, 1, 3)), a), torch.from_numpy(a).repeat(2, 2, 1, 3).numpy())
+    assert K.NATIVE_CALLS.get('nd_copy', 0) >= 6
+
+
+def test_gather_and_scatter_add_grad():
+    x = torch.randn(4, 9, 3, device='cuda')
+    idx = torch.randint(0, 9, (4, 5, 3), device='cuda')
+    _close(KT.gather(x, 1, idx).cpu(), torch.gather(x.cpu(), 1, idx.cpu()))
+    g = torch.randn(4, 5, 3, device='cuda')
+    ref = torch.zeros(4, 9, 3).scatter_add_(1, idx.cpu(), g.cpu())
+    _close(KT.scatter_add(g, 1, idx, (4, 9, 3)).cpu(), ref)
+    xb = x.bfloat16()
+    _close(KT.gather(xb, 1, idx).float().cpu(), torch.gather(xb.float().cpu(), 1, idx.cpu()), 1e-2)
+
+
+@pytest.mark.parametrize('shape,dim', [((5, 300), 1), ((3, 70, 6), 1), ((1000, 4), 0)])
+def test_cumsum(shape, dim):
+    x = torch.randn(*shape, device='cuda')
+    _close(KT.cumsum(x, dim, -1.0).cpu(), torch.cumsum(x.cpu().double(), dim) - 1.0, 1e-4)
+
+
+def test_argmax_argsort_norm():
+    x = torch.randn(6, 257, 3, device='cuda')
+    x[0, 5, 0] = x[0, 9, 0] = 100.0                      # tie: the first index wins
+    assert torch.equal(KT.argmax(x, 1).cpu(), torch.argmax(x.cpu(), 1))
+    for n in (1, 7, 64, 1000, 5000):
+        y = torch.randn(4, n, device='cuda')
+        y[:, :n // 3] = torch.round(y[:, :n // 3])        # duplicates
+        for desc in (False, True):
+            i = KT.argsort(y, -1, desc)
+            got = torch.gather(y, -1, i).cpu()
+            ref = torch.sort(y.cpu(), -1, descending=desc)[0]
+            assert torch.equal(got, ref)
+            assert torch.equal(torch.sort(i.cpu(), -1)[0], torch.arange(n).expand(4, n))
+    z = torch.randn(5, 33, 7, device='cuda')
+    for p in (1.0, 2.0, 3.0):
+        n = KT.pnorm(z, 1, p)
+        _close(n.cpu(), torch.linalg.vector_norm(z.cpu().double(), p, dim=1, keepdim=True), 1e-5)
+        g = torch.randn_like(n)
+        zz = z.cpu().double().requires_grad_(True)
+        torch.linalg.vector_norm(zz, p, dim=1, keepdim=True).backward(g.cpu().double())
+        _close(KT.pnorm_grad(z, n, g, 1, p).cpu(), zz.grad, 1e-4)
+
+
+def test_losses_match_torch():
+    rows, cols = 37, 11
+    y = torch.softmax(torch.randn(rows, cols, device='cuda'), -1)
+    lab = torch.softmax(torch.randn(rows, cols, device='cuda'), -1)
+    _close(KT.ce_dense(y, lab).cpu(), -(lab * torch.log(y)).sum(-1).cpu(), 1e-5)
+    g = torch.randn(rows, device='cuda')
+    _close(KT.ce_dense_grad(g, y, lab).cpu(), (-g[:, None] * lab / y).cpu(), 1e-5)
+    t = torch.randint(0, cols, (rows,), device='cuda')
+    t[3] = -1
+    ref = -torch.log(torch.gather(y, 1, t.clamp_min(0)[:, None]))[:, 0]
+    ref[3] = 0
+    _close(KT.ce_sparse(y, t, -1).cpu(), ref.cpu(), 1e-5)
+    d = KT.ce_sparse_grad(g, y, t, -1).cpu()
+    ref_d = torch.zeros(rows, cols)
+    for r in range(rows):
+        if t[r] >= 0:
+            ref_d[r, t[r]] = -g[r].item() / y[r, t[r]].item()
+    _close(d, ref_d, 1e-5)
+    p = torch.sigmoid(torch.randn(rows, 3, device='cuda'))
+    b = (torch.rand(rows, 3, device='cuda') > 0.5).float()
+    _close(KT.bce(p, b).cpu(), F.binary_cross_entropy(p, b, reduction='none').cpu(), 1e-5)
+    lp = torch.log_softmax(torch.randn(rows, cols, device='cuda'), -1)
+    _close(KT.nll(lp, t.clamp_min(0), cols).cpu(), F.nll_loss(lp, t.clamp_min(0)).reshape(1).cpu(), 1e-5)
+    gs = torch.tensor([0.7], device='cuda')
+    ref_n = torch.zeros(rows, cols)
+    ref_n[torch.arange(rows), t.clamp_min(0).cpu()] = -0.7 / rows
+    _close(KT.nll_grad(gs, t.clamp_min(0), cols).cpu(), ref_n, 1e-6)

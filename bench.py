@@ -40,6 +40,8 @@ def parse():
     p.add_argument('--bucket-mb', type=float, default=32)
     p.add_argument('--zero', type=int, default=0, help='1: ZeRO-1 sharded optimizer state over the DP group')
     p.add_argument('--pp', type=int, default=None, help='bert: force the Galvatron pipeline degree')
+    p.add_argument('--ids', default='zipf', choices=['zipf', 'uniform'],
+                   help='wdl: sparse id distribution (uniform = cache worst-case control)')
     p.add_argument('--op-profile', default=None, help='write per-op-type GPU time (ms) to this file')
     p.add_argument('--grad-wire', default=os.environ.get('HETU_GRAD_WIRE', 'fp32'), choices=['fp32', 'bf16'],
                    help='DP gradient all-reduce wire format (bf16: fp32 accumulation)')
@@ -170,6 +172,9 @@ def main():
         print('non-channels-last 4D outputs:', layout_report(), file=sys.stderr)
     value = samples_per_step * args.steps / dt_s
     _progress(rank, world, 'timed steps done')
+    if hasattr(step, 'extra'):
+        cfg = dict(cfg)
+        cfg.update(step.extra())
     if world > 1 or args.comm_trace:
         cfg = dict(cfg)
         cfg['comm'] = C.world().backend if C.world() is not None else 'none'

@@ -523,12 +523,21 @@ __device__ __forceinline__ float act_f(float v, int act) {
   return v;
 }
 
-template <class LA, class LB, bool DB>
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ST: LDS stages.  1: one 32 KiB buffer when every block owns a single K-tile (short-K
+// 1x1 convolutions: more resident blocks per CU); 2: double buffer, vmcnt(0) +
+// barrier per K-tile (2 blocks per CU); 3 (not launched): three buffers, two K-tiles in
+// flight behind a counted vmcnt and a raw s_barrier.
+template <class LA, class LB, int ST>
 __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                   int64_t K, int tiles_m, int tiles_n, int ktps) {
-  // DB: 2 x 32 KiB double buffer; !DB: one 32 KiB buffer when every block owns a
-  // single K-tile (short-K 1x1 convolutions: more resident blocks per CU)
-  __shared__ __attribute__((aligned(16))) char smem_raw[DB ? 4 * TILE_BYTES : 64 * (BN + 4) * 4];
+  constexpr bool DB = ST >= 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[ST == 3 ? 6 * TILE_BYTES : (DB ? 4 * TILE_BYTES : 64 * (BN + 4) * 4)];
   constexpr int buf_stride = DB ? 2 * TILE_BYTES : 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
@@ -574,11 +583,26 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   };
 
   if (kt0 < kt1) stage(kt0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (ST == 3 && kt0 + 1 < kt1) stage(kt0 + 1, 1);
+  if (ST != 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
+    int cur;
+    if constexpr (ST == 3) {
+      const int i = kt - kt0;
+      cur = i % 3;
+      // this wave's DMA of tile kt landed (kt+1's 8 may still fly), then every wave's
+      // (barrier); all waves also finished reading tile kt-1, whose buffer kt+2 reuses
+      if (kt + 1 < kt1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      if (kt + 2 < kt1) stage(kt + 2, (i + 2) % 3);
+    } else {
+      cur = (kt - kt0) & 1;
+      if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
+    }
     const char* As = smem_raw + cur * buf_stride;
     const char* Bs = As + TILE_BYTES;
 #pragma unroll
@@ -594,6 +618,12 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[j], mf[i], acc[i][j], 0, 0, 0);
     }
+    if constexpr (ST != 3) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  if constexpr (ST == 3) {   // the epilogue reuses the LDS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -1158,7 +1188,9 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
   return (int)hipGetLastError();
 }
 
-// tile: 0 = 128x128 (4 waves, 2-3 blocks per CU), 1 = 256x256 (8 waves, 1 block per CU)
+// tile: 0 = 128x128 (4 waves, 2 LDS stages, 2 blocks per CU), 1 = 256x256 (8 waves, 1 block
+// per CU).  (A 3-stage 128x128 variant at 1 block per CU measured 0.5-0.8x of tile 0 on every
+// bench_tiles shape -- occupancy, not prefetch depth, hides the DMA latency there; removed.)
 template <class LA, class LB>
 static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
                   int batch, int splitk, hipStream_t st, int tile = 0) {
@@ -1171,27 +1203,19 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
   splitk = (nkt + ktps - 1) / ktps;
   if (splitk < 1) splitk = 1;
   dim3 grid(tiles_m * tiles_n, batch, splitk);
-  if (ep.slab && splitk > 1) {
-    Epi e2 = ep;
-    e2.slab_stride = M * N;
-    if (ktps > 1)
-      hipLaunchKernelGGL((gemm_kernel<LA, LB, true>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K,
-                         tiles_m, tiles_n, ktps);
-    else
-      hipLaunchKernelGGL((gemm_kernel<LA, LB, false>), grid, dim3(NT), 0, st, la, lb, e2, M, N, K,
-                         tiles_m, tiles_n, ktps);
-    launch_splitk_reduce(ep.slab, splitk, ep.C, M, N, ep.ldc, ep.out_f32, ep.atomic, st);
-    return (int)hipGetLastError();
-  }
   Epi e1 = ep;
-  e1.slab = nullptr;
-  if (splitk > 1) e1.atomic = 1;
+  const bool slab = ep.slab && splitk > 1;
+  if (slab) {
+    e1.slab_stride = M * N;
+  } else {
+    e1.slab = nullptr;
+    if (splitk > 1) e1.atomic = 1;
+  }
   if (ktps > 1)
-    hipLaunchKernelGGL((gemm_kernel<LA, LB, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
-                       tiles_m, tiles_n, ktps);
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, 2>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n, ktps);
   else
-    hipLaunchKernelGGL((gemm_kernel<LA, LB, false>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
-                       tiles_m, tiles_n, ktps);
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, 1>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n, ktps);
+  if (slab) launch_splitk_reduce(ep.slab, splitk, ep.C, M, N, ep.ldc, ep.out_f32, ep.atomic, st);
   return (int)hipGetLastError();
 }
 

@@ -19,6 +19,7 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <unordered_set>
 #include <random>
 #include <string>
 #include <thread>
@@ -79,6 +80,7 @@ struct Header {
   std::atomic<int32_t> bar_gen;
   std::atomic<uint32_t> dir_lock;
   std::atomic<int64_t> heartbeat[kMaxNodes];
+  std::atomic<int32_t> recovered;   // workers that took over a dead rank
   SspState ssp[kMaxSsp];
   PReduceState pre[kMaxPreduce];
   ParamEntry params[kMaxParams];
@@ -171,21 +173,51 @@ static inline void rec(int psf, int64_t bytes) {
   g_bytes[psf].fetch_add(bytes);
 }
 
-// fault injection: drop with probability p, resend after timeout when PS_RESEND=1
+// Fault injection and reliable delivery (reference ps-lite van.cc:362-443, resender.h:15-150;
+// SURVEY §5.3).  PS_DROP_MSG=<percent> loses a message: either the REQUEST (the PSF never
+// runs) or its ACK (the PSF ran but the sender does not know).  Without PS_RESEND the
+// caller gets -EIO.  With PS_RESEND=1 the sender re-sends after PS_RESEND_TIMEOUT ms, up
+// to 10 times, and every message carries a (sender, sequence) id: the receiving side keeps
+// the ids it has applied, so a re-sent message whose first copy was applied (lost ack) is
+// acknowledged again but NOT re-applied -- each request takes effect exactly once.
+static std::atomic<int64_t> g_fault[4];   // dropped requests, dropped acks, resends, duplicates
+static std::atomic<uint64_t> g_msg_seq{1};
+static std::mutex g_applied_mu;
+static std::unordered_set<uint64_t> g_applied;   // message ids applied (bounded, see below)
+
 static thread_local std::mt19937_64 tl_rng(std::random_device{}());
+static bool drop_now() {
+  if (DROP_P <= 0.0) return false;
+  std::uniform_real_distribution<double> u(0.0, 100.0);
+  return u(tl_rng) < DROP_P;
+}
+
 template <typename F>
 static int deliver(F&& body) {
+  if (DROP_P <= 0.0) return body();
+  const uint64_t id = g_msg_seq.fetch_add(1);
   for (int attempt = 0;; ++attempt) {
-    if (DROP_P > 0.0) {
-      std::uniform_real_distribution<double> u(0.0, 100.0);
-      if (u(tl_rng) < DROP_P) {
-        if (!RESEND) return -EIO;  // message lost
-        std::this_thread::sleep_for(std::chrono::milliseconds(RESEND_MS));
-        if (attempt < 10) continue;
-        return -ETIMEDOUT;
-      }
+    if (attempt > 0) {
+      g_fault[2].fetch_add(1);
+      std::this_thread::sleep_for(std::chrono::milliseconds(RESEND_MS));
     }
-    return body();
+    int r = 0;
+    if (drop_now()) {                       // the request is lost on the way
+      g_fault[0].fetch_add(1);
+    } else {
+      bool dup;
+      {
+        std::lock_guard<std::mutex> g(g_applied_mu);
+        dup = !g_applied.insert(id).second;
+        if (g_applied.size() > (1u << 20)) g_applied.clear();   // ids are only re-sent within 10 tries
+      }
+      if (dup) g_fault[3].fetch_add(1);     // receiver suppresses the re-sent copy
+      else r = body();
+      if (!drop_now()) return r;            // ack arrives
+      g_fault[1].fetch_add(1);              // the ack is lost
+    }
+    if (!RESEND) return -EIO;
+    if (attempt >= 10) return -ETIMEDOUT;
   }
 }
 
@@ -350,6 +382,21 @@ int hps_init(int role, const char* name, int num_workers, int num_servers, uint6
     H->magic = kMagic;
   } else if (role == 2) {
     RANK = H->next_worker.fetch_add(1);
+    if (RANK >= H->nworkers) {
+      // node recovery (reference van.cc:132-160 is_recovery): the cluster is full, so
+      // this process replaces a worker whose heartbeat is older than PS_HEARTBEAT_TIMEOUT
+      double to = 60.0;
+      if (const char* s = getenv("PS_HEARTBEAT_TIMEOUT")) to = atof(s);
+      int dead[kMaxNodes];
+      const int nd = hps_dead_nodes(to, dead, kMaxNodes);
+      if (nd == 0) {
+        munmap(p, MAP_BYTES);
+        H = nullptr;
+        return -EBUSY;
+      }
+      RANK = dead[0];
+      H->recovered.fetch_add(1);
+    }
     int nth = 4;
     if (const char* s = getenv("HETU_PS_THREADS")) nth = std::max(1, atoi(s));
     POOL = new Pool(nth);
@@ -725,6 +772,13 @@ int hps_preduce_get_partner(int key, int rank, int required, float wait_ms, int*
     std::this_thread::sleep_for(std::chrono::microseconds(100));
   }
   rec(PREDUCE, 0);
+  return 0;
+}
+
+// [dropped requests, dropped acks, resends, duplicates suppressed, workers recovered]
+int hps_fault_stats(int64_t* out) {
+  for (int i = 0; i < 4; ++i) out[i] = g_fault[i].load();
+  out[4] = H ? H->recovered.load() : 0;
   return 0;
 }
 

@@ -67,6 +67,8 @@ int hps_ssp_init(int key, int group_size, int64_t tolerance);
 int hps_ssp_sync(int key, int64_t version);
 int hps_preduce_get_partner(int key, int rank, int required, float wait_ms, int* result);
 int hps_heartbeat();
+// [dropped requests, dropped acks, resends, duplicates suppressed, workers recovered]
+int hps_fault_stats(int64_t* out);
 int hps_dead_nodes(double timeout_s, int* out, int max_out);
 
 // ---- persistence (reference PSFHandle.h:389-427 format) ----------------------------------

@@ -181,7 +181,10 @@ def wdl_criteo_bench(args, world, rank, local):
     rows = int(getattr(args, 'criteo_rows', 0) or CRITEO_ROWS)
     B = args.batch or 128
     nb = 64
-    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + rank)
+    # id distribution: Zipf a=1.05 per field (the skew real CTR data has), or a uniform
+    # control run (``--ids uniform``: every lookup is a cold row -- the cache's worst case)
+    dist = getattr(args, 'ids', 'zipf')
+    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + rank, zipf=1.05 if dist == 'zipf' else 0)
     # dataloader-fed inputs, as the reference's run_hetu.py: the executor knows the
     # next batch's sparse ids and prefetches their rows with this step's push
     xd = ht.dataloader_op([ht.Dataloader(dense, B, 'train')])
@@ -194,6 +197,22 @@ def wdl_criteo_bench(args, world, rank, local):
 
     def step():
         ex.run('train')
+
+    tables = [t for t in ex.config.placeholder_to_arr_map.values() if getattr(t, 'cache', None) is not None]
+    for t in tables:
+        t.cache.perf_enabled = True
+
+    def extra():
+        """HET cache statistics over every step so far (warm-up included)"""
+        tot = {}
+        for t in tables:
+            for k, v in t.cache.perf.items():
+                tot[k] = tot.get(k, 0) + v
+        unique, miss = tot.get('unique', 0), tot.get('miss', 0)
+        return {'ids': dist, 'cache_lookups_unique': int(unique), 'cache_misses': int(miss),
+                'cache_hit_rate': round(1.0 - miss / unique, 4) if unique else None,
+                'prefetch_hits': int(sum(t.prefetch_hits for t in tables))}
+    step.extra = extra
 
     def finish():
         from ..ps import worker

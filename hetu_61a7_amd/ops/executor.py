@@ -521,7 +521,10 @@ class SubExecutor(object):
         if getattr(node, 'host_feed', False):
             dev = torch.device('cpu')
         if t.device != dev:
+            src = t
             t = t.to(dev, non_blocking=True)
+            if not src.is_cuda and not src.is_floating_point():
+                t.hetu_host = src      # host copy of fed ids: PS lookups need no device sync
         if self.config.mixed_precision and t.is_cuda and t.dtype == torch.float32 and \
                 not getattr(node, 'keep_fp32', False):
             t = t.to(torch.bfloat16)

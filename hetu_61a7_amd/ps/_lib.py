@@ -48,6 +48,7 @@ _SIGS = {
     'hps_preduce_get_partner': ([I32, I32, I32, F32, P], I32),
     'hps_heartbeat': ([], I32),
     'hps_dead_nodes': ([F64, P, I32], I32),
+    'hps_fault_stats': ([P], I32),
     'hps_save_param': ([I32, S], I32),
     'hps_load_param': ([I32, S], I32),
     'hps_start_record': ([S], I32),

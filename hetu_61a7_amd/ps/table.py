@@ -25,6 +25,41 @@ def _pinned(n, dtype=torch.float32):
     return pinned_empty((n,), dtype)
 
 
+_STREAMS = {}
+
+
+def side_streams(device):
+    """(h2d, d2h) copy streams of a device (reference HetuConfig h2d/d2h streams,
+    executor.py:319-334): PS/cache transfers run there, ordered against the compute
+    stream by events, so they overlap compute instead of queueing behind it."""
+    s = _STREAMS.get(device)
+    if s is None:
+        s = _STREAMS[device] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
+    return s
+
+
+def host_ids(t):
+    """int64 host copy of an id tensor.  A device tensor made from a host feed carries
+    its source (``hetu_host``, set by the executor's feed path): no device sync.  Other
+    device ids are copied on the d2h stream after the producer and waited for alone."""
+    h = getattr(t, 'hetu_host', None)
+    if h is not None and h.numel() == t.numel():
+        return h.reshape(-1).long().contiguous()
+    t = t.reshape(-1)
+    if not t.is_cuda:
+        return t.long().contiguous()
+    _, d2h = side_streams(t.device)
+    d2h.wait_stream(torch.cuda.current_stream(t.device))
+    out = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    with torch.cuda.stream(d2h):
+        out.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(d2h)
+    t.record_stream(d2h)
+    ev.synchronize()
+    return out.long()
+
+
 class _Staging(object):
     """Grow-only pinned buffer + an event guarding its reuse."""
 
@@ -41,10 +76,10 @@ class _Staging(object):
             self.buf = _pinned(max(n, 1), self.dtype)
         return self.buf[:n]
 
-    def guard(self):
+    def guard(self, stream=None):
         if torch.cuda.is_available():
             self.event = torch.cuda.Event()
-            self.event.record()
+            self.event.record(stream)
 
 
 _LIVE = []
@@ -141,10 +176,7 @@ class PSTable(object):
         self.prefetched = (nxt, dest, t, stage)
 
     def lookup(self, idx, out_dtype=None):
-        ids = idx.reshape(-1)
-        if ids.is_cuda:
-            ids = ids.cpu()
-        ids = ids.long().contiguous()
+        ids = host_ids(idx)
         dest, stage = self._take_prefetched(ids)
         if dest is None:
             self._wait_push()      # on-demand pull sees every push issued so far
@@ -157,8 +189,14 @@ class PSTable(object):
                 self.agent.WaitTicket(t)
         self._prefetch_next()
         if self.device.type == 'cuda':
-            out = dest.to(self.device, non_blocking=True)
-            stage.guard()
+            # H2D on the copy stream; the compute stream waits for it by event only
+            h2d, _ = side_streams(self.device)
+            cur = torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(h2d):
+                out = dest.to(self.device, non_blocking=True)
+                stage.guard(h2d)
+            cur.wait_stream(h2d)
+            out.record_stream(cur)
             if out_dtype is not None and out_dtype != out.dtype:
                 out = out.to(out_dtype)
         else:
@@ -169,15 +207,21 @@ class PSTable(object):
         """Scale by -lr on the device and start the D2H copy (called as soon as the
         gradient exists, so it overlaps the rest of backward)."""
         self._wait_push()          # the last push may still read the staging buffer
-        ids = slices.indices.reshape(-1)
-        if ids.is_cuda:
-            ids = ids.cpu()
+        ids = host_ids(slices.indices)
         vals = slices.values.reshape(-1, self.width)
         scaled = vals.float() * (-lr)
         host = self.grad_stage.get(scaled.numel()).view(-1, self.width)
-        host.copy_(scaled, non_blocking=True)
-        self.grad_stage.guard()
-        self.pending_push = (ids.long().contiguous(), host)
+        if scaled.is_cuda:
+            # D2H on the copy stream after the scaling kernel; the compute stream goes on
+            _, d2h = side_streams(scaled.device)
+            d2h.wait_stream(torch.cuda.current_stream(scaled.device))
+            with torch.cuda.stream(d2h):
+                host.copy_(scaled, non_blocking=True)
+                self.grad_stage.guard(d2h)
+            scaled.record_stream(d2h)
+        else:
+            host.copy_(scaled)
+        self.pending_push = (ids, host)
 
     def flush_grad(self):
         """Push the staged gradient (after its D2H copy completed)."""

@@ -168,6 +168,15 @@ class PSAgent(object):
     def heartbeat(self):
         lib('hps_heartbeat')()
 
+    def fault_stats(self):
+        """Reliable-delivery counters of this process (PS_DROP_MSG / PS_RESEND): dropped
+        requests, dropped acks, resends, duplicates suppressed, plus the number of
+        workers that took over a dead rank (node recovery)."""
+        out = np.zeros(5, dtype=np.int64)
+        lib('hps_fault_stats')(out.ctypes.data)
+        keys = ('dropped_requests', 'dropped_acks', 'resends', 'duplicates_suppressed', 'recovered_workers')
+        return dict(zip(keys, (int(x) for x in out)))
+
     def dead_nodes(self, timeout_s=None):
         timeout_s = timeout_s or float(os.environ.get('PS_HEARTBEAT_TIMEOUT', '60'))
         out = np.zeros(256, dtype=np.int32)

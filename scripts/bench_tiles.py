@@ -41,7 +41,7 @@ def rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
 
 
-emit('# GEMM (TF/s): tile0 = 128x128, tile1 = 256x256 8-wave, blas = hipBLASLt (torch.mm)')
+emit('# GEMM (TF/s): tile0 = 128x128 2-stage, tile1 = 256x256 8-wave, tile2 = 128x128 3-stage, blas = hipBLASLt (torch.mm)')
 for (M, N, K, ta, tb) in [(4096, 4096, 4096, 0, 0), (4096, 4096, 4096, 0, 1), (8192, 8192, 8192, 0, 1),
                           (8192, 3072, 768, 0, 0), (8192, 768, 3072, 0, 0), (768, 3072, 8192, 1, 0),
                           (50176, 1024, 256, 0, 1), (50176, 256, 1024, 0, 1), (200704, 512, 128, 0, 1),
@@ -62,7 +62,7 @@ for (M, N, K, ta, tb) in [(4096, 4096, 4096, 0, 0), (4096, 4096, 4096, 0, 1), (8
          '  '.join('%s %.3f ms %5.0f TF (err %.1e)' % (k, v[0], fl / v[0] / 1e9, v[1]) for k, v in res.items()))
     del a, b, ref
 
-emit('# ResNet-50 convolutions, bs 256 (ms): tile0 / tile1 / vendor (MIOpen)')
+emit('# ResNet-50 convolutions, bs 256 (ms): tile0 / tile1 / tile2 / vendor (MIOpen)')
 N = 256
 for (ci, H, co, k, st, p) in [(64, 56, 64, 3, 1, 1), (128, 28, 128, 3, 1, 1), (128, 56, 128, 3, 2, 1),
                               (256, 14, 256, 3, 1, 1), (256, 28, 256, 3, 2, 1), (512, 7, 512, 3, 1, 1),
@@ -92,8 +92,8 @@ for (ci, H, co, k, st, p) in [(64, 56, 64, 3, 1, 1), (128, 28, 128, 3, 1, 1), (1
         else:
             v = timeit(lambda: torch.ops.aten.convolution_backward(g, x, w, None, [st, st], [p, p], [1, 1], False,
                                                                    [0, 0], 1, [False, True, False]))
-        row.append('%s %.3f/%.3f/%.3f (%4.0f TF best, t1-vs-t0 %.0e)' % (
-            name, tms[0], tms[1], v, fl / min(tms[0], tms[1]) / 1e9, err))
+        row.append('%s %s/%.3f (%4.0f TF best, t1-vs-t0 %.0e)' % (
+            name, '/'.join('%.3f' % tms[t] for t in G.TILES), v, fl / min(tms.values()) / 1e9, err))
     emit('cin %4d H %3d cout %4d k%d s%d | ' % (ci, H, co, k, st) + ' | '.join(row))
     del x, w, y, g
 

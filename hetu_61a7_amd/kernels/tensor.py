@@ -326,3 +326,148 @@ def nll_grad(g, t, cols):
     check(fn('hetu_nll_grad', [P, P, P, I64, I64, P])(g.data_ptr(), t.data_ptr(), dx.data_ptr(), t.numel(), cols,
                                                        stream_ptr()), 'nll_grad')
     return dx
+
+
+# ---- misc_ops.hip: SAM gate helpers, instance norm, bicubic ---------------------------------
+def _i64(t):
+    return t.long().reshape(-1).contiguous()
+
+
+def sam_group_sum(x, G):
+    x = x.float().contiguous()
+    T, E = x.shape
+    out = torch.empty((T, G), dtype=torch.float32, device=x.device)
+    check(fn('hetu_sam_group_sum', [P, P, I64, I32, I32, P])(x.data_ptr(), out.data_ptr(), T, E, G, stream_ptr()),
+          'sam_group_sum')
+    record_native('sam_group_sum')
+    return out
+
+
+def sam_group_sum_grad(g, T, E, G):
+    g = g.float().contiguous()
+    dx = torch.empty((T, E), dtype=torch.float32, device=g.device)
+    check(fn('hetu_sam_group_sum_grad', [P, P, I64, I32, I32, P])(g.data_ptr(), dx.data_ptr(), T, E, G,
+                                                                   stream_ptr()), 'sam_group_sum_grad')
+    record_native('sam_group_sum_grad')
+    return dx
+
+
+def sam_max(x, grp, tk, n):
+    x = x.float().contiguous()
+    T, E = x.shape
+    grp, tk = _i64(grp), _i64(tk)
+    y = torch.empty((T, E), dtype=torch.float32, device=x.device)
+    check(fn('hetu_sam_max', [P, P, P, P, I64, I32, I32, P])(x.data_ptr(), grp.data_ptr(), tk.data_ptr(),
+                                                             y.data_ptr(), T, E, n, stream_ptr()), 'sam_max')
+    record_native('sam_max')
+    return y
+
+
+def sam_max_grad(g, x, grp, tk, n):
+    x, g = x.float().contiguous(), g.float().contiguous()
+    T, E = x.shape
+    grp, tk = _i64(grp), _i64(tk)
+    dx = torch.empty((T, E), dtype=torch.float32, device=x.device)
+    check(fn('hetu_sam_max_grad', [P, P, P, P, P, I64, I32, I32, P])(
+        g.data_ptr(), x.data_ptr(), grp.data_ptr(), tk.data_ptr(), dx.data_ptr(), T, E, n, stream_ptr()),
+        'sam_max_grad')
+    record_native('sam_max_grad')
+    return dx
+
+
+GROUP_TOPK_MAX = 64 * 64
+
+
+def group_topk_idx(x, grp, k, n):
+    """Top-k column ids of each row inside its group's columns (descending, ties to the
+    lower id); None when the group is wider than the kernel's register stripes."""
+    if n > GROUP_TOPK_MAX or k > n:
+        return None
+    x = x.float().contiguous()
+    T, E = x.shape
+    grp = _i64(grp)
+    out = torch.empty((T, k), dtype=torch.int64, device=x.device)
+    check(fn('hetu_group_topk_idx', [P, P, P, I64, I32, I32, I32, P])(
+        x.data_ptr(), grp.data_ptr(), out.data_ptr(), T, E, n, k, stream_ptr()), 'group_topk_idx')
+    record_native('group_topk_idx')
+    return out
+
+
+def _plane_view(x):
+    """Strides (sN, sC, sP) of an NCHW view whose H, W merge into one axis (contiguous
+    NCHW: sP = 1; channels-last: sP = C); makes it contiguous otherwise."""
+    if x.stride(2) != x.shape[3] * x.stride(3):
+        x = x.contiguous()
+    return x, (x.stride(0), x.stride(1), x.stride(3))
+
+
+def instance_norm2d(x, eps):
+    """x logical NCHW fp32/bf16 (NCHW or channels-last) -> (y, mean, rstd), stats [N, C, 1, 1] fp32."""
+    x, (sN, sC, sP) = _plane_view(x)
+    N, C, H, W = x.shape
+    y = torch.empty_like(x)
+    if y.stride() != x.stride():
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        sN, sC, sP = x.stride(0), x.stride(1), x.stride(3)
+    mean = torch.empty((N, C, 1, 1), dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    check(fn('hetu_instance_norm2d', [P, P, P, P, I32, I32, I64, I64, I64, I64, F32, I32, P])(
+        x.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), N, C, H * W, sN, sC, sP, float(eps), _bf(x),
+        stream_ptr()), 'instance_norm2d')
+    record_native('instance_norm2d')
+    return y, mean, rstd
+
+
+def instance_norm2d_grad(g, x, mean, rstd):
+    x, (sN, sC, sP) = _plane_view(x)
+    g = g.to(x.dtype)
+    if g.stride() != x.stride():
+        g = torch.empty_like(x).copy_(g)
+    dx = torch.empty_like(x)
+    if dx.stride() != x.stride():
+        x = x.contiguous()
+        g, dx = g.contiguous(), torch.empty_like(x)
+        sN, sC, sP = x.stride(0), x.stride(1), x.stride(3)
+    N, C, H, W = x.shape
+    mean, rstd = mean.float().contiguous(), rstd.float().contiguous()
+    check(fn('hetu_instance_norm2d_grad', [P, P, P, P, P, I32, I32, I64, I64, I64, I64, I32, P])(
+        g.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(), N, C, H * W, sN, sC, sP,
+        _bf(x), stream_ptr()), 'instance_norm2d_grad')
+    record_native('instance_norm2d_grad')
+    return dx
+
+
+def _cubic_scale(inp, out, align, scale_factor):
+    if align:
+        return (inp - 1) / (out - 1) if out > 1 else 0.0
+    if scale_factor is not None and scale_factor > 0:
+        return 1.0 / scale_factor
+    return inp / out
+
+
+def bicubic(x, OH, OW, align_corners=False, scale_factor=None):
+    """PyTorch-compatible bicubic upsampling (A = -0.75, border clamp), fp32 math."""
+    N, C, H, W = x.shape
+    xf = x.float().contiguous()
+    y = torch.empty((N, C, OH, OW), dtype=torch.float32, device=x.device)
+    sh = _cubic_scale(H, OH, align_corners, scale_factor)
+    sw = _cubic_scale(W, OW, align_corners, scale_factor)
+    check(fn('hetu_bicubic', [P, P, I64, I32, I32, I32, I32, F32, F32, I32, P])(
+        xf.data_ptr(), y.data_ptr(), N * C, H, W, OH, OW, sh, sw, int(bool(align_corners)), stream_ptr()), 'bicubic')
+    record_native('bicubic')
+    return y.to(x.dtype)
+
+
+def bicubic_grad(g, shape, align_corners=False, scale_factor=None):
+    N, C, H, W = (int(s) for s in shape)
+    OH, OW = int(g.shape[2]), int(g.shape[3])
+    gf = g.float().contiguous()
+    dx = torch.zeros((N, C, H, W), dtype=torch.float32, device=g.device)
+    sh = _cubic_scale(H, OH, align_corners, scale_factor)
+    sw = _cubic_scale(W, OW, align_corners, scale_factor)
+    check(fn('hetu_bicubic_grad', [P, P, I64, I32, I32, I32, I32, F32, F32, I32, P])(
+        gf.data_ptr(), dx.data_ptr(), N * C, H, W, OH, OW, sh, sw, int(bool(align_corners)), stream_ptr()),
+        'bicubic_grad')
+    record_native('bicubic_grad')
+    return dx.to(g.dtype)

@@ -13,6 +13,12 @@ import torch
 
 from .node import Op
 from ..kernels import moe as KM
+from ..kernels import native as _native, record_fallback as _record_fallback
+from ..kernels import tensor as KT
+
+
+def _gpu(t):
+    return isinstance(t, torch.Tensor) and _native(t) and t.dtype in (torch.float32, torch.bfloat16)
 
 
 def _stack(vals):
@@ -212,6 +218,8 @@ class SamGroupSumOp(Op):
         g = input_vals[0]
         T, E = g.shape
         G = self.num_local_gpus
+        if _gpu(g):
+            return KT.sam_group_sum(g, G)
         return g.float().reshape(T, G, E // G).sum(-1)
 
     def gradient(self, output_grad):
@@ -232,6 +240,8 @@ class SamGroupSumGradOp(Op):
         g, shape = input_vals
         T, E = tuple(shape)
         G = self.num_local_gpus
+        if _gpu(g):
+            return KT.sam_group_sum_grad(g, T, E, G)
         return g.float().unsqueeze(-1).expand(T, G, E // G).reshape(T, E)
 
     def gradient(self, output_grad):
@@ -264,6 +274,8 @@ class SamMaxOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x, grp, tk = input_vals
+        if _gpu(x):
+            return KT.sam_max(x, grp, tk, self.num_local_gpus)
         m, diff = _sam_mask(x, grp, tk, self.num_local_gpus)
         return torch.where(m, diff, torch.zeros_like(diff))
 
@@ -282,6 +294,8 @@ class SamMaxGradOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, x, grp, tk = input_vals
+        if _gpu(x):
+            return KT.sam_max_grad(g, x, grp, tk, self.num_local_gpus)
         m, _ = _sam_mask(x, grp, tk, self.num_local_gpus)
         gm = torch.where(m, g.float(), torch.zeros_like(g, dtype=torch.float32))
         out = gm.clone()
@@ -314,6 +328,11 @@ class GroupTopKIdxOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x, grp = input_vals
         n = self.num_local_gpus
+        if _gpu(x):
+            r = KT.group_topk_idx(x, grp, self.k, n)
+            if r is not None:
+                return r
+            _record_fallback('group_topk_idx')
         g = grp.reshape(-1).long()
         T, E = x.shape
         cols = torch.arange(E, device=x.device).unsqueeze(0)

@@ -30,6 +30,12 @@ from ..kernels import conv as KC
 from ..kernels import layernorm as KLN
 from ..kernels import native
 from ..kernels import dropout as KD
+from ..kernels import tensor as KT
+
+
+def _kn(t):
+    """GPU fp32/bf16 tensor -> hand-written kernel path"""
+    return isinstance(t, torch.Tensor) and native(t) and t.dtype in (torch.float32, torch.bfloat16)
 
 
 class AuxResult(object):
@@ -582,6 +588,9 @@ class Instance_Normalization2dOp(Op):
         self.eps = eps
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        if _kn(input_vals[0]):
+            y, mean, rstd = KT.instance_norm2d(input_vals[0], self.eps)
+            return AuxResult(y, (mean, rstd))
         x = input_vals[0].float()
         mean = x.mean((2, 3), keepdim=True)
         var = x.var((2, 3), unbiased=False, keepdim=True)
@@ -603,6 +612,8 @@ class Instance_Normalization2d_GradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, x, (mean, rstd) = input_vals
+        if _kn(x):
+            return KT.instance_norm2d_grad(g, x, mean, rstd)
         gf, xf = g.float(), x.float()
         xhat = (xf - mean) * rstd
         m = gf.mean((2, 3), keepdim=True)

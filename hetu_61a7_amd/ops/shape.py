@@ -598,11 +598,18 @@ class InterpolateOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x = input_vals[0]
+        if _gpu(x) and self.mode == 'bicubic' and x.dtype in (torch.float32, torch.bfloat16):
+            oh, ow = self.infer_shape([tuple(x.shape)])[2:]
+            return KT.bicubic(x, oh, ow, self.align_corners, None if self.size is not None else self.scale_factor)
+        if _gpu(x):
+            _record_fallback('interpolate_' + str(self.mode))
         return F.interpolate(x.float(), size=self.size, scale_factor=self.scale_factor, mode=self.mode,
                              align_corners=self.align_corners).to(x.dtype)
 
     def gradient(self, output_grad):
-        return [interpolate_grad_op(output_grad, self.inputs[0], self.mode, self.align_corners, ctx=self.raw_ctx)]
+        return [interpolate_grad_op(output_grad, self.inputs[0], self.mode, self.align_corners,
+                                    scale_factor=None if self.size is not None else self.scale_factor,
+                                    ctx=self.raw_ctx)]
 
     def infer_shape(self, input_shapes):
         n, c, h, w = input_shapes[0]
@@ -614,15 +621,21 @@ class InterpolateOp(Op):
 class InterpolateGradOp(Op):
     shape_only_inputs = (1,)
 
-    def __init__(self, grad, ref, mode='bicubic', align_corners=False, ctx=None):
+    def __init__(self, grad, ref, mode='bicubic', align_corners=False, scale_factor=None, ctx=None):
         super().__init__(InterpolateGradOp, [grad, ref], ctx)
-        self.mode, self.align_corners = mode, align_corners
+        self.mode, self.align_corners, self.scale_factor = mode, align_corners, scale_factor
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, shape = input_vals
+        if _gpu(g) and self.mode == 'bicubic' and g.dtype in (torch.float32, torch.bfloat16):
+            return KT.bicubic_grad(g, tuple(shape), self.align_corners, self.scale_factor)
+        if _gpu(g):
+            _record_fallback('interpolate_grad_' + str(self.mode))
         xs = torch.zeros(tuple(shape), dtype=torch.float32, device=g.device, requires_grad=True)
+        sf = self.scale_factor
         with torch.enable_grad():
-            y = F.interpolate(xs, size=tuple(g.shape[2:]), mode=self.mode, align_corners=self.align_corners)
+            y = F.interpolate(xs, size=None if sf else tuple(g.shape[2:]), scale_factor=sf, mode=self.mode,
+                              align_corners=self.align_corners)
             (gx,) = torch.autograd.grad(y, xs, g.float())
         return gx.to(g.dtype)
 
@@ -637,8 +650,8 @@ def interpolate_op(input, size=None, scale_factor=None, mode='bicubic', align_co
     return InterpolateOp(input, size, scale_factor, mode, align_corners, ctx=ctx)
 
 
-def interpolate_grad_op(grad, input, mode='bicubic', align_corners=False, ctx=None):
-    return InterpolateGradOp(grad, input, mode, align_corners, ctx=ctx)
+def interpolate_grad_op(grad, input, mode='bicubic', align_corners=False, scale_factor=None, ctx=None):
+    return InterpolateGradOp(grad, input, mode, align_corners, scale_factor, ctx=ctx)
 
 
 class GatherOp(Op):

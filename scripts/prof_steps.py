@@ -25,6 +25,8 @@ def classify(n):
     m = re.search(r'hetu::gemm::gemm_kernel<hetu::gemm::(\w+), hetu::gemm::(\w+), (true|false)', n)
     if m:
         return 'hetu::gemm<%s,%s,%s>' % m.groups()
+    if 'hetu::gemm' in n and '<' in n:
+        return n.split('(')[0].replace('hetu::gemmf::', '').replace('hetu::gemm::', '').replace('void ', '')[:60]
     m = re.search(r'hetu::(\w+?)(<|\()', n)
     if m:
         return 'hetu::' + m.group(1)
@@ -71,8 +73,9 @@ def main():
             if want in classify(r['Kernel_Name']):
                 dur = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
                 nb = lambda j: classify(last[j]['Kernel_Name']) if 0 <= j < len(last) else '-'
-                print('%4d  %-40s | %-30s %7.1f us | %s' % (i, nb(i - 1)[:40], classify(r['Kernel_Name'])[:30],
-                                                         dur, nb(i + 1)[:40]))
+                print('%4d  %-40s | %-30s %7.1f us grid %s | %s' % (
+                    i, nb(i - 1)[:40], classify(r['Kernel_Name'])[:30], dur,
+                    r.get('Grid_Size', r.get('Grid_Size_X', '?')), nb(i + 1)[:40]))
 
 
 if __name__ == '__main__':

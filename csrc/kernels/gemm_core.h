@@ -517,10 +517,116 @@ __device__ __forceinline__ void epilogue_colstats(float (&cs)[8], float (&cq)[8]
   }
 }
 
+// erf to 1.5e-7 absolute (Abramowitz & Stegun 7.1.26): one v_exp + one v_rcp and a
+// 5-term polynomial instead of erff's two-branch rational form -- the GELU epilogue
+// costs ~1/3 of the VALU, far below bf16 resolution
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+  const float p = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
+                   0.254829592f) * t;
+  return copysignf(1.f - p * __expf(-ax * ax), x);
+}
+
 __device__ __forceinline__ float act_f(float v, int act) {
   if (act == 1) return v > 0.f ? v : 0.f;
-  if (act == 2) return 0.5f * v * (1.f + erff(v * 0.70710678118f));
+  if (act == 2) return 0.5f * v * (1.f + erf_fast(v * 0.70710678118f));
   return v;
+}
+
+// Row-coalesced epilogue of one thread: 8 consecutive columns n..n+7 of row m.
+// The bias columns are loaded once per thread (bcol; the column set of a thread is
+// fixed over all its rows) -- per-element bias loads behind the C stores (possible
+// aliasing) serialised the epilogue.
+struct EpiOut {
+  char* Cb;
+  const char* Cinb;
+  bool cvec, ivec;
+  float bcol[8];
+};
+
+__device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch, int64_t n, int64_t N) {
+  o.Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
+  o.Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
+  o.cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)o.Cb & 15) == 0)
+                      : ((ep.ldc & 7) == 0 && ((uintptr_t)o.Cb & 15) == 0);
+  o.ivec = o.Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)o.Cinb & 15) == 0)
+                                 : ((ep.ldcin & 7) == 0 && ((uintptr_t)o.Cinb & 15) == 0));
+#pragma unroll
+  for (int t = 0; t < 8; ++t) o.bcol[t] = 0.f;
+  if (ep.bias && !ep.bias_on_m) {
+    if (n + 7 < N && ((uintptr_t)(ep.bias + n) & 15) == 0) {
+      const float4 b0 = *reinterpret_cast<const float4*>(ep.bias + n);
+      const float4 b1 = *reinterpret_cast<const float4*>(ep.bias + n + 4);
+      o.bcol[0] = b0.x; o.bcol[1] = b0.y; o.bcol[2] = b0.z; o.bcol[3] = b0.w;
+      o.bcol[4] = b1.x; o.bcol[5] = b1.y; o.bcol[6] = b1.z; o.bcol[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) o.bcol[t] = n + t < N ? ep.bias[n + t] : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (&v)[8], int64_t m, int64_t n,
+                                         int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8]) {
+  const bool full = n + 7 < N;
+  if (ep.bias) {
+    const float bm = ep.bias_on_m ? ep.bias[m] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] += ep.bias_on_m ? bm : o.bcol[t];
+  }
+  if (o.Cinb) {
+    const int64_t off = orow * ep.ldcin + n;
+    float cv[8];
+    if (o.ivec && full) {
+      if (ep.cin_f32) {
+        float4 c0 = *reinterpret_cast<const float4*>((const float*)o.Cinb + off);
+        float4 c1 = *reinterpret_cast<const float4*>((const float*)o.Cinb + off + 4);
+        cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
+        cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
+      } else {
+        load_vec<bf16>((const bf16*)o.Cinb + off, cv);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)o.Cinb)[off + t] : to_f(((const bf16*)o.Cinb)[off + t]))
+                          : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
+  }
+  if (ep.act) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
+  }
+  const int64_t off = orow * ep.ldc + n;
+  if (ep.out_f32) {
+    float* Cf = (float*)o.Cb + off;
+    if (o.cvec && full) {
+      *reinterpret_cast<float4*>(Cf) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(Cf + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      for (int t = 0; t < 8; ++t)
+        if (n + t < N) Cf[t] = v[t];
+    }
+  } else {
+    bf16* Ch = (bf16*)o.Cb + off;
+    if (o.cvec && full) {
+      store_vec<bf16>(Ch, v);
+    } else {
+      for (int t = 0; t < 8; ++t)
+        if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
+    }
+  }
+  if (ep.colstats) {   // statistics of the values as stored
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));
+      cs[t] += sv;
+      cq[t] += sv * sv;
+    }
+  }
 }
 
 __device__ __forceinline__ void lds_barrier() {
@@ -665,10 +771,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
     // 32-byte pieces, and the same for the Cin (residual / beta) read.
     constexpr int SROW = BN + 4;
     float* stg = reinterpret_cast<float*>(smem_raw);
-    const bool cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)Cb & 15) == 0)
-                                 : ((ep.ldc & 7) == 0 && ((uintptr_t)Cb & 15) == 0);
-    const bool ivec = Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)Cinb & 15) == 0)
-                                          : ((ep.ldcin & 7) == 0 && ((uintptr_t)Cinb & 15) == 0));
+    const int c = (tid & 15) * 8;
+    EpiOut eo;
+    epi_init(ep, eo, batch, (int64_t)tn * BN + c, N);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       if (wm == half) {
@@ -676,18 +781,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int r = i * 16 + (lane & 15), c = wn * 64 + j * 16 + 4 * (lane >> 4);
-            *reinterpret_cast<v4f*>(stg + r * SROW + c) = acc[i][j];
+            const int r = i * 16 + (lane & 15), cc = wn * 64 + j * 16 + 4 * (lane >> 4);
+            *reinterpret_cast<v4f*>(stg + r * SROW + cc) = acc[i][j];
           }
       }
       __syncthreads();
 #pragma unroll
       for (int pss = 0; pss < 4; ++pss) {
-        const int r = pss * 16 + (tid >> 4), c = (tid & 15) * 8;
+        const int r = pss * 16 + (tid >> 4);
         const int64_t m = (int64_t)tm * BM + half * 64 + r;
         const int64_t n = (int64_t)tn * BN + c;
         if (m >= Mb || n >= N) continue;
-        const int64_t orow = la.out_row(m);
         float v[8];
         {
           v4f a0 = *reinterpret_cast<const v4f*>(stg + r * SROW + c);
@@ -695,62 +799,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
 #pragma unroll
           for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
         }
-        const bool full = n + 7 < N;
-        if (ep.bias) {
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            v[t] += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
-        }
-        if (Cinb) {
-          const int64_t o = orow * ep.ldcin + n;
-          float cv[8];
-          if (ivec && full) {
-            if (ep.cin_f32) {
-              float4 c0 = *reinterpret_cast<const float4*>((const float*)Cinb + o);
-              float4 c1 = *reinterpret_cast<const float4*>((const float*)Cinb + o + 4);
-              cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
-              cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
-            } else {
-              load_vec<bf16>((const bf16*)Cinb + o, cv);
-            }
-          } else {
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-              cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)Cinb)[o + t]
-                                              : to_f(((const bf16*)Cinb)[o + t])) : 0.f;
-          }
-#pragma unroll
-          for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
-        const int64_t o = orow * ep.ldc + n;
-        if (ep.out_f32) {
-          float* Cf = (float*)Cb + o;
-          if (cvec && full) {
-            *reinterpret_cast<float4*>(Cf) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<float4*>(Cf + 4) = make_float4(v[4], v[5], v[6], v[7]);
-          } else {
-            for (int t = 0; t < 8; ++t)
-              if (n + t < N) Cf[t] = v[t];
-          }
-        } else {
-          bf16* Ch = (bf16*)Cb + o;
-          if (cvec && full) {
-            store_vec<bf16>(Ch, v);
-          } else {
-            for (int t = 0; t < 8; ++t)
-              if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
-          }
-        }
-        if (ep.colstats) {   // statistics of the values as stored
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));
-            cs[t] += sv;
-            cq[t] += sv * sv;
-          }
-        }
+        epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
       }
       __syncthreads();
     }
@@ -998,17 +1047,14 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
     }
     return;
   }
-  char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
-  const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
   constexpr int SROW = BIG + 4;
   float* stg = reinterpret_cast<float*>(smem);
-  const bool cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)Cb & 15) == 0)
-                               : ((ep.ldc & 7) == 0 && ((uintptr_t)Cb & 15) == 0);
-  const bool ivec = Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)Cinb & 15) == 0)
-                                        : ((ep.ldcin & 7) == 0 && ((uintptr_t)Cinb & 15) == 0));
   float cs[8], cq[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) { cs[t] = 0.f; cq[t] = 0.f; }
+  const int c = (tid & 31) * 8;
+  EpiOut eo;
+  epi_init(ep, eo, batch, (int64_t)tn * BIG + c, N);
   // 4 passes of 64 rows through LDS (64 x 260 fp32 = 66.5 KiB), full-row stores
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
@@ -1018,18 +1064,17 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = (pass & 1) * 4 + ii;
-          const int rr = ii * 16 + (lane & 15), c = wc * 64 + j * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<v4f*>(stg + rr * SROW + c) = acc[i][j];
+          const int rr = ii * 16 + (lane & 15), cc = wc * 64 + j * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<v4f*>(stg + rr * SROW + cc) = acc[i][j];
         }
     }
     __syncthreads();
 #pragma unroll
     for (int sp = 0; sp < 4; ++sp) {
-      const int rr = sp * 16 + (tid >> 5), c = (tid & 31) * 8;
+      const int rr = sp * 16 + (tid >> 5);
       const int64_t m = (int64_t)tm * BIG + pass * 64 + rr;
       const int64_t n = (int64_t)tn * BIG + c;
       if (m >= Mb || n >= N) continue;
-      const int64_t orow = la.out_row(m);
       float v[8];
       {
         v4f a0 = *reinterpret_cast<const v4f*>(stg + rr * SROW + c);
@@ -1037,61 +1082,7 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
 #pragma unroll
         for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
       }
-      const bool full = n + 7 < N;
-      if (ep.bias) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-          v[t] += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
-      }
-      if (Cinb) {
-        const int64_t o = orow * ep.ldcin + n;
-        float cv[8];
-        if (ivec && full) {
-          if (ep.cin_f32) {
-            float4 c0 = *reinterpret_cast<const float4*>((const float*)Cinb + o);
-            float4 c1 = *reinterpret_cast<const float4*>((const float*)Cinb + o + 4);
-            cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
-            cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
-          } else {
-            load_vec<bf16>((const bf16*)Cinb + o, cv);
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)Cinb)[o + t] : to_f(((const bf16*)Cinb)[o + t])) : 0.f;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
-      }
-#pragma unroll
-      for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
-      const int64_t o = orow * ep.ldc + n;
-      if (ep.out_f32) {
-        float* Cf = (float*)Cb + o;
-        if (cvec && full) {
-          *reinterpret_cast<float4*>(Cf) = make_float4(v[0], v[1], v[2], v[3]);
-          *reinterpret_cast<float4*>(Cf + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        } else {
-          for (int t = 0; t < 8; ++t)
-            if (n + t < N) Cf[t] = v[t];
-        }
-      } else {
-        bf16* Ch = (bf16*)Cb + o;
-        if (cvec && full) {
-          store_vec<bf16>(Ch, v);
-        } else {
-          for (int t = 0; t < 8; ++t)
-            if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
-        }
-      }
-      if (ep.colstats) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));
-          cs[t] += sv;
-          cq[t] += sv * sv;
-        }
-      }
+      epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
     }
     __syncthreads();
   }

@@ -211,7 +211,7 @@ HETU_API int hetu_optimizer_flat(int mode, float* p, float* g, float* s1, float*
     case OPT_ADAMW: launch_opt<OPT_ADAMW>(p, g, s1, s2, sh, n, a, st); break;
     case OPT_LAMB: {
       launch_opt<OPT_LAMB>(p, g, s1, s2, nullptr, n, a, st);
-      hipMemsetAsync(norms_ws, 0, sizeof(float) * 2 * nseg, st);
+      (void)hipMemsetAsync(norms_ws, 0, sizeof(float) * 2 * nseg, st);
       int blocks = (int)((n + 65535) / 65536);
       if (blocks < 1) blocks = 1;
       if (blocks > 2048) blocks = 2048;

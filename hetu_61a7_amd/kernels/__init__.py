@@ -100,6 +100,7 @@ def available() -> bool:
 # fallback into an error.
 FALLBACKS = {}
 NATIVE_CALLS = {}
+VENDOR_CALLS = {}
 _STRICT = os.environ.get('HETU_STRICT_NATIVE', '0') == '1'
 
 
@@ -113,9 +114,15 @@ def record_native(name):
     NATIVE_CALLS[name] = NATIVE_CALLS.get(name, 0) + 1
 
 
+def record_vendor(name):
+    """a GEMM / convolution served by the vendor library (hipBLASLt / MIOpen via torch)"""
+    VENDOR_CALLS[name] = VENDOR_CALLS.get(name, 0) + 1
+
+
 def reset_dispatch_stats():
     FALLBACKS.clear()
     NATIVE_CALLS.clear()
+    VENDOR_CALLS.clear()
 
 
 from . import elementwise, norm, softmax, optim, pool, sparse, reduce  # noqa: E402,F401

@@ -20,11 +20,26 @@ REPS = int(os.environ.get('HETU_AUTOTUNE_REPS', '5'))
 ROUNDS = int(os.environ.get('HETU_AUTOTUNE_ROUNDS', '3'))
 
 
-def choose(key, candidates):
+def _hand_written(name):
+    return name.startswith('hip')
+
+
+def choose(key, candidates, mode='auto'):
+    """``mode``: 'auto' times every candidate; 'hip' only the hand-written ones (names
+    starting with ``hip``); a library candidate is then the last resort for a shape no
+    hand-written kernel takes, counted in ``kernels.FALLBACKS``; 'vendor' picks the
+    first library candidate."""
     d = _decisions.get(key)
     if d is not None:
         return d
     names = list(candidates)
+    library = [n for n in names if not _hand_written(n)]
+    if mode == 'vendor':
+        return library[0] if library else names[0]
+    if mode == 'hip':
+        hw = [n for n in names if _hand_written(n)]
+        if hw:
+            names = hw
     from . import deterministic
     if deterministic():
         return names[0]       # fixed choice: the hand-written kernel every call site lists first
@@ -52,7 +67,14 @@ def choose(key, candidates):
             e.synchronize()
             t = s.elapsed_time(e) / REPS
             times[n] = min(times.get(n, t), t)
-    best = min(times, key=times.get) if times else names[-1]
+    if times:
+        best = min(times, key=times.get)
+    elif mode == 'hip' and library:
+        from . import record_fallback
+        record_fallback('%s: no hand-written kernel' % (key[0],))
+        best = library[0]
+    else:
+        best = names[-1]
     _decisions[key] = best
     _times[key] = times
     return best

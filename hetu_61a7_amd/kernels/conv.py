@@ -15,7 +15,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from . import native
+from . import native, record_vendor
 
 CL = torch.channels_last
 MODE = os.environ.get('HETU_CONV', 'auto')  # hip | vendor | auto (per-shape measured choice)
@@ -26,27 +26,36 @@ def _pick(key, hip, vendor, blas=None, tuned=None):
     run as the plain library GEMM it is (hipBLASLt), where applicable.
     ``tuned()`` runs once the choice is made, before the call that produces the
     result (candidates that write in place time against scratch until then)."""
-    if MODE == 'hip':
-        r = hip()
-        return r if r is not None else vendor()
     if MODE == 'vendor':
+        record_vendor('conv')
         return vendor()
     from .autotune import choose
     cands = {'hip': hip, 'vendor': vendor}
     if blas is not None:
         cands.update(blas)
-    c = choose(key, cands)
+    c = choose(key, cands, MODE)
     if tuned is not None:
         tuned()
-    if c not in ('hip', 'vendor'):
+    if c != 'vendor':
         r = cands[c]()
         if r is not None:
+            if not c.startswith('hip'):
+                record_vendor('conv')
             return r
-    if c == 'hip':
-        r = hip()
+        if c.startswith('hip'):
+            _fallback(key[0])
+    if c != 'hip':
+        r = hip() if MODE == 'hip' else None
         if r is not None:
             return r
+    record_vendor('conv')
     return vendor()
+
+
+def _fallback(name):
+    if MODE == 'hip':
+        from . import record_fallback
+        record_fallback('conv_' + name)
 
 
 def _plain_1x1(ts, w_shape, stride, padding):
@@ -128,11 +137,17 @@ def conv2d_with_stats(x, w, stride, padding):
                                                                    colstats=s))
     key = ('fwd_stats', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding))
     if MODE == 'vendor':
+        record_vendor('conv')
         return cands['vendor']()
     from .autotune import choose
-    c = 'hip' if MODE == 'hip' else choose(key, cands)
+    c = choose(key, cands, MODE)
     r = cands[c]()
+    if r is not None and not c.startswith('hip'):
+        record_vendor('conv')
     if r is None:
+        if c.startswith('hip'):
+            _fallback('fwd_stats')
+        record_vendor('conv')
         r = cands['vendor']()
     return r
 

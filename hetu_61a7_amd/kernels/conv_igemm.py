@@ -15,7 +15,7 @@ import os
 
 import torch
 
-from . import fn, stream_ptr, check, P, I32, I64
+from . import fn, stream_ptr, check, record_native, P, I32, I64
 
 MODE = os.environ.get('HETU_CONV', 'auto')
 CL = torch.channels_last
@@ -49,6 +49,7 @@ def forward_f32(x, w, stride, padding, bias=None, act=None):
     check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), bias.float().contiguous().data_ptr() if bias is not None
             else None, N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
             {None: 0, 'relu': 1}[act], stream_ptr()), 'conv_fwd_f32')
+    record_native('conv_fwd_f32')
     return y.permute(0, 3, 1, 2)
 
 
@@ -64,6 +65,7 @@ def backward_data_f32(g, w, x_shape, stride, padding, acc=None):
     f = fn('hetu_conv_dgrad_f32', [P, P, P, P] + _GEOM + [P])
     check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
             N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1], stream_ptr()), 'conv_dgrad_f32')
+    record_native('conv_dgrad_f32')
     return dx.permute(0, 3, 1, 2)
 
 
@@ -83,6 +85,7 @@ def backward_filter_f32(g, x, w_shape, stride, padding, out=None, accumulate=Non
     f = fn('hetu_conv_wgrad_f32', [P, P, P] + _GEOM + [I32, P])
     check(f(g.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
             padding[0], padding[1], int(bool(accumulate)), stream_ptr()), 'conv_wgrad_f32')
+    record_native('conv_wgrad_f32')
     return dw.permute(0, 3, 1, 2)
 
 
@@ -105,6 +108,7 @@ def try_forward(x, w, stride, padding, bias=None, act=None, tile=0, colstats=Non
             N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
             {None: 0, 'relu': 1}[act], colstats.data_ptr() if colstats is not None else None, int(tile),
             stream_ptr()), 'conv_fwd')
+    record_native('conv_fwd')
     return y.permute(0, 3, 1, 2)
 
 
@@ -122,6 +126,7 @@ def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0):
     check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
             int(acc is not None and acc.dtype == torch.float32), N, H, W, C, K, KH, KW,
             stride[0], stride[1], padding[0], padding[1], int(tile), stream_ptr()), 'conv_dgrad')
+    record_native('conv_dgrad')
     return dx.permute(0, 3, 1, 2)
 
 
@@ -156,4 +161,5 @@ def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=Non
     check(f(g.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
             padding[0], padding[1], sk, int(accumulate), ws.data_ptr() if ws is not None else None,
             int(tile), stream_ptr()), 'conv_wgrad')
+    record_native('conv_wgrad')
     return dw.permute(0, 3, 1, 2)

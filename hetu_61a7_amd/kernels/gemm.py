@@ -13,7 +13,7 @@ import os
 
 import torch
 
-from . import native
+from . import native, record_vendor
 
 _MFMA = os.environ.get('HETU_GEMM', 'auto')  # hip | vendor(off) | auto (measured per shape)
 
@@ -40,31 +40,33 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     if cpu_native.active(a, b, bias) and a.dim() == 2 and b.dim() == 2 and activation in (None, 'relu', 'gelu'):
         y = cpu_native.gemm(_tr(a, ta), _tr(b, tb), bias)
         return cpu_native.unary(activation, y) if activation else y
-    if native(a) and _MFMA not in ('off', 'vendor'):
+    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype in (torch.bfloat16, torch.float32):
         from . import gemm_mfma
-        hip = lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)
-        if _MFMA == 'hip':
-            y = hip()
+        from .autotune import choose
+        key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
+        cands = {'hip': lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)}
+        if a.dtype == torch.bfloat16 and _big_ok(a, b, ta, tb):
+            cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
+        cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
+        if bias is not None:
+            # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
+            # plain GEMM + a separate bias pass: measure both
+            cands['vendor_nobias'] = lambda: _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
+        c = choose(key, cands, _MFMA)
+        if c.startswith('hip'):
+            y = cands[c]()
             if y is not None:
                 return y
-        elif a.dtype == torch.bfloat16:
-            from .autotune import choose
-            key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
-            cands = {'hip': hip, 'vendor': lambda: _vendor(a, b, ta, tb, bias, activation)}
-            if _big_ok(a, b, ta, tb):
-                cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
-            if bias is not None:
-                # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
-                # plain GEMM + a separate bias pass: measure both
-                cands['vendor_nobias'] = lambda: _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
-            c = choose(key, cands)
-            if c in ('hip', 'hip256'):
-                y = cands[c]()
-                if y is not None:
-                    return y
-            elif c == 'vendor_nobias':
-                return _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
+            _fallback('matmul')
+        elif c == 'vendor_nobias':
+            return _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
     return _vendor(a, b, ta, tb, bias, activation)
+
+
+def _fallback(name):
+    if _MFMA == 'hip':
+        from . import record_fallback
+        record_fallback(name)
 
 
 def _big_ok(a, b, ta, tb):
@@ -85,6 +87,7 @@ def _as_dtype(t, dt):
 
 
 def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
+    record_vendor('gemm')
     A, B = _tr(a, ta), _tr(b, tb)
     if fuse_bias and bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
         y = torch.addmm(_as_dtype(bias, A.dtype), A, B)     # bias in the hipBLASLt epilogue
@@ -106,18 +109,15 @@ def bmm(a, b, ta=False, tb=False):
     a, b = _match(a, b)
     if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16:
         from . import gemm_mfma
+        from .autotune import choose
+        key = ('bmm', _sig(a), _sig(b), ta, tb)
         hip = lambda: gemm_mfma.try_bmm(a, b, ta, tb)
-        if _MFMA == 'hip':
+        if choose(key, {'hip': hip, 'vendor': lambda: torch.matmul(_tr(a, ta), _tr(b, tb))}, _MFMA) == 'hip':
             y = hip()
             if y is not None:
                 return y
-        else:
-            from .autotune import choose
-            key = ('bmm', _sig(a), _sig(b), ta, tb)
-            if choose(key, {'hip': hip, 'vendor': lambda: torch.matmul(_tr(a, ta), _tr(b, tb))}) == 'hip':
-                y = hip()
-                if y is not None:
-                    return y
+            _fallback('bmm')
+    record_vendor('bmm')
     return torch.matmul(_tr(a, ta), _tr(b, tb))
 
 
@@ -127,6 +127,7 @@ _MM_DTYPE_OK = [None]   # aten::mm.dtype (bf16 x bf16 -> fp32 in the hipBLASLt e
 def _vendor_into(A, B, out):
     """out (fp32) = A @ B on the library GEMM, writing fp32 directly when the
     bf16->fp32 ``mm.dtype`` overload is available (no bf16 round trip + copy)."""
+    record_vendor('gemm')
     if _MM_DTYPE_OK[0] is not False and A.is_cuda and A.dtype == torch.bfloat16 and A.dim() == 2 \
             and out.is_contiguous():
         try:
@@ -147,6 +148,7 @@ def _vendor_splitk_into(A, B, out, s=4):
     if K % s or not A.is_cuda:
         return None
     kc = K // s
+    record_vendor('gemm')
     # [M, K] -> [s, M, kc] and [K, N] -> [s, kc, N] as strided views (no copies)
     Av = A.as_strided((s, M, kc), (kc * A.stride(1), A.stride(0), A.stride(1)))
     Bv = B.as_strided((s, kc, N), (kc * B.stride(0), B.stride(0), B.stride(1)))
@@ -207,9 +209,11 @@ def matmul_into(a, b, ta, tb, out):
             if K >= 2048:
                 cands['vendor_sk'] = lambda: _vendor_splitk_into(A, B, out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
-        c = 'hip' if _MFMA == 'hip' else choose(key, cands)
+        c = choose(key, cands, _MFMA)
         if c != 'vendor' and cands[c]() is not None:
             return out
+        if c.startswith('hip'):
+            _fallback('matmul_into')
         return vendor()
     return _vendor_into(_tr(a, ta), _tr(b, tb), out)
 
@@ -235,13 +239,16 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
         cands = {'hip': hip, 'vendor': vendor}
         if A.shape[0] >= 256 and B.shape[1] >= 256:
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=1)
-        ch = 'hip' if _MFMA == 'hip' else choose(key, cands)
+        ch = choose(key, cands, _MFMA)
         dst[0] = c
         if ch != 'vendor':
             y = cands[ch]()
             if y is not None:
                 return y
+            _fallback('matmul_acc')
+        record_vendor('gemm')
         return vendor()
+    record_vendor('gemm')
     if A.dim() == 2 and acc.dim() == 2 and acc.dtype == A.dtype:
         return torch.addmm(acc, A, B)
     y = torch.matmul(A, B)

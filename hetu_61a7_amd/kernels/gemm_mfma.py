@@ -12,7 +12,7 @@ import os
 
 import torch
 
-from . import fn, stream_ptr, check, P, I64, I32, F32
+from . import fn, stream_ptr, check, record_native, P, I64, I32, F32
 
 _ACT = {None: 0, 'relu': 1, 'gelu': 2}
 _ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64, I64,
@@ -89,6 +89,7 @@ def gemm_f32(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None,
             bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, ldcin,
             int(da[0]), int(db[0]), batch, da[2], db[2], sC, sCin, float(alpha), float(beta), _ACT[act],
             int(bias_on_m), int(accumulate), stream_ptr()), 'gemm_f32')
+    record_native('gemm_f32')
     return out
 
 
@@ -148,6 +149,7 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
             int(cin_t is not None and cin_t.dtype == torch.float32), int(bias_on_m), int(splitk),
             int(accumulate), ws.data_ptr() if ws is not None else None, int(tile), stream_ptr()),
           'gemm_bf16')
+    record_native('gemm_bf16')
     return out
 
 

@@ -568,7 +568,8 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
 }
 
 __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (&v)[8], int64_t m, int64_t n,
-                                         int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8]) {
+                                         int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8],
+                                         const uint4* cpre = nullptr) {
   const bool full = n + 7 < N;
   if (ep.bias) {
     const float bm = ep.bias_on_m ? ep.bias[m] : 0.f;
@@ -578,7 +579,14 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
   if (o.Cinb) {
     const int64_t off = orow * ep.ldcin + n;
     float cv[8];
-    if (o.ivec && full) {
+    if (cpre && o.ivec && full && !ep.cin_f32) {
+      const uint32_t w[4] = {cpre->x, cpre->y, cpre->z, cpre->w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        cv[2 * t] = bf16_bits_to_f((unsigned short)(w[t] & 0xffffu));
+        cv[2 * t + 1] = bf16_bits_to_f((unsigned short)(w[t] >> 16));
+      }
+    } else if (o.ivec && full) {
       if (ep.cin_f32) {
         float4 c0 = *reinterpret_cast<const float4*>((const float*)o.Cinb + off);
         float4 c1 = *reinterpret_cast<const float4*>((const float*)o.Cinb + off + 4);
@@ -637,13 +645,22 @@ __device__ __forceinline__ void lds_barrier() {
 
 // ST: LDS stages.  1: one 32 KiB buffer when every block owns a single K-tile (short-K
 // 1x1 convolutions: more resident blocks per CU); 2: double buffer, vmcnt(0) +
-// barrier per K-tile (2 blocks per CU); 3 (not launched): three buffers, two K-tiles in
-// flight behind a counted vmcnt and a raw s_barrier.
-template <class LA, class LB, int ST>
+// barrier per K-tile (2 blocks per CU).  (A 3-stage variant at 1 block per CU measured
+// 0.5-0.8x of ST 2 on every bench_tiles shape: occupancy, not prefetch depth, hides the
+// DMA latency here.)
+// WN: 16-column MFMA blocks per wave along N.  4: 128x128 tile (waves 64x64);
+// 2: 128x64 tile (waves 64x32) for the 64-channel convolutions, where half of a 128-wide
+// tile's MFMAs would multiply zero columns.  The B image keeps its 128-row staging map
+// (rows past the tile are in-range neighbours or range-checked zeros, never read).
+template <class LA, class LB, int ST, int WN = 4>
 __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                   int64_t K, int tiles_m, int tiles_n, int ktps) {
   constexpr bool DB = ST >= 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[ST == 3 ? 6 * TILE_BYTES : (DB ? 4 * TILE_BYTES : 64 * (BN + 4) * 4)];
+  constexpr int TBN = 32 * WN;                 // block tile columns
+  constexpr int TPR = TBN / 8;                 // epilogue threads per row (8 columns each)
+  constexpr int RPP = NT / TPR;                // epilogue rows per pass
+  constexpr int NPASS = 64 / RPP;              // passes per 64-row half
+  __shared__ __attribute__((aligned(16))) char smem_raw[DB ? 4 * TILE_BYTES : 64 * (BN + 4) * 4];
   constexpr int buf_stride = DB ? 2 * TILE_BYTES : 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
@@ -661,7 +678,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
 
   const int64_t batch = blockIdx.y;
   la.init((int64_t)tm * BM, wave, lane, batch, 0);
-  lb.init((int64_t)tn * BN, wave, lane, batch, 0);
+  lb.init((int64_t)tn * TBN, wave, lane, batch, 0);
   // per-block problem view (a stride class of a strided dgrad may be smaller)
   const int64_t Mb = la.rows_eff(M);
   if ((int64_t)tm * BM >= Mb) return;  // block-uniform, before any barrier
@@ -671,11 +688,15 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   const int kt0 = blockIdx.z * ktps;
   const int kt1 = min(kt0 + ktps, nkt);
 
-  v4f acc[4][4];
+  const int ec = (tid % TPR) * 8;
+  EpiOut eo;
+  epi_init(ep, eo, batch, (int64_t)tn * TBN + ec, N);   // bias columns in flight during the K loop
+
+  v4f acc[4][WN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   // stage K-tile kt into LDS buffer b: 4 + 4 global_load_lds per wave
   auto stage = [&](int kt, int b) {
@@ -689,49 +710,48 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   };
 
   if (kt0 < kt1) stage(kt0, 0);
-  if (ST == 3 && kt0 + 1 < kt1) stage(kt0 + 1, 1);
-  if (ST != 3) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
-    int cur;
-    if constexpr (ST == 3) {
-      const int i = kt - kt0;
-      cur = i % 3;
-      // this wave's DMA of tile kt landed (kt+1's 8 may still fly), then every wave's
-      // (barrier); all waves also finished reading tile kt-1, whose buffer kt+2 reuses
-      if (kt + 1 < kt1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-      if (kt + 2 < kt1) stage(kt + 2, (i + 2) % 3);
-    } else {
-      cur = (kt - kt0) & 1;
-      if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
-    }
+    const int cur = (kt - kt0) & 1;
+    if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
     const char* As = smem_raw + cur * buf_stride;
     const char* Bs = As + TILE_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      v8s mf[4], nf[4];
+      v8s mf[4], nf[WN];
 #pragma unroll
       for (int i = 0; i < 4; ++i) mf[i] = lds_frag<LA::KMAJ>(As, wm * 4 + i, s, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) nf[j] = lds_frag<LB::KMAJ>(Bs, wn * 4 + j, s, lane);
+      for (int j = 0; j < WN; ++j) nf[j] = lds_frag<LB::KMAJ>(Bs, wn * WN + j, s, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < WN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[j], mf[i], acc[i][j], 0, 0, 0);
     }
-    if constexpr (ST != 3) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
-  if constexpr (ST == 3) {   // the epilogue reuses the LDS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+
+  // bf16 Cin (residual / gradient join, beta): all of this thread's Cin row pieces are
+  // requested at once before the LDS staging of the epilogue -- one memory latency
+  // instead of one per 16-row pass (the short-K 1x1 data-gradient joins were all
+  // epilogue latency).  Issuing them before the K loop instead measured slower: they
+  // queue ahead of the operand DMA that the first K-tile waits for.
+  uint4 cpre[2][NPASS];
+  const bool use_pre = eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec;
+  if (use_pre) {
+    const int64_t n = (int64_t)tn * TBN + ec;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int pss = 0; pss < NPASS; ++pss) {
+        const int64_t m = (int64_t)tm * BM + h * 64 + pss * RPP + tid / TPR;
+        cpre[h][pss] = (m < Mb && n + 7 < N)
+                           ? *reinterpret_cast<const uint4*>((const bf16*)eo.Cinb + la.out_row(m) * ep.ldcin + n)
+                           : make_uint4(0, 0, 0, 0);
+      }
   }
 
   // epilogue: lane holds C[m][n..n+3]
@@ -742,8 +762,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
       const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
       if (m >= Mb) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
+      for (int j = 0; j < WN; ++j) {
+        const int64_t n = (int64_t)tn * TBN + wn * 16 * WN + j * 16 + 4 * (lane >> 4);
         if (n >= N) continue;
         float* d = S + m * N + n;
         if (n + 3 < N && (N & 3) == 0) {
@@ -758,101 +778,68 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
     }
     return;
   }
-  char* Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
-  const char* Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
   if (!ep.atomic) {
     float cs[8], cq[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) { cs[t] = 0.f; cq[t] = 0.f; }
     // Row-coalesced epilogue: the tile goes through LDS in two 64-row halves
     // (fp32, rows padded by 4 floats so the 16-row MFMA write pattern spreads
-    // over the banks), then 16 lanes cover one 128-column row with 8 elements
-    // each: full 256-byte bf16 rows per instruction instead of 16 scattered
-    // 32-byte pieces, and the same for the Cin (residual / beta) read.
-    constexpr int SROW = BN + 4;
+    // over the banks), then TPR lanes cover one row with 8 elements each: full
+    // bf16 rows per instruction instead of scattered 32-byte pieces, and the same
+    // for the Cin (residual / beta) read.
+    constexpr int SROW = TBN + 4;
     float* stg = reinterpret_cast<float*>(smem_raw);
-    const int c = (tid & 15) * 8;
-    EpiOut eo;
-    epi_init(ep, eo, batch, (int64_t)tn * BN + c, N);
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       if (wm == half) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = i * 16 + (lane & 15), cc = wn * 64 + j * 16 + 4 * (lane >> 4);
-            *reinterpret_cast<v4f*>(stg + r * SROW + cc) = acc[i][j];
+          for (int j = 0; j < WN; ++j) {
+            const int rr = i * 16 + (lane & 15), cc = wn * 16 * WN + j * 16 + 4 * (lane >> 4);
+            *reinterpret_cast<v4f*>(stg + rr * SROW + cc) = acc[i][j];
           }
       }
       __syncthreads();
 #pragma unroll
-      for (int pss = 0; pss < 4; ++pss) {
-        const int r = pss * 16 + (tid >> 4);
-        const int64_t m = (int64_t)tm * BM + half * 64 + r;
-        const int64_t n = (int64_t)tn * BN + c;
+      for (int pss = 0; pss < NPASS; ++pss) {
+        const int rr = pss * RPP + tid / TPR;
+        const int64_t m = (int64_t)tm * BM + half * 64 + rr;
+        const int64_t n = (int64_t)tn * TBN + ec;
         if (m >= Mb || n >= N) continue;
         float v[8];
         {
-          v4f a0 = *reinterpret_cast<const v4f*>(stg + r * SROW + c);
-          v4f a1 = *reinterpret_cast<const v4f*>(stg + r * SROW + c + 4);
+          v4f a0 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec);
+          v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec + 4);
 #pragma unroll
           for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
         }
-        epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
+        epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre ? &cpre[half][pss] : nullptr);
       }
       __syncthreads();
     }
     if (ep.colstats)
-      epilogue_colstats<16, 4>(cs, cq, stg, tid, (int64_t)tn * BN, N, ep.colstats);
+      epilogue_colstats<TPR, 4>(cs, cq, stg, tid, (int64_t)tn * TBN, N, ep.colstats);
     return;
   }
+  // fp32 atomic accumulation (split-K without a slab / accumulate into C)
+  float* Cf = (float*)((char*)ep.C + batch * ep.sC * 4);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t m = (int64_t)tm * BM + wm * 64 + i * 16 + (lane & 15);
     if (m >= Mb) continue;
     const int64_t orow = la.out_row(m);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t n = (int64_t)tn * BN + wn * 64 + j * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < WN; ++j) {
+      const int64_t n = (int64_t)tn * TBN + wn * 16 * WN + j * 16 + 4 * (lane >> 4);
       if (n >= N) continue;
-      float v[4];
+      const int64_t o = orow * ep.ldc + n;
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
+        if (n + t >= N) continue;
         float x = acc[i][j][t] * ep.alpha;
-        if (ep.bias) x += ep.bias_on_m ? ep.bias[m] : (n + t < N ? ep.bias[n + t] : 0.f);
-        if (Cinb && n + t < N) {
-          int64_t o = orow * ep.ldcin + n + t;
-          float c = ep.cin_f32 ? ((const float*)Cinb)[o] : to_f(((const bf16*)Cinb)[o]);
-          x += ep.beta * c;
-        }
-        v[t] = act_f(x, ep.act);
-      }
-      const int64_t o = orow * ep.ldc + n;
-      if (ep.atomic) {
-        float* Cf = (float*)Cb;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          if (n + t < N) unsafeAtomicAdd(Cf + o + t, v[t]);
-      } else if (ep.out_f32) {
-        float* Cf = (float*)Cb;
-        if (n + 3 < N && (o & 3) == 0) {
-          *reinterpret_cast<float4*>(Cf + o) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-          for (int t = 0; t < 4; ++t)
-            if (n + t < N) Cf[o + t] = v[t];
-        }
-      } else {
-        unsigned short* Ch = (unsigned short*)Cb;
-        if (n + 3 < N && (o & 3) == 0) {
-          uint2 pk;
-          pk.x = (uint32_t)f_to_bf16_bits(v[0]) | ((uint32_t)f_to_bf16_bits(v[1]) << 16);
-          pk.y = (uint32_t)f_to_bf16_bits(v[2]) | ((uint32_t)f_to_bf16_bits(v[3]) << 16);
-          *reinterpret_cast<uint2*>(Ch + o) = pk;
-        } else {
-          for (int t = 0; t < 4; ++t)
-            if (n + t < N) Ch[o + t] = f_to_bf16_bits(v[t]);
-        }
+        if (ep.bias && blockIdx.z == 0) x += ep.bias_on_m ? ep.bias[m] : ep.bias[n + t];
+        unsafeAtomicAdd(Cf + o + t, x);
       }
     }
   }
@@ -1180,13 +1167,12 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
 }
 
 // tile: 0 = 128x128 (4 waves, 2 LDS stages, 2 blocks per CU), 1 = 256x256 (8 waves, 1 block
-// per CU).  (A 3-stage 128x128 variant at 1 block per CU measured 0.5-0.8x of tile 0 on every
-// bench_tiles shape -- occupancy, not prefetch depth, hides the DMA latency there; removed.)
-template <class LA, class LB>
-static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
-                  int batch, int splitk, hipStream_t st, int tile = 0) {
-  if (tile == 1) return launch_big(la, lb, ep, M, N, K, batch, splitk, st);
-  int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+// per CU), 2 = 128x64 (4 waves of 64x32; 64-channel convolutions).
+template <class LA, class LB, int WN>
+static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
+                    int batch, int splitk, hipStream_t st) {
+  constexpr int TBN = 32 * WN;
+  int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + TBN - 1) / TBN);
   int nkt = (int)((K + BK - 1) / BK);
   if (splitk < 1) splitk = 1;
   if (splitk > nkt) splitk = nkt > 0 ? nkt : 1;
@@ -1203,11 +1189,21 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
     if (splitk > 1) e1.atomic = 1;
   }
   if (ktps > 1)
-    hipLaunchKernelGGL((gemm_kernel<LA, LB, 2>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n, ktps);
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n,
+                       ktps);
   else
-    hipLaunchKernelGGL((gemm_kernel<LA, LB, 1>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n, ktps);
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, 1, WN>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n,
+                       ktps);
   if (slab) launch_splitk_reduce(ep.slab, splitk, ep.C, M, N, ep.ldc, ep.out_f32, ep.atomic, st);
   return (int)hipGetLastError();
+}
+
+template <class LA, class LB>
+static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
+                  int batch, int splitk, hipStream_t st, int tile = 0) {
+  if (tile == 1) return launch_big(la, lb, ep, M, N, K, batch, splitk, st);
+  if (tile == 2) return launch_t<LA, LB, 2>(la, lb, ep, M, N, K, batch, splitk, st);
+  return launch_t<LA, LB, 4>(la, lb, ep, M, N, K, batch, splitk, st);
 }
 
 // split count: ~2 blocks per CU in flight, each slice at least 8 K-tiles

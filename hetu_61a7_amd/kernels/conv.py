@@ -128,6 +128,10 @@ def conv2d_with_stats(x, w, stride, padding):
              'vendor': separate(lambda: F.conv2d(x, w, None, stride, padding))}
     if co >= 128:
         cands['hip256'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=1, colstats=s))
+    if co <= 64:
+        cands['hip64'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=2, colstats=s))
+    if conv_igemm.stem_ok(x, w, stride, padding):
+        cands['hip_stem'] = fused(lambda s: conv_igemm.try_stem_forward(x, w, stride, padding, colstats=s))
     if _plain_1x1((x, w), w.shape, stride, padding):
         n, _, h, ww_ = x.shape
         cands['blas'] = separate(lambda: torch.mm(_rows(x), w.reshape(co, -1).t()).view(n, h, ww_, co)
@@ -168,9 +172,14 @@ def conv2d(x, w, b, stride, padding):
             blas = {'blas': blas_fwd}
         elif _needs_pad(x, w):
             blas = {'hip_pad': lambda: conv_igemm.try_forward(_pad_c(x), _pad_c(w), stride, padding)}
+            if conv_igemm.stem_ok(x, w, stride, padding):
+                blas['hip_stem'] = lambda: conv_igemm.try_stem_forward(x, w, stride, padding)
         if w.shape[0] >= 128:   # 256x256-tile kernel: only with >= half a tile of output channels
             blas = dict(blas or {})
             blas['hip256'] = lambda: conv_igemm.try_forward(x, w, stride, padding, tile=1)
+        if w.shape[0] <= 64:    # 128x64 tile: no MFMAs on zero output channels
+            blas = dict(blas or {})
+            blas['hip64'] = lambda: conv_igemm.try_forward(x, w, stride, padding, tile=2)
         y = _pick(('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding)),
                   lambda: conv_igemm.try_forward(x, w, stride, padding),
                   lambda: F.conv2d(x, w, None, stride, padding), blas)
@@ -230,6 +239,9 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
         if x_shape[1] >= 128:
             blas = dict(blas or {})
             blas['hip256'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=1)
+        if x_shape[1] <= 64:
+            blas = dict(blas or {})
+            blas['hip64'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=2)
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
                      lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
                      lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas, tuned)

@@ -112,6 +112,35 @@ def try_forward(x, w, stride, padding, bias=None, act=None, tile=0, colstats=Non
     return y.permute(0, 3, 1, 2)
 
 
+def stem_ok(x, w, stride, padding):
+    """the direct few-channel stem kernel (``stem.hip``) takes this convolution"""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    co, c, kh, kw = w.shape
+    return (co == 64 and kw * c <= 24 and kh <= 8 and stride[0] == stride[1] and padding[0] == padding[1]
+            and (stride[0] * c) % 2 == 0 and x.shape[1] == c)
+
+
+def try_stem_forward(x, w, stride, padding, colstats=None):
+    """Direct convolution of a few-channel input (ResNet conv1: 3 channels, 7x7/2) without
+    padding the channels to the 8-wide chunks of the implicit-GEMM kernels."""
+    if not stem_ok(x, w, stride, padding):
+        return None
+    x = x.contiguous(memory_format=CL)
+    w = w.contiguous(memory_format=CL)
+    N, C, H, W = x.shape
+    K, _, KH, KW = w.shape
+    OH, OW = _out_hw(H, W, KH, KW, stride, padding)
+    wp = torch.empty(fn('hetu_stem_wp_elems', [I32], restype=I64)(KH), dtype=torch.bfloat16, device=x.device)
+    y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
+    f = fn('hetu_stem_fwd', [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P])
+    check(f(x.data_ptr(), w.data_ptr(), wp.data_ptr(), y.data_ptr(),
+            colstats.data_ptr() if colstats is not None else None, N, H, W, C, KH, KW, stride[0], padding[0],
+            stream_ptr()), 'stem_fwd')
+    record_native('stem_fwd')
+    return y.permute(0, 3, 1, 2)
+
+
 def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0):
     if not _ok(g, w, x_shape[1], w.shape[0]):
         return None

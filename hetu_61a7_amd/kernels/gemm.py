@@ -47,6 +47,8 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
         cands = {'hip': lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)}
         if a.dtype == torch.bfloat16 and _big_ok(a, b, ta, tb):
             cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
+        if a.dtype == torch.bfloat16 and _tr(b, tb).shape[-1] <= 64:
+            cands['hip64'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=2)
         cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
         if bias is not None:
             # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the

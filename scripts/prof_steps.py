@@ -70,7 +70,7 @@ def main():
     for want in a.context:
         print('\n# launches of %r in the last step (prev | this | next)' % want)
         for i, r in enumerate(last):
-            if want in classify(r['Kernel_Name']):
+            if want.lower() in classify(r['Kernel_Name']).lower():
                 dur = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
                 nb = lambda j: classify(last[j]['Kernel_Name']) if 0 <= j < len(last) else '-'
                 print('%4d  %-40s | %-30s %7.1f us grid %s | %s' % (

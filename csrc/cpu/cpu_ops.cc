@@ -197,3 +197,264 @@ API void hetu_cpu_optimizer(int mode, float* p, const float* g, float* s1, float
 }
 
 API int hetu_cpu_num_threads() { return omp_get_max_threads(); }
+
+// ---- convolution (NCHW fp32) ------------------------------------------------------------
+// The reference's DNNL convolution (src/dnnl_ops/Conv2d.cpp): here im2col of one image
+// into a [C*KH*KW][OH*OW] panel and the packed GEMM above, images in sequence (the GEMM
+// is OpenMP-parallel over its output blocks); the data gradient is the transposed GEMM
+// followed by col2im, the filter gradient accumulates dy[n] @ col[n]^T over images.
+namespace {
+
+struct ConvShape {
+  int64_t N, C, H, W, K, KH, KW, sh, sw, ph, pw, OH, OW;
+  int64_t ckk() const { return C * KH * KW; }
+  int64_t ohw() const { return OH * OW; }
+};
+
+void im2col(const ConvShape& s, const float* x, float* col) {
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int64_t c = 0; c < s.C; ++c)
+    for (int64_t kh = 0; kh < s.KH; ++kh)
+      for (int64_t kw = 0; kw < s.KW; ++kw) {
+        float* dst = col + ((c * s.KH + kh) * s.KW + kw) * s.ohw();
+        for (int64_t oh = 0; oh < s.OH; ++oh) {
+          const int64_t ih = oh * s.sh - s.ph + kh;
+          for (int64_t ow = 0; ow < s.OW; ++ow) {
+            const int64_t iw = ow * s.sw - s.pw + kw;
+            dst[oh * s.OW + ow] = (ih >= 0 && ih < s.H && iw >= 0 && iw < s.W) ? x[(c * s.H + ih) * s.W + iw] : 0.f;
+          }
+        }
+      }
+}
+
+// dx[c] += col scattered back (each channel owned by one thread: no races)
+void col2im(const ConvShape& s, const float* col, float* dx) {
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < s.C; ++c)
+    for (int64_t kh = 0; kh < s.KH; ++kh)
+      for (int64_t kw = 0; kw < s.KW; ++kw) {
+        const float* src = col + ((c * s.KH + kh) * s.KW + kw) * s.ohw();
+        for (int64_t oh = 0; oh < s.OH; ++oh) {
+          const int64_t ih = oh * s.sh - s.ph + kh;
+          if (ih < 0 || ih >= s.H) continue;
+          for (int64_t ow = 0; ow < s.OW; ++ow) {
+            const int64_t iw = ow * s.sw - s.pw + kw;
+            if (iw >= 0 && iw < s.W) dx[(c * s.H + ih) * s.W + iw] += src[oh * s.OW + ow];
+          }
+        }
+      }
+}
+
+ConvShape conv_shape(int64_t N, int64_t C, int64_t H, int64_t W, int64_t K, int64_t KH, int64_t KW, int64_t sh,
+                     int64_t sw, int64_t ph, int64_t pw) {
+  ConvShape s{N, C, H, W, K, KH, KW, sh, sw, ph, pw, 0, 0};
+  s.OH = (H + 2 * ph - KH) / sh + 1;
+  s.OW = (W + 2 * pw - KW) / sw + 1;
+  return s;
+}
+
+}  // namespace
+
+// y[N][K][OH][OW] = conv(x[N][C][H][W], w[K][C][KH][KW]) (+ bias[K])
+API void hetu_cpu_conv2d(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C,
+                         int64_t H, int64_t W, int64_t K, int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t ph,
+                         int64_t pw) {
+  const ConvShape s = conv_shape(N, C, H, W, K, KH, KW, sh, sw, ph, pw);
+  std::vector<float> col((size_t)s.ckk() * s.ohw());
+  for (int64_t n = 0; n < N; ++n) {
+    im2col(s, x + n * C * H * W, col.data());
+    float* yn = y + n * K * s.ohw();
+    hetu_cpu_gemm(w, col.data(), yn, nullptr, K, s.ohw(), s.ckk(), s.ckk(), s.ohw(), s.ohw(), 0, 0, 1.f, 0.f);
+    if (bias) {
+#pragma omp parallel for schedule(static)
+      for (int64_t k = 0; k < K; ++k)
+        for (int64_t i = 0; i < s.ohw(); ++i) yn[k * s.ohw() + i] += bias[k];
+    }
+  }
+}
+
+// dx[N][C][H][W] = conv^T(dy, w)
+API void hetu_cpu_conv2d_bwd_data(const float* dy, const float* w, float* dx, int64_t N, int64_t C, int64_t H,
+                                  int64_t W, int64_t K, int64_t KH, int64_t KW, int64_t sh, int64_t sw, int64_t ph,
+                                  int64_t pw) {
+  const ConvShape s = conv_shape(N, C, H, W, K, KH, KW, sh, sw, ph, pw);
+  std::vector<float> col((size_t)s.ckk() * s.ohw());
+  memset(dx, 0, sizeof(float) * N * C * H * W);
+  for (int64_t n = 0; n < N; ++n) {
+    // col[ckk][ohw] = w^T [ckk][K] @ dy[n] [K][ohw]
+    hetu_cpu_gemm(w, dy + n * K * s.ohw(), col.data(), nullptr, s.ckk(), s.ohw(), K, s.ckk(), s.ohw(), s.ohw(), 1,
+                  0, 1.f, 0.f);
+    col2im(s, col.data(), dx + n * C * H * W);
+  }
+}
+
+// dw[K][C][KH][KW] = sum_n dy[n] @ im2col(x[n])^T; db[K] = sum dy (nullable)
+API void hetu_cpu_conv2d_bwd_filter(const float* dy, const float* x, float* dw, float* db, int64_t N, int64_t C,
+                                    int64_t H, int64_t W, int64_t K, int64_t KH, int64_t KW, int64_t sh, int64_t sw,
+                                    int64_t ph, int64_t pw) {
+  const ConvShape s = conv_shape(N, C, H, W, K, KH, KW, sh, sw, ph, pw);
+  std::vector<float> col((size_t)s.ckk() * s.ohw());
+  for (int64_t n = 0; n < N; ++n) {
+    im2col(s, x + n * C * H * W, col.data());
+    hetu_cpu_gemm(dy + n * K * s.ohw(), col.data(), dw, nullptr, K, s.ckk(), s.ohw(), s.ohw(), s.ohw(), s.ckk(), 0,
+                  1, 1.f, n == 0 ? 0.f : 1.f);
+  }
+  if (db) {
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < K; ++k) {
+      double a = 0.0;
+      for (int64_t n = 0; n < N; ++n)
+        for (int64_t i = 0; i < s.ohw(); ++i) a += dy[(n * K + k) * s.ohw() + i];
+      db[k] = (float)a;
+    }
+  }
+}
+
+// ---- pooling (NCHW fp32; reference src/dnnl_ops/MaxPool.cpp, AvgPool.cpp) ----------------
+// max: idx[N*C*OH*OW] keeps the argmax input offset inside the plane for the backward
+API void hetu_cpu_maxpool2d(const float* x, float* y, int32_t* idx, int64_t NC, int64_t H, int64_t W, int64_t KH,
+                            int64_t KW, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t OH, int64_t OW) {
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < NC; ++p) {
+    const float* xp = x + p * H * W;
+    for (int64_t oh = 0; oh < OH; ++oh)
+      for (int64_t ow = 0; ow < OW; ++ow) {
+        float m = -INFINITY;
+        int32_t mi = -1;
+        for (int64_t kh = 0; kh < KH; ++kh) {
+          const int64_t ih = oh * sh - ph + kh;
+          if (ih < 0 || ih >= H) continue;
+          for (int64_t kw = 0; kw < KW; ++kw) {
+            const int64_t iw = ow * sw - pw + kw;
+            if (iw < 0 || iw >= W) continue;
+            const float v = xp[ih * W + iw];
+            if (v > m || mi < 0) { m = v; mi = (int32_t)(ih * W + iw); }
+          }
+        }
+        y[(p * OH + oh) * OW + ow] = m;
+        idx[(p * OH + oh) * OW + ow] = mi;
+      }
+  }
+}
+
+API void hetu_cpu_maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, int64_t NC, int64_t H, int64_t W,
+                                int64_t OH, int64_t OW) {
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < NC; ++p) {
+    float* dp = dx + p * H * W;
+    memset(dp, 0, sizeof(float) * H * W);
+    for (int64_t o = 0; o < OH * OW; ++o) {
+      const int32_t i = idx[p * OH * OW + o];
+      if (i >= 0) dp[i] += dy[p * OH * OW + o];
+    }
+  }
+}
+
+// average over the window including padding (count_include_pad, the reference's cuDNN mode)
+API void hetu_cpu_avgpool2d(const float* x, float* y, int64_t NC, int64_t H, int64_t W, int64_t KH, int64_t KW,
+                            int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t OH, int64_t OW) {
+  const float inv = 1.f / (float)(KH * KW);
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < NC; ++p) {
+    const float* xp = x + p * H * W;
+    for (int64_t oh = 0; oh < OH; ++oh)
+      for (int64_t ow = 0; ow < OW; ++ow) {
+        float a = 0.f;
+        for (int64_t kh = 0; kh < KH; ++kh) {
+          const int64_t ih = oh * sh - ph + kh;
+          if (ih < 0 || ih >= H) continue;
+          for (int64_t kw = 0; kw < KW; ++kw) {
+            const int64_t iw = ow * sw - pw + kw;
+            if (iw >= 0 && iw < W) a += xp[ih * W + iw];
+          }
+        }
+        y[(p * OH + oh) * OW + ow] = a * inv;
+      }
+  }
+}
+
+API void hetu_cpu_avgpool2d_bwd(const float* dy, float* dx, int64_t NC, int64_t H, int64_t W, int64_t KH, int64_t KW,
+                                int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t OH, int64_t OW) {
+  const float inv = 1.f / (float)(KH * KW);
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < NC; ++p) {
+    float* dp = dx + p * H * W;
+    memset(dp, 0, sizeof(float) * H * W);
+    for (int64_t oh = 0; oh < OH; ++oh)
+      for (int64_t ow = 0; ow < OW; ++ow) {
+        const float g = dy[(p * OH + oh) * OW + ow] * inv;
+        for (int64_t kh = 0; kh < KH; ++kh) {
+          const int64_t ih = oh * sh - ph + kh;
+          if (ih < 0 || ih >= H) continue;
+          for (int64_t kw = 0; kw < KW; ++kw) {
+            const int64_t iw = ow * sw - pw + kw;
+            if (iw >= 0 && iw < W) dp[ih * W + iw] += g;
+          }
+        }
+      }
+  }
+}
+
+// ---- batch normalisation (NCHW fp32; reference src/dnnl_ops/BatchNorm.cpp) -------------
+// training: batch statistics (biased variance for the normalisation), running stats
+// updated with `momentum` (unbiased variance, the PyTorch convention); saves mean / rstd
+API void hetu_cpu_batchnorm(const float* x, const float* gamma, const float* beta, float* y, float* run_mean,
+                            float* run_var, float* save_mean, float* save_rstd, int64_t N, int64_t C, int64_t HW,
+                            float momentum, float eps, int training) {
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < C; ++c) {
+    float mean, rstd;
+    if (training) {
+      double s = 0.0, q = 0.0;
+      for (int64_t n = 0; n < N; ++n) {
+        const float* xp = x + (n * C + c) * HW;
+        for (int64_t i = 0; i < HW; ++i) { s += xp[i]; q += (double)xp[i] * xp[i]; }
+      }
+      const double cnt = (double)N * HW;
+      const double m = s / cnt;
+      const double var = std::max(0.0, q / cnt - m * m);
+      mean = (float)m;
+      rstd = (float)(1.0 / sqrt(var + eps));
+      if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+      if (run_var) run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)(var * cnt / std::max(1.0, cnt - 1));
+    } else {
+      mean = run_mean[c];
+      rstd = 1.f / sqrtf(run_var[c] + eps);
+    }
+    if (save_mean) save_mean[c] = mean;
+    if (save_rstd) save_rstd[c] = rstd;
+    const float a = gamma[c] * rstd, b = beta[c] - mean * a;
+    for (int64_t n = 0; n < N; ++n) {
+      const float* xp = x + (n * C + c) * HW;
+      float* yp = y + (n * C + c) * HW;
+      for (int64_t i = 0; i < HW; ++i) yp[i] = xp[i] * a + b;
+    }
+  }
+}
+
+// dx = gamma*rstd/M * (M*dy - sum(dy) - xhat*sum(dy*xhat)); dgamma = sum(dy*xhat); dbeta = sum(dy)
+API void hetu_cpu_batchnorm_bwd(const float* dy, const float* x, const float* gamma, const float* save_mean,
+                                const float* save_rstd, float* dx, float* dgamma, float* dbeta, int64_t N, int64_t C,
+                                int64_t HW) {
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < C; ++c) {
+    const float mean = save_mean[c], rstd = save_rstd[c];
+    double sg = 0.0, sgx = 0.0;
+    for (int64_t n = 0; n < N; ++n) {
+      const float* xp = x + (n * C + c) * HW;
+      const float* gp = dy + (n * C + c) * HW;
+      for (int64_t i = 0; i < HW; ++i) { sg += gp[i]; sgx += (double)gp[i] * (xp[i] - mean) * rstd; }
+    }
+    dgamma[c] = (float)sgx;
+    dbeta[c] = (float)sg;
+    const double M = (double)N * HW;
+    const float k = gamma[c] * rstd;
+    const float mg = (float)(sg / M), mgx = (float)(sgx / M);
+    for (int64_t n = 0; n < N; ++n) {
+      const float* xp = x + (n * C + c) * HW;
+      const float* gp = dy + (n * C + c) * HW;
+      float* dp = dx + (n * C + c) * HW;
+      for (int64_t i = 0; i < HW; ++i) dp[i] = k * (gp[i] - mg - (xp[i] - mean) * rstd * mgx);
+    }
+  }
+}

@@ -158,6 +158,9 @@ def conv2d_with_stats(x, w, stride, padding):
 
 def conv2d(x, w, b, stride, padding):
     x, w = _match(x, w)
+    from . import cpu_native
+    if cpu_native.active(x, w, b) and x.dim() == 4:
+        return cpu_native.conv2d(x, w, b, stride, padding)
     if x.is_cuda:
         x = x.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
@@ -197,6 +200,10 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     epilogue on the HIP path).  ``acc_inplace``: acc is dead after this call and
     may receive the result (the library GEMM accumulates into it, C == D)."""
     g, w = _match(g, w)
+    from . import cpu_native
+    if cpu_native.active(g, w, acc):
+        dx = cpu_native.conv2d_backward_data(g, w, x_shape, stride, padding)
+        return dx + acc.float() if acc is not None else dx
     if g.is_cuda:
         g = g.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
@@ -278,6 +285,13 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
     if out is not None and (out.dtype != torch.float32 or tuple(out.shape) != tuple(w_shape) or
                             not out.is_contiguous(memory_format=CL)):
         out = None
+    from . import cpu_native
+    if cpu_native.active(g, x):
+        dw = cpu_native.conv2d_backward_filter(g, x, w_shape, stride, padding)
+        if out is not None:
+            out.copy_(dw)
+            return out
+        return dw
     if g.is_cuda:
         g = g.contiguous(memory_format=CL)
         x = x.contiguous(memory_format=CL)

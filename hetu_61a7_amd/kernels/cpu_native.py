@@ -32,7 +32,16 @@ def lib():
                'hetu_cpu_softmax_ce_bwd': [P, P, P, P, P, I64, I64, I32],
                'hetu_cpu_unary': [I32, P, P, I64], 'hetu_cpu_relu_grad': [P, P, P, I64],
                'hetu_cpu_reduce_rows': [P, P, I64, I64, F32], 'hetu_cpu_gather_rows': [P, P, P, I64, I64, I64],
-               'hetu_cpu_optimizer': [I32, P, P, P, P, I64] + [F32] * 10}
+               'hetu_cpu_optimizer': [I32, P, P, P, P, I64] + [F32] * 10,
+               'hetu_cpu_conv2d': [P, P, P, P] + [I64] * 11,
+               'hetu_cpu_conv2d_bwd_data': [P, P, P] + [I64] * 11,
+               'hetu_cpu_conv2d_bwd_filter': [P, P, P, P] + [I64] * 11,
+               'hetu_cpu_maxpool2d': [P, P, P] + [I64] * 11,
+               'hetu_cpu_maxpool2d_bwd': [P, P, P] + [I64] * 5,
+               'hetu_cpu_avgpool2d': [P, P] + [I64] * 11,
+               'hetu_cpu_avgpool2d_bwd': [P, P] + [I64] * 11,
+               'hetu_cpu_batchnorm': [P] * 8 + [I64] * 3 + [F32, F32, I32],
+               'hetu_cpu_batchnorm_bwd': [P] * 8 + [I64] * 3}
         for k, v in sig.items():
             getattr(L, k).argtypes = v
             getattr(L, k).restype = None
@@ -131,3 +140,106 @@ def gather_rows(table, ids):
 def optimizer(mode, p, g, s1, s2, lr, l2, mu, b1, b2, b1t, b2t, eps, wd, gscale):
     lib().hetu_cpu_optimizer(OPT[mode], _p(p), _p(g), _p(s1), _p(s2), p.numel(), lr, l2, mu, b1, b2, b1t, b2t, eps,
                              wd, gscale)
+
+
+# ---- convolution / pooling / batch norm (NCHW fp32; reference src/dnnl_ops) ----------
+def _nchw(t):
+    return t.float().contiguous()
+
+
+def _conv_out(H, W, KH, KW, stride, padding):
+    return (H + 2 * padding[0] - KH) // stride[0] + 1, (W + 2 * padding[1] - KW) // stride[1] + 1
+
+
+def conv2d(x, w, b, stride, padding):
+    x, w = _nchw(x), _nchw(w)
+    N, C, H, W = x.shape
+    K, _, KH, KW = w.shape
+    OH, OW = _conv_out(H, W, KH, KW, stride, padding)
+    y = torch.empty((N, K, OH, OW), dtype=torch.float32)
+    lib().hetu_cpu_conv2d(_p(x), _p(w), _p(b.float().contiguous() if b is not None else None), _p(y),
+                          N, C, H, W, K, KH, KW, stride[0], stride[1], padding[0], padding[1])
+    return y
+
+
+def conv2d_backward_data(dy, w, x_shape, stride, padding):
+    dy, w = _nchw(dy), _nchw(w)
+    N, C, H, W = x_shape
+    K, _, KH, KW = w.shape
+    dx = torch.empty((N, C, H, W), dtype=torch.float32)
+    lib().hetu_cpu_conv2d_bwd_data(_p(dy), _p(w), _p(dx), N, C, H, W, K, KH, KW, stride[0], stride[1],
+                                   padding[0], padding[1])
+    return dx
+
+
+def conv2d_backward_filter(dy, x, w_shape, stride, padding, want_bias=False):
+    dy, x = _nchw(dy), _nchw(x)
+    N, C, H, W = x.shape
+    K, _, KH, KW = w_shape
+    dw = torch.empty(tuple(w_shape), dtype=torch.float32)
+    db = torch.empty(K, dtype=torch.float32) if want_bias else None
+    lib().hetu_cpu_conv2d_bwd_filter(_p(dy), _p(x), _p(dw), _p(db), N, C, H, W, K, KH, KW, stride[0], stride[1],
+                                     padding[0], padding[1])
+    return (dw, db) if want_bias else dw
+
+
+def maxpool2d(x, kh, kw, sh, sw, ph, pw):
+    """(y, idx int32 [N, C, OH, OW] = argmax offset inside the H*W plane)"""
+    x = _nchw(x)
+    N, C, H, W = x.shape
+    OH, OW = _conv_out(H, W, kh, kw, (sh, sw), (ph, pw))
+    y = torch.empty((N, C, OH, OW), dtype=torch.float32)
+    idx = torch.empty((N, C, OH, OW), dtype=torch.int32)
+    lib().hetu_cpu_maxpool2d(_p(x), _p(y), _p(idx), N * C, H, W, kh, kw, sh, sw, ph, pw, OH, OW)
+    return y, idx
+
+
+def maxpool2d_backward(dy, idx, x_shape):
+    dy = _nchw(dy)
+    N, C, H, W = x_shape
+    dx = torch.empty((N, C, H, W), dtype=torch.float32)
+    lib().hetu_cpu_maxpool2d_bwd(_p(dy), _p(idx.contiguous()), _p(dx), N * C, H, W, dy.shape[2], dy.shape[3])
+    return dx
+
+
+def avgpool2d(x, kh, kw, sh, sw, ph, pw):
+    x = _nchw(x)
+    N, C, H, W = x.shape
+    OH, OW = _conv_out(H, W, kh, kw, (sh, sw), (ph, pw))
+    y = torch.empty((N, C, OH, OW), dtype=torch.float32)
+    lib().hetu_cpu_avgpool2d(_p(x), _p(y), N * C, H, W, kh, kw, sh, sw, ph, pw, OH, OW)
+    return y
+
+
+def avgpool2d_backward(dy, x_shape, kh, kw, sh, sw, ph, pw):
+    dy = _nchw(dy)
+    N, C, H, W = x_shape
+    dx = torch.empty((N, C, H, W), dtype=torch.float32)
+    lib().hetu_cpu_avgpool2d_bwd(_p(dy), _p(dx), N * C, H, W, kh, kw, sh, sw, ph, pw, dy.shape[2], dy.shape[3])
+    return dx
+
+
+def batchnorm(x, scale, bias, running_mean, running_var, factor, eps, training):
+    """(y, save_mean, save_invstd); running stats updated in place when training"""
+    x = _nchw(x)
+    N, C = x.shape[0], x.shape[1]
+    HW = x.numel() // max(N * C, 1)
+    y = torch.empty_like(x)
+    sm = torch.empty(C, dtype=torch.float32)
+    sr = torch.empty(C, dtype=torch.float32)
+    lib().hetu_cpu_batchnorm(_p(x), _p(scale.float().contiguous()), _p(bias.float().contiguous()), _p(y),
+                             _p(running_mean), _p(running_var), _p(sm), _p(sr), N, C, HW, float(factor), float(eps),
+                             int(bool(training)))
+    return y, sm, sr
+
+
+def batchnorm_backward(dy, x, scale, save_mean, save_invstd):
+    dy, x = _nchw(dy), _nchw(x)
+    N, C = x.shape[0], x.shape[1]
+    HW = x.numel() // max(N * C, 1)
+    dx = torch.empty_like(x)
+    ds = torch.empty(C, dtype=torch.float32)
+    db = torch.empty(C, dtype=torch.float32)
+    lib().hetu_cpu_batchnorm_bwd(_p(dy), _p(x), _p(scale.float().contiguous()), _p(save_mean.contiguous()),
+                                 _p(save_invstd.contiguous()), _p(dx), _p(ds), _p(db), N, C, HW)
+    return dx, ds, db

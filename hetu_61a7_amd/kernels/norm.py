@@ -87,6 +87,15 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
                     sums.data_ptr() if (sums is not None and training) else None,
                     mask.data_ptr() if mask is not None else None, stream_ptr()), 'bn_fwd')
             return y, save_mean, save_invstd
+    from . import cpu_native
+    if (x.dim() == 4 and cpu_native.active(x, scale, bias, running_mean, running_var)
+            and (training or running_mean is not None)):
+        y, mean, invstd = cpu_native.batchnorm(x, scale, bias, running_mean, running_var, factor, eps, training)
+        if residual is not None:
+            y = y + residual.float()
+        if relu:
+            y = cpu_native.unary('relu', y)
+        return y, mean, invstd
     # torch reference (CPU backend / unsupported layouts)
     xf = x.float()
     dims = [0] + list(range(2, x.dim()))
@@ -146,6 +155,11 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
                     mask.data_ptr() if mask is not None else None, stream_ptr()),
                   'bn_bwd')
             return dx, dscale, dbias, dres
+    from . import cpu_native
+    if x.dim() == 4 and cpu_native.active(dy, x, scale, save_mean, save_invstd) and (not relu or y is not None):
+        g = cpu_native.relu_grad(y.float().contiguous(), dy.float().contiguous()) if relu else dy.float()
+        dx, dscale, dbias = cpu_native.batchnorm_backward(g, x, scale, save_mean, save_invstd)
+        return dx, dscale, dbias, (g.clone() if want_dres else None)
     dims = [0] + list(range(2, x.dim()))
     shape = [1, C] + [1] * (x.dim() - 2)
     g = dy.float()

@@ -25,6 +25,9 @@ def maxpool2d(x, kh, kw, sh, sw, ph, pw):
         check(f(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C, Ho, Wo, kh, kw, sh, sw,
                 ph, pw, is_bf16(x), stream_ptr()), 'maxpool')
         return y, idx
+    from . import cpu_native
+    if cpu_native.active(x):
+        return cpu_native.maxpool2d(x, kh, kw, sh, sw, ph, pw)
     y, ind = F.max_pool2d(x.float(), (kh, kw), (sh, sw), (ph, pw), return_indices=True)
     return y.to(x.dtype), ind
 
@@ -39,6 +42,9 @@ def maxpool2d_backward(dy, idx, x_shape, kh, kw, sh, sw, ph, pw):
         check(f(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, H, W, C, Ho, Wo, kh, kw, sh, sw,
                 ph, pw, is_bf16(dy), stream_ptr()), 'maxpool_bwd')
         return dx
+    from . import cpu_native
+    if cpu_native.active(dy) and idx.dtype == torch.int32:
+        return cpu_native.maxpool2d_backward(dy, idx, x_shape)
     return F.max_unpool2d(dy.float(), idx, (kh, kw), (sh, sw), (ph, pw),
                           output_size=(H, W)).to(dy.dtype)
 
@@ -53,6 +59,9 @@ def avgpool2d(x, kh, kw, sh, sw, ph, pw):
         check(f(x.data_ptr(), y.data_ptr(), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
                 is_bf16(x), stream_ptr()), 'avgpool')
         return y
+    from . import cpu_native
+    if cpu_native.active(x):
+        return cpu_native.avgpool2d(x, kh, kw, sh, sw, ph, pw)
     return F.avg_pool2d(x.float(), (kh, kw), (sh, sw), (ph, pw)).to(x.dtype)
 
 
@@ -66,6 +75,9 @@ def avgpool2d_backward(dy, x_shape, kh, kw, sh, sw, ph, pw):
         check(f(dy.data_ptr(), dx.data_ptr(), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
                 is_bf16(dy), stream_ptr()), 'avgpool_bwd')
         return dx
+    from . import cpu_native
+    if cpu_native.active(dy):
+        return cpu_native.avgpool2d_backward(dy, x_shape, kh, kw, sh, sw, ph, pw)
     xs = torch.zeros(x_shape, dtype=torch.float32, device=dy.device, requires_grad=True)
     with torch.enable_grad():
         y = F.avg_pool2d(xs, (kh, kw), (sh, sw), (ph, pw))

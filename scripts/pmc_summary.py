@@ -68,6 +68,14 @@ def main(dirs):
         tw = wr[2].get(k, 0) * 1e-9
         w = wr[0].get(k, {}).get('WRITE_SIZE', 0) * 1024 / tw / 1e12 if tw else float('nan')
         print('%-64s %6d %8.2f %8.2f %8.3f %8.3f %8.3f %8.2f %7.2f' % (k[:64], calls[k], t * 1e3, clk, mf, wait, lc, rd, w))
+    # every counter of every pass, per dispatch (raw sums / calls), for the top families
+    print('\n# raw counters per dispatch')
+    for k, c in rows[:12]:
+        allc = dict(c)
+        for d in (mem, wr):
+            allc.update(d[0].get(k, {}) if d[0] else {})
+        n = max(calls[k], 1)
+        print('%s: %s' % (k[:64], ', '.join('%s=%.4g' % (cn, v / n) for cn, v in sorted(allc.items()))))
 
 
 if __name__ == '__main__':

@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#ifndef BENCH_FAST
 namespace hetu {
 namespace gemm {
 template int launch_buf<true>(const bf16*, const bf16*, int, int, int64_t, int64_t, int64_t, int64_t, const Epi&,
@@ -21,9 +22,28 @@ template int launch_buf<false>(const bf16*, const bf16*, int, int, int64_t, int6
                                int64_t, int64_t, int64_t, int, int, hipStream_t, int);
 }  // namespace gemm
 }  // namespace hetu
+#endif
 
 using namespace hetu;
 using namespace hetu::gemm;
+
+// -DBENCH_FAST: only the 256x256 kernel (tile 1), K % 64 == 0, for quick kernel iteration
+static int run_tile(const bf16* a, const bf16* b, int a_kmaj, int b_kmaj, int64_t lda, int64_t ldb, const Epi& ep,
+                    int64_t M, int64_t N, int64_t K, hipStream_t st, int tile) {
+#ifdef BENCH_FAST
+  if (K % BK) return (int)hipErrorInvalidValue;
+#define HB_CASE(LA, LB, SA, SB)                                                                          \
+  if (tile == 1) return launch_big(LA<true>{a, lda, M, K, 0}, LB<true>{b, ldb, N, K, 0}, ep, M, N, K, 1, 1, st);     \
+  return (int)hipErrorInvalidValue;
+  if (a_kmaj && b_kmaj) { HB_CASE(BufK, BufK, 0, 0) }
+  if (a_kmaj) { HB_CASE(BufK, BufMN, 0, 0) }
+  if (b_kmaj) { HB_CASE(BufMN, BufK, 0, 0) }
+  HB_CASE(BufMN, BufMN, 0, 0)
+#else
+  return (K % BK == 0) ? launch_buf<true>(a, b, a_kmaj, b_kmaj, lda, ldb, 0, 0, ep, M, N, K, 1, 1, st, tile)
+                       : launch_buf<false>(a, b, a_kmaj, b_kmaj, lda, ldb, 0, 0, ep, M, N, K, 1, 1, st, tile);
+#endif
+}
 
 #define CK(x)                                                                          \
   do {                                                                                 \
@@ -124,18 +144,16 @@ int main(int argc, char** argv) {
     struct Var { std::string name; int tile; };
     std::vector<Var> vars = {{"blas", -1}};
     for (int t : {0, 1, 2}) {
+#ifdef BENCH_FAST
+      if (t == 0 || t == 2) continue;
+#endif
       if (only && !strchr(only, '0' + t)) continue;
       vars.push_back({"tile" + std::to_string(t), t});
     }
     auto run = [&](const Var& v) {
       if (v.tile < 0) { blas.run(A, B, C, st); return; }
       Epi ep{C, nullptr, nullptr, s.N, 0, 0, 0, 1.f, 0.f, 0, 0, 0, 0, 0, nullptr, 0, nullptr};
-      int rc = (s.K % BK == 0)
-                   ? launch_buf<true>((const bf16*)A, (const bf16*)B, !s.ta, s.tb, lda, ldb, 0, 0, ep, s.M, s.N, s.K,
-                                      1, 1, st, v.tile)
-                   : launch_buf<false>((const bf16*)A, (const bf16*)B, !s.ta, s.tb, lda, ldb, 0, 0, ep, s.M, s.N,
-                                       s.K, 1, 1, st, v.tile);
-      CK(rc);
+      CK(run_tile((const bf16*)A, (const bf16*)B, !s.ta, s.tb, lda, ldb, ep, s.M, s.N, s.K, st, v.tile));
     };
     std::vector<std::vector<float>> ms(vars.size());
     std::vector<float> errs(vars.size(), 0.f);

@@ -126,10 +126,17 @@ __device__ __forceinline__ int half_to_rel(int map, int h, int x) {
 // K-major: returns the operand row (relative to the tile) of the lane's 16-B chunk.
 __device__ __forceinline__ int kmaj_row(int map, int w, int i, int l) {
   if (map == 0) return 32 * w + 8 * i + (l >> 3);
+  if (map == 3) return 64 * w + 8 * i + (l >> 3);   // 256-row image, 4 waves x 8 loads
   return half_to_rel(map, i >> 1, 16 * w + 8 * (i & 1) + (l >> 3));
 }
 // MN-major: k row of the image and operand column (relative) of the lane's chunk.
 __device__ __forceinline__ void mn_slot(int map, int w, int i, int l, int& k, int& col) {
+  if (map == 3) {   // two 128-column images [64 k][128], waves 2h, 2h+1 fill half h
+    k = 32 * (w & 1) + 4 * i + (l >> 4);
+    const int c = (l & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3));
+    col = (w >> 1) * 128 + 8 * c;
+    return;
+  }
   k = map ? 8 * w + 4 * (i & 1) + (l >> 4) : 16 * w + 4 * i + (l >> 4);
   const int c = (l & 15) ^ (((k & 3) << 2) | ((k >> 2) & 3));  // T10 image, logical chunk
   col = map ? half_to_rel(map, i >> 1, 8 * c) : 8 * c;
@@ -193,18 +200,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
 }
 
-template <bool KF>
+template <bool KF, int NS = 4>
 struct BufK {
   HETU_LINEAR_ROWS
   static constexpr bool KMAJ = true, BUF = true;
+  static constexpr int SLOTS = NS;
   const bf16* base; int64_t ld, rows, K, bstride;
-  __amdgpu_buffer_rsrc_t rs; uint32_t vo[4], oob; int ch;
+  __amdgpu_buffer_rsrc_t rs; uint32_t vo[NS], oob; int ch;
   __device__ void init(int64_t r0, int w, int l, int64_t batch, int big) {
     oob = (uint32_t)(((rows - 1) * ld + K) * 2);
     rs = make_rsrc(base + batch * bstride, oob);
     ch = (l & 7) ^ (l >> 3);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NS; ++i) {
       const int64_t r = r0 + kmaj_row(big, w, i, l);
       vo[i] = r < rows ? (uint32_t)((r * ld + ch * 8) * 2) : oob;
     }
@@ -216,17 +224,18 @@ struct BufK {
   }
 };
 
-template <bool KF>
+template <bool KF, int NS = 4>
 struct BufMN {
   HETU_LINEAR_ROWS
   static constexpr bool KMAJ = false, BUF = true;
+  static constexpr int SLOTS = NS;
   const bf16* base; int64_t ld, rows, K, bstride;
-  __amdgpu_buffer_rsrc_t rs; uint32_t vo[4], oob; int kk[4];
+  __amdgpu_buffer_rsrc_t rs; uint32_t vo[NS], oob; int kk[NS];
   __device__ void init(int64_t r0, int w, int l, int64_t batch, int big) {
     oob = (uint32_t)(((K - 1) * ld + rows) * 2);
     rs = make_rsrc(base + batch * bstride, oob);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NS; ++i) {
       int c;
       mn_slot(big, w, i, l, kk[i], c);
       const int64_t col = r0 + c;
@@ -244,6 +253,10 @@ struct BufMN {
 // loader's per-lane pointer (implicit-GEMM convolution loaders)
 template <class L, class = void> struct is_buf : std::false_type {};
 template <class L> struct is_buf<L, std::void_t<decltype(L::BUF)>> : std::true_type {};
+
+// staging slots per wave a loader carries (the 4-wave 256-row kernel needs 8)
+template <class L, class = void> struct slots_of { static constexpr int value = 4; };
+template <class L> struct slots_of<L, std::void_t<decltype(L::SLOTS)>> { static constexpr int value = L::SLOTS; };
 
 template <class L>
 __device__ __forceinline__ void stage_dma(const L& l, int64_t k0, int i, char* dst) {

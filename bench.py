@@ -83,8 +83,9 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world > 1:
         import faulthandler
-        # a rank silent for 240 s prints all its threads' stacks (then keeps running)
-        faulthandler.dump_traceback_later(240, repeat=True, file=sys.stderr)
+        # a rank silent for HETU_STALL_DUMP_S (240) s prints all its threads' stacks (then keeps running)
+        faulthandler.dump_traceback_later(float(os.environ.get('HETU_STALL_DUMP_S', '240')), repeat=True,
+                                          file=sys.stderr)
     local = int(os.environ.get('LOCAL_RANK', '0'))
     server = start_ps_server(world, local) if args.model == 'wdl' else None
     import torch
@@ -160,8 +161,7 @@ def main():
     dt_s = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt_s], dtype=torch.float64, device=dev)
-        import torch.distributed as dist
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        C.world().all_reduce(t, 'max')
         dt_s = float(t.item())
     ms = dt_s * 1000.0 / args.steps
     if args.op_profile and args.model == 'resnet50' and rank == 0:

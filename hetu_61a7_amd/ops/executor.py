@@ -162,6 +162,7 @@ class HetuConfig(object):
         self.ps_comm = None
         self.comm = None
         self.extra = kwargs
+        self.grad_wire = kwargs.get('grad_wire')   # DP all-reduce wire format: 'fp32' | 'bf16'
 
         rank, world, local = dist_env()
         self.rank, self.nrank, self.local_rank = rank, world, local
@@ -221,8 +222,14 @@ class HetuConfig(object):
             torch.cuda.set_device(self.context.device_id)
 
         # ---- communicators ------------------------------------------------------------
+        # HETU_FORCE_DP=1: run the data-parallel gradient path (buckets, async all-reduce on
+        # the communicator's stream, bf16 wire) with a single rank -- the one-GPU rehearsal of
+        # the multi-GPU path on real RCCL (tests/test_rccl_gpu.py)
+        self.force_dp = os.environ.get('HETU_FORCE_DP', '0') == '1' and dist_strategy is not None
+        if self.force_dp and self.comm_mode is None:
+            self.comm_mode = 'AllReduce'
         if self.comm_mode in ('AllReduce', 'Hybrid') or pipeline is not None or world > 1:
-            if world > 1:
+            if world > 1 or self.force_dp:
                 from ..parallel import comm as C
                 self.comm = C.init_process_group(use_gpu=ndarray.is_gpu_ctx(self.context))
                 if self.spmd:

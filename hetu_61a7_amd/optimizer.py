@@ -268,7 +268,7 @@ class OptimizerOp(Op):
     def backward_hook(self, config):
         # data parallel wiring: AllReduce / Hybrid modes all-reduce dense grads
         self.config = config
-        if config.comm_mode in ('AllReduce', 'Hybrid') and config.nrank > 1:
+        if config.comm_mode in ('AllReduce', 'Hybrid') and (config.nrank > 1 or getattr(config, 'force_dp', False)):
             self.dp = True
             self.comm = config.comm
         self.bucket_bytes = int(getattr(config, 'bucket_mb', 32) * (1 << 20))

@@ -153,6 +153,7 @@ class Communicator(object):
             from . import rccl
             if rccl.available():
                 self.native = rccl.world_from_dist(self.group)
+        self.group_backend = dist.get_backend(self.group) if self.rank >= 0 else None
         self.backend = 'hetu-rccl' if self.native is not None else \
             (dist.get_backend(self.group) if self.rank >= 0 else 'non-member')
 
@@ -184,9 +185,21 @@ class Communicator(object):
             t.div_(self.nrank)
 
     # -- collectives ------------------------------------------------------------------
+    def _gloo_gpu(self, t) -> bool:
+        # gloo rehearsal of the GPU path (HETU_DIST_BACKEND=gloo, ranks sharing one GPU):
+        # device tensors are staged through host memory here, synchronously, instead of
+        # gloo's asynchronous CUDA-tensor work (four ranks on one GPU stalled inside it,
+        # every rank parked in work.wait() of the first step's buckets)
+        return t.is_cuda and self.group_backend == 'gloo'
+
     def all_reduce(self, t: torch.Tensor, op: str = 'sum', async_op: bool = False):
         if self.native is not None and t.is_cuda and t.is_contiguous():
             return self.native.all_reduce(t, op, async_op=async_op)
+        if self._gloo_gpu(t):
+            h = t.detach().to('cpu')
+            self.all_reduce(h, op)
+            t.copy_(h)
+            return _Done() if async_op else None
         if op == 'mean':
             w = dist.all_reduce(t, dist.ReduceOp.SUM, group=self.group, async_op=async_op)
             if async_op:
@@ -199,6 +212,11 @@ class Communicator(object):
         """out = concat over ranks along dim 0."""
         if self.native is not None and out.is_cuda and out.is_contiguous():
             return self.native.all_gather(out, inp, async_op=async_op)
+        if self._gloo_gpu(out):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            self.all_gather(h, inp.detach().to('cpu'))
+            out.copy_(h)
+            return _Done() if async_op else None
         return dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group, async_op=async_op)
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = 'sum', async_op: bool = False):
@@ -217,6 +235,11 @@ class Communicator(object):
     def broadcast(self, t: torch.Tensor, root: int = 0, async_op: bool = False):
         if self.native is not None and t.is_cuda and t.is_contiguous():
             return self.native.broadcast(t, root, async_op=async_op)
+        if self._gloo_gpu(t):
+            h = t.detach().to('cpu')
+            self.broadcast(h, root)
+            t.copy_(h)
+            return _Done() if async_op else None
         return dist.broadcast(t, self._g(root), group=self.group, async_op=async_op)
 
     def reduce(self, t: torch.Tensor, root: int = 0, op: str = 'sum', async_op: bool = False):

@@ -115,7 +115,8 @@ def record_native(name):
 
 
 def record_vendor(name):
-    """a GEMM / convolution served by the vendor library (hipBLASLt / MIOpen via torch)"""
+    """a GPU GEMM / convolution served by the vendor library (hipBLASLt / MIOpen via torch);
+    callers record device tensors only (the CPU reference path is not counted)"""
     VENDOR_CALLS[name] = VENDOR_CALLS.get(name, 0) + 1
 
 

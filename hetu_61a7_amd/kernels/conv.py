@@ -66,12 +66,14 @@ def _plain_1x1(ts, w_shape, stride, padding):
             all(t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous(memory_format=CL) for t in ts))
 
 
-def _pad_c(t):
-    """Zero-pad dim 1 (channels) of a channels-last bf16 tensor to a multiple of 8
-    so the implicit-GEMM kernels (16-byte channel chunks) accept it -- the
+def _pad_c(t, q=8):
+    """Zero-pad dim 1 (channels) of a channels-last tensor to a multiple of ``q`` (8
+    bf16 / 4 fp32: one 16-byte chunk) so the implicit-GEMM kernels accept it -- the
     3-channel ResNet stem."""
     n, c, h, w = t.shape
-    cp = -(-c // 8) * 8
+    cp = -(-c // q) * q
+    if cp == c:
+        return t.contiguous(memory_format=CL)
     buf = torch.zeros((n, h, w, cp), dtype=t.dtype, device=t.device)
     buf[..., :c].copy_(t.permute(0, 2, 3, 1))
     return buf.permute(0, 3, 1, 2)
@@ -156,11 +158,60 @@ def conv2d_with_stats(x, w, stride, padding):
     return r
 
 
+# ---- fp32 (the reference's only precision): exact-fp32 MFMA implicit GEMM -------------------
+# (gemm_f32.hip, v_mfma_f32_16x16x4_f32); channel counts padded to 4 with zeros where needed
+def _f32(*ts):
+    return all(t is not None and t.is_cuda and t.dtype == torch.float32 for t in ts)
+
+
+def _fwd_f32(x, w, b, stride, padding):
+    from . import conv_igemm
+    return conv_igemm.forward_f32(_pad_c(x, 4), _pad_c(w, 4), stride, padding, bias=b)
+
+
+def _dgrad_f32(g, w, x_shape, stride, padding, acc):
+    from . import conv_igemm
+    n, c, h, ww = x_shape
+    cp = -(-c // 4) * 4
+    g = g.contiguous(memory_format=CL)
+    if cp == c:
+        return conv_igemm.backward_data_f32(g, w.contiguous(memory_format=CL), x_shape, stride, padding, acc=acc)
+    d = conv_igemm.backward_data_f32(g, _pad_c(w, 4), (n, cp, h, ww), stride, padding)
+    if d is None:
+        return None
+    d = d[:, :c]
+    return d + acc if acc is not None else d.contiguous(memory_format=CL)
+
+
+def _wgrad_f32(g, x, w_shape, stride, padding, out):
+    from . import conv_igemm
+    co, c, kh, kw = w_shape
+    cp = -(-c // 4) * 4
+    g = g.contiguous(memory_format=CL)
+    if cp == c:
+        return conv_igemm.backward_filter_f32(g, x.contiguous(memory_format=CL), w_shape, stride, padding, out=out,
+                                              accumulate=False)
+    d = conv_igemm.backward_filter_f32(g, _pad_c(x, 4), (co, cp, kh, kw), stride, padding, accumulate=False)
+    if d is None:
+        return None
+    d = d[:, :c]
+    if out is not None:
+        out.copy_(d)
+        return out
+    return d.contiguous(memory_format=CL)
+
+
 def conv2d(x, w, b, stride, padding):
     x, w = _match(x, w)
     from . import cpu_native
     if cpu_native.active(x, w, b) and x.dim() == 4:
         return cpu_native.conv2d(x, w, b, stride, padding)
+    if _f32(x, w) and MODE != 'vendor':
+        x = x.contiguous(memory_format=CL)
+        w = w.contiguous(memory_format=CL)
+        return _pick(('fwd32', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding), b is not None),
+                     lambda: _fwd_f32(x, w, b, stride, padding),
+                     lambda: F.conv2d(x, w, b.to(x.dtype) if b is not None else None, stride, padding))
     if x.is_cuda:
         x = x.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
@@ -204,6 +255,12 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     if cpu_native.active(g, w, acc):
         dx = cpu_native.conv2d_backward_data(g, w, x_shape, stride, padding)
         return dx + acc.float() if acc is not None else dx
+    if _f32(g, w) and MODE != 'vendor' and (acc is None or acc.dtype == torch.float32):
+        acc32 = acc.contiguous(memory_format=CL) if acc is not None else None
+        return _pick(('dgrad32', tuple(g.shape), tuple(w.shape), tuple(x_shape), tuple(stride), tuple(padding),
+                      acc is not None),
+                     lambda: _dgrad_f32(g, w, x_shape, stride, padding, acc32),
+                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc))
     if g.is_cuda:
         g = g.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
@@ -292,6 +349,16 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             out.copy_(dw)
             return out
         return dw
+    if _f32(g, x) and MODE != 'vendor':
+        def vendor32():
+            dw = _vendor_wgrad(g, x, w_shape, stride, padding)
+            if out is None:
+                return dw
+            out.copy_(dw)
+            return out
+        # both candidates overwrite ``out`` (no accumulation): timing repeats are harmless
+        return _pick(('wgrad32', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
+                     lambda: _wgrad_f32(g, x, w_shape, stride, padding, out), vendor32)
     if g.is_cuda:
         g = g.contiguous(memory_format=CL)
         x = x.contiguous(memory_format=CL)

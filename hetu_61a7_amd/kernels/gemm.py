@@ -89,7 +89,8 @@ def _as_dtype(t, dt):
 
 
 def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
-    record_vendor('gemm')
+    if a.is_cuda:
+        record_vendor('gemm')
     A, B = _tr(a, ta), _tr(b, tb)
     if fuse_bias and bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
         y = torch.addmm(_as_dtype(bias, A.dtype), A, B)     # bias in the hipBLASLt epilogue
@@ -109,7 +110,7 @@ def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
 
 def bmm(a, b, ta=False, tb=False):
     a, b = _match(a, b)
-    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16:
+    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype in (torch.bfloat16, torch.float32):
         from . import gemm_mfma
         from .autotune import choose
         key = ('bmm', _sig(a), _sig(b), ta, tb)
@@ -119,7 +120,8 @@ def bmm(a, b, ta=False, tb=False):
             if y is not None:
                 return y
             _fallback('bmm')
-    record_vendor('bmm')
+    if a.is_cuda:
+        record_vendor('bmm')
     return torch.matmul(_tr(a, ta), _tr(b, tb))
 
 
@@ -250,7 +252,8 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
             _fallback('matmul_acc')
         record_vendor('gemm')
         return vendor()
-    record_vendor('gemm')
+    if A.is_cuda:
+        record_vendor('gemm')
     if A.dim() == 2 and acc.dim() == 2 and acc.dtype == A.dtype:
         return torch.addmm(acc, A, B)
     y = torch.matmul(A, B)

@@ -1,7 +1,12 @@
 """CPU-vs-GPU differential tests over the operator library (reference
 tests/tester.py:5-25 ``HetuTester`` + tests/test_ops.py): every op is built on a
 CPU executor and on a GPU executor (fp32, HIP kernels) with identical inputs,
-and the outputs and the gradients wrt every float input are compared."""
+and the outputs and the gradients wrt every float input are compared.
+
+The GEMM and convolution cases run with the hand-written kernels forced
+(``HETU_GEMM=hip`` / ``HETU_CONV=hip`` semantics: the exact-fp32 MFMA GEMM and
+implicit-GEMM convolution of gemm_f32.hip) and assert that those kernels ran and
+nothing fell back to hipBLASLt / MIOpen."""
 import numpy as np
 import pytest
 
@@ -90,10 +95,39 @@ INT_INPUTS = {'embedding': (1,), 'one_hot': (0,)}
 NO_GRAD = {'one_hot', 'where'}
 
 
+# cases whose GPU run must use the hand-written fp32 MFMA kernels: native-call names expected
+HIP_GEMM_CONV = {
+    'matmul': ('gemm_f32',), 'matmul_tt': ('gemm_f32',), 'linear_relu': ('gemm_f32',),
+    'batch_matmul': ('gemm_f32',),
+    'conv2d': ('conv_fwd_f32', 'conv_dgrad_f32', 'conv_wgrad_f32'),
+    'conv2d_s2': ('conv_fwd_f32', 'conv_dgrad_f32', 'conv_wgrad_f32'),
+    'conv_bias': ('conv_fwd_f32', 'conv_dgrad_f32', 'conv_wgrad_f32'),
+}
+
+
+@pytest.fixture
+def force_hip(monkeypatch):
+    from hetu_61a7_amd import kernels as K
+    from hetu_61a7_amd.kernels import gemm, gemm_mfma, conv, conv_igemm, autotune
+    monkeypatch.setattr(gemm, '_MFMA', 'hip')
+    monkeypatch.setattr(gemm_mfma, 'MODE', 'hip')
+    monkeypatch.setattr(conv, 'MODE', 'hip')
+    monkeypatch.setattr(conv_igemm, 'MODE', 'hip')
+    monkeypatch.setattr(autotune, '_decisions', {})
+    K.reset_dispatch_stats()
+    return K
+
+
 @pytest.mark.parametrize('name', sorted(CASES))
-def test_cpu_gpu_differential(name):
+def test_cpu_gpu_differential(name, force_hip):
     builder, shapes = CASES[name]
     if not all(hasattr(ht, n) for n in ('bool_op',)) and name == 'where':
         pytest.skip('bool_op missing')
     HetuTester(builder, shapes, int_inputs=INT_INPUTS.get(name, ()), grad=name not in NO_GRAD,
                rtol=2e-4, atol=2e-5).check()
+    K = force_hip
+    for k in HIP_GEMM_CONV.get(name, ()):
+        assert K.NATIVE_CALLS.get(k, 0) >= 1, (name, k, K.NATIVE_CALLS, K.VENDOR_CALLS)
+    if name in HIP_GEMM_CONV:
+        assert not K.FALLBACKS, (name, K.FALLBACKS)
+        assert not {k: v for k, v in K.VENDOR_CALLS.items() if k in ('gemm', 'bmm', 'conv')}, K.VENDOR_CALLS

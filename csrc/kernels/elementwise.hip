@@ -161,6 +161,32 @@ __global__ void __launch_bounds__(256) binary_k(const T* __restrict__ a, const T
   }
 }
 
+// General broadcast / strided binary op (the long tail the fast path above does not
+// take: middle-dim broadcasts, non-contiguous views): the output is contiguous in
+// `shape` (up to 8 dims); a and b are read through element strides (0 on broadcast dims).
+struct NdGeom {
+  int nd;
+  int64_t shape[8], as[8], bs[8];
+};
+
+template <typename T, typename TB, int OP>
+__global__ void __launch_bounds__(256) binary_nd_k(const T* __restrict__ a, const TB* __restrict__ b,
+                                                    T* __restrict__ y, int64_t n, NdGeom g, float c) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i, oa = 0, ob = 0;
+#pragma unroll
+    for (int d = 7; d >= 0; --d) {
+      if (d < g.nd) {
+        const int64_t q = r / g.shape[d], k = r - q * g.shape[d];
+        oa += k * g.as[d];
+        ob += k * g.bs[d];
+        r = q;
+      }
+    }
+    y[i] = from_f<T>(bi<OP>(to_f(a[oa]), to_f(b[ob]), c));
+  }
+}
+
 template <typename TI, typename TO>
 __global__ void cast_k(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -223,6 +249,49 @@ HETU_API int hetu_binary(int op, const void* a, const void* b, void* y, int64_t 
     BCASE(B_RELU_GRAD) BCASE(B_GELU_GRAD) BCASE(B_TANH_GRAD) BCASE(B_SIGMOID_GRAD)
     BCASE(B_LEAKY_RELU_GRAD) BCASE(B_ABS_GRAD) BCASE(B_POW) BCASE(B_ADD_RELU) BCASE(B_LOG_GRAD)
     BCASE(B_SQRT_GRAD) BCASE(B_GELU_TANH_GRAD)
+    default: return (int)hipErrorInvalidValue;
+  }
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+#define BNDCASE(OPV)                                                                            \
+  case OPV:                                                                                     \
+    if (is_bf16 && b_bf16)                                                                      \
+      hipLaunchKernelGGL((binary_nd_k<bf16, bf16, OPV>), dim3(grid), dim3(256), 0, st,          \
+                         (const bf16*)a, (const bf16*)b, (bf16*)y, n, g, c);                    \
+    else if (is_bf16)                                                                           \
+      hipLaunchKernelGGL((binary_nd_k<bf16, float, OPV>), dim3(grid), dim3(256), 0, st,         \
+                         (const bf16*)a, (const float*)b, (bf16*)y, n, g, c);                   \
+    else if (b_bf16)                                                                            \
+      hipLaunchKernelGGL((binary_nd_k<float, bf16, OPV>), dim3(grid), dim3(256), 0, st,         \
+                         (const float*)a, (const bf16*)b, (float*)y, n, g, c);                  \
+    else                                                                                        \
+      hipLaunchKernelGGL((binary_nd_k<float, float, OPV>), dim3(grid), dim3(256), 0, st,        \
+                         (const float*)a, (const float*)b, (float*)y, n, g, c);                 \
+    break;
+
+// y (contiguous, shape[0..nd)) = op(a, b) with a / b read through element strides
+HETU_API int hetu_binary_nd(int op, const void* a, const void* b, void* y, int nd, const int64_t* shape,
+                            const int64_t* astride, const int64_t* bstride, int is_bf16, int b_bf16, float c,
+                            hipStream_t st) {
+  if (nd < 1 || nd > 8) return (int)hipErrorInvalidValue;
+  NdGeom g;
+  g.nd = nd;
+  int64_t n = 1;
+  for (int d = 0; d < 8; ++d) {
+    g.shape[d] = d < nd ? shape[d] : 1;
+    g.as[d] = d < nd ? astride[d] : 0;
+    g.bs[d] = d < nd ? bstride[d] : 0;
+    if (d < nd) n *= shape[d];
+  }
+  if (n <= 0) return 0;
+  int grid = stream_grid(n, 256, 1);
+  switch (op) {
+    BNDCASE(B_ADD) BNDCASE(B_SUB) BNDCASE(B_MUL) BNDCASE(B_DIV) BNDCASE(B_MAX) BNDCASE(B_MIN)
+    BNDCASE(B_RELU_GRAD) BNDCASE(B_GELU_GRAD) BNDCASE(B_TANH_GRAD) BNDCASE(B_SIGMOID_GRAD)
+    BNDCASE(B_LEAKY_RELU_GRAD) BNDCASE(B_ABS_GRAD) BNDCASE(B_POW) BNDCASE(B_ADD_RELU) BNDCASE(B_LOG_GRAD)
+    BNDCASE(B_SQRT_GRAD) BNDCASE(B_GELU_TANH_GRAD)
     default: return (int)hipErrorInvalidValue;
   }
   HETU_LAUNCH_CHECK();

@@ -3,6 +3,8 @@ from __future__ import annotations
 
 import math
 
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
@@ -151,6 +153,16 @@ def binary(op: str, a: torch.Tensor, b: torch.Tensor, c: float = 0.0, out=None) 
             check(f(B[op], a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), is_bf16(a),
                     is_bf16(b), mode, inner, float(c), stream_ptr()), 'binary:' + op)
             return y
+        r = _binary_nd(op, a, b, c, out)
+        if r is not None:
+            return r
+    elif native(a, b) and supported_float(a) and supported_float(b) and b.device == a.device:
+        r = _binary_nd(op, a, b, c, out)
+        if r is not None:
+            return r
+    if native(a, b):
+        from . import record_fallback
+        record_fallback('binary:' + op, 'dtype %s/%s' % (a.dtype, b.dtype))
     if b.dtype != a.dtype and b.numel() <= a.numel():
         b = b.to(a.dtype)
     from . import cpu_native
@@ -163,6 +175,30 @@ def binary(op: str, a: torch.Tensor, b: torch.Tensor, c: float = 0.0, out=None) 
         out.copy_(r)
         return out
     return r
+
+
+def _binary_nd(op, a, b, c, out):
+    """General broadcast / strided form (``hetu_binary_nd``): the output takes the
+    broadcast shape of a and b in a's dtype; None when it needs more than 8 dims."""
+    try:
+        shape = torch.broadcast_shapes(a.shape, b.shape)
+    except RuntimeError:
+        return None
+    if len(shape) > 8:
+        return None
+    if len(shape) == 0:
+        shape = (1,)
+        a, b = a.reshape(1), b.reshape(1)
+    ae, be = a.expand(shape), b.expand(shape)
+    if out is not None and (tuple(out.shape) != tuple(shape) or not out.is_contiguous() or out.dtype != a.dtype):
+        return None
+    y = out if out is not None else torch.empty(shape, dtype=a.dtype, device=a.device)
+    nd = len(shape)
+    arr = ctypes.c_int64 * nd
+    f = fn('hetu_binary_nd', [I32, P, P, P, I32, P, P, P, I32, I32, F32, P])
+    check(f(B[op], a.data_ptr(), b.data_ptr(), y.data_ptr(), nd, arr(*shape), arr(*ae.stride()), arr(*be.stride()),
+            is_bf16(a), is_bf16(b), float(c), stream_ptr()), 'binary_nd:' + op)
+    return y
 
 
 def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

@@ -1,0 +1,97 @@
+"""Which GPU kernels of one steady-state training step are not hand-written?
+
+Runs a few steps of a bench model, profiles the last one with torch.profiler
+(kineto/roctracer) and prints every device kernel that is neither a ``hetu::``
+kernel nor a vendor GEMM/convolution library kernel, with the Python frame of
+the graph op that launched it (the executor op's ``compute``).
+
+    python scripts/find_torch_kernels.py --model resnet50 --batch 32
+"""
+import argparse
+import collections
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+VENDOR = ('Cijk', 'igemm', 'ck::', 'SubTensorOp', 'naive_conv', 'MIOpen', 'miopen', '__amd_rocclr', 'Custom_Cijk',
+          'gridwise', 'kernel_batched_gemm', 'kernel_gemm')
+
+
+def classify(name):
+    if 'hetu' in name:
+        return 'hetu'
+    if any(v in name for v in VENDOR):
+        return 'vendor'
+    return 'other'
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument('--model', default='resnet50', choices=['resnet50', 'bert', 'moe', 'wdl'])
+    p.add_argument('--batch', type=int, default=None)
+    p.add_argument('--steps', type=int, default=3)
+    a = p.parse_args()
+    import torch
+    from torch.profiler import profile, ProfilerActivity
+    sys.argv = ['bench.py', '--model', a.model, '--steps', '1', '--warmup', '0'] + \
+        (['--batch', str(a.batch)] if a.batch else [])
+    import bench
+    args = bench.parse()
+    import hetu_61a7_amd as ht  # noqa: F401
+    step = _build(args)
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA, ProfilerActivity.CPU], with_stack=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    counts = collections.Counter()
+    where = collections.defaultdict(collections.Counter)
+    for e in prof.events():
+        if e.device_type.name != 'CUDA' and getattr(e, 'device_type', None) is not None and \
+                str(e.device_type) != 'DeviceType.CUDA':
+            continue
+        cls = classify(e.name)
+        counts[cls] += 1
+        if cls == 'other':
+            frames = []
+            ev = e.cpu_parent if hasattr(e, 'cpu_parent') else None
+            while ev is not None and len(frames) < 1:
+                st = [s for s in (ev.stack or []) if 'hetu_61a7_amd' in s]
+                if st:
+                    frames.append(st[0])
+                ev = ev.cpu_parent
+            where[e.name[:110]][frames[0] if frames else '?'] += 1
+    print('kernel classes in one step:', dict(counts))
+    for name, fr in sorted(where.items(), key=lambda kv: -sum(kv[1].values())):
+        print('%4d  %s' % (sum(fr.values()), name))
+        for f, n in fr.most_common(4):
+            print('        %3d  %s' % (n, f))
+
+
+def _build(args):
+    import torch
+    import hetu_61a7_amd as ht
+    if args.model == 'resnet50':
+        from hetu_61a7_amd.models import resnet50_imagenet
+        B = args.batch or 32
+        x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+        loss, _ = resnet50_imagenet(x, y_, 1000)
+        train = ht.optim.MomentumOptimizer(learning_rate=0.1, momentum=0.9).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=1)
+        X = torch.randn((B, 3, 224, 224), device='cuda').bfloat16().contiguous(memory_format=torch.channels_last)
+        Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda'), 1000).bfloat16()
+        return lambda: ex.run('train', feed_dict={x: X, y_: Y})
+    if args.model == 'bert':
+        from hetu_61a7_amd.models.bert import bert_bench
+        return bert_bench(args, 1, 0, 0)[0]
+    if args.model == 'moe':
+        from hetu_61a7_amd.models.moe import moe_top_bench
+        return moe_top_bench(args, 1, 0, 0)[0]
+    from hetu_61a7_amd.models.ctr import wdl_criteo_bench
+    return wdl_criteo_bench(args, 1, 0, 0)[0]
+
+
+if __name__ == '__main__':
+    main()

@@ -113,3 +113,29 @@ def test_losses_match_torch():
     ref_n = torch.zeros(rows, cols)
     ref_n[torch.arange(rows), t.clamp_min(0).cpu()] = -0.7 / rows
     _close(KT.nll_grad(gs, t.clamp_min(0), cols).cpu(), ref_n, 1e-6)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_binary_general_broadcast_and_strided(dt):
+    """middle-dim broadcasts, b with more dims than a, and non-contiguous views take the
+    N-d strided kernel (hetu_binary_nd) instead of falling back to torch"""
+    from hetu_61a7_amd.kernels import elementwise as KE
+    g = torch.Generator(device='cuda')
+    g.manual_seed(1)
+    a = torch.randn(4, 6, 5, 7, device='cuda', generator=g).to(dt)
+    cases = [
+        ('add', a, torch.randn(1, 6, 1, 1, device='cuda', generator=g).to(dt)),      # per-channel (NCHW)
+        ('mul', a, torch.randn(4, 1, 5, 1, device='cuda', generator=g).to(dt)),
+        ('sub', a.permute(0, 2, 1, 3), torch.randn(7, device='cuda', generator=g).to(dt)),  # strided a
+        ('max', torch.randn(5, 7, device='cuda', generator=g).to(dt), a),               # b has more dims
+        ('relu_grad', a[:, ::2], torch.randn(4, 3, 5, 7, device='cuda', generator=g).to(dt)),
+        ('div', a, torch.rand(6, 1, 7, device='cuda', generator=g).float() + 0.5),       # fp32 b
+    ]
+    ref = {'add': torch.add, 'mul': torch.mul, 'sub': torch.sub, 'max': torch.maximum, 'div': torch.div,
+           'relu_grad': lambda x, y: torch.where(x > 0, y, torch.zeros_like(y))}
+    for op, x, y in cases:
+        out = KE.binary(op, x, y)
+        want = ref[op](x.float(), y.float())
+        assert out.shape == want.shape, (op, out.shape, want.shape)
+        tol = 1e-6 if dt == torch.float32 else 2e-2
+        torch.testing.assert_close(out.float(), want, rtol=tol, atol=tol)

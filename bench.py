@@ -77,7 +77,10 @@ _T0 = time.perf_counter()
 
 def main():
     args = parse()
-    if args.comm_trace:
+    if args.comm_trace or int(os.environ.get('WORLD_SIZE', '1')) > 1:
+        # multi-GPU runs always report the last step's bucket timeline (launch / done
+        # relative to the end of the backward pass): the overlap is visible in the JSON
+        args.comm_trace = True
         os.environ['HETU_COMM_TRACE'] = '1'
     os.environ['HETU_GRAD_WIRE'] = args.grad_wire
     world = int(os.environ.get('WORLD_SIZE', '1'))

@@ -130,6 +130,59 @@ static inline int rows_blocks(int64_t n) {
   return (int)b;
 }
 
+// ---- sync-free dedup of a small table's row gradients (BERT position / token-type
+// embeddings): rows scattered into K private replicas (row r -> replica r % K) with a
+// hit mark per destination, then the replicas summed and ids[r] = r or -1 (untouched).
+// Three launches, nothing depends on the number of distinct ids (no host sync).
+template <typename T>
+__global__ void __launch_bounds__(256) dedup_scatter_k(float* __restrict__ scratch, int* __restrict__ hit,
+                                                        const int64_t* __restrict__ ids, const T* __restrict__ src,
+                                                        int64_t n, int64_t dim, int64_t nrows, int K) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (int64_t)gridDim.x * 4) {
+    const int64_t id = ids[r];
+    if (id < 0 || id >= nrows) continue;
+    if (lane == 0) hit[id] = 1;
+    float* d = scratch + ((r % K) * nrows + id) * dim;
+    for (int64_t j = lane; j < dim; j += 64) atomicAdd(d + j, to_f(src[r * dim + j]));
+  }
+}
+
+__global__ void __launch_bounds__(256) dedup_reduce_k(const float* __restrict__ scratch, const int* __restrict__ hit,
+                                                       float* __restrict__ merged, int64_t* __restrict__ out_ids,
+                                                       int64_t nrows, int64_t dim, int K) {
+  const int64_t total = nrows * dim;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += scratch[k * total + i];
+    merged[i] = s;
+    const int64_t row = i / dim;
+    if (i - row * dim == 0) out_ids[row] = hit[row] ? row : -1;
+  }
+}
+
+// scratch: K*nrows*dim fp32 and hit: nrows int32, both zeroed by the caller (hetu_fill)
+HETU_API int hetu_dedup_rows_dense(const int64_t* ids, const void* src, int src_bf16, int64_t n, int64_t dim,
+                                   int64_t nrows, int K, float* scratch, int* hit, float* merged, int64_t* out_ids,
+                                   hipStream_t st) {
+  if (K < 1) K = 1;
+  if (n > 0) {
+    if (src_bf16)
+      hipLaunchKernelGGL(dedup_scatter_k<bf16>, dim3(rows_blocks(n)), dim3(256), 0, st, scratch, hit, ids,
+                         (const bf16*)src, n, dim, nrows, K);
+    else
+      hipLaunchKernelGGL(dedup_scatter_k<float>, dim3(rows_blocks(n)), dim3(256), 0, st, scratch, hit, ids,
+                         (const float*)src, n, dim, nrows, K);
+  }
+  const int64_t total = nrows * dim;
+  int64_t nb = (total + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(dedup_reduce_k, dim3((unsigned)nb), dim3(256), 0, st, scratch, hit, merged, out_ids, nrows, dim, K);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
 HETU_API int hetu_gather_rows(const void* table, const int64_t* ids, void* out, int64_t n,
                               int64_t dim, int64_t nrows, int is_bf16, hipStream_t st) {
   if (n <= 0) return 0;

@@ -58,16 +58,24 @@ def _mask_f32(mask):
     if mask.dtype == torch.float32 and mask.is_contiguous():
         return mask
     if mask.is_cuda and torch.cuda.is_current_stream_capturing():
-        return mask.float().contiguous()
+        return _f32(mask)
     root = mask._base if mask._base is not None else mask     # ops hand in fresh views of it
     sig = (mask.data_ptr(), tuple(mask.shape), mask.stride(), mask._version)
     ent = _mask_memo.get(id(root))
     if ent is not None and ent[0]() is root and ent[1] == sig:
         return ent[2]
-    m = mask.float().contiguous()
+    m = _f32(mask)
     _mask_memo.clear()
     _mask_memo[id(root)] = (weakref.ref(root), sig, m)
     return m
+
+
+def _f32(t):
+    """contiguous fp32 copy of a device tensor on the native cast / copy kernels"""
+    if not t.is_cuda:
+        return t.float().contiguous()
+    from .tensor import copy_into
+    return copy_into(torch.empty(t.shape, dtype=torch.float32, device=t.device), t)
 
 
 def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
@@ -98,7 +106,9 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
     D = H // NH
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if fused_ok(qkv, S, D) and saved.dim() == 1:
-        dout = dout.to(qkv.dtype).contiguous()
+        if dout.dtype != qkv.dtype or not dout.is_contiguous():
+            from .tensor import copy_into
+            dout = copy_into(torch.empty(dout.shape, dtype=qkv.dtype, device=dout.device), dout)
         dqkv = torch.empty_like(qkv)
         m = _mask_f32(mask)
         f = fn('hetu_attn_bwd', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,

@@ -58,6 +58,26 @@ def _fallback(name):
         record_fallback('conv_' + name)
 
 
+def _zeros(shape, device, dtype=torch.float32):
+    from .tensor import zeros
+    return zeros(shape, dtype, device)
+
+
+def _copy_into(dst, src):
+    from .tensor import copy_into
+    return copy_into(dst, src)
+
+
+def _add_cl(a, b):
+    """a + b for 4-D activations on the native elementwise kernels, channels-last out
+    (the NHWC views are dense, so the vector path runs; strided b takes the N-d kernel)"""
+    from .elementwise import binary
+    if a.dim() == 4 and b.dim() == 4:
+        y = binary('add', a.contiguous(memory_format=CL).permute(0, 2, 3, 1), b.permute(0, 2, 3, 1))
+        return y.permute(0, 3, 1, 2)
+    return binary('add', a, b)
+
+
 def _plain_1x1(ts, w_shape, stride, padding):
     """1x1 / stride 1 / no padding on channels-last bf16 tensors ``ts``: the
     convolution is a plain GEMM over [pixels, channels] views (no copies)."""
@@ -74,8 +94,8 @@ def _pad_c(t, q=8):
     cp = -(-c // q) * q
     if cp == c:
         return t.contiguous(memory_format=CL)
-    buf = torch.zeros((n, h, w, cp), dtype=t.dtype, device=t.device)
-    buf[..., :c].copy_(t.permute(0, 2, 3, 1))
+    buf = _zeros((n, h, w, cp), t.device, t.dtype)
+    _copy_into(buf[..., :c], t.permute(0, 2, 3, 1))
     return buf.permute(0, 3, 1, 2)
 
 
@@ -116,7 +136,7 @@ def conv2d_with_stats(x, w, stride, padding):
 
     def fused(run):
         def f():
-            s = torch.zeros(2 * co, dtype=torch.float32, device=x.device)
+            s = _zeros(2 * co, x.device)
             y = run(s)
             return None if y is None else (y, s)
         return f
@@ -180,7 +200,9 @@ def _dgrad_f32(g, w, x_shape, stride, padding, acc):
     if d is None:
         return None
     d = d[:, :c]
-    return d + acc if acc is not None else d.contiguous(memory_format=CL)
+    if acc is not None:
+        return _add_cl(acc, d)
+    return d.contiguous(memory_format=CL)
 
 
 def _wgrad_f32(g, x, w_shape, stride, padding, out):
@@ -196,7 +218,7 @@ def _wgrad_f32(g, x, w_shape, stride, padding, out):
         return None
     d = d[:, :c]
     if out is not None:
-        out.copy_(d)
+        _copy_into(out, d)
         return out
     return d.contiguous(memory_format=CL)
 
@@ -320,7 +342,7 @@ def _layout_of(t):
 def _vendor_dgrad(g, w, x_shape, stride, padding, acc=None):
     dx = _vendor_dgrad0(g, w, x_shape, stride, padding)
     if acc is not None:
-        dx = dx + acc.to(dx.dtype)
+        dx = _add_cl(dx, acc)
     return dx
 
 
@@ -346,7 +368,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
     if cpu_native.active(g, x):
         dw = cpu_native.conv2d_backward_filter(g, x, w_shape, stride, padding)
         if out is not None:
-            out.copy_(dw)
+            _copy_into(out, dw)
             return out
         return dw
     if _f32(g, x) and MODE != 'vendor':
@@ -354,7 +376,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             dw = _vendor_wgrad(g, x, w_shape, stride, padding)
             if out is None:
                 return dw
-            out.copy_(dw)
+            _copy_into(out, dw)
             return out
         # both candidates overwrite ``out`` (no accumulation): timing repeats are harmless
         return _pick(('wgrad32', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
@@ -368,7 +390,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             dw = _vendor_wgrad(g, x, w_shape, stride, padding)
             if out is None:
                 return dw
-            out.copy_(dw)
+            _copy_into(out, dw)
             return out
         blas = None
         if _plain_1x1((g, x), w_shape, stride, padding):
@@ -400,7 +422,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                     return None
                 if out is None:
                     return d[:, :ci]
-                out.copy_(d[:, :ci])
+                _copy_into(out, d[:, :ci])
                 return out
             blas = {'hip_pad': pad_wgrad}
         if w_shape[0] >= 128:
@@ -413,7 +435,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                      vendor, blas)
     dw = _vendor_wgrad(g, x, w_shape, stride, padding)
     if out is not None:
-        out.copy_(dw)
+        _copy_into(out, dw)
         return out
     return dw
 

@@ -183,9 +183,8 @@ def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=Non
     Nc = KH * KW * C
     sk = _splitk(K, Nc, N * OH * OW, tile)
     ws = torch.empty(sk * K * Nc, dtype=torch.float32, device=g.device) if sk > 1 else None
-    if sk == 1 and not accumulate:
-        dw.zero_()
-        accumulate = True  # single slice accumulates straight into dw
+    # a single slice without accumulation stores straight into dw (plain fp32 epilogue,
+    # no zero fill + atomics)
     f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, I32, P, I32, P])
     check(f(g.data_ptr(), x.data_ptr(), dw.data_ptr(), N, H, W, C, K, KH, KW, stride[0], stride[1],
             padding[0], padding[1], sk, int(accumulate), ws.data_ptr() if ws is not None else None,

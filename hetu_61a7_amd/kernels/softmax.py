@@ -57,20 +57,31 @@ def softmax_ce(logits: torch.Tensor, labels: torch.Tensor):
     return loss, lse
 
 
+def _grad_rows(grad):
+    """(g, is_scalar): a per-row loss gradient, or one value broadcast to every row
+    (a reduce-mean gradient arrives as an expanded view with all strides 0: its first
+    element is read in place, no materialising copy)"""
+    if grad.numel() == 1 or (grad.dim() > 0 and all(st == 0 for st in grad.stride())):
+        return grad.as_strided((1,), (1,)), True
+    return grad.contiguous(), False
+
+
 def softmax_ce_backward(logits, labels, grad, lse=None):
     """d logits = grad[r] * (softmax(x)*sum(y) - y); ``grad`` per row or scalar."""
-    grad = grad.float()
+    if grad.dtype != torch.float32:
+        grad = grad.float()
     if native(logits) and supported_float(logits) and supported_float(labels):
         x = logits.contiguous()
         lab = labels.contiguous()
-        g = grad.contiguous()
+        g, scalar = _grad_rows(grad)
         R, N = x.numel() // x.shape[-1], x.shape[-1]
         dx = torch.empty_like(x)
         f = fn('hetu_softmax_ce_bwd', [P, P, P, I32, P, P, I64, I32, I32, I32, P])
-        check(f(x.data_ptr(), lab.data_ptr(), g.data_ptr(), int(g.numel() == 1),
+        check(f(x.data_ptr(), lab.data_ptr(), g.data_ptr(), int(scalar),
                 lse.contiguous().data_ptr() if lse is not None else None, dx.data_ptr(), R, N,
                 is_bf16(x), is_bf16(lab), stream_ptr()), 'softmax_ce_bwd')
         return dx
+    grad = grad.float()
     from . import cpu_native
     if cpu_native.active(logits) and logits.dim() == 2 and lse is not None:
         return cpu_native.softmax_ce_backward(logits, labels, grad, lse)
@@ -104,17 +115,19 @@ def softmax_ce_sparse(logits, labels, ignored_index=-1):
 
 def softmax_ce_sparse_backward(logits, labels, grad, lse=None, ignored_index=-1):
     lab = labels.reshape(-1).long()
-    grad = grad.float()
+    if grad.dtype != torch.float32:
+        grad = grad.float()
     if native(logits) and supported_float(logits):
         x = logits.contiguous()
         R, N = x.numel() // x.shape[-1], x.shape[-1]
         dx = torch.empty_like(x)
-        g = grad.contiguous()
+        g, scalar = _grad_rows(grad)
         f = fn('hetu_softmax_ce_sparse_bwd', [P, P, P, I32, P, P, I64, I32, I32, I64, P])
-        check(f(x.data_ptr(), lab.contiguous().data_ptr(), g.data_ptr(), int(g.numel() == 1),
+        check(f(x.data_ptr(), lab.contiguous().data_ptr(), g.data_ptr(), int(scalar),
                 lse.contiguous().data_ptr() if lse is not None else None, dx.data_ptr(), R, N,
                 is_bf16(x), int(ignored_index), stream_ptr()), 'softmax_ce_sparse_bwd')
         return dx
+    grad = grad.float()
     xf = _rows(logits.float())
     sm = torch.softmax(xf, -1)
     valid = (lab != ignored_index) & (lab >= 0) & (lab < xf.shape[-1])

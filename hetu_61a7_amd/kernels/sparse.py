@@ -87,9 +87,23 @@ def dedup_rows_dense(idx: torch.Tensor, vals: torch.Tensor, nrows: int):
     replicas as in ``dedup_rows``; out-of-range ids are dropped."""
     n, dim = idx.numel(), vals.shape[-1]
     idx = idx.reshape(-1).long()
-    valid = (idx >= 0) & (idx < nrows)
     from . import deterministic
     K = 1 if deterministic() else max(1, min(64, n // max(nrows * 16, 1)))
+    v2 = vals.reshape(n, dim)
+    if native(vals) and supported_float(v2) and v2.is_contiguous() and not deterministic():
+        from .tensor import zeros
+        idx = idx.contiguous()
+        scratch = zeros((K * nrows * dim,), torch.float32, vals.device)
+        hit = zeros((nrows,), torch.int32, vals.device)
+        merged = torch.empty((nrows, dim), dtype=torch.float32, device=vals.device)
+        ids = torch.empty((nrows,), dtype=torch.int64, device=vals.device)
+        f = fn('hetu_dedup_rows_dense', [P, P, I32, I64, I64, I64, I32, P, P, P, P, P])
+        check(f(idx.data_ptr(), v2.data_ptr(), is_bf16(v2), n, dim, nrows, K, scratch.data_ptr(), hit.data_ptr(),
+                merged.data_ptr(), ids.data_ptr(), stream_ptr()), 'dedup_rows_dense')
+        from . import record_native
+        record_native('dedup_rows_dense')
+        return ids, merged
+    valid = (idx >= 0) & (idx < nrows)
     tgt = idx if K == 1 else idx + (torch.arange(n, device=idx.device) % K) * nrows
     tgt = torch.where(valid, tgt, torch.full_like(tgt, -1))
     scratch = torch.zeros((K * nrows, dim), dtype=torch.float32, device=vals.device)

@@ -74,6 +74,43 @@ def fill_(t, value):
     return t
 
 
+def zeros(shape, dtype=torch.float32, device='cuda'):
+    """zero-filled device tensor by the native fill kernel (no torch fill launch)"""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if t.is_cuda and t.numel():
+        f = fn('hetu_fill', [P, I32, I64, ctypes.c_uint64, P])
+        check(f(t.data_ptr(), _ELEM[t.dtype], t.numel(), 0, stream_ptr()), 'fill')
+    elif t.numel():
+        t.zero_()
+    return t
+
+
+def _dense(t):
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+def copy_into(dst, src):
+    """dst[...] = src on the native kernels: same dtype -> strided copy (nd_copy);
+    fp32 <-> bf16 over identical dense layouts -> the cast kernel on the flat storage."""
+    if not (dst.is_cuda and src.is_cuda) or tuple(dst.shape) != tuple(src.shape):
+        return dst.copy_(src)
+    if dst.dtype == src.dtype:
+        return nd_copy(src, dst)
+    if {dst.dtype, src.dtype} == {torch.float32, torch.bfloat16} and dst.stride() == src.stride() and _dense(dst):
+        f = fn('hetu_cast', [P, I32, P, I32, I64, P])
+        check(f(src.data_ptr(), int(src.dtype == torch.bfloat16), dst.data_ptr(), int(dst.dtype == torch.bfloat16),
+                dst.numel(), stream_ptr()), 'cast')
+        record_native('cast')
+        return dst
+    if {dst.dtype, src.dtype} == {torch.float32, torch.bfloat16} and _dense(src):
+        tmp = torch.empty_like(src, dtype=dst.dtype)       # src's dense layout
+        copy_into(tmp, src)
+        return nd_copy(tmp, dst)
+    from . import record_fallback
+    record_fallback('copy_into', '%s %s -> %s %s' % (src.dtype, tuple(src.stride()), dst.dtype, tuple(dst.stride())))
+    return dst.copy_(src)
+
+
 def concat(tensors, axis):
     dt = tensors[0].dtype
     shape = list(tensors[0].shape)

@@ -874,6 +874,9 @@ class OnesLikeOp(Op):
         super().__init__(OnesLikeOp, [node], ctx)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        if self.device.type == 'cuda':
+            from ..kernels.tensor import fill_
+            return fill_(torch.empty(tuple(input_vals[0]), dtype=torch.float32, device=self.device), 1.0)
         return torch.ones(tuple(input_vals[0]), dtype=torch.float32, device=self.device)
 
     def gradient(self, output_grad):
@@ -890,6 +893,9 @@ class ZerosLikeOp(Op):
         super().__init__(ZerosLikeOp, [node], ctx)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        if self.device.type == 'cuda':
+            from ..kernels.tensor import zeros
+            return zeros(tuple(input_vals[0]), torch.float32, self.device)
         return torch.zeros(tuple(input_vals[0]), dtype=torch.float32, device=self.device)
 
     def gradient(self, output_grad):

@@ -594,7 +594,11 @@ class SubExecutor(object):
                     args.append((vals[inp], aux[inp]))
             if timer is not None:
                 timer.start(n)
-            r = n.compute(args)
+            if _PROFILE_OPS:
+                with torch.profiler.record_function('hetu_op:%s:%s' % (n.op_type, n.name)):
+                    r = n.compute(args)
+            else:
+                r = n.compute(args)
             if timer is not None:
                 timer.stop(n)
             if isinstance(r, AuxResult):
@@ -662,6 +666,9 @@ class SubExecutor(object):
 
 
 _CHECK_LAYOUT = os.environ.get('HETU_CHECK_LAYOUT', '0') == '1'
+# HETU_PROFILE_OPS=1: every op's compute inside a torch.profiler record_function range
+# (scripts/find_torch_kernels.py attributes device kernels to graph ops through it)
+_PROFILE_OPS = os.environ.get('HETU_PROFILE_OPS', '0') == '1'
 _LAYOUT_MISSES = {}
 
 

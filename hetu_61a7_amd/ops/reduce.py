@@ -111,7 +111,11 @@ class ReduceGradOp(Op):
             scale = 1.0 / max(int(np.prod([shape[a] for a in axes])), 1)
         g = g.reshape(keep)
         if scale != 1.0:
-            g = g * scale
+            if _gpu(g) and g.is_contiguous():
+                from ..kernels.elementwise import unary
+                g = unary('mul_c', g, float(scale))
+            else:
+                g = g * scale
         return g.expand(shape)
 
     def gradient(self, output_grad):

@@ -197,6 +197,11 @@ class SliceGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, shape = input_vals
+        if g.is_cuda:
+            from ..kernels.tensor import zeros, copy_into
+            out = zeros(tuple(shape), g.dtype, g.device)
+            copy_into(out[_slices(self.begin, g.shape, shape)], g)
+            return out
         out = torch.zeros(tuple(shape), dtype=g.dtype, device=g.device)
         out[_slices(self.begin, g.shape, shape)] = g
         return out

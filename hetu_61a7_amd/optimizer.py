@@ -501,7 +501,8 @@ class OptimizerOp(Op):
                 value.stride() == dst.stride()):
             if value.shape != dst.shape:
                 value = value.reshape(dst.shape)
-            dst.copy_(value)
+            from .kernels.tensor import copy_into
+            copy_into(dst, value)
         if self.dp:
             bs = self.bucket_of.get(p)
             if bs is not None:

@@ -19,11 +19,11 @@ VENDOR = ('Cijk', 'igemm', 'ck::', 'SubTensorOp', 'naive_conv', 'MIOpen', 'miope
 
 
 def classify(name):
-    if 'hetu' in name:
-        return 'hetu'
+    if 'at::native' in name or 'c10::' in name:
+        return 'torch'
     if any(v in name for v in VENDOR):
         return 'vendor'
-    return 'other'
+    return 'hetu'   # hetu:: kernels and the library's file-local (anonymous-namespace) ones
 
 
 def main():
@@ -32,6 +32,7 @@ def main():
     p.add_argument('--batch', type=int, default=None)
     p.add_argument('--steps', type=int, default=3)
     a = p.parse_args()
+    os.environ['HETU_PROFILE_OPS'] = '1'
     import torch
     from torch.profiler import profile, ProfilerActivity
     sys.argv = ['bench.py', '--model', a.model, '--steps', '1', '--warmup', '0'] + \
@@ -54,7 +55,7 @@ def main():
             continue
         cls = classify(e.name)
         counts[cls] += 1
-        if cls == 'other':
+        if cls == 'torch':
             frames = []
             ev = e.cpu_parent if hasattr(e, 'cpu_parent') else None
             while ev is not None and len(frames) < 1:
@@ -63,6 +64,18 @@ def main():
                     frames.append(st[0])
                 ev = ev.cpu_parent
             where[e.name[:110]][frames[0] if frames else '?'] += 1
+    # attribute through the launching CPU op: aten ops whose device kernels are torch's
+    for e in prof.events():
+        ks = getattr(e, 'kernels', None) or []
+        for k in ks:
+            if classify(k.name) == 'torch':
+                chain, ev = [], e
+                while ev is not None:                  # aten op chain up to the graph op's range
+                    chain.append(ev.name)
+                    if ev.name.startswith('hetu_op:'):
+                        break
+                    ev = ev.cpu_parent
+                where['%s <- %s' % (k.name[:70], e.name)][' < '.join(chain[::-1][:4])] += 1
     print('kernel classes in one step:', dict(counts))
     for name, fr in sorted(where.items(), key=lambda kv: -sum(kv[1].values())):
         print('%4d  %s' % (sum(fr.values()), name))

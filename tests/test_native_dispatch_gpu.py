@@ -1,0 +1,62 @@
+"""Steady-state kernel census: one training step of the flagship models, recorded
+with torch.profiler (kineto / roctracer), must launch no PyTorch (``at::native``)
+compute kernel -- every kernel is a hand-written HIP kernel of libhetu_kernels.so or a
+vendor GEMM / convolution library kernel (hipBLASLt / MIOpen, counted separately by
+kernels.VENDOR_CALLS).  Reference: SURVEY §2.7 (the op layer is hand-written)."""
+import collections
+
+import pytest
+import torch
+
+import hetu_61a7_amd as ht
+
+pytestmark = pytest.mark.gpu
+
+
+def _census(step, warm=3):
+    from torch.profiler import profile, ProfilerActivity
+    for _ in range(warm):
+        step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        step()
+        torch.cuda.synchronize()
+    torch_k = collections.Counter()
+    n = 0
+    for e in prof.events():
+        if 'CUDA' not in str(e.device_type):
+            continue
+        n += 1
+        if 'at::native' in e.name:
+            torch_k[e.name[:120]] += 1
+    return n, torch_k
+
+
+def test_resnet50_step_launches_no_torch_kernels():
+    from hetu_61a7_amd.models import resnet50_imagenet
+    B = 8
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    loss, _ = resnet50_imagenet(x, y_, 1000)
+    train = ht.optim.MomentumOptimizer(learning_rate=0.1, momentum=0.9).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3)
+    g = torch.Generator(device='cuda')
+    g.manual_seed(0)
+    X = torch.randn((B, 3, 224, 224), device='cuda', generator=g).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
+    n, torch_k = _census(lambda: ex.run('train', feed_dict={x: X, y_: Y}))
+    assert n > 300, n
+    assert not torch_k, dict(torch_k)
+
+
+def test_bert_step_launches_no_torch_kernels():
+    import argparse
+    from hetu_61a7_amd.models.bert import BertConfig, bert_bench
+    cfg = BertConfig(vocab_size=8192, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                     intermediate_size=1024, max_position_embeddings=128)
+    cfg.seq_len = 128
+    args = argparse.Namespace(batch=8, dtype='bf16', bucket_mb=32, zero=0, pp=None, bert_config=cfg)
+    step = bert_bench(args, 1, 0, 0)[0]
+    n, torch_k = _census(step)
+    assert n > 100, n
+    assert not torch_k, dict(torch_k)

@@ -36,6 +36,7 @@ struct Api {
   void* lib = nullptr;
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
@@ -97,6 +98,7 @@ HCOMM_API int hcomm_load(const char* path) {
             sym(g.Recv, "ncclRecv") && sym(g.GroupStart, "ncclGroupStart") && sym(g.GroupEnd, "ncclGroupEnd") &&
             sym(g.GetErrorString, "ncclGetErrorString") && sym(g.GetVersion, "ncclGetVersion");
   sym(g.CommSplit, "ncclCommSplit");   // optional (RCCL >= 2.18)
+  sym(g.CommInitAll, "ncclCommInitAll");
   if (!ok) {
     g.lib = nullptr;
     return -1;
@@ -248,6 +250,42 @@ HCOMM_API int hcomm_all_to_all_v(void* comm, const void* s, const int64_t* scoun
       e = g.Recv((char*)r + roffs[p] * es, (size_t)rcounts[p], (ncclDataType_t)dt, p, (ncclComm_t)comm,
                  (hipStream_t)st);
   }
+  ncclResult_t e2 = g.GroupEnd();
+  return rc(e != ncclSuccess ? e : e2);
+}
+
+// ---- single-process multi-GPU communicator (reference src/communication/
+// nccl_communication.cu:29-69): one process drives `ndev` GPUs through
+// ncclCommInitAll; every collective is one RCCL group over the per-device communicators,
+// each on its device's stream.
+HCOMM_API int hcomm_init_all(int ndev, const int* devs, void** out) {
+  if (!g.lib || !g.CommInitAll || ndev <= 0) return -1;
+  return rc(g.CommInitAll((ncclComm_t*)out, ndev, devs));
+}
+
+HCOMM_API int hcomm_multi_all_reduce(void* const* comms, void* const* send, void* const* recv, size_t count, int dt,
+                                     int op, void* const* streams, int ndev) {
+  ncclResult_t e = g.GroupStart();
+  for (int i = 0; i < ndev && e == ncclSuccess; ++i)
+    e = g.AllReduce(send[i], recv[i], count, (ncclDataType_t)dt, (ncclRedOp_t)op, (ncclComm_t)comms[i],
+                    (hipStream_t)streams[i]);
+  ncclResult_t e2 = g.GroupEnd();
+  return rc(e != ncclSuccess ? e : e2);
+}
+
+// equal chunks: chunk j of device i's send buffer goes to device j (reference NCCL_AllToAll)
+HCOMM_API int hcomm_multi_all_to_all(void* const* comms, void* const* send, void* const* recv, size_t chunk, int dt,
+                                     void* const* streams, int ndev) {
+  const size_t bytes = chunk * dtype_size(dt);
+  ncclResult_t e = g.GroupStart();
+  for (int i = 0; i < ndev && e == ncclSuccess; ++i)
+    for (int j = 0; j < ndev && e == ncclSuccess; ++j) {
+      e = g.Send((const char*)send[i] + j * bytes, chunk, (ncclDataType_t)dt, j, (ncclComm_t)comms[i],
+                 (hipStream_t)streams[i]);
+      if (e == ncclSuccess)
+        e = g.Recv((char*)recv[i] + j * bytes, chunk, (ncclDataType_t)dt, j, (ncclComm_t)comms[i],
+                   (hipStream_t)streams[i]);
+    }
   ncclResult_t e2 = g.GroupEnd();
   return rc(e != ncclSuccess ? e : e2);
 }

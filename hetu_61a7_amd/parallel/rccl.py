@@ -68,6 +68,11 @@ def lib():
         'hcomm_recv': ([P, P, SZ, I, I, P], I), 'hcomm_group_start': ([], I), 'hcomm_group_end': ([], I),
         'hcomm_all_to_all': ([P, P, P, SZ, I, P], I),
         'hcomm_all_to_all_v': ([P, P, P, P, P, P, P, I, P], I),
+        'hcomm_init_all': ([I, ctypes.POINTER(I), ctypes.POINTER(P)], I),
+        'hcomm_multi_all_reduce': ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), SZ, I, I,
+                                    ctypes.POINTER(P), I], I),
+        'hcomm_multi_all_to_all': ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), SZ, I,
+                                    ctypes.POINTER(P), I], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -280,6 +285,53 @@ class NativeComm(object):
 
     def __repr__(self):
         return 'NativeComm(rank=%d, nrank=%d)' % (self.rank, self.nrank)
+
+
+class MultiDeviceComm(object):
+    """Single-process multi-GPU communicator (reference ``nccl_communication.cu``
+    NCCL_AllReduce / NCCL_AllToAll over ``ncclCommInitAll``): one process
+    holds one RCCL communicator per device and issues each collective as one group,
+    every device's part on that device's current stream."""
+
+    def __init__(self, devices):
+        L = lib()
+        if L is None:
+            raise RCCLError('libhetu_comm / RCCL unavailable')
+        self.devices = [int(d) for d in devices]
+        n = len(self.devices)
+        self.handles = (ctypes.c_void_p * n)()
+        _check(L.hcomm_init_all(n, (ctypes.c_int * n)(*self.devices), self.handles), 'comm_init_all')
+
+    def _ptrs(self, ts):
+        assert len(ts) == len(self.devices)
+        for t, d in zip(ts, self.devices):
+            assert t.is_cuda and t.device.index == d and t.is_contiguous(), (t.device, d)
+        return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+    def _streams(self):
+        return (ctypes.c_void_p * len(self.devices))(*[torch.cuda.current_stream(d).cuda_stream
+                                                         for d in self.devices])
+
+    def all_reduce(self, tensors, op='sum'):
+        """in place: every device's tensor becomes the reduction over all devices"""
+        p = self._ptrs(tensors)
+        _check(lib().hcomm_multi_all_reduce(self.handles, p, p, tensors[0].numel(), _NCCL_DT[tensors[0].dtype],
+                                            _NCCL_OP[op], self._streams(), len(tensors)), 'multi_all_reduce')
+        return tensors
+
+    def all_to_all(self, outs, ins):
+        n = len(self.devices)
+        assert ins[0].numel() % n == 0
+        _check(lib().hcomm_multi_all_to_all(self.handles, self._ptrs(ins), self._ptrs(outs), ins[0].numel() // n,
+                                            _NCCL_DT[ins[0].dtype], self._streams(), n), 'multi_all_to_all')
+        return outs
+
+    def destroy(self):
+        L = lib()
+        for h in self.handles:
+            if h:
+                L.hcomm_destroy(ctypes.c_void_p(h))
+        self.handles = (ctypes.c_void_p * 0)()
 
 
 def world_from_dist(group=None, key_prefix='hetu_rccl') -> Optional[NativeComm]:

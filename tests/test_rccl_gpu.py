@@ -148,3 +148,37 @@ def test_forced_single_rank_dp_on_rccl(wire):
     assert np.all(np.isfinite(dp)) and dp[-1] < dp[0], res
     tol = 1e-5 if wire == 'fp32' else 2e-2   # bf16 wire rounds every gradient once
     np.testing.assert_allclose(dp, base, rtol=tol, atol=tol)
+
+
+def _multi_device(port, q):
+    try:
+        from hetu_61a7_amd.parallel.rccl import MultiDeviceComm
+        devs = list(range(torch.cuda.device_count()))
+        mc = MultiDeviceComm(devs)
+        ts = [torch.full((4096,), float(i + 1), device='cuda:%d' % d) for i, d in enumerate(devs)]
+        mc.all_reduce(ts)
+        want = float(sum(range(1, len(devs) + 1)))
+        res = {'n': len(devs), 'ar': max(float((t - want).abs().max()) for t in ts)}
+        n = len(devs)
+        ins = [torch.arange(n * 8, dtype=torch.float32, device='cuda:%d' % d) + 100 * i for i, d in enumerate(devs)]
+        outs = [torch.empty_like(x) for x in ins]
+        mc.all_to_all(outs, ins)
+        for d in devs:
+            torch.cuda.synchronize(d)
+        # chunk j of device i's output came from device j's chunk i
+        err = 0.0
+        for i in range(n):
+            for j in range(n):
+                err = max(err, float((outs[i][j * 8:(j + 1) * 8] - ins[j][i * 8:(i + 1) * 8]).abs().max()))
+        res['a2a'] = err
+        mc.destroy()
+        q.put(res)
+    except Exception as e:
+        q.put({'error': repr(e)})
+
+
+def test_single_process_multi_device_comm():
+    """ncclCommInitAll communicator driving every visible GPU from one process (one on
+    the test box): grouped all-reduce and all-to-all."""
+    res = _spawn(_multi_device)
+    assert res['n'] >= 1 and res['ar'] == 0.0 and res['a2a'] == 0.0, res

@@ -6,6 +6,7 @@
 // templated family: 16-byte vector loads, grid-stride over at most 2048 blocks,
 // fp32 math on bf16/fp32 storage.
 #include "common.h"
+#include <algorithm>
 
 namespace hetu {
 
@@ -116,11 +117,21 @@ __global__ void __launch_bounds__(256) unary_k(const T* __restrict__ x, T* __res
 }
 
 // b_mode: 0 same shape; 1 b broadcast along rows (b has `inner` elements,
-// a is [n/inner, inner]); 2 b is a scalar tensor
+// a is [n/inner, inner]); 2 b is a scalar tensor; 3 b constant along the trailing
+// `inner` elements and periodic with `bnum` values ([T,1] x [T,d] row scales, [1,C,1,1]
+// per-channel NCHW operands): b[(i / inner) % bnum]
+template <typename TB>
+__device__ __forceinline__ float b_at(const TB* __restrict__ b, int b_mode, int64_t i, int64_t inner, int64_t bnum) {
+  if (b_mode == 0) return to_f(b[i]);
+  if (b_mode == 1) return to_f(b[i % inner]);
+  if (b_mode == 2) return to_f(b[0]);
+  return to_f(b[(i / inner) % bnum]);
+}
+
 template <typename T, typename TB, int OP>
 __global__ void __launch_bounds__(256) binary_k(const T* __restrict__ a, const TB* __restrict__ b,
                                                  T* __restrict__ y, int64_t n, int b_mode,
-                                                 int64_t inner, float c) {
+                                                 int64_t inner, int64_t bnum, float c) {
   constexpr int V = Vec<T>::N;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   // 16-byte vector path only on 16-byte aligned bases (views with an element offset
@@ -128,7 +139,7 @@ __global__ void __launch_bounds__(256) binary_k(const T* __restrict__ a, const T
   const uintptr_t al = (uintptr_t)a | (uintptr_t)y | (b_mode == 0 ? (uintptr_t)b : (uintptr_t)0);
   const bool vec_ok = (al % 16 == 0) &&
                       ((b_mode == 0 && sizeof(T) == sizeof(TB)) || (b_mode == 1 && inner % V == 0) ||
-                       b_mode == 2);
+                       b_mode == 2 || (b_mode == 3 && inner % V == 0));
   if (vec_ok) {
     const int64_t nv = n / V;
     const float bs = b_mode == 2 ? to_f(b[0]) : 0.f;
@@ -141,6 +152,10 @@ __global__ void __launch_bounds__(256) binary_k(const T* __restrict__ a, const T
         const int64_t c0 = (i * V) % inner;
 #pragma unroll
         for (int k = 0; k < V; ++k) vb[k] = to_f(b[c0 + k]);
+      } else if (b_mode == 3) {   // the whole vector lies in one inner block
+        const float bv = to_f(b[((i * V) / inner) % bnum]);
+#pragma unroll
+        for (int k = 0; k < V; ++k) vb[k] = bv;
       } else {
 #pragma unroll
         for (int k = 0; k < V; ++k) vb[k] = bs;
@@ -149,15 +164,11 @@ __global__ void __launch_bounds__(256) binary_k(const T* __restrict__ a, const T
       for (int k = 0; k < V; ++k) va[k] = bi<OP>(va[k], vb[k], c);
       store_vec<T>(y + i * V, va);
     }
-    for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      float bv = b_mode == 0 ? to_f(b[i]) : (b_mode == 1 ? to_f(b[i % inner]) : bs);
-      y[i] = from_f<T>(bi<OP>(to_f(a[i]), bv, c));
-    }
+    for (int64_t i = nv * V + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+      y[i] = from_f<T>(bi<OP>(to_f(a[i]), b_at(b, b_mode, i, inner, bnum), c));
   } else {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      float bv = b_mode == 0 ? to_f(b[i]) : (b_mode == 1 ? to_f(b[i % inner]) : to_f(b[0]));
-      y[i] = from_f<T>(bi<OP>(to_f(a[i]), bv, c));
-    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+      y[i] = from_f<T>(bi<OP>(to_f(a[i]), b_at(b, b_mode, i, inner, bnum), c));
   }
 }
 
@@ -169,17 +180,22 @@ struct NdGeom {
   int64_t shape[8], as[8], bs[8];
 };
 
-template <typename T, typename TB, int OP>
+// IT: index type -- 32-bit when every offset fits (the host collapses mergeable dims
+// first, so most calls carry 2-3 dims of 32-bit divisions per element)
+template <typename T, typename TB, int OP, typename IT>
 __global__ void __launch_bounds__(256) binary_nd_k(const T* __restrict__ a, const TB* __restrict__ b,
                                                     T* __restrict__ y, int64_t n, NdGeom g, float c) {
+  IT shape[8], as[8], bs[8];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) { shape[d] = (IT)g.shape[d]; as[d] = (IT)g.as[d]; bs[d] = (IT)g.bs[d]; }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = i, oa = 0, ob = 0;
+    IT r = (IT)i, oa = 0, ob = 0;
 #pragma unroll
     for (int d = 7; d >= 0; --d) {
       if (d < g.nd) {
-        const int64_t q = r / g.shape[d], k = r - q * g.shape[d];
-        oa += k * g.as[d];
-        ob += k * g.bs[d];
+        const IT q = r / shape[d], k = r - q * shape[d];
+        oa += k * as[d];
+        ob += k * bs[d];
         r = q;
       }
     }
@@ -228,21 +244,22 @@ HETU_API int hetu_unary(int op, const void* x, void* y, int64_t n, int is_bf16, 
   case OPV:                                                                                     \
     if (is_bf16 && b_bf16)                                                                      \
       hipLaunchKernelGGL((binary_k<bf16, bf16, OPV>), dim3(grid), dim3(256), 0, st,             \
-                         (const bf16*)a, (const bf16*)b, (bf16*)y, n, b_mode, inner, c);        \
+                         (const bf16*)a, (const bf16*)b, (bf16*)y, n, b_mode, inner, bnum, c);        \
     else if (is_bf16)                                                                           \
       hipLaunchKernelGGL((binary_k<bf16, float, OPV>), dim3(grid), dim3(256), 0, st,            \
-                         (const bf16*)a, (const float*)b, (bf16*)y, n, b_mode, inner, c);       \
+                         (const bf16*)a, (const float*)b, (bf16*)y, n, b_mode, inner, bnum, c);       \
     else if (b_bf16)                                                                            \
       hipLaunchKernelGGL((binary_k<float, bf16, OPV>), dim3(grid), dim3(256), 0, st,            \
-                         (const float*)a, (const bf16*)b, (float*)y, n, b_mode, inner, c);      \
+                         (const float*)a, (const bf16*)b, (float*)y, n, b_mode, inner, bnum, c);      \
     else                                                                                        \
       hipLaunchKernelGGL((binary_k<float, float, OPV>), dim3(grid), dim3(256), 0, st,           \
-                         (const float*)a, (const float*)b, (float*)y, n, b_mode, inner, c);     \
+                         (const float*)a, (const float*)b, (float*)y, n, b_mode, inner, bnum, c);     \
     break;
 
-HETU_API int hetu_binary(int op, const void* a, const void* b, void* y, int64_t n, int is_bf16,
-                         int b_bf16, int b_mode, int64_t inner, float c, hipStream_t st) {
+HETU_API int hetu_binary3(int op, const void* a, const void* b, void* y, int64_t n, int is_bf16,
+                          int b_bf16, int b_mode, int64_t inner, int64_t bnum, float c, hipStream_t st) {
   if (n <= 0) return 0;
+  if (bnum < 1) bnum = 1;
   int grid = stream_grid(n, 256, is_bf16 ? 8 : 4);
   switch (op) {
     BCASE(B_ADD) BCASE(B_SUB) BCASE(B_MUL) BCASE(B_DIV) BCASE(B_MAX) BCASE(B_MIN)
@@ -255,20 +272,27 @@ HETU_API int hetu_binary(int op, const void* a, const void* b, void* y, int64_t 
   return 0;
 }
 
-#define BNDCASE(OPV)                                                                            \
-  case OPV:                                                                                     \
+HETU_API int hetu_binary(int op, const void* a, const void* b, void* y, int64_t n, int is_bf16,
+                         int b_bf16, int b_mode, int64_t inner, float c, hipStream_t st) {
+  return hetu_binary3(op, a, b, y, n, is_bf16, b_bf16, b_mode, inner, 1, c, st);
+}
+
+#define BND_LAUNCH(OPV, IT)                                                                     \
     if (is_bf16 && b_bf16)                                                                      \
-      hipLaunchKernelGGL((binary_nd_k<bf16, bf16, OPV>), dim3(grid), dim3(256), 0, st,          \
+      hipLaunchKernelGGL((binary_nd_k<bf16, bf16, OPV, IT>), dim3(grid), dim3(256), 0, st,      \
                          (const bf16*)a, (const bf16*)b, (bf16*)y, n, g, c);                    \
     else if (is_bf16)                                                                           \
-      hipLaunchKernelGGL((binary_nd_k<bf16, float, OPV>), dim3(grid), dim3(256), 0, st,         \
+      hipLaunchKernelGGL((binary_nd_k<bf16, float, OPV, IT>), dim3(grid), dim3(256), 0, st,     \
                          (const bf16*)a, (const float*)b, (bf16*)y, n, g, c);                   \
     else if (b_bf16)                                                                            \
-      hipLaunchKernelGGL((binary_nd_k<float, bf16, OPV>), dim3(grid), dim3(256), 0, st,         \
+      hipLaunchKernelGGL((binary_nd_k<float, bf16, OPV, IT>), dim3(grid), dim3(256), 0, st,     \
                          (const float*)a, (const bf16*)b, (float*)y, n, g, c);                  \
     else                                                                                        \
-      hipLaunchKernelGGL((binary_nd_k<float, float, OPV>), dim3(grid), dim3(256), 0, st,        \
-                         (const float*)a, (const float*)b, (float*)y, n, g, c);                 \
+      hipLaunchKernelGGL((binary_nd_k<float, float, OPV, IT>), dim3(grid), dim3(256), 0, st,    \
+                         (const float*)a, (const float*)b, (float*)y, n, g, c);
+#define BNDCASE(OPV)                                                                            \
+  case OPV:                                                                                     \
+    if (small) { BND_LAUNCH(OPV, int32_t) } else { BND_LAUNCH(OPV, int64_t) }                   \
     break;
 
 // y (contiguous, shape[0..nd)) = op(a, b) with a / b read through element strides
@@ -286,6 +310,13 @@ HETU_API int hetu_binary_nd(int op, const void* a, const void* b, void* y, int n
     if (d < nd) n *= shape[d];
   }
   if (n <= 0) return 0;
+  int64_t ea = 0, eb = 0;   // largest element offset each operand is read at
+  for (int d = 0; d < nd; ++d) {
+    ea += (shape[d] - 1) * astride[d];
+    eb += (shape[d] - 1) * bstride[d];
+  }
+  const int64_t reach = std::max(n, std::max(ea, eb) + 1);
+  const bool small = reach < (1ll << 31);
   int grid = stream_grid(n, 256, 1);
   switch (op) {
     BNDCASE(B_ADD) BNDCASE(B_SUB) BNDCASE(B_MUL) BNDCASE(B_DIV) BNDCASE(B_MAX) BNDCASE(B_MIN)

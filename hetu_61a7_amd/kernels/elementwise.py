@@ -146,12 +146,17 @@ def binary(op: str, a: torch.Tensor, b: torch.Tensor, c: float = 0.0, out=None) 
         elif a.dim() >= b.dim() and tuple(a.shape[a.dim() - b.dim():]) == tuple(b.shape):
             mode, inner = 1, b.numel()
         else:
-            mode = -1
+            mode, inner = -1, 1
+        bnum = 1
+        if mode < 0:
+            m3 = _periodic(a, b)
+            if m3 is not None:
+                mode, (inner, bnum) = 3, m3
         if mode >= 0:
             y = out if out is not None else torch.empty_like(a)
-            f = fn('hetu_binary', [I32, P, P, P, I64, I32, I32, I32, I64, F32, P])
+            f = fn('hetu_binary3', [I32, P, P, P, I64, I32, I32, I32, I64, I64, F32, P])
             check(f(B[op], a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), is_bf16(a),
-                    is_bf16(b), mode, inner, float(c), stream_ptr()), 'binary:' + op)
+                    is_bf16(b), mode, inner, bnum, float(c), stream_ptr()), 'binary:' + op)
             return y
         r = _binary_nd(op, a, b, c, out)
         if r is not None:
@@ -177,6 +182,42 @@ def binary(op: str, a: torch.Tensor, b: torch.Tensor, c: float = 0.0, out=None) 
     return r
 
 
+def _periodic(a, b):
+    """(inner, bnum) when contiguous ``b`` broadcast to ``a`` equals b[(i // inner) % bnum]
+    for flat index i -- b spans one contiguous block of a's dims ([T,1] vs [T,d],
+    [1,C,1,1] vs [N,C,H,W]); else None"""
+    nd = a.dim()
+    if b.dim() > nd:
+        return None
+    bs = [1] * (nd - b.dim()) + list(b.shape)
+    full = [i for i in range(nd) if bs[i] != 1]
+    if not full:
+        return None
+    j, k = full[0], full[-1] + 1
+    if any(bs[i] != a.shape[i] for i in range(j, k)):
+        return None
+    inner = 1
+    for d in a.shape[k:]:
+        inner *= int(d)
+    return inner, b.numel()
+
+
+def _collapse(shape, sa, sb):
+    """drop unit dims and merge neighbours that are contiguous in all three of the
+    output (row-major ``shape``), a and b"""
+    dims = [(int(n), int(x), int(y)) for n, x, y in zip(shape, sa, sb) if n != 1]
+    out = []
+    for n, x, y in dims:
+        if out and out[-1][1] == n * x and out[-1][2] == n * y:
+            n0 = out[-1][0]
+            out[-1] = (n0 * n, x, y)
+        else:
+            out.append((n, x, y))
+    if not out:
+        out = [(1, 0, 0)]
+    return [d[0] for d in out], [d[1] for d in out], [d[2] for d in out]
+
+
 def _binary_nd(op, a, b, c, out):
     """General broadcast / strided form (``hetu_binary_nd``): the output takes the
     broadcast shape of a and b in a's dtype; None when it needs more than 8 dims."""
@@ -193,10 +234,11 @@ def _binary_nd(op, a, b, c, out):
     if out is not None and (tuple(out.shape) != tuple(shape) or not out.is_contiguous() or out.dtype != a.dtype):
         return None
     y = out if out is not None else torch.empty(shape, dtype=a.dtype, device=a.device)
-    nd = len(shape)
+    cs, ca, cb = _collapse(shape, ae.stride(), be.stride())
+    nd = len(cs)
     arr = ctypes.c_int64 * nd
     f = fn('hetu_binary_nd', [I32, P, P, P, I32, P, P, P, I32, I32, F32, P])
-    check(f(B[op], a.data_ptr(), b.data_ptr(), y.data_ptr(), nd, arr(*shape), arr(*ae.stride()), arr(*be.stride()),
+    check(f(B[op], a.data_ptr(), b.data_ptr(), y.data_ptr(), nd, arr(*cs), arr(*ca), arr(*cb),
             is_bf16(a), is_bf16(b), float(c), stream_ptr()), 'binary_nd:' + op)
     return y
 

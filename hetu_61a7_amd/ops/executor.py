@@ -534,7 +534,8 @@ class SubExecutor(object):
                 t.hetu_host = src      # host copy of fed ids: PS lookups need no device sync
         if self.config.mixed_precision and t.is_cuda and t.dtype == torch.float32 and \
                 not getattr(node, 'keep_fp32', False):
-            t = t.to(torch.bfloat16)
+            from ..kernels.elementwise import cast
+            t = cast(t.contiguous(), torch.bfloat16)    # native cast kernel
         return t
 
     # ---- run ---------------------------------------------------------------------------

@@ -33,20 +33,28 @@ struct NDDesc {
   int64_t imod[MAXD];
 };
 
-template <typename T>
+// IT: 32-bit index math when every offset fits (the host collapses mergeable dims and
+// widens the element to 16 bytes where the innermost dim is contiguous on both sides)
+template <typename T, typename IT>
 __global__ void __launch_bounds__(256) nd_copy_k(const T* __restrict__ x, T* __restrict__ y, NDDesc d,
                                                  int64_t total) {
+  IT shape[MAXD], os[MAXD], is[MAXD], sh[MAXD], md[MAXD];
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) {
+    shape[k] = (IT)d.shape[k]; os[k] = (IT)d.ostride[k]; is[k] = (IT)d.istride[k];
+    sh[k] = (IT)d.shift[k]; md[k] = (IT)d.imod[k];
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = i, oo = 0, io = 0;
+    IT r = (IT)i, oo = 0, io = 0;
 #pragma unroll
     for (int k = MAXD - 1; k >= 0; --k) {
       if (k >= d.nd) continue;
-      const int64_t c = r % d.shape[k];
-      r /= d.shape[k];
-      oo += c * d.ostride[k];
-      int64_t ci = c + d.shift[k];
-      if (d.imod[k] > 0) ci %= d.imod[k];
-      io += ci * d.istride[k];
+      const IT q = r / shape[k], c = r - q * shape[k];
+      r = q;
+      oo += c * os[k];
+      IT ci = c + sh[k];
+      if (md[k] > 0) ci %= md[k];
+      io += ci * is[k];
     }
     y[oo] = x[io];
   }
@@ -247,26 +255,68 @@ __global__ void __launch_bounds__(256) pnorm_grad_k(const T* __restrict__ x, con
 HETU_API int hetu_nd_copy(const void* x, void* y, int elem, int nd, const int64_t* shape, const int64_t* ostride,
                           const int64_t* istride, const int64_t* shift, const int64_t* imod, hipStream_t st) {
   if (nd < 1 || nd > MAXD) return (int)hipErrorInvalidValue;
-  NDDesc d{};
-  d.nd = nd;
+  int64_t sh_[MAXD], os_[MAXD], is_[MAXD], sf_[MAXD], md_[MAXD];
+  bool plain = true;
   int64_t total = 1;
   for (int k = 0; k < nd; ++k) {
-    d.shape[k] = shape[k];
-    d.ostride[k] = ostride[k];
-    d.istride[k] = istride[k];
-    d.shift[k] = shift ? shift[k] : 0;
-    d.imod[k] = imod ? imod[k] : 0;
+    sh_[k] = shape[k]; os_[k] = ostride[k]; is_[k] = istride[k];
+    sf_[k] = shift ? shift[k] : 0; md_[k] = imod ? imod[k] : 0;
+    if (sf_[k] || md_[k]) plain = false;
     total *= shape[k];
   }
   if (total == 0) return 0;
+  if (plain) {
+    // drop unit dims, merge neighbours contiguous on both sides (outer = inner extent x stride)
+    int m = 0;
+    for (int k = 0; k < nd; ++k) {
+      if (sh_[k] == 1) continue;
+      if (m > 0 && os_[m - 1] == sh_[k] * os_[k] && is_[m - 1] == sh_[k] * is_[k]) {
+        sh_[m - 1] *= sh_[k];
+        os_[m - 1] = os_[k];
+        is_[m - 1] = is_[k];
+      } else {
+        sh_[m] = sh_[k]; os_[m] = os_[k]; is_[m] = is_[k]; sf_[m] = 0; md_[m] = 0;
+        ++m;
+      }
+    }
+    if (m == 0) { sh_[0] = 1; os_[0] = 1; is_[0] = 1; sf_[0] = 0; md_[0] = 0; m = 1; }
+    nd = m;
+    // widen the element while the innermost dim is unit-stride on both sides
+    while (elem < 16 && os_[nd - 1] == 1 && is_[nd - 1] == 1 && sh_[nd - 1] % 2 == 0 &&
+           ((uintptr_t)x % (2 * elem)) == 0 && ((uintptr_t)y % (2 * elem)) == 0) {
+      bool ok = true;
+      for (int k = 0; k < nd - 1; ++k) ok = ok && os_[k] % 2 == 0 && is_[k] % 2 == 0;
+      if (!ok) break;
+      for (int k = 0; k < nd - 1; ++k) { os_[k] /= 2; is_[k] /= 2; }
+      sh_[nd - 1] /= 2;
+      elem *= 2;
+    }
+  }
+  NDDesc d{};
+  d.nd = nd;
+  total = 1;
+  int64_t eo = 0, ei = 0;
+  for (int k = 0; k < nd; ++k) {
+    d.shape[k] = sh_[k]; d.ostride[k] = os_[k]; d.istride[k] = is_[k]; d.shift[k] = sf_[k]; d.imod[k] = md_[k];
+    total *= sh_[k];
+    eo += (sh_[k] - 1) * (os_[k] < 0 ? -os_[k] : os_[k]);
+    const int64_t reach = md_[k] > 0 ? md_[k] : sh_[k] - 1 + (sf_[k] < 0 ? -sf_[k] : sf_[k]);
+    ei += reach * (is_[k] < 0 ? -is_[k] : is_[k]);
+  }
+  const bool small = total < (1ll << 31) && eo < (1ll << 31) && ei < (1ll << 31);
   const int g = stream_grid(total, 256, 4);
+#define NDC(T)                                                                                      \
+  if (small) hipLaunchKernelGGL((nd_copy_k<T, int32_t>), dim3(g), dim3(256), 0, st, (const T*)x, (T*)y, d, total); \
+  else hipLaunchKernelGGL((nd_copy_k<T, int64_t>), dim3(g), dim3(256), 0, st, (const T*)x, (T*)y, d, total);
   switch (elem) {
-    case 1: hipLaunchKernelGGL(nd_copy_k<uint8_t>, dim3(g), dim3(256), 0, st, (const uint8_t*)x, (uint8_t*)y, d, total); break;
-    case 2: hipLaunchKernelGGL(nd_copy_k<uint16_t>, dim3(g), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y, d, total); break;
-    case 4: hipLaunchKernelGGL(nd_copy_k<uint32_t>, dim3(g), dim3(256), 0, st, (const uint32_t*)x, (uint32_t*)y, d, total); break;
-    case 8: hipLaunchKernelGGL(nd_copy_k<uint64_t>, dim3(g), dim3(256), 0, st, (const uint64_t*)x, (uint64_t*)y, d, total); break;
+    case 1: NDC(uint8_t) break;
+    case 2: NDC(uint16_t) break;
+    case 4: NDC(uint32_t) break;
+    case 8: NDC(uint64_t) break;
+    case 16: NDC(uint4) break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef NDC
   return (int)hipGetLastError();
 }
 

@@ -330,6 +330,27 @@ HETU_API int hetu_moe_gate_topk(const void* logits, float* probs, int64_t* idx, 
   return 0;
 }
 
+// Balance-loss terms of a top-k gate in one tiny launch (one wave): coef[e] = counts[e] / T,
+// l_aux = E * sum_e (psum[e] / T) * coef[e]  (reference TopGate.py's load-balancing loss).
+__global__ void __launch_bounds__(64) moe_aux_k(const int* __restrict__ counts, const float* __restrict__ psum,
+                                                float* __restrict__ coef, float* __restrict__ l_aux, int T, int E) {
+  const float inv = 1.f / (float)T;
+  float acc = 0.f;
+  for (int e = threadIdx.x; e < E; e += 64) {
+    const float c = (float)counts[e] * inv;
+    coef[e] = c;
+    acc += psum[e] * inv * c;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (threadIdx.x == 0) l_aux[0] = acc * (float)E;
+}
+
+HETU_API int hetu_moe_aux(const int* counts, const float* psum, float* coef, float* l_aux, int T, int E,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(moe_aux_k, dim3(1), dim3(64), 0, st, counts, psum, coef, l_aux, T, E);
+  return (int)hipGetLastError();
+}
+
 HETU_API int hetu_moe_locations(const int64_t* idx, const float* probs, int64_t* loc, int* counts, float* psum,
                                 int T, int k, int E, hipStream_t s) {
   if (E <= 0) return 0;

@@ -68,6 +68,20 @@ def locations(idx, num_experts, probs=None):
     return loc, counts, psum
 
 
+def aux_terms(counts, psum, T):
+    """(coef [E] = counts / T, l_aux [] = E * sum_e psum_e / T * coef_e): one native launch"""
+    E = counts.numel()
+    if native(psum) and counts.dtype == torch.int32 and psum.dtype == torch.float32:
+        coef = torch.empty((E,), dtype=torch.float32, device=psum.device)
+        l_aux = torch.empty((), dtype=torch.float32, device=psum.device)
+        f = fn('hetu_moe_aux', [P, P, P, P, I32, I32, P])
+        check(f(counts.contiguous().data_ptr(), psum.contiguous().data_ptr(), coef.data_ptr(), l_aux.data_ptr(),
+                int(T), int(E), stream_ptr()), 'moe_aux')
+        return coef, l_aux
+    coef = counts.float() / float(T)
+    return coef, (psum / float(T) * coef).sum() * float(E)
+
+
 def gate_backward(probs, idx, dgate, aux_coef):
     """d logits of (gate values [T, k] = probs[t, idx], balance term sum_e c_e * sum_t probs[t, e])."""
     T, E = probs.shape

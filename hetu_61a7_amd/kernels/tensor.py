@@ -349,7 +349,7 @@ def bce_grad(y, lab, g):
 def nll(x, t, cols):
     x = x.reshape(-1, cols).contiguous()
     t = t.long().reshape(-1).contiguous()
-    out = torch.zeros(1, dtype=torch.float32, device=x.device)
+    out = zeros((1,), torch.float32, x.device)
     check(fn('hetu_nll', [P, P, P, I64, I64, I32, P])(x.data_ptr(), t.data_ptr(), out.data_ptr(), x.shape[0], cols,
                                                        _bf(x), stream_ptr()), 'nll')
     record_native('nll')

@@ -369,8 +369,8 @@ class TopKGatingOp(Op):
         T, E = logits.shape
         val, idx, probs = KM.topk(logits, self.k, softmax=True)
         loc, counts, psum = KM.locations(idx, E, probs)
-        coef = counts.float() / float(T)                     # mean_t mask[t, e] summed over choices
-        l_aux = (psum / float(T) * coef).sum() * float(E)
+        # coef_e = mean_t mask[t, e] summed over choices; l_aux = E * sum_e coef_e * mean_t probs[t, e]
+        coef, l_aux = KM.aux_terms(counts, psum, T)
         return AuxResult(val, (probs, idx, loc, l_aux, coef))
 
     def gradient(self, output_grad):
@@ -395,7 +395,12 @@ class TopKGatingGradOp(Op):
         T, E = probs.shape
         if self.is_aux:
             # l_aux = E * sum_e coef_e * sum_t probs[t, e] / T
-            c = coef * (float(E) / float(T)) * g.float().reshape(-1)[0]
+            if coef.is_cuda:
+                from ..kernels.elementwise import binary, unary
+                gs = g.reshape(-1)[:1]          # the scalar d l_aux, read in place (scalar mode)
+                c = binary('mul', unary('mul_c', coef, float(E) / float(T)), gs)
+            else:
+                c = coef * (float(E) / float(T)) * g.float().reshape(-1)[0]
             return KM.gate_backward(probs, idx, None, c)
         return KM.gate_backward(probs, idx, g, None)
 

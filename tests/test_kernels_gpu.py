@@ -50,6 +50,7 @@ def test_binary_modes(op, dt):
 def test_batchnorm_nhwc(dt, relu, res, N, C, H, W):
     # C >= 512 in bf16 puts 512 channels in one stats tile (more than the 256
     # threads that fold it): the ResNet-50 stage 2-4 shapes
+    torch.manual_seed(1000 + N + C + H)
     x = torch.randn(N, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
     r = torch.randn(N, C, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last) if res else None
     scale = torch.rand(C, device=DEV) + 0.5
@@ -73,11 +74,15 @@ def test_batchnorm_nhwc(dt, relu, res, N, C, H, W):
     ref.backward(dy.float())
     dx, ds, db, dres = KN.bn_backward(dy, y, x, scale, mean, invstd, relu=relu, want_dres=res, bias=bias)
     tol = dict(rtol=5e-2, atol=5e-2) if dt == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
-    torch.testing.assert_close(dx.float(), xf.grad, **tol)
+    # an output within rounding of 0 can take the other side of the ReLU in the fused kernel
+    # (x*a + b folded, bf16 store) than in the fp32 reference: compare where both agree
+    agree = ((y.float() > 0) == (ref.detach() > 0)) if relu else torch.ones_like(ref, dtype=torch.bool)
+    assert agree.float().mean() > 0.9999
+    torch.testing.assert_close(torch.where(agree, dx.float(), xf.grad), xf.grad, **tol)
     torch.testing.assert_close(ds, sf.grad, rtol=2e-2, atol=2e-1 if dt == torch.bfloat16 else 1e-2)
     torch.testing.assert_close(db, bf.grad, rtol=2e-2, atol=2e-1 if dt == torch.bfloat16 else 1e-2)
     if res:
-        torch.testing.assert_close(dres.float(), rf.grad, **tol)
+        torch.testing.assert_close(torch.where(agree, dres.float(), rf.grad), rf.grad, **tol)
 
 
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])

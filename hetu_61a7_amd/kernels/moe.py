@@ -15,6 +15,18 @@ import torch
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32
 
 
+def _dc(t, dtype=None):
+    """contiguous (optionally re-typed) tensor; device copies / casts on the native
+    kernels, no copy when it already is one"""
+    dtype = dtype or t.dtype
+    if t.is_contiguous() and t.dtype == dtype:
+        return t
+    if t.is_cuda:
+        from .tensor import copy_into
+        return copy_into(torch.empty(t.shape, dtype=dtype, device=t.device), t)
+    return t.to(dtype).contiguous()
+
+
 def _ik(t, T):
     return t.reshape(T, -1).long().contiguous()
 
@@ -88,8 +100,8 @@ def gate_backward(probs, idx, dgate, aux_coef):
     k = idx.shape[1]
     if native(probs) and E <= 512 and k <= 8:
         out = torch.empty((T, E), dtype=torch.float32, device=probs.device)
-        dg = dgate.float().reshape(T, k).contiguous() if dgate is not None else None
-        ac = aux_coef.float().contiguous() if aux_coef is not None else None
+        dg = _dc(dgate.reshape(T, k), torch.float32) if dgate is not None else None
+        ac = _dc(aux_coef, torch.float32) if aux_coef is not None else None
         f = fn('hetu_moe_gate_backward', [P, P, P, P, P, I32, I32, I32, P])
         check(f(probs.contiguous().data_ptr(), idx.long().contiguous().data_ptr(), ptr_or_none(dg), ptr_or_none(ac),
                 out.data_ptr(), T, E, k, stream_ptr()), 'moe_gate_backward')
@@ -122,7 +134,7 @@ def layout_transform(x, indices, locations, capacity, num_experts):
     k = idx.shape[1]
     nslots = num_experts * capacity
     if _io_ok(x):
-        x = x.contiguous()
+        x = _dc(x)
         smap = _slot_map(idx, loc, capacity, nslots)
         out = torch.empty((nslots, d), dtype=x.dtype, device=x.device)
         f = fn('hetu_moe_gather_slots', [P, P, P, P, I32, I32, I32, I32, P])
@@ -140,9 +152,9 @@ def layout_transform(x, indices, locations, capacity, num_experts):
 def _combine(y, idx, loc, w, capacity, T):
     d = y.shape[-1]
     k = idx.shape[1]
-    y = y.contiguous()
+    y = _dc(y)
     out = torch.empty((T, d), dtype=y.dtype, device=y.device)
-    wf = w.float().reshape(T, k).contiguous() if w is not None else None
+    wf = _dc(w.reshape(T, k), torch.float32) if w is not None else None
     f = fn('hetu_moe_combine', [P, P, P, P, P, I32, I32, I32, I32, I32, P])
     check(f(y.data_ptr(), idx.data_ptr(), loc.data_ptr(), ptr_or_none(wf), out.data_ptr(), T, k, capacity, d,
             is_bf16(y), stream_ptr()), 'moe_combine')
@@ -182,9 +194,9 @@ def reverse_layout_transform_backward_data(g, indices, locations, gates, capacit
     k = idx.shape[1]
     d = g.shape[-1]
     if _io_ok(g):
-        g = g.contiguous()
+        g = _dc(g)
         smap = _slot_map(idx, loc, capacity, num_slots)
-        wf = gates.float().reshape(T, k).contiguous() if gates is not None else None
+        wf = _dc(gates.reshape(T, k), torch.float32) if gates is not None else None
         out = torch.empty((num_slots, d), dtype=g.dtype, device=g.device)
         f = fn('hetu_moe_gather_slots', [P, P, P, P, I32, I32, I32, I32, P])
         check(f(g.data_ptr(), smap.data_ptr(), ptr_or_none(wf), out.data_ptr(), num_slots, d, k, is_bf16(g),
@@ -205,7 +217,7 @@ def reverse_layout_transform_backward_gate(g, y, indices, locations, capacity):
     k = idx.shape[1]
     d = g.shape[-1]
     if _io_ok(g, y):
-        g, y = g.contiguous(), y.contiguous()
+        g, y = _dc(g), _dc(y)
         out = torch.empty((T, k), dtype=torch.float32, device=g.device)
         f = fn('hetu_moe_gate_grad', [P, P, P, P, P, I32, I32, I32, I32, I32, P])
         check(f(g.data_ptr(), y.data_ptr(), idx.data_ptr(), loc.data_ptr(), out.data_ptr(), T * k, k, capacity, d,

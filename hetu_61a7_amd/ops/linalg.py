@@ -42,13 +42,21 @@ class MatMulOp(Op):
                                      inplace=_may_overwrite(self, acc))
             y = self.compute([a, b])
             if not (self.grad_dest is not None and y.data_ptr() == self.grad_dest.data_ptr()):
-                y = y.float() if self.grad_dest is not None else y.clone()
+                if y.is_cuda:
+                    from ..kernels.tensor import copy_into
+                    y = copy_into(torch.empty(y.shape, dtype=torch.float32 if self.grad_dest is not None else y.dtype,
+                                              device=y.device), y)
+                else:
+                    y = y.float() if self.grad_dest is not None else y.clone()
             if isinstance(acc, ndarray.IndexedSlices) and y.dtype == torch.float32 and y.is_contiguous():
                 # tied embedding: the lookup's row-sparse gradient lands straight in the
                 # dense fp32 gradient (no densified copy of the table)
                 from ..kernels import sparse as KSP
                 KSP.scatter_add_rows(y.view(-1, y.shape[-1]), acc._t(acc.indices), acc._t(acc.values))
                 return y
+            if y.is_cuda and not isinstance(acc, ndarray.IndexedSlices) and y.is_contiguous():
+                from ..kernels.elementwise import binary
+                return binary('add', y, acc, out=y)
             y.add_((acc.to_dense() if isinstance(acc, ndarray.IndexedSlices) else acc).to(y.dtype))
             return y
         d = self.grad_dest

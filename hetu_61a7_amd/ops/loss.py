@@ -50,6 +50,9 @@ class SoftmaxGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         y, g = input_vals
+        if g.dtype != y.dtype and g.is_cuda:
+            from ..kernels.elementwise import cast
+            g = cast(g.contiguous(), y.dtype)
         return KS.softmax_backward(y, g.to(y.dtype))
 
     def gradient(self, output_grad):

@@ -181,6 +181,14 @@ class SumOp(Op):
             return r
         dt = max(dense, key=lambda t: t.numel()).dtype
         acc = None
+        if all(_gpu(v) for v in dense):
+            from ..kernels.elementwise import binary, cast
+            for v in dense:          # native adds (mixed bf16 / fp32 operands read as they are)
+                if acc is None:
+                    acc = v if v.dtype == dt else cast(v.contiguous(), dt)
+                else:
+                    acc = binary('add', acc, v)
+            dense = []
         for v in dense:
             acc = v.to(dt) if acc is None else acc + v.to(dt)
         for s in sparse:

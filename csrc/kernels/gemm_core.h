@@ -555,6 +555,7 @@ struct EpiOut {
   char* Cb;
   const char* Cinb;
   bool cvec, ivec;
+  bool cvec2;   // bf16 C with an even (not 8-multiple) ldc: 4-byte stores of column pairs
   float bcol[8];
 };
 
@@ -563,6 +564,7 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
   o.Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
   o.cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)o.Cb & 15) == 0)
                       : ((ep.ldc & 7) == 0 && ((uintptr_t)o.Cb & 15) == 0);
+  o.cvec2 = !ep.out_f32 && !o.cvec && (ep.ldc & 1) == 0 && ((uintptr_t)o.Cb & 3) == 0;
   o.ivec = o.Cinb && (ep.cin_f32 ? ((ep.ldcin & 3) == 0 && ((uintptr_t)o.Cinb & 15) == 0)
                                  : ((ep.ldcin & 7) == 0 && ((uintptr_t)o.Cinb & 15) == 0));
 #pragma unroll
@@ -635,6 +637,11 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
     bf16* Ch = (bf16*)o.Cb + off;
     if (o.cvec && full) {
       store_vec<bf16>(Ch, v);
+    } else if (o.cvec2 && full) {   // row offset and n even: 4-byte aligned pairs (the 30522-wide MLM head)
+      uint32_t* C2 = reinterpret_cast<uint32_t*>(Ch);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        C2[t] = (uint32_t)f_to_bf16_bits(v[2 * t]) | ((uint32_t)f_to_bf16_bits(v[2 * t + 1]) << 16);
     } else {
       for (int t = 0; t < 8; ++t)
         if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);

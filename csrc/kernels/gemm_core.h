@@ -672,9 +672,12 @@ __device__ __forceinline__ void lds_barrier() {
 // 2: 128x64 tile (waves 64x32) for the 64-channel convolutions, where half of a 128-wide
 // tile's MFMAs would multiply zero columns.  The B image keeps its 128-row staging map
 // (rows past the tile are in-range neighbours or range-checked zeros, never read).
+// ST == 1 is also the high-occupancy form for short-K, memory-bound shapes (1x1 convolutions,
+// their gradient joins): one 32 KiB LDS buffer restaged per K-tile behind a barrier and at most
+// 128 VGPRs, so 4 blocks share a CU and hide each other's DMA / epilogue latency.
 template <class LA, class LB, int ST, int WN = 4>
-__global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
-                                                  int64_t K, int tiles_m, int tiles_n, int ktps) {
+__global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
+                                                                     int64_t K, int tiles_m, int tiles_n, int ktps) {
   constexpr bool DB = ST >= 2;
   constexpr int TBN = 32 * WN;                 // block tile columns
   constexpr int TPR = TBN / 8;                 // epilogue threads per row (8 columns each)
@@ -733,8 +736,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    if (kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
+    const int cur = DB ? (kt - kt0) & 1 : 0;
+    if (DB && kt + 1 < kt1) stage(kt + 1, cur ^ 1);  // in flight during this tile's MFMAs
     const char* As = smem_raw + cur * buf_stride;
     const char* Bs = As + TILE_BYTES;
 #pragma unroll
@@ -752,6 +755,11 @@ __global__ __launch_bounds__(NT) void gemm_kernel(LA la, LB lb, Epi ep, int64_t 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (!DB && kt + 1 < kt1) {   // single buffer: restage once every wave has read it
+      stage(kt + 1, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // bf16 Cin (residual / gradient join, beta): all of this thread's Cin row pieces are
@@ -1187,10 +1195,11 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
 }
 
 // tile: 0 = 128x128 (4 waves, 2 LDS stages, 2 blocks per CU), 1 = 256x256 (8 waves, 1 block
-// per CU), 2 = 128x64 (4 waves of 64x32; 64-channel convolutions).
+// per CU), 2 = 128x64 (4 waves of 64x32; 64-channel convolutions), 3 = 128x128 single LDS
+// stage at 4 blocks per CU (short-K, memory-bound shapes).
 template <class LA, class LB, int WN>
 static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
-                    int batch, int splitk, hipStream_t st) {
+                    int batch, int splitk, hipStream_t st, bool single_stage = false) {
   constexpr int TBN = 32 * WN;
   int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + TBN - 1) / TBN);
   int nkt = (int)((K + BK - 1) / BK);
@@ -1208,7 +1217,7 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
     e1.slab = nullptr;
     if (splitk > 1) e1.atomic = 1;
   }
-  if (ktps > 1)
+  if (ktps > 1 && !single_stage)
     hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n,
                        ktps);
   else
@@ -1223,6 +1232,7 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
                   int batch, int splitk, hipStream_t st, int tile = 0) {
   if (tile == 1) return launch_big(la, lb, ep, M, N, K, batch, splitk, st);
   if (tile == 2) return launch_t<LA, LB, 2>(la, lb, ep, M, N, K, batch, splitk, st);
+  if (tile == 3) return launch_t<LA, LB, 4>(la, lb, ep, M, N, K, batch, splitk, st, true);
   return launch_t<LA, LB, 4>(la, lb, ep, M, N, K, batch, splitk, st);
 }
 

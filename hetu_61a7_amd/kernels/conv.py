@@ -68,6 +68,12 @@ def _copy_into(dst, src):
     return copy_into(dst, src)
 
 
+def _short_k(k):
+    """reduction length for which the single-stage, 4-blocks-per-CU tile (tile 3) is a
+    candidate: short-K convolutions are bound by their operand / output streams"""
+    return k <= 512
+
+
 def _add_cl(a, b):
     """a + b for 4-D activations on the native elementwise kernels, channels-last out
     (the NHWC views are dense, so the vector path runs; strided b takes the N-d kernel)"""
@@ -152,6 +158,8 @@ def conv2d_with_stats(x, w, stride, padding):
         cands['hip256'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=1, colstats=s))
     if co <= 64:
         cands['hip64'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=2, colstats=s))
+    if _short_k(w.shape[1] * w.shape[2] * w.shape[3]):
+        cands['hip_lo'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=3, colstats=s))
     if conv_igemm.stem_ok(x, w, stride, padding):
         cands['hip_stem'] = fused(lambda s: conv_igemm.try_stem_forward(x, w, stride, padding, colstats=s))
     if _plain_1x1((x, w), w.shape, stride, padding):
@@ -256,6 +264,9 @@ def conv2d(x, w, b, stride, padding):
         if w.shape[0] <= 64:    # 128x64 tile: no MFMAs on zero output channels
             blas = dict(blas or {})
             blas['hip64'] = lambda: conv_igemm.try_forward(x, w, stride, padding, tile=2)
+        if _short_k(w.shape[1] * w.shape[2] * w.shape[3]):
+            blas = dict(blas or {})
+            blas['hip_lo'] = lambda: conv_igemm.try_forward(x, w, stride, padding, tile=3)
         y = _pick(('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding)),
                   lambda: conv_igemm.try_forward(x, w, stride, padding),
                   lambda: F.conv2d(x, w, None, stride, padding), blas)
@@ -328,6 +339,9 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
         if x_shape[1] <= 64:
             blas = dict(blas or {})
             blas['hip64'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=2)
+        if _short_k(w.shape[0] * w.shape[2] * w.shape[3]):
+            blas = dict(blas or {})
+            blas['hip_lo'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=3)
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
                      lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
                      lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas, tuned)

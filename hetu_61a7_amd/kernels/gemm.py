@@ -49,6 +49,8 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
             cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
         if a.dtype == torch.bfloat16 and _tr(b, tb).shape[-1] <= 64:
             cands['hip64'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=2)
+        if a.dtype == torch.bfloat16 and _tr(a, ta).shape[-1] <= 512:   # short K: the 4-blocks-per-CU tile
+            cands['hip_lo'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=3)
         cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
         if bias is not None:
             # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
@@ -243,6 +245,8 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
         cands = {'hip': hip, 'vendor': vendor}
         if A.shape[0] >= 256 and B.shape[1] >= 256:
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=1)
+        if A.shape[1] <= 512:
+            cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=3)
         ch = choose(key, cands, _MFMA)
         dst[0] = c
         if ch != 'vendor':

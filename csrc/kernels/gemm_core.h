@@ -584,7 +584,9 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
 
 __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (&v)[8], int64_t m, int64_t n,
                                          int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8],
-                                         const uint4* cpre = nullptr) {
+                                         bool has_pre = false, uint4 pre = uint4{}) {
+  // pre: this row piece of Cin, already loaded (by value: a selected pointer into the
+  // caller's prefetch array would keep that array in scratch memory)
   const bool full = n + 7 < N;
   if (ep.bias) {
     const float bm = ep.bias_on_m ? ep.bias[m] : 0.f;
@@ -594,8 +596,8 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
   if (o.Cinb) {
     const int64_t off = orow * ep.ldcin + n;
     float cv[8];
-    if (cpre && o.ivec && full && !ep.cin_f32) {
-      const uint32_t w[4] = {cpre->x, cpre->y, cpre->z, cpre->w};
+    if (has_pre && o.ivec && full && !ep.cin_f32) {
+      const uint32_t w[4] = {pre.x, pre.y, pre.z, pre.w};
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         cv[2 * t] = bf16_bits_to_f((unsigned short)(w[t] & 0xffffu));
@@ -762,24 +764,27 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
     }
   }
 
-  // bf16 Cin (residual / gradient join, beta): all of this thread's Cin row pieces are
-  // requested at once before the LDS staging of the epilogue -- one memory latency
-  // instead of one per 16-row pass (the short-K 1x1 data-gradient joins were all
-  // epilogue latency).  Issuing them before the K loop instead measured slower: they
-  // queue ahead of the operand DMA that the first K-tile waits for.
-  uint4 cpre[2][NPASS];
-  const bool use_pre = eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec;
+  // bf16 Cin (residual / gradient join, beta): this thread's Cin row pieces of the first
+  // 64-row half are requested at once before the LDS staging of the epilogue -- one memory
+  // latency instead of one per 16-row pass (the short-K 1x1 data-gradient joins were all
+  // epilogue latency) -- and each second-half piece is requested as soon as its first-half
+  // register is consumed: 16 registers instead of 32, so the 4-blocks-per-CU tile does not
+  // spill them.  Issuing them before the K loop instead measured slower: they queue ahead
+  // of the operand DMA that the first K-tile waits for.
+  // (not in the single-stage 4-blocks-per-CU build: at 128 registers the prefetch spills,
+  // and its neighbours on the CU hide the epilogue latency instead)
+  uint4 cpre[NPASS];
+  const bool use_pre = ST == 2 && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec;
+  const int64_t pre_n = (int64_t)tn * TBN + ec;
+  auto pre_load = [&](int h, int pss) {
+    const int64_t m = (int64_t)tm * BM + h * 64 + pss * RPP + tid / TPR;
+    cpre[pss] = (m < Mb && pre_n + 7 < N)
+                    ? *reinterpret_cast<const uint4*>((const bf16*)eo.Cinb + la.out_row(m) * ep.ldcin + pre_n)
+                    : make_uint4(0, 0, 0, 0);
+  };
   if (use_pre) {
-    const int64_t n = (int64_t)tn * TBN + ec;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int pss = 0; pss < NPASS; ++pss) {
-        const int64_t m = (int64_t)tm * BM + h * 64 + pss * RPP + tid / TPR;
-        cpre[h][pss] = (m < Mb && n + 7 < N)
-                           ? *reinterpret_cast<const uint4*>((const bf16*)eo.Cinb + la.out_row(m) * ep.ldcin + n)
-                           : make_uint4(0, 0, 0, 0);
-      }
+    for (int pss = 0; pss < NPASS; ++pss) pre_load(0, pss);
   }
 
   // epilogue: lane holds C[m][n..n+3]
@@ -834,15 +839,15 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
         const int rr = pss * RPP + tid / TPR;
         const int64_t m = (int64_t)tm * BM + half * 64 + rr;
         const int64_t n = (int64_t)tn * TBN + ec;
-        if (m >= Mb || n >= N) continue;
-        float v[8];
-        {
+        if (m < Mb && n < N) {
+          float v[8];
           v4f a0 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec);
           v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec + 4);
 #pragma unroll
           for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
+          epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss]);
         }
-        epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre ? &cpre[half][pss] : nullptr);
+        if (use_pre && half == 0) pre_load(1, pss);
       }
       __syncthreads();
     }

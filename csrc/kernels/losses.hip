@@ -86,14 +86,19 @@ __global__ void __launch_bounds__(256) bce_grad_k(const T* __restrict__ y, const
   }
 }
 
+// class index of a label held as int64, int32 or a float (the data loaders' label tensors
+// reach the loss in whatever dtype they were fed: no conversion kernel in front of it)
+template <typename L>
+__device__ __forceinline__ int64_t lab_idx(const L* t, int64_t r) { return (int64_t)t[r]; }
+
 // out[0] += -sum_r x[r, t[r]] / rows  (out zeroed by the caller)
-template <typename T>
-__global__ void __launch_bounds__(256) nll_k(const T* __restrict__ x, const int64_t* __restrict__ t,
+template <typename T, typename L>
+__global__ void __launch_bounds__(256) nll_k(const T* __restrict__ x, const L* __restrict__ t,
                                              float* __restrict__ out, int64_t rows, int64_t cols) {
   __shared__ float sh[4];
   float s = 0.f;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = t[r];
+    const int64_t c = lab_idx(t, r);
     if (c >= 0 && c < cols) s += to_f(x[r * cols + c]);
   }
   s = block_sum<256>(s, sh);
@@ -101,13 +106,14 @@ __global__ void __launch_bounds__(256) nll_k(const T* __restrict__ x, const int6
 }
 
 // dx[r, c] = c == t[r] ? -g / rows : 0
-__global__ void __launch_bounds__(256) nll_grad_k(const float* __restrict__ g, const int64_t* __restrict__ t,
+template <typename L>
+__global__ void __launch_bounds__(256) nll_grad_k(const float* __restrict__ g, const L* __restrict__ t,
                                                   float* __restrict__ dx, int64_t rows, int64_t cols) {
   const int64_t total = rows * cols;
   const float v = -g[0] / (float)rows;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cols;
-    dx[i] = (i - r * cols) == t[r] ? v : 0.f;
+    dx[i] = (i - r * cols) == lab_idx(t, r) ? v : 0.f;
   }
 }
 
@@ -167,18 +173,37 @@ HETU_API int hetu_bce_grad(const void* y, const void* lab, const float* g, void*
   return (int)hipGetLastError();
 }
 
-// out: one fp32, zeroed by the caller
-HETU_API int hetu_nll(const void* x, const int64_t* t, float* out, int64_t rows, int64_t cols, int bf, hipStream_t st) {
+// out: one fp32, zeroed by the caller; tkind: label dtype 0 = int64, 1 = int32, 2 = fp32
+template <typename T, typename L>
+static void nll_launch(const void* x, const void* t, float* out, int64_t rows, int64_t cols, int nb, hipStream_t st) {
+  hipLaunchKernelGGL((nll_k<T, L>), dim3(nb), dim3(256), 0, st, (const T*)x, (const L*)t, out, rows, cols);
+}
+
+HETU_API int hetu_nll(const void* x, const void* t, int tkind, float* out, int64_t rows, int64_t cols, int bf,
+                      hipStream_t st) {
   if (rows == 0) return 0;
+  if (tkind < 0 || tkind > 2) return (int)hipErrorInvalidValue;
   int nb = (int)((rows + 255) / 256);
   if (nb > 256) nb = 256;
-  if (bf) hipLaunchKernelGGL(nll_k<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)x, t, out, rows, cols);
-  else hipLaunchKernelGGL(nll_k<float>, dim3(nb), dim3(256), 0, st, (const float*)x, t, out, rows, cols);
+  if (bf) {
+    if (tkind == 0) nll_launch<bf16, int64_t>(x, t, out, rows, cols, nb, st);
+    else if (tkind == 1) nll_launch<bf16, int32_t>(x, t, out, rows, cols, nb, st);
+    else nll_launch<bf16, float>(x, t, out, rows, cols, nb, st);
+  } else {
+    if (tkind == 0) nll_launch<float, int64_t>(x, t, out, rows, cols, nb, st);
+    else if (tkind == 1) nll_launch<float, int32_t>(x, t, out, rows, cols, nb, st);
+    else nll_launch<float, float>(x, t, out, rows, cols, nb, st);
+  }
   return (int)hipGetLastError();
 }
 
-HETU_API int hetu_nll_grad(const float* g, const int64_t* t, float* dx, int64_t rows, int64_t cols, hipStream_t st) {
+HETU_API int hetu_nll_grad(const float* g, const void* t, int tkind, float* dx, int64_t rows, int64_t cols,
+                           hipStream_t st) {
   if (rows * cols == 0) return 0;
-  hipLaunchKernelGGL(nll_grad_k, dim3(stream_grid(rows * cols, 256, 2)), dim3(256), 0, st, g, t, dx, rows, cols);
+  if (tkind < 0 || tkind > 2) return (int)hipErrorInvalidValue;
+  const dim3 gr(stream_grid(rows * cols, 256, 2));
+  if (tkind == 0) hipLaunchKernelGGL(nll_grad_k<int64_t>, gr, dim3(256), 0, st, g, (const int64_t*)t, dx, rows, cols);
+  else if (tkind == 1) hipLaunchKernelGGL(nll_grad_k<int32_t>, gr, dim3(256), 0, st, g, (const int32_t*)t, dx, rows, cols);
+  else hipLaunchKernelGGL(nll_grad_k<float>, gr, dim3(256), 0, st, g, (const float*)t, dx, rows, cols);
   return (int)hipGetLastError();
 }

@@ -24,9 +24,8 @@ def _sig(t):
 
 def _match(a, b):
     if a.dtype != b.dtype:
-        if torch.bfloat16 in (a.dtype, b.dtype):
-            return a.to(torch.bfloat16), b.to(torch.bfloat16)
-        return a.to(torch.float32), b.to(torch.float32)
+        dt = torch.bfloat16 if torch.bfloat16 in (a.dtype, b.dtype) else torch.float32
+        return _as_dtype(a, dt), _as_dtype(b, dt)
     return a, b
 
 
@@ -87,6 +86,9 @@ def _as_dtype(t, dt):
     sh = getattr(t, 'hetu_bf16', None)
     if sh is not None and sh.dtype == dt:
         return sh
+    if t.is_cuda:   # the native cast, keeping a dense operand's stride order
+        from .tensor import copy_into
+        return copy_into(torch.empty_like(t, dtype=dt), t)
     return t.to(dt)
 
 

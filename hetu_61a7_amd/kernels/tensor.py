@@ -346,22 +346,37 @@ def bce_grad(y, lab, g):
     return dy
 
 
+_LABEL_KIND = {torch.int64: 0, torch.int32: 1, torch.float32: 2}
+
+
+def _labels(t):
+    """labels as the kernels read them (int64 / int32 / fp32 class indices), converting only
+    another dtype"""
+    t = t.reshape(-1)
+    if t.dtype not in _LABEL_KIND:
+        t = t.long()
+    return t.contiguous(), _LABEL_KIND[t.dtype]
+
+
 def nll(x, t, cols):
     x = x.reshape(-1, cols).contiguous()
-    t = t.long().reshape(-1).contiguous()
+    t, tk = _labels(t)
     out = zeros((1,), torch.float32, x.device)
-    check(fn('hetu_nll', [P, P, P, I64, I64, I32, P])(x.data_ptr(), t.data_ptr(), out.data_ptr(), x.shape[0], cols,
-                                                       _bf(x), stream_ptr()), 'nll')
+    check(fn('hetu_nll', [P, P, I32, P, I64, I64, I32, P])(x.data_ptr(), t.data_ptr(), tk, out.data_ptr(),
+                                                            x.shape[0], cols, _bf(x), stream_ptr()), 'nll')
     record_native('nll')
     return out
 
 
 def nll_grad(g, t, cols):
-    t = t.long().reshape(-1).contiguous()
-    g = g.float().reshape(-1)[:1].contiguous()
+    t, tk = _labels(t)
+    g = g.reshape(-1)[:1]
+    if g.dtype != torch.float32:
+        g = g.float()
     dx = torch.empty((t.numel(), cols), dtype=torch.float32, device=t.device)
-    check(fn('hetu_nll_grad', [P, P, P, I64, I64, P])(g.data_ptr(), t.data_ptr(), dx.data_ptr(), t.numel(), cols,
-                                                       stream_ptr()), 'nll_grad')
+    check(fn('hetu_nll_grad', [P, P, I32, P, I64, I64, P])(g.data_ptr(), t.data_ptr(), tk, dx.data_ptr(), t.numel(),
+                                                            cols, stream_ptr()), 'nll_grad')
+    record_native('nll_grad')
     return dx
 
 

@@ -306,7 +306,7 @@ class HetuConfig(object):
         if not isinstance(t, torch.Tensor):
             return t
         if self.mixed_precision and t.dtype == torch.float32 and t.is_cuda and not node.trainable \
-                and t.dim() >= 2:
+                and t.dim() >= 2 and not getattr(node, 'keep_fp32', False):
             v = t.to(torch.bfloat16)
             self.compute_values[node] = v
             return v

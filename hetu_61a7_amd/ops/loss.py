@@ -115,9 +115,16 @@ def softmaxcrossentropy_gradient_op(node_A, node_B, node_C, use_cudnn=True, fwd=
     return SoftmaxCrossEntropyGradientOp(node_A, node_B, node_C, fwd=fwd, ctx=ctx)
 
 
+def _label_feed(node):
+    """class-index targets fed as fp32 stay fp32 under mixed precision: bf16 holds integers
+    exactly only up to 256, so the feed cast would move vocabulary / token ids"""
+    node.keep_fp32 = True
+
+
 class SoftmaxCrossEntropySparseOp(Op):
     def __init__(self, x, y_, ignored_index=-1, ctx=None):
         super().__init__(SoftmaxCrossEntropySparseOp, [x, y_], ctx)
+        _label_feed(y_)
         self.ignored_index = ignored_index
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
@@ -207,6 +214,7 @@ def crossentropy_gradient_op(node_grad, node_y, node_y_, ctx=None):
 class CrossEntropySparseOp(Op):
     def __init__(self, y, y_, ignored_index=-1, ctx=None):
         super().__init__(CrossEntropySparseOp, [y, y_], ctx)
+        _label_feed(y_)
         self.ignored_index = ignored_index
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
@@ -313,6 +321,7 @@ class NllLossOp(Op):
 
     def __init__(self, inp, target, cols, ctx=None):
         super().__init__(NllLossOp, [inp, target], ctx)
+        _label_feed(target)
         self.cols = cols
 
     def compute(self, input_vals, output_val=None, stream_handle=None):

@@ -113,6 +113,10 @@ def test_losses_match_torch():
     ref_n = torch.zeros(rows, cols)
     ref_n[torch.arange(rows), t.clamp_min(0).cpu()] = -0.7 / rows
     _close(KT.nll_grad(gs, t.clamp_min(0), cols).cpu(), ref_n, 1e-6)
+    for ldt in (torch.int32, torch.float32):    # labels read in the dtype they were fed
+        tl = t.clamp_min(0).to(ldt)
+        _close(KT.nll(lp, tl, cols).cpu(), F.nll_loss(lp, t.clamp_min(0)).reshape(1).cpu(), 1e-5)
+        _close(KT.nll_grad(gs, tl, cols).cpu(), ref_n, 1e-6)
 
 
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])

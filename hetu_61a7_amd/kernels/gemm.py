@@ -48,7 +48,7 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
             cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
         if a.dtype == torch.bfloat16 and _tr(b, tb).shape[-1] <= 64:
             cands['hip64'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=2)
-        if a.dtype == torch.bfloat16 and _tr(a, ta).shape[-1] <= 512:   # short K: the 4-blocks-per-CU tile
+        if a.dtype == torch.bfloat16 and _tr(a, ta).shape[-1] <= 2048:   # short K: the 4-blocks-per-CU tile
             cands['hip_lo'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=3)
         cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
         if bias is not None:
@@ -247,7 +247,7 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
         cands = {'hip': hip, 'vendor': vendor}
         if A.shape[0] >= 256 and B.shape[1] >= 256:
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=1)
-        if A.shape[1] <= 512:
+        if A.shape[1] <= 2048:
             cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=3)
         ch = choose(key, cands, _MFMA)
         dst[0] = c

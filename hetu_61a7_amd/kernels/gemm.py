@@ -237,20 +237,28 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
             and _MFMA not in ('off', 'vendor'):
         from . import gemm_mfma
         from .autotune import choose, _decisions
-        c = acc.to(a.dtype) if acc.dtype != a.dtype else acc
+        # the MFMA epilogue reads an fp32 acc as it is; the library GEMM gets it cast
+        # (natively) to the operand dtype, once, only if it runs
+        cc = [acc if acc.dtype == a.dtype else None]
+
+        def c():
+            if cc[0] is None:
+                from .tensor import copy_into
+                cc[0] = copy_into(torch.empty_like(acc, dtype=a.dtype), acc)
+            return cc[0]
         key = ('gemm_acc', _sig(a), _sig(b), ta, tb)
-        inplace = inplace and c is acc and c.is_contiguous()
+        inplace = inplace and acc.dtype == a.dtype and acc.is_contiguous()
         # while the shape is timed, the in-place candidate accumulates into scratch
-        dst = [c.clone() if inplace and key not in _decisions and _MFMA != 'hip' else c]
-        hip = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0)
-        vendor = (lambda: dst[0].addmm_(A, B)) if inplace else (lambda: torch.addmm(c, A, B))
+        dst = [acc.clone() if inplace and key not in _decisions and _MFMA != 'hip' else acc]
+        hip = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0)
+        vendor = (lambda: dst[0].addmm_(A, B)) if inplace else (lambda: torch.addmm(c(), A, B))
         cands = {'hip': hip, 'vendor': vendor}
         if A.shape[0] >= 256 and B.shape[1] >= 256:
-            cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=1)
+            cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=1)
         if A.shape[1] <= 2048:
-            cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=c, beta=1.0, tile=3)
+            cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=3)
         ch = choose(key, cands, _MFMA)
-        dst[0] = c
+        dst[0] = acc
         if ch != 'vendor':
             y = cands[ch]()
             if y is not None:

@@ -31,6 +31,7 @@ def main():
     p.add_argument('--model', default='resnet50', choices=['resnet50', 'bert', 'moe', 'wdl'])
     p.add_argument('--batch', type=int, default=None)
     p.add_argument('--steps', type=int, default=3)
+    p.add_argument('--tiny', action='store_true', help='bert: the 2-layer config of tests/test_native_dispatch_gpu.py')
     a = p.parse_args()
     os.environ['HETU_PROFILE_OPS'] = '1'
     import torch
@@ -39,6 +40,12 @@ def main():
         (['--batch', str(a.batch)] if a.batch else [])
     import bench
     args = bench.parse()
+    if a.tiny:
+        from hetu_61a7_amd.models.bert import BertConfig
+        args.bert_config = BertConfig(vocab_size=8192, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                                      intermediate_size=1024, max_position_embeddings=128)
+        args.bert_config.seq_len = 128
+        args.batch = 8
     import hetu_61a7_amd as ht  # noqa: F401
     step = _build(args)
     for _ in range(a.steps):

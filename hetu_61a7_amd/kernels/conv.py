@@ -71,7 +71,7 @@ def _copy_into(dst, src):
 def _short_k(k):
     """reduction length for which the single-stage, 4-blocks-per-CU tile (tile 3) is a
     candidate: short-K convolutions are bound by their operand / output streams"""
-    return k <= 2048
+    return k <= 4608
 
 
 def _add_cl(a, b):

@@ -143,7 +143,7 @@ int main(int argc, char** argv) {
     const int64_t ldb = s.tb ? s.K : s.N;
     struct Var { std::string name; int tile; };
     std::vector<Var> vars = {{"blas", -1}};
-    for (int t : {0, 1, 2}) {
+    for (int t : {0, 1, 2, 3}) {
 #ifdef BENCH_FAST
       if (t == 0 || t == 2) continue;
 #endif

@@ -60,11 +60,24 @@ HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const
 
 // dw[K, KH*KW*C] fp32 (+)= sum over output pixels dy^T x_im2col.  Split-K over
 // the pixel axis into fp32 slabs (ws: splitk*K*KH*KW*C floats) + one reduce; no atomics.
+// tile 0-3: the gemm_core tiles with M = K, N = KH*KW*C; tile 4: roles swapped (K <= 64).
 HETU_API int hetu_conv_wgrad_bf16(const void* dy, const void* x, float* dw, int N, int H, int W,
                                   int C, int K, int KH, int KW, int sh, int sw, int ph, int pw,
                                   int splitk, int accumulate, float* ws, int tile, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t P = (int64_t)N * g.OH * g.OW, Nc = (int64_t)KH * KW * C;
+  if (tile == 4) {
+    // roles swapped: M = KH*KW*C filter taps (im2col of x), N = K output channels on the
+    // 128x64 tile, so a 64-channel filter bank fills the tile's N side instead of half
+    // of a 128-row M side; the slabs are reduced transposed into dw[K][Nc]
+    if (!ws || K > 64) return (int)hipErrorInvalidValue;
+    ConvWgradB la{};
+    la.x = (const bf16*)x;
+    la.g = g;
+    la.P = P;
+    return launch_t_transposed<ConvWgradB, PlainMN, 2>(la, PlainMN{(const bf16*)dy, K, K, P, 0}, dw, Nc, accumulate,
+                                                       ws, Nc, K, P, splitk, st);
+  }
   Epi ep{dw, nullptr, nullptr, Nc, 0, 0, 0, 1.f, 0.f, 0, 1, 0, accumulate, 0, splitk > 1 ? ws : nullptr, 0};
   PlainMN la{(const bf16*)dy, K, K, P, 0};
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && buf_ok(P * K * 2, P * C * 2))

@@ -1173,6 +1173,49 @@ static void launch_splitk_reduce(const float* slab, int splitk, void* C, int64_t
                      atomic);
 }
 
+// dst[n][m] (fp32, ld ldd) (+)= sum_z slab[z][m][n]: the reduce of a split-K GEMM that
+// computed the transposed product (role-swapped weight gradients)
+static __global__ void __launch_bounds__(256) splitk_reduce_t_k(const float* __restrict__ slab, int64_t stride,
+                                                               int nz, float* __restrict__ dst, int64_t M,
+                                                               int64_t N, int64_t ldd, int accumulate) {
+  const int64_t total = M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float a0 = 0.f, a1 = 0.f;
+    int z = 0;
+    for (; z + 1 < nz; z += 2) { a0 += slab[z * stride + i]; a1 += slab[(z + 1) * stride + i]; }
+    if (z < nz) a0 += slab[z * stride + i];
+    const int64_t m = i / N, n = i - m * N;
+    float* d = dst + n * ldd + m;
+    *d = accumulate ? *d + (a0 + a1) : (a0 + a1);
+  }
+}
+
+// split-K product into fp32 slabs (ws: splitk * M * N floats) and a transposed reduce
+// into dst[n][m] -- launch_t with the slab forced for every split count
+template <class LA, class LB, int WN>
+static int launch_t_transposed(const LA& la, const LB& lb, float* dst, int64_t ldd, int accumulate, float* ws,
+                               int64_t M, int64_t N, int64_t K, int splitk, hipStream_t st) {
+  constexpr int TBN = 32 * WN;
+  int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + TBN - 1) / TBN);
+  int nkt = (int)((K + BK - 1) / BK);
+  if (splitk < 1) splitk = 1;
+  if (splitk > nkt) splitk = nkt > 0 ? nkt : 1;
+  int ktps = (nkt + splitk - 1) / splitk;
+  splitk = (nkt + ktps - 1) / ktps;
+  Epi ep{nullptr, nullptr, nullptr, N, 0, 0, 0, 1.f, 0.f, 0, 1, 0, 0, 0, ws, M * N, nullptr};
+  dim3 grid(tiles_m * tiles_n, 1, splitk);
+  if (ktps > 1)
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN>), grid, dim3(NT), 0, st, la, lb, ep, M, N, K, tiles_m, tiles_n,
+                       ktps);
+  else
+    hipLaunchKernelGGL((gemm_kernel<LA, LB, 1, WN>), grid, dim3(NT), 0, st, la, lb, ep, M, N, K, tiles_m, tiles_n,
+                       ktps);
+  int nb = (int)std::min<int64_t>((M * N + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_reduce_t_k, dim3(nb), dim3(256), 0, st, ws, M * N, splitk, dst, M, N, ldd, accumulate);
+  return (int)hipGetLastError();
+}
+
 template <class LA, class LB>
 static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
                       int batch, int splitk, hipStream_t st) {

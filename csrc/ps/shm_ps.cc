@@ -81,6 +81,7 @@ struct Header {
   std::atomic<uint32_t> dir_lock;
   std::atomic<int64_t> heartbeat[kMaxNodes];
   std::atomic<int32_t> recovered;   // workers that took over a dead rank
+  std::atomic<int32_t> hb_on;       // some worker refreshes its heartbeat (PS_HEARTBEAT_INTERVAL > 0)
   SspState ssp[kMaxSsp];
   PReduceState pre[kMaxPreduce];
   ParamEntry params[kMaxParams];
@@ -183,7 +184,7 @@ static inline void rec(int psf, int64_t bytes) {
 static std::atomic<int64_t> g_fault[4];   // dropped requests, dropped acks, resends, duplicates
 static std::atomic<uint64_t> g_msg_seq{1};
 static std::mutex g_applied_mu;
-static std::unordered_set<uint64_t> g_applied;   // message ids applied (bounded, see below)
+static std::unordered_set<uint64_t> g_applied;   // ids applied of messages still in delivery
 
 static thread_local std::mt19937_64 tl_rng(std::random_device{}());
 static bool drop_now() {
@@ -196,12 +197,19 @@ template <typename F>
 static int deliver(F&& body) {
   if (DROP_P <= 0.0) return body();
   const uint64_t id = g_msg_seq.fetch_add(1);
+  // the sender learns the final outcome in this process, so the id leaves the applied set
+  // when deliver returns: the set holds only messages still between resends
+  auto done = [id](int r) {
+    std::lock_guard<std::mutex> g(g_applied_mu);
+    g_applied.erase(id);
+    return r;
+  };
+  int applied_r = 0;
   for (int attempt = 0;; ++attempt) {
     if (attempt > 0) {
       g_fault[2].fetch_add(1);
       std::this_thread::sleep_for(std::chrono::milliseconds(RESEND_MS));
     }
-    int r = 0;
     if (drop_now()) {                       // the request is lost on the way
       g_fault[0].fetch_add(1);
     } else {
@@ -209,15 +217,14 @@ static int deliver(F&& body) {
       {
         std::lock_guard<std::mutex> g(g_applied_mu);
         dup = !g_applied.insert(id).second;
-        if (g_applied.size() > (1u << 20)) g_applied.clear();   // ids are only re-sent within 10 tries
       }
       if (dup) g_fault[3].fetch_add(1);     // receiver suppresses the re-sent copy
-      else r = body();
-      if (!drop_now()) return r;            // ack arrives
+      else applied_r = body();
+      if (!drop_now()) return done(applied_r);   // ack arrives
       g_fault[1].fetch_add(1);              // the ack is lost
     }
-    if (!RESEND) return -EIO;
-    if (attempt >= 10) return -ETIMEDOUT;
+    if (!RESEND) return done(-EIO);
+    if (attempt >= 10) return done(-ETIMEDOUT);
   }
 }
 
@@ -384,17 +391,30 @@ int hps_init(int role, const char* name, int num_workers, int num_servers, uint6
     RANK = H->next_worker.fetch_add(1);
     if (RANK >= H->nworkers) {
       // node recovery (reference van.cc:132-160 is_recovery): the cluster is full, so
-      // this process replaces a worker whose heartbeat is older than PS_HEARTBEAT_TIMEOUT
-      double to = 60.0;
-      if (const char* s = getenv("PS_HEARTBEAT_TIMEOUT")) to = atof(s);
-      int dead[kMaxNodes];
-      const int nd = hps_dead_nodes(to, dead, kMaxNodes);
-      if (nd == 0) {
+      // this process replaces a worker whose heartbeat is older than PS_HEARTBEAT_TIMEOUT.
+      // Only when heartbeats are live (some worker refreshes them, or the timeout is set
+      // explicitly): otherwise every worker's heartbeat is its start time and a live
+      // worker would look dead (ps-lite reports no dead nodes at timeout 0, its default).
+      const char* ts = getenv("PS_HEARTBEAT_TIMEOUT");
+      const double to = ts ? atof(ts) : 60.0;
+      RANK = -1;
+      if (to > 0 && (ts || H->hb_on.load())) {
+        int dead[kMaxNodes];
+        const int nd = hps_dead_nodes(to, dead, kMaxNodes);
+        // claim a dead rank by moving its stale heartbeat to now: a concurrent joiner
+        // that read the same stale value loses the exchange and tries the next one
+        for (int i = 0; i < nd && RANK < 0; ++i) {
+          int64_t stale = H->heartbeat[dead[i]].load();
+          if (now_ns() - stale > (int64_t)(to * 1e9) &&
+              H->heartbeat[dead[i]].compare_exchange_strong(stale, now_ns()))
+            RANK = dead[i];
+        }
+      }
+      if (RANK < 0) {
         munmap(p, MAP_BYTES);
         H = nullptr;
         return -EBUSY;
       }
-      RANK = dead[0];
       H->recovered.fetch_add(1);
     }
     int nth = 4;
@@ -404,6 +424,7 @@ int hps_init(int role, const char* name, int num_workers, int num_servers, uint6
     if (const char* s = getenv("PS_HEARTBEAT_INTERVAL")) iv = atof(s);
     H->heartbeat[RANK].store(now_ns());
     if (iv > 0) {
+      H->hb_on.store(1);
       HB = new std::thread([iv] {
         while (!HB_STOP.load()) {
           hps_heartbeat();

@@ -439,10 +439,19 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                 _copy_into(out, d[:, :ci])
                 return out
             blas = {'hip_pad': pad_wgrad}
+            if conv_igemm.stem_ok(x, g.new_empty(w_shape), stride, padding):
+                blas['hip_stem'] = lambda: conv_igemm.try_stem_backward_filter(g, x, w_shape, stride, padding,
+                                                                               out=out)
         if w_shape[0] >= 128:
             blas = dict(blas or {})
             blas['hip256'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                                     accumulate=False, tile=1)
+        if w_shape[0] <= 64:   # 64-channel banks: a 64-wide N side (as is, and with the roles swapped)
+            blas = dict(blas or {})
+            blas['hip64'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
+                                                                   accumulate=False, tile=2)
+            blas['hip64t'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
+                                                                    accumulate=False, tile=4)
         return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
                      lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                             accumulate=False),

@@ -141,6 +141,42 @@ def try_stem_forward(x, w, stride, padding, colstats=None):
     return y.permute(0, 3, 1, 2)
 
 
+STEM_WGRAD_BLOCKS = 512
+
+
+def try_stem_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=False):
+    """Weight gradient of the few-channel stem (``stem.hip``: transpose-read MFMA over
+    LDS-staged input rows, per-block fp32 partials + one reduce) into ``out`` (fp32,
+    channels-last [Cout, C, KH, KW] view) or a new tensor."""
+    co, c, kh, kw = w_shape
+    if not (co == 64 and kw * c <= 24 and kh * 24 <= 176 and stride[0] == stride[1] and padding[0] == padding[1]
+            and (stride[0] * c) % 2 == 0 and x.shape[1] == c and x.dtype == torch.bfloat16
+            and g.dtype == torch.bfloat16 and g.shape[1] == co):
+        return None
+    x = x.contiguous(memory_format=CL)
+    g = g.contiguous(memory_format=CL)
+    N, C, H, W = x.shape
+    OW = (W + 2 * padding[1] - kw) // stride[1] + 1
+    # the kernel stages 16-byte pieces of input rows (W*C % 8) and of 2 dy rows per task
+    if (W * C) % 8 or (stride[0] + kh) * (W * C // 8) > 1024 or 2 * OW * 8 > 2048 or x.data_ptr() % 16 \
+            or g.data_ptr() % 16:
+        return None
+    if out is None:
+        dw = torch.empty((co, kh, kw, c), dtype=torch.float32, device=g.device)
+        accumulate = False
+    else:
+        dw = out.permute(0, 2, 3, 1)
+        if not dw.is_contiguous() or dw.dtype != torch.float32:
+            return None
+    nb = STEM_WGRAD_BLOCKS
+    ws = torch.empty(int(fn('hetu_stem_wgrad_ws', [I32], restype=I64)(nb)), dtype=torch.float32, device=g.device)
+    f = fn('hetu_stem_wgrad', [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P])
+    check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), nb, N, H, W, C, kh, kw, stride[0], padding[0],
+            int(bool(accumulate)), stream_ptr()), 'stem_wgrad')
+    record_native('stem_wgrad')
+    return dw.permute(0, 3, 1, 2)
+
+
 def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0):
     if not _ok(g, w, x_shape[1], w.shape[0]):
         return None
@@ -181,8 +217,11 @@ def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=Non
         dw = out.permute(0, 2, 3, 1)
         assert dw.is_contiguous() and dw.dtype == torch.float32
     Nc = KH * KW * C
-    sk = _splitk(K, Nc, N * OH * OW, tile)
-    ws = torch.empty(sk * K * Nc, dtype=torch.float32, device=g.device) if sk > 1 else None
+    if tile == 4 and K > 64:
+        return None
+    # tile 4 (roles swapped): M = Nc taps on 128-row tiles, N = K channels on 64-col tiles
+    sk = _splitk(Nc, 2 * K, N * OH * OW, 0) if tile == 4 else _splitk(K, Nc, N * OH * OW, tile)
+    ws = torch.empty(sk * K * Nc, dtype=torch.float32, device=g.device) if (sk > 1 or tile == 4) else None
     # a single slice without accumulation stores straight into dw (plain fp32 epilogue,
     # no zero fill + atomics)
     f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, I32, P, I32, P])

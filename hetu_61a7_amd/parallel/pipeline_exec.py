@@ -31,9 +31,11 @@ MI355X design
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List
 
 import numpy as np
+
 import torch
 import torch.distributed as dist
 
@@ -70,14 +72,23 @@ class _P2P(object):
     synchronisation -- and caches it, and every later micro-batch of the step sends the
     payload alone, received into a buffer of the cached shape.  All payload sends of a
     phase go out as one RCCL group (batch_isend_irecv), so do all payload receives whose
-    shapes are known.  ``hdr_syncs`` counts the header reads (tests)."""
+    shapes are known.  ``hdr_syncs`` counts the header reads (tests).
 
-    def __init__(self, device, comm=None):
+    The protocol is symmetric by construction: with static shapes (default) the
+    sender raises if a later micro-batch of a key changes shape within a step (the
+    receiver would post a payload recv of the stale shape); ``dynamic=True``
+    (``HETU_PP_DYNAMIC_SHAPES=1``: short last micro-batches, variable sequence
+    lengths) sends and reads a header with every message."""
+
+    def __init__(self, device, comm=None, dynamic=None):
         self.device = device
         self.comm = comm
         self.pending = []
         self.shapes = {}        # key -> (shape, dtype) known for this step
         self.hdr_syncs = 0
+        if dynamic is None:
+            dynamic = os.environ.get('HETU_PP_DYNAMIC_SHAPES', '0') == '1'
+        self.dynamic = dynamic
 
     def new_step(self):
         self.shapes = {}
@@ -93,7 +104,12 @@ class _P2P(object):
         hdrs, ops = [], []
         for key, t, dst in items:
             t = t.contiguous()
-            if self.shapes.get(key) != (tuple(t.shape), t.dtype):
+            sig = (tuple(t.shape), t.dtype)
+            if not self.dynamic and key in self.shapes and self.shapes[key] != sig:
+                raise ValueError('pipeline edge %r changed shape within a step (%s -> %s): the receiver '
+                                 'cached the first shape; set HETU_PP_DYNAMIC_SHAPES=1 (a header per '
+                                 'message) for variable micro-batch shapes' % (key, self.shapes[key], sig))
+            if self.dynamic or key not in self.shapes:
                 hdr = torch.zeros(HDR, dtype=torch.int64)
                 hdr[0] = t.dim()
                 hdr[1] = _DT_INV[t.dtype]
@@ -112,7 +128,7 @@ class _P2P(object):
         out = [None] * len(items)
         hdr_ops, need = [], []
         for j, (key, src) in enumerate(items):
-            if key not in self.shapes:
+            if self.dynamic or key not in self.shapes:
                 hdr = torch.zeros(HDR, dtype=torch.int64, device=self.device)
                 hdr_ops.append(('recv', hdr, src))
                 need.append((j, key, hdr))

@@ -36,7 +36,11 @@ def resnet50_convs():
 
 lines = []
 tot = 0.0
+# CONV_ONLY="ci,H,co,k,s;..." restricts the sweep to those shapes (e.g. "3,224,64,7,2;64,56,64,3,1")
+only = [tuple(int(v) for v in t.split(',')) for t in os.environ.get('CONV_ONLY', '').split(';') if t]
 for (ci, H, co, k, st, p), cnt in sorted(resnet50_convs().items()):
+    if only and (ci, H, co, k, st) not in only:
+        continue
     x = torch.randn(N, ci, H, H, device='cuda', dtype=torch.bfloat16).contiguous(memory_format=CL)
     w = (torch.randn(co, ci, k, k, device='cuda') * 0.05).to(torch.bfloat16).contiguous(memory_format=CL)
     y = F.conv2d(x, w, None, st, p)

@@ -15,6 +15,14 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
 
 
+def _tol(y):
+    """bound on the relative-norm error against fp32 math on the same bf16 operands:
+    bf16 x bf16 products are exact in fp32 and the fp32 accumulation error is ~1e-7 *
+    sqrt(K), so a bf16 output is off by its own rounding (rms ~2^-9 relative) and an fp32
+    output by almost nothing.  A dropped K-tail or a 0.5 % systematic error fails."""
+    return 4e-3 if y.dtype == torch.bfloat16 else 2e-5
+
+
 @pytest.mark.parametrize('tile', G.TILES)
 @pytest.mark.parametrize('ta', [False, True])
 @pytest.mark.parametrize('tb', [False, True])
@@ -27,7 +35,7 @@ def test_gemm_modes(ta, tb, mnk, tile):
     y = G.gemm(a, b, tile=tile)
     assert y is not None
     ref = a.float() @ b.float()
-    assert _rel(y, ref) < 1e-2
+    assert _rel(y, ref) < _tol(y)
 
 
 @pytest.mark.parametrize('tile', G.TILES)
@@ -44,7 +52,7 @@ def test_gemm_epilogue(act, tile):
         ref = torch.relu(ref)
     elif act == 'gelu':
         ref = F.gelu(ref)
-    assert _rel(y, ref) < 1e-2
+    assert _rel(y, ref) < _tol(y)
 
 
 @pytest.mark.parametrize('tile', G.TILES)
@@ -52,22 +60,23 @@ def test_gemm_batched_and_splitk(tile):
     a = torch.randn(6, 128, 64, device=DEV).bfloat16()
     b = torch.randn(6, 128, 64, device=DEV).bfloat16().transpose(1, 2)  # [6, 64, 128]
     y = G.gemm(a, b, tile=tile)
-    assert _rel(y, a.float() @ b.float()) < 1e-2
+    assert _rel(y, a.float() @ b.float()) < _tol(y)
     x = torch.randn(8192, 96, device=DEV).bfloat16()
     g = torch.randn(8192, 136, device=DEV).bfloat16()
     out = torch.zeros(96, 136, device=DEV)
     G.gemm(x.t(), g, out=out, accumulate=True, splitk=16, tile=tile)
-    assert _rel(out, x.float().t() @ g.float()) < 1e-2
+    assert _rel(out, x.float().t() @ g.float()) < _tol(out)
     # split-K through fp32 slabs + reduce (bf16 output)
     y2 = G.gemm(x.t(), g, splitk=4, tile=tile)
-    assert _rel(y2, x.float().t() @ g.float()) < 1e-2
+    assert _rel(y2, x.float().t() @ g.float()) < _tol(y2)
 
 
 CONV_SHAPES = [  # N, C, H, K, k, stride, pad
     (4, 64, 14, 64, 1, 1, 0), (4, 64, 14, 128, 3, 1, 1), (4, 128, 15, 64, 3, 2, 1),
     (2, 256, 14, 128, 1, 2, 0), (2, 8, 32, 64, 7, 2, 3), (3, 72, 9, 40, 3, 1, 0),
     (2, 64, 16, 64, 3, 2, 1), (2, 32, 13, 64, 5, 2, 2), (2, 64, 11, 32, 3, 3, 1),
-    (2, 64, 13, 128, 3, 2, 1), (2, 192, 9, 64, 3, 1, 1), (2, 128, 7, 192, 3, 1, 1)]
+    (2, 64, 13, 128, 3, 2, 1), (2, 192, 9, 64, 3, 1, 1), (2, 128, 7, 192, 3, 1, 1),
+    (2, 512, 7, 512, 3, 1, 1)]   # K = 3*3*512 = 4608: the tile-3 (short-K) candidacy edge
 
 
 @pytest.mark.parametrize('tile', G.TILES)
@@ -81,17 +90,37 @@ def test_conv_passes(shape, tile):
     wf = w.float().requires_grad_(True)
     ref = F.conv2d(xf, wf, None, s, p)
     assert y is not None and y.is_contiguous(memory_format=CL)
-    assert _rel(y, ref) < 1e-2
+    assert _rel(y, ref) < _tol(y)
     dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
     ref.backward(dy.float())
     dx = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p), tile=tile)
-    assert dx is not None and _rel(dx, xf.grad) < 1e-2
+    assert dx is not None and _rel(dx, xf.grad) < _tol(dx)
     r = torch.randn_like(x)
     dx2 = CI.try_backward_data(dy, w, x.shape, (s, s), (p, p), acc=r, tile=tile)
-    assert dx2 is not None and _rel(dx2, xf.grad + r.float()) < 1e-2
+    assert dx2 is not None and _rel(dx2, xf.grad + r.float()) < _tol(dx2)
     dw = CI.try_backward_filter(dy, x, w.shape, (s, s), (p, p), tile=tile)
     assert dw is not None and dw.dtype == torch.float32
-    assert _rel(dw, wf.grad) < 1e-2
+    assert _rel(dw, wf.grad) < _tol(dw)
+
+
+@pytest.mark.parametrize('tile', [2, 4])
+@pytest.mark.parametrize('shape', [s for s in CONV_SHAPES if s[3] <= 64] + [(3, 64, 56, 64, 3, 1, 1)])
+@pytest.mark.parametrize('accumulate', [False, True])
+def test_conv_wgrad_64_channel_tiles(shape, tile, accumulate):
+    """64-channel weight gradients on the 128x64 tile, as is (2) and with the roles
+    swapped (4: filter taps on M, the transposed slab reduce into dw[K][taps])."""
+    N, C, H, K, k, s, p = shape
+    x = torch.randn(N, C, H, H, device=DEV).bfloat16().contiguous(memory_format=CL)
+    wf = torch.zeros(K, C, k, k, device=DEV, requires_grad=True)
+    ref = F.conv2d(x.float(), wf, None, s, p)
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
+    ref.backward(dy.float())
+    out = torch.randn(K, C, k, k, device=DEV).contiguous(memory_format=CL)
+    base = out.clone()
+    dw = CI.try_backward_filter(dy, x, (K, C, k, k), (s, s), (p, p), out=out, accumulate=accumulate, tile=tile)
+    assert dw is not None and dw.data_ptr() == out.data_ptr()
+    got = out - base if accumulate else out
+    assert _rel(got, wf.grad) < (1e-4 if accumulate else 2e-5)
 
 
 @pytest.mark.parametrize('tile', G.TILES)
@@ -145,7 +174,7 @@ def test_dgrad_join_accumulates_in_place():
             autotune._decisions[key] = forced
         a = acc.clone(memory_format=CL)
         dx = KC.conv2d_backward_data(g, w, (4, 32, 14, 14), (1, 1), (0, 0), acc=a, acc_inplace=True)
-        assert _rel(dx, ref) < 1e-2
+        assert _rel(dx, ref) < _tol(dx)
         if forced == 'blas':
             assert dx.data_ptr() == a.data_ptr() and dx.is_contiguous(memory_format=CL)
         elif autotune._decisions[key] != 'blas':
@@ -166,9 +195,25 @@ def test_matmul_join_accumulates_in_place():
             autotune._decisions[key] = forced
         c = acc.clone()
         y = KG.matmul_acc(a, b, False, True, c, inplace=True)
-        assert _rel(y, ref) < 1e-2
+        assert _rel(y, ref) < _tol(y)
         if forced == 'vendor':
             assert y.data_ptr() == c.data_ptr()
         elif autotune._decisions[key] != 'vendor':
             assert torch.equal(c, acc)
     autotune._decisions.pop(key, None)
+
+
+def test_vendor_dgrad_mixed_layout_regression():
+    """The A/B vendor path (HETU_CONV=vendor) with the operand mix that aborted in round 2:
+    an NCHW fp32 output gradient, a channels-last filter, 3 input channels.  The shape-only
+    placeholder now follows g's layout, so MIOpen sees one layout per call."""
+    from hetu_61a7_amd.kernels import conv as KC
+    for _ in range(3):
+        x = torch.randn(2, 3, 20, 20, device=DEV, requires_grad=True)
+        w = (torch.randn(16, 3, 3, 3, device=DEV) * 0.1).contiguous(memory_format=CL)
+        y = F.conv2d(x, w, None, 1, 1)
+        g = torch.randn_like(y).contiguous()
+        y.backward(g)
+        dx = KC._vendor_dgrad(g, w, tuple(x.shape), (1, 1), (1, 1))
+        torch.cuda.synchronize()
+        assert _rel(dx, x.grad) < 1e-5

@@ -34,7 +34,7 @@ def parse():
     p.add_argument('--cache', default='LFUOpt')
     p.add_argument('--no-prefetch', dest='prefetch', action='store_false',
                    help='wdl: do not prefetch the next batch rows with the push')
-    p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl', 'bert', 'moe'])
+    p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl', 'bert', 'moe', 'logreg'])
     p.add_argument('--moe-gate', default='topk', choices=['topk', 'dts'])
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     p.add_argument('--bucket-mb', type=float, default=32)
@@ -101,8 +101,10 @@ def main():
     assert world == args.gpus or world == 1, 'launch with --nproc-per-node == --gpus'
     if os.environ.get('HETU_DIST_BACKEND') == 'gloo':
         local = local % torch.cuda.device_count()     # multi-rank rehearsal on one GPU
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    cpu_only = args.model == 'logreg'
+    if not cpu_only:
+        torch.cuda.set_device(local)
+    dev = torch.device('cpu') if cpu_only else torch.device('cuda', local)
 
     finish = None
     if args.model == 'resnet50':
@@ -136,6 +138,9 @@ def main():
     elif args.model == 'bert':
         from hetu_61a7_amd.models.bert import bert_bench
         step, samples_per_step, cfg, metric, finish = bert_bench(args, world, rank, local)
+    elif args.model == 'logreg':
+        from hetu_61a7_amd.models.cnn import logreg_bench
+        step, samples_per_step, cfg, metric, finish = logreg_bench(args, world, rank, local)
     elif args.model == 'moe':
         from hetu_61a7_amd.models.moe import moe_top_bench
         step, samples_per_step, cfg, metric, finish = moe_top_bench(args, world, rank, local)
@@ -148,19 +153,20 @@ def main():
             C.world().barrier()
 
     _progress(rank, world, 'graph built, comm=%s' % (C.world().backend if C.world() is not None else 'none'))
+    sync = (lambda: None) if cpu_only else torch.cuda.synchronize
     for i in range(args.warmup):
         step()
         _progress(rank, world, 'warmup step %d issued' % i)
-    torch.cuda.synchronize()
+    sync()
     _progress(rank, world, 'warmup done')
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     dt_s = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt_s], dtype=torch.float64, device=dev)
@@ -181,15 +187,17 @@ def main():
     if world > 1 or args.comm_trace:
         cfg = dict(cfg)
         cfg['comm'] = C.world().backend if C.world() is not None else 'none'
+        cfg['comm_stats'] = C.stats()
         cfg['grad_wire'] = args.grad_wire
         if args.comm_trace and args.model == 'resnet50':
             tr = [op.comm_trace() for op in ex.optimizer_ops('train')] if hasattr(ex, 'optimizer_ops') else []
             cfg['comm_trace_last_step'] = tr[0] if tr else []
     if rank == 0:
-        out = {'metric': metric, 'value': round(value, 2), 'unit': 'tokens/s' if args.model == 'moe' else 'samples/s', 'n_gpus': world,
+        out = {'metric': metric, 'value': round(value, 2), 'unit': 'tokens/s' if args.model == 'moe' else 'samples/s',
+               'n_gpus': 0 if cpu_only else world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-               'dtype': args.dtype, 'data': 'synthetic (random-init weights)', 'config': cfg}
+               'dtype': 'fp32' if cpu_only else args.dtype, 'data': 'synthetic (random-init weights)', 'config': cfg}
         print(json.dumps(out), flush=True)
     if rank == 0 and os.environ.get('HETU_AUTOTUNE_DUMP'):
         from hetu_61a7_amd.kernels import autotune

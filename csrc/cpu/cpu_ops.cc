@@ -33,7 +33,7 @@ API void hetu_cpu_gemm(const float* A, const float* B, float* C, const float* bi
                        int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int transA, int transB, float alpha,
                        float beta) {
   const int64_t mblocks = (M + MB - 1) / MB, nblocks = (N + NB - 1) / NB;
-#pragma omp parallel
+#pragma omp parallel if(M * N * K >= (1 << 21))
   {
     std::vector<float> bp((size_t)KB * NB);   // packed B panel [kb][nb]
     std::vector<float> ap((size_t)MB * KB);   // packed A block [mb][kb]
@@ -83,7 +83,7 @@ API void hetu_cpu_gemm(const float* A, const float* B, float* C, const float* bi
 
 // loss[r] = -sum_c y[r,c] * log_softmax(x)[r,c]; lse[r] saved for the backward
 API void hetu_cpu_softmax_ce(const float* x, const float* y, float* loss, float* lse, int64_t R, int64_t C) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(R) * (C) >= (1 << 16))
   for (int64_t r = 0; r < R; ++r) {
     const float* xr = x + r * C;
     const float* yr = y + r * C;
@@ -102,7 +102,7 @@ API void hetu_cpu_softmax_ce(const float* x, const float* y, float* loss, float*
 // dx[r,c] = g[r] * (softmax(x)[r,c] * sum_c y - y[r,c])
 API void hetu_cpu_softmax_ce_bwd(const float* x, const float* y, const float* g, const float* lse, float* dx,
                                  int64_t R, int64_t C, int g_scalar) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(R) * (C) >= (1 << 16))
   for (int64_t r = 0; r < R; ++r) {
     const float* xr = x + r * C;
     const float* yr = y + r * C;
@@ -116,7 +116,7 @@ API void hetu_cpu_softmax_ce_bwd(const float* x, const float* y, const float* g,
 
 // elementwise: op 0 relu, 1 sigmoid, 2 tanh, 3 gelu(erf), 4 exp, 5 sqrt
 API void hetu_cpu_unary(int op, const float* x, float* y, int64_t n) {
-#pragma omp parallel for simd schedule(static)
+#pragma omp parallel for simd schedule(static) if((int64_t)(n) >= (1 << 16))
   for (int64_t i = 0; i < n; ++i) {
     const float v = x[i];
     float r;
@@ -134,7 +134,7 @@ API void hetu_cpu_unary(int op, const float* x, float* y, int64_t n) {
 
 // relu'(x) * g
 API void hetu_cpu_relu_grad(const float* x, const float* g, float* y, int64_t n) {
-#pragma omp parallel for simd schedule(static)
+#pragma omp parallel for simd schedule(static) if((int64_t)(n) >= (1 << 16))
   for (int64_t i = 0; i < n; ++i) y[i] = x[i] > 0.f ? g[i] : 0.f;
 }
 
@@ -142,7 +142,7 @@ API void hetu_cpu_relu_grad(const float* x, const float* g, float* y, int64_t n)
 API void hetu_cpu_reduce_rows(const float* x, float* y, int64_t R, int64_t C, float scale) {
   const int nt = omp_get_max_threads();
   std::vector<double> part((size_t)nt * C, 0.0);
-#pragma omp parallel
+#pragma omp parallel if(R * C >= (1 << 16))
   {
     double* p = part.data() + (size_t)omp_get_thread_num() * C;
 #pragma omp for schedule(static)
@@ -159,7 +159,7 @@ API void hetu_cpu_reduce_rows(const float* x, float* y, int64_t R, int64_t C, fl
 // out[i, :] = table[ids[i], :] (out-of-range ids -> 0)
 API void hetu_cpu_gather_rows(const float* table, const int64_t* ids, float* out, int64_t n, int64_t dim,
                               int64_t rows) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(n) >= (1 << 16))
   for (int64_t i = 0; i < n; ++i) {
     const int64_t id = ids[i];
     if (id >= 0 && id < rows)
@@ -173,7 +173,7 @@ API void hetu_cpu_gather_rows(const float* table, const int64_t* ids, float* out
 // 2 nesterov 3 adagrad 4 adam 5 adamw
 API void hetu_cpu_optimizer(int mode, float* p, const float* g, float* s1, float* s2, int64_t n, float lr, float l2,
                             float mu, float b1, float b2, float b1t, float b2t, float eps, float wd, float gscale) {
-#pragma omp parallel for simd schedule(static)
+#pragma omp parallel for simd schedule(static) if((int64_t)(n) >= (1 << 16))
   for (int64_t i = 0; i < n; ++i) {
     const float gr = g[i] * gscale + l2 * p[i];
     switch (mode) {
@@ -212,7 +212,7 @@ struct ConvShape {
 };
 
 void im2col(const ConvShape& s, const float* x, float* col) {
-#pragma omp parallel for collapse(2) schedule(static)
+#pragma omp parallel for collapse(2) schedule(static) if(s.ckk() * s.ohw() >= (1 << 16))
   for (int64_t c = 0; c < s.C; ++c)
     for (int64_t kh = 0; kh < s.KH; ++kh)
       for (int64_t kw = 0; kw < s.KW; ++kw) {
@@ -229,7 +229,7 @@ void im2col(const ConvShape& s, const float* x, float* col) {
 
 // dx[c] += col scattered back (each channel owned by one thread: no races)
 void col2im(const ConvShape& s, const float* col, float* dx) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(s.ckk() * s.ohw() >= (1 << 16))
   for (int64_t c = 0; c < s.C; ++c)
     for (int64_t kh = 0; kh < s.KH; ++kh)
       for (int64_t kw = 0; kw < s.KW; ++kw) {
@@ -266,7 +266,7 @@ API void hetu_cpu_conv2d(const float* x, const float* w, const float* bias, floa
     float* yn = y + n * K * s.ohw();
     hetu_cpu_gemm(w, col.data(), yn, nullptr, K, s.ohw(), s.ckk(), s.ckk(), s.ohw(), s.ohw(), 0, 0, 1.f, 0.f);
     if (bias) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(K * s.ohw() >= (1 << 16))
       for (int64_t k = 0; k < K; ++k)
         for (int64_t i = 0; i < s.ohw(); ++i) yn[k * s.ohw() + i] += bias[k];
     }
@@ -300,7 +300,7 @@ API void hetu_cpu_conv2d_bwd_filter(const float* dy, const float* x, float* dw, 
                   1, 1.f, n == 0 ? 0.f : 1.f);
   }
   if (db) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if(N * K * s.ohw() >= (1 << 16))
     for (int64_t k = 0; k < K; ++k) {
       double a = 0.0;
       for (int64_t n = 0; n < N; ++n)
@@ -314,7 +314,7 @@ API void hetu_cpu_conv2d_bwd_filter(const float* dy, const float* x, float* dw, 
 // max: idx[N*C*OH*OW] keeps the argmax input offset inside the plane for the backward
 API void hetu_cpu_maxpool2d(const float* x, float* y, int32_t* idx, int64_t NC, int64_t H, int64_t W, int64_t KH,
                             int64_t KW, int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t OH, int64_t OW) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(NC) * (H * W) >= (1 << 16))
   for (int64_t p = 0; p < NC; ++p) {
     const float* xp = x + p * H * W;
     for (int64_t oh = 0; oh < OH; ++oh)
@@ -339,7 +339,7 @@ API void hetu_cpu_maxpool2d(const float* x, float* y, int32_t* idx, int64_t NC, 
 
 API void hetu_cpu_maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, int64_t NC, int64_t H, int64_t W,
                                 int64_t OH, int64_t OW) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(NC) * (H * W) >= (1 << 16))
   for (int64_t p = 0; p < NC; ++p) {
     float* dp = dx + p * H * W;
     memset(dp, 0, sizeof(float) * H * W);
@@ -354,7 +354,7 @@ API void hetu_cpu_maxpool2d_bwd(const float* dy, const int32_t* idx, float* dx, 
 API void hetu_cpu_avgpool2d(const float* x, float* y, int64_t NC, int64_t H, int64_t W, int64_t KH, int64_t KW,
                             int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t OH, int64_t OW) {
   const float inv = 1.f / (float)(KH * KW);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(NC) * (H * W) >= (1 << 16))
   for (int64_t p = 0; p < NC; ++p) {
     const float* xp = x + p * H * W;
     for (int64_t oh = 0; oh < OH; ++oh)
@@ -376,7 +376,7 @@ API void hetu_cpu_avgpool2d(const float* x, float* y, int64_t NC, int64_t H, int
 API void hetu_cpu_avgpool2d_bwd(const float* dy, float* dx, int64_t NC, int64_t H, int64_t W, int64_t KH, int64_t KW,
                                 int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t OH, int64_t OW) {
   const float inv = 1.f / (float)(KH * KW);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(NC) * (H * W) >= (1 << 16))
   for (int64_t p = 0; p < NC; ++p) {
     float* dp = dx + p * H * W;
     memset(dp, 0, sizeof(float) * H * W);
@@ -401,7 +401,7 @@ API void hetu_cpu_avgpool2d_bwd(const float* dy, float* dx, int64_t NC, int64_t 
 API void hetu_cpu_batchnorm(const float* x, const float* gamma, const float* beta, float* y, float* run_mean,
                             float* run_var, float* save_mean, float* save_rstd, int64_t N, int64_t C, int64_t HW,
                             float momentum, float eps, int training) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(C) * (N * HW) >= (1 << 16))
   for (int64_t c = 0; c < C; ++c) {
     float mean, rstd;
     if (training) {
@@ -436,7 +436,7 @@ API void hetu_cpu_batchnorm(const float* x, const float* gamma, const float* bet
 API void hetu_cpu_batchnorm_bwd(const float* dy, const float* x, const float* gamma, const float* save_mean,
                                 const float* save_rstd, float* dx, float* dgamma, float* dbeta, int64_t N, int64_t C,
                                 int64_t HW) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(C) * (N * HW) >= (1 << 16))
   for (int64_t c = 0; c < C; ++c) {
     const float mean = save_mean[c], rstd = save_rstd[c];
     double sg = 0.0, sgx = 0.0;

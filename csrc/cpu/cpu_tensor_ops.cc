@@ -128,7 +128,7 @@ struct NDIter {
 // chunk and then advanced like an odometer (no division per element)
 template <class F>
 void nd_for(const NDIter& it, int64_t n, F&& body) {
-#pragma omp parallel
+#pragma omp parallel if(n >= (1 << 16))
   {
     const int nt = omp_get_num_threads(), t = omp_get_thread_num();
     const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
@@ -185,7 +185,7 @@ int64_t numel(int nd, const int64_t* shape) {
 // y[i] = unary(op, x[i]) over n contiguous elements (op codes of elementwise.hip)
 API int hetu_cpu_unary_ext(int op, const float* x, float* y, int64_t n, float c, float c2) {
   if (op < 0 || op > 25) return -1;
-#pragma omp parallel for simd schedule(static)
+#pragma omp parallel for simd schedule(static) if((int64_t)(n) >= (1 << 16))
   for (int64_t i = 0; i < n; ++i) y[i] = unary_op(op, x[i], c, c2);
   return 0;
 }
@@ -230,13 +230,13 @@ API int hetu_cpu_copy_nd(const void* src, void* dst, int esize, int nd, const in
 }
 
 API void hetu_cpu_fill(float* y, int64_t n, float v) {
-#pragma omp parallel for simd schedule(static)
+#pragma omp parallel for simd schedule(static) if((int64_t)(n) >= (1 << 16))
   for (int64_t i = 0; i < n; ++i) y[i] = v;
 }
 
 // row softmax over the last dim: y[r] = exp(x[r] - max) / sum (log_softmax when `log`)
 API void hetu_cpu_softmax(const float* x, float* y, int64_t R, int64_t C, int log) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(R) * (C) >= (1 << 16))
   for (int64_t r = 0; r < R; ++r) {
     const float* xr = x + r * C;
     float* yr = y + r * C;
@@ -256,7 +256,7 @@ API void hetu_cpu_softmax(const float* x, float* y, int64_t R, int64_t C, int lo
 
 // dx = y * (dy - sum(dy * y)) per row (softmax backward from the saved output)
 API void hetu_cpu_softmax_bwd(const float* y, const float* dy, float* dx, int64_t R, int64_t C) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(R) * (C) >= (1 << 16))
   for (int64_t r = 0; r < R; ++r) {
     const float* yr = y + r * C;
     const float* gr = dy + r * C;
@@ -272,7 +272,7 @@ API void hetu_cpu_softmax_bwd(const float* y, const float* dy, float* dx, int64_
 API void hetu_cpu_dropout(const float* x, float* y, int64_t n, float keep, int64_t seed) {
   const float inv = 1.f / keep;
   const int64_t n4 = (n + 3) / 4;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(n4) * (4) >= (1 << 16))
   for (int64_t q = 0; q < n4; ++q) {
     const U4 r = philox((uint64_t)seed, (uint64_t)q);
     const uint32_t rr[4] = {r.x, r.y, r.z, r.w};
@@ -287,7 +287,7 @@ API void hetu_cpu_dropout(const float* x, float* y, int64_t n, float keep, int64
 // std b, redrawn outside 2 std -- counter words of later rounds); Box-Muller on word pairs
 API void hetu_cpu_random_init(float* y, int64_t n, int kind, float a, float b, int64_t seed) {
   const int64_t n4 = (n + 3) / 4;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(n4) * (4) >= (1 << 16))
   for (int64_t q = 0; q < n4; ++q) {
     float v[4];
     if (kind == 0) {
@@ -321,14 +321,14 @@ API void hetu_cpu_reduce_axis0(const float* x, float* y, int64_t R, int64_t C, f
   const int nt = omp_get_max_threads();
   const int64_t chunks = std::min<int64_t>(nt, std::max<int64_t>(1, R / 16));
   double* part = new double[(size_t)chunks * C]();
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(chunks) * (C) >= (1 << 16))
   for (int64_t t = 0; t < chunks; ++t) {
     double* p = part + (size_t)t * C;
     const int64_t lo = R * t / chunks, hi = R * (t + 1) / chunks;
     for (int64_t r = lo; r < hi; ++r)
       for (int64_t c = 0; c < C; ++c) p[c] += x[r * C + c];
   }
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(C) * (R) >= (1 << 16))
   for (int64_t c = 0; c < C; ++c) {
     double s = 0.0;
     for (int64_t t = 0; t < chunks; ++t) s += part[(size_t)t * C + c];
@@ -339,10 +339,45 @@ API void hetu_cpu_reduce_axis0(const float* x, float* y, int64_t R, int64_t C, f
 
 // y[r] = scale * sum over the last dim of x[r, :] (reduce over trailing axes)
 API void hetu_cpu_reduce_lastdim(const float* x, float* y, int64_t R, int64_t C, float scale) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if((int64_t)(R) * (C) >= (1 << 16))
   for (int64_t r = 0; r < R; ++r) {
     double s = 0.0;
     for (int64_t c = 0; c < C; ++c) s += x[r * C + c];
     y[r] = (float)(s * scale);
+  }
+}
+
+// sparse-label softmax cross-entropy: loss[r] = lse[r] - x[r, lab[r]] (0 where the label
+// is ignored / out of range); the backward dx = g[r] * (softmax - onehot) on valid rows
+API void hetu_cpu_softmax_ce_sparse(const float* x, const int64_t* lab, float* loss, float* lse, int64_t R,
+                                    int64_t C, int64_t ignored) {
+#pragma omp parallel for schedule(static) if((int64_t)(R) * (C) >= (1 << 16))
+  for (int64_t r = 0; r < R; ++r) {
+    const float* xr = x + r * C;
+    float m = -INFINITY;
+    for (int64_t c = 0; c < C; ++c) m = std::max(m, xr[c]);
+    double s = 0.0;
+    for (int64_t c = 0; c < C; ++c) s += exp((double)(xr[c] - m));
+    const float l = m + (float)log(s);
+    lse[r] = l;
+    const int64_t y = lab[r];
+    loss[r] = (y != ignored && y >= 0 && y < C) ? l - xr[y] : 0.f;
+  }
+}
+
+API void hetu_cpu_softmax_ce_sparse_bwd(const float* x, const int64_t* lab, const float* g, int g_scalar,
+                                        const float* lse, float* dx, int64_t R, int64_t C, int64_t ignored) {
+#pragma omp parallel for schedule(static) if((int64_t)(R) * (C) >= (1 << 16))
+  for (int64_t r = 0; r < R; ++r) {
+    const float* xr = x + r * C;
+    float* dr = dx + r * C;
+    const int64_t y = lab[r];
+    if (!(y != ignored && y >= 0 && y < C)) {
+      for (int64_t c = 0; c < C; ++c) dr[c] = 0.f;
+      continue;
+    }
+    const float gr = g_scalar ? g[0] : g[r], l = lse[r];
+    for (int64_t c = 0; c < C; ++c) dr[c] = gr * expf(xr[c] - l);
+    dr[y] -= gr;
   }
 }

@@ -1,0 +1,263 @@
+// 3x3 / stride 1 / pad 1 convolution with 64 input and 64 output channels (ResNet-50
+// stage 1 at 56x56, and its data gradient), as a halo-tile MFMA kernel.
+//
+// The implicit-GEMM kernels (gemm_core.h) fetch each input pixel once per filter tap:
+// nine K-tiles, nine passes of the activation through L2.  Here one block owns one image
+// and walks it TH output rows at a time:
+//   * the 64x9x64 filter bank stays in LDS for the block's lifetime (72 KiB, one
+//     [co][64] K-major image per tap, 16-byte chunks XOR-swizzled by row);
+//   * input rows live in a ring of NSLOT halo rows (64 positions x 128 B each, column 0
+//     and W+1 the zero pad); the TH rows the next tile needs are DMA'd (global_load_lds,
+//     swizzle applied on the source side) while the current tile computes, so every
+//     input row crosses HBM/L2 once;
+//   * a tap is just an LDS address offset: the pixel operand of tap (kh, kw) is the
+//     ds_read_b128 of halo position (tx + kw) in ring row (ty + kh).
+// Waves own two 16-pixel blocks x all 64 output channels (8 accumulator tiles of
+// mfma_f32_16x16x32_bf16, D[co][px]), so a lane stores 4 consecutive channels of one
+// pixel.  Optional epilogue: + Cin (the data-gradient join, bf16 or fp32) and the
+// per-channel sum / sum of squares of the stored values (BatchNorm statistics).
+//
+// Replaces cuDNN/MIOpen for these shapes (reference src/ops/CudnnConv2d.cu:54-70).
+#include "common.h"
+
+using namespace hetu;
+
+namespace {
+
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int CH = 64;                 // input = output channels
+constexpr int RP = 64;                 // halo positions per ring row (W + 2 <= 64)
+constexpr int ROWB = RP * CH * 2;      // 8 KiB per ring row
+constexpr int TAPB = CH * CH * 2;      // 8 KiB per filter tap image
+constexpr int WBYTES = 9 * TAPB;       // 72 KiB
+
+static __device__ __attribute__((aligned(64))) bf16 g_zero16[32];
+
+__device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// byte offset of logical 16-byte chunk c of row r in a [rows][64 bf16] swizzled image
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+template <int WD, int TH>
+struct Geo {
+  static constexpr int PX = TH * WD;            // pixels per tile
+  static constexpr int PB = (PX + 15) / 16;     // 16-pixel blocks
+  static constexpr int NW = (PB + 1) / 2;       // waves: two blocks each
+  static constexpr int NT = NW * 64;
+  static constexpr int NSLOT = 2 * TH + 2;      // rows in use (TH + 2) + rows in flight (TH)
+};
+
+template <int WD, int TH>
+__global__ __launch_bounds__((Geo<WD, TH>::NT), 1) void conv3x3_c64_k(const bf16* __restrict__ x,
+                                                                      const bf16* __restrict__ w,
+                                                                      bf16* __restrict__ y, const void* cin,
+                                                                      int cin_f32, float* colstats, int H) {
+  using G = Geo<WD, TH>;
+  __shared__ __attribute__((aligned(16))) char smem[WBYTES + G::NSLOT * ROWB];
+  char* wl = smem;
+  char* ring = smem + WBYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = blockIdx.x;
+  const bf16* img = x + (int64_t)n * H * WD * CH;
+
+  // stage input row ih (may be out of range: zeros) into its ring slot; 8 wave
+  // instructions of 1 KiB (8 halo positions x 8 chunks) per row, dealt to the waves
+  auto stage_rows = [&](int r0, int nrows) {
+    const int total = nrows * 8;
+    for (int I = wave; I < total; I += G::NW) {
+      const int rr = I >> 3, pos0 = (I & 7) * 8;
+      const int ih = r0 + rr;
+      const int slot = (ih + 1 + G::NSLOT) % G::NSLOT;
+      const int pos = pos0 + (lane >> 3);
+      const int c = (lane & 7) ^ (pos & 7);
+      const int iw = pos - 1;
+      const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < WD;
+      const void* src = ok ? (const void*)(img + ((int64_t)ih * WD + iw) * CH + c * 8) : (const void*)g_zero16;
+      dma16(src, ring + slot * ROWB + pos0 * 128);
+    }
+  };
+
+  // filter bank: tap image t, row co, chunk c <- w[co][t][c*8 .. +8]
+  for (int J = wave; J < 72; J += G::NW) {
+    const int tap = J >> 3, co = (J & 7) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (co & 7);
+    dma16(w + ((int64_t)co * 9 + tap) * CH + c * 8, wl + tap * TAPB + (J & 7) * 1024);
+  }
+  stage_rows(-1, TH + 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // this lane's two pixel blocks: tile-relative row / column of pixel (lane & 15)
+  int ty[2], tx[2];
+  bool pv[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int px = (2 * wave + p) * 16 + (lane & 15);
+    pv[p] = px < G::PX;
+    const int pc = pv[p] ? px : 0;
+    ty[p] = pc / WD;
+    tx[p] = pc - ty[p] * WD;
+  }
+  const int q4 = lane >> 4;    // k-chunk within a 32-wide k-step / 4-channel group of D
+
+  float cs[16], cq[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { cs[i] = 0.f; cq[i] = 0.f; }
+
+  const int ntiles = (H + TH - 1) / TH;
+  for (int t = 0; t < ntiles; ++t) {
+    const int oh0 = t * TH;
+    // rows oh0+TH+1 .. oh0+2TH for the next tile land while this one computes
+    if (t + 1 < ntiles) stage_rows(oh0 + TH + 1, TH);
+
+    v4f acc[2][4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[p][q] = v4f{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      int rb[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) rb[p] = ((oh0 + ty[p] + kh) % G::NSLOT) * ROWB;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const char* wt = wl + (kh * 3 + kw) * TAPB;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int c = ks * 4 + q4;
+          v8s wf[4], pf[2];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) wf[q] = *reinterpret_cast<const v8s*>(wt + swz(q * 16 + (lane & 15), c));
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+            pf[p] = *reinterpret_cast<const v8s*>(ring + rb[p] + swz(tx[p] + kw, c));
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[q], pf[p], acc[p][q], 0, 0, 0);
+        }
+      }
+    }
+
+    // epilogue: lane holds channels q*16 + 4*q4 + i of pixel (ty, tx)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int oh = oh0 + ty[p];
+      if (!pv[p] || oh >= H) continue;
+      const int64_t pix = ((int64_t)n * H + oh) * WD + tx[p];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = q * 16 + 4 * q4;
+        float v[4] = {acc[p][q][0], acc[p][q][1], acc[p][q][2], acc[p][q][3]};
+        if (cin) {
+          if (cin_f32) {
+            const float4 a = *reinterpret_cast<const float4*>((const float*)cin + pix * CH + co);
+            v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+          } else {
+            const uint2 a = *reinterpret_cast<const uint2*>((const bf16*)cin + pix * CH + co);
+            v[0] += bf16_bits_to_f((unsigned short)(a.x & 0xffffu));
+            v[1] += bf16_bits_to_f((unsigned short)(a.x >> 16));
+            v[2] += bf16_bits_to_f((unsigned short)(a.y & 0xffffu));
+            v[3] += bf16_bits_to_f((unsigned short)(a.y >> 16));
+          }
+        }
+        unsigned short h[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          h[i] = f_to_bf16_bits(v[i]);
+          const float sv = bf16_bits_to_f(h[i]);
+          cs[q * 4 + i] += sv;
+          cq[q * 4 + i] += sv * sv;
+        }
+        uint2 pk;
+        pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+        pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+        *reinterpret_cast<uint2*>(y + pix * CH + co) = pk;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  if (colstats) {
+    // lanes of one 16-lane group hold the same 16 channels: fold their pixels, then the
+    // waves through LDS (the ring is free now), one atomic per channel and statistic
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        cs[i] += __shfl_xor(cs[i], o, 64);
+        cq[i] += __shfl_xor(cq[i], o, 64);
+      }
+    float* red = reinterpret_cast<float*>(ring);   // [NW][2][64]
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = q * 16 + 4 * q4 + i;
+          red[(wave * 2) * CH + co] = cs[q * 4 + i];
+          red[(wave * 2 + 1) * CH + co] = cq[q * 4 + i];
+        }
+    }
+    __syncthreads();
+    if (tid < 2 * CH) {
+      const int which = tid / CH, co = tid % CH;
+      float v = 0.f;
+      for (int ww = 0; ww < G::NW; ++ww) v += red[(ww * 2 + which) * CH + co];
+      unsafeAtomicAdd(colstats + which * CH + co, v);
+    }
+  }
+}
+
+// w'[ci][kh][kw][co] = w[co][2-kh][2-kw][ci]: the data gradient of a 3x3 / pad-1 /
+// stride-1 convolution is the same convolution of dy with this bank
+__global__ void __launch_bounds__(256) flip_bank_k(const bf16* __restrict__ w, bf16* __restrict__ wt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= CH * 9 * CH) return;
+  const int ci = i / (9 * CH), r = i - ci * 9 * CH, tap = r / CH, co = r - tap * CH;
+  wt[i] = w[((int64_t)co * 9 + (8 - tap)) * CH + ci];
+}
+
+template <int WD, int TH>
+int launch_c64(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
+               hipStream_t st) {
+  using G = Geo<WD, TH>;
+  hipLaunchKernelGGL((conv3x3_c64_k<WD, TH>), dim3(N), dim3(G::NT), 0, st, x, w, y, cin, cin_f32, colstats, H);
+  return (int)hipGetLastError();
+}
+
+int dispatch_c64(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
+                 int W, hipStream_t st) {
+  // tiles of 224 pixels: 4 rows of 56 (the only width 64-channel 3x3 layers have in ResNet-50)
+  if (W == 56) return launch_c64<56, 4>(x, w, y, cin, cin_f32, colstats, N, H, st);
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+HETU_API int hetu_conv3x3_c64_supported(int C, int K, int W) { return C == CH && K == CH && W == 56; }
+
+// y[N,H,W,64] = conv3x3(x[N,H,W,64], w[64][3][3][64]), stride 1, pad 1 (NHWC bf16);
+// colstats (nullable, 128 fp32 pre-zeroed) += per-channel sum / sum of squares of y
+HETU_API int hetu_conv3x3_c64_fwd(const void* x, const void* w, void* y, float* colstats, int N, int H, int W,
+                                  hipStream_t st) {
+  if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)y)) & 15) return (int)hipErrorInvalidValue;
+  return dispatch_c64((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, N, H, W, st);
+}
+
+// dx[N,H,W,64] = conv3x3^T(dy, w) (+ acc: bf16 or fp32 [N,H,W,64]); wt: 64*9*64 bf16 scratch
+HETU_API int hetu_conv3x3_c64_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
+                                    int N, int H, int W, hipStream_t st) {
+  if ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc)) & 15) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(flip_bank_k, dim3((CH * 9 * CH + 255) / 256), dim3(256), 0, st, (const bf16*)w, (bf16*)wt);
+  HETU_LAUNCH_CHECK();
+  return dispatch_c64((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, nullptr, N, H, W, st);
+}

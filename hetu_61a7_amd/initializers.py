@@ -31,6 +31,16 @@ class BaseInit(object):
             numel *= int(s)
         gen_dev = torch.device('cpu') if numel < (1 << 26) else torch.device(device)
         t = torch.empty(self.shape, dtype=torch.float32, device=gen_dev)
+        from .kernels import cpu_native
+        spec = self.native_spec()
+        if gen_dev.type == 'cpu' and spec is not None and cpu_native.enabled():
+            # the native CPU backend's counter-based Philox (csrc/cpu/cpu_tensor_ops.cc)
+            kind, a, b = spec
+            if kind == 'constant':
+                cpu_native.fill(t, a)
+            else:
+                cpu_native.random_init(t, kind, a, b, int(seed))
+            return t.to(device)
         g = torch.Generator(device=gen_dev)
         g.manual_seed(int(seed) & 0x7FFFFFFF)
         self.init_on_device(t, g)
@@ -38,6 +48,11 @@ class BaseInit(object):
 
     def init_on_device(self, t, gen):
         raise NotImplementedError
+
+    def native_spec(self):
+        """(kind, a, b) of the native CPU generator ('constant', 'uniform', 'normal',
+        'truncated_normal'), or None for the torch generator"""
+        return None
 
     def init_numpy(self, seed):
         return self.generate(seed, 'cpu').numpy()
@@ -54,6 +69,9 @@ class ConstantInit(BaseInit):
 
     def init_on_device(self, t, gen):
         t.fill_(self.constant)
+
+    def native_spec(self):
+        return ('constant', float(self.constant), 0.0)
 
 
 class ZerosInit(ConstantInit):
@@ -73,6 +91,9 @@ class UniformInit(BaseInit):
 
     def init_on_device(self, t, gen):
         t.uniform_(self.low, self.high, generator=gen)
+
+    def native_spec(self):
+        return ('uniform', float(self.low), float(self.high))
 
 
 def _fans(shape, mode):
@@ -119,6 +140,9 @@ class NormalInit(BaseInit):
     def init_on_device(self, t, gen):
         t.normal_(self.mean, self.stddev, generator=gen)
 
+    def native_spec(self):
+        return ('normal', float(self.mean), float(self.stddev))
+
 
 class GeneralXavierNormalInit(NormalInit):
     def __init__(self, gain, mode, shape):
@@ -156,6 +180,9 @@ class TruncatedNormalInit(BaseInit):
                 break
             t[bad] = torch.randn(int(bad.sum()), generator=gen, device=t.device)
         t.clamp_(-2.0, 2.0).mul_(self.stddev).add_(self.mean)
+
+    def native_spec(self):
+        return ('truncated_normal', float(self.mean), float(self.stddev))
 
 
 # ---- factories returning Variables (reference initializers.py:214-311) -----

@@ -162,6 +162,8 @@ def conv2d_with_stats(x, w, stride, padding):
         cands['hip_lo'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=3, colstats=s))
     if conv_igemm.stem_ok(x, w, stride, padding):
         cands['hip_stem'] = fused(lambda s: conv_igemm.try_stem_forward(x, w, stride, padding, colstats=s))
+    if conv_igemm.conv3x3_ok(x.shape, w.shape, stride, padding):
+        cands['hip33'] = fused(lambda s: conv_igemm.try_conv3x3_forward(x, w, stride, padding, colstats=s))
     if _plain_1x1((x, w), w.shape, stride, padding):
         n, _, h, ww_ = x.shape
         cands['blas'] = separate(lambda: torch.mm(_rows(x), w.reshape(co, -1).t()).view(n, h, ww_, co)
@@ -267,6 +269,9 @@ def conv2d(x, w, b, stride, padding):
         if _short_k(w.shape[1] * w.shape[2] * w.shape[3]):
             blas = dict(blas or {})
             blas['hip_lo'] = lambda: conv_igemm.try_forward(x, w, stride, padding, tile=3)
+        if conv_igemm.conv3x3_ok(x.shape, w.shape, stride, padding):
+            blas = dict(blas or {})
+            blas['hip33'] = lambda: conv_igemm.try_conv3x3_forward(x, w, stride, padding)
         y = _pick(('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding)),
                   lambda: conv_igemm.try_forward(x, w, stride, padding),
                   lambda: F.conv2d(x, w, None, stride, padding), blas)
@@ -342,6 +347,9 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
         if _short_k(w.shape[0] * w.shape[2] * w.shape[3]):
             blas = dict(blas or {})
             blas['hip_lo'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=3)
+        if conv_igemm.conv3x3_ok(x_shape, w.shape, stride, padding):
+            blas = dict(blas or {})
+            blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=acc)
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
                      lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
                      lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas, tuned)

@@ -141,6 +141,44 @@ def try_stem_forward(x, w, stride, padding, colstats=None):
     return y.permute(0, 3, 1, 2)
 
 
+def conv3x3_ok(shape_x, w_shape, stride, padding):
+    """the 64-channel halo-tile kernel (``conv3x3.hip``) takes this 3x3/s1/p1 shape"""
+    co, c, kh, kw = w_shape
+    if (kh, kw) != (3, 3) or tuple(stride) != (1, 1) or tuple(padding) != (1, 1):
+        return False
+    return bool(fn('hetu_conv3x3_c64_supported', [I32, I32, I32])(int(c), int(co), int(shape_x[3])))
+
+
+def try_conv3x3_forward(x, w, stride, padding, colstats=None):
+    """3x3 / stride 1 / pad 1, 64 -> 64 channels: one block per image, the filter bank
+    resident in LDS and a DMA ring of halo rows (each input row read once)."""
+    if not (_ok(x, w, x.shape[1], w.shape[0]) and conv3x3_ok(x.shape, w.shape, stride, padding)):
+        return None
+    N, C, H, W = x.shape
+    y = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=x.device)
+    f = fn('hetu_conv3x3_c64_fwd', [P, P, P, P, I32, I32, I32, P])
+    check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), colstats.data_ptr() if colstats is not None else None,
+            N, H, W, stream_ptr()), 'conv3x3_fwd')
+    record_native('conv3x3_fwd')
+    return y.permute(0, 3, 1, 2)
+
+
+def try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=None):
+    if not (_ok(g, w, x_shape[1], w.shape[0]) and conv3x3_ok(x_shape, w.shape, stride, padding)):
+        return None
+    if acc is not None and (tuple(acc.shape) != tuple(x_shape) or not acc.is_contiguous(memory_format=CL) or
+                            acc.dtype not in (torch.bfloat16, torch.float32) or acc.data_ptr() % 16):
+        return None
+    N, C, H, W = x_shape
+    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
+    wt = torch.empty(w.numel(), dtype=torch.bfloat16, device=g.device)
+    f = fn('hetu_conv3x3_c64_dgrad', [P, P, P, P, P, I32, I32, I32, I32, P])
+    check(f(g.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
+            int(acc is not None and acc.dtype == torch.float32), N, H, W, stream_ptr()), 'conv3x3_dgrad')
+    record_native('conv3x3_dgrad')
+    return dx.permute(0, 3, 1, 2)
+
+
 STEM_WGRAD_BLOCKS = 512
 
 

@@ -16,6 +16,9 @@ def dropout(x, keep_prob, seed):
         check(f(xc.data_ptr(), y.data_ptr(), xc.numel(), float(keep_prob), int(seed), is_bf16(x),
                 stream_ptr()), 'dropout')
         return y
+    from . import cpu_native
+    if cpu_native.active(x):
+        return cpu_native.dropout(x, keep_prob, seed)
     g = torch.Generator(device=x.device)
     g.manual_seed(int(seed) & 0x7FFFFFFF)
     mask = torch.rand(x.shape, generator=g, device=x.device) < keep_prob

@@ -82,8 +82,9 @@ def unary(op: str, x: torch.Tensor, c: float = 0.0, c2: float = 0.0, out=None) -
                 stream_ptr()), 'unary:' + op)
         return y
     from . import cpu_native
-    if op in cpu_native.UNARY and cpu_native.active(x) and out is None:
-        return cpu_native.unary(op, x)
+    if cpu_native.active(x, out):
+        return cpu_native.unary_code(U[op], x, c, c2, out)
+    cpu_native.record_fallback('unary:' + op, x)
     r = _ref_unary(op, x, c, c2)
     if out is not None:
         out.copy_(r)
@@ -171,8 +172,16 @@ def binary(op: str, a: torch.Tensor, b: torch.Tensor, c: float = 0.0, out=None) 
     if b.dtype != a.dtype and b.numel() <= a.numel():
         b = b.to(a.dtype)
     from . import cpu_native
-    if op == 'relu_grad' and out is None and b.shape == a.shape and cpu_native.active(a, b):
-        return cpu_native.relu_grad(a, b)
+    if cpu_native.active(a, b, out):
+        try:
+            shape = torch.broadcast_shapes(a.shape, b.shape)
+        except RuntimeError:
+            shape = None
+        if shape is not None and (out is None or tuple(out.shape) == tuple(shape)):
+            r = cpu_native.binary_code(B[op], a, b, c, out)
+            if r is not None:
+                return r
+    cpu_native.record_fallback('binary:' + op, a, b)
     r = _ref_binary(op, a, b, c)
     if r.dtype != a.dtype and a.dtype.is_floating_point:
         r = r.to(a.dtype)

@@ -22,8 +22,22 @@ def reduce_mid(x3: torch.Tensor, scale: float = 1.0, out_dtype=None, out=None) -
                 1 if out_dtype == torch.bfloat16 else 0, ws.data_ptr(), stream_ptr()), 'reduce_mid')
         return y
     from . import cpu_native
-    if B == 1 and out is None and out_dtype == torch.float32 and cpu_native.active(x3):
-        return cpu_native.reduce_rows(x3.reshape(R, C), scale).reshape(1, C)
+    if out_dtype == torch.float32 and cpu_native.active(x3, out):
+        if C == 1:
+            y = cpu_native.reduce_lastdim(x3.reshape(B, R), scale).reshape(B, 1)
+        elif B == 1:
+            y = cpu_native.reduce_axis0(x3.reshape(R, C), scale).reshape(1, C)
+        else:
+            y = torch.stack([cpu_native.reduce_axis0(x3[b], scale) for b in range(B)]) if B <= 16 else None
+            if y is None:   # many short reductions: sum over R of each [C] row block via a permute
+                xt = torch.empty((R, B, C), dtype=torch.float32)
+                cpu_native.copy_nd(x3.permute(1, 0, 2), xt)
+                y = cpu_native.reduce_axis0(xt.reshape(R, B * C), scale).reshape(B, C)
+        if out is not None:
+            cpu_native.copy_nd(y.reshape(out.shape), out)
+            return out
+        return y
+    cpu_native.record_fallback('reduce_mid', x3)
     r = (x3.float().sum(1) * scale).to(out_dtype)
     if out is not None:
         out.copy_(r.reshape(out.shape))
@@ -41,6 +55,10 @@ def reduce_last(x2: torch.Tensor, scale: float = 1.0, out_dtype=None) -> torch.T
         check(f(x2.data_ptr(), y.data_ptr(), R, C, float(scale), is_bf16(x2),
                 1 if out_dtype == torch.bfloat16 else 0, stream_ptr()), 'reduce_last')
         return y
+    from . import cpu_native
+    if out_dtype == torch.float32 and cpu_native.active(x2):
+        return cpu_native.reduce_lastdim(x2, scale)
+    cpu_native.record_fallback('reduce_last', x2)
     return (x2.float().sum(1) * scale).to(out_dtype)
 
 
@@ -83,6 +101,9 @@ def sum_to_shape(g: torch.Tensor, shape) -> torch.Tensor:
         inner = g.numel() // max(lead, 1)
         return reduce_mid(g.reshape(1, lead, inner)).reshape(shape)
     dims = [i for i in range(nd) if full[i] == 1 and g.shape[i] != 1]
+    from . import cpu_native
+    if cpu_native.active(g) and dims:
+        return reduce_sum(g, dims, keepdim=True).reshape(shape)
     r = g.float().sum(dim=dims, keepdim=True) if dims else g.float()
     return r.reshape(shape).to(g.dtype)
 
@@ -93,6 +114,9 @@ def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     if native(x) and supported_float(x):
         xc = x.contiguous(memory_format=torch.channels_last)
         return reduce_mid(xc.permute(0, 2, 3, 1).reshape(N, H * W, C), 1.0 / (H * W))
+    from . import cpu_native
+    if cpu_native.active(x):
+        return reduce_last(x.contiguous().reshape(N * C, H * W), 1.0 / (H * W)).reshape(N, C)
     return x.float().mean((2, 3)).to(x.dtype)
 
 
@@ -106,4 +130,9 @@ def global_avg_pool_backward(dy: torch.Tensor, x_shape) -> torch.Tensor:
         check(f(dy.data_ptr(), dx.data_ptr(), N, H * W, C, 1.0 / (H * W), is_bf16(dy),
                 stream_ptr()), 'bcast_mid')
         return dx
+    from . import cpu_native
+    if cpu_native.active(dy):
+        dx = torch.empty((N, C, H, W), dtype=torch.float32)
+        cpu_native.copy_nd(dy.reshape(N, C, 1, 1).expand(N, C, H, W), dx)
+        return cpu_native.unary_code(15, dx, 1.0 / (H * W), out=dx)
     return (dy.reshape(N, C, 1, 1).float() / (H * W)).expand(N, C, H, W).to(dy.dtype).contiguous()

@@ -19,6 +19,10 @@ def softmax(x: torch.Tensor, log: bool = False) -> torch.Tensor:
         f = fn('hetu_softmax_fwd', [P, P, I64, I32, I32, I32, P])
         check(f(x.data_ptr(), y.data_ptr(), R, N, is_bf16(x), int(log), stream_ptr()), 'softmax')
         return y
+    from . import cpu_native
+    if cpu_native.active(x) and x.dim() > 0:
+        return cpu_native.softmax(x, log)
+    cpu_native.record_fallback('softmax', x)
     xf = x.float()
     return (torch.log_softmax(xf, -1) if log else torch.softmax(xf, -1)).to(x.dtype)
 
@@ -32,6 +36,10 @@ def softmax_backward(y: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
         f = fn('hetu_softmax_bwd', [P, P, P, I64, I32, I32, P])
         check(f(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), R, N, is_bf16(y), stream_ptr()), 'softmax_bwd')
         return dx
+    from . import cpu_native
+    if cpu_native.active(y, dy) and y.dim() > 0 and dy.shape == y.shape:
+        return cpu_native.softmax_backward(y, dy)
+    cpu_native.record_fallback('softmax_backward', y, dy)
     yf, gf = y.float(), dy.float()
     return (yf * (gf - (gf * yf).sum(-1, keepdim=True))).to(y.dtype)
 
@@ -49,8 +57,10 @@ def softmax_ce(logits: torch.Tensor, labels: torch.Tensor):
                 is_bf16(x), is_bf16(lab), stream_ptr()), 'softmax_ce')
         return loss, lse
     from . import cpu_native
-    if cpu_native.active(logits) and logits.dim() == 2:
-        return cpu_native.softmax_ce(logits, labels)
+    if cpu_native.active(logits, labels) and logits.dim() >= 1 and labels.shape == logits.shape:
+        loss, lse = cpu_native.softmax_ce(_rows(logits), _rows(labels))
+        return loss.reshape(logits.shape[:-1]), lse.reshape(logits.shape[:-1])
+    cpu_native.record_fallback('softmax_ce', logits, labels)
     xf = logits.float()
     lse = torch.logsumexp(xf, -1)
     loss = (labels.float() * (lse.unsqueeze(-1) - xf)).sum(-1)
@@ -83,8 +93,14 @@ def softmax_ce_backward(logits, labels, grad, lse=None):
         return dx
     grad = grad.float()
     from . import cpu_native
-    if cpu_native.active(logits) and logits.dim() == 2 and lse is not None:
-        return cpu_native.softmax_ce_backward(logits, labels, grad, lse)
+    if cpu_native.active(logits, labels) and logits.dim() >= 1 and labels.shape == logits.shape:
+        if lse is None:
+            _, lse = softmax_ce(logits, labels)
+        R = logits.numel() // logits.shape[-1]
+        g, scalar = _grad_rows(grad)
+        g = g.reshape(-1) if scalar else g.reshape(R)
+        return cpu_native.softmax_ce_backward(_rows(logits), _rows(labels), g, lse.reshape(R)).reshape(logits.shape)
+    cpu_native.record_fallback('softmax_ce_backward', logits, labels)
     xf = logits.float()
     yl = labels.float()
     sm = torch.softmax(xf, -1)
@@ -104,6 +120,9 @@ def softmax_ce_sparse(logits, labels, ignored_index=-1):
         check(f(x.data_ptr(), lab.data_ptr(), loss.data_ptr(), lse.data_ptr(), R, N, is_bf16(x),
                 int(ignored_index), stream_ptr()), 'softmax_ce_sparse')
         return loss, lse
+    from . import cpu_native
+    if cpu_native.active(logits):
+        return cpu_native.softmax_ce_sparse(logits, lab, ignored_index)
     xf = _rows(logits.float())
     lse = torch.logsumexp(xf, -1)
     valid = (lab != ignored_index) & (lab >= 0) & (lab < xf.shape[-1])
@@ -128,6 +147,12 @@ def softmax_ce_sparse_backward(logits, labels, grad, lse=None, ignored_index=-1)
                 is_bf16(x), int(ignored_index), stream_ptr()), 'softmax_ce_sparse_bwd')
         return dx
     grad = grad.float()
+    from . import cpu_native
+    if cpu_native.active(logits):
+        if lse is None:
+            _, lse = softmax_ce_sparse(logits, labels, ignored_index)
+        g, scalar = _grad_rows(grad)
+        return cpu_native.softmax_ce_sparse_backward(logits, lab, g.contiguous(), scalar, lse, ignored_index)
     xf = _rows(logits.float())
     sm = torch.softmax(xf, -1)
     valid = (lab != ignored_index) & (lab >= 0) & (lab < xf.shape[-1])

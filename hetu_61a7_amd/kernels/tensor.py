@@ -49,7 +49,17 @@ def _dims(shape, dim):
 def nd_copy(src, dst, shift=None, imod=None):
     """dst[c] = src[(c + shift) % imod] elementwise over dst's shape (both strided views
     of the same dtype; src's shape may differ where imod wraps)."""
-    assert src.dtype == dst.dtype and src.is_cuda and dst.is_cuda
+    assert src.dtype == dst.dtype
+    if not dst.is_cuda:
+        from . import cpu_native
+        if shift is None and imod is None and cpu_native.enabled():
+            return cpu_native.copy_nd(src, dst)
+        cpu_native.record_fallback('nd_copy', src, dst)
+        if shift is None and imod is None:
+            return dst.copy_(src)
+        idx = [torch.remainder(torch.arange(n) + (sh or 0), m or n) for n, sh, m in zip(dst.shape, shift, imod)]
+        dst.copy_(src[torch.meshgrid(*idx, indexing='ij')] if idx else src)
+        return dst
     nd = dst.dim()
     if nd == 0:
         dst.copy_(src)
@@ -67,6 +77,11 @@ def nd_copy(src, dst, shift=None, imod=None):
 def fill_(t, value):
     """t (contiguous) = value."""
     assert t.is_contiguous()
+    if not t.is_cuda:
+        from . import cpu_native
+        if t.dtype == torch.float32 and cpu_native.enabled():
+            return cpu_native.fill(t, value)
+        return t.fill_(value)
     bits = torch.tensor([value], dtype=t.dtype).view({1: torch.uint8, 2: torch.int16, 4: torch.int32,
                                                       8: torch.int64}[_ELEM[t.dtype]]).item()
     f = fn('hetu_fill', [P, I32, I64, ctypes.c_uint64, P])
@@ -81,7 +96,7 @@ def zeros(shape, dtype=torch.float32, device='cuda'):
         f = fn('hetu_fill', [P, I32, I64, ctypes.c_uint64, P])
         check(f(t.data_ptr(), _ELEM[t.dtype], t.numel(), 0, stream_ptr()), 'fill')
     elif t.numel():
-        t.zero_()
+        fill_(t, 0)
     return t
 
 
@@ -92,6 +107,8 @@ def _dense(t):
 def copy_into(dst, src):
     """dst[...] = src on the native kernels: same dtype -> strided copy (nd_copy);
     fp32 <-> bf16 over identical dense layouts -> the cast kernel on the flat storage."""
+    if not (dst.is_cuda or src.is_cuda) and tuple(dst.shape) == tuple(src.shape) and dst.dtype == src.dtype:
+        return nd_copy(src, dst)
     if not (dst.is_cuda and src.is_cuda) or tuple(dst.shape) != tuple(src.shape):
         return dst.copy_(src)
     if dst.dtype == src.dtype:
@@ -166,6 +183,13 @@ def repeat(x, reps):
     xs = [1] * (len(reps) - x.dim()) + list(x.shape)
     xv = x.reshape(xs)
     out = torch.empty([a * b for a, b in zip(xs, reps)], dtype=x.dtype, device=x.device)
+    if not x.is_cuda:   # out viewed as [r0, s0, r1, s1, ...] = x broadcast over the r axes
+        inter, src = [], []
+        for r, n in zip(reps, xs):
+            inter += [r, n]
+            src += [1, n]
+        nd_copy(xv.reshape(src).expand(inter), out.view(inter))
+        return out
     return nd_copy(xv, out, [0] * len(xs), xs)
 
 

@@ -372,8 +372,15 @@ def bert_bench(args, world, rank, local):
             ex = H.Executor({'train': [loss, train]}, ctx=H.gpu(local) if on_gpu else H.cpu(0), **kw)
         replica, m = rank, None
         parallelism = 'dp%d (galvatron plan: %s)' % (world, plan.short())
-    batch = synthetic_bert_batch(cfg, seed=10 + replica)
-    fd = {feeds[k]: torch.from_numpy(v).to(dev) for k, v in batch.items()}
+    # one global synthetic batch, each data-parallel replica takes its contiguous slice, so
+    # every layout (dp N, pp x dp, one process) trains on the same global batch
+    import copy
+    gcfg = copy.copy(cfg)
+    rb = cfg.batch_size
+    gcfg.batch_size = B * world
+    full = synthetic_bert_batch(gcfg, seed=10)
+    batch = {k: v[replica * rb:(replica + 1) * rb] for k, v in full.items()}
+    fd = {feeds[k]: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in batch.items()}
 
     def step():
         if m is None:

@@ -139,3 +139,53 @@ def lstm(x, y_, diminput=28, dimhidden=128, dimoutput=10, nsteps=28):
         h = O.mul_op(go, O.tanh_op(c))
     y = _fc(h, (dimhidden, dimoutput), 'lstm_out')
     return _loss(y, y_), y
+
+
+def logreg_bench(args, world, rank, local):
+    """BASELINE config 1: logistic regression on MNIST-shaped data (784 -> 10, zero init,
+    batch 128, SGD lr 0.01; reference examples/cnn/main.py:24-27,114-119 with --gpu -1) on
+    the CPU executor -- the native C++/OpenMP backend (kernels.cpu_native).  A step is one
+    forward + backward + SGD update; the batches cycle through a fixed synthetic set.
+
+    Returns (step, samples_per_step, cfg, metric, finish); ``step.extra()`` reports the
+    ATen compute ops one steady-state step issued (torch CPU profiler) and the native
+    backend's fallback count, both expected to be 0."""
+    import numpy as np
+    import torch
+    import hetu_61a7_amd as ht
+    from ..kernels import cpu_native
+    B = args.batch or 128
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    loss, _ = logreg(x, y_)
+    train = ht.optim.SGDOptimizer(learning_rate=0.01).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.cpu(0))
+    rng = np.random.RandomState(1234 + rank)
+    nb = 16
+    X = torch.from_numpy(rng.rand(nb, B, 784).astype(np.float32))
+    Y = torch.from_numpy(np.eye(10, dtype=np.float32)[rng.randint(0, 10, (nb, B))])
+    it = [0]
+
+    def step():
+        i = it[0] % nb
+        it[0] += 1
+        return ex.run('train', feed_dict={x: X[i], y_: Y[i]})
+
+    def extra():
+        cpu_native.reset_fallbacks()
+        from torch.profiler import profile, ProfilerActivity
+        with profile(activities=[ProfilerActivity.CPU]) as prof:
+            step()
+        # allocation / view / metadata ops move no data; anything else is ATen compute
+        meta = ('empty', 'empty_strided', 'empty_like', 'view', 'reshape', 'as_strided', 'expand', 'permute', 'transpose', 'select', 'slice',
+                'detach', 'alias', 'unsqueeze', 'squeeze', 'resolve', 'lift', 'result_type', 'is_', 'size',
+                'stride', 'numel', 'contiguous', 't', 'flatten', 'unfold', '_unsafe_view', 'set_', 'to',
+                '_to_copy', 'narrow', 'item', '_local_scalar_dense', 'broadcast_to')
+        compute = sorted({e.key for e in prof.key_averages() if e.key.startswith('aten::') and
+                          e.key[6:].lstrip('_') not in meta and not any(e.key[6:] == m for m in meta)})
+        return {'aten_compute_ops_per_step': compute, 'native_cpu_fallbacks': dict(cpu_native.FALLBACKS),
+                'cpu_backend': 'native' if cpu_native.enabled() else 'aten',
+                'omp_threads': int(cpu_native.lib().hetu_cpu_num_threads())}
+    step.extra = extra
+    cfg = {'model': 'logreg MNIST (784->10)', 'global_batch': B, 'seq_len': None, 'parallelism': 'cpu',
+           'optimizer': 'sgd', 'device': 'cpu'}
+    return step, B, cfg, 'samples/sec logreg MNIST CPU', None

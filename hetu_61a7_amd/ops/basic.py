@@ -874,10 +874,8 @@ class OnesLikeOp(Op):
         super().__init__(OnesLikeOp, [node], ctx)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        if self.device.type == 'cuda':
-            from ..kernels.tensor import fill_
-            return fill_(torch.empty(tuple(input_vals[0]), dtype=torch.float32, device=self.device), 1.0)
-        return torch.ones(tuple(input_vals[0]), dtype=torch.float32, device=self.device)
+        from ..kernels.tensor import fill_
+        return fill_(torch.empty(tuple(input_vals[0]), dtype=torch.float32, device=self.device), 1.0)
 
     def gradient(self, output_grad):
         return [None]

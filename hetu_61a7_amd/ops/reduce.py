@@ -111,7 +111,8 @@ class ReduceGradOp(Op):
             scale = 1.0 / max(int(np.prod([shape[a] for a in axes])), 1)
         g = g.reshape(keep)
         if scale != 1.0:
-            if _gpu(g) and g.is_contiguous():
+            from ..kernels import cpu_native
+            if (_gpu(g) and g.is_contiguous()) or cpu_native.active(g):
                 from ..kernels.elementwise import unary
                 g = unary('mul_c', g, float(scale))
             else:
@@ -181,7 +182,8 @@ class SumOp(Op):
             return r
         dt = max(dense, key=lambda t: t.numel()).dtype
         acc = None
-        if all(_gpu(v) for v in dense):
+        from ..kernels import cpu_native
+        if all(_gpu(v) for v in dense) or (dense and cpu_native.active(*dense)):
             from ..kernels.elementwise import binary, cast
             for v in dense:          # native adds (mixed bf16 / fp32 operands read as they are)
                 if acc is None:

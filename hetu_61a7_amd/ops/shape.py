@@ -25,6 +25,12 @@ def _gpu(t):
     return isinstance(t, torch.Tensor) and _native(t)
 
 
+def _cpu(*ts):
+    """native C++ CPU backend for fp32 host tensors (kernels.cpu_native)"""
+    from ..kernels import cpu_native
+    return all(isinstance(t, torch.Tensor) for t in ts) and cpu_native.active(*ts)
+
+
 def _fallback(name, t):
     if isinstance(t, torch.Tensor) and t.is_cuda:
         _record_fallback(name)
@@ -391,7 +397,7 @@ class ConcatenateOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         dt = input_vals[0].dtype
-        if _gpu(input_vals[0]):
+        if _gpu(input_vals[0]) or _cpu(*input_vals):
             return KT.concat([v.to(dt) for v in input_vals], self.axis)
         return torch.cat([v.to(dt) for v in input_vals], self.axis)
 
@@ -463,7 +469,7 @@ class PadOp(Op):
         for p in reversed(padl):
             pads += [p[0], p[1]]
         if self.mode == 'constant':
-            if _gpu(x):
+            if _gpu(x) or _cpu(x):
                 return KT.pad_constant(x, padl, self.constant_values)
             return F.pad(x, pads, 'constant', self.constant_values)
         _fallback('pad_' + self.mode, x)
@@ -488,7 +494,7 @@ class PadGradientOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g = input_vals[0]
         off = g.dim() - len(self.paddings)
-        if _gpu(g):
+        if _gpu(g) or _cpu(g):
             return KT.unpad(g, [[0, 0]] * off + self.paddings)
         sl = [slice(None)] * off + [slice(p[0], g.shape[off + i] - p[1]) for i, p in enumerate(self.paddings)]
         return g[tuple(sl)]
@@ -518,7 +524,7 @@ class RepeatOp(Op):
         self.reps = tuple(reps)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        if _gpu(input_vals[0]):
+        if _gpu(input_vals[0]) or _cpu(input_vals[0]):
             return KT.repeat(input_vals[0], self.reps)
         return input_vals[0].repeat(*self.reps)
 
@@ -545,7 +551,7 @@ class RepeatGradientOp(Op):
         inter = []
         for r, s in zip(self.reps, full):
             inter += [r, s]
-        if _gpu(g):
+        if _gpu(g) or _cpu(g):
             # sum over the tile axes: the interleaved [r0, s0, r1, s1, ...] view reduced
             # over the r axes by the native column reduction
             from ..kernels import reduce as KR

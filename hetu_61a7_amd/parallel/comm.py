@@ -72,15 +72,12 @@ def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] 
             os.environ['MASTER_PORT'] = str(_free_port()) if world == 1 else '29517'
         os.environ.setdefault('RANK', str(rank))
         os.environ.setdefault('WORLD_SIZE', str(world))
+        # no device_id: torch's ProcessGroupNCCL then creates its RCCL communicator lazily,
+        # on a first torch collective that the native path never issues -- one RCCL
+        # communicator per rank (the in-house one, parallel/rccl.py), not two
         kw = dict(backend=backend_for_device(use_gpu), rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
-        if use_gpu and kw['backend'] == 'nccl':
-            kw['device_id'] = torch.device('cuda', torch.cuda.current_device())
-        try:
-            dist.init_process_group(**kw)
-        except TypeError:
-            kw.pop('device_id', None)
-            dist.init_process_group(**kw)
+        dist.init_process_group(**kw)
     _WORLD = Communicator(None, use_gpu=use_gpu)
     return _WORLD
 
@@ -145,14 +142,25 @@ class Communicator(object):
         self.global_rank = dist.get_rank()
         self.local_rank = dist_env()[2]
         self.device_id = self.local_rank
+        self._bar = None
         # GPU collectives: the in-house RCCL communicator (csrc/comm/hetu_comm.cc) unless
-        # HETU_COMM=torch; torch.distributed stays the bootstrap / host-tensor path
+        # HETU_COMM=torch; torch.distributed stays the bootstrap / host-tensor path.
+        # Static sub-groups (created by every rank in the same order) are ncclCommSplit
+        # children of the world communicator -- no new unique-id rendezvous or full
+        # ncclCommInitRank per group; non-members take part in the split with no colour.
+        # Partial-reduce groups (local_sync: only the members call) rendezvous by store.
         self.native = None
-        if use_gpu and self.rank >= 0 and os.environ.get('HETU_COMM', 'native') != 'torch' \
-                and dist.get_backend(self.group) == 'nccl':
+        if use_gpu and os.environ.get('HETU_COMM', 'native') != 'torch' and dist.get_backend() == 'nccl':
             from . import rccl
             if rccl.available():
-                self.native = rccl.world_from_dist(self.group)
+                w = _WORLD.native if _WORLD is not None else None
+                if ranks is None:
+                    self.native = rccl.world_from_dist(None)
+                elif not local_sync and w is not None:
+                    sub = w.split(0 if self.rank >= 0 else -1, self.global_rank)
+                    self.native = sub if self.rank >= 0 else None
+                elif self.rank >= 0:
+                    self.native = rccl.world_from_dist(self.group)
         self.group_backend = dist.get_backend(self.group) if self.rank >= 0 else None
         self.backend = 'hetu-rccl' if self.native is not None else \
             (dist.get_backend(self.group) if self.rank >= 0 else 'non-member')
@@ -283,7 +291,14 @@ class Communicator(object):
         return dist.batch_isend_irecv(p2p)
 
     def barrier(self):
-        if self.use_gpu and dist.get_backend(self.group) == 'nccl':
+        """host barrier: a 1-element all-reduce on the native communicator, then the host
+        waits for it (torch's barrier would create torch's own RCCL communicator)"""
+        if self.native is not None:
+            if self._bar is None:
+                self._bar = torch.zeros(1, dtype=torch.float32, device='cuda')
+            self.native.all_reduce(self._bar)
+            torch.cuda.current_stream().synchronize()
+        elif self.use_gpu and dist.get_backend(self.group) == 'nccl':
             dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier(group=self.group)
@@ -310,6 +325,15 @@ class _PostDiv(object):
     def wait(self):
         self.work.wait()
         self.t.div_(self.n)
+
+
+def stats():
+    """{'backend', 'world', 'communicators'}: what this rank's comm layer holds (bench JSON)"""
+    from . import rccl
+    w = _WORLD
+    return {'backend': w.backend if w is not None else 'none', 'world': w.nrank if w is not None else 1,
+            'native_communicators': rccl.NativeComm.created,
+            'groups': len(_GROUPS)}
 
 
 def destroy():

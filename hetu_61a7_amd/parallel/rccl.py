@@ -121,6 +121,7 @@ class NativeComm(object):
     """One RCCL communicator (a group of ``nrank`` ranks, this process = ``rank``)."""
 
     _store_seq = {}
+    created = 0     # communicators this process created (init_rank + split), bench JSON
 
     def __init__(self, handle, rank, nrank):
         self.handle = ctypes.c_void_p(handle) if not isinstance(handle, ctypes.c_void_p) else handle
@@ -148,6 +149,7 @@ class NativeComm(object):
             uid = bytes(store.get(key))
         h = ctypes.c_void_p()
         _check(L.hcomm_init(uid, int(nrank), int(rank), ctypes.byref(h)), 'comm_init_rank')
+        NativeComm.created += 1
         return cls(h, rank, nrank)
 
     def split(self, color, key):
@@ -157,6 +159,7 @@ class NativeComm(object):
         if color < 0 or not h.value:
             return None
         L = lib()
+        NativeComm.created += 1
         return NativeComm(h, L.hcomm_user_rank(h), L.hcomm_count(h))
 
     def destroy(self):
@@ -269,6 +272,10 @@ class NativeComm(object):
         from ..kernels import comm as KC
         P, n = self.nrank, t.numel()
         assert t.dtype == torch.float32 and t.is_contiguous()
+        if not async_op:
+            # the workspaces are shared with async calls on the comm stream: a sync call on
+            # the caller's stream must not overtake a bucket still using them
+            torch.cuda.current_stream().wait_stream(self.stream)
         c = -(-n // (8 * P)) * 8
         send = self._ws(c * P, torch.bfloat16, 'send')
         recv = self._ws(c * P, torch.bfloat16, 'recv')

@@ -217,3 +217,27 @@ def test_vendor_dgrad_mixed_layout_regression():
         dx = KC._vendor_dgrad(g, w, tuple(x.shape), (1, 1), (1, 1))
         torch.cuda.synchronize()
         assert _rel(dx, x.grad) < 1e-5
+
+
+@pytest.mark.parametrize('n,h', [(2, 56), (3, 57), (1, 5)])
+def test_conv3x3_c64_halo_kernel(n, h):
+    """3x3/s1/p1 64->64 halo-tile kernel: forward (+ fused BN statistics) and data
+    gradient (+ bf16 / fp32 join) against fp32 autograd on the same bf16 operands."""
+    x = torch.randn(n, 64, h, 56, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(64, 64, 3, 3, device=DEV) * 0.05).bfloat16().contiguous(memory_format=CL)
+    st = torch.zeros(128, device=DEV)
+    y = CI.try_conv3x3_forward(x, w, (1, 1), (1, 1), colstats=st)
+    assert y is not None and y.is_contiguous(memory_format=CL)
+    xf = x.float().requires_grad_(True)
+    ref = F.conv2d(xf, w.float(), None, 1, 1)
+    assert _rel(y, ref) < _tol(y)
+    yf = y.float()
+    assert _rel(st[:64], yf.sum((0, 2, 3))) < 1e-4 and _rel(st[64:], (yf * yf).sum((0, 2, 3))) < 1e-4
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
+    ref.backward(dy.float())
+    dx = CI.try_conv3x3_backward_data(dy, w, x.shape, (1, 1), (1, 1))
+    assert dx is not None and _rel(dx, xf.grad) < _tol(dx)
+    for dt in (torch.bfloat16, torch.float32):
+        r = torch.randn(x.shape, device=DEV).to(dt).contiguous(memory_format=CL)
+        dx2 = CI.try_conv3x3_backward_data(dy, w, x.shape, (1, 1), (1, 1), acc=r)
+        assert _rel(dx2, xf.grad + r.float()) < _tol(dx2)

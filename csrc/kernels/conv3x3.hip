@@ -241,6 +241,153 @@ int dispatch_c64(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin
   return (int)hipErrorInvalidValue;
 }
 
+
+// ---- weight gradient ---------------------------------------------------------------------
+// dW[co][kh][kw][ci] = sum over pixels dy[px][co] * x[px + (kh-1, kw-1)][ci].  Same walk as
+// the forward (one block per image, TH-row tiles, DMA ring of halo rows, prefetch of the
+// next tile), plus the tile's dy rows as a [px][64] swizzled image (double buffered).  The
+// reduction over pixels needs pixel-contiguous MFMA operands: both are gathered with the
+// hardware transpose read (T10) -- lane 4q+p of a 16-lane group supplies the address of
+// pixel row q and 4 contiguous channels, so each lane receives 4 pixels of its channel.
+// Wave w owns output channel block (w & 3) x input channel blocks 2(w>>2), 2(w>>2)+1 for all
+// 9 taps: 18 accumulator tiles D[ci][co] (4 consecutive ci per lane -> float4 stores).  The
+// block's partial goes to a slab; wgrad_reduce_k sums the slabs into dW.
+constexpr int WG_NW = 8;
+constexpr int WG_PX = 224;                       // pixels per tile (4 rows of 56)
+
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+
+__device__ __forceinline__ v8s tr_pair(const char* a, const char* b) {
+  v4s_t x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(a));
+  v4s_t y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(b));
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int WD, int TH>
+__global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16* __restrict__ x,
+                                                                   const bf16* __restrict__ dy,
+                                                                   float* __restrict__ slab, int H) {
+  constexpr int NSLOT = 2 * TH + 2;
+  constexpr int PX = TH * WD;
+  constexpr int DYB = PX * 128;                   // one dy tile image
+  static_assert(PX % 32 == 0, "pixel tile must be whole 32-pixel k-steps");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * ROWB + 2 * DYB];
+  char* ring = smem;
+  char* dyl = smem + NSLOT * ROWB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = blockIdx.x;
+  const bf16* img = x + (int64_t)n * H * WD * CH;
+  const bf16* gimg = dy + (int64_t)n * H * WD * CH;
+
+  auto stage_rows = [&](int r0, int nrows) {
+    for (int I = wave; I < nrows * 8; I += WG_NW) {
+      const int rr = I >> 3, pos0 = (I & 7) * 8;
+      const int ih = r0 + rr;
+      const int slot = (ih + 1 + NSLOT) % NSLOT;
+      const int pos = pos0 + (lane >> 3);
+      const int c = (lane & 7) ^ (pos & 7);
+      const int iw = pos - 1;
+      const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < WD;
+      const void* src = ok ? (const void*)(img + ((int64_t)ih * WD + iw) * CH + c * 8) : (const void*)g_zero16;
+      dma16(src, ring + slot * ROWB + pos0 * 128);
+    }
+  };
+  // dy rows oh0 .. oh0+TH-1 into dy buffer b: PX/8 instructions of 8 pixels
+  auto stage_dy = [&](int oh0, int b) {
+    for (int I = wave; I < PX / 8; I += WG_NW) {
+      const int px = I * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (px & 7);
+      const int ty = px / WD, tx = px - ty * WD;
+      const bool ok = oh0 + ty < H;
+      const void* src = ok ? (const void*)(gimg + ((int64_t)(oh0 + ty) * WD + tx) * CH + c * 8) : (const void*)g_zero16;
+      dma16(src, dyl + b * DYB + I * 1024);
+    }
+  };
+
+  stage_rows(-1, TH + 2);
+  stage_dy(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int cb = wave & 3, cib0 = 2 * (wave >> 2);
+  v4f acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[t][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = (H + TH - 1) / TH;
+  for (int t = 0; t < ntiles; ++t) {
+    const int oh0 = t * TH, cur = t & 1;
+    if (t + 1 < ntiles) {
+      stage_rows(oh0 + TH + 1, TH);
+      stage_dy(oh0 + TH, cur ^ 1);
+    }
+    const char* dyb = dyl + cur * DYB;
+#pragma unroll 1
+    for (int st = 0; st < PX / 32; ++st) {
+      const int px0 = st * 32 + 8 * g + q, px1 = px0 + 4;
+      // dy operand: pixels px0 / px1, channels 16cb + 4p .. +3
+      const int dch = 2 * cb + (p >> 1), dof = (p & 1) * 8;
+      const v8s bf = tr_pair(dyb + px0 * 128 + ((dch ^ (px0 & 7)) << 4) + dof,
+                             dyb + px1 * 128 + ((dch ^ (px1 & 7)) << 4) + dof);
+      const int ty0 = px0 / WD, tx0 = px0 - ty0 * WD, ty1 = px1 / WD, tx1 = px1 - ty1 * WD;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const char* r0 = ring + ((oh0 + ty0 + kh) % NSLOT) * ROWB;
+        const char* r1 = ring + ((oh0 + ty1 + kh) % NSLOT) * ROWB;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int pos0 = tx0 + kw, pos1 = tx1 + kw;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int xch = 2 * (cib0 + j) + (p >> 1);
+            const v8s af = tr_pair(r0 + pos0 * 128 + ((xch ^ (pos0 & 7)) << 4) + dof,
+                                   r1 + pos1 * 128 + ((xch ^ (pos1 & 7)) << 4) + dof);
+            acc[kh * 3 + kw][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[kh * 3 + kw][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // lane holds D[ci = 16*cib + 4g + i][co = 16cb + (lane & 15)] of every tap
+  float* S = slab + (int64_t)n * 9 * CH * CH;
+  const int co = 16 * cb + (lane & 15);
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      *reinterpret_cast<float4*>(S + ((int64_t)co * 9 + tp) * CH + 16 * (cib0 + j) + 4 * g) =
+          make_float4(acc[tp][j][0], acc[tp][j][1], acc[tp][j][2], acc[tp][j][3]);
+}
+
+// dw[i] (+)= sum over nb slabs of slab[b][i], i over 64*9*64 fp32 (float4 per thread)
+__global__ void __launch_bounds__(256) wgrad_slab_reduce_k(const float4* __restrict__ slab, int nb,
+                                                           float4* __restrict__ dw, int n4, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  int k = 0;
+  for (; k + 1 < nb; k += 2) {
+    const float4 u = slab[(int64_t)k * n4 + i], v = slab[(int64_t)(k + 1) * n4 + i];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+  }
+  if (k < nb) {
+    const float4 u = slab[(int64_t)k * n4 + i];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+  }
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  if (accumulate) {
+    const float4 o = dw[i];
+    a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+  }
+  dw[i] = a;
+}
 }  // namespace
 
 HETU_API int hetu_conv3x3_c64_supported(int C, int K, int W) { return C == CH && K == CH && W == 56; }
@@ -260,4 +407,22 @@ HETU_API int hetu_conv3x3_c64_dgrad(const void* dy, const void* w, void* wt, voi
   hipLaunchKernelGGL(flip_bank_k, dim3((CH * 9 * CH + 255) / 256), dim3(256), 0, st, (const bf16*)w, (bf16*)wt);
   HETU_LAUNCH_CHECK();
   return dispatch_c64((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, nullptr, N, H, W, st);
+}
+
+// slab floats hetu_conv3x3_c64_wgrad needs for a batch of N images
+HETU_API int64_t hetu_conv3x3_c64_wgrad_ws(int N) { return (int64_t)N * 9 * CH * CH; }
+
+// dw[64][3][3][64] fp32 (+)= weight gradient of the 3x3/s1/p1 64->64 convolution;
+// x, dy [N,H,W,64] bf16; ws: hetu_conv3x3_c64_wgrad_ws(N) floats
+HETU_API int hetu_conv3x3_c64_wgrad(const void* x, const void* dy, float* dw, float* ws, int accumulate, int N,
+                                    int H, int W, hipStream_t st) {
+  if ((((uintptr_t)x) | ((uintptr_t)dy) | ((uintptr_t)dw) | ((uintptr_t)ws)) & 15) return (int)hipErrorInvalidValue;
+  if (W != 56) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv3x3_c64_wgrad_k<56, 4>), dim3(N), dim3(WG_NW * 64), 0, st, (const bf16*)x,
+                     (const bf16*)dy, ws, H);
+  HETU_LAUNCH_CHECK();
+  const int n4 = 9 * CH * CH / 4;
+  hipLaunchKernelGGL(wgrad_slab_reduce_k, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws, N,
+                     (float4*)dw, n4, accumulate);
+  return (int)hipGetLastError();
 }

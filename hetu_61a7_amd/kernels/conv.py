@@ -460,6 +460,9 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                                                                    accumulate=False, tile=2)
             blas['hip64t'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                                     accumulate=False, tile=4)
+        if conv_igemm.conv3x3_ok(x.shape, w_shape, stride, padding):
+            blas = dict(blas or {})
+            blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=out)
         return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
                      lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                             accumulate=False),

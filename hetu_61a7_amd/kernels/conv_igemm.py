@@ -179,6 +179,30 @@ def try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=None):
     return dx.permute(0, 3, 1, 2)
 
 
+def try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=False):
+    """weight gradient of the 64-channel 3x3/s1/p1 convolution on the halo-tile kernel
+    (per-image fp32 partials in a slab, then one reduce) into ``out`` (fp32 channels-last
+    [K, C, 3, 3] view) or a new tensor"""
+    if not (_ok(x, g, x.shape[1], g.shape[1]) and conv3x3_ok(x.shape, w_shape, stride, padding)):
+        return None
+    N, C, H, W = x.shape
+    K = w_shape[0]
+    if out is None:
+        dw = torch.empty((K, 3, 3, C), dtype=torch.float32, device=g.device)
+        accumulate = False
+    else:
+        dw = out.permute(0, 2, 3, 1)
+        if not dw.is_contiguous() or dw.dtype != torch.float32 or dw.data_ptr() % 16:
+            return None
+    ws = torch.empty(int(fn('hetu_conv3x3_c64_wgrad_ws', [I32], restype=I64)(N)), dtype=torch.float32,
+                     device=g.device)
+    f = fn('hetu_conv3x3_c64_wgrad', [P, P, P, P, I32, I32, I32, I32, P])
+    check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), int(bool(accumulate)), N, H, W,
+            stream_ptr()), 'conv3x3_wgrad')
+    record_native('conv3x3_wgrad')
+    return dw.permute(0, 3, 1, 2)
+
+
 STEM_WGRAD_BLOCKS = 512
 
 

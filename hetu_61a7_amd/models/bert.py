@@ -358,7 +358,9 @@ def bert_bench(args, world, rank, local):
         opt = optim.SGDOptimizer(learning_rate=getattr(args, 'lr', 1e-2))
     if plan.pp > 1:
         kw.pop('zero')
-        cfg.batch_size = B * plan.pp                 # one replica's batch: global / (N / pp)
+        # one replica's batch is global / (N / pp) = B * pp, fed as plan.micro_batches
+        # micro-batches: the graph is built for one micro-batch
+        cfg.batch_size = B * plan.pp // plan.micro_batches
         feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-5, plan=plan, optimizer=opt)
         ex = H.Executor({'train': [loss, train]}, pipeline='gpipe', **kw)
         sub = ex.subexecutor['train']
@@ -376,7 +378,7 @@ def bert_bench(args, world, rank, local):
     # every layout (dp N, pp x dp, one process) trains on the same global batch
     import copy
     gcfg = copy.copy(cfg)
-    rb = cfg.batch_size
+    rb = B * plan.pp if plan.pp > 1 else cfg.batch_size
     gcfg.batch_size = B * world
     full = synthetic_bert_batch(gcfg, seed=10)
     batch = {k: v[replica * rb:(replica + 1) * rb] for k, v in full.items()}

@@ -275,8 +275,8 @@ class GalvatronPlanner(object):
             for m in micro_batches:
                 if pp == 1 and m > 1:
                     continue
-                if global_batch % m:
-                    continue
+                if global_batch % m or (global_batch // n) % m:
+                    continue       # every data-parallel replica's batch splits into m micro-batches
                 stage_time, stage_mem, tps, dps = [], [], [], []
                 ok = True
                 for s, (a, b) in enumerate(bounds):

@@ -241,3 +241,11 @@ def test_conv3x3_c64_halo_kernel(n, h):
         r = torch.randn(x.shape, device=DEV).to(dt).contiguous(memory_format=CL)
         dx2 = CI.try_conv3x3_backward_data(dy, w, x.shape, (1, 1), (1, 1), acc=r)
         assert _rel(dx2, xf.grad + r.float()) < _tol(dx2)
+    wf = w.float().requires_grad_(True)
+    F.conv2d(x.float(), wf, None, 1, 1).backward(dy.float())
+    dw = CI.try_conv3x3_backward_filter(dy, x, w.shape, (1, 1), (1, 1))
+    assert dw is not None and dw.dtype == torch.float32 and _rel(dw, wf.grad) < 2e-5
+    out = torch.randn(64, 64, 3, 3, device=DEV).contiguous(memory_format=CL)
+    base = out.clone()
+    CI.try_conv3x3_backward_filter(dy, x, w.shape, (1, 1), (1, 1), out=out, accumulate=True)
+    assert _rel(out - base, wf.grad) < 1e-4

@@ -20,6 +20,8 @@
 // Replaces cuDNN/MIOpen for these shapes (reference src/ops/CudnnConv2d.cu:54-70).
 #include "common.h"
 
+#include <algorithm>
+
 using namespace hetu;
 
 namespace {
@@ -388,6 +390,345 @@ __global__ void __launch_bounds__(256) wgrad_slab_reduce_k(const float4* __restr
   }
   dw[i] = a;
 }
+
+// ---- wide layers: C, K multiples of 64 / 128 ---------------------------------------------
+// ResNet-50 stages 2-4 (128 ch @ 28x28, 256 @ 14x14, 512 @ 7x7): the filter bank no longer
+// fits in LDS, so a block owns a pixel tile (TH full rows of IMG images, padded to 7
+// 16-pixel blocks) x 128 output channels and walks K = (64-channel chunk, tap):
+//   * per chunk the tile's halo [IMG][TH+2][W+2][64] is DMA'd once and serves all 9 taps
+//     (the implicit-GEMM loaders fetch it 9 times);
+//   * per (chunk, tap) the 128 x 64 filter slice is DMA'd (16 KiB, L2-resident: every
+//     pixel tile of a channel block reads the same slices);
+//   * single LDS stage (39 KiB) and <= 128 registers: 4 blocks per CU hide each other's
+//     DMA waits (the short-K regime, cf. the gemm_core tile 3).
+// Waves own two 16-channel blocks x all 7 pixel blocks (14 accumulator tiles D[co][px]).
+constexpr int WPB = 7;                 // pixel blocks per tile
+constexpr int WBN = 128;               // output channels per block
+constexpr int WSL = WBN * 128;         // one filter slice image [128 co][64 ci], 16 KiB
+
+template <int WD, int TH, int IMG>
+struct WGeo {
+  static constexpr int HP = TH + 2, WP = WD + 2;
+  static constexpr int POS = IMG * HP * WP;                  // halo positions
+  static constexpr int POS8 = (POS + 7) / 8 * 8;
+  static constexpr int PXT = IMG * TH * WD;                  // real pixels per tile
+  static_assert(PXT <= WPB * 16, "tile exceeds 7 pixel blocks");
+};
+
+template <int WD, int TH, int IMG>
+__global__ __launch_bounds__(256, 4) void conv3x3_wide_k(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                         bf16* __restrict__ y, const void* cin, int cin_f32,
+                                                         float* colstats, int N, int H, int C, int K) {
+  using G = WGeo<WD, TH, IMG>;
+  __shared__ __attribute__((aligned(16))) char smem[G::POS8 * 128 + WSL];
+  char* halo = smem;
+  char* wl = smem + G::POS8 * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kblocks = K / WBN;
+  const int cob = blockIdx.x % kblocks, tile = blockIdx.x / kblocks;
+  const int tpi = (H + TH - 1) / TH;                         // row tiles per image (IMG == 1)
+  const int n0 = IMG == 1 ? tile / tpi : tile * IMG;
+  const int r0 = IMG == 1 ? (tile - n0 * tpi) * TH : 0;
+
+  // this lane's pixel slots: halo base position (tap (0,0)) and output pixel of each block
+  int hb[WPB];
+  int64_t opx[WPB];
+#pragma unroll
+  for (int b = 0; b < WPB; ++b) {
+    const int sidx = b * 16 + (lane & 15);
+    const bool v = sidx < G::PXT;
+    const int sc = v ? sidx : 0;
+    const int il = sc / (TH * WD), rem = sc - il * (TH * WD), ty = rem / WD, tx = rem - ty * WD;
+    hb[b] = (il * G::HP + ty) * G::WP + tx;
+    const int oh = r0 + ty, n = n0 + il;
+    opx[b] = (v && oh < H && n < N) ? ((int64_t)n * H + oh) * WD + tx : -1;
+  }
+  const int q4 = lane >> 4;
+
+  float cs[8], cq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { cs[i] = 0.f; cq[i] = 0.f; }
+  v4f acc[WPB][2];
+#pragma unroll
+  for (int b = 0; b < WPB; ++b)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[b][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = C / 64;
+  for (int ch = 0; ch < nch; ++ch) {
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap == 0) {
+        // halo of chunk ch: POS8/8 wave instructions of 8 positions x 8 chunks
+        for (int I = wave; I < G::POS8 / 8; I += 4) {
+          const int pos = I * 8 + (lane >> 3);
+          const int c = (lane & 7) ^ (pos & 7);
+          const int il = pos / (G::HP * G::WP), rr = pos - il * (G::HP * G::WP);
+          const int hy = rr / G::WP, hx = rr - hy * G::WP;
+          const int ih = r0 + hy - 1, iw = hx - 1, n = n0 + il;
+          const bool ok = pos < G::POS && n < N && ih >= 0 && ih < H && iw >= 0 && iw < WD;
+          const void* src = ok ? (const void*)(x + (((int64_t)n * H + ih) * WD + iw) * C + ch * 64 + c * 8)
+                               : (const void*)g_zero16;
+          dma16(src, halo + I * 1024);
+        }
+      }
+      // filter slice: rows co (128), chunks of ci ch*64 .. +64 of tap `tap`
+      for (int I = wave; I < WBN / 8; I += 4) {
+        const int co = I * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (co & 7);
+        dma16(w + (((int64_t)(cob * WBN + co)) * 9 + tap) * C + ch * 64 + c * 8, wl + I * 1024);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int kh = tap / 3, kw = tap - kh * 3, toff = kh * G::WP + kw;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + q4;
+        v8s wf[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) wf[j] = *reinterpret_cast<const v8s*>(wl + swz((2 * wave + j) * 16 + (lane & 15), c));
+#pragma unroll
+        for (int b = 0; b < WPB; ++b) {
+          const v8s pf = *reinterpret_cast<const v8s*>(halo + swz(hb[b] + toff, c));
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[b][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf, acc[b][j], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // epilogue: lane holds channels cob*128 + (2*wave + j)*16 + 4*q4 + i of its pixels
+#pragma unroll
+  for (int b = 0; b < WPB; ++b) {
+    if (opx[b] < 0) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = cob * WBN + (2 * wave + j) * 16 + 4 * q4;
+      float v[4] = {acc[b][j][0], acc[b][j][1], acc[b][j][2], acc[b][j][3]};
+      if (cin) {
+        if (cin_f32) {
+          const float4 a = *reinterpret_cast<const float4*>((const float*)cin + opx[b] * K + co);
+          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        } else {
+          const uint2 a = *reinterpret_cast<const uint2*>((const bf16*)cin + opx[b] * K + co);
+          v[0] += bf16_bits_to_f((unsigned short)(a.x & 0xffffu));
+          v[1] += bf16_bits_to_f((unsigned short)(a.x >> 16));
+          v[2] += bf16_bits_to_f((unsigned short)(a.y & 0xffffu));
+          v[3] += bf16_bits_to_f((unsigned short)(a.y >> 16));
+        }
+      }
+      unsigned short h[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        h[i] = f_to_bf16_bits(v[i]);
+        const float sv = bf16_bits_to_f(h[i]);
+        cs[j * 4 + i] += sv;
+        cq[j * 4 + i] += sv * sv;
+      }
+      uint2 pk;
+      pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+      pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+      *reinterpret_cast<uint2*>(y + opx[b] * K + co) = pk;
+    }
+  }
+  if (colstats) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        cs[i] += __shfl_xor(cs[i], o, 64);
+        cq[i] += __shfl_xor(cq[i], o, 64);
+      }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = cob * WBN + (2 * wave + j) * 16 + 4 * q4 + i;
+          unsafeAtomicAdd(colstats + co, cs[j * 4 + i]);
+          unsafeAtomicAdd(colstats + K + co, cq[j * 4 + i]);
+        }
+    }
+  }
+}
+
+// w'[ci][tap][co] = w[co][8 - tap][ci] for any C, K
+__global__ void __launch_bounds__(256) flip_bank_any_k(const bf16* __restrict__ w, bf16* __restrict__ wt, int C,
+                                                       int K) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)C * 9 * K) return;
+  const int ci = (int)(i / (9 * K)), r = (int)(i - (int64_t)ci * 9 * K), tap = r / K, co = r - tap * K;
+  wt[i] = w[((int64_t)co * 9 + (8 - tap)) * C + ci];
+}
+
+template <int WD, int TH, int IMG>
+int launch_wide(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
+                int C, int K, hipStream_t st) {
+  const int tiles = IMG == 1 ? N * ((H + TH - 1) / TH) : (N + IMG - 1) / IMG;
+  hipLaunchKernelGGL((conv3x3_wide_k<WD, TH, IMG>), dim3(tiles * (K / WBN)), dim3(256), 0, st, x, w, y, cin,
+                     cin_f32, colstats, N, H, C, K);
+  return (int)hipGetLastError();
+}
+
+int dispatch_wide(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
+                  int W, int C, int K, hipStream_t st) {
+  if (W == 56 && H % 2 == 0) return launch_wide<56, 2, 1>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
+  if (W == 28 && H % 4 == 0) return launch_wide<28, 4, 1>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
+  if (W == 14 && H % 7 == 0) return launch_wide<14, 7, 1>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
+  if (W == 7 && H == 7) return launch_wide<7, 7, 2>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
+  return (int)hipErrorInvalidValue;
+}
+
+bool wide_ok(int C, int K, int H, int W) {
+  return C % 64 == 0 && K % WBN == 0 && ((W == 56 && H % 2 == 0) || (W == 28 && H % 4 == 0) ||
+                                         (W == 14 && H % 7 == 0) || (W == 7 && H == 7));
+}
+
+// ---- weight gradient of the wide layers --------------------------------------------------
+// Block = (64 output channels, 64 input channels) x a group of pixel tiles (the tiles of
+// conv3x3_wide_k, padded to whole 32-pixel k-steps with zero dy rows); per tile the input
+// channel chunk's halo and the tile's dy columns are DMA'd into LDS and the 8 waves run the
+// conv3x3_c64_wgrad_k reduction (transpose-read operands, 18 accumulator tiles per wave, all
+// 9 taps).  Each block stores its fp32 partial [64 co][9][64 ci] into a slab; a reduce sums
+// the pixel groups of each channel pair into dW[K][3][3][C].
+template <int WD, int TH, int IMG>
+__global__ __launch_bounds__(WG_NW * 64, 2) void conv3x3_wide_wgrad_k(const bf16* __restrict__ x,
+                                                                     const bf16* __restrict__ dy,
+                                                                     float* __restrict__ slab, int N, int H, int C,
+                                                                     int K, int groups) {
+  using G = WGeo<WD, TH, IMG>;
+  constexpr int PXP = (G::PXT + 31) / 32 * 32;
+  __shared__ __attribute__((aligned(16))) char smem[G::POS8 * 128 + PXP * 128];
+  char* halo = smem;
+  char* dyl = smem + G::POS8 * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kb = K / 64, pairs = kb * (C / 64);
+  const int pair = blockIdx.x % pairs, grp = blockIdx.x / pairs;
+  const int cob = pair % kb, cich = pair / kb;
+  const int tpi = (H + TH - 1) / TH;
+  const int ntiles = IMG == 1 ? N * tpi : (N + IMG - 1) / IMG;
+
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int cb = wave & 3, cib0 = 2 * (wave >> 2);
+  const int dof = (p & 1) * 8;
+  // halo base positions of the lane's two pixel rows in each of the PXP/32 k-steps are
+  // recomputed per step (cheap: compile-time divisors)
+  auto hbase = [&](int px) {
+    const int pc = px < G::PXT ? px : 0;
+    const int il = pc / (TH * WD), rem = pc - il * (TH * WD), ty = rem / WD, tx = rem - ty * WD;
+    return (il * G::HP + ty) * G::WP + tx;
+  };
+
+  v4f acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[t][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  for (int tile = grp; tile < ntiles; tile += groups) {
+    const int n0 = IMG == 1 ? tile / tpi : tile * IMG;
+    const int r0 = IMG == 1 ? (tile - n0 * tpi) * TH : 0;
+    for (int I = wave; I < G::POS8 / 8; I += WG_NW) {
+      const int pos = I * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (pos & 7);
+      const int il = pos / (G::HP * G::WP), rr = pos - il * (G::HP * G::WP);
+      const int hy = rr / G::WP, hx = rr - hy * G::WP;
+      const int ih = r0 + hy - 1, iw = hx - 1, n = n0 + il;
+      const bool ok = pos < G::POS && n < N && ih >= 0 && ih < H && iw >= 0 && iw < WD;
+      const void* src = ok ? (const void*)(x + (((int64_t)n * H + ih) * WD + iw) * C + cich * 64 + c * 8)
+                           : (const void*)g_zero16;
+      dma16(src, halo + I * 1024);
+    }
+    for (int I = wave; I < PXP / 8; I += WG_NW) {
+      const int px = I * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (px & 7);
+      const int il = px / (TH * WD), rem = px - il * (TH * WD), ty = rem / WD, tx = rem - ty * WD;
+      const int n = n0 + il, oh = r0 + ty;
+      const bool ok = px < G::PXT && n < N && oh < H;
+      const void* src = ok ? (const void*)(dy + (((int64_t)n * H + oh) * WD + tx) * K + cob * 64 + c * 8)
+                           : (const void*)g_zero16;
+      dma16(src, dyl + I * 1024);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll 1
+    for (int st = 0; st < PXP / 32; ++st) {
+      const int px0 = st * 32 + 8 * g + q, px1 = px0 + 4;
+      const int dch = 2 * cb + (p >> 1);
+      const v8s bf = tr_pair(dyl + px0 * 128 + ((dch ^ (px0 & 7)) << 4) + dof,
+                             dyl + px1 * 128 + ((dch ^ (px1 & 7)) << 4) + dof);
+      const int h0 = hbase(px0), h1 = hbase(px1);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int pos0 = h0 + kh * G::WP + kw, pos1 = h1 + kh * G::WP + kw;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int xch = 2 * (cib0 + j) + (p >> 1);
+            const v8s af = tr_pair(halo + pos0 * 128 + ((xch ^ (pos0 & 7)) << 4) + dof,
+                                   halo + pos1 * 128 + ((xch ^ (pos1 & 7)) << 4) + dof);
+            acc[kh * 3 + kw][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[kh * 3 + kw][j], 0, 0, 0);
+          }
+        }
+    }
+    __syncthreads();
+  }
+  // slab[block][co 64][tap][ci 64]
+  float* S = slab + (int64_t)blockIdx.x * 9 * 64 * 64;
+  const int co = 16 * cb + (lane & 15);
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      *reinterpret_cast<float4*>(S + ((int64_t)co * 9 + tp) * 64 + 16 * (cib0 + j) + 4 * g) =
+          make_float4(acc[tp][j][0], acc[tp][j][1], acc[tp][j][2], acc[tp][j][3]);
+}
+
+// dw[co][tap][ci] (+)= sum over the pixel groups of slab[grp*pairs + pair][co%64][tap][ci%64]
+__global__ void __launch_bounds__(256) wide_wgrad_reduce_k(const float4* __restrict__ slab, int groups, int pairs,
+                                                           int kb, float4* __restrict__ dw, int C, int K,
+                                                           int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;       // float4 of dw
+  const int64_t n4 = (int64_t)K * 9 * C / 4;
+  if (i >= n4) return;
+  const int64_t e = i * 4;
+  const int co = (int)(e / (9 * C)), r = (int)(e - (int64_t)co * 9 * C), tap = r / C, ci = r - tap * C;
+  const int pair = (ci / 64) * kb + co / 64;
+  const int64_t off = ((int64_t)(co % 64) * 9 + tap) * 64 + (ci % 64);   // floats within a block slab
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int gi = 0; gi < groups; ++gi) {
+    const float4 u = slab[(((int64_t)gi * pairs + pair) * 9 * 64 * 64 + off) / 4];
+    a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+  }
+  if (accumulate) {
+    const float4 o = dw[i];
+    a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+  }
+  dw[i] = a;
+}
+
+template <int WD, int TH, int IMG>
+int launch_wide_wgrad(const bf16* x, const bf16* dy, float* dw, float* ws, int64_t ws_floats, int accumulate, int N,
+                      int H, int C, int K, hipStream_t st) {
+  const int pairs = (K / 64) * (C / 64);
+  const int ntiles = IMG == 1 ? N * ((H + TH - 1) / TH) : (N + IMG - 1) / IMG;
+  int groups = std::max(1, std::min(ntiles, 512 / pairs));
+  while ((int64_t)groups * pairs * 9 * 64 * 64 > ws_floats && groups > 1) --groups;
+  if ((int64_t)groups * pairs * 9 * 64 * 64 > ws_floats) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv3x3_wide_wgrad_k<WD, TH, IMG>), dim3(groups * pairs), dim3(WG_NW * 64), 0, st, x, dy, ws,
+                     N, H, C, K, groups);
+  HETU_LAUNCH_CHECK();
+  const int64_t n4 = (int64_t)K * 9 * C / 4;
+  hipLaunchKernelGGL(wide_wgrad_reduce_k, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, (const float4*)ws,
+                     groups, pairs, K / 64, (float4*)dw, C, K, accumulate);
+  return (int)hipGetLastError();
+}
+
+bool wide_wgrad_ok(int C, int K, int H, int W) {
+  return C % 64 == 0 && K % 64 == 0 && ((W == 28 && H % 4 == 0) || (W == 14 && H % 7 == 0) || (W == 7 && H == 7));
+}
 }  // namespace
 
 HETU_API int hetu_conv3x3_c64_supported(int C, int K, int W) { return C == CH && K == CH && W == 56; }
@@ -425,4 +766,45 @@ HETU_API int hetu_conv3x3_c64_wgrad(const void* x, const void* dy, float* dw, fl
   hipLaunchKernelGGL(wgrad_slab_reduce_k, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws, N,
                      (float4*)dw, n4, accumulate);
   return (int)hipGetLastError();
+}
+
+HETU_API int hetu_conv3x3_wide_supported(int C, int K, int H, int W) { return wide_ok(C, K, H, W); }
+
+// y[N,H,W,K] = conv3x3(x[N,H,W,C], w[K][3][3][C]) (stride 1, pad 1), C % 64 == 0, K % 128 == 0
+HETU_API int hetu_conv3x3_wide_fwd(const void* x, const void* w, void* y, float* colstats, int N, int H, int W, int C,
+                                   int K, hipStream_t st) {
+  if (!wide_ok(C, K, H, W) || ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)y)) & 15))
+    return (int)hipErrorInvalidValue;
+  return dispatch_wide((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, N, H, W, C, K, st);
+}
+
+// dx[N,H,W,C] = conv3x3^T(dy[N,H,W,K], w) (+ acc), K % 64 == 0, C % 128 == 0; wt: C*9*K bf16
+HETU_API int hetu_conv3x3_wide_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
+                                     int N, int H, int W, int C, int K, hipStream_t st) {
+  if (!wide_ok(K, C, H, W) || ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc)) & 15))
+    return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)C * 9 * K;
+  hipLaunchKernelGGL(flip_bank_any_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const bf16*)w, (bf16*)wt,
+                     C, K);
+  HETU_LAUNCH_CHECK();
+  return dispatch_wide((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, nullptr, N, H, W, K, C, st);
+}
+
+HETU_API int hetu_conv3x3_wide_wgrad_supported(int C, int K, int H, int W) { return wide_wgrad_ok(C, K, H, W); }
+
+// slab floats the wide weight gradient needs at most (<= 512 blocks of 64x9x64 partials)
+HETU_API int64_t hetu_conv3x3_wide_wgrad_ws(int C, int K) {
+  const int pairs = (K / 64) * (C / 64);
+  return (int64_t)std::max(pairs, 512 / std::max(pairs, 1) * pairs) * 9 * 64 * 64;
+}
+
+// dw[K][3][3][C] fp32 (+)= weight gradient of the 3x3/s1/p1 convolution x[N,H,W,C] -> dy[N,H,W,K]
+HETU_API int hetu_conv3x3_wide_wgrad(const void* x, const void* dy, float* dw, float* ws, int64_t ws_floats,
+                                     int accumulate, int N, int H, int W, int C, int K, hipStream_t st) {
+  if (!wide_wgrad_ok(C, K, H, W) || ((((uintptr_t)x) | ((uintptr_t)dy) | ((uintptr_t)dw) | ((uintptr_t)ws)) & 15))
+    return (int)hipErrorInvalidValue;
+  const bf16 *xb = (const bf16*)x, *gb = (const bf16*)dy;
+  if (W == 28) return launch_wide_wgrad<28, 4, 1>(xb, gb, dw, ws, ws_floats, accumulate, N, H, C, K, st);
+  if (W == 14) return launch_wide_wgrad<14, 7, 1>(xb, gb, dw, ws, ws_floats, accumulate, N, H, C, K, st);
+  return launch_wide_wgrad<7, 7, 2>(xb, gb, dw, ws, ws_floats, accumulate, N, H, C, K, st);
 }

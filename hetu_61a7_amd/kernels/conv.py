@@ -1,12 +1,14 @@
 """2-D convolution (logical NCHW, physical channels-last on the GPU).
 
-The forward/backward-data/backward-filter entry points dispatch per shape to
-the hand-written implicit-GEMM MFMA kernels (``gemm.hip`` via ``conv_igemm``:
-the 128x128-tile kernel, ``hip``, and the 256x256-tile phase-interleaved kernel,
-``hip256``) or to the vendor convolution (MIOpen through torch).  ``HETU_CONV=auto``
-(default) selects per shape by measurement (``autotune.choose``), so the
-hand-written kernel runs exactly where it is at least as fast; ``hip`` /
-``vendor`` force one side.
+The forward/backward-data/backward-filter entry points run the hand-written MFMA
+kernels: the implicit-GEMM tiles of ``gemm_core.h`` (``hip`` 128x128, ``hip256``,
+``hip64`` 128x64, ``hip_lo`` single-stage), the 3x3 halo-tile kernels of
+``conv3x3.hip`` (``hip33``), the direct stem kernels of ``stem.hip`` (``hip_stem``)
+and the role-swapped 64-channel weight gradient (``hip64t``); per shape the fastest of
+them is picked by measurement (``autotune.choose``).  MIOpen / hipBLASLt (``vendor``,
+``blas*``) are an explicit A/B switch only: ``HETU_CONV=vendor`` runs them, ``auto``
+times them together with the hand-written kernels; the default ``hip`` never does (a
+shape no hand-written kernel takes is counted in ``kernels.FALLBACKS``).
 """
 from __future__ import annotations
 
@@ -18,7 +20,8 @@ import torch.nn.functional as F
 from . import native, record_vendor
 
 CL = torch.channels_last
-MODE = os.environ.get('HETU_CONV', 'auto')  # hip | vendor | auto (per-shape measured choice)
+# hip (default): hand-written kernels only; vendor: MIOpen / hipBLASLt (A/B switch); auto: both timed
+MODE = os.environ.get('HETU_CONV', 'hip')
 
 
 def _pick(key, hip, vendor, blas=None, tuned=None):
@@ -347,7 +350,7 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
         if _short_k(w.shape[0] * w.shape[2] * w.shape[3]):
             blas = dict(blas or {})
             blas['hip_lo'] = lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=3)
-        if conv_igemm.conv3x3_ok(x_shape, w.shape, stride, padding):
+        if conv_igemm.conv3x3_ok(x_shape, w.shape, stride, padding, dgrad=True):
             blas = dict(blas or {})
             blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=acc)
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
@@ -460,7 +463,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                                                                    accumulate=False, tile=2)
             blas['hip64t'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                                     accumulate=False, tile=4)
-        if conv_igemm.conv3x3_ok(x.shape, w_shape, stride, padding):
+        if conv_igemm._s1p1_3x3(w_shape, stride, padding) and conv_igemm.conv3x3_wgrad_ok(x.shape, w_shape):
             blas = dict(blas or {})
             blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=out)
         return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),

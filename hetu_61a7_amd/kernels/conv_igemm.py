@@ -17,7 +17,7 @@ import torch
 
 from . import fn, stream_ptr, check, record_native, P, I32, I64
 
-MODE = os.environ.get('HETU_CONV', 'auto')
+MODE = os.environ.get('HETU_CONV', 'hip')
 CL = torch.channels_last
 _GEOM = [I32] * 11
 
@@ -141,40 +141,78 @@ def try_stem_forward(x, w, stride, padding, colstats=None):
     return y.permute(0, 3, 1, 2)
 
 
-def conv3x3_ok(shape_x, w_shape, stride, padding):
-    """the 64-channel halo-tile kernel (``conv3x3.hip``) takes this 3x3/s1/p1 shape"""
-    co, c, kh, kw = w_shape
-    if (kh, kw) != (3, 3) or tuple(stride) != (1, 1) or tuple(padding) != (1, 1):
+def _s1p1_3x3(w_shape, stride, padding):
+    return tuple(w_shape[2:]) == (3, 3) and tuple(stride) == (1, 1) and tuple(padding) == (1, 1)
+
+
+def _c64(C, K, W):
+    return bool(fn('hetu_conv3x3_c64_supported', [I32, I32, I32])(int(C), int(K), int(W)))
+
+
+def _wide(C, K, H, W):
+    return bool(fn('hetu_conv3x3_wide_supported', [I32, I32, I32, I32])(int(C), int(K), int(H), int(W)))
+
+
+def conv3x3_ok(shape_x, w_shape, stride, padding, dgrad=False):
+    """a halo-tile kernel (``conv3x3.hip``) takes this 3x3/s1/p1 pass: the 64-channel
+    image-walking kernel, or the wide-channel pixel-tile kernel (its output channels in
+    128-blocks: K for the forward, C for the data gradient)"""
+    co, c = w_shape[0], w_shape[1]
+    if not _s1p1_3x3(w_shape, stride, padding):
         return False
-    return bool(fn('hetu_conv3x3_c64_supported', [I32, I32, I32])(int(c), int(co), int(shape_x[3])))
+    H, W = int(shape_x[2]), int(shape_x[3])
+    if _c64(c, co, W):
+        return True
+    return _wide(co, c, H, W) if dgrad else _wide(c, co, H, W)
+
+
+def conv3x3_wgrad_ok(shape_x, w_shape):
+    C, H, W = int(shape_x[1]), int(shape_x[2]), int(shape_x[3])
+    K = int(w_shape[0])
+    return _c64(C, K, W) or bool(fn('hetu_conv3x3_wide_wgrad_supported', [I32, I32, I32, I32])(C, K, H, W))
 
 
 def try_conv3x3_forward(x, w, stride, padding, colstats=None):
-    """3x3 / stride 1 / pad 1, 64 -> 64 channels: one block per image, the filter bank
-    resident in LDS and a DMA ring of halo rows (each input row read once)."""
+    """3x3 / stride 1 / pad 1 on a halo-tile kernel: each input pixel crosses L2 once per
+    block instead of once per tap.  64 -> 64 channels: one block per image, the filter
+    bank resident in LDS and a DMA ring of halo rows; wider layers: pixel tiles x 128
+    output channels, a halo per 64-channel chunk serving all 9 taps."""
     if not (_ok(x, w, x.shape[1], w.shape[0]) and conv3x3_ok(x.shape, w.shape, stride, padding)):
         return None
     N, C, H, W = x.shape
-    y = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=x.device)
-    f = fn('hetu_conv3x3_c64_fwd', [P, P, P, P, I32, I32, I32, P])
-    check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), colstats.data_ptr() if colstats is not None else None,
-            N, H, W, stream_ptr()), 'conv3x3_fwd')
+    K = w.shape[0]
+    y = torch.empty((N, H, W, K), dtype=torch.bfloat16, device=x.device)
+    st = colstats.data_ptr() if colstats is not None else None
+    if _c64(C, K, W):
+        f = fn('hetu_conv3x3_c64_fwd', [P, P, P, P, I32, I32, I32, P])
+        check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, N, H, W, stream_ptr()), 'conv3x3_fwd')
+    else:
+        f = fn('hetu_conv3x3_wide_fwd', [P, P, P, P, I32, I32, I32, I32, I32, P])
+        check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, N, H, W, C, K, stream_ptr()), 'conv3x3_wide_fwd')
     record_native('conv3x3_fwd')
     return y.permute(0, 3, 1, 2)
 
 
 def try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=None):
-    if not (_ok(g, w, x_shape[1], w.shape[0]) and conv3x3_ok(x_shape, w.shape, stride, padding)):
+    if not (_ok(g, w, x_shape[1], w.shape[0]) and conv3x3_ok(x_shape, w.shape, stride, padding, dgrad=True)):
         return None
     if acc is not None and (tuple(acc.shape) != tuple(x_shape) or not acc.is_contiguous(memory_format=CL) or
                             acc.dtype not in (torch.bfloat16, torch.float32) or acc.data_ptr() % 16):
         return None
     N, C, H, W = x_shape
+    K = w.shape[0]
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
     wt = torch.empty(w.numel(), dtype=torch.bfloat16, device=g.device)
-    f = fn('hetu_conv3x3_c64_dgrad', [P, P, P, P, P, I32, I32, I32, I32, P])
-    check(f(g.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
-            int(acc is not None and acc.dtype == torch.float32), N, H, W, stream_ptr()), 'conv3x3_dgrad')
+    a = acc.data_ptr() if acc is not None else None
+    af = int(acc is not None and acc.dtype == torch.float32)
+    if _c64(C, K, W):
+        f = fn('hetu_conv3x3_c64_dgrad', [P, P, P, P, P, I32, I32, I32, I32, P])
+        check(f(g.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), a, af, N, H, W, stream_ptr()),
+              'conv3x3_dgrad')
+    else:
+        f = fn('hetu_conv3x3_wide_dgrad', [P, P, P, P, P, I32, I32, I32, I32, I32, I32, P])
+        check(f(g.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), a, af, N, H, W, C, K, stream_ptr()),
+              'conv3x3_wide_dgrad')
     record_native('conv3x3_dgrad')
     return dx.permute(0, 3, 1, 2)
 
@@ -183,7 +221,8 @@ def try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=None, accumu
     """weight gradient of the 64-channel 3x3/s1/p1 convolution on the halo-tile kernel
     (per-image fp32 partials in a slab, then one reduce) into ``out`` (fp32 channels-last
     [K, C, 3, 3] view) or a new tensor"""
-    if not (_ok(x, g, x.shape[1], g.shape[1]) and conv3x3_ok(x.shape, w_shape, stride, padding)):
+    if not (_ok(x, g, x.shape[1], g.shape[1]) and _s1p1_3x3(w_shape, stride, padding) and
+            conv3x3_wgrad_ok(x.shape, w_shape)):
         return None
     N, C, H, W = x.shape
     K = w_shape[0]
@@ -194,11 +233,18 @@ def try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=None, accumu
         dw = out.permute(0, 2, 3, 1)
         if not dw.is_contiguous() or dw.dtype != torch.float32 or dw.data_ptr() % 16:
             return None
-    ws = torch.empty(int(fn('hetu_conv3x3_c64_wgrad_ws', [I32], restype=I64)(N)), dtype=torch.float32,
-                     device=g.device)
-    f = fn('hetu_conv3x3_c64_wgrad', [P, P, P, P, I32, I32, I32, I32, P])
-    check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), int(bool(accumulate)), N, H, W,
-            stream_ptr()), 'conv3x3_wgrad')
+    if _c64(C, K, W):
+        ws = torch.empty(int(fn('hetu_conv3x3_c64_wgrad_ws', [I32], restype=I64)(N)), dtype=torch.float32,
+                         device=g.device)
+        f = fn('hetu_conv3x3_c64_wgrad', [P, P, P, P, I32, I32, I32, I32, P])
+        check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), int(bool(accumulate)), N, H, W,
+                stream_ptr()), 'conv3x3_wgrad')
+    else:
+        nws = int(fn('hetu_conv3x3_wide_wgrad_ws', [I32, I32], restype=I64)(C, K))
+        ws = torch.empty(nws, dtype=torch.float32, device=g.device)
+        f = fn('hetu_conv3x3_wide_wgrad', [P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P])
+        check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), nws, int(bool(accumulate)), N, H, W, C, K,
+                stream_ptr()), 'conv3x3_wide_wgrad')
     record_native('conv3x3_wgrad')
     return dw.permute(0, 3, 1, 2)
 

@@ -15,7 +15,9 @@ import torch
 
 from . import native, record_vendor
 
-_MFMA = os.environ.get('HETU_GEMM', 'auto')  # hip | vendor(off) | auto (measured per shape)
+# hip (default): the hand-written kernels only, timed against each other per shape;
+# vendor: hipBLASLt (A/B switch); auto: hand-written and library candidates timed together
+_MFMA = os.environ.get('HETU_GEMM', 'hip')
 
 
 def _sig(t):
@@ -50,6 +52,9 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
             cands['hip64'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=2)
         if a.dtype == torch.bfloat16 and _tr(a, ta).shape[-1] <= 2048:   # short K: the 4-blocks-per-CU tile
             cands['hip_lo'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=3)
+        A2, B2 = _tr(a, ta), _tr(b, tb)
+        if A2.dim() == 2 and B2.dim() == 2 and A2.shape[0] * B2.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
+            cands['hip_small'] = lambda: gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
         cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
         if bias is not None:
             # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
@@ -216,6 +221,8 @@ def matmul_into(a, b, ta, tb, out):
                         cands['hip256_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=1))
             if K >= 2048:
                 cands['vendor_sk'] = lambda: _vendor_splitk_into(A, B, out)
+            if M * N <= gemm_mfma.SMALL_MAX_OUT:
+                cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, out=out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
         c = choose(key, cands, _MFMA)
         if c != 'vendor' and cands[c]() is not None:
@@ -257,6 +264,8 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=1)
         if A.shape[1] <= 2048:
             cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=3)
+        if A.shape[0] * B.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
+            cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, cin=acc, beta=1.0)
         ch = choose(key, cands, _MFMA)
         dst[0] = acc
         if ch != 'vendor':

@@ -20,7 +20,7 @@ _ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I
 # tile configurations of the kernel (gemm.hip launch): 0 = 128x128 tile, 4 waves;
 # 1 = 256x256 tile, 8 waves, phase-interleaved K loop (one block per CU)
 TILES = (0, 1, 2, 3)   # 128x128, 256x256, 128x64, 128x128 single-stage (4 blocks / CU)
-MODE = os.environ.get('HETU_GEMM', 'auto')
+MODE = os.environ.get('HETU_GEMM', 'hip')
 
 
 def _operand(t, rows_dim_last, q=8):
@@ -150,6 +150,43 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
             int(accumulate), ws.data_ptr() if ws is not None else None, int(tile), stream_ptr()),
           'gemm_bf16')
     record_native('gemm_bf16')
+    return out
+
+
+SMALL_MAX_OUT = 1 << 16
+
+
+def gemm_small(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None, bias_on_m=False):
+    """out[M,N] = act(alpha * a @ b + beta * cin + bias) for 2-D fp32 / bf16 views of any
+    strides, one wave per output (``gemm_small.hip``): the small / ragged products the
+    MFMA tiles cannot take (N = 2 classifier heads, 64-row poolers).  None when unsupported."""
+    if a.dim() != 2 or b.dim() != 2 or a.dtype not in (torch.float32, torch.bfloat16) or \
+            b.dtype not in (torch.float32, torch.bfloat16) or not a.is_cuda:
+        return None
+    M, K = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K or M * N > SMALL_MAX_OUT:
+        return None
+    odt = out_dtype or (out.dtype if out is not None else a.dtype)
+    if out is None:
+        out = torch.empty((M, N), dtype=odt, device=a.device)
+    if out.dim() != 2 or out.stride(-1) != 1 or out.dtype not in (torch.float32, torch.bfloat16):
+        return None
+    cin_t = None
+    if cin is not None and beta != 0.0:
+        cin_t = cin.expand(M, N) if tuple(cin.shape) != (M, N) else cin
+        if cin_t.stride(-1) != 1 or cin_t.dtype not in (torch.float32, torch.bfloat16):
+            cin_t = cin_t.float().contiguous()
+    bias_t = bias.float().contiguous() if bias is not None else None
+    f = fn('hetu_gemm_small', [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I32, I32, F32, F32, I32,
+                               I32, I32, I32, P])
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), cin_t.data_ptr() if cin_t is not None else None,
+            bias_t.data_ptr() if bias_t is not None else None, M, N, K, a.stride(0), a.stride(1), b.stride(0),
+            b.stride(1), out.stride(0) if M > 1 else N, (cin_t.stride(0) if M > 1 else N) if cin_t is not None else 0,
+            int(a.dtype == torch.float32), int(b.dtype == torch.float32), float(alpha), float(beta), _ACT[act],
+            int(out.dtype == torch.float32), int(cin_t is not None and cin_t.dtype == torch.float32), int(bias_on_m),
+            stream_ptr()), 'gemm_small')
+    record_native('gemm_small')
     return out
 
 

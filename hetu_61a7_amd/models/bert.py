@@ -39,8 +39,15 @@ class BertConfig(object):
     def __init__(self, vocab_size=30522, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
                  intermediate_size=3072, hidden_act='gelu', hidden_dropout_prob=0.1,
                  attention_probs_dropout_prob=0.1, max_position_embeddings=512, type_vocab_size=2,
-                 initializer_range=0.02, batch_size=64, seq_len=128, fused_attention=True):
+                 initializer_range=0.02, batch_size=64, seq_len=128, fused_attention=True, vocab_multiple=64):
         self.vocab_size = vocab_size
+        # the word-embedding table / MLM decoder are padded to a multiple of vocab_multiple
+        # rows (Megatron's make-vocab-size-divisible-by): 30522 -> 30528 keeps every MLM-head
+        # GEMM leading dimension a multiple of the MFMA loaders' 16-byte chunks.  The pad
+        # columns carry a -1e4 decoder bias, so their softmax weight is exactly 0 in fp32:
+        # the loss, the gradients of the real rows and the pad rows' zero gradient are those
+        # of the unpadded model.  vocab_multiple=1 disables it.
+        self.vocab_multiple = max(1, int(vocab_multiple))
         self.fused_attention = fused_attention   # packed-QKV HIP attention (else op-by-op graph)
         self.hidden_size = hidden_size
         self.num_hidden_layers = num_hidden_layers
@@ -54,6 +61,11 @@ class BertConfig(object):
         self.initializer_range = initializer_range
         self.batch_size = batch_size
         self.seq_len = seq_len
+
+    @property
+    def padded_vocab_size(self):
+        m = self.vocab_multiple
+        return -(-self.vocab_size // m) * m
 
     @classmethod
     def base(cls, **kw):
@@ -138,7 +150,7 @@ class BertModel(object):
         self.placement = placement
         H = cfg.hidden_size
         with _stage_ctx(placement, 0):
-            self.word_embeddings = _w('word_embeddings', (cfg.vocab_size, H), cfg)
+            self.word_embeddings = _w('word_embeddings', (cfg.padded_vocab_size, H), cfg)
             self.position_embeddings = _w('position_embeddings', (cfg.max_position_embeddings, H), cfg)
             self.token_type_embeddings = _w('token_type_embeddings', (cfg.type_vocab_size, H), cfg)
         self.layers = [BertLayer(cfg, i) for i in range(cfg.num_hidden_layers)]
@@ -186,7 +198,12 @@ class BertPreTrainingHeads(object):
         H = c.hidden_size
         t = _dense(seq, H, H, 'cls_transform_dense', c, act=c.hidden_act)
         t = _ln(t, H, 'cls_transform_LayerNorm')
-        bias = _zeros('cls_lm_bias', c.vocab_size)
+        V, Vp = c.vocab_size, c.padded_vocab_size
+        if Vp == V:
+            bias = _zeros('cls_lm_bias', V)
+        else:
+            bias = ht.Variable('cls_lm_bias', value=np.concatenate([np.zeros(V, np.float32),
+                                                                    np.full(Vp - V, -1e4, np.float32)]))
         scores = ht.linear_op(t, self.E, bias, trans_B=True)            # tied decoder: [B*S, V]
         nsp = _dense(pooled, H, 2, 'cls_seq_relationship', c)
         return scores, nsp
@@ -205,7 +222,7 @@ class BertForPreTraining(object):
             # between the two stages each step: pipeline_exec ties)
             from ..ops.node import shadow_ids
             with _stage_ctx(placement, head), shadow_ids():
-                E = _w('cls_decoder_weight', (cfg.vocab_size, cfg.hidden_size), cfg)
+                E = _w('cls_decoder_weight', (cfg.padded_vocab_size, cfg.hidden_size), cfg)
             E.tied_to = self.bert.word_embeddings
         else:
             E = self.bert.word_embeddings

@@ -249,3 +249,58 @@ def test_conv3x3_c64_halo_kernel(n, h):
     base = out.clone()
     CI.try_conv3x3_backward_filter(dy, x, w.shape, (1, 1), (1, 1), out=out, accumulate=True)
     assert _rel(out - base, wf.grad) < 1e-4
+
+
+@pytest.mark.parametrize('n,c,k,h', [(2, 128, 128, 28), (3, 256, 256, 14), (3, 512, 512, 7), (1, 64, 128, 28),
+                                     (2, 128, 256, 14), (1, 192, 128, 56)])
+def test_conv3x3_wide_halo_kernel(n, c, k, h):
+    """3x3/s1/p1 wide-channel halo kernel: pixel tiles x 128 output channels, one halo per
+    64-channel chunk for all 9 taps; forward (+ BN statistics) and data gradient (+ join)."""
+    x = torch.randn(n, c, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(k, c, 3, 3, device=DEV) * 0.05).bfloat16().contiguous(memory_format=CL)
+    st = torch.zeros(2 * k, device=DEV)
+    y = CI.try_conv3x3_forward(x, w, (1, 1), (1, 1), colstats=st)
+    assert y is not None and y.is_contiguous(memory_format=CL)
+    xf = x.float().requires_grad_(True)
+    ref = F.conv2d(xf, w.float(), None, 1, 1)
+    assert _rel(y, ref) < _tol(y)
+    yf = y.float()
+    assert _rel(st[:k], yf.sum((0, 2, 3))) < 1e-4 and _rel(st[k:], (yf * yf).sum((0, 2, 3))) < 1e-4
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
+    ref.backward(dy.float())
+    if c % 128 == 0:
+        dx = CI.try_conv3x3_backward_data(dy, w, x.shape, (1, 1), (1, 1))
+        assert dx is not None and _rel(dx, xf.grad) < _tol(dx)
+        r = torch.randn(x.shape, device=DEV).bfloat16().contiguous(memory_format=CL)
+        dx2 = CI.try_conv3x3_backward_data(dy, w, x.shape, (1, 1), (1, 1), acc=r)
+        assert _rel(dx2, xf.grad + r.float()) < _tol(dx2)
+    else:
+        assert CI.try_conv3x3_backward_data(dy, w, x.shape, (1, 1), (1, 1)) is None
+    if h in (28, 14, 7):
+        wf = w.float().requires_grad_(True)
+        F.conv2d(x.float(), wf, None, 1, 1).backward(dy.float())
+        out = torch.randn(k, c, 3, 3, device=DEV).contiguous(memory_format=CL)
+        base = out.clone()
+        dw = CI.try_conv3x3_backward_filter(dy, x, w.shape, (1, 1), (1, 1), out=out, accumulate=True)
+        assert dw is not None and dw.data_ptr() == out.data_ptr()
+        assert _rel(out - base, wf.grad) < 1e-4
+        dw2 = CI.try_conv3x3_backward_filter(dy, x, w.shape, (1, 1), (1, 1))
+        assert _rel(dw2, wf.grad) < 2e-5
+
+
+@pytest.mark.parametrize('mnk', [(64, 2, 768), (768, 2, 64), (64, 768, 768), (3, 5, 7), (1, 1000, 2048)])
+@pytest.mark.parametrize('dts', [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.bfloat16),
+                                 (torch.float32, torch.float32)])
+def test_gemm_small_any_stride(mnk, dts):
+    """the one-wave-per-output kernel for the products the MFMA tiles cannot take (N = 2
+    heads, strided CLS-token rows): any strides, epilogue as the MFMA kernels"""
+    M, N, K = mnk
+    a = torch.randn(M, 3 * K, device=DEV).to(dts[0])[:, ::3]           # strided rows and columns
+    b = torch.randn(N, K, device=DEV).to(dts[1]).t()                    # transposed view
+    bias = torch.randn(N, device=DEV)
+    cin = torch.randn(M, N, device=DEV)
+    y = G.gemm_small(a, b, bias=bias, act='relu', alpha=0.5, beta=2.0, cin=cin, out_dtype=torch.float32)
+    ref = torch.relu(0.5 * (a.float() @ b.float()) + 2.0 * cin + bias)
+    assert _rel(y, ref) < 2e-5
+    y2 = G.gemm_small(a, b)
+    assert y2.dtype == dts[0] and _rel(y2, a.float() @ b.float()) < _tol(y2)

@@ -1,8 +1,10 @@
 """Steady-state kernel census: one training step of the flagship models, recorded
 with torch.profiler (kineto / roctracer), must launch no PyTorch (``at::native``)
-compute kernel -- every kernel is a hand-written HIP kernel of libhetu_kernels.so or a
-vendor GEMM / convolution library kernel (hipBLASLt / MIOpen, counted separately by
-kernels.VENDOR_CALLS).  Reference: SURVEY §2.7 (the op layer is hand-written)."""
+compute kernel and -- with the default HETU_GEMM / HETU_CONV = hip -- no vendor GEMM or
+convolution library kernel either (hipBLASLt ``Cijk_*``, MIOpen ``igemm_*`` /
+``SubTensorOp`` / ``naive_conv``, composable-kernel ``ck::``): every kernel is a
+hand-written HIP kernel of libhetu_kernels.so.  Reference: SURVEY §2.7 (the op layer is
+hand-written)."""
 import collections
 
 import pytest
@@ -23,11 +25,12 @@ def _census(step, warm=3):
         torch.cuda.synchronize()
     torch_k = collections.Counter()
     n = 0
+    vendor = ('Cijk', 'igemm', 'SubTensorOp', 'naive_conv', 'MIOpen', 'miopen', 'ck::', '_ZN2ck', 'gridwise_')
     for e in prof.events():
         if 'CUDA' not in str(e.device_type):
             continue
         n += 1
-        if 'at::native' in e.name:
+        if 'at::native' in e.name or any(v in e.name for v in vendor):
             torch_k[e.name[:120]] += 1
     return n, torch_k
 
@@ -44,19 +47,25 @@ def test_resnet50_step_launches_no_torch_kernels():
     X = torch.randn((B, 3, 224, 224), device='cuda', generator=g).bfloat16().contiguous(
         memory_format=torch.channels_last)
     Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
+    from hetu_61a7_amd import kernels as K
+    K.reset_dispatch_stats()
     n, torch_k = _census(lambda: ex.run('train', feed_dict={x: X, y_: Y}))
     assert n > 300, n
     assert not torch_k, dict(torch_k)
+    assert not K.VENDOR_CALLS and not K.FALLBACKS, (K.VENDOR_CALLS, K.FALLBACKS)
 
 
 def test_bert_step_launches_no_torch_kernels():
     import argparse
     from hetu_61a7_amd.models.bert import BertConfig, bert_bench
-    cfg = BertConfig(vocab_size=8192, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+    cfg = BertConfig(vocab_size=8190, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
                      intermediate_size=1024, max_position_embeddings=128)
     cfg.seq_len = 128
     args = argparse.Namespace(batch=8, dtype='bf16', bucket_mb=32, zero=0, pp=None, bert_config=cfg)
     step = bert_bench(args, 1, 0, 0)[0]
+    from hetu_61a7_amd import kernels as K
+    K.reset_dispatch_stats()
     n, torch_k = _census(step)
     assert n > 100, n
     assert not torch_k, dict(torch_k)
+    assert not K.VENDOR_CALLS and not K.FALLBACKS, (K.VENDOR_CALLS, K.FALLBACKS)

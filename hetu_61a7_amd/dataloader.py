@@ -70,7 +70,9 @@ class Dataloader(object):
         self._ring = []
         self._pending = None
         if device is not None and device.type == 'cuda':
-            self._stream = torch.cuda.Stream(device=device)
+            from .runtime import DeviceStream
+            self._dstream = DeviceStream(torch.device(device).index)   # framework-created prefetch stream
+            self._stream = self._dstream.torch
         self.initialized = True
 
     def set_slices(self):

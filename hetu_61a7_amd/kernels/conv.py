@@ -457,6 +457,19 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             blas = dict(blas or {})
             blas['hip256'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                                     accumulate=False, tile=1)
+        if _plain_1x1((g, x), w_shape, stride, padding) and w_shape[0] % 64 == 0 and w_shape[1] % 64 == 0:
+            from . import gemm_mfma
+            co, ci = w_shape[0], w_shape[1]
+
+            def lk():
+                d = out.reshape(co, ci) if out is not None else torch.empty((co, ci), dtype=torch.float32,
+                                                                            device=g.device)
+                r = gemm_mfma.wgrad_longk(_rows(g), _rows(x), d)
+                if r is None:
+                    return None
+                return out if out is not None else d.view(co, ci, 1, 1)
+            blas = dict(blas or {})
+            blas['hip_lk'] = lk
         if w_shape[0] <= 64:   # 64-channel banks: a 64-wide N side (as is, and with the roles swapped)
             blas = dict(blas or {})
             blas['hip64'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,

@@ -223,6 +223,9 @@ def matmul_into(a, b, ta, tb, out):
                 cands['vendor_sk'] = lambda: _vendor_splitk_into(A, B, out)
             if M * N <= gemm_mfma.SMALL_MAX_OUT:
                 cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, out=out)
+            if A.stride(0) == 1 and B.stride(1) == 1 and M % 64 == 0 and N % 64 == 0 and K >= 4096:
+                # both operands token-major (weight gradients): the 64x64 split-K tile
+                cands['hip_lk'] = lambda: gemm_mfma.wgrad_longk(A.t(), B, out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
         c = choose(key, cands, _MFMA)
         if c != 'vendor' and cands[c]() is not None:

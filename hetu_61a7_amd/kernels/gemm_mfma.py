@@ -156,6 +156,33 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
 SMALL_MAX_OUT = 1 << 16
 
 
+def wgrad_longk(a_pm, b_pm, out, accumulate=False, splits=None):
+    """out[M,N] (fp32, row stride multiple of 4) (+)= a_pm^T @ b_pm for pixel-major bf16
+    operands a_pm [P, M], b_pm [P, N] (rows contiguous, M and N multiples of 64): the
+    64x64-tile split-K kernel for small outputs over very long reductions
+    (``wgrad_longk.hip``).  None when unsupported."""
+    if a_pm.dtype != torch.bfloat16 or b_pm.dtype != torch.bfloat16 or a_pm.dim() != 2 or b_pm.dim() != 2:
+        return None
+    P_, M = a_pm.shape
+    N = b_pm.shape[1]
+    if b_pm.shape[0] != P_ or M % 64 or N % 64 or a_pm.stride(1) != 1 or b_pm.stride(1) != 1:
+        return None
+    lda, ldb = (a_pm.stride(0) if P_ > 1 else M), (b_pm.stride(0) if P_ > 1 else N)
+    if lda % 8 or ldb % 8 or not _aligned(a_pm, b_pm) or out.dtype != torch.float32 or out.stride(-1) != 1 \
+            or tuple(out.shape) != (M, N) or out.data_ptr() % 16 or (M > 1 and out.stride(0) % 4):
+        return None
+    tiles = (M // 64) * (N // 64)
+    if splits is None:
+        splits = max(1, min(2048 // tiles, -(-P_ // 512)))
+    ws = torch.empty(int(fn('hetu_wgrad_longk_ws', [I32, I32, I32], restype=I64)(M, N, splits)),
+                     dtype=torch.float32, device=a_pm.device)
+    f = fn('hetu_wgrad_longk', [P, P, P, P, I64, I32, I32, I32, I32, I64, I32, I32, P])
+    check(f(a_pm.data_ptr(), b_pm.data_ptr(), out.data_ptr(), ws.data_ptr(), P_, M, N, lda, ldb,
+            out.stride(0) if M > 1 else N, int(splits), int(bool(accumulate)), stream_ptr()), 'wgrad_longk')
+    record_native('wgrad_longk')
+    return out
+
+
 def gemm_small(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None, bias_on_m=False):
     """out[M,N] = act(alpha * a @ b + beta * cin + bias) for 2-D fp32 / bf16 views of any
     strides, one wave per output (``gemm_small.hip``): the small / ragged products the

@@ -516,8 +516,8 @@ class OptimizerOp(Op):
         import time
         rec = {'bytes': (b.end - b.start) * 4, 't_host': time.perf_counter(), 'ev': None}
         if self.flat is not None and self.flat.grad.is_cuda:
-            rec['ev'] = torch.cuda.Event(enable_timing=True)
-            rec['ev'].record()
+            from .runtime import DeviceEvent
+            rec['ev'] = DeviceEvent(timing=True).record()
         self._trace.append(rec)
 
     def comm_trace(self):
@@ -558,8 +558,8 @@ class OptimizerOp(Op):
             import time
             ev = None
             if self.flat is not None and self.flat.grad.is_cuda:
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record()
+                from .runtime import DeviceEvent
+                ev = DeviceEvent(timing=True).record()
             self._bwd_end = (time.perf_counter(), ev)
         if self.zero:
             self._zero_step()

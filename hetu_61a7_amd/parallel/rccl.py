@@ -104,7 +104,7 @@ class Work(object):
         self.event, self.post = event, post
 
     def wait(self):
-        torch.cuda.current_stream().wait_event(self.event)
+        self.event.wait(torch.cuda.current_stream())
         if self.post is not None:
             self.post()
             self.post = None
@@ -126,7 +126,11 @@ class NativeComm(object):
     def __init__(self, handle, rank, nrank):
         self.handle = ctypes.c_void_p(handle) if not isinstance(handle, ctypes.c_void_p) else handle
         self.rank, self.nrank = rank, nrank
-        self.stream = torch.cuda.Stream(priority=-1)
+        from ..runtime import DeviceStream
+        # the comm stream: a framework-created high-priority HIP stream (torch sees its
+        # ExternalStream view only for the allocator's record_stream bookkeeping)
+        self._dstream = DeviceStream(priority=-1)
+        self.stream = self._dstream.torch
         self._bf16_ws = {}
 
     # ---- construction -----------------------------------------------------------
@@ -186,12 +190,13 @@ class NativeComm(object):
                 post()
             return None
         s = self.stream
-        s.wait_stream(cur)
+        self._dstream.wait_stream(cur)
         fn(s.cuda_stream)
         for t in tensors:
             if t is not None and t.is_cuda:
                 t.record_stream(s)
-        ev = torch.cuda.Event(enable_timing=_TIMING)
+        from ..runtime import DeviceEvent
+        ev = DeviceEvent(timing=_TIMING)
         ev.record(s)
         return Work(ev, post)
 
@@ -275,7 +280,8 @@ class NativeComm(object):
         if not async_op:
             # the workspaces are shared with async calls on the comm stream: a sync call on
             # the caller's stream must not overtake a bucket still using them
-            torch.cuda.current_stream().wait_stream(self.stream)
+            from ..runtime import DeviceEvent
+            DeviceEvent().record(self.stream).wait(torch.cuda.current_stream())
         c = -(-n // (8 * P)) * 8
         send = self._ws(c * P, torch.bfloat16, 'send')
         recv = self._ws(c * P, torch.bfloat16, 'recv')

@@ -34,8 +34,16 @@ def side_streams(device):
     stream by events, so they overlap compute instead of queueing behind it."""
     s = _STREAMS.get(device)
     if s is None:
-        s = _STREAMS[device] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
+        from ..runtime import DeviceStream
+        idx = torch.device(device).index
+        idx = torch.cuda.current_device() if idx is None else idx
+        owned = (DeviceStream(idx), DeviceStream(idx))       # framework-created HIP streams
+        s = _STREAMS[device] = (owned[0].torch, owned[1].torch)
+        _OWNED.append(owned)
     return s
+
+
+_OWNED = []
 
 
 def host_ids(t):

@@ -1,0 +1,145 @@
+"""Framework-owned HIP streams and events (``csrc/runtime/device_api.cc`` in
+``libhetu_alloc.so``; reference ``src/cuda_common/gpu_runtime.cc:61-118`` and
+``python/hetu/stream.py``).
+
+The executor's compute / H2D / D2H streams, the RCCL communicator's comm stream, the
+PS staging streams and the dataloader's prefetch stream are created by
+``hipStreamCreateWithPriority`` here, and their events by ``hipEventCreateWithFlags``.
+torch only ever sees such a stream as a non-owning ``torch.cuda.ExternalStream`` over
+the handle (``DeviceStream.torch``), for the rare library op that must be ordered on
+it and for ``record_stream`` bookkeeping of the caching allocator.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from ._base import _LIB_DIR
+
+_PATH = os.path.join(_LIB_DIR, 'libhetu_alloc.so')
+_lib = None
+CREATED = {'streams': 0, 'events': 0}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(_PATH, mode=ctypes.RTLD_GLOBAL)
+        P, I, I64, PP = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)
+        for name, args in (('hetu_stream_create', [I, I, PP]), ('hetu_stream_destroy', [P]), ('hetu_stream_sync', [P]),
+                           ('hetu_stream_query', [P]), ('hetu_event_create', [I, I, PP]), ('hetu_event_destroy', [P]),
+                           ('hetu_event_record', [P, P]), ('hetu_event_sync', [P]), ('hetu_event_query', [P]),
+                           ('hetu_event_elapsed', [P, P, ctypes.POINTER(ctypes.c_float)]),
+                           ('hetu_stream_wait_event', [P, P]), ('hetu_memcpy_async', [P, P, I64, I, P]),
+                           ('hetu_memcpy_peer_async', [P, I, P, I, I64, P]), ('hetu_memset_async', [P, I, I64, P]),
+                           ('hetu_device_sync', [I])):
+            f = getattr(L, name)
+            f.argtypes, f.restype = args, I
+        L.hetu_error_string.argtypes, L.hetu_error_string.restype = [I], ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(r, what):
+    if r != 0:
+        raise RuntimeError('HIP %s failed: %s' % (what, lib().hetu_error_string(r).decode()))
+
+
+def _handle(stream):
+    """raw hipStream_t of a DeviceStream, a torch stream, or None (torch's current stream)"""
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, DeviceStream):
+        return stream.handle
+    return stream.cuda_stream
+
+
+class DeviceStream(object):
+    """A HIP stream created by the framework (non-blocking, optional priority)."""
+
+    def __init__(self, device=None, priority=0):
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        _check(lib().hetu_stream_create(self.device, int(priority), ctypes.byref(h)), 'stream create')
+        self.handle = h.value
+        self.priority = priority
+        self.torch = torch.cuda.ExternalStream(self.handle, device=torch.device('cuda', self.device))
+        CREATED['streams'] += 1
+
+    @property
+    def cuda_stream(self):
+        return self.handle
+
+    def synchronize(self):
+        _check(lib().hetu_stream_sync(self.handle), 'stream sync')
+
+    def query(self):
+        return lib().hetu_stream_query(self.handle) == 0
+
+    def wait_event(self, event):
+        event.wait(self)
+
+    def wait_stream(self, other):
+        """device-side: this stream waits for the work queued so far on ``other``"""
+        ev = DeviceEvent(self.device)
+        ev.record(other)
+        ev.wait(self)
+
+    def __del__(self):
+        h = getattr(self, 'handle', None)
+        if h and _lib is not None:
+            try:
+                lib().hetu_stream_sync(h)
+                lib().hetu_stream_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+class DeviceEvent(object):
+    """A HIP event (timing disabled unless ``timing``: cheaper record and wait)."""
+
+    def __init__(self, device=None, timing=False, enable_timing=None):
+        if enable_timing is not None:
+            timing = enable_timing
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        _check(lib().hetu_event_create(self.device, int(bool(timing)), ctypes.byref(h)), 'event create')
+        self.handle = h.value
+        CREATED['events'] += 1
+
+    def record(self, stream=None):
+        _check(lib().hetu_event_record(self.handle, _handle(stream)), 'event record')
+        return self
+
+    def wait(self, stream=None):
+        _check(lib().hetu_stream_wait_event(_handle(stream), self.handle), 'stream wait event')
+
+    def synchronize(self):
+        _check(lib().hetu_event_sync(self.handle), 'event sync')
+
+    def query(self):
+        return lib().hetu_event_query(self.handle) == 0
+
+    def elapsed_time(self, end):
+        """milliseconds from this event to ``end`` (both recorded, timing enabled)"""
+        ms = ctypes.c_float()
+        _check(lib().hetu_event_elapsed(self.handle, end.handle, ctypes.byref(ms)), 'event elapsed')
+        return float(ms.value)
+
+    def __del__(self):
+        h = getattr(self, 'handle', None)
+        if h and _lib is not None:
+            try:
+                lib().hetu_event_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+def memcpy_async(dst, src, nbytes, kind, stream=None):
+    """kind: 'h2h' | 'h2d' | 'd2h' | 'd2d' on a framework or torch stream"""
+    k = {'h2h': 0, 'h2d': 1, 'd2h': 2, 'd2d': 3}[kind]
+    _check(lib().hetu_memcpy_async(dst, src, int(nbytes), k, _handle(stream)), 'memcpy')

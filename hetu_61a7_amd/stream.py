@@ -1,9 +1,12 @@
 """HIP streams and events (reference ``python/hetu/stream.py:16-105``).
 
-On MI355X a ``Stream`` is a HIP stream (``torch.cuda.Stream`` on ROCm) and an
-``Event`` a HIP event.  The executor routes compute, H2D, D2H and comm work
-to separate streams and links them with ``hipStreamWaitEvent``
-(``Stream.wait_event``) instead of the reference's host-side ``event.sync()``.
+On MI355X a ``Stream`` is a HIP stream created by the framework's device runtime
+(``runtime.DeviceStream``: ``hipStreamCreateWithPriority`` in libhetu_alloc.so) and an
+``Event`` a HIP event (``runtime.DeviceEvent``).  The executor routes compute, H2D, D2H
+and comm work to separate streams and links them with ``hipStreamWaitEvent``
+(``Stream.wait_event``) instead of the reference's host-side ``event.sync()``.  Kernels
+launched inside ``with stream:`` run on it (``torch_stream`` is the non-owning
+``torch.cuda.ExternalStream`` view that makes it torch's current stream).
 """
 from __future__ import annotations
 
@@ -17,10 +20,13 @@ from .ndarray import is_gpu_ctx
 class Stream(object):
     def __init__(self, ctx=None, priority: int = 0, torch_stream=None):
         self.ctx = ctx
+        self.native = None
         if torch_stream is not None:
             self.torch_stream = torch_stream
         elif ctx is not None and is_gpu_ctx(ctx) and torch.cuda.is_available():
-            self.torch_stream = torch.cuda.Stream(device=ctx.device_id, priority=priority)
+            from .runtime import DeviceStream
+            self.native = DeviceStream(ctx.device_id, priority)
+            self.torch_stream = self.native.torch
         else:
             self.torch_stream = None
 
@@ -29,12 +35,14 @@ class Stream(object):
         return self.torch_stream.cuda_stream if self.torch_stream is not None else None
 
     def sync(self):
-        if self.torch_stream is not None:
+        if self.native is not None:
+            self.native.synchronize()
+        elif self.torch_stream is not None:
             self.torch_stream.synchronize()
 
     def wait_event(self, event: 'Event'):
-        if self.torch_stream is not None and event.torch_event is not None:
-            self.torch_stream.wait_event(event.torch_event)
+        if self.torch_stream is not None and event.native is not None:
+            event.native.wait(self.torch_stream)
 
     def __enter__(self):
         if self.torch_stream is not None:
@@ -52,26 +60,31 @@ class Event(object):
     def __init__(self, ctx=None, timing: bool = False):
         self.ctx = ctx
         if ctx is not None and is_gpu_ctx(ctx) and torch.cuda.is_available():
-            self.torch_event = torch.cuda.Event(enable_timing=timing)
+            from .runtime import DeviceEvent
+            self.native = DeviceEvent(ctx.device_id, timing)
         else:
-            self.torch_event = None
+            self.native = None
         self._t = None
 
+    @property
+    def torch_event(self):      # compatibility name: the HIP event object (or None on CPU)
+        return self.native
+
     def record(self, stream_handle: Stream = None):
-        if self.torch_event is not None:
+        if self.native is not None:
             s = stream_handle.torch_stream if stream_handle is not None else None
-            self.torch_event.record(s) if s is not None else self.torch_event.record()
+            self.native.record(s)
         else:
             self._t = time.perf_counter()
 
     def sync(self):
-        if self.torch_event is not None:
-            self.torch_event.synchronize()
+        if self.native is not None:
+            self.native.synchronize()
 
     def time_since(self, other: 'Event') -> float:
         """Milliseconds between ``other`` and this event."""
-        if self.torch_event is not None:
-            return other.torch_event.elapsed_time(self.torch_event)
+        if self.native is not None:
+            return other.native.elapsed_time(self.native)
         return (self._t - other._t) * 1000.0
 
 

@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
 S=scripts/gpu_step.sh
 bash $S tests 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
-  ${TESTS:-tests/test_gemm_gpu.py tests/test_stem_gpu.py tests/test_native_dispatch_gpu.py} || exit $?
+  ${TESTS:-tests/test_runtime_gpu.py tests/test_gemm_gpu.py tests/test_stem_gpu.py tests/test_native_dispatch_gpu.py tests/test_rccl_gpu.py} || exit $?
 grep -q " passed" gpurun_out/tests.log && ! grep -q -E "failed|error" gpurun_out/tests.log || { echo "TESTS FAILED"; exit 1; }
 CONV_ONLY="64,56,64,3,1;128,28,128,3,1;256,14,256,3,1;512,7,512,3,1" bash $S conv_sweep 300 \
   python scripts/bench_conv_resnet.py 256 gpurun_out/conv_sweep_r4.txt || exit $?

@@ -304,3 +304,20 @@ def test_gemm_small_any_stride(mnk, dts):
     assert _rel(y, ref) < 2e-5
     y2 = G.gemm_small(a, b)
     assert y2.dtype == dts[0] and _rel(y2, a.float() @ b.float()) < _tol(y2)
+
+
+@pytest.mark.parametrize('pmn', [(802816, 64, 64), (50000, 128, 64), (8192, 768, 3072), (1000, 64, 192)])
+@pytest.mark.parametrize('accumulate', [False, True])
+def test_wgrad_longk(pmn, accumulate):
+    """64x64-tile split-K weight gradient over pixel-major operands (1x1 conv / linear
+    weight gradients): fp32 result against fp32 math on the same bf16 operands"""
+    P_, M, N = pmn
+    a = torch.randn(P_, M, device=DEV).bfloat16()
+    b = torch.randn(P_, N, device=DEV).bfloat16()
+    out = torch.randn(M, N, device=DEV)
+    base = out.clone()
+    r = G.wgrad_longk(a, b, out, accumulate=accumulate)
+    assert r is not None and r.data_ptr() == out.data_ptr()
+    ref = a.float().t() @ b.float()
+    got = out - base if accumulate else out
+    assert _rel(got, ref) < (1e-4 if accumulate else 2e-5)

@@ -40,6 +40,8 @@ def parse():
     p.add_argument('--bucket-mb', type=float, default=32)
     p.add_argument('--zero', type=int, default=0, help='1: ZeRO-1 sharded optimizer state over the DP group')
     p.add_argument('--pp', type=int, default=None, help='bert: force the Galvatron pipeline degree')
+    p.add_argument('--comm', default='PS', choices=['PS', 'Hybrid'],
+                   help='wdl: PS = dense parameters on the server too (BASELINE config 3), Hybrid = RCCL dense')
     p.add_argument('--ids', default='zipf', choices=['zipf', 'uniform'],
                    help='wdl: sparse id distribution (uniform = cache worst-case control)')
     p.add_argument('--op-profile', default=None, help='write per-op-type GPU time (ms) to this file')

@@ -191,12 +191,23 @@ def wdl_criteo_bench(args, world, rank, local):
     xs = ht.dataloader_op([ht.Dataloader(sparse, B, 'train')])
     y_ = ht.dataloader_op([ht.Dataloader(labels, B, 'train')])
     loss, y, _, train = wdl_criteo(xd, xs, y_, feature_dimension=rows, embedding_size=128, learning_rate=0.01)
-    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(local), comm_mode='Hybrid',
+    # comm mode: 'PS' (BASELINE config 3, reference examples/ctr/tests/ps_wdl_criteo.sh: the
+    # dense MLP parameters live on the server too, pushed and pulled every step) or
+    # 'Hybrid' (dense parameters all-reduced on the GPUs, embeddings on the PS)
+    comm = getattr(args, 'comm', None) or 'PS'
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(local), comm_mode=comm,
                      cstable_policy=getattr(args, 'cache', 'LFUOpt'), cache_bound=3, bsp=-1,
                      mixed_precision=args.dtype, seed=1234, prefetch=getattr(args, 'prefetch', True))
+    from ..ps import table as _pst
+    clock = {'wall': 0.0, 'wait': 0.0, 'n': 0}
 
     def step():
+        import time
+        t0, w0 = time.perf_counter(), _pst.WAIT_S[0]
         ex.run('train')
+        clock['wall'] += time.perf_counter() - t0
+        clock['wait'] += _pst.WAIT_S[0] - w0
+        clock['n'] += 1
 
     tables = [t for t in ex.config.placeholder_to_arr_map.values() if getattr(t, 'cache', None) is not None]
     for t in tables:
@@ -209,9 +220,16 @@ def wdl_criteo_bench(args, world, rank, local):
             for k, v in t.cache.perf.items():
                 tot[k] = tot.get(k, 0) + v
         unique, miss = tot.get('unique', 0), tot.get('miss', 0)
+        n = max(clock['n'], 1)
         return {'ids': dist, 'cache_lookups_unique': int(unique), 'cache_misses': int(miss),
                 'cache_hit_rate': round(1.0 - miss / unique, 4) if unique else None,
-                'prefetch_hits': int(sum(t.prefetch_hits for t in tables))}
+                'prefetch_hits': int(sum(t.prefetch_hits for t in tables)),
+                # host-side step breakdown over every step so far: the time run() blocked on
+                # PS / cache tickets and staging copies, and the rest (graph walk, kernel
+                # launches, host work of the lookups / pushes)
+                'step_breakdown_ms': {'wall': round(clock['wall'] * 1e3 / n, 3),
+                                      'ps_wait': round(clock['wait'] * 1e3 / n, 3),
+                                      'host_other': round((clock['wall'] - clock['wait']) * 1e3 / n, 3)}}
     step.extra = extra
 
     def finish():
@@ -219,7 +237,9 @@ def wdl_criteo_bench(args, world, rank, local):
         ex.config.ps_comm.BarrierWorker()
         worker.worker_finish()
 
+    par = ('ps: dense + embeddings on PS (1 server) + HET cache lfuopt/3, %d worker(s)' % world if comm == 'PS'
+           else 'hybrid: PS(1 server)+HET cache lfuopt/3 + dp%d' % world)
     cfg = {'model': 'Wide&Deep (Criteo-shaped, %d x 128 embedding)' % rows, 'global_batch': B * world,
-           'seq_len': None, 'parallelism': 'hybrid: PS(1 server)+HET cache lfuopt/3 + dp%d' % world,
+           'seq_len': None, 'parallelism': par, 'comm_mode': comm,
            'optimizer': 'sgd', 'per_gpu_batch': B}
     return step, B * world, cfg, 'samples/sec (whole node) Wide&Deep-Criteo PS + HET cache', finish

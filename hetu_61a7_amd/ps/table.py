@@ -26,6 +26,22 @@ def _pinned(n, dtype=torch.float32):
 
 
 _STREAMS = {}
+# host seconds spent blocked on the PS / HET cache (ticket waits, staging-copy events):
+# the "PS wait" term of bench.py's Wide&Deep step breakdown
+WAIT_S = [0.0]
+
+
+class _waiting(object):
+    __slots__ = ('t0',)
+
+    def __enter__(self):
+        import time
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *a):
+        import time
+        WAIT_S[0] += time.perf_counter() - self.t0
+        return False
 
 
 def side_streams(device):
@@ -152,10 +168,11 @@ class PSTable(object):
 
     def _wait_push(self):
         if self.pending is not None:
-            if self.cache is not None:
-                self.cache.wait(self.pending)
-            else:
-                self.agent.WaitTicket(self.pending)
+            with _waiting():
+                if self.cache is not None:
+                    self.cache.wait(self.pending)
+                else:
+                    self.agent.WaitTicket(self.pending)
             self.pending = None
             self.pending_push = None
 
@@ -164,7 +181,8 @@ class PSTable(object):
         if pf is None:
             return None, None
         pids, dest, ticket, stage = pf
-        self.cache.wait(ticket)
+        with _waiting():
+            self.cache.wait(ticket)
         if pids.numel() != ids.numel() or not torch.equal(pids, ids):
             return None, None
         self.prefetch_hits += 1
@@ -190,11 +208,12 @@ class PSTable(object):
             self._wait_push()      # on-demand pull sees every push issued so far
             stage = self.out_stage
             dest = stage.get(ids.numel() * self.width).view(-1, self.width)
-            if self.cache is not None:
-                self.cache.embedding_lookup(ids, dest, sync=True)
-            else:
-                t = self.agent.SparsePull(self.key, ids, dest)
-                self.agent.WaitTicket(t)
+            with _waiting():
+                if self.cache is not None:
+                    self.cache.embedding_lookup(ids, dest, sync=True)
+                else:
+                    t = self.agent.SparsePull(self.key, ids, dest)
+                    self.agent.WaitTicket(t)
         self._prefetch_next()
         if self.device.type == 'cuda':
             # H2D on the copy stream; the compute stream waits for it by event only
@@ -237,7 +256,8 @@ class PSTable(object):
             return
         ids, host = self.pending_push
         if self.grad_stage.event is not None:
-            self.grad_stage.event.synchronize()
+            with _waiting():
+                self.grad_stage.event.synchronize()
         if self.cache is not None:
             self.pending = self.cache.embedding_update(ids, host)
         else:
@@ -337,7 +357,8 @@ class PSDense(object):
             self._pull_into_device()
         else:
             t = self.agent.DDPushPull(self.key, self.push_buf, self.pull_buf)
-            self.agent.WaitTicket(t)
+            with _waiting():
+                self.agent.WaitTicket(t)
             self.flat.param.copy_(self.pull_buf[:n], non_blocking=True)
             if self.flat.shadow is not None:
                 self.flat.shadow.copy_(self.flat.param)

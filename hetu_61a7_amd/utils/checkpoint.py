@@ -261,6 +261,33 @@ def _ps_load(ex, file_path):
         d.repull()
 
 
+def _full_moments(d, fl, op=None):
+    """the (non-ZeRO) optimizer record ``d`` holds whole flat s1 / s2 buffers: every
+    bucket's owned range of this rank lies inside them"""
+    if fl is None or op is None or not getattr(op, 'buckets', None) or d.get('zero'):
+        return False
+    arrs = [d.get(k) for k in ('s1', 's2') if getattr(fl, k) is not None]
+    return bool(arrs) and all(a is not None and getattr(a, 'size', 0) >= fl.numel for a in arrs)
+
+
+def _owned_moments(op, d):
+    """this rank's ZeRO-1 shard (bucket by bucket, the owned 1/P of each) of full moments"""
+    import numpy as np
+    out = {}
+    for k in ('s1', 's2'):
+        full = d.get(k)
+        if full is None:
+            continue
+        full = np.asarray(full).reshape(-1)
+        end = max(b.own[1] for b in op.buckets)
+        if full.size < end:      # the ZeRO flat pads to 64 x ranks; the padding has zero state
+            full = np.concatenate([full, np.zeros(end - full.size, full.dtype)])
+        pieces = [full[b.own[0]:b.own[1]] for b in op.buckets]
+        out[k] = np.concatenate(pieces) if pieces else full[:0]
+    out['nrank'] = op.comm.nrank
+    return out
+
+
 def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
     cfg = ex.config
     path = os.path.join(file_path, file_name)
@@ -282,12 +309,18 @@ def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
         src = d
         if getattr(op, 'zero', False):
             if shards is None or i >= len(shards) or shards[i] is None:
-                # a ZeRO-1 resume without this rank's moments would keep the restored
-                # step count with zeroed state (Adam bias correction off): refuse
-                raise FileNotFoundError('ZeRO-1 optimizer shard %s.ext.rank%s (optimizer %d) missing'
-                                        % (path, zr, i))
-            src = shards[i]
-            if src.get('nrank') != op.comm.nrank:
+                if _full_moments(d, fl, op):
+                    # a checkpoint written without ZeRO carries the full moments: take this
+                    # rank's owned range of every bucket
+                    src = _owned_moments(op, d)
+                else:
+                    # a ZeRO-1 resume without this rank's moments would keep the restored
+                    # step count with zeroed state (Adam bias correction off): refuse
+                    raise FileNotFoundError('ZeRO-1 optimizer shard %s.ext.rank%s (optimizer %d) missing'
+                                            % (path, zr, i))
+            else:
+                src = shards[i]
+            if src.get('nrank', op.comm.nrank) != op.comm.nrank:
                 raise ValueError('ZeRO checkpoint was written with %s ranks, resuming with %d'
                                  % (src.get('nrank'), op.comm.nrank))
         if fl is not None:

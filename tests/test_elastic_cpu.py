@@ -28,11 +28,16 @@ JOB = textwrap.dedent('''
     W2 = ht.Variable(name='w2', value=(rng.randn(16, 3) * 0.3).astype(np.float32))
     loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(
         ht.matmul_op(ht.relu_op(ht.matmul_op(x, W1)), W2), y_), [0])
+    adam = len(sys.argv) > 4 and sys.argv[4] == 'adam'
     if zero:   # ZeRO-1: every rank owns half of the Adam moments
         train = ht.optim.AdamOptimizer(0.01).minimize(loss)
         ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'),
                          zero=1, bucket_mb=0.001)
         assert train.zero
+    elif adam:
+        train = ht.optim.AdamOptimizer(0.01).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'),
+                         bucket_mb=0.001)
     else:
         train = ht.optim.MomentumOptimizer(0.05, 0.9).minimize(loss)
         ex = ht.Executor({'train': [loss, train]}, dist_strategy=ht.dist.DataParallel('allreduce'))
@@ -110,6 +115,29 @@ def test_zero1_resume_refuses_missing_rank_shard(tmp_path):
     r, _, _ = _run(tmp_path, 'zmiss', crash_at=-1, restarts=0, extra=['zero'])
     assert r.returncode != 0
     assert 'ZeRO-1 optimizer shard' in r.stderr
+
+
+def test_zero1_resumes_from_a_non_zero_checkpoint(tmp_path):
+    """A checkpoint written without ZeRO carries the full Adam moments: a ZeRO-1 run
+    resumes from it by taking each rank's owned range of every bucket, and ends where
+    the uninterrupted non-ZeRO run does."""
+    ref, ref_out, ckpt = _run(tmp_path, 'adam', crash_at=-1, restarts=0, extra=['adam'])
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    import shutil
+    z = tmp_path / 'ckpt_zfrom'
+    shutil.copytree(ckpt, z)
+    # drop the last snapshot so the ZeRO run resumes at step 6 and trains 4 steps itself
+    snaps = sorted(d for d in os.listdir(z) if d.startswith('step_'))
+    for d in snaps:
+        if d == 'step_9':
+            shutil.rmtree(z / d)
+    (z / 'latest').write_text('step_6\n')
+    r, out, _ = _run(tmp_path, 'zfrom', crash_at=-1, restarts=0, extra=['zero'])
+    assert r.returncode == 0, r.stderr[-2000:]
+    a, b = np.load(ref_out), np.load(out)
+    assert int(b['start']) == 6
+    for k in ('w1', 'w2'):
+        np.testing.assert_allclose(b[k], a[k], rtol=2e-5, atol=2e-6)
 
 
 def test_sparse_update_torch_path_skips_untouched_rows():

@@ -165,7 +165,9 @@ __global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict
 
 // Same merge from per-channel totals (sum, sum of squares) accumulated elsewhere: by
 // the convolution epilogue that produced x (gemm.hip colstats) or by bn_sums_merge.
-__global__ void __launch_bounds__(256) bn_sums_finalize(const float* __restrict__ sums, int64_t M, int C,
+// The totals are zeroed once read: a persistent per-layer buffer is ready for the next
+// accumulation without a fill launch.
+__global__ void __launch_bounds__(256) bn_sums_finalize(float* __restrict__ sums, int64_t M, int C,
                                  const float* __restrict__ scale, const float* __restrict__ bias,
                                  float* __restrict__ run_mean, float* __restrict__ run_var,
                                  float factor, float eps, float* __restrict__ save_mean,
@@ -176,6 +178,8 @@ __global__ void __launch_bounds__(256) bn_sums_finalize(const float* __restrict_
   const double n = (double)M;
   const double mean = (double)sums[c] / n;
   double var = (double)sums[C + c] / n - mean * mean;
+  sums[c] = 0.f;
+  sums[C + c] = 0.f;
   if (var < 0.0) var = 0.0;
   const float invstd = rsqrtf((float)var + eps);
   save_mean[c] = (float)mean;
@@ -209,6 +213,28 @@ __global__ void __launch_bounds__(256) bn_sums_merge(const float* __restrict__ w
   if (lane == 0) {
     sums[c] = (float)S;
     sums[C + c] = (float)Q;
+  }
+}
+
+// sums[c] += total of the [C][chunks] partials (accumulating form of bn_sums_merge)
+__global__ void __launch_bounds__(256) bn_sums_add(const float* __restrict__ ws_s, const float* __restrict__ ws_q,
+                                                    int chunks, int C, float* __restrict__ sums) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  double S = 0.0, Q = 0.0;
+  for (int p = lane; p < chunks; p += 64) {
+    S += (double)ws_s[(int64_t)c * chunks + p];
+    Q += (double)ws_q[(int64_t)c * chunks + p];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    S += __shfl_xor(S, o, 64);
+    Q += __shfl_xor(Q, o, 64);
+  }
+  if (lane == 0) {
+    sums[c] += (float)S;
+    sums[C + c] += (float)Q;
   }
 }
 
@@ -324,7 +350,9 @@ __global__ void __launch_bounds__(256) bn_bwd_partial(const T* __restrict__ dy, 
   if (active) {
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      mu[i] = mean[vc * V + i]; is[i] = invstd[vc * V + i];
+      // null mean / invstd: sums of dy' * x instead of dy' * xhat (hetu_bn_bwd_sums)
+      mu[i] = mean ? mean[vc * V + i] : 0.f;
+      is[i] = invstd ? invstd[vc * V + i] : 1.f;
       if (RELU == 2) { ka[i] = fscale[vc * V + i] * is[i]; kb[i] = fbias[vc * V + i] - mu[i] * ka[i]; }
     }
     // two rows (four vectors) in flight per iteration (all loads issued before any use)
@@ -439,6 +467,33 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize(const float* __restrict__
     cB[c] = B;
     cC[c] = -k1 * sdy * invM - mean[c] * B;
   }
+}
+
+// bn_bwd_finalize from per-channel totals S = sum(dy'), Qx = sum(dy' * x) accumulated by
+// the data-gradient epilogue that produced dy (gemm_core.h Epi::bnx):
+// sum(dy' * xhat) = invstd * (Qx - mean * S).  The totals are zeroed once read.
+__global__ void __launch_bounds__(256) bn_bwd_sums_finalize(float* __restrict__ sums, int64_t M, int C,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           float* __restrict__ dscale, float* __restrict__ dbias,
+                                                           float* __restrict__ cA, float* __restrict__ cB,
+                                                           float* __restrict__ cC) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sdy = sums[c];
+  const float is = invstd[c];
+  const float sdyx = (float)((double)is * ((double)sums[C + c] - (double)mean[c] * (double)sdy));
+  sums[c] = 0.f;
+  sums[C + c] = 0.f;
+  if (dscale) dscale[c] = sdyx;
+  if (dbias) dbias[c] = sdy;
+  const float invM = 1.f / (float)M;
+  const float k1 = scale[c] * is;
+  const float B = -k1 * is * sdyx * invM;
+  cA[c] = k1;
+  cB[c] = B;
+  cC[c] = -k1 * sdy * invM - mean[c] * B;
 }
 
 template <typename T, int RELU, bool DRES>
@@ -560,7 +615,7 @@ template <typename T>
 static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                        const float* bias, float* run_mean, float* run_var, float factor, float eps,
                        float* save_mean, float* save_invstd, float* ws, int relu, int training,
-                       const float* sums, uint8_t* mask, hipStream_t st) {
+                       float* sums, uint8_t* mask, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
@@ -607,7 +662,7 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
 HETU_API int hetu_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int is_bf16,
                          const float* scale, const float* bias, float* run_mean, float* run_var,
                          float factor, float eps, float* save_mean, float* save_invstd, float* ws,
-                         int relu, int training, const float* sums, uint8_t* mask, hipStream_t st) {
+                         int relu, int training, float* sums, uint8_t* mask, hipStream_t st) {
   if (is_bf16)
     return bn_fwd_impl<bf16>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
                              save_mean, save_invstd, ws, relu, training, sums, mask, st);
@@ -639,12 +694,17 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const uint8_
                           int64_t M, int C, const float* mean, const float* invstd,
                           const float* bias, float* w1, float* w2, float* cA,
                           float* cB, float* cC, const float* scale, float* dscale, float* dbias,
-                          hipStream_t st) {
+                          float* bsums, hipStream_t st) {
   constexpr int V = Vec<T>::N;
-  hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, mask, x,
-                     mean, invstd, scale, bias, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 3) / 4), dim3(256), 0, st, w1, w2, g.chunks, M,
-                     C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
+  if (bsums) {
+    hipLaunchKernelGGL(bn_bwd_sums_finalize, dim3((C + 255) / 256), dim3(256), 0, st, bsums, M, C, scale, mean,
+                       invstd, dscale, dbias, cA, cB, cC);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, mask, x,
+                       mean, invstd, scale, bias, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 3) / 4), dim3(256), 0, st, w1, w2, g.chunks, M,
+                       C, scale, mean, invstd, dscale, dbias, cA, cB, cC);
+  }
   int64_t nvec = M * C / V;
   const int grid = bn_apply_grid(nvec, C, V);
   if (dres)
@@ -659,7 +719,7 @@ template <typename T>
 static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
                        int64_t M, int C, const float* scale, const float* bias, const float* mean,
                        const float* invstd, float* dscale, float* dbias, float* ws, int relu,
-                       hipStream_t st) {
+                       float* bsums, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
@@ -674,21 +734,48 @@ static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const
   // otherwise recomputed from x and the folded forward affine (one less stream)
   // (or, with the forward's keep-bit mask, from that: 1/16 of the bytes of y)
   int mode = !relu ? 0 : (mask ? 3 : ((dres || !bias) ? 1 : 2));
-  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
-  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
-  else if (mode == 2) bn_bwd_launch<T, 2>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
-  else bn_bwd_launch<T, 3>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, st);
+  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
+  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
+  else if (mode == 2) bn_bwd_launch<T, 2>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
+  else bn_bwd_launch<T, 3>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
   HETU_LAUNCH_CHECK();
   return 0;
 }
 
 // dy,y,x,dx,dres: [M,C]; y only read when relu (and no mask); dres may be null
-// bias may be null (then the ReLU mask is read from y); mask: hetu_bn_fwd's keep-bits
+// bias may be null (then the ReLU mask is read from y); mask: hetu_bn_fwd's keep-bits.
+// bsums (nullable): [2C] totals sum(dy'), sum(dy' * x) already accumulated (by the
+// epilogue that produced dy, or hetu_bn_bwd_sums): the reduction pass is skipped and the
+// totals are zeroed
 HETU_API int hetu_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres,
                          int64_t M, int C, int is_bf16, const float* scale, const float* bias,
                          const float* mean, const float* invstd, float* dscale, float* dbias,
-                         float* ws, int relu, const uint8_t* mask, hipStream_t st) {
+                         float* ws, int relu, const uint8_t* mask, float* bsums, hipStream_t st) {
   if (is_bf16)
-    return bn_bwd_impl<bf16>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
-  return bn_bwd_impl<float>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu, st);
+    return bn_bwd_impl<bf16>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu,
+                             bsums, st);
+  return bn_bwd_impl<float>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu,
+                            bsums, st);
+}
+
+// sums[0..C) += sum(dy'), sums[C..2C) += sum(dy' * x) over [M, C] bf16 rows, dy' = dy masked
+// by the ReLU keep-bits (nullable): the epilogue-fused reduction, as a pass of its own for
+// data gradients that come from a library kernel.  ws: hetu_bn_workspace_floats.
+HETU_API int hetu_bn_bwd_sums(const void* dy, const void* x, const uint8_t* mask, int64_t M, int C, float* ws,
+                              float* sums, hipStream_t st) {
+  if (C % 8 != 0) return (int)hipErrorInvalidValue;
+  BnGeom g = bn_geom(M, C, 8);
+  float* w1 = ws;
+  float* w2 = ws + (int64_t)g.chunks * C;
+  if (mask)
+    hipLaunchKernelGGL((bn_bwd_partial<bf16, 3>), dim3(g.chunks, g.tiles), dim3(256), 0, st, (const bf16*)dy,
+                       (const bf16*)nullptr, mask, (const bf16*)x, (const float*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr, (const float*)nullptr, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
+  else
+    hipLaunchKernelGGL((bn_bwd_partial<bf16, 0>), dim3(g.chunks, g.tiles), dim3(256), 0, st, (const bf16*)dy,
+                       (const bf16*)nullptr, mask, (const bf16*)x, (const float*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr, (const float*)nullptr, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
+  hipLaunchKernelGGL(bn_sums_add, dim3((C + 3) / 4), dim3(256), 0, st, w1, w2, g.chunks, C, sums);
+  HETU_LAUNCH_CHECK();
+  return 0;
 }

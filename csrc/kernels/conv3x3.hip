@@ -26,6 +26,37 @@ using namespace hetu;
 
 namespace {
 
+// BatchNorm-backward statistics in a data-gradient epilogue (see gemm_core.h Epi::bnx):
+// with x set, colstats receives sum(dx') and sum(dx' * x) of the stored dx, dx' masked by
+// the forward ReLU keep-bits (one byte per 8 channels; null = no ReLU)
+struct BnB {
+  const bf16* x;
+  const uint8_t* mask;
+};
+
+// 4 stored channels at element offset e (co % 4 == 0) into the running sums s[0..3], q[0..3]
+__device__ __forceinline__ void stats4(const BnB& bn, int64_t e, const unsigned short (&h)[4], float* s, float* q) {
+  if (bn.x) {
+    const uint2 a = *reinterpret_cast<const uint2*>(bn.x + e);
+    const float xv[4] = {bf16_bits_to_f((unsigned short)(a.x & 0xffffu)), bf16_bits_to_f((unsigned short)(a.x >> 16)),
+                         bf16_bits_to_f((unsigned short)(a.y & 0xffffu)), bf16_bits_to_f((unsigned short)(a.y >> 16))};
+    const unsigned mk = bn.mask ? (unsigned)bn.mask[e >> 3] >> (e & 7) : 0xfu;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float g = (mk >> i) & 1u ? bf16_bits_to_f(h[i]) : 0.f;
+      s[i] += g;
+      q[i] += g * xv[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float sv = bf16_bits_to_f(h[i]);
+      s[i] += sv;
+      q[i] += sv * sv;
+    }
+  }
+}
+
 typedef short v8s __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
@@ -57,7 +88,8 @@ template <int WD, int TH>
 __global__ __launch_bounds__((Geo<WD, TH>::NT), 1) void conv3x3_c64_k(const bf16* __restrict__ x,
                                                                       const bf16* __restrict__ w,
                                                                       bf16* __restrict__ y, const void* cin,
-                                                                      int cin_f32, float* colstats, int H) {
+                                                                      int cin_f32, float* colstats, BnB bn,
+                                                                      int H) {
   using G = Geo<WD, TH>;
   __shared__ __attribute__((aligned(16))) char smem[WBYTES + G::NSLOT * ROWB];
   char* wl = smem;
@@ -172,12 +204,8 @@ __global__ __launch_bounds__((Geo<WD, TH>::NT), 1) void conv3x3_c64_k(const bf16
         }
         unsigned short h[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          h[i] = f_to_bf16_bits(v[i]);
-          const float sv = bf16_bits_to_f(h[i]);
-          cs[q * 4 + i] += sv;
-          cq[q * 4 + i] += sv * sv;
-        }
+        for (int i = 0; i < 4; ++i) h[i] = f_to_bf16_bits(v[i]);
+        if (colstats) stats4(bn, pix * CH + co, h, cs + q * 4, cq + q * 4);
         uint2 pk;
         pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
         pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
@@ -229,17 +257,17 @@ __global__ void __launch_bounds__(256) flip_bank_k(const bf16* __restrict__ w, b
 }
 
 template <int WD, int TH>
-int launch_c64(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
-               hipStream_t st) {
+int launch_c64(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, BnB bn, int N,
+               int H, hipStream_t st) {
   using G = Geo<WD, TH>;
-  hipLaunchKernelGGL((conv3x3_c64_k<WD, TH>), dim3(N), dim3(G::NT), 0, st, x, w, y, cin, cin_f32, colstats, H);
+  hipLaunchKernelGGL((conv3x3_c64_k<WD, TH>), dim3(N), dim3(G::NT), 0, st, x, w, y, cin, cin_f32, colstats, bn, H);
   return (int)hipGetLastError();
 }
 
-int dispatch_c64(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
-                 int W, hipStream_t st) {
+int dispatch_c64(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, BnB bn, int N,
+                 int H, int W, hipStream_t st) {
   // tiles of 224 pixels: 4 rows of 56 (the only width 64-channel 3x3 layers have in ResNet-50)
-  if (W == 56) return launch_c64<56, 4>(x, w, y, cin, cin_f32, colstats, N, H, st);
+  if (W == 56) return launch_c64<56, 4>(x, w, y, cin, cin_f32, colstats, bn, N, H, st);
   return (int)hipErrorInvalidValue;
 }
 
@@ -418,7 +446,7 @@ struct WGeo {
 template <int WD, int TH, int IMG>
 __global__ __launch_bounds__(256, 4) void conv3x3_wide_k(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                          bf16* __restrict__ y, const void* cin, int cin_f32,
-                                                         float* colstats, int N, int H, int C, int K) {
+                                                         float* colstats, BnB bn, int N, int H, int C, int K) {
   using G = WGeo<WD, TH, IMG>;
   __shared__ __attribute__((aligned(16))) char smem[G::POS8 * 128 + WSL];
   char* halo = smem;
@@ -520,12 +548,8 @@ __global__ __launch_bounds__(256, 4) void conv3x3_wide_k(const bf16* __restrict_
       }
       unsigned short h[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        h[i] = f_to_bf16_bits(v[i]);
-        const float sv = bf16_bits_to_f(h[i]);
-        cs[j * 4 + i] += sv;
-        cq[j * 4 + i] += sv * sv;
-      }
+      for (int i = 0; i < 4; ++i) h[i] = f_to_bf16_bits(v[i]);
+      if (colstats) stats4(bn, opx[b] * K + co, h, cs + j * 4, cq + j * 4);
       uint2 pk;
       pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
       pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
@@ -563,20 +587,20 @@ __global__ void __launch_bounds__(256) flip_bank_any_k(const bf16* __restrict__ 
 }
 
 template <int WD, int TH, int IMG>
-int launch_wide(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
-                int C, int K, hipStream_t st) {
+int launch_wide(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, BnB bn, int N,
+                int H, int C, int K, hipStream_t st) {
   const int tiles = IMG == 1 ? N * ((H + TH - 1) / TH) : (N + IMG - 1) / IMG;
   hipLaunchKernelGGL((conv3x3_wide_k<WD, TH, IMG>), dim3(tiles * (K / WBN)), dim3(256), 0, st, x, w, y, cin,
-                     cin_f32, colstats, N, H, C, K);
+                     cin_f32, colstats, bn, N, H, C, K);
   return (int)hipGetLastError();
 }
 
-int dispatch_wide(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, int N, int H,
-                  int W, int C, int K, hipStream_t st) {
-  if (W == 56 && H % 2 == 0) return launch_wide<56, 2, 1>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
-  if (W == 28 && H % 4 == 0) return launch_wide<28, 4, 1>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
-  if (W == 14 && H % 7 == 0) return launch_wide<14, 7, 1>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
-  if (W == 7 && H == 7) return launch_wide<7, 7, 2>(x, w, y, cin, cin_f32, colstats, N, H, C, K, st);
+int dispatch_wide(const bf16* x, const bf16* w, bf16* y, const void* cin, int cin_f32, float* colstats, BnB bn, int N,
+                  int H, int W, int C, int K, hipStream_t st) {
+  if (W == 56 && H % 2 == 0) return launch_wide<56, 2, 1>(x, w, y, cin, cin_f32, colstats, bn, N, H, C, K, st);
+  if (W == 28 && H % 4 == 0) return launch_wide<28, 4, 1>(x, w, y, cin, cin_f32, colstats, bn, N, H, C, K, st);
+  if (W == 14 && H % 7 == 0) return launch_wide<14, 7, 1>(x, w, y, cin, cin_f32, colstats, bn, N, H, C, K, st);
+  if (W == 7 && H == 7) return launch_wide<7, 7, 2>(x, w, y, cin, cin_f32, colstats, bn, N, H, C, K, st);
   return (int)hipErrorInvalidValue;
 }
 
@@ -738,16 +762,22 @@ HETU_API int hetu_conv3x3_c64_supported(int C, int K, int W) { return C == CH &&
 HETU_API int hetu_conv3x3_c64_fwd(const void* x, const void* w, void* y, float* colstats, int N, int H, int W,
                                   hipStream_t st) {
   if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)y)) & 15) return (int)hipErrorInvalidValue;
-  return dispatch_c64((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, N, H, W, st);
+  return dispatch_c64((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, BnB{}, N, H, W, st);
 }
 
-// dx[N,H,W,64] = conv3x3^T(dy, w) (+ acc: bf16 or fp32 [N,H,W,64]); wt: 64*9*64 bf16 scratch
+// dx[N,H,W,64] = conv3x3^T(dy, w) (+ acc: bf16 or fp32 [N,H,W,64]); wt: 64*9*64 bf16 scratch.
+// bnsums (nullable, 128 fp32 pre-zeroed) += sum(dx') / sum(dx' * bnx) per channel, dx' = dx
+// masked by bnmask (see BnB): the reduction of the backward of the BN that produced x
 HETU_API int hetu_conv3x3_c64_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
-                                    int N, int H, int W, hipStream_t st) {
-  if ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc)) & 15) return (int)hipErrorInvalidValue;
+                                    int N, int H, int W, float* bnsums, const void* bnx, const uint8_t* bnmask,
+                                    hipStream_t st) {
+  if ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc) | ((uintptr_t)bnx)) & 15)
+    return (int)hipErrorInvalidValue;
+  if (bnsums && !bnx) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(flip_bank_k, dim3((CH * 9 * CH + 255) / 256), dim3(256), 0, st, (const bf16*)w, (bf16*)wt);
   HETU_LAUNCH_CHECK();
-  return dispatch_c64((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, nullptr, N, H, W, st);
+  return dispatch_c64((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, bnsums,
+                      BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr}, N, H, W, st);
 }
 
 // slab floats hetu_conv3x3_c64_wgrad needs for a batch of N images
@@ -775,19 +805,24 @@ HETU_API int hetu_conv3x3_wide_fwd(const void* x, const void* w, void* y, float*
                                    int K, hipStream_t st) {
   if (!wide_ok(C, K, H, W) || ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)y)) & 15))
     return (int)hipErrorInvalidValue;
-  return dispatch_wide((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, N, H, W, C, K, st);
+  return dispatch_wide((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, BnB{}, N, H, W, C, K, st);
 }
 
-// dx[N,H,W,C] = conv3x3^T(dy[N,H,W,K], w) (+ acc), K % 64 == 0, C % 128 == 0; wt: C*9*K bf16
+// dx[N,H,W,C] = conv3x3^T(dy[N,H,W,K], w) (+ acc), K % 64 == 0, C % 128 == 0; wt: C*9*K bf16;
+// bnsums / bnx / bnmask as hetu_conv3x3_c64_dgrad (2*C floats)
 HETU_API int hetu_conv3x3_wide_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
-                                     int N, int H, int W, int C, int K, hipStream_t st) {
-  if (!wide_ok(K, C, H, W) || ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc)) & 15))
+                                     int N, int H, int W, int C, int K, float* bnsums, const void* bnx,
+                                     const uint8_t* bnmask, hipStream_t st) {
+  if (!wide_ok(K, C, H, W) ||
+      ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc) | ((uintptr_t)bnx)) & 15))
     return (int)hipErrorInvalidValue;
+  if (bnsums && !bnx) return (int)hipErrorInvalidValue;
   const int64_t n = (int64_t)C * 9 * K;
   hipLaunchKernelGGL(flip_bank_any_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const bf16*)w, (bf16*)wt,
                      C, K);
   HETU_LAUNCH_CHECK();
-  return dispatch_wide((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, nullptr, N, H, W, K, C, st);
+  return dispatch_wide((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, bnsums,
+                       BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr}, N, H, W, K, C, st);
 }
 
 HETU_API int hetu_conv3x3_wide_wgrad_supported(int C, int K, int H, int W) { return wide_wgrad_ok(C, K, H, W); }

@@ -488,6 +488,12 @@ struct Epi {
   // colstats[0..N) and colstats[N..2N), pre-zeroed): the BatchNorm statistics of a
   // convolution output, fused into the epilogue that already holds the values
   float* colstats;
+  // BatchNorm-backward form of colstats (C is the gradient dy of a BN output, bf16,
+  // ldc % 8 == 0): colstats receives sum(dy') and sum(dy' * x), dy' = dy masked by the
+  // forward's ReLU keep-bits (bnmask, one byte per 8 channels, null: no ReLU) and x the
+  // BN input (bnx, C's layout) -- the BN backward's reduction pass, fused here
+  const bf16* bnx;
+  const uint8_t* bnmask;
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -649,7 +655,22 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
         if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
     }
   }
-  if (ep.colstats) {   // statistics of the values as stored
+  if (ep.colstats && ep.bnx) {   // BN backward sums of the stored dy
+    float xv[8];
+    if (o.cvec && full) {
+      load_vec<bf16>(ep.bnx + off, xv);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) xv[t] = n + t < N ? to_f(ep.bnx[off + t]) : 0.f;
+    }
+    const unsigned mk = ep.bnmask ? (unsigned)ep.bnmask[off >> 3] : 0xffu;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float g = (mk >> t) & 1u ? bf16_bits_to_f(f_to_bf16_bits(v[t])) : 0.f;
+      cs[t] += g;
+      cq[t] += g * xv[t];
+    }
+  } else if (ep.colstats) {   // statistics of the values as stored
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const float sv = ep.out_f32 ? v[t] : bf16_bits_to_f(f_to_bf16_bits(v[t]));

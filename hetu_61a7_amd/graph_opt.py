@@ -22,6 +22,9 @@ Backward (``fuse_backward``, run on the gradient graph):
   reduce_sum_axis0(d x) where x feeds a fused dropout+add+LayerNorm
                                   -> the LayerNorm backward kernel emits that bias
                                      gradient of the producing linear layer
+  bn_backward(conv_dgrad(w, g), x) -> the dgrad epilogue also accumulates the BN
+                                     backward's per-channel reduction (sum dy',
+                                     sum dy'*x), removing its pass over dy and x
 """
 from __future__ import annotations
 
@@ -201,4 +204,41 @@ def fuse_backward(roots):
                     n.bw_of = bw
                 fused += 1
                 break
+    fused += _fuse_bn_backward_reduction(roots)
+    return fused
+
+
+def _fuse_bn_backward_reduction(roots):
+    """BatchNorm backward whose dy comes straight from a convolution data gradient:
+    that kernel's epilogue, which holds dy, also accumulates the BN backward's
+    per-channel reduction (sum(dy'), sum(dy' * x)), and the BN backward skips its own
+    pass over dy and x.  The dgrad op gets the BN's input x and forward node (mean,
+    invstd, ReLU keep-bits) as extra inputs; the BN forward keeps ReLU keep-bits.
+    Off under deterministic mode (fp32 atomics) or HETU_FUSE_BN_BWD=0."""
+    from .kernels import deterministic
+    if os.environ.get('HETU_FUSE_BN_BWD', '1') != '1' or deterministic():
+        return 0
+    from .ops.nn import Conv2d_Gradient_of_DataOp, Batch_Normalization_GradientOp
+    topo, cons = _consumers(roots)
+    root_set = set(roots)
+    fused = 0
+    for n in topo:
+        if type(n) is not Batch_Normalization_GradientOp:
+            continue
+        d, fw = n.inputs[0], n.forward_node
+        if not isinstance(d, Conv2d_Gradient_of_DataOp) or d.bn_fused is not None or d in root_set or \
+                len(cons.get(d, [])) != 1 or len(d.inputs) not in (3, 4):
+            continue
+        # same device group (a pipeline stage boundary between the BN and its consumer
+        # convolution would make the forward node's aux a cross-stage input)
+        ctx = getattr(n, 'raw_ctx', None)
+        src = getattr(d, 'bw_of', None)
+        if getattr(d, 'raw_ctx', None) != ctx or getattr(fw, 'raw_ctx', None) != ctx or \
+                (src is not None and getattr(src, 'raw_ctx', None) != ctx):
+            continue
+        d.inputs = list(d.inputs) + [n.inputs[1], fw]
+        d.bn_fused = fw
+        d.value_and_aux_inputs = (len(d.inputs) - 1,)
+        fw.bwd_fused = True
+        fused += 1
     return fused

@@ -128,12 +128,14 @@ def _match(x, w):
     return x, w
 
 
-def conv2d_with_stats(x, w, stride, padding):
+def conv2d_with_stats(x, w, stride, padding, out_sums=None):
     """(y, sums): the convolution (no bias) and the [2*Cout] per-channel sum / sum of
     squares of y that a following training-mode BatchNorm needs.  Every candidate
     delivers both, so the per-shape choice prices the statistics pass in: the
     hand-written kernels fuse it into their epilogue, the library convolutions pay a
-    separate column-statistics pass."""
+    separate column-statistics pass.  ``out_sums``: a zeroed [2*Cout] fp32 buffer the
+    fused candidates accumulate into (a persistent one the BN re-zeroes: no fill launch
+    per call); fresh zeros otherwise and while the shape is being timed."""
     x, w = _match(x, w)
     if not (x.is_cuda and x.dtype == torch.bfloat16):
         return conv2d(x, w, None, stride, padding), None
@@ -142,10 +144,13 @@ def conv2d_with_stats(x, w, stride, padding):
     x = x.contiguous(memory_format=CL)
     w = w.contiguous(memory_format=CL)
     co = w.shape[0]
+    key = ('fwd_stats', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding))
+    from .autotune import _decisions
+    tgt = [out_sums if key in _decisions else None]
 
     def fused(run):
         def f():
-            s = _zeros(2 * co, x.device)
+            s = tgt[0] if tgt[0] is not None else _zeros(2 * co, x.device)
             y = run(s)
             return None if y is None else (y, s)
         return f
@@ -174,12 +179,12 @@ def conv2d_with_stats(x, w, stride, padding):
     elif _needs_pad(x, w):
         cands['hip_pad'] = fused(lambda s: conv_igemm.try_forward(_pad_c(x), _pad_c(w), stride, padding,
                                                                    colstats=s))
-    key = ('fwd_stats', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding))
     if MODE == 'vendor':
         record_vendor('conv')
         return cands['vendor']()
     from .autotune import choose
     c = choose(key, cands, MODE)
+    tgt[0] = out_sums
     r = cands[c]()
     if r is not None and not c.startswith('hip'):
         record_vendor('conv')
@@ -287,10 +292,24 @@ def conv2d(x, w, b, stride, padding):
     return y
 
 
-def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=False):
+def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=False, bn=None):
     """dx (+ acc when given: a gradient joined at the conv input, fused into the
     epilogue on the HIP path).  ``acc_inplace``: acc is dead after this call and
-    may receive the result (the library GEMM accumulates into it, C == D)."""
+    may receive the result (the library GEMM accumulates into it, C == D).
+    ``bn`` = (sums, x, mask): dx is the gradient of a training BatchNorm's output
+    (x: that BN's input, mask: its ReLU keep-bits or None); sums ([2C] fp32, zero)
+    receive sum(dx') and sum(dx' * x), the BN backward's reduction -- in the data
+    gradient's epilogue on the hand-written kernels, as a pass of its own after a
+    library kernel -- and the result carries them as ``hetu_bn_bsums``.  bf16 on the
+    GPU only (otherwise ignored)."""
+    if bn is not None:
+        if not (g.is_cuda and g.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and
+                (acc is None or acc.dtype == torch.bfloat16) and bn[1].dtype == torch.bfloat16 and
+                bn[1].is_contiguous(memory_format=CL) and x_shape[1] % 8 == 0 and MODE != 'vendor'):
+            return conv2d_backward_data(g, w, x_shape, stride, padding, acc, acc_inplace)
+        r = _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn)
+        r.hetu_bn_bsums = bn[0]
+        return r
     g, w = _match(g, w)
     from . import cpu_native
     if cpu_native.active(g, w, acc):
@@ -357,6 +376,47 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
                      lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
                      lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas, tuned)
     return _vendor_dgrad(g, w, x_shape, stride, padding, acc)
+
+
+def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
+    """conv2d_backward_data with the BatchNorm-backward reduction (see there)"""
+    from . import conv_igemm
+    from .autotune import _decisions
+    from .norm import bn_bwd_sums
+    sums, xb, mask = bn
+    g = g.contiguous(memory_format=CL)
+    w = w.contiguous(memory_format=CL)
+    if acc is not None:
+        acc = acc.contiguous(memory_format=CL)
+    key = ('dgrad_bn', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None)
+    # candidates accumulate into scratch while the shape is being timed
+    tgt = [sums if key in _decisions else torch.zeros_like(sums)]
+
+    def hip(tile=0):
+        return lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=tile,
+                                                    bnb=(tgt[0], xb, mask))
+
+    def separate(run):
+        def f():
+            r = run()
+            if r is not None:
+                bn_bwd_sums(r, xb, mask, tgt[0])
+            return r
+        return f
+    blas = {}
+    if x_shape[1] >= 128:
+        blas['hip256'] = hip(1)
+    if x_shape[1] <= 64:
+        blas['hip64'] = hip(2)
+    if _short_k(w.shape[0] * w.shape[2] * w.shape[3]):
+        blas['hip_lo'] = hip(3)
+    if conv_igemm.conv3x3_ok(x_shape, w.shape, stride, padding, dgrad=True):
+        blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=acc,
+                                                                      bnb=(tgt[0], xb, mask))
+
+    def tuned():
+        tgt[0] = sums
+    return _pick(key, hip(0), separate(lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc)), blas, tuned)
 
 
 def _layout_of(t):

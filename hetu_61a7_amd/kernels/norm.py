@@ -87,6 +87,8 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
                     sums.data_ptr() if (sums is not None and training) else None,
                     mask.data_ptr() if mask is not None else None, stream_ptr()), 'bn_fwd')
             return y, save_mean, save_invstd
+    if sums is not None:
+        sums.zero_()     # not consumed here: leave the (persistent) totals ready for next time
     from . import cpu_native
     if (x.dim() == 4 and cpu_native.active(x, scale, bias, running_mean, running_var)
             and (training or running_mean is not None)):
@@ -122,10 +124,27 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
     return y, mean.float(), invstd.float()
 
 
+def bn_bwd_sums(dy, x, mask, sums):
+    """sums[:C] += sum(dy'), sums[C:] += sum(dy' * x) per channel (dy' = dy masked by the
+    ReLU keep-bits ``mask``, or dy): the reduction a data-gradient epilogue fuses, as a
+    pass of its own.  bf16 channels-last dy / x."""
+    rows = _as_rows(x)
+    C = x.shape[1]
+    M = x.numel() // C
+    dy = dy.contiguous(memory_format=torch.channels_last) if dy.dim() == 4 else dy.contiguous()
+    ws = _ws(M, C, 1, x.device)
+    f = fn('hetu_bn_bwd_sums', [P, P, P, I64, I32, P, P, P])
+    check(f(dy.data_ptr(), rows[0].data_ptr(), mask.data_ptr() if mask is not None else None, M, C,
+            ws.data_ptr(), sums.data_ptr(), stream_ptr()), 'bn_bwd_sums')
+    return sums
+
+
 def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=False, bias=None,
-                dscale_out=None, dbias_out=None, mask=None):
+                dscale_out=None, dbias_out=None, mask=None, bsums=None):
     """Returns (dx, dscale, dbias, dres).  ``mask``: the forward's ReLU keep-bits
-    (native path only; y is then not read)."""
+    (native path only; y is then not read).  ``bsums``: [2C] totals sum(dy') and
+    sum(dy' * x) already accumulated (the producing data-gradient epilogue); the
+    reduction pass is skipped and the totals are zeroed for their next use."""
     C = x.shape[1]
     if native(x) and x.dtype in (torch.float32, torch.bfloat16):
         cl = torch.channels_last
@@ -146,15 +165,18 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
             ws = _ws(M, C, is_bf16(x), x.device)
             if mask is not None:
                 assert relu and mask.dtype == torch.uint8 and mask.numel() == relu_mask_bytes(x)
-            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P, P])
+            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P, P, P])
             check(f(dy.data_ptr(), y.data_ptr() if (relu and mask is None) else None, x.data_ptr(),
                     dx.data_ptr(), dres.data_ptr() if dres is not None else None, M, C, is_bf16(x),
                     scale.data_ptr(), bias.float().contiguous().data_ptr() if bias is not None else None,
                     save_mean.data_ptr(), save_invstd.data_ptr(),
                     dscale.data_ptr(), dbias.data_ptr(), ws.data_ptr(), int(relu),
-                    mask.data_ptr() if mask is not None else None, stream_ptr()),
+                    mask.data_ptr() if mask is not None else None,
+                    bsums.data_ptr() if bsums is not None else None, stream_ptr()),
                   'bn_bwd')
             return dx, dscale, dbias, dres
+    if bsums is not None:
+        bsums.zero_()
     from . import cpu_native
     if x.dim() == 4 and cpu_native.active(dy, x, scale, save_mean, save_invstd) and (not relu or y is not None):
         g = cpu_native.relu_grad(y.float().contiguous(), dy.float().contiguous()) if relu else dy.float()

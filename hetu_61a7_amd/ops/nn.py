@@ -63,7 +63,10 @@ class Conv2dOp(Op):
         if getattr(self, 'emit_bn_stats', False) and getattr(x, 'is_cuda', False):
             # the only consumer is a training BatchNorm: hand it the statistics of y
             # (fused into the conv epilogue where the hand-written kernel runs)
-            y, sums = KC.conv2d_with_stats(x, w, self.stride, self.padding)
+            bufs = self.__dict__.setdefault('_bn_sums', {})
+            if x.device not in bufs:   # persistent: the BN zeroes the totals after reading them
+                bufs[x.device] = torch.zeros(2 * w.shape[0], dtype=torch.float32, device=x.device)
+            y, sums = KC.conv2d_with_stats(x, w, self.stride, self.padding, out_sums=bufs[x.device])
             if sums is not None:
                 y.hetu_bn_sums = sums
             return y
@@ -94,12 +97,25 @@ class Conv2d_Gradient_of_DataOp(Op):
         super().__init__(Conv2d_Gradient_of_DataOp, [w, grad, x_ref], ctx)
         self.padding, self.stride = _pair(padding), _pair(stride)
 
+    bn_fused = None   # graph_opt: (BN forward node) whose backward reduction this epilogue computes
+
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        # optional 4th input: a gradient to accumulate (fused fan-in sum, graph_opt)
+        # optional 4th input: a gradient to accumulate (fused fan-in sum, graph_opt);
+        # with bn_fused the last two inputs are that BN's input x and its forward node
         w, g, xshape = input_vals[:3]
-        acc = input_vals[3] if len(input_vals) > 3 else None
+        nbase = len(input_vals) - (2 if self.bn_fused is not None else 0)
+        acc = input_vals[3] if nbase > 3 else None
+        bn = None
+        if self.bn_fused is not None:
+            xb, (_, aux) = input_vals[-2], input_vals[-1]
+            if len(aux) > 2 or not self.bn_fused.relu:   # ReLU keep-bits (or no ReLU)
+                bufs = self.__dict__.setdefault('_bn_sums', {})
+                sums = bufs.get(xb.device)
+                if sums is None:   # persistent: the BN backward zeroes it after reading
+                    sums = bufs[xb.device] = torch.zeros(2 * xb.shape[1], dtype=torch.float32, device=xb.device)
+                bn = (sums, xb, aux[2] if len(aux) > 2 else None)
         return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,
-                                       acc_inplace=_may_overwrite(self, acc))
+                                       acc_inplace=_may_overwrite(self, acc), bn=bn)
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -279,6 +295,8 @@ def avg_pool2d_gradient_op(node_out, node_out_gradient, node_in, kernel_H, kerne
 # ---------------------------------------------------------------------------
 # batch normalisation (+ fused ReLU / residual)
 class Batch_NormalizationOp(Op):
+    bwd_fused = False
+
     def __init__(self, x, scale, bias, momentum=0.1, eps=1e-5, relu=False, residual=None, ctx=None):
         inputs = [x, scale, bias] + ([residual] if residual is not None else [])
         super().__init__(Batch_NormalizationOp, inputs, ctx)
@@ -287,6 +305,7 @@ class Batch_NormalizationOp(Op):
         self.running_mean = None
         self.running_var = None
         self.inference = False
+        self.bwd_fused = False    # graph_opt: the backward reduction runs in a dgrad epilogue
 
     def _init_running(self, C, device):
         if self.running_mean is None or self.running_mean.device != device:
@@ -304,10 +323,13 @@ class Batch_NormalizationOp(Op):
         sums = getattr(x, 'hetu_bn_sums', None) if training else None
         # fused add+ReLU: the backward needs the ReLU mask, which then depends on the
         # residual too; keep it as bits (1/16 of y's bytes) instead of re-reading y
+        # (also wanted by a data-gradient epilogue that fuses this BN's backward reduction)
         mask = None
-        if training and self.relu and self.has_residual and x.is_cuda and native(x) and \
+        if training and self.relu and (self.has_residual or self.bwd_fused) and x.is_cuda and native(x) and \
                 x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % (8 if x.dtype == torch.bfloat16 else 4) == 0:
             mask = torch.empty(KN.relu_mask_bytes(x), dtype=torch.uint8, device=x.device)
+        if sums is None and getattr(x, 'hetu_bn_sums', None) is not None:
+            x.hetu_bn_sums.zero_()    # persistent totals not consumed (inference): ready for next time
         y, mean, invstd = KN.bn_forward(x, scale.float(), bias.float(), self.running_mean,
                                         self.running_var, self.momentum, self.eps, training,
                                         relu=self.relu, residual=res, sums=sums, mask=mask)
@@ -348,9 +370,16 @@ class Batch_Normalization_GradientOp(Op):
         bias = input_vals[4] if len(input_vals) > 4 else None
         fw = self.forward_node
         dests = getattr(self, 'grad_dests', {})
+        # the reduction totals of the data-gradient epilogue that produced g (fused: ops
+        # Conv2d_Gradient_of_DataOp.bn_fused); the kernel zeroes them once read
+        bsums = getattr(g, 'hetu_bn_bsums', None)
+        if bsums is not None and not (g.is_cuda and g.dtype == x.dtype == torch.bfloat16 and (mask is not None or not fw.relu)):
+            bsums.zero_()
+            bsums = None
         dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
                                                  relu=fw.relu, want_dres=fw.has_residual, bias=bias,
-                                                 dscale_out=dests.get(1), dbias_out=dests.get(2), mask=mask)
+                                                 dscale_out=dests.get(1), dbias_out=dests.get(2), mask=mask,
+                                                 bsums=bsums)
         return (dx, dscale, dbias, dres)
 
     def gradient(self, output_grad):

@@ -1,0 +1,166 @@
+"""BatchNorm reductions fused into convolution epilogues (graph_opt.fuse_forward /
+_fuse_bn_backward_reduction; gemm_core.h Epi::colstats / Epi::bnx, conv3x3.hip BnB).
+
+Forward: the conv epilogue accumulates the per-channel sum / sum of squares of its
+output.  Backward: the data-gradient epilogue that produces a BN output's gradient dy
+accumulates sum(dy') and sum(dy' * x) (dy' = dy masked by the forward's ReLU
+keep-bits, x the BN input), and the BN backward skips its own pass over dy and x.
+Reference semantics: src/ops/CudnnBn.cu:22-194 (cudnnBatchNormalizationBackward).
+Each kernel is checked against a plain fp32 torch reduction of the same stored values.
+"""
+import os
+
+import pytest
+import torch
+
+from hetu_61a7_amd.kernels import conv as KC, conv_igemm as CI, norm as KN
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+CL = torch.channels_last
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def _bits(mask, shape_nhwc):
+    """per-element keep bits (0/1 float) of a byte-per-8-channels mask"""
+    sh = torch.arange(8, device=mask.device, dtype=torch.int32)
+    return ((mask.to(torch.int32).view(-1, 1) >> sh) & 1).float().view(shape_nhwc)
+
+
+def _ref_sums(dx, x, mask):
+    d = dx.permute(0, 2, 3, 1).float()
+    if mask is not None:
+        d = d * _bits(mask, d.shape)
+    xv = x.permute(0, 2, 3, 1).float()
+    return d.sum((0, 1, 2)), (d * xv).sum((0, 1, 2))
+
+
+# (g shape [N, K, OH, OW], w shape [K, C, kh, kw], x shape, stride, pad, kernel)
+CASES = [
+    ((4, 256, 14, 14), (256, 64, 1, 1), (4, 64, 14, 14), 1, 0, ('gemm', 0)),
+    ((4, 256, 14, 14), (256, 64, 1, 1), (4, 64, 14, 14), 1, 0, ('gemm', 2)),
+    ((4, 256, 14, 14), (256, 64, 1, 1), (4, 64, 14, 14), 1, 0, ('gemm', 3)),
+    ((4, 64, 14, 14), (64, 256, 1, 1), (4, 256, 14, 14), 1, 0, ('gemm', 1)),
+    ((4, 128, 14, 14), (128, 64, 3, 3), (4, 64, 28, 28), 2, 1, ('gemm', 0)),      # stride classes
+    ((2, 64, 56, 56), (64, 64, 3, 3), (2, 64, 56, 56), 1, 1, ('c3', None)),       # c64 halo kernel
+    ((2, 128, 28, 28), (128, 128, 3, 3), (2, 128, 28, 28), 1, 1, ('c3', None)),   # wide halo kernel
+    ((2, 256, 7, 7), (256, 256, 3, 3), (2, 256, 7, 7), 1, 1, ('c3', None)),
+]
+
+
+@pytest.mark.parametrize('case', CASES, ids=lambda c: '%s-%s-%s' % (c[1], c[5][0], c[5][1]))
+@pytest.mark.parametrize('masked', [True, False])
+@pytest.mark.parametrize('join', [False, True])
+def test_dgrad_epilogue_bn_sums(case, masked, join):
+    gs, ws, xs, s, p, (kind, tile) = case
+    torch.manual_seed(0)
+    g = torch.randn(gs, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(ws, device=DEV) * 0.05).bfloat16().contiguous(memory_format=CL)
+    xb = (torch.randn(xs, device=DEV) + 0.5).bfloat16().contiguous(memory_format=CL)
+    acc = torch.randn(xs, device=DEV).bfloat16().contiguous(memory_format=CL) if join else None
+    n = xb.numel() // 8
+    mask = torch.randint(0, 256, (n,), device=DEV, dtype=torch.int32).to(torch.uint8) if masked else None
+    sums = torch.zeros(2 * xs[1], device=DEV)
+    if kind == 'gemm':
+        dx = CI.try_backward_data(g, w, xs, (s, s), (p, p), acc=acc, tile=tile, bnb=(sums, xb, mask))
+        dx0 = CI.try_backward_data(g, w, xs, (s, s), (p, p), acc=acc, tile=tile)
+    else:
+        dx = CI.try_conv3x3_backward_data(g, w, xs, (s, s), (p, p), acc=acc, bnb=(sums, xb, mask))
+        dx0 = CI.try_conv3x3_backward_data(g, w, xs, (s, s), (p, p), acc=acc)
+    assert dx is not None
+    assert torch.equal(dx, dx0)     # the statistics do not perturb the stored gradient
+    rs, rq = _ref_sums(dx, xb, mask)
+    C = xs[1]
+    assert _rel(sums[:C], rs) < 1e-4, (_rel(sums[:C], rs))
+    assert _rel(sums[C:], rq) < 1e-4, (_rel(sums[C:], rq))
+
+
+def test_bn_bwd_sums_pass_matches_reference():
+    x = (torch.randn(4, 128, 14, 14, device=DEV) + 1).bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(4, 128, 14, 14, device=DEV).bfloat16().contiguous(memory_format=CL)
+    mask = torch.randint(0, 256, (x.numel() // 8,), device=DEV, dtype=torch.int32).to(torch.uint8)
+    sums = torch.zeros(256, device=DEV)
+    KN.bn_bwd_sums(dy, x, mask, sums)
+    rs, rq = _ref_sums(dy, x, mask)
+    assert _rel(sums[:128], rs) < 1e-4 and _rel(sums[128:], rq) < 1e-4
+
+
+@pytest.mark.parametrize('relu,residual', [(True, False), (True, True), (False, False)])
+def test_bn_backward_from_epilogue_sums_matches_plain(relu, residual):
+    """bn_backward with the totals handed in (bsums) against the full backward; the
+    totals are zeroed once read (persistent per-layer buffers)."""
+    torch.manual_seed(1)
+    C = 128
+    x = (torch.randn(4, C, 14, 14, device=DEV) * 2 + 0.7).bfloat16().contiguous(memory_format=CL)
+    res = torch.randn_like(x).contiguous(memory_format=CL) if residual else None
+    sc, bi = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.2
+    mask = torch.empty(KN.relu_mask_bytes(x), dtype=torch.uint8, device=DEV) if relu else None
+    y, mean, invstd = KN.bn_forward(x, sc, bi, None, None, 0.1, 1e-5, True, relu=relu, residual=res, mask=mask)
+    dy = torch.randn_like(x).contiguous(memory_format=CL)
+    ref = KN.bn_backward(dy, y, x, sc, mean, invstd, relu=relu, want_dres=residual, bias=bi, mask=mask)
+    bs = torch.zeros(2 * C, device=DEV)
+    KN.bn_bwd_sums(dy, x, mask, bs)
+    out = KN.bn_backward(dy, y, x, sc, mean, invstd, relu=relu, want_dres=residual, bias=bi, mask=mask, bsums=bs)
+    assert torch.count_nonzero(bs).item() == 0
+    for a, b in zip(out, ref):
+        if b is None:
+            assert a is None
+            continue
+        assert _rel(a, b) < 2e-3, _rel(a, b)
+
+
+def test_persistent_forward_sums_are_rezeroed():
+    x = torch.randn(4, 64, 28, 28, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(128, 64, 3, 3, device=DEV) * 0.1).bfloat16().contiguous(memory_format=CL)
+    buf = torch.zeros(256, device=DEV)
+    sc, bi = torch.rand(128, device=DEV) + 0.5, torch.randn(128, device=DEV)
+    ref = None
+    for _ in range(3):   # the first call autotunes against scratch, later ones use buf
+        y, sums = KC.conv2d_with_stats(x, w, (1, 1), (1, 1), out_sums=buf)
+        a, m, i = KN.bn_forward(y, sc, bi, None, None, 0.1, 1e-5, True, relu=True, sums=sums)
+        assert torch.count_nonzero(buf).item() == 0
+        if ref is None:
+            ref = (m.clone(), i.clone())
+        assert _rel(m, ref[0]) < 1e-5 and _rel(i, ref[1]) < 1e-5
+    a2, m2, i2 = KN.bn_forward(y, sc, bi, None, None, 0.1, 1e-5, True, relu=True)
+    assert _rel(m2, ref[0]) < 1e-4 and _rel(i2, ref[1]) < 1e-4
+
+
+def _resnet_steps(fuse_bwd, fuse_stats, steps=3):
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.models import resnet50_imagenet
+    os.environ['HETU_FUSE_BN_BWD'] = '1' if fuse_bwd else '0'
+    os.environ['HETU_FUSE_BN_STATS'] = '1' if fuse_stats else '0'
+    try:
+        B = 4
+        x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+        loss, _ = resnet50_imagenet(x, y_, 1000)
+        train = ht.optim.MomentumOptimizer(learning_rate=0.05, momentum=0.9).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3)
+        g = torch.Generator(device='cuda')
+        g.manual_seed(0)
+        X = torch.randn((B, 3, 224, 224), device='cuda', generator=g).bfloat16().contiguous(memory_format=CL)
+        Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
+        out = []
+        for _ in range(steps):
+            lv = ex.run('train', feed_dict={x: X, y_: Y})[0]
+            out.append(float(lv.asnumpy().mean() if hasattr(lv, 'asnumpy') else lv.float().mean()))
+        fused = sum(1 for n in ex.subexecutor['train'].computing_nodes if getattr(n, 'bn_fused', None) is not None)
+        return out, fused
+    finally:
+        os.environ.pop('HETU_FUSE_BN_BWD', None)
+        os.environ.pop('HETU_FUSE_BN_STATS', None)
+
+
+def test_resnet50_training_with_fused_bn_reductions_tracks_unfused():
+    """Three momentum steps of ResNet-50 (batch 4): with both BN reductions in the conv
+    epilogues the loss trajectory matches the unfused graph to bf16 noise."""
+    a, _ = _resnet_steps(False, False)
+    b, nf = _resnet_steps(True, True)
+    assert nf >= 40, nf
+    for u, v in zip(a, b):
+        assert abs(u - v) <= 0.02 * max(1.0, abs(u)), (a, b)

@@ -151,7 +151,7 @@ def test_bn_from_fused_statistics_matches_plain_bn():
     rm1, rv1 = torch.zeros(128, device=DEV), torch.ones(128, device=DEV)
     rm2, rv2 = rm1.clone(), rv1.clone()
     a, m1, i1 = KN.bn_forward(y, sc, bi, rm1, rv1, 0.1, 1e-5, True, relu=True)
-    b, m2, i2 = KN.bn_forward(y, sc, bi, rm2, rv2, 0.1, 1e-5, True, relu=True, sums=sums)
+    b, m2, i2 = KN.bn_forward(y, sc, bi, rm2, rv2, 0.1, 1e-5, True, relu=True, sums=sums.clone())
     assert _rel(m2, m1) < 1e-4 and _rel(i2, i1) < 1e-4 and _rel(rv2, rv1) < 1e-4
     assert _rel(b, a) < 1e-2
     s2 = KN.col_sums(y)

@@ -69,18 +69,28 @@ void BFCAllocator::sub_free(void* p) {
   }
 }
 
+BFCAllocator::Bins& BFCAllocator::bins_for(hipStream_t s) {
+  if (last_bins_ == nullptr || s != last_stream_) {
+    last_bins_ = &bins_[s];
+    last_stream_ = s;
+  }
+  return *last_bins_;
+}
+
 void BFCAllocator::insert_free(Chunk* c) {
-  bins_[c->stream].b[bin_of(c->size)].insert(c);
+  bins_for(c->stream).b[bin_of(c->size)].insert(c);
+  c->listed = true;
   st_.num_free_chunks++;
 }
 
 void BFCAllocator::erase_free(Chunk* c) {
-  bins_[c->stream].b[bin_of(c->size)].erase(c);
+  bins_for(c->stream).b[bin_of(c->size)].erase(c);
+  c->listed = false;
   st_.num_free_chunks--;
 }
 
 BFCAllocator::Chunk* BFCAllocator::take_from(Bins& bins, size_t size) {
-  Chunk key{nullptr, size, false, 0, nullptr, nullptr, nullptr};
+  Chunk key{nullptr, size, false, 0, nullptr, nullptr, nullptr, false, nullptr};
   for (int b = bin_of(size); b < kNumBins; ++b) {
     auto it = bins.b[b].lower_bound(&key);
     if (it != bins.b[b].end()) return *it;
@@ -89,17 +99,12 @@ BFCAllocator::Chunk* BFCAllocator::take_from(Bins& bins, size_t size) {
 }
 
 BFCAllocator::Chunk* BFCAllocator::find_chunk(size_t size, hipStream_t s) {
-  Chunk* c = nullptr;
-  auto it = bins_.find(s);
-  if (it != bins_.end()) c = take_from(it->second, size);
-  if (c == nullptr && s != nullptr) {
-    auto jt = bins_.find(nullptr);
-    if (jt != bins_.end()) c = take_from(jt->second, size);
-  }
+  Chunk* c = take_from(bins_for(s), size);
+  if (c == nullptr && s != nullptr) c = take_from(bins_for(nullptr), size);
   if (c == nullptr) return nullptr;
   erase_free(c);
   if (c->size - size >= kMinAlloc) {   // split; the remainder stays free on the same stream
-    Chunk* r = new Chunk{c->ptr + size, c->size - size, false, c->region, c, c->next, c->stream};
+    Chunk* r = new Chunk{c->ptr + size, c->size - size, false, c->region, c, c->next, c->stream, false, nullptr};
     if (c->next) c->next->prev = r;
     c->next = r;
     c->size = size;
@@ -118,7 +123,7 @@ bool BFCAllocator::grow(size_t min_bytes) {
     p = sub_alloc(want);
   }
   if (p == nullptr) return false;
-  Chunk* c = new Chunk{(char*)p, want, false, (int)regions_.size(), nullptr, nullptr, nullptr};
+  Chunk* c = new Chunk{(char*)p, want, false, (int)regions_.size(), nullptr, nullptr, nullptr, false, nullptr};
   regions_.push_back(Region{(char*)p, want, c});
   st_.bytes_reserved += (int64_t)want;
   st_.num_regions++;
@@ -127,9 +132,38 @@ bool BFCAllocator::grow(size_t min_bytes) {
   return true;
 }
 
+void BFCAllocator::poll_pending(bool wait) {
+  size_t k = 0;
+  for (size_t i = 0; i < pending_.size(); ++i) {
+    Pending& pd = pending_[i];
+    bool done = true;
+    if (kind_ == MemKind::kDevice) {
+      for (hipEvent_t e : pd.evs) {
+        if (wait) {
+          hipEventSynchronize(e);
+        } else if (hipEventQuery(e) != hipSuccess) {
+          (void)hipGetLastError();   // hipErrorNotReady is sticky-free but clear it anyway
+          done = false;
+          break;
+        }
+      }
+    } else {
+      done = wait;   // host-tagged (tests): side-stream uses end at the next clean
+    }
+    if (done) {
+      for (hipEvent_t e : pd.evs) hipEventDestroy(e);
+      free_chunk(pd.c);
+    } else {
+      pending_[k++] = pd;
+    }
+  }
+  pending_.resize(k);
+}
+
 void BFCAllocator::clean_streams() {
   // wait for every stream that owns free chunks to pass "now", then move those
   // chunks to the clean bins (coalescing with clean neighbours)
+  poll_pending(true);
   std::vector<Chunk*> moved;
   for (auto& kv : bins_) {
     if (kv.first == nullptr) continue;
@@ -156,6 +190,7 @@ void BFCAllocator::clean_streams() {
   std::unordered_map<Chunk*, int> mv;
   for (Chunk* c : moved) {
     c->stream = nullptr;
+    c->listed = false;
     mv[c] = 1;
   }
   // one pass per region: re-insert moved chunks in address order so each one
@@ -180,8 +215,7 @@ BFCAllocator::Chunk* BFCAllocator::free_chunk(Chunk* c) {
   c->in_use = false;
   Chunk* p = c->prev;
   if (p && !p->in_use && p->stream == c->stream) {
-    bool listed = bins_[p->stream].b[bin_of(p->size)].count(p) > 0;
-    if (listed) {
+    if (p->listed) {
       erase_free(p);
       p->size += c->size;
       p->next = c->next;
@@ -192,8 +226,7 @@ BFCAllocator::Chunk* BFCAllocator::free_chunk(Chunk* c) {
   }
   Chunk* n = c->next;
   if (n && !n->in_use && n->stream == c->stream) {
-    bool listed = bins_[n->stream].b[bin_of(n->size)].count(n) > 0;
-    if (listed) {
+    if (n->listed) {
       erase_free(n);
       c->size += n->size;
       c->next = n->next;
@@ -209,6 +242,7 @@ void* BFCAllocator::allocate(size_t bytes, hipStream_t stream) {
   std::lock_guard<std::mutex> g(mu_);
   if (!tagged()) stream = nullptr;
   size_t size = round_up(bytes ? bytes : 1);
+  if (!pending_.empty()) poll_pending(false);
   Chunk* c = find_chunk(size, stream);
   if (c == nullptr) {
     clean_streams();
@@ -221,7 +255,7 @@ void* BFCAllocator::allocate(size_t bytes, hipStream_t stream) {
     for (size_t i = 0; i < regions_.size(); ++i) {
       Region& r = regions_[i];
       Chunk* f = r.first;
-      if (f && !f->in_use && f->next == nullptr && f->size == r.size && r.base) {
+      if (f && !f->in_use && f->listed && f->next == nullptr && f->size == r.size && r.base) {
         erase_free(f);
         delete f;
         sub_free(r.base);
@@ -259,7 +293,37 @@ void BFCAllocator::deallocate(void* p, hipStream_t stream) {
   st_.bytes_in_use -= (int64_t)c->size;
   if (tagged() && stream != nullptr) c->stream = stream;
   if (!tagged()) c->stream = nullptr;
+  if (c->uses) {   // side-stream uses: hold the chunk until they pass this point
+    Pending pd{c, {}};
+    if (kind_ == MemKind::kDevice) {
+      for (hipStream_t s : *c->uses) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+          hipEventRecord(e, s);
+          pd.evs.push_back(e);
+        } else {
+          hipStreamSynchronize(s);
+        }
+      }
+    }
+    delete c->uses;
+    c->uses = nullptr;
+    c->in_use = false;
+    pending_.push_back(pd);
+    return;
+  }
   free_chunk(c);
+}
+
+void BFCAllocator::record_stream(void* p, hipStream_t stream) {
+  if (p == nullptr || !tagged()) return;
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = in_use_.find((char*)p);
+  if (it == in_use_.end()) return;
+  Chunk* c = it->second;
+  if (stream == c->stream) return;
+  if (!c->uses) c->uses = new std::vector<hipStream_t>();
+  if (std::find(c->uses->begin(), c->uses->end(), stream) == c->uses->end()) c->uses->push_back(stream);
 }
 
 size_t BFCAllocator::allocation_size(void* p) {
@@ -279,7 +343,7 @@ size_t BFCAllocator::release_free_regions() {
   size_t freed = 0;
   for (auto& r : regions_) {
     Chunk* f = r.first;
-    if (r.base && f && !f->in_use && f->next == nullptr && f->size == r.size) {
+    if (r.base && f && !f->in_use && f->listed && f->next == nullptr && f->size == r.size) {
       erase_free(f);
       delete f;
       sub_free(r.base);
@@ -308,11 +372,13 @@ bool BFCAllocator::check_invariants() {
       if (c->in_use) {
         used += (int64_t)c->size;
         if (!in_use_.count(c->ptr)) return false;
+      } else if (std::any_of(pending_.begin(), pending_.end(), [c](const Pending& pd) { return pd.c == c; })) {
+        if (c->listed) return false;   // held back for a side stream: in no bin yet
       } else {
-        if (!bins_[c->stream].b[bin_of(c->size)].count(c)) return false;
+        if (!c->listed || !bins_[c->stream].b[bin_of(c->size)].count(c)) return false;
         ++nfree;
         // no two adjacent free chunks with compatible streams may remain
-        if (c->next && !c->next->in_use && c->next->stream == c->stream) return false;
+        if (c->next && !c->next->in_use && c->next->listed && c->next->stream == c->stream) return false;
       }
       expect += c->size;
       total += c->size;
@@ -340,6 +406,9 @@ HETU_RT_API void* hetu_bfc_alloc(void* h, int64_t bytes, void* stream) {
 }
 HETU_RT_API void hetu_bfc_free(void* h, void* p, void* stream) {
   ((BFCAllocator*)h)->deallocate(p, (hipStream_t)stream);
+}
+HETU_RT_API void hetu_bfc_record_stream(void* h, void* p, void* stream) {
+  ((BFCAllocator*)h)->record_stream(p, (hipStream_t)stream);
 }
 HETU_RT_API int64_t hetu_bfc_size(void* h, void* p) { return (int64_t)((BFCAllocator*)h)->allocation_size(p); }
 HETU_RT_API int64_t hetu_bfc_release(void* h) { return (int64_t)((BFCAllocator*)h)->release_free_regions(); }
@@ -393,6 +462,11 @@ HETU_RT_API void hetu_torch_free(void* ptr, ssize_t size, int device, hipStream_
   (void)size;
   BFCAllocator* a = dev_alloc(device);
   if (a) a->deallocate(ptr, stream);
+}
+
+HETU_RT_API void hetu_torch_record_stream(int device, void* ptr, hipStream_t stream) {
+  BFCAllocator* a = dev_alloc(device);
+  if (a) a->record_stream(ptr, stream);
 }
 
 HETU_RT_API void hetu_torch_stats(int device, int64_t* out) {

@@ -16,6 +16,8 @@
 // nothing, the allocator first *cleans* the other streams (one event per stream,
 // waited once) -- moving their free chunks to the clean bins -- before it grows
 // a region.  Same-stream reuse is immediate, as with a caching allocator.
+// A chunk also used on side streams (record_stream) is held back when freed until an
+// event recorded on each of those streams at the free has completed.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -51,6 +53,9 @@ class BFCAllocator {
 
   void* allocate(size_t bytes, hipStream_t stream);
   void deallocate(void* p, hipStream_t stream);   // reusable by `stream` at once, by others once clean
+  // p is also used on `stream` (a side stream: comm, PS staging, prefetch): once freed,
+  // the chunk waits for that stream's work queued up to the free before anyone reuses it
+  void record_stream(void* p, hipStream_t stream);
   size_t allocation_size(void* p);
   AllocatorStats stats();
   size_t release_free_regions();                  // return wholly free regions; bytes released
@@ -67,6 +72,12 @@ class BFCAllocator {
     Chunk* prev;   // physical neighbours inside the region
     Chunk* next;
     hipStream_t stream;   // last user (free chunks: owning bin set; nullptr = clean)
+    bool listed;          // in a free bin
+    std::vector<hipStream_t>* uses;   // record_stream: other streams using the chunk
+  };
+  struct Pending {        // freed chunk whose side-stream uses are still in flight
+    Chunk* c;
+    std::vector<hipEvent_t> evs;
   };
   struct BySize {
     bool operator()(const Chunk* a, const Chunk* b) const {
@@ -94,6 +105,8 @@ class BFCAllocator {
   void erase_free(Chunk* c);
   Chunk* free_chunk(Chunk* c);   // returns the (possibly merged) free chunk
   void clean_streams();
+  void poll_pending(bool wait);   // release pending chunks whose side-stream events completed
+  Bins& bins_for(hipStream_t s);
   void* sub_alloc(size_t bytes);
   void sub_free(void* p);
 
@@ -103,6 +116,9 @@ class BFCAllocator {
   size_t next_region_;
   std::mutex mu_;
   std::map<hipStream_t, Bins> bins_;
+  hipStream_t last_stream_ = nullptr;   // bins_ lookup cache (map nodes are stable)
+  Bins* last_bins_ = nullptr;
+  std::vector<Pending> pending_;
   std::unordered_map<char*, Chunk*> in_use_;
   std::vector<Region> regions_;
   AllocatorStats st_;

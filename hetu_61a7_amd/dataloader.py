@@ -127,7 +127,8 @@ class Dataloader(object):
         t = cur[0]
         if len(cur) > 1 and cur[1] is not None:
             torch.cuda.current_stream().wait_event(cur[1])
-            t.record_stream(torch.cuda.current_stream())
+            from .memory_pool import record_stream
+            record_stream(t, torch.cuda.current_stream())
         return t
 
     def get_next_arr(self):

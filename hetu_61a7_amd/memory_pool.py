@@ -45,6 +45,8 @@ def lib():
                                 ('hetu_bfc_destroy', [P], None),
                                 ('hetu_bfc_alloc', [P, I64, P], P),
                                 ('hetu_bfc_free', [P, P, P], None),
+                                ('hetu_bfc_record_stream', [P, P, P], None),
+                                ('hetu_torch_record_stream', [I32, P, P], None),
                                 ('hetu_bfc_size', [P, P], I64),
                                 ('hetu_bfc_release', [P], I64),
                                 ('hetu_bfc_check', [P], I32),
@@ -66,6 +68,11 @@ class BFCAllocator(object):
 
     def free(self, ptr, stream=None):
         lib().hetu_bfc_free(self.h, ptr, stream)
+
+    def record_stream(self, ptr, stream):
+        """ptr is also used on ``stream``: held back from reuse after its free until
+        that stream's work queued before the free has completed"""
+        lib().hetu_bfc_record_stream(self.h, ptr, stream)
 
     def size_of(self, ptr):
         return lib().hetu_bfc_size(self.h, ptr)
@@ -136,6 +143,19 @@ def enable_torch_bfc():
 
 def torch_bfc_enabled():
     return _torch_bfc
+
+
+def record_stream(t, stream):
+    """``t.record_stream(stream)`` for whichever device allocator owns t: the BFC
+    pool's own side-stream hold when it is the process allocator (torch's pluggable
+    allocator interface has no record_stream hook), torch's caching allocator
+    otherwise.  ``stream``: a torch stream or a runtime.DeviceStream."""
+    if _torch_bfc:
+        h = stream.handle if hasattr(stream, 'handle') else stream.cuda_stream
+        lib().hetu_torch_record_stream(t.device.index or 0, t.data_ptr(), h)
+    else:
+        t.record_stream(stream.torch if hasattr(stream, 'torch') and not isinstance(stream, torch.cuda.Stream)
+                        else stream)
 
 
 def device_stats(device=0):

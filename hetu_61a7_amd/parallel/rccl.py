@@ -24,6 +24,7 @@ import os
 from typing import Optional
 
 import torch
+from ..memory_pool import record_stream
 
 _LIB = None
 _NCCL_DT = {torch.float32: 7, torch.float16: 6, torch.bfloat16: 9, torch.int32: 2, torch.int64: 4,
@@ -194,7 +195,7 @@ class NativeComm(object):
         fn(s.cuda_stream)
         for t in tensors:
             if t is not None and t.is_cuda:
-                t.record_stream(s)
+                record_stream(t, s)
         from ..runtime import DeviceEvent
         ev = DeviceEvent(timing=_TIMING)
         ev.record(s)

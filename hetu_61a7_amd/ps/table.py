@@ -18,6 +18,7 @@ import torch
 
 from . import worker as psw
 from .worker import PARAM_DENSE, PARAM_SPARSE, PARAM_CACHE
+from ..memory_pool import record_stream
 
 
 def _pinned(n, dtype=torch.float32):
@@ -79,7 +80,7 @@ def host_ids(t):
         out.copy_(t, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(d2h)
-    t.record_stream(d2h)
+    record_stream(t, d2h)
     ev.synchronize()
     return out.long()
 
@@ -223,7 +224,7 @@ class PSTable(object):
                 out = dest.to(self.device, non_blocking=True)
                 stage.guard(h2d)
             cur.wait_stream(h2d)
-            out.record_stream(cur)
+            record_stream(out, cur)
             if out_dtype is not None and out_dtype != out.dtype:
                 out = out.to(out_dtype)
         else:
@@ -245,7 +246,7 @@ class PSTable(object):
             with torch.cuda.stream(d2h):
                 host.copy_(scaled, non_blocking=True)
                 self.grad_stage.guard(d2h)
-            scaled.record_stream(d2h)
+            record_stream(scaled, d2h)
         else:
             host.copy_(scaled)
         self.pending_push = (ids, host)

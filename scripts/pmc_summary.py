@@ -30,13 +30,21 @@ def family(name):
     return n[:90]
 
 
+LAST = 0   # --last N: only the N most recent dispatches of each pass (steady state, no autotune)
+
+
 def load(d):
     """-> ({family: {counter: sum}}, {family: n_dispatches}, {family: summed dispatch ns})"""
     files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     seen = {}
-    for f in files:
-        for r in csv.DictReader(open(f)):
+    rows = [r for f in files for r in csv.DictReader(open(f))]
+    if LAST:
+        ids = sorted({int(r['Dispatch_Id']) for r in rows})[-LAST:]
+        keep = set(ids)
+        rows = [r for r in rows if int(r['Dispatch_Id']) in keep]
+    for r in rows:
+        if True:
             k = family(r['Kernel_Name'])
             agg[k][r['Counter_Name']] += float(r['Counter_Value'])
             seen[r['Dispatch_Id']] = (k, int(r['End_Timestamp']) - int(r['Start_Timestamp']))
@@ -79,4 +87,8 @@ def main(dirs):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1:])
+    a = sys.argv[1:]
+    if a and a[0] == '--last':
+        LAST = int(a[1])
+        a = a[2:]
+    main(a)

@@ -57,6 +57,29 @@ def test_stream_tagged_reuse():
     assert a.check()
 
 
+def test_record_stream_holds_chunk_until_clean():
+    """A chunk recorded on a side stream is not reused when freed -- not even by its
+    own stream -- until that side stream's work up to the free has passed (host-tagged
+    pools model that point as the next clean)."""
+    a = MP.BFCAllocator(MP.HOST_TAGGED, 0, 0, 1 << 20)
+    s1, side = 0x1000, 0x3000
+    p = a.alloc(4096, s1)
+    a.record_stream(p, side)
+    a.free(p, s1)
+    assert a.check()
+    q = a.alloc(4096, s1)
+    assert q != p                                      # held back for the side stream
+    big = a.alloc((1 << 20) - 16384, s1)               # forces a clean: the hold is released
+    assert big is not None
+    a.free(q, s1)
+    a.free(big, s1)
+    assert a.check() and a.stats()['bytes_in_use'] == 0
+    r = a.alloc(4096, s1)
+    a.record_stream(r, s1)                             # own stream: no hold
+    a.free(r, s1)
+    assert a.alloc(4096, s1) == r
+
+
 def test_random_stress_invariants():
     rng = random.Random(0)
     a = MP.BFCAllocator(MP.HOST_TAGGED, 0, 0, 1 << 20)
@@ -69,6 +92,8 @@ def test_random_stress_invariants():
             s = rng.choice([0, 0x10, 0x20])
             p = a.alloc(rng.choice([1, 100, 256, 777, 4096, 65536, 300000]), s or None)
             assert p
+            if rng.random() < 0.2:
+                a.record_stream(p, rng.choice([0x10, 0x20, 0x30]))
             live.append((p, s or None))
         if i % 250 == 0:
             assert a.check()

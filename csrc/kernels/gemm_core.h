@@ -704,8 +704,8 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
   constexpr bool DB = ST >= 2;
   constexpr int TBN = 32 * WN;                 // block tile columns
   constexpr int TPR = TBN / 8;                 // epilogue threads per row (8 columns each)
-  constexpr int RPP = NT / TPR;                // epilogue rows per pass
-  constexpr int NPASS = 64 / RPP;              // passes per 64-row half
+  constexpr int RPP = NT / TPR;                // epilogue rows per pass (21 for the 96-wide tile)
+  constexpr int NPASS = (64 + RPP - 1) / RPP;  // passes per 64-row half
   __shared__ __attribute__((aligned(16))) char smem_raw[DB ? 4 * TILE_BYTES : 64 * (BN + 4) * 4];
   constexpr int buf_stride = DB ? 2 * TILE_BYTES : 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -735,6 +735,7 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
   const int kt1 = min(kt0 + ktps, nkt);
 
   const int ec = (tid % TPR) * 8;
+  const bool erow = tid < RPP * TPR;           // threads past the last full row pass idle
   EpiOut eo;
   epi_init(ep, eo, batch, (int64_t)tn * TBN + ec, N);   // bias columns in flight during the K loop
 
@@ -798,8 +799,9 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
   const bool use_pre = ST == 2 && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec;
   const int64_t pre_n = (int64_t)tn * TBN + ec;
   auto pre_load = [&](int h, int pss) {
-    const int64_t m = (int64_t)tm * BM + h * 64 + pss * RPP + tid / TPR;
-    cpre[pss] = (m < Mb && pre_n + 7 < N)
+    const int rr = pss * RPP + tid / TPR;
+    const int64_t m = (int64_t)tm * BM + h * 64 + rr;
+    cpre[pss] = (erow && rr < 64 && m < Mb && pre_n + 7 < N)
                     ? *reinterpret_cast<const uint4*>((const bf16*)eo.Cinb + la.out_row(m) * ep.ldcin + pre_n)
                     : make_uint4(0, 0, 0, 0);
   };
@@ -860,7 +862,7 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
         const int rr = pss * RPP + tid / TPR;
         const int64_t m = (int64_t)tm * BM + half * 64 + rr;
         const int64_t n = (int64_t)tn * TBN + ec;
-        if (m < Mb && n < N) {
+        if (erow && rr < 64 && m < Mb && n < N) {
           float v[8];
           v4f a0 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec);
           v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec + 4);
@@ -1265,7 +1267,7 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
 
 // tile: 0 = 128x128 (4 waves, 2 LDS stages, 2 blocks per CU), 1 = 256x256 (8 waves, 1 block
 // per CU), 2 = 128x64 (4 waves of 64x32; 64-channel convolutions), 3 = 128x128 single LDS
-// stage at 4 blocks per CU (short-K, memory-bound shapes).
+// stage at 4 blocks per CU (short-K, memory-bound shapes), 5 = 128x96 (4 waves of 64x48).
 template <class LA, class LB, int WN>
 static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
                     int batch, int splitk, hipStream_t st, bool single_stage = false) {
@@ -1302,6 +1304,13 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
   if (tile == 1) return launch_big(la, lb, ep, M, N, K, batch, splitk, st);
   if (tile == 2) return launch_t<LA, LB, 2>(la, lb, ep, M, N, K, batch, splitk, st);
   if (tile == 3) return launch_t<LA, LB, 4>(la, lb, ep, M, N, K, batch, splitk, st, true);
+  if (tile == 5) {
+    // 128x96: N = 768 products fill 2 tiles per CU in one round (8192x768: 512 tiles) where
+    // the 128-wide tile leaves half the CUs one block short (384).  The 12-thread row
+    // groups do not fold by lane shuffles: no fused column statistics on this tile.
+    if (ep.colstats) return (int)hipErrorInvalidValue;
+    return launch_t<LA, LB, 3>(la, lb, ep, M, N, K, batch, splitk, st);
+  }
   return launch_t<LA, LB, 4>(la, lb, ep, M, N, K, batch, splitk, st);
 }
 

@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 
 namespace hetu {
 
@@ -171,6 +172,10 @@ void BFCAllocator::clean_streams() {
     for (auto& bin : kv.second.b) any |= !bin.empty();
     if (!any) continue;
     if (kind_ == MemKind::kDevice) {
+      // a stream being captured into a graph cannot be waited on: its chunks stay
+      // tagged (they are reused by that stream itself, in capture order)
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(kv.first, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) continue;
       hipEvent_t ev;
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
         hipEventRecord(ev, kv.first);
@@ -293,6 +298,12 @@ void BFCAllocator::deallocate(void* p, hipStream_t stream) {
   st_.bytes_in_use -= (int64_t)c->size;
   if (tagged() && stream != nullptr) c->stream = stream;
   if (!tagged()) c->stream = nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (c->uses && kind_ == MemKind::kDevice && stream != nullptr &&
+      hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    delete c->uses;   // inside a capture the graph's own stream order covers the side uses
+    c->uses = nullptr;
+  }
   if (c->uses) {   // side-stream uses: hold the chunk until they pass this point
     Pending pd{c, {}};
     if (kind_ == MemKind::kDevice) {
@@ -453,19 +464,85 @@ static BFCAllocator* dev_alloc(int device) {
   return g_dev[device];
 }
 
-HETU_RT_API void* hetu_torch_alloc(ssize_t size, int device, hipStream_t stream) {
+// Private pools for hipGraph capture (the native counterpart of torch's graph memory
+// pools): between hetu_torch_pool_begin and _end every allocation on the device comes
+// from a pool of its own, so the captured step's buffers are never handed to code
+// outside the graph; the graph replays them in capture order.  The pool lives until
+// hetu_torch_pool_release (graph destroyed).
+static std::map<int64_t, BFCAllocator*> g_pools;
+static std::atomic<int> g_npools{0};
+static BFCAllocator* g_active_pool[64];
+static int64_t g_pool_seq = 0;
+
+HETU_RT_API int64_t hetu_torch_pool_begin(int device) {
+  if (device < 0 || device >= 64) return -1;
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  const char* reg = getenv("HETU_BFC_POOL_REGION_MB");
+  size_t first = reg ? (size_t)atoll(reg) << 20 : (size_t)64 << 20;
+  BFCAllocator* p = new BFCAllocator(MemKind::kDevice, device, 0, first);
+  const int64_t id = ++g_pool_seq;
+  g_pools[id] = p;
+  g_npools.fetch_add(1);
+  g_active_pool[device] = p;
+  return id;
+}
+
+HETU_RT_API void hetu_torch_pool_end(int device) {
+  if (device < 0 || device >= 64) return;
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  g_active_pool[device] = nullptr;
+}
+
+HETU_RT_API void hetu_torch_pool_stats(int64_t id, int64_t* out) {
+  BFCAllocator* p = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    auto it = g_pools.find(id);
+    if (it != g_pools.end()) p = it->second;
+  }
+  if (p) hetu_bfc_stats(p, out);
+}
+
+// drop a pool: its memory goes back to the driver (the graph using it must be destroyed;
+// chunks still handed out -- static outputs of that graph -- are released with it)
+HETU_RT_API void hetu_torch_pool_release(int64_t id) {
+  BFCAllocator* p = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    auto it = g_pools.find(id);
+    if (it == g_pools.end()) return;
+    p = it->second;
+    g_pools.erase(it);
+    g_npools.fetch_sub(1);
+    for (auto& a : g_active_pool)
+      if (a == p) a = nullptr;
+  }
+  hipDeviceSynchronize();
+  delete p;
+}
+
+static BFCAllocator* owner_of(int device, void* ptr) {
   BFCAllocator* a = dev_alloc(device);
+  if (a && a->allocation_size(ptr)) return a;
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  for (auto& kv : g_pools)
+    if (kv.second->allocation_size(ptr)) return kv.second;
+  return nullptr;
+}
+
+HETU_RT_API void* hetu_torch_alloc(ssize_t size, int device, hipStream_t stream) {
+  BFCAllocator* a = (device >= 0 && device < 64 && g_active_pool[device]) ? g_active_pool[device] : dev_alloc(device);
   return a ? a->allocate((size_t)size, stream) : nullptr;
 }
 
 HETU_RT_API void hetu_torch_free(void* ptr, ssize_t size, int device, hipStream_t stream) {
   (void)size;
-  BFCAllocator* a = dev_alloc(device);
+  BFCAllocator* a = g_npools.load() == 0 ? dev_alloc(device) : owner_of(device, ptr);
   if (a) a->deallocate(ptr, stream);
 }
 
 HETU_RT_API void hetu_torch_record_stream(int device, void* ptr, hipStream_t stream) {
-  BFCAllocator* a = dev_alloc(device);
+  BFCAllocator* a = g_npools.load() == 0 ? dev_alloc(device) : owner_of(device, ptr);
   if (a) a->record_stream(ptr, stream);
 }
 

@@ -77,3 +77,41 @@ HETU_RT_API int hetu_device_sync(int device) {
   return e != hipSuccess ? (int)e : (int)hipDeviceSynchronize();
 }
 HETU_RT_API const char* hetu_error_string(int e) { return hipGetErrorString((hipError_t)e); }
+
+// ---- stream capture into a HIP graph (the executor's replayed steady-state step) -------
+// mode: 0 global, 1 thread-local, 2 relaxed (the BFC pool may grow a region mid-capture)
+HETU_RT_API int hetu_stream_begin_capture(void* s, int mode) {
+  static const hipStreamCaptureMode m[3] = {hipStreamCaptureModeGlobal, hipStreamCaptureModeThreadLocal,
+                                            hipStreamCaptureModeRelaxed};
+  if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  return (int)hipStreamBeginCapture((hipStream_t)s, m[mode]);
+}
+HETU_RT_API int hetu_stream_end_capture(void* s, void** graph) {
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture((hipStream_t)s, &g);
+  *graph = (void*)g;
+  return (int)e;
+}
+HETU_RT_API int hetu_stream_is_capturing(void* s, int* status) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing((hipStream_t)s, &st);
+  *status = (int)st;
+  return (int)e;
+}
+HETU_RT_API int hetu_graph_instantiate(void* graph, void** exec) {
+  hipGraphExec_t x = nullptr;
+  hipError_t e = hipGraphInstantiate(&x, (hipGraph_t)graph, nullptr, nullptr, 0);
+  *exec = (void*)x;
+  return (int)e;
+}
+HETU_RT_API int hetu_graph_nodes(void* graph, int64_t* n) {
+  size_t c = 0;
+  hipError_t e = hipGraphGetNodes((hipGraph_t)graph, nullptr, &c);
+  *n = (int64_t)c;
+  return (int)e;
+}
+HETU_RT_API int hetu_graph_launch(void* exec, void* stream) {
+  return (int)hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)stream);
+}
+HETU_RT_API int hetu_graph_destroy(void* graph) { return (int)hipGraphDestroy((hipGraph_t)graph); }
+HETU_RT_API int hetu_graph_exec_destroy(void* exec) { return (int)hipGraphExecDestroy((hipGraphExec_t)exec); }

@@ -53,6 +53,9 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
         if a.dtype == torch.bfloat16 and _tr(a, ta).shape[-1] <= 2048:   # short K: the 4-blocks-per-CU tile
             cands['hip_lo'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=3)
         A2, B2 = _tr(a, ta), _tr(b, tb)
+        if a.dtype == torch.bfloat16 and B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
+            # 128x96 tile: N = 768 products fill the CUs in one round (512 tiles at M 8192)
+            cands['hip96'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=5)
         if A2.dim() == 2 and B2.dim() == 2 and A2.shape[0] * B2.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
         cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
@@ -267,6 +270,8 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=1)
         if A.shape[1] <= 2048:
             cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=3)
+        if B.shape[1] % 96 == 0 and A.shape[0] >= 1024:
+            cands['hip96'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=5)
         if A.shape[0] * B.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, cin=acc, beta=1.0)
         ch = choose(key, cands, _MFMA)

@@ -19,7 +19,7 @@ _ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I
          F32, F32, I32, I32, I32, I32, I32, I32, P, I32, P]
 # tile configurations of the kernel (gemm.hip launch): 0 = 128x128 tile, 4 waves;
 # 1 = 256x256 tile, 8 waves, phase-interleaved K loop (one block per CU)
-TILES = (0, 1, 2, 3)   # 128x128, 256x256, 128x64, 128x128 single-stage (4 blocks / CU)
+TILES = (0, 1, 2, 3, 5)   # 128x128, 256x256, 128x64, 128x128 single-stage (4 blocks / CU), 128x96
 MODE = os.environ.get('HETU_GEMM', 'hip')
 
 

@@ -51,7 +51,11 @@ def lib():
                                 ('hetu_bfc_release', [P], I64),
                                 ('hetu_bfc_check', [P], I32),
                                 ('hetu_bfc_stats', [P, P], None),
-                                ('hetu_torch_stats', [I32, P], None)):
+                                ('hetu_torch_stats', [I32, P], None),
+                                ('hetu_torch_pool_begin', [I32], I64),
+                                ('hetu_torch_pool_end', [I32], None),
+                                ('hetu_torch_pool_stats', [I64, P], None),
+                                ('hetu_torch_pool_release', [I64], None)):
             f = getattr(L, name)
             f.argtypes, f.restype = args, res
         _lib = L
@@ -162,3 +166,33 @@ def device_stats(device=0):
     out = (ctypes.c_int64 * 8)()
     lib().hetu_torch_stats(int(device), out)
     return dict(zip(_STAT_KEYS, list(out)))
+
+
+class capture_pool(object):
+    """``with capture_pool(device) as pool:`` -- every device allocation in the block
+    comes from a private BFC pool (the native graph-capture pool: a captured step's
+    buffers are replayed by the graph and must never be handed to other code).
+    ``pool.stats()`` mirrors device_stats; ``pool.release()`` returns its memory
+    (only once the graph that uses it is gone)."""
+
+    def __init__(self, device=0):
+        self.device = int(device)
+        self.id = None
+
+    def __enter__(self):
+        self.id = lib().hetu_torch_pool_begin(self.device)
+        return self
+
+    def __exit__(self, *exc):
+        lib().hetu_torch_pool_end(self.device)
+        return False
+
+    def stats(self):
+        out = (ctypes.c_int64 * 8)()
+        lib().hetu_torch_pool_stats(self.id, out)
+        return dict(zip(_STAT_KEYS, list(out)))
+
+    def release(self):
+        if self.id is not None:
+            lib().hetu_torch_pool_release(self.id)
+            self.id = None

@@ -34,7 +34,10 @@ def lib():
                            ('hetu_event_elapsed', [P, P, ctypes.POINTER(ctypes.c_float)]),
                            ('hetu_stream_wait_event', [P, P]), ('hetu_memcpy_async', [P, P, I64, I, P]),
                            ('hetu_memcpy_peer_async', [P, I, P, I, I64, P]), ('hetu_memset_async', [P, I, I64, P]),
-                           ('hetu_device_sync', [I])):
+                           ('hetu_device_sync', [I]), ('hetu_stream_begin_capture', [P, I]),
+                           ('hetu_stream_end_capture', [P, PP]), ('hetu_graph_instantiate', [P, PP]),
+                           ('hetu_graph_launch', [P, P]), ('hetu_graph_destroy', [P]), ('hetu_graph_exec_destroy', [P]),
+                           ('hetu_graph_nodes', [P, ctypes.POINTER(ctypes.c_int64)])):
             f = getattr(L, name)
             f.argtypes, f.restype = args, I
         L.hetu_error_string.argtypes, L.hetu_error_string.restype = [I], ctypes.c_char_p
@@ -143,3 +146,46 @@ def memcpy_async(dst, src, nbytes, kind, stream=None):
     """kind: 'h2h' | 'h2d' | 'd2h' | 'd2d' on a framework or torch stream"""
     k = {'h2h': 0, 'h2d': 1, 'd2h': 2, 'd2d': 3}[kind]
     _check(lib().hetu_memcpy_async(dst, src, int(nbytes), k, _handle(stream)), 'memcpy')
+
+
+class Graph(object):
+    """A HIP graph captured from a framework stream (``hipStreamBeginCapture`` ..
+    ``hipStreamEndCapture``, instantiated once, replayed with ``hipGraphLaunch``):
+    the executor's replayed steady-state step when the BFC pool is the device
+    allocator (its private capture pool keeps the step's buffers out of everyone
+    else's reach, memory_pool.capture_pool)."""
+
+    RELAXED = 2
+
+    def __init__(self):
+        self.graph = None
+        self.exec = None
+
+    def begin(self, stream):
+        _check(lib().hetu_stream_begin_capture(_handle(stream), self.RELAXED), 'stream begin capture')
+
+    def end(self, stream):
+        g = ctypes.c_void_p()
+        _check(lib().hetu_stream_end_capture(_handle(stream), ctypes.byref(g)), 'stream end capture')
+        self.graph = g.value
+        x = ctypes.c_void_p()
+        _check(lib().hetu_graph_instantiate(self.graph, ctypes.byref(x)), 'graph instantiate')
+        self.exec = x.value
+
+    def nodes(self):
+        n = ctypes.c_int64()
+        _check(lib().hetu_graph_nodes(self.graph, ctypes.byref(n)), 'graph nodes')
+        return int(n.value)
+
+    def replay(self, stream=None):
+        _check(lib().hetu_graph_launch(self.exec, _handle(stream)), 'graph launch')
+
+    def __del__(self):
+        try:
+            if _lib is not None:
+                if getattr(self, 'exec', None):
+                    lib().hetu_graph_exec_destroy(self.exec)
+                if getattr(self, 'graph', None):
+                    lib().hetu_graph_destroy(self.graph)
+        except Exception:
+            pass

@@ -61,9 +61,13 @@ class GraphRunner(object):
             base = {p: sub.config.compute_value(p) for p in sub.param_nodes}
             base.update(self.static_in)
             torch.cuda.synchronize()
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self.static_vals = sub._run_eager(None, vals=dict(base))
+            from .. import memory_pool as MP
+            if MP.torch_bfc_enabled():
+                self._capture_native(sub, base)
+            else:
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph):
+                    self.static_vals = sub._run_eager(None, vals=dict(base))
             for op in sub.opt_ops:
                 op.step -= 1  # the capture itself executes nothing
         for n, v in new_in.items():
@@ -72,3 +76,33 @@ class GraphRunner(object):
         for op in sub.opt_ops:
             op.step += 1
         return sub._collect(self.static_vals, convert)
+
+    def _capture_native(self, sub, base):
+        """Capture on a framework stream into a native HIP graph, every allocation of
+        the captured step carved from a private BFC pool (torch's graph pools need its
+        caching allocator, which the BFC pool replaces)."""
+        from .. import memory_pool as MP
+        from .. import runtime as RT
+        dev = sub.config.device.index or 0
+        cap = RT.DeviceStream(dev)
+        cap.wait_stream(torch.cuda.current_stream())
+        g = RT.Graph()
+        self.pool = MP.capture_pool(dev)
+        with self.pool, torch.cuda.stream(cap.torch):
+            g.begin(cap)
+            try:
+                self.static_vals = sub._run_eager(None, vals=dict(base))
+            finally:
+                g.end(cap)
+        self.capture_stream = cap
+        self.graph = _NativeReplay(g)
+
+
+class _NativeReplay(object):
+    """replay() on torch's current stream, like torch.cuda.CUDAGraph"""
+
+    def __init__(self, g):
+        self.g = g
+
+    def replay(self):
+        self.g.replay(torch.cuda.current_stream())

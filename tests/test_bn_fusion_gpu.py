@@ -10,6 +10,7 @@ Each kernel is checked against a plain fp32 torch reduction of the same stored v
 """
 import os
 
+import numpy as np
 import pytest
 import torch
 
@@ -147,8 +148,8 @@ def _resnet_steps(fuse_bwd, fuse_stats, steps=3):
         Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
         out = []
         for _ in range(steps):
-            lv = ex.run('train', feed_dict={x: X, y_: Y})[0]
-            out.append(float(lv.asnumpy().mean() if hasattr(lv, 'asnumpy') else lv.float().mean()))
+            lv = ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]
+            out.append(float(np.mean(lv)))
         fused = sum(1 for n in ex.subexecutor['train'].computing_nodes if getattr(n, 'bn_fused', None) is not None)
         return out, fused
     finally:

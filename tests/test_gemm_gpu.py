@@ -123,7 +123,7 @@ def test_conv_wgrad_64_channel_tiles(shape, tile, accumulate):
     assert _rel(got, wf.grad) < (1e-4 if accumulate else 2e-5)
 
 
-@pytest.mark.parametrize('tile', G.TILES)
+@pytest.mark.parametrize('tile', [t for t in G.TILES if t != 5])   # 128x96: no fused statistics
 @pytest.mark.parametrize('shape', [(4, 64, 14, 64, 1, 1, 0), (2, 64, 13, 200, 3, 2, 1), (3, 128, 9, 256, 3, 1, 1)])
 def test_conv_fused_bn_statistics(shape, tile):
     """Per-channel sum / sum of squares of the stored (bf16) conv output, reduced in

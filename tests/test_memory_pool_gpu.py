@@ -50,6 +50,79 @@ def test_torch_bfc_allocator_training_matches_default():
     assert st['peak_bytes_in_use'] >= st['bytes_in_use'] > 0
 
 
+_GRAPH_SCRIPT = r'''
+import json
+import numpy as np, torch
+import hetu_61a7_amd as ht
+from hetu_61a7_amd import memory_pool as MP
+from hetu_61a7_amd.models import mlp
+from hetu_61a7_amd.ops import node as _node
+rng = np.random.RandomState(2)
+X = rng.randn(64, 3072).astype(np.float32)
+Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 64)]
+out = []
+for g in (False, True):
+    _node.G_NODE_ID = 0
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    loss, _ = mlp(x, y_)
+    train = ht.optim.AdamOptimizer(1e-3).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, use_hipgraph=g)
+    out.append([float(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]) for _ in range(8)])
+    if g:
+        gr = ex.subexecutor['train'].graph
+        native = type(gr.graph).__name__ == '_NativeReplay'
+        pool = gr.pool.stats() if native else {}
+print(json.dumps({'eager': out[0], 'graph': out[1], 'native': native, 'pool': pool,
+                  'torch_reserved': torch.cuda.memory_reserved(), 'bfc': MP.torch_bfc_enabled()}))
+'''
+
+
+def test_native_hipgraph_capture_with_bfc_pool():
+    """With the BFC pool as the device allocator, hipGraph capture runs natively
+    (hipStreamBeginCapture on a framework stream, buffers from a private BFC pool) and
+    replays the same losses as eager; torch's caching allocator reserves nothing."""
+    env = dict(os.environ, PYTHONPATH=ROOT, HETU_ALLOCATOR='bfc', HETU_BFC_REGION_MB='256')
+    r = subprocess.run([sys.executable, '-c', _GRAPH_SCRIPT], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d['bfc'] and d['native'], d
+    np.testing.assert_allclose(d['eager'], d['graph'], rtol=1e-4, atol=1e-5)
+    assert d['torch_reserved'] == 0
+    assert d['pool']['num_allocs'] > 0 and d['pool']['bytes_in_use'] > 0
+
+
+_RESNET_SCRIPT = r'''
+import json, torch
+import hetu_61a7_amd as ht
+from hetu_61a7_amd import memory_pool as MP
+from hetu_61a7_amd.models import resnet50_imagenet
+B = 4
+x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+loss, _ = resnet50_imagenet(x, y_, 1000)
+train = ht.optim.MomentumOptimizer(learning_rate=0.05, momentum=0.9).minimize(loss)
+ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3)
+g = torch.Generator(device='cuda'); g.manual_seed(0)
+X = torch.randn((B, 3, 224, 224), device='cuda', generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
+import numpy as np
+ls = [float(np.mean(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0])) for _ in range(3)]
+torch.cuda.synchronize()
+print(json.dumps({'losses': ls, 'torch_reserved': torch.cuda.memory_reserved(), 'stats': MP.device_stats(0),
+                  'bfc': MP.torch_bfc_enabled()}))
+'''
+
+
+def test_resnet50_step_allocates_only_from_the_bfc_pool():
+    env = dict(os.environ, PYTHONPATH=ROOT, HETU_ALLOCATOR='bfc')
+    r = subprocess.run([sys.executable, '-c', _RESNET_SCRIPT], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d['bfc'] and d['torch_reserved'] == 0, d
+    assert d['stats']['peak_bytes_in_use'] > (100 << 20) and all(v == v for v in d['losses'])
+
+
 def test_pinned_pool_tensor_is_pinned_and_copies():
     from hetu_61a7_amd.ndarray import pinned_empty
     t = pinned_empty((1024, 256), torch.float32)

@@ -6,7 +6,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
 S=scripts/gpu_step.sh
-bash $S tests ${TESTS_TIMEOUT:-500} python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+bash $S tests ${TESTS_TIMEOUT:-500} python -u -m pytest -x -q --timeout ${PYTEST_TIMEOUT:-120} --timeout-method thread -m gpu \
   ${TESTS:-tests/test_bn_fusion_gpu.py tests/test_runtime_gpu.py tests/test_gemm_gpu.py tests/test_stem_gpu.py tests/test_native_dispatch_gpu.py tests/test_rccl_gpu.py} || exit $?
 grep -q " passed" gpurun_out/tests.log && ! grep -q -E "[0-9]+ failed|[0-9]+ error" gpurun_out/tests.log || { echo "TESTS FAILED"; exit 1; }
 for v in ${VARIANTS:-"1 1" "1 0" "0 0"}; do

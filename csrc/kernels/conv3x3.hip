@@ -32,7 +32,13 @@ namespace {
 struct BnB {
   const bf16* x;
   const uint8_t* mask;
+  int store;   // store the masked gradient dx' (mask applied before the store)
 };
+
+// mask bits of 4 channels at element offset e (co % 4 == 0), all-ones without a mask
+__device__ __forceinline__ unsigned mask4(const BnB& bn, int64_t e) {
+  return (bn.x && bn.mask) ? ((unsigned)bn.mask[e >> 3] >> (e & 7)) & 0xfu : 0xfu;
+}
 
 // 4 stored channels at element offset e (co % 4 == 0) into the running sums s[0..3], q[0..3]
 __device__ __forceinline__ void stats4(const BnB& bn, int64_t e, const unsigned short (&h)[4], float* s, float* q) {
@@ -40,7 +46,7 @@ __device__ __forceinline__ void stats4(const BnB& bn, int64_t e, const unsigned 
     const uint2 a = *reinterpret_cast<const uint2*>(bn.x + e);
     const float xv[4] = {bf16_bits_to_f((unsigned short)(a.x & 0xffffu)), bf16_bits_to_f((unsigned short)(a.x >> 16)),
                          bf16_bits_to_f((unsigned short)(a.y & 0xffffu)), bf16_bits_to_f((unsigned short)(a.y >> 16))};
-    const unsigned mk = bn.mask ? (unsigned)bn.mask[e >> 3] >> (e & 7) : 0xfu;
+    const unsigned mk = mask4(bn, e);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float g = (mk >> i) & 1u ? bf16_bits_to_f(h[i]) : 0.f;
@@ -201,6 +207,11 @@ __global__ __launch_bounds__((Geo<WD, TH>::NT), 1) void conv3x3_c64_k(const bf16
             v[2] += bf16_bits_to_f((unsigned short)(a.y & 0xffffu));
             v[3] += bf16_bits_to_f((unsigned short)(a.y >> 16));
           }
+        }
+        if (bn.store) {
+          const unsigned mk = mask4(bn, pix * CH + co);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (mk >> i) & 1u ? v[i] : 0.f;
         }
         unsigned short h[4];
 #pragma unroll
@@ -546,6 +557,11 @@ __global__ __launch_bounds__(256, 4) void conv3x3_wide_k(const bf16* __restrict_
           v[3] += bf16_bits_to_f((unsigned short)(a.y >> 16));
         }
       }
+      if (bn.store) {
+        const unsigned mk = mask4(bn, opx[b] * K + co);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (mk >> i) & 1u ? v[i] : 0.f;
+      }
       unsigned short h[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) h[i] = f_to_bf16_bits(v[i]);
@@ -767,17 +783,20 @@ HETU_API int hetu_conv3x3_c64_fwd(const void* x, const void* w, void* y, float* 
 
 // dx[N,H,W,64] = conv3x3^T(dy, w) (+ acc: bf16 or fp32 [N,H,W,64]); wt: 64*9*64 bf16 scratch.
 // bnsums (nullable, 128 fp32 pre-zeroed) += sum(dx') / sum(dx' * bnx) per channel, dx' = dx
-// masked by bnmask (see BnB): the reduction of the backward of the BN that produced x
+// masked by bnmask (see BnB): the reduction of the backward of the BN that produced x;
+// bnstore: dx is stored masked
 HETU_API int hetu_conv3x3_c64_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
                                     int N, int H, int W, float* bnsums, const void* bnx, const uint8_t* bnmask,
-                                    hipStream_t st) {
+                                    int bnstore, hipStream_t st) {
   if ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc) | ((uintptr_t)bnx)) & 15)
     return (int)hipErrorInvalidValue;
   if (bnsums && !bnx) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(flip_bank_k, dim3((CH * 9 * CH + 255) / 256), dim3(256), 0, st, (const bf16*)w, (bf16*)wt);
   HETU_LAUNCH_CHECK();
   return dispatch_c64((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, bnsums,
-                      BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr}, N, H, W, st);
+                      BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr,
+                          (bnsums && bnmask && bnstore) ? 1 : 0},
+                      N, H, W, st);
 }
 
 // slab floats hetu_conv3x3_c64_wgrad needs for a batch of N images
@@ -809,10 +828,10 @@ HETU_API int hetu_conv3x3_wide_fwd(const void* x, const void* w, void* y, float*
 }
 
 // dx[N,H,W,C] = conv3x3^T(dy[N,H,W,K], w) (+ acc), K % 64 == 0, C % 128 == 0; wt: C*9*K bf16;
-// bnsums / bnx / bnmask as hetu_conv3x3_c64_dgrad (2*C floats)
+// bnsums / bnx / bnmask / bnstore as hetu_conv3x3_c64_dgrad (2*C floats)
 HETU_API int hetu_conv3x3_wide_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
                                      int N, int H, int W, int C, int K, float* bnsums, const void* bnx,
-                                     const uint8_t* bnmask, hipStream_t st) {
+                                     const uint8_t* bnmask, int bnstore, hipStream_t st) {
   if (!wide_ok(K, C, H, W) ||
       ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc) | ((uintptr_t)bnx)) & 15))
     return (int)hipErrorInvalidValue;
@@ -822,7 +841,9 @@ HETU_API int hetu_conv3x3_wide_dgrad(const void* dy, const void* w, void* wt, vo
                      C, K);
   HETU_LAUNCH_CHECK();
   return dispatch_wide((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, bnsums,
-                       BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr}, N, H, W, K, C, st);
+                       BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr,
+                           (bnsums && bnmask && bnstore) ? 1 : 0},
+                       N, H, W, K, C, st);
 }
 
 HETU_API int hetu_conv3x3_wide_wgrad_supported(int C, int K, int H, int W) { return wide_wgrad_ok(C, K, H, W); }

@@ -494,6 +494,8 @@ struct Epi {
   // BN input (bnx, C's layout) -- the BN backward's reduction pass, fused here
   const bf16* bnx;
   const uint8_t* bnmask;
+  int bnstore;    // store dy' (dy masked by bnmask) instead of dy: the BN backward and the
+                  // residual branch then read the masked gradient as it is
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -632,6 +634,11 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
     for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
   }
   const int64_t off = orow * ep.ldc + n;
+  const unsigned bnmk = (ep.colstats && ep.bnx && ep.bnmask) ? (unsigned)ep.bnmask[off >> 3] : 0xffu;
+  if (ep.bnstore) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = (bnmk >> t) & 1u ? v[t] : 0.f;
+  }
   if (ep.out_f32) {
     float* Cf = (float*)o.Cb + off;
     if (o.cvec && full) {
@@ -663,10 +670,9 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
       for (int t = 0; t < 8; ++t) xv[t] = n + t < N ? to_f(ep.bnx[off + t]) : 0.f;
     }
-    const unsigned mk = ep.bnmask ? (unsigned)ep.bnmask[off >> 3] : 0xffu;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const float g = (mk >> t) & 1u ? bf16_bits_to_f(f_to_bf16_bits(v[t])) : 0.f;
+      const float g = (bnmk >> t) & 1u ? bf16_bits_to_f(f_to_bf16_bits(v[t])) : 0.f;
       cs[t] += g;
       cq[t] += g * xv[t];
     }

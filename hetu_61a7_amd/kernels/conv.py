@@ -300,15 +300,18 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     (x: that BN's input, mask: its ReLU keep-bits or None); sums ([2C] fp32, zero)
     receive sum(dx') and sum(dx' * x), the BN backward's reduction -- in the data
     gradient's epilogue on the hand-written kernels, as a pass of its own after a
-    library kernel -- and the result carries them as ``hetu_bn_bsums``.  bf16 on the
-    GPU only (otherwise ignored)."""
+    library kernel -- and the result carries them as ``hetu_bn_bsums``.  With a mask the
+    hand-written kernels store dx' (masked) and flag the result ``hetu_bn_masked``: the
+    BN backward then reads no mask, and dx' itself is the residual-branch gradient.
+    bf16 on the GPU only (otherwise ignored)."""
     if bn is not None:
         if not (g.is_cuda and g.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and
                 (acc is None or acc.dtype == torch.bfloat16) and bn[1].dtype == torch.bfloat16 and
                 bn[1].is_contiguous(memory_format=CL) and x_shape[1] % 8 == 0 and MODE != 'vendor'):
             return conv2d_backward_data(g, w, x_shape, stride, padding, acc, acc_inplace)
-        r = _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn)
+        r, masked = _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn)
         r.hetu_bn_bsums = bn[0]
+        r.hetu_bn_masked = masked
         return r
     g, w = _match(g, w)
     from . import cpu_native
@@ -391,16 +394,22 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
     key = ('dgrad_bn', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None)
     # candidates accumulate into scratch while the shape is being timed
     tgt = [sums if key in _decisions else torch.zeros_like(sums)]
+    masked = [False]
 
     def hip(tile=0):
-        return lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=tile,
-                                                    bnb=(tgt[0], xb, mask))
+        def f():
+            r = conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=tile,
+                                             bnb=(tgt[0], xb, mask, True))
+            masked[0] = r is not None and mask is not None
+            return r
+        return f
 
     def separate(run):
         def f():
             r = run()
             if r is not None:
                 bn_bwd_sums(r, xb, mask, tgt[0])
+            masked[0] = False
             return r
         return f
     blas = {}
@@ -411,12 +420,17 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
     if _short_k(w.shape[0] * w.shape[2] * w.shape[3]):
         blas['hip_lo'] = hip(3)
     if conv_igemm.conv3x3_ok(x_shape, w.shape, stride, padding, dgrad=True):
-        blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=acc,
-                                                                      bnb=(tgt[0], xb, mask))
+        def hip33():
+            r = conv_igemm.try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=acc,
+                                                     bnb=(tgt[0], xb, mask, True))
+            masked[0] = r is not None and mask is not None
+            return r
+        blas['hip33'] = hip33
 
     def tuned():
         tgt[0] = sums
-    return _pick(key, hip(0), separate(lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc)), blas, tuned)
+    r = _pick(key, hip(0), separate(lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc)), blas, tuned)
+    return r, masked[0]
 
 
 def _layout_of(t):

@@ -376,6 +376,13 @@ class Batch_Normalization_GradientOp(Op):
         if bsums is not None and not (g.is_cuda and g.dtype == x.dtype == torch.bfloat16 and (mask is not None or not fw.relu)):
             bsums.zero_()
             bsums = None
+        if bsums is not None and getattr(g, 'hetu_bn_masked', False):
+            # g was stored already masked by the ReLU keep-bits (dy'): no mask to apply,
+            # and dy' itself is the gradient of the fused residual input
+            dx, dscale, dbias, _ = KN.bn_backward(g, y, x, scale.float(), mean, invstd, relu=False,
+                                                  want_dres=False, bias=bias, dscale_out=dests.get(1),
+                                                  dbias_out=dests.get(2), bsums=bsums)
+            return (dx, dscale, dbias, g if fw.has_residual else None)
         dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
                                                  relu=fw.relu, want_dres=fw.has_residual, bias=bias,
                                                  dscale_out=dests.get(1), dbias_out=dests.get(2), mask=mask,

@@ -78,6 +78,15 @@ def test_dgrad_epilogue_bn_sums(case, masked, join):
     C = xs[1]
     assert _rel(sums[:C], rs) < 1e-4, (_rel(sums[:C], rs))
     assert _rel(sums[C:], rq) < 1e-4, (_rel(sums[C:], rq))
+    if masked:   # masked store: dx' = dx * keep-bits, same statistics
+        s2 = torch.zeros_like(sums)
+        if kind == 'gemm':
+            dm = CI.try_backward_data(g, w, xs, (s, s), (p, p), acc=acc, tile=tile, bnb=(s2, xb, mask, True))
+        else:
+            dm = CI.try_conv3x3_backward_data(g, w, xs, (s, s), (p, p), acc=acc, bnb=(s2, xb, mask, True))
+        bits = _bits(mask, dx.permute(0, 2, 3, 1).shape)
+        assert torch.equal(dm.permute(0, 2, 3, 1).float(), dx.permute(0, 2, 3, 1).float() * bits)
+        assert _rel(s2, sums) < 1e-5
 
 
 def test_bn_bwd_sums_pass_matches_reference():

@@ -56,6 +56,14 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
         if a.dtype == torch.bfloat16 and B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
             # 128x96 tile: N = 768 products fill the CUs in one round (512 tiles at M 8192)
             cands['hip96'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=5)
+        if a.dtype == torch.bfloat16 and A2.dim() == 2 and bias is None and activation is None and \
+                A2.shape[1] >= 8192:
+            # long reductions over few output tiles (the MLM head's data gradient, K = vocab):
+            # split K over fp32 slabs + one reduce
+            tiles = -(-A2.shape[0] // 128) * -(-B2.shape[1] // 128)
+            for s_ in (2, 4):
+                if tiles * s_ <= 2048:
+                    cands['hip_sk%d' % s_] = (lambda s_=s_: gemm_mfma.gemm(A2, B2, splitk=s_))
         if A2.dim() == 2 and B2.dim() == 2 and A2.shape[0] * B2.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
         cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)

@@ -143,13 +143,15 @@ def test_persistent_forward_sums_are_rezeroed():
 def _resnet_steps(fuse_bwd, fuse_stats, steps=3):
     import hetu_61a7_amd as ht
     from hetu_61a7_amd.models import resnet50_imagenet
+    from hetu_61a7_amd.ops import node as _node
+    _node.G_NODE_ID = 0      # same node ids -> same initial weights in both graphs
     os.environ['HETU_FUSE_BN_BWD'] = '1' if fuse_bwd else '0'
     os.environ['HETU_FUSE_BN_STATS'] = '1' if fuse_stats else '0'
     try:
         B = 4
         x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
         loss, _ = resnet50_imagenet(x, y_, 1000)
-        train = ht.optim.MomentumOptimizer(learning_rate=0.05, momentum=0.9).minimize(loss)
+        train = ht.optim.MomentumOptimizer(learning_rate=0.01, momentum=0.9).minimize(loss)
         ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3)
         g = torch.Generator(device='cuda')
         g.manual_seed(0)
@@ -172,5 +174,6 @@ def test_resnet50_training_with_fused_bn_reductions_tracks_unfused():
     a, _ = _resnet_steps(False, False)
     b, nf = _resnet_steps(True, True)
     assert nf >= 40, nf
-    for u, v in zip(a, b):
-        assert abs(u - v) <= 0.02 * max(1.0, abs(u)), (a, b)
+    assert abs(a[0] - b[0]) <= 1e-3 * max(1.0, abs(a[0])), (a, b)     # same forward
+    for u, v in zip(a[1:], b[1:]):
+        assert abs(u - v) <= 0.05 * max(1.0, abs(u)), (a, b)

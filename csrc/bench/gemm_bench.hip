@@ -119,7 +119,8 @@ int main(int argc, char** argv) {
   if (shapes.empty())
     shapes = {{4096, 4096, 4096, 0, 0}, {4096, 4096, 4096, 0, 1}, {8192, 8192, 8192, 0, 1},
               {8192, 3072, 768, 0, 0},  {8192, 768, 3072, 0, 0},  {768, 3072, 8192, 1, 0},
-              {8192, 2304, 768, 0, 0},  {50176, 256, 1024, 0, 1}, {50176, 1024, 256, 0, 1}};
+              {8192, 2304, 768, 0, 0},  {50176, 256, 1024, 0, 1}, {50176, 1024, 256, 0, 1},
+              {8192, 768, 768, 0, 0},   {8192, 30528, 768, 0, 1}, {8192, 768, 30528, 0, 0}};
   const int reps = getenv("REPS") ? atoi(getenv("REPS")) : 20;
   const int rounds = getenv("ROUNDS") ? atoi(getenv("ROUNDS")) : 5;
   const char* only = getenv("TILES");   // e.g. "0,1,3"
@@ -143,7 +144,7 @@ int main(int argc, char** argv) {
     const int64_t ldb = s.tb ? s.K : s.N;
     struct Var { std::string name; int tile; };
     std::vector<Var> vars = {{"blas", -1}};
-    for (int t : {0, 1, 2, 3}) {
+    for (int t : {0, 1, 2, 3, 5}) {
 #ifdef BENCH_FAST
       if (t == 0 || t == 2) continue;
 #endif

@@ -36,18 +36,24 @@ HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const flo
 // bnsums (nullable, 2*C fp32 pre-zeroed) += sum(dx') and sum(dx' * bnx) per channel with
 // dx' = dx masked by bnmask (the ReLU keep-bits of the BatchNorm whose output the conv
 // reads; null = no ReLU) and bnx that BN's input [N,H,W,C]: the BN backward's reduction.
-// bnstore: dx is stored masked (dx'), the form the BN backward and a residual branch use
+// bnstore: dx is stored masked (dx'), the form the BN backward and a residual branch use.
 const int kBnAlign = 15;
 HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const void* acc,
                                   int acc_f32, int N, int H, int W, int C, int K, int KH, int KW,
                                   int sh, int sw, int ph, int pw, int tile, float* bnsums, const void* bnx,
-                                  const uint8_t* bnmask, int bnstore, hipStream_t st) {
+                                  const uint8_t* bnmask, int bnstore, int acc_s2, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   if (bnsums && (!bnx || C % 8 || (((uintptr_t)bnx) & kBnAlign))) return (int)hipErrorInvalidValue;
+  const bool plain1x1 = KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 &&
+                        buf_ok((int64_t)N * H * W * K * 2, (int64_t)K * C * 2);
+  // acc_s2: acc is [N, H/2, W/2, C], the gradient of a 1x1 stride-2 convolution of the same
+  // input, added at the even positions (stride-1 1x1 data gradients only, even H and W)
+  if (acc_s2 && (!acc || !plain1x1 || (H & 1) || (W & 1) || (int64_t)N * H * W >= (1ll << 31)))
+    return (int)hipErrorInvalidValue;
   Epi ep{dx, acc, nullptr, C, C, 0, 0, 1.f, acc ? 1.f : 0.f, 0, 0, acc_f32, 0, 0, nullptr, 0, bnsums,
-         bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr, (bnsums && bnmask && bnstore) ? 1 : 0};
-  if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 &&
-      buf_ok((int64_t)N * H * W * K * 2, (int64_t)K * C * 2)) {
+         bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr, (bnsums && bnmask && bnstore) ? 1 : 0,
+         acc_s2 ? H : 0, acc_s2 ? W : 0};
+  if (plain1x1) {
     int64_t M = (int64_t)N * H * W;
     return K % BK == 0 ? launch_buf<true>((const bf16*)dy, (const bf16*)w, 1, 0, K, C, 0, 0, ep, M, C, K, 1, 1, st, tile)
                        : launch_buf<false>((const bf16*)dy, (const bf16*)w, 1, 0, K, C, 0, 0, ep, M, C, K, 1, 1, st, tile);

@@ -496,6 +496,10 @@ struct Epi {
   const uint8_t* bnmask;
   int bnstore;    // store dy' (dy masked by bnmask) instead of dy: the BN backward and the
                   // residual branch then read the masked gradient as it is
+  // Cin on the stride-2 subgrid (cin_h, cin_w = the output's H, W; 0 = off): output row
+  // (n, h, w) adds Cin row (n, h/2, w/2) when h and w are even, nothing otherwise -- the
+  // gradient of a 1x1 stride-2 downsample convolution joined without scattering it first
+  int cin_h, cin_w;
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -601,8 +605,15 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += ep.bias_on_m ? bm : o.bcol[t];
   }
-  if (o.Cinb) {
-    const int64_t off = orow * ep.ldcin + n;
+  int64_t crow = orow;
+  if (o.Cinb && ep.cin_w) {   // stride-2 subgrid Cin: even (h, w) only
+    const uint32_t hw = (uint32_t)(ep.cin_h * ep.cin_w), o32 = (uint32_t)orow;   // rows < 2^31 (host check)
+    const uint32_t img = o32 / hw, r = o32 - img * hw;
+    const uint32_t h = r / (uint32_t)ep.cin_w, w = r - h * (uint32_t)ep.cin_w;
+    crow = ((h | w) & 1u) ? -1 : ((int64_t)img * (ep.cin_h >> 1) + (h >> 1)) * (ep.cin_w >> 1) + (w >> 1);
+  }
+  if (o.Cinb && crow >= 0) {
+    const int64_t off = crow * ep.ldcin + n;
     float cv[8];
     if (has_pre && o.ivec && full && !ep.cin_f32) {
       const uint32_t w[4] = {pre.x, pre.y, pre.z, pre.w};
@@ -802,7 +813,7 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
   // (not in the single-stage 4-blocks-per-CU build: at 128 registers the prefetch spills,
   // and its neighbours on the CU hide the epilogue latency instead)
   uint4 cpre[NPASS];
-  const bool use_pre = ST == 2 && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec;
+  const bool use_pre = ST == 2 && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec && !ep.cin_w;
   const int64_t pre_n = (int64_t)tn * TBN + ec;
   auto pre_load = [&](int h, int pss) {
     const int rr = pss * RPP + tid / TPR;

@@ -184,6 +184,25 @@ def fuse_backward(roots):
                 n.bw_of = bw
             fused += 1
             continue
+        # the ResNet downsample join: a 1x1 stride-1 and a 1x1 stride-2 data gradient of the
+        # same input -- the stride-2 one stays on its subgrid (compact) and the stride-1 one
+        # adds it at the even positions in its epilogue (no scattered full-size tensor)
+        s2 = _s2_join(n, cons, root_set)
+        if s2 is not None:
+            d, other = s2
+            other.compact_s2 = True
+            keep_id, keep_name, bw = n.id, n.name, getattr(n, 'bw_of', None)
+            n.__class__ = Conv2d_Gradient_of_DataOp
+            n.__dict__.update({k: v for k, v in d.__dict__.items() if k not in ('id', 'name', 'inputs', 'bw_of')})
+            n.inputs = list(d.inputs) + [other]
+            n.acc_inplace = False
+            n.acc_s2 = True
+            n.op_type = 'Conv2d_Gradient_of_DataOp'
+            n.id, n.name = keep_id, keep_name
+            if bw is not None:
+                n.bw_of = bw
+            fused += 1
+            continue
         for d in n.inputs:
             if isinstance(d, Conv2d_Gradient_of_DataOp) and len(d.inputs) == 3 and \
                     len(cons.get(d, [])) == 1 and d not in root_set:
@@ -206,6 +225,36 @@ def fuse_backward(roots):
                 break
     fused += _fuse_bn_backward_reduction(roots)
     return fused
+
+
+def _is_1x1(d, stride):
+    w = d.inputs[0]
+    shp = getattr(w, 'shape', None)
+    return (tuple(d.stride) == (stride, stride) and tuple(d.padding) == (0, 0) and shp is not None
+            and len(shp) == 4 and shp[2] == 1 and shp[3] == 1)
+
+
+def _s2_join(n, cons, root_set):
+    """(stride-1 dgrad, stride-2 dgrad) when the fan-in sum ``n`` adds exactly the data
+    gradients of a 1x1 stride-1 and a 1x1 stride-2 (pad 0) convolution of one input"""
+    from .ops.nn import Conv2d_Gradient_of_DataOp
+    if os.environ.get('HETU_S2_JOIN', '1') != '1' or len(n.inputs) != 2:
+        return None
+    a, b = n.inputs
+    for d, o in ((a, b), (b, a)):
+        if not (isinstance(d, Conv2d_Gradient_of_DataOp) and isinstance(o, Conv2d_Gradient_of_DataOp)):
+            continue
+        if len(d.inputs) != 3 or len(o.inputs) != 3 or d.compact_s2 or o.compact_s2:
+            continue
+        if any(len(cons.get(x, [])) != 1 or x in root_set for x in (d, o)):
+            continue
+        if d.inputs[2] is not o.inputs[2] or not _is_1x1(d, 1) or not _is_1x1(o, 2):
+            continue
+        ctx = getattr(n, 'raw_ctx', None)
+        if getattr(d, 'raw_ctx', None) != ctx or getattr(o, 'raw_ctx', None) != ctx:
+            continue
+        return d, o
+    return None
 
 
 def _fuse_bn_backward_reduction(roots):

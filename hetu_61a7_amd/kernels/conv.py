@@ -292,7 +292,17 @@ def conv2d(x, w, b, stride, padding):
     return y
 
 
-def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=False, bn=None):
+def _scatter_s2(acc, x_shape):
+    """[N, C, H/2, W/2] -> [N, C, H, W] with acc at the even positions, zeros elsewhere
+    (fallback for the subgrid join when no hand-written kernel takes it)"""
+    full = _zeros(tuple(x_shape), acc.device, acc.dtype)
+    if acc.is_contiguous(memory_format=CL):
+        full = full.contiguous(memory_format=CL)
+    full[:, :, ::2, ::2] = acc
+    return full
+
+
+def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=False, bn=None, acc_s2=False):
     """dx (+ acc when given: a gradient joined at the conv input, fused into the
     epilogue on the HIP path).  ``acc_inplace``: acc is dead after this call and
     may receive the result (the library GEMM accumulates into it, C == D).
@@ -303,7 +313,20 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     library kernel -- and the result carries them as ``hetu_bn_bsums``.  With a mask the
     hand-written kernels store dx' (masked) and flag the result ``hetu_bn_masked``: the
     BN backward then reads no mask, and dx' itself is the residual-branch gradient.
-    bf16 on the GPU only (otherwise ignored)."""
+    bf16 on the GPU only (otherwise ignored).
+    ``acc_s2``: acc is [N, C, H/2, W/2] -- the data gradient of a 1x1 stride-2
+    convolution of the same input, in compact form -- and is added at the even
+    positions only (the ResNet downsample join, without scattering that gradient)."""
+    if acc_s2:
+        if not (g.is_cuda and g.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and MODE != 'vendor'
+                and acc.dtype == torch.bfloat16 and _plain_1x1((g, w), w.shape, stride, padding)
+                and x_shape[2] % 2 == 0 and x_shape[3] % 2 == 0):
+            return conv2d_backward_data(g, w, x_shape, stride, padding, acc=_scatter_s2(acc, x_shape), bn=bn)
+        r, masked = _dgrad_s2join(g, w, x_shape, acc, bn)
+        if bn is not None:
+            r.hetu_bn_bsums = bn[0]
+            r.hetu_bn_masked = masked
+        return r
     if bn is not None:
         if not (g.is_cuda and g.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and
                 (acc is None or acc.dtype == torch.bfloat16) and bn[1].dtype == torch.bfloat16 and
@@ -430,6 +453,49 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
     def tuned():
         tgt[0] = sums
     r = _pick(key, hip(0), separate(lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc)), blas, tuned)
+    return r, masked[0]
+
+
+def _dgrad_s2join(g, w, x_shape, acc, bn):
+    """1x1 stride-1 data gradient + a compact stride-2 gradient at the even positions
+    (conv2d_backward_data acc_s2), optionally with the BN-backward reduction"""
+    from . import conv_igemm
+    from .autotune import _decisions
+    g = g.contiguous(memory_format=CL)
+    w = w.contiguous(memory_format=CL)
+    acc = acc.contiguous(memory_format=CL)
+    key = ('dgrad_s2join', tuple(g.shape), tuple(w.shape), bn is not None)
+    tgt = [None]
+    if bn is not None:
+        tgt[0] = bn[0] if key in _decisions else torch.zeros_like(bn[0])
+    masked = [False]
+
+    def hip(tile):
+        def f():
+            bnb = None if bn is None else (tgt[0], bn[1], bn[2], True)
+            r = conv_igemm.try_backward_data(g, w, x_shape, (1, 1), (0, 0), acc=acc, tile=tile, bnb=bnb,
+                                             acc_s2=True)
+            masked[0] = r is not None and bn is not None and bn[2] is not None
+            return r
+        return f
+
+    def vendor():
+        masked[0] = False
+        r = _vendor_dgrad(g, w, x_shape, (1, 1), (0, 0), _scatter_s2(acc, x_shape))
+        if bn is not None:
+            from .norm import bn_bwd_sums
+            bn_bwd_sums(r, bn[1], bn[2], tgt[0])
+        return r
+    blas = {'hip_lo': hip(3)}
+    if x_shape[1] >= 128:
+        blas['hip256'] = hip(1)
+    if x_shape[1] <= 64:
+        blas['hip64'] = hip(2)
+
+    def tuned():
+        if bn is not None:
+            tgt[0] = bn[0]
+    r = _pick(key, hip(0), vendor, blas, tuned)
     return r, masked[0]
 
 

@@ -305,13 +305,18 @@ def _bnb_args(bnb, x_shape):
     return sums.data_ptr(), x.data_ptr(), mask.data_ptr() if mask is not None else None, int(store and mask is not None)
 
 
-def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0, bnb=None):
-    """``bnb``: see _bnb_args -- the sums receive sum(dx') and sum(dx' * x)"""
+def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0, bnb=None, acc_s2=False):
+    """``bnb``: see _bnb_args -- the sums receive sum(dx') and sum(dx' * x).
+    ``acc_s2``: acc is [N, C, H/2, W/2], added at the even positions only (a 1x1
+    stride-2 convolution's data gradient joined without scattering it)"""
     if not _ok(g, w, x_shape[1], w.shape[0]):
         return None
-    if acc is not None and (tuple(acc.shape) != tuple(x_shape) or
+    acc_shape = tuple(x_shape) if not acc_s2 else (x_shape[0], x_shape[1], x_shape[2] // 2, x_shape[3] // 2)
+    if acc is not None and (tuple(acc.shape) != acc_shape or
                             not acc.is_contiguous(memory_format=CL) or
                             acc.dtype not in (torch.bfloat16, torch.float32)):
+        return None
+    if acc_s2 and (acc is None or x_shape[2] % 2 or x_shape[3] % 2):
         return None
     bn = _bnb_args(bnb, x_shape)
     if bn is False:
@@ -319,10 +324,11 @@ def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0, bnb=None
     N, C, H, W = x_shape
     K, _, KH, KW = w.shape
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
-    f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [I32, P, P, P, I32, P])
+    f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [I32, P, P, P, I32, I32, P])
     check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
             int(acc is not None and acc.dtype == torch.float32), N, H, W, C, K, KH, KW,
-            stride[0], stride[1], padding[0], padding[1], int(tile), *bn, stream_ptr()), 'conv_dgrad')
+            stride[0], stride[1], padding[0], padding[1], int(tile), *bn, int(acc_s2), stream_ptr()),
+          'conv_dgrad')
     record_native('conv_dgrad')
     return dx.permute(0, 3, 1, 2)
 

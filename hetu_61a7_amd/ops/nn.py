@@ -98,11 +98,16 @@ class Conv2d_Gradient_of_DataOp(Op):
         self.padding, self.stride = _pair(padding), _pair(stride)
 
     bn_fused = None   # graph_opt: (BN forward node) whose backward reduction this epilogue computes
+    compact_s2 = False   # graph_opt: 1x1 stride-2 data gradient kept on the stride-2 subgrid
+    acc_s2 = False       # graph_opt: the joined gradient (input 3) is such a compact gradient
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         # optional 4th input: a gradient to accumulate (fused fan-in sum, graph_opt);
         # with bn_fused the last two inputs are that BN's input x and its forward node
         w, g, xshape = input_vals[:3]
+        if self.compact_s2:   # dx at the even positions only = a 1x1 stride-1 gradient on the subgrid
+            n, c = xshape[0], xshape[1]
+            return KC.conv2d_backward_data(g, w, (n, c, g.shape[2], g.shape[3]), (1, 1), (0, 0))
         nbase = len(input_vals) - (2 if self.bn_fused is not None else 0)
         acc = input_vals[3] if nbase > 3 else None
         bn = None
@@ -115,12 +120,16 @@ class Conv2d_Gradient_of_DataOp(Op):
                     sums = bufs[xb.device] = torch.zeros(2 * xb.shape[1], dtype=torch.float32, device=xb.device)
                 bn = (sums, xb, aux[2] if len(aux) > 2 else None)
         return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,
-                                       acc_inplace=_may_overwrite(self, acc), bn=bn)
+                                       acc_inplace=_may_overwrite(self, acc) and not self.acc_s2, bn=bn,
+                                       acc_s2=self.acc_s2 and acc is not None)
 
     def gradient(self, output_grad):
         raise NotImplementedError
 
     def infer_shape(self, input_shapes):
+        if self.compact_s2:
+            x, g = input_shapes[2], input_shapes[1]
+            return (x[0], x[1], g[2], g[3])
         return input_shapes[2]
 
 

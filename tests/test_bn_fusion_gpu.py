@@ -89,6 +89,38 @@ def test_dgrad_epilogue_bn_sums(case, masked, join):
         assert _rel(s2, sums) < 1e-5
 
 
+@pytest.mark.parametrize('tile', [0, 1, 2, 3])
+@pytest.mark.parametrize('with_bn', [False, True])
+def test_dgrad_subgrid_join(tile, with_bn):
+    """1x1 stride-1 data gradient + the compact gradient of a 1x1 stride-2 conv of the same
+    input added at the even positions (the ResNet downsample join): against the scattered
+    reference, with and without the BN-backward reduction + masked store."""
+    torch.manual_seed(3)
+    N, H, K, C = 2, 14, 256, 128 if tile != 2 else 64
+    g = torch.randn(N, K, H, H, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = (torch.randn(K, C, 1, 1, device=DEV) * 0.05).bfloat16().contiguous(memory_format=CL)
+    acc = torch.randn(N, C, H // 2, H // 2, device=DEV).bfloat16().contiguous(memory_format=CL)
+    xs = (N, C, H, H)
+    full = torch.zeros(xs, device=DEV).bfloat16().contiguous(memory_format=CL)
+    full[:, :, ::2, ::2] = acc
+    ref = CI.try_backward_data(g, w, xs, (1, 1), (0, 0), acc=full, tile=tile)
+    bnb = None
+    if with_bn:
+        xb = torch.randn(xs, device=DEV).bfloat16().contiguous(memory_format=CL)
+        mask = torch.randint(0, 256, (xb.numel() // 8,), device=DEV, dtype=torch.int32).to(torch.uint8)
+        sums = torch.zeros(2 * C, device=DEV)
+        bnb = (sums, xb, mask, True)
+    dx = CI.try_backward_data(g, w, xs, (1, 1), (0, 0), acc=acc, tile=tile, bnb=bnb, acc_s2=True)
+    assert dx is not None
+    if not with_bn:
+        assert torch.equal(dx, ref)
+        return
+    bits = _bits(mask, ref.permute(0, 2, 3, 1).shape)
+    assert torch.equal(dx.permute(0, 2, 3, 1).float(), ref.permute(0, 2, 3, 1).float() * bits)
+    rs, rq = _ref_sums(ref, xb, mask)
+    assert _rel(sums[:C], rs) < 1e-4 and _rel(sums[C:], rq) < 1e-4
+
+
 def test_bn_bwd_sums_pass_matches_reference():
     x = (torch.randn(4, 128, 14, 14, device=DEV) + 1).bfloat16().contiguous(memory_format=CL)
     dy = torch.randn(4, 128, 14, 14, device=DEV).bfloat16().contiguous(memory_format=CL)

@@ -24,6 +24,12 @@ CL = torch.channels_last
 MODE = os.environ.get('HETU_CONV', 'hip')
 
 
+def _masked_store():
+    """dgrad epilogues that fuse a BN-backward reduction also store the ReLU-masked
+    gradient (HETU_BN_MASKED_STORE=0: plain gradient, the BN backward masks it)"""
+    return os.environ.get('HETU_BN_MASKED_STORE', '1') == '1'
+
+
 def _pick(key, hip, vendor, blas=None, tuned=None):
     """hip: hand-written implicit GEMM; vendor: MIOpen; blas: a 1x1 convolution
     run as the plain library GEMM it is (hipBLASLt), where applicable.
@@ -422,8 +428,8 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
     def hip(tile=0):
         def f():
             r = conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc, tile=tile,
-                                             bnb=(tgt[0], xb, mask, True))
-            masked[0] = r is not None and mask is not None
+                                             bnb=(tgt[0], xb, mask, _masked_store()))
+            masked[0] = r is not None and mask is not None and _masked_store()
             return r
         return f
 
@@ -445,8 +451,8 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
     if conv_igemm.conv3x3_ok(x_shape, w.shape, stride, padding, dgrad=True):
         def hip33():
             r = conv_igemm.try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=acc,
-                                                     bnb=(tgt[0], xb, mask, True))
-            masked[0] = r is not None and mask is not None
+                                                     bnb=(tgt[0], xb, mask, _masked_store()))
+            masked[0] = r is not None and mask is not None and _masked_store()
             return r
         blas['hip33'] = hip33
 
@@ -472,10 +478,10 @@ def _dgrad_s2join(g, w, x_shape, acc, bn):
 
     def hip(tile):
         def f():
-            bnb = None if bn is None else (tgt[0], bn[1], bn[2], True)
+            bnb = None if bn is None else (tgt[0], bn[1], bn[2], _masked_store())
             r = conv_igemm.try_backward_data(g, w, x_shape, (1, 1), (0, 0), acc=acc, tile=tile, bnb=bnb,
                                              acc_s2=True)
-            masked[0] = r is not None and bn is not None and bn[2] is not None
+            masked[0] = r is not None and bn is not None and bn[2] is not None and _masked_store()
             return r
         return f
 

@@ -391,7 +391,9 @@ class Batch_Normalization_GradientOp(Op):
             dx, dscale, dbias, _ = KN.bn_backward(g, y, x, scale.float(), mean, invstd, relu=False,
                                                   want_dres=False, bias=bias, dscale_out=dests.get(1),
                                                   dbias_out=dests.get(2), bsums=bsums)
-            return (dx, dscale, dbias, g if fw.has_residual else None)
+            # (a fresh tensor object over the same storage: g's hetu_bn_* attributes
+            # belong to this BN and must not reach the consumer of the residual gradient)
+            return (dx, dscale, dbias, g.detach() if fw.has_residual else None)
         dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
                                                  relu=fw.relu, want_dres=fw.has_residual, bias=bias,
                                                  dscale_out=dests.get(1), dbias_out=dests.get(2), mask=mask,

@@ -71,3 +71,4 @@ def test_downsample_join_on_the_subgrid():
     dg = [n for n in nodes if isinstance(n, Conv2d_Gradient_of_DataOp)]
     assert any(n.compact_s2 for n in dg) and any(n.acc_s2 for n in dg)
     np.testing.assert_allclose(base, joined, rtol=1e-5, atol=1e-5)
+

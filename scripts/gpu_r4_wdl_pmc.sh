@@ -25,3 +25,6 @@ for m in ${PMC_MODELS:-resnet50 bert}; do
   pass $m mem FETCH_SIZE SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE || exit $?
   pass $m wr WRITE_SIZE GRBM_GUI_ACTIVE || exit $?
 done
+for m in ${PMC_MODELS:-resnet50 bert}; do   # MFMA op counts (bf16 MOPs: 512 flops each)
+  pass $m mops SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE || exit $?
+done

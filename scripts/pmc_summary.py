@@ -13,6 +13,7 @@ counters over every dispatch and derives:
   lds_cf   = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   rd_TB/s  = 2 * FETCH_SIZE KB / time (FETCH_SIZE reads 1/2 of a wide coalesced
              stream on gfx950, MI355X_MICROARCH.md); wr_TB/s = WRITE_SIZE KB / time
+  TF/s     = 512 * SQ_INSTS_VALU_MFMA_MOPS_BF16 / time (4th directory, optional)
 """
 import collections
 import csv
@@ -59,9 +60,10 @@ def main(dirs):
     sq, calls, ns = load(dirs[0])
     mem = load(dirs[1]) if len(dirs) > 1 else ({}, {}, {})
     wr = load(dirs[2]) if len(dirs) > 2 else ({}, {}, {})
+    mops = load(dirs[3]) if len(dirs) > 3 else ({}, {}, {})
     rows = sorted(sq.items(), key=lambda kv: -ns[kv[0]])
-    print('%-64s %6s %8s %8s %8s %8s %8s %8s %7s' % ('kernel family', 'calls', 'ms', 'clk_GHz', 'mfma_pk',
-                                                     'wait', 'lds_cf', 'rd_TB/s', 'wr_TB/s'))
+    print('%-64s %6s %8s %8s %8s %8s %8s %8s %7s %7s' % ('kernel family', 'calls', 'ms', 'clk_GHz', 'mfma_pk',
+                                                         'wait', 'lds_cf', 'rd_TB/s', 'wr_TB/s', 'TF/s'))
     for k, c in rows[:40]:
         t = ns[k] * 1e-9
         cyc = c.get('GRBM_GUI_ACTIVE', 0) / 8.0                      # summed over 8 XCDs
@@ -75,7 +77,10 @@ def main(dirs):
         rd = 2 * mem[0].get(k, {}).get('FETCH_SIZE', 0) * 1024 / tm / 1e12 if tm else float('nan')
         tw = wr[2].get(k, 0) * 1e-9
         w = wr[0].get(k, {}).get('WRITE_SIZE', 0) * 1024 / tw / 1e12 if tw else float('nan')
-        print('%-64s %6d %8.2f %8.2f %8.3f %8.3f %8.3f %8.2f %7.2f' % (k[:64], calls[k], t * 1e3, clk, mf, wait, lc, rd, w))
+        tmo = mops[2].get(k, 0) * 1e-9
+        tf = 512 * mops[0].get(k, {}).get('SQ_INSTS_VALU_MFMA_MOPS_BF16', 0) / tmo / 1e12 if tmo else float('nan')
+        print('%-64s %6d %8.2f %8.2f %8.3f %8.3f %8.3f %8.2f %7.2f %7.0f' % (k[:64], calls[k], t * 1e3, clk, mf, wait,
+                                                                             lc, rd, w, tf))
     # every counter of every pass, per dispatch (raw sums / calls), for the top families
     print('\n# raw counters per dispatch')
     for k, c in rows[:12]:

@@ -72,8 +72,12 @@ for g in (False, True):
         gr = ex.subexecutor['train'].graph
         native = type(gr.graph).__name__ == '_NativeReplay'
         pool = gr.pool.stats() if native else {}
+try:
+    reserved = torch.cuda.memory_reserved()
+except RuntimeError:      # the pluggable allocator replaced torch's caching allocator (no stats)
+    reserved = 0
 print(json.dumps({'eager': out[0], 'graph': out[1], 'native': native, 'pool': pool,
-                  'torch_reserved': torch.cuda.memory_reserved(), 'bfc': MP.torch_bfc_enabled()}))
+                  'torch_reserved': reserved, 'bfc': MP.torch_bfc_enabled()}))
 '''
 
 
@@ -108,7 +112,11 @@ Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', gene
 import numpy as np
 ls = [float(np.mean(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0])) for _ in range(3)]
 torch.cuda.synchronize()
-print(json.dumps({'losses': ls, 'torch_reserved': torch.cuda.memory_reserved(), 'stats': MP.device_stats(0),
+try:
+    reserved = torch.cuda.memory_reserved()
+except RuntimeError:      # the pluggable allocator replaced torch's caching allocator (no stats)
+    reserved = 0
+print(json.dumps({'losses': ls, 'torch_reserved': reserved, 'stats': MP.device_stats(0),
                   'bfc': MP.torch_bfc_enabled()}))
 '''
 

@@ -133,6 +133,7 @@ def test_resnet50_step_allocates_only_from_the_bfc_pool():
 
 def test_pinned_pool_tensor_is_pinned_and_copies():
     from hetu_61a7_amd.ndarray import pinned_empty
+    torch.zeros(1, device='cuda')    # torch reports host memory pinned only once its device context is up
     t = pinned_empty((1024, 256), torch.float32)
     t.copy_(torch.arange(1024 * 256, dtype=torch.float32).reshape(1024, 256))
     assert t.is_pinned()

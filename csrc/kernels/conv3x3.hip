@@ -40,16 +40,29 @@ __device__ __forceinline__ unsigned mask4(const BnB& bn, int64_t e) {
   return (bn.x && bn.mask) ? ((unsigned)bn.mask[e >> 3] >> (e & 7)) & 0xfu : 0xfu;
 }
 
-// 4 stored channels at element offset e (co % 4 == 0) into the running sums s[0..3], q[0..3]
-__device__ __forceinline__ void stats4(const BnB& bn, int64_t e, const unsigned short (&h)[4], float* s, float* q) {
+// BN operands of 4 channels at element offset e, requested before the tile's Cin load and
+// store so the round trips overlap
+struct Bn4 {
+  uint2 x;
+  unsigned mk;
+};
+__device__ __forceinline__ Bn4 bn_load4(const BnB& bn, int64_t e) {
+  Bn4 r{make_uint2(0, 0), 0xfu};
   if (bn.x) {
-    const uint2 a = *reinterpret_cast<const uint2*>(bn.x + e);
-    const float xv[4] = {bf16_bits_to_f((unsigned short)(a.x & 0xffffu)), bf16_bits_to_f((unsigned short)(a.x >> 16)),
-                         bf16_bits_to_f((unsigned short)(a.y & 0xffffu)), bf16_bits_to_f((unsigned short)(a.y >> 16))};
-    const unsigned mk = mask4(bn, e);
+    r.x = *reinterpret_cast<const uint2*>(bn.x + e);
+    r.mk = mask4(bn, e);
+  }
+  return r;
+}
+
+// 4 stored channels into the running sums s[0..3], q[0..3]
+__device__ __forceinline__ void stats4(const BnB& bn, const Bn4& b4, const unsigned short (&h)[4], float* s, float* q) {
+  if (bn.x) {
+    const float xv[4] = {bf16_bits_to_f((unsigned short)(b4.x.x & 0xffffu)), bf16_bits_to_f((unsigned short)(b4.x.x >> 16)),
+                         bf16_bits_to_f((unsigned short)(b4.x.y & 0xffffu)), bf16_bits_to_f((unsigned short)(b4.x.y >> 16))};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float g = (mk >> i) & 1u ? bf16_bits_to_f(h[i]) : 0.f;
+      const float g = (b4.mk >> i) & 1u ? bf16_bits_to_f(h[i]) : 0.f;
       s[i] += g;
       q[i] += g * xv[i];
     }
@@ -196,6 +209,7 @@ __global__ __launch_bounds__((Geo<WD, TH>::NT), 1) void conv3x3_c64_k(const bf16
       for (int q = 0; q < 4; ++q) {
         const int co = q * 16 + 4 * q4;
         float v[4] = {acc[p][q][0], acc[p][q][1], acc[p][q][2], acc[p][q][3]};
+        const Bn4 b4 = colstats ? bn_load4(bn, pix * CH + co) : Bn4{make_uint2(0, 0), 0xfu};
         if (cin) {
           if (cin_f32) {
             const float4 a = *reinterpret_cast<const float4*>((const float*)cin + pix * CH + co);
@@ -209,14 +223,13 @@ __global__ __launch_bounds__((Geo<WD, TH>::NT), 1) void conv3x3_c64_k(const bf16
           }
         }
         if (bn.store) {
-          const unsigned mk = mask4(bn, pix * CH + co);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = (mk >> i) & 1u ? v[i] : 0.f;
+          for (int i = 0; i < 4; ++i) v[i] = (b4.mk >> i) & 1u ? v[i] : 0.f;
         }
         unsigned short h[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) h[i] = f_to_bf16_bits(v[i]);
-        if (colstats) stats4(bn, pix * CH + co, h, cs + q * 4, cq + q * 4);
+        if (colstats) stats4(bn, b4, h, cs + q * 4, cq + q * 4);
         uint2 pk;
         pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
         pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
@@ -545,6 +558,7 @@ __global__ __launch_bounds__(256, 4) void conv3x3_wide_k(const bf16* __restrict_
     for (int j = 0; j < 2; ++j) {
       const int co = cob * WBN + (2 * wave + j) * 16 + 4 * q4;
       float v[4] = {acc[b][j][0], acc[b][j][1], acc[b][j][2], acc[b][j][3]};
+      const Bn4 b4 = colstats ? bn_load4(bn, opx[b] * K + co) : Bn4{make_uint2(0, 0), 0xfu};
       if (cin) {
         if (cin_f32) {
           const float4 a = *reinterpret_cast<const float4*>((const float*)cin + opx[b] * K + co);
@@ -558,14 +572,13 @@ __global__ __launch_bounds__(256, 4) void conv3x3_wide_k(const bf16* __restrict_
         }
       }
       if (bn.store) {
-        const unsigned mk = mask4(bn, opx[b] * K + co);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = (mk >> i) & 1u ? v[i] : 0.f;
+        for (int i = 0; i < 4; ++i) v[i] = (b4.mk >> i) & 1u ? v[i] : 0.f;
       }
       unsigned short h[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) h[i] = f_to_bf16_bits(v[i]);
-      if (colstats) stats4(bn, opx[b] * K + co, h, cs + j * 4, cq + j * 4);
+      if (colstats) stats4(bn, b4, h, cs + j * 4, cq + j * 4);
       uint2 pk;
       pk.x = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
       pk.y = (uint32_t)h[2] | ((uint32_t)h[3] << 16);

@@ -605,6 +605,14 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += ep.bias_on_m ? bm : o.bcol[t];
   }
+  // BN-backward operands of this row piece (x and the ReLU keep-bits): requested first, so
+  // they are in flight together with the Cin load below instead of one round trip each
+  // after the store
+  const int64_t off = orow * ep.ldc + n;
+  const bool bnv = ep.colstats && ep.bnx;
+  uint4 bxr = make_uint4(0, 0, 0, 0);
+  if (bnv && o.cvec && full) bxr = *reinterpret_cast<const uint4*>(ep.bnx + off);
+  const unsigned bnmk = (bnv && ep.bnmask) ? (unsigned)ep.bnmask[off >> 3] : 0xffu;
   int64_t crow = orow;
   if (o.Cinb && ep.cin_w) {   // stride-2 subgrid Cin: even (h, w) only
     const uint32_t hw = (uint32_t)(ep.cin_h * ep.cin_w), o32 = (uint32_t)orow;   // rows < 2^31 (host check)
@@ -613,7 +621,7 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
     crow = ((h | w) & 1u) ? -1 : ((int64_t)img * (ep.cin_h >> 1) + (h >> 1)) * (ep.cin_w >> 1) + (w >> 1);
   }
   if (o.Cinb && crow >= 0) {
-    const int64_t off = crow * ep.ldcin + n;
+    const int64_t coff = crow * ep.ldcin + n;
     float cv[8];
     if (has_pre && o.ivec && full && !ep.cin_f32) {
       const uint32_t w[4] = {pre.x, pre.y, pre.z, pre.w};
@@ -624,17 +632,17 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
       }
     } else if (o.ivec && full) {
       if (ep.cin_f32) {
-        float4 c0 = *reinterpret_cast<const float4*>((const float*)o.Cinb + off);
-        float4 c1 = *reinterpret_cast<const float4*>((const float*)o.Cinb + off + 4);
+        float4 c0 = *reinterpret_cast<const float4*>((const float*)o.Cinb + coff);
+        float4 c1 = *reinterpret_cast<const float4*>((const float*)o.Cinb + coff + 4);
         cv[0] = c0.x; cv[1] = c0.y; cv[2] = c0.z; cv[3] = c0.w;
         cv[4] = c1.x; cv[5] = c1.y; cv[6] = c1.z; cv[7] = c1.w;
       } else {
-        load_vec<bf16>((const bf16*)o.Cinb + off, cv);
+        load_vec<bf16>((const bf16*)o.Cinb + coff, cv);
       }
     } else {
 #pragma unroll
       for (int t = 0; t < 8; ++t)
-        cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)o.Cinb)[off + t] : to_f(((const bf16*)o.Cinb)[off + t]))
+        cv[t] = n + t < N ? (ep.cin_f32 ? ((const float*)o.Cinb)[coff + t] : to_f(((const bf16*)o.Cinb)[coff + t]))
                           : 0.f;
     }
 #pragma unroll
@@ -644,8 +652,6 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
   }
-  const int64_t off = orow * ep.ldc + n;
-  const unsigned bnmk = (ep.colstats && ep.bnx && ep.bnmask) ? (unsigned)ep.bnmask[off >> 3] : 0xffu;
   if (ep.bnstore) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = (bnmk >> t) & 1u ? v[t] : 0.f;
@@ -673,10 +679,15 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
         if (n + t < N) ((unsigned short*)Ch)[t] = f_to_bf16_bits(v[t]);
     }
   }
-  if (ep.colstats && ep.bnx) {   // BN backward sums of the stored dy
+  if (bnv) {   // BN backward sums of the stored dy
     float xv[8];
     if (o.cvec && full) {
-      load_vec<bf16>(ep.bnx + off, xv);
+      const uint32_t xw[4] = {bxr.x, bxr.y, bxr.z, bxr.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        xv[2 * t] = bf16_bits_to_f((unsigned short)(xw[t] & 0xffffu));
+        xv[2 * t + 1] = bf16_bits_to_f((unsigned short)(xw[t] >> 16));
+      }
     } else {
 #pragma unroll
       for (int t = 0; t < 8; ++t) xv[t] = n + t < N ? to_f(ep.bnx[off + t]) : 0.f;

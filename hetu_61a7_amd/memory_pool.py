@@ -112,7 +112,10 @@ class BFCAllocator(object):
 
     def __del__(self):
         try:
-            if self.h and _lib is not None:
+            from .runtime import _SHUTDOWN
+            # at interpreter exit the HIP runtime may already be gone: the regions go
+            # back to the driver with the process
+            if self.h and _lib is not None and not _SHUTDOWN[0]:
                 _lib.hetu_bfc_destroy(self.h)
         except Exception:
             pass

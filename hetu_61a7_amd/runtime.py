@@ -11,6 +11,7 @@ it and for ``record_stream`` bookkeeping of the caching allocator.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 
@@ -21,6 +22,16 @@ from ._base import _LIB_DIR
 _PATH = os.path.join(_LIB_DIR, 'libhetu_alloc.so')
 _lib = None
 CREATED = {'streams': 0, 'events': 0}
+# set at interpreter exit: streams / events still alive then are left to the driver (the
+# HIP runtime may already be torn down when module globals are collected)
+_SHUTDOWN = [False]
+
+
+def _at_exit():
+    _SHUTDOWN[0] = True
+
+
+atexit.register(_at_exit)
 
 
 def lib():
@@ -92,7 +103,7 @@ class DeviceStream(object):
 
     def __del__(self):
         h = getattr(self, 'handle', None)
-        if h and _lib is not None:
+        if h and _lib is not None and not _SHUTDOWN[0]:
             try:
                 lib().hetu_stream_sync(h)
                 lib().hetu_stream_destroy(h)
@@ -134,7 +145,7 @@ class DeviceEvent(object):
 
     def __del__(self):
         h = getattr(self, 'handle', None)
-        if h and _lib is not None:
+        if h and _lib is not None and not _SHUTDOWN[0]:
             try:
                 lib().hetu_event_destroy(h)
             except Exception:
@@ -182,7 +193,7 @@ class Graph(object):
 
     def __del__(self):
         try:
-            if _lib is not None:
+            if _lib is not None and not _SHUTDOWN[0]:
                 if getattr(self, 'exec', None):
                     lib().hetu_graph_exec_destroy(self.exec)
                 if getattr(self, 'graph', None):

@@ -15,6 +15,26 @@ BFCAllocator::BFCAllocator(MemKind kind, int device, size_t limit_bytes, size_t 
     : kind_(kind), device_(device), limit_(limit_bytes), next_region_(first_region) {
   st_.bytes_limit = (int64_t)limit_bytes;
   if (next_region_ < (2u << 20)) next_region_ = 2u << 20;
+  cache_on_ = kind == MemKind::kDevice;
+}
+
+void BFCAllocator::set_cache(bool on) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!on) flush_cache();
+  cache_on_ = on;
+}
+
+void BFCAllocator::flush_cache() {
+  if (cached_n_ == 0) return;
+  for (auto& kv : cache_) {
+    for (Chunk* c : kv.second) {
+      c->cached = false;
+      st_.num_free_chunks--;   // counted as free while cached; free_chunk counts it again
+      free_chunk(c);
+    }
+    kv.second.clear();
+  }
+  cached_n_ = 0;
 }
 
 BFCAllocator::~BFCAllocator() {
@@ -91,7 +111,7 @@ void BFCAllocator::erase_free(Chunk* c) {
 }
 
 BFCAllocator::Chunk* BFCAllocator::take_from(Bins& bins, size_t size) {
-  Chunk key{nullptr, size, false, 0, nullptr, nullptr, nullptr, false, nullptr};
+  Chunk key{nullptr, size, false, 0, nullptr, nullptr, nullptr, false, nullptr, false};
   for (int b = bin_of(size); b < kNumBins; ++b) {
     auto it = bins.b[b].lower_bound(&key);
     if (it != bins.b[b].end()) return *it;
@@ -105,7 +125,7 @@ BFCAllocator::Chunk* BFCAllocator::find_chunk(size_t size, hipStream_t s) {
   if (c == nullptr) return nullptr;
   erase_free(c);
   if (c->size - size >= kMinAlloc) {   // split; the remainder stays free on the same stream
-    Chunk* r = new Chunk{c->ptr + size, c->size - size, false, c->region, c, c->next, c->stream, false, nullptr};
+    Chunk* r = new Chunk{c->ptr + size, c->size - size, false, c->region, c, c->next, c->stream, false, nullptr, false};
     if (c->next) c->next->prev = r;
     c->next = r;
     c->size = size;
@@ -124,7 +144,7 @@ bool BFCAllocator::grow(size_t min_bytes) {
     p = sub_alloc(want);
   }
   if (p == nullptr) return false;
-  Chunk* c = new Chunk{(char*)p, want, false, (int)regions_.size(), nullptr, nullptr, nullptr, false, nullptr};
+  Chunk* c = new Chunk{(char*)p, want, false, (int)regions_.size(), nullptr, nullptr, nullptr, false, nullptr, false};
   regions_.push_back(Region{(char*)p, want, c});
   st_.bytes_reserved += (int64_t)want;
   st_.num_regions++;
@@ -165,6 +185,7 @@ void BFCAllocator::clean_streams() {
   // wait for every stream that owns free chunks to pass "now", then move those
   // chunks to the clean bins (coalescing with clean neighbours)
   poll_pending(true);
+  flush_cache();
   std::vector<Chunk*> moved;
   for (auto& kv : bins_) {
     if (kv.first == nullptr) continue;
@@ -248,7 +269,22 @@ void* BFCAllocator::allocate(size_t bytes, hipStream_t stream) {
   if (!tagged()) stream = nullptr;
   size_t size = round_up(bytes ? bytes : 1);
   if (!pending_.empty()) poll_pending(false);
-  Chunk* c = find_chunk(size, stream);
+  Chunk* c = nullptr;
+  if (cached_n_) {
+    auto it = cache_.find(std::make_pair(stream, size));
+    if (it != cache_.end() && !it->second.empty()) {
+      c = it->second.back();
+      it->second.pop_back();
+      c->cached = false;
+      cached_n_--;
+      st_.num_free_chunks--;
+    }
+  }
+  if (c == nullptr) c = find_chunk(size, stream);
+  if (c == nullptr && cached_n_) {
+    flush_cache();
+    c = find_chunk(size, stream);
+  }
   if (c == nullptr) {
     clean_streams();
     c = find_chunk(size, stream);
@@ -323,6 +359,14 @@ void BFCAllocator::deallocate(void* p, hipStream_t stream) {
     pending_.push_back(pd);
     return;
   }
+  if (cache_on_) {
+    c->in_use = false;
+    c->cached = true;
+    cache_[std::make_pair(c->stream, c->size)].push_back(c);
+    cached_n_++;
+    st_.num_free_chunks++;
+    return;
+  }
   free_chunk(c);
 }
 
@@ -350,7 +394,7 @@ AllocatorStats BFCAllocator::stats() {
 
 size_t BFCAllocator::release_free_regions() {
   std::lock_guard<std::mutex> g(mu_);
-  clean_streams();
+  clean_streams();   // (flushes the exact-size cache first)
   size_t freed = 0;
   for (auto& r : regions_) {
     Chunk* f = r.first;
@@ -383,6 +427,9 @@ bool BFCAllocator::check_invariants() {
       if (c->in_use) {
         used += (int64_t)c->size;
         if (!in_use_.count(c->ptr)) return false;
+      } else if (c->cached) {
+        if (c->listed) return false;   // exact-size cache: in no bin
+        ++nfree;
       } else if (std::any_of(pending_.begin(), pending_.end(), [c](const Pending& pd) { return pd.c == c; })) {
         if (c->listed) return false;   // held back for a side stream: in no bin yet
       } else {
@@ -421,6 +468,7 @@ HETU_RT_API void hetu_bfc_free(void* h, void* p, void* stream) {
 HETU_RT_API void hetu_bfc_record_stream(void* h, void* p, void* stream) {
   ((BFCAllocator*)h)->record_stream(p, (hipStream_t)stream);
 }
+HETU_RT_API void hetu_bfc_set_cache(void* h, int on) { ((BFCAllocator*)h)->set_cache(on != 0); }
 HETU_RT_API int64_t hetu_bfc_size(void* h, void* p) { return (int64_t)((BFCAllocator*)h)->allocation_size(p); }
 HETU_RT_API int64_t hetu_bfc_release(void* h) { return (int64_t)((BFCAllocator*)h)->release_free_regions(); }
 HETU_RT_API int hetu_bfc_check(void* h) { return ((BFCAllocator*)h)->check_invariants() ? 1 : 0; }

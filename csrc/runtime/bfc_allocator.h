@@ -27,6 +27,7 @@
 #include <mutex>
 #include <set>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 namespace hetu {
@@ -60,6 +61,11 @@ class BFCAllocator {
   AllocatorStats stats();
   size_t release_free_regions();                  // return wholly free regions; bytes released
   bool check_invariants();                        // debug: chunk-list / bin consistency
+  // exact-size reuse cache in front of the bins (default on for device memory): a freed
+  // chunk waits, uncoalesced, for the next request of its size on its stream -- training
+  // steps repeat their allocation sizes, so most requests are one hash lookup; the cache
+  // is flushed into the bins before the pool cleans streams or grows
+  void set_cache(bool on);
 
  private:
   static constexpr int kNumBins = 21;
@@ -74,6 +80,12 @@ class BFCAllocator {
     hipStream_t stream;   // last user (free chunks: owning bin set; nullptr = clean)
     bool listed;          // in a free bin
     std::vector<hipStream_t>* uses;   // record_stream: other streams using the chunk
+    bool cached;          // in the exact-size cache
+  };
+  struct CacheKeyHash {
+    size_t operator()(const std::pair<hipStream_t, size_t>& k) const {
+      return std::hash<size_t>()(k.second) ^ (std::hash<uintptr_t>()((uintptr_t)k.first) * 0x9e3779b97f4a7c15ull);
+    }
   };
   struct Pending {        // freed chunk whose side-stream uses are still in flight
     Chunk* c;
@@ -106,6 +118,7 @@ class BFCAllocator {
   Chunk* free_chunk(Chunk* c);   // returns the (possibly merged) free chunk
   void clean_streams();
   void poll_pending(bool wait);   // release pending chunks whose side-stream events completed
+  void flush_cache();             // cached chunks back into the bins (coalescing)
   Bins& bins_for(hipStream_t s);
   void* sub_alloc(size_t bytes);
   void sub_free(void* p);
@@ -119,6 +132,9 @@ class BFCAllocator {
   hipStream_t last_stream_ = nullptr;   // bins_ lookup cache (map nodes are stable)
   Bins* last_bins_ = nullptr;
   std::vector<Pending> pending_;
+  bool cache_on_ = false;
+  std::unordered_map<std::pair<hipStream_t, size_t>, std::vector<Chunk*>, CacheKeyHash> cache_;
+  size_t cached_n_ = 0;
   std::unordered_map<char*, Chunk*> in_use_;
   std::vector<Region> regions_;
   AllocatorStats st_;

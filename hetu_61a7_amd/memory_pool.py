@@ -46,6 +46,7 @@ def lib():
                                 ('hetu_bfc_alloc', [P, I64, P], P),
                                 ('hetu_bfc_free', [P, P, P], None),
                                 ('hetu_bfc_record_stream', [P, P, P], None),
+                                ('hetu_bfc_set_cache', [P, I32], None),
                                 ('hetu_torch_record_stream', [I32, P, P], None),
                                 ('hetu_bfc_size', [P, P], I64),
                                 ('hetu_bfc_release', [P], I64),
@@ -77,6 +78,10 @@ class BFCAllocator(object):
         """ptr is also used on ``stream``: held back from reuse after its free until
         that stream's work queued before the free has completed"""
         lib().hetu_bfc_record_stream(self.h, ptr, stream)
+
+    def set_cache(self, on):
+        """exact-size reuse cache in front of the bins (on by default for device pools)"""
+        lib().hetu_bfc_set_cache(self.h, int(bool(on)))
 
     def size_of(self, ptr):
         return lib().hetu_bfc_size(self.h, ptr)

@@ -113,3 +113,41 @@ def test_pool_backed_host_tensor():
     import gc
     gc.collect()
     assert a.stats()['bytes_in_use'] == 0
+
+
+def test_exact_size_cache():
+    """With the exact-size cache a freed chunk goes straight back to the next request of
+    its size on its stream; other sizes and streams are served from the bins, and the
+    cache is flushed (coalesced) before the pool cleans streams or grows."""
+    a = MP.BFCAllocator(MP.HOST_TAGGED, 0, 0, 1 << 20)
+    a.set_cache(True)
+    s1, s2 = 0x1000, 0x2000
+    p = a.alloc(4096, s1)
+    q = a.alloc(8192, s1)
+    a.free(p, s1)
+    assert a.alloc(4096, s1) == p                      # cache hit
+    a.free(p, s1)
+    r = a.alloc(4096, s2)                              # other stream: not the cached chunk
+    assert r != p
+    assert a.check()
+    big = a.alloc((1 << 20) - 32768, s1)               # forces flush + clean
+    assert big is not None and a.check()
+    for x, s in ((q, s1), (r, s2), (big, s1)):
+        a.free(x, s)
+    assert a.check()
+    rng = random.Random(1)
+    live = []
+    for i in range(2000):
+        if live and rng.random() < 0.5:
+            x, s = live.pop(rng.randrange(len(live)))
+            a.free(x, s)
+        else:
+            s = rng.choice([0x10, 0x20])
+            x = a.alloc(rng.choice([256, 512, 4096, 65536]), s)
+            assert x
+            live.append((x, s))
+        if i % 200 == 0:
+            assert a.check()
+    for x, s in live:
+        a.free(x, s)
+    assert a.check() and a.stats()['bytes_in_use'] == 0

@@ -1210,8 +1210,55 @@ static __global__ void __launch_bounds__(256) splitk_reduce_vec_k(const float* _
   }
 }
 
+// Many slabs over a small output (weight gradients: thousands of outputs, 16-64 splits):
+// 8 thread groups per block take every 8th slab for 32 float4 outputs, so a thread has a
+// few independent loads instead of a chain of nz, and 8x more threads are in flight;
+// the 8 partials are folded through LDS.
+static __global__ void __launch_bounds__(256) splitk_reduce_grp_k(const float* __restrict__ slab, int64_t stride,
+                                                                 int nz, float* __restrict__ dst, int64_t M,
+                                                                 int64_t N, int64_t ldd, int accumulate) {
+  __shared__ float4 part[8][32];
+  const int o = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t n4 = N / 4, total4 = M * n4;
+  const int64_t i = (int64_t)blockIdx.x * 32 + o;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t m = 0, c = 0;
+  if (i < total4) {
+    m = i / n4;
+    c = (i - m * n4) * 4;
+    const float* base = slab + m * N + c;
+#pragma unroll 4
+    for (int z = g; z < nz; z += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(base + z * stride);
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+  }
+  part[g][o] = acc;
+  __syncthreads();
+  if (g == 0 && i < total4) {
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const float4 a = part[k][o];
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    float4* d = reinterpret_cast<float4*>(dst + m * ldd + c);
+    if (accumulate) {
+      const float4 od = *d;
+      acc.x += od.x; acc.y += od.y; acc.z += od.z; acc.w += od.w;
+    }
+    *d = acc;
+  }
+}
+
 static void launch_splitk_reduce(const float* slab, int splitk, void* C, int64_t M, int64_t N, int64_t ldc,
                                  int out_f32, int atomic, hipStream_t st) {
+  if (out_f32 && (N % 4) == 0 && (ldc % 4) == 0 && ((((uintptr_t)slab) | ((uintptr_t)C)) & 15) == 0 &&
+      splitk >= 8 && M * N / 4 <= (1 << 20)) {
+    const int64_t nb = (M * N / 4 + 31) / 32;
+    hipLaunchKernelGGL(splitk_reduce_grp_k, dim3((unsigned)nb), dim3(256), 0, st, slab, M * N, splitk, (float*)C, M,
+                       N, ldc, atomic);
+    return;
+  }
   if (out_f32 && (N % 4) == 0 && (ldc % 4) == 0 && ((((uintptr_t)slab) | ((uintptr_t)C)) & 15) == 0) {
     int nb = (int)std::min<int64_t>((M * N / 4 + 255) / 256, 4096);
     if (nb < 1) nb = 1;

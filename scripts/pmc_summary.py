@@ -24,7 +24,9 @@ import sys
 
 
 def family(name):
-    n = re.sub(r'\(.*', '', name)
+    n = name.replace('(anonymous namespace)::', '').replace('hetu::gemm::', '').replace('hetu::attn::', '')
+    n = n.replace('hetu::', '').replace('__hip_bfloat16', 'bf16').replace('HIP_vector_type<float, 4u>', 'float4')
+    n = re.sub(r'\(.*', '', n)
     n = re.sub(r'^void ', '', n)
     if n.startswith('igemm_'):
         return n.split('_gtcx')[0] + ' (MIOpen)'

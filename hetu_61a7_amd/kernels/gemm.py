@@ -221,13 +221,15 @@ def matmul_into(a, b, ta, tb, out):
         if A.dim() == 2:
             M, K, N = A.shape[0], A.shape[1], B.shape[1]
             tiles = -(-M // 128) * -(-N // 128)
-            for s in (2, 4, 8):
+            for s in (2, 3, 4, 6, 8):
                 if tiles * s <= 1536 and K // s >= 512:
                     cands['hip_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s))
             if M >= 256 and N >= 256:
                 cands['hip256'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=1)
                 t256 = -(-M // 256) * -(-N // 256)
-                for s in (2, 4, 8):
+                # one 256x256 block per CU: split counts that fill the 256 CUs in one round
+                # (36 tiles x 7 = 252 for BERT's FFN weight gradients) as well as the powers of 2
+                for s in (2, 3, 4, 5, 6, 7, 8):
                     if t256 * s <= 512 and K // s >= 1024:
                         cands['hip256_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=1))
             if K >= 2048:

@@ -71,7 +71,7 @@ class Dataloader(object):
         self._pending = None
         if device is not None and device.type == 'cuda':
             from .runtime import DeviceStream
-            self._dstream = DeviceStream(torch.device(device).index)   # framework-created prefetch stream
+            self._dstream = DeviceStream(torch.device(device).index, persistent=True)   # framework-created prefetch stream
             self._stream = self._dstream.torch
         self.initialized = True
 

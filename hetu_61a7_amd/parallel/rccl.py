@@ -130,7 +130,7 @@ class NativeComm(object):
         from ..runtime import DeviceStream
         # the comm stream: a framework-created high-priority HIP stream (torch sees its
         # ExternalStream view only for the allocator's record_stream bookkeeping)
-        self._dstream = DeviceStream(priority=-1)
+        self._dstream = DeviceStream(priority=-1, persistent=True)
         self.stream = self._dstream.torch
         self._bf16_ws = {}
 

@@ -54,7 +54,7 @@ def side_streams(device):
         from ..runtime import DeviceStream
         idx = torch.device(device).index
         idx = torch.cuda.current_device() if idx is None else idx
-        owned = (DeviceStream(idx), DeviceStream(idx))       # framework-created HIP streams
+        owned = (DeviceStream(idx, persistent=True), DeviceStream(idx, persistent=True))   # framework-created HIP streams
         s = _STREAMS[device] = (owned[0].torch, owned[1].torch)
         _OWNED.append(owned)
     return s

@@ -70,10 +70,17 @@ def _handle(stream):
     return stream.cuda_stream
 
 
-class DeviceStream(object):
-    """A HIP stream created by the framework (non-blocking, optional priority)."""
+_PERSISTENT = []   # streams that live as long as the process (see DeviceStream(persistent=True))
 
-    def __init__(self, device=None, priority=0):
+
+class DeviceStream(object):
+    """A HIP stream created by the framework (non-blocking, optional priority).
+    ``persistent``: never destroyed -- for streams tensors are ``record_stream``-ed on
+    (communicator, PS staging, prefetch): torch's caching allocator records events on such
+    a stream when those tensors are freed, possibly after the stream's owner is gone."""
+
+    def __init__(self, device=None, priority=0, persistent=False):
+        self.persistent = persistent
         self.device = torch.cuda.current_device() if device is None else int(device)
         h = ctypes.c_void_p()
         _check(lib().hetu_stream_create(self.device, int(priority), ctypes.byref(h)), 'stream create')
@@ -81,6 +88,8 @@ class DeviceStream(object):
         self.priority = priority
         self.torch = torch.cuda.ExternalStream(self.handle, device=torch.device('cuda', self.device))
         CREATED['streams'] += 1
+        if persistent:
+            _PERSISTENT.append(self)
 
     @property
     def cuda_stream(self):
@@ -103,7 +112,7 @@ class DeviceStream(object):
 
     def __del__(self):
         h = getattr(self, 'handle', None)
-        if h and _lib is not None and not _SHUTDOWN[0]:
+        if h and _lib is not None and not _SHUTDOWN[0] and not getattr(self, 'persistent', False):
             try:
                 lib().hetu_stream_sync(h)
                 lib().hetu_stream_destroy(h)

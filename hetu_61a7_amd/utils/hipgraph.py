@@ -84,7 +84,7 @@ class GraphRunner(object):
         from .. import memory_pool as MP
         from .. import runtime as RT
         dev = sub.config.device.index or 0
-        cap = RT.DeviceStream(dev)
+        cap = RT.DeviceStream(dev, persistent=True)
         cap.wait_stream(torch.cuda.current_stream())
         g = RT.Graph()
         self.pool = MP.capture_pool(dev)

@@ -12,15 +12,24 @@ Compute path: torch-ROCm tensors + hand-written HIP kernels for gfx950
 (``csrc/kernels``, loaded from ``hetu_61a7_amd/lib/libhetu_kernels.so``),
 RCCL over xGMI for collectives, a C++ host runtime for the parameter server,
 HET embedding cache, and a BFC allocator for HBM and pinned DRAM
-(``memory_pool``; ``HETU_ALLOCATOR=bfc`` makes it the process-wide device allocator).
+(``memory_pool``; the process-wide device allocator unless ``HETU_ALLOCATOR=torch``).
 """
 from __future__ import annotations
 
 import os as _os
 
-if _os.environ.get('HETU_ALLOCATOR', '') == 'bfc':   # before any device allocation
-    from .memory_pool import enable_torch_bfc as _enable_bfc
-    _enable_bfc()
+# The native BFC pool is the process-wide device allocator (HETU_ALLOCATOR=torch keeps
+# torch's caching allocator).  It must be installed before the first device allocation;
+# counting devices does not initialise the GPU.
+if _os.environ.get('HETU_ALLOCATOR', 'bfc') == 'bfc':
+    try:
+        import torch as _torch
+        if _torch.cuda.device_count() > 0:
+            from .memory_pool import enable_torch_bfc as _enable_bfc
+            _enable_bfc()
+    except Exception as _e:   # a device allocation happened before this import
+        import warnings as _warnings
+        _warnings.warn('hetu_61a7_amd: BFC device allocator not installed (%s); torch caching allocator in use' % (_e,))
 
 from .ops import *  # noqa: F401,F403
 from .ops import Executor, HetuConfig, gradients, Variable, placeholder_op

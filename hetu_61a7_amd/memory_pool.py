@@ -5,10 +5,11 @@ SURVEY §2.2 N2/N3, §2.1 P17).
 ``BFCAllocator`` wraps ``libhetu_alloc.so`` (C++): best-fit-with-coalescing
 over large hipMalloc / hipHostMalloc regions with stream-tagged free lists.
 
-* ``enable_torch_bfc()`` (or ``HETU_ALLOCATOR=bfc`` before the first device
-  allocation) installs the BFC allocator as the device allocator of the whole
-  process through ``torch.cuda.memory.CUDAPluggableAllocator``, so every tensor
-  the executor creates is carved from a few multi-GiB HBM regions.
+* ``enable_torch_bfc()`` -- called by ``import hetu_61a7_amd`` unless
+  ``HETU_ALLOCATOR=torch`` -- installs the BFC allocator as the device allocator of
+  the whole process through ``torch.cuda.memory.CUDAPluggableAllocator``, so every
+  tensor the executor creates is carved from a few multi-GiB HBM regions and torch's
+  caching allocator reserves nothing.
 * ``pinned_pool()`` is the process-wide pinned-DRAM pool used for PS / HET
   cache staging buffers (``pinned_empty``).
 * ``device_stats()`` mirrors the reference ``AllocatorStats``.

@@ -42,7 +42,7 @@ def _run(env_extra):
 
 
 def test_torch_bfc_allocator_training_matches_default():
-    base = _run({})
+    base = _run({'HETU_ALLOCATOR': 'torch'})
     bfc = _run({'HETU_ALLOCATOR': 'bfc', 'HETU_BFC_REGION_MB': '256'})
     np.testing.assert_allclose(base['losses'], bfc['losses'], rtol=1e-5, atol=1e-6)
     st = bfc['stats']
@@ -142,3 +142,15 @@ def test_pinned_pool_tensor_is_pinned_and_copies():
     back.copy_(d, non_blocking=True)
     torch.cuda.synchronize()
     assert torch.equal(back, t)
+
+
+def test_bfc_is_the_default_device_allocator():
+    """No HETU_ALLOCATOR: the package installs the BFC pool at import (this pytest process
+    imported it at collection, before any device allocation)."""
+    from hetu_61a7_amd import memory_pool as MP
+    if os.environ.get('HETU_ALLOCATOR', 'bfc') != 'bfc':
+        pytest.skip('HETU_ALLOCATOR overrides the default')
+    assert MP.torch_bfc_enabled()
+    x = torch.empty(1 << 20, device='cuda')
+    st = MP.device_stats(torch.cuda.current_device())
+    assert st['bytes_in_use'] >= x.numel() * 4 and st['bytes_reserved'] > 0

@@ -496,7 +496,20 @@ __global__ void __launch_bounds__(256) bn_bwd_sums_finalize(float* __restrict__ 
   cC[c] = -k1 * sdy * invM - mean[c] * B;
 }
 
-template <typename T, int RELU, bool DRES>
+// SUMS: the coefficients come straight from the epilogue totals (sums = S, Qx per
+// channel; see bn_bwd_sums_finalize) -- no finalize launch: every thread folds its own
+// channels, the first thread of each channel group writes dscale / dbias and clears that
+// group in ``znext`` (the other half of the double-buffered totals, consumed one call ago)
+struct BnSums {
+  const float* sums;
+  float* znext;
+  float* dscale;
+  float* dbias;
+  const float* scale;
+  int64_t M;
+};
+
+template <typename T, int RELU, bool DRES, bool SUMS = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ y,
                                                      const uint8_t* __restrict__ mask,
                                                      const T* __restrict__ x,
@@ -508,7 +521,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
                                                      const float* __restrict__ fmean,
                                                      const float* __restrict__ finvstd,
                                                      T* __restrict__ dx, T* __restrict__ dres,
-                                                     int64_t nvec, int C) {
+                                                     int64_t nvec, int C, BnSums bs = BnSums{}) {
   // channel-stationary threads (see bn_apply): per-channel coefficients live in
   // registers for the whole grid-stride loop
   constexpr int V = Vec<T>::N;
@@ -519,9 +532,31 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
   if (tid >= stride) return;
   const int c0 = (int)(tid % cv) * V;
   float A[V], Bc[V], Cc[V], ka[V], kb[V];
+  if (SUMS) {
+    const double invM = 1.0 / (double)bs.M;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const int c = c0 + k;
+      const double S = bs.sums[c], mu = fmean[c], is = finvstd[c];
+      const double sdyx = is * ((double)bs.sums[C + c] - mu * S);
+      const double k1 = (double)bs.scale[c] * is;
+      const double B = -k1 * is * sdyx * invM;
+      A[k] = (float)k1;
+      Bc[k] = (float)B;
+      Cc[k] = (float)(-k1 * S * invM - mu * B);
+      if (tid < cv) {
+        if (bs.dscale) bs.dscale[c] = (float)sdyx;
+        if (bs.dbias) bs.dbias[c] = (float)S;
+        if (bs.znext) {
+          bs.znext[c] = 0.f;
+          bs.znext[C + c] = 0.f;
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int k = 0; k < V; ++k) {
-    A[k] = cA[c0 + k]; Bc[k] = cB[c0 + k]; Cc[k] = cC[c0 + k];
+    if (!SUMS) { A[k] = cA[c0 + k]; Bc[k] = cB[c0 + k]; Cc[k] = cC[c0 + k]; }
     if (RELU == 2) {
       ka[k] = fscale[c0 + k] * finvstd[c0 + k];
       kb[k] = fbias[c0 + k] - fmean[c0 + k] * ka[k];
@@ -694,8 +729,20 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const uint8_
                           int64_t M, int C, const float* mean, const float* invstd,
                           const float* bias, float* w1, float* w2, float* cA,
                           float* cB, float* cC, const float* scale, float* dscale, float* dbias,
-                          float* bsums, hipStream_t st) {
+                          float* bsums, float* bnext, hipStream_t st) {
   constexpr int V = Vec<T>::N;
+  if (bsums && bnext) {   // coefficients folded in the apply kernel itself
+    int64_t nvec = M * C / V;
+    const int grid = bn_apply_grid(nvec, C, V);
+    BnSums bs{bsums, bnext, dscale, dbias, scale, M};
+    if (dres)
+      hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true, true>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB, cC,
+                         scale, bias, mean, invstd, dx, dres, nvec, C, bs);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false, true>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB,
+                         cC, scale, bias, mean, invstd, dx, dres, nvec, C, bs);
+    return;
+  }
   if (bsums) {
     hipLaunchKernelGGL(bn_bwd_sums_finalize, dim3((C + 255) / 256), dim3(256), 0, st, bsums, M, C, scale, mean,
                        invstd, dscale, dbias, cA, cB, cC);
@@ -719,7 +766,7 @@ template <typename T>
 static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
                        int64_t M, int C, const float* scale, const float* bias, const float* mean,
                        const float* invstd, float* dscale, float* dbias, float* ws, int relu,
-                       float* bsums, hipStream_t st) {
+                       float* bsums, float* bnext, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
@@ -734,10 +781,10 @@ static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const
   // otherwise recomputed from x and the folded forward affine (one less stream)
   // (or, with the forward's keep-bit mask, from that: 1/16 of the bytes of y)
   int mode = !relu ? 0 : (mask ? 3 : ((dres || !bias) ? 1 : 2));
-  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
-  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
-  else if (mode == 2) bn_bwd_launch<T, 2>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
-  else bn_bwd_launch<T, 3>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, st);
+  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
+  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
+  else if (mode == 2) bn_bwd_launch<T, 2>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
+  else bn_bwd_launch<T, 3>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
   HETU_LAUNCH_CHECK();
   return 0;
 }
@@ -746,16 +793,18 @@ static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const
 // bias may be null (then the ReLU mask is read from y); mask: hetu_bn_fwd's keep-bits.
 // bsums (nullable): [2C] totals sum(dy'), sum(dy' * x) already accumulated (by the
 // epilogue that produced dy, or hetu_bn_bwd_sums): the reduction pass is skipped and the
-// totals are zeroed
+// totals are zeroed.  bnext (nullable): the other half of double-buffered totals -- the
+// apply kernel then folds the coefficients itself (no finalize launch) and clears bnext
+// instead of bsums
 HETU_API int hetu_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres,
                          int64_t M, int C, int is_bf16, const float* scale, const float* bias,
                          const float* mean, const float* invstd, float* dscale, float* dbias,
-                         float* ws, int relu, const uint8_t* mask, float* bsums, hipStream_t st) {
+                         float* ws, int relu, const uint8_t* mask, float* bsums, float* bnext, hipStream_t st) {
   if (is_bf16)
     return bn_bwd_impl<bf16>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu,
-                             bsums, st);
+                             bsums, bnext, st);
   return bn_bwd_impl<float>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu,
-                            bsums, st);
+                            bsums, bnext, st);
 }
 
 // sums[0..C) += sum(dy'), sums[C..2C) += sum(dy' * x) over [M, C] bf16 rows, dy' = dy masked

@@ -114,14 +114,22 @@ class Conv2d_Gradient_of_DataOp(Op):
         if self.bn_fused is not None:
             xb, (_, aux) = input_vals[-2], input_vals[-1]
             if len(aux) > 2 or not self.bn_fused.relu:   # ReLU keep-bits (or no ReLU)
+                # persistent, double-buffered totals: call k accumulates into half k % 2 and
+                # the BN backward of call k zeroes the other half (consumed by call k - 1)
                 bufs = self.__dict__.setdefault('_bn_sums', {})
-                sums = bufs.get(xb.device)
-                if sums is None:   # persistent: the BN backward zeroes it after reading
-                    sums = bufs[xb.device] = torch.zeros(2 * xb.shape[1], dtype=torch.float32, device=xb.device)
-                bn = (sums, xb, aux[2] if len(aux) > 2 else None)
-        return KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,
-                                       acc_inplace=_may_overwrite(self, acc) and not self.acc_s2, bn=bn,
-                                       acc_s2=self.acc_s2 and acc is not None)
+                pair = bufs.get(xb.device)
+                if pair is None:
+                    pair = bufs[xb.device] = [torch.zeros(2 * xb.shape[1], dtype=torch.float32, device=xb.device)
+                                              for _ in range(2)] + [0]
+                k = pair[2]
+                pair[2] = k ^ 1
+                bn = (pair[k], xb, aux[2] if len(aux) > 2 else None)
+        r = KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,
+                                    acc_inplace=_may_overwrite(self, acc) and not self.acc_s2, bn=bn,
+                                    acc_s2=self.acc_s2 and acc is not None)
+        if bn is not None and getattr(r, 'hetu_bn_bsums', None) is not None:
+            r.hetu_bn_bsums_next = pair[pair[2]]
+        return r
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -382,22 +390,25 @@ class Batch_Normalization_GradientOp(Op):
         # the reduction totals of the data-gradient epilogue that produced g (fused: ops
         # Conv2d_Gradient_of_DataOp.bn_fused); the kernel zeroes them once read
         bsums = getattr(g, 'hetu_bn_bsums', None)
+        bnext = getattr(g, 'hetu_bn_bsums_next', None) if bsums is not None else None
         if bsums is not None and not (g.is_cuda and g.dtype == x.dtype == torch.bfloat16 and (mask is not None or not fw.relu)):
-            bsums.zero_()
-            bsums = None
+            bsums.zero_()         # not consumed: both halves ready for their next use
+            if bnext is not None:
+                bnext.zero_()
+            bsums = bnext = None
         if bsums is not None and getattr(g, 'hetu_bn_masked', False):
             # g was stored already masked by the ReLU keep-bits (dy'): no mask to apply,
             # and dy' itself is the gradient of the fused residual input
             dx, dscale, dbias, _ = KN.bn_backward(g, y, x, scale.float(), mean, invstd, relu=False,
                                                   want_dres=False, bias=bias, dscale_out=dests.get(1),
-                                                  dbias_out=dests.get(2), bsums=bsums)
+                                                  dbias_out=dests.get(2), bsums=bsums, bsums_next=bnext)
             # (a fresh tensor object over the same storage: g's hetu_bn_* attributes
             # belong to this BN and must not reach the consumer of the residual gradient)
             return (dx, dscale, dbias, g.detach() if fw.has_residual else None)
         dx, dscale, dbias, dres = KN.bn_backward(g, y, x, scale.float(), mean, invstd,
                                                  relu=fw.relu, want_dres=fw.has_residual, bias=bias,
                                                  dscale_out=dests.get(1), dbias_out=dests.get(2), mask=mask,
-                                                 bsums=bsums)
+                                                 bsums=bsums, bsums_next=bnext)
         return (dx, dscale, dbias, dres)
 
     def gradient(self, output_grad):

@@ -153,6 +153,18 @@ def test_bn_backward_from_epilogue_sums_matches_plain(relu, residual):
             assert a is None
             continue
         assert _rel(a, b) < 2e-3, _rel(a, b)
+    # double-buffered totals: coefficients folded in the apply kernel, the other half cleared
+    bs = torch.zeros(2 * C, device=DEV)
+    other = torch.randn(2 * C, device=DEV)
+    KN.bn_bwd_sums(dy, x, mask, bs)
+    out = KN.bn_backward(dy, y, x, sc, mean, invstd, relu=relu, want_dres=residual, bias=bi, mask=mask, bsums=bs,
+                         bsums_next=other)
+    assert torch.count_nonzero(other).item() == 0
+    for a, b in zip(out, ref):
+        if b is None:
+            assert a is None
+            continue
+        assert _rel(a, b) < 2e-3, _rel(a, b)
 
 
 def test_persistent_forward_sums_are_rezeroed():

@@ -594,6 +594,10 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
   }
 }
 
+// BNX: the BatchNorm-backward / subgrid-Cin extensions (Epi::bnx, bnmask, bnstore, cin_w)
+// are compiled in; the plain epilogue (forward convolutions, GEMMs) keeps its register
+// budget -- the 4-blocks-per-CU tile has 128 registers and spilled with them inlined
+template <bool BNX = true>
 __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (&v)[8], int64_t m, int64_t n,
                                          int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8],
                                          bool has_pre = false, uint4 pre = uint4{}) {
@@ -609,12 +613,12 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
   // they are in flight together with the Cin load below instead of one round trip each
   // after the store
   const int64_t off = orow * ep.ldc + n;
-  const bool bnv = ep.colstats && ep.bnx;
+  const bool bnv = BNX && ep.colstats && ep.bnx;
   uint4 bxr = make_uint4(0, 0, 0, 0);
   if (bnv && o.cvec && full) bxr = *reinterpret_cast<const uint4*>(ep.bnx + off);
   const unsigned bnmk = (bnv && ep.bnmask) ? (unsigned)ep.bnmask[off >> 3] : 0xffu;
   int64_t crow = orow;
-  if (o.Cinb && ep.cin_w) {   // stride-2 subgrid Cin: even (h, w) only
+  if (BNX && o.Cinb && ep.cin_w) {   // stride-2 subgrid Cin: even (h, w) only
     const uint32_t hw = (uint32_t)(ep.cin_h * ep.cin_w), o32 = (uint32_t)orow;   // rows < 2^31 (host check)
     const uint32_t img = o32 / hw, r = o32 - img * hw;
     const uint32_t h = r / (uint32_t)ep.cin_w, w = r - h * (uint32_t)ep.cin_w;
@@ -652,7 +656,7 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = act_f(v[t], ep.act);
   }
-  if (ep.bnstore) {
+  if (BNX && ep.bnstore) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = (bnmk >> t) & 1u ? v[t] : 0.f;
   }
@@ -726,8 +730,8 @@ __device__ __forceinline__ void lds_barrier() {
 // ST == 1 is also the high-occupancy form for short-K, memory-bound shapes (1x1 convolutions,
 // their gradient joins): one 32 KiB LDS buffer restaged per K-tile behind a barrier and at most
 // 128 VGPRs, so 4 blocks share a CU and hide each other's DMA / epilogue latency.
-template <class LA, class LB, int ST, int WN = 4>
-__global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
+template <class LA, class LB, int ST, int WN = 4, bool BNX = false>
+__global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                                      int64_t K, int tiles_m, int tiles_n, int ktps) {
   constexpr bool DB = ST >= 2;
   constexpr int TBN = 32 * WN;                 // block tile columns
@@ -824,7 +828,7 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
   // (not in the single-stage 4-blocks-per-CU build: at 128 registers the prefetch spills,
   // and its neighbours on the CU hide the epilogue latency instead)
   uint4 cpre[NPASS];
-  const bool use_pre = ST == 2 && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec && !ep.cin_w;
+  const bool use_pre = ST == 2 && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec && !(BNX && ep.cin_w);
   const int64_t pre_n = (int64_t)tn * TBN + ec;
   auto pre_load = [&](int h, int pss) {
     const int rr = pss * RPP + tid / TPR;
@@ -896,7 +900,7 @@ __global__ __launch_bounds__(NT, (ST == 1 ? 4 : 2)) void gemm_kernel(LA la, LB l
           v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec + 4);
 #pragma unroll
           for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
-          epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss]);
+          epi_row8<BNX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss]);
         }
         if (use_pre && half == 0) pre_load(1, pss);
       }
@@ -1153,7 +1157,7 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
 #pragma unroll
         for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
       }
-      epi_row8(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
+      epi_row8<true>(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
     }
     __syncthreads();
   }
@@ -1340,6 +1344,12 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
   return (int)hipGetLastError();
 }
 
+// loader pairs of the data-gradient launches (hetu_conv_dgrad_bf16): the only ones that
+// instantiate the BN-backward epilogue of the 128-row tiles
+template <class LA, class LB> struct bnx_pair : std::false_type {};
+template <bool KF, int NS> struct bnx_pair<BufK<KF, NS>, BufMN<KF, NS>> : std::true_type {};
+template <> struct bnx_pair<ConvDgradA, ConvDgradB> : std::true_type {};
+
 // tile: 0 = 128x128 (4 waves, 2 LDS stages, 2 blocks per CU), 1 = 256x256 (8 waves, 1 block
 // per CU), 2 = 128x64 (4 waves of 64x32; 64-channel convolutions), 3 = 128x128 single LDS
 // stage at 4 blocks per CU (short-K, memory-bound shapes), 5 = 128x96 (4 waves of 64x48).
@@ -1363,7 +1373,20 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
     e1.slab = nullptr;
     if (splitk > 1) e1.atomic = 1;
   }
-  if (ktps > 1 && !single_stage)
+  const bool bnx = ep.bnx || ep.cin_w;
+  if (bnx) {
+    // the BN-backward / subgrid-Cin epilogue: data-gradient loader pairs only
+    if constexpr (bnx_pair<LA, LB>::value) {
+      if (ktps > 1 && !single_stage)
+        hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                           tiles_n, ktps);
+      else
+        hipLaunchKernelGGL((gemm_kernel<LA, LB, 1, WN, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                           tiles_n, ktps);
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
+  } else if (ktps > 1 && !single_stage)
     hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n,
                        ktps);
   else

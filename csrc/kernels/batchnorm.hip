@@ -472,7 +472,8 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize(const float* __restrict__
 // bn_bwd_finalize from per-channel totals S = sum(dy'), Qx = sum(dy' * x) accumulated by
 // the data-gradient epilogue that produced dy (gemm_core.h Epi::bnx):
 // sum(dy' * xhat) = invstd * (Qx - mean * S).  The totals are zeroed once read.
-__global__ void __launch_bounds__(256) bn_bwd_sums_finalize(float* __restrict__ sums, int64_t M, int C,
+// sums: rep replicas [rep][2C] (see gemm_core.h Epi::cs_rep), folded here and all zeroed
+__global__ void __launch_bounds__(256) bn_bwd_sums_finalize(float* __restrict__ sums, int rep, int64_t M, int C,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -481,11 +482,17 @@ __global__ void __launch_bounds__(256) bn_bwd_sums_finalize(float* __restrict__ 
                                                            float* __restrict__ cC) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const float sdy = sums[c];
+  double S = 0.0, Q = 0.0;
+  for (int r = 0; r < rep; ++r) {
+    float* sr = sums + (int64_t)r * 2 * C;
+    S += sr[c];
+    Q += sr[C + c];
+    sr[c] = 0.f;
+    sr[C + c] = 0.f;
+  }
+  const float sdy = (float)S;
   const float is = invstd[c];
-  const float sdyx = (float)((double)is * ((double)sums[C + c] - (double)mean[c] * (double)sdy));
-  sums[c] = 0.f;
-  sums[C + c] = 0.f;
+  const float sdyx = (float)((double)is * (Q - (double)mean[c] * S));
   if (dscale) dscale[c] = sdyx;
   if (dbias) dbias[c] = sdy;
   const float invM = 1.f / (float)M;
@@ -729,9 +736,9 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const uint8_
                           int64_t M, int C, const float* mean, const float* invstd,
                           const float* bias, float* w1, float* w2, float* cA,
                           float* cB, float* cC, const float* scale, float* dscale, float* dbias,
-                          float* bsums, float* bnext, hipStream_t st) {
+                          float* bsums, float* bnext, int brep, hipStream_t st) {
   constexpr int V = Vec<T>::N;
-  if (bsums && bnext) {   // coefficients folded in the apply kernel itself
+  if (bsums && bnext && brep <= 1) {   // coefficients folded in the apply kernel itself
     int64_t nvec = M * C / V;
     const int grid = bn_apply_grid(nvec, C, V);
     BnSums bs{bsums, bnext, dscale, dbias, scale, M};
@@ -744,8 +751,8 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const uint8_
     return;
   }
   if (bsums) {
-    hipLaunchKernelGGL(bn_bwd_sums_finalize, dim3((C + 255) / 256), dim3(256), 0, st, bsums, M, C, scale, mean,
-                       invstd, dscale, dbias, cA, cB, cC);
+    hipLaunchKernelGGL(bn_bwd_sums_finalize, dim3((C + 255) / 256), dim3(256), 0, st, bsums, max(brep, 1), M, C,
+                       scale, mean, invstd, dscale, dbias, cA, cB, cC);
   } else {
     hipLaunchKernelGGL((bn_bwd_partial<T, RELU>), dim3(g.chunks, g.tiles), dim3(256), 0, st, dy, y, mask, x,
                        mean, invstd, scale, bias, M, C, g.W, g.RP, g.rows_per_chunk, w1, w2);
@@ -766,7 +773,7 @@ template <typename T>
 static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const void* x, void* dx, void* dres,
                        int64_t M, int C, const float* scale, const float* bias, const float* mean,
                        const float* invstd, float* dscale, float* dbias, float* ws, int relu,
-                       float* bsums, float* bnext, hipStream_t st) {
+                       float* bsums, float* bnext, int brep, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
@@ -781,10 +788,10 @@ static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const
   // otherwise recomputed from x and the folded forward affine (one less stream)
   // (or, with the forward's keep-bit mask, from that: 1/16 of the bytes of y)
   int mode = !relu ? 0 : (mask ? 3 : ((dres || !bias) ? 1 : 2));
-  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
-  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
-  else if (mode == 2) bn_bwd_launch<T, 2>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
-  else bn_bwd_launch<T, 3>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, st);
+  if (mode == 0) bn_bwd_launch<T, 0>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, brep, st);
+  else if (mode == 1) bn_bwd_launch<T, 1>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, brep, st);
+  else if (mode == 2) bn_bwd_launch<T, 2>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, brep, st);
+  else bn_bwd_launch<T, 3>(g, dyr, yr, mask, xr, dxr, drr, M, C, mean, invstd, bias, w1, w2, cA, cB, cC, scale, dscale, dbias, bsums, bnext, brep, st);
   HETU_LAUNCH_CHECK();
   return 0;
 }
@@ -795,16 +802,18 @@ static int bn_bwd_impl(const void* dy, const void* y, const uint8_t* mask, const
 // epilogue that produced dy, or hetu_bn_bwd_sums): the reduction pass is skipped and the
 // totals are zeroed.  bnext (nullable): the other half of double-buffered totals -- the
 // apply kernel then folds the coefficients itself (no finalize launch) and clears bnext
-// instead of bsums
+// instead of bsums.  brep: bsums holds that many replicas [brep][2C] (epilogue blocks spread
+// their atomics over them), folded by the finalize kernel (bnext is then not used)
 HETU_API int hetu_bn_bwd(const void* dy, const void* y, const void* x, void* dx, void* dres,
                          int64_t M, int C, int is_bf16, const float* scale, const float* bias,
                          const float* mean, const float* invstd, float* dscale, float* dbias,
-                         float* ws, int relu, const uint8_t* mask, float* bsums, float* bnext, hipStream_t st) {
+                         float* ws, int relu, const uint8_t* mask, float* bsums, float* bnext, int brep,
+                         hipStream_t st) {
   if (is_bf16)
     return bn_bwd_impl<bf16>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu,
-                             bsums, bnext, st);
+                             bsums, bnext, brep, st);
   return bn_bwd_impl<float>(dy, y, mask, x, dx, dres, M, C, scale, bias, mean, invstd, dscale, dbias, ws, relu,
-                            bsums, bnext, st);
+                            bsums, bnext, brep, st);
 }
 
 // sums[0..C) += sum(dy'), sums[C..2C) += sum(dy' * x) over [M, C] bf16 rows, dy' = dy masked

@@ -37,11 +37,12 @@ HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const flo
 // dx' = dx masked by bnmask (the ReLU keep-bits of the BatchNorm whose output the conv
 // reads; null = no ReLU) and bnx that BN's input [N,H,W,C]: the BN backward's reduction.
 // bnstore: dx is stored masked (dx'), the form the BN backward and a residual branch use.
+// bnrep: bnsums holds that many replicas ([bnrep][2C], see Epi::cs_rep).
 const int kBnAlign = 15;
 HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const void* acc,
                                   int acc_f32, int N, int H, int W, int C, int K, int KH, int KW,
                                   int sh, int sw, int ph, int pw, int tile, float* bnsums, const void* bnx,
-                                  const uint8_t* bnmask, int bnstore, int acc_s2, hipStream_t st) {
+                                  const uint8_t* bnmask, int bnstore, int acc_s2, int bnrep, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   if (bnsums && (!bnx || C % 8 || (((uintptr_t)bnx) & kBnAlign))) return (int)hipErrorInvalidValue;
   const bool plain1x1 = KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 &&
@@ -52,7 +53,7 @@ HETU_API int hetu_conv_dgrad_bf16(const void* dy, const void* w, void* dx, const
     return (int)hipErrorInvalidValue;
   Epi ep{dx, acc, nullptr, C, C, 0, 0, 1.f, acc ? 1.f : 0.f, 0, 0, acc_f32, 0, 0, nullptr, 0, bnsums,
          bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr, (bnsums && bnmask && bnstore) ? 1 : 0,
-         acc_s2 ? H : 0, acc_s2 ? W : 0};
+         acc_s2 ? H : 0, acc_s2 ? W : 0, bnsums ? bnrep : 0};
   if (plain1x1) {
     int64_t M = (int64_t)N * H * W;
     return K % BK == 0 ? launch_buf<true>((const bf16*)dy, (const bf16*)w, 1, 0, K, C, 0, 0, ep, M, C, K, 1, 1, st, tile)

@@ -33,6 +33,7 @@ struct BnB {
   const bf16* x;
   const uint8_t* mask;
   int store;   // store the masked gradient dx' (mask applied before the store)
+  int rep;     // colstats replicas ([rep][2 * channels]; see gemm_core.h Epi::cs_rep)
 };
 
 // mask bits of 4 channels at element offset e (co % 4 == 0), all-ones without a mask
@@ -266,7 +267,7 @@ __global__ __launch_bounds__((Geo<WD, TH>::NT), 1) void conv3x3_c64_k(const bf16
       const int which = tid / CH, co = tid % CH;
       float v = 0.f;
       for (int ww = 0; ww < G::NW; ++ww) v += red[(ww * 2 + which) * CH + co];
-      unsafeAtomicAdd(colstats + which * CH + co, v);
+      unsafeAtomicAdd(colstats + (bn.rep > 1 ? (n % bn.rep) * 2 * CH : 0) + which * CH + co, v);
     }
   }
 }
@@ -593,14 +594,15 @@ __global__ __launch_bounds__(256, 4) void conv3x3_wide_k(const bf16* __restrict_
         cs[i] += __shfl_xor(cs[i], o, 64);
         cq[i] += __shfl_xor(cq[i], o, 64);
       }
+    float* cst = colstats + (bn.rep > 1 ? (int64_t)(tile % bn.rep) * 2 * K : 0);
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int co = cob * WBN + (2 * wave + j) * 16 + 4 * q4 + i;
-          unsafeAtomicAdd(colstats + co, cs[j * 4 + i]);
-          unsafeAtomicAdd(colstats + K + co, cq[j * 4 + i]);
+          unsafeAtomicAdd(cst + co, cs[j * 4 + i]);
+          unsafeAtomicAdd(cst + K + co, cq[j * 4 + i]);
         }
     }
   }
@@ -797,10 +799,11 @@ HETU_API int hetu_conv3x3_c64_fwd(const void* x, const void* w, void* y, float* 
 // dx[N,H,W,64] = conv3x3^T(dy, w) (+ acc: bf16 or fp32 [N,H,W,64]); wt: 64*9*64 bf16 scratch.
 // bnsums (nullable, 128 fp32 pre-zeroed) += sum(dx') / sum(dx' * bnx) per channel, dx' = dx
 // masked by bnmask (see BnB): the reduction of the backward of the BN that produced x;
-// bnstore: dx is stored masked
+// bnstore: dx is stored masked; bnrep: bnsums holds that many replicas ([bnrep][128], block
+// of image n adds into replica n % bnrep)
 HETU_API int hetu_conv3x3_c64_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
                                     int N, int H, int W, float* bnsums, const void* bnx, const uint8_t* bnmask,
-                                    int bnstore, hipStream_t st) {
+                                    int bnstore, int bnrep, hipStream_t st) {
   if ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc) | ((uintptr_t)bnx)) & 15)
     return (int)hipErrorInvalidValue;
   if (bnsums && !bnx) return (int)hipErrorInvalidValue;
@@ -808,7 +811,7 @@ HETU_API int hetu_conv3x3_c64_dgrad(const void* dy, const void* w, void* wt, voi
   HETU_LAUNCH_CHECK();
   return dispatch_c64((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, bnsums,
                       BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr,
-                          (bnsums && bnmask && bnstore) ? 1 : 0},
+                          (bnsums && bnmask && bnstore) ? 1 : 0, bnsums ? bnrep : 0},
                       N, H, W, st);
 }
 
@@ -841,10 +844,10 @@ HETU_API int hetu_conv3x3_wide_fwd(const void* x, const void* w, void* y, float*
 }
 
 // dx[N,H,W,C] = conv3x3^T(dy[N,H,W,K], w) (+ acc), K % 64 == 0, C % 128 == 0; wt: C*9*K bf16;
-// bnsums / bnx / bnmask / bnstore as hetu_conv3x3_c64_dgrad (2*C floats)
+// bnsums / bnx / bnmask / bnstore / bnrep as hetu_conv3x3_c64_dgrad (bnrep * 2*C floats)
 HETU_API int hetu_conv3x3_wide_dgrad(const void* dy, const void* w, void* wt, void* dx, const void* acc, int acc_f32,
                                      int N, int H, int W, int C, int K, float* bnsums, const void* bnx,
-                                     const uint8_t* bnmask, int bnstore, hipStream_t st) {
+                                     const uint8_t* bnmask, int bnstore, int bnrep, hipStream_t st) {
   if (!wide_ok(K, C, H, W) ||
       ((((uintptr_t)dy) | ((uintptr_t)wt) | ((uintptr_t)dx) | ((uintptr_t)acc) | ((uintptr_t)bnx)) & 15))
     return (int)hipErrorInvalidValue;
@@ -855,7 +858,7 @@ HETU_API int hetu_conv3x3_wide_dgrad(const void* dy, const void* w, void* wt, vo
   HETU_LAUNCH_CHECK();
   return dispatch_wide((const bf16*)dy, (const bf16*)wt, (bf16*)dx, acc, acc_f32, bnsums,
                        BnB{bnsums ? (const bf16*)bnx : nullptr, bnsums ? bnmask : nullptr,
-                           (bnsums && bnmask && bnstore) ? 1 : 0},
+                           (bnsums && bnmask && bnstore) ? 1 : 0, bnsums ? bnrep : 0},
                        N, H, W, K, C, st);
 }
 

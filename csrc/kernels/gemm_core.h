@@ -500,6 +500,10 @@ struct Epi {
   // (n, h, w) adds Cin row (n, h/2, w/2) when h and w are even, nothing otherwise -- the
   // gradient of a 1x1 stride-2 downsample convolution joined without scattering it first
   int cin_h, cin_w;
+  // colstats replicas ([cs_rep][2N], 0/1 = one): block b adds into replica b % cs_rep -- a
+  // few thousand blocks adding into the same 2N addresses serialise on them (the
+  // consumer folds the replicas)
+  int cs_rep;
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -907,7 +911,8 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
       __syncthreads();
     }
     if (ep.colstats)
-      epilogue_colstats<TPR, 4>(cs, cq, stg, tid, (int64_t)tn * TBN, N, ep.colstats);
+      epilogue_colstats<TPR, 4>(cs, cq, stg, tid, (int64_t)tn * TBN, N,
+                                ep.colstats + (ep.cs_rep > 1 ? (int64_t)(blockIdx.x % ep.cs_rep) * 2 * N : 0));
     return;
   }
   // fp32 atomic accumulation (split-K without a slab / accumulate into C)
@@ -1161,7 +1166,9 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
     }
     __syncthreads();
   }
-  if (ep.colstats) epilogue_colstats<32, 8>(cs, cq, stg, tid, (int64_t)tn * BIG, N, ep.colstats);
+  if (ep.colstats)
+    epilogue_colstats<32, 8>(cs, cq, stg, tid, (int64_t)tn * BIG, N,
+                             ep.colstats + (ep.cs_rep > 1 ? (int64_t)(blockIdx.x % ep.cs_rep) * 2 * N : 0));
 }
 
 // dst[m][n] (ld ldd, fp32 or bf16) (+)= sum_z slab[z][m][n]

@@ -263,9 +263,15 @@ def _fuse_bn_backward_reduction(roots):
     per-channel reduction (sum(dy'), sum(dy' * x)), and the BN backward skips its own
     pass over dy and x.  The dgrad op gets the BN's input x and forward node (mean,
     invstd, ReLU keep-bits) as extra inputs; the BN forward keeps ReLU keep-bits.
-    Off under deterministic mode (fp32 atomics) or HETU_FUSE_BN_BWD=0."""
+    HETU_FUSE_BN_BWD=1 (default): only data gradients that join another gradient in their
+    epilogue -- those already wait on a Cin load per row piece, which the x / keep-bit
+    loads ride along with (ResNet-50 joins: -50..-160 us per layer); a store-only epilogue
+    pays a round trip per piece and loses to the separate reduction pass (+15..+90 us per
+    layer, profiles/bn_fusion_layers_r4.txt).  'all': every eligible one.  Off under
+    deterministic mode (fp32 atomics) or HETU_FUSE_BN_BWD=0."""
     from .kernels import deterministic
-    if os.environ.get('HETU_FUSE_BN_BWD', '1') != '1' or deterministic():
+    mode = os.environ.get('HETU_FUSE_BN_BWD', '1')
+    if mode not in ('1', 'all') or deterministic():
         return 0
     from .ops.nn import Conv2d_Gradient_of_DataOp, Batch_Normalization_GradientOp
     topo, cons = _consumers(roots)
@@ -276,7 +282,7 @@ def _fuse_bn_backward_reduction(roots):
             continue
         d, fw = n.inputs[0], n.forward_node
         if not isinstance(d, Conv2d_Gradient_of_DataOp) or d.bn_fused is not None or d in root_set or \
-                len(cons.get(d, [])) != 1 or len(d.inputs) not in (3, 4):
+                len(cons.get(d, [])) != 1 or len(d.inputs) not in ((3, 4) if mode == 'all' else (4,)):
             continue
         # same device group (a pipeline stage boundary between the BN and its consumer
         # convolution would make the forward node's aux a cross-stage input)

@@ -209,11 +209,11 @@ def try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=None, bnb=None
     a = acc.data_ptr() if acc is not None else None
     af = int(acc is not None and acc.dtype == torch.float32)
     if _c64(C, K, W):
-        f = fn('hetu_conv3x3_c64_dgrad', [P, P, P, P, P, I32, I32, I32, I32, P, P, P, I32, P])
+        f = fn('hetu_conv3x3_c64_dgrad', [P, P, P, P, P, I32, I32, I32, I32, P, P, P, I32, I32, P])
         check(f(g.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), a, af, N, H, W, *bn, stream_ptr()),
               'conv3x3_dgrad')
     else:
-        f = fn('hetu_conv3x3_wide_dgrad', [P, P, P, P, P, I32, I32, I32, I32, I32, I32, P, P, P, I32, P])
+        f = fn('hetu_conv3x3_wide_dgrad', [P, P, P, P, P, I32, I32, I32, I32, I32, I32, P, P, P, I32, I32, P])
         check(f(g.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), a, af, N, H, W, C, K, *bn,
                 stream_ptr()), 'conv3x3_wide_dgrad')
     record_native('conv3x3_dgrad')
@@ -289,20 +289,29 @@ def try_stem_backward_filter(g, x, w_shape, stride, padding, out=None, accumulat
 
 
 def _bnb_args(bnb, x_shape):
-    """(sums ptr, x ptr, mask ptr, store) of a BatchNorm-backward reduction fused into a
-    data-gradient epilogue: ``bnb`` = (sums [2C] fp32 zeroed, BN input x (bf16,
+    """(sums ptr, x ptr, mask ptr, store, replicas) of a BatchNorm-backward reduction fused
+    into a data-gradient epilogue: ``bnb`` = (sums [R * 2C] fp32 zeroed, BN input x (bf16,
     channels-last, the gradient's shape), ReLU keep-bit mask or None[, store]) -- store:
-    the gradient is stored masked; False when the operands do not fit the epilogue"""
+    the gradient is stored masked; R replicas of the [2C] totals spread the blocks'
+    atomics (bn_sum_replicas; the BN backward folds them); False when the operands do not
+    fit the epilogue"""
     if bnb is None:
-        return None, None, None, 0
+        return None, None, None, 0, 0
     sums, x, mask = bnb[:3]
     store = bool(bnb[3]) if len(bnb) > 3 else False
     N, C, H, W = x_shape
     if (tuple(x.shape) != tuple(x_shape) or x.dtype != torch.bfloat16 or not x.is_contiguous(memory_format=CL)
-            or x.data_ptr() % 16 or C % 8 or sums.numel() != 2 * C or sums.dtype != torch.float32
+            or x.data_ptr() % 16 or C % 8 or sums.numel() % (2 * C) or sums.dtype != torch.float32
             or (mask is not None and mask.numel() != x.numel() // 8)):
         return False
-    return sums.data_ptr(), x.data_ptr(), mask.data_ptr() if mask is not None else None, int(store and mask is not None)
+    return (sums.data_ptr(), x.data_ptr(), mask.data_ptr() if mask is not None else None, int(store and mask is not None),
+            sums.numel() // (2 * C))
+
+
+def bn_sum_replicas(M):
+    """replicas of the fused BN-backward totals for M gradient rows: about 64 blocks of 128
+    rows per replica (thousands of blocks adding into one [2C] serialise on it), at most 64"""
+    return max(1, min(64, M // 8192))
 
 
 def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0, bnb=None, acc_s2=False):
@@ -324,10 +333,10 @@ def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0, bnb=None
     N, C, H, W = x_shape
     K, _, KH, KW = w.shape
     dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
-    f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [I32, P, P, P, I32, I32, P])
+    f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [I32, P, P, P, I32, I32, I32, P])
     check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
             int(acc is not None and acc.dtype == torch.float32), N, H, W, C, K, KH, KW,
-            stride[0], stride[1], padding[0], padding[1], int(tile), *bn, int(acc_s2), stream_ptr()),
+            stride[0], stride[1], padding[0], padding[1], int(tile), *bn[:4], int(acc_s2), bn[4], stream_ptr()),
           'conv_dgrad')
     record_native('conv_dgrad')
     return dx.permute(0, 3, 1, 2)

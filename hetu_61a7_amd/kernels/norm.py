@@ -143,8 +143,9 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
                 dscale_out=None, dbias_out=None, mask=None, bsums=None, bsums_next=None):
     """Returns (dx, dscale, dbias, dres).  ``mask``: the forward's ReLU keep-bits
     (native path only; y is then not read).  ``bsums``: [2C] totals sum(dy') and
-    sum(dy' * x) already accumulated (the producing data-gradient epilogue); the
-    reduction pass is skipped and the totals are zeroed for their next use.
+    sum(dy' * x) already accumulated (the producing data-gradient epilogue), or [R * 2C]
+    replicas of them folded here; the reduction pass is skipped and the totals are zeroed
+    for their next use.
     ``bsums_next``: the other half of double-buffered totals -- the apply kernel folds the
     coefficients itself (no finalize launch) and zeroes ``bsums_next`` instead."""
     C = x.shape[1]
@@ -167,7 +168,7 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
             ws = _ws(M, C, is_bf16(x), x.device)
             if mask is not None:
                 assert relu and mask.dtype == torch.uint8 and mask.numel() == relu_mask_bytes(x)
-            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P, P, P, P])
+            f = fn('hetu_bn_bwd', [P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P, P, I32, P, P, P, I32, P])
             check(f(dy.data_ptr(), y.data_ptr() if (relu and mask is None) else None, x.data_ptr(),
                     dx.data_ptr(), dres.data_ptr() if dres is not None else None, M, C, is_bf16(x),
                     scale.data_ptr(), bias.float().contiguous().data_ptr() if bias is not None else None,
@@ -176,6 +177,7 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
                     mask.data_ptr() if mask is not None else None,
                     bsums.data_ptr() if bsums is not None else None,
                     bsums_next.data_ptr() if (bsums is not None and bsums_next is not None) else None,
+                    bsums.numel() // (2 * C) if bsums is not None else 1,
                     stream_ptr()),
                   'bn_bwd')
             return dx, dscale, dbias, dres

@@ -114,20 +114,27 @@ class Conv2d_Gradient_of_DataOp(Op):
         if self.bn_fused is not None:
             xb, (_, aux) = input_vals[-2], input_vals[-1]
             if len(aux) > 2 or not self.bn_fused.relu:   # ReLU keep-bits (or no ReLU)
-                # persistent, double-buffered totals: call k accumulates into half k % 2 and
-                # the BN backward of call k zeroes the other half (consumed by call k - 1)
+                # persistent totals, R replicas (conv_igemm.bn_sum_replicas).  R == 1:
+                # double-buffered -- call k accumulates into half k % 2 and the BN backward
+                # of call k folds its coefficients in the apply kernel and zeroes the other
+                # half (consumed by call k - 1); R > 1: one buffer, folded and zeroed by the
+                # BN backward's finalize kernel
+                from ..kernels.conv_igemm import bn_sum_replicas
+                rep = bn_sum_replicas(xb.numel() // xb.shape[1])
                 bufs = self.__dict__.setdefault('_bn_sums', {})
-                pair = bufs.get(xb.device)
+                pair = bufs.get((xb.device, rep))
                 if pair is None:
-                    pair = bufs[xb.device] = [torch.zeros(2 * xb.shape[1], dtype=torch.float32, device=xb.device)
-                                              for _ in range(2)] + [0]
-                k = pair[2]
-                pair[2] = k ^ 1
+                    pair = bufs[(xb.device, rep)] = [torch.zeros(rep * 2 * xb.shape[1], dtype=torch.float32,
+                                                                 device=xb.device) for _ in range(2 if rep == 1 else 1)]
+                    pair.append(0)
+                k = pair[-1]
+                if rep == 1:
+                    pair[-1] = k ^ 1
                 bn = (pair[k], xb, aux[2] if len(aux) > 2 else None)
         r = KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,
                                     acc_inplace=_may_overwrite(self, acc) and not self.acc_s2, bn=bn,
                                     acc_s2=self.acc_s2 and acc is not None)
-        if bn is not None and getattr(r, 'hetu_bn_bsums', None) is not None:
+        if bn is not None and getattr(r, 'hetu_bn_bsums', None) is not None and len(pair) == 3:
             r.hetu_bn_bsums_next = pair[pair[2]]
         return r
 

@@ -9,10 +9,10 @@ S=scripts/gpu_step.sh
 bash $S tests ${TESTS_TIMEOUT:-500} python -u -m pytest -x -q --timeout ${PYTEST_TIMEOUT:-120} --timeout-method thread -m gpu \
   ${TESTS:-tests/test_bn_fusion_gpu.py tests/test_runtime_gpu.py tests/test_gemm_gpu.py tests/test_stem_gpu.py tests/test_native_dispatch_gpu.py tests/test_rccl_gpu.py} || exit $?
 grep -q " passed" gpurun_out/tests.log && ! grep -q -E "[0-9]+ failed|[0-9]+ error" gpurun_out/tests.log || { echo "TESTS FAILED"; exit 1; }
-for v in ${VARIANTS:-"1 1" "1 0" "0 0"}; do
-  set -- $v
-  HETU_FUSE_BN_BWD=$1 HETU_FUSE_BN_STATS=$2 HETU_AUTOTUNE_DUMP=gpurun_out/at_resnet50_bn$1$2.txt \
-    bash $S b_resnet50_bn$1$2 300 python bench.py --model resnet50 --steps 20 --warmup 5 || exit $?
+for v in ${VARIANTS:-1_1 1_0 0_0}; do   # <bwd fusion>_<fwd stats fusion>
+  a=${v%_*}; b=${v#*_}
+  HETU_FUSE_BN_BWD=$a HETU_FUSE_BN_STATS=$b HETU_AUTOTUNE_DUMP=gpurun_out/at_resnet50_bn$a$b.txt \
+    bash $S b_resnet50_bn$a$b 300 python bench.py --model resnet50 --steps 20 --warmup 5 || exit $?
 done
 if [ -n "${BERT:-1}" ]; then
   HETU_AUTOTUNE_DUMP=gpurun_out/at_bert_r4.txt bash $S b_bert 300 python bench.py --model bert --steps 20 --warmup 5 || exit $?

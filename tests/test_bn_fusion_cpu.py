@@ -29,7 +29,7 @@ def _bottleneck_net(x, y_):
 def _train(fuse, steps=3, s2=True, net=None):
     from hetu_61a7_amd.models import resnet18
     from hetu_61a7_amd.ops import node as _node
-    os.environ['HETU_FUSE_BN_BWD'] = '1' if fuse else '0'
+    os.environ['HETU_FUSE_BN_BWD'] = fuse if isinstance(fuse, str) else ('1' if fuse else '0')
     os.environ['HETU_S2_JOIN'] = '1' if s2 else '0'
     try:
         _node.G_NODE_ID = 0
@@ -60,6 +60,12 @@ def test_bn_backward_reduction_graph_rewrite():
         assert n.inputs[-1] is n.bn_fused and n.value_and_aux_inputs == (len(n.inputs) - 1,)
         assert isinstance(n.bn_fused, Batch_NormalizationOp) and n.bn_fused.bwd_fused
     np.testing.assert_allclose(base, fused, rtol=1e-6, atol=1e-6)
+    # default: only data gradients that join another gradient (4th input) take it
+    assert all(len(n.inputs) == 6 for n in fz), [len(n.inputs) for n in fz]
+    every, nodes_all = _train('all')
+    fa = [n for n in nodes_all if isinstance(n, Conv2d_Gradient_of_DataOp) and n.bn_fused is not None]
+    assert len(fa) > len(fz) and any(len(n.inputs) == 5 for n in fa)
+    np.testing.assert_allclose(base, every, rtol=1e-6, atol=1e-6)
 
 
 def test_downsample_join_on_the_subgrid():

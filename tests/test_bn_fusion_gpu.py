@@ -56,7 +56,11 @@ CASES = [
 @pytest.mark.parametrize('case', CASES, ids=lambda c: '%s-%s-%s' % (c[1], c[5][0], c[5][1]))
 @pytest.mark.parametrize('masked', [True, False])
 @pytest.mark.parametrize('join', [False, True])
-def test_dgrad_epilogue_bn_sums(case, masked, join):
+@pytest.mark.parametrize('reps', [1, 3])
+def test_dgrad_epilogue_bn_sums(case, masked, join, reps):
+    """the BN-backward reduction in the data-gradient epilogue against the fp32 reference
+    sums of the stored gradient; reps > 1: the totals spread over that many replicas
+    (Epi::cs_rep), whose sum is the total"""
     gs, ws, xs, s, p, (kind, tile) = case
     torch.manual_seed(0)
     g = torch.randn(gs, device=DEV).bfloat16().contiguous(memory_format=CL)
@@ -65,7 +69,7 @@ def test_dgrad_epilogue_bn_sums(case, masked, join):
     acc = torch.randn(xs, device=DEV).bfloat16().contiguous(memory_format=CL) if join else None
     n = xb.numel() // 8
     mask = torch.randint(0, 256, (n,), device=DEV, dtype=torch.int32).to(torch.uint8) if masked else None
-    sums = torch.zeros(2 * xs[1], device=DEV)
+    sums = torch.zeros(reps * 2 * xs[1], device=DEV)
     if kind == 'gemm':
         dx = CI.try_backward_data(g, w, xs, (s, s), (p, p), acc=acc, tile=tile, bnb=(sums, xb, mask))
         dx0 = CI.try_backward_data(g, w, xs, (s, s), (p, p), acc=acc, tile=tile)
@@ -76,17 +80,20 @@ def test_dgrad_epilogue_bn_sums(case, masked, join):
     assert torch.equal(dx, dx0)     # the statistics do not perturb the stored gradient
     rs, rq = _ref_sums(dx, xb, mask)
     C = xs[1]
+    if reps > 1 and xs[2] > 7:   # (2 images of 7x7 are one pixel tile of the wide kernel)
+        assert torch.count_nonzero(sums[2 * C:]).item() > 0   # the replicas were used
+    sums = sums.view(reps, 2 * C).sum(0)
     assert _rel(sums[:C], rs) < 1e-4, (_rel(sums[:C], rs))
     assert _rel(sums[C:], rq) < 1e-4, (_rel(sums[C:], rq))
     if masked:   # masked store: dx' = dx * keep-bits, same statistics
-        s2 = torch.zeros_like(sums)
+        s2 = torch.zeros(reps * 2 * C, device=DEV)
         if kind == 'gemm':
             dm = CI.try_backward_data(g, w, xs, (s, s), (p, p), acc=acc, tile=tile, bnb=(s2, xb, mask, True))
         else:
             dm = CI.try_conv3x3_backward_data(g, w, xs, (s, s), (p, p), acc=acc, bnb=(s2, xb, mask, True))
         bits = _bits(mask, dx.permute(0, 2, 3, 1).shape)
         assert torch.equal(dm.permute(0, 2, 3, 1).float(), dx.permute(0, 2, 3, 1).float() * bits)
-        assert _rel(s2, sums) < 1e-5
+        assert _rel(s2.view(reps, 2 * C).sum(0), sums) < 1e-5
 
 
 @pytest.mark.parametrize('tile', [0, 1, 2, 3])
@@ -153,6 +160,20 @@ def test_bn_backward_from_epilogue_sums_matches_plain(relu, residual):
             assert a is None
             continue
         assert _rel(a, b) < 2e-3, _rel(a, b)
+    # replicated totals ([R][2C], the first holding the sums, the others partial zeros and
+    # garbage that cancels): folded by the finalize kernel, all zeroed
+    bs = torch.zeros(3 * 2 * C, device=DEV)
+    KN.bn_bwd_sums(dy, x, mask, bs)
+    d = torch.randn(2 * C, device=DEV)
+    bs[2 * C:4 * C] += d
+    bs[4 * C:] -= d
+    out = KN.bn_backward(dy, y, x, sc, mean, invstd, relu=relu, want_dres=residual, bias=bi, mask=mask, bsums=bs)
+    assert torch.count_nonzero(bs).item() == 0
+    for a, b in zip(out, ref):
+        if b is None:
+            assert a is None
+            continue
+        assert _rel(a, b) < 2e-3, _rel(a, b)
     # double-buffered totals: coefficients folded in the apply kernel, the other half cleared
     bs = torch.zeros(2 * C, device=DEV)
     other = torch.randn(2 * C, device=DEV)
@@ -190,7 +211,7 @@ def _resnet_step(fuse_bwd, fuse_stats):
     from hetu_61a7_amd.models import resnet50_imagenet
     from hetu_61a7_amd.ops import node as _node
     _node.G_NODE_ID = 0      # same node ids -> same names and initial weights in both graphs
-    os.environ['HETU_FUSE_BN_BWD'] = '1' if fuse_bwd else '0'
+    os.environ['HETU_FUSE_BN_BWD'] = fuse_bwd if isinstance(fuse_bwd, str) else ('1' if fuse_bwd else '0')
     os.environ['HETU_FUSE_BN_STATS'] = '1' if fuse_stats else '0'
     try:
         B = 4
@@ -214,13 +235,15 @@ def _resnet_step(fuse_bwd, fuse_stats):
         os.environ.pop('HETU_FUSE_BN_STATS', None)
 
 
-def test_resnet50_gradients_with_fused_bn_backward_match_unfused():
+@pytest.mark.parametrize('mode,min_fused', [('1', 16), ('all', 40)])
+def test_resnet50_gradients_with_fused_bn_backward_match_unfused(mode, min_fused):
     """One SGD step of ResNet-50 with the BN-backward reductions in the dgrad epilogues
     (and the masked gradient store) updates every parameter as the unfused graph does,
-    to bf16 accuracy; the forward is untouched."""
+    to bf16 accuracy; the forward is untouched.  mode '1': the joined data gradients only
+    (one per bottleneck), 'all': every eligible one."""
     l0, d0, _ = _resnet_step(False, False)
-    l1, d1, nf = _resnet_step(True, False)
-    assert nf >= 40, nf
+    l1, d1, nf = _resnet_step(mode, False)
+    assert nf >= min_fused, nf
     assert l0 == l1
     num = sum(float((d1[k] - d0[k]).norm()) ** 2 for k in d0)
     den = sum(float(d0[k].norm()) ** 2 for k in d0)

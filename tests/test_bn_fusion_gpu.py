@@ -235,12 +235,13 @@ def _resnet_step(fuse_bwd, fuse_stats):
         os.environ.pop('HETU_FUSE_BN_STATS', None)
 
 
-@pytest.mark.parametrize('mode,min_fused', [('1', 16), ('all', 40)])
+@pytest.mark.parametrize('mode,min_fused', [('1', 15), ('all', 40)])
 def test_resnet50_gradients_with_fused_bn_backward_match_unfused(mode, min_fused):
     """One SGD step of ResNet-50 with the BN-backward reductions in the dgrad epilogues
     (and the masked gradient store) updates every parameter as the unfused graph does,
     to bf16 accuracy; the forward is untouched.  mode '1': the joined data gradients only
-    (one per bottleneck), 'all': every eligible one."""
+    (one per bottleneck past the first, whose input is the max-pool output), 'all': every
+    eligible one."""
     l0, d0, _ = _resnet_step(False, False)
     l1, d1, nf = _resnet_step(mode, False)
     assert nf >= min_fused, nf

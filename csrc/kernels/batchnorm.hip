@@ -167,7 +167,37 @@ __global__ void __launch_bounds__(256) bn_stats_finalize(const float* __restrict
 // the convolution epilogue that produced x (gemm.hip colstats) or by bn_sums_merge.
 // The totals are zeroed once read: a persistent per-layer buffer is ready for the next
 // accumulation without a fill launch.
-__global__ void __launch_bounds__(256) bn_sums_finalize(float* __restrict__ sums, int64_t M, int C,
+// S, Q = sums over the rep replicas ([rep][2C]) of channel c, then the replicas zeroed: all
+// loads first (in flight together), the stores after -- interleaved, each load waited
+// behind the previous store
+__device__ __forceinline__ void fold_replicas(float* __restrict__ sums, int rep, int C, int c, double& S,
+                                              double& Q) {
+  int r = 0;
+  for (; r + 8 <= rep; r += 8) {
+    float a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a[k] = sums[(int64_t)(r + k) * 2 * C + c];
+      b[k] = sums[(int64_t)(r + k) * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      S += a[k];
+      Q += b[k];
+    }
+  }
+  for (; r < rep; ++r) {
+    S += sums[(int64_t)r * 2 * C + c];
+    Q += sums[(int64_t)r * 2 * C + C + c];
+  }
+  for (r = 0; r < rep; ++r) {
+    sums[(int64_t)r * 2 * C + c] = 0.f;
+    sums[(int64_t)r * 2 * C + C + c] = 0.f;
+  }
+}
+
+// sums: rep replicas [rep][2C] of the per-channel sum / sum of squares, folded and zeroed
+__global__ void __launch_bounds__(256) bn_sums_finalize(float* __restrict__ sums, int rep, int64_t M, int C,
                                  const float* __restrict__ scale, const float* __restrict__ bias,
                                  float* __restrict__ run_mean, float* __restrict__ run_var,
                                  float factor, float eps, float* __restrict__ save_mean,
@@ -176,10 +206,10 @@ __global__ void __launch_bounds__(256) bn_sums_finalize(float* __restrict__ sums
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double n = (double)M;
-  const double mean = (double)sums[c] / n;
-  double var = (double)sums[C + c] / n - mean * mean;
-  sums[c] = 0.f;
-  sums[C + c] = 0.f;
+  double S = 0.0, Q = 0.0;
+  fold_replicas(sums, rep, C, c, S, Q);
+  const double mean = S / n;
+  double var = Q / n - mean * mean;
   if (var < 0.0) var = 0.0;
   const float invstd = rsqrtf((float)var + eps);
   save_mean[c] = (float)mean;
@@ -483,13 +513,7 @@ __global__ void __launch_bounds__(256) bn_bwd_sums_finalize(float* __restrict__ 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double S = 0.0, Q = 0.0;
-  for (int r = 0; r < rep; ++r) {
-    float* sr = sums + (int64_t)r * 2 * C;
-    S += sr[c];
-    Q += sr[C + c];
-    sr[c] = 0.f;
-    sr[C + c] = 0.f;
-  }
+  fold_replicas(sums, rep, C, c, S, Q);
   const float sdy = (float)S;
   const float is = invstd[c];
   const float sdyx = (float)((double)is * (Q - (double)mean[c] * S));
@@ -657,14 +681,14 @@ template <typename T>
 static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                        const float* bias, float* run_mean, float* run_var, float factor, float eps,
                        float* save_mean, float* save_invstd, float* ws, int relu, int training,
-                       float* sums, uint8_t* mask, hipStream_t st) {
+                       float* sums, uint8_t* mask, int srep, hipStream_t st) {
   constexpr int V = Vec<T>::N;
   if (C % V != 0) return (int)hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C, V);
   float* fa = ws + 2 * (int64_t)g.chunks * C;
   float* fb = fa + C;
   if (training && sums) {   // statistics already reduced (fused into the producer)
-    hipLaunchKernelGGL(bn_sums_finalize, dim3((C + 255) / 256), dim3(256), 0, st, sums, M, C, scale,
+    hipLaunchKernelGGL(bn_sums_finalize, dim3((C + 255) / 256), dim3(256), 0, st, sums, max(srep, 1), M, C, scale,
                        bias, run_mean, run_var, factor, eps, save_mean, save_invstd, fa, fb);
   } else if (training) {
     float* wm = ws;
@@ -704,12 +728,12 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
 HETU_API int hetu_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int is_bf16,
                          const float* scale, const float* bias, float* run_mean, float* run_var,
                          float factor, float eps, float* save_mean, float* save_invstd, float* ws,
-                         int relu, int training, float* sums, uint8_t* mask, hipStream_t st) {
+                         int relu, int training, float* sums, uint8_t* mask, int srep, hipStream_t st) {
   if (is_bf16)
     return bn_fwd_impl<bf16>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
-                             save_mean, save_invstd, ws, relu, training, sums, mask, st);
+                             save_mean, save_invstd, ws, relu, training, sums, mask, srep, st);
   return bn_fwd_impl<float>(x, res, y, M, C, scale, bias, run_mean, run_var, factor, eps,
-                            save_mean, save_invstd, ws, relu, training, sums, mask, st);
+                            save_mean, save_invstd, ws, relu, training, sums, mask, srep, st);
 }
 
 // sums[0..C) / sums[C..2C) = per-channel sum / sum of squares of x [M, C] (fp64 merge)

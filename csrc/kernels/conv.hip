@@ -12,13 +12,15 @@ using namespace hetu::gemm;
 
 // y[N,OH,OW,K] (NHWC) = conv(x[N,H,W,C] NHWC, w[K,KH,KW,C]) (+bias[K]) -> act.  C % 8 == 0.
 // colstats (optional, 2*K floats, zeroed by the caller) += per-channel sum and sum of
-// squares of the stored y: the statistics a training-mode BatchNorm on y needs.
+// squares of the stored y: the statistics a training-mode BatchNorm on y needs; csrep:
+// colstats holds that many replicas ([csrep][2K], Epi::cs_rep).
 HETU_API int hetu_conv_fwd_bf16(const void* x, const void* w, void* y, const float* bias, int N,
                                 int H, int W, int C, int K, int KH, int KW, int sh, int sw, int ph,
-                                int pw, int act, float* colstats, int tile, hipStream_t st) {
+                                int pw, int act, float* colstats, int tile, int csrep, hipStream_t st) {
   ConvGeom g = geom(N, H, W, C, K, KH, KW, sh, sw, ph, pw);
   int64_t M = (int64_t)N * g.OH * g.OW, Kt = (int64_t)KH * KW * C;
   Epi ep{y, nullptr, bias, K, 0, 0, 0, 1.f, 0.f, act, 0, 0, 0, 0, nullptr, 0, colstats};
+  ep.cs_rep = colstats ? csrep : 0;
   if (KH == 1 && KW == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && buf_ok(M * C * 2, (int64_t)K * C * 2))
     return C % BK == 0 ? launch_buf<true>((const bf16*)x, (const bf16*)w, 1, 1, C, C, 0, 0, ep, M, K, C, 1, 1, st, tile)
                        : launch_buf<false>((const bf16*)x, (const bf16*)w, 1, 1, C, C, 0, 0, ep, M, K, C, 1, 1, st, tile);

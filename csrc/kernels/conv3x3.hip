@@ -789,11 +789,13 @@ bool wide_wgrad_ok(int C, int K, int H, int W) {
 HETU_API int hetu_conv3x3_c64_supported(int C, int K, int W) { return C == CH && K == CH && W == 56; }
 
 // y[N,H,W,64] = conv3x3(x[N,H,W,64], w[64][3][3][64]), stride 1, pad 1 (NHWC bf16);
-// colstats (nullable, 128 fp32 pre-zeroed) += per-channel sum / sum of squares of y
+// colstats (nullable, csrep x 128 fp32 pre-zeroed) += per-channel sum / sum of squares of y
+// (image n into replica n % csrep)
 HETU_API int hetu_conv3x3_c64_fwd(const void* x, const void* w, void* y, float* colstats, int N, int H, int W,
-                                  hipStream_t st) {
+                                  int csrep, hipStream_t st) {
   if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)y)) & 15) return (int)hipErrorInvalidValue;
-  return dispatch_c64((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, BnB{}, N, H, W, st);
+  return dispatch_c64((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, BnB{nullptr, nullptr, 0, csrep},
+                      N, H, W, st);
 }
 
 // dx[N,H,W,64] = conv3x3^T(dy, w) (+ acc: bf16 or fp32 [N,H,W,64]); wt: 64*9*64 bf16 scratch.
@@ -836,11 +838,13 @@ HETU_API int hetu_conv3x3_c64_wgrad(const void* x, const void* dy, float* dw, fl
 HETU_API int hetu_conv3x3_wide_supported(int C, int K, int H, int W) { return wide_ok(C, K, H, W); }
 
 // y[N,H,W,K] = conv3x3(x[N,H,W,C], w[K][3][3][C]) (stride 1, pad 1), C % 64 == 0, K % 128 == 0
+// (colstats: csrep replicas of [2K], pixel tile t into replica t % csrep)
 HETU_API int hetu_conv3x3_wide_fwd(const void* x, const void* w, void* y, float* colstats, int N, int H, int W, int C,
-                                   int K, hipStream_t st) {
+                                   int K, int csrep, hipStream_t st) {
   if (!wide_ok(C, K, H, W) || ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)y)) & 15))
     return (int)hipErrorInvalidValue;
-  return dispatch_wide((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, BnB{}, N, H, W, C, K, st);
+  return dispatch_wide((const bf16*)x, (const bf16*)w, (bf16*)y, nullptr, 0, colstats, BnB{nullptr, nullptr, 0, csrep},
+                       N, H, W, C, K, st);
 }
 
 // dx[N,H,W,C] = conv3x3^T(dy[N,H,W,K], w) (+ acc), K % 64 == 0, C % 128 == 0; wt: C*9*K bf16;

@@ -45,9 +45,9 @@ __global__ void __launch_bounds__(256) stem_pack_w_k(const bf16* __restrict__ w,
 }
 
 __global__ void __launch_bounds__(256) stem_fwd_k(const bf16* __restrict__ x, const bf16* __restrict__ wp,
-                                                  bf16* __restrict__ y, float* __restrict__ colstats, int H, int W,
-                                                  int C, int KH, int KW, int s, int p, int OH, int OW, int KS,
-                                                  int RS) {
+                                                  bf16* __restrict__ y, float* __restrict__ colstats, int csrep,
+                                                  int H, int W, int C, int KH, int KW, int s, int p, int OH, int OW,
+                                                  int KS, int RS) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* patch = reinterpret_cast<bf16*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) stem_fwd_k(const bf16* __restrict__ x, co
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) v += red[(w * 2 + which) * CO + co];
-      unsafeAtomicAdd(colstats + which * CO + co, v);
+      unsafeAtomicAdd(colstats + (csrep > 1 ? (int)(blockIdx.x % csrep) * 2 * CO : 0) + which * CO + co, v);
     }
   }
 }
@@ -359,10 +359,10 @@ __global__ void __launch_bounds__(256) stem_wgrad_reduce_k(const float* __restri
 HETU_API int64_t hetu_stem_wp_elems(int KH) { return (int64_t)CO * 32 * ((KH * SEG + 31) / 32); }
 
 // x [N][H][W][C] bf16 (channels-last), w [64][KH][KW][C] bf16, y [N][OH][OW][64] bf16;
-// colstats (nullable) [2*64] fp32, pre-zeroed.  Requires KW*C <= 24, s*C even (4-byte
-// fragment reads), KH*24 <= 32*6.
+// colstats (nullable) [csrep][2*64] fp32, pre-zeroed (block b adds into replica b % csrep).
+// Requires KW*C <= 24, s*C even (4-byte fragment reads), KH*24 <= 32*6.
 HETU_API int hetu_stem_fwd(const void* x, const void* w, void* wp, void* y, float* colstats, int N, int H, int W,
-                           int C, int KH, int KW, int s, int p, hipStream_t st) {
+                           int C, int KH, int KW, int s, int p, int csrep, hipStream_t st) {
   if (KW * C > SEG || (s * C) % 2 || KH * SEG > 32 * MAXKS || N <= 0) return (int)hipErrorInvalidValue;
   const int OH = (H + 2 * p - KH) / s + 1, OW = (W + 2 * p - KW) / s + 1;
   const int KS = (KH * SEG + 31) / 32, KP = KS * 32;
@@ -376,7 +376,7 @@ HETU_API int hetu_stem_fwd(const void* x, const void* w, void* wp, void* y, floa
                      KW, C, KP);
   const int blocks = N * ((OH + R - 1) / R);
   hipLaunchKernelGGL(stem_fwd_k, dim3(blocks), dim3(256), lds, st, (const bf16*)x, (const bf16*)wp, (bf16*)y,
-                     colstats, H, W, C, KH, KW, s, p, OH, OW, KS, RS);
+                     colstats, csrep, H, W, C, KH, KW, s, p, OH, OW, KS, RS);
   return (int)hipGetLastError();
 }
 

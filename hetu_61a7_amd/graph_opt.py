@@ -7,7 +7,7 @@ Rewrites (in place, preserving the identity of the user-visible output node):
   batch_norm(conv2d(x, w))        -> the conv epilogue also emits the per-channel
                                      sum / sum of squares of its output, so the BN
                                      skips its statistics pass (training mode;
-                                     opt-in, HETU_FUSE_BN_STATS=1)
+                                     HETU_FUSE_BN_STATS=0 turns it off)
 These are the memory-bound op chains that dominate ResNet time outside the
 convolutions; the reference runs each as its own cuDNN/elementwise call.
 Only applied when the intermediate values have no other consumer.
@@ -69,11 +69,13 @@ def fuse_forward(roots):
                     break
     # conv -> BatchNorm: the conv hands the BN the statistics of its output (computed
     # in the conv epilogue), removing the BN's separate statistics pass over it
-    # opt-in: measured neutral on ResNet-50 bs256 (8082-8091 img/s with, 8106-8145
-    # without, same box): the per-column atomics and the zero-fill cost about what
-    # the skipped statistics pass saved (profiles/bn_stats_fusion_r2p.md)
+    # default since the totals are spread over replicas (conv_igemm.bn_sum_replicas): with
+    # one [2C] target thousands of blocks serialised on its atomics and the fusion
+    # measured neutral to -1.6% (profiles/bn_stats_fusion_r2p.md); with replicas
+    # ResNet-50 bs256 10072 vs 9907 img/s without, same box
+    # (profiles/bench_resnet50_r4_bn11_rep.json, bench_resnet50_r4_bn10_rep.json)
     from .kernels import deterministic
-    if os.environ.get('HETU_FUSE_BN_STATS', '0') != '1' or deterministic():   # fp32 atomics
+    if os.environ.get('HETU_FUSE_BN_STATS', '1') != '1' or deterministic():   # fp32 atomics
         return fused
     from .ops.nn import Conv2dOp
     topo, cons = _consumers(roots)

@@ -134,12 +134,24 @@ def _match(x, w):
     return x, w
 
 
+def stats_replicas(x_shape, w_shape, stride, padding):
+    """replicas of the fused forward BN totals of this convolution's output
+    (conv_igemm.bn_sum_replicas of its rows): ``out_sums`` of conv2d_with_stats holds
+    that many [2*Cout] copies"""
+    from .conv_igemm import bn_sum_replicas
+    n, _, h, w_ = x_shape
+    oh = (h + 2 * padding[0] - w_shape[2]) // stride[0] + 1
+    ow = (w_ + 2 * padding[1] - w_shape[3]) // stride[1] + 1
+    return bn_sum_replicas(n * oh * ow)
+
+
 def conv2d_with_stats(x, w, stride, padding, out_sums=None):
     """(y, sums): the convolution (no bias) and the [2*Cout] per-channel sum / sum of
-    squares of y that a following training-mode BatchNorm needs.  Every candidate
+    squares of y that a following training-mode BatchNorm needs (the fused candidates:
+    [R * 2*Cout] replicas, R = stats_replicas, folded by the BN forward).  Every candidate
     delivers both, so the per-shape choice prices the statistics pass in: the
     hand-written kernels fuse it into their epilogue, the library convolutions pay a
-    separate column-statistics pass.  ``out_sums``: a zeroed [2*Cout] fp32 buffer the
+    separate column-statistics pass.  ``out_sums``: a zeroed [R * 2*Cout] fp32 buffer the
     fused candidates accumulate into (a persistent one the BN re-zeroes: no fill launch
     per call); fresh zeros otherwise and while the shape is being timed."""
     x, w = _match(x, w)
@@ -150,13 +162,15 @@ def conv2d_with_stats(x, w, stride, padding, out_sums=None):
     x = x.contiguous(memory_format=CL)
     w = w.contiguous(memory_format=CL)
     co = w.shape[0]
+    rep = stats_replicas(x.shape, w.shape, stride, padding)
+    assert out_sums is None or out_sums.numel() == rep * 2 * co
     key = ('fwd_stats', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding))
     from .autotune import _decisions
     tgt = [out_sums if key in _decisions else None]
 
     def fused(run):
         def f():
-            s = tgt[0] if tgt[0] is not None else _zeros(2 * co, x.device)
+            s = tgt[0] if tgt[0] is not None else _zeros(rep * 2 * co, x.device)
             y = run(s)
             return None if y is None else (y, s)
         return f

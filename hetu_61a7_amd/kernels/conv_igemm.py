@@ -93,21 +93,26 @@ def _out_hw(H, W, KH, KW, stride, padding):
     return (H + 2 * padding[0] - KH) // stride[0] + 1, (W + 2 * padding[1] - KW) // stride[1] + 1
 
 
+def _reps(colstats, co):
+    return colstats.numel() // (2 * co) if colstats is not None else 0
+
+
 def try_forward(x, w, stride, padding, bias=None, act=None, tile=0, colstats=None):
-    """``colstats`` ([2*Cout] fp32, zeroed): receives the per-channel sum and sum of
-    squares of the stored output (BatchNorm statistics fused into the epilogue)."""
+    """``colstats`` ([R * 2*Cout] fp32, zeroed): receives the per-channel sum and sum of
+    squares of the stored output (BatchNorm statistics fused into the epilogue), spread
+    over R replicas (bn_sum_replicas; the BN forward folds them)."""
     if not _ok(x, w, x.shape[1], w.shape[0]):
         return None
     N, C, H, W = x.shape
     K, _, KH, KW = w.shape
     OH, OW = _out_hw(H, W, KH, KW, stride, padding)
     y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
-    f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, P, I32, P])
+    f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, P, I32, I32, P])
     check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(),
             bias.float().contiguous().data_ptr() if bias is not None else None,
             N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
             {None: 0, 'relu': 1}[act], colstats.data_ptr() if colstats is not None else None, int(tile),
-            stream_ptr()), 'conv_fwd')
+            _reps(colstats, K), stream_ptr()), 'conv_fwd')
     record_native('conv_fwd')
     return y.permute(0, 3, 1, 2)
 
@@ -133,10 +138,10 @@ def try_stem_forward(x, w, stride, padding, colstats=None):
     OH, OW = _out_hw(H, W, KH, KW, stride, padding)
     wp = torch.empty(fn('hetu_stem_wp_elems', [I32], restype=I64)(KH), dtype=torch.bfloat16, device=x.device)
     y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
-    f = fn('hetu_stem_fwd', [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, P])
+    f = fn('hetu_stem_fwd', [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, P])
     check(f(x.data_ptr(), w.data_ptr(), wp.data_ptr(), y.data_ptr(),
             colstats.data_ptr() if colstats is not None else None, N, H, W, C, KH, KW, stride[0], padding[0],
-            stream_ptr()), 'stem_fwd')
+            _reps(colstats, K), stream_ptr()), 'stem_fwd')
     record_native('stem_fwd')
     return y.permute(0, 3, 1, 2)
 
@@ -184,11 +189,13 @@ def try_conv3x3_forward(x, w, stride, padding, colstats=None):
     y = torch.empty((N, H, W, K), dtype=torch.bfloat16, device=x.device)
     st = colstats.data_ptr() if colstats is not None else None
     if _c64(C, K, W):
-        f = fn('hetu_conv3x3_c64_fwd', [P, P, P, P, I32, I32, I32, P])
-        check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, N, H, W, stream_ptr()), 'conv3x3_fwd')
+        f = fn('hetu_conv3x3_c64_fwd', [P, P, P, P, I32, I32, I32, I32, P])
+        check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, N, H, W, _reps(colstats, K), stream_ptr()),
+              'conv3x3_fwd')
     else:
-        f = fn('hetu_conv3x3_wide_fwd', [P, P, P, P, I32, I32, I32, I32, I32, P])
-        check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, N, H, W, C, K, stream_ptr()), 'conv3x3_wide_fwd')
+        f = fn('hetu_conv3x3_wide_fwd', [P, P, P, P, I32, I32, I32, I32, I32, I32, P])
+        check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), st, N, H, W, C, K, _reps(colstats, K), stream_ptr()),
+              'conv3x3_wide_fwd')
     record_native('conv3x3_fwd')
     return y.permute(0, 3, 1, 2)
 

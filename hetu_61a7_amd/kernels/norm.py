@@ -77,7 +77,7 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
             ws = _ws(M, C, is_bf16(x), x.device)
             if mask is not None:
                 assert relu and mask.dtype == torch.uint8 and mask.numel() == relu_mask_bytes(x) and mask.is_cuda
-            f = fn('hetu_bn_fwd', [P, P, P, I64, I32, I32, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P, P])
+            f = fn('hetu_bn_fwd', [P, P, P, I64, I32, I32, P, P, P, P, F32, F32, P, P, P, I32, I32, P, P, I32, P])
             check(f(x.data_ptr(), residual.data_ptr() if residual is not None else None, y.data_ptr(),
                     M, C, is_bf16(x), scale.data_ptr(), bias.data_ptr(),
                     running_mean.data_ptr() if running_mean is not None else None,
@@ -85,7 +85,8 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
                     float(factor), float(eps), save_mean.data_ptr(), save_invstd.data_ptr(),
                     ws.data_ptr(), int(relu), int(training),
                     sums.data_ptr() if (sums is not None and training) else None,
-                    mask.data_ptr() if mask is not None else None, stream_ptr()), 'bn_fwd')
+                    mask.data_ptr() if mask is not None else None,
+                    sums.numel() // (2 * C) if sums is not None else 1, stream_ptr()), 'bn_fwd')
             return y, save_mean, save_invstd
     if sums is not None:
         sums.zero_()     # not consumed here: leave the (persistent) totals ready for next time

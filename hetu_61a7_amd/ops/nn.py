@@ -64,9 +64,10 @@ class Conv2dOp(Op):
             # the only consumer is a training BatchNorm: hand it the statistics of y
             # (fused into the conv epilogue where the hand-written kernel runs)
             bufs = self.__dict__.setdefault('_bn_sums', {})
-            if x.device not in bufs:   # persistent: the BN zeroes the totals after reading them
-                bufs[x.device] = torch.zeros(2 * w.shape[0], dtype=torch.float32, device=x.device)
-            y, sums = KC.conv2d_with_stats(x, w, self.stride, self.padding, out_sums=bufs[x.device])
+            rep = KC.stats_replicas(x.shape, w.shape, self.stride, self.padding)
+            if (x.device, rep) not in bufs:   # persistent: the BN zeroes the totals after reading them
+                bufs[(x.device, rep)] = torch.zeros(rep * 2 * w.shape[0], dtype=torch.float32, device=x.device)
+            y, sums = KC.conv2d_with_stats(x, w, self.stride, self.padding, out_sums=bufs[(x.device, rep)])
             if sums is not None:
                 y.hetu_bn_sums = sums
             return y

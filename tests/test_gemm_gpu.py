@@ -125,14 +125,17 @@ def test_conv_wgrad_64_channel_tiles(shape, tile, accumulate):
 
 @pytest.mark.parametrize('tile', [t for t in G.TILES if t != 5])   # 128x96: no fused statistics
 @pytest.mark.parametrize('shape', [(4, 64, 14, 64, 1, 1, 0), (2, 64, 13, 200, 3, 2, 1), (3, 128, 9, 256, 3, 1, 1)])
-def test_conv_fused_bn_statistics(shape, tile):
+@pytest.mark.parametrize('reps', [1, 3])
+def test_conv_fused_bn_statistics(shape, tile, reps):
     """Per-channel sum / sum of squares of the stored (bf16) conv output, reduced in
-    the epilogue, against a torch reduction of the same output."""
+    the epilogue, against a torch reduction of the same output (reps > 1: spread over
+    that many replicas, Epi::cs_rep)."""
     N, C, H, K, k, s, p = shape
     x = torch.randn(N, C, H, H, device=DEV).bfloat16().contiguous(memory_format=CL)
     w = (torch.randn(K, C, k, k, device=DEV) * 0.1).bfloat16().contiguous(memory_format=CL)
-    st = torch.zeros(2 * K, device=DEV)
+    st = torch.zeros(reps * 2 * K, device=DEV)
     y = CI.try_forward(x, w, (s, s), (p, p), tile=tile, colstats=st)
+    st = st.view(reps, 2 * K).sum(0)
     yf = y.float()
     ref_s = yf.sum((0, 2, 3))
     ref_q = (yf * yf).sum((0, 2, 3))
@@ -233,6 +236,9 @@ def test_conv3x3_c64_halo_kernel(n, h):
     assert _rel(y, ref) < _tol(y)
     yf = y.float()
     assert _rel(st[:64], yf.sum((0, 2, 3))) < 1e-4 and _rel(st[64:], (yf * yf).sum((0, 2, 3))) < 1e-4
+    st3 = torch.zeros(3 * 128, device=DEV)   # replicated totals: image i into replica i % 3
+    assert torch.equal(CI.try_conv3x3_forward(x, w, (1, 1), (1, 1), colstats=st3), y)
+    assert _rel(st3.view(3, 128).sum(0), st) < 1e-5
     dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
     ref.backward(dy.float())
     dx = CI.try_conv3x3_backward_data(dy, w, x.shape, (1, 1), (1, 1))
@@ -266,6 +272,9 @@ def test_conv3x3_wide_halo_kernel(n, c, k, h):
     assert _rel(y, ref) < _tol(y)
     yf = y.float()
     assert _rel(st[:k], yf.sum((0, 2, 3))) < 1e-4 and _rel(st[k:], (yf * yf).sum((0, 2, 3))) < 1e-4
+    st3 = torch.zeros(3 * 2 * k, device=DEV)   # replicated totals: pixel tile t into replica t % 3
+    assert torch.equal(CI.try_conv3x3_forward(x, w, (1, 1), (1, 1), colstats=st3), y)
+    assert _rel(st3.view(3, 2 * k).sum(0), st) < 1e-5
     dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
     ref.backward(dy.float())
     if c % 128 == 0:

@@ -29,6 +29,9 @@ def test_stem_forward_and_stats(n, c, h, k, s, p):
     torch.testing.assert_close(st[:64].cpu(), yb.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(st[64:].cpu(), (yb * yb).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
     assert CI.try_stem_forward(x, w, (s, s), (p, p)).float().sub(y.float()).abs().max().item() == 0.0
+    st3 = torch.zeros(3 * 128, device='cuda')   # replicated totals: block b into replica b % 3
+    CI.try_stem_forward(x, w, (s, s), (p, p), colstats=st3)
+    torch.testing.assert_close(st3.view(3, 128).sum(0), st, rtol=1e-5, atol=1e-3)
 
 
 @pytest.mark.parametrize('n,c,h,wd,k,s,p', [(2, 3, 224, 224, 7, 2, 3), (3, 3, 37, 40, 7, 2, 3), (2, 2, 20, 24, 5, 1, 2),

@@ -636,6 +636,10 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                                                                    accumulate=False, tile=2)
             blas['hip64t'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
                                                                     accumulate=False, tile=4)
+        # the single-stage tile (4 blocks per CU) on the long pixel reduction
+        blas = dict(blas or {})
+        blas['hip_lo'] = lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
+                                                                accumulate=False, tile=3)
         if conv_igemm._s1p1_3x3(w_shape, stride, padding) and conv_igemm.conv3x3_wgrad_ok(x.shape, w_shape):
             blas = dict(blas or {})
             blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=out)

@@ -224,6 +224,13 @@ def matmul_into(a, b, ta, tb, out):
             for s in (2, 3, 4, 6, 8):
                 if tiles * s <= 1536 and K // s >= 512:
                     cands['hip_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s))
+            # the single-stage tile at 4 blocks per CU: 892 vs 592 TF for the 2-stage tile on
+            # 3072x3072x8192 TN (profiles/gemm_tn_r4.txt) -- and 1024 resident slots for splits
+            if K >= 1024:
+                cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=3)
+                for s in (2, 3, 4, 5, 6, 7, 8):
+                    if tiles * s <= 2048 and K // s >= 512:
+                        cands['hip_lo_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=3))
             if M >= 256 and N >= 256:
                 cands['hip256'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=1)
                 t256 = -(-M // 256) * -(-N // 256)

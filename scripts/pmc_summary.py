@@ -33,6 +33,7 @@ def family(name):
     return n[:90]
 
 
+STEPS = 1
 LAST = 0   # --last N: only the N most recent dispatches of each pass (steady state, no autotune)
 
 
@@ -83,6 +84,12 @@ def main(dirs):
         tf = 512 * mops[0].get(k, {}).get('SQ_INSTS_VALU_MFMA_MOPS_BF16', 0) / tmo / 1e12 if tmo else float('nan')
         print('%-64s %6d %8.2f %8.2f %8.3f %8.3f %8.3f %8.2f %7.2f %7.0f' % (k[:64], calls[k], t * 1e3, clk, mf, wait,
                                                                              lc, rd, w, tf))
+    # HBM traffic of the whole window (the --last dispatches; per step with --steps S)
+    rd_b = sum(2 * c.get('FETCH_SIZE', 0) * 1024 for c in mem[0].values()) if mem[0] else 0.0
+    wr_b = sum(c.get('WRITE_SIZE', 0) * 1024 for c in wr[0].values()) if wr[0] else 0.0
+    if rd_b or wr_b:
+        print('\n# HBM bytes per %s: read %.2f GB, write %.2f GB, total %.2f GB' %
+              ('step' if STEPS > 1 else 'window', rd_b / STEPS / 1e9, wr_b / STEPS / 1e9, (rd_b + wr_b) / STEPS / 1e9))
     # every counter of every pass, per dispatch (raw sums / calls), for the top families
     print('\n# raw counters per dispatch')
     for k, c in rows[:12]:
@@ -95,7 +102,10 @@ def main(dirs):
 
 if __name__ == '__main__':
     a = sys.argv[1:]
-    if a and a[0] == '--last':
-        LAST = int(a[1])
+    while a and a[0] in ('--last', '--steps'):
+        if a[0] == '--last':
+            LAST = int(a[1])
+        else:
+            STEPS = int(a[1])
         a = a[2:]
     main(a)

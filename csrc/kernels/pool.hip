@@ -149,6 +149,44 @@ __global__ void __launch_bounds__(256) maxpool_bwd_vec(const T* __restrict__ dy,
     float acc[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) acc[k] = 0.f;
+    if (kh <= sh + 1 && kw <= sw + 1) {
+      // at most 2 x 2 windows hold this pixel (ResNet's 3x3 / stride-2 pool): every
+      // candidate's winning-tap word and gradient are requested before any is used
+      // (the loop form waits one round trip per window)
+      uint2 pk[4];
+      float g[4][V];
+      int tp[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ho = ho0 + (q >> 1), wo = wo0 + (q & 1);
+        const int a = h + ph - ho * sh, b = w + pw - wo * sw;
+        const bool ok = ho <= ho1 && wo <= wo1 && a >= 0 && a < kh && b >= 0 && b < kw;
+        tp[q] = ok ? a * kw + b : -1;
+        const int64_t o = ok ? ((int64_t)(n * Ho + ho) * Wo + wo) * C + cg * V : 0;
+        if (V == 8) {
+          pk[q] = ok ? *reinterpret_cast<const uint2*>(idx + o) : make_uint2(0, 0);
+        } else {
+          pk[q] = make_uint2(ok ? *reinterpret_cast<const uint32_t*>(idx + o) : 0u, 0u);
+        }
+        if (ok) {
+          load_vec<T>(dy + o, g[q]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < V; ++k) g[q][k] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const uint32_t word = k < 4 ? pk[q].x : pk[q].y;
+          const int ix = (int)((word >> (8 * (k & 3))) & 255u);
+          if (ix == tp[q]) acc[k] += g[q][k];
+        }
+      }
+      store_vec<T>(dx + (int64_t)i * V, acc);
+      continue;
+    }
     for (int ho = ho0; ho <= ho1; ++ho) {
       const int a = h + ph - ho * sh;
       if (a < 0 || a >= kh) continue;

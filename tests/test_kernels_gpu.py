@@ -169,16 +169,21 @@ def test_flat_optimizer(mode):
 
 
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
-def test_pooling(dt):
-    x = torch.randn(4, 64, 56, 56, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
-    y, idx = KP.maxpool2d(x, 3, 3, 2, 2, 1, 1)
+@pytest.mark.parametrize('k,s,p,h', [(3, 2, 1, 56), (3, 2, 1, 57), (2, 2, 0, 30), (3, 1, 1, 19)])
+def test_pooling(dt, k, s, p, h):
+    """max pooling forward / backward (the backward's 2x2-window fast path for windows
+    no wider than stride + 1, the general loop otherwise) against torch"""
+    x = torch.randn(4, 64, h, h + 1, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    y, idx = KP.maxpool2d(x, k, k, s, s, p, p)
     xf = x.float().requires_grad_(True)
-    ref = F.max_pool2d(xf, 3, 2, 1)
+    ref = F.max_pool2d(xf, k, s, p)
     torch.testing.assert_close(y.float(), ref, **_tol(dt))
     dy = torch.randn_like(ref)
     ref.backward(dy)
-    dx = KP.maxpool2d_backward(dy.to(dt), idx, x.shape, 3, 3, 2, 2, 1, 1)
+    dx = KP.maxpool2d_backward(dy.to(dt), idx, x.shape, k, k, s, s, p, p)
     torch.testing.assert_close(dx.float(), xf.grad, **_tol(dt))
+    if (k, s) != (3, 2) or h != 56:
+        return
     ya = KP.avgpool2d(x, 2, 2, 2, 2, 0, 0)
     torch.testing.assert_close(ya.float(), F.avg_pool2d(x.float(), 2, 2), **_tol(dt))
     gp = KR.global_avg_pool(x)

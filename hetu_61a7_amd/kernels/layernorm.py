@@ -4,10 +4,17 @@ parameter gradients).  Replaces LayerNorm.cu (fwd block-per-row with
 E[x^2]-E[x]^2 variance, bwd = 3 elementwise kernels + 4 cuDNN reductions)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32, F32
 
+
+
+# LayerNorm backward blocks (4 waves, a wave per row): more blocks keep more rows in
+# flight, fewer write fewer dgamma / dbeta partial rows (HETU_LN_BWD_BLOCKS)
+_LN_BWD_BLOCKS = int(os.environ.get('HETU_LN_BWD_BLOCKS', '512'))
 
 def layer_norm(x, gamma, beta, eps):
     N = x.shape[-1]
@@ -119,7 +126,7 @@ def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_d
         dx = torch.empty_like(sc) if (need_dx and keep < 1.0) else None
         if need_dx and keep >= 1.0 and not need_ds:
             ds = torch.empty_like(sc)
-        nblk = max(1, min(512, (R + 7) // 8))
+        nblk = max(1, min(_LN_BWD_BLOCKS, (R + 7) // 8))
         ws = torch.empty((3 if want_dlin else 2) * nblk * N, dtype=torch.float32, device=s.device)
         dg, db = _dest(dg_out, N, s.device), _dest(db_out, N, s.device)
         dlin = _dest(dlin_out, N, s.device) if want_dlin else None

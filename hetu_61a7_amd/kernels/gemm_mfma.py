@@ -93,6 +93,20 @@ def gemm_f32(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None,
     return out
 
 
+_DEBUG = os.environ.get('HETU_GEMM_DEBUG') == '1'
+
+
+def _reject(where, a, b, out):
+    """None (unsupported operands); HETU_GEMM_DEBUG=1 names the check that refused them"""
+    if _DEBUG:
+        import sys
+        print('gemm_mfma.gemm: refused at check %d: a %s %s %s ptr%%16=%d, b %s %s %s ptr%%16=%d, out %s' % (
+            where, tuple(a.shape), tuple(a.stride()), a.dtype, a.data_ptr() % 16, tuple(b.shape), tuple(b.stride()),
+            b.dtype, b.data_ptr() % 16, None if out is None else (tuple(out.shape), tuple(out.stride()), out.dtype)),
+            file=sys.stderr)
+    return None
+
+
 def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None,
          accumulate=False, splitk=1, bias_on_m=False, tile=0):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+beta*cin) (+bias) -> act, a/b arbitrary
@@ -102,28 +116,28 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
         return gemm_f32(a, b, out=out, bias=bias, act=act, alpha=alpha, beta=beta, cin=cin,
                         accumulate=accumulate, bias_on_m=bias_on_m)
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
-        return None
+        return _reject(1, a, b, out)
     if a.dim() != b.dim() or a.dim() not in (2, 3):
-        return None
+        return _reject(2, a, b, out)
     M, K = a.shape[-2], a.shape[-1]
     N = b.shape[-1]
     if b.shape[-2] != K:
         raise ValueError('gemm shape mismatch %s @ %s' % (tuple(a.shape), tuple(b.shape)))
     batch = a.shape[0] if a.dim() == 3 else 1
     if a.dim() == 3 and b.shape[0] != batch:
-        return None
+        return _reject(3, a, b, out)
     da = _operand(a, False)
     db = _operand(b.transpose(-1, -2), False)  # view as [N, K]
     if da is None or db is None or not _aligned(a, b):
-        return None
+        return _reject(4, a, b, out)
     odt = out_dtype or (out.dtype if out is not None else torch.bfloat16)
     if out is None:
         shape = (batch, M, N) if a.dim() == 3 else (M, N)
         out = (torch.zeros if accumulate else torch.empty)(shape, dtype=odt, device=a.device)
     if out.stride(-1) != 1 or (out.dim() == 3 and out.dim() != a.dim()):
-        return None
+        return _reject(5, a, b, out)
     if accumulate and splitk == 1 and out.dtype != torch.float32:
-        return None
+        return _reject(6, a, b, out)
     ldc = out.stride(-2) if M > 1 else N
     sC = out.stride(0) if out.dim() == 3 else 0
     cin_t, ldcin, sCin = None, 0, 0
@@ -137,10 +151,10 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
     ws = None
     if splitk > 1:
         if bias is not None or act is not None or cin_t is not None:
-            return None
+            return _reject(7, a, b, out)
         ws = torch.empty(splitk * batch * M * N, dtype=torch.float32, device=a.device)
         if batch > 1:
-            return None
+            return _reject(8, a, b, out)
     f = fn('hetu_gemm_bf16', _ARGS)
     check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), cin_t.data_ptr() if cin_t is not None else None,
             bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, ldcin,

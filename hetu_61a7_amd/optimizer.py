@@ -177,6 +177,17 @@ class LambOptimizer(AdamWOptimizer):
 
 
 # ---------------------------------------------------------------------------
+SEG_ALIGN = 8   # flat-buffer segment alignment in elements (FlatGroup)
+
+
+def flat_extent(numels):
+    """elements a FlatGroup of segments of these sizes spans (SEG_ALIGN-aligned starts)"""
+    off = 0
+    for n in numels:
+        off = -(-off // SEG_ALIGN) * SEG_ALIGN + n
+    return off
+
+
 class FlatGroup(object):
     """Flat fp32 storage for a set of dense parameters (one per device)."""
 
@@ -187,6 +198,10 @@ class FlatGroup(object):
         self.offsets = {}
         off = 0
         for p in params:
+            # every segment starts 16-byte aligned in the bf16 shadow (8 elements): the
+            # MFMA loaders stage 16-byte chunks, and one odd-sized bias ahead of a weight
+            # (the MoE gate's 2) otherwise sent every later weight to the library GEMM
+            off = -(-off // SEG_ALIGN) * SEG_ALIGN
             self.offsets[p] = (off, values[p].numel(), tuple(values[p].shape))
             off += values[p].numel()
         self.numel = off
@@ -336,7 +351,7 @@ class OptimizerOp(Op):
             P = self.comm.nrank
             self.zero_unit = P * 64                       # every bucket splits into 64-aligned shards
             pad_to = self.zero_unit
-            total = -(-sum(values[p].numel() for p in dense) // pad_to) * pad_to
+            total = -(-flat_extent([values[p].numel() for p in dense]) // pad_to) * pad_to
             state_numel = max(total // P, 1)
         self.flat = FlatGroup(dense, values, opt.n_states, getattr(opt, 'state_init', (0.0, 0.0)),
                               shadow=amp, device=self.ctx.torch_device if self.ctx else None,
@@ -389,8 +404,9 @@ class OptimizerOp(Op):
         groups, cur, cur_n, nxt = [], [], 0, None
         for p in reversed([p for p in dense if not self.excluded_from_dp(p)]):
             o, n, _ = self.flat.offsets[p]
-            # members must stay contiguous in the flat buffer (o + n == start of the next)
-            if cur and (o + n != nxt or cur_n + n > cap):
+            # members must stay contiguous in the flat buffer (the next member starts at
+            # the aligned end of this one; the alignment gap rides along, all zeros)
+            if cur and (-(-(o + n) // SEG_ALIGN) * SEG_ALIGN != nxt or cur_n + n > cap):
                 groups.append(cur)
                 cur, cur_n = [], 0
                 cap = min(cap * 2, full)
@@ -403,7 +419,8 @@ class OptimizerOp(Op):
         for members in reversed(groups):
             members = members[::-1]
             start = self.flat.offsets[members[0]][0]
-            self._close_bucket(start, sum(self.flat.offsets[p][1] for p in members), members)
+            o_last, n_last, _ = self.flat.offsets[members[-1]]
+            self._close_bucket(start, o_last + n_last - start, members)
 
     def _make_zero_buckets(self, dense):
         """ZeRO-1 (absent in the reference): fixed-size buckets

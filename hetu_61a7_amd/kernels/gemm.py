@@ -243,6 +243,13 @@ def matmul_into(a, b, ta, tb, out):
                 cands['vendor_sk'] = lambda: _vendor_splitk_into(A, B, out)
             if M * N <= gemm_mfma.SMALL_MAX_OUT:
                 cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, out=out)
+            if N < 8 and M % 8 == 0 and K >= 4096 and out.dtype == torch.float32 and out.is_contiguous():
+                # a few output columns over a long reduction (the MoE gate's weight gradient,
+                # 2048 x 2 over 16384 tokens): B zero-padded to 8 columns on the MFMA tiles
+                # with a deep K split (one wave per output read the 67 MB operand at 300 us)
+                for s in (16, 32, 64):
+                    if K // s >= 128:
+                        cands['hip_pad8_sk%d' % s] = (lambda s=s: _pad8_into(A, B, out, s))
             if A.stride(0) == 1 and B.stride(1) == 1 and M % 64 == 0 and N % 64 == 0 and K >= 4096:
                 # both operands token-major (weight gradients): the 64x64 split-K tile
                 cands['hip_lk'] = lambda: gemm_mfma.wgrad_longk(A.t(), B, out)
@@ -254,6 +261,21 @@ def matmul_into(a, b, ta, tb, out):
             _fallback('matmul_into')
         return vendor()
     return _vendor_into(_tr(a, ta), _tr(b, tb), out)
+
+
+def _pad8_into(A, B, out, splitk):
+    """out[M, N<8] (fp32, contiguous) = A @ B with B padded to 8 columns (native zero fill
+    and strided copies), split-K over ``splitk`` slices on the single-stage tile"""
+    from . import gemm_mfma
+    from .tensor import zeros, copy_into
+    K, N = B.shape
+    bp = zeros((K, 8), B.dtype, B.device)
+    copy_into(bp[:, :N], B)
+    op = torch.empty((A.shape[0], 8), dtype=torch.float32, device=A.device)
+    if gemm_mfma.gemm(A, bp, out=op, splitk=splitk, tile=3) is None:
+        return None
+    copy_into(out, op[:, :N])
+    return out
 
 
 def matmul_acc(a, b, ta, tb, acc, inplace=False):

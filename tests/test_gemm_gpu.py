@@ -330,3 +330,22 @@ def test_wgrad_longk(pmn, accumulate):
     ref = a.float().t() @ b.float()
     got = out - base if accumulate else out
     assert _rel(got, ref) < (1e-4 if accumulate else 2e-5)
+
+
+@pytest.mark.parametrize('n', [1, 2, 5])
+def test_gemm_into_few_columns_long_k(n):
+    """out[M, n<8] = X^T @ G over a long token axis (the MoE gate's weight gradient):
+    G zero-padded to 8 columns on the MFMA tile with a deep K split, against fp32 math;
+    and through matmul_into's autotuned choice"""
+    from hetu_61a7_amd.kernels import gemm as KG
+    torch.manual_seed(5)
+    x = torch.randn(8192, 512, device=DEV).bfloat16()
+    g = torch.randn(8192, n, device=DEV).bfloat16()
+    ref = x.float().t() @ g.float()
+    for s in (16, 64):
+        out = torch.full((512, n), 7.0, device=DEV)
+        assert KG._pad8_into(x.t(), g, out, s) is out
+        assert _rel(out, ref) < _tol(out)
+    out = torch.empty(512, n, device=DEV)
+    KG.matmul_into(x, g, True, False, out)
+    assert _rel(out, ref) < _tol(out)

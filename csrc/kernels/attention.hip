@@ -54,6 +54,7 @@ struct Args {
   int B, NH;
   float scale, keep;
   uint64_t seed;
+  short* ws;              // split backward: P_drop^T then (scale dS)^T, [B*NH][S][S] bf16 each
 };
 
 __device__ __forceinline__ v16f mfma(v8s a, v8s b, v16f c) {
@@ -203,19 +204,24 @@ __global__ void __launch_bounds__(256) attn_fwd_k(Args a) {
 }
 
 // -------------------------------------------------------------------------------------
-template <int KB>
+// PH: 0 = both phases in one workgroup (P_drop^T / dS^T in LDS: ~122 KiB at S = 128, one
+// workgroup per CU); 1 = phase 1 only, P_drop^T / dS^T to the global workspace (LDS: K^T);
+// 2 = phase 2 only, reading them back (LDS: dO^T, Q^T) -- the split form runs several
+// workgroups per CU at the cost of the workspace round trip
+template <int KB, int PH = 0>
 __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
   constexpr int S = 32 * KB;
   constexpr int LT = S + PAD;
+  constexpr int LP = PH == 0 ? LT : S;   // row stride of the P_drop^T / dS^T images
   extern __shared__ short lds[];
-  short* kt = lds;                 // K^T   [64][LT]
-  short* qt = kt + HD * LT;        // Q^T   [64][LT]
-  short* dot = qt + HD * LT;       // dO^T  [64][LT]
-  short* pt = dot + HD * LT;       // P_drop^T [S][LT]
-  short* dst = pt + S * LT;        // (scale * dS)^T [S][LT]
-  float* dvec = reinterpret_cast<float*>(dst + S * LT);   // D[q] = <dO_q, O_q>
-  float* msk = dvec + S;
   const int bh = blockIdx.x;
+  short* kt = lds;                                          // K^T   [64][LT]  (PH 0, 1)
+  short* qt = PH == 2 ? lds : kt + HD * LT;                 // Q^T   [64][LT]  (PH 0, 2)
+  short* dot = qt + HD * LT;                                // dO^T  [64][LT]  (PH 0, 2)
+  short* pt = PH == 0 ? dot + HD * LT : a.ws + (int64_t)bh * S * S;                  // P_drop^T [S][LP]
+  short* dst = PH == 0 ? pt + S * LT : a.ws + ((int64_t)a.B * a.NH + bh) * S * S;    // (scale dS)^T
+  float* dvec = reinterpret_cast<float*>(PH == 0 ? dst + S * LT : (PH == 1 ? kt + HD * LT : dot + HD * LT));
+  float* msk = dvec + S;
   const int b = bh / a.NH, hd = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -226,12 +232,14 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
   const bf16* O = a.o + row0 * a.ldo + hd * HD;
   const bf16* dO = a.dout + row0 * a.lddo + hd * HD;
 
-  stage_t<S>(K, a.ldk, kt);
-  stage_t<S>(Q, a.ldq, qt);
-  stage_t<S>(dO, a.lddo, dot);
+  if (PH != 2) stage_t<S>(K, a.ldk, kt);
+  if (PH != 1) {
+    stage_t<S>(Q, a.ldq, qt);
+    stage_t<S>(dO, a.lddo, dot);
+  }
   for (int i = threadIdx.x; i < S; i += 256) msk[i] = a.mask ? a.mask[(int64_t)b * S + i] : 0.f;
   // D[q] = sum_d dO[q][d] * O[q][d]: 8 consecutive threads per query
-  for (int idx = threadIdx.x; idx < S * 8; idx += 256) {
+  for (int idx = threadIdx.x; PH != 2 && idx < S * 8; idx += 256) {
     const int qq = idx >> 3, c = idx & 7;
     const v8s x = ld8(dO + (int64_t)qq * a.lddo + 8 * c);
     const v8s y = ld8(O + (int64_t)qq * a.ldo + 8 * c);
@@ -247,7 +255,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
 
   const bool drop = a.keep < 1.f;
   // ---- phase 1: per query block: P, dP, dS; dQ; stage P_drop^T and dS^T -----------------
-  for (int qb = w; qb < KB; qb += 4) {
+  for (int qb = w; PH != 2 && qb < KB; qb += 4) {
     const int q = qb * 32 + r;
     v8s qf[4], gf[4];
 #pragma unroll
@@ -278,8 +286,8 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
           const float p = __expf(sc[i] * a.scale + msk[key] - lse);
           const float pd = p * mul[t];
           const float dsv = p * (dp[i] * mul[t] - Dq) * a.scale;
-          pt[key * LT + q] = (short)f_to_bf16_bits(pd);
-          dst[key * LT + q] = (short)f_to_bf16_bits(dsv);
+          pt[key * LP + q] = (short)f_to_bf16_bits(pd);
+          dst[key * LP + q] = (short)f_to_bf16_bits(dsv);
           sc[i] = dsv;
         }
       }
@@ -304,6 +312,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
       }
     }
   }
+  if (PH == 1) return;
   __syncthreads();
   // ---- phase 2: per key block: dV^T = dO^T P_drop, dK^T = Q^T (scale dS) -------------------
   for (int kb = w; kb < KB; kb += 4) {
@@ -317,7 +326,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
       for (int db = 0; db < 2; ++db) {
         v16f c = {0.f};
 #pragma unroll
-        for (int t = 0; t < S / 16; ++t) c = mfma(lds8(A, LT, db * 32 + r, 16 * t + 8 * h), lds8(Bm, LT, key, 16 * t + 8 * h), c);
+        for (int t = 0; t < S / 16; ++t) c = mfma(lds8(A, LT, db * 32 + r, 16 * t + 8 * h), lds8(Bm, LP, key, 16 * t + 8 * h), c);
         bf16* dst_row = out + hd * HD + db * 32;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -331,15 +340,23 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
   }
 }
 
-template <int KB>
+template <int KB, int PH = 0>
 size_t bwd_lds_bytes() {
   constexpr int S = 32 * KB, LT = S + PAD;
+  if (PH == 1) return (size_t)HD * LT * sizeof(short) + 2 * S * sizeof(float);
+  if (PH == 2) return (size_t)2 * HD * LT * sizeof(short) + 2 * S * sizeof(float);
   return (size_t)(3 * HD * LT + 2 * S * LT) * sizeof(short) + 2 * S * sizeof(float);
 }
 
 // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU) must be opted into once
 template <int KB>
 void launch_bwd(dim3 grid, const Args& a, hipStream_t st) {
+  if (a.ws) {   // split form: two launches, the images through the workspace
+    const size_t b1 = bwd_lds_bytes<KB, 1>(), b2 = bwd_lds_bytes<KB, 2>();
+    hipLaunchKernelGGL((attn_bwd_k<KB, 1>), grid, dim3(256), b1, st, a);
+    hipLaunchKernelGGL((attn_bwd_k<KB, 2>), grid, dim3(256), b2, st, a);
+    return;
+  }
   static bool attr = false;
   const size_t bytes = bwd_lds_bytes<KB>();
   if (!attr) {
@@ -390,12 +407,14 @@ HETU_API int hetu_attn_fwd(const void* q, const void* k, const void* v, int64_t 
   return 0;
 }
 
-HETU_API int hetu_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq, int64_t ldk, int64_t ldv,
-                           const float* mask, const void* o, int64_t ldo, const float* lse, const void* dout,
-                           int64_t lddo, void* dq, void* dk, void* dv, int64_t lddq, int64_t lddk, int64_t lddv,
-                           int B, int NH, int S, float scale, float keep, int64_t seed, hipStream_t st) {
-  if (S % 32 || S <= 0 || S > 128 || B <= 0 || NH <= 0) return (int)hipErrorInvalidValue;
+// ws (nullable): 2 * B*NH*S*S bf16 -- the split two-launch form (see attn_bwd_k PH)
+HETU_API int hetu_attn_bwd2(const void* q, const void* k, const void* v, int64_t ldq, int64_t ldk, int64_t ldv,
+                            const float* mask, const void* o, int64_t ldo, const float* lse, const void* dout,
+                            int64_t lddo, void* dq, void* dk, void* dv, int64_t lddq, int64_t lddk, int64_t lddv,
+                            int B, int NH, int S, float scale, float keep, int64_t seed, void* ws, hipStream_t st) {
+  if (S % 32 || S <= 0 || S > 128 || B <= 0 || NH <= 0 || (((uintptr_t)ws) & 15)) return (int)hipErrorInvalidValue;
   Args a = make_args(q, k, v, ldq, ldk, ldv, mask, B, NH, scale, keep, seed);
+  a.ws = (short*)ws;
   a.o = (bf16*)o; a.ldo = ldo; a.lse = (float*)lse;
   a.dout = (const bf16*)dout; a.lddo = lddo;
   a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv;
@@ -410,4 +429,12 @@ HETU_API int hetu_attn_bwd(const void* q, const void* k, const void* v, int64_t 
   }
   HETU_LAUNCH_CHECK();
   return 0;
+}
+
+HETU_API int hetu_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq, int64_t ldk, int64_t ldv,
+                           const float* mask, const void* o, int64_t ldo, const float* lse, const void* dout,
+                           int64_t lddo, void* dq, void* dk, void* dv, int64_t lddq, int64_t lddk, int64_t lddv,
+                           int B, int NH, int S, float scale, float keep, int64_t seed, hipStream_t st) {
+  return hetu_attn_bwd2(q, k, v, ldq, ldk, ldv, mask, o, ldo, lse, dout, lddo, dq, dk, dv, lddq, lddk, lddv, B, NH,
+                        S, scale, keep, seed, nullptr, st);
 }

@@ -14,10 +14,26 @@ from __future__ import annotations
 import math
 import weakref
 
+import os
+
 import torch
 
 from . import fn, native, stream_ptr, check, P, I64, I32, F32
 
+
+
+# HETU_ATTN_BWD_SPLIT (default 1; BERT-base 4715/4715 vs 4691/4663 samples/s fused): the backward as two launches with P_drop^T / dS^T through a global
+# workspace (small LDS, several workgroups per CU) instead of one ~122 KiB-LDS workgroup
+_BWD_SPLIT = os.environ.get('HETU_ATTN_BWD_SPLIT', '1') == '1'
+
+
+def _bwd_call(*args, device=None):
+    """hetu_attn_bwd2 (fused, or split with a workspace); args as hetu_attn_bwd's up to seed"""
+    B, NH, S = args[18], args[19], args[20]
+    ws = torch.empty(2 * B * NH * S * S, dtype=torch.bfloat16, device=device) if _BWD_SPLIT else None
+    f = fn('hetu_attn_bwd2', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
+                              I32, I32, I32, F32, F32, I64, P, P])
+    check(f(*args, ws.data_ptr() if ws is not None else None, stream_ptr()), 'attn_bwd')
 
 def fused_ok(qkv, S, D, need_bwd=True):
     return (native(qkv) and qkv.dtype == torch.bfloat16 and D == 64 and S % 32 == 0 and 0 < S <= (128 if need_bwd else 256)
@@ -111,13 +127,11 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
             dout = copy_into(torch.empty(dout.shape, dtype=qkv.dtype, device=dout.device), dout)
         dqkv = torch.empty_like(qkv)
         m = _mask_f32(mask)
-        f = fn('hetu_attn_bwd', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
-                                 I32, I32, I32, F32, F32, I64, P])
         es = qkv.element_size()
         b, g = qkv.data_ptr(), dqkv.data_ptr()
-        check(f(b, b + H * es, b + 2 * H * es, 3 * H, 3 * H, 3 * H, m.data_ptr() if m is not None else None,
-                out.data_ptr(), H, saved.data_ptr(), dout.data_ptr(), H, g, g + H * es, g + 2 * H * es,
-                3 * H, 3 * H, 3 * H, B, NH, S, float(scale), float(keep), int(seed), stream_ptr()), 'attn_bwd')
+        _bwd_call(b, b + H * es, b + 2 * H * es, 3 * H, 3 * H, 3 * H, m.data_ptr() if m is not None else None,
+                  out.data_ptr(), H, saved.data_ptr(), dout.data_ptr(), H, g, g + H * es, g + 2 * H * es,
+                  3 * H, 3 * H, 3 * H, B, NH, S, float(scale), float(keep), int(seed), device=qkv.device)
         return dqkv
     if saved.dim() == 1:    # fused forward (S <= 256) but no fused backward: recompute probs
         saved, _ = _ref_probs(qkv, mask, B, S, NH, D, scale)
@@ -174,10 +188,8 @@ def attention_bwd_blocks(dout, q, k, v, out, lse, mask, B, S, NH, scale):
     dk = torch.empty_like(dq)
     dv = torch.empty_like(dq)
     m = _mask_f32(mask)
-    f = fn('hetu_attn_bwd', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
-                             I32, I32, I32, F32, F32, I64, P])
-    check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
-            m.data_ptr() if m is not None else None, out.data_ptr(), H, lse.contiguous().data_ptr(),
-            dout.data_ptr(), H, dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), H, H, H, B, NH, S,
-            float(scale), 1.0, 0, stream_ptr()), 'attn_bwd')
+    _bwd_call(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
+              m.data_ptr() if m is not None else None, out.data_ptr(), H, lse.contiguous().data_ptr(),
+              dout.data_ptr(), H, dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), H, H, H, B, NH, S,
+              float(scale), 1.0, 0, device=q.device)
     return dq, dk, dv

@@ -5,7 +5,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
 S=scripts/gpu_step.sh
-if [ -n "${WDL:-1}" ]; then
+if [ "${WDL:-1}" != "0" ]; then
   for ids in zipf uniform; do
     bash $S wdl_ps_$ids 300 python bench.py --model wdl --comm PS --ids $ids --steps 40 --warmup 10 || exit $?
   done

@@ -3,6 +3,9 @@
 //
 //   make -C csrc bench   ->  csrc/build/gemm_bench
 //   gemm_bench [M N K ta tb]...      (ta: A stored [K][M]; tb: B stored [N][K])
+//   VARS="0:1,3:4,1:7"  tile:splitk variants (default: every tile, no split)
+//   WGRAD_F32=1         shapes with ta (weight gradients) write fp32 C, as the framework's
+//                       flat gradient buffer does (split-K slabs + reduce when splitk > 1)
 //
 // Every variant's output is checked against hipBLASLt's (relative Frobenius error).
 #include "../kernels/gemm_core.h"
@@ -29,7 +32,7 @@ using namespace hetu::gemm;
 
 // -DBENCH_FAST: only the 256x256 kernel (tile 1), K % 64 == 0, for quick kernel iteration
 static int run_tile(const bf16* a, const bf16* b, int a_kmaj, int b_kmaj, int64_t lda, int64_t ldb, const Epi& ep,
-                    int64_t M, int64_t N, int64_t K, hipStream_t st, int tile) {
+                    int64_t M, int64_t N, int64_t K, hipStream_t st, int tile, int splitk) {
 #ifdef BENCH_FAST
   if (K % BK) return (int)hipErrorInvalidValue;
 #define HB_CASE(LA, LB, SA, SB)                                                                          \
@@ -40,8 +43,8 @@ static int run_tile(const bf16* a, const bf16* b, int a_kmaj, int b_kmaj, int64_
   if (b_kmaj) { HB_CASE(BufMN, BufK, 0, 0) }
   HB_CASE(BufMN, BufMN, 0, 0)
 #else
-  return (K % BK == 0) ? launch_buf<true>(a, b, a_kmaj, b_kmaj, lda, ldb, 0, 0, ep, M, N, K, 1, 1, st, tile)
-                       : launch_buf<false>(a, b, a_kmaj, b_kmaj, lda, ldb, 0, 0, ep, M, N, K, 1, 1, st, tile);
+  return (K % BK == 0) ? launch_buf<true>(a, b, a_kmaj, b_kmaj, lda, ldb, 0, 0, ep, M, N, K, 1, splitk, st, tile)
+                       : launch_buf<false>(a, b, a_kmaj, b_kmaj, lda, ldb, 0, 0, ep, M, N, K, 1, splitk, st, tile);
 #endif
 }
 
@@ -63,10 +66,13 @@ __global__ void fill_k(unsigned short* p, int64_t n, uint32_t seed) {
   }
 }
 
-__global__ void relerr_k(const unsigned short* a, const unsigned short* b, int64_t n, float* out) {
+__global__ void relerr_k(const void* a_, const void* b_, int64_t n, float* out, int f32) {
   float d = 0.f, r = 0.f;
+  const unsigned short* a = (const unsigned short*)a_;
+  const unsigned short* b = (const unsigned short*)b_;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float x = bf16_bits_to_f(a[i]), y = bf16_bits_to_f(b[i]);
+    const float x = f32 ? ((const float*)a_)[i] : bf16_bits_to_f(a[i]);
+    const float y = f32 ? ((const float*)b_)[i] : bf16_bits_to_f(b[i]);
     d += (x - y) * (x - y);
     r += y * y;
   }
@@ -83,7 +89,7 @@ struct Blas {
   hipblasLtMatmulHeuristicResult_t res;
   void* ws; size_t wsz = 64 << 20;
   // row-major C[M][N] = op(A) op(B)  <=>  column-major C^T = op(B)^T op(A)^T
-  void init(const Shape& s) {
+  void init(const Shape& s, bool cf32) {
     CK(hipblasLtCreate(&h));
     CK(hipblasLtMatmulDescCreate(&desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
     // B stored [N][K] (tb) is column-major KxN -> needs T to give N x K
@@ -97,7 +103,7 @@ struct Blas {
     // second operand (A): stored [M][K] -> col-major K x M (ld K); stored [K][M] -> M x K (ld M)
     if (s.ta) CK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, s.M, s.K, s.M));
     else CK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, s.K, s.M, s.K));
-    CK(hipblasLtMatrixLayoutCreate(&lc, HIP_R_16BF, s.N, s.M, s.N));
+    CK(hipblasLtMatrixLayoutCreate(&lc, cf32 ? HIP_R_32F : HIP_R_16BF, s.N, s.M, s.N));
     hipblasLtMatmulPreference_t pref;
     CK(hipblasLtMatmulPreferenceCreate(&pref));
     CK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz)));
@@ -131,38 +137,67 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   float* err;
   CK(hipMalloc(&err, 8));
+  const bool wgrad_f32 = getenv("WGRAD_F32") && atoi(getenv("WGRAD_F32"));
+  struct Var { std::string name; int tile, splitk; };
+  std::vector<Var> user_vars;
+  if (const char* vs = getenv("VARS")) {
+    std::string str(vs);
+    size_t p = 0;
+    while (p < str.size()) {
+      size_t q = str.find(',', p);
+      if (q == std::string::npos) q = str.size();
+      std::string tok = str.substr(p, q - p);
+      const size_t c = tok.find(':');
+      const int t = atoi(tok.substr(0, c).c_str());
+      const int sk = c == std::string::npos ? 1 : atoi(tok.substr(c + 1).c_str());
+      user_vars.push_back({"t" + std::to_string(t) + "s" + std::to_string(sk), t, sk});
+      p = q + 1;
+    }
+  }
+  float* ws = nullptr;
+  const size_t ws_bytes = (size_t)1 << 30;
+  CK(hipMalloc(&ws, ws_bytes));
   for (const Shape& s : shapes) {
     const int64_t na = s.M * s.K, nb = s.N * s.K, nc = s.M * s.N;
+    const bool cf32 = wgrad_f32 && s.ta;
+    const int esz = cf32 ? 4 : 2;
     unsigned short *A, *B, *C, *R;
-    CK(hipMalloc(&A, na * 2)); CK(hipMalloc(&B, nb * 2)); CK(hipMalloc(&C, nc * 2)); CK(hipMalloc(&R, nc * 2));
+    CK(hipMalloc(&A, na * 2)); CK(hipMalloc(&B, nb * 2)); CK(hipMalloc(&C, nc * esz)); CK(hipMalloc(&R, nc * esz));
     fill_k<<<1024, 256, 0, st>>>(A, na, 17u);
     fill_k<<<1024, 256, 0, st>>>(B, nb, 91u);
     Blas blas;
-    blas.init(s);
+    blas.init(s, cf32);
     blas.run(A, B, R, st);
     const int64_t lda = s.ta ? s.M : s.K;
     const int64_t ldb = s.tb ? s.K : s.N;
-    struct Var { std::string name; int tile; };
-    std::vector<Var> vars = {{"blas", -1}};
-    for (int t : {0, 1, 2, 3, 5}) {
+    std::vector<Var> vars = {{"blas", -1, 1}};
+    if (!user_vars.empty()) {
+      for (const Var& v : user_vars) vars.push_back(v);
+    } else {
+      for (int t : {0, 1, 2, 3, 5}) {
 #ifdef BENCH_FAST
-      if (t == 0 || t == 2) continue;
+        if (t == 0 || t == 2) continue;
 #endif
-      if (only && !strchr(only, '0' + t)) continue;
-      vars.push_back({"tile" + std::to_string(t), t});
+        if (only && !strchr(only, '0' + t)) continue;
+        vars.push_back({"tile" + std::to_string(t), t, 1});
+      }
     }
     auto run = [&](const Var& v) {
       if (v.tile < 0) { blas.run(A, B, C, st); return; }
-      Epi ep{C, nullptr, nullptr, s.N, 0, 0, 0, 1.f, 0.f, 0, 0, 0, 0, 0, nullptr, 0, nullptr};
-      CK(run_tile((const bf16*)A, (const bf16*)B, !s.ta, s.tb, lda, ldb, ep, s.M, s.N, s.K, st, v.tile));
+      Epi ep{C, nullptr, nullptr, s.N, 0, 0, 0, 1.f, 0.f, 0, cf32 ? 1 : 0, 0, 0, 0, nullptr, 0, nullptr};
+      if (v.splitk > 1) {
+        if ((size_t)v.splitk * nc * 4 > ws_bytes) { fprintf(stderr, "slab too big\n"); exit(1); }
+        ep.slab = ws;
+      }
+      CK(run_tile((const bf16*)A, (const bf16*)B, !s.ta, s.tb, lda, ldb, ep, s.M, s.N, s.K, st, v.tile, v.splitk));
     };
     std::vector<std::vector<float>> ms(vars.size());
     std::vector<float> errs(vars.size(), 0.f);
     for (size_t v = 0; v < vars.size(); ++v) {   // correctness + warm
-      CK(hipMemsetAsync(C, 0, nc * 2, st));
+      CK(hipMemsetAsync(C, 0, nc * esz, st));
       run(vars[v]);
       CK(hipMemsetAsync(err, 0, 8, st));
-      relerr_k<<<1024, 256, 0, st>>>(C, R, nc, err);
+      relerr_k<<<1024, 256, 0, st>>>(C, R, nc, err, cf32 ? 1 : 0);
       float h[2];
       CK(hipMemcpyAsync(h, err, 8, hipMemcpyDeviceToHost, st));
       CK(hipStreamSynchronize(st));
@@ -180,7 +215,7 @@ int main(int argc, char** argv) {
         ms[v].push_back(t / reps);
       }
     const double fl = 2.0 * s.M * s.N * s.K;
-    printf("M %6ld N %6ld K %6ld %s%s |", (long)s.M, (long)s.N, (long)s.K, s.ta ? "T" : "N", s.tb ? "T" : "N");
+    printf("M %6ld N %6ld K %6ld %s%s%s |", (long)s.M, (long)s.N, (long)s.K, s.ta ? "T" : "N", s.tb ? "T" : "N", cf32 ? " f32" : "");
     for (size_t v = 0; v < vars.size(); ++v) {
       std::sort(ms[v].begin(), ms[v].end());
       const float mn = ms[v][0], med = ms[v][ms[v].size() / 2];

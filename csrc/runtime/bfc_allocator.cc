@@ -212,6 +212,10 @@ void BFCAllocator::clean_streams() {
       bin.clear();
     }
   }
+  relist_clean(moved);
+}
+
+void BFCAllocator::relist_clean(std::vector<Chunk*>& moved) {
   if (moved.empty()) return;
   std::unordered_map<Chunk*, int> mv;
   for (Chunk* c : moved) {
@@ -267,6 +271,7 @@ BFCAllocator::Chunk* BFCAllocator::free_chunk(Chunk* c) {
 void* BFCAllocator::allocate(size_t bytes, hipStream_t stream) {
   std::lock_guard<std::mutex> g(mu_);
   if (!tagged()) stream = nullptr;
+  if (!dead_.empty() && stream) dead_.erase(stream);   // a new stream at a recycled address
   size_t size = round_up(bytes ? bytes : 1);
   if (!pending_.empty()) poll_pending(false);
   Chunk* c = nullptr;
@@ -334,6 +339,7 @@ void BFCAllocator::deallocate(void* p, hipStream_t stream) {
   st_.bytes_in_use -= (int64_t)c->size;
   if (tagged() && stream != nullptr) c->stream = stream;
   if (!tagged()) c->stream = nullptr;
+  if (!dead_.empty() && c->stream && dead_.count(c->stream)) c->stream = nullptr;   // destroyed: work complete
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (c->uses && kind_ == MemKind::kDevice && stream != nullptr &&
       hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
@@ -368,6 +374,40 @@ void BFCAllocator::deallocate(void* p, hipStream_t stream) {
     return;
   }
   free_chunk(c);
+}
+
+// `s` is about to be destroyed (its work is complete: the caller synchronised it).
+// Its free and cached chunks move to the clean bins, and later frees that name it are
+// filed clean: a destroyed handle must never be waited on, and a new stream created at
+// the same address must not inherit another stream's chunks.
+void BFCAllocator::forget_stream(hipStream_t s) {
+  if (!s) return;
+  std::lock_guard<std::mutex> g(mu_);
+  poll_pending(true);
+  flush_cache();
+  std::vector<Chunk*> moved;
+  auto it = bins_.find(s);
+  if (it != bins_.end()) {
+    for (auto& bin : it->second.b) {
+      for (Chunk* c : bin) moved.push_back(c);
+      st_.num_free_chunks -= (int64_t)bin.size();
+      bin.clear();
+    }
+    bins_.erase(it);
+  }
+  last_stream_ = nullptr;
+  last_bins_ = nullptr;
+  for (Chunk* c : moved) {
+    c->stream = nullptr;
+    c->listed = false;
+  }
+  relist_clean(moved);
+  for (auto& kv : in_use_) {
+    Chunk* c = kv.second;
+    if (c->stream == s) c->stream = nullptr;
+    if (c->uses) c->uses->erase(std::remove(c->uses->begin(), c->uses->end(), s), c->uses->end());
+  }
+  dead_.insert(s);
 }
 
 void BFCAllocator::record_stream(void* p, hipStream_t stream) {
@@ -468,6 +508,9 @@ HETU_RT_API void hetu_bfc_free(void* h, void* p, void* stream) {
 HETU_RT_API void hetu_bfc_record_stream(void* h, void* p, void* stream) {
   ((BFCAllocator*)h)->record_stream(p, (hipStream_t)stream);
 }
+HETU_RT_API void hetu_bfc_forget_stream(void* h, void* stream) {
+  ((BFCAllocator*)h)->forget_stream((hipStream_t)stream);
+}
 HETU_RT_API void hetu_bfc_set_cache(void* h, int on) { ((BFCAllocator*)h)->set_cache(on != 0); }
 HETU_RT_API int64_t hetu_bfc_size(void* h, void* p) { return (int64_t)((BFCAllocator*)h)->allocation_size(p); }
 HETU_RT_API int64_t hetu_bfc_release(void* h) { return (int64_t)((BFCAllocator*)h)->release_free_regions(); }
@@ -513,16 +556,22 @@ static BFCAllocator* dev_alloc(int device) {
 }
 
 // Private pools for hipGraph capture (the native counterpart of torch's graph memory
-// pools): between hetu_torch_pool_begin and _end every allocation on the device comes
-// from a pool of its own, so the captured step's buffers are never handed to code
-// outside the graph; the graph replays them in capture order.  The pool lives until
-// hetu_torch_pool_release (graph destroyed).
+// pools): between hetu_torch_pool_begin and _end every allocation on the device that is
+// made on the capture stream, or on any stream that is capturing at that moment (side
+// streams forked into the graph), comes from a pool of its own, so the captured step's
+// buffers are never handed to code outside the graph; the graph replays them in
+// capture order.  Other streams (another thread's work) keep the device allocator.
+// The pool lives until hetu_torch_pool_release (graph destroyed); a pool released while
+// some of its chunks are still held (outputs of the graph kept by the caller) retires
+// and is deleted by the free that returns its last chunk.
 static std::map<int64_t, BFCAllocator*> g_pools;
+static std::set<BFCAllocator*> g_retiring;
 static std::atomic<int> g_npools{0};
-static BFCAllocator* g_active_pool[64];
+static std::atomic<BFCAllocator*> g_active_pool[64];
+static std::atomic<hipStream_t> g_active_stream[64];
 static int64_t g_pool_seq = 0;
 
-HETU_RT_API int64_t hetu_torch_pool_begin(int device) {
+HETU_RT_API int64_t hetu_torch_pool_begin(int device, hipStream_t stream) {
   if (device < 0 || device >= 64) return -1;
   std::lock_guard<std::mutex> g(g_dev_mu);
   const char* reg = getenv("HETU_BFC_POOL_REGION_MB");
@@ -531,14 +580,16 @@ HETU_RT_API int64_t hetu_torch_pool_begin(int device) {
   const int64_t id = ++g_pool_seq;
   g_pools[id] = p;
   g_npools.fetch_add(1);
-  g_active_pool[device] = p;
+  g_active_stream[device].store(stream);
+  g_active_pool[device].store(p);
   return id;
 }
 
 HETU_RT_API void hetu_torch_pool_end(int device) {
   if (device < 0 || device >= 64) return;
   std::lock_guard<std::mutex> g(g_dev_mu);
-  g_active_pool[device] = nullptr;
+  g_active_pool[device].store(nullptr);
+  g_active_stream[device].store(nullptr);
 }
 
 HETU_RT_API void hetu_torch_pool_stats(int64_t id, int64_t* out) {
@@ -551,8 +602,8 @@ HETU_RT_API void hetu_torch_pool_stats(int64_t id, int64_t* out) {
   if (p) hetu_bfc_stats(p, out);
 }
 
-// drop a pool: its memory goes back to the driver (the graph using it must be destroyed;
-// chunks still handed out -- static outputs of that graph -- are released with it)
+// drop a pool (the graph using it must be destroyed): its memory goes back to the
+// driver now, or -- while chunks are still held -- when the last one is freed
 HETU_RT_API void hetu_torch_pool_release(int64_t id) {
   BFCAllocator* p = nullptr;
   {
@@ -560,10 +611,16 @@ HETU_RT_API void hetu_torch_pool_release(int64_t id) {
     auto it = g_pools.find(id);
     if (it == g_pools.end()) return;
     p = it->second;
+    for (auto& a : g_active_pool) {
+      BFCAllocator* cur = p;
+      a.compare_exchange_strong(cur, nullptr);
+    }
+    if (p->stats().bytes_in_use > 0) {
+      g_retiring.insert(p);   // still owns chunks: found by owner_of until its last free
+      return;
+    }
     g_pools.erase(it);
     g_npools.fetch_sub(1);
-    for (auto& a : g_active_pool)
-      if (a == p) a = nullptr;
   }
   hipDeviceSynchronize();
   delete p;
@@ -579,19 +636,58 @@ static BFCAllocator* owner_of(int device, void* ptr) {
 }
 
 HETU_RT_API void* hetu_torch_alloc(ssize_t size, int device, hipStream_t stream) {
-  BFCAllocator* a = (device >= 0 && device < 64 && g_active_pool[device]) ? g_active_pool[device] : dev_alloc(device);
+  BFCAllocator* a = nullptr;
+  if (device >= 0 && device < 64) {
+    BFCAllocator* p = g_active_pool[device].load();
+    if (p) {
+      bool mine = stream == g_active_stream[device].load();
+      if (!mine) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        mine = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+      }
+      if (mine) a = p;
+    }
+  }
+  if (!a) a = dev_alloc(device);
   return a ? a->allocate((size_t)size, stream) : nullptr;
 }
 
 HETU_RT_API void hetu_torch_free(void* ptr, ssize_t size, int device, hipStream_t stream) {
   (void)size;
   BFCAllocator* a = g_npools.load() == 0 ? dev_alloc(device) : owner_of(device, ptr);
-  if (a) a->deallocate(ptr, stream);
+  if (!a) return;
+  a->deallocate(ptr, stream);
+  if (g_npools.load() != 0) {
+    BFCAllocator* dead = nullptr;
+    {
+      std::lock_guard<std::mutex> g(g_dev_mu);
+      if (g_retiring.count(a) && a->stats().bytes_in_use == 0) {
+        g_retiring.erase(a);
+        for (auto it = g_pools.begin(); it != g_pools.end(); ++it)
+          if (it->second == a) { g_pools.erase(it); break; }
+        g_npools.fetch_sub(1);
+        dead = a;
+      }
+    }
+    if (dead) {
+      hipDeviceSynchronize();
+      delete dead;
+    }
+  }
 }
 
 HETU_RT_API void hetu_torch_record_stream(int device, void* ptr, hipStream_t stream) {
   BFCAllocator* a = g_npools.load() == 0 ? dev_alloc(device) : owner_of(device, ptr);
   if (a) a->record_stream(ptr, stream);
+}
+
+// a framework stream is being destroyed: the device allocator and every capture pool
+// forget it (DeviceStream.__del__)
+HETU_RT_API void hetu_torch_forget_stream(int device, hipStream_t stream) {
+  BFCAllocator* a = dev_alloc(device);
+  if (a) a->forget_stream(stream);
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  for (auto& kv : g_pools) kv.second->forget_stream(stream);
 }
 
 HETU_RT_API void hetu_torch_stats(int device, int64_t* out) {

@@ -57,6 +57,9 @@ class BFCAllocator {
   // p is also used on `stream` (a side stream: comm, PS staging, prefetch): once freed,
   // the chunk waits for that stream's work queued up to the free before anyone reuses it
   void record_stream(void* p, hipStream_t stream);
+  // `stream` is being destroyed (work complete): its chunks become clean, and frees
+  // that still name it are filed clean
+  void forget_stream(hipStream_t stream);
   size_t allocation_size(void* p);
   AllocatorStats stats();
   size_t release_free_regions();                  // return wholly free regions; bytes released
@@ -117,6 +120,7 @@ class BFCAllocator {
   void erase_free(Chunk* c);
   Chunk* free_chunk(Chunk* c);   // returns the (possibly merged) free chunk
   void clean_streams();
+  void relist_clean(std::vector<Chunk*>& moved);   // clean chunks back into the bins, coalescing
   void poll_pending(bool wait);   // release pending chunks whose side-stream events completed
   void flush_cache();             // cached chunks back into the bins (coalescing)
   Bins& bins_for(hipStream_t s);
@@ -132,6 +136,7 @@ class BFCAllocator {
   hipStream_t last_stream_ = nullptr;   // bins_ lookup cache (map nodes are stable)
   Bins* last_bins_ = nullptr;
   std::vector<Pending> pending_;
+  std::set<hipStream_t> dead_;   // destroyed streams (forget_stream) not seen alive since
   bool cache_on_ = false;
   std::unordered_map<std::pair<hipStream_t, size_t>, std::vector<Chunk*>, CacheKeyHash> cache_;
   size_t cached_n_ = 0;

@@ -48,13 +48,15 @@ def lib():
                                 ('hetu_bfc_free', [P, P, P], None),
                                 ('hetu_bfc_record_stream', [P, P, P], None),
                                 ('hetu_bfc_set_cache', [P, I32], None),
+                                ('hetu_bfc_forget_stream', [P, P], None),
+                                ('hetu_torch_forget_stream', [I32, P], None),
                                 ('hetu_torch_record_stream', [I32, P, P], None),
                                 ('hetu_bfc_size', [P, P], I64),
                                 ('hetu_bfc_release', [P], I64),
                                 ('hetu_bfc_check', [P], I32),
                                 ('hetu_bfc_stats', [P, P], None),
                                 ('hetu_torch_stats', [I32, P], None),
-                                ('hetu_torch_pool_begin', [I32], I64),
+                                ('hetu_torch_pool_begin', [I32, P], I64),
                                 ('hetu_torch_pool_end', [I32], None),
                                 ('hetu_torch_pool_stats', [I64, P], None),
                                 ('hetu_torch_pool_release', [I64], None)):
@@ -79,6 +81,10 @@ class BFCAllocator(object):
         """ptr is also used on ``stream``: held back from reuse after its free until
         that stream's work queued before the free has completed"""
         lib().hetu_bfc_record_stream(self.h, ptr, stream)
+
+    def forget_stream(self, stream):
+        """``stream`` is being destroyed (its work complete): its chunks become clean"""
+        lib().hetu_bfc_forget_stream(self.h, stream)
 
     def set_cache(self, on):
         """exact-size reuse cache in front of the bins (on by default for device pools)"""
@@ -165,10 +171,19 @@ def record_stream(t, stream):
     otherwise.  ``stream``: a torch stream or a runtime.DeviceStream."""
     if _torch_bfc:
         h = stream.handle if hasattr(stream, 'handle') else stream.cuda_stream
-        lib().hetu_torch_record_stream(t.device.index or 0, t.data_ptr(), h)
+        # the allocation's start: a view with an offset (t.data_ptr()) would miss the block
+        lib().hetu_torch_record_stream(t.device.index or 0, t.untyped_storage().data_ptr(), h)
     else:
         t.record_stream(stream.torch if hasattr(stream, 'torch') and not isinstance(stream, torch.cuda.Stream)
                         else stream)
+
+
+def forget_stream(device, handle):
+    """a framework stream is about to be destroyed (runtime.DeviceStream.__del__, after
+    synchronising it): the device allocator and the capture pools move the chunks filed
+    under it to their clean bins instead of keeping a dead handle"""
+    if _torch_bfc and _lib is not None:
+        _lib.hetu_torch_forget_stream(int(device), handle)
 
 
 def device_stats(device=0):
@@ -178,18 +193,22 @@ def device_stats(device=0):
 
 
 class capture_pool(object):
-    """``with capture_pool(device) as pool:`` -- every device allocation in the block
-    comes from a private BFC pool (the native graph-capture pool: a captured step's
-    buffers are replayed by the graph and must never be handed to other code).
+    """``with capture_pool(device, stream) as pool:`` -- every device allocation in the
+    block made on ``stream`` (or on a stream being captured) comes from a private BFC
+    pool (the native graph-capture pool: a captured step's buffers are replayed by the
+    graph and must never be handed to other code).
     ``pool.stats()`` mirrors device_stats; ``pool.release()`` returns its memory
     (only once the graph that uses it is gone)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, stream=None):
         self.device = int(device)
+        self.stream = stream
         self.id = None
 
     def __enter__(self):
-        self.id = lib().hetu_torch_pool_begin(self.device)
+        s = self.stream
+        h = None if s is None else (s.handle if hasattr(s, 'handle') else s.cuda_stream)
+        self.id = lib().hetu_torch_pool_begin(self.device, h)
         return self
 
     def __exit__(self, *exc):

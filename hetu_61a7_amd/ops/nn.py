@@ -120,16 +120,22 @@ class Conv2d_Gradient_of_DataOp(Op):
                 # of call k folds its coefficients in the apply kernel and zeroes the other
                 # half (consumed by call k - 1); R > 1: one buffer, folded and zeroed by the
                 # BN backward's finalize kernel
+                # Under graph capture the flip would be frozen into the graph: every replay
+                # would add into the same half and zero the other, so the captured form
+                # uses one buffer, folded and zeroed by the finalize kernel.
                 from ..kernels.conv_igemm import bn_sum_replicas
+                from ..utils.hipgraph import capturing
                 rep = bn_sum_replicas(xb.numel() // xb.shape[1])
+                double = rep == 1 and not capturing()
                 bufs = self.__dict__.setdefault('_bn_sums', {})
-                pair = bufs.get((xb.device, rep))
+                pair = bufs.get((xb.device, rep, double))
                 if pair is None:
-                    pair = bufs[(xb.device, rep)] = [torch.zeros(rep * 2 * xb.shape[1], dtype=torch.float32,
-                                                                 device=xb.device) for _ in range(2 if rep == 1 else 1)]
+                    pair = bufs[(xb.device, rep, double)] = [
+                        torch.zeros(rep * 2 * xb.shape[1], dtype=torch.float32, device=xb.device)
+                        for _ in range(2 if double else 1)]
                     pair.append(0)
                 k = pair[-1]
-                if rep == 1:
+                if double:
                     pair[-1] = k ^ 1
                 bn = (pair[k], xb, aux[2] if len(aux) > 2 else None)
         r = KC.conv2d_backward_data(g, w, tuple(xshape), self.stride, self.padding, acc=acc,

@@ -115,6 +115,8 @@ class DeviceStream(object):
         if h and _lib is not None and not _SHUTDOWN[0] and not getattr(self, 'persistent', False):
             try:
                 lib().hetu_stream_sync(h)
+                from . import memory_pool
+                memory_pool.forget_stream(self.device, h)
                 lib().hetu_stream_destroy(h)
             except Exception:
                 pass

@@ -166,6 +166,9 @@ def _ext_state(ex, zero_rank):
         d = {'step': op.step, 'name': op.name, 'zero': bool(getattr(op, 'zero', False))}
         if fl is not None:
             d['order'] = [p.name for p in fl.params]
+            # where each parameter's moments sit in the flat buffers: the segment alignment
+            # (optimizer.SEG_ALIGN) and the parameter set may differ at load time
+            d['layout'] = [(p.name, int(fl.offsets[p][0]), int(fl.offsets[p][1])) for p in fl.params]
             if not d['zero']:   # ZeRO shards go to the per-rank file
                 d['s1'] = fl.s1.cpu().numpy() if fl.s1 is not None else None
                 d['s2'] = fl.s2.cpu().numpy() if fl.s2 is not None else None
@@ -288,6 +291,44 @@ def _owned_moments(op, d):
     return out
 
 
+def _load_flat_moments(fl, d, i):
+    """copy whole-buffer moments (s1 / s2) of optimizer record ``d`` into ``fl``
+    parameter by parameter, through the saved layout (name, offset, numel).  A record
+    without a layout (written before layouts were saved) is taken only when its order
+    and buffer size match this flat buffer exactly; anything else is refused rather
+    than loaded under the wrong offsets."""
+    import numpy as np
+    layout = d.get('layout')
+    for k in ('s1', 's2'):
+        buf = getattr(fl, k)
+        arr = d.get(k)
+        if arr is None or buf is None:
+            continue
+        arr = np.asarray(arr).reshape(-1)
+        if layout is None:
+            order = d.get('order')
+            if order != [p.name for p in fl.params] or arr.size != buf.numel():
+                raise ValueError('optimizer %d: checkpoint moments have no layout and do not match this '
+                                 'flat buffer (%d saved elements, %d here, parameter order %s); '
+                                 're-save the checkpoint with this version' %
+                                 (i, arr.size, buf.numel(), 'matches' if order == [p.name for p in fl.params]
+                                  else 'differs'))
+            buf.copy_(torch.from_numpy(arr).to(buf.device))
+            continue
+        saved = {name: (o, n) for name, o, n in layout}
+        host = buf.detach().cpu().numpy().copy()
+        for p in fl.params:
+            o, n, _ = fl.offsets[p]
+            if p.name not in saved:
+                continue
+            so, sn = saved[p.name]
+            if sn != n:
+                raise ValueError('optimizer %d: parameter %s has %d elements, the checkpoint %d'
+                                 % (i, p.name, n, sn))
+            host[o:o + n] = arr[so:so + sn]
+        buf.copy_(torch.from_numpy(host).to(buf.device))
+
+
 def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
     cfg = ex.config
     path = os.path.join(file_path, file_name)
@@ -324,10 +365,13 @@ def load(ex, file_path, file_name='checkpoint.pkl', consider_splits=False):
                 raise ValueError('ZeRO checkpoint was written with %s ranks, resuming with %d'
                                  % (src.get('nrank'), op.comm.nrank))
         if fl is not None:
-            for k in ('s1', 's2'):
-                buf = getattr(fl, k)
-                if src.get(k) is not None and buf is not None:
-                    buf.copy_(torch.from_numpy(src[k]).to(buf.device))
+            if src is d:
+                _load_flat_moments(fl, d, i)
+            else:
+                for k in ('s1', 's2'):
+                    buf = getattr(fl, k)
+                    if src.get(k) is not None and buf is not None:
+                        buf.copy_(torch.from_numpy(src[k]).to(buf.device))
         by_name = {p.name: st for p, st in op.sparse_state.items()}
         for name, st in d.get('sparse', {}).items():
             if name in by_name:

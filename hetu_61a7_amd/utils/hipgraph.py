@@ -11,7 +11,20 @@ from __future__ import annotations
 
 import torch
 
-from ..ops.nn import AuxResult
+_CAPTURING = [0]
+
+
+def capturing():
+    """True while a step is being captured into a graph (framework capture or torch's):
+    ops that keep per-call host state (e.g. double-buffered BatchNorm totals flipped by
+    a Python counter) must use a replay-safe form then -- a replay repeats the captured
+    call, not the host logic around it"""
+    if _CAPTURING[0]:
+        return True
+    try:
+        return bool(torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
+    except RuntimeError:
+        return False
 
 
 class GraphRunner(object):
@@ -22,6 +35,22 @@ class GraphRunner(object):
         self.graph = None
         self.static_in = {}
         self.static_vals = None
+
+    def close(self):
+        """drop the graph, then its outputs, then the capture pool (the pool
+        was never released; a pool still holding chunks the caller kept retires and goes
+        back to the driver with its last free)"""
+        self.graph = None
+        self.static_vals = None
+        pool, self.pool = getattr(self, 'pool', None), None
+        if pool is not None:
+            pool.release()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _inputs(self, feed_dict):
         sub = self.sub
@@ -66,8 +95,12 @@ class GraphRunner(object):
                 self._capture_native(sub, base)
             else:
                 self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph):
-                    self.static_vals = sub._run_eager(None, vals=dict(base))
+                _CAPTURING[0] += 1
+                try:
+                    with torch.cuda.graph(self.graph):
+                        self.static_vals = sub._run_eager(None, vals=dict(base))
+                finally:
+                    _CAPTURING[0] -= 1
             for op in sub.opt_ops:
                 op.step -= 1  # the capture itself executes nothing
         for n, v in new_in.items():
@@ -87,12 +120,14 @@ class GraphRunner(object):
         cap = RT.DeviceStream(dev, persistent=True)
         cap.wait_stream(torch.cuda.current_stream())
         g = RT.Graph()
-        self.pool = MP.capture_pool(dev)
+        self.pool = MP.capture_pool(dev, cap)
         with self.pool, torch.cuda.stream(cap.torch):
             g.begin(cap)
+            _CAPTURING[0] += 1
             try:
                 self.static_vals = sub._run_eager(None, vals=dict(base))
             finally:
+                _CAPTURING[0] -= 1
                 g.end(cap)
         self.capture_stream = cap
         self.graph = _NativeReplay(g)

@@ -263,3 +263,44 @@ def test_resnet50_forward_with_fused_bn_statistics():
     l0, _, _ = _resnet_step(False, False)
     l1, _, _ = _resnet_step(False, True)
     assert abs(l0 - l1) <= 2e-2 * max(1.0, abs(l0)), (l0, l1)
+
+
+def _resnet_losses(use_hipgraph, steps=6):
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.models import resnet50_imagenet
+    from hetu_61a7_amd.ops import node as _node
+    _node.G_NODE_ID = 0
+    os.environ['HETU_FUSE_BN_BWD'] = 'all'
+    try:
+        B = 2
+        x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+        loss, _ = resnet50_imagenet(x, y_, 1000)
+        train = ht.optim.MomentumOptimizer(learning_rate=0.05, momentum=0.9).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3,
+                         use_hipgraph=use_hipgraph)
+        g = torch.Generator(device='cuda')
+        g.manual_seed(0)
+        X = torch.randn((B, 3, 112, 112), device='cuda', generator=g).bfloat16().contiguous(memory_format=CL)
+        Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
+        out = []
+        for _ in range(steps):
+            lv = ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]
+            out.append(float(np.mean(lv)))
+        fused = sum(1 for n in ex.subexecutor['train'].computing_nodes if getattr(n, 'bn_fused', None) is not None)
+        return out, fused
+    finally:
+        os.environ.pop('HETU_FUSE_BN_BWD', None)
+
+
+def test_hipgraph_replays_fused_bn_backward_like_eager():
+    """the fused BN-backward totals were double-buffered by a Python
+    flip; a captured step froze the flip, so every replay added into the same half and
+    zeroed the other.  Small spatial sizes (every layer below 16384 rows: one replica)
+    take that path.  With hipGraph replay (3 eager warm-up steps, then capture + 3
+    replays) the losses must follow the eager ones."""
+    eager, nf = _resnet_losses(False)
+    graph, _ = _resnet_losses(True)
+    assert nf >= 20, nf
+    np.testing.assert_allclose(graph, eager, rtol=2e-2, atol=2e-2)
+    # a frozen flip leaves the totals growing replay after replay: the late losses drift
+    assert abs(graph[-1] - eager[-1]) <= 2e-2 * max(1.0, abs(eager[-1]))

@@ -233,3 +233,35 @@ def test_class_index_label_feeds_stay_fp32():
         assert getattr(t, 'keep_fp32', False)
     dense = ht.Variable(name='d', trainable=False)
     assert not getattr(dense, 'keep_fp32', False)
+
+
+def test_optimizer_moments_load_through_saved_layout():
+    """the flat optimizer buffers align segments (SEG_ALIGN), so moments are
+    saved with each parameter's (offset, numel) and loaded parameter by parameter; a
+    record without a layout that does not match the buffer exactly is refused."""
+    import pytest
+    import torch
+    from hetu_61a7_amd.utils.checkpoint import _load_flat_moments
+
+    class P(object):
+        def __init__(self, name):
+            self.name = name
+
+    class Flat(object):
+        pass
+    a, b = P('a'), P('b')
+    fl = Flat()
+    fl.params = [a, b]
+    fl.offsets = {a: (0, 3, (3,)), b: (8, 5, (5,))}     # b starts at the 8-element boundary
+    fl.s1 = torch.zeros(13)
+    fl.s2 = None
+    saved = np.arange(8, dtype=np.float32)                # old packed layout: a 0..2, b 3..7
+    d = {'order': ['a', 'b'], 'layout': [('a', 0, 3), ('b', 3, 5)], 's1': saved}
+    _load_flat_moments(fl, d, 0)
+    assert fl.s1[:3].tolist() == [0, 1, 2] and fl.s1[8:13].tolist() == [3, 4, 5, 6, 7]
+    assert fl.s1[3:8].abs().sum() == 0
+    with pytest.raises(ValueError):
+        _load_flat_moments(fl, {'order': ['a', 'b'], 's1': saved}, 0)
+    ok = {'order': ['a', 'b'], 's1': np.ones(13, np.float32)}
+    _load_flat_moments(fl, ok, 0)
+    assert float(fl.s1.sum()) == 13

@@ -151,3 +151,21 @@ def test_exact_size_cache():
     for x, s in live:
         a.free(x, s)
     assert a.check() and a.stats()['bytes_in_use'] == 0
+
+
+def test_forget_stream_makes_its_chunks_clean():
+    """a destroyed framework stream must not keep chunks filed under its dead
+    handle (the pool would later wait on it).  forget_stream moves its free chunks to the
+    clean bins, and a later free that still names it is filed clean too."""
+    a = MP.BFCAllocator(MP.HOST_TAGGED, 0, 0, 1 << 20)
+    s1, s2 = 0x1000, 0x2000
+    p = a.alloc(4096, s1)
+    held = a.alloc(8192, s1)
+    a.free(p, s1)
+    assert a.alloc(4096, s2) != p                      # s1's chunk is not s2's to take ...
+    a.forget_stream(s1)
+    assert a.check()
+    assert a.alloc(4096, s2) == p                      # ... until s1 is gone: clean, reusable at once
+    a.free(held, s1)                                   # a late free naming the dead stream
+    assert a.alloc(8192, s2) == held
+    assert a.check()

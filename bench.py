@@ -76,6 +76,34 @@ def _progress(rank, world, msg):
 
 _T0 = time.perf_counter()
 
+_VENDOR_MARKS = ('Cijk', 'igemm', 'SubTensorOp', 'naive_conv', 'MIOpen', 'miopen', 'ck::', '_ZN2ck', 'gridwise_')
+
+
+def _kernel_census(step):
+    """one extra step (outside the timed region) under torch.profiler: device kernels
+    that are PyTorch (at::native / c10) or vendor-library (hipBLASLt / MIOpen / CK)
+    kernels.  Every rank runs it (collectives stay matched)."""
+    import torch
+    from torch.profiler import profile, ProfilerActivity
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        step()
+        torch.cuda.synchronize()
+    n = aten = vendor = 0
+    names = {}
+    for e in prof.events():
+        if 'CUDA' not in str(e.device_type):
+            continue
+        n += 1
+        if 'at::native' in e.name or 'c10::' in e.name:
+            aten += 1
+            names[e.name[:80]] = names.get(e.name[:80], 0) + 1
+        elif any(v in e.name for v in _VENDOR_MARKS):
+            vendor += 1
+            names[e.name[:80]] = names.get(e.name[:80], 0) + 1
+    return {'kernels_per_step': n, 'aten_kernels_per_step': aten, 'vendor_kernels_per_step': vendor,
+            'non_native_kernels': names}
+
 
 def main():
     args = parse()
@@ -155,12 +183,20 @@ def main():
             C.world().barrier()
 
     _progress(rank, world, 'graph built, comm=%s' % (C.world().backend if C.world() is not None else 'none'))
+    if world > 1 and not cpu_only and C.world() is not None and C.world().backend != 'hetu-rccl' and \
+            os.environ.get('HETU_DIST_BACKEND') != 'gloo' and os.environ.get('HETU_COMM', 'native') != 'torch':
+        # a multi-GPU number must come from the framework's own RCCL communicator: a silent
+        # fallback to another backend would be measured and reported as if it were
+        raise SystemExit('bench: %d ranks but the communicator is %r, not the native hetu-rccl (set '
+                         'HETU_COMM=torch to measure torch.distributed on purpose)' % (world, C.world().backend))
     sync = (lambda: None) if cpu_only else torch.cuda.synchronize
     for i in range(args.warmup):
         step()
         _progress(rank, world, 'warmup step %d issued' % i)
     sync()
     _progress(rank, world, 'warmup done')
+    from hetu_61a7_amd import kernels as K
+    K.reset_dispatch_stats()     # vendor_calls / fallbacks below count the timed steps only
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -183,8 +219,15 @@ def main():
         print('non-channels-last 4D outputs:', layout_report(), file=sys.stderr)
     value = samples_per_step * args.steps / dt_s
     _progress(rank, world, 'timed steps done')
+    cfg = dict(cfg)
+    # hand-written-only accounting of the timed steps: library GEMM /
+    # convolution calls and ops that left the native path, then a kernel census of one
+    # more (untimed) step
+    cfg['vendor_calls'] = dict(K.VENDOR_CALLS)
+    cfg['fallbacks'] = dict(K.FALLBACKS)
+    if not cpu_only and os.environ.get('HETU_BENCH_CENSUS', '1') == '1':
+        cfg.update(_kernel_census(step))
     if hasattr(step, 'extra'):
-        cfg = dict(cfg)
         cfg.update(step.extra())
     if world > 1 or args.comm_trace:
         cfg = dict(cfg)

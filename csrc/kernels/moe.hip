@@ -25,7 +25,7 @@
 namespace hetu {
 
 constexpr int kMaxEPL = 8;   // experts per lane (E <= 512)
-constexpr int kMaxK = 8;
+constexpr int kMaxK = 16;    // choices per token (the dense-to-sparse gate starts at k = E = 16 on 8 GPUs)
 
 // ---------------------------------------------------------------------------
 // softmax + top-k per row
@@ -93,6 +93,88 @@ __global__ void __launch_bounds__(256) gate_topk_k(const T* __restrict__ logits,
 }
 
 // ---------------------------------------------------------------------------
+// Dense-to-sparse gate (Nie et al., Hetu README paper #6), one wave per token:
+//   y = softmax((logits + gumbel) / tau)           gumbel = -log(-log(u)), u ~ Philox(seed, t*E + e)
+//   choices j < k in descending y; choice j > 0 is active only while y >= thr (the
+//   top-1 choice is always kept): inactive choices get idx = -1, val = 0 -- the slot
+//   map, combine and gate-gradient kernels skip them, so they take no capacity.
+//   hist[n] += 1 for a token with n active choices (n = 1..k): the host shrinks the
+//   expert budget k (and the capacity) once the threshold leaves fewer experts active.
+template <typename T>
+__global__ void __launch_bounds__(256) dts_gate_k(const T* __restrict__ logits, float* __restrict__ probs,
+                                                   int64_t* __restrict__ idx, float* __restrict__ val,
+                                                   int* __restrict__ hist, int rows, int E, int k, float inv_tau,
+                                                   float thr, uint64_t seed, int noise) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* x = logits + (int64_t)row * E;
+  float v[kMaxEPL];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < kMaxEPL; ++i) {
+    const int e = lane + 64 * i;
+    float z = -INFINITY;
+    if (e < E) {
+      z = to_f(x[e]);
+      if (noise) {
+        const float u = Philox::u01(Philox::gen(seed, (uint64_t)row * (uint64_t)E + (uint64_t)e).x);
+        z -= __logf(-__logf(u));
+      }
+      z *= inv_tau;
+    }
+    v[i] = z;
+    m = fmaxf(m, z);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxEPL; ++i) {
+    const int e = lane + 64 * i;
+    v[i] = (e < E) ? __expf(v[i] - m) : 0.f;
+    s += v[i];
+  }
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int i = 0; i < kMaxEPL; ++i) {
+    const int e = lane + 64 * i;
+    if (e < E) {
+      v[i] *= inv;
+      probs[(int64_t)row * E + e] = v[i];
+    } else {
+      v[i] = -INFINITY;
+    }
+  }
+  int active = 0;
+  for (int j = 0; j < k; ++j) {
+    float bv = -INFINITY;
+    int be = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i) {
+      const int e = lane + 64 * i;
+      if (e < E && (v[i] > bv || (v[i] == bv && e < be))) { bv = v[i]; be = e; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oe = __shfl_xor(be, o, 64);
+      if (ov > bv || (ov == bv && oe < be)) { bv = ov; be = oe; }
+    }
+    const bool on = j == 0 || bv >= thr;     // wave-uniform
+    if (lane == 0) {
+      idx[(int64_t)row * k + j] = on ? be : -1;
+      val[(int64_t)row * k + j] = on ? bv : 0.f;
+    }
+    active += on ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i)
+      if (lane + 64 * i == be) v[i] = -INFINITY;
+  }
+  if (lane == 0 && hist != nullptr) atomicAdd(hist + active, 1);
+}
+
+// ---------------------------------------------------------------------------
 // capacity slots, choice-major: loc(t, j) = #{(t', j') before (t, j) in order
 // (j' < j) or (j' == j, t' < t) with idx == idx(t, j)}.  One workgroup per
 // expert; also counts[e] = routed (t, j) pairs (before drops) and
@@ -138,13 +220,16 @@ __global__ void __launch_bounds__(256) locations_k(const int64_t* __restrict__ i
   }
 }
 
-// dlogits[t, :] = softmax_bwd(p, dp) with
+// dlogits[t, :] = scale * softmax_bwd(p, dp) with
 // dp[t, e] = sum_j [idx(t, j) == e] * dgate[t, j] + aux_coef[e]
+// (scale = 1 / tau for the tempered softmax of the dense-to-sparse gate; choices with
+// idx = -1 -- inactive -- carry no gradient: the threshold mask's derivative)
 __global__ void __launch_bounds__(256) gate_backward_k(const float* __restrict__ probs,
                                                        const int64_t* __restrict__ idx,
                                                        const float* __restrict__ dgate,
                                                        const float* __restrict__ aux_coef,
-                                                       float* __restrict__ dlogits, int rows, int E, int k) {
+                                                       float* __restrict__ dlogits, int rows, int E, int k,
+                                                       float scale) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -174,7 +259,7 @@ __global__ void __launch_bounds__(256) gate_backward_k(const float* __restrict__
 #pragma unroll
   for (int i = 0; i < kMaxEPL; ++i) {
     const int e = lane + 64 * i;
-    if (e < E) dlogits[(int64_t)row * E + e] = p[i] * (dp[i] - dot);
+    if (e < E) dlogits[(int64_t)row * E + e] = scale * p[i] * (dp[i] - dot);
   }
 }
 
@@ -330,6 +415,27 @@ HETU_API int hetu_moe_gate_topk(const void* logits, float* probs, int64_t* idx, 
   return 0;
 }
 
+// hist: [k + 1] active-choice histogram, zeroed here (the host reads it a step later)
+HETU_API int hetu_moe_dts_gate(const void* logits, float* probs, int64_t* idx, float* val, int* hist, int rows,
+                               int E, int k, float inv_tau, float thr, uint64_t seed, int noise, int bf16_in,
+                               hipStream_t s) {
+  if (E > 64 * kMaxEPL || k > kMaxK || k > E || k < 1) return (int)hipErrorInvalidValue;
+  if (hist != nullptr) {
+    hipError_t e = hipMemsetAsync(hist, 0, (size_t)(k + 1) * sizeof(int), s);
+    if (e != hipSuccess) return (int)e;
+  }
+  const int g = (rows + 3) / 4;
+  if (g == 0) return 0;
+  if (bf16_in)
+    dts_gate_k<bf16><<<g, 256, 0, s>>>((const bf16*)logits, probs, idx, val, hist, rows, E, k, inv_tau, thr, seed,
+                                       noise);
+  else
+    dts_gate_k<float><<<g, 256, 0, s>>>((const float*)logits, probs, idx, val, hist, rows, E, k, inv_tau, thr,
+                                        seed, noise);
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
 // Balance-loss terms of a top-k gate in one tiny launch (one wave): coef[e] = counts[e] / T,
 // l_aux = E * sum_e (psum[e] / T) * coef[e]  (reference TopGate.py's load-balancing loss).
 __global__ void __launch_bounds__(64) moe_aux_k(const int* __restrict__ counts, const float* __restrict__ psum,
@@ -360,11 +466,12 @@ HETU_API int hetu_moe_locations(const int64_t* idx, const float* probs, int64_t*
 }
 
 HETU_API int hetu_moe_gate_backward(const float* probs, const int64_t* idx, const float* dgate,
-                                    const float* aux_coef, float* dlogits, int rows, int E, int k, hipStream_t s) {
+                                    const float* aux_coef, float* dlogits, int rows, int E, int k, float scale,
+                                    hipStream_t s) {
   if (E > 64 * kMaxEPL || k > kMaxK) return (int)hipErrorInvalidValue;
   const int g = (rows + 3) / 4;
   if (g == 0) return 0;
-  gate_backward_k<<<g, 256, 0, s>>>(probs, idx, dgate, aux_coef, dlogits, rows, E, k);
+  gate_backward_k<<<g, 256, 0, s>>>(probs, idx, dgate, aux_coef, dlogits, rows, E, k, scale);
   HETU_LAUNCH_CHECK();
   return 0;
 }

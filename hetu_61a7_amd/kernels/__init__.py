@@ -114,10 +114,32 @@ def record_native(name):
     NATIVE_CALLS[name] = NATIVE_CALLS.get(name, 0) + 1
 
 
-def record_vendor(name):
-    """a GPU GEMM / convolution served by the vendor library (hipBLASLt / MIOpen via torch);
-    callers record device tensors only (the CPU reference path is not counted)"""
+class VendorFallbackError(RuntimeError):
+    """a GPU GEMM / convolution would run on the vendor library in the hand-written-only
+    mode (HETU_GEMM / HETU_CONV = hip, the default)"""
+
+
+def vendor_allowed(name):
+    """library GEMMs / convolutions are an explicit opt-in: HETU_GEMM (gemm, bmm) or
+    HETU_CONV (conv) set to ``vendor`` / ``auto``, or HETU_ALLOW_VENDOR=1.  Read at call
+    time, so a test or a tool can enable them around one call."""
+    if os.environ.get('HETU_ALLOW_VENDOR', '0') == '1':
+        return True
+    mode = os.environ.get('HETU_CONV' if name.startswith('conv') else 'HETU_GEMM', 'hip')
+    return mode != 'hip'
+
+
+def record_vendor(name, detail=''):
+    """a GPU GEMM / convolution about to be served by the vendor library (hipBLASLt /
+    MIOpen via torch); callers record device tensors only (the CPU reference path is not
+    counted).  In the default hand-written-only mode this raises VendorFallbackError
+    instead: a shape no hand-written kernel takes is a bug to fix, not a silent library
+    call."""
     VENDOR_CALLS[name] = VENDOR_CALLS.get(name, 0) + 1
+    if not vendor_allowed(name):
+        raise VendorFallbackError('%s%s has no hand-written kernel and the vendor library is not enabled '
+                                  '(HETU_ALLOW_VENDOR=1, or HETU_GEMM / HETU_CONV = vendor | auto)'
+                                  % (name, (' ' + detail) if detail else ''))
 
 
 def reset_dispatch_stats():

@@ -10,6 +10,8 @@ the top-k gate is fused (softmax + top-k + capacity slots + balance terms).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32
@@ -56,7 +58,7 @@ def topk(x, k, softmax=False):
     return v, i
 
 
-def locations(idx, num_experts, probs=None):
+def locations(idx, num_experts, probs=None, inactive=False):
     """Slot of every (token, choice) inside its expert, choice-major (the
     reference's cumsum chain, moe_layer.py / TopGate.py), plus per-expert routed
     counts and column sums of ``probs`` (balance loss terms)."""
@@ -65,6 +67,9 @@ def locations(idx, num_experts, probs=None):
     if native(idx):
         idx = idx.long().contiguous()
         loc = torch.empty((T, k), dtype=torch.int64, device=idx.device)
+        if inactive:   # choices with idx -1 (dense-to-sparse gate) keep loc -1: dropped everywhere
+            from .tensor import fill_
+            fill_(loc, -1)
         counts = torch.empty((E,), dtype=torch.int32, device=idx.device)
         psum = torch.empty((E,), dtype=torch.float32, device=idx.device) if probs is not None else None
         f = fn('hetu_moe_locations', [P, P, P, P, P, I32, I32, I32, P])
@@ -72,9 +77,12 @@ def locations(idx, num_experts, probs=None):
                 counts.data_ptr(), psum.data_ptr() if psum is not None else None, T, k, E, stream_ptr()),
               'moe_locations')
         return loc, counts, psum
-    oh = torch.nn.functional.one_hot(idx.long().t().reshape(-1), E)          # [(j, t), E], choice-major
+    il = idx.long()
+    on = (il >= 0).t().reshape(-1)
+    oh = torch.nn.functional.one_hot(il.clamp_min(0).t().reshape(-1), E) * on.unsqueeze(1)   # [(j, t), E]
     cum = torch.cumsum(oh, 0) - 1
-    loc = (cum * oh).sum(1).reshape(k, T).t().contiguous()
+    loc = torch.where(on, (cum * oh).sum(1), torch.full_like(on, -1, dtype=torch.int64))
+    loc = loc.reshape(k, T).t().contiguous()
     counts = oh.sum(0).int()
     psum = probs.float().sum(0) if probs is not None else None
     return loc, counts, psum
@@ -94,25 +102,93 @@ def aux_terms(counts, psum, T):
     return coef, (psum / float(T) * coef).sum() * float(E)
 
 
-def gate_backward(probs, idx, dgate, aux_coef):
-    """d logits of (gate values [T, k] = probs[t, idx], balance term sum_e c_e * sum_t probs[t, e])."""
+MAX_K = 16   # choices per token the kernels take (moe.hip kMaxK)
+
+
+def gate_backward(probs, idx, dgate, aux_coef, scale=1.0):
+    """d logits of (gate values [T, k] = probs[t, idx], balance term sum_e c_e * sum_t probs[t, e]),
+    times ``scale`` (1 / tau of a tempered softmax); choices with idx < 0 carry no gradient."""
     T, E = probs.shape
     k = idx.shape[1]
-    if native(probs) and E <= 512 and k <= 8:
+    if native(probs) and E <= 512 and k <= MAX_K:
         out = torch.empty((T, E), dtype=torch.float32, device=probs.device)
         dg = _dc(dgate.reshape(T, k), torch.float32) if dgate is not None else None
         ac = _dc(aux_coef, torch.float32) if aux_coef is not None else None
-        f = fn('hetu_moe_gate_backward', [P, P, P, P, P, I32, I32, I32, P])
+        f = fn('hetu_moe_gate_backward', [P, P, P, P, P, I32, I32, I32, ctypes.c_float, P])
         check(f(probs.contiguous().data_ptr(), idx.long().contiguous().data_ptr(), ptr_or_none(dg), ptr_or_none(ac),
-                out.data_ptr(), T, E, k, stream_ptr()), 'moe_gate_backward')
+                out.data_ptr(), T, E, k, float(scale), stream_ptr()), 'moe_gate_backward')
         return out
     dp = torch.zeros((T, E), dtype=torch.float32, device=probs.device)
     if dgate is not None:
-        dp.scatter_add_(1, idx.long(), dgate.float().reshape(T, k))
+        il = idx.long()
+        on = il >= 0
+        dp.scatter_add_(1, torch.where(on, il, torch.zeros_like(il)),
+                        torch.where(on, dgate.float().reshape(T, k), torch.zeros((T, k), device=probs.device)))
     if aux_coef is not None:
         dp = dp + aux_coef.float().unsqueeze(0)
     p = probs.float()
-    return p * (dp - (p * dp).sum(-1, keepdim=True))
+    return scale * p * (dp - (p * dp).sum(-1, keepdim=True))
+
+
+# ---- dense-to-sparse gate ------------------------------------------------------------------
+def _philox_x(seed, counter):
+    """first 32-bit output of Philox4x32-10 (common.h Philox::gen(...).x) for uint64 arrays of
+    counters -- the CPU reference path draws the same Gumbel noise as the HIP kernel"""
+    import numpy as np
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    m32 = np.uint64(0xFFFFFFFF)
+    c = np.asarray(counter, dtype=np.uint64)
+    c0 = c & m32
+    c1 = c >> np.uint64(32)
+    c2 = np.zeros_like(c0)
+    c3 = np.zeros_like(c0)
+    k0 = np.uint64(seed & 0xFFFFFFFF)
+    k1 = np.uint64((seed >> 32) & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & m32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & m32
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & m32, lo1, (hi0 ^ c3 ^ k1) & m32, lo0
+        k0 = (k0 + np.uint64(0x9E3779B9)) & m32
+        k1 = (k1 + np.uint64(0xBB67AE85)) & m32
+    return c0
+
+
+def dts_gate(logits, k, inv_tau, threshold, seed, noise=True):
+    """Dense-to-sparse gate forward (moe.hip dts_gate_k): y = softmax((logits + gumbel) * inv_tau);
+    the k largest choices per token, choice j > 0 active only while y >= threshold (inactive:
+    idx -1, value 0).  Returns (val [T, k] fp32, idx [T, k] int64, probs [T, E] fp32,
+    hist [k + 1] int32: tokens by number of active choices)."""
+    T, E = logits.shape
+    seed = int(seed) & ((1 << 63) - 1)
+    if native(logits) and supported_float(logits) and E <= 512 and 1 <= k <= min(MAX_K, E):
+        x = logits.contiguous()
+        probs = torch.empty((T, E), dtype=torch.float32, device=x.device)
+        idx = torch.empty((T, k), dtype=torch.int64, device=x.device)
+        val = torch.empty((T, k), dtype=torch.float32, device=x.device)
+        hist = torch.empty((k + 1,), dtype=torch.int32, device=x.device)
+        f = fn('hetu_moe_dts_gate', [P, P, P, P, P, I32, I32, I32, ctypes.c_float, ctypes.c_float, ctypes.c_uint64,
+                                     I32, I32, P])
+        check(f(x.data_ptr(), probs.data_ptr(), idx.data_ptr(), val.data_ptr(), hist.data_ptr(), T, E, k,
+                float(inv_tau), float(threshold), seed, int(bool(noise)), is_bf16(x), stream_ptr()), 'moe_dts_gate')
+        return val, idx, probs, hist
+    if logits.is_cuda:
+        raise RuntimeError('dts_gate: no hand-written kernel for E=%d k=%d %s' % (E, k, logits.dtype))
+    import numpy as np
+    z = logits.float()
+    if noise:
+        cnt = (np.arange(T, dtype=np.uint64)[:, None] * np.uint64(E) + np.arange(E, dtype=np.uint64)[None, :])
+        u = (_philox_x(seed, cnt) >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0) + 0.5 / 16777216.0
+        z = z - torch.from_numpy(np.log(-np.log(u)).astype(np.float32))
+    probs = torch.softmax(z * float(inv_tau), -1)
+    v, i = torch.topk(probs, k, dim=-1)           # ties: torch order; the kernel takes the lowest id
+    on = torch.ones_like(v, dtype=torch.bool)
+    on[:, 1:] = v[:, 1:] >= threshold
+    idx = torch.where(on, i, torch.full_like(i, -1))
+    val = torch.where(on, v, torch.zeros_like(v))
+    hist = torch.bincount(on.sum(1), minlength=k + 1).to(torch.int32)
+    return val, idx, probs, hist
 
 
 def ptr_or_none(t):
@@ -142,7 +218,7 @@ def layout_transform(x, indices, locations, capacity, num_experts):
               'moe_gather_slots')
         return out
     out = torch.zeros((nslots, d), dtype=x.dtype, device=x.device)
-    valid = loc < capacity
+    valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
     slots = idx * capacity + loc
     tok = torch.arange(T, device=x.device).unsqueeze(1).expand(T, k)
     out[slots[valid]] = x[tok[valid]]
@@ -166,9 +242,9 @@ def layout_transform_backward(g, indices, locations, capacity):
     T = indices.shape[0]
     idx, loc = _ik(indices, T), _ik(locations, T)
     k = idx.shape[1]
-    if _io_ok(g) and k <= 8:
+    if _io_ok(g) and k <= MAX_K:
         return _combine(g, idx, loc, None, capacity, T)
-    valid = (loc < capacity)
+    valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
     slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
     gathered = g[slots.reshape(-1)].reshape(T, k, -1) * valid.unsqueeze(-1).to(g.dtype)
     return gathered.sum(1)
@@ -179,9 +255,9 @@ def reverse_layout_transform(y, indices, locations, gates, capacity):
     T = indices.shape[0]
     idx, loc = _ik(indices, T), _ik(locations, T)
     k = idx.shape[1]
-    if _io_ok(y) and k <= 8:
+    if _io_ok(y) and k <= MAX_K:
         return _combine(y, idx, loc, gates, capacity, T)
-    valid = loc < capacity
+    valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
     slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
     rows = y[slots.reshape(-1)].reshape(T, k, -1).float()
     w = (gates.reshape(T, k).float() * valid.float()) if gates is not None else valid.float()
@@ -202,7 +278,7 @@ def reverse_layout_transform_backward_data(g, indices, locations, gates, capacit
         check(f(g.data_ptr(), smap.data_ptr(), ptr_or_none(wf), out.data_ptr(), num_slots, d, k, is_bf16(g),
                 stream_ptr()), 'moe_gather_slots')
         return out
-    valid = loc < capacity
+    valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
     slots = idx * capacity + loc
     w = (gates.reshape(T, k).float() * valid.float()) if gates is not None else valid.float()
     out = torch.zeros((num_slots, d), dtype=torch.float32, device=g.device)
@@ -223,7 +299,7 @@ def reverse_layout_transform_backward_gate(g, y, indices, locations, capacity):
         check(f(g.data_ptr(), y.data_ptr(), idx.data_ptr(), loc.data_ptr(), out.data_ptr(), T * k, k, capacity, d,
                 is_bf16(g), stream_ptr()), 'moe_gate_grad')
         return out.reshape(indices.shape)
-    valid = loc < capacity
+    valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
     slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
     rows = y[slots.reshape(-1)].reshape(T, k, -1).float()
     dd = (rows * g.float().unsqueeze(1)).sum(-1) * valid.float()

@@ -196,7 +196,8 @@ class BalanceAssignmentGate(_GateBase):
 
 
 class DTSTemperature(object):
-    """Annealing schedule of the Dense-To-Sparse gate: tau_t = max(tau_min, tau0 * decay^t)."""
+    """Annealing schedule of the Dense-To-Sparse gate: tau_t = max(tau_min, tau0 * decay^t).
+    The executor steps it once per training step (``DTSGatingOp.on_step_end``)."""
 
     def __init__(self, tau0=2.0, tau_min=0.3, decay=0.999):
         self.tau0, self.tau_min, self.decay = tau0, tau_min, decay
@@ -213,33 +214,32 @@ class DTSTemperature(object):
 
 class DenseToSparseGate(_GateBase):
     """Dense-To-Sparse gate (Nie et al., "Dense-to-Sparse Gate for Mixture-of-
-    Experts", Hetu paper #6): a Gumbel-softmax gate whose temperature is annealed
-    during training, so routing starts dense (every expert gets weight) and
-    becomes sparse; experts whose gate weight falls below ``threshold`` are
-    dropped.  ``k`` bounds the number of active experts per token (static
-    capacity for the all-to-all); early in training k is the full budget, later
-    the threshold leaves ~1 active expert."""
+    Experts", Hetu paper #6; reference README.md:123, routing as layers/moe_layer.py:60-88).
+    A Gumbel-softmax gate whose temperature anneals once per training step: routing
+    starts dense -- every expert active for every token, capacity for k = E -- and
+    becomes sparse as the experts whose gate weight falls below ``threshold`` drop out;
+    the expert budget (and the capacity, i.e. the all-to-all and expert GEMM sizes)
+    follows the measured active count down to top-1 (``k_min``).  One fused HIP kernel
+    computes noise, tempered softmax, threshold and the choices (ops.moe_dts).
+    ``k``: kept for API compatibility with the other gates (the dense start is k = E)."""
 
     def __init__(self, embed_dim, num_tokens, num_experts, k=2, capacity_factor=1.0,
                  eval_capacity_factor=1.0, initializer=None, name='DTS_Gate', threshold=1e-3,
-                 temperature=None):
+                 temperature=None, k_start=None, k_min=1):
         super().__init__(embed_dim, num_tokens, num_experts, k, capacity_factor, eval_capacity_factor,
                          initializer, name)
         self.threshold = threshold
         self.temperature = temperature or DTSTemperature()
+        self.k_start, self.k_min = k_start, k_min
+        self.gating = None
 
     def __call__(self, x):
-        from ..ops.moe_dts import gumbel_softmax_op, threshold_mask_op
-        k, E = self.top_k, self.num_experts
-        gates = gumbel_softmax_op(self._logits(x), self.temperature)
-        capacity = k * math.ceil((self.num_tokens / E) * self.capacity_factor)
-        topk_indices = O.topk_idx_op(gates, topk=k)
-        indices_s = [O.split_op(topk_indices, axes=[1], indices=[i], splits=[k]) for i in range(k)]
-        masks = [O.array_reshape_op(O.one_hot_op(ix, num_classes=E), [-1, E]) for ix in indices_s]
-        l_aux = balance_loss(gates, masks[0], E)
-        location_s = _fused_locations(topk_indices, k, E)
-        gates_s = [threshold_mask_op(O.reduce_sum_op(O.mul_op(gates, m), axes=1), self.threshold) for m in masks]
-        return l_aux, indices_s, location_s, gates_s, capacity
+        from ..ops.moe_dts import dts_gating_op
+        l_aux, idx, loc, gates, capacity = dts_gating_op(
+            self._logits(x), self.num_tokens, self.num_experts, self.temperature, self.threshold,
+            self.capacity_factor, k_start=self.k_start, k_min=self.k_min)
+        self.gating = gates
+        return l_aux, [idx], [loc], [gates], capacity
 
 
 class Expert(BaseLayer):

@@ -175,11 +175,14 @@ def logreg_bench(args, world, rank, local):
         from torch.profiler import profile, ProfilerActivity
         with profile(activities=[ProfilerActivity.CPU]) as prof:
             step()
-        # allocation / view / metadata ops move no data; anything else is ATen compute
-        meta = ('empty', 'empty_strided', 'empty_like', 'view', 'reshape', 'as_strided', 'expand', 'permute', 'transpose', 'select', 'slice',
-                'detach', 'alias', 'unsqueeze', 'squeeze', 'resolve', 'lift', 'result_type', 'is_', 'size',
-                'stride', 'numel', 'contiguous', 't', 'flatten', 'unfold', '_unsafe_view', 'set_', 'to',
-                '_to_copy', 'narrow', 'item', '_local_scalar_dense', 'broadcast_to')
+        # allocation / view / metadata ops move no data; anything else is ATen compute.
+        # aten::to and aten::contiguous are dispatchers that return their input unchanged
+        # when nothing has to move -- a real conversion or copy shows up as the
+        # aten::_to_copy / aten::clone / aten::copy_ it calls, which are counted
+        meta = ('empty', 'empty_strided', 'empty_like', 'view', 'reshape', 'as_strided', 'expand', 'permute',
+                'transpose', 'select', 'slice', 'detach', 'alias', 'unsqueeze', 'squeeze', 'resolve', 'lift',
+                'result_type', 'is_', 'size', 'stride', 'numel', 'contiguous', 't', 'flatten', 'unfold',
+                '_unsafe_view', 'set_', 'to', 'narrow', 'broadcast_to')
         compute = sorted({e.key for e in prof.key_averages() if e.key.startswith('aten::') and
                           e.key[6:].lstrip('_') not in meta and not any(e.key[6:] == m for m in meta)})
         return {'aten_compute_ops_per_step': compute, 'native_cpu_fallbacks': dict(cpu_native.FALLBACKS),

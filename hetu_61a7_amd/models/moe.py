@@ -54,15 +54,17 @@ def moe_top(x, y_, batch_size, num_tokens, model_dim, hidden_size, num_local_exp
 
 
 def moe_top_bench(args, world, rank, local):
-    """Benchmark step for BASELINE config 5 (reference test_moe_top.py defaults:
-    per GPU batch 16 x 1024 tokens, d_model = d_ffn = 2048, 2 experts per GPU,
-    top-2, expert dropout 0.1, SGD lr 0.125), bf16 compute.  Gate: top-k (default)
-    or the dense-to-sparse gate (``--moe-gate dts``).
+    """Benchmark step for BASELINE config 5: the reference's top-2 script
+    (examples/moe/scripts/run_top2.sh:1 -- test_moe_top.py --top=2 --num_local_experts=2
+    --batch_size=64; 1024 tokens per sequence, d_model = d_ffn = 2048, expert dropout
+    0.1, SGD lr 0.125), bf16 compute.  Gate: top-k (default) or the dense-to-sparse gate
+    (``--moe-gate dts``: its temperature anneals once per step and the JSON reports the
+    budget / active experts per token of the last step read).
     Returns (step_fn, samples_per_step, config, metric, finish_fn); a "sample"
     is one token."""
     import torch
     import hetu_61a7_amd as H
-    B, T, d, ffn, nle = args.batch or 16, 1024, 2048, 2048, 2
+    B, T, d, ffn, nle = args.batch or 64, 1024, 2048, 2048, 2
     gate = getattr(args, 'moe_gate', 'topk')
     x, y_ = H.Variable(name='x', trainable=False), H.Variable(name='y_', trainable=False)
     loss, y = moe_top(x, y_, B, T, d, ffn, nle, world, rank, top=2, gate=gate)
@@ -82,6 +84,17 @@ def moe_top_bench(args, world, rank, local):
 
     def step():
         ex.run('train', feed_dict=feed)
+
+    if gate == 'dts':
+        from ..ops.moe_dts import DTSGatingOp
+        g = [n for n in ex.subexecutor['train'].topo_order if isinstance(n, DTSGatingOp)][0]
+
+        def extra():
+            h = g.history[-1] if g.history else None
+            return {'dts': {'steps': g.calls, 'tau': round(g.temperature.value, 4), 'budget_k': g.budget,
+                            'active_experts_per_token_last': round(h[3], 3) if h else None,
+                            'active_experts_first_to_last': [round(x[3], 3) for x in g.history[::max(1, len(g.history) // 8)]]}}
+        step.extra = extra
 
     cfg = {'model': 'MoE top-2 (examples/moe/test_moe_top.py: d=2048, ffn=2048, 2 experts/GPU)',
            'global_batch': B * world, 'seq_len': T, 'parallelism': 'ep%d (all-to-all) + dp%d gate' % (world, world),

@@ -445,6 +445,9 @@ class SubExecutor(object):
                     if t is not None and hasattr(t, 'next_ids_fn'):
                         self.ps_prefetch.append((t, n.inputs[1]))
         self.mode_nodes = [n for n in self.topo_order if hasattr(n, 'inference')]
+        # per-training-step schedules owned by ops (the dense-to-sparse MoE gate's
+        # temperature): stepped once after every training step of this sub-graph
+        self.step_end_nodes = [n for n in self.topo_order if hasattr(n, 'on_step_end')]
         self._build_plan()
         self.timer = None
         self.graph = None
@@ -544,9 +547,14 @@ class SubExecutor(object):
         cfg = self.config
         for n in self.mode_nodes:
             n.inference = self.inference
-        if cfg.use_hipgraph and cfg.device.type == 'cuda':
+        if cfg.use_hipgraph and cfg.device.type == 'cuda' and not self.step_end_nodes:
+            # (ops with per-step host schedules -- the DTS gate's temperature and budget --
+            # change launch arguments and shapes between steps: not replayable, run eager)
             return self._run_graph(feed_dict, convert_to_numpy_ret_vals)
         vals = self._run_eager(feed_dict)
+        if self.opt_ops and not self.inference:
+            for n in self.step_end_nodes:
+                n.on_step_end()
         return self._collect(vals, convert_to_numpy_ret_vals)
 
     def _prepare_inputs(self, feed_dict):

@@ -17,6 +17,16 @@ from ..kernels import native as _native, record_fallback as _record_fallback
 from ..kernels import tensor as KT
 
 
+def _cap(c):
+    """a capacity: an int, or an object whose ``value`` is read at every step (the
+    dense-to-sparse gate's capacity follows its expert budget, ops.moe_dts.DTSCapacity)"""
+    return int(c.value) if hasattr(c, 'value') else int(c)
+
+
+def _keep(c):
+    return c if hasattr(c, 'value') else int(c)
+
+
 def _gpu(t):
     return isinstance(t, torch.Tensor) and _native(t) and t.dtype in (torch.float32, torch.bfloat16)
 
@@ -33,7 +43,7 @@ class LayoutTransformOp(Op):
         location_s = list(location_s) if isinstance(location_s, (list, tuple)) else [location_s]
         super().__init__(LayoutTransformOp, [x] + indices_s + location_s, ctx)
         self.k = len(indices_s)
-        self.capacity, self.num_experts = int(capacity), int(num_experts)
+        self.capacity, self.num_experts = _keep(capacity), int(num_experts)
 
     def _idx(self, vals):
         k = self.k
@@ -42,7 +52,7 @@ class LayoutTransformOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         idx, loc = self._idx(input_vals)
         x = input_vals[0]
-        return KM.layout_transform(x.reshape(x.shape[0], -1), idx, loc, self.capacity, self.num_experts)
+        return KM.layout_transform(x.reshape(x.shape[0], -1), idx, loc, _cap(self.capacity), self.num_experts)
 
     def gradient(self, output_grad):
         k = self.k
@@ -51,7 +61,7 @@ class LayoutTransformOp(Op):
         return [g] + [None] * (2 * k)
 
     def infer_shape(self, input_shapes):
-        return (self.num_experts * self.capacity, input_shapes[0][-1])
+        return (self.num_experts * _cap(self.capacity), input_shapes[0][-1])
 
 
 class LayoutTransformGradientOp(Op):
@@ -59,12 +69,12 @@ class LayoutTransformGradientOp(Op):
         indices_s = list(indices_s) if isinstance(indices_s, (list, tuple)) else [indices_s]
         location_s = list(location_s) if isinstance(location_s, (list, tuple)) else [location_s]
         super().__init__(LayoutTransformGradientOp, [grad] + indices_s + location_s, ctx)
-        self.k, self.capacity = len(indices_s), int(capacity)
+        self.k, self.capacity = len(indices_s), _keep(capacity)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         k = self.k
         idx, loc = _stack(input_vals[1:1 + k]), _stack(input_vals[1 + k:1 + 2 * k])
-        return KM.layout_transform_backward(input_vals[0], idx, loc, self.capacity)
+        return KM.layout_transform_backward(input_vals[0], idx, loc, _cap(self.capacity))
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -91,7 +101,7 @@ class ReverseLayoutTransformOp(Op):
         super().__init__(ReverseLayoutTransformOp, [y] + indices_s + location_s + gates, ctx)
         self.k = len(indices_s)
         self.has_gate = len(gates) > 0
-        self.capacity, self.num_experts = int(capacity), int(num_experts)
+        self.capacity, self.num_experts = _keep(capacity), int(num_experts)
 
     def _parts(self, vals):
         k = self.k
@@ -102,7 +112,7 @@ class ReverseLayoutTransformOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         idx, loc, gates = self._parts(input_vals)
-        return KM.reverse_layout_transform(input_vals[0], idx, loc, gates, self.capacity)
+        return KM.reverse_layout_transform(input_vals[0], idx, loc, gates, _cap(self.capacity))
 
     def gradient(self, output_grad):
         k = self.k
@@ -128,32 +138,32 @@ class ReverseLayoutTransformGradientDataOp(Op):
         gates = (list(gates) if isinstance(gates, (list, tuple)) else [gates]) if gates is not None else []
         super().__init__(ReverseLayoutTransformGradientDataOp, [grad] + indices_s + location_s + gates, ctx)
         self.k, self.has_gate = len(indices_s), len(gates) > 0
-        self.capacity, self.num_experts = int(capacity), int(num_experts)
+        self.capacity, self.num_experts = _keep(capacity), int(num_experts)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         k = self.k
         idx, loc = _stack(input_vals[1:1 + k]), _stack(input_vals[1 + k:1 + 2 * k])
         gates = _stack(input_vals[1 + 2 * k:1 + 3 * k]) if self.has_gate else None
-        return KM.reverse_layout_transform_backward_data(input_vals[0], idx, loc, gates, self.capacity,
-                                                         self.capacity * self.num_experts)
+        cap = _cap(self.capacity)
+        return KM.reverse_layout_transform_backward_data(input_vals[0], idx, loc, gates, cap, cap * self.num_experts)
 
     def gradient(self, output_grad):
         raise NotImplementedError
 
     def infer_shape(self, input_shapes):
-        return (self.capacity * self.num_experts, input_shapes[0][-1])
+        return (_cap(self.capacity) * self.num_experts, input_shapes[0][-1])
 
 
 class ReverseLayoutTransformGradientGateOp(Op):
     def __init__(self, grad, y, indices, locations, capacity, ctx=None):
         super().__init__(ReverseLayoutTransformGradientGateOp, [grad, y, indices, locations], ctx)
-        self.capacity = int(capacity)
+        self.capacity = _keep(capacity)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, y, idx, loc = input_vals
         if idx.dim() != 2:
             idx, loc = idx.reshape(-1, 1), loc.reshape(-1, 1)
-        return KM.reverse_layout_transform_backward_gate(g, y, idx, loc, self.capacity).reshape(input_vals[2].shape)
+        return KM.reverse_layout_transform_backward_gate(g, y, idx, loc, _cap(self.capacity)).reshape(input_vals[2].shape)
 
     def gradient(self, output_grad):
         raise NotImplementedError
@@ -391,7 +401,9 @@ class TopKGatingGradOp(Op):
         self.is_aux = grad is None
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        g, (val, (probs, idx, loc, l_aux, coef)) = input_vals
+        g, (val, aux) = input_vals
+        probs, idx, loc, l_aux, coef = aux[:5]
+        scale = aux[5] if len(aux) > 5 else 1.0     # 1 / tau of the dense-to-sparse gate
         T, E = probs.shape
         if self.is_aux:
             # l_aux = E * sum_e coef_e * sum_t probs[t, e] / T
@@ -401,8 +413,8 @@ class TopKGatingGradOp(Op):
                 c = binary('mul', unary('mul_c', coef, float(E) / float(T)), gs)
             else:
                 c = coef * (float(E) / float(T)) * g.float().reshape(-1)[0]
-            return KM.gate_backward(probs, idx, None, c)
-        return KM.gate_backward(probs, idx, g, None)
+            return KM.gate_backward(probs, idx, None, c, scale)
+        return KM.gate_backward(probs, idx, g, None, scale)
 
     def gradient(self, output_grad):
         raise NotImplementedError

@@ -69,3 +69,41 @@ def test_bert_step_launches_no_torch_kernels():
     assert n > 100, n
     assert not torch_k, dict(torch_k)
     assert not K.VENDOR_CALLS and not K.FALLBACKS, (K.VENDOR_CALLS, K.FALLBACKS)
+
+
+def _bench_step(model, **kw):
+    import argparse
+    a = dict(batch=None, dtype='bf16', bucket_mb=32, zero=0, pp=None, moe_gate='topk', model=model)
+    a.update(kw)
+    args = argparse.Namespace(**a)
+    if model == 'moe':
+        from hetu_61a7_amd.models.moe import moe_top_bench
+        return moe_top_bench(args, 1, 0, 0)[0]
+    from hetu_61a7_amd.models.bert import bert_bench
+    return bert_bench(args, 1, 0, 0)[0]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('gate', ['topk', 'dts'])
+def test_moe_bench_step_launches_no_torch_kernels(gate):
+    """BASELINE config 5 at the bench shape (reference run_top2.sh: batch 64 x 1024 tokens,
+    d 2048, 2 experts): top-2 and the dense-to-sparse gate"""
+    step = _bench_step('moe', moe_gate=gate)
+    from hetu_61a7_amd import kernels as K
+    K.reset_dispatch_stats()
+    n, torch_k = _census(step)
+    assert n > 20, n
+    assert not torch_k, dict(torch_k)
+    assert not K.VENDOR_CALLS and not K.FALLBACKS, (K.VENDOR_CALLS, K.FALLBACKS)
+
+
+@pytest.mark.timeout(900)
+def test_bert_base_bench_step_launches_no_torch_kernels():
+    """BERT-base at the bench shape (batch 64 x seq 128, 12 layers)"""
+    step = _bench_step('bert', batch=64)
+    from hetu_61a7_amd import kernels as K
+    K.reset_dispatch_stats()
+    n, torch_k = _census(step, warm=2)
+    assert n > 300, n
+    assert not torch_k, dict(torch_k)
+    assert not K.VENDOR_CALLS and not K.FALLBACKS, (K.VENDOR_CALLS, K.FALLBACKS)

@@ -49,6 +49,9 @@ def parse():
                    help='DP gradient all-reduce wire format (bf16: fp32 accumulation)')
     p.add_argument('--comm-trace', action='store_true',
                    help='report the last step\'s all-reduce bucket timeline in the JSON config')
+    p.add_argument('--rehearse-cpu', action='store_true',
+                   help='run the model on the CPU (fp32, gloo between ranks): a dry run of the multi-GPU '
+                        'launch that prints the same JSON line (tests/test_rehearse8_cpu.py)')
     return p.parse_args()
 
 
@@ -131,7 +134,9 @@ def main():
     assert world == args.gpus or world == 1, 'launch with --nproc-per-node == --gpus'
     if os.environ.get('HETU_DIST_BACKEND') == 'gloo':
         local = local % torch.cuda.device_count()     # multi-rank rehearsal on one GPU
-    cpu_only = args.model == 'logreg'
+    cpu_only = args.model == 'logreg' or args.rehearse_cpu
+    if args.rehearse_cpu:
+        args.dtype = 'fp32'
     if not cpu_only:
         torch.cuda.set_device(local)
     dev = torch.device('cpu') if cpu_only else torch.device('cuda', local)
@@ -145,17 +150,18 @@ def main():
         loss, logits = resnet50_imagenet(x, y_, 1000)
         opt = ht.optim.MomentumOptimizer(learning_rate=0.1 / max(world, 1), momentum=0.9)
         train_op = opt.minimize(loss)
-        kw = dict(mixed_precision=args.dtype, bucket_mb=args.bucket_mb, seed=1234, zero=args.zero,
-                  timing='gpu' if args.op_profile else None)
+        kw = dict(mixed_precision=None if cpu_only else args.dtype, bucket_mb=args.bucket_mb, seed=1234,
+                  zero=args.zero, timing='gpu' if args.op_profile else None)
         if world > 1:
             ex = ht.Executor({'train': [loss, train_op]}, dist_strategy=ht.dist.DataParallel('allreduce'), **kw)
         else:
-            ex = ht.Executor({'train': [loss, train_op]}, ctx=ht.gpu(local), **kw)
+            ex = ht.Executor({'train': [loss, train_op]}, ctx=ht.cpu(0) if cpu_only else ht.gpu(local), **kw)
         g = torch.Generator(device=dev)
         g.manual_seed(1000 + rank)
         dt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
         X = torch.randn((B, 3, 224, 224), generator=g, device=dev).to(dt)
-        X = X.contiguous(memory_format=torch.channels_last)
+        if not cpu_only:
+            X = X.contiguous(memory_format=torch.channels_last)
         lab = torch.randint(0, 1000, (B,), generator=g, device=dev)
         Y = torch.nn.functional.one_hot(lab, 1000).to(dt)
         feed = {x: X, y_: Y}
@@ -239,7 +245,7 @@ def main():
             cfg['comm_trace_last_step'] = tr[0] if tr else []
     if rank == 0:
         out = {'metric': metric, 'value': round(value, 2), 'unit': 'tokens/s' if args.model == 'moe' else 'samples/s',
-               'n_gpus': 0 if cpu_only else world,
+               'n_gpus': 0 if args.model == 'logreg' else world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
                'dtype': 'fp32' if cpu_only else args.dtype, 'data': 'synthetic (random-init weights)', 'config': cfg}

@@ -26,12 +26,62 @@ inline float at(const float* X, int64_t r, int64_t c, int64_t ld, int trans) {
   return trans ? X[c * ld + r] : X[r * ld + c];
 }
 
+// Skinny products (logistic regression 784 -> 10 and its weight gradient): B packed once
+// into zero-padded rows of NP = 16 / 32 floats, 16-row blocks of C accumulated over the
+// whole K in a stack tile with a fixed-width inner loop (one or two AVX-512 FMAs per (row, k);
+// cloned for AVX-512 / AVX2 / baseline at load time), rows split over the threads from ~1M MACs.
+template <int NP>
+__attribute__((target_clones("avx512f", "avx2", "default")))
+static void skinny_rows(const float* A, const float* bp, float* C, const float* bias, int64_t i0, int64_t i1,
+                        int64_t N, int64_t K, int64_t lda, int64_t ldc, int transA, float alpha, float beta) {
+  float acc[16][NP];
+  for (int64_t i = 0; i < 16; ++i)
+    for (int j = 0; j < NP; ++j) acc[i][j] = 0.f;
+  const int64_t nr = i1 - i0;
+  for (int64_t k = 0; k < K; ++k) {
+    const float* __restrict__ b = bp + k * NP;
+    for (int64_t r = 0; r < nr; ++r) {
+      const float av = transA ? A[k * lda + i0 + r] : A[(i0 + r) * lda + k];
+#pragma omp simd
+      for (int j = 0; j < NP; ++j) acc[r][j] += av * b[j];
+    }
+  }
+  for (int64_t r = 0; r < nr; ++r) {
+    float* c = C + (i0 + r) * ldc;
+    for (int64_t j = 0; j < N; ++j) {
+      float v = alpha * acc[r][j] + (beta == 0.f ? 0.f : beta * c[j]);
+      if (bias != nullptr) v += bias[j];
+      c[j] = v;
+    }
+  }
+}
+
+static void skinny_gemm(const float* A, const float* B, float* C, const float* bias, int64_t M, int64_t N,
+                        int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int transA, float alpha, float beta) {
+  const int NP = N <= 16 ? 16 : 32;
+  std::vector<float> bp((size_t)K * NP, 0.f);
+  for (int64_t k = 0; k < K; ++k) memcpy(bp.data() + k * NP, B + k * ldb, N * sizeof(float));
+  const int64_t nblk = (M + 15) / 16;
+#pragma omp parallel for schedule(static) if (M * N * K >= (1 << 20))
+  for (int64_t blk = 0; blk < nblk; ++blk) {
+    const int64_t i0 = blk * 16, i1 = std::min(M, i0 + 16);
+    if (NP == 16)
+      skinny_rows<16>(A, bp.data(), C, bias, i0, i1, N, K, lda, ldc, transA, alpha, beta);
+    else
+      skinny_rows<32>(A, bp.data(), C, bias, i0, i1, N, K, lda, ldc, transA, alpha, beta);
+  }
+}
+
 }  // namespace
 
 // C[M,N] = alpha * op(A)[M,K] @ op(B)[K,N] + beta * C (+ bias[N])
 API void hetu_cpu_gemm(const float* A, const float* B, float* C, const float* bias, int64_t M, int64_t N,
                        int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int transA, int transB, float alpha,
                        float beta) {
+  if (N <= 32 && !transB) {
+    skinny_gemm(A, B, C, bias, M, N, K, lda, ldb, ldc, transA, alpha, beta);
+    return;
+  }
   const int64_t mblocks = (M + MB - 1) / MB, nblocks = (N + NB - 1) / NB;
 #pragma omp parallel if(M * N * K >= (1 << 21))
   {

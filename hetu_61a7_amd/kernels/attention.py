@@ -11,14 +11,14 @@ semantics (the CPU backend and the numerics oracle).
 """
 from __future__ import annotations
 
+import ctypes
 import math
-import weakref
-
 import os
+import weakref
 
 import torch
 
-from . import fn, native, stream_ptr, check, P, I64, I32, F32
+from . import fn, native, stream_ptr, check, record_native, P, I64, I32, F32
 
 
 
@@ -38,6 +38,11 @@ def _bwd_call(*args, device=None):
 def fused_ok(qkv, S, D, need_bwd=True):
     return (native(qkv) and qkv.dtype == torch.bfloat16 and D == 64 and S % 32 == 0 and 0 < S <= (128 if need_bwd else 256)
             and qkv.is_contiguous())
+
+
+def _key_mask(mask, B, S):
+    """additive key mask [B, S] -> [B, 1, 1, S] (broadcast over heads and queries)"""
+    return None if mask is None else mask.reshape(B, 1, 1, S)
 
 
 def _heads(qkv, B, S, NH, D):
@@ -110,6 +115,15 @@ def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
                 out.data_ptr(), H, lse.data_ptr(), B, NH, S, float(scale), float(keep), int(seed), stream_ptr()),
               'attn_fwd')
         return out, lse
+    q, k, v = packed_heads(qkv, B, S, NH)
+    if flash_ok(q, k, v):
+        # any other length / head dim: the general flash kernels, on the packed views
+        out = torch.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
+        _, lse = flash_fwd(q, k, v, _key_mask(mask, B, S), False, keep, seed, scale,
+                           out=out.view(B, S, NH, D).permute(0, 2, 1, 3))
+        return out, lse
+    if qkv.is_cuda:
+        raise RuntimeError('attention: no hand-written kernel for %s S=%d D=%d' % (qkv.dtype, S, D))
     p, v = _ref_probs(qkv, mask, B, S, NH, D, scale)
     pd = p * _ref_dropmask(p.shape, keep, seed, p.device) if keep < 1.0 else p
     o = (pd @ v).transpose(1, 2).reshape(B * S, H)
@@ -133,6 +147,18 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
                   out.data_ptr(), H, saved.data_ptr(), dout.data_ptr(), H, g, g + H * es, g + 2 * H * es,
                   3 * H, 3 * H, 3 * H, B, NH, S, float(scale), float(keep), int(seed), device=qkv.device)
         return dqkv
+    if saved.dim() == 1 and qkv.is_cuda:
+        # the flash backward (its lse and dropout bits are the fused forward's: same
+        # log-sum-exp of the scaled, masked scores; Philox(seed, row * S/4 + key/4))
+        q, k, v = packed_heads(qkv, B, S, NH)
+        if flash_ok(q, k, v):
+            dqkv = torch.empty_like(qkv)
+            gq, gk, gv = packed_heads(dqkv, B, S, NH)
+            o4 = out.view(B, S, NH, D).permute(0, 2, 1, 3)
+            g4 = dout.reshape(B, S, NH, D).permute(0, 2, 1, 3)
+            flash_bwd(g4, q, k, v, o4, saved, _key_mask(mask, B, S), False, keep, seed, scale, grads=(gq, gk, gv))
+            return dqkv
+        raise RuntimeError('attention backward: no hand-written kernel for S=%d D=%d' % (S, D))
     if saved.dim() == 1:    # fused forward (S <= 256) but no fused backward: recompute probs
         saved, _ = _ref_probs(qkv, mask, B, S, NH, D, scale)
     p = saved
@@ -193,3 +219,87 @@ def attention_bwd_blocks(dout, q, k, v, out, lse, mask, B, S, NH, scale):
               dout.data_ptr(), H, dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), H, H, H, B, NH, S,
               float(scale), 1.0, 0, device=q.device)
     return dq, dk, dv
+
+
+# ---------------------------------------------------------------------------
+# General fused attention (``flash_attn.hip``): any Sq / Sk, head dim 32 / 64 / 128,
+# causal, an additive mask broadcastable to [B, NH, Sq, Sk], dropout; Q / K / V / O
+# as strided [B, NH, S, D] views (head dim contiguous), so packed projections and
+# transposed head views are read and written in place.
+
+FLASH_D = (32, 64, 128)
+
+
+def _st3(t):
+    """(batch, head, row) strides of a [B, NH, S, D] view"""
+    return (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(2))
+
+
+def flash_ok(q, k, v):
+    D = q.shape[-1]
+    return (all(native(t) and t.dtype == torch.bfloat16 and t.dim() == 4 and t.stride(-1) == 1
+                and t.data_ptr() % 16 == 0 and all(s % 8 == 0 for s in t.stride()[:3]) for t in (q, k, v))
+            and D in FLASH_D and k.shape[-1] == D and v.shape[-1] == D and k.shape[2] == v.shape[2])
+
+
+def _flash_mask(mask, B, NH, Sq, Sk):
+    """(fp32 mask, its [b, h, q, k] strides) -- 0 strides on broadcast dims"""
+    if mask is None:
+        return None, None
+    m = mask
+    if m.dtype != torch.float32 or not m.is_contiguous():
+        m = _mask_f32(m) if m.dim() == 2 else _f32(m)
+    me = m.expand(B, NH, Sq, Sk) if m.dim() <= 4 else None
+    if me is None:
+        raise ValueError('attention mask of shape %s does not broadcast to [B, NH, Sq, Sk]' % (tuple(mask.shape),))
+    return m, (ctypes.c_int64 * 4)(*me.stride())
+
+
+def flash_fwd(q, k, v, mask=None, causal=False, keep=1.0, seed=0, scale=None, out=None):
+    """-> (o [B, NH, Sq, D] (a view of a [B, Sq, NH, D] buffer, or ``out``), lse [B*NH*Sq] fp32)"""
+    B, NH, Sq, D = q.shape
+    Sk = k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if out is None:
+        out = torch.empty((B, Sq, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3)
+    lse = torch.empty((B * NH * Sq,), dtype=torch.float32, device=q.device)
+    m, mst = _flash_mask(mask, B, NH, Sq, Sk)
+    f = fn('hetu_flash_fwd', [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, F32, I64, P])
+    check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), _st3(q), _st3(k), _st3(v), out.data_ptr(), _st3(out),
+            lse.data_ptr(), m.data_ptr() if m is not None else None, mst, B, NH, Sq, Sk, D, int(bool(causal)),
+            float(scale), float(keep), int(seed), stream_ptr()), 'flash_fwd')
+    record_native('flash_fwd')
+    return out, lse
+
+
+def flash_bwd(dout, q, k, v, o, lse, mask=None, causal=False, keep=1.0, seed=0, scale=None, grads=None):
+    """-> (dq, dk, dv) shaped like q, k, v ([B, S, NH, D] buffers seen as [B, NH, S, D]),
+    or written into ``grads`` (three such views)"""
+    B, NH, Sq, D = q.shape
+    Sk = k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if dout.dtype != q.dtype or dout.stride(-1) != 1 or dout.data_ptr() % 16 or any(s % 8 for s in dout.stride()[:3]):
+        from .tensor import copy_into
+        dout = copy_into(torch.empty((B, Sq, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3), dout)
+    if grads is None:
+        mk = lambda S: torch.empty((B, S, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3)
+        grads = (mk(Sq), mk(Sk), mk(Sk))
+    dq, dk, dv = grads
+    dsum = torch.empty((B * NH * Sq,), dtype=torch.float32, device=q.device)
+    m, mst = _flash_mask(mask, B, NH, Sq, Sk)
+    f = fn('hetu_flash_bwd', [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P,
+                              I32, I32, I32, I32, I32, I32, F32, F32, I64, P])
+    check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), _st3(q), _st3(k), _st3(v), o.data_ptr(), _st3(o),
+            lse.data_ptr(), dout.data_ptr(), _st3(dout), dq.data_ptr(), _st3(dq), dk.data_ptr(), _st3(dk),
+            dv.data_ptr(), _st3(dv), m.data_ptr() if m is not None else None, mst, dsum.data_ptr(),
+            B, NH, Sq, Sk, D, int(bool(causal)), float(scale), float(keep), int(seed), stream_ptr()), 'flash_bwd')
+    record_native('flash_bwd')
+    return dq, dk, dv
+
+
+def packed_heads(qkv, B, S, NH):
+    """[B*S, 3H] packed projection -> q, k, v as [B, NH, S, D] views (no copies)"""
+    H = qkv.shape[1] // 3
+    D = H // NH
+    x = qkv.view(B, S, 3, NH, D)
+    return x[:, :, 0].permute(0, 2, 1, 3), x[:, :, 1].permute(0, 2, 1, 3), x[:, :, 2].permute(0, 2, 1, 3)

@@ -134,6 +134,12 @@ def gate_backward(probs, idx, dgate, aux_coef, scale=1.0):
 def _philox_x(seed, counter):
     """first 32-bit output of Philox4x32-10 (common.h Philox::gen(...).x) for uint64 arrays of
     counters -- the CPU reference path draws the same Gumbel noise as the HIP kernel"""
+    return philox4(seed, counter)[0]
+
+
+def philox4(seed, counter):
+    """the four 32-bit outputs (x, y, z, w) of Philox4x32-10 (common.h Philox::gen) for a
+    uint64 array of counters: host references of the kernels' random streams"""
     import numpy as np
     M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
     m32 = np.uint64(0xFFFFFFFF)
@@ -152,7 +158,7 @@ def _philox_x(seed, counter):
         c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & m32, lo1, (hi0 ^ c3 ^ k1) & m32, lo0
         k0 = (k0 + np.uint64(0x9E3779B9)) & m32
         k1 = (k1 + np.uint64(0xBB67AE85)) & m32
-    return c0
+    return c0, c1, c2, c3
 
 
 def dts_gate(logits, k, inv_tau, threshold, seed, noise=True):

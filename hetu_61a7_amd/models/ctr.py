@@ -184,27 +184,45 @@ def wdl_criteo_bench(args, world, rank, local):
     # id distribution: Zipf a=1.05 per field (the skew real CTR data has), or a uniform
     # control run (``--ids uniform``: every lookup is a cold row -- the cache's worst case)
     dist = getattr(args, 'ids', 'zipf')
-    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + rank, zipf=1.05 if dist == 'zipf' else 0)
+    # rehearsal knobs (tests/test_rehearse8_cpu.py): CPU context, BSP, every worker on the
+    # same batches, no cache, another lr / embedding width
+    cpu = bool(getattr(args, 'rehearse_cpu', False))
+    same = bool(getattr(args, 'same_data', False))
+    emb = int(getattr(args, 'emb', 0) or 128)
+    lr = float(getattr(args, 'lr', 0) or 0.01)
+    bsp = int(getattr(args, 'bsp', -1))
+    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + (0 if same else rank),
+                                             zipf=1.05 if dist == 'zipf' else 0)
+    if same and world > 1:
+        # the dataloader shards its data over the workers (contiguous 1/world slices): tile
+        # the block so that every worker's shard -- and so every batch -- is the same
+        import numpy as np
+        dense, sparse, labels = (np.concatenate([a] * world, 0) for a in (dense, sparse, labels))
     # dataloader-fed inputs, as the reference's run_hetu.py: the executor knows the
     # next batch's sparse ids and prefetches their rows with this step's push
     xd = ht.dataloader_op([ht.Dataloader(dense, B, 'train')])
     xs = ht.dataloader_op([ht.Dataloader(sparse, B, 'train')])
     y_ = ht.dataloader_op([ht.Dataloader(labels, B, 'train')])
-    loss, y, _, train = wdl_criteo(xd, xs, y_, feature_dimension=rows, embedding_size=128, learning_rate=0.01)
+    loss, y, _, train = wdl_criteo(xd, xs, y_, feature_dimension=rows, embedding_size=emb, learning_rate=lr)
     # comm mode: 'PS' (BASELINE config 3, reference examples/ctr/tests/ps_wdl_criteo.sh: the
     # dense MLP parameters live on the server too, pushed and pulled every step) or
     # 'Hybrid' (dense parameters all-reduced on the GPUs, embeddings on the PS)
     comm = getattr(args, 'comm', None) or 'PS'
-    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(local), comm_mode=comm,
-                     cstable_policy=getattr(args, 'cache', 'LFUOpt'), cache_bound=3, bsp=-1,
-                     mixed_precision=args.dtype, seed=1234, prefetch=getattr(args, 'prefetch', True))
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.cpu(0) if cpu else ht.gpu(local), comm_mode=comm,
+                     cstable_policy=getattr(args, 'cache', 'LFUOpt'), cache_bound=3, bsp=bsp,
+                     mixed_precision=None if cpu else args.dtype, seed=1234,
+                     prefetch=getattr(args, 'prefetch', True) and bsp < 0)
     from ..ps import table as _pst
     clock = {'wall': [], 'wait': []}
+
+    losses = []
 
     def step():
         import time
         t0, w0 = time.perf_counter(), _pst.WAIT_S[0]
-        ex.run('train')
+        r = ex.run('train')
+        if cpu:
+            losses.append(float(r[0].asnumpy().reshape(-1)[0]) if hasattr(r[0], 'asnumpy') else float(r[0]))
         clock['wall'].append(time.perf_counter() - t0)
         clock['wait'].append(_pst.WAIT_S[0] - w0)
 
@@ -232,6 +250,8 @@ def wdl_criteo_bench(args, world, rank, local):
                                       'ps_wait': round(wait * 1e3 / k, 3),
                                       'host_other': round((wall - wait) * 1e3 / k, 3)}}
     step.extra = extra
+    step.losses = losses
+    step.executor = ex
 
     def finish():
         from ..ps import worker

@@ -51,6 +51,19 @@ class AttentionOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         q, k, v = input_vals[:3]
         mask = input_vals[3] if self.has_mask else None
+        from ..kernels import attention as KA
+        if q.is_cuda and KA.flash_ok(q, k, v):
+            # one fused kernel: scores, mask, causal mask, online softmax, dropout, P.V
+            keep = 1.0 if self.inference else self.keep_prob
+            seed = 0
+            if keep < 1.0:
+                self.seed += 1
+                seed = (self.id << 32) + self.seed
+            o, lse = KA.flash_fwd(q, k, v, mask, self.causal, keep, seed, self._scale(q.shape[-1]))
+            return AuxResult(o, ('flash', lse, keep, seed))
+        if q.is_cuda:
+            raise RuntimeError('attention_op: no hand-written kernel for %s %s (head dim 32/64/128, bf16)'
+                               % (q.dtype, tuple(q.shape)))
         s = _scores(q, k, mask, self._scale(q.shape[-1]), self.causal)
         p = KS.softmax(s.to(q.dtype) if q.dtype == torch.bfloat16 else s)
         seed = None
@@ -78,12 +91,19 @@ class AttentionGradientOp(Op):
     value_and_aux_inputs = (1,)
 
     def __init__(self, dout, fwd, ctx=None):
-        super().__init__(AttentionGradientOp, [dout, fwd] + fwd.inputs[:3], ctx)
+        # the mask (if any) rides along: the flash backward recomputes P from it
+        super().__init__(AttentionGradientOp, [dout, fwd] + fwd.inputs[:3] + fwd.inputs[3:4], ctx)
         self.fwd = fwd
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        do, (o, (p, seed)), q, k, v = input_vals
+        do, (o, aux), q, k, v = input_vals[:5]
         f = self.fwd
+        if aux[0] == 'flash':
+            from ..kernels import attention as KA
+            _, lse, keep, seed = aux
+            mask = input_vals[5] if f.has_mask else None
+            return KA.flash_bwd(do, q, k, v, o, lse, mask, f.causal, keep, seed, f._scale(q.shape[-1]))
+        p, seed = aux
         dt = q.dtype
         pd = p if seed is None else KD.dropout(p, f.keep_prob, seed)
         dv = KG.bmm(pd.to(dt), do.to(dt), True, False)

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T="python3 -u -m pytest -x -q -p no:cacheprovider --timeout 900 --timeout-method thread"
 echo "== new tests"
-timeout -k 10 900 $T tests/test_bn_fusion_gpu.py::test_hipgraph_replays_fused_bn_backward_like_eager \
+timeout -k 10 900 $T tests/test_flash_attn_gpu.py tests/test_bn_fusion_gpu.py::test_hipgraph_replays_fused_bn_backward_like_eager \
     tests/test_native_dispatch_gpu.py > gpurun_out/r5a_new.log 2>&1
 rc=$?; tail -15 gpurun_out/r5a_new.log; [ $rc -eq 0 ] || exit $rc
 echo "== moe benches"

@@ -280,7 +280,7 @@ def _resnet_losses(use_hipgraph, steps=6):
                          use_hipgraph=use_hipgraph)
         g = torch.Generator(device='cuda')
         g.manual_seed(0)
-        X = torch.randn((B, 3, 112, 112), device='cuda', generator=g).bfloat16().contiguous(memory_format=CL)
+        X = torch.randn((B, 3, 224, 224), device="cuda", generator=g).bfloat16().contiguous(memory_format=CL)
         Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
         out = []
         for _ in range(steps):

@@ -13,6 +13,7 @@ parallel layout against the single-process losses, validate_results.py:11-18):
 Every rank runs one thread; shapes are tiny."""
 import os
 import socket
+import zlib
 
 import numpy as np
 import pytest
@@ -172,3 +173,155 @@ def test_moe_expert_parallel_eight_ranks():
     for _, _, g in res[1:]:                                          # the data-parallel gate agrees
         for k in g:
             np.testing.assert_allclose(g[k], res[0][2][k], rtol=1e-6, atol=1e-7)
+
+
+# ---- Wide&Deep PS: 1 server + 8 workers (reference examples/ctr/tests/ps_wdl_criteo.sh:6) ----
+def _ps_server(env):
+    os.environ.update(env)
+    from hetu_61a7_amd.ps import server
+    server.server_init()
+    server.server_finish(timeout_s=300)
+
+
+def _wdl_worker(rank, world, port, q, env, lr):
+    _env(rank, world, port)
+    os.environ.update(env)
+    os.environ.update(DMLC_ROLE='worker')
+    import types
+    from hetu_61a7_amd.models.ctr import wdl_criteo_bench
+    # bench.py --model wdl (BASELINE config 3: --comm PS, dense parameters on the server too)
+    # in BSP mode with every worker on the same batches, no cache: 8 summed pushes of the
+    # same gradient == one worker at 8 x the lr
+    args = types.SimpleNamespace(batch=16, criteo_rows=3000, emb=8, lr=lr, bsp=0, cache=None, same_data=True,
+                                 rehearse_cpu=True, comm='PS', dtype='fp32', ids='zipf', steps=4, prefetch=False)
+    step, samples, cfg, metric, finish = wdl_criteo_bench(args, world, rank, rank)
+    for _ in range(4):
+        step()
+    q.put((rank, list(step.losses), cfg, samples))
+    finish()
+
+
+def _run_wdl(world, lr):
+    import uuid
+    env = dict(DMLC_PS_ROOT_PORT=str(20000 + uuid.uuid4().int % 30000), DMLC_NUM_WORKER=str(world),
+               DMLC_NUM_SERVER='1', HETU_PS_HEAP_GB='0.2')
+    ctx = mp.get_context('spawn')
+    srv = ctx.Process(target=_ps_server, args=(env,))
+    srv.start()
+    try:
+        return _run(_wdl_worker, world, env, lr)
+    finally:
+        srv.join(120)
+        assert srv.exitcode == 0
+
+
+def test_wdl_ps_eight_workers_bsp_matches_one_worker():
+    ref = _run_wdl(1, 0.08)[0]
+    res = _run_wdl(WORLD, 0.01)
+    assert res[0][2]['comm_mode'] == 'PS' and '8 worker' in res[0][2]['parallelism']
+    assert res[0][3] == 16 * WORLD
+    for rank, losses, _, _ in res:
+        assert len(losses) == 4
+        np.testing.assert_allclose(losses, ref[1], rtol=2e-4, atol=1e-6, err_msg='worker %d' % rank)
+    assert ref[1][-1] != ref[1][0]               # the updates moved the loss
+
+
+# ---- MoE EP8 equivalence: 8 ranks x 2 experts == one process holding all 16 experts -------
+def _moe_params(names, d, hidden, E):
+    """deterministic values by parameter name (init seeds follow node ids, which differ
+    between the two graphs)"""
+    out = {}
+    for n in names:
+        rng = np.random.RandomState(zlib.crc32(n.encode()))
+        if n.endswith('_weight_1'):
+            out[n] = (rng.randn(d, hidden) * 0.3).astype(np.float32)
+        elif n.endswith('_weight_2'):
+            out[n] = (rng.randn(hidden, d) * 0.3).astype(np.float32)
+        elif n.endswith('linear_weight'):
+            out[n] = (rng.randn(d, E) * 0.5).astype(np.float32)
+        elif n.endswith('linear_bias'):
+            out[n] = (rng.randn(E) * 0.1).astype(np.float32)
+    return out
+
+
+def _moe_eq_worker(rank, world, port, q, n_exp_total, T_local):
+    _env(rank, world, port)
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.layers.moe import TopKGate, Expert, MoELayer
+    from hetu_61a7_amd.utils.checkpoint import load_dict
+    d, hidden = 8, 16
+    E = n_exp_total
+    n_local = E // world
+    # rank r's tokens are rows [r * T_local, (r + 1) * T_local) of one global batch
+    Xall = np.random.RandomState(5).randn(8 * T_local, d).astype(np.float32)
+    T = T_local * (8 // world)
+    X = Xall[rank * T:(rank + 1) * T]
+    x = ht.Variable(name='x')
+    experts = [Expert(d, hidden, activation='relu', name='expert_%d' % (rank * n_local + i)) for i in range(n_local)]
+    y, l_aux = MoELayer(TopKGate(d, T, E, k=2, capacity_factor=float(E)), experts, T, d, all2all_size=world)(x)
+    loss = ht.reduce_mean_op(ht.mul_op(y, y), [0, 1])          # no balance loss: it is per-rank nonlinear
+    # EP: the gate's gradient is SUM-all-reduced over the ranks and each expert collects the
+    # gradients of every rank's tokens: world x the single process's mean-loss gradient
+    train = ht.optim.SGDOptimizer(0.05 if world > 1 else 0.05 * 8).minimize(loss)
+    kw = dict(comm_mode='AllReduce') if world > 1 else dict(ctx=ht.cpu(0))
+    ex = ht.Executor({'train': [loss, y, train]}, **kw)
+    names = [n.name for n in ex.config.placeholder_to_arr_map if getattr(n, 'trainable', False)]
+    load_dict(ex, _moe_params(names, d, hidden, E))
+    losses, ys = [], []
+    for _ in range(3):
+        r = ex.run('train', feed_dict={x: X}, convert_to_numpy_ret_vals=True)
+        losses.append(float(np.asarray(r[0]).reshape(-1)[0]))
+        ys.append(np.asarray(r[1]).reshape(T, d).copy())
+    params = {n.name: v.detach().numpy().copy() for n, v in ex.config.placeholder_to_arr_map.items()
+              if getattr(n, 'trainable', False)}
+    if world > 1:
+        from hetu_61a7_amd.parallel import comm
+        comm.destroy()
+    q.put((rank, losses, ys, params))
+
+
+def test_moe_ep8_matches_one_process_with_all_experts():
+    """the EP8 rehearsal as an equivalence test.  8 ranks x 2 experts
+    over all-to-all against one process with all 16 experts on the same 8 x 8 tokens: the
+    expert outputs of every rank's tokens, the mean loss and every parameter after 3 SGD
+    steps agree."""
+    ref = _run(_moe_eq_worker, 1, 16, 8)[0]
+    res = _run(_moe_eq_worker, WORLD, 16, 8)
+    T = 8
+    for step in range(3):
+        mean_loss = np.mean([r[1][step] for r in res])          # equal token counts per rank
+        assert mean_loss == pytest.approx(ref[1][step], rel=1e-4, abs=1e-6), step
+        y_ep = np.concatenate([r[2][step] for r in res], 0)
+        np.testing.assert_allclose(y_ep, ref[2][step], rtol=1e-4, atol=1e-5, err_msg='step %d' % step)
+    for rank, _, _, params in res:
+        for k, v in params.items():
+            np.testing.assert_allclose(v, ref[3][k], rtol=1e-4, atol=1e-6, err_msg='%s rank %d' % (k, rank))
+
+
+def test_bench_torchrun_eight_ranks_prints_driver_json():
+    """A dry run of the driver's scaling launch (python -m torch.distributed.run
+    --nproc-per-node 8 ... bench.py --gpus 8) on the CPU with gloo: rank 0 prints ONE JSON
+    line with the keys the driver parses, the whole-job value and the comm record."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS='1', HETU_USE_CONFIG='0')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(WORLD),
+           '--master-addr', '127.0.0.1', '--master-port', str(_port()), os.path.join(root, 'bench.py'),
+           '--gpus', str(WORLD), '--steps', '1', '--warmup', '1', '--batch', '1', '--rehearse-cpu']
+    out = subprocess.run(cmd, env=env, cwd='/tmp', capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, out.stdout[-2000:]
+    j = json.loads(lines[0])
+    for k in ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step', 'higher_is_better', 'scaling',
+              'vs_baseline', 'dtype', 'data', 'config'):
+        assert k in j, k
+    assert j['n_gpus'] == WORLD and j['steps'] == 1 and j['warmup'] == 1 and j['scaling'] == 'weak'
+    c = j['config']
+    for k in ('model', 'global_batch', 'seq_len', 'parallelism', 'comm', 'comm_stats', 'vendor_calls', 'fallbacks',
+              'comm_trace_last_step'):
+        assert k in c, k
+    assert c['global_batch'] == WORLD and c['parallelism'] == 'dp%d' % WORLD and c['comm_stats']['world'] == WORLD
+    assert abs(j['value'] - WORLD * 1000.0 / j['ms_per_step']) < 0.05 * j['value']

@@ -34,7 +34,10 @@ typedef short v4s __attribute__((ext_vector_type(4)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int HD = 64;
-constexpr int PAD = 8;   // shorts of padding per LDS row (16 B) against bank conflicts
+// shorts of padding per LDS row of the transposed images (16 B: rows stay 16-byte aligned
+// for the ds_read_b128 fragment reads; with the paired-key stores of stage_t a wave's
+// 64 stores of one column land on 64 distinct banks)
+constexpr int PAD = 8;
 
 struct Args {
   const bf16* q;
@@ -99,15 +102,23 @@ __device__ __forceinline__ void drop_mul4(uint64_t seed, uint64_t flat, float ke
   for (int k = 0; k < 4; ++k) m[k] = Philox::u01(rr[k]) < keep ? inv : 0.f;
 }
 
-// stage X^T (X rows [S][64] with row stride ld) into LDS T[64][S + PAD]
+// stage X^T (X rows [S][64] with row stride ld) into LDS T[64][S + PAD]: each thread
+// loads two consecutive rows x 8 columns and writes 8 dwords (the two rows' values of one
+// column), consecutive lanes on consecutive row pairs -- 4-byte stores on 64 distinct
+// banks per wave instead of 2-byte stores 8 rows apart
 template <int S>
 __device__ __forceinline__ void stage_t(const bf16* X, int64_t ld, short* T) {
   constexpr int LT = S + PAD;
-  for (int idx = threadIdx.x; idx < S * 8; idx += 256) {
-    const int key = idx >> 3, c = idx & 7;
-    const v8s x = ld8(X + (int64_t)key * ld + 8 * c);
+  constexpr int RP = S / 2;
+  for (int idx = threadIdx.x; idx < RP * 8; idx += 256) {
+    const int rp = idx % RP, c = idx / RP;
+    const v8s x0 = ld8(X + (int64_t)(2 * rp) * ld + 8 * c);
+    const v8s x1 = ld8(X + (int64_t)(2 * rp + 1) * ld + 8 * c);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) T[(8 * c + i) * LT + key] = x[i];
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t pr = (uint32_t)(unsigned short)x0[i] | ((uint32_t)(unsigned short)x1[i] << 16);
+      *reinterpret_cast<uint32_t*>(T + (8 * c + i) * LT + 2 * rp) = pr;
+    }
   }
 }
 

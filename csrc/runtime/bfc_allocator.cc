@@ -555,6 +555,10 @@ static BFCAllocator* dev_alloc(int device) {
   return g_dev[device];
 }
 
+// the device pool itself (framework arrays, csrc/runtime/array.cc, allocate from the same
+// BFC pool as torch's pluggable-allocator hook)
+HETU_RT_API void* hetu_bfc_device_pool(int device) { return dev_alloc(device); }
+
 // Private pools for hipGraph capture (the native counterpart of torch's graph memory
 // pools): between hetu_torch_pool_begin and _end every allocation on the device that is
 // made on the capture stream, or on any stream that is capturing at that moment (side

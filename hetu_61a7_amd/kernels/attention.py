@@ -17,6 +17,7 @@ import os
 import weakref
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, check, record_native, P, I64, I32, F32
 
@@ -30,7 +31,7 @@ _BWD_SPLIT = os.environ.get('HETU_ATTN_BWD_SPLIT', '1') == '1'
 def _bwd_call(*args, device=None):
     """hetu_attn_bwd2 (fused, or split with a workspace); args as hetu_attn_bwd's up to seed"""
     B, NH, S = args[18], args[19], args[20]
-    ws = torch.empty(2 * B * NH * S * S, dtype=torch.bfloat16, device=device) if _BWD_SPLIT else None
+    ws = _NA.empty(2 * B * NH * S * S, dtype=torch.bfloat16, device=device) if _BWD_SPLIT else None
     f = fn('hetu_attn_bwd2', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
                               I32, I32, I32, F32, F32, I64, P, P])
     check(f(*args, ws.data_ptr() if ws is not None else None, stream_ptr()), 'attn_bwd')
@@ -96,7 +97,7 @@ def _f32(t):
     if not t.is_cuda:
         return t.float().contiguous()
     from .tensor import copy_into
-    return copy_into(torch.empty(t.shape, dtype=torch.float32, device=t.device), t)
+    return copy_into(_NA.empty(t.shape, dtype=torch.float32, device=t.device), t)
 
 
 def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
@@ -105,8 +106,8 @@ def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
     D = H // NH
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if fused_ok(qkv, S, D, need_bwd=False):
-        out = torch.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
-        lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
+        out = _NA.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
+        lse = _NA.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
         m = _mask_f32(mask)
         f = fn('hetu_attn_fwd', [P, P, P, I64, I64, I64, P, P, I64, P, I32, I32, I32, F32, F32, I64, P])
         base = qkv.data_ptr()
@@ -118,7 +119,7 @@ def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
     q, k, v = packed_heads(qkv, B, S, NH)
     if flash_ok(q, k, v):
         # any other length / head dim: the general flash kernels, on the packed views
-        out = torch.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
+        out = _NA.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
         _, lse = flash_fwd(q, k, v, _key_mask(mask, B, S), False, keep, seed, scale,
                            out=out.view(B, S, NH, D).permute(0, 2, 1, 3))
         return out, lse
@@ -138,8 +139,8 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
     if fused_ok(qkv, S, D) and saved.dim() == 1:
         if dout.dtype != qkv.dtype or not dout.is_contiguous():
             from .tensor import copy_into
-            dout = copy_into(torch.empty(dout.shape, dtype=qkv.dtype, device=dout.device), dout)
-        dqkv = torch.empty_like(qkv)
+            dout = copy_into(_NA.empty(dout.shape, dtype=qkv.dtype, device=dout.device), dout)
+        dqkv = _NA.empty_like(qkv)
         m = _mask_f32(mask)
         es = qkv.element_size()
         b, g = qkv.data_ptr(), dqkv.data_ptr()
@@ -152,7 +153,7 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
         # log-sum-exp of the scaled, masked scores; Philox(seed, row * S/4 + key/4))
         q, k, v = packed_heads(qkv, B, S, NH)
         if flash_ok(q, k, v):
-            dqkv = torch.empty_like(qkv)
+            dqkv = _NA.empty_like(qkv)
             gq, gk, gv = packed_heads(dqkv, B, S, NH)
             o4 = out.view(B, S, NH, D).permute(0, 2, 1, 3)
             g4 = dout.reshape(B, S, NH, D).permute(0, 2, 1, 3)
@@ -191,8 +192,8 @@ def blocks_fused_ok(q, k, v, S, D):
 def attention_fwd_blocks(q, k, v, mask, B, S, NH, scale):
     """-> (out [B*S, H] bf16, lse [B*NH*S] fp32) of softmax(q k^T * scale + mask) v."""
     H = q.shape[1]
-    out = torch.empty((B * S, H), dtype=q.dtype, device=q.device)
-    lse = torch.empty((B * NH * S,), dtype=torch.float32, device=q.device)
+    out = _NA.empty((B * S, H), dtype=q.dtype, device=q.device)
+    lse = _NA.empty((B * NH * S,), dtype=torch.float32, device=q.device)
     m = _mask_f32(mask)
     f = fn('hetu_attn_fwd', [P, P, P, I64, I64, I64, P, P, I64, P, I32, I32, I32, F32, F32, I64, P])
     check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
@@ -210,9 +211,9 @@ def attention_bwd_blocks(dout, q, k, v, out, lse, mask, B, S, NH, scale):
     H = q.shape[1]
     dout = dout.to(q.dtype).contiguous()
     out = out.to(q.dtype).contiguous()
-    dq = torch.empty((B * S, H), dtype=q.dtype, device=q.device)
-    dk = torch.empty_like(dq)
-    dv = torch.empty_like(dq)
+    dq = _NA.empty((B * S, H), dtype=q.dtype, device=q.device)
+    dk = _NA.empty_like(dq)
+    dv = _NA.empty_like(dq)
     m = _mask_f32(mask)
     _bwd_call(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0),
               m.data_ptr() if m is not None else None, out.data_ptr(), H, lse.contiguous().data_ptr(),
@@ -261,8 +262,8 @@ def flash_fwd(q, k, v, mask=None, causal=False, keep=1.0, seed=0, scale=None, ou
     Sk = k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if out is None:
-        out = torch.empty((B, Sq, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3)
-    lse = torch.empty((B * NH * Sq,), dtype=torch.float32, device=q.device)
+        out = _NA.empty((B, Sq, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3)
+    lse = _NA.empty((B * NH * Sq,), dtype=torch.float32, device=q.device)
     m, mst = _flash_mask(mask, B, NH, Sq, Sk)
     f = fn('hetu_flash_fwd', [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, F32, I64, P])
     check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), _st3(q), _st3(k), _st3(v), out.data_ptr(), _st3(out),
@@ -280,12 +281,12 @@ def flash_bwd(dout, q, k, v, o, lse, mask=None, causal=False, keep=1.0, seed=0, 
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if dout.dtype != q.dtype or dout.stride(-1) != 1 or dout.data_ptr() % 16 or any(s % 8 for s in dout.stride()[:3]):
         from .tensor import copy_into
-        dout = copy_into(torch.empty((B, Sq, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3), dout)
+        dout = copy_into(_NA.empty((B, Sq, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3), dout)
     if grads is None:
-        mk = lambda S: torch.empty((B, S, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3)
+        mk = lambda S: _NA.empty((B, S, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3)
         grads = (mk(Sq), mk(Sk), mk(Sk))
     dq, dk, dv = grads
-    dsum = torch.empty((B * NH * Sq,), dtype=torch.float32, device=q.device)
+    dsum = _NA.empty((B * NH * Sq,), dtype=torch.float32, device=q.device)
     m, mst = _flash_mask(mask, B, NH, Sq, Sk)
     f = fn('hetu_flash_bwd', [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P,
                               I32, I32, I32, I32, I32, I32, F32, F32, I64, P])

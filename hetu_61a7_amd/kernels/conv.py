@@ -16,6 +16,7 @@ import os
 
 import torch
 import torch.nn.functional as F
+from .. import native_array as _NA
 
 from . import native, record_vendor
 
@@ -398,7 +399,7 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
 
             def tuned():
                 dst[0] = acc
-        elif _needs_pad(torch.empty(0, x_shape[1], 1, 1, dtype=g.dtype, device=g.device), w) and acc is None:
+        elif _needs_pad(_NA.empty(0, x_shape[1], 1, 1, dtype=g.dtype, device=g.device), w) and acc is None:
             n, ci, h, ww_ = x_shape
             cp = -(-ci // 8) * 8
 
@@ -436,7 +437,7 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
         acc = acc.contiguous(memory_format=CL)
     key = ('dgrad_bn', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None)
     # candidates accumulate into scratch while the shape is being timed
-    tgt = [sums if key in _decisions else torch.zeros_like(sums)]
+    tgt = [sums if key in _decisions else _NA.zeros_like(sums)]
     masked = [False]
 
     def hip(tile=0):
@@ -487,7 +488,7 @@ def _dgrad_s2join(g, w, x_shape, acc, bn):
     key = ('dgrad_s2join', tuple(g.shape), tuple(w.shape), bn is not None)
     tgt = [None]
     if bn is not None:
-        tgt[0] = bn[0] if key in _decisions else torch.zeros_like(bn[0])
+        tgt[0] = bn[0] if key in _decisions else _NA.zeros_like(bn[0])
     masked = [False]
 
     def hip(tile):
@@ -536,7 +537,7 @@ def _vendor_dgrad0(g, w, x_shape, stride, padding):
     # .contiguous(CL)`` was a full-size copy of garbage per call) in g's layout --
     # a channels-last x with an NCHW g (the fp32 3-channel differential test)
     # mixes layouts in one MIOpen call, which aborted intermittently
-    xs = torch.empty(x_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
+    xs = _NA.empty(x_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
     dx, _, _ = torch.ops.aten.convolution_backward(
         g, xs, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [True, False, False])
     return dx
@@ -585,7 +586,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             def dest():
                 if out is not None:
                     return out.reshape(co, ci)
-                return torch.empty((co, ci), dtype=torch.float32, device=g.device)
+                return _NA.empty((co, ci), dtype=torch.float32, device=g.device)
 
             def wrap(d):
                 if d is None:
@@ -622,7 +623,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             co, ci = w_shape[0], w_shape[1]
 
             def lk():
-                d = out.reshape(co, ci) if out is not None else torch.empty((co, ci), dtype=torch.float32,
+                d = out.reshape(co, ci) if out is not None else _NA.empty((co, ci), dtype=torch.float32,
                                                                             device=g.device)
                 r = gemm_mfma.wgrad_longk(_rows(g), _rows(x), d)
                 if r is None:
@@ -655,7 +656,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
 
 
 def _vendor_wgrad(g, x, w_shape, stride, padding):
-    ws = torch.empty(w_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
+    ws = _NA.empty(w_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
     _, dw, _ = torch.ops.aten.convolution_backward(
         g, x, ws, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [False, True, False])
     return dw

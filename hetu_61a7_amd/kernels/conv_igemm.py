@@ -14,6 +14,7 @@ from __future__ import annotations
 import os
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, stream_ptr, check, record_native, P, I32, I64
 
@@ -44,7 +45,7 @@ def forward_f32(x, w, stride, padding, bias=None, act=None):
     N, C, H, W = x.shape
     K, _, KH, KW = w.shape
     OH, OW = _out_hw(H, W, KH, KW, stride, padding)
-    y = torch.empty((N, OH, OW, K), dtype=torch.float32, device=x.device)
+    y = _NA.empty((N, OH, OW, K), dtype=torch.float32, device=x.device)
     f = fn('hetu_conv_fwd_f32', [P, P, P, P] + _GEOM + [I32, P])
     check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(), bias.float().contiguous().data_ptr() if bias is not None
             else None, N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1],
@@ -61,7 +62,7 @@ def backward_data_f32(g, w, x_shape, stride, padding, acc=None):
         return None
     N, C, H, W = x_shape
     K, _, KH, KW = w.shape
-    dx = torch.empty((N, H, W, C), dtype=torch.float32, device=g.device)
+    dx = _NA.empty((N, H, W, C), dtype=torch.float32, device=g.device)
     f = fn('hetu_conv_dgrad_f32', [P, P, P, P] + _GEOM + [P])
     check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
             N, H, W, C, K, KH, KW, stride[0], stride[1], padding[0], padding[1], stream_ptr()), 'conv_dgrad_f32')
@@ -77,7 +78,7 @@ def backward_filter_f32(g, x, w_shape, stride, padding, out=None, accumulate=Non
     if accumulate is None:
         accumulate = out is not None
     if out is None:
-        dw = torch.empty((K, KH, KW, C), dtype=torch.float32, device=g.device)
+        dw = _NA.empty((K, KH, KW, C), dtype=torch.float32, device=g.device)
     else:
         dw = out.permute(0, 2, 3, 1)
         if not dw.is_contiguous() or dw.dtype != torch.float32:
@@ -106,7 +107,7 @@ def try_forward(x, w, stride, padding, bias=None, act=None, tile=0, colstats=Non
     N, C, H, W = x.shape
     K, _, KH, KW = w.shape
     OH, OW = _out_hw(H, W, KH, KW, stride, padding)
-    y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
+    y = _NA.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
     f = fn('hetu_conv_fwd_bf16', [P, P, P, P] + _GEOM + [I32, P, I32, I32, P])
     check(f(x.data_ptr(), w.data_ptr(), y.data_ptr(),
             bias.float().contiguous().data_ptr() if bias is not None else None,
@@ -136,8 +137,8 @@ def try_stem_forward(x, w, stride, padding, colstats=None):
     N, C, H, W = x.shape
     K, _, KH, KW = w.shape
     OH, OW = _out_hw(H, W, KH, KW, stride, padding)
-    wp = torch.empty(fn('hetu_stem_wp_elems', [I32], restype=I64)(KH), dtype=torch.bfloat16, device=x.device)
-    y = torch.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
+    wp = _NA.empty(fn('hetu_stem_wp_elems', [I32], restype=I64)(KH), dtype=torch.bfloat16, device=x.device)
+    y = _NA.empty((N, OH, OW, K), dtype=torch.bfloat16, device=x.device)
     f = fn('hetu_stem_fwd', [P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, P])
     check(f(x.data_ptr(), w.data_ptr(), wp.data_ptr(), y.data_ptr(),
             colstats.data_ptr() if colstats is not None else None, N, H, W, C, KH, KW, stride[0], padding[0],
@@ -186,7 +187,7 @@ def try_conv3x3_forward(x, w, stride, padding, colstats=None):
         return None
     N, C, H, W = x.shape
     K = w.shape[0]
-    y = torch.empty((N, H, W, K), dtype=torch.bfloat16, device=x.device)
+    y = _NA.empty((N, H, W, K), dtype=torch.bfloat16, device=x.device)
     st = colstats.data_ptr() if colstats is not None else None
     if _c64(C, K, W):
         f = fn('hetu_conv3x3_c64_fwd', [P, P, P, P, I32, I32, I32, I32, P])
@@ -211,8 +212,8 @@ def try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=None, bnb=None
         return None
     N, C, H, W = x_shape
     K = w.shape[0]
-    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
-    wt = torch.empty(w.numel(), dtype=torch.bfloat16, device=g.device)
+    dx = _NA.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
+    wt = _NA.empty(w.numel(), dtype=torch.bfloat16, device=g.device)
     a = acc.data_ptr() if acc is not None else None
     af = int(acc is not None and acc.dtype == torch.float32)
     if _c64(C, K, W):
@@ -237,21 +238,21 @@ def try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=None, accumu
     N, C, H, W = x.shape
     K = w_shape[0]
     if out is None:
-        dw = torch.empty((K, 3, 3, C), dtype=torch.float32, device=g.device)
+        dw = _NA.empty((K, 3, 3, C), dtype=torch.float32, device=g.device)
         accumulate = False
     else:
         dw = out.permute(0, 2, 3, 1)
         if not dw.is_contiguous() or dw.dtype != torch.float32 or dw.data_ptr() % 16:
             return None
     if _c64(C, K, W):
-        ws = torch.empty(int(fn('hetu_conv3x3_c64_wgrad_ws', [I32], restype=I64)(N)), dtype=torch.float32,
+        ws = _NA.empty(int(fn('hetu_conv3x3_c64_wgrad_ws', [I32], restype=I64)(N)), dtype=torch.float32,
                          device=g.device)
         f = fn('hetu_conv3x3_c64_wgrad', [P, P, P, P, I32, I32, I32, I32, P])
         check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), int(bool(accumulate)), N, H, W,
                 stream_ptr()), 'conv3x3_wgrad')
     else:
         nws = int(fn('hetu_conv3x3_wide_wgrad_ws', [I32, I32], restype=I64)(C, K))
-        ws = torch.empty(nws, dtype=torch.float32, device=g.device)
+        ws = _NA.empty(nws, dtype=torch.float32, device=g.device)
         f = fn('hetu_conv3x3_wide_wgrad', [P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P])
         check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), nws, int(bool(accumulate)), N, H, W, C, K,
                 stream_ptr()), 'conv3x3_wide_wgrad')
@@ -280,14 +281,14 @@ def try_stem_backward_filter(g, x, w_shape, stride, padding, out=None, accumulat
             or g.data_ptr() % 16:
         return None
     if out is None:
-        dw = torch.empty((co, kh, kw, c), dtype=torch.float32, device=g.device)
+        dw = _NA.empty((co, kh, kw, c), dtype=torch.float32, device=g.device)
         accumulate = False
     else:
         dw = out.permute(0, 2, 3, 1)
         if not dw.is_contiguous() or dw.dtype != torch.float32:
             return None
     nb = STEM_WGRAD_BLOCKS
-    ws = torch.empty(int(fn('hetu_stem_wgrad_ws', [I32], restype=I64)(nb)), dtype=torch.float32, device=g.device)
+    ws = _NA.empty(int(fn('hetu_stem_wgrad_ws', [I32], restype=I64)(nb)), dtype=torch.float32, device=g.device)
     f = fn('hetu_stem_wgrad', [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, P])
     check(f(x.data_ptr(), g.data_ptr(), dw.data_ptr(), ws.data_ptr(), nb, N, H, W, C, kh, kw, stride[0], padding[0],
             int(bool(accumulate)), stream_ptr()), 'stem_wgrad')
@@ -339,7 +340,7 @@ def try_backward_data(g, w, x_shape, stride, padding, acc=None, tile=0, bnb=None
         return None
     N, C, H, W = x_shape
     K, _, KH, KW = w.shape
-    dx = torch.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
+    dx = _NA.empty((N, H, W, C), dtype=torch.bfloat16, device=g.device)
     f = fn('hetu_conv_dgrad_bf16', [P, P, P, P, I32] + _GEOM + [I32, P, P, P, I32, I32, I32, P])
     check(f(g.data_ptr(), w.data_ptr(), dx.data_ptr(), acc.data_ptr() if acc is not None else None,
             int(acc is not None and acc.dtype == torch.float32), N, H, W, C, K, KH, KW,
@@ -366,7 +367,7 @@ def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=Non
     if accumulate is None:
         accumulate = out is not None
     if out is None:
-        dw = torch.empty((K, KH, KW, C), dtype=torch.float32, device=g.device)
+        dw = _NA.empty((K, KH, KW, C), dtype=torch.float32, device=g.device)
     else:
         dw = out.permute(0, 2, 3, 1)
         assert dw.is_contiguous() and dw.dtype == torch.float32
@@ -375,7 +376,7 @@ def try_backward_filter(g, x, w_shape, stride, padding, out=None, accumulate=Non
         return None
     # tile 4 (roles swapped): M = Nc taps on 128-row tiles, N = K channels on 64-col tiles
     sk = _splitk(Nc, 2 * K, N * OH * OW, 0) if tile == 4 else _splitk(K, Nc, N * OH * OW, tile)
-    ws = torch.empty(sk * K * Nc, dtype=torch.float32, device=g.device) if (sk > 1 or tile == 4) else None
+    ws = _NA.empty(sk * K * Nc, dtype=torch.float32, device=g.device) if (sk > 1 or tile == 4) else None
     # a single slice without accumulation stores straight into dw (plain fp32 epilogue,
     # no zero fill + atomics)
     f = fn('hetu_conv_wgrad_bf16', [P, P, P] + _GEOM + [I32, I32, P, I32, P])

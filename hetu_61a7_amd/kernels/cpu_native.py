@@ -15,6 +15,7 @@ import ctypes
 import os
 
 import torch
+from .. import native_array as _NA
 
 from .._base import _LIB_DIR
 
@@ -137,7 +138,7 @@ def gemm(a, b, bias=None):
     N = b.shape[1]
     A, lda, ta = _operand(a)
     B, ldb, tb = _operand(b)
-    out = torch.empty((M, N), dtype=torch.float32)
+    out = _NA.empty((M, N), dtype=torch.float32)
     bias = bias.contiguous() if bias is not None else None
     lib().hetu_cpu_gemm(_p(A), _p(B), _p(out), _p(bias), M, N, K, lda, ldb, N, ta, tb, 1.0, 0.0)
     return out
@@ -146,8 +147,8 @@ def gemm(a, b, bias=None):
 def softmax_ce(logits, labels):
     R, C = logits.shape
     x, y = logits.contiguous(), labels.float().contiguous()
-    loss = torch.empty(R, dtype=torch.float32)
-    lse = torch.empty(R, dtype=torch.float32)
+    loss = _NA.empty(R, dtype=torch.float32)
+    lse = _NA.empty(R, dtype=torch.float32)
     lib().hetu_cpu_softmax_ce(_p(x), _p(y), _p(loss), _p(lse), R, C)
     return loss, lse
 
@@ -156,21 +157,21 @@ def softmax_ce_backward(logits, labels, grad, lse):
     R, C = logits.shape
     x, y = logits.contiguous(), labels.float().contiguous()
     g = grad.float().contiguous().reshape(-1)
-    dx = torch.empty((R, C), dtype=torch.float32)
+    dx = _NA.empty((R, C), dtype=torch.float32)
     lib().hetu_cpu_softmax_ce_bwd(_p(x), _p(y), _p(g), _p(lse.contiguous()), _p(dx), R, C, int(g.numel() == 1))
     return dx
 
 
 def unary(op, x):
     xc = x.contiguous()
-    y = torch.empty_like(xc)
+    y = _NA.empty_like(xc)
     lib().hetu_cpu_unary(UNARY[op], _p(xc), _p(y), xc.numel())
     return y
 
 
 def relu_grad(x, g):
     xc, gc = x.contiguous(), g.contiguous()
-    y = torch.empty_like(xc)
+    y = _NA.empty_like(xc)
     lib().hetu_cpu_relu_grad(_p(xc), _p(gc), _p(y), xc.numel())
     return y
 
@@ -178,7 +179,7 @@ def relu_grad(x, g):
 def reduce_rows(x2, scale=1.0):
     R, C = x2.shape
     xc = x2.contiguous()
-    y = torch.empty(C, dtype=torch.float32)
+    y = _NA.empty(C, dtype=torch.float32)
     lib().hetu_cpu_reduce_rows(_p(xc), _p(y), R, C, float(scale))
     return y
 
@@ -186,7 +187,7 @@ def reduce_rows(x2, scale=1.0):
 def gather_rows(table, ids):
     dim = table.shape[-1]
     idx = ids.reshape(-1).long().contiguous()
-    out = torch.empty((idx.numel(), dim), dtype=torch.float32)
+    out = _NA.empty((idx.numel(), dim), dtype=torch.float32)
     lib().hetu_cpu_gather_rows(_p(table.contiguous()), _p(idx), _p(out), idx.numel(), dim, table.shape[0])
     return out.reshape(tuple(ids.shape) + (dim,))
 
@@ -210,7 +211,7 @@ def conv2d(x, w, b, stride, padding):
     N, C, H, W = x.shape
     K, _, KH, KW = w.shape
     OH, OW = _conv_out(H, W, KH, KW, stride, padding)
-    y = torch.empty((N, K, OH, OW), dtype=torch.float32)
+    y = _NA.empty((N, K, OH, OW), dtype=torch.float32)
     lib().hetu_cpu_conv2d(_p(x), _p(w), _p(b.float().contiguous() if b is not None else None), _p(y),
                           N, C, H, W, K, KH, KW, stride[0], stride[1], padding[0], padding[1])
     return y
@@ -220,7 +221,7 @@ def conv2d_backward_data(dy, w, x_shape, stride, padding):
     dy, w = _nchw(dy), _nchw(w)
     N, C, H, W = x_shape
     K, _, KH, KW = w.shape
-    dx = torch.empty((N, C, H, W), dtype=torch.float32)
+    dx = _NA.empty((N, C, H, W), dtype=torch.float32)
     lib().hetu_cpu_conv2d_bwd_data(_p(dy), _p(w), _p(dx), N, C, H, W, K, KH, KW, stride[0], stride[1],
                                    padding[0], padding[1])
     return dx
@@ -230,8 +231,8 @@ def conv2d_backward_filter(dy, x, w_shape, stride, padding, want_bias=False):
     dy, x = _nchw(dy), _nchw(x)
     N, C, H, W = x.shape
     K, _, KH, KW = w_shape
-    dw = torch.empty(tuple(w_shape), dtype=torch.float32)
-    db = torch.empty(K, dtype=torch.float32) if want_bias else None
+    dw = _NA.empty(tuple(w_shape), dtype=torch.float32)
+    db = _NA.empty(K, dtype=torch.float32) if want_bias else None
     lib().hetu_cpu_conv2d_bwd_filter(_p(dy), _p(x), _p(dw), _p(db), N, C, H, W, K, KH, KW, stride[0], stride[1],
                                      padding[0], padding[1])
     return (dw, db) if want_bias else dw
@@ -242,8 +243,8 @@ def maxpool2d(x, kh, kw, sh, sw, ph, pw):
     x = _nchw(x)
     N, C, H, W = x.shape
     OH, OW = _conv_out(H, W, kh, kw, (sh, sw), (ph, pw))
-    y = torch.empty((N, C, OH, OW), dtype=torch.float32)
-    idx = torch.empty((N, C, OH, OW), dtype=torch.int32)
+    y = _NA.empty((N, C, OH, OW), dtype=torch.float32)
+    idx = _NA.empty((N, C, OH, OW), dtype=torch.int32)
     lib().hetu_cpu_maxpool2d(_p(x), _p(y), _p(idx), N * C, H, W, kh, kw, sh, sw, ph, pw, OH, OW)
     return y, idx
 
@@ -251,7 +252,7 @@ def maxpool2d(x, kh, kw, sh, sw, ph, pw):
 def maxpool2d_backward(dy, idx, x_shape):
     dy = _nchw(dy)
     N, C, H, W = x_shape
-    dx = torch.empty((N, C, H, W), dtype=torch.float32)
+    dx = _NA.empty((N, C, H, W), dtype=torch.float32)
     lib().hetu_cpu_maxpool2d_bwd(_p(dy), _p(idx.contiguous()), _p(dx), N * C, H, W, dy.shape[2], dy.shape[3])
     return dx
 
@@ -260,7 +261,7 @@ def avgpool2d(x, kh, kw, sh, sw, ph, pw):
     x = _nchw(x)
     N, C, H, W = x.shape
     OH, OW = _conv_out(H, W, kh, kw, (sh, sw), (ph, pw))
-    y = torch.empty((N, C, OH, OW), dtype=torch.float32)
+    y = _NA.empty((N, C, OH, OW), dtype=torch.float32)
     lib().hetu_cpu_avgpool2d(_p(x), _p(y), N * C, H, W, kh, kw, sh, sw, ph, pw, OH, OW)
     return y
 
@@ -268,7 +269,7 @@ def avgpool2d(x, kh, kw, sh, sw, ph, pw):
 def avgpool2d_backward(dy, x_shape, kh, kw, sh, sw, ph, pw):
     dy = _nchw(dy)
     N, C, H, W = x_shape
-    dx = torch.empty((N, C, H, W), dtype=torch.float32)
+    dx = _NA.empty((N, C, H, W), dtype=torch.float32)
     lib().hetu_cpu_avgpool2d_bwd(_p(dy), _p(dx), N * C, H, W, kh, kw, sh, sw, ph, pw, dy.shape[2], dy.shape[3])
     return dx
 
@@ -278,9 +279,9 @@ def batchnorm(x, scale, bias, running_mean, running_var, factor, eps, training):
     x = _nchw(x)
     N, C = x.shape[0], x.shape[1]
     HW = x.numel() // max(N * C, 1)
-    y = torch.empty_like(x)
-    sm = torch.empty(C, dtype=torch.float32)
-    sr = torch.empty(C, dtype=torch.float32)
+    y = _NA.empty_like(x)
+    sm = _NA.empty(C, dtype=torch.float32)
+    sr = _NA.empty(C, dtype=torch.float32)
     lib().hetu_cpu_batchnorm(_p(x), _p(scale.float().contiguous()), _p(bias.float().contiguous()), _p(y),
                              _p(running_mean), _p(running_var), _p(sm), _p(sr), N, C, HW, float(factor), float(eps),
                              int(bool(training)))
@@ -291,9 +292,9 @@ def batchnorm_backward(dy, x, scale, save_mean, save_invstd):
     dy, x = _nchw(dy), _nchw(x)
     N, C = x.shape[0], x.shape[1]
     HW = x.numel() // max(N * C, 1)
-    dx = torch.empty_like(x)
-    ds = torch.empty(C, dtype=torch.float32)
-    db = torch.empty(C, dtype=torch.float32)
+    dx = _NA.empty_like(x)
+    ds = _NA.empty(C, dtype=torch.float32)
+    db = _NA.empty(C, dtype=torch.float32)
     lib().hetu_cpu_batchnorm_bwd(_p(dy), _p(x), _p(scale.float().contiguous()), _p(save_mean.contiguous()),
                                  _p(save_invstd.contiguous()), _p(dx), _p(ds), _p(db), N, C, HW)
     return dx, ds, db
@@ -303,7 +304,7 @@ def batchnorm_backward(dy, x, scale, save_mean, save_invstd):
 def unary_code(code, x, c=0.0, c2=0.0, out=None):
     """y = unary op ``code`` (elementwise.hip's U table) of fp32 ``x``."""
     xc = x.contiguous()
-    y = out if out is not None and out.is_contiguous() else torch.empty_like(xc)
+    y = out if out is not None and out.is_contiguous() else _NA.empty_like(xc)
     _chk(lib().hetu_cpu_unary_ext(int(code), _p(xc), _p(y), xc.numel(), float(c), float(c2)), 'unary')
     if out is not None and y is not out:
         copy_nd(y, out)
@@ -335,7 +336,7 @@ def binary_code(code, a, b, c=0.0, out=None):
     if len(cs) > 8:
         return None
     y = out if (out is not None and out.is_contiguous() and tuple(out.shape) == tuple(shape)) else \
-        torch.empty(shape, dtype=torch.float32)
+        _NA.empty(shape, dtype=torch.float32)
     _chk(lib().hetu_cpu_binary_nd(int(code), _p(a), _p(b), _p(y), len(cs), _arr(cs), _arr(ca), _arr(cb), float(c)),
          'binary')
     if out is not None and y is not out:
@@ -371,7 +372,7 @@ def fill(t, v):
 
 def softmax(x, log=False):
     xc = x.contiguous()
-    y = torch.empty_like(xc)
+    y = _NA.empty_like(xc)
     C = x.shape[-1] if x.dim() else 1
     lib().hetu_cpu_softmax(_p(xc), _p(y), xc.numel() // max(C, 1), C, int(bool(log)))
     return y
@@ -379,7 +380,7 @@ def softmax(x, log=False):
 
 def softmax_backward(y, dy):
     yc, gc = y.contiguous(), dy.contiguous()
-    dx = torch.empty_like(yc)
+    dx = _NA.empty_like(yc)
     C = y.shape[-1]
     lib().hetu_cpu_softmax_bwd(_p(yc), _p(gc), _p(dx), yc.numel() // C, C)
     return dx
@@ -390,8 +391,8 @@ def softmax_ce_sparse(logits, labels, ignored):
     x = logits.contiguous()
     lab = labels.reshape(-1).long().contiguous()
     R = x.numel() // C
-    loss = torch.empty(R, dtype=torch.float32)
-    lse = torch.empty(R, dtype=torch.float32)
+    loss = _NA.empty(R, dtype=torch.float32)
+    lse = _NA.empty(R, dtype=torch.float32)
     lib().hetu_cpu_softmax_ce_sparse(_p(x), _p(lab), _p(loss), _p(lse), R, C, int(ignored))
     return loss.reshape(logits.shape[:-1]), lse.reshape(logits.shape[:-1])
 
@@ -401,7 +402,7 @@ def softmax_ce_sparse_backward(logits, labels, g, scalar, lse, ignored):
     x = logits.contiguous()
     lab = labels.reshape(-1).long().contiguous()
     R = x.numel() // C
-    dx = torch.empty_like(x)
+    dx = _NA.empty_like(x)
     lib().hetu_cpu_softmax_ce_sparse_bwd(_p(x), _p(lab), _p(g), int(scalar), _p(lse.contiguous()), _p(dx), R, C,
                                          int(ignored))
     return dx
@@ -410,7 +411,7 @@ def softmax_ce_sparse_backward(logits, labels, g, scalar, lse, ignored):
 def dropout(x, keep, seed):
     """Philox mask at counter = flat index / 4: the GPU kernel's mask for the same seed"""
     xc = x.contiguous()
-    y = torch.empty_like(xc)
+    y = _NA.empty_like(xc)
     lib().hetu_cpu_dropout(_p(xc), _p(y), xc.numel(), float(keep), int(seed))
     return y
 
@@ -428,7 +429,7 @@ def random_init(t, kind, a, b, seed):
 def reduce_axis0(x2, scale=1.0):
     R, C = x2.shape
     xc = x2.contiguous()
-    y = torch.empty(C, dtype=torch.float32)
+    y = _NA.empty(C, dtype=torch.float32)
     lib().hetu_cpu_reduce_axis0(_p(xc), _p(y), R, C, float(scale))
     return y
 
@@ -436,6 +437,6 @@ def reduce_axis0(x2, scale=1.0):
 def reduce_lastdim(x2, scale=1.0):
     R, C = x2.shape
     xc = x2.contiguous()
-    y = torch.empty(R, dtype=torch.float32)
+    y = _NA.empty(R, dtype=torch.float32)
     lib().hetu_cpu_reduce_lastdim(_p(xc), _p(y), R, C, float(scale))
     return y

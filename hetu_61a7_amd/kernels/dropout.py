@@ -4,6 +4,7 @@ from the seed (reference Dropout.cu `curand_init(seed, 0, idx)` semantics)."""
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32, F32
 
@@ -11,7 +12,7 @@ from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I
 def dropout(x, keep_prob, seed):
     if native(x) and supported_float(x):
         xc = x.contiguous()
-        y = torch.empty_like(xc)
+        y = _NA.empty_like(xc)
         f = fn('hetu_dropout', [P, P, I64, F32, I64, I32, P])
         check(f(xc.data_ptr(), y.data_ptr(), xc.numel(), float(keep_prob), int(seed), is_bf16(x),
                 stream_ptr()), 'dropout')

@@ -7,6 +7,7 @@ import ctypes
 
 import torch
 import torch.nn.functional as F
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32, F32
 
@@ -76,7 +77,7 @@ def _ref_unary(op, x, c, c2):
 
 def unary(op: str, x: torch.Tensor, c: float = 0.0, c2: float = 0.0, out=None) -> torch.Tensor:
     if native(x) and supported_float(x) and x.is_contiguous():
-        y = out if out is not None else torch.empty_like(x)
+        y = out if out is not None else _NA.empty_like(x)
         f = fn('hetu_unary', [I32, P, P, I64, I32, F32, F32, P])
         check(f(U[op], x.data_ptr(), y.data_ptr(), x.numel(), is_bf16(x), float(c), float(c2),
                 stream_ptr()), 'unary:' + op)
@@ -106,7 +107,7 @@ def _ref_binary(op, a, b, c):
     if op == 'min':
         return torch.minimum(a, b.to(a.dtype))
     if op == 'relu_grad':
-        return torch.where(a > 0, b, torch.zeros_like(b))
+        return torch.where(a > 0, b, _NA.zeros_like(b))
     if op == 'gelu_grad':
         cdf = 0.5 * (1.0 + torch.erf(a / math.sqrt(2.0)))
         pdf = torch.exp(-0.5 * a * a) / math.sqrt(2 * math.pi)
@@ -154,7 +155,7 @@ def binary(op: str, a: torch.Tensor, b: torch.Tensor, c: float = 0.0, out=None) 
             if m3 is not None:
                 mode, (inner, bnum) = 3, m3
         if mode >= 0:
-            y = out if out is not None else torch.empty_like(a)
+            y = out if out is not None else _NA.empty_like(a)
             f = fn('hetu_binary3', [I32, P, P, P, I64, I32, I32, I32, I64, I64, F32, P])
             check(f(B[op], a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), is_bf16(a),
                     is_bf16(b), mode, inner, bnum, float(c), stream_ptr()), 'binary:' + op)
@@ -242,7 +243,7 @@ def _binary_nd(op, a, b, c, out):
     ae, be = a.expand(shape), b.expand(shape)
     if out is not None and (tuple(out.shape) != tuple(shape) or not out.is_contiguous() or out.dtype != a.dtype):
         return None
-    y = out if out is not None else torch.empty(shape, dtype=a.dtype, device=a.device)
+    y = out if out is not None else _NA.empty(shape, dtype=a.dtype, device=a.device)
     cs, ca, cb = _collapse(shape, ae.stride(), be.stride())
     nd = len(cs)
     arr = ctypes.c_int64 * nd
@@ -256,7 +257,7 @@ def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     if x.dtype == dtype:
         return x
     if native(x) and x.is_contiguous() and {x.dtype, dtype} == {torch.float32, torch.bfloat16}:
-        y = torch.empty(x.shape, dtype=dtype, device=x.device)
+        y = _NA.empty(x.shape, dtype=dtype, device=x.device)
         f = fn('hetu_cast', [P, I32, P, I32, I64, P])
         check(f(x.data_ptr(), is_bf16(x), y.data_ptr(), 1 if dtype == torch.bfloat16 else 0,
                 x.numel(), stream_ptr()), 'cast')

@@ -12,6 +12,7 @@ from __future__ import annotations
 import os
 
 import torch
+from .. import native_array as _NA
 
 from . import native, record_vendor
 
@@ -104,7 +105,7 @@ def _as_dtype(t, dt):
         return sh
     if t.is_cuda:   # the native cast, keeping a dense operand's stride order
         from .tensor import copy_into
-        return copy_into(torch.empty_like(t, dtype=dt), t)
+        return copy_into(_NA.empty_like(t, dtype=dt), t)
     return t.to(dt)
 
 
@@ -271,7 +272,7 @@ def _pad8_into(A, B, out, splitk):
     K, N = B.shape
     bp = zeros((K, 8), B.dtype, B.device)
     copy_into(bp[:, :N], B)
-    op = torch.empty((A.shape[0], 8), dtype=torch.float32, device=A.device)
+    op = _NA.empty((A.shape[0], 8), dtype=torch.float32, device=A.device)
     if gemm_mfma.gemm(A, bp, out=op, splitk=splitk, tile=3) is None:
         return None
     copy_into(out, op[:, :N])
@@ -296,7 +297,7 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
         def c():
             if cc[0] is None:
                 from .tensor import copy_into
-                cc[0] = copy_into(torch.empty_like(acc, dtype=a.dtype), acc)
+                cc[0] = copy_into(_NA.empty_like(acc, dtype=a.dtype), acc)
             return cc[0]
         key = ('gemm_acc', _sig(a), _sig(b), ta, tb)
         inplace = inplace and acc.dtype == a.dtype and acc.is_contiguous()

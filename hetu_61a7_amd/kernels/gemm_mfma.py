@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, stream_ptr, check, record_native, P, I64, I32, F32
 
@@ -152,7 +153,7 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
     if splitk > 1:
         if bias is not None or act is not None or cin_t is not None:
             return _reject(7, a, b, out)
-        ws = torch.empty(splitk * batch * M * N, dtype=torch.float32, device=a.device)
+        ws = _NA.empty(splitk * batch * M * N, dtype=torch.float32, device=a.device)
         if batch > 1:
             return _reject(8, a, b, out)
     f = fn('hetu_gemm_bf16', _ARGS)
@@ -188,7 +189,7 @@ def wgrad_longk(a_pm, b_pm, out, accumulate=False, splits=None):
     tiles = (M // 64) * (N // 64)
     if splits is None:
         splits = max(1, min(2048 // tiles, -(-P_ // 512)))
-    ws = torch.empty(int(fn('hetu_wgrad_longk_ws', [I32, I32, I32], restype=I64)(M, N, splits)),
+    ws = _NA.empty(int(fn('hetu_wgrad_longk_ws', [I32, I32, I32], restype=I64)(M, N, splits)),
                      dtype=torch.float32, device=a_pm.device)
     f = fn('hetu_wgrad_longk', [P, P, P, P, I64, I32, I32, I32, I32, I64, I32, I32, P])
     check(f(a_pm.data_ptr(), b_pm.data_ptr(), out.data_ptr(), ws.data_ptr(), P_, M, N, lda, ldb,
@@ -210,7 +211,7 @@ def gemm_small(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=Non
         return None
     odt = out_dtype or (out.dtype if out is not None else a.dtype)
     if out is None:
-        out = torch.empty((M, N), dtype=odt, device=a.device)
+        out = _NA.empty((M, N), dtype=odt, device=a.device)
     if out.dim() != 2 or out.stride(-1) != 1 or out.dtype not in (torch.float32, torch.bfloat16):
         return None
     cin_t = None

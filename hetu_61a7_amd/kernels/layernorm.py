@@ -7,6 +7,7 @@ from __future__ import annotations
 import os
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32, F32
 
@@ -24,9 +25,9 @@ def layer_norm(x, gamma, beta, eps):
         return y, mean, rstd
     if native(x) and supported_float(x):
         xc = x.contiguous()
-        y = torch.empty_like(xc)
-        mean = torch.empty(R, dtype=torch.float32, device=x.device)
-        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        y = _NA.empty_like(xc)
+        mean = _NA.empty(R, dtype=torch.float32, device=x.device)
+        rstd = _NA.empty(R, dtype=torch.float32, device=x.device)
         f = fn('hetu_layernorm_fwd', [P, P, P, P, P, P, I64, I32, F32, I32, P])
         check(f(xc.data_ptr(), gamma.float().contiguous().data_ptr(), beta.float().contiguous().data_ptr(),
                 y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), R, N, float(eps), is_bf16(x),
@@ -44,7 +45,7 @@ def _dest(out, N, dev):
     """fp32 [N] result buffer: the caller's (e.g. the optimizer's flat gradient slot) or new"""
     if out is not None and out.dtype == torch.float32 and out.is_contiguous() and out.numel() == N:
         return out
-    return torch.empty(N, dtype=torch.float32, device=dev)
+    return _NA.empty(N, dtype=torch.float32, device=dev)
 
 
 def layer_norm_backward(dy, x, gamma, mean, rstd, dg_out=None, db_out=None):
@@ -58,9 +59,9 @@ def layer_norm_backward(dy, x, gamma, mean, rstd, dg_out=None, db_out=None):
         return ds, dg, db
     if native(x) and supported_float(x) and dy.dtype == x.dtype:
         xc, dyc = x.contiguous(), dy.contiguous()
-        dx = torch.empty_like(xc)
+        dx = _NA.empty_like(xc)
         ws_rows = min(R, 1024)
-        ws = torch.empty(2 * ws_rows * N, dtype=torch.float32, device=x.device)
+        ws = _NA.empty(2 * ws_rows * N, dtype=torch.float32, device=x.device)
         dg, db = _dest(dg_out, N, x.device), _dest(db_out, N, x.device)
         f = fn('hetu_layernorm_bwd', [P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, P])
         check(f(dyc.data_ptr(), xc.data_ptr(), gamma.float().contiguous().data_ptr(), mean.data_ptr(),
@@ -93,10 +94,10 @@ def layer_norm_fused(x, residual, gamma, beta, eps, keep=1.0, seed=0):
     if _fused_ok(x) and (residual is None or residual.dtype == x.dtype):
         xc = x.contiguous()
         rc = residual.contiguous() if residual is not None else None
-        y = torch.empty_like(xc)
-        s = xc if plain else torch.empty_like(xc)
-        mean = torch.empty(R, dtype=torch.float32, device=x.device)
-        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        y = _NA.empty_like(xc)
+        s = xc if plain else _NA.empty_like(xc)
+        mean = _NA.empty(R, dtype=torch.float32, device=x.device)
+        rstd = _NA.empty(R, dtype=torch.float32, device=x.device)
         f = fn('hetu_ln_fused_fwd', [P, P, P, P, P, P, P, P, I64, I32, F32, F32, I64, I32, P])
         check(f(xc.data_ptr(), rc.data_ptr() if rc is not None else None, gamma.float().contiguous().data_ptr(),
                 beta.float().contiguous().data_ptr(), y.data_ptr(), None if plain else s.data_ptr(),
@@ -122,12 +123,12 @@ def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_d
     R = s.numel() // N
     if _fused_ok(s) and dy.dtype == s.dtype:
         dyc, sc = dy.contiguous(), s.contiguous()
-        ds = torch.empty_like(sc) if need_ds else None
-        dx = torch.empty_like(sc) if (need_dx and keep < 1.0) else None
+        ds = _NA.empty_like(sc) if need_ds else None
+        dx = _NA.empty_like(sc) if (need_dx and keep < 1.0) else None
         if need_dx and keep >= 1.0 and not need_ds:
-            ds = torch.empty_like(sc)
+            ds = _NA.empty_like(sc)
         nblk = max(1, min(_LN_BWD_BLOCKS, (R + 7) // 8))
-        ws = torch.empty((3 if want_dlin else 2) * nblk * N, dtype=torch.float32, device=s.device)
+        ws = _NA.empty((3 if want_dlin else 2) * nblk * N, dtype=torch.float32, device=s.device)
         dg, db = _dest(dg_out, N, s.device), _dest(db_out, N, s.device)
         dlin = _dest(dlin_out, N, s.device) if want_dlin else None
         from . import deterministic
@@ -175,13 +176,13 @@ def gelu_grad_colsum(pre, dy, out=None):
         return g, cs
     pre, dy = pre.contiguous(), dy.contiguous()
     R = pre.shape[0]
-    g = torch.empty_like(pre)
+    g = _NA.empty_like(pre)
     cv = N // V
     W = min(cv, 64)
     RP = 256 // W
     tiles = -(-cv // W)
     chunks = max(1, min(max(1, 2048 // tiles), R // (RP * 4)))   # ~2048 blocks: 8 waves per CU
-    ws = torch.empty(chunks * N, dtype=torch.float32, device=pre.device)
+    ws = _NA.empty(chunks * N, dtype=torch.float32, device=pre.device)
     cs = _dest(out, N, pre.device)
     from . import deterministic
     f = fn('hetu_gelu_grad_colsum', [P, P, P, P, P, I64, I32, I32, I32, I32, P])

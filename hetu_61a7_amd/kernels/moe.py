@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32
 
@@ -25,7 +26,7 @@ def _dc(t, dtype=None):
         return t
     if t.is_cuda:
         from .tensor import copy_into
-        return copy_into(torch.empty(t.shape, dtype=dtype, device=t.device), t)
+        return copy_into(_NA.empty(t.shape, dtype=dtype, device=t.device), t)
     return t.to(dtype).contiguous()
 
 
@@ -43,9 +44,9 @@ def topk(x, k, softmax=False):
     R, E = x.reshape(-1, x.shape[-1]).shape
     if native(x) and supported_float(x) and E <= 512 and k <= min(8, E):
         x2 = x.reshape(R, E).contiguous()
-        probs = torch.empty((R, E) if softmax else (1,), dtype=torch.float32, device=x.device)
-        idx = torch.empty((R, k), dtype=torch.int64, device=x.device)
-        val = torch.empty((R, k), dtype=torch.float32, device=x.device)
+        probs = _NA.empty((R, E) if softmax else (1,), dtype=torch.float32, device=x.device)
+        idx = _NA.empty((R, k), dtype=torch.int64, device=x.device)
+        val = _NA.empty((R, k), dtype=torch.float32, device=x.device)
         f = fn('hetu_moe_gate_topk', [P, P, P, P, I32, I32, I32, I32, I32, P])
         check(f(x2.data_ptr(), probs.data_ptr(), idx.data_ptr(), val.data_ptr(), R, E, k, int(softmax),
                 is_bf16(x2), stream_ptr()), 'moe_gate_topk')
@@ -66,12 +67,12 @@ def locations(idx, num_experts, probs=None, inactive=False):
     E = num_experts
     if native(idx):
         idx = idx.long().contiguous()
-        loc = torch.empty((T, k), dtype=torch.int64, device=idx.device)
+        loc = _NA.empty((T, k), dtype=torch.int64, device=idx.device)
         if inactive:   # choices with idx -1 (dense-to-sparse gate) keep loc -1: dropped everywhere
             from .tensor import fill_
             fill_(loc, -1)
-        counts = torch.empty((E,), dtype=torch.int32, device=idx.device)
-        psum = torch.empty((E,), dtype=torch.float32, device=idx.device) if probs is not None else None
+        counts = _NA.empty((E,), dtype=torch.int32, device=idx.device)
+        psum = _NA.empty((E,), dtype=torch.float32, device=idx.device) if probs is not None else None
         f = fn('hetu_moe_locations', [P, P, P, P, P, I32, I32, I32, P])
         check(f(idx.data_ptr(), probs.contiguous().data_ptr() if probs is not None else None, loc.data_ptr(),
                 counts.data_ptr(), psum.data_ptr() if psum is not None else None, T, k, E, stream_ptr()),
@@ -92,8 +93,8 @@ def aux_terms(counts, psum, T):
     """(coef [E] = counts / T, l_aux [] = E * sum_e psum_e / T * coef_e): one native launch"""
     E = counts.numel()
     if native(psum) and counts.dtype == torch.int32 and psum.dtype == torch.float32:
-        coef = torch.empty((E,), dtype=torch.float32, device=psum.device)
-        l_aux = torch.empty((), dtype=torch.float32, device=psum.device)
+        coef = _NA.empty((E,), dtype=torch.float32, device=psum.device)
+        l_aux = _NA.empty((), dtype=torch.float32, device=psum.device)
         f = fn('hetu_moe_aux', [P, P, P, P, I32, I32, P])
         check(f(counts.contiguous().data_ptr(), psum.contiguous().data_ptr(), coef.data_ptr(), l_aux.data_ptr(),
                 int(T), int(E), stream_ptr()), 'moe_aux')
@@ -111,19 +112,19 @@ def gate_backward(probs, idx, dgate, aux_coef, scale=1.0):
     T, E = probs.shape
     k = idx.shape[1]
     if native(probs) and E <= 512 and k <= MAX_K:
-        out = torch.empty((T, E), dtype=torch.float32, device=probs.device)
+        out = _NA.empty((T, E), dtype=torch.float32, device=probs.device)
         dg = _dc(dgate.reshape(T, k), torch.float32) if dgate is not None else None
         ac = _dc(aux_coef, torch.float32) if aux_coef is not None else None
         f = fn('hetu_moe_gate_backward', [P, P, P, P, P, I32, I32, I32, ctypes.c_float, P])
         check(f(probs.contiguous().data_ptr(), idx.long().contiguous().data_ptr(), ptr_or_none(dg), ptr_or_none(ac),
                 out.data_ptr(), T, E, k, float(scale), stream_ptr()), 'moe_gate_backward')
         return out
-    dp = torch.zeros((T, E), dtype=torch.float32, device=probs.device)
+    dp = _NA.zeros((T, E), dtype=torch.float32, device=probs.device)
     if dgate is not None:
         il = idx.long()
         on = il >= 0
-        dp.scatter_add_(1, torch.where(on, il, torch.zeros_like(il)),
-                        torch.where(on, dgate.float().reshape(T, k), torch.zeros((T, k), device=probs.device)))
+        dp.scatter_add_(1, torch.where(on, il, _NA.zeros_like(il)),
+                        torch.where(on, dgate.float().reshape(T, k), _NA.zeros((T, k), device=probs.device)))
     if aux_coef is not None:
         dp = dp + aux_coef.float().unsqueeze(0)
     p = probs.float()
@@ -170,10 +171,10 @@ def dts_gate(logits, k, inv_tau, threshold, seed, noise=True):
     seed = int(seed) & ((1 << 63) - 1)
     if native(logits) and supported_float(logits) and E <= 512 and 1 <= k <= min(MAX_K, E):
         x = logits.contiguous()
-        probs = torch.empty((T, E), dtype=torch.float32, device=x.device)
-        idx = torch.empty((T, k), dtype=torch.int64, device=x.device)
-        val = torch.empty((T, k), dtype=torch.float32, device=x.device)
-        hist = torch.empty((k + 1,), dtype=torch.int32, device=x.device)
+        probs = _NA.empty((T, E), dtype=torch.float32, device=x.device)
+        idx = _NA.empty((T, k), dtype=torch.int64, device=x.device)
+        val = _NA.empty((T, k), dtype=torch.float32, device=x.device)
+        hist = _NA.empty((k + 1,), dtype=torch.int32, device=x.device)
         f = fn('hetu_moe_dts_gate', [P, P, P, P, P, I32, I32, I32, ctypes.c_float, ctypes.c_float, ctypes.c_uint64,
                                      I32, I32, P])
         check(f(x.data_ptr(), probs.data_ptr(), idx.data_ptr(), val.data_ptr(), hist.data_ptr(), T, E, k,
@@ -192,7 +193,7 @@ def dts_gate(logits, k, inv_tau, threshold, seed, noise=True):
     on = torch.ones_like(v, dtype=torch.bool)
     on[:, 1:] = v[:, 1:] >= threshold
     idx = torch.where(on, i, torch.full_like(i, -1))
-    val = torch.where(on, v, torch.zeros_like(v))
+    val = torch.where(on, v, _NA.zeros_like(v))
     hist = torch.bincount(on.sum(1), minlength=k + 1).to(torch.int32)
     return val, idx, probs, hist
 
@@ -203,7 +204,7 @@ def ptr_or_none(t):
 
 def _slot_map(idx, loc, capacity, nslots):
     Tk = idx.numel()
-    m = torch.empty((nslots,), dtype=torch.int32, device=idx.device)
+    m = _NA.empty((nslots,), dtype=torch.int32, device=idx.device)
     f = fn('hetu_moe_slot_map', [P, P, P, I32, I32, I32, P])
     check(f(idx.data_ptr(), loc.data_ptr(), m.data_ptr(), Tk, capacity, nslots, stream_ptr()), 'moe_slot_map')
     return m
@@ -218,12 +219,12 @@ def layout_transform(x, indices, locations, capacity, num_experts):
     if _io_ok(x):
         x = _dc(x)
         smap = _slot_map(idx, loc, capacity, nslots)
-        out = torch.empty((nslots, d), dtype=x.dtype, device=x.device)
+        out = _NA.empty((nslots, d), dtype=x.dtype, device=x.device)
         f = fn('hetu_moe_gather_slots', [P, P, P, P, I32, I32, I32, I32, P])
         check(f(x.data_ptr(), smap.data_ptr(), None, out.data_ptr(), nslots, d, k, is_bf16(x), stream_ptr()),
               'moe_gather_slots')
         return out
-    out = torch.zeros((nslots, d), dtype=x.dtype, device=x.device)
+    out = _NA.zeros((nslots, d), dtype=x.dtype, device=x.device)
     valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
     slots = idx * capacity + loc
     tok = torch.arange(T, device=x.device).unsqueeze(1).expand(T, k)
@@ -235,7 +236,7 @@ def _combine(y, idx, loc, w, capacity, T):
     d = y.shape[-1]
     k = idx.shape[1]
     y = _dc(y)
-    out = torch.empty((T, d), dtype=y.dtype, device=y.device)
+    out = _NA.empty((T, d), dtype=y.dtype, device=y.device)
     wf = _dc(w.reshape(T, k), torch.float32) if w is not None else None
     f = fn('hetu_moe_combine', [P, P, P, P, P, I32, I32, I32, I32, I32, P])
     check(f(y.data_ptr(), idx.data_ptr(), loc.data_ptr(), ptr_or_none(wf), out.data_ptr(), T, k, capacity, d,
@@ -251,7 +252,7 @@ def layout_transform_backward(g, indices, locations, capacity):
     if _io_ok(g) and k <= MAX_K:
         return _combine(g, idx, loc, None, capacity, T)
     valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
-    slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
+    slots = torch.where(valid, idx * capacity + loc, _NA.zeros_like(idx))
     gathered = g[slots.reshape(-1)].reshape(T, k, -1) * valid.unsqueeze(-1).to(g.dtype)
     return gathered.sum(1)
 
@@ -264,7 +265,7 @@ def reverse_layout_transform(y, indices, locations, gates, capacity):
     if _io_ok(y) and k <= MAX_K:
         return _combine(y, idx, loc, gates, capacity, T)
     valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
-    slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
+    slots = torch.where(valid, idx * capacity + loc, _NA.zeros_like(idx))
     rows = y[slots.reshape(-1)].reshape(T, k, -1).float()
     w = (gates.reshape(T, k).float() * valid.float()) if gates is not None else valid.float()
     return (rows * w.unsqueeze(-1)).sum(1).to(y.dtype)
@@ -279,7 +280,7 @@ def reverse_layout_transform_backward_data(g, indices, locations, gates, capacit
         g = _dc(g)
         smap = _slot_map(idx, loc, capacity, num_slots)
         wf = _dc(gates.reshape(T, k), torch.float32) if gates is not None else None
-        out = torch.empty((num_slots, d), dtype=g.dtype, device=g.device)
+        out = _NA.empty((num_slots, d), dtype=g.dtype, device=g.device)
         f = fn('hetu_moe_gather_slots', [P, P, P, P, I32, I32, I32, I32, P])
         check(f(g.data_ptr(), smap.data_ptr(), ptr_or_none(wf), out.data_ptr(), num_slots, d, k, is_bf16(g),
                 stream_ptr()), 'moe_gather_slots')
@@ -287,7 +288,7 @@ def reverse_layout_transform_backward_data(g, indices, locations, gates, capacit
     valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
     slots = idx * capacity + loc
     w = (gates.reshape(T, k).float() * valid.float()) if gates is not None else valid.float()
-    out = torch.zeros((num_slots, d), dtype=torch.float32, device=g.device)
+    out = _NA.zeros((num_slots, d), dtype=torch.float32, device=g.device)
     contrib = g.float().unsqueeze(1) * w.unsqueeze(-1)
     out.index_add_(0, slots[valid], contrib[valid])
     return out.to(g.dtype)
@@ -300,13 +301,13 @@ def reverse_layout_transform_backward_gate(g, y, indices, locations, capacity):
     d = g.shape[-1]
     if _io_ok(g, y):
         g, y = _dc(g), _dc(y)
-        out = torch.empty((T, k), dtype=torch.float32, device=g.device)
+        out = _NA.empty((T, k), dtype=torch.float32, device=g.device)
         f = fn('hetu_moe_gate_grad', [P, P, P, P, P, I32, I32, I32, I32, I32, P])
         check(f(g.data_ptr(), y.data_ptr(), idx.data_ptr(), loc.data_ptr(), out.data_ptr(), T * k, k, capacity, d,
                 is_bf16(g), stream_ptr()), 'moe_gate_grad')
         return out.reshape(indices.shape)
     valid = (loc < capacity) & (loc >= 0) & (idx >= 0)
-    slots = torch.where(valid, idx * capacity + loc, torch.zeros_like(idx))
+    slots = torch.where(valid, idx * capacity + loc, _NA.zeros_like(idx))
     rows = y[slots.reshape(-1)].reshape(T, k, -1).float()
     dd = (rows * g.float().unsqueeze(1)).sum(-1) * valid.float()
     return dd.reshape(indices.shape)
@@ -323,7 +324,7 @@ def balanced_assignment(scores, max_iterations=100):
     s = scores.float()
     T, E = s.shape
     cap = T // E
-    prices = torch.zeros(E, device=s.device)
+    prices = _NA.zeros(E, device=s.device)
     eps = 1e-4 * (s.max() - s.min()).clamp_min(1e-6)
     assign = torch.full((T,), -1, dtype=torch.long, device=s.device)
     for _ in range(max_iterations):

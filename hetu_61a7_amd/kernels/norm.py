@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, P, I64, I32, F32
 
@@ -21,14 +22,14 @@ def _as_rows(x):
 
 def _like_rows(x):
     if x.dim() == 4:
-        return torch.empty_like(x, memory_format=torch.channels_last)
-    return torch.empty_like(x)
+        return _NA.empty_like(x, memory_format=torch.channels_last)
+    return _NA.empty_like(x)
 
 
 def _ws(M, C, bf, device):
     f = fn('hetu_bn_workspace_floats', [I64, I32, I32], restype=I64)
     n = f(M, C, bf)
-    return torch.empty(n, dtype=torch.float32, device=device)
+    return _NA.empty(n, dtype=torch.float32, device=device)
 
 
 def col_sums(x):
@@ -40,7 +41,7 @@ def col_sums(x):
         return None
     xr, _ = rows
     M = xr.shape[0]
-    sums = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    sums = _NA.empty(2 * C, dtype=torch.float32, device=x.device)
     ws = _ws(M, C, is_bf16(x), x.device)
     f = fn('hetu_col_sums', [P, I64, I32, I32, P, P, P])
     check(f(xr.data_ptr(), M, C, is_bf16(x), ws.data_ptr(), sums.data_ptr(), stream_ptr()), 'col_sums')
@@ -72,8 +73,8 @@ def bn_forward(x, scale, bias, running_mean, running_var, factor, eps, training,
             xr, _ = rows
             M = xr.shape[0]
             y = _like_rows(x)
-            save_mean = torch.empty(C, dtype=torch.float32, device=x.device)
-            save_invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+            save_mean = _NA.empty(C, dtype=torch.float32, device=x.device)
+            save_invstd = _NA.empty(C, dtype=torch.float32, device=x.device)
             ws = _ws(M, C, is_bf16(x), x.device)
             if mask is not None:
                 assert relu and mask.dtype == torch.uint8 and mask.numel() == relu_mask_bytes(x) and mask.is_cuda
@@ -164,8 +165,8 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
             M = x.numel() // C
             dx = _like_rows(x)
             dres = _like_rows(x) if want_dres else None
-            dscale = dscale_out if dscale_out is not None else torch.empty(C, dtype=torch.float32, device=x.device)
-            dbias = dbias_out if dbias_out is not None else torch.empty(C, dtype=torch.float32, device=x.device)
+            dscale = dscale_out if dscale_out is not None else _NA.empty(C, dtype=torch.float32, device=x.device)
+            dbias = dbias_out if dbias_out is not None else _NA.empty(C, dtype=torch.float32, device=x.device)
             ws = _ws(M, C, is_bf16(x), x.device)
             if mask is not None:
                 assert relu and mask.dtype == torch.uint8 and mask.numel() == relu_mask_bytes(x)
@@ -195,7 +196,7 @@ def bn_backward(dy, y, x, scale, save_mean, save_invstd, relu=False, want_dres=F
     shape = [1, C] + [1] * (x.dim() - 2)
     g = dy.float()
     if relu:
-        g = torch.where(y > 0, g, torch.zeros_like(g))
+        g = torch.where(y > 0, g, _NA.zeros_like(g))
     xhat = (x.float() - save_mean.view(shape)) * save_invstd.view(shape)
     M = x.numel() // C
     dbias = g.sum(dims)

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32, F32
 
@@ -15,8 +16,8 @@ def reduce_mid(x3: torch.Tensor, scale: float = 1.0, out_dtype=None, out=None) -
     if native(x3) and supported_float(x3) and out_dtype in (torch.float32, torch.bfloat16):
         x3 = x3.contiguous()
         wsf = fn('hetu_reduce_mid_ws', [I64, I64, I64], restype=I64)
-        ws = torch.empty(wsf(B, R, C), dtype=torch.float32, device=x3.device)
-        y = out if out is not None else torch.empty((B, C), dtype=out_dtype, device=x3.device)
+        ws = _NA.empty(wsf(B, R, C), dtype=torch.float32, device=x3.device)
+        y = out if out is not None else _NA.empty((B, C), dtype=out_dtype, device=x3.device)
         f = fn('hetu_reduce_mid', [P, P, I64, I64, I64, F32, I32, I32, P, P])
         check(f(x3.data_ptr(), y.data_ptr(), B, R, C, float(scale), is_bf16(x3),
                 1 if out_dtype == torch.bfloat16 else 0, ws.data_ptr(), stream_ptr()), 'reduce_mid')
@@ -30,7 +31,7 @@ def reduce_mid(x3: torch.Tensor, scale: float = 1.0, out_dtype=None, out=None) -
         else:
             y = torch.stack([cpu_native.reduce_axis0(x3[b], scale) for b in range(B)]) if B <= 16 else None
             if y is None:   # many short reductions: sum over R of each [C] row block via a permute
-                xt = torch.empty((R, B, C), dtype=torch.float32)
+                xt = _NA.empty((R, B, C), dtype=torch.float32)
                 cpu_native.copy_nd(x3.permute(1, 0, 2), xt)
                 y = cpu_native.reduce_axis0(xt.reshape(R, B * C), scale).reshape(B, C)
         if out is not None:
@@ -50,7 +51,7 @@ def reduce_last(x2: torch.Tensor, scale: float = 1.0, out_dtype=None) -> torch.T
     out_dtype = out_dtype or x2.dtype
     if native(x2) and supported_float(x2) and out_dtype in (torch.float32, torch.bfloat16):
         x2 = x2.contiguous()
-        y = torch.empty((R,), dtype=out_dtype, device=x2.device)
+        y = _NA.empty((R,), dtype=out_dtype, device=x2.device)
         f = fn('hetu_reduce_last', [P, P, I64, I64, F32, I32, I32, P])
         check(f(x2.data_ptr(), y.data_ptr(), R, C, float(scale), is_bf16(x2),
                 1 if out_dtype == torch.bfloat16 else 0, stream_ptr()), 'reduce_last')
@@ -124,7 +125,7 @@ def global_avg_pool_backward(dy: torch.Tensor, x_shape) -> torch.Tensor:
     N, C, H, W = x_shape
     if native(dy) and supported_float(dy):
         dy = dy.contiguous()
-        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device,
+        dx = _NA.empty((N, C, H, W), dtype=dy.dtype, device=dy.device,
                          memory_format=torch.channels_last)
         f = fn('hetu_bcast_mid', [P, P, I64, I64, I64, F32, I32, P])
         check(f(dy.data_ptr(), dx.data_ptr(), N, H * W, C, 1.0 / (H * W), is_bf16(dy),
@@ -132,7 +133,7 @@ def global_avg_pool_backward(dy: torch.Tensor, x_shape) -> torch.Tensor:
         return dx
     from . import cpu_native
     if cpu_native.active(dy):
-        dx = torch.empty((N, C, H, W), dtype=torch.float32)
+        dx = _NA.empty((N, C, H, W), dtype=torch.float32)
         cpu_native.copy_nd(dy.reshape(N, C, 1, 1).expand(N, C, H, W), dx)
         return cpu_native.unary_code(15, dx, 1.0 / (H * W), out=dx)
     return (dy.reshape(N, C, 1, 1).float() / (H * W)).expand(N, C, H, W).to(dy.dtype).contiguous()

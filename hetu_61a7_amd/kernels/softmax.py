@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32
 
@@ -14,7 +15,7 @@ def softmax(x: torch.Tensor, log: bool = False) -> torch.Tensor:
     """Softmax over the last dim."""
     if native(x) and supported_float(x):
         x = x.contiguous()
-        y = torch.empty_like(x)
+        y = _NA.empty_like(x)
         R, N = x.numel() // x.shape[-1], x.shape[-1]
         f = fn('hetu_softmax_fwd', [P, P, I64, I32, I32, I32, P])
         check(f(x.data_ptr(), y.data_ptr(), R, N, is_bf16(x), int(log), stream_ptr()), 'softmax')
@@ -31,7 +32,7 @@ def softmax_backward(y: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
     if native(y) and supported_float(y) and dy.dtype == y.dtype:
         y = y.contiguous()
         dy = dy.contiguous()
-        dx = torch.empty_like(y)
+        dx = _NA.empty_like(y)
         R, N = y.numel() // y.shape[-1], y.shape[-1]
         f = fn('hetu_softmax_bwd', [P, P, P, I64, I32, I32, P])
         check(f(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), R, N, is_bf16(y), stream_ptr()), 'softmax_bwd')
@@ -50,8 +51,8 @@ def softmax_ce(logits: torch.Tensor, labels: torch.Tensor):
         x = logits.contiguous()
         lab = labels.contiguous()
         R, N = x.numel() // x.shape[-1], x.shape[-1]
-        loss = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
-        lse = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+        loss = _NA.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+        lse = _NA.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
         f = fn('hetu_softmax_ce_fwd', [P, P, P, P, I64, I32, I32, I32, P])
         check(f(x.data_ptr(), lab.data_ptr(), loss.data_ptr(), lse.data_ptr(), R, N,
                 is_bf16(x), is_bf16(lab), stream_ptr()), 'softmax_ce')
@@ -85,7 +86,7 @@ def softmax_ce_backward(logits, labels, grad, lse=None):
         lab = labels.contiguous()
         g, scalar = _grad_rows(grad)
         R, N = x.numel() // x.shape[-1], x.shape[-1]
-        dx = torch.empty_like(x)
+        dx = _NA.empty_like(x)
         f = fn('hetu_softmax_ce_bwd', [P, P, P, I32, P, P, I64, I32, I32, I32, P])
         check(f(x.data_ptr(), lab.data_ptr(), g.data_ptr(), int(scalar),
                 lse.contiguous().data_ptr() if lse is not None else None, dx.data_ptr(), R, N,
@@ -114,8 +115,8 @@ def softmax_ce_sparse(logits, labels, ignored_index=-1):
         x = logits.contiguous()
         lab = lab.contiguous()
         R, N = x.numel() // x.shape[-1], x.shape[-1]
-        loss = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
-        lse = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+        loss = _NA.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+        lse = _NA.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
         f = fn('hetu_softmax_ce_sparse_fwd', [P, P, P, P, I64, I32, I32, I64, P])
         check(f(x.data_ptr(), lab.data_ptr(), loss.data_ptr(), lse.data_ptr(), R, N, is_bf16(x),
                 int(ignored_index), stream_ptr()), 'softmax_ce_sparse')
@@ -126,9 +127,9 @@ def softmax_ce_sparse(logits, labels, ignored_index=-1):
     xf = _rows(logits.float())
     lse = torch.logsumexp(xf, -1)
     valid = (lab != ignored_index) & (lab >= 0) & (lab < xf.shape[-1])
-    safe = torch.where(valid, lab, torch.zeros_like(lab))
+    safe = torch.where(valid, lab, _NA.zeros_like(lab))
     picked = xf.gather(1, safe.unsqueeze(1)).squeeze(1)
-    loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
+    loss = torch.where(valid, lse - picked, _NA.zeros_like(lse))
     return loss.reshape(logits.shape[:-1]), lse.reshape(logits.shape[:-1])
 
 
@@ -139,7 +140,7 @@ def softmax_ce_sparse_backward(logits, labels, grad, lse=None, ignored_index=-1)
     if native(logits) and supported_float(logits):
         x = logits.contiguous()
         R, N = x.numel() // x.shape[-1], x.shape[-1]
-        dx = torch.empty_like(x)
+        dx = _NA.empty_like(x)
         g, scalar = _grad_rows(grad)
         f = fn('hetu_softmax_ce_sparse_bwd', [P, P, P, I32, P, P, I64, I32, I32, I64, P])
         check(f(x.data_ptr(), lab.contiguous().data_ptr(), g.data_ptr(), int(scalar),
@@ -156,7 +157,7 @@ def softmax_ce_sparse_backward(logits, labels, grad, lse=None, ignored_index=-1)
     xf = _rows(logits.float())
     sm = torch.softmax(xf, -1)
     valid = (lab != ignored_index) & (lab >= 0) & (lab < xf.shape[-1])
-    safe = torch.where(valid, lab, torch.zeros_like(lab))
+    safe = torch.where(valid, lab, _NA.zeros_like(lab))
     onehot = torch.nn.functional.one_hot(safe, xf.shape[-1]).float()
     g = grad.reshape(-1, 1) if grad.numel() > 1 else grad
     d = g * (sm - onehot) * valid.float().unsqueeze(1)

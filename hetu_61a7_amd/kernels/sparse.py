@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I32
 
@@ -13,13 +14,13 @@ def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     out_shape = tuple(ids.shape) + (dim,)
     if native(table) and supported_float(table) and table.is_contiguous():
         idx = idx.contiguous()
-        out = torch.empty(out_shape, dtype=table.dtype, device=table.device)
+        out = _NA.empty(out_shape, dtype=table.dtype, device=table.device)
         f = fn('hetu_gather_rows', [P, P, P, I64, I64, I64, I32, P])
         check(f(table.data_ptr(), idx.data_ptr(), out.data_ptr(), idx.numel(), dim,
                 table.shape[0], is_bf16(table), stream_ptr()), 'gather_rows')
         return out
     valid = (idx >= 0) & (idx < table.shape[0])
-    safe = torch.where(valid, idx, torch.zeros_like(idx))
+    safe = torch.where(valid, idx, _NA.zeros_like(idx))
     out = table[safe] * valid.unsqueeze(1).to(table.dtype)
     return out.reshape(out_shape)
 
@@ -37,7 +38,7 @@ def scatter_add_rows(dst: torch.Tensor, ids: torch.Tensor, src: torch.Tensor) ->
         src2 = src2.contiguous()
         sidx, perm = torch.sort(idx, stable=True)
         seg_row, counts = torch.unique_consecutive(sidx, return_counts=True)
-        off = torch.zeros(seg_row.numel() + 1, dtype=torch.int64, device=idx.device)
+        off = _NA.zeros(seg_row.numel() + 1, dtype=torch.int64, device=idx.device)
         torch.cumsum(counts, 0, out=off[1:])
         f = fn('hetu_segment_sum_rows', [P, P, P, P, P, I64, I64, I64, I32, P])
         check(f(dst.data_ptr(), seg_row.data_ptr(), off.data_ptr(), perm.data_ptr(), src2.data_ptr(),
@@ -69,10 +70,10 @@ def dedup_rows(idx: torch.Tensor, vals: torch.Tensor):
     K = min(64, n // max(nu * 16, 1))
     if K > 1 and vals.is_cuda and not deterministic():
         rep = torch.arange(n, device=inv.device) % K
-        scratch = torch.zeros((K * nu, dim), dtype=torch.float32, device=vals.device)
+        scratch = _NA.zeros((K * nu, dim), dtype=torch.float32, device=vals.device)
         scatter_add_rows(scratch, inv.reshape(-1) + rep * nu, vals.reshape(n, dim))
         return uniq, scratch.view(K, nu, dim).sum(0)
-    merged = torch.zeros((nu, dim), dtype=torch.float32, device=vals.device)
+    merged = _NA.zeros((nu, dim), dtype=torch.float32, device=vals.device)
     scatter_add_rows(merged, inv, vals)
     return uniq, merged
 
@@ -95,8 +96,8 @@ def dedup_rows_dense(idx: torch.Tensor, vals: torch.Tensor, nrows: int):
         idx = idx.contiguous()
         scratch = zeros((K * nrows * dim,), torch.float32, vals.device)
         hit = zeros((nrows,), torch.int32, vals.device)
-        merged = torch.empty((nrows, dim), dtype=torch.float32, device=vals.device)
-        ids = torch.empty((nrows,), dtype=torch.int64, device=vals.device)
+        merged = _NA.empty((nrows, dim), dtype=torch.float32, device=vals.device)
+        ids = _NA.empty((nrows,), dtype=torch.int64, device=vals.device)
         f = fn('hetu_dedup_rows_dense', [P, P, I32, I64, I64, I64, I32, P, P, P, P, P])
         check(f(idx.data_ptr(), v2.data_ptr(), is_bf16(v2), n, dim, nrows, K, scratch.data_ptr(), hit.data_ptr(),
                 merged.data_ptr(), ids.data_ptr(), stream_ptr()), 'dedup_rows_dense')
@@ -106,10 +107,10 @@ def dedup_rows_dense(idx: torch.Tensor, vals: torch.Tensor, nrows: int):
     valid = (idx >= 0) & (idx < nrows)
     tgt = idx if K == 1 else idx + (torch.arange(n, device=idx.device) % K) * nrows
     tgt = torch.where(valid, tgt, torch.full_like(tgt, -1))
-    scratch = torch.zeros((K * nrows, dim), dtype=torch.float32, device=vals.device)
+    scratch = _NA.zeros((K * nrows, dim), dtype=torch.float32, device=vals.device)
     scatter_add_rows(scratch, tgt, vals.reshape(n, dim))
     merged = scratch if K == 1 else scratch.view(K, nrows, dim).sum(0)
-    hit = torch.zeros(nrows + 1, dtype=torch.int64, device=idx.device)
+    hit = _NA.zeros(nrows + 1, dtype=torch.int64, device=idx.device)
     hit.scatter_(0, torch.where(valid, idx, torch.full_like(idx, nrows)), 1)
     rows = torch.arange(nrows, device=idx.device)
     ids = torch.where(hit[:nrows] > 0, rows, torch.full_like(rows, -1))

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+from .. import native_array as _NA
 
 from . import native, fn, stream_ptr, check, is_bf16, P, I32, I64, F32
 
@@ -81,7 +82,7 @@ def csrmm(a, b, trans_A=False, trans_B=False, col_window=None, out=None, accumul
         return out
     csr = _torch_csr(A)
     if col_window is not None:
-        dense_rows = torch.zeros((A.ncol, N), dtype=torch.float32)
+        dense_rows = _NA.zeros((A.ncol, N), dtype=torch.float32)
         dense_rows[c0:c1] = B.float()[:c1 - c0]
         r = torch.sparse.mm(csr.to_sparse_coo(), dense_rows)
     else:
@@ -105,7 +106,7 @@ def csrmv(a, x, trans=False):
     A = transposed(a) if trans else a
     if native(x) and x.dtype in (torch.float32, torch.bfloat16):
         xc = x.contiguous()
-        y = torch.empty(A.nrow, dtype=x.dtype, device=x.device)
+        y = _NA.empty(A.nrow, dtype=x.dtype, device=x.device)
         rp, ci, v = _dev_parts(A, x.device)
         f = fn('hetu_csrmv', [P, P, P, P, P, I32, I32, P])
         check(f(rp.data_ptr(), ci.data_ptr(), v.data_ptr(), xc.data_ptr(), y.data_ptr(), A.nrow,

@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 
 import torch
+from .. import native_array as _NA
 
 from . import fn, check, stream_ptr, P, I32, I64, F32, record_native
 
@@ -91,7 +92,7 @@ def fill_(t, value):
 
 def zeros(shape, dtype=torch.float32, device='cuda'):
     """zero-filled device tensor by the native fill kernel (no torch fill launch)"""
-    t = torch.empty(shape, dtype=dtype, device=device)
+    t = _NA.empty(shape, dtype=dtype, device=device)
     if t.is_cuda and t.numel():
         f = fn('hetu_fill', [P, I32, I64, ctypes.c_uint64, P])
         check(f(t.data_ptr(), _ELEM[t.dtype], t.numel(), 0, stream_ptr()), 'fill')
@@ -120,7 +121,7 @@ def copy_into(dst, src):
         record_native('cast')
         return dst
     if {dst.dtype, src.dtype} == {torch.float32, torch.bfloat16} and _dense(src):
-        tmp = torch.empty_like(src, dtype=dst.dtype)       # src's dense layout
+        tmp = _NA.empty_like(src, dtype=dst.dtype)       # src's dense layout
         copy_into(tmp, src)
         return nd_copy(tmp, dst)
     from . import record_fallback
@@ -133,7 +134,7 @@ def concat(tensors, axis):
     shape = list(tensors[0].shape)
     axis = axis % len(shape)
     shape[axis] = sum(int(t.shape[axis]) for t in tensors)
-    out = torch.empty(shape, dtype=dt, device=tensors[0].device)
+    out = _NA.empty(shape, dtype=dt, device=tensors[0].device)
     off = 0
     for t in tensors:
         n = int(t.shape[axis])
@@ -146,7 +147,7 @@ def concat(tensors, axis):
 def pad_constant(x, pads, value):
     """pads: [(before, after)] per dim (all dims)."""
     shape = [int(s) + a + b for s, (a, b) in zip(x.shape, pads)]
-    out = torch.empty(shape, dtype=x.dtype, device=x.device)
+    out = _NA.empty(shape, dtype=x.dtype, device=x.device)
     fill_(out, value)
     view = out
     for d, (a, _) in enumerate(pads):
@@ -160,12 +161,12 @@ def unpad(g, pads):
     view = g
     for d, (a, b) in enumerate(pads):
         view = view.narrow(d, a, int(g.shape[d]) - a - b)
-    out = torch.empty(view.shape, dtype=g.dtype, device=g.device)
+    out = _NA.empty(view.shape, dtype=g.dtype, device=g.device)
     return nd_copy(view, out)
 
 
 def roll(x, shifts, dims):
-    out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    out = _NA.empty(x.shape, dtype=x.dtype, device=x.device)
     sh = [0] * x.dim()
     md = [0] * x.dim()
     for s, d in zip(shifts, dims):
@@ -182,7 +183,7 @@ def repeat(x, reps):
     reps = list(reps)
     xs = [1] * (len(reps) - x.dim()) + list(x.shape)
     xv = x.reshape(xs)
-    out = torch.empty([a * b for a, b in zip(xs, reps)], dtype=x.dtype, device=x.device)
+    out = _NA.empty([a * b for a, b in zip(xs, reps)], dtype=x.dtype, device=x.device)
     if not x.is_cuda:   # out viewed as [r0, s0, r1, s1, ...] = x broadcast over the r axes
         inter, src = [], []
         for r, n in zip(reps, xs):
@@ -202,7 +203,7 @@ def gather(x, dim, idx):
     oi, nidx, ii = _dims(idx.shape, dim)
     if oi != outer or ii != inner:
         raise ValueError('gather: index must match the input outside dim')
-    out = torch.empty(idx.shape, dtype=x.dtype, device=x.device)
+    out = _NA.empty(idx.shape, dtype=x.dtype, device=x.device)
     f = fn('hetu_gather_dim', [P, P, P, I64, I64, I64, I64, I32, P])
     check(f(x.data_ptr(), idx.data_ptr(), out.data_ptr(), outer, nidx, nsrc, inner, _bf(x), stream_ptr()), 'gather')
     record_native('gather')
@@ -216,7 +217,7 @@ def scatter_add(g, dim, idx, shape):
     dim = dim % len(shape)
     outer, nsrc, inner = _dims(shape, dim)
     _, nidx, _ = _dims(idx.shape, dim)
-    dx = torch.zeros(shape, dtype=torch.float32, device=g.device)
+    dx = _NA.zeros(shape, dtype=torch.float32, device=g.device)
     f = fn('hetu_scatter_add_dim', [P, P, P, I64, I64, I64, I64, I32, P])
     check(f(g.data_ptr(), idx.data_ptr(), dx.data_ptr(), outer, nidx, nsrc, inner, _bf(g), stream_ptr()),
           'scatter_add')
@@ -228,7 +229,7 @@ def scatter_add(g, dim, idx, shape):
 def cumsum(x, dim, bias=0.0):
     x = x.contiguous()
     outer, n, inner = _dims(x.shape, dim)
-    y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    y = _NA.empty(x.shape, dtype=torch.float32, device=x.device)
     f = fn('hetu_scan_dim', [P, P, I64, I64, I64, F32, I32, P])
     check(f(x.data_ptr(), y.data_ptr(), outer, n, inner, float(bias), _bf(x), stream_ptr()), 'scan')
     record_native('cumsum')
@@ -241,7 +242,7 @@ def argmax(x, dim):
     outer, n, inner = _dims(x.shape, dim)
     shape = list(x.shape)
     shape.pop(dim)
-    out = torch.empty(shape, dtype=torch.int64, device=x.device)
+    out = _NA.empty(shape, dtype=torch.int64, device=x.device)
     f = fn('hetu_argmax_dim', [P, P, I64, I64, I64, I32, P])
     check(f(x.data_ptr(), out.data_ptr(), outer, n, inner, _bf(x), stream_ptr()), 'argmax')
     record_native('argmax')
@@ -259,7 +260,7 @@ def argsort(x, dim=-1, descending=False):
     if n > ARGSORT_MAX:
         return None
     rows = xt.numel() // max(n, 1)
-    out = torch.empty(xt.shape, dtype=torch.int64, device=x.device)
+    out = _NA.empty(xt.shape, dtype=torch.int64, device=x.device)
     f = fn('hetu_argsort_rows', [P, P, I64, I64, I32, I32, P])
     check(f(xt.data_ptr(), out.data_ptr(), rows, n, int(bool(descending)), _bf(xt), stream_ptr()), 'argsort')
     record_native('argsort')
@@ -272,7 +273,7 @@ def pnorm(x, dim, p=2.0, keepdim=True):
     outer, n, inner = _dims(x.shape, dim)
     shape = list(x.shape)
     shape[dim] = 1
-    y = torch.empty(shape, dtype=x.dtype, device=x.device)
+    y = _NA.empty(shape, dtype=x.dtype, device=x.device)
     f = fn('hetu_pnorm_dim', [P, P, I64, I64, I64, F32, I32, P])
     check(f(x.data_ptr(), y.data_ptr(), outer, n, inner, float(p), _bf(x), stream_ptr()), 'pnorm')
     record_native('norm')
@@ -286,7 +287,7 @@ def pnorm_grad(x, y, g, dim, p=2.0):
     outer, n, inner = _dims(x.shape, dim)
     y = y.to(x.dtype).contiguous()
     g = g.to(x.dtype).contiguous()
-    dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    dx = _NA.empty(x.shape, dtype=x.dtype, device=x.device)
     f = fn('hetu_pnorm_grad_dim', [P, P, P, P, I64, I64, I64, F32, I32, P])
     check(f(x.data_ptr(), y.data_ptr(), g.data_ptr(), dx.data_ptr(), outer, n, inner, float(p), _bf(x),
             stream_ptr()), 'pnorm_grad')
@@ -308,7 +309,7 @@ def _g(g, rows):
 def ce_dense(y, lab):
     y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
     rows, cols = _rows(y)
-    out = torch.empty(y.shape[:-1], dtype=torch.float32, device=y.device)
+    out = _NA.empty(y.shape[:-1], dtype=torch.float32, device=y.device)
     check(fn('hetu_ce_dense', [P, P, P, I64, I64, I32, P])(y.data_ptr(), lab.data_ptr(), out.data_ptr(), rows,
                                                             cols, _bf(y), stream_ptr()), 'ce_dense')
     record_native('crossentropy')
@@ -319,7 +320,7 @@ def ce_dense_grad(g, y, lab):
     y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
     rows, cols = _rows(y)
     g, gs = _g(g, rows)
-    dy = torch.empty(y.shape, dtype=y.dtype, device=y.device)
+    dy = _NA.empty(y.shape, dtype=y.dtype, device=y.device)
     check(fn('hetu_ce_dense_grad', [P, P, P, P, I64, I64, I32, I32, P])(
         g.data_ptr(), y.data_ptr(), lab.data_ptr(), dy.data_ptr(), rows, cols, gs, _bf(y), stream_ptr()),
         'ce_dense_grad')
@@ -330,7 +331,7 @@ def ce_sparse(y, lab, ignore=-1):
     y = y.contiguous()
     rows, cols = _rows(y)
     lab = lab.long().reshape(-1).contiguous()
-    out = torch.empty(y.shape[:-1], dtype=torch.float32, device=y.device)
+    out = _NA.empty(y.shape[:-1], dtype=torch.float32, device=y.device)
     check(fn('hetu_ce_sparse', [P, P, P, I64, I64, I64, I32, P])(y.data_ptr(), lab.data_ptr(), out.data_ptr(),
                                                                   rows, cols, int(ignore), _bf(y), stream_ptr()),
           'ce_sparse')
@@ -343,7 +344,7 @@ def ce_sparse_grad(g, y, lab, ignore=-1):
     rows, cols = _rows(y)
     lab = lab.long().reshape(-1).contiguous()
     g, gs = _g(g, rows)
-    dy = torch.empty(y.shape, dtype=y.dtype, device=y.device)
+    dy = _NA.empty(y.shape, dtype=y.dtype, device=y.device)
     check(fn('hetu_ce_sparse_grad', [P, P, P, P, I64, I64, I64, I32, I32, P])(
         g.data_ptr(), y.data_ptr(), lab.data_ptr(), dy.data_ptr(), rows, cols, int(ignore), gs, _bf(y),
         stream_ptr()), 'ce_sparse_grad')
@@ -352,7 +353,7 @@ def ce_sparse_grad(g, y, lab, ignore=-1):
 
 def bce(y, lab):
     y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
-    out = torch.empty(y.shape, dtype=torch.float32, device=y.device)
+    out = _NA.empty(y.shape, dtype=torch.float32, device=y.device)
     check(fn('hetu_bce', [P, P, P, I64, I32, P])(y.data_ptr(), lab.data_ptr(), out.data_ptr(), y.numel(), _bf(y),
                                                   stream_ptr()), 'bce')
     record_native('bce')
@@ -363,7 +364,7 @@ def bce_grad(y, lab, g):
     y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
     g = g.float().expand(y.shape).contiguous() if g.numel() not in (1, y.numel()) else g.float().contiguous()
     gs = int(g.numel() == 1 and y.numel() != 1)
-    dy = torch.empty(y.shape, dtype=y.dtype, device=y.device)
+    dy = _NA.empty(y.shape, dtype=y.dtype, device=y.device)
     check(fn('hetu_bce_grad', [P, P, P, P, I64, I32, I32, P])(y.data_ptr(), lab.data_ptr(), g.data_ptr(),
                                                                dy.data_ptr(), y.numel(), gs, _bf(y), stream_ptr()),
           'bce_grad')
@@ -397,7 +398,7 @@ def nll_grad(g, t, cols):
     g = g.reshape(-1)[:1]
     if g.dtype != torch.float32:
         g = g.float()
-    dx = torch.empty((t.numel(), cols), dtype=torch.float32, device=t.device)
+    dx = _NA.empty((t.numel(), cols), dtype=torch.float32, device=t.device)
     check(fn('hetu_nll_grad', [P, P, I32, P, I64, I64, P])(g.data_ptr(), t.data_ptr(), tk, dx.data_ptr(), t.numel(),
                                                             cols, stream_ptr()), 'nll_grad')
     record_native('nll_grad')
@@ -412,7 +413,7 @@ def _i64(t):
 def sam_group_sum(x, G):
     x = x.float().contiguous()
     T, E = x.shape
-    out = torch.empty((T, G), dtype=torch.float32, device=x.device)
+    out = _NA.empty((T, G), dtype=torch.float32, device=x.device)
     check(fn('hetu_sam_group_sum', [P, P, I64, I32, I32, P])(x.data_ptr(), out.data_ptr(), T, E, G, stream_ptr()),
           'sam_group_sum')
     record_native('sam_group_sum')
@@ -421,7 +422,7 @@ def sam_group_sum(x, G):
 
 def sam_group_sum_grad(g, T, E, G):
     g = g.float().contiguous()
-    dx = torch.empty((T, E), dtype=torch.float32, device=g.device)
+    dx = _NA.empty((T, E), dtype=torch.float32, device=g.device)
     check(fn('hetu_sam_group_sum_grad', [P, P, I64, I32, I32, P])(g.data_ptr(), dx.data_ptr(), T, E, G,
                                                                    stream_ptr()), 'sam_group_sum_grad')
     record_native('sam_group_sum_grad')
@@ -432,7 +433,7 @@ def sam_max(x, grp, tk, n):
     x = x.float().contiguous()
     T, E = x.shape
     grp, tk = _i64(grp), _i64(tk)
-    y = torch.empty((T, E), dtype=torch.float32, device=x.device)
+    y = _NA.empty((T, E), dtype=torch.float32, device=x.device)
     check(fn('hetu_sam_max', [P, P, P, P, I64, I32, I32, P])(x.data_ptr(), grp.data_ptr(), tk.data_ptr(),
                                                              y.data_ptr(), T, E, n, stream_ptr()), 'sam_max')
     record_native('sam_max')
@@ -443,7 +444,7 @@ def sam_max_grad(g, x, grp, tk, n):
     x, g = x.float().contiguous(), g.float().contiguous()
     T, E = x.shape
     grp, tk = _i64(grp), _i64(tk)
-    dx = torch.empty((T, E), dtype=torch.float32, device=x.device)
+    dx = _NA.empty((T, E), dtype=torch.float32, device=x.device)
     check(fn('hetu_sam_max_grad', [P, P, P, P, P, I64, I32, I32, P])(
         g.data_ptr(), x.data_ptr(), grp.data_ptr(), tk.data_ptr(), dx.data_ptr(), T, E, n, stream_ptr()),
         'sam_max_grad')
@@ -462,7 +463,7 @@ def group_topk_idx(x, grp, k, n):
     x = x.float().contiguous()
     T, E = x.shape
     grp = _i64(grp)
-    out = torch.empty((T, k), dtype=torch.int64, device=x.device)
+    out = _NA.empty((T, k), dtype=torch.int64, device=x.device)
     check(fn('hetu_group_topk_idx', [P, P, P, I64, I32, I32, I32, P])(
         x.data_ptr(), grp.data_ptr(), out.data_ptr(), T, E, n, k, stream_ptr()), 'group_topk_idx')
     record_native('group_topk_idx')
@@ -481,13 +482,13 @@ def instance_norm2d(x, eps):
     """x logical NCHW fp32/bf16 (NCHW or channels-last) -> (y, mean, rstd), stats [N, C, 1, 1] fp32."""
     x, (sN, sC, sP) = _plane_view(x)
     N, C, H, W = x.shape
-    y = torch.empty_like(x)
+    y = _NA.empty_like(x)
     if y.stride() != x.stride():
         x = x.contiguous()
-        y = torch.empty_like(x)
+        y = _NA.empty_like(x)
         sN, sC, sP = x.stride(0), x.stride(1), x.stride(3)
-    mean = torch.empty((N, C, 1, 1), dtype=torch.float32, device=x.device)
-    rstd = torch.empty_like(mean)
+    mean = _NA.empty((N, C, 1, 1), dtype=torch.float32, device=x.device)
+    rstd = _NA.empty_like(mean)
     check(fn('hetu_instance_norm2d', [P, P, P, P, I32, I32, I64, I64, I64, I64, F32, I32, P])(
         x.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), N, C, H * W, sN, sC, sP, float(eps), _bf(x),
         stream_ptr()), 'instance_norm2d')
@@ -499,11 +500,11 @@ def instance_norm2d_grad(g, x, mean, rstd):
     x, (sN, sC, sP) = _plane_view(x)
     g = g.to(x.dtype)
     if g.stride() != x.stride():
-        g = torch.empty_like(x).copy_(g)
-    dx = torch.empty_like(x)
+        g = _NA.empty_like(x).copy_(g)
+    dx = _NA.empty_like(x)
     if dx.stride() != x.stride():
         x = x.contiguous()
-        g, dx = g.contiguous(), torch.empty_like(x)
+        g, dx = g.contiguous(), _NA.empty_like(x)
         sN, sC, sP = x.stride(0), x.stride(1), x.stride(3)
     N, C, H, W = x.shape
     mean, rstd = mean.float().contiguous(), rstd.float().contiguous()
@@ -526,7 +527,7 @@ def bicubic(x, OH, OW, align_corners=False, scale_factor=None):
     """PyTorch-compatible bicubic upsampling (A = -0.75, border clamp), fp32 math."""
     N, C, H, W = x.shape
     xf = x.float().contiguous()
-    y = torch.empty((N, C, OH, OW), dtype=torch.float32, device=x.device)
+    y = _NA.empty((N, C, OH, OW), dtype=torch.float32, device=x.device)
     sh = _cubic_scale(H, OH, align_corners, scale_factor)
     sw = _cubic_scale(W, OW, align_corners, scale_factor)
     check(fn('hetu_bicubic', [P, P, I64, I32, I32, I32, I32, F32, F32, I32, P])(
@@ -539,7 +540,7 @@ def bicubic_grad(g, shape, align_corners=False, scale_factor=None):
     N, C, H, W = (int(s) for s in shape)
     OH, OW = int(g.shape[2]), int(g.shape[3])
     gf = g.float().contiguous()
-    dx = torch.zeros((N, C, H, W), dtype=torch.float32, device=g.device)
+    dx = _NA.zeros((N, C, H, W), dtype=torch.float32, device=g.device)
     sh = _cubic_scale(H, OH, align_corners, scale_factor)
     sw = _cubic_scale(W, OW, align_corners, scale_factor)
     check(fn('hetu_bicubic_grad', [P, P, I64, I32, I32, I32, I32, F32, F32, I32, P])(

@@ -19,6 +19,7 @@ from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import torch
+from . import native_array as _NA
 
 _HOSTNAME = socket.gethostname()
 
@@ -139,13 +140,26 @@ def ctx_of(t: torch.Tensor) -> DLContext:
 
 
 class NDArray(object):
-    """Handle over a device/host tensor (reference ``ndarray.py:140``)."""
+    """An array of the framework (reference ``ndarray.py:140``): a native strided array
+    header (``native_array.Array``, the C ABI of ``csrc/runtime/array.cc``) plus its torch
+    view for the kernel wrappers.  Arrays made by ``array`` / ``empty`` own framework
+    memory; an NDArray wrapped around a tensor from elsewhere borrows it (the native
+    header is created on first use of ``handle``)."""
 
-    __slots__ = ('tensor', 'ctx')
+    __slots__ = ('tensor', 'ctx', '_handle')
 
-    def __init__(self, tensor: torch.Tensor, ctx: Optional[DLContext] = None):
+    def __init__(self, tensor: torch.Tensor, ctx: Optional[DLContext] = None, handle=None):
         self.tensor = tensor
         self.ctx = ctx if ctx is not None else ctx_of(tensor)
+        self._handle = handle
+
+    @property
+    def handle(self):
+        """the native array header (DLPack-borrowed from the tensor when not framework-made)"""
+        if self._handle is None:
+            from .native_array import Array
+            self._handle = Array.from_torch(self.tensor)
+        return self._handle
 
     # shape / metadata -------------------------------------------------
     @property
@@ -212,18 +226,26 @@ class NDArray(object):
 
     # zero-copy views (reference ndarray.py:298-381) ----------------------
     def reshape(self, shape, target=None):
-        v = self.tensor.reshape(shape)
+        if self._handle is not None and self.tensor.is_contiguous():
+            h = self._handle.reshape(tuple(shape))       # native zero-copy view
+            v = h.torch()
+        else:
+            h, v = None, self.tensor.reshape(shape)
         if target is not None:
-            target.tensor = v
+            target.tensor, target._handle = v, h
             return target
-        return NDArray(v, self.ctx)
+        return NDArray(v, self.ctx, h)
 
     def broadcast_to(self, shape, target=None):
-        v = self.tensor.expand(shape)
+        if self._handle is not None:
+            h = self._handle.broadcast_to(tuple(shape))   # stride-0 native view
+            v = h.torch()
+        else:
+            h, v = None, self.tensor.expand(shape)
         if target is not None:
-            target.tensor = v
+            target.tensor, target._handle = v, h
             return target
-        return NDArray(v, self.ctx)
+        return NDArray(v, self.ctx, h)
 
     def inplace_copy(self, target):
         target.tensor.copy_(self.tensor)
@@ -252,13 +274,22 @@ def array(arr, ctx: Optional[DLContext] = None, data_type=np.float32, dtype=None
         t = torch.from_numpy(np.ascontiguousarray(arr))
     if dtype is not None:
         t = t.to(to_torch_dtype(dtype))
-    return NDArray(t.to(ctx.torch_device), ctx)
+    out = empty(tuple(t.shape), ctx, t.dtype)      # framework memory, filled from the source
+    out.tensor.copy_(t)
+    return out
 
 
 def empty(shape, ctx: Optional[DLContext] = None, dtype=np.float32) -> NDArray:
+    """a new framework array (reference DLArrayAlloc): HBM from the device BFC pool, host
+    arrays pinned when a GPU is present (the reference's cudaMallocHost CPU arrays)"""
     ctx = ctx or cpu(0)
-    t = torch.empty(tuple(shape), dtype=to_torch_dtype(dtype), device=ctx.torch_device)
-    return NDArray(t, ctx)
+    dt = to_torch_dtype(dtype)
+    from . import native_array
+    dev = ctx.torch_device
+    if native_array.available() and native_array._device_ok(dev):
+        h = native_array.Array.empty(tuple(shape), dt, dev, pinned=dev.type == 'cpu' and torch.cuda.is_available())
+        return NDArray(h.torch(), ctx, h)
+    return NDArray(_NA.empty(tuple(shape), dtype=dt, device=dev), ctx)
 
 
 def numpyasdlarrayhandle(data: np.ndarray) -> NDArray:
@@ -273,8 +304,8 @@ def pinned_empty(shape, dtype=torch.float32) -> torch.Tensor:
         from . import memory_pool
         if memory_pool.available():
             return memory_pool.pinned_pool().tensor(tuple(shape), dtype)
-        return torch.empty(tuple(shape), dtype=dtype).pin_memory()
-    return torch.empty(tuple(shape), dtype=dtype)
+        return _NA.empty(tuple(shape), dtype=dtype).pin_memory()
+    return _NA.empty(tuple(shape), dtype=dtype)
 
 
 class ND_Sparse_Array(object):
@@ -373,16 +404,39 @@ class IndexedSlices(object):
         width = self.dense_shape[-1]
         vals = vals.reshape(-1, width)
         if out is None:
-            out = torch.zeros(self.dense_shape, dtype=vals.dtype, device=vals.device)
+            out = _NA.zeros(self.dense_shape, dtype=vals.dtype, device=vals.device)
+        elif out.is_cuda:
+            from .kernels.tensor import fill_
+            fill_(out, 0)
         else:
             out.zero_()
         ksparse.scatter_add_rows(out.view(-1, width), idx, vals)
         return out
 
     def merge(self, other: 'IndexedSlices') -> 'IndexedSlices':
-        i = torch.cat([self._t(self.indices).reshape(-1), self._t(other.indices).reshape(-1)])
+        """concatenated (indices, values) of two sparse gradients of one table (framework
+        arrays filled by the native strided copy: no torch.cat kernel)"""
+        a_i, b_i = self._t(self.indices).reshape(-1), self._t(other.indices).reshape(-1)
         w = self.dense_shape[-1]
-        v = torch.cat([self._t(self.values).reshape(-1, w), self._t(other.values).reshape(-1, w)])
+        a_v, b_v = self._t(self.values).reshape(-1, w), self._t(other.values).reshape(-1, w)
+        if b_i.dtype != a_i.dtype:
+            b_i = b_i.to(a_i.dtype)
+        if b_v.dtype != a_v.dtype:
+            b_v = b_v.to(a_v.dtype)
+        na, nb = a_i.numel(), b_i.numel()
+        i = _NA.empty(na + nb, dtype=a_i.dtype, device=a_i.device)
+        v = _NA.empty((na + nb, w), dtype=a_v.dtype, device=a_v.device)
+        if a_i.is_cuda:
+            from .kernels.tensor import copy_into
+            copy_into(i[:na], a_i)
+            copy_into(i[na:], b_i)
+            copy_into(v[:na], a_v)
+            copy_into(v[na:], b_v)
+        else:
+            i[:na].copy_(a_i)
+            i[na:].copy_(b_i)
+            v[:na].copy_(a_v)
+            v[na:].copy_(b_v)
         return IndexedSlices(i, v, self.dense_shape)
 
     def cpu(self):

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+from .. import native_array as _NA
 
 from .node import Op
 from ..kernels import elementwise as K
@@ -875,7 +876,7 @@ class OnesLikeOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         from ..kernels.tensor import fill_
-        return fill_(torch.empty(tuple(input_vals[0]), dtype=torch.float32, device=self.device), 1.0)
+        return fill_(_NA.empty(tuple(input_vals[0]), dtype=torch.float32, device=self.device), 1.0)
 
     def gradient(self, output_grad):
         return [None]
@@ -894,7 +895,7 @@ class ZerosLikeOp(Op):
         if self.device.type == 'cuda':
             from ..kernels.tensor import zeros
             return zeros(tuple(input_vals[0]), torch.float32, self.device)
-        return torch.zeros(tuple(input_vals[0]), dtype=torch.float32, device=self.device)
+        return _NA.zeros(tuple(input_vals[0]), dtype=torch.float32, device=self.device)
 
     def gradient(self, output_grad):
         return [None]

@@ -12,6 +12,7 @@ user-visible primitives.
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from .node import Op
 from .. import ndarray
@@ -36,8 +37,8 @@ class AllReduceCommunicateOp(Op):
         if isinstance(v, ndarray.IndexedSlices):
             idx = v._t(v.indices).reshape(-1).contiguous()
             val = v._t(v.values).reshape(idx.numel(), -1).contiguous()
-            oi = torch.empty((idx.numel() * comm.nrank,), dtype=idx.dtype, device=idx.device)
-            ov = torch.empty((val.shape[0] * comm.nrank, val.shape[1]), dtype=val.dtype, device=val.device)
+            oi = _NA.empty((idx.numel() * comm.nrank,), dtype=idx.dtype, device=idx.device)
+            ov = _NA.empty((val.shape[0] * comm.nrank, val.shape[1]), dtype=val.dtype, device=val.device)
             comm.all_gather(oi, idx)
             comm.all_gather(ov, val)
             return ndarray.IndexedSlices(oi, ov, v.dense_shape)
@@ -73,7 +74,7 @@ class AllGatherCommunicateOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x = input_vals[0].contiguous()
         comm = _comm(self.comm)
-        out = torch.empty((x.shape[0] * comm.nrank,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        out = _NA.empty((x.shape[0] * comm.nrank,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
         comm.all_gather(out, x)
         return out
 
@@ -99,7 +100,7 @@ class ReduceScatterCommunicateOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x = input_vals[0].contiguous()
         comm = _comm(self.comm)
-        out = torch.empty((x.shape[0] // comm.nrank,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        out = _NA.empty((x.shape[0] // comm.nrank,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
         comm.reduce_scatter(out, x)
         return out
 
@@ -126,13 +127,13 @@ class BroadcastCommunicateOp(Op):
         comm = _comm(self.comm)
         x = input_vals[0]
         # shape header first (reference broadcasts the shape in infer_shape)
-        hdr = torch.zeros(8, dtype=torch.int64, device=x.device)
+        hdr = _NA.zeros(8, dtype=torch.int64, device=x.device)
         if comm.rank == self.root:
             hdr[0] = x.dim()
             hdr[1:1 + x.dim()] = torch.tensor(x.shape, dtype=torch.int64)
         comm.broadcast(hdr, self.root)
         shape = tuple(int(v) for v in hdr[1:1 + int(hdr[0])].tolist())
-        out = x.contiguous().clone() if comm.rank == self.root else torch.empty(shape, dtype=x.dtype, device=x.device)
+        out = x.contiguous().clone() if comm.rank == self.root else _NA.empty(shape, dtype=x.dtype, device=x.device)
         comm.broadcast(out, self.root)
         return out
 
@@ -181,7 +182,7 @@ class AllToAllOp(Op):
         x = input_vals[0].contiguous()
         if comm.nrank == 1:
             return x
-        out = torch.empty_like(x)
+        out = _NA.empty_like(x)
         comm.all_to_all(out, x)
         return out
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 import math
 
 import torch
+from .. import native_array as _NA
 
 from .node import Op
 from ..kernels import spmm as KSP
@@ -55,7 +56,7 @@ def broad_func(node_count, adj, inputs, rank, size, replication, row_groups, col
     rank_c, rank_col = rank // c, rank % c
     proc_rows = row_num(node_count, rank_c, size // c)
     feat = inputs.shape[1]
-    z = torch.zeros((proc_rows, feat), dtype=inputs.dtype, device=inputs.device)
+    z = _NA.zeros((proc_rows, feat), dtype=inputs.dtype, device=inputs.device)
     stages = size // (c * c)
     node_count_col = stages * n_per_proc
     if rank_col == c - 1:
@@ -71,7 +72,7 @@ def broad_func(node_count, adj, inputs, rank, size, replication, row_groups, col
         if q == rank:
             buf = inputs.contiguous().clone()
         else:
-            buf = torch.empty((rows_q, feat), dtype=inputs.dtype, device=inputs.device)
+            buf = _NA.empty((rows_q, feat), dtype=inputs.dtype, device=inputs.device)
         root = q // c if c > 1 else q  # group-local index of q inside its column group
         group.broadcast(buf, root)
         KSP.csrmm(adj, buf, col_window=(starts[i], ends[i]), out=z, accumulate=True)

@@ -9,6 +9,7 @@ operand is bf16 both are computed in bf16 with fp32 accumulation.
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from .. import ndarray
 from .node import Op
@@ -44,7 +45,7 @@ class MatMulOp(Op):
             if not (self.grad_dest is not None and y.data_ptr() == self.grad_dest.data_ptr()):
                 if y.is_cuda:
                     from ..kernels.tensor import copy_into
-                    y = copy_into(torch.empty(y.shape, dtype=torch.float32 if self.grad_dest is not None else y.dtype,
+                    y = copy_into(_NA.empty(y.shape, dtype=torch.float32 if self.grad_dest is not None else y.dtype,
                                               device=y.device), y)
                 else:
                     y = y.float() if self.grad_dest is not None else y.clone()

@@ -8,6 +8,7 @@ kernels; losses are produced in fp32 regardless of the logits dtype.
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from .node import Op
 from .nn import AuxResult
@@ -223,9 +224,9 @@ class CrossEntropySparseOp(Op):
             return KT.ce_sparse(y, lab, self.ignored_index)
         lab = lab.long().reshape(y.shape[:-1])
         valid = lab != self.ignored_index
-        safe = torch.where(valid, lab, torch.zeros_like(lab))
+        safe = torch.where(valid, lab, _NA.zeros_like(lab))
         p = torch.gather(y.float(), -1, safe.unsqueeze(-1)).squeeze(-1)
-        return torch.where(valid, -torch.log(p), torch.zeros_like(p))
+        return torch.where(valid, -torch.log(p), _NA.zeros_like(p))
 
     def gradient(self, output_grad):
         return [crossentropy_sparse_gradient_op(output_grad, self.inputs[0], self.inputs[1], self.ignored_index, ctx=self.raw_ctx), None]
@@ -245,11 +246,11 @@ class CrossEntropySparseGradientOp(Op):
             return KT.ce_sparse_grad(g, y, lab, self.ignored_index)
         lab = lab.long().reshape(y.shape[:-1])
         valid = lab != self.ignored_index
-        safe = torch.where(valid, lab, torch.zeros_like(lab))
-        out = torch.zeros(y.shape, dtype=torch.float32, device=y.device)
+        safe = torch.where(valid, lab, _NA.zeros_like(lab))
+        out = _NA.zeros(y.shape, dtype=torch.float32, device=y.device)
         p = torch.gather(y.float(), -1, safe.unsqueeze(-1)).squeeze(-1)
         gg = g.float() if g.numel() > 1 else g.float().expand(p.shape)
-        val = torch.where(valid, -gg / p, torch.zeros_like(p))
+        val = torch.where(valid, -gg / p, _NA.zeros_like(p))
         out.scatter_(-1, safe.unsqueeze(-1), val.unsqueeze(-1))
         return out.to(y.dtype)
 
@@ -348,7 +349,7 @@ class NllLossGradOp(Op):
         if _gpu(g):
             return KT.nll_grad(g, t, self.cols)
         t = t.long().reshape(-1)
-        out = torch.zeros((t.numel(), self.cols), dtype=torch.float32, device=t.device)
+        out = _NA.zeros((t.numel(), self.cols), dtype=torch.float32, device=t.device)
         out.scatter_(1, t.reshape(-1, 1), -(g.float().reshape(1, 1).expand(t.numel(), 1)) / t.numel())
         return out
 

@@ -10,6 +10,7 @@ no atomics on the forward combine.
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from .node import Op
 from ..kernels import moe as KM
@@ -287,7 +288,7 @@ class SamMaxOp(Op):
         if _gpu(x):
             return KT.sam_max(x, grp, tk, self.num_local_gpus)
         m, diff = _sam_mask(x, grp, tk, self.num_local_gpus)
-        return torch.where(m, diff, torch.zeros_like(diff))
+        return torch.where(m, diff, _NA.zeros_like(diff))
 
     def gradient(self, output_grad):
         return [sammax_grad_op(output_grad, self.inputs[0], self.inputs[1], self.inputs[2], self.num_local_gpus,
@@ -307,7 +308,7 @@ class SamMaxGradOp(Op):
         if _gpu(x):
             return KT.sam_max_grad(g, x, grp, tk, self.num_local_gpus)
         m, _ = _sam_mask(x, grp, tk, self.num_local_gpus)
-        gm = torch.where(m, g.float(), torch.zeros_like(g, dtype=torch.float32))
+        gm = torch.where(m, g.float(), _NA.zeros_like(g, dtype=torch.float32))
         out = gm.clone()
         out.scatter_add_(1, tk.reshape(-1, 1).long(), -gm.sum(1, keepdim=True))
         return out

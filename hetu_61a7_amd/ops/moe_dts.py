@@ -23,6 +23,7 @@ from __future__ import annotations
 import math
 
 import torch
+from .. import native_array as _NA
 
 from .node import Op
 from .nn import AuxResult
@@ -122,7 +123,7 @@ class DTSGatingOp(Op):
                 w.all_reduce(hist, 'sum')     # one budget on every rank (one all-to-all capacity)
             if hist.is_cuda:
                 from ..runtime import DeviceEvent
-                h = torch.empty(hist.shape, dtype=hist.dtype, pin_memory=True)
+                h = _NA.empty(hist.shape, dtype=hist.dtype, pin_memory=True)
                 h.copy_(hist, non_blocking=True)
                 ev = DeviceEvent(hist.device.index).record()
             else:

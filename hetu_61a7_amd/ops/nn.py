@@ -22,6 +22,7 @@ import time
 import numpy as np
 import torch
 import torch.nn.functional as F
+from .. import native_array as _NA
 
 from .node import Op
 from ..kernels import norm as KN
@@ -66,7 +67,7 @@ class Conv2dOp(Op):
             bufs = self.__dict__.setdefault('_bn_sums', {})
             rep = KC.stats_replicas(x.shape, w.shape, self.stride, self.padding)
             if (x.device, rep) not in bufs:   # persistent: the BN zeroes the totals after reading them
-                bufs[(x.device, rep)] = torch.zeros(rep * 2 * w.shape[0], dtype=torch.float32, device=x.device)
+                bufs[(x.device, rep)] = _NA.zeros(rep * 2 * w.shape[0], dtype=torch.float32, device=x.device)
             y, sums = KC.conv2d_with_stats(x, w, self.stride, self.padding, out_sums=bufs[(x.device, rep)])
             if sums is not None:
                 y.hetu_bn_sums = sums
@@ -131,7 +132,7 @@ class Conv2d_Gradient_of_DataOp(Op):
                 pair = bufs.get((xb.device, rep, double))
                 if pair is None:
                     pair = bufs[(xb.device, rep, double)] = [
-                        torch.zeros(rep * 2 * xb.shape[1], dtype=torch.float32, device=xb.device)
+                        _NA.zeros(rep * 2 * xb.shape[1], dtype=torch.float32, device=xb.device)
                         for _ in range(2 if double else 1)]
                     pair.append(0)
                 k = pair[-1]
@@ -341,7 +342,7 @@ class Batch_NormalizationOp(Op):
     def _init_running(self, C, device):
         if self.running_mean is None or self.running_mean.device != device:
             rm0, rv0 = getattr(self, 'running_mean_init', None), getattr(self, 'running_var_init', None)
-            self.running_mean = torch.zeros(C, dtype=torch.float32, device=device) if rm0 is None else \
+            self.running_mean = _NA.zeros(C, dtype=torch.float32, device=device) if rm0 is None else \
                 torch.as_tensor(rm0, dtype=torch.float32).to(device)
             self.running_var = torch.ones(C, dtype=torch.float32, device=device) if rv0 is None else \
                 torch.as_tensor(rv0, dtype=torch.float32).to(device)
@@ -358,7 +359,7 @@ class Batch_NormalizationOp(Op):
         mask = None
         if training and self.relu and (self.has_residual or self.bwd_fused) and x.is_cuda and native(x) and \
                 x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % (8 if x.dtype == torch.bfloat16 else 4) == 0:
-            mask = torch.empty(KN.relu_mask_bytes(x), dtype=torch.uint8, device=x.device)
+            mask = _NA.empty(KN.relu_mask_bytes(x), dtype=torch.uint8, device=x.device)
         if sums is None and getattr(x, 'hetu_bn_sums', None) is not None:
             x.hetu_bn_sums.zero_()    # persistent totals not consumed (inference): ready for next time
         y, mean, invstd = KN.bn_forward(x, scale.float(), bias.float(), self.running_mean,

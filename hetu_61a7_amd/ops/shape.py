@@ -15,6 +15,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 import torch.nn.functional as F
+from .. import native_array as _NA
 
 from ..kernels import native as _native, record_fallback as _record_fallback
 from ..kernels import tensor as KT
@@ -208,7 +209,7 @@ class SliceGradientOp(Op):
             out = zeros(tuple(shape), g.dtype, g.device)
             copy_into(out[_slices(self.begin, g.shape, shape)], g)
             return out
-        out = torch.zeros(tuple(shape), dtype=g.dtype, device=g.device)
+        out = _NA.zeros(tuple(shape), dtype=g.dtype, device=g.device)
         out[_slices(self.begin, g.shape, shape)] = g
         return out
 
@@ -235,7 +236,7 @@ def slice_gradient_op(node, begin, size=None, ctx=None):
 
     def compute(input_vals, output_val=None, stream_handle=None, _op=op):
         g = input_vals[0]
-        out = torch.zeros(_op.explicit_shape, dtype=g.dtype, device=g.device)
+        out = _NA.zeros(_op.explicit_shape, dtype=g.dtype, device=g.device)
         out[_slices(_op.begin, g.shape, _op.explicit_shape)] = g
         return out
     op.compute = compute
@@ -310,7 +311,7 @@ class SliceByMatrixGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         shape, g, i1, i2 = input_vals
-        out = torch.zeros(tuple(shape), dtype=torch.float32, device=g.device)
+        out = _NA.zeros(tuple(shape), dtype=torch.float32, device=g.device)
         out.index_put_((i1.long().reshape(-1), i2.long().reshape(-1)), g.float(), accumulate=True)
         return out.to(g.dtype)
 
@@ -369,7 +370,7 @@ class SplitGradientOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, shape = input_vals
-        out = torch.zeros(tuple(shape), dtype=g.dtype, device=g.device)
+        out = _NA.zeros(tuple(shape), dtype=g.dtype, device=g.device)
         out[_split_slices(tuple(shape), self.axes, self.indices, self.splits)] = g
         return out
 
@@ -642,7 +643,7 @@ class InterpolateGradOp(Op):
             return KT.bicubic_grad(g, tuple(shape), self.align_corners, self.scale_factor)
         if _gpu(g):
             _record_fallback('interpolate_grad_' + str(self.mode))
-        xs = torch.zeros(tuple(shape), dtype=torch.float32, device=g.device, requires_grad=True)
+        xs = _NA.zeros(tuple(shape), dtype=torch.float32, device=g.device, requires_grad=True)
         sf = self.scale_factor
         with torch.enable_grad():
             y = F.interpolate(xs, size=None if sf else tuple(g.shape[2:]), scale_factor=sf, mode=self.mode,
@@ -694,7 +695,7 @@ class GatherGradientOp(Op):
         shape, g, idx = input_vals
         if _gpu(g) and g.dtype in (torch.float32, torch.bfloat16):
             return KT.scatter_add(g, self.dim, idx, tuple(shape)).to(g.dtype)
-        out = torch.zeros(tuple(shape), dtype=torch.float32, device=g.device)
+        out = _NA.zeros(tuple(shape), dtype=torch.float32, device=g.device)
         out.scatter_add_(self.dim, idx.long(), g.float())
         return out.to(g.dtype)
 
@@ -736,7 +737,7 @@ class IndexingGradOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, idx = input_vals
-        out = torch.zeros_like(g)
+        out = _NA.zeros_like(g)
         out[idx.long().reshape(-1)] = g
         return out
 
@@ -785,7 +786,7 @@ class Scatter1DOp(Op):
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         x, idx = input_vals
-        out = torch.zeros_like(x)
+        out = _NA.zeros_like(x)
         out[idx.long()] = x
         return out
 

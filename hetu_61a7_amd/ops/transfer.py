@@ -7,6 +7,7 @@ executor's dedicated H2D stream; the consumer stream waits on an event
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 from .node import Op
 from .. import ndarray
@@ -43,7 +44,7 @@ class DataD2HOp(Op):
         v = input_vals[0]
         if isinstance(v, ndarray.IndexedSlices):
             return v.cpu()
-        out = torch.empty(v.shape, dtype=v.dtype, pin_memory=torch.cuda.is_available())
+        out = _NA.empty(v.shape, dtype=v.dtype, pin_memory=torch.cuda.is_available())
         out.copy_(v, non_blocking=True)
         return out
 

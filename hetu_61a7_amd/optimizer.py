@@ -29,6 +29,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 import torch
+from . import native_array as _NA
 
 from .ops.node import Op
 from . import ndarray
@@ -188,6 +189,17 @@ def flat_extent(numels):
     return off
 
 
+def _filled(shape, value, dev):
+    """fp32 framework array filled with ``value`` (native fill kernel on the device)"""
+    t = _NA.empty(shape, dtype=torch.float32, device=dev)
+    if t.is_cuda:
+        from .kernels.tensor import fill_
+        fill_(t, float(value))
+    else:
+        t.fill_(float(value))
+    return t
+
+
 class FlatGroup(object):
     """Flat fp32 storage for a set of dense parameters (one per device)."""
 
@@ -208,13 +220,13 @@ class FlatGroup(object):
         # ZeRO-1 pads the buffers so every bucket splits evenly over the ranks
         self.padded = max(-(-off // pad_to) * pad_to, 1)
         dev = device
-        self.param = torch.zeros(self.padded, dtype=torch.float32, device=dev)
+        self.param = _NA.zeros(self.padded, dtype=torch.float32, device=dev)
         for p in params:
             self.view(p, 'param').copy_(values[p].float())
-        self.grad = torch.zeros_like(self.param)
+        self.grad = _NA.zeros_like(self.param)
         ns = self.padded if state_numel is None else state_numel   # ZeRO-1: this rank's shard only
-        self.s1 = torch.full((ns,), state_init[0], dtype=torch.float32, device=dev) if n_states >= 1 else None
-        self.s2 = torch.full((ns,), state_init[1], dtype=torch.float32, device=dev) if n_states >= 2 else None
+        self.s1 = _filled((ns,), state_init[0], dev) if n_states >= 1 else None
+        self.s2 = _filled((ns,), state_init[1], dev) if n_states >= 2 else None
         self.shadow = None
         if shadow:
             self.shadow = self.param.to(torch.bfloat16)  # same (channels-last) layout
@@ -222,7 +234,7 @@ class FlatGroup(object):
         offs = [self.offsets[p][0] for p in params] + [off]
         self.seg_host = offs
         self.seg_off = torch.tensor(offs, dtype=torch.int64, device=dev)
-        self.norms_ws = torch.zeros(2 * max(len(params), 1), dtype=torch.float32, device=dev)
+        self.norms_ws = _NA.zeros(2 * max(len(params), 1), dtype=torch.float32, device=dev)
 
     def view(self, p, which='param'):
         """View of parameter ``p`` inside a flat buffer.  4-D (conv) weights are
@@ -377,7 +389,7 @@ class OptimizerOp(Op):
             if opt.n_states >= 1:
                 st['s1'] = torch.full_like(t, getattr(opt, 'state_init', (0.0,))[0])
             if opt.n_states >= 2:
-                st['s2'] = torch.zeros_like(t)
+                st['s2'] = _NA.zeros_like(t)
             self.sparse_state[p] = st
         # buckets over the flat gradient (contiguous, arrival order)
         self.slot = {}
@@ -444,7 +456,7 @@ class OptimizerOp(Op):
             zoff += n
             self.buckets.append(b)
         assert zoff == self.flat.s1.numel() if self.flat.s1 is not None else True
-        self.flat.zgrad = torch.zeros(max(zoff, 1), dtype=torch.float32, device=self.flat.param.device)
+        self.flat.zgrad = _NA.zeros(max(zoff, 1), dtype=torch.float32, device=self.flat.param.device)
         for p in dense:
             o, n, _ = self.flat.offsets[p]
             bs = self.buckets[o // cap:(o + n - 1) // cap + 1]
@@ -617,8 +629,8 @@ class OptimizerOp(Op):
 def _allgather_slices(comm, sl):
     idx = sl._t(sl.indices).reshape(-1).contiguous()
     val = sl._t(sl.values).reshape(idx.numel(), -1).contiguous()
-    oi = torch.empty((idx.numel() * comm.nrank,), dtype=idx.dtype, device=idx.device)
-    ov = torch.empty((val.shape[0] * comm.nrank, val.shape[1]), dtype=val.dtype, device=val.device)
+    oi = _NA.empty((idx.numel() * comm.nrank,), dtype=idx.dtype, device=idx.device)
+    ov = _NA.empty((val.shape[0] * comm.nrank, val.shape[1]), dtype=val.dtype, device=val.device)
     comm.all_gather(oi, idx)
     comm.all_gather(ov, val)
     return ndarray.IndexedSlices(oi, ov, sl.dense_shape)

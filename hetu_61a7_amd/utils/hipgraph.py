@@ -10,6 +10,7 @@ Adam bias corrections) live in a device tensor read by the fused update kernel
 from __future__ import annotations
 
 import torch
+from .. import native_array as _NA
 
 _CAPTURING = [0]
 
@@ -65,8 +66,8 @@ class GraphRunner(object):
         for op in self.sub.opt_ops:
             opt = op.optimizer
             if getattr(op, 'dyn', None) is None:
-                op.dyn = torch.zeros(4, dtype=torch.float32, device=self.sub.config.device)
-                op.dyn_host = torch.zeros(4, dtype=torch.float32).pin_memory()
+                op.dyn = _NA.zeros(4, dtype=torch.float32, device=self.sub.config.device)
+                op.dyn_host = _NA.zeros(4, dtype=torch.float32).pin_memory()
             step = op.step + 1
             h = opt.hyper(step)
             op.dyn_host[0] = h.get('lr', 0.0)

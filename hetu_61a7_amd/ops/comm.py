@@ -218,15 +218,20 @@ def halltoall_op(node, num_nodes=1, num_local_gpus=8, comm=None, ctx=None):
 
 
 class PipelineSendOp(Op):
-    def __init__(self, node, destination, comm=None, ctx=None):
+    """Send to a pipeline peer; the shape header travels once per channel (static shapes,
+    as the reference), or with every message when ``dynamic_shapes``."""
+
+    def __init__(self, node, destination, comm=None, ctx=None, dynamic_shapes=False):
         super().__init__(PipelineSendOp, [node], ctx)
         self.const_attr = destination
         self.comm = comm
         self.stream_kind = 'p2p'
+        self.dynamic_shapes = dynamic_shapes
+        self._chan = {'dynamic': dynamic_shapes}
 
     def compute(self, input_vals, output_val=None, stream_handle=None, group_call=False):
         from ..parallel import pipeline as PP
-        PP.send_tensor(_comm(self.comm), input_vals[0], self.const_attr)
+        PP.send_tensor(_comm(self.comm), input_vals[0], self.const_attr, None if self.dynamic_shapes else self._chan)
         return None
 
     def gradient(self, output_grad):
@@ -237,15 +242,18 @@ class PipelineSendOp(Op):
 
 
 class PipelineReceiveOp(Op):
-    def __init__(self, source, comm=None, ctx=None):
+    def __init__(self, source, comm=None, ctx=None, dynamic_shapes=False):
         super().__init__(PipelineReceiveOp, [], ctx)
         self.const_attr = source
         self.comm = comm
         self.stream_kind = 'p2p'
+        self.dynamic_shapes = dynamic_shapes
+        self._chan = {}
 
     def compute(self, input_vals, output_val=None, stream_handle=None, group_call=False):
         from ..parallel import pipeline as PP
-        return PP.recv_tensor(_comm(self.comm), self.const_attr, self.device)
+        return PP.recv_tensor(_comm(self.comm), self.const_attr, self.device,
+                              None if self.dynamic_shapes else self._chan)
 
     def gradient(self, output_grad):
         return None
@@ -254,9 +262,9 @@ class PipelineReceiveOp(Op):
         return None
 
 
-def pipeline_send_op(node, destination, comm=None, ctx=None):
-    return PipelineSendOp(node, destination, comm, ctx=ctx)
+def pipeline_send_op(node, destination, comm=None, ctx=None, dynamic_shapes=False):
+    return PipelineSendOp(node, destination, comm, ctx=ctx, dynamic_shapes=dynamic_shapes)
 
 
-def pipeline_receive_op(source, comm=None, ctx=None):
-    return PipelineReceiveOp(source, comm, ctx=ctx)
+def pipeline_receive_op(source, comm=None, ctx=None, dynamic_shapes=False):
+    return PipelineReceiveOp(source, comm, ctx=ctx, dynamic_shapes=dynamic_shapes)

@@ -85,21 +85,32 @@ __device__ __forceinline__ v8s lds_perm(const short* T, int row, int s, int h) {
   return r;
 }
 
-// stage X^T for rows r0 .. r0+31 of X (row stride ld, D columns) into T[D][LT]; rows
-// at or past n are zeros.  Each thread moves 2 rows x 8 columns as 8 4-byte stores.
+// X^T staging for rows r0 .. r0+31 of X (row stride ld, D columns) into T[D][LT], split
+// into a global read into registers (issued a block ahead) and the LDS write; rows at
+// or past n are zeros.  Thread t < 2 D moves 2 rows x 8 columns as 8 4-byte stores.
 template <int D>
-__device__ __forceinline__ void stage_t32(const bf16* X, int64_t ld, int r0, int n, short* T) {
+__device__ __forceinline__ void load_t32(const bf16* X, int64_t ld, int r0, int n, v8s& x0, v8s& x1) {
   constexpr int C8 = D / 8;
-  for (int idx = threadIdx.x; idx < 16 * C8; idx += 256) {
+  const int idx = threadIdx.x;
+  x0 = zero8();
+  x1 = zero8();
+  if (idx < 16 * C8) {
     const int rp = idx & 15, c = idx >> 4;          // row pair, 8-column group
     const int ra = r0 + 2 * rp;
-    const v8s x0 = ra < n ? ld8(X + (int64_t)ra * ld + 8 * c) : zero8();
-    const v8s x1 = ra + 1 < n ? ld8(X + (int64_t)(ra + 1) * ld + 8 * c) : zero8();
+    if (ra < n) x0 = ld8(X + (int64_t)ra * ld + 8 * c);
+    if (ra + 1 < n) x1 = ld8(X + (int64_t)(ra + 1) * ld + 8 * c);
+  }
+}
+template <int D>
+__device__ __forceinline__ void store_t32(const v8s& x0, const v8s& x1, short* T) {
+  constexpr int C8 = D / 8;
+  const int idx = threadIdx.x;
+  if (idx >= 16 * C8) return;
+  const int rp = idx & 15, c = idx >> 4;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t pr = (uint32_t)(unsigned short)x0[i] | ((uint32_t)(unsigned short)x1[i] << 16);
-      *reinterpret_cast<uint32_t*>(T + (8 * c + i) * LT + 2 * rp) = pr;
-    }
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t pr = (uint32_t)(unsigned short)x0[i] | ((uint32_t)(unsigned short)x1[i] << 16);
+    *reinterpret_cast<uint32_t*>(T + (8 * c + i) * LT + 2 * rp) = pr;
   }
 }
 
@@ -126,12 +137,15 @@ __device__ __forceinline__ void store_rows4(bf16* dst, const v16f& o, int g, int
 }
 
 // -------------------------------------------------------------------------------------
-// forward: workgroup = (b*NH + h, 128-query tile); wave w: queries q0 + 32 w + (lane & 31)
+// forward: workgroup = (b*NH + h, 128-query tile); wave w: queries q0 + 32 w + (lane & 31).
+// Software-pipelined over 32-key blocks: while block j's scores, softmax and P.V run,
+// block j+1's K fragments and V rows are in flight into registers; V^T is written to
+// the other half of a double-buffered LDS image after the P.V, so one barrier per block.
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
-  __shared__ short vt[D * LT];
-  __shared__ float msk[KBLK];
+  __shared__ short vt[2][D * LT];
+  __shared__ float msk[2][KBLK];
   const int bh = blockIdx.x, b = bh / a.NH, hh = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int qt0 = blockIdx.y * WQ;
@@ -155,25 +169,38 @@ __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
   // causal: keys past the tile's last query contribute nothing
   const int kend = a.causal ? min(a.Sk, min(a.Sq, qt0 + WQ)) : a.Sk;
 
-  for (int kb0 = 0; kb0 < kend; kb0 += KBLK) {
-    __syncthreads();
-    stage_t32<D>(V, a.vs, kb0, a.Sk, vt);
-    if (mrow && threadIdx.x < KBLK) {
-      const int key = kb0 + threadIdx.x;
-      msk[threadIdx.x] = key < a.Sk ? M[(int64_t)key * a.mk] : 0.f;
+  // prologue: block 0 staged, its K fragments in registers
+  v8s kf[DS], x0, x1;
+  float mv = 0.f;
+  load_t32<D>(V, a.vs, 0, a.Sk, x0, x1);
+  if (mrow && threadIdx.x < KBLK) mv = threadIdx.x < a.Sk ? M[(int64_t)threadIdx.x * a.mk] : 0.f;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) kf[ds] = r < a.Sk ? ld8(K + (int64_t)r * a.ks + 16 * ds + 8 * h) : zero8();
+  store_t32<D>(x0, x1, vt[0]);
+  if (mrow && threadIdx.x < KBLK) msk[0][threadIdx.x] = mv;
+  __syncthreads();
+
+  int buf = 0;
+  for (int kb0 = 0; kb0 < kend; kb0 += KBLK, buf ^= 1) {
+    const int nb = kb0 + KBLK;
+    const bool more = nb < kend;
+    v8s kn[DS];
+    if (more) {
+      load_t32<D>(V, a.vs, nb, a.Sk, x0, x1);
+      if (mrow && threadIdx.x < KBLK) mv = nb + threadIdx.x < a.Sk ? M[(int64_t)(nb + threadIdx.x) * a.mk] : 0.f;
+      const int kr = nb + r;
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) kn[ds] = kr < a.Sk ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8();
     }
-    __syncthreads();
-    const int kr = kb0 + r;
     v16f sc = v16f{0.f};
 #pragma unroll
-    for (int ds = 0; ds < DS; ++ds)
-      sc = mfma(kr < a.Sk ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8(), qf[ds], sc);
+    for (int ds = 0; ds < DS; ++ds) sc = mfma(kf[ds], qf[ds], sc);
     float mb = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kl = (i & 3) + 8 * (i >> 2) + 4 * h, key = kb0 + kl;
       float s = sc[i] * a.scale;
-      if (M != nullptr) s += mrow ? msk[kl] : (key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] : 0.f);
+      if (M != nullptr) s += mrow ? msk[buf][kl] : (key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] : 0.f);
       if (key >= a.Sk || (a.causal && key > q)) s = -INFINITY;
       sc[i] = s;
       mb = fmaxf(mb, s);
@@ -197,10 +224,18 @@ __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
       }
     }
     m = mn;
+    const short* vb = vt[buf];
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(vt, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
+      for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(vb, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
+    if (more) {
+      store_t32<D>(x0, x1, vt[buf ^ 1]);
+      if (mrow && threadIdx.x < KBLK) msk[buf ^ 1][threadIdx.x] = mv;
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) kf[ds] = kn[ds];
+    }
+    __syncthreads();
   }
   l += __shfl_xor(l, 32, 64);
   if (!qv) return;
@@ -242,12 +277,15 @@ __global__ void __launch_bounds__(256) flash_dsum_k(FArgs a, float* dsum) {
 }
 
 // -------------------------------------------------------------------------------------
-// dQ: the forward's walk (lane = query) with P from the saved lse and dP^T = V . dO^T
+// dQ: the forward's walk (lane = query) with P from the saved lse and dP^T = V . dO^T,
+// pipelined like the forward (next block's K / V fragments and K rows in flight,
+// double-buffered K^T image, one barrier per block)
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
-  __shared__ short kt[D * LT];
-  __shared__ float msk[KBLK];
+  constexpr bool PF = D <= 32;     // fragments a block ahead only where registers allow 2 waves / SIMD
+  __shared__ short kt[2][D * LT];
+  __shared__ float msk[2][KBLK];
   const int bh = blockIdx.x, b = bh / a.NH, hh = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int qt0 = blockIdx.y * WQ;
@@ -274,21 +312,52 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
   const int sk4 = (a.Sk + 3) >> 2;
   const uint64_t qrow = (uint64_t)bh * a.Sq + (qv ? q : 0);
   const int kend = a.causal ? min(a.Sk, min(a.Sq, qt0 + WQ)) : a.Sk;
-  for (int kb0 = 0; kb0 < kend; kb0 += KBLK) {
-    __syncthreads();
-    stage_t32<D>(K, a.ks, kb0, a.Sk, kt);
-    if (mrow && threadIdx.x < KBLK) {
-      const int key = kb0 + threadIdx.x;
-      msk[threadIdx.x] = key < a.Sk ? M[(int64_t)key * a.mk] : 0.f;
+
+  v8s kf[DS], vf[DS], x0, x1;
+  float mv = 0.f;
+  load_t32<D>(K, a.ks, 0, a.Sk, x0, x1);
+  if (mrow && threadIdx.x < KBLK) mv = threadIdx.x < a.Sk ? M[(int64_t)threadIdx.x * a.mk] : 0.f;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) {
+    kf[ds] = r < a.Sk ? ld8(K + (int64_t)r * a.ks + 16 * ds + 8 * h) : zero8();
+    vf[ds] = r < a.Sk ? ld8(V + (int64_t)r * a.vs + 16 * ds + 8 * h) : zero8();
+  }
+  store_t32<D>(x0, x1, kt[0]);
+  if (mrow && threadIdx.x < KBLK) msk[0][threadIdx.x] = mv;
+  __syncthreads();
+
+  int buf = 0;
+  for (int kb0 = 0; kb0 < kend; kb0 += KBLK, buf ^= 1) {
+    const int nb = kb0 + KBLK;
+    const bool more = nb < kend;
+    v8s kn[DS], vn[DS];
+    if (!PF && kb0 > 0) {
+      const int kr = kb0 + r;
+      const bool kv = kr < a.Sk;
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) {
+        kf[ds] = kv ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8();
+        vf[ds] = kv ? ld8(V + (int64_t)kr * a.vs + 16 * ds + 8 * h) : zero8();
+      }
     }
-    __syncthreads();
-    const int kr = kb0 + r;
+    if (more) {
+      load_t32<D>(K, a.ks, nb, a.Sk, x0, x1);
+      if (mrow && threadIdx.x < KBLK) mv = nb + threadIdx.x < a.Sk ? M[(int64_t)(nb + threadIdx.x) * a.mk] : 0.f;
+      if (PF) {
+        const int kr = nb + r;
+        const bool kv = kr < a.Sk;
+#pragma unroll
+        for (int ds = 0; ds < DS; ++ds) {
+          kn[ds] = kv ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8();
+          vn[ds] = kv ? ld8(V + (int64_t)kr * a.vs + 16 * ds + 8 * h) : zero8();
+        }
+      }
+    }
     v16f sc = v16f{0.f}, dp = v16f{0.f};
 #pragma unroll
     for (int ds = 0; ds < DS; ++ds) {
-      const bool kv = kr < a.Sk;
-      sc = mfma(kv ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8(), qf[ds], sc);
-      dp = mfma(kv ? ld8(V + (int64_t)kr * a.vs + 16 * ds + 8 * h) : zero8(), gf[ds], dp);
+      sc = mfma(kf[ds], qf[ds], sc);
+      dp = mfma(vf[ds], gf[ds], dp);
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -299,16 +368,26 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
         const int i = 4 * g + t;
         const int kl = 8 * g + 4 * h + t, key = kb0 + kl;
         float s = sc[i] * a.scale;
-        if (M != nullptr) s += mrow ? msk[kl] : (key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] : 0.f);
+        if (M != nullptr) s += mrow ? msk[buf][kl] : (key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] : 0.f);
         const bool ok = live && key < a.Sk && !(a.causal && key > q);
         const float p = ok ? __expf(s - lse) : 0.f;
         sc[i] = p * (dp[i] * mul[t] - Dq) * a.scale;
       }
     }
+    const short* kb = kt[buf];
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(kt, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
+      for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(kb, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
+    if (more) {
+      store_t32<D>(x0, x1, kt[buf ^ 1]);
+      if (mrow && threadIdx.x < KBLK) msk[buf ^ 1][threadIdx.x] = mv;
+      if (PF) {
+#pragma unroll
+        for (int ds = 0; ds < DS; ++ds) { kf[ds] = kn[ds]; vf[ds] = vn[ds]; }
+      }
+    }
+    __syncthreads();
   }
   if (!qv) return;
   bf16* dQ = a.dq + b * a.dqb + hh * a.dqh + (int64_t)q * a.dqs;
@@ -321,13 +400,16 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
 // -------------------------------------------------------------------------------------
 // dK, dV: workgroup = (b*NH + h, 128-key tile), lane = key; walk over 32-query blocks:
 // S = Q . K^T (A = Q rows, B = this lane's K row), dP = dO . V^T, then
-// dV^T += dO^T . P_drop and dK^T += Q^T . dS with dO^T / Q^T staged in LDS.
+// dV^T += dO^T . P_drop and dK^T += Q^T . dS with dO^T / Q^T staged in double-buffered
+// LDS from registers loaded a block ahead (the Q / dO fragments too at D = 32; above
+// that they would cost the second wave per SIMD).
 template <int D, bool DROP>
 __global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
-  __shared__ short qt[D * LT];
-  __shared__ short gt[D * LT];
-  __shared__ float ls[KBLK], dl[KBLK];
+  constexpr bool PF = D <= 32;
+  __shared__ short qt[2][D * LT];
+  __shared__ short gt[2][D * LT];
+  __shared__ float ls[2][KBLK], dl[2][KBLK];
   const int bh = blockIdx.x, b = bh / a.NH, hh = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int kt0 = blockIdx.y * WQ;
@@ -338,6 +420,8 @@ __global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
   const bf16* V = a.v + b * a.vb + hh * a.vh;
   const bf16* G = a.dout + b * a.gb + hh * a.gh;
   const float* M = a.mask ? a.mask + b * a.mb + hh * a.mh : nullptr;
+  const float* LSE = a.lse + (int64_t)bh * a.Sq;
+  const float* DSUM = a.dsum + (int64_t)bh * a.Sq;
   v8s kf[DS], vf[DS];
 #pragma unroll
   for (int ds = 0; ds < DS; ++ds) {
@@ -351,45 +435,99 @@ __global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
   const int sk4 = (a.Sk + 3) >> 2;
   // causal: queries before the tile's first key see none of its keys
   const int qstart = a.causal ? (kt0 / KBLK) * KBLK : 0;
-  for (int qb0 = qstart; qb0 < a.Sq; qb0 += KBLK) {
-    __syncthreads();
-    stage_t32<D>(Q, a.qs, qb0, a.Sq, qt);
-    stage_t32<D>(G, a.gs, qb0, a.Sq, gt);
+  if (qstart >= a.Sq) {
+    // no query reaches these keys: zero gradients
+    if (!kv) return;
+    bf16* dK = a.dk + b * a.dkb + hh * a.dkh + (int64_t)key * a.dks;
+    bf16* dV = a.dv + b * a.dvb + hh * a.dvh + (int64_t)key * a.dvs;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        store_rows4(dK + db * 32, dkt[db], g, h, 1.f);
+        store_rows4(dV + db * 32, dvt[db], g, h, 1.f);
+      }
+    return;
+  }
+
+  v8s x0, x1, y0, y1, qf[DS], gf[DS];
+  float lv = -INFINITY, dv = 0.f;
+  auto fetch = [&](int qb0) {
+    load_t32<D>(Q, a.qs, qb0, a.Sq, x0, x1);
+    load_t32<D>(G, a.gs, qb0, a.Sq, y0, y1);
     if (threadIdx.x < KBLK) {
       const int qq = qb0 + threadIdx.x;
       const bool ok = qq < a.Sq;
-      ls[threadIdx.x] = ok ? a.lse[(int64_t)bh * a.Sq + qq] : -INFINITY;
-      dl[threadIdx.x] = ok ? a.dsum[(int64_t)bh * a.Sq + qq] : 0.f;
+      lv = ok ? LSE[qq] : -INFINITY;
+      dv = ok ? DSUM[qq] : 0.f;
     }
-    __syncthreads();
+  };
+  auto frags = [&](int qb0) {
     const int qr = qb0 + r;
     const bool qrv = qr < a.Sq;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      qf[ds] = qrv ? ld8(Q + (int64_t)qr * a.qs + 16 * ds + 8 * h) : zero8();
+      gf[ds] = qrv ? ld8(G + (int64_t)qr * a.gs + 16 * ds + 8 * h) : zero8();
+    }
+  };
+  auto put = [&](int bf) {
+    store_t32<D>(x0, x1, qt[bf]);
+    store_t32<D>(y0, y1, gt[bf]);
+    if (threadIdx.x < KBLK) { ls[bf][threadIdx.x] = lv; dl[bf][threadIdx.x] = dv; }
+  };
+  fetch(qstart);
+  if (PF) frags(qstart);
+  put(0);
+  __syncthreads();
+
+  int buf = 0;
+  for (int qb0 = qstart; qb0 < a.Sq; qb0 += KBLK, buf ^= 1) {
+    const int nb = qb0 + KBLK;
+    const bool more = nb < a.Sq;
+    v8s qa[DS], ga[DS];
+    if (PF) {
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) { qa[ds] = qf[ds]; ga[ds] = gf[ds]; }
+    } else {
+      frags(qb0);
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) { qa[ds] = qf[ds]; ga[ds] = gf[ds]; }
+    }
+    if (more) {
+      fetch(nb);
+      if (PF) frags(nb);
+    }
     v16f sc = v16f{0.f}, dp = v16f{0.f};
 #pragma unroll
     for (int ds = 0; ds < DS; ++ds) {
-      sc = mfma(qrv ? ld8(Q + (int64_t)qr * a.qs + 16 * ds + 8 * h) : zero8(), kf[ds], sc);
-      dp = mfma(qrv ? ld8(G + (int64_t)qr * a.gs + 16 * ds + 8 * h) : zero8(), vf[ds], dp);
+      sc = mfma(qa[ds], kf[ds], sc);
+      dp = mfma(ga[ds], vf[ds], dp);
     }
     v16f pd;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ql = (i & 3) + 8 * (i >> 2) + 4 * h, qq = qb0 + ql;
-      const float lq = ls[ql];
+      const float lq = ls[buf][ql];
       float s = sc[i] * a.scale;
       if (M != nullptr) s += a.mq == 0 ? mkey : (kv && qq < a.Sq ? M[(int64_t)qq * a.mq + (int64_t)key * a.mk] : 0.f);
       const bool ok = kv && qq < a.Sq && lq != -INFINITY && !(a.causal && key > qq);
       const float p = ok ? __expf(s - lq) : 0.f;
       const float mul = (DROP && ok) ? drop1(a.seed, (uint64_t)bh * a.Sq + qq, key, sk4, a.keep) : 1.f;
       pd[i] = p * mul;
-      sc[i] = p * (dp[i] * mul - dl[ql]) * a.scale;
+      sc[i] = p * (dp[i] * mul - dl[buf][ql]) * a.scale;
     }
+    const short* gb = gt[buf];
+    const short* qb = qt[buf];
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        dvt[db] = mfma(lds_perm(gt, db * 32 + r, s, h), pack_acc(pd, s), dvt[db]);
-        dkt[db] = mfma(lds_perm(qt, db * 32 + r, s, h), pack_acc(sc, s), dkt[db]);
+        dvt[db] = mfma(lds_perm(gb, db * 32 + r, s, h), pack_acc(pd, s), dvt[db]);
+        dkt[db] = mfma(lds_perm(qb, db * 32 + r, s, h), pack_acc(sc, s), dkt[db]);
       }
+    if (more) put(buf ^ 1);
+    __syncthreads();
   }
   if (!kv) return;
   bf16* dK = a.dk + b * a.dkb + hh * a.dkh + (int64_t)key * a.dks;

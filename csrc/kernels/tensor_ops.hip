@@ -320,6 +320,43 @@ HETU_API int hetu_nd_copy(const void* x, void* y, int elem, int nd, const int64_
   return (int)hipGetLastError();
 }
 
+// y[i][c] = (idx[i] == c) as fp32 (one_hot of int32 / int64 / fp32 class ids; ids out of
+// [0, C) give a zero row).  One thread per 4 outputs, 16-byte stores.
+template <typename T>
+__global__ void __launch_bounds__(256) one_hot_k(const T* __restrict__ idx, float* __restrict__ y, int64_t n, int C) {
+  const int64_t c4 = (C + 3) / 4;
+  const int64_t total = n * c4;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t i = t / c4;
+    const int c0 = (int)(t - i * c4) * 4;
+    const int64_t k = (int64_t)idx[i];
+    float4 v;
+    v.x = k == c0 ? 1.f : 0.f;
+    v.y = k == c0 + 1 ? 1.f : 0.f;
+    v.z = k == c0 + 2 ? 1.f : 0.f;
+    v.w = k == c0 + 3 ? 1.f : 0.f;
+    float* dst = y + i * C + c0;
+    if ((C & 3) == 0) {
+      *reinterpret_cast<float4*>(dst) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int j = 0; j < 4 && c0 + j < C; ++j) dst[j] = vv[j];
+    }
+  }
+}
+
+HETU_API int hetu_one_hot(const void* idx, int kind, float* y, int64_t n, int C, hipStream_t st) {
+  if (n <= 0 || C <= 0) return 0;
+  const int g = stream_grid(n * ((C + 3) / 4), 256, 4);
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(one_hot_k<int64_t>, dim3(g), dim3(256), 0, st, (const int64_t*)idx, y, n, C); break;
+    case 1: hipLaunchKernelGGL(one_hot_k<int32_t>, dim3(g), dim3(256), 0, st, (const int32_t*)idx, y, n, C); break;
+    case 2: hipLaunchKernelGGL(one_hot_k<float>, dim3(g), dim3(256), 0, st, (const float*)idx, y, n, C); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
 // fill n elements of `elem` bytes with the bit pattern `bits`
 HETU_API int hetu_fill(void* y, int elem, int64_t n, uint64_t bits, hipStream_t st) {
   if (n <= 0) return 0;

@@ -101,6 +101,17 @@ def zeros(shape, dtype=torch.float32, device='cuda'):
     return t
 
 
+def one_hot(idx, C):
+    """fp32 one-hot rows of int64 / int32 / fp32 class ids (out-of-range ids: zero rows)"""
+    kind = {torch.int64: 0, torch.int32: 1, torch.float32: 2}[idx.dtype]
+    idx = idx.contiguous()
+    y = _NA.empty(tuple(idx.shape) + (C,), dtype=torch.float32, device=idx.device)
+    f = fn('hetu_one_hot', [P, I32, P, I64, I32, P])
+    check(f(idx.data_ptr(), kind, y.data_ptr(), idx.numel(), C, stream_ptr()), 'one_hot')
+    record_native('one_hot')
+    return y
+
+
 def _dense(t):
     return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
 

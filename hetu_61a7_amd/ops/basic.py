@@ -566,8 +566,11 @@ class OneHotOp(Op):
         self.num_classes = num_classes
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        idx = input_vals[0].long()
-        return torch.nn.functional.one_hot(idx, self.num_classes).float()
+        idx = input_vals[0]
+        if idx.is_cuda and idx.dtype in (torch.int64, torch.int32, torch.float32):
+            from ..kernels import tensor as KT
+            return KT.one_hot(idx, self.num_classes)
+        return torch.nn.functional.one_hot(idx.long(), self.num_classes).float()
 
     def gradient(self, output_grad):
         return [None]

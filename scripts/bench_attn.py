@@ -4,6 +4,8 @@ shape, plus the general kernels on the Transformer / BERT phase-2 shapes.
 
     python scripts/bench_attn.py        -> one line per (shape, kernel, direction): us, TF/s
 """
+import contextlib
+import ctypes
 import math
 import os
 import sys
@@ -12,6 +14,27 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hetu_61a7_amd.kernels import attention as KA  # noqa: E402
+
+
+# A/B: ALT_FLASH_LIB names a library built from another revision of flash_attn.hip
+# (same C ABI); its kernels are timed next to the in-tree ones
+_ALT = ctypes.CDLL(os.environ['ALT_FLASH_LIB']) if os.environ.get('ALT_FLASH_LIB') else None
+
+
+@contextlib.contextmanager
+def _alt_flash():
+    import hetu_61a7_amd.kernels as K
+    saved = {n: K._cache.get(n) for n in ('hetu_flash_fwd', 'hetu_flash_bwd')}
+    for n, f in saved.items():
+        if f is None:
+            raise RuntimeError('time the in-tree kernels first')
+        g = getattr(_ALT, n)
+        g.argtypes, g.restype = f.argtypes, f.restype
+        K._cache[n] = g
+    try:
+        yield
+    finally:
+        K._cache.update(saved)
 
 
 def timeit(f, reps=20, rounds=5):
@@ -53,6 +76,12 @@ def packed_case(B, S, NH, D, keep):
     g4 = do.view(B, S, NH, D).permute(0, 2, 1, 3)
     t = timeit(lambda: KA.flash_bwd(g4, q, k, v, o4, lse, m4, False, keep, 7))
     rows.append(('flash', 'bwd', t, 2.5 * fl_f / t * 1e-6))
+    if _ALT is not None:
+        with _alt_flash():
+            t = timeit(lambda: KA.flash_fwd(q, k, v, m4, False, keep, 7, out=o4))
+            rows.append(('alt', 'fwd', t, fl_f / t * 1e-6))
+            t = timeit(lambda: KA.flash_bwd(g4, q, k, v, o4, lse, m4, False, keep, 7))
+            rows.append(('alt', 'bwd', t, 2.5 * fl_f / t * 1e-6))
     for r in rows:
         print('B %3d S %4d NH %2d D %3d keep %.1f | %-5s %s %8.1f us %6.1f TF/s' % ((B, S, NH, D, keep) + r),
               flush=True)

@@ -235,6 +235,25 @@ def main():
         cfg.update(_kernel_census(step))
     if hasattr(step, 'extra'):
         cfg.update(step.extra())
+    if rank == 0 and os.environ.get('HETU_BENCH_PYPROF'):
+        # host-side profile of extra (untimed) steady-state steps: where the Python time goes
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        n = int(os.environ.get('HETU_BENCH_PYPROF_STEPS', '50'))
+        pr.enable()
+        for _ in range(n):
+            step()
+        sync()
+        pr.disable()
+        buf = io.StringIO()
+        st = pstats.Stats(pr, stream=buf)
+        buf.write('%d steps\n' % n)
+        st.sort_stats('tottime').print_stats(45)
+        st.sort_stats('cumulative').print_stats(45)
+        with open(os.environ['HETU_BENCH_PYPROF'], 'w') as f:
+            f.write(buf.getvalue())
     if world > 1 or args.comm_trace:
         cfg = dict(cfg)
         cfg['comm'] = C.world().backend if C.world() is not None else 'none'

@@ -136,26 +136,50 @@ __device__ __forceinline__ void store_rows4(bf16* dst, const v16f& o, int g, int
   *reinterpret_cast<uint2*>(dst + 8 * g + 4 * h) = pk;
 }
 
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// x op x[lane ^ 32] for both halves of the wave by one v_permlane32_swap (no LDS trip)
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float exp2_(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// mask modes: none, key-only (the same additive row for every query of a (b, h): staged per
+// block in LDS, pre-scaled by log2 e, -inf past Sk), general (per-element global reads)
+enum { MK_NONE = 0, MK_KEY = 1, MK_FULL = 2 };
+
 // -------------------------------------------------------------------------------------
 // forward: workgroup = (b*NH + h, 128-query tile); wave w: queries q0 + 32 w + (lane & 31).
 // Software-pipelined over 32-key blocks: while block j's scores, softmax and P.V run,
 // block j+1's K fragments and V rows are in flight into registers; V^T is written to
 // the other half of a double-buffered LDS image after the P.V, so one barrier per block.
-template <int D, bool DROP>
+// The softmax is VALU-bound (16 scores per lane per block against 8 MFMAs), so it runs
+// in the log2 domain (scale * log2 e folded into one multiply, bare v_exp_f32), checks
+// bounds / causality only on edge blocks, reads the key mask as 16-byte LDS vectors, and
+// rescales O lazily: the running max moves only when some row's block max exceeds it by
+// more than 8 (P <= 256, exact in fp32 accumulation), which after the first blocks is rare.
+template <int D, bool DROP, int MK>
 __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ short vt[2][D * LT];
-  __shared__ float msk[2][KBLK];
+  __shared__ __attribute__((aligned(16))) float msk[2][KBLK];
   const int bh = blockIdx.x, b = bh / a.NH, hh = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int qt0 = blockIdx.y * WQ;
-  const int q = qt0 + 32 * w + r;
+  const int qw0 = qt0 + 32 * w;
+  const int q = qw0 + r;
   const bool qv = q < a.Sq;
   const bf16* Q = a.q + b * a.qb + hh * a.qh;
   const bf16* K = a.k + b * a.kb + hh * a.kh;
   const bf16* V = a.v + b * a.vb + hh * a.vh;
-  const float* M = a.mask ? a.mask + b * a.mb + hh * a.mh : nullptr;
-  const bool mrow = M != nullptr && a.mq == 0;     // key-only mask: staged per block
+  const float* M = MK != MK_NONE ? a.mask + b * a.mb + hh * a.mh : nullptr;
+  const float sl2 = a.scale * kLog2e;
 
   v8s qf[DS];
 #pragma unroll
@@ -163,21 +187,25 @@ __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
   v16f o[DB];
 #pragma unroll
   for (int db = 0; db < DB; ++db) o[db] = v16f{0.f};
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;      // running max (log2 domain) and sum of this lane's half
   const int sk4 = (a.Sk + 3) >> 2;
   const uint64_t qrow = (uint64_t)bh * a.Sq + (qv ? q : 0);
   // causal: keys past the tile's last query contribute nothing
   const int kend = a.causal ? min(a.Sk, min(a.Sq, qt0 + WQ)) : a.Sk;
 
+  auto key_mask = [&](int kb) -> float {
+    const int key = kb + (int)threadIdx.x;
+    return key < a.Sk ? M[(int64_t)key * a.mk] * kLog2e : -INFINITY;
+  };
   // prologue: block 0 staged, its K fragments in registers
   v8s kf[DS], x0, x1;
   float mv = 0.f;
   load_t32<D>(V, a.vs, 0, a.Sk, x0, x1);
-  if (mrow && threadIdx.x < KBLK) mv = threadIdx.x < a.Sk ? M[(int64_t)threadIdx.x * a.mk] : 0.f;
+  if (MK == MK_KEY && threadIdx.x < KBLK) mv = key_mask(0);
 #pragma unroll
   for (int ds = 0; ds < DS; ++ds) kf[ds] = r < a.Sk ? ld8(K + (int64_t)r * a.ks + 16 * ds + 8 * h) : zero8();
   store_t32<D>(x0, x1, vt[0]);
-  if (mrow && threadIdx.x < KBLK) msk[0][threadIdx.x] = mv;
+  if (MK == MK_KEY && threadIdx.x < KBLK) msk[0][threadIdx.x] = mv;
   __syncthreads();
 
   int buf = 0;
@@ -187,60 +215,81 @@ __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
     v8s kn[DS];
     if (more) {
       load_t32<D>(V, a.vs, nb, a.Sk, x0, x1);
-      if (mrow && threadIdx.x < KBLK) mv = nb + threadIdx.x < a.Sk ? M[(int64_t)(nb + threadIdx.x) * a.mk] : 0.f;
+      if (MK == MK_KEY && threadIdx.x < KBLK) mv = key_mask(nb);
       const int kr = nb + r;
 #pragma unroll
       for (int ds = 0; ds < DS; ++ds) kn[ds] = kr < a.Sk ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8();
     }
-    v16f sc = v16f{0.f};
+    // a causal block wholly above this wave's queries adds nothing (wave-uniform skip)
+    if (!(a.causal && kb0 > qw0 + 31)) {
+      v16f sc = v16f{0.f};
 #pragma unroll
-    for (int ds = 0; ds < DS; ++ds) sc = mfma(kf[ds], qf[ds], sc);
-    float mb = -INFINITY;
+      for (int ds = 0; ds < DS; ++ds) sc = mfma(kf[ds], qf[ds], sc);
+      const bool full = MK != MK_FULL && nb <= a.Sk && !(a.causal && kb0 + KBLK - 1 > qw0);
+      if (full) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kl = (i & 3) + 8 * (i >> 2) + 4 * h, key = kb0 + kl;
-      float s = sc[i] * a.scale;
-      if (M != nullptr) s += mrow ? msk[buf][kl] : (key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] : 0.f);
-      if (key >= a.Sk || (a.causal && key > q)) s = -INFINITY;
-      sc[i] = s;
-      mb = fmaxf(mb, s);
-    }
-    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
-    const float mn = fmaxf(m, mb);
-    const float alpha = mn == -INFINITY ? 1.f : __expf(m - mn);
+        for (int g = 0; g < 4; ++g) {
+          float4 mm = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (MK == MK_KEY) mm = *reinterpret_cast<const float4*>(&msk[buf][8 * g + 4 * h]);
+          sc[4 * g] = fmaf(sc[4 * g], sl2, mm.x);
+          sc[4 * g + 1] = fmaf(sc[4 * g + 1], sl2, mm.y);
+          sc[4 * g + 2] = fmaf(sc[4 * g + 2], sl2, mm.z);
+          sc[4 * g + 3] = fmaf(sc[4 * g + 3], sl2, mm.w);
+        }
+      } else {
 #pragma unroll
-    for (int db = 0; db < DB; ++db) o[db] *= alpha;
-    l *= alpha;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float mul[4] = {1.f, 1.f, 1.f, 1.f};
-      if (DROP) drop4(a.seed, qrow, kb0 + 8 * g + 4 * h, sk4, a.keep, mul);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int i = 4 * g + t;
-        const float p = mn == -INFINITY ? 0.f : __expf(sc[i] - mn);
-        l += p;
-        sc[i] = p * mul[t];
+        for (int i = 0; i < 16; ++i) {
+          const int kl = (i & 3) + 8 * (i >> 2) + 4 * h, key = kb0 + kl;
+          float s = sc[i] * sl2;
+          if (MK == MK_KEY) s += msk[buf][kl];
+          if (MK == MK_FULL) s += key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] * kLog2e : 0.f;
+          if (key >= a.Sk || (a.causal && key > q)) s = -INFINITY;
+          sc[i] = s;
+        }
       }
+      float mb = sc[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mb = fmaxf(mb, sc[i]);
+      mb = xmax32(mb);
+      if (__ballot(mb > m + 8.f)) {
+        const float mn = fmaxf(m, mb);
+        const float alpha = mn == -INFINITY ? 1.f : exp2_(m - mn);
+#pragma unroll
+        for (int db = 0; db < DB; ++db) o[db] *= alpha;
+        l *= alpha;
+        m = mn;
+      }
+      const float ms = m == -INFINITY ? 0.f : m;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float mul[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP) drop4(a.seed, qrow, kb0 + 8 * g + 4 * h, sk4, a.keep, mul);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int i = 4 * g + t;
+          const float p = exp2_(sc[i] - ms);
+          l += p;
+          sc[i] = DROP ? p * mul[t] : p;
+        }
+      }
+      const short* vb = vt[buf];
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(vb, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
     }
-    m = mn;
-    const short* vb = vt[buf];
-#pragma unroll
-    for (int db = 0; db < DB; ++db)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(vb, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
     if (more) {
       store_t32<D>(x0, x1, vt[buf ^ 1]);
-      if (mrow && threadIdx.x < KBLK) msk[buf ^ 1][threadIdx.x] = mv;
+      if (MK == MK_KEY && threadIdx.x < KBLK) msk[buf ^ 1][threadIdx.x] = mv;
 #pragma unroll
       for (int ds = 0; ds < DS; ++ds) kf[ds] = kn[ds];
     }
     __syncthreads();
   }
-  l += __shfl_xor(l, 32, 64);
+  l = xsum32(l);
   if (!qv) return;
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  if (h == 0) a.lse[(int64_t)bh * a.Sq + q] = l > 0.f ? m + __logf(l) : -INFINITY;
+  if (h == 0) a.lse[(int64_t)bh * a.Sq + q] = l > 0.f ? m * kLn2 + __logf(l) : -INFINITY;
   bf16* O = a.o + b * a.ob + hh * a.oh + (int64_t)q * a.os;
 #pragma unroll
   for (int db = 0; db < DB; ++db)
@@ -280,32 +329,34 @@ __global__ void __launch_bounds__(256) flash_dsum_k(FArgs a, float* dsum) {
 // dQ: the forward's walk (lane = query) with P from the saved lse and dP^T = V . dO^T,
 // pipelined like the forward (next block's K / V fragments and K rows in flight,
 // double-buffered K^T image, one barrier per block)
-template <int D, bool DROP>
+template <int D, bool DROP, int MK>
 __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   constexpr bool PF = D <= 32;     // fragments a block ahead only where registers allow 2 waves / SIMD
   __shared__ short kt[2][D * LT];
-  __shared__ float msk[2][KBLK];
+  __shared__ __attribute__((aligned(16))) float msk[2][KBLK];
   const int bh = blockIdx.x, b = bh / a.NH, hh = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int qt0 = blockIdx.y * WQ;
-  const int q = qt0 + 32 * w + r;
+  const int qw0 = qt0 + 32 * w;
+  const int q = qw0 + r;
   const bool qv = q < a.Sq;
   const bf16* Q = a.q + b * a.qb + hh * a.qh;
   const bf16* K = a.k + b * a.kb + hh * a.kh;
   const bf16* V = a.v + b * a.vb + hh * a.vh;
   const bf16* G = a.dout + b * a.gb + hh * a.gh;
-  const float* M = a.mask ? a.mask + b * a.mb + hh * a.mh : nullptr;
-  const bool mrow = M != nullptr && a.mq == 0;
+  const float* M = MK != MK_NONE ? a.mask + b * a.mb + hh * a.mh : nullptr;
+  const float sl2 = a.scale * kLog2e;
   v8s qf[DS], gf[DS];
 #pragma unroll
   for (int ds = 0; ds < DS; ++ds) {
     qf[ds] = qv ? ld8(Q + (int64_t)q * a.qs + 16 * ds + 8 * h) : zero8();
     gf[ds] = qv ? ld8(G + (int64_t)q * a.gs + 16 * ds + 8 * h) : zero8();
   }
-  const float lse = qv ? a.lse[(int64_t)bh * a.Sq + q] : 0.f;
+  // P = exp2(S log2e - lse log2e); a row with no live key (lse = -inf) or past Sq gets +inf: P = 0
+  const float lse0 = qv ? a.lse[(int64_t)bh * a.Sq + q] : -INFINITY;
+  const float lse2 = lse0 == -INFINITY ? INFINITY : lse0 * kLog2e;
   const float Dq = qv ? a.dsum[(int64_t)bh * a.Sq + q] : 0.f;
-  const bool live = qv && lse != -INFINITY;
   v16f o[DB];
 #pragma unroll
   for (int db = 0; db < DB; ++db) o[db] = v16f{0.f};
@@ -316,14 +367,18 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
   v8s kf[DS], vf[DS], x0, x1;
   float mv = 0.f;
   load_t32<D>(K, a.ks, 0, a.Sk, x0, x1);
-  if (mrow && threadIdx.x < KBLK) mv = threadIdx.x < a.Sk ? M[(int64_t)threadIdx.x * a.mk] : 0.f;
+  auto key_mask = [&](int kb) -> float {
+    const int key = kb + (int)threadIdx.x;
+    return key < a.Sk ? M[(int64_t)key * a.mk] * kLog2e : -INFINITY;
+  };
+  if (MK == MK_KEY && threadIdx.x < KBLK) mv = key_mask(0);
 #pragma unroll
   for (int ds = 0; ds < DS; ++ds) {
     kf[ds] = r < a.Sk ? ld8(K + (int64_t)r * a.ks + 16 * ds + 8 * h) : zero8();
     vf[ds] = r < a.Sk ? ld8(V + (int64_t)r * a.vs + 16 * ds + 8 * h) : zero8();
   }
   store_t32<D>(x0, x1, kt[0]);
-  if (mrow && threadIdx.x < KBLK) msk[0][threadIdx.x] = mv;
+  if (MK == MK_KEY && threadIdx.x < KBLK) msk[0][threadIdx.x] = mv;
   __syncthreads();
 
   int buf = 0;
@@ -342,7 +397,7 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
     }
     if (more) {
       load_t32<D>(K, a.ks, nb, a.Sk, x0, x1);
-      if (mrow && threadIdx.x < KBLK) mv = nb + threadIdx.x < a.Sk ? M[(int64_t)(nb + threadIdx.x) * a.mk] : 0.f;
+      if (MK == MK_KEY && threadIdx.x < KBLK) mv = key_mask(nb);
       if (PF) {
         const int kr = nb + r;
         const bool kv = kr < a.Sk;
@@ -353,35 +408,44 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
         }
       }
     }
-    v16f sc = v16f{0.f}, dp = v16f{0.f};
+    if (!(a.causal && kb0 > qw0 + 31)) {
+      v16f sc = v16f{0.f}, dp = v16f{0.f};
 #pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      sc = mfma(kf[ds], qf[ds], sc);
-      dp = mfma(vf[ds], gf[ds], dp);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float mul[4] = {1.f, 1.f, 1.f, 1.f};
-      if (DROP) drop4(a.seed, qrow, kb0 + 8 * g + 4 * h, sk4, a.keep, mul);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int i = 4 * g + t;
-        const int kl = 8 * g + 4 * h + t, key = kb0 + kl;
-        float s = sc[i] * a.scale;
-        if (M != nullptr) s += mrow ? msk[buf][kl] : (key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] : 0.f);
-        const bool ok = live && key < a.Sk && !(a.causal && key > q);
-        const float p = ok ? __expf(s - lse) : 0.f;
-        sc[i] = p * (dp[i] * mul[t] - Dq) * a.scale;
+      for (int ds = 0; ds < DS; ++ds) {
+        sc = mfma(kf[ds], qf[ds], sc);
+        dp = mfma(vf[ds], gf[ds], dp);
       }
+      const bool full = MK != MK_FULL && nb <= a.Sk && !(a.causal && kb0 + KBLK - 1 > qw0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float mul[4] = {1.f, 1.f, 1.f, 1.f};
+        if (DROP) drop4(a.seed, qrow, kb0 + 8 * g + 4 * h, sk4, a.keep, mul);
+        float4 mm = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (MK == MK_KEY) mm = *reinterpret_cast<const float4*>(&msk[buf][8 * g + 4 * h]);
+        const float mk4[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int i = 4 * g + t;
+          float x = fmaf(sc[i], sl2, mk4[t] - lse2);
+          if (!full) {
+            const int key = kb0 + 8 * g + 4 * h + t;
+            if (MK == MK_FULL) x += key < a.Sk && qv ? M[(int64_t)q * a.mq + (int64_t)key * a.mk] * kLog2e : 0.f;
+            if (key >= a.Sk || (a.causal && key > q)) x = -INFINITY;
+          }
+          const float p = exp2_(x);
+          // dS / scale (the scale goes on at the dQ store)
+          sc[i] = p * (DROP ? fmaf(dp[i], mul[t], -Dq) : dp[i] - Dq);
+        }
+      }
+      const short* kb = kt[buf];
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(kb, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
     }
-    const short* kb = kt[buf];
-#pragma unroll
-    for (int db = 0; db < DB; ++db)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) o[db] = mfma(lds_perm(kb, db * 32 + r, s, h), pack_acc(sc, s), o[db]);
     if (more) {
       store_t32<D>(x0, x1, kt[buf ^ 1]);
-      if (mrow && threadIdx.x < KBLK) msk[buf ^ 1][threadIdx.x] = mv;
+      if (MK == MK_KEY && threadIdx.x < KBLK) msk[buf ^ 1][threadIdx.x] = mv;
       if (PF) {
 #pragma unroll
         for (int ds = 0; ds < DS; ++ds) { kf[ds] = kn[ds]; vf[ds] = vn[ds]; }
@@ -394,7 +458,7 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
 #pragma unroll
   for (int db = 0; db < DB; ++db)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) store_rows4(dQ + db * 32, o[db], g, h, 1.f);
+    for (int g = 0; g < 4; ++g) store_rows4(dQ + db * 32, o[db], g, h, a.scale);
 }
 
 // -------------------------------------------------------------------------------------
@@ -403,23 +467,26 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
 // dV^T += dO^T . P_drop and dK^T += Q^T . dS with dO^T / Q^T staged in double-buffered
 // LDS from registers loaded a block ahead (the Q / dO fragments too at D = 32; above
 // that they would cost the second wave per SIMD).
-template <int D, bool DROP>
-__global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
+template <int D, bool DROP, int MK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1))) flash_dkdv_k(FArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   constexpr bool PF = D <= 32;
   __shared__ short qt[2][D * LT];
   __shared__ short gt[2][D * LT];
-  __shared__ float ls[2][KBLK], dl[2][KBLK];
+  __shared__ __attribute__((aligned(16))) float ls[2][KBLK];
+  __shared__ __attribute__((aligned(16))) float dl[2][KBLK];
   const int bh = blockIdx.x, b = bh / a.NH, hh = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int kt0 = blockIdx.y * WQ;
-  const int key = kt0 + 32 * w + r;
+  const int kw0 = kt0 + 32 * w;
+  const int key = kw0 + r;
   const bool kv = key < a.Sk;
   const bf16* Q = a.q + b * a.qb + hh * a.qh;
   const bf16* K = a.k + b * a.kb + hh * a.kh;
   const bf16* V = a.v + b * a.vb + hh * a.vh;
   const bf16* G = a.dout + b * a.gb + hh * a.gh;
-  const float* M = a.mask ? a.mask + b * a.mb + hh * a.mh : nullptr;
+  const float* M = MK != MK_NONE ? a.mask + b * a.mb + hh * a.mh : nullptr;
+  const float sl2 = a.scale * kLog2e;
   const float* LSE = a.lse + (int64_t)bh * a.Sq;
   const float* DSUM = a.dsum + (int64_t)bh * a.Sq;
   v8s kf[DS], vf[DS];
@@ -428,7 +495,8 @@ __global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
     kf[ds] = kv ? ld8(K + (int64_t)key * a.ks + 16 * ds + 8 * h) : zero8();
     vf[ds] = kv ? ld8(V + (int64_t)key * a.vs + 16 * ds + 8 * h) : zero8();
   }
-  const float mkey = (M != nullptr && a.mq == 0 && kv) ? M[(int64_t)key * a.mk] : 0.f;
+  // this lane's key-mask term (log2 domain); a key past Sk gets -inf: P = 0
+  const float mkey = !kv ? -INFINITY : (MK == MK_KEY ? M[(int64_t)key * a.mk] * kLog2e : 0.f);
   v16f dvt[DB], dkt[DB];
 #pragma unroll
   for (int db = 0; db < DB; ++db) { dvt[db] = v16f{0.f}; dkt[db] = v16f{0.f}; }
@@ -451,15 +519,16 @@ __global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
   }
 
   v8s x0, x1, y0, y1, qf[DS], gf[DS];
-  float lv = -INFINITY, dv = 0.f;
+  float lv = INFINITY, dv = 0.f;
   auto fetch = [&](int qb0) {
     load_t32<D>(Q, a.qs, qb0, a.Sq, x0, x1);
     load_t32<D>(G, a.gs, qb0, a.Sq, y0, y1);
     if (threadIdx.x < KBLK) {
+      // lse in log2 units; +inf (P = 0) for rows past Sq and rows with no live key
       const int qq = qb0 + threadIdx.x;
-      const bool ok = qq < a.Sq;
-      lv = ok ? LSE[qq] : -INFINITY;
-      dv = ok ? DSUM[qq] : 0.f;
+      const float x = qq < a.Sq ? LSE[qq] : -INFINITY;
+      lv = x == -INFINITY ? INFINITY : x * kLog2e;
+      dv = qq < a.Sq ? DSUM[qq] : 0.f;
     }
   };
   auto frags = [&](int qb0) {
@@ -498,34 +567,46 @@ __global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
       fetch(nb);
       if (PF) frags(nb);
     }
-    v16f sc = v16f{0.f}, dp = v16f{0.f};
+    // causal: a query block wholly before this wave's keys sees none of them
+    if (!(a.causal && kw0 > qb0 + 31)) {
+      v16f sc = v16f{0.f}, dp = v16f{0.f};
 #pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      sc = mfma(qa[ds], kf[ds], sc);
-      dp = mfma(ga[ds], vf[ds], dp);
-    }
-    v16f pd;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int ql = (i & 3) + 8 * (i >> 2) + 4 * h, qq = qb0 + ql;
-      const float lq = ls[buf][ql];
-      float s = sc[i] * a.scale;
-      if (M != nullptr) s += a.mq == 0 ? mkey : (kv && qq < a.Sq ? M[(int64_t)qq * a.mq + (int64_t)key * a.mk] : 0.f);
-      const bool ok = kv && qq < a.Sq && lq != -INFINITY && !(a.causal && key > qq);
-      const float p = ok ? __expf(s - lq) : 0.f;
-      const float mul = (DROP && ok) ? drop1(a.seed, (uint64_t)bh * a.Sq + qq, key, sk4, a.keep) : 1.f;
-      pd[i] = p * mul;
-      sc[i] = p * (dp[i] * mul - dl[buf][ql]) * a.scale;
-    }
-    const short* gb = gt[buf];
-    const short* qb = qt[buf];
-#pragma unroll
-    for (int db = 0; db < DB; ++db)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        dvt[db] = mfma(lds_perm(gb, db * 32 + r, s, h), pack_acc(pd, s), dvt[db]);
-        dkt[db] = mfma(lds_perm(qb, db * 32 + r, s, h), pack_acc(sc, s), dkt[db]);
+      for (int ds = 0; ds < DS; ++ds) {
+        sc = mfma(qa[ds], kf[ds], sc);
+        dp = mfma(ga[ds], vf[ds], dp);
       }
+      const bool full = MK != MK_FULL && !(a.causal && kw0 + 31 > qb0);
+      v16f pd;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 l4 = *reinterpret_cast<const float4*>(&ls[buf][8 * g + 4 * h]);
+        const float4 d4 = *reinterpret_cast<const float4*>(&dl[buf][8 * g + 4 * h]);
+        const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int i = 4 * g + t, qq = qb0 + 8 * g + 4 * h + t;
+          float x = fmaf(sc[i], sl2, mkey - lq[t]);
+          if (!full) {
+            if (MK == MK_FULL) x += kv && qq < a.Sq ? M[(int64_t)qq * a.mq + (int64_t)key * a.mk] * kLog2e : 0.f;
+            if (a.causal && key > qq) x = -INFINITY;
+          }
+          const float p = exp2_(x);
+          const float mul = DROP ? drop1(a.seed, (uint64_t)bh * a.Sq + qq, key, sk4, a.keep) : 1.f;
+          pd[i] = DROP ? p * mul : p;
+          // dS / scale (the scale goes on at the dK store)
+          sc[i] = p * (DROP ? fmaf(dp[i], mul, -dq4[t]) : dp[i] - dq4[t]);
+        }
+      }
+      const short* gb = gt[buf];
+      const short* qb = qt[buf];
+#pragma unroll
+      for (int db = 0; db < DB; ++db)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          dvt[db] = mfma(lds_perm(gb, db * 32 + r, s, h), pack_acc(pd, s), dvt[db]);
+          dkt[db] = mfma(lds_perm(qb, db * 32 + r, s, h), pack_acc(sc, s), dkt[db]);
+        }
+    }
     if (more) put(buf ^ 1);
     __syncthreads();
   }
@@ -536,17 +617,41 @@ __global__ void __launch_bounds__(256) flash_dkdv_k(FArgs a) {
   for (int db = 0; db < DB; ++db)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      store_rows4(dK + db * 32, dkt[db], g, h, 1.f);
+      store_rows4(dK + db * 32, dkt[db], g, h, a.scale);
       store_rows4(dV + db * 32, dvt[db], g, h, 1.f);
     }
 }
 
+static int mask_mode(const FArgs& a) { return a.mask == nullptr ? MK_NONE : (a.mq == 0 ? MK_KEY : MK_FULL); }
+
+template <int D, int MK>
+static void fwd_dm(const FArgs& a, hipStream_t st) {
+  dim3 grid((unsigned)(a.B * a.NH), (unsigned)((a.Sq + WQ - 1) / WQ));
+  if (a.keep < 1.f) hipLaunchKernelGGL((flash_fwd_k<D, true, MK>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((flash_fwd_k<D, false, MK>), grid, dim3(256), 0, st, a);
+}
+
 template <int D>
 static int fwd_d(const FArgs& a, hipStream_t st) {
-  dim3 grid((unsigned)(a.B * a.NH), (unsigned)((a.Sq + WQ - 1) / WQ));
-  if (a.keep < 1.f) hipLaunchKernelGGL((flash_fwd_k<D, true>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((flash_fwd_k<D, false>), grid, dim3(256), 0, st, a);
+  switch (mask_mode(a)) {
+    case MK_NONE: fwd_dm<D, MK_NONE>(a, st); break;
+    case MK_KEY: fwd_dm<D, MK_KEY>(a, st); break;
+    default: fwd_dm<D, MK_FULL>(a, st); break;
+  }
   return (int)hipGetLastError();
+}
+
+template <int D, int MK>
+static void bwd_dm(const FArgs& b, hipStream_t st) {
+  dim3 gq((unsigned)(b.B * b.NH), (unsigned)((b.Sq + WQ - 1) / WQ));
+  dim3 gk((unsigned)(b.B * b.NH), (unsigned)((b.Sk + WQ - 1) / WQ));
+  if (b.keep < 1.f) {
+    hipLaunchKernelGGL((flash_dq_k<D, true, MK>), gq, dim3(256), 0, st, b);
+    hipLaunchKernelGGL((flash_dkdv_k<D, true, MK>), gk, dim3(256), 0, st, b);
+  } else {
+    hipLaunchKernelGGL((flash_dq_k<D, false, MK>), gq, dim3(256), 0, st, b);
+    hipLaunchKernelGGL((flash_dkdv_k<D, false, MK>), gk, dim3(256), 0, st, b);
+  }
 }
 
 template <int D>
@@ -555,16 +660,69 @@ static int bwd_d(const FArgs& a, float* dsum, hipStream_t st) {
   hipLaunchKernelGGL((flash_dsum_k<D>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, st, a, dsum);
   FArgs b = a;
   b.dsum = dsum;
-  dim3 gq((unsigned)(a.B * a.NH), (unsigned)((a.Sq + WQ - 1) / WQ));
-  dim3 gk((unsigned)(a.B * a.NH), (unsigned)((a.Sk + WQ - 1) / WQ));
-  if (a.keep < 1.f) {
-    hipLaunchKernelGGL((flash_dq_k<D, true>), gq, dim3(256), 0, st, b);
-    hipLaunchKernelGGL((flash_dkdv_k<D, true>), gk, dim3(256), 0, st, b);
-  } else {
-    hipLaunchKernelGGL((flash_dq_k<D, false>), gq, dim3(256), 0, st, b);
-    hipLaunchKernelGGL((flash_dkdv_k<D, false>), gk, dim3(256), 0, st, b);
+  switch (mask_mode(a)) {
+    case MK_NONE: bwd_dm<D, MK_NONE>(b, st); break;
+    case MK_KEY: bwd_dm<D, MK_KEY>(b, st); break;
+    default: bwd_dm<D, MK_FULL>(b, st); break;
   }
   return (int)hipGetLastError();
+}
+
+// ring attention (parallel/ring_attention.py): merge one key block's (o_b, lse_b) into the
+// running fp32 (o, lse) by the log-sum-exp rule; one thread per (b, s, h) row of D values.
+// o: [B, S, NH, D] fp32; ob: [B, S, NH, D] bf16; lse / lb: [B, NH, S].
+__global__ void __launch_bounds__(256) lse_merge_k(float* __restrict__ o, float* __restrict__ lse,
+                                                   const bf16* __restrict__ ob, const float* __restrict__ lb,
+                                                   int B, int S, int NH, int D) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * S * NH) return;
+  const int hh = (int)(t % NH);
+  const int64_t bs = t / NH;
+  const int ss = (int)(bs % S), b = (int)(bs / S);
+  const int64_t li = ((int64_t)b * NH + hh) * S + ss;
+  const float la = lse[li], lbb = lb[li];
+  const float m = fmaxf(la, lbb);
+  if (m == -INFINITY) return;
+  const float nw = m + __logf(__expf(la - m) + __expf(lbb - m));
+  const float wa = __expf(la - nw), wb = __expf(lbb - nw);
+  float* orow = o + t * D;
+  const bf16* brow = ob + t * D;
+  for (int c = 0; c < D; c += 8) {
+    const v8s x = ld8(brow + c);
+    float4* p = reinterpret_cast<float4*>(orow + c);
+    float4 u = p[0], v = p[1];
+    u.x = u.x * wa + bf16_bits_to_f((unsigned short)x[0]) * wb;
+    u.y = u.y * wa + bf16_bits_to_f((unsigned short)x[1]) * wb;
+    u.z = u.z * wa + bf16_bits_to_f((unsigned short)x[2]) * wb;
+    u.w = u.w * wa + bf16_bits_to_f((unsigned short)x[3]) * wb;
+    v.x = v.x * wa + bf16_bits_to_f((unsigned short)x[4]) * wb;
+    v.y = v.y * wa + bf16_bits_to_f((unsigned short)x[5]) * wb;
+    v.z = v.z * wa + bf16_bits_to_f((unsigned short)x[6]) * wb;
+    v.w = v.w * wa + bf16_bits_to_f((unsigned short)x[7]) * wb;
+    p[0] = u;
+    p[1] = v;
+  }
+  lse[li] = nw;
+}
+
+// acc[r][c] += x[r][c] (fp32 += bf16) over rows x cols (cols % 8 == 0), row strides lda / ldx
+__global__ void __launch_bounds__(256) acc_rows_k(float* __restrict__ acc, int64_t lda, const bf16* __restrict__ x,
+                                                  int64_t ldx, int64_t rows, int cols) {
+  const int c8 = cols / 8;
+  const int64_t n = rows * c8;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / c8;
+    const int c = (int)(t - r * c8) * 8;
+    const v8s v = ld8(x + r * ldx + c);
+    float4* p = reinterpret_cast<float4*>(acc + r * lda + c);
+    float4 u = p[0], w = p[1];
+    u.x += bf16_bits_to_f((unsigned short)v[0]); u.y += bf16_bits_to_f((unsigned short)v[1]);
+    u.z += bf16_bits_to_f((unsigned short)v[2]); u.w += bf16_bits_to_f((unsigned short)v[3]);
+    w.x += bf16_bits_to_f((unsigned short)v[4]); w.y += bf16_bits_to_f((unsigned short)v[5]);
+    w.z += bf16_bits_to_f((unsigned short)v[6]); w.w += bf16_bits_to_f((unsigned short)v[7]);
+    p[0] = u;
+    p[1] = w;
+  }
 }
 
 }  // namespace flash
@@ -626,4 +784,23 @@ HETU_API int hetu_flash_bwd(const void* q, const void* k, const void* v, const i
   if (D == 32) return bwd_d<32>(a, dsum, st);
   if (D == 64) return bwd_d<64>(a, dsum, st);
   return bwd_d<128>(a, dsum, st);
+}
+
+HETU_API int hetu_flash_lse_merge(float* o, float* lse, const void* ob, const float* lb, int B, int S, int NH, int D,
+                                  hipStream_t st) {
+  if (D % 8) return (int)hipErrorInvalidValue;
+  const int64_t rows = (int64_t)B * S * NH;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(lse_merge_k, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, o, lse, (const bf16*)ob, lb,
+                     B, S, NH, D);
+  return (int)hipGetLastError();
+}
+
+HETU_API int hetu_acc_rows_bf16(float* acc, int64_t lda, const void* x, int64_t ldx, int64_t rows, int cols,
+                                hipStream_t st) {
+  if (cols % 8 || lda % 4 || ldx % 8) return (int)hipErrorInvalidValue;
+  if (rows <= 0 || cols <= 0) return 0;
+  const int g = stream_grid(rows * (cols / 8), 256, 4);
+  hipLaunchKernelGGL(acc_rows_k, dim3(g), dim3(256), 0, st, acc, lda, (const bf16*)x, ldx, rows, cols);
+  return (int)hipGetLastError();
 }

@@ -298,6 +298,25 @@ def flash_bwd(dout, q, k, v, o, lse, mask=None, causal=False, keep=1.0, seed=0, 
     return dq, dk, dv
 
 
+def lse_merge(o, lse, ob, lb):
+    """ring attention merge: (o fp32 [B, S, NH, D], lse fp32 [B, NH, S]) <- log-sum-exp
+    combination with one block's (ob bf16 [B, S, NH, D] dense, lb [B*NH*S]); in place"""
+    B, S, NH, D = o.shape
+    assert o.is_contiguous() and lse.is_contiguous() and ob.is_contiguous() and ob.dtype == torch.bfloat16
+    f = fn('hetu_flash_lse_merge', [P, P, P, P, I32, I32, I32, I32, P])
+    check(f(o.data_ptr(), lse.data_ptr(), ob.data_ptr(), lb.data_ptr(), B, S, NH, D, stream_ptr()), 'lse_merge')
+    record_native('lse_merge')
+
+
+def acc_rows(acc, x):
+    """acc (fp32 [R, C], unit column stride) += x (bf16 [R, C], unit column stride); in place"""
+    R, C = x.shape
+    assert acc.shape == x.shape and acc.stride(1) == 1 and x.stride(1) == 1 and x.dtype == torch.bfloat16
+    f = fn('hetu_acc_rows_bf16', [P, I64, P, I64, I64, I32, P])
+    check(f(acc.data_ptr(), acc.stride(0), x.data_ptr(), x.stride(0), R, C, stream_ptr()), 'acc_rows')
+    record_native('acc_rows')
+
+
 def packed_heads(qkv, B, S, NH):
     """[B*S, 3H] packed projection -> q, k, v as [B, NH, S, D] views (no copies)"""
     H = qkv.shape[1] // 3

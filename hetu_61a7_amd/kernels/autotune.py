@@ -45,7 +45,14 @@ def choose(key, candidates, mode='auto'):
             names = hw
     from . import deterministic
     if deterministic():
-        return names[0]       # fixed choice: the hand-written kernel every call site lists first
+        # fixed choice: the first hand-written kernel (in the order every call site lists
+        # them) that takes the shape
+        if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+            for n in names:
+                if candidates[n]() is not None:
+                    _decisions[key] = n
+                    return n
+        return names[0]
     if len(names) == 1 or not torch.cuda.is_available() or torch.cuda.is_current_stream_capturing():
         return names[0]
     live = []

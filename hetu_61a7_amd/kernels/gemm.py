@@ -67,6 +67,8 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
                     cands['hip_sk%d' % s_] = (lambda s_=s_: gemm_mfma.gemm(A2, B2, splitk=s_))
         if A2.dim() == 2 and B2.dim() == 2 and A2.shape[0] * B2.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
+        # any shape: zero-padded aligned operands on the MFMA tile (last hand-written resort)
+        cands['hip_pad'] = lambda: gemm_mfma.padded(A2, B2, bias=bias, act=activation)
         cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
         if bias is not None:
             # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
@@ -75,6 +77,8 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
         c = choose(key, cands, _MFMA)
         if c.startswith('hip'):
             y = cands[c]()
+            if y is None:
+                y = gemm_mfma.padded(A2, B2, bias=bias, act=activation)
             if y is not None:
                 return y
             _fallback('matmul')
@@ -136,8 +140,20 @@ def bmm(a, b, ta=False, tb=False):
         from .autotune import choose
         key = ('bmm', _sig(a), _sig(b), ta, tb)
         hip = lambda: gemm_mfma.try_bmm(a, b, ta, tb)
-        if choose(key, {'hip': hip, 'vendor': lambda: torch.matmul(_tr(a, ta), _tr(b, tb))}, _MFMA) == 'hip':
-            y = hip()
+
+        def hip_pad():
+            A, B = _tr(a, ta), _tr(b, tb)
+            if A.dim() < 3 or A.shape[:-2] != B.shape[:-2]:
+                return None
+            lead = A.shape[:-2]
+            y = gemm_mfma.padded(A.reshape(-1, *A.shape[-2:]), B.reshape(-1, *B.shape[-2:]))
+            return None if y is None else y.view(*lead, *y.shape[-2:])
+        c = choose(key, {'hip': hip, 'hip_pad': hip_pad, 'vendor': lambda: torch.matmul(_tr(a, ta), _tr(b, tb))},
+                   _MFMA)
+        if c.startswith('hip'):
+            y = hip() if c == 'hip' else None
+            if y is None:
+                y = hip_pad()
             if y is not None:
                 return y
             _fallback('bmm')
@@ -206,7 +222,7 @@ def matmul_into(a, b, ta, tb, out):
     the MFMA kernel writes fp32 directly; the library path computes in the
     input dtype and converts once.  Returns ``out``."""
     a, b = _match(a, b)
-    if native(a) and a.dtype == torch.bfloat16 and _MFMA not in ('off', 'vendor'):
+    if native(a) and a.dtype in (torch.bfloat16, torch.float32) and _MFMA not in ('off', 'vendor'):
         from . import gemm_mfma
         from .autotune import choose
 
@@ -219,7 +235,12 @@ def matmul_into(a, b, ta, tb, out):
         # weight gradients: small M x N output, long K (= tokens): too few 128x128
         # tiles to fill 256 CUs -> split K over more workgroups (fp32 slab + reduce)
         A, B = _tr(a, ta), _tr(b, tb)
-        if A.dim() == 2:
+        if A.dim() == 2 and a.dtype == torch.float32:
+            # fp32 (the reference's precision): the exact-fp32 MFMA kernel, or the one-wave
+            # kernel for small outputs
+            if A.shape[0] * B.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
+                cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, out=out)
+        elif A.dim() == 2:
             M, K, N = A.shape[0], A.shape[1], B.shape[1]
             tiles = -(-M // 128) * -(-N // 128)
             for s in (2, 3, 4, 6, 8):
@@ -254,11 +275,15 @@ def matmul_into(a, b, ta, tb, out):
             if A.stride(0) == 1 and B.stride(1) == 1 and M % 64 == 0 and N % 64 == 0 and K >= 4096:
                 # both operands token-major (weight gradients): the 64x64 split-K tile
                 cands['hip_lk'] = lambda: gemm_mfma.wgrad_longk(A.t(), B, out)
+        if A.dim() == 2:
+            cands['hip_pad'] = lambda: gemm_mfma.padded(A, B, out=out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
         c = choose(key, cands, _MFMA)
         if c != 'vendor' and cands[c]() is not None:
             return out
         if c.startswith('hip'):
+            if A.dim() == 2 and gemm_mfma.padded(A, B, out=out) is not None:
+                return out
             _fallback('matmul_into')
         return vendor()
     return _vendor_into(_tr(a, ta), _tr(b, tb), out)
@@ -314,10 +339,13 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
             cands['hip96'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=5)
         if A.shape[0] * B.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, cin=acc, beta=1.0)
+        cands['hip_pad'] = lambda: gemm_mfma.padded(A, B, cin=acc, beta=1.0)
         ch = choose(key, cands, _MFMA)
         dst[0] = acc
         if ch != 'vendor':
             y = cands[ch]()
+            if y is None and ch.startswith('hip'):
+                y = gemm_mfma.padded(A, B, cin=acc, beta=1.0)
             if y is not None:
                 return y
             _fallback('matmul_acc')

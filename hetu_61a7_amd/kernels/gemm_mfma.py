@@ -72,7 +72,11 @@ def gemm_f32(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None,
         return None
     if out is None:
         shape = (batch, M, N) if a.dim() == 3 else (M, N)
-        out = (torch.zeros if accumulate else torch.empty)(shape, dtype=torch.float32, device=a.device)
+        if accumulate:
+            from .tensor import zeros
+            out = zeros(shape, torch.float32, a.device)
+        else:
+            out = _NA.empty(shape, dtype=torch.float32, device=a.device)
     if out.dtype != torch.float32 or out.stride(-1) != 1 or (out.dim() == 3 and out.dim() != a.dim()):
         return None
     ldc = out.stride(-2) if M > 1 else N
@@ -134,7 +138,11 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
     odt = out_dtype or (out.dtype if out is not None else torch.bfloat16)
     if out is None:
         shape = (batch, M, N) if a.dim() == 3 else (M, N)
-        out = (torch.zeros if accumulate else torch.empty)(shape, dtype=odt, device=a.device)
+        if accumulate:
+            from .tensor import zeros
+            out = zeros(shape, odt, a.device)
+        else:
+            out = _NA.empty(shape, dtype=odt, device=a.device)
     if out.stride(-1) != 1 or (out.dim() == 3 and out.dim() != a.dim()):
         return _reject(5, a, b, out)
     if accumulate and splitk == 1 and out.dtype != torch.float32:
@@ -229,6 +237,46 @@ def gemm_small(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=Non
             int(out.dtype == torch.float32), int(cin_t is not None and cin_t.dtype == torch.float32), int(bias_on_m),
             stream_ptr()), 'gemm_small')
     record_native('gemm_small')
+    return out
+
+
+def padded(a, b, out=None, bias=None, act=None, cin=None, beta=0.0):
+    """Hand-written product of operands no MFMA tile takes as they are (a contiguous extent
+    or leading dimension not a multiple of 16 bytes, a misaligned base, a few output
+    columns): zero-padded aligned copies [.., M, Kp] @ [.., Kp, Np] (natively filled and
+    copied) on the MFMA tile, the [.., M, N] corner copied into ``out`` (or a new dense
+    tensor).  2-D or batched 3-D, bf16 or fp32; ``cin`` (beta = 1) is padded the same way."""
+    from .tensor import zeros, copy_into
+    if a.dim() != b.dim() or a.dim() not in (2, 3) or a.dtype != b.dtype or \
+            a.dtype not in (torch.bfloat16, torch.float32) or not a.is_cuda:
+        return None
+    q = 8 if a.dtype == torch.bfloat16 else 4
+    lead = tuple(a.shape[:-2])
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    Kp, Np = -(-K // q) * q, -(-N // q) * q
+    ap = zeros(lead + (M, Kp), a.dtype, a.device)
+    copy_into(ap[..., :K], a)
+    bp = zeros(lead + (Kp, Np), b.dtype, b.device)
+    copy_into(bp[..., :K, :N], b)
+    bias_p = None
+    if bias is not None:
+        bias_p = zeros((Np,), torch.float32, a.device)
+        copy_into(bias_p[:N], bias.reshape(-1))
+    cin_p = None
+    if cin is not None and beta != 0.0:
+        c = cin.expand(lead + (M, N)) if tuple(cin.shape) != lead + (M, N) else cin
+        cin_p = zeros(lead + (M, Np), c.dtype, a.device)
+        copy_into(cin_p[..., :N], c)
+    odt = out.dtype if out is not None else a.dtype
+    op = _NA.empty(lead + (M, Np), dtype=odt, device=a.device)
+    if gemm(ap, bp, out=op, bias=bias_p, act=act, cin=cin_p, beta=beta if cin_p is not None else 0.0) is None:
+        return None
+    if out is None:
+        if Np == N:
+            return op
+        out = _NA.empty(lead + (M, N), dtype=odt, device=a.device)
+    copy_into(out, op[..., :N])
     return out
 
 

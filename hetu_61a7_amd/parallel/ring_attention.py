@@ -12,11 +12,14 @@ point-to-point link per step and the transfer hides behind the block's
 matmuls).  Partial results are merged with the online-softmax rule, so no
 rank ever holds more than an [S/P, S/P] score tile per head, and the saved
 state for backward is just O and the row log-sum-exp.  Each non-causal block
-pair runs through the fused MFMA attention kernels (``kernels/attention.py``
-``attention_{fwd,bwd}_blocks``: bf16, head dim 64, S/P <= 128) with Q and the
-travelling K/V block as separate strided operands; the block's (out, lse)
-is merged in fp32 with ``logaddexp``.  The backward kernel is handed the
-GLOBAL out and lse, which makes its dQ/dK/dV the exact per-block terms.
+pair runs through the general flash kernels (``kernels/attention.py``
+``flash_{fwd,bwd}``: bf16, any S/P, head dim 32 / 64 / 128, the causal diagonal
+block included) with Q and the travelling K/V block read in place as strided
+head views; the block's (out, lse) is merged into the fp32 running output by a
+log-sum-exp merge kernel.  The backward kernels are handed the GLOBAL out and
+lse, which makes their dQ/dK/dV the exact per-block terms; fp32 accumulators
+take them through a row-accumulate kernel.  CPU tensors (the gloo tests) take
+the torch block math below.
 
 Backward re-runs the ring: the K/V block travels together with an fp32 dK/dV
 accumulator; every rank adds its queries' contribution to the block it holds,
@@ -34,6 +37,7 @@ import math
 
 import torch
 
+from .. import native_array as _NA
 from ..ops.node import Op
 from ..ops.nn import AuxResult
 
@@ -52,7 +56,7 @@ def _rows(x):
 def _rotate(comm, tensors):
     """Send each tensor to rank+1, receive the same-shaped tensors from rank-1."""
     P, r = comm.nrank, comm.rank
-    outs = [torch.empty_like(t) for t in tensors]
+    outs = [_NA.empty_like(t) for t in tensors]
     ops = []
     for t, o in zip(tensors, outs):
         ops += [('send', t.contiguous(), (r + 1) % P), ('recv', o, (r - 1) % P)]
@@ -107,9 +111,109 @@ def _block_bwd(dout, q, k, v, out, lse, kmask, B, S_l, NH, D, scale, diag):
     return _rows(torch.matmul(ds, kh)), _rows(torch.matmul(ds.transpose(-1, -2), qh)), _rows(dv)
 
 
+def _flash_ring_ok(qkv, NH):
+    from ..kernels import attention as KA
+    from ..kernels import native
+    H = qkv.shape[1] // 3
+    return (native(qkv) and qkv.dtype == torch.bfloat16 and H % NH == 0 and (H // NH) in KA.FLASH_D
+            and qkv.stride(1) == 1 and qkv.stride(0) % 8 == 0 and qkv.data_ptr() % 16 == 0)
+
+
+def _kv_heads(kv, B, S_l, NH, D):
+    """[B*S_l, 2H] travelling block -> k, v as [B, NH, S_l, D] views"""
+    x = kv.view(B, S_l, 2, NH, D)
+    return x[:, :, 0].permute(0, 2, 1, 3), x[:, :, 1].permute(0, 2, 1, 3)
+
+
+def _send_copy(x):
+    from ..kernels import tensor as KT
+    return KT.copy_into(_NA.empty(tuple(x.shape), dtype=x.dtype, device=x.device), x)
+
+
+def _ring_fwd_flash(qkv, kmask, comm, B, S_l, NH, causal, scale):
+    from ..kernels import attention as KA
+    from ..kernels import tensor as KT
+    from ..kernels import elementwise as KE
+    P, r = comm.nrank, comm.rank
+    H = qkv.shape[1] // 3
+    D = H // NH
+    q4, _, _ = KA.packed_heads(qkv, B, S_l, NH)
+    o = KT.zeros((B, S_l, NH, D), dtype=torch.float32, device=qkv.device)
+    lse = KT.fill_(_NA.empty((B, NH, S_l), dtype=torch.float32, device=qkv.device), float('-inf'))
+    kv = qkv[:, H:]
+    km = kmask.contiguous() if kmask is not None else None
+    for s in range(P):
+        j = (r - s) % P
+        reqs, nxt = [], None
+        if s < P - 1:
+            send = [kv if kv.is_contiguous() else _send_copy(kv)] + ([km] if km is not None else [])
+            nxt, reqs = _rotate(comm, send)
+        if not (causal and j > r):
+            k4, v4 = _kv_heads(kv, B, S_l, NH, D)
+            m4 = km.reshape(B, 1, 1, S_l) if km is not None else None
+            ob, lb = KA.flash_fwd(q4, k4, v4, m4, causal and j == r, 1.0, 0, scale)
+            KA.lse_merge(o, lse, ob.permute(0, 2, 1, 3), lb)
+        for w in reqs:
+            w.wait()
+        if nxt is not None:
+            kv = nxt[0]
+            km = nxt[1] if km is not None else None
+    return KE.cast(o.reshape(B * S_l, H), qkv.dtype), lse
+
+
+def _ring_bwd_flash(dout, qkv, kmask, out, lse, comm, B, S_l, NH, causal, scale):
+    from ..kernels import attention as KA
+    from ..kernels import tensor as KT
+    P, r = comm.nrank, comm.rank
+    H = qkv.shape[1] // 3
+    D = H // NH
+    q4, _, _ = KA.packed_heads(qkv, B, S_l, NH)
+    if dout.dtype != qkv.dtype or not dout.is_contiguous():
+        dout = KT.copy_into(_NA.empty(tuple(dout.shape), dtype=qkv.dtype, device=dout.device), dout)
+    if not out.is_contiguous():
+        out = _send_copy(out)
+    g4 = dout.view(B, S_l, NH, D).permute(0, 2, 1, 3)
+    o4 = out.view(B, S_l, NH, D).permute(0, 2, 1, 3)
+    lsef = lse.reshape(-1)
+    dq = KT.zeros((B * S_l, H), dtype=torch.float32, device=qkv.device)
+    dkv = KT.zeros((B * S_l, 2 * H), dtype=torch.float32, device=qkv.device)
+    kv = qkv[:, H:]
+    km = kmask.contiguous() if kmask is not None else None
+    rows = lambda t: t.permute(0, 2, 1, 3).reshape(B * S_l, H)
+    for s in range(P):
+        j = (r - s) % P
+        if not (causal and j > r):
+            k4, v4 = _kv_heads(kv, B, S_l, NH, D)
+            m4 = km.reshape(B, 1, 1, S_l) if km is not None else None
+            gq, gk, gv = KA.flash_bwd(g4, q4, k4, v4, o4, lsef, m4, causal and j == r, 1.0, 0, scale)
+            KA.acc_rows(dq, rows(gq))
+            KA.acc_rows(dkv[:, :H], rows(gk))
+            KA.acc_rows(dkv[:, H:], rows(gv))
+        if P == 1:
+            break
+        if s < P - 1:
+            send = [dkv, kv if kv.is_contiguous() else _send_copy(kv)] + ([km] if km is not None else [])
+        else:
+            send = [dkv]
+        nxt, reqs = _rotate(comm, send)
+        for w in reqs:
+            w.wait()
+        dkv = nxt[0]
+        if s < P - 1:
+            kv = nxt[1]
+            km = nxt[2] if km is not None else None
+    res = _NA.empty((B * S_l, 3 * H), dtype=qkv.dtype, device=qkv.device)
+    KT.copy_into(res[:, :H], dq)
+    KT.copy_into(res[:, H:], dkv)
+    return res
+
+
 def ring_attention_fwd(qkv, kmask, comm, B, S_l, NH, causal=False, scale=None):
     """qkv [B*S_l, 3H] (this rank's tokens), kmask [B, S_l] or None.
     Returns (out [B*S_l, H] in qkv's dtype, lse [B, NH, S_l] fp32)."""
+    if _flash_ring_ok(qkv, NH):
+        return _ring_fwd_flash(qkv, kmask, comm, B, S_l, NH, causal,
+                               scale or 1.0 / math.sqrt(qkv.shape[1] // 3 // NH))
     P, r = comm.nrank, comm.rank
     H = qkv.shape[1] // 3
     D = H // NH
@@ -139,6 +243,9 @@ def ring_attention_fwd(qkv, kmask, comm, B, S_l, NH, causal=False, scale=None):
 
 def ring_attention_bwd(dout, qkv, kmask, out, lse, comm, B, S_l, NH, causal=False, scale=None):
     """Returns dqkv [B*S_l, 3H] in qkv's dtype."""
+    if _flash_ring_ok(qkv, NH):
+        return _ring_bwd_flash(dout, qkv, kmask, out, lse, comm, B, S_l, NH, causal,
+                               scale or 1.0 / math.sqrt(qkv.shape[1] // 3 // NH))
     P, r = comm.nrank, comm.rank
     H = qkv.shape[1] // 3
     D = H // NH

@@ -8,8 +8,9 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T="python3 -u -m pytest -q -p no:cacheprovider --timeout 900 --timeout-method thread"
 echo "== flash tests"
-timeout -k 10 600 $T -x tests/test_flash_attn_gpu.py > gpurun_out/r5c_flash.log 2>&1
-rc=$?; tail -8 gpurun_out/r5c_flash.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 $T --maxfail=3 tests/test_flash_attn_gpu.py tests/test_ring_attention_gpu.py > gpurun_out/r5c_flash.log 2>&1
+rc=$?; tail -8 gpurun_out/r5c_flash.log
+case $rc in 0|1) ;; *) exit $rc ;; esac
 echo "== attention timing"
 ALT_FLASH_LIB=csrc/build/libfa_old.so timeout -k 10 300 python3 scripts/bench_attn.py > gpurun_out/r5c_attn.txt 2>&1
 rc=$?; cat gpurun_out/r5c_attn.txt | tail -24; [ $rc -eq 0 ] || exit $rc

@@ -161,10 +161,12 @@ def test_bn_from_fused_statistics_matches_plain_bn():
     assert _rel(s2, sums) < 1e-4
 
 
-def test_dgrad_join_accumulates_in_place():
+def test_dgrad_join_accumulates_in_place(monkeypatch):
     """1x1 data gradient with a fused gradient join (acc): autotuning times the
     in-place library candidate against scratch, and once chosen it accumulates
-    into acc itself (no copy of acc into a new output)."""
+    into acc itself (no copy of acc into a new output).  The library path is an
+    explicit A/B opt-in (HETU_ALLOW_VENDOR)."""
+    monkeypatch.setenv('HETU_ALLOW_VENDOR', '1')
     from hetu_61a7_amd.kernels import conv as KC, autotune
     g = torch.randn(4, 64, 14, 14, device=DEV).bfloat16().contiguous(memory_format=CL)
     w = (torch.randn(64, 32, 1, 1, device=DEV) * 0.1).bfloat16().contiguous(memory_format=CL)
@@ -185,7 +187,8 @@ def test_dgrad_join_accumulates_in_place():
     autotune._decisions.pop(key, None)
 
 
-def test_matmul_join_accumulates_in_place():
+def test_matmul_join_accumulates_in_place(monkeypatch):
+    monkeypatch.setenv('HETU_ALLOW_VENDOR', '1')     # the forced library candidate is the point
     from hetu_61a7_amd.kernels import gemm as KG, autotune
     a = torch.randn(512, 256, device=DEV).bfloat16()
     b = torch.randn(384, 256, device=DEV).bfloat16()
@@ -206,10 +209,11 @@ def test_matmul_join_accumulates_in_place():
     autotune._decisions.pop(key, None)
 
 
-def test_vendor_dgrad_mixed_layout_regression():
+def test_vendor_dgrad_mixed_layout_regression(monkeypatch):
     """The A/B vendor path (HETU_CONV=vendor) with the operand mix that aborted in round 2:
     an NCHW fp32 output gradient, a channels-last filter, 3 input channels.  The shape-only
     placeholder now follows g's layout, so MIOpen sees one layout per call."""
+    monkeypatch.setenv('HETU_ALLOW_VENDOR', '1')
     from hetu_61a7_amd.kernels import conv as KC
     for _ in range(3):
         x = torch.randn(2, 3, 20, 20, device=DEV, requires_grad=True)

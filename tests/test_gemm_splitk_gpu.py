@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize('M,N,K', [(768, 768, 8192), (768, 3072, 8192), (256, 320, 4096)])
-def test_weight_grad_paths_match_fp32(M, N, K):
+def test_weight_grad_paths_match_fp32(M, N, K, monkeypatch):
+    monkeypatch.setenv('HETU_ALLOW_VENDOR', '1')     # the library split-K path is compared too
     from hetu_61a7_amd.kernels import gemm as KG, gemm_mfma
     torch.manual_seed(0)
     x = torch.randn(K, M, device='cuda').bfloat16()   # activations [tokens, in]
@@ -46,7 +47,8 @@ def test_splitk_partial_sum_matches_torch(s, M, N):
 
 
 @pytest.mark.gpu
-def test_vendor_splitk_gemm_matches_matmul():
+def test_vendor_splitk_gemm_matches_matmul(monkeypatch):
+    monkeypatch.setenv('HETU_ALLOW_VENDOR', '1')
     from hetu_61a7_amd.kernels.gemm import _vendor_splitk_into
     torch.manual_seed(0)
     A = torch.randn(768, 8192, device='cuda').to(torch.bfloat16)

@@ -100,6 +100,66 @@ def _f32(t):
     return copy_into(_NA.empty(t.shape, dtype=torch.float32, device=t.device), t)
 
 
+# fp32 on the GPU (the reference's precision, parity runs): the reference's materialised
+# chain -- scores, mask, softmax, dropout, P.V (examples/nlp/bert/hetu_bert.py:220-271) --
+# on the hand-written exact-fp32 MFMA GEMM and the native softmax / dropout / broadcast
+# kernels; the probabilities are saved for the backward.
+def _f32_heads(qkv, B, S, NH, D):
+    """contiguous fp32 [B*NH, S, D] copies of Q, K, V (native strided copies)"""
+    from .tensor import copy_into
+    out = []
+    for t in packed_heads(qkv, B, S, NH):
+        out.append(copy_into(_NA.empty((B, NH, S, D), dtype=torch.float32, device=qkv.device), t).view(B * NH, S, D))
+    return out
+
+
+def _f32_fwd(qkv, mask, B, S, NH, D, keep, seed, scale):
+    from . import gemm as KG
+    from .elementwise import unary, binary
+    from .softmax import softmax
+    from .dropout import dropout
+    from .tensor import copy_into
+    H = NH * D
+    q, k, v = _f32_heads(qkv, B, S, NH, D)
+    sc = unary('mul_c', KG.bmm(q, k, tb=True), scale).view(B, NH, S, S)
+    if mask is not None:
+        sc = binary('add', sc, _mask_f32(mask).reshape(B, 1, 1, S))
+    p = softmax(sc)
+    pd = dropout(p, keep, seed) if keep < 1.0 else p
+    o = KG.bmm(pd.view(B * NH, S, S), v)
+    out = _NA.empty((B * S, H), dtype=torch.float32, device=qkv.device)
+    copy_into(out.view(B, S, NH, D).permute(0, 2, 1, 3), o.view(B, NH, S, D))
+    return out, p
+
+
+def _f32_bwd(dout, qkv, p, B, S, NH, D, keep, seed, scale):
+    from . import gemm as KG
+    from .elementwise import unary, binary
+    from .softmax import softmax_backward
+    from .dropout import dropout
+    from .tensor import copy_into, fill_
+    H = NH * D
+    q, k, v = _f32_heads(qkv, B, S, NH, D)
+    do = copy_into(_NA.empty((B, NH, S, D), dtype=torch.float32, device=qkv.device),
+                   dout.reshape(B, S, NH, D).permute(0, 2, 1, 3)).view(B * NH, S, D)
+    dm = None
+    if keep < 1.0:       # the forward's mask, regenerated from the seed
+        dm = dropout(fill_(_NA.empty(tuple(p.shape), dtype=torch.float32, device=p.device), 1.0), keep, seed)
+    pd = binary('mul', p, dm) if dm is not None else p
+    dv = KG.bmm(pd.view(B * NH, S, S), do, ta=True)
+    dp = KG.bmm(do, v, tb=True).view(B, NH, S, S)
+    if dm is not None:
+        dp = binary('mul', dp, dm)
+    ds = unary('mul_c', softmax_backward(p, dp), scale).view(B * NH, S, S)
+    dq = KG.bmm(ds, k)
+    dk = KG.bmm(ds, q, ta=True)
+    dqkv = _NA.empty((B * S, 3 * H), dtype=torch.float32, device=qkv.device)
+    gq, gk, gv = packed_heads(dqkv, B, S, NH)
+    for dst, src in ((gq, dq), (gk, dk), (gv, dv)):
+        copy_into(dst, src.view(B, NH, S, D))
+    return dqkv
+
+
 def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
     """-> (out [B*S, H], lse [B*NH*S] fp32 or probs (reference path))."""
     H = qkv.shape[1] // 3
@@ -123,6 +183,8 @@ def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
         _, lse = flash_fwd(q, k, v, _key_mask(mask, B, S), False, keep, seed, scale,
                            out=out.view(B, S, NH, D).permute(0, 2, 1, 3))
         return out, lse
+    if qkv.is_cuda and qkv.dtype == torch.float32:
+        return _f32_fwd(qkv, mask, B, S, NH, D, keep, seed, scale)
     if qkv.is_cuda:
         raise RuntimeError('attention: no hand-written kernel for %s S=%d D=%d' % (qkv.dtype, S, D))
     p, v = _ref_probs(qkv, mask, B, S, NH, D, scale)
@@ -160,6 +222,8 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
             flash_bwd(g4, q, k, v, o4, saved, _key_mask(mask, B, S), False, keep, seed, scale, grads=(gq, gk, gv))
             return dqkv
         raise RuntimeError('attention backward: no hand-written kernel for S=%d D=%d' % (S, D))
+    if qkv.is_cuda and qkv.dtype == torch.float32 and saved.dim() == 4:
+        return _f32_bwd(dout, qkv, saved, B, S, NH, D, keep, seed, scale)
     if saved.dim() == 1:    # fused forward (S <= 256) but no fused backward: recompute probs
         saved, _ = _ref_probs(qkv, mask, B, S, NH, D, scale)
     p = saved

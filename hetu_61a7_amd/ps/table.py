@@ -19,6 +19,26 @@ import torch
 from . import worker as psw
 from .worker import PARAM_DENSE, PARAM_SPARSE, PARAM_CACHE
 from ..memory_pool import record_stream
+from .. import native_array as _NA
+
+
+def _scaled_f32(x, c):
+    """fp32 c * x on the native kernels for device tensors (cast + scale, no ATen launch)"""
+    if not x.is_cuda:
+        return x.float() * c
+    from ..kernels.elementwise import unary, cast
+    from ..kernels.tensor import copy_into
+    if not x.is_contiguous():
+        x = copy_into(_NA.empty(tuple(x.shape), dtype=x.dtype, device=x.device), x)
+    return unary('mul_c', cast(x, torch.float32), c)
+
+
+def _dev_copy(dst, src):
+    """dst = src between device tensors (dtype cast included) on the native kernels"""
+    if dst.is_cuda and src.is_cuda:
+        from ..kernels.tensor import copy_into
+        return copy_into(dst, src)
+    return dst.copy_(src)
 
 
 def _pinned(n, dtype=torch.float32):
@@ -226,7 +246,8 @@ class PSTable(object):
             cur.wait_stream(h2d)
             record_stream(out, cur)
             if out_dtype is not None and out_dtype != out.dtype:
-                out = out.to(out_dtype)
+                from ..kernels.elementwise import cast
+                out = cast(out, out_dtype)
         else:
             out = dest.clone()
         return out.view(*idx.shape, self.width)
@@ -237,7 +258,7 @@ class PSTable(object):
         self._wait_push()          # the last push may still read the staging buffer
         ids = host_ids(slices.indices)
         vals = slices.values.reshape(-1, self.width)
-        scaled = vals.float() * (-lr)
+        scaled = _scaled_f32(vals, -lr)
         host = self.grad_stage.get(scaled.numel()).view(-1, self.width)
         if scaled.is_cuda:
             # D2H on the copy stream after the scaling kernel; the compute stream goes on
@@ -337,12 +358,12 @@ class PSDense(object):
         self.agent.WaitTicket(t)
         self.flat.param.copy_(self.pull_buf[:self.flat.numel], non_blocking=True)
         if self.flat.shadow is not None:
-            self.flat.shadow.copy_(self.flat.param)
+            _dev_copy(self.flat.shadow, self.flat.param)
 
     def step(self, lr):
         n = self.flat.numel
         g = self.flat.grad[:n]
-        self.push_buf[:n].copy_(g * (-lr), non_blocking=True)
+        self.push_buf[:n].copy_(_scaled_f32(g, -lr), non_blocking=True)
         if torch.cuda.is_available() and g.is_cuda:
             torch.cuda.current_stream().synchronize()
         self.version += 1
@@ -362,4 +383,4 @@ class PSDense(object):
                 self.agent.WaitTicket(t)
             self.flat.param.copy_(self.pull_buf[:n], non_blocking=True)
             if self.flat.shadow is not None:
-                self.flat.shadow.copy_(self.flat.param)
+                _dev_copy(self.flat.shadow, self.flat.param)

@@ -286,19 +286,20 @@ def _resnet_updates(use_hipgraph, steps=6):
         g.manual_seed(0)
         X = torch.randn((B, 3, 224, 224), device="cuda", generator=g).bfloat16().contiguous(memory_format=CL)
         Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
-        names = sorted(k for k, v in ex.return_tensor_values().items()
-                       if isinstance(v, torch.Tensor) and v.is_floating_point())
+        pm = ex.config.placeholder_to_arr_map
+        names = sorted(n.name for n, v in pm.items() if getattr(n, 'trainable', False)
+                       and isinstance(v, torch.Tensor) and v.is_floating_point())
 
         def flat():
             vals = ex.return_tensor_values()
-            return torch.cat([vals[k].detach().float().reshape(-1) for k in names])
+            return {k: vals[k].detach().float().clone() for k in names}
         out, ups = [], []
         prev = flat()
         for _ in range(steps):
             lv = ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]
             out.append(float(np.mean(lv)))
             cur = flat()
-            ups.append(cur - prev)
+            ups.append({k: cur[k] - prev[k] for k in names})
             prev = cur
         fused = sum(1 for n in ex.subexecutor['train'].computing_nodes if getattr(n, 'bn_fused', None) is not None)
         return out, ups, fused
@@ -320,5 +321,8 @@ def test_hipgraph_replays_fused_bn_backward_like_eager():
     # the BN totals replay after replay, far outside them
     np.testing.assert_allclose(graph, eager, rtol=0.1, atol=0.1)
     for k, (a, b) in enumerate(zip(ug, ue)):
-        rel = float((a - b).norm() / b.norm().clamp_min(1e-20))
-        assert rel < 0.25, (k, rel)
+        num = sum(float((a[n] - b[n]).norm()) ** 2 for n in b)
+        den = sum(float(b[n].norm()) ** 2 for n in b)
+        rel = (num / max(den, 1e-30)) ** 0.5
+        worst = sorted(((float((a[n] - b[n]).norm() / b[n].norm().clamp_min(1e-20)), n) for n in b), reverse=True)[:5]
+        assert rel < 0.25, (k, rel, worst)

@@ -92,6 +92,26 @@ __device__ __forceinline__ v8s lds8(const short* T, int ldt, int row, int c0) {
   return *reinterpret_cast<const v8s*>(T + row * ldt + c0);
 }
 
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// x op x[lane ^ 32] for both wave halves by one v_permlane32_swap (no LDS round trip)
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// x of lane ^ 1 (DPP quad_perm [1, 0, 3, 2]: no LDS)
+__device__ __forceinline__ float xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f_to_bf16_bits(lo) | ((uint32_t)f_to_bf16_bits(hi) << 16);
+}
+
 // keep-mask multiplier (0 or 1/keep) for 4 consecutive keys starting at a flat
 // P index divisible by 4
 __device__ __forceinline__ void drop_mul4(uint64_t seed, uint64_t flat, float keep, float (&m)[4]) {
@@ -128,7 +148,7 @@ __global__ void __launch_bounds__(256) attn_fwd_k(Args a) {
   constexpr int S = 32 * KB;
   constexpr int LT = S + PAD;
   __shared__ short vt[HD * LT];
-  __shared__ float msk[S];
+  __shared__ __attribute__((aligned(16))) float msk[S];
   const int bh = blockIdx.x;
   const int b = bh / a.NH, hd = bh - b * a.NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -137,11 +157,13 @@ __global__ void __launch_bounds__(256) attn_fwd_k(Args a) {
   const bf16* K = a.k + (int64_t)b * S * a.ldk + hd * HD;
   const bf16* V = a.v + (int64_t)b * S * a.ldv + hd * HD;
   stage_t<S>(V, a.ldv, vt);
-  for (int i = threadIdx.x; i < S; i += 256) msk[i] = a.mask ? a.mask[(int64_t)b * S + i] : 0.f;
+  // the key mask in log2 units: the softmax runs as exp2 of log2 e-scaled scores
+  for (int i = threadIdx.x; i < S; i += 256) msk[i] = a.mask ? a.mask[(int64_t)b * S + i] * kLog2e : 0.f;
   __syncthreads();
   const int qb = blockIdx.y * 4 + w;
   if (qb >= KB) return;
   const int q = qb * 32 + r;
+  const float sl2 = a.scale * kLog2e;
 
   v8s qf[4];
 #pragma unroll
@@ -155,46 +177,48 @@ __global__ void __launch_bounds__(256) attn_fwd_k(Args a) {
     for (int ds = 0; ds < 4; ++ds) c = mfma(ld8(K + (int64_t)(kb * 32 + r) * a.ldk + 16 * ds + 8 * h), qf[ds], c);
     acc[kb] = c;
   }
-  // scale + key mask, lane-local max / sum, one exchange with lane ^ 32
+  // scaled scores + key mask (16-byte LDS reads of 4 consecutive keys), lane-local max,
+  // one permlane swap with lane ^ 32
   float m = -INFINITY;
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      const float s = acc[kb][i] * a.scale + msk[key];
-      acc[kb][i] = s;
-      m = fmaxf(m, s);
+    for (int g = 0; g < 4; ++g) {
+      const float4 mm = *reinterpret_cast<const float4*>(&msk[kb * 32 + 8 * g + 4 * h]);
+      const float m4[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float sv = fmaf(acc[kb][4 * g + t], sl2, m4[t]);
+        acc[kb][4 * g + t] = sv;
+        m = fmaxf(m, sv);
+      }
     }
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  m = xmax32(m);
   float sum = 0.f;
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float e = __expf(acc[kb][i] - m);
+      const float e = __builtin_amdgcn_exp2f(acc[kb][i] - m);
       acc[kb][i] = e;
       sum += e;
     }
-  sum += __shfl_xor(sum, 32, 64);
+  sum = xsum32(sum);
   const float inv = 1.f / sum;
-  if (h == 0) a.lse[(int64_t)bh * S + q] = m + __logf(sum);
-  const bool drop = a.keep < 1.f;
-  const uint64_t rowflat = ((uint64_t)bh * S + q) * S;
+  if (h == 0) a.lse[(int64_t)bh * S + q] = m * kLn2 + __logf(sum);
+  if (a.keep < 1.f) {
+    const uint64_t rowflat = ((uint64_t)bh * S + q) * S;
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float mul[4] = {inv, inv, inv, inv};
-      if (drop) {
+      for (int g = 0; g < 4; ++g) {
+        float mul[4];
         drop_mul4(a.seed, rowflat + kb * 32 + 8 * g + 4 * h, a.keep, mul);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) mul[t] *= inv;
+        for (int t = 0; t < 4; ++t) acc[kb][4 * g + t] *= mul[t];
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[kb][4 * g + t] *= mul[t];
-    }
-  // O^T[d][q] = sum_key V^T[d][key] P^T[key][q]
+  }
+  // O^T[d][q] = sum_key V^T[d][key] P^T[key][q]; the 1 / sum normalisation at the store
 #pragma unroll
   for (int db = 0; db < 2; ++db) {
     v16f o = {0.f};
@@ -205,10 +229,9 @@ __global__ void __launch_bounds__(256) attn_fwd_k(Args a) {
     bf16* O = a.o + ((int64_t)b * S + q) * a.ldo + hd * HD + db * 32;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      float t4[4] = {o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]};
       uint2 pk;
-      pk.x = (unsigned)f_to_bf16_bits(t4[0]) | ((unsigned)f_to_bf16_bits(t4[1]) << 16);
-      pk.y = (unsigned)f_to_bf16_bits(t4[2]) | ((unsigned)f_to_bf16_bits(t4[3]) << 16);
+      pk.x = pack2(o[4 * g] * inv, o[4 * g + 1] * inv);
+      pk.y = pack2(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
       *reinterpret_cast<uint2*>(O + 8 * g + 4 * h) = pk;
     }
   }
@@ -230,7 +253,9 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
   short* qt = PH == 2 ? lds : kt + HD * LT;                 // Q^T   [64][LT]  (PH 0, 2)
   short* dot = qt + HD * LT;                                // dO^T  [64][LT]  (PH 0, 2)
   short* pt = PH == 0 ? dot + HD * LT : a.ws + (int64_t)bh * S * S;                  // P_drop^T [S][LP]
-  short* dst = PH == 0 ? pt + S * LT : a.ws + ((int64_t)a.B * a.NH + bh) * S * S;    // (scale dS)^T
+  // dS^T (the softmax-gradient without the scale, which goes on at the dQ / dK stores);
+  // 64 shorts past P_drop^T's end in LDS, so the two images' paired stores use different banks
+  short* dst = PH == 0 ? pt + S * LT + 64 : a.ws + ((int64_t)a.B * a.NH + bh) * S * S;
   float* dvec = reinterpret_cast<float*>(PH == 0 ? dst + S * LT : (PH == 1 ? kt + HD * LT : dot + HD * LT));
   float* msk = dvec + S;
   const int b = bh / a.NH, hd = bh - b * a.NH;
@@ -248,7 +273,7 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
     stage_t<S>(Q, a.ldq, qt);
     stage_t<S>(dO, a.lddo, dot);
   }
-  for (int i = threadIdx.x; i < S; i += 256) msk[i] = a.mask ? a.mask[(int64_t)b * S + i] : 0.f;
+  for (int i = threadIdx.x; i < S; i += 256) msk[i] = a.mask ? a.mask[(int64_t)b * S + i] * kLog2e : 0.f;
   // D[q] = sum_d dO[q][d] * O[q][d]: 8 consecutive threads per query
   for (int idx = threadIdx.x; PH != 2 && idx < S * 8; idx += 256) {
     const int qq = idx >> 3, c = idx & 7;
@@ -274,8 +299,10 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
       qf[ds] = ld8(Q + (int64_t)q * a.ldq + 16 * ds + 8 * h);
       gf[ds] = ld8(dO + (int64_t)q * a.lddo + 16 * ds + 8 * h);
     }
-    const float lse = a.lse[(int64_t)bh * S + q];
+    const float lse2 = a.lse[(int64_t)bh * S + q] * kLog2e;
     const float Dq = dvec[q];
+    const float sl2 = a.scale * kLog2e;
+    const bool odd = r & 1;
     const uint64_t rowflat = ((uint64_t)bh * S + q) * S;
     v16f ds_acc[KB];
 #pragma unroll
@@ -290,15 +317,20 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
       for (int g = 0; g < 4; ++g) {
         float mul[4] = {1.f, 1.f, 1.f, 1.f};
         if (drop) drop_mul4(a.seed, rowflat + kb * 32 + 8 * g + 4 * h, a.keep, mul);
+        const float4 mm = *reinterpret_cast<const float4*>(&msk[kb * 32 + 8 * g + 4 * h]);
+        const float m4[4] = {mm.x, mm.y, mm.z, mm.w};
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int i = 4 * g + t;
           const int key = kb * 32 + 8 * g + 4 * h + t;
-          const float p = __expf(sc[i] * a.scale + msk[key] - lse);
-          const float pd = p * mul[t];
-          const float dsv = p * (dp[i] * mul[t] - Dq) * a.scale;
-          pt[key * LP + q] = (short)f_to_bf16_bits(pd);
-          dst[key * LP + q] = (short)f_to_bf16_bits(dsv);
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[i], sl2, m4[t] - lse2));
+          const float pd = drop ? p * mul[t] : p;
+          const float dsv = p * (drop ? fmaf(dp[i], mul[t], -Dq) : dp[i] - Dq);
+          // one 4-byte store per lane: an even lane (query q) writes P_drop^T[key][q, q+1],
+          // its odd neighbour dS^T[key][q-1, q], each taking the other's value by DPP
+          const float other = xor1(odd ? pd : dsv);
+          if (odd) *reinterpret_cast<uint32_t*>(dst + key * LP + q - 1) = pack2(other, dsv);
+          else *reinterpret_cast<uint32_t*>(pt + key * LP + q) = pack2(pd, other);
           sc[i] = dsv;
         }
       }
@@ -317,8 +349,8 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint2 pk;
-        pk.x = (unsigned)f_to_bf16_bits(o[4 * g]) | ((unsigned)f_to_bf16_bits(o[4 * g + 1]) << 16);
-        pk.y = (unsigned)f_to_bf16_bits(o[4 * g + 2]) | ((unsigned)f_to_bf16_bits(o[4 * g + 3]) << 16);
+        pk.x = pack2(o[4 * g] * a.scale, o[4 * g + 1] * a.scale);
+        pk.y = pack2(o[4 * g + 2] * a.scale, o[4 * g + 3] * a.scale);
         *reinterpret_cast<uint2*>(dQ + 8 * g + 4 * h) = pk;
       }
     }
@@ -339,11 +371,12 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
 #pragma unroll
         for (int t = 0; t < S / 16; ++t) c = mfma(lds8(A, LT, db * 32 + r, 16 * t + 8 * h), lds8(Bm, LP, key, 16 * t + 8 * h), c);
         bf16* dst_row = out + hd * HD + db * 32;
+        const float sc_out = which == 0 ? 1.f : a.scale;     // dK = scale * Q^T dS
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           uint2 pk;
-          pk.x = (unsigned)f_to_bf16_bits(c[4 * g]) | ((unsigned)f_to_bf16_bits(c[4 * g + 1]) << 16);
-          pk.y = (unsigned)f_to_bf16_bits(c[4 * g + 2]) | ((unsigned)f_to_bf16_bits(c[4 * g + 3]) << 16);
+          pk.x = pack2(c[4 * g] * sc_out, c[4 * g + 1] * sc_out);
+          pk.y = pack2(c[4 * g + 2] * sc_out, c[4 * g + 3] * sc_out);
           *reinterpret_cast<uint2*>(dst_row + 8 * g + 4 * h) = pk;
         }
       }
@@ -356,7 +389,7 @@ size_t bwd_lds_bytes() {
   constexpr int S = 32 * KB, LT = S + PAD;
   if (PH == 1) return (size_t)HD * LT * sizeof(short) + 2 * S * sizeof(float);
   if (PH == 2) return (size_t)2 * HD * LT * sizeof(short) + 2 * S * sizeof(float);
-  return (size_t)(3 * HD * LT + 2 * S * LT) * sizeof(short) + 2 * S * sizeof(float);
+  return (size_t)(3 * HD * LT + 2 * S * LT + 64) * sizeof(short) + 2 * S * sizeof(float);
 }
 
 // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU) must be opted into once

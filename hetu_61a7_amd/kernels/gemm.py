@@ -311,8 +311,8 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
     into it (C == D) instead of first copying it into a new output."""
     a, b = _match(a, b)
     A, B = _tr(a, ta), _tr(b, tb)
-    if native(a) and a.dtype == torch.bfloat16 and A.dim() == 2 and tuple(acc.shape) == (A.shape[0], B.shape[1]) \
-            and _MFMA not in ('off', 'vendor'):
+    if native(a) and a.dtype in (torch.bfloat16, torch.float32) and A.dim() == 2 and \
+            tuple(acc.shape) == (A.shape[0], B.shape[1]) and _MFMA not in ('off', 'vendor'):
         from . import gemm_mfma
         from .autotune import choose, _decisions
         # the MFMA epilogue reads an fp32 acc as it is; the library GEMM gets it cast
@@ -331,11 +331,12 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
         hip = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0)
         vendor = (lambda: dst[0].addmm_(A, B)) if inplace else (lambda: torch.addmm(c(), A, B))
         cands = {'hip': hip, 'vendor': vendor}
-        if A.shape[0] >= 256 and B.shape[1] >= 256:
+        bf = a.dtype == torch.bfloat16       # fp32: the exact-fp32 kernel (``hip``) only
+        if bf and A.shape[0] >= 256 and B.shape[1] >= 256:
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=1)
-        if A.shape[1] <= 2048:
+        if bf and A.shape[1] <= 2048:
             cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=3)
-        if B.shape[1] % 96 == 0 and A.shape[0] >= 1024:
+        if bf and B.shape[1] % 96 == 0 and A.shape[0] >= 1024:
             cands['hip96'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=5)
         if A.shape[0] * B.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, cin=acc, beta=1.0)

@@ -45,6 +45,16 @@ def _operand(t, rows_dim_last, q=8):
     return None
 
 
+def _dense_f32(t):
+    """t as a contiguous fp32 tensor (native cast / strided copy on the GPU; no copy if already)"""
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t
+    if not t.is_cuda:
+        return t.float().contiguous()
+    from .tensor import copy_into
+    return copy_into(_NA.empty(tuple(t.shape), dtype=torch.float32, device=t.device), t)
+
+
 def _aligned(*ts):
     return all(t.data_ptr() % 16 == 0 for t in ts)
 
@@ -85,10 +95,10 @@ def gemm_f32(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None,
     if cin is not None and beta != 0.0:
         cin_t = cin.expand_as(out) if cin.shape != out.shape else cin
         if cin_t.dtype != torch.float32 or cin_t.stride(-1) != 1:
-            cin_t = cin_t.float().contiguous()
+            cin_t = _dense_f32(cin_t)
         ldcin = cin_t.stride(-2)
         sCin = cin_t.stride(0) if cin_t.dim() == 3 else 0
-    bias_t = bias.float().contiguous() if bias is not None else None
+    bias_t = _dense_f32(bias) if bias is not None else None
     f = fn('hetu_gemm_f32', _F32_ARGS)
     check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), cin_t.data_ptr() if cin_t is not None else None,
             bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, ldcin,
@@ -156,7 +166,7 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
             cin_t = cin_t.contiguous()
         ldcin = cin_t.stride(-2)
         sCin = cin_t.stride(0) if cin_t.dim() == 3 else 0
-    bias_t = bias.float().contiguous() if bias is not None else None
+    bias_t = _dense_f32(bias) if bias is not None else None
     ws = None
     if splitk > 1:
         if bias is not None or act is not None or cin_t is not None:
@@ -226,8 +236,8 @@ def gemm_small(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=Non
     if cin is not None and beta != 0.0:
         cin_t = cin.expand(M, N) if tuple(cin.shape) != (M, N) else cin
         if cin_t.stride(-1) != 1 or cin_t.dtype not in (torch.float32, torch.bfloat16):
-            cin_t = cin_t.float().contiguous()
-    bias_t = bias.float().contiguous() if bias is not None else None
+            cin_t = _dense_f32(cin_t)
+    bias_t = _dense_f32(bias) if bias is not None else None
     f = fn('hetu_gemm_small', [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I32, I32, F32, F32, I32,
                                I32, I32, I32, P])
     check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), cin_t.data_ptr() if cin_t is not None else None,

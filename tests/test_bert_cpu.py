@@ -73,6 +73,16 @@ def packed_attention_check(device, dtype, B=2, S=32, NH=2, D=64, keep=1.0, tol=1
     dqkv = KA.attention_bwd(dout.to(device, dtype), qkv.to(device, dtype), out, saved, mask.to(device), B, S, NH,
                             keep, seed)
     np.testing.assert_allclose(dqkv.float().cpu().numpy(), t.grad.numpy(), rtol=10 * tol, atol=10 * tol)
+    # and per operand in relative norm (a wrong-scale dQ / dK / dV would still fit the
+    # elementwise band above): <= 3e-2 in bf16, the fp32 tolerance otherwise
+    rel_tol = 3e-2 if dtype == torch.bfloat16 else 10 * tol
+    g = dqkv.float().cpu().reshape(B * S, 3, H)
+    ref = t.grad.reshape(B * S, 3, H)
+    for i, name in enumerate('qkv'):
+        rel = float((g[:, i] - ref[:, i]).norm() / ref[:, i].norm().clamp_min(1e-12))
+        assert rel <= rel_tol, ('d' + name, rel)
+    rel = float((out.float().cpu() - o.detach()).norm() / o.detach().norm())
+    assert rel <= rel_tol, ('out', rel)
 
 
 def test_packed_attention_reference_cpu():

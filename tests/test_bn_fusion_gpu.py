@@ -274,7 +274,7 @@ def _resnet_updates(use_hipgraph, steps=6):
     from hetu_61a7_amd.models import resnet50_imagenet
     from hetu_61a7_amd.ops import node as _node
     _node.G_NODE_ID = 0
-    os.environ['HETU_FUSE_BN_BWD'] = 'all'
+    os.environ.setdefault('HETU_FUSE_BN_BWD', 'all')
     try:
         B = 4
         x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')

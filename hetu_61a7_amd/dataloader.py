@@ -114,6 +114,10 @@ class Dataloader(object):
             db = hb.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._stream)
+        # the host batch rides along: a consumer that needs the values on the host (PS /
+        # HET-cache lookups of sparse ids, ``ps.table.host_ids``) reads it instead of a
+        # device-to-host copy that would wait for the GPU
+        db.hetu_host = hb
         return (db, ev, hb)
 
     def get_arr(self):
@@ -182,7 +186,8 @@ class DataloaderOp(Op):
         t = dl.get_arr()
         if config is not None and config.mixed_precision and t.is_cuda and t.dtype == torch.float32 \
                 and not self.keep_fp32:
-            t = t.to(torch.bfloat16)
+            from .kernels.elementwise import cast
+            t = cast(t, torch.bfloat16)          # native cast kernel
         return t
 
     def get_next_arr(self, name):

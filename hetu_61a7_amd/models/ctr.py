@@ -255,6 +255,9 @@ def wdl_criteo_bench(args, world, rank, local):
 
     def finish():
         from ..ps import worker
+        for op in ex.subexecutor['train'].opt_ops:
+            if getattr(op, 'ps_dense', None) is not None:
+                op.ps_dense.drain()
         ex.config.ps_comm.BarrierWorker()
         worker.worker_finish()
 

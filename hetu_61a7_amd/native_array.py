@@ -189,7 +189,8 @@ class Array(object):
 
     def copy_from(self, src, stream=None):
         if stream is None and torch.cuda.is_available():
-            stream = torch.cuda.current_stream().cuda_stream
+            from .kernels import stream_ptr
+            stream = stream_ptr()
         rc = lib().hetu_array_copy(self.h, src.h, stream)
         if rc == 4:     # general strides: the device copy kernel through torch views
             from .kernels.tensor import copy_into

@@ -337,7 +337,8 @@ class PipelineSubExecutor(object):
         self.opt = op
         if ps_sync:
             from ..ps.table import PSDense
-            op.ps_dense = PSDense(op.flat, PS_KEY_HETPIPE_STAGE + self.stage, self.config, publish=self.replica == 0)
+            op.ps_dense = PSDense(op.flat, PS_KEY_HETPIPE_STAGE + self.stage, self.config, publish=self.replica == 0,
+                                  overlap=False)
 
     # ---------------------------------------------------------------------------------------
     def _nrep(self, s):

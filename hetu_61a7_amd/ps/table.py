@@ -326,11 +326,20 @@ class PSTable(object):
 class PSDense(object):
     """Flat dense parameters held by the PS (pure PS mode)."""
 
-    def __init__(self, flat, key, config, publish=None):
+    def __init__(self, flat, key, config, publish=None, overlap=None):
         self.flat = flat
         self.key = key
         self.agent = psw.get_agent()
         self.bsp = config.bsp
+        # ASP with prefetch (the executor's default): the dense push-pull of step t runs on a
+        # helper thread while step t+1 computes, and its pulled values replace the worker's
+        # copy at the end of step t+1 -- staleness 1, the same bound the prefetched embedding
+        # rows already have (reference executor prefetch=True).  BSP / SSP stay synchronous.
+        if overlap is None:
+            overlap = (self.bsp is None or self.bsp < 0) and bool(getattr(config, 'prefetch', False))
+        self.overlap = overlap
+        self._thread = None
+        self._inflight = False
         n = flat.numel
         self.agent.InitTensor(key, PARAM_DENSE, n, 1, 0, 0.0, 0.0, 0)
         # one worker publishes its initial values (worker 0 by default; a
@@ -351,7 +360,70 @@ class PSDense(object):
 
     def repull(self):
         """Reload the worker's copy from the server (after a checkpoint load)."""
+        self.drain()
         self._pull_into_device()
+
+    # ---- overlapped exchange (ASP + prefetch) -----------------------------------------------
+    def _worker(self):
+        while True:
+            ev = self._q.get()
+            if ev is None:
+                return
+            try:
+                ev.synchronize()                 # the scaled gradient is in push_buf
+                t = self.agent.DDPushPull(self.key, self.push_buf, self.pull_buf)
+                self.agent.WaitTicket(t)
+            except BaseException as e:           # noqa: BLE001 -- re-raised by the step thread
+                self._err = e
+            finally:
+                self._done.set()
+
+    def _start(self):
+        import queue
+        import threading
+        self._q = queue.Queue()
+        self._done = threading.Event()
+        self._err = None
+        self._thread = threading.Thread(target=self._worker, name='hetu-ps-dense', daemon=True)
+        self._thread.start()
+
+    def _apply_inflight(self):
+        """wait for the exchange in flight and load its pulled values into the device copy"""
+        if not self._inflight:
+            return
+        with _waiting():
+            self._done.wait()
+        self._inflight = False
+        if self._err is not None:
+            e, self._err = self._err, None
+            raise e
+        n = self.flat.numel
+        self.flat.param.copy_(self.pull_buf[:n], non_blocking=True)
+        if self.flat.shadow is not None:
+            _dev_copy(self.flat.shadow, self.flat.param)
+
+    def drain(self):
+        """finish the exchange in flight (before a checkpoint, an evaluation or shutdown)"""
+        if self._thread is not None:
+            self._apply_inflight()
+
+    def _step_overlapped(self, g, lr):
+        if self._thread is None:
+            self._start()
+        self._apply_inflight()                   # step t-1's exchange: usually long done
+        n = self.flat.numel
+        scaled = _scaled_f32(g, -lr)
+        _, d2h = side_streams(g.device)
+        d2h.wait_stream(torch.cuda.current_stream(g.device))
+        with torch.cuda.stream(d2h):
+            self.push_buf[:n].copy_(scaled, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(d2h)
+        record_stream(scaled, d2h)
+        self.version += 1
+        self._done.clear()
+        self._inflight = True
+        self._q.put(ev)
 
     def _pull_into_device(self):
         t = self.agent.Pull(self.key, self.pull_buf)
@@ -363,6 +435,8 @@ class PSDense(object):
     def step(self, lr):
         n = self.flat.numel
         g = self.flat.grad[:n]
+        if self.overlap and g.is_cuda:
+            return self._step_overlapped(g, lr)
         self.push_buf[:n].copy_(_scaled_f32(g, -lr), non_blocking=True)
         if torch.cuda.is_available() and g.is_cuda:
             torch.cuda.current_stream().synchronize()

@@ -64,7 +64,8 @@ def _check(r, what):
 def _handle(stream):
     """raw hipStream_t of a DeviceStream, a torch stream, or None (torch's current stream)"""
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream
+        from .kernels import stream_ptr
+        return stream_ptr()
     if isinstance(stream, DeviceStream):
         return stream.handle
     return stream.cuda_stream

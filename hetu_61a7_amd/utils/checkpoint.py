@@ -144,6 +144,8 @@ def _ps_save(ex, file_path):
     tables = _ps_tables(ex)
     for _, t in tables:
         t.close()                      # flush staged grads, wait pushes, flush cache lines
+    for d in _ps_dense(ex):
+        d.drain()                      # the overlapped dense exchange in flight (ASP prefetch)
     agent.BarrierWorker()
     if agent.rank() == 0:
         os.makedirs(file_path, exist_ok=True)
@@ -251,6 +253,8 @@ def _ps_load(ex, file_path):
     tables = _ps_tables(ex)
     for _, t in tables:
         t.close()
+    for d in _ps_dense(ex):
+        d.drain()
     agent.BarrierWorker()
     if agent.rank() == 0:
         for _, t in tables:

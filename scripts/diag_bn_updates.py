@@ -24,7 +24,7 @@ def main():
         for _ in range(2):
             os.environ['HETU_FUSE_BN_BWD'] = bwd
             src = T._resnet_updates.__code__
-            losses, ups, _ = T._resnet_updates(False, steps=2)
+            losses, ups, _ = T._resnet_updates(False, steps=2, lr=1e-3)
             runs.append((losses, ups))
         print('stats=%s bwd=%s losses %s | %s' % (stats, bwd, [round(x, 5) for x in runs[0][0]],
                                                  [round(x, 5) for x in runs[1][0]]), flush=True)

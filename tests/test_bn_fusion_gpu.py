@@ -265,21 +265,27 @@ def test_resnet50_forward_with_fused_bn_statistics():
     assert abs(l0 - l1) <= 2e-2 * max(1.0, abs(l0)), (l0, l1)
 
 
-def _resnet_updates(use_hipgraph, steps=6):
-    """losses and per-step parameter updates (flat fp32) of plain SGD at a small rate: the
-    weights barely move, so the updates of step k in two runs are the same gradients up to
-    bf16 / atomic-order noise and a broken replay shows as a per-step update mismatch
-    (a chaotic high-rate run would amplify that noise past any useful tolerance)"""
+def _resnet_updates(use_hipgraph, steps=6, lr=1e-5):
+    """losses and per-step parameter updates of plain SGD at a tiny rate: the weights barely
+    move, so the updates of step k in two runs are the same gradients up to atomic-order noise
+    and a broken replay shows as a per-step update mismatch.  Batch-4 BatchNorm is chaotic:
+    at lr 1e-3 a 2 % difference in one step's update (the fused backward totals' atomic order)
+    makes the next step's gradients uncorrelated (scripts/diag_bn_updates.py,
+    profiles/bn_update_repro_r5.txt), and the forward statistics fused into the conv epilogues
+    (atomic replicas) move the batch-4 variances of near-constant channels enough to do the
+    same at step 0 -- so the forward statistics take the deterministic two-pass kernel here."""
     import hetu_61a7_amd as ht
     from hetu_61a7_amd.models import resnet50_imagenet
     from hetu_61a7_amd.ops import node as _node
     _node.G_NODE_ID = 0
     os.environ.setdefault('HETU_FUSE_BN_BWD', 'all')
+    stats0 = os.environ.get('HETU_FUSE_BN_STATS')
+    os.environ.setdefault('HETU_FUSE_BN_STATS', '0')
     try:
         B = 4
         x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
         loss, _ = resnet50_imagenet(x, y_, 1000)
-        train = ht.optim.SGDOptimizer(learning_rate=1e-3).minimize(loss)
+        train = ht.optim.SGDOptimizer(learning_rate=lr).minimize(loss)
         ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3,
                          use_hipgraph=use_hipgraph)
         g = torch.Generator(device='cuda')
@@ -305,6 +311,10 @@ def _resnet_updates(use_hipgraph, steps=6):
         return out, ups, fused
     finally:
         os.environ.pop('HETU_FUSE_BN_BWD', None)
+        if stats0 is None:
+            os.environ.pop('HETU_FUSE_BN_STATS', None)
+        else:
+            os.environ['HETU_FUSE_BN_STATS'] = stats0
 
 
 def test_hipgraph_replays_fused_bn_backward_like_eager():
@@ -316,13 +326,11 @@ def test_hipgraph_replays_fused_bn_backward_like_eager():
     eager, ue, nf = _resnet_updates(False)
     graph, ug, _ = _resnet_updates(True)
     assert nf >= 20, nf
-    # two eager runs already differ by up to ~6 % in the late losses (atomic-order bf16 noise
-    # through 50 batch-4 BN layers), so the bounds are loose; a frozen flip doubles and triples
-    # the BN totals replay after replay, far outside them
-    np.testing.assert_allclose(graph, eager, rtol=0.1, atol=0.1)
+    # a frozen flip doubles and triples the BN totals replay after replay: O(1) update errors
+    np.testing.assert_allclose(graph, eager, rtol=1e-2, atol=1e-2)
     for k, (a, b) in enumerate(zip(ug, ue)):
         num = sum(float((a[n] - b[n]).norm()) ** 2 for n in b)
         den = sum(float(b[n].norm()) ** 2 for n in b)
         rel = (num / max(den, 1e-30)) ** 0.5
         worst = sorted(((float((a[n] - b[n]).norm() / b[n].norm().clamp_min(1e-20)), n) for n in b), reverse=True)[:5]
-        assert rel < 0.25, (k, rel, worst)
+        assert rel < 0.1, (k, rel, worst)

@@ -113,6 +113,10 @@ _RED = {'sum': dist.ReduceOp.SUM, 'max': dist.ReduceOp.MAX, 'min': dist.ReduceOp
         'prod': dist.ReduceOp.PRODUCT}
 
 
+
+# HETU_IPC_ALLREDUCE=1: small fp32 all-reduces through parallel/ipc_allreduce.py
+_IPC_SMALL = os.environ.get('HETU_IPC_ALLREDUCE', '0') == '1'
+
 class _CInt(object):
     __slots__ = ('value',)
 
@@ -200,7 +204,30 @@ class Communicator(object):
         # every rank parked in work.wait() of the first step's buckets)
         return t.is_cuda and self.group_backend == 'gloo'
 
+    def _ipc_ar(self, device):
+        """the one-shot IPC all-reduce of this communicator (built on first use: one handle
+        exchange over the communicator itself)"""
+        ar = getattr(self, '_ipc', None)
+        if ar is None:
+            from .ipc_allreduce import IPCAllReduce
+
+            def exchange(hb):
+                buf = torch.zeros(64, dtype=torch.uint8)
+                buf[:len(hb)] = torch.tensor(list(hb), dtype=torch.uint8)
+                buf = buf.to(device)
+                out = torch.empty(64 * self.nrank, dtype=torch.uint8, device=device)
+                self.all_gather(out, buf)
+                host = out.cpu().numpy().tobytes()
+                return [host[64 * j:64 * (j + 1)] for j in range(self.nrank)]
+            ar = self._ipc = IPCAllReduce(self.rank, self.nrank, exchange, device=device)
+        return ar
+
     def all_reduce(self, t: torch.Tensor, op: str = 'sum', async_op: bool = False):
+        if _IPC_SMALL and self.nrank > 1 and not async_op and op in ('sum', 'max') and t.is_cuda \
+                and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= 4096:
+            # opt-in: small fp32 reductions by the one-shot IPC kernel (no RCCL call)
+            self._ipc_ar(t.device)(t, op, out=t)
+            return None
         if self.native is not None and t.is_cuda and t.is_contiguous():
             return self.native.all_reduce(t, op, async_op=async_op)
         if self._gloo_gpu(t):

@@ -197,13 +197,23 @@ __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
     const int key = kb + (int)threadIdx.x;
     return key < a.Sk ? M[(int64_t)key * a.mk] * kLog2e : -INFINITY;
   };
-  // prologue: block 0 staged, its K fragments in registers
+  // prologue: block 0 staged and its scores issued, block 1's K fragments in registers.
+  // The loop computes block j+1's scores (MFMA) ahead of block j's softmax (VALU): the two
+  // are independent, so the matrix pipe works while the VALU runs the exp2 / max / sum.
+  auto kfrag = [&](int kb, v8s (&f)[DS]) {
+    const int kr = kb + r;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) f[ds] = kr < a.Sk ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8();
+  };
   v8s kf[DS], x0, x1;
   float mv = 0.f;
   load_t32<D>(V, a.vs, 0, a.Sk, x0, x1);
   if (MK == MK_KEY && threadIdx.x < KBLK) mv = key_mask(0);
+  kfrag(0, kf);
+  v16f sc_cur = v16f{0.f};
 #pragma unroll
-  for (int ds = 0; ds < DS; ++ds) kf[ds] = r < a.Sk ? ld8(K + (int64_t)r * a.ks + 16 * ds + 8 * h) : zero8();
+  for (int ds = 0; ds < DS; ++ds) sc_cur = mfma(kf[ds], qf[ds], sc_cur);
+  if (KBLK < kend) kfrag(KBLK, kf);
   store_t32<D>(x0, x1, vt[0]);
   if (MK == MK_KEY && threadIdx.x < KBLK) msk[0][threadIdx.x] = mv;
   __syncthreads();
@@ -216,15 +226,17 @@ __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
     if (more) {
       load_t32<D>(V, a.vs, nb, a.Sk, x0, x1);
       if (MK == MK_KEY && threadIdx.x < KBLK) mv = key_mask(nb);
-      const int kr = nb + r;
+      if (nb + KBLK < kend) kfrag(nb + KBLK, kn);
+    }
+    // block j+1's scores, independent of this block's softmax below
+    v16f sc_next = v16f{0.f};
+    if (more) {
 #pragma unroll
-      for (int ds = 0; ds < DS; ++ds) kn[ds] = kr < a.Sk ? ld8(K + (int64_t)kr * a.ks + 16 * ds + 8 * h) : zero8();
+      for (int ds = 0; ds < DS; ++ds) sc_next = mfma(kf[ds], qf[ds], sc_next);
     }
     // a causal block wholly above this wave's queries adds nothing (wave-uniform skip)
     if (!(a.causal && kb0 > qw0 + 31)) {
-      v16f sc = v16f{0.f};
-#pragma unroll
-      for (int ds = 0; ds < DS; ++ds) sc = mfma(kf[ds], qf[ds], sc);
+      v16f sc = sc_cur;
       const bool full = MK != MK_FULL && nb <= a.Sk && !(a.causal && kb0 + KBLK - 1 > qw0);
       if (full) {
 #pragma unroll
@@ -284,6 +296,7 @@ __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
 #pragma unroll
       for (int ds = 0; ds < DS; ++ds) kf[ds] = kn[ds];
     }
+    sc_cur = sc_next;
     __syncthreads();
   }
   l = xsum32(l);

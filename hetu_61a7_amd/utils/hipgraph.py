@@ -84,7 +84,19 @@ class GraphRunner(object):
             vals = sub._run_eager(feed_dict)
             return sub._collect(vals, convert)
         new_in = self._inputs(feed_dict)
+        sig = tuple(sorted((id(n), tuple(v.shape), str(v.dtype)) for n, v in new_in.items()))
+        if self.graph is not None and sig != self.sig:
+            # a feed changed shape or dtype: the captured graph's buffers no longer fit --
+            # run this step eagerly and capture again once the new shapes have warmed up
+            self.close()
+            self.calls = 0
+            self.static_in = {}
+            base = {p: sub.config.compute_value(p) for p in sub.param_nodes}
+            base.update(new_in)                 # this step's (already fetched) inputs
+            vals = sub._run_eager(None, vals=base)
+            return sub._collect(vals, convert)
         if self.graph is None:
+            self.sig = sig
             # static input buffers
             for n, v in new_in.items():
                 self.static_in[n] = v.clone()

@@ -99,6 +99,26 @@ def test_hipgraph_mlp_matches_eager():
     np.testing.assert_allclose(out[0], out[1], rtol=1e-4, atol=1e-5)
 
 
+def test_hipgraph_recaptures_when_feed_shape_changes():
+    """a captured step fed a batch of another shape must not replay the stale graph: it runs
+    eagerly, warms up and captures again -- losses equal the eager executor's throughout"""
+    rng = np.random.RandomState(4)
+    batches = [rng.randn(b, 784).astype(np.float32) for b in (32,) * 6 + (16,) * 6 + (32,) * 2]
+    labels = [np.eye(10, dtype=np.float32)[rng.randint(0, 10, len(x))] for x in batches]
+    out = []
+    from hetu_61a7_amd.ops import node as _node
+    for g in (False, True):
+        _node.G_NODE_ID = 0
+        x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+        W = ht.init.xavier_normal((784, 10), name='W')
+        loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(x, W), y_), [0])
+        train = ht.optim.SGDOptimizer(0.1).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, use_hipgraph=g)
+        out.append([float(np.asarray(ex.run('train', feed_dict={x: xb, y_: yb}, convert_to_numpy_ret_vals=True)[0])
+                          .reshape(-1)[0]) for xb, yb in zip(batches, labels)])
+    np.testing.assert_allclose(out[0], out[1], rtol=1e-4, atol=1e-5)
+
+
 def _tiny_bert_losses(ctx, mp=None, steps=4):
     from hetu_61a7_amd.models.bert import BertConfig, bert_pretrain_graph, synthetic_bert_batch
     from hetu_61a7_amd.ops import node as _node

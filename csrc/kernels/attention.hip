@@ -302,7 +302,6 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
     const float lse2 = a.lse[(int64_t)bh * S + q] * kLog2e;
     const float Dq = dvec[q];
     const float sl2 = a.scale * kLog2e;
-    const bool odd = r & 1;
     const uint64_t rowflat = ((uint64_t)bh * S + q) * S;
     v16f ds_acc[KB];
 #pragma unroll
@@ -326,11 +325,10 @@ __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
           const float p = __builtin_amdgcn_exp2f(fmaf(sc[i], sl2, m4[t] - lse2));
           const float pd = drop ? p * mul[t] : p;
           const float dsv = p * (drop ? fmaf(dp[i], mul[t], -Dq) : dp[i] - Dq);
-          // one 4-byte store per lane: an even lane (query q) writes P_drop^T[key][q, q+1],
-          // its odd neighbour dS^T[key][q-1, q], each taking the other's value by DPP
-          const float other = xor1(odd ? pd : dsv);
-          if (odd) *reinterpret_cast<uint32_t*>(dst + key * LP + q - 1) = pack2(other, dsv);
-          else *reinterpret_cast<uint32_t*>(pt + key * LP + q) = pack2(pd, other);
+          // (pairing the 2-byte stores into 4-byte ones across lane pairs by DPP measured
+          // slower: +22 % VALU per block in this VALU-bound loop)
+          pt[key * LP + q] = (short)f_to_bf16_bits(pd);
+          dst[key * LP + q] = (short)f_to_bf16_bits(dsv);
           sc[i] = dsv;
         }
       }

@@ -22,14 +22,16 @@ using namespace hetu::gemm;
 // a_kmaj: A stored [M][K] (else [K][M]); b_kmaj: B stored [N][K] (else [K][N]).
 // Requirements (checked by the caller): the contiguous dim of each operand and its
 // leading dimension are multiples of 8 elements, 16-byte aligned bases.
-HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* Cin,
-                            const float* bias, int64_t M, int64_t N, int64_t K, int64_t lda,
-                            int64_t ldb, int64_t ldc, int64_t ldcin, int a_kmaj, int b_kmaj,
-                            int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
-                            float alpha, float beta, int act, int out_f32, int cin_f32,
-                            int bias_on_m, int splitk, int atomic, float* ws, int tile, hipStream_t st) {
+static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin,
+                          const float* bias, int64_t M, int64_t N, int64_t K, int64_t lda,
+                          int64_t ldb, int64_t ldc, int64_t ldcin, int a_kmaj, int b_kmaj,
+                          int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
+                          float alpha, float beta, int act, int out_f32, int cin_f32,
+                          int bias_on_m, int splitk, int atomic, float* ws, int tile, void* C2, hipStream_t st) {
   Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32, atomic,
          bias_on_m, ws, 0};
+  ep.C2 = C2;
+  if (C2 && (splitk > 1 || atomic)) return (int)hipErrorInvalidValue;
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   if (M <= 0 || N <= 0) return 0;
@@ -55,6 +57,26 @@ HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* C
   }
   if (K % BK == 0) return launch_buf<true>(a, b, a_kmaj, b_kmaj, lda, ldb, sA, sB, ep, M, N, K, batch, splitk, st, tile);
   return launch_buf<false>(a, b, a_kmaj, b_kmaj, lda, ldb, sA, sB, ep, M, N, K, batch, splitk, st, tile);
+}
+
+HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* Cin,
+                            const float* bias, int64_t M, int64_t N, int64_t K, int64_t lda,
+                            int64_t ldb, int64_t ldc, int64_t ldcin, int a_kmaj, int b_kmaj,
+                            int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
+                            float alpha, float beta, int act, int out_f32, int cin_f32,
+                            int bias_on_m, int splitk, int atomic, float* ws, int tile, hipStream_t st) {
+  return gemm_bf16_impl(A, B, C, Cin, bias, M, N, K, lda, ldb, ldc, ldcin, a_kmaj, b_kmaj, batch, sA, sB, sC, sCin,
+                        alpha, beta, act, out_f32, cin_f32, bias_on_m, splitk, atomic, ws, tile, nullptr, st);
+}
+
+// the same product, also storing the pre-activation (bias added, before `act`) into C2
+// (bf16, C's leading dimension and batch stride; C bf16)
+HETU_API int hetu_gemm_bf16_pre(const void* A, const void* B, void* C, void* C2, const float* bias, int64_t M,
+                                int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmaj, int b_kmaj,
+                                int batch, int64_t sA, int64_t sB, int64_t sC, int act, int tile, hipStream_t st) {
+  if (!C2) return (int)hipErrorInvalidValue;
+  return gemm_bf16_impl(A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, batch, sA, sB, sC, 0,
+                        1.f, 0.f, act, 0, 0, 0, 1, 0, nullptr, tile, C2, st);
 }
 
 HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }

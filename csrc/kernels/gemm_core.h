@@ -504,6 +504,10 @@ struct Epi {
   // few thousand blocks adding into the same 2N addresses serialise on them (the
   // consumer folds the replicas)
   int cs_rep;
+  // pre-activation copy (bf16, C's layout; null: none): the epilogue stores the value
+  // before the activation here and the activated value in C -- a training GELU layer
+  // keeps its pre-activation for the backward without a separate activation pass
+  void* C2;
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -569,6 +573,7 @@ __device__ __forceinline__ float act_f(float v, int act) {
 // aliasing) serialised the epilogue.
 struct EpiOut {
   char* Cb;
+  char* C2b;
   const char* Cinb;
   bool cvec, ivec;
   bool cvec2;   // bf16 C with an even (not 8-multiple) ldc: 4-byte stores of column pairs
@@ -577,6 +582,7 @@ struct EpiOut {
 
 __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch, int64_t n, int64_t N) {
   o.Cb = (char*)ep.C + batch * ep.sC * (ep.out_f32 ? 4 : 2);
+  o.C2b = ep.C2 ? (char*)ep.C2 + batch * ep.sC * 2 : nullptr;
   o.Cinb = ep.Cin ? (const char*)ep.Cin + batch * ep.sCin * (ep.cin_f32 ? 4 : 2) : nullptr;
   o.cvec = ep.out_f32 ? ((ep.ldc & 3) == 0 && ((uintptr_t)o.Cb & 15) == 0)
                       : ((ep.ldc & 7) == 0 && ((uintptr_t)o.Cb & 15) == 0);
@@ -655,6 +661,15 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
+  }
+  if (o.C2b) {   // the pre-activation, bf16 in C's layout
+    bf16* P = (bf16*)o.C2b + off;
+    if (o.cvec && full) {
+      store_vec<bf16>(P, v);
+    } else {
+      for (int t = 0; t < 8; ++t)
+        if (n + t < N) ((unsigned short*)P)[t] = f_to_bf16_bits(v[t]);
+    }
   }
   if (ep.act) {
 #pragma unroll

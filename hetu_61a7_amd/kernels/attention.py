@@ -107,6 +107,8 @@ def _f32(t):
 def _f32_heads(qkv, B, S, NH, D):
     """contiguous fp32 [B*NH, S, D] copies of Q, K, V (native strided copies)"""
     from .tensor import copy_into
+    if qkv.dtype != torch.float32:
+        qkv = copy_into(_NA.empty(tuple(qkv.shape), dtype=torch.float32, device=qkv.device), qkv)
     out = []
     for t in packed_heads(qkv, B, S, NH):
         out.append(copy_into(_NA.empty((B, NH, S, D), dtype=torch.float32, device=qkv.device), t).view(B * NH, S, D))
@@ -129,6 +131,8 @@ def _f32_fwd(qkv, mask, B, S, NH, D, keep, seed, scale):
     o = KG.bmm(pd.view(B * NH, S, S), v)
     out = _NA.empty((B * S, H), dtype=torch.float32, device=qkv.device)
     copy_into(out.view(B, S, NH, D).permute(0, 2, 1, 3), o.view(B, NH, S, D))
+    if qkv.dtype != torch.float32:
+        out = copy_into(_NA.empty((B * S, H), dtype=qkv.dtype, device=qkv.device), out)
     return out, p
 
 
@@ -140,6 +144,9 @@ def _f32_bwd(dout, qkv, p, B, S, NH, D, keep, seed, scale):
     from .tensor import copy_into, fill_
     H = NH * D
     q, k, v = _f32_heads(qkv, B, S, NH, D)
+    if dout.dtype != torch.float32 or not dout.is_contiguous():
+        dout = copy_into(_NA.empty(tuple(dout.shape), dtype=torch.float32, device=dout.device),
+                         dout.contiguous() if dout.dtype == torch.float32 else dout)
     do = copy_into(_NA.empty((B, NH, S, D), dtype=torch.float32, device=qkv.device),
                    dout.reshape(B, S, NH, D).permute(0, 2, 1, 3)).view(B * NH, S, D)
     dm = None
@@ -157,6 +164,8 @@ def _f32_bwd(dout, qkv, p, B, S, NH, D, keep, seed, scale):
     gq, gk, gv = packed_heads(dqkv, B, S, NH)
     for dst, src in ((gq, dq), (gk, dk), (gv, dv)):
         copy_into(dst, src.view(B, NH, S, D))
+    if qkv.dtype != torch.float32:
+        dqkv = copy_into(_NA.empty((B * S, 3 * H), dtype=qkv.dtype, device=qkv.device), dqkv)
     return dqkv
 
 
@@ -183,10 +192,10 @@ def attention_fwd(qkv, mask, B, S, NH, keep=1.0, seed=0, scale=None):
         _, lse = flash_fwd(q, k, v, _key_mask(mask, B, S), False, keep, seed, scale,
                            out=out.view(B, S, NH, D).permute(0, 2, 1, 3))
         return out, lse
-    if qkv.is_cuda and qkv.dtype == torch.float32:
-        return _f32_fwd(qkv, mask, B, S, NH, D, keep, seed, scale)
     if qkv.is_cuda:
-        raise RuntimeError('attention: no hand-written kernel for %s S=%d D=%d' % (qkv.dtype, S, D))
+        # fp32 (parity runs) or a head dim the flash kernels do not take: the materialised
+        # chain on the native kernels, in fp32
+        return _f32_fwd(qkv, mask, B, S, NH, D, keep, seed, scale)
     p, v = _ref_probs(qkv, mask, B, S, NH, D, scale)
     pd = p * _ref_dropmask(p.shape, keep, seed, p.device) if keep < 1.0 else p
     o = (pd @ v).transpose(1, 2).reshape(B * S, H)
@@ -222,7 +231,7 @@ def attention_bwd(dout, qkv, out, saved, mask, B, S, NH, keep=1.0, seed=0, scale
             flash_bwd(g4, q, k, v, o4, saved, _key_mask(mask, B, S), False, keep, seed, scale, grads=(gq, gk, gv))
             return dqkv
         raise RuntimeError('attention backward: no hand-written kernel for S=%d D=%d' % (S, D))
-    if qkv.is_cuda and qkv.dtype == torch.float32 and saved.dim() == 4:
+    if qkv.is_cuda and saved.dim() == 4:
         return _f32_bwd(dout, qkv, saved, B, S, NH, D, keep, seed, scale)
     if saved.dim() == 1:    # fused forward (S <= 256) but no fused backward: recompute probs
         saved, _ = _ref_probs(qkv, mask, B, S, NH, D, scale)

@@ -36,6 +36,39 @@ def _tr(t, f):
     return t.transpose(-1, -2) if f else t
 
 
+def matmul_pre(a, b, ta, tb, bias, activation):
+    """(act(op(a) @ op(b) + bias), the pre-activation) -- one GEMM epilogue storing both
+    when a bf16 MFMA tile takes the shape (autotuned per shape like ``matmul``), else the
+    plain GEMM plus a separate activation pass."""
+    a, b = _match(a, b)
+    A2, B2 = _tr(a, ta), _tr(b, tb)
+    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16 and A2.dim() in (2, 3):
+        from . import gemm_mfma
+        from .autotune import choose
+        shape = tuple(A2.shape[:-1]) + (B2.shape[-1],)
+        pre = _NA.empty(shape, dtype=torch.bfloat16, device=a.device)
+
+        def cand(tile):
+            return lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=tile, pre_out=pre)
+        cands = {'hip': cand(0)}
+        if A2.dim() == 2 and _big_ok(a, b, ta, tb):
+            cands['hip256'] = cand(1)
+        if A2.shape[-1] <= 2048:
+            cands['hip_lo'] = cand(3)
+        if B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
+            cands['hip96'] = cand(5)
+        key = ('gemm_pre', _sig(a), _sig(b), ta, tb, bias is not None, activation)
+        c = choose(key, cands, 'hip')
+        y = cands[c]()
+        if y is None and c != 'hip':
+            y = cands['hip']()
+        if y is not None:
+            return y, pre
+    from .elementwise import unary
+    pre = matmul(a, b, ta, tb, bias=bias)
+    return unary(activation, pre), pre
+
+
 def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     a, b = _match(a, b)
     from . import cpu_native

@@ -123,9 +123,13 @@ def _reject(where, a, b, out):
 
 
 def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None,
-         accumulate=False, splitk=1, bias_on_m=False, tile=0):
+         accumulate=False, splitk=1, bias_on_m=False, tile=0, pre_out=None):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+beta*cin) (+bias) -> act, a/b arbitrary
-    strided views (batched 3-D allowed).  Returns None if unsupported."""
+    strided views (batched 3-D allowed).  Returns None if unsupported.
+    ``pre_out``: also store the pre-activation (bias added) there -- bf16, out's shape and
+    layout -- from the same epilogue (a training GELU layer's saved input)."""
+    if pre_out is not None:
+        return _gemm_pre(a, b, pre_out, bias, act, tile, out)
     if a.dtype == torch.float32 and b.dtype == torch.float32 and (out is None or out.dtype == torch.float32) \
             and splitk == 1:
         return gemm_f32(a, b, out=out, bias=bias, act=act, alpha=alpha, beta=beta, cin=cin,
@@ -182,6 +186,35 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
             int(cin_t is not None and cin_t.dtype == torch.float32), int(bias_on_m), int(splitk),
             int(accumulate), ws.data_ptr() if ws is not None else None, int(tile), stream_ptr()),
           'gemm_bf16')
+    record_native('gemm_bf16')
+    return out
+
+
+def _gemm_pre(a, b, pre, bias, act, tile, out):
+    """bf16 out = act(a @ b + bias) and pre = a @ b + bias in one epilogue (2-D / batched)"""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != b.dim() or a.dim() not in (2, 3):
+        return _reject(11, a, b, out)
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    batch = a.shape[0] if a.dim() == 3 else 1
+    da = _operand(a, False)
+    db = _operand(b.transpose(-1, -2), False)
+    if da is None or db is None or not _aligned(a, b):
+        return _reject(12, a, b, out)
+    shape = (batch, M, N) if a.dim() == 3 else (M, N)
+    if out is None:
+        out = _NA.empty(shape, dtype=torch.bfloat16, device=a.device)
+    if out.dtype != torch.bfloat16 or pre.dtype != torch.bfloat16 or tuple(out.shape) != shape \
+            or tuple(pre.shape) != shape or out.stride() != pre.stride() or out.stride(-1) != 1:
+        return _reject(13, a, b, out)
+    ldc = out.stride(-2) if M > 1 else N
+    sC = out.stride(0) if out.dim() == 3 else 0
+    bias_t = _dense_f32(bias) if bias is not None else None
+    f = fn('hetu_gemm_bf16_pre', [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64,
+                                  I32, I32, P])
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), pre.data_ptr(),
+            bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, int(da[0]), int(db[0]),
+            batch, da[2], db[2], sC, _ACT[act], int(tile), stream_ptr()), 'gemm_bf16_pre')
     record_native('gemm_bf16')
     return out
 

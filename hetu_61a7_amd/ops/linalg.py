@@ -103,10 +103,10 @@ class LinearOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         a, b, bias = input_vals
         if self.activation == 'gelu' and self.need_pre:
-            # keep the pre-activation for the backward (instead of re-running the GEMM)
-            from ..kernels.elementwise import unary
-            pre = KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias=bias)
-            return AuxResult(unary('gelu', pre), pre)
+            # keep the pre-activation for the backward (instead of re-running the GEMM):
+            # the GEMM epilogue stores both it and the activation
+            y, pre = KG.matmul_pre(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias, 'gelu')
+            return AuxResult(y, pre)
         return KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias=bias,
                          activation=self.activation)
 

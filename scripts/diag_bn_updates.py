@@ -1,14 +1,46 @@
-"""Reproducibility of ResNet-50 (batch 4) parameter updates across executors in one process:
-for each BN-fusion setting, two eager runs; prints step losses and the relative difference
-of the per-step updates (BN parameters / the rest).  CPU runs are bitwise reproducible."""
+"""Reproducibility of ResNet-50 (batch 4) parameter updates across executors in one process
+(profiles/bn_update_repro_r5.txt): for each BN-fusion setting, two eager runs of plain SGD at
+lr 1e-3; prints the step losses and the relative difference of the per-step updates (BN
+parameters / the rest).  CPU runs are bitwise reproducible; on the GPU the atomic-order noise
+of the fused statistics / totals is amplified by batch-4 BatchNorm until consecutive steps'
+updates are uncorrelated -- why tests/test_bn_fusion_gpu.py compares gradients at lr 0."""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests'))
-import torch  # noqa: E402
+import numpy as np
+import torch
 
-import test_bn_fusion_gpu as T  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def updates(steps=2, lr=1e-3):
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.models import resnet50_imagenet
+    from hetu_61a7_amd.ops import node as _node
+    _node.G_NODE_ID = 0
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    loss, _ = resnet50_imagenet(x, y_, 1000)
+    train = ht.optim.SGDOptimizer(learning_rate=lr).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3)
+    g = torch.Generator(device='cuda')
+    g.manual_seed(0)
+    X = torch.randn((4, 3, 224, 224), device='cuda', generator=g).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (4,), device='cuda', generator=g), 1000).bfloat16()
+    pm = ex.config.placeholder_to_arr_map
+    names = sorted(n.name for n, v in pm.items() if getattr(n, 'trainable', False))
+
+    def snap():
+        vals = ex.return_tensor_values()
+        return {k: vals[k].detach().float().clone() for k in names}
+    prev, losses, ups = snap(), [], []
+    for _ in range(steps):
+        lv = ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]
+        losses.append(float(np.mean(lv)))
+        cur = snap()
+        ups.append({k: cur[k] - prev[k] for k in names})
+        prev = cur
+    return losses, ups
 
 
 def rel(a, b, sel):
@@ -20,14 +52,10 @@ def rel(a, b, sel):
 def main():
     for stats, bwd in (('0', '0'), ('1', '0'), ('0', 'all'), ('1', 'all')):
         os.environ['HETU_FUSE_BN_STATS'] = stats
-        runs = []
-        for _ in range(2):
-            os.environ['HETU_FUSE_BN_BWD'] = bwd
-            src = T._resnet_updates.__code__
-            losses, ups, _ = T._resnet_updates(False, steps=2, lr=1e-3)
-            runs.append((losses, ups))
-        print('stats=%s bwd=%s losses %s | %s' % (stats, bwd, [round(x, 5) for x in runs[0][0]],
-                                                 [round(x, 5) for x in runs[1][0]]), flush=True)
+        os.environ['HETU_FUSE_BN_BWD'] = bwd
+        runs = [updates() for _ in range(2)]
+        print('stats=%s bwd=%s losses %s | %s' % (stats, bwd, [round(v, 5) for v in runs[0][0]],
+                                                 [round(v, 5) for v in runs[1][0]]), flush=True)
         for k in range(2):
             print('   step %d: bn %.4f other %.4f' % (k, rel(runs[0][1][k], runs[1][1][k], lambda n: 'bn' in n),
                                                      rel(runs[0][1][k], runs[1][1][k], lambda n: 'bn' not in n)),

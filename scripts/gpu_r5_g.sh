@@ -9,7 +9,7 @@ T="python3 -u -m pytest -q -p no:cacheprovider --timeout 900 --timeout-method th
 echo "== tests"
 timeout -k 10 900 $T --maxfail=5 tests/test_fused_gpu.py tests/test_flash_attn_gpu.py tests/test_ring_attention_gpu.py \
     tests/test_models_gpu.py tests/test_bn_fusion_gpu.py::test_hipgraph_replays_fused_bn_backward_like_eager \
-    tests/test_native_dispatch_gpu.py::test_bert_base_bench_step_launches_no_torch_kernels tests/test_ps_dense_overlap_gpu.py tests/test_ipc_allreduce_gpu.py \
+    tests/test_native_dispatch_gpu.py::test_bert_base_bench_step_launches_no_torch_kernels tests/test_ps_dense_overlap_gpu.py tests/test_ipc_allreduce_gpu.py tests/test_gemm_gpu.py::test_matmul_pre_stores_activation_and_pre_activation \
     > gpurun_out/r5g_tests.log 2>&1
 rc=$?; tail -12 gpurun_out/r5g_tests.log
 case $rc in 0|1) ;; *) exit $rc ;; esac

@@ -265,56 +265,45 @@ def test_resnet50_forward_with_fused_bn_statistics():
     assert abs(l0 - l1) <= 2e-2 * max(1.0, abs(l0)), (l0, l1)
 
 
-def _resnet_updates(use_hipgraph, steps=6, lr=1e-5):
-    """losses and per-step parameter updates of plain SGD at a tiny rate: the weights barely
-    move, so the updates of step k in two runs are the same gradients up to atomic-order noise
-    and a broken replay shows as a per-step update mismatch.  Batch-4 BatchNorm is chaotic:
-    at lr 1e-3 a 2 % difference in one step's update (the fused backward totals' atomic order)
-    makes the next step's gradients uncorrelated (scripts/diag_bn_updates.py,
-    profiles/bn_update_repro_r5.txt), and the forward statistics fused into the conv epilogues
-    (atomic replicas) move the batch-4 variances of near-constant channels enough to do the
-    same at step 0 -- so the forward statistics take the deterministic two-pass kernel here."""
+def _resnet_grads(use_hipgraph, steps=6):
+    """losses and the flat fp32 gradient of every step of ResNet-50 (batch 4, fused BN
+    backward for every eligible layer) at learning rate 0: the weights never move, so every
+    step computes the same gradient -- up to the atomic-order noise of the fused BN totals.
+    (Comparing trajectories instead is hopeless: batch-4 BatchNorm is chaotic, a 2 % change
+    in one step's update decorrelates the next step's gradient, profiles/bn_update_repro_r5.txt.)
+    The forward statistics take the deterministic two-pass kernel."""
     import hetu_61a7_amd as ht
     from hetu_61a7_amd.models import resnet50_imagenet
     from hetu_61a7_amd.ops import node as _node
     _node.G_NODE_ID = 0
-    os.environ.setdefault('HETU_FUSE_BN_BWD', 'all')
-    stats0 = os.environ.get('HETU_FUSE_BN_STATS')
-    os.environ.setdefault('HETU_FUSE_BN_STATS', '0')
+    saved = {k: os.environ.get(k) for k in ('HETU_FUSE_BN_BWD', 'HETU_FUSE_BN_STATS')}
+    os.environ['HETU_FUSE_BN_BWD'] = 'all'
+    os.environ['HETU_FUSE_BN_STATS'] = '0'
     try:
         B = 4
         x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
         loss, _ = resnet50_imagenet(x, y_, 1000)
-        train = ht.optim.SGDOptimizer(learning_rate=lr).minimize(loss)
+        train = ht.optim.SGDOptimizer(learning_rate=0.0).minimize(loss)
         ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=3,
                          use_hipgraph=use_hipgraph)
         g = torch.Generator(device='cuda')
         g.manual_seed(0)
         X = torch.randn((B, 3, 224, 224), device="cuda", generator=g).bfloat16().contiguous(memory_format=CL)
         Y = torch.nn.functional.one_hot(torch.randint(0, 1000, (B,), device='cuda', generator=g), 1000).bfloat16()
-        pm = ex.config.placeholder_to_arr_map
-        names = sorted(n.name for n, v in pm.items() if getattr(n, 'trainable', False)
-                       and isinstance(v, torch.Tensor) and v.is_floating_point())
-
-        def flat():
-            vals = ex.return_tensor_values()
-            return {k: vals[k].detach().float().clone() for k in names}
-        out, ups = [], []
-        prev = flat()
+        out, grads = [], []
         for _ in range(steps):
             lv = ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0]
             out.append(float(np.mean(lv)))
-            cur = flat()
-            ups.append({k: cur[k] - prev[k] for k in names})
-            prev = cur
+            op = ex.subexecutor['train'].opt_ops[0]
+            grads.append(op.flat.grad[:op.flat.numel].float().clone())
         fused = sum(1 for n in ex.subexecutor['train'].computing_nodes if getattr(n, 'bn_fused', None) is not None)
-        return out, ups, fused
+        return out, grads, fused
     finally:
-        os.environ.pop('HETU_FUSE_BN_BWD', None)
-        if stats0 is None:
-            os.environ.pop('HETU_FUSE_BN_STATS', None)
-        else:
-            os.environ['HETU_FUSE_BN_STATS'] = stats0
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def test_hipgraph_replays_fused_bn_backward_like_eager():
@@ -322,15 +311,12 @@ def test_hipgraph_replays_fused_bn_backward_like_eager():
     flip; a captured step froze the flip, so every replay added into the same half and
     zeroed the other.  Small spatial sizes (every layer below 16384 rows: one replica)
     take that path.  With hipGraph replay (3 eager warm-up steps, then capture + 3
-    replays) every step's parameter update must match the eager run's."""
-    eager, ue, nf = _resnet_updates(False)
-    graph, ug, _ = _resnet_updates(True)
+    replays) every step's gradient must match the eager run's (a frozen flip doubles and
+    triples the BN totals replay after replay)."""
+    eager, ge, nf = _resnet_grads(False)
+    graph, gg, _ = _resnet_grads(True)
     assert nf >= 20, nf
-    # a frozen flip doubles and triples the BN totals replay after replay: O(1) update errors
-    np.testing.assert_allclose(graph, eager, rtol=1e-2, atol=1e-2)
-    for k, (a, b) in enumerate(zip(ug, ue)):
-        num = sum(float((a[n] - b[n]).norm()) ** 2 for n in b)
-        den = sum(float(b[n].norm()) ** 2 for n in b)
-        rel = (num / max(den, 1e-30)) ** 0.5
-        worst = sorted(((float((a[n] - b[n]).norm() / b[n].norm().clamp_min(1e-20)), n) for n in b), reverse=True)[:5]
-        assert rel < 0.1, (k, rel, worst)
+    np.testing.assert_allclose(graph, eager, rtol=1e-3, atol=1e-3)
+    for k, (a, b) in enumerate(zip(gg, ge)):
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-20))
+        assert rel < 0.05, (k, rel)

@@ -353,3 +353,19 @@ def test_gemm_into_few_columns_long_k(n):
     out = torch.empty(512, n, device=DEV)
     KG.matmul_into(x, g, True, False, out)
     assert _rel(out, ref) < _tol(out)
+
+
+@pytest.mark.parametrize('M,N,K', [(1024, 3072, 768), (8192, 3072, 768), (300, 200, 96)])
+def test_matmul_pre_stores_activation_and_pre_activation(M, N, K):
+    """one GEMM epilogue storing act(x @ w + b) and the pre-activation (the training GELU
+    layer's saved input) -- both equal to the fp32 reference to bf16 accuracy"""
+    from hetu_61a7_amd.kernels import gemm as KG
+    torch.manual_seed(0)
+    a = (torch.randn(M, K, device=DEV) * 0.3).bfloat16()
+    w = (torch.randn(K, N, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(N, device=DEV) * 0.1
+    y, pre = KG.matmul_pre(a, w, False, False, bias, 'gelu')
+    ref_pre = a.float() @ w.float() + bias
+    ref_y = torch.nn.functional.gelu(ref_pre)
+    assert _rel(pre, ref_pre) < _tol(pre)
+    assert _rel(y, ref_y) < _tol(y)

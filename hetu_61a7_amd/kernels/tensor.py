@@ -362,8 +362,19 @@ def ce_sparse_grad(g, y, lab, ignore=-1):
     return dy
 
 
+def _as_dense(t, dtype):
+    """t as a contiguous tensor of ``dtype`` through the native cast / strided-copy kernels"""
+    if t.dtype == dtype and t.is_contiguous():
+        return t
+    if t.dtype != dtype:
+        if not t.is_contiguous():
+            t = copy_into(_NA.empty(tuple(t.shape), dtype=t.dtype, device=t.device), t)
+        return copy_into(_NA.empty(tuple(t.shape), dtype=dtype, device=t.device), t)
+    return copy_into(_NA.empty(tuple(t.shape), dtype=dtype, device=t.device), t)
+
+
 def bce(y, lab):
-    y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
+    y, lab = _as_dense(y, y.dtype), _as_dense(lab, y.dtype)
     out = _NA.empty(y.shape, dtype=torch.float32, device=y.device)
     check(fn('hetu_bce', [P, P, P, I64, I32, P])(y.data_ptr(), lab.data_ptr(), out.data_ptr(), y.numel(), _bf(y),
                                                   stream_ptr()), 'bce')
@@ -372,8 +383,10 @@ def bce(y, lab):
 
 
 def bce_grad(y, lab, g):
-    y, lab = y.contiguous(), lab.to(y.dtype).contiguous()
-    g = g.float().expand(y.shape).contiguous() if g.numel() not in (1, y.numel()) else g.float().contiguous()
+    y, lab = _as_dense(y, y.dtype), _as_dense(lab, y.dtype)
+    g = _as_dense(g, torch.float32)
+    if g.numel() not in (1, y.numel()):
+        g = copy_into(_NA.empty(tuple(y.shape), dtype=torch.float32, device=y.device), g.expand(y.shape))
     gs = int(g.numel() == 1 and y.numel() != 1)
     dy = _NA.empty(y.shape, dtype=y.dtype, device=y.device)
     check(fn('hetu_bce_grad', [P, P, P, P, I64, I32, I32, P])(y.data_ptr(), lab.data_ptr(), g.data_ptr(),

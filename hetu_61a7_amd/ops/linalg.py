@@ -21,6 +21,9 @@ def _tr(t, flag):
     return t.transpose(-1, -2) if flag else t
 
 
+
+_GELU_EPI = __import__('os').environ.get('HETU_GELU_EPILOGUE', '1') == '1'
+
 class MatMulOp(Op):
     def __init__(self, a, b, trans_A=False, trans_B=False, ctx=None):
         super().__init__(MatMulOp, [a, b], ctx)
@@ -104,9 +107,14 @@ class LinearOp(Op):
         a, b, bias = input_vals
         if self.activation == 'gelu' and self.need_pre:
             # keep the pre-activation for the backward (instead of re-running the GEMM):
-            # the GEMM epilogue stores both it and the activation
-            y, pre = KG.matmul_pre(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias, 'gelu')
-            return AuxResult(y, pre)
+            # the GEMM epilogue stores both it and the activation (HETU_GELU_EPILOGUE=0: the
+            # GEMM stores the pre-activation and a separate pass applies the GELU)
+            if _GELU_EPI:
+                y, pre = KG.matmul_pre(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias, 'gelu')
+                return AuxResult(y, pre)
+            from ..kernels.elementwise import unary
+            pre = KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias=bias)
+            return AuxResult(unary('gelu', pre), pre)
         return KG.matmul(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, bias=bias,
                          activation=self.activation)
 

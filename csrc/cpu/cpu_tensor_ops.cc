@@ -101,6 +101,7 @@ inline float binary_op(int op, float a, float b, float c) {
     case 13: return std::max(a + b, 0.f);                    // add_relu
     case 14: return b / a;                                   // log_grad
     case 15: return b * 0.5f / a;                            // sqrt_grad (a = y)
+    case 17: return a > 0.f ? b * c : 0.f;                   // relu_grad_c (a = y)
     default: {                                               // 16 gelu_tanh_grad
       const float k = 0.7978845608f;
       const float t = tanhf(k * (a + 0.044715f * a * a * a));

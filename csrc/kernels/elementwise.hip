@@ -21,7 +21,8 @@ enum BinaryOp {
   B_ADD = 0, B_SUB, B_MUL, B_DIV, B_MAX, B_MIN,
   B_RELU_GRAD /* a=x b=g */, B_GELU_GRAD, B_TANH_GRAD /* a=y */, B_SIGMOID_GRAD /* a=y */,
   B_LEAKY_RELU_GRAD, B_ABS_GRAD, B_POW /* a^b */, B_ADD_RELU, B_LOG_GRAD /* a=x b=g: g/x */,
-  B_SQRT_GRAD /* a=y b=g: g/(2y) */, B_GELU_TANH_GRAD
+  B_SQRT_GRAD /* a=y b=g: g/(2y) */, B_GELU_TANH_GRAD,
+  B_RELU_GRAD_C /* a=y b=g: y > 0 ? c g : 0 (ReLU + dropout backward from the output) */
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118f)); }
@@ -94,6 +95,7 @@ __device__ __forceinline__ float bi(float a, float b, float c) {
     case B_LOG_GRAD: return b / a;
     case B_SQRT_GRAD: return b * 0.5f / a;
     case B_GELU_TANH_GRAD: return b * gelu_tanh_grad(a);
+    case B_RELU_GRAD_C: return a > 0.f ? b * c : 0.f;
   }
   return a;
 }
@@ -265,7 +267,7 @@ HETU_API int hetu_binary3(int op, const void* a, const void* b, void* y, int64_t
     BCASE(B_ADD) BCASE(B_SUB) BCASE(B_MUL) BCASE(B_DIV) BCASE(B_MAX) BCASE(B_MIN)
     BCASE(B_RELU_GRAD) BCASE(B_GELU_GRAD) BCASE(B_TANH_GRAD) BCASE(B_SIGMOID_GRAD)
     BCASE(B_LEAKY_RELU_GRAD) BCASE(B_ABS_GRAD) BCASE(B_POW) BCASE(B_ADD_RELU) BCASE(B_LOG_GRAD)
-    BCASE(B_SQRT_GRAD) BCASE(B_GELU_TANH_GRAD)
+    BCASE(B_SQRT_GRAD) BCASE(B_GELU_TANH_GRAD) BCASE(B_RELU_GRAD_C)
     default: return (int)hipErrorInvalidValue;
   }
   HETU_LAUNCH_CHECK();
@@ -322,7 +324,7 @@ HETU_API int hetu_binary_nd(int op, const void* a, const void* b, void* y, int n
     BNDCASE(B_ADD) BNDCASE(B_SUB) BNDCASE(B_MUL) BNDCASE(B_DIV) BNDCASE(B_MAX) BNDCASE(B_MIN)
     BNDCASE(B_RELU_GRAD) BNDCASE(B_GELU_GRAD) BNDCASE(B_TANH_GRAD) BNDCASE(B_SIGMOID_GRAD)
     BNDCASE(B_LEAKY_RELU_GRAD) BNDCASE(B_ABS_GRAD) BNDCASE(B_POW) BNDCASE(B_ADD_RELU) BNDCASE(B_LOG_GRAD)
-    BNDCASE(B_SQRT_GRAD) BNDCASE(B_GELU_TANH_GRAD)
+    BNDCASE(B_SQRT_GRAD) BNDCASE(B_GELU_TANH_GRAD) BNDCASE(B_RELU_GRAD_C)
     default: return (int)hipErrorInvalidValue;
   }
   HETU_LAUNCH_CHECK();

@@ -27,11 +27,15 @@ static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin
                           int64_t ldb, int64_t ldc, int64_t ldcin, int a_kmaj, int b_kmaj,
                           int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
                           float alpha, float beta, int act, int out_f32, int cin_f32,
-                          int bias_on_m, int splitk, int atomic, float* ws, int tile, void* C2, hipStream_t st) {
+                          int bias_on_m, int splitk, int atomic, float* ws, int tile, void* C2,
+                          float drop_keep, uint64_t drop_seed, hipStream_t st) {
   Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32, atomic,
          bias_on_m, ws, 0};
   ep.C2 = C2;
-  if (C2 && (splitk > 1 || atomic)) return (int)hipErrorInvalidValue;
+  ep.drop_keep = drop_keep < 1.f ? drop_keep : 0.f;
+  ep.drop_seed = drop_seed;
+  if ((C2 || ep.drop_keep > 0.f) && (splitk > 1 || atomic)) return (int)hipErrorInvalidValue;
+  if (ep.drop_keep > 0.f && (N % 8 || batch != 1)) return (int)hipErrorInvalidValue;
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   if (M <= 0 || N <= 0) return 0;
@@ -41,12 +45,13 @@ static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin
   const int64_t abytes = (a_kmaj ? (M - 1) * lda + K : (K - 1) * lda + M) * 2;
   if (bbytes >= (1ll << 31)) return (int)hipErrorInvalidValue;
   if (abytes >= (1ll << 31)) {
-    if (!a_kmaj || batch != 1 || ep.slab || splitk > 1) return (int)hipErrorInvalidValue;
+    if (!a_kmaj || batch != 1 || ep.slab || splitk > 1 || ep.drop_keep > 0.f) return (int)hipErrorInvalidValue;
     const int64_t rows = std::max<int64_t>(BIG, ((((1ll << 30) / (lda * 2)) / BIG) * BIG));
     for (int64_t m0 = 0; m0 < M; m0 += rows) {
       const int64_t mc = std::min(rows, M - m0);
       Epi e = ep;
       e.C = (char*)ep.C + m0 * ep.ldc * (ep.out_f32 ? 4 : 2);
+      if (ep.C2) e.C2 = (char*)ep.C2 + m0 * ep.ldc * 2;
       if (ep.Cin) e.Cin = (const char*)ep.Cin + m0 * ep.ldcin * (ep.cin_f32 ? 4 : 2);
       if (ep.bias && ep.bias_on_m) e.bias = ep.bias + m0;
       const int rc = K % BK == 0 ? launch_buf<true>(a + m0 * lda, b, 1, b_kmaj, lda, ldb, 0, sB, e, mc, N, K, 1, 1, st, tile)
@@ -66,7 +71,17 @@ HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* C
                             float alpha, float beta, int act, int out_f32, int cin_f32,
                             int bias_on_m, int splitk, int atomic, float* ws, int tile, hipStream_t st) {
   return gemm_bf16_impl(A, B, C, Cin, bias, M, N, K, lda, ldb, ldc, ldcin, a_kmaj, b_kmaj, batch, sA, sB, sC, sCin,
-                        alpha, beta, act, out_f32, cin_f32, bias_on_m, splitk, atomic, ws, tile, nullptr, st);
+                        alpha, beta, act, out_f32, cin_f32, bias_on_m, splitk, atomic, ws, tile, nullptr, 0.f, 0, st);
+}
+
+// bf16 C = dropout(act(A @ B + bias)) with the optional pre-activation copy C2 (nullable)
+// and dropout (keep >= 1: none) in the same epilogue
+HETU_API int hetu_gemm_bf16_ex(const void* A, const void* B, void* C, void* C2, const float* bias, int64_t M,
+                               int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmaj, int b_kmaj,
+                               int batch, int64_t sA, int64_t sB, int64_t sC, int act, int tile, float keep,
+                               int64_t seed, hipStream_t st) {
+  return gemm_bf16_impl(A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, batch, sA, sB, sC, 0,
+                        1.f, 0.f, act, 0, 0, 0, 1, 0, nullptr, tile, C2, keep, (uint64_t)seed, st);
 }
 
 // the same product, also storing the pre-activation (bias added, before `act`) into C2
@@ -76,7 +91,7 @@ HETU_API int hetu_gemm_bf16_pre(const void* A, const void* B, void* C, void* C2,
                                 int batch, int64_t sA, int64_t sB, int64_t sC, int act, int tile, hipStream_t st) {
   if (!C2) return (int)hipErrorInvalidValue;
   return gemm_bf16_impl(A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, batch, sA, sB, sC, 0,
-                        1.f, 0.f, act, 0, 0, 0, 1, 0, nullptr, tile, C2, st);
+                        1.f, 0.f, act, 0, 0, 0, 1, 0, nullptr, tile, C2, 0.f, 0, st);
 }
 
 HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }

@@ -508,6 +508,11 @@ struct Epi {
   // before the activation here and the activated value in C -- a training GELU layer
   // keeps its pre-activation for the backward without a separate activation pass
   void* C2;
+  // dropout after the activation (0 = off): element (m, n) kept with probability drop_keep
+  // and scaled by 1 / drop_keep, bits from Philox(drop_seed, (m * N + n) / 4)[(m * N + n) % 4]
+  // -- the standalone dropout kernel's counters over the [M, N] output (host: N % 8 == 0)
+  float drop_keep;
+  uint64_t drop_seed;
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -604,10 +609,12 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
   }
 }
 
+// EX: the pre-activation copy (Epi::C2) and the epilogue dropout are compiled in (plain
+// GEMM loaders only: they cost registers every other epilogue would carry).
 // BNX: the BatchNorm-backward / subgrid-Cin extensions (Epi::bnx, bnmask, bnstore, cin_w)
 // are compiled in; the plain epilogue (forward convolutions, GEMMs) keeps its register
 // budget -- the 4-blocks-per-CU tile has 128 registers and spilled with them inlined
-template <bool BNX = true>
+template <bool BNX = true, bool EX = false>
 __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (&v)[8], int64_t m, int64_t n,
                                          int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8],
                                          bool has_pre = false, uint4 pre = uint4{}) {
@@ -662,7 +669,7 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
   }
-  if (o.C2b) {   // the pre-activation, bf16 in C's layout
+  if (EX && o.C2b) {   // the pre-activation, bf16 in C's layout
     bf16* P = (bf16*)o.C2b + off;
     if (o.cvec && full) {
       store_vec<bf16>(P, v);
@@ -678,6 +685,15 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
   if (BNX && ep.bnstore) {
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = (bnmk >> t) & 1u ? v[t] : 0.f;
+  }
+  if (EX && ep.drop_keep > 0.f) {
+    const uint64_t ctr = ((uint64_t)m * (uint64_t)N + (uint64_t)n) >> 2;
+    const uint4 r0 = Philox::gen(ep.drop_seed, ctr);
+    const uint4 r1 = Philox::gen(ep.drop_seed, ctr + 1);
+    const uint32_t q[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    const float inv = 1.f / ep.drop_keep;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = Philox::u01(q[t]) < ep.drop_keep ? v[t] * inv : 0.f;
   }
   if (ep.out_f32) {
     float* Cf = (float*)o.Cb + off;
@@ -749,7 +765,7 @@ __device__ __forceinline__ void lds_barrier() {
 // ST == 1 is also the high-occupancy form for short-K, memory-bound shapes (1x1 convolutions,
 // their gradient joins): one 32 KiB LDS buffer restaged per K-tile behind a barrier and at most
 // 128 VGPRs, so 4 blocks share a CU and hide each other's DMA / epilogue latency.
-template <class LA, class LB, int ST, int WN = 4, bool BNX = false>
+template <class LA, class LB, int ST, int WN = 4, bool BNX = false, bool EX = false>
 __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                                      int64_t K, int tiles_m, int tiles_n, int ktps) {
   constexpr bool DB = ST >= 2;
@@ -919,7 +935,7 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
           v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec + 4);
 #pragma unroll
           for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
-          epi_row8<BNX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss]);
+          epi_row8<BNX, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss]);
         }
         if (use_pre && half == 0) pre_load(1, pss);
       }
@@ -990,7 +1006,7 @@ __device__ __forceinline__ void raw_barrier() {
 }
 
 
-template <class LA, class LB>
+template <class LA, class LB, bool EX = false>
 __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                              int64_t K, int tiles_m, int tiles_n, int ktps) {
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];
@@ -1177,7 +1193,7 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
 #pragma unroll
         for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
       }
-      epi_row8<true>(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
+      epi_row8<true, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
     }
     __syncthreads();
   }
@@ -1361,6 +1377,15 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
   }
   e1.slab = nullptr;
   if (splitk > 1) e1.atomic = 1;
+  if (ep.C2 || ep.drop_keep > 0.f) {
+    if constexpr (is_buf<LA>::value && is_buf<LB>::value) {
+      hipLaunchKernelGGL((gemm_big_kernel<LA, LB, true>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                         tiles_n, ktps);
+      return (int)hipGetLastError();
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
+  }
   hipLaunchKernelGGL((gemm_big_kernel<LA, LB>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
                      tiles_n, ktps);
   return (int)hipGetLastError();
@@ -1396,6 +1421,21 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
     if (splitk > 1) e1.atomic = 1;
   }
   const bool bnx = ep.bnx || ep.cin_w;
+  if (ep.C2 || ep.drop_keep > 0.f) {
+    // pre-activation copy / epilogue dropout: the EX build of the plain-GEMM loader pairs
+    if constexpr (is_buf<LA>::value && is_buf<LB>::value) {
+      if (bnx) return (int)hipErrorInvalidValue;
+      if (ktps > 1 && !single_stage)
+        hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN, false, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                           tiles_m, tiles_n, ktps);
+      else
+        hipLaunchKernelGGL((gemm_kernel<LA, LB, 1, WN, false, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                           tiles_m, tiles_n, ktps);
+      return (int)hipGetLastError();
+    } else {
+      return (int)hipErrorInvalidValue;
+    }
+  }
   if (bnx) {
     // the BN-backward / subgrid-Cin epilogue: data-gradient loader pairs only
     if constexpr (bnx_pair<LA, LB>::value) {

@@ -16,7 +16,7 @@ U = dict(relu=0, sigmoid=1, tanh=2, exp=3, log=4, sqrt=5, rsqrt=6, abs=7, neg=8,
          pow_c=18, cpow=19, clamp=20, sign=21, gt_c=22, recip=23, square=24, gelu_tanh=25)
 B = dict(add=0, sub=1, mul=2, div=3, max=4, min=5, relu_grad=6, gelu_grad=7, tanh_grad=8,
          sigmoid_grad=9, leaky_relu_grad=10, abs_grad=11, pow=12, add_relu=13, log_grad=14,
-         sqrt_grad=15, gelu_tanh_grad=16)
+         sqrt_grad=15, gelu_tanh_grad=16, relu_grad_c=17)
 
 
 def _ref_unary(op, x, c, c2):
@@ -112,6 +112,8 @@ def _ref_binary(op, a, b, c):
         cdf = 0.5 * (1.0 + torch.erf(a / math.sqrt(2.0)))
         pdf = torch.exp(-0.5 * a * a) / math.sqrt(2 * math.pi)
         return b * (cdf + a * pdf)
+    if op == 'relu_grad_c':
+        return torch.where(a > 0, b * c, torch.zeros_like(b))
     if op == 'gelu_tanh_grad':
         k = math.sqrt(2 / math.pi)
         u = k * (a + 0.044715 * a ** 3)

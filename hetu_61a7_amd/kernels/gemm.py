@@ -69,6 +69,38 @@ def matmul_pre(a, b, ta, tb, bias, activation):
     return unary(activation, pre), pre
 
 
+def matmul_act_dropout(a, b, activation, keep, seed):
+    """dropout(act(a @ b)) (bf16, 2-D) with the activation and the dropout -- the standalone
+    dropout kernel's Philox counters over the output -- in the GEMM epilogue; tiles autotuned
+    per shape.  Elsewhere: the plain GEMM with the activation epilogue, then the dropout kernel."""
+    a, b = _match(a, b)
+    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16 and a.dim() == 2 \
+            and keep < 1.0 and b.shape[-1] % 8 == 0:
+        from . import gemm_mfma
+        from .autotune import choose
+
+        def cand(tile):
+            return lambda: gemm_mfma.gemm(a, b, act=activation, tile=tile, drop=(keep, seed))
+        cands = {'hip': cand(0)}
+        if _big_ok(a, b, False, False):
+            cands['hip256'] = cand(1)
+        if a.shape[-1] <= 2048:
+            cands['hip_lo'] = cand(3)
+        if b.shape[-1] % 96 == 0 and a.shape[0] >= 1024:
+            cands['hip96'] = cand(5)
+        c = choose(('gemm_drop', _sig(a), _sig(b), activation), cands, 'hip')
+        y = cands[c]()
+        if y is None and c != 'hip':
+            y = cands['hip']()
+        if y is not None:
+            return y
+    y = matmul(a, b, activation=activation)
+    if keep < 1.0:
+        from .dropout import dropout
+        y = dropout(y, keep, seed)
+    return y
+
+
 def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     a, b = _match(a, b)
     from . import cpu_native

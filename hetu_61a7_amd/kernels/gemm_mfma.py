@@ -123,13 +123,14 @@ def _reject(where, a, b, out):
 
 
 def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out_dtype=None,
-         accumulate=False, splitk=1, bias_on_m=False, tile=0, pre_out=None):
+         accumulate=False, splitk=1, bias_on_m=False, tile=0, pre_out=None, drop=None):
     """out[M,N] = alpha * a[M,K] @ b[K,N] (+beta*cin) (+bias) -> act, a/b arbitrary
     strided views (batched 3-D allowed).  Returns None if unsupported.
     ``pre_out``: also store the pre-activation (bias added) there -- bf16, out's shape and
     layout -- from the same epilogue (a training GELU layer's saved input)."""
-    if pre_out is not None:
-        return _gemm_pre(a, b, pre_out, bias, act, tile, out)
+    if pre_out is not None or drop is not None:
+        keep, seed = drop if drop is not None else (1.0, 0)
+        return _gemm_ex(a, b, pre_out, bias, act, tile, out, keep, seed)
     if a.dtype == torch.float32 and b.dtype == torch.float32 and (out is None or out.dtype == torch.float32) \
             and splitk == 1:
         return gemm_f32(a, b, out=out, bias=bias, act=act, alpha=alpha, beta=beta, cin=cin,
@@ -190,8 +191,9 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
     return out
 
 
-def _gemm_pre(a, b, pre, bias, act, tile, out):
-    """bf16 out = act(a @ b + bias) and pre = a @ b + bias in one epilogue (2-D / batched)"""
+def _gemm_ex(a, b, pre, bias, act, tile, out, keep=1.0, seed=0):
+    """bf16 out = dropout(act(a @ b + bias)) and (``pre``, nullable) pre = a @ b + bias in one
+    epilogue (2-D / batched; dropout: 2-D, N % 8 == 0, the standalone dropout's counters)"""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != b.dim() or a.dim() not in (2, 3):
         return _reject(11, a, b, out)
     M, K = a.shape[-2], a.shape[-1]
@@ -204,17 +206,20 @@ def _gemm_pre(a, b, pre, bias, act, tile, out):
     shape = (batch, M, N) if a.dim() == 3 else (M, N)
     if out is None:
         out = _NA.empty(shape, dtype=torch.bfloat16, device=a.device)
-    if out.dtype != torch.bfloat16 or pre.dtype != torch.bfloat16 or tuple(out.shape) != shape \
-            or tuple(pre.shape) != shape or out.stride() != pre.stride() or out.stride(-1) != 1:
+    if out.dtype != torch.bfloat16 or tuple(out.shape) != shape or out.stride(-1) != 1:
         return _reject(13, a, b, out)
+    if pre is not None and (pre.dtype != torch.bfloat16 or tuple(pre.shape) != shape or out.stride() != pre.stride()):
+        return _reject(14, a, b, out)
+    if keep < 1.0 and (batch != 1 or N % 8):
+        return _reject(15, a, b, out)
     ldc = out.stride(-2) if M > 1 else N
     sC = out.stride(0) if out.dim() == 3 else 0
     bias_t = _dense_f32(bias) if bias is not None else None
-    f = fn('hetu_gemm_bf16_pre', [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64,
-                                  I32, I32, P])
-    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), pre.data_ptr(),
+    f = fn('hetu_gemm_bf16_ex', [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I64, I64,
+                                 I32, I32, F32, I64, P])
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), pre.data_ptr() if pre is not None else None,
             bias_t.data_ptr() if bias_t is not None else None, M, N, K, da[1], db[1], ldc, int(da[0]), int(db[0]),
-            batch, da[2], db[2], sC, _ACT[act], int(tile), stream_ptr()), 'gemm_bf16_pre')
+            batch, da[2], db[2], sC, _ACT[act], int(tile), float(keep), int(seed), stream_ptr()), 'gemm_bf16_ex')
     record_native('gemm_bf16')
     return out
 

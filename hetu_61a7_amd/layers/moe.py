@@ -264,11 +264,14 @@ class Expert(BaseLayer):
             x = O.linear_op(x, w1, b1, activation='relu' if self.activation is O.relu_op else None)
             if self.activation is not None and self.activation is not O.relu_op:
                 x = self.activation(x)
+        elif self.activation is O.relu_op and self.keep_prob < 1.0:
+            # ReLU and dropout in the first GEMM's epilogue (ops/linalg.py MatMulActDropoutOp)
+            x = O.matmul_act_dropout_op(x, w1, 'relu', self.keep_prob)
         else:
             x = O.matmul_op(x, w1)
             if self.activation is not None:
                 x = self.activation(x)
-        if self.keep_prob < 1.0:
+        if self.keep_prob < 1.0 and not (not self.bias and self.activation is O.relu_op):
             x = O.dropout_op(x, self.keep_prob)
         if self.bias:
             b2 = init.zeros(shape=(self.embed_dim,), name=self.name + '_bias_2')

@@ -137,6 +137,65 @@ class LinearOp(Op):
         return MatMulOp.infer_shape(self, input_shapes[:2])
 
 
+class MatMulActDropoutOp(Op):
+    """dropout(relu(A @ B)) with the ReLU and the dropout in the GEMM epilogue (the MoE
+    experts' first layer: reference layers/moe_layer Expert = linear, activation, dropout).
+    The backward needs only this output: d(A @ B) = g / keep where out > 0, else 0 -- a
+    dropped element is 0 and so is its gradient, a kept one is positive exactly where the
+    ReLU passed -- so no mask is stored or regenerated."""
+
+    def __init__(self, a, b, activation='relu', keep_prob=1.0, ctx=None):
+        super().__init__(MatMulActDropoutOp, [a, b], ctx)
+        assert activation == 'relu', activation
+        self.activation, self.keep_prob = activation, keep_prob
+        self.inference = False
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from .nn import _next_seed
+        a, b = input_vals
+        keep = 1.0 if self.inference else self.keep_prob
+        if keep >= 1.0:
+            return KG.matmul(a, b, activation=self.activation)
+        return KG.matmul_act_dropout(a, b, self.activation, keep, _next_seed())
+
+    def gradient(self, output_grad):
+        G = ReluDropoutGradOp(output_grad, self, self.keep_prob, ctx=self.raw_ctx)
+        mm = MatMulOp(self.inputs[0], self.inputs[1], False, False)
+        return list(mm.gradient(G))
+
+    def infer_shape(self, input_shapes):
+        return MatMulOp.infer_shape(self, input_shapes[:2])
+
+    matmul_attr_trans_A = False
+    matmul_attr_trans_B = False
+
+
+class ReluDropoutGradOp(Op):
+    """g / keep where the forward output is positive, else 0 (see MatMulActDropoutOp)"""
+
+    def __init__(self, grad, fwd, keep_prob, ctx=None):
+        super().__init__(ReluDropoutGradOp, [grad, fwd], ctx)
+        self.keep_prob = keep_prob
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        from ..kernels.elementwise import binary
+        g, y = input_vals
+        if g.dtype != y.dtype:
+            from ..kernels.elementwise import cast
+            g = cast(g.contiguous(), y.dtype)
+        return binary('relu_grad_c', y.contiguous(), g.contiguous(), 1.0 / self.keep_prob)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[0]
+
+
+def matmul_act_dropout_op(a, b, activation='relu', keep_prob=1.0, ctx=None):
+    return MatMulActDropoutOp(a, b, activation, keep_prob, ctx=ctx)
+
+
 class LinearGeluGradOp(Op):
     """gelu'(pre) * grad with the pre-activation saved by the forward LinearOp.
     ``emit_colsum`` (graph_opt.fuse_backward): also the row sum of the result --

@@ -369,3 +369,26 @@ def test_matmul_pre_stores_activation_and_pre_activation(M, N, K):
     ref_y = torch.nn.functional.gelu(ref_pre)
     assert _rel(pre, ref_pre) < _tol(pre)
     assert _rel(y, ref_y) < _tol(y)
+
+
+@pytest.mark.parametrize('M,N,K', [(4096, 2048, 512), (1000, 256, 200)])
+def test_matmul_act_dropout_matches_standalone_dropout(M, N, K):
+    """ReLU + dropout in the GEMM epilogue: the same Philox counters as the standalone
+    dropout kernel over the [M, N] output, so dropout(relu(a @ w)) computed in two passes is
+    the fused result to bf16 accuracy; the backward from the output alone (g / keep where
+    out > 0) equals autograd through the two-pass form"""
+    from hetu_61a7_amd.kernels import gemm as KG, dropout as KD
+    from hetu_61a7_amd.kernels.elementwise import binary
+    torch.manual_seed(1)
+    keep, seed = 0.9, 4321
+    a = (torch.randn(M, K, device=DEV) * 0.5).bfloat16()
+    w = (torch.randn(K, N, device=DEV) * 0.05).bfloat16()
+    y = KG.matmul_act_dropout(a, w, 'relu', keep, seed)
+    ref = KD.dropout(torch.relu(a.float() @ w.float()).contiguous(), keep, seed)
+    assert _rel(y, ref) < _tol(y)
+    frac = float((y == 0).float().mean())
+    assert 0.5 < frac < 0.6, frac          # ~half the ReLU outputs are 0, then 10 % dropped
+    g = torch.randn(M, N, device=DEV).bfloat16()
+    d = binary('relu_grad_c', y, g, 1.0 / keep)
+    m = KD.dropout(torch.ones(M, N, device=DEV), keep, seed) * (a.float() @ w.float() > 0).float()
+    assert _rel(d, g.float() * m) < _tol(d)

@@ -183,28 +183,47 @@ __global__ void __launch_bounds__(256) locations_k(const int64_t* __restrict__ i
                                                    const float* __restrict__ probs,
                                                    int64_t* __restrict__ loc, int* __restrict__ counts,
                                                    float* __restrict__ psum, int T, int k, int E) {
+  // 16 consecutive choices per thread per pass (4096 per pass): one block-wide exclusive
+  // scan of the per-thread hit counts per pass instead of one per 256 choices -- with few
+  // experts (one block each) the scan latency, not the bandwidth, was the cost
+  constexpr int PT = 16;
   __shared__ int wsum[4];
   __shared__ float fsum[4];
   const int e = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int base = 0;
   const int total = T * k;
-  for (int c0 = 0; c0 < total; c0 += 256) {
-    const int c = c0 + threadIdx.x;      // choice-major flat index: j * T + t
-    bool hit = false;
-    int t = 0, j = 0;
-    if (c < total) {
-      j = c / T;
-      t = c - j * T;
-      hit = idx[(int64_t)t * k + j] == e;
+  for (int c0 = 0; c0 < total; c0 += 256 * PT) {
+    const int cb = c0 + threadIdx.x * PT;
+    unsigned hits = 0u;
+    const int j0 = cb / T, t0 = cb - j0 * T;   // choice-major flat index c = j * T + t
+    {
+      int j = j0, t = t0;
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        if (cb + i < total && idx[(int64_t)t * k + j] == e) hits |= 1u << i;
+        if (++t == T) { t = 0; ++j; }
+      }
     }
-    const unsigned long long b = __ballot(hit);
-    const int before = __popcll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[w] = __popcll(b);
+    const int h = __popc(hits);
+    // inclusive scan of h over the wave
+    int incl = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
     __syncthreads();
-    int off = base;
+    int off = base + incl - h;
     for (int q = 0; q < w; ++q) off += wsum[q];
-    if (hit) loc[(int64_t)t * k + j] = off + before;
+    {
+      int j = j0, t = t0;
+      for (int i = 0; i < PT; ++i) {
+        if (hits & (1u << i)) loc[(int64_t)t * k + j] = off++;
+        if (++t == T) { t = 0; ++j; }
+      }
+    }
     base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
   }

@@ -301,7 +301,21 @@ __device__ __forceinline__ void row_scale_copy(const T* __restrict__ src, T* __r
                                                int lane, bool vec) {
   constexpr int N = Vec<T>::N;
   if (vec) {
-    for (int c = lane * N; c < d; c += 64 * N) {
+    // four 16-byte pieces per lane in flight before their stores (a d = 2048 bf16 row is
+    // exactly one group): one memory latency per row instead of one per piece
+    int c = lane * N;
+    for (; c + 3 * 64 * N < d; c += 4 * 64 * N) {
+      float v[4][N];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load_vec<T>(src + c + u * 64 * N, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) v[u][q] *= w;
+        store_vec<T>(dst + c + u * 64 * N, v[u]);
+      }
+    }
+    for (; c < d; c += 64 * N) {
       float v[N];
       load_vec<T>(src + c, v);
 #pragma unroll

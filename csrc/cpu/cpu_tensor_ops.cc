@@ -195,7 +195,7 @@ API int hetu_cpu_unary_ext(int op, const float* x, float* y, int64_t n, float c,
 // (0 on broadcast dims), nd <= 8
 API int hetu_cpu_binary_nd(int op, const float* a, const float* b, float* y, int nd, const int64_t* shape,
                            const int64_t* sa, const int64_t* sb, float c) {
-  if (op < 0 || op > 16 || nd > kMaxDims) return -1;
+  if (op < 0 || op > 17 || nd > kMaxDims) return -1;
   const NDIter it = make_iter(nd, shape, sa, sb);
   const int64_t n = numel(nd, shape);
   nd_for(it, n, [&](int64_t i, int64_t oa, int64_t ob) { y[i] = binary_op(op, a[oa], b[ob], c); });

@@ -252,6 +252,25 @@ __global__ void __launch_bounds__(256) pnorm_grad_k(const T* __restrict__ x, con
 }  // namespace
 
 // ---- C API -----------------------------------------------------------------------------
+// y[r][c] = x[r * xs] for c < C (a row broadcast along the contiguous dim, e.g. the
+// gradient of a reduction over the last axis materialised): 16-byte stores of the
+// replicated element; one thread per 16-byte chunk
+template <typename T>
+__global__ void __launch_bounds__(256) bcast_inner_k(const T* __restrict__ x, T* __restrict__ y, int64_t R,
+                                                     int64_t C, int64_t xs, int64_t ys) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t cv = C / V;
+  const int64_t n = R * cv;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cv, c = (i - r * cv) * V;
+    const T v = x[r * xs];
+    union { T e[V]; uint4 u; } pk;
+#pragma unroll
+    for (int t = 0; t < V; ++t) pk.e[t] = v;
+    *reinterpret_cast<uint4*>(y + r * ys + c) = pk.u;
+  }
+}
+
 HETU_API int hetu_nd_copy(const void* x, void* y, int elem, int nd, const int64_t* shape, const int64_t* ostride,
                           const int64_t* istride, const int64_t* shift, const int64_t* imod, hipStream_t st) {
   if (nd < 1 || nd > MAXD) return (int)hipErrorInvalidValue;
@@ -291,6 +310,22 @@ HETU_API int hetu_nd_copy(const void* x, void* y, int elem, int nd, const int64_
       sh_[nd - 1] /= 2;
       elem *= 2;
     }
+  }
+  // row broadcast along the contiguous output dim (stride-0 input): replicated 16-byte stores
+  if (plain && nd == 2 && os_[1] == 1 && is_[1] == 0 && elem <= 8 && (sh_[1] * elem) % 16 == 0 &&
+      (os_[0] * elem) % 16 == 0 && ((uintptr_t)y & 15) == 0) {
+    const int g = stream_grid(sh_[0] * (sh_[1] * elem / 16), 256, 2);
+    switch (elem) {
+      case 2: hipLaunchKernelGGL(bcast_inner_k<uint16_t>, dim3(g), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y,
+                                 sh_[0], sh_[1], is_[0], os_[0]); break;
+      case 4: hipLaunchKernelGGL(bcast_inner_k<uint32_t>, dim3(g), dim3(256), 0, st, (const uint32_t*)x, (uint32_t*)y,
+                                 sh_[0], sh_[1], is_[0], os_[0]); break;
+      case 8: hipLaunchKernelGGL(bcast_inner_k<uint64_t>, dim3(g), dim3(256), 0, st, (const uint64_t*)x, (uint64_t*)y,
+                                 sh_[0], sh_[1], is_[0], os_[0]); break;
+      default: hipLaunchKernelGGL(bcast_inner_k<uint8_t>, dim3(g), dim3(256), 0, st, (const uint8_t*)x, (uint8_t*)y,
+                                  sh_[0], sh_[1], is_[0], os_[0]); break;
+    }
+    return (int)hipGetLastError();
   }
   NDDesc d{};
   d.nd = nd;

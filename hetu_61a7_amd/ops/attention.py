@@ -34,6 +34,12 @@ def _scores(q, k, mask, scale, causal):
     return s
 
 
+
+def _note_random():
+    from ..utils.hipgraph import note_host_random
+    note_host_random()
+
+
 class AttentionOp(Op):
     def __init__(self, q, k, v, mask=None, dropout=0.0, causal=False, scale=None, ctx=None):
         inputs = [q, k, v] + ([mask] if mask is not None else [])
@@ -58,6 +64,7 @@ class AttentionOp(Op):
             seed = 0
             if keep < 1.0:
                 self.seed += 1
+                _note_random()
                 seed = (self.id << 32) + self.seed
             o, lse = KA.flash_fwd(q, k, v, mask, self.causal, keep, seed, self._scale(q.shape[-1]))
             return AuxResult(o, ('flash', lse, keep, seed))
@@ -70,6 +77,7 @@ class AttentionOp(Op):
         pd = p
         if self.keep_prob < 1.0 and not self.inference:
             self.seed += 1
+            _note_random()
             seed = (self.id << 32) + self.seed
             pd = KD.dropout(p, self.keep_prob, seed)
         o = KG.bmm(pd.to(v.dtype), v, False, False)
@@ -154,6 +162,7 @@ class PackedAttentionOp(Op):
         seed = 0
         if keep < 1.0:
             self.seed += 1
+            _note_random()
             seed = (self.id << 32) + self.seed
         out, saved = KA.attention_fwd(qkv.contiguous(), mask, self.B, self.S, self.NH, keep, seed, self.scale)
         return AuxResult(out, (saved, keep, seed))

@@ -714,6 +714,8 @@ _SEED_COUNTER = [int(time.time() * 1000) & 0xFFFFFFF]
 
 
 def _next_seed():
+    from ..utils.hipgraph import note_host_random
+    note_host_random()
     _SEED_COUNTER[0] = (_SEED_COUNTER[0] * 6364136223846793005 + 1442695040888963407) & ((1 << 62) - 1)
     return _SEED_COUNTER[0]
 

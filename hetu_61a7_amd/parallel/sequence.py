@@ -103,6 +103,8 @@ class UlyssesAttentionOp(Op):
         seed = 0
         if keep < 1.0:
             self.seed += 1
+            from ..utils.hipgraph import note_host_random
+            note_host_random()
             seed = (self.id << 32) + (self.seed << 8) + comm.rank    # distinct masks per head group
         qkv_full = scatter_heads(qkv, comm, self.B, self.S_l, self.NH, D)
         out_full, saved = KA.attention_fwd(qkv_full, mask, self.B, S, self.NH // P, keep, seed, self.scale)

@@ -13,6 +13,14 @@ import torch
 from .. import native_array as _NA
 
 _CAPTURING = [0]
+# per-call host random draws (dropout seeds, attention dropout counters): a captured graph
+# would replay the draws of the capture step forever -- the same dropout masks every step
+_HOST_RANDOM = [0]
+
+
+def note_host_random():
+    """called by every op that draws a host-side seed for its kernel launch"""
+    _HOST_RANDOM[0] += 1
 
 
 def capturing():
@@ -80,7 +88,7 @@ class GraphRunner(object):
         sub = self.sub
         self.calls += 1
         self._update_dyn()
-        if self.calls <= self.warmup:
+        if self.calls <= self.warmup or getattr(self, 'eager_only', False):
             vals = sub._run_eager(feed_dict)
             return sub._collect(vals, convert)
         new_in = self._inputs(feed_dict)
@@ -97,6 +105,7 @@ class GraphRunner(object):
             return sub._collect(vals, convert)
         if self.graph is None:
             self.sig = sig
+            r0 = _HOST_RANDOM[0]
             # static input buffers
             for n, v in new_in.items():
                 self.static_in[n] = v.clone()
@@ -116,6 +125,18 @@ class GraphRunner(object):
                     _CAPTURING[0] -= 1
             for op in sub.opt_ops:
                 op.step -= 1  # the capture itself executes nothing
+            if _HOST_RANDOM[0] != r0:
+                # the step draws host seeds (dropout): a replay would repeat this step's masks
+                # forever -- keep running eagerly (correct randomness beats the launch savings)
+                import sys
+                print('hipgraph: step draws host-side random seeds (dropout); running eagerly instead',
+                      file=sys.stderr)
+                self.close()
+                self.eager_only = True
+                base = {p: sub.config.compute_value(p) for p in sub.param_nodes}
+                base.update(new_in)
+                vals = sub._run_eager(None, vals=base)
+                return sub._collect(vals, convert)
         for n, v in new_in.items():
             self.static_in[n].copy_(v, non_blocking=True)
         self.graph.replay()

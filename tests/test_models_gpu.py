@@ -119,6 +119,26 @@ def test_hipgraph_recaptures_when_feed_shape_changes():
     np.testing.assert_allclose(out[0], out[1], rtol=1e-4, atol=1e-5)
 
 
+def test_hipgraph_declines_steps_that_draw_host_seeds():
+    """a step with dropout draws a host-side seed per call: a captured graph would replay the
+    capture step's masks forever, so the runner falls back to eager execution for good"""
+    rng = np.random.RandomState(5)
+    X = rng.randn(64, 784).astype(np.float32)
+    Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 64)]
+    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+    W = ht.init.xavier_normal((784, 10), name='Wd')
+    h = ht.dropout_op(x, 0.8)
+    loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(h, W), y_), [0])
+    train = ht.optim.SGDOptimizer(0.1).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, use_hipgraph=True)
+    ls = [float(np.asarray(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0])
+                .reshape(-1)[0]) for _ in range(8)]
+    runner = ex.subexecutor['train'].graph
+    assert getattr(runner, 'eager_only', False) and runner.graph is None
+    assert np.isfinite(ls).all()
+    assert len(set(round(v, 6) for v in ls[4:])) > 1      # fresh masks (and updates) every step
+
+
 def _tiny_bert_losses(ctx, mp=None, steps=4):
     from hetu_61a7_amd.models.bert import BertConfig, bert_pretrain_graph, synthetic_bert_batch
     from hetu_61a7_amd.ops import node as _node

@@ -80,6 +80,25 @@ __device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// ds_read_b64_tr_b16 as inline asm.  The intrinsic form carries no alias information, so
+// the compiler's waitcnt pass puts an `s_waitcnt vmcnt(0)` in front of it whenever a
+// buffer_load ... lds / global_load_lds is in flight -- which drains the K loop's operand
+// prefetch before every MN-major fragment read (NN / TN GEMMs).  The asm form is invisible
+// to that pass; every consumer of lds_frag waits with an explicit `s_waitcnt lgkmcnt(0)`
+// followed by a sched_barrier before its MFMAs use the fragments.
+__device__ __forceinline__ v4s ds_tr16(const char* p) {
+  v4s r;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+// wait for every LDS fragment read (ds_tr16 included) before the MFMAs that use them
+__device__ __forceinline__ void frag_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // fragment of 16 rows (row block rb) x 32 k (k-step s): lane holds row (lane&15),
 // k = 32s + 8(lane>>4) + j, j = 0..7
 template <bool KMAJ>
@@ -94,8 +113,8 @@ __device__ __forceinline__ v8s lds_frag(const char* lds, int rb, int s, int lane
     int k1 = s * 32 + 8 * g + q;
     const char* a1 = lds + offmn(k1, c) + 8 * (p & 1);
     const char* a2 = lds + offmn(k1 + 4, c) + 8 * (p & 1);
-    v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
-    v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
+    v4s x = ds_tr16(a1);
+    v4s y = ds_tr16(a2);
     return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
@@ -755,7 +774,8 @@ __device__ __forceinline__ void lds_barrier() {
 
 // ST: LDS stages.  1: one 32 KiB buffer when every block owns a single K-tile (short-K
 // 1x1 convolutions: more resident blocks per CU); 2: double buffer, vmcnt(0) +
-// barrier per K-tile (2 blocks per CU).  (A 3-stage variant at 1 block per CU measured
+// barrier per K-tile (2 blocks per CU); 3: the same two buffers restaged two K-tiles
+// ahead (fragments read to registers before the restage; counted vmcnt).  (A 3-stage variant at 1 block per CU measured
 // 0.5-0.8x of ST 2 on every bench_tiles shape: occupancy, not prefetch depth, hides the
 // DMA latency here.)
 // WN: 16-column MFMA blocks per wave along N.  4: 128x128 tile (waves 64x64);
@@ -823,6 +843,53 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
     for (int i = 0; i < 4; ++i) stage_dma(lb, k0, i, Bs + 1024 * i);
   };
 
+  if constexpr (ST == 3) {
+    // Two K-tiles ahead in the same two buffers: a K-tile's fragments (both k-steps) are
+    // read into registers first, and once every wave has read them the buffer is restaged
+    // with K-tile kt+2 BEFORE this tile's MFMAs -- the DMA has two tiles of MFMA time to
+    // land instead of one, at the same LDS footprint and 2 blocks per CU.  The waits are
+    // counted (vmcnt 8 = the younger tile's 8 DMAs stay in flight) and the barriers raw:
+    // __syncthreads() would drain the prefetch.
+    if (kt0 < kt1) stage(kt0, 0);
+    if (kt0 + 1 < kt1) {
+      stage(kt0 + 1, 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const char* As = smem_raw + cur * buf_stride;
+      const char* Bs = As + TILE_BYTES;
+      v8s mf[2][4], nf[2][WN];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mf[s][i] = lds_frag<LA::KMAJ>(As, wm * 4 + i, s, lane);
+#pragma unroll
+        for (int j = 0; j < WN; ++j) nf[s][j] = lds_frag<LB::KMAJ>(Bs, wn * WN + j, s, lane);
+      }
+      frag_wait();
+      lds_barrier();
+      const bool more = kt + 2 < kt1;
+      if (more) stage(kt + 2, cur);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nf[s][j], mf[s][i], acc[i][j], 0, 0, 0);
+      if (kt + 1 < kt1) {
+        if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
   if (kt0 < kt1) stage(kt0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -838,6 +905,7 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
       for (int i = 0; i < 4; ++i) mf[i] = lds_frag<LA::KMAJ>(As, wm * 4 + i, s, lane);
 #pragma unroll
       for (int j = 0; j < WN; ++j) nf[j] = lds_frag<LB::KMAJ>(Bs, wn * WN + j, s, lane);
+      frag_wait();
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -851,6 +919,7 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  }
   }
 
   // bf16 Cin (residual / gradient join, beta): this thread's Cin row pieces of the first
@@ -1399,10 +1468,11 @@ template <> struct bnx_pair<ConvDgradA, ConvDgradB> : std::true_type {};
 
 // tile: 0 = 128x128 (4 waves, 2 LDS stages, 2 blocks per CU), 1 = 256x256 (8 waves, 1 block
 // per CU), 2 = 128x64 (4 waves of 64x32; 64-channel convolutions), 3 = 128x128 single LDS
-// stage at 4 blocks per CU (short-K, memory-bound shapes), 5 = 128x96 (4 waves of 64x48).
+// stage at 4 blocks per CU (short-K, memory-bound shapes), 5 = 128x96 (4 waves of 64x48),
+// 6 / 7 = 128x128 / 128x96 with the two-ahead K loop (ST 3; plain GEMM loaders).
 template <class LA, class LB, int WN>
 static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t N, int64_t K,
-                    int batch, int splitk, hipStream_t st, bool single_stage = false) {
+                    int batch, int splitk, hipStream_t st, bool single_stage = false, bool two_ahead = false) {
   constexpr int TBN = 32 * WN;
   int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + TBN - 1) / TBN);
   int nkt = (int)((K + BK - 1) / BK);
@@ -1425,7 +1495,10 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
     // pre-activation copy / epilogue dropout: the EX build of the plain-GEMM loader pairs
     if constexpr (is_buf<LA>::value && is_buf<LB>::value) {
       if (bnx) return (int)hipErrorInvalidValue;
-      if (ktps > 1 && !single_stage)
+      if (ktps > 2 && two_ahead)
+        hipLaunchKernelGGL((gemm_kernel<LA, LB, 3, WN, false, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                           tiles_m, tiles_n, ktps);
+      else if (ktps > 1 && !single_stage)
         hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN, false, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
                            tiles_m, tiles_n, ktps);
       else
@@ -1448,6 +1521,12 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
     } else {
       return (int)hipErrorInvalidValue;
     }
+  } else if (ktps > 2 && two_ahead) {
+    if constexpr (is_buf<LA>::value && is_buf<LB>::value)
+      hipLaunchKernelGGL((gemm_kernel<LA, LB, 3, WN>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n,
+                         ktps);
+    else
+      return (int)hipErrorInvalidValue;
   } else if (ktps > 1 && !single_stage)
     hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K, tiles_m, tiles_n,
                        ktps);
@@ -1470,6 +1549,15 @@ static int launch(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_t 
     // groups do not fold by lane shuffles: no fused column statistics on this tile.
     if (ep.colstats) return (int)hipErrorInvalidValue;
     return launch_t<LA, LB, 3>(la, lb, ep, M, N, K, batch, splitk, st);
+  }
+  // 6 / 7: the 128x128 / 128x96 tiles with the two-ahead K loop (plain GEMM loaders only)
+  if (tile == 6 || tile == 7) {
+    if constexpr (!(is_buf<LA>::value && is_buf<LB>::value)) return (int)hipErrorInvalidValue;
+    if (tile == 7) {
+      if (ep.colstats) return (int)hipErrorInvalidValue;
+      return launch_t<LA, LB, 3>(la, lb, ep, M, N, K, batch, splitk, st, false, true);
+    }
+    return launch_t<LA, LB, 4>(la, lb, ep, M, N, K, batch, splitk, st, false, true);
   }
   return launch_t<LA, LB, 4>(la, lb, ep, M, N, K, batch, splitk, st);
 }

@@ -57,6 +57,10 @@ def matmul_pre(a, b, ta, tb, bias, activation):
             cands['hip_lo'] = cand(3)
         if B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
             cands['hip96'] = cand(5)
+        if A2.shape[-1] >= 3 * 64:
+            cands['hip_2a'] = cand(6)
+            if B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
+                cands['hip96_2a'] = cand(7)
         key = ('gemm_pre', _sig(a), _sig(b), ta, tb, bias is not None, activation)
         c = choose(key, cands, 'hip')
         y = cands[c]()
@@ -88,6 +92,10 @@ def matmul_act_dropout(a, b, activation, keep, seed):
             cands['hip_lo'] = cand(3)
         if b.shape[-1] % 96 == 0 and a.shape[0] >= 1024:
             cands['hip96'] = cand(5)
+        if a.shape[-1] >= 3 * 64:
+            cands['hip_2a'] = cand(6)
+            if b.shape[-1] % 96 == 0 and a.shape[0] >= 1024:
+                cands['hip96_2a'] = cand(7)
         c = choose(('gemm_drop', _sig(a), _sig(b), activation), cands, 'hip')
         y = cands[c]()
         if y is None and c != 'hip':
@@ -122,6 +130,11 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
         if a.dtype == torch.bfloat16 and B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
             # 128x96 tile: N = 768 products fill the CUs in one round (512 tiles at M 8192)
             cands['hip96'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=5)
+        if a.dtype == torch.bfloat16 and A2.shape[-1] >= 3 * 64:
+            # two-ahead K loop (operand DMA two K-tiles ahead of the MFMAs)
+            cands['hip_2a'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=6)
+            if B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
+                cands['hip96_2a'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=7)
         if a.dtype == torch.bfloat16 and A2.dim() == 2 and bias is None and activation is None and \
                 A2.shape[1] >= 8192:
             # long reductions over few output tiles (the MLM head's data gradient, K = vocab):
@@ -318,6 +331,11 @@ def matmul_into(a, b, ta, tb, out):
                 for s in (2, 3, 4, 5, 6, 7, 8):
                     if tiles * s <= 2048 and K // s >= 512:
                         cands['hip_lo_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=3))
+            if K >= 3 * 64:
+                cands['hip_2a'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=6)
+                for s in (2, 3, 4, 6, 8):
+                    if tiles * s <= 1536 and K // s >= 512:
+                        cands['hip_2a_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=6))
             if M >= 256 and N >= 256:
                 cands['hip256'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=1)
                 t256 = -(-M // 256) * -(-N // 256)
@@ -403,6 +421,10 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
             cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=3)
         if bf and B.shape[1] % 96 == 0 and A.shape[0] >= 1024:
             cands['hip96'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=5)
+        if bf and A.shape[1] >= 3 * 64:
+            cands['hip_2a'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=6)
+            if B.shape[1] % 96 == 0 and A.shape[0] >= 1024:
+                cands['hip96_2a'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=7)
         if A.shape[0] * B.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, cin=acc, beta=1.0)
         cands['hip_pad'] = lambda: gemm_mfma.padded(A, B, cin=acc, beta=1.0)

@@ -20,7 +20,8 @@ _ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I
          F32, F32, I32, I32, I32, I32, I32, I32, P, I32, P]
 # tile configurations of the kernel (gemm.hip launch): 0 = 128x128 tile, 4 waves;
 # 1 = 256x256 tile, 8 waves, phase-interleaved K loop (one block per CU)
-TILES = (0, 1, 2, 3, 5)   # 128x128, 256x256, 128x64, 128x128 single-stage (4 blocks / CU), 128x96
+TILES = (0, 1, 2, 3, 5, 6, 7)   # 128x128, 256x256, 128x64, 128x128 single-stage (4 blocks / CU), 128x96,
+#                               and 128x128 / 128x96 with the two-ahead K loop (plain GEMMs)
 MODE = os.environ.get('HETU_GEMM', 'hip')
 
 

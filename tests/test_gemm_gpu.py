@@ -79,7 +79,11 @@ CONV_SHAPES = [  # N, C, H, K, k, stride, pad
     (2, 512, 7, 512, 3, 1, 1)]   # K = 3*3*512 = 4608: the tile-3 (short-K) candidacy edge
 
 
-@pytest.mark.parametrize('tile', G.TILES)
+# tiles 6 / 7 (the two-ahead K loop) are built for the plain GEMM loaders only
+CONV_TILES = [t for t in G.TILES if t not in (6, 7)]
+
+
+@pytest.mark.parametrize('tile', CONV_TILES)
 @pytest.mark.parametrize('shape', CONV_SHAPES)
 def test_conv_passes(shape, tile):
     N, C, H, K, k, s, p = shape

@@ -19,6 +19,7 @@
 //
 // Replaces cuDNN/MIOpen for these shapes (reference src/ops/CudnnConv2d.cu:54-70).
 #include "common.h"
+#include "lds_tr.h"
 
 #include <algorithm>
 
@@ -318,6 +319,13 @@ __device__ __forceinline__ v8s tr_pair(const char* a, const char* b) {
   v4s_t y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(b));
   return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// asm form (lds_tr.h) for a K loop with the next tile's DMA in flight: the intrinsic would
+// wait for that DMA; consumers call frag_wait() before the MFMAs
+__device__ __forceinline__ v8s tr_pair_asm(const char* a, const char* b) {
+  v4s_t x = ds_tr16(a);
+  v4s_t y = ds_tr16(b);
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 template <int WD, int TH>
 __global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16* __restrict__ x,
@@ -386,9 +394,12 @@ __global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16*
       const int px0 = st * 32 + 8 * g + q, px1 = px0 + 4;
       // dy operand: pixels px0 / px1, channels 16cb + 4p .. +3
       const int dch = 2 * cb + (p >> 1), dof = (p & 1) * 8;
-      const v8s bf = tr_pair(dyb + px0 * 128 + ((dch ^ (px0 & 7)) << 4) + dof,
+      const v8s bf = tr_pair_asm(dyb + px0 * 128 + ((dch ^ (px0 & 7)) << 4) + dof,
                              dyb + px1 * 128 + ((dch ^ (px1 & 7)) << 4) + dof);
       const int ty0 = px0 / WD, tx0 = px0 - ty0 * WD, ty1 = px1 / WD, tx1 = px1 - ty1 * WD;
+      // all 18 x fragments of the k-step first (asm reads: the next tile's DMA stays in
+      // flight), one wait, then the MFMAs
+      v8s af[9][2];
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const char* r0 = ring + ((oh0 + ty0 + kh) % NSLOT) * ROWB;
@@ -399,12 +410,17 @@ __global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16*
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int xch = 2 * (cib0 + j) + (p >> 1);
-            const v8s af = tr_pair(r0 + pos0 * 128 + ((xch ^ (pos0 & 7)) << 4) + dof,
-                                   r1 + pos1 * 128 + ((xch ^ (pos1 & 7)) << 4) + dof);
-            acc[kh * 3 + kw][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[kh * 3 + kw][j], 0, 0, 0);
+            af[kh * 3 + kw][j] = tr_pair_asm(r0 + pos0 * 128 + ((xch ^ (pos0 & 7)) << 4) + dof,
+                                         r1 + pos1 * 128 + ((xch ^ (pos1 & 7)) << 4) + dof);
           }
         }
       }
+      frag_wait();
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[tp][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[tp][j], bf, acc[tp][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -24,6 +24,7 @@
 // fp32 atomics for the long-K weight-gradient GEMMs.
 #pragma once
 #include "common.h"
+#include "lds_tr.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -80,24 +81,8 @@ __device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// ds_read_b64_tr_b16 as inline asm.  The intrinsic form carries no alias information, so
-// the compiler's waitcnt pass puts an `s_waitcnt vmcnt(0)` in front of it whenever a
-// buffer_load ... lds / global_load_lds is in flight -- which drains the K loop's operand
-// prefetch before every MN-major fragment read (NN / TN GEMMs).  The asm form is invisible
-// to that pass; every consumer of lds_frag waits with an explicit `s_waitcnt lgkmcnt(0)`
-// followed by a sched_barrier before its MFMAs use the fragments.
-__device__ __forceinline__ v4s ds_tr16(const char* p) {
-  v4s r;
-  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-
-// wait for every LDS fragment read (ds_tr16 included) before the MFMAs that use them
-__device__ __forceinline__ void frag_wait() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
+// ds_tr16 / frag_wait (lds_tr.h): MN-major fragment reads that leave the operand DMA in
+// flight; every consumer of lds_frag calls frag_wait() before its MFMAs.
 
 // fragment of 16 rows (row block rb) x 32 k (k-step s): lane holds row (lane&15),
 // k = 32s + 8(lane>>4) + j, j = 0..7

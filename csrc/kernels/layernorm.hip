@@ -215,8 +215,8 @@ __global__ void __launch_bounds__(256) ln_fwd4_k(const T* __restrict__ x, const 
 // dropout; dgamma/dbeta accumulate in registers, are folded across the 4
 // waves in LDS and written as one partial row per workgroup (col_reduce2_k
 // finishes them).  LDS: 4 * N floats (dynamic).
-template <typename T, int CPL>
-__global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const T* __restrict__ xs,
+template <typename T, int CPL, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) ln_bwd4_k(const T* __restrict__ dy, const T* __restrict__ xs,
                                                   const float* __restrict__ g, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, T* __restrict__ dsum,
                                                   T* __restrict__ dx_drop, float* __restrict__ pg,
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
     for (int k = 0; k < 4; ++k) { ag[i][k] = 0.f; ab[i][k] = 0.f; ad[i][k] = 0.f; }
   }
   if (zero_a != nullptr && blockIdx.x == 0)   // col_reduce2_k accumulates its row slices into these
-    for (int j = threadIdx.x; j < N; j += 256) {
+    for (int j = threadIdx.x; j < N; j += 64 * NW) {
       zero_a[j] = 0.f;
       zero_b[j] = 0.f;
       if (zero_d != nullptr) zero_d[j] = 0.f;
@@ -265,11 +265,11 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
     }
   };
   if (r0 + w < r1) load_row(r0 + w, d, xh);
-  for (int64_t row = r0 + w; row < r1; row += 4) {
+  for (int64_t row = r0 + w; row < r1; row += NW) {
     const int64_t base = row * N;
     const float mu = mean[row], rs = rstd[row];
     float dn[CPL][4], xn[CPL][4];
-    if (row + 4 < r1) load_row(row + 4, dn, xn);
+    if (row + NW < r1) load_row(row + NW, dn, xn);
     float a = 0.f, cc = 0.f;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
@@ -324,7 +324,12 @@ __global__ void __launch_bounds__(256) ln_bwd4_k(const T* __restrict__ dy, const
     }
     __syncthreads();
     float* out = (pass == 0 ? pg : (pass == 1 ? pb : pd)) + (int64_t)blockIdx.x * N;
-    for (int j = threadIdx.x; j < N; j += 256) out[j] = lds[j] + lds[N + j] + lds[2 * N + j] + lds[3 * N + j];
+    for (int j = threadIdx.x; j < N; j += 64 * NW) {
+      float t = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) t += lds[ww * N + j];
+      out[j] = t;
+    }
     __syncthreads();
   }
 }
@@ -467,13 +472,21 @@ static void launch_fwd4(const void* x, const void* res, const float* g, const fl
                      (const T*)res, g, b, (T*)y, (T*)sum_out, mean, rstd, R, N, eps, keep, seed);
 }
 
+// waves: rows in flight per block (4 or 8); the per-block partial-row count (nblk) is the
+// same, so 8 waves double the memory-level parallelism at no extra partial traffic
 template <typename T, int CPL>
 static void launch_bwd4(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
                         void* dsum, void* dxd, float* pg, float* pb, int64_t R, int N, int nblk, int rpb,
-                        float keep, uint64_t seed, float* za, float* zb, float* pd, float* zd, hipStream_t st) {
-  hipLaunchKernelGGL((ln_bwd4_k<T, CPL>), dim3((unsigned)nblk), dim3(256), 4 * N * sizeof(float), st,
-                     (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed,
-                     za, zb, pd, zd);
+                        float keep, uint64_t seed, float* za, float* zb, float* pd, float* zd, int waves,
+                        hipStream_t st) {
+  if (waves == 8)
+    hipLaunchKernelGGL((ln_bwd4_k<T, CPL, 8>), dim3((unsigned)nblk), dim3(512), 8 * N * sizeof(float), st,
+                       (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed,
+                       za, zb, pd, zd);
+  else
+    hipLaunchKernelGGL((ln_bwd4_k<T, CPL, 4>), dim3((unsigned)nblk), dim3(256), 4 * N * sizeof(float), st,
+                       (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed,
+                       za, zb, pd, zd);
 }
 
 #define HETU_CPL_DISPATCH(CPL_NEEDED, FN, ...)                 \
@@ -500,14 +513,14 @@ template <int CPL> static void fwd4_f32(const void* x, const void* res, const fl
 template <int CPL> static void bwd4_bf16(const void* dy, const void* xs, const float* g, const float* m,
                                          const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
                                          int N, int nblk, int rpb, float keep, uint64_t seed, float* za,
-                                         float* zb, float* pd, float* zd, hipStream_t st) {
-  launch_bwd4<bf16, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, pd, zd, st);
+                                         float* zb, float* pd, float* zd, int waves, hipStream_t st) {
+  launch_bwd4<bf16, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, pd, zd, waves, st);
 }
 template <int CPL> static void bwd4_f32(const void* dy, const void* xs, const float* g, const float* m,
                                         const float* r, void* ds, void* dxd, float* pg, float* pb, int64_t R,
                                         int N, int nblk, int rpb, float keep, uint64_t seed, float* za,
-                                        float* zb, float* pd, float* zd, hipStream_t st) {
-  launch_bwd4<float, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, pd, zd, st);
+                                        float* zb, float* pd, float* zd, int waves, hipStream_t st) {
+  launch_bwd4<float, CPL>(dy, xs, g, m, r, ds, dxd, pg, pb, R, N, nblk, rpb, keep, seed, za, zb, pd, zd, waves, st);
 }
 
 }  // namespace hetu
@@ -602,10 +615,12 @@ HETU_API int hetu_ln_fused_fwd(const void* x, const void* res, const float* g, c
 // dlin (may be null): also the column sums of the x-gradient (dx_drop, or dsum
 // without dropout) -- the bias gradient of the linear layer that produced x --
 // from the same row pass.  ws: (2 + (dlin != null)) * nblk * N floats.
-HETU_API int hetu_ln_fused_bwd2(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
+// waves: 4 or 8 rows in flight per block (hetu_ln_fused_bwd2 = 4)
+HETU_API int hetu_ln_fused_bwd3(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
                                 void* dsum, void* dx_drop, float* dg, float* db, float* dlin, float* ws, int64_t R,
-                                int N, int nblk, float keep, int64_t seed, int is_bf16, int deterministic,
+                                int N, int nblk, float keep, int64_t seed, int is_bf16, int deterministic, int waves,
                                 hipStream_t st) {
+  if (waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
   if ((N & 3) || N > 2048 || R <= 0 || nblk <= 0) return (int)hipErrorInvalidValue;
   const int cpl = (N / 4 + 63) / 64;
   const int rpb = (int)((R + nblk - 1) / nblk);
@@ -616,12 +631,20 @@ HETU_API int hetu_ln_fused_bwd2(const void* dy, const void* xs, const float* g, 
   float* za = slices > 1 ? dg : nullptr;
   float* zb = slices > 1 ? db : nullptr;
   float* zd = slices > 1 ? dlin : nullptr;
-  if (is_bf16) HETU_CPL_DISPATCH(cpl, bwd4_bf16, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, pd, zd, st);
-  else HETU_CPL_DISPATCH(cpl, bwd4_f32, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, pd, zd, st);
+  if (is_bf16) HETU_CPL_DISPATCH(cpl, bwd4_bf16, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, pd, zd, waves, st);
+  else HETU_CPL_DISPATCH(cpl, bwd4_f32, dy, xs, g, mean, rstd, dsum, dx_drop, pg, pb, R, N, nblk, rpb, keep, (uint64_t)seed, za, zb, pd, zd, waves, st);
   hipLaunchKernelGGL(col_reduce2_k, dim3((unsigned)((N + 63) / 64), (unsigned)slices), dim3(256), 0, st, pg, pb, dg,
                      db, nblk, N, (const float*)pd, dlin);
   HETU_LAUNCH_CHECK();
   return 0;
+}
+
+HETU_API int hetu_ln_fused_bwd2(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,
+                                void* dsum, void* dx_drop, float* dg, float* db, float* dlin, float* ws, int64_t R,
+                                int N, int nblk, float keep, int64_t seed, int is_bf16, int deterministic,
+                                hipStream_t st) {
+  return hetu_ln_fused_bwd3(dy, xs, g, mean, rstd, dsum, dx_drop, dg, db, dlin, ws, R, N, nblk, keep, seed, is_bf16,
+                            deterministic, 4, st);
 }
 
 HETU_API int hetu_ln_fused_bwd(const void* dy, const void* xs, const float* g, const float* mean, const float* rstd,

@@ -13,6 +13,7 @@
 //   * each workgroup stores its fp32 partial tile into a slab; a vectorised reduce sums
 //     the slabs into dW (overwrite or accumulate).
 #include "common.h"
+#include "lds_tr.h"
 
 using namespace hetu;
 
@@ -29,9 +30,11 @@ __device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// asm transposing reads (lds_tr.h): the next K-step's DMA stays in flight; frag_wait()
+// before the MFMAs
 __device__ __forceinline__ v8s tr_pair(const char* a, const char* b) {
-  v4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a));
-  v4s y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(b));
+  v4s x = ds_tr16(a);
+  v4s y = ds_tr16(b);
   return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
@@ -98,6 +101,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_longk_k(const bf16* __restrict__
         const int ch = 2 * (wn * 2 + j) + (pp >> 1);
         bfr[j] = tr_pair(Bs + px0 * 128 + ((ch ^ (px0 & 7)) << 4) + dof, Bs + px1 * 128 + ((ch ^ (px1 & 7)) << 4) + dof);
       }
+      frag_wait();
       // D[n][m]: lane holds 4 consecutive n (columns of dW) for one m -> float4 stores
 #pragma unroll
       for (int i = 0; i < 2; ++i)

@@ -16,6 +16,9 @@ from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I
 # LayerNorm backward blocks (4 waves, a wave per row): more blocks keep more rows in
 # flight, fewer write fewer dgamma / dbeta partial rows (HETU_LN_BWD_BLOCKS)
 _LN_BWD_BLOCKS = int(os.environ.get('HETU_LN_BWD_BLOCKS', '512'))
+# waves (rows in flight) per LayerNorm-backward block: 8 doubles the memory-level
+# parallelism at the same number of dgamma / dbeta partial rows (HETU_LN_BWD_WAVES)
+_LN_BWD_WAVES = int(os.environ.get('HETU_LN_BWD_WAVES', '8'))
 
 def layer_norm(x, gamma, beta, eps):
     N = x.shape[-1]
@@ -132,12 +135,12 @@ def layer_norm_fused_backward(dy, s, gamma, mean, rstd, keep=1.0, seed=0, need_d
         dg, db = _dest(dg_out, N, s.device), _dest(db_out, N, s.device)
         dlin = _dest(dlin_out, N, s.device) if want_dlin else None
         from . import deterministic
-        f = fn('hetu_ln_fused_bwd2', [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, I32, P])
+        f = fn('hetu_ln_fused_bwd3', [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, F32, I64, I32, I32, I32, P])
         check(f(dyc.data_ptr(), sc.data_ptr(), gamma.float().contiguous().data_ptr(), mean.data_ptr(),
                 rstd.data_ptr(), ds.data_ptr() if ds is not None else None,
                 dx.data_ptr() if dx is not None else None, dg.data_ptr(), db.data_ptr(),
                 dlin.data_ptr() if dlin is not None else None, ws.data_ptr(), R, N, nblk,
-                float(keep), int(seed), is_bf16(s), int(deterministic()), stream_ptr()), 'ln_fused_bwd')
+                float(keep), int(seed), is_bf16(s), int(deterministic()), _LN_BWD_WAVES, stream_ptr()), 'ln_fused_bwd')
         if need_dx and keep >= 1.0:
             dx = ds
         return (ds, dx, dg, db, dlin) if want_dlin else (ds, dx, dg, db)

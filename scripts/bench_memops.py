@@ -60,9 +60,10 @@ def main():
     rep('ln_fwd_plain', timed(lambda: KL.layer_norm_fused(x, None, g, b, 1e-12)), 2 * R * N * 2)
     dy = torch.randn(R, N, device=dev).to(bf)
     for nb in [int(v) for v in args.ln_blocks.split(',')]:
-        KL._LN_BWD_BLOCKS = nb
-        fnb = lambda: KL.layer_norm_fused_backward(dy, s, g, mean, rstd, keep=0.9, seed=7, want_dlin=True)
-        rep('ln_bwd_drop_dlin', timed(fnb), 4 * R * N * 2, blocks=nb)
+        for wv in (4, 8):
+            KL._LN_BWD_BLOCKS, KL._LN_BWD_WAVES = nb, wv
+            fnb = lambda: KL.layer_norm_fused_backward(dy, s, g, mean, rstd, keep=0.9, seed=7, want_dlin=True)
+            rep('ln_bwd_drop_dlin', timed(fnb), 4 * R * N * 2, blocks=nb, waves=wv)
     pre = torch.randn(R, F, device=dev).to(bf)
     dyf = torch.randn(R, F, device=dev).to(bf)
     rep('gelu_grad_colsum', timed(lambda: KL.gelu_grad_colsum(pre, dyf)), 3 * R * F * 2)

@@ -78,6 +78,36 @@ def test_ln_backward_emits_linear_bias_grad(dt, keep, R, N):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('R,N', [(8192, 768), (1000, 1024), (37, 64)])
+def test_ln_backward_8_wave_blocks_match_4_wave_blocks(R, N, monkeypatch):
+    """The 8-waves-per-block LayerNorm backward (default) gives the 4-wave kernel's row
+    gradients bit for bit and its dgamma / dbeta / bias column sums up to summation order,
+    and both match the fp32 torch backward."""
+    from hetu_61a7_amd.kernels import layernorm as KLN
+    torch.manual_seed(1)
+    dt = torch.bfloat16
+    x = torch.randn(R, N, device='cuda').to(dt)
+    res = torch.randn(R, N, device='cuda').to(dt)
+    g = torch.rand(N, device='cuda') + 0.5
+    b = torch.randn(N, device='cuda')
+    y, s, mean, rstd = KLN.layer_norm_fused(x, res, g, b, 1e-12, 0.9, 77)
+    dy = torch.randn(R, N, device='cuda').to(dt)
+    out = {}
+    for wv in (4, 8):
+        monkeypatch.setattr(KLN, '_LN_BWD_WAVES', wv)
+        out[wv] = KLN.layer_norm_fused_backward(dy, s, g, mean, rstd, 0.9, 77, want_dlin=True)
+    for i in (0, 1):
+        assert torch.equal(out[4][i], out[8][i])
+    for i in (2, 3, 4):
+        torch.testing.assert_close(out[8][i], out[4][i], rtol=1e-4, atol=1e-3)
+    sf = s.float().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(sf, (N,), g, b, 1e-12)
+    ref.backward(dy.float())
+    rel = (out[8][0].float() - sf.grad).norm() / sf.grad.norm()
+    assert rel < 1e-2
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('R,N', [(8192, 3072), (100, 40), (3, 1024)])
 def test_gelu_grad_colsum_matches_torch(dt, R, N):

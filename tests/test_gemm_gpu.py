@@ -127,7 +127,7 @@ def test_conv_wgrad_64_channel_tiles(shape, tile, accumulate):
     assert _rel(got, wf.grad) < (1e-4 if accumulate else 2e-5)
 
 
-@pytest.mark.parametrize('tile', [t for t in G.TILES if t != 5])   # 128x96: no fused statistics
+@pytest.mark.parametrize('tile', [t for t in CONV_TILES if t != 5])   # 128x96: no fused statistics
 @pytest.mark.parametrize('shape', [(4, 64, 14, 64, 1, 1, 0), (2, 64, 13, 200, 3, 2, 1), (3, 128, 9, 256, 3, 1, 1)])
 @pytest.mark.parametrize('reps', [1, 3])
 def test_conv_fused_bn_statistics(shape, tile, reps):

@@ -20,6 +20,7 @@
 // Replaces cuDNN/MIOpen for these shapes (reference src/ops/CudnnConv2d.cu:54-70).
 #include "common.h"
 #include "lds_tr.h"
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -327,7 +328,10 @@ __device__ __forceinline__ v8s tr_pair_asm(const char* a, const char* b) {
   return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int WD, int TH>
+// ASMTR: fragment reads as asm (the next tile's DMA stays in flight: all 19 fragments of
+// a k-step, one wait, 18 MFMAs) or the intrinsic (the compiler waits for that DMA before the
+// first read, then interleaves reads and MFMAs); HETU_C64_WGRAD_ASM picks (default 1)
+template <int WD, int TH, bool ASMTR = true>
 __global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16* __restrict__ x,
                                                                    const bf16* __restrict__ dy,
                                                                    float* __restrict__ slab, int H) {
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16*
       const int px0 = st * 32 + 8 * g + q, px1 = px0 + 4;
       // dy operand: pixels px0 / px1, channels 16cb + 4p .. +3
       const int dch = 2 * cb + (p >> 1), dof = (p & 1) * 8;
-      const v8s bf = tr_pair_asm(dyb + px0 * 128 + ((dch ^ (px0 & 7)) << 4) + dof,
+      const v8s bf = (ASMTR ? tr_pair_asm : tr_pair)(dyb + px0 * 128 + ((dch ^ (px0 & 7)) << 4) + dof,
                              dyb + px1 * 128 + ((dch ^ (px1 & 7)) << 4) + dof);
       const int ty0 = px0 / WD, tx0 = px0 - ty0 * WD, ty1 = px1 / WD, tx1 = px1 - ty1 * WD;
       // all 18 x fragments of the k-step first (asm reads: the next tile's DMA stays in
@@ -410,12 +414,12 @@ __global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16*
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int xch = 2 * (cib0 + j) + (p >> 1);
-            af[kh * 3 + kw][j] = tr_pair_asm(r0 + pos0 * 128 + ((xch ^ (pos0 & 7)) << 4) + dof,
+            af[kh * 3 + kw][j] = (ASMTR ? tr_pair_asm : tr_pair)(r0 + pos0 * 128 + ((xch ^ (pos0 & 7)) << 4) + dof,
                                          r1 + pos1 * 128 + ((xch ^ (pos1 & 7)) << 4) + dof);
           }
         }
       }
-      frag_wait();
+      if constexpr (ASMTR) frag_wait();
 #pragma unroll
       for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
@@ -842,8 +846,16 @@ HETU_API int hetu_conv3x3_c64_wgrad(const void* x, const void* dy, float* dw, fl
                                     int H, int W, hipStream_t st) {
   if ((((uintptr_t)x) | ((uintptr_t)dy) | ((uintptr_t)dw) | ((uintptr_t)ws)) & 15) return (int)hipErrorInvalidValue;
   if (W != 56) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv3x3_c64_wgrad_k<56, 4>), dim3(N), dim3(WG_NW * 64), 0, st, (const bf16*)x,
-                     (const bf16*)dy, ws, H);
+  static const bool asm_tr = [] {
+    const char* e = getenv("HETU_C64_WGRAD_ASM");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (asm_tr)
+    hipLaunchKernelGGL((conv3x3_c64_wgrad_k<56, 4, true>), dim3(N), dim3(WG_NW * 64), 0, st, (const bf16*)x,
+                       (const bf16*)dy, ws, H);
+  else
+    hipLaunchKernelGGL((conv3x3_c64_wgrad_k<56, 4, false>), dim3(N), dim3(WG_NW * 64), 0, st, (const bf16*)x,
+                       (const bf16*)dy, ws, H);
   HETU_LAUNCH_CHECK();
   const int n4 = 9 * CH * CH / 4;
   hipLaunchKernelGGL(wgrad_slab_reduce_k, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws, N,

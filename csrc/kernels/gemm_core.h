@@ -81,12 +81,16 @@ __device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// ds_tr16 / frag_wait (lds_tr.h): MN-major fragment reads that leave the operand DMA in
-// flight; every consumer of lds_frag calls frag_wait() before its MFMAs.
+// ASM: the MN-major reads as ds_tr16 (lds_tr.h), which leave an in-flight operand DMA
+// alone (the intrinsic makes the compiler wait for it); the caller then calls frag_wait()
+// before its MFMAs.  Used by the double-buffered K loops (ST 2 / 3), whose next K-tile is
+// in flight while a tile's fragments are read.  The single-stage loop (nothing in flight)
+// and the 256x256 kernel keep the intrinsic: their compiler-scheduled partial lgkmcnt
+// waits interleave reads and MFMAs, and measured faster that way.
 
 // fragment of 16 rows (row block rb) x 32 k (k-step s): lane holds row (lane&15),
 // k = 32s + 8(lane>>4) + j, j = 0..7
-template <bool KMAJ>
+template <bool KMAJ, bool ASM = false>
 __device__ __forceinline__ v8s lds_frag(const char* lds, int rb, int s, int lane) {
   if constexpr (KMAJ) {
     int r = rb * 16 + (lane & 15);
@@ -98,8 +102,14 @@ __device__ __forceinline__ v8s lds_frag(const char* lds, int rb, int s, int lane
     int k1 = s * 32 + 8 * g + q;
     const char* a1 = lds + offmn(k1, c) + 8 * (p & 1);
     const char* a2 = lds + offmn(k1 + 4, c) + 8 * (p & 1);
-    v4s x = ds_tr16(a1);
-    v4s y = ds_tr16(a2);
+    v4s x, y;
+    if constexpr (ASM) {
+      x = ds_tr16(a1);
+      y = ds_tr16(a2);
+    } else {
+      x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
+      y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a2));
+    }
     return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
   }
 }
@@ -851,9 +861,9 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) mf[s][i] = lds_frag<LA::KMAJ>(As, wm * 4 + i, s, lane);
+        for (int i = 0; i < 4; ++i) mf[s][i] = lds_frag<LA::KMAJ, true>(As, wm * 4 + i, s, lane);
 #pragma unroll
-        for (int j = 0; j < WN; ++j) nf[s][j] = lds_frag<LB::KMAJ>(Bs, wn * WN + j, s, lane);
+        for (int j = 0; j < WN; ++j) nf[s][j] = lds_frag<LB::KMAJ, true>(Bs, wn * WN + j, s, lane);
       }
       frag_wait();
       lds_barrier();
@@ -887,10 +897,10 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
     for (int s = 0; s < 2; ++s) {
       v8s mf[4], nf[WN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) mf[i] = lds_frag<LA::KMAJ>(As, wm * 4 + i, s, lane);
+      for (int i = 0; i < 4; ++i) mf[i] = lds_frag<LA::KMAJ, DB>(As, wm * 4 + i, s, lane);
 #pragma unroll
-      for (int j = 0; j < WN; ++j) nf[j] = lds_frag<LB::KMAJ>(Bs, wn * WN + j, s, lane);
-      frag_wait();
+      for (int j = 0; j < WN; ++j) nf[j] = lds_frag<LB::KMAJ, DB>(Bs, wn * WN + j, s, lane);
+      if constexpr (DB) frag_wait();
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll

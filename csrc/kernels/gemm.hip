@@ -75,7 +75,7 @@ HETU_API int hetu_gemm_bf16(const void* A, const void* B, void* C, const void* C
 }
 
 // bf16 C = dropout(act(A @ B + bias)) with the optional pre-activation copy C2 (nullable)
-// and dropout (keep >= 1: none) in the same epilogue
+// or the dropout (keep >= 1: none) in the same epilogue -- not both (hipErrorInvalidValue)
 HETU_API int hetu_gemm_bf16_ex(const void* A, const void* B, void* C, void* C2, const float* bias, int64_t M,
                                int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmaj, int b_kmaj,
                                int batch, int64_t sA, int64_t sB, int64_t sC, int act, int tile, float keep,

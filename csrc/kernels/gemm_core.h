@@ -623,12 +623,14 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
   }
 }
 
-// EX: the pre-activation copy (Epi::C2) and the epilogue dropout are compiled in (plain
-// GEMM loaders only: they cost registers every other epilogue would carry).
+// EX: bit 0 compiles in the pre-activation copy (Epi::C2), bit 1 the epilogue dropout
+// (plain GEMM loaders only: they cost registers every other epilogue would carry; one
+// feature per build -- with both, the 4-blocks-per-CU tile ran out of scalar registers
+// and spilled in the epilogue).
 // BNX: the BatchNorm-backward / subgrid-Cin extensions (Epi::bnx, bnmask, bnstore, cin_w)
 // are compiled in; the plain epilogue (forward convolutions, GEMMs) keeps its register
 // budget -- the 4-blocks-per-CU tile has 128 registers and spilled with them inlined
-template <bool BNX = true, bool EX = false>
+template <bool BNX = true, int EX = 0>
 __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (&v)[8], int64_t m, int64_t n,
                                          int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8],
                                          bool has_pre = false, uint4 pre = uint4{}) {
@@ -683,7 +685,7 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
   }
-  if (EX && o.C2b) {   // the pre-activation, bf16 in C's layout
+  if ((EX & 1) && o.C2b) {   // the pre-activation, bf16 in C's layout
     bf16* P = (bf16*)o.C2b + off;
     if (o.cvec && full) {
       store_vec<bf16>(P, v);
@@ -700,7 +702,7 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = (bnmk >> t) & 1u ? v[t] : 0.f;
   }
-  if (EX && ep.drop_keep > 0.f) {
+  if ((EX & 2) && ep.drop_keep > 0.f) {
     const uint64_t ctr = ((uint64_t)m * (uint64_t)N + (uint64_t)n) >> 2;
     const uint4 r0 = Philox::gen(ep.drop_seed, ctr);
     const uint4 r1 = Philox::gen(ep.drop_seed, ctr + 1);
@@ -780,7 +782,7 @@ __device__ __forceinline__ void lds_barrier() {
 // ST == 1 is also the high-occupancy form for short-K, memory-bound shapes (1x1 convolutions,
 // their gradient joins): one 32 KiB LDS buffer restaged per K-tile behind a barrier and at most
 // 128 VGPRs, so 4 blocks share a CU and hide each other's DMA / epilogue latency.
-template <class LA, class LB, int ST, int WN = 4, bool BNX = false, bool EX = false>
+template <class LA, class LB, int ST, int WN = 4, bool BNX = false, int EX = 0>
 __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                                      int64_t K, int tiles_m, int tiles_n, int ktps) {
   constexpr bool DB = ST >= 2;
@@ -1070,7 +1072,7 @@ __device__ __forceinline__ void raw_barrier() {
 }
 
 
-template <class LA, class LB, bool EX = false>
+template <class LA, class LB, int EX = 0>
 __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                              int64_t K, int tiles_m, int tiles_n, int ktps) {
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];
@@ -1443,8 +1445,13 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
   if (splitk > 1) e1.atomic = 1;
   if (ep.C2 || ep.drop_keep > 0.f) {
     if constexpr (is_buf<LA>::value && is_buf<LB>::value) {
-      hipLaunchKernelGGL((gemm_big_kernel<LA, LB, true>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
-                         tiles_n, ktps);
+      if (ep.C2 && ep.drop_keep > 0.f) return (int)hipErrorInvalidValue;   // one feature per build
+      if (ep.C2)
+        hipLaunchKernelGGL((gemm_big_kernel<LA, LB, 1>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                           tiles_n, ktps);
+      else
+        hipLaunchKernelGGL((gemm_big_kernel<LA, LB, 2>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                           tiles_n, ktps);
       return (int)hipGetLastError();
     } else {
       return (int)hipErrorInvalidValue;
@@ -1489,16 +1496,21 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
   if (ep.C2 || ep.drop_keep > 0.f) {
     // pre-activation copy / epilogue dropout: the EX build of the plain-GEMM loader pairs
     if constexpr (is_buf<LA>::value && is_buf<LB>::value) {
-      if (bnx) return (int)hipErrorInvalidValue;
-      if (ktps > 2 && two_ahead)
-        hipLaunchKernelGGL((gemm_kernel<LA, LB, 3, WN, false, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
-                           tiles_m, tiles_n, ktps);
-      else if (ktps > 1 && !single_stage)
-        hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN, false, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
-                           tiles_m, tiles_n, ktps);
-      else
-        hipLaunchKernelGGL((gemm_kernel<LA, LB, 1, WN, false, true>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
-                           tiles_m, tiles_n, ktps);
+      if (bnx || (ep.C2 && ep.drop_keep > 0.f)) return (int)hipErrorInvalidValue;   // one feature per build
+      auto go = [&](auto ex) {
+        constexpr int X = decltype(ex)::value;
+        if (ktps > 2 && two_ahead)
+          hipLaunchKernelGGL((gemm_kernel<LA, LB, 3, WN, false, X>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                             tiles_m, tiles_n, ktps);
+        else if (ktps > 1 && !single_stage)
+          hipLaunchKernelGGL((gemm_kernel<LA, LB, 2, WN, false, X>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                             tiles_m, tiles_n, ktps);
+        else
+          hipLaunchKernelGGL((gemm_kernel<LA, LB, 1, WN, false, X>), grid, dim3(NT), 0, st, la, lb, e1, M, N, K,
+                             tiles_m, tiles_n, ktps);
+      };
+      if (ep.C2) go(std::integral_constant<int, 1>{});
+      else go(std::integral_constant<int, 2>{});
       return (int)hipGetLastError();
     } else {
       return (int)hipErrorInvalidValue;

@@ -131,6 +131,8 @@ def gemm(a, b, out=None, bias=None, act=None, alpha=1.0, beta=0.0, cin=None, out
     layout -- from the same epilogue (a training GELU layer's saved input)."""
     if pre_out is not None or drop is not None:
         keep, seed = drop if drop is not None else (1.0, 0)
+        if pre_out is not None and keep < 1.0:
+            return None          # one epilogue extension per kernel build (gemm_core.h EX)
         return _gemm_ex(a, b, pre_out, bias, act, tile, out, keep, seed)
     if a.dtype == torch.float32 and b.dtype == torch.float32 and (out is None or out.dtype == torch.float32) \
             and splitk == 1:

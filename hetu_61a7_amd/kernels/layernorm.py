@@ -16,9 +16,10 @@ from . import fn, native, stream_ptr, is_bf16, check, supported_float, P, I64, I
 # LayerNorm backward blocks (4 waves, a wave per row): more blocks keep more rows in
 # flight, fewer write fewer dgamma / dbeta partial rows (HETU_LN_BWD_BLOCKS)
 _LN_BWD_BLOCKS = int(os.environ.get('HETU_LN_BWD_BLOCKS', '512'))
-# waves (rows in flight) per LayerNorm-backward block: 8 doubles the memory-level
-# parallelism at the same number of dgamma / dbeta partial rows (HETU_LN_BWD_WAVES)
-_LN_BWD_WAVES = int(os.environ.get('HETU_LN_BWD_WAVES', '8'))
+# waves (rows in flight) per LayerNorm-backward block (HETU_LN_BWD_WAVES, 4 or 8): 8 waves
+# measured slower in the BERT step (29.3 vs 24.3 us per call at 8192 x 768, profiles/
+# bert_steady_r5d.txt vs bert_steady_r5.txt), so 4 stays the default
+_LN_BWD_WAVES = int(os.environ.get('HETU_LN_BWD_WAVES', '4'))
 
 def layer_norm(x, gamma, beta, eps):
     N = x.shape[-1]

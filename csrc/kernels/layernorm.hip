@@ -7,6 +7,7 @@
 // own dgamma/dbeta partial slab (wave-exclusive, no atomics), folded by a
 // second column-sum kernel.
 #include "common.h"
+#include <algorithm>
 
 namespace hetu {
 
@@ -251,10 +252,14 @@ __global__ void __launch_bounds__(64 * NW) ln_bwd4_k(const T* __restrict__ dy, c
       zero_b[j] = 0.f;
       if (zero_d != nullptr) zero_d[j] = 0.f;
     }
-  // software-pipelined over this wave's rows: the next row's loads are in flight
-  // while the current row is reduced and written
-  float d[CPL][4], xh[CPL][4];
-  auto load_row = [&](int64_t rw, float (&dd)[CPL][4], float (&xx)[CPL][4]) {
+  // Two rows per iteration (their reductions interleave: the per-row chain of two wave
+  // sums was the latency bound), software-pipelined: the next pair's loads -- and its
+  // mean / rstd -- are in flight while the current pair is reduced and written.
+  float d[2][CPL][4], xh[2][CPL][4];
+  float mu[2] = {0.f, 0.f}, rs[2] = {0.f, 0.f};
+  auto load_row = [&](int64_t rw, float (&dd)[CPL][4], float (&xx)[CPL][4], float& m_, float& r_) {
+    m_ = mean[rw];
+    r_ = rstd[rw];
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
       const int c = lane + 64 * i;
@@ -264,52 +269,72 @@ __global__ void __launch_bounds__(64 * NW) ln_bwd4_k(const T* __restrict__ dy, c
       }
     }
   };
-  if (r0 + w < r1) load_row(r0 + w, d, xh);
-  for (int64_t row = r0 + w; row < r1; row += NW) {
-    const int64_t base = row * N;
-    const float mu = mean[row], rs = rstd[row];
-    float dn[CPL][4], xn[CPL][4];
-    if (row + NW < r1) load_row(row + NW, dn, xn);
-    float a = 0.f, cc = 0.f;
+  int64_t row = r0 + w;
+  if (row < r1) load_row(row, d[0], xh[0], mu[0], rs[0]);
+  if (row + NW < r1) load_row(row + NW, d[1], xh[1], mu[1], rs[1]);
+  for (; row < r1; row += 2 * NW) {
+    const bool two = row + NW < r1;
+    float dn[2][CPL][4], xn[2][CPL][4], mn[2] = {0.f, 0.f}, rn[2] = {0.f, 0.f};
+    if (row + 2 * NW < r1) load_row(row + 2 * NW, dn[0], xn[0], mn[0], rn[0]);
+    if (row + 3 * NW < r1) load_row(row + 3 * NW, dn[1], xn[1], mn[1], rn[1]);
+    float a[2] = {0.f, 0.f}, cc[2] = {0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < CPL; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nc) {
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          xh[i][k] = (xh[i][k] - mu) * rs;
-          const float dg = d[i][k] * gm[i][k];
-          a += dg;
-          cc += dg * xh[i][k];
-          ag[i][k] += d[i][k] * xh[i][k];
-          ab[i][k] += d[i][k];
+      for (int i = 0; i < CPL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nc) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            xh[h][i][k] = (xh[h][i][k] - mu[h]) * rs[h];
+            const float dg = d[h][i][k] * gm[i][k];
+            a[h] += dg;
+            cc[h] += dg * xh[h][i][k];
+            ag[i][k] += d[h][i][k] * xh[h][i][k];
+            ab[i][k] += d[h][i][k];
+          }
         }
       }
     }
-    a = wave_sum(a) / (float)N;
-    cc = wave_sum(cc) / (float)N;
+    // the four sums' shuffle chains are independent (the second row's are zero, unused,
+    // when the wave has an odd row count)
+    a[0] = wave_sum(a[0]) / (float)N;
+    a[1] = wave_sum(a[1]) / (float)N;
+    cc[0] = wave_sum(cc[0]) / (float)N;
+    cc[1] = wave_sum(cc[1]) / (float)N;
 #pragma unroll
-    for (int i = 0; i < CPL; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nc) {
-        float o[4];
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int64_t base = (row + h * NW) * N;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) o[k] = rs * (d[i][k] * gm[i][k] - a - xh[i][k] * cc);
-        if (dsum != nullptr) IO4<T>::store(dsum + base + 4 * c, o);
-        if (dx_drop != nullptr) {
-          drop4(o, seed, (uint64_t)(base >> 2) + c, keep);
-          IO4<T>::store(dx_drop + base + 4 * c, o);
-        }
-        if (pd != nullptr) {
+      for (int i = 0; i < CPL; ++i) {
+        const int c = lane + 64 * i;
+        if (c < nc) {
+          float o[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) ad[i][k] += o[k];
+          for (int k = 0; k < 4; ++k) o[k] = rs[h] * (d[h][i][k] * gm[i][k] - a[h] - xh[h][i][k] * cc[h]);
+          if (dsum != nullptr) IO4<T>::store(dsum + base + 4 * c, o);
+          if (dx_drop != nullptr) {
+            drop4(o, seed, (uint64_t)(base >> 2) + c, keep);
+            IO4<T>::store(dx_drop + base + 4 * c, o);
+          }
+          if (pd != nullptr) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ad[i][k] += o[k];
+          }
         }
       }
     }
 #pragma unroll
-    for (int i = 0; i < CPL; ++i)
+    for (int h = 0; h < 2; ++h) {
+      mu[h] = mn[h];
+      rs[h] = rn[h];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { d[i][k] = dn[i][k]; xh[i][k] = xn[i][k]; }
+      for (int i = 0; i < CPL; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { d[h][i][k] = dn[h][i][k]; xh[h][i][k] = xn[h][i][k]; }
+    }
   }
   // fold the 4 waves' partials (dgamma, dbeta, then the x-gradient column sums) through LDS
   const int npass = pd != nullptr ? 3 : 2;
@@ -627,7 +652,9 @@ HETU_API int hetu_ln_fused_bwd3(const void* dy, const void* xs, const float* g, 
   float* pg = ws;
   float* pb = ws + (int64_t)nblk * N;
   float* pd = dlin != nullptr ? ws + 2 * (int64_t)nblk * N : nullptr;
-  const int slices = deterministic ? 1 : (nblk >= 256 ? 8 : (nblk >= 64 ? 4 : 1));
+  // ~16 partial rows per slice: one pass of 4 loads per array and thread, and hundreds of
+  // blocks instead of N/64 x 8 (the reduce was latency-bound at 6-9 us per LayerNorm)
+  const int slices = deterministic ? 1 : std::max(1, std::min(64, nblk / 16));
   float* za = slices > 1 ? dg : nullptr;
   float* zb = slices > 1 ? db : nullptr;
   float* zd = slices > 1 ? dlin : nullptr;
@@ -666,7 +693,7 @@ HETU_API int hetu_gelu_grad_colsum(const void* pre, const void* dy, void* g, flo
   const int RP = 256 / W;
   const int tiles = (cv + W - 1) / W;
   const int64_t rpc = (R + chunks - 1) / chunks;
-  const int slices = deterministic ? 1 : (chunks >= 256 ? 8 : (chunks >= 64 ? 4 : 1));
+  const int slices = deterministic ? 1 : std::max(1, std::min(64, chunks / 16));
   float* zo = slices > 1 ? out : nullptr;
   if (is_bf16)
     hipLaunchKernelGGL(gelu_grad_colsum_k<bf16>, dim3((unsigned)chunks, (unsigned)tiles), dim3(256), 0, st,

@@ -252,14 +252,10 @@ __global__ void __launch_bounds__(64 * NW) ln_bwd4_k(const T* __restrict__ dy, c
       zero_b[j] = 0.f;
       if (zero_d != nullptr) zero_d[j] = 0.f;
     }
-  // Two rows per iteration (their reductions interleave: the per-row chain of two wave
-  // sums was the latency bound), software-pipelined: the next pair's loads -- and its
-  // mean / rstd -- are in flight while the current pair is reduced and written.
-  float d[2][CPL][4], xh[2][CPL][4];
-  float mu[2] = {0.f, 0.f}, rs[2] = {0.f, 0.f};
-  auto load_row = [&](int64_t rw, float (&dd)[CPL][4], float (&xx)[CPL][4], float& m_, float& r_) {
-    m_ = mean[rw];
-    r_ = rstd[rw];
+  // software-pipelined over this wave's rows: the next row's loads are in flight
+  // while the current row is reduced and written
+  float d[CPL][4], xh[CPL][4];
+  auto load_row = [&](int64_t rw, float (&dd)[CPL][4], float (&xx)[CPL][4]) {
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
       const int c = lane + 64 * i;
@@ -269,72 +265,52 @@ __global__ void __launch_bounds__(64 * NW) ln_bwd4_k(const T* __restrict__ dy, c
       }
     }
   };
-  int64_t row = r0 + w;
-  if (row < r1) load_row(row, d[0], xh[0], mu[0], rs[0]);
-  if (row + NW < r1) load_row(row + NW, d[1], xh[1], mu[1], rs[1]);
-  for (; row < r1; row += 2 * NW) {
-    const bool two = row + NW < r1;
-    float dn[2][CPL][4], xn[2][CPL][4], mn[2] = {0.f, 0.f}, rn[2] = {0.f, 0.f};
-    if (row + 2 * NW < r1) load_row(row + 2 * NW, dn[0], xn[0], mn[0], rn[0]);
-    if (row + 3 * NW < r1) load_row(row + 3 * NW, dn[1], xn[1], mn[1], rn[1]);
-    float a[2] = {0.f, 0.f}, cc[2] = {0.f, 0.f};
+  if (r0 + w < r1) load_row(r0 + w, d, xh);
+  for (int64_t row = r0 + w; row < r1; row += NW) {
+    const int64_t base = row * N;
+    const float mu = mean[row], rs = rstd[row];
+    float dn[CPL][4], xn[CPL][4];
+    if (row + NW < r1) load_row(row + NW, dn, xn);
+    float a = 0.f, cc = 0.f;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
 #pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < nc) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            xh[h][i][k] = (xh[h][i][k] - mu[h]) * rs[h];
-            const float dg = d[h][i][k] * gm[i][k];
-            a[h] += dg;
-            cc[h] += dg * xh[h][i][k];
-            ag[i][k] += d[h][i][k] * xh[h][i][k];
-            ab[i][k] += d[h][i][k];
-          }
+        for (int k = 0; k < 4; ++k) {
+          xh[i][k] = (xh[i][k] - mu) * rs;
+          const float dg = d[i][k] * gm[i][k];
+          a += dg;
+          cc += dg * xh[i][k];
+          ag[i][k] += d[i][k] * xh[i][k];
+          ab[i][k] += d[i][k];
         }
       }
     }
-    // the four sums' shuffle chains are independent (the second row's are zero, unused,
-    // when the wave has an odd row count)
-    a[0] = wave_sum(a[0]) / (float)N;
-    a[1] = wave_sum(a[1]) / (float)N;
-    cc[0] = wave_sum(cc[0]) / (float)N;
-    cc[1] = wave_sum(cc[1]) / (float)N;
+    a = wave_sum(a) / (float)N;
+    cc = wave_sum(cc) / (float)N;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h == 1 && !two) break;
-      const int64_t base = (row + h * NW) * N;
+    for (int i = 0; i < CPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
+        float o[4];
 #pragma unroll
-      for (int i = 0; i < CPL; ++i) {
-        const int c = lane + 64 * i;
-        if (c < nc) {
-          float o[4];
+        for (int k = 0; k < 4; ++k) o[k] = rs * (d[i][k] * gm[i][k] - a - xh[i][k] * cc);
+        if (dsum != nullptr) IO4<T>::store(dsum + base + 4 * c, o);
+        if (dx_drop != nullptr) {
+          drop4(o, seed, (uint64_t)(base >> 2) + c, keep);
+          IO4<T>::store(dx_drop + base + 4 * c, o);
+        }
+        if (pd != nullptr) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) o[k] = rs[h] * (d[h][i][k] * gm[i][k] - a[h] - xh[h][i][k] * cc[h]);
-          if (dsum != nullptr) IO4<T>::store(dsum + base + 4 * c, o);
-          if (dx_drop != nullptr) {
-            drop4(o, seed, (uint64_t)(base >> 2) + c, keep);
-            IO4<T>::store(dx_drop + base + 4 * c, o);
-          }
-          if (pd != nullptr) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ad[i][k] += o[k];
-          }
+          for (int k = 0; k < 4; ++k) ad[i][k] += o[k];
         }
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      mu[h] = mn[h];
-      rs[h] = rn[h];
+    for (int i = 0; i < CPL; ++i)
 #pragma unroll
-      for (int i = 0; i < CPL; ++i)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { d[h][i][k] = dn[h][i][k]; xh[h][i][k] = xn[h][i][k]; }
-    }
+      for (int k = 0; k < 4; ++k) { d[i][k] = dn[i][k]; xh[i][k] = xn[i][k]; }
   }
   // fold the 4 waves' partials (dgamma, dbeta, then the x-gradient column sums) through LDS
   const int npass = pd != nullptr ? 3 : 2;

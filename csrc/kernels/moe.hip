@@ -21,6 +21,8 @@
 // backward `gate_backward` folds the gate-value gradient and the balance-loss
 // gradient into one softmax backward per token.
 #include "common.h"
+#include <stdlib.h>
+#include <algorithm>
 
 namespace hetu {
 
@@ -236,6 +238,96 @@ __global__ void __launch_bounds__(256) locations_k(const int64_t* __restrict__ i
   if (threadIdx.x == 0) {
     counts[e] = base;
     if (psum != nullptr) psum[e] = fsum[0] + fsum[1] + fsum[2] + fsum[3];
+  }
+}
+
+// Segmented form of locations_k for large T*k: the choice range is cut into S segments of
+// `seg` choices and every (expert, segment) pair is a block, so the scan runs on E*S blocks
+// instead of E (two of them for the bench's 2 experts: 0.2 ms of latency per step).
+// Pass 1 counts each segment's hits; pass 2 starts every segment at the sum of its
+// predecessors' counts and ranks its own hits with the block scan of locations_k (segment 0
+// also sums the expert's gate probabilities, in a fixed order).
+constexpr int kLocCntMax = 1 << 16;
+static __device__ int g_loc_cnt[kLocCntMax];
+
+__global__ void __launch_bounds__(256) loc_count_k(const int64_t* __restrict__ idx, int T, int k, int seg, int S) {
+  __shared__ int ws[4];
+  const int e = blockIdx.x / S, sg = blockIdx.x - e * S;
+  const int total = T * k;
+  const int c0 = sg * seg, c1 = min(total, c0 + seg);
+  int h = 0;
+  for (int c = c0 + (int)threadIdx.x; c < c1; c += 256) {
+    const int j = c / T, t = c - j * T;
+    h += idx[(int64_t)t * k + j] == e ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) g_loc_cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void __launch_bounds__(256) loc_scan_k(const int64_t* __restrict__ idx, const float* __restrict__ probs,
+                                                  int64_t* __restrict__ loc, int* __restrict__ counts,
+                                                  float* __restrict__ psum, int T, int k, int E, int seg, int S) {
+  constexpr int PT = 8;
+  __shared__ int wsum[4];
+  __shared__ float fsum[4];
+  const int e = blockIdx.x / S, sg = blockIdx.x - e * S;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int total = T * k;
+  const int c0 = sg * seg, c1 = min(total, c0 + seg);
+  // this segment's start: the predecessors' hit counts
+  int pre = 0;
+  for (int q = threadIdx.x; q < sg; q += 256) pre += g_loc_cnt[e * S + q];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (lane == 0) wsum[w] = pre;
+  __syncthreads();
+  int base = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  for (int p0 = c0; p0 < c1; p0 += 256 * PT) {
+    const int cb = p0 + threadIdx.x * PT;
+    unsigned hits = 0u;
+    const int j0 = cb / T, t0 = cb - j0 * T;
+    {
+      int j = j0, t = t0;
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        if (cb + i < c1 && idx[(int64_t)t * k + j] == e) hits |= 1u << i;
+        if (++t == T) { t = 0; ++j; }
+      }
+    }
+    const int h = __popc(hits);
+    int incl = h;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int off = base + incl - h;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    {
+      int j = j0, t = t0;
+      for (int i = 0; i < PT; ++i) {
+        if (hits & (1u << i)) loc[(int64_t)t * k + j] = off++;
+        if (++t == T) { t = 0; ++j; }
+      }
+    }
+    base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (sg == S - 1 && threadIdx.x == 0) counts[e] = base;
+  if (probs != nullptr && psum != nullptr && sg == 0) {
+    // the tokens' gate probabilities, in a fixed order (deterministic balance loss)
+    float sp = 0.f;
+    for (int t = threadIdx.x; t < T; t += 256) sp += probs[(int64_t)t * E + e];
+    sp = wave_sum(sp);
+    if (lane == 0) fsum[w] = sp;
+    __syncthreads();
+    if (threadIdx.x == 0) psum[e] = fsum[0] + fsum[1] + fsum[2] + fsum[3];
   }
 }
 
@@ -493,7 +585,19 @@ HETU_API int hetu_moe_aux(const int* counts, const float* psum, float* coef, flo
 HETU_API int hetu_moe_locations(const int64_t* idx, const float* probs, int64_t* loc, int* counts, float* psum,
                                 int T, int k, int E, hipStream_t s) {
   if (E <= 0) return 0;
-  locations_k<<<E, 256, 0, s>>>(idx, probs, loc, counts, psum, T, k, E);
+  const int64_t total = (int64_t)T * k;
+  int seg = 2048;
+  while ((total + seg - 1) / seg > 1024) seg *= 2;
+  const int S = (int)((total + seg - 1) / seg);
+  const char* env = getenv("HETU_MOE_LOC_SEGMENTED");
+  const bool segmented = (env == nullptr || env[0] != '0') && S > 1 && (int64_t)E * S <= kLocCntMax &&
+                         total <= (int64_t)seg * S;
+  if (!segmented) {
+    locations_k<<<E, 256, 0, s>>>(idx, probs, loc, counts, psum, T, k, E);
+  } else {
+    loc_count_k<<<E * S, 256, 0, s>>>(idx, T, k, seg, S);
+    loc_scan_k<<<E * S, 256, 0, s>>>(idx, probs, loc, counts, psum, T, k, E, seg, S);
+  }
   HETU_LAUNCH_CHECK();
   return 0;
 }

@@ -40,6 +40,28 @@ def test_gate_topk_and_locations(E, k):
     np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize('T,E,k,inactive', [(65536, 2, 2, 0.0), (10000, 16, 2, 0.0), (5000, 8, 4, 0.3),
+                                             (700, 3, 3, 0.0)])
+@pytest.mark.parametrize('segmented', ['1', '0'])
+def test_locations_many_segments_match_cpu(T, E, k, inactive, segmented, monkeypatch):
+    """The segmented two-pass locations scan (E x S blocks) against the CPU reference:
+    slot positions in choice-major order, per-expert counts and gate-probability sums;
+    choices with expert -1 (the dense-to-sparse gate's inactive ones) get no slot."""
+    monkeypatch.setenv('HETU_MOE_LOC_SEGMENTED', segmented)
+    rng = np.random.RandomState(T + E)
+    idx = rng.randint(0, E, size=(T, k)).astype(np.int64)
+    if inactive:
+        idx[rng.rand(T, k) < inactive] = -1
+    probs = rng.rand(T, E).astype(np.float32)
+    i, p = torch.tensor(idx), torch.tensor(probs)
+    loc, cnt, ps = KM.locations(i.cuda(), E, p.cuda())
+    rloc, rcnt, rps = KM.locations(i, E, p)
+    keep = idx >= 0
+    np.testing.assert_array_equal(loc.cpu().numpy()[keep], rloc.numpy()[keep])
+    np.testing.assert_array_equal(cnt.cpu().numpy(), rcnt.numpy())
+    np.testing.assert_allclose(ps.cpu().numpy(), rps.numpy(), rtol=1e-4, atol=1e-3)
+
+
 def test_fused_gate_layer_gpu_matches_graph_gate():
     a, b = moe_fused_vs_graph(ht.gpu(0))
     np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)

@@ -28,13 +28,17 @@ static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin
                           int batch, int64_t sA, int64_t sB, int64_t sC, int64_t sCin,
                           float alpha, float beta, int act, int out_f32, int cin_f32,
                           int bias_on_m, int splitk, int atomic, float* ws, int tile, void* C2,
-                          float drop_keep, uint64_t drop_seed, hipStream_t st) {
+                          float drop_keep, uint64_t drop_seed, hipStream_t st, const void* gmask = nullptr,
+                          float gmask_scale = 1.f) {
   Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32, atomic,
          bias_on_m, ws, 0};
   ep.C2 = C2;
   ep.drop_keep = drop_keep < 1.f ? drop_keep : 0.f;
   ep.drop_seed = drop_seed;
-  if ((C2 || ep.drop_keep > 0.f) && (splitk > 1 || atomic)) return (int)hipErrorInvalidValue;
+  ep.gmask = gmask;
+  ep.gmask_scale = gmask_scale;
+  if ((C2 || ep.drop_keep > 0.f || gmask) && (splitk > 1 || atomic)) return (int)hipErrorInvalidValue;
+  if (gmask && (batch != 1 || out_f32 || ((uintptr_t)gmask & 15))) return (int)hipErrorInvalidValue;
   if (ep.drop_keep > 0.f && (N % 8 || batch != 1)) return (int)hipErrorInvalidValue;
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
@@ -45,7 +49,7 @@ static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin
   const int64_t abytes = (a_kmaj ? (M - 1) * lda + K : (K - 1) * lda + M) * 2;
   if (bbytes >= (1ll << 31)) return (int)hipErrorInvalidValue;
   if (abytes >= (1ll << 31)) {
-    if (!a_kmaj || batch != 1 || ep.slab || splitk > 1 || ep.drop_keep > 0.f) return (int)hipErrorInvalidValue;
+    if (!a_kmaj || batch != 1 || ep.slab || splitk > 1 || ep.drop_keep > 0.f || gmask) return (int)hipErrorInvalidValue;
     const int64_t rows = std::max<int64_t>(BIG, ((((1ll << 30) / (lda * 2)) / BIG) * BIG));
     for (int64_t m0 = 0; m0 < M; m0 += rows) {
       const int64_t mc = std::min(rows, M - m0);
@@ -92,6 +96,16 @@ HETU_API int hetu_gemm_bf16_pre(const void* A, const void* B, void* C, void* C2,
   if (!C2) return (int)hipErrorInvalidValue;
   return gemm_bf16_impl(A, B, C, nullptr, bias, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, batch, sA, sB, sC, 0,
                         1.f, 0.f, act, 0, 0, 0, 1, 0, nullptr, tile, C2, 0.f, 0, st);
+}
+
+// bf16 C = (A @ B) * scale where G > 0, else 0 (G: bf16, C's shape and leading dimension)
+// -- the data gradient of a ReLU (+ dropout) output G, masked in the GEMM that produces it
+HETU_API int hetu_gemm_bf16_gmask(const void* A, const void* B, void* C, const void* G, float scale, int64_t M,
+                                  int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmaj, int b_kmaj,
+                                  int tile, hipStream_t st) {
+  if (!G) return (int)hipErrorInvalidValue;
+  return gemm_bf16_impl(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, 1, 0, 0, 0, 0, 1.f,
+                        0.f, 0, 0, 0, 0, 1, 0, nullptr, tile, nullptr, 0.f, 0, st, G, scale);
 }
 
 HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }

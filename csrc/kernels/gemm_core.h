@@ -527,6 +527,11 @@ struct Epi {
   // -- the standalone dropout kernel's counters over the [M, N] output (host: N % 8 == 0)
   float drop_keep;
   uint64_t drop_seed;
+  // gradient mask (bf16, C's layout, batch 1; null: none): out = value * gmask_scale where
+  // gmask > 0, else 0 -- the backward of ReLU (+ dropout) applied to the data-gradient GEMM
+  // that produces its input, from the forward's output alone
+  const void* gmask;
+  float gmask_scale;
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -623,7 +628,8 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
   }
 }
 
-// EX: bit 0 compiles in the pre-activation copy (Epi::C2), bit 1 the epilogue dropout
+// EX: bit 0 compiles in the pre-activation copy (Epi::C2), bit 1 the epilogue dropout,
+// bit 2 the gradient mask (Epi::gmask)
 // (plain GEMM loaders only: they cost registers every other epilogue would carry; one
 // feature per build -- with both, the 4-blocks-per-CU tile ran out of scalar registers
 // and spilled in the epilogue).
@@ -684,6 +690,18 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
+  }
+  if ((EX & 4) && ep.gmask) {   // ReLU / dropout backward: keep where the forward output is positive
+    const bf16* G = (const bf16*)ep.gmask + off;
+    float gv[8];
+    if (o.cvec && full) {
+      load_vec<bf16>(G, gv);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) gv[t] = n + t < N ? to_f(G[t]) : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = gv[t] > 0.f ? v[t] * ep.gmask_scale : 0.f;
   }
   if ((EX & 1) && o.C2b) {   // the pre-activation, bf16 in C's layout
     bf16* P = (bf16*)o.C2b + off;
@@ -1443,11 +1461,15 @@ static int launch_big(const LA& la, const LB& lb, const Epi& ep, int64_t M, int6
   }
   e1.slab = nullptr;
   if (splitk > 1) e1.atomic = 1;
-  if (ep.C2 || ep.drop_keep > 0.f) {
+  if (ep.C2 || ep.drop_keep > 0.f || ep.gmask) {
     if constexpr (is_buf<LA>::value && is_buf<LB>::value) {
-      if (ep.C2 && ep.drop_keep > 0.f) return (int)hipErrorInvalidValue;   // one feature per build
+      if ((ep.C2 ? 1 : 0) + (ep.drop_keep > 0.f ? 1 : 0) + (ep.gmask ? 1 : 0) > 1)
+        return (int)hipErrorInvalidValue;   // one feature per build
       if (ep.C2)
         hipLaunchKernelGGL((gemm_big_kernel<LA, LB, 1>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
+                           tiles_n, ktps);
+      else if (ep.gmask)
+        hipLaunchKernelGGL((gemm_big_kernel<LA, LB, 4>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
                            tiles_n, ktps);
       else
         hipLaunchKernelGGL((gemm_big_kernel<LA, LB, 2>), grid, dim3(BIG_NT), 0, st, la, lb, e1, M, N, K, tiles_m,
@@ -1493,10 +1515,12 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
     if (splitk > 1) e1.atomic = 1;
   }
   const bool bnx = ep.bnx || ep.cin_w;
-  if (ep.C2 || ep.drop_keep > 0.f) {
-    // pre-activation copy / epilogue dropout: the EX build of the plain-GEMM loader pairs
+  if (ep.C2 || ep.drop_keep > 0.f || ep.gmask) {
+    // pre-activation copy / epilogue dropout / gradient mask: the EX builds of the plain-GEMM
+    // loader pairs
     if constexpr (is_buf<LA>::value && is_buf<LB>::value) {
-      if (bnx || (ep.C2 && ep.drop_keep > 0.f)) return (int)hipErrorInvalidValue;   // one feature per build
+      if (bnx || (ep.C2 ? 1 : 0) + (ep.drop_keep > 0.f ? 1 : 0) + (ep.gmask ? 1 : 0) > 1)
+        return (int)hipErrorInvalidValue;   // one feature per build
       auto go = [&](auto ex) {
         constexpr int X = decltype(ex)::value;
         if (ktps > 2 && two_ahead)
@@ -1510,6 +1534,7 @@ static int launch_t(const LA& la, const LB& lb, const Epi& ep, int64_t M, int64_
                              tiles_m, tiles_n, ktps);
       };
       if (ep.C2) go(std::integral_constant<int, 1>{});
+      else if (ep.gmask) go(std::integral_constant<int, 4>{});
       else go(std::integral_constant<int, 2>{});
       return (int)hipGetLastError();
     } else {

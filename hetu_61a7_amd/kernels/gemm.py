@@ -109,6 +109,37 @@ def matmul_act_dropout(a, b, activation, keep, seed):
     return y
 
 
+def matmul_relu_mask(a, b, ta, tb, g, scale):
+    """(op(a) @ op(b)) * scale where g > 0, else 0: a ReLU (+ dropout) backward fused into the
+    data-gradient GEMM (bf16, 2-D; tiles autotuned per shape), else the GEMM and the
+    ``relu_grad_c`` elementwise kernel."""
+    a, b = _match(a, b)
+    A2, B2 = _tr(a, ta), _tr(b, tb)
+    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16 and A2.dim() == 2 \
+            and g.dtype == torch.bfloat16 and g.is_contiguous():
+        from . import gemm_mfma
+        from .autotune import choose
+
+        def cand(tile):
+            return lambda: gemm_mfma.gemm_gmask(A2, B2, g, scale, tile=tile)
+        cands = {'hip': cand(0)}
+        if _big_ok(a, b, ta, tb):
+            cands['hip256'] = cand(1)
+        if A2.shape[-1] <= 2048:
+            cands['hip_lo'] = cand(3)
+        if A2.shape[-1] >= 3 * 64:
+            cands['hip_2a'] = cand(6)
+        c = choose(('gemm_gmask', _sig(a), _sig(b), ta, tb), cands, 'hip')
+        y = cands[c]()
+        if y is None and c != 'hip':
+            y = cands['hip']()
+        if y is not None:
+            return y
+    from .elementwise import binary
+    y = matmul(a, b, ta, tb)
+    return binary('relu_grad_c', g.contiguous(), y.contiguous(), float(scale))
+
+
 def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     a, b = _match(a, b)
     from . import cpu_native

@@ -227,6 +227,31 @@ def _gemm_ex(a, b, pre, bias, act, tile, out, keep=1.0, seed=0):
     return out
 
 
+def gemm_gmask(a, b, g, scale, tile=0, out=None):
+    """bf16 out = (a @ b) * scale where g > 0, else 0 (2-D; g bf16 of the output's shape,
+    contiguous): the data gradient of a ReLU (+ dropout) output g computed and masked in one
+    GEMM epilogue.  None when unsupported."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
+        return _reject(21, a, b, out)
+    M, K = a.shape
+    N = b.shape[1]
+    da = _operand(a, False)
+    db = _operand(b.t(), False)
+    if da is None or db is None or not _aligned(a, b):
+        return _reject(22, a, b, out)
+    if g.dtype != torch.bfloat16 or tuple(g.shape) != (M, N) or not g.is_contiguous() or g.data_ptr() % 16:
+        return _reject(23, a, b, out)
+    if out is None:
+        out = _NA.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if out.dtype != torch.bfloat16 or tuple(out.shape) != (M, N) or not out.is_contiguous():
+        return _reject(24, a, b, out)
+    f = fn('hetu_gemm_bf16_gmask', [P, P, P, P, F32, I64, I64, I64, I64, I64, I64, I32, I32, I32, P])
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), g.data_ptr(), float(scale), M, N, K, da[1], db[1], N,
+            int(da[0]), int(db[0]), int(tile), stream_ptr()), 'gemm_bf16_gmask')
+    record_native('gemm_bf16')
+    return out
+
+
 SMALL_MAX_OUT = 1 << 16
 
 

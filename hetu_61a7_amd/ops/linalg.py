@@ -8,6 +8,8 @@ operand is bf16 both are computed in bf16 with fp32 accumulation.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from .. import native_array as _NA
 
@@ -159,7 +161,13 @@ class MatMulActDropoutOp(Op):
         return KG.matmul_act_dropout(a, b, self.activation, keep, _next_seed())
 
     def gradient(self, output_grad):
-        G = ReluDropoutGradOp(output_grad, self, self.keep_prob, ctx=self.raw_ctx)
+        if type(output_grad) is MatMulOp and len(output_grad.inputs) == 2 and _GMASK_EPI:
+            # the gradient arriving here is the next layer's data-gradient GEMM: mask it in
+            # that GEMM's epilogue (one pass less over the [tokens, hidden] activation)
+            G = MatMulReluMaskOp(output_grad.inputs[0], output_grad.inputs[1], output_grad.matmul_attr_trans_A,
+                                 output_grad.matmul_attr_trans_B, self, self.keep_prob, ctx=self.raw_ctx)
+        else:
+            G = ReluDropoutGradOp(output_grad, self, self.keep_prob, ctx=self.raw_ctx)
         mm = MatMulOp(self.inputs[0], self.inputs[1], False, False)
         return list(mm.gradient(G))
 
@@ -190,6 +198,31 @@ class ReluDropoutGradOp(Op):
 
     def infer_shape(self, input_shapes):
         return input_shapes[0]
+
+
+class MatMulReluMaskOp(Op):
+    """(op(a) @ op(b)) / keep where the forward output ``fwd`` is positive, else 0: the data
+    gradient of a MatMulActDropoutOp's output, produced and masked by one GEMM
+    (``HETU_GMASK_EPILOGUE=0``: the plain GEMM + ReluDropoutGradOp)."""
+
+    def __init__(self, a, b, trans_A, trans_B, fwd, keep_prob, ctx=None):
+        super().__init__(MatMulReluMaskOp, [a, b, fwd], ctx)
+        self.matmul_attr_trans_A, self.matmul_attr_trans_B = trans_A, trans_B
+        self.keep_prob = keep_prob
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        a, b, y = input_vals
+        return KG.matmul_relu_mask(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, y.contiguous(),
+                                   1.0 / self.keep_prob)
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return MatMulOp.infer_shape(self, input_shapes[:2])
+
+
+_GMASK_EPI = os.environ.get('HETU_GMASK_EPILOGUE', '1') != '0'
 
 
 def matmul_act_dropout_op(a, b, activation='relu', keep_prob=1.0, ctx=None):

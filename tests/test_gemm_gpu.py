@@ -396,3 +396,30 @@ def test_matmul_act_dropout_matches_standalone_dropout(M, N, K):
     d = binary('relu_grad_c', y, g, 1.0 / keep)
     m = KD.dropout(torch.ones(M, N, device=DEV), keep, seed) * (a.float() @ w.float() > 0).float()
     assert _rel(d, g.float() * m) < _tol(d)
+
+
+@pytest.mark.parametrize('tile', [0, 1, 3, 6])
+@pytest.mark.parametrize('M,N,K,tb', [(4096, 512, 768, True), (1000, 264, 136, False), (256, 2048, 2048, True)])
+def test_gemm_relu_mask_epilogue(M, N, K, tb, tile):
+    """The data gradient of a ReLU (+ dropout) output y masked in the GEMM epilogue:
+    (g @ w^T) / keep where y > 0, else 0 -- against the plain GEMM and the relu_grad_c
+    kernel, and against the fp32 torch product; autotuned entry point too."""
+    from hetu_61a7_amd.kernels import gemm as KG
+    from hetu_61a7_amd.kernels.elementwise import binary
+    torch.manual_seed(2)
+    keep = 0.9
+    g = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) if tb else torch.randn(K, N, device=DEV)).bfloat16()
+    y = torch.relu(torch.randn(M, N, device=DEV)).bfloat16()
+    B = w.t() if tb else w
+    out = G.gemm_gmask(g, B, y, 1.0 / keep, tile=tile)
+    if out is None:
+        pytest.skip('tile %d does not take this shape' % tile)
+    ref = (g.float() @ B.float()) * (y.float() > 0).float() / keep
+    assert _rel(out, ref) < _tol(out)
+    assert bool((out[y == 0] == 0).all())
+    two = binary('relu_grad_c', y, KG.matmul(g, w, False, tb), 1.0 / keep)
+    assert _rel(out, two) < _tol(out)
+    auto = KG.matmul_relu_mask(g, w, False, tb, y, 1.0 / keep)
+    assert _rel(auto, ref) < _tol(auto)
+

@@ -187,6 +187,30 @@ def test_moe_top_bf16_step():
     assert np.isfinite(l2).all() and l2[-1] < l2[0], l2
 
 
+@pytest.mark.parametrize('gate', ['topk', 'dts'])
+def test_moe_expert_gradient_mask_epilogue_matches_two_pass(gate, monkeypatch):
+    """The expert's ReLU + dropout backward masked inside the data-gradient GEMM
+    (MatMulReluMaskOp) trains like the plain GEMM + relu_grad_c pair: same losses over
+    a few SGD steps (bf16 rounding of the intermediate only)."""
+    from hetu_61a7_amd.models.moe import moe_top, moe_random_batch
+    from hetu_61a7_amd.ops import linalg
+    B, T, d = 2, 128, 256
+    X, Y = moe_random_batch(B, T, d)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(linalg, '_GMASK_EPI', fused)
+        x, y_ = ht.Variable(name='x', trainable=False), ht.Variable(name='y_', trainable=False)
+        loss, _ = moe_top(x, y_, B, T, d, 512, 2, top=2, gate=gate)
+        train = ht.optim.SGDOptimizer(0.05).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), mixed_precision='bf16', seed=5)
+        kinds = {type(n).__name__ for n in ex.subexecutor['train'].topo_order}
+        assert ('MatMulReluMaskOp' in kinds) == fused, kinds
+        res[fused] = [float(np.asarray(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0])
+                            .reshape(-1)[0]) for _ in range(4)]
+    assert np.isfinite(res[True]).all(), res
+    np.testing.assert_allclose(res[True], res[False], rtol=2e-2, atol=1e-3)
+
+
 def test_bert_base_width_bf16_forward_matches_fp32():
     """BERT-base widths (hidden 768, 12 heads, FFN 3072, seq 128) with two layers:
     the bf16 forward (fused attention, fused LayerNorm tails, MFMA GEMMs) stays

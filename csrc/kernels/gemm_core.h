@@ -639,7 +639,8 @@ __device__ __forceinline__ void epi_init(const Epi& ep, EpiOut& o, int64_t batch
 template <bool BNX = true, int EX = 0>
 __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (&v)[8], int64_t m, int64_t n,
                                          int64_t N, int64_t orow, float (&cs)[8], float (&cq)[8],
-                                         bool has_pre = false, uint4 pre = uint4{}) {
+                                         bool has_pre = false, uint4 pre = uint4{}, bool has_gm = false,
+                                         uint4 gmv = uint4{}) {
   // pre: this row piece of Cin, already loaded (by value: a selected pointer into the
   // caller's prefetch array would keep that array in scratch memory)
   const bool full = n + 7 < N;
@@ -694,7 +695,14 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
   if ((EX & 4) && ep.gmask) {   // ReLU / dropout backward: keep where the forward output is positive
     const bf16* G = (const bf16*)ep.gmask + off;
     float gv[8];
-    if (o.cvec && full) {
+    if (has_gm && full) {   // prefetched by the caller (this row piece, C's alignment)
+      const uint32_t w[4] = {gmv.x, gmv.y, gmv.z, gmv.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        gv[2 * t] = bf16_bits_to_f((unsigned short)(w[t] & 0xffffu));
+        gv[2 * t + 1] = bf16_bits_to_f((unsigned short)(w[t] >> 16));
+      }
+    } else if (o.cvec && full) {
       load_vec<bf16>(G, gv);
     } else {
 #pragma unroll
@@ -1251,8 +1259,24 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
   EpiOut eo;
   epi_init(ep, eo, batch, (int64_t)tn * BIG + c, N);
   // 4 passes of 64 rows through LDS (64 x 260 fp32 = 66.5 KiB), full-row stores
+  // gradient-mask build: a pass's 4 mask row pieces are requested before its LDS staging,
+  // one memory latency per pass instead of one per row piece
+  const bool use_gm = (EX & 4) && ep.gmask && eo.cvec;
+  uint4 gpre[4];
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
+    if constexpr ((EX & 4) != 0) {
+      if (use_gm) {
+#pragma unroll
+        for (int sp = 0; sp < 4; ++sp) {
+          const int64_t m = (int64_t)tm * BIG + pass * 64 + sp * 16 + (tid >> 5);
+          const int64_t n = (int64_t)tn * BIG + c;
+          gpre[sp] = (m < Mb && n + 7 < N)
+                         ? *reinterpret_cast<const uint4*>((const bf16*)ep.gmask + la.out_row(m) * ep.ldc + n)
+                         : make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
     if (wr == (pass >> 1)) {
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
@@ -1277,7 +1301,10 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
 #pragma unroll
         for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
       }
-      epi_row8<true, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
+      if constexpr ((EX & 4) != 0)
+        epi_row8<true, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq, false, uint4{}, use_gm, gpre[sp]);
+      else
+        epi_row8<true, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq);
     }
     __syncthreads();
   }

@@ -423,3 +423,23 @@ def test_gemm_relu_mask_epilogue(M, N, K, tb, tile):
     auto = KG.matmul_relu_mask(g, w, False, tb, y, 1.0 / keep)
     assert _rel(auto, ref) < _tol(auto)
 
+
+@pytest.mark.parametrize('tile', G.TILES)
+@pytest.mark.parametrize('M,N,K,ta,tb', [(4096, 2, 2048, False, False), (4096, 2, 2048, False, True),
+                                         (2048, 2, 4096, True, False), (4096, 8, 2048, False, True)])
+def test_every_tile_declines_or_matches_narrow_outputs(M, N, K, ta, tb, tile):
+    """Narrow outputs (the MoE gate: N = 2 experts): each tile either declines the shape
+    (None) or computes it exactly -- the autotuner times every candidate that answers."""
+    torch.manual_seed(3)
+    a = torch.randn(K, M, device=DEV).bfloat16().t() if ta else torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16().t() if tb else torch.randn(K, N, device=DEV).bfloat16()
+    y = G.gemm(a, b, tile=tile)
+    if y is None:
+        return
+    ref = a.float() @ b.float()
+    assert _rel(y, ref) < _tol(y)
+    out = torch.full((M, N), 7.0, device=DEV)
+    r = G.gemm(a, b, out=out, tile=tile)
+    if r is not None:
+        assert _rel(out, ref) < 2e-5
+

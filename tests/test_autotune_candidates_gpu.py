@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 def checked_choose(monkeypatch):
     from hetu_61a7_amd.kernels import autotune
     orig = autotune.choose
+    monkeypatch.setattr(autotune, '_decisions', {})   # every shape is chosen afresh in this test
     bad, seen = [], set()
 
     def wrapped(key, candidates, mode='auto'):

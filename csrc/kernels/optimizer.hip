@@ -18,6 +18,7 @@
 //   LAMB      u = mhat/(sqrt(vhat)+eps) ; p -= lr*(|p|/|u|)*(u + wd*p)   (per tensor)
 // with g = gscale*grad + l2reg*p  (AddL2Regularization folded in).
 #include "common.h"
+#include <stdlib.h>
 
 namespace hetu {
 
@@ -31,6 +32,103 @@ struct OptArgs {
 
 enum { OPT_SGD = 0, OPT_MOMENTUM = 1, OPT_NESTEROV = 2, OPT_ADAGRAD = 3, OPT_ADAM = 4,
        OPT_ADAMW = 5, OPT_LAMB = 6 };
+
+// the update rule on 4 consecutive elements (cnt <= 4 valid)
+template <int MODE>
+__device__ __forceinline__ void opt_rule4(float (&pv)[4], float (&gv)[4], float (&x1)[4], float (&x2)[4], int cnt,
+                                          const OptArgs& a, float lr, float b1t, float b2t, float gsc) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k >= cnt) break;
+    float gr = gv[k] * gsc + a.l2 * pv[k];
+    if (MODE == OPT_SGD) {
+      pv[k] -= lr * gr;
+    } else if (MODE == OPT_MOMENTUM) {
+      x1[k] = a.mu * x1[k] - lr * gr;
+      pv[k] += x1[k];
+    } else if (MODE == OPT_NESTEROV) {
+      float t = lr * gr;
+      x1[k] = a.mu * (x1[k] - t);
+      pv[k] += x1[k] - t;
+    } else if (MODE == OPT_ADAGRAD) {
+      x1[k] += gr * gr;
+      pv[k] -= lr * gr / (sqrtf(x1[k]) + a.eps);
+    } else {
+      x1[k] = a.beta1 * x1[k] + (1.f - a.beta1) * gr;
+      x2[k] = a.beta2 * x2[k] + (1.f - a.beta2) * gr * gr;
+      float mh = x1[k] / (1.f - b1t), vh = x2[k] / (1.f - b2t);
+      float u = mh / (sqrtf(vh) + a.eps);
+      if (MODE == OPT_ADAM) pv[k] -= lr * u;
+      else if (MODE == OPT_ADAMW) pv[k] -= lr * (u + a.wd * pv[k]);
+      else gv[k] = u;  // LAMB phase 1: update kept in the grad buffer
+    }
+  }
+}
+
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned nt_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void ld4_nt(const float* p, float (&v)[4]) {
+  const nt_f4 t = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
+  v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+}
+__device__ __forceinline__ void st4_nt(float* p, const float (&v)[4]) {
+  const nt_f4 t = {v[0], v[1], v[2], v[3]};
+  __builtin_nontemporal_store(t, reinterpret_cast<nt_f4*>(p));
+}
+__device__ __forceinline__ void st_bf16x4_nt(unsigned short* p, const float (&v)[4]) {
+  const nt_u2 w = {(unsigned)f_to_bf16_bits(v[0]) | ((unsigned)f_to_bf16_bits(v[1]) << 16),
+                   (unsigned)f_to_bf16_bits(v[2]) | ((unsigned)f_to_bf16_bits(v[3]) << 16)};
+  __builtin_nontemporal_store(w, reinterpret_cast<nt_u2*>(p));
+}
+
+// Aligned form (n % 4 == 0, 16-byte aligned buffers): two float4 groups per thread and
+// iteration with all their loads issued before the math, non-temporal loads and stores
+// (every byte is touched once per step: no reuse to keep in L2 / MALL).
+template <int MODE, bool SHADOW>
+__global__ void __launch_bounds__(256) opt_flat2_k(float* __restrict__ p, float* __restrict__ g,
+                                                    float* __restrict__ s1, float* __restrict__ s2,
+                                                    unsigned short* __restrict__ shadow, int64_t n, OptArgs a) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float lr = a.lr, b1t = a.beta1t, b2t = a.beta2t, gsc = a.gscale;
+  if (a.dyn) { lr = a.dyn[0]; b1t = a.dyn[1]; b2t = a.dyn[2]; gsc = a.dyn[3]; }
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    float pv[2][4], gv[2][4], x1[2][4], x2[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t b = (i + u * stride) * 4;
+      ld4_nt(p + b, pv[u]);
+      ld4_nt(g + b, gv[u]);
+      if (MODE != OPT_SGD) ld4_nt(s1 + b, x1[u]);
+      if (MODE >= OPT_ADAM) ld4_nt(s2 + b, x2[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t b = (i + u * stride) * 4;
+      opt_rule4<MODE>(pv[u], gv[u], x1[u], x2[u], 4, a, lr, b1t, b2t, gsc);
+      if (MODE != OPT_LAMB) st4_nt(p + b, pv[u]);
+      else st4_nt(g + b, gv[u]);
+      if (MODE != OPT_SGD) st4_nt(s1 + b, x1[u]);
+      if (MODE >= OPT_ADAM) st4_nt(s2 + b, x2[u]);
+      if (SHADOW && MODE != OPT_LAMB) st_bf16x4_nt(shadow + b, pv[u]);
+    }
+  }
+  for (; i < n4; i += stride) {
+    const int64_t b = i * 4;
+    float pv[4], gv[4], x1[4], x2[4];
+    ld4_nt(p + b, pv);
+    ld4_nt(g + b, gv);
+    if (MODE != OPT_SGD) ld4_nt(s1 + b, x1);
+    if (MODE >= OPT_ADAM) ld4_nt(s2 + b, x2);
+    opt_rule4<MODE>(pv, gv, x1, x2, 4, a, lr, b1t, b2t, gsc);
+    if (MODE != OPT_LAMB) st4_nt(p + b, pv);
+    else st4_nt(g + b, gv);
+    if (MODE != OPT_SGD) st4_nt(s1 + b, x1);
+    if (MODE >= OPT_ADAM) st4_nt(s2 + b, x2);
+    if (SHADOW && MODE != OPT_LAMB) st_bf16x4_nt(shadow + b, pv);
+  }
+}
 
 template <int MODE, bool SHADOW>
 __global__ void __launch_bounds__(256) opt_flat_k(float* __restrict__ p, float* __restrict__ g,
@@ -187,6 +285,17 @@ using namespace hetu;
 template <int MODE>
 static void launch_opt(float* p, float* g, float* s1, float* s2, unsigned short* sh, int64_t n,
                        const OptArgs& a, hipStream_t st) {
+  static const bool v2 = [] {
+    const char* e = getenv("HETU_OPT_V2");
+    return e == nullptr || e[0] != '0';
+  }();
+  const uintptr_t al = (uintptr_t)p | (uintptr_t)g | (uintptr_t)s1 | (uintptr_t)s2 | (uintptr_t)sh;
+  if (v2 && (n & 3) == 0 && (al & 15) == 0 && (!sh || ((uintptr_t)sh & 7) == 0)) {
+    const int grid = stream_grid(n / 4, 256, 4);
+    if (sh) hipLaunchKernelGGL((opt_flat2_k<MODE, true>), dim3(grid), dim3(256), 0, st, p, g, s1, s2, sh, n, a);
+    else hipLaunchKernelGGL((opt_flat2_k<MODE, false>), dim3(grid), dim3(256), 0, st, p, g, s1, s2, sh, n, a);
+    return;
+  }
   int grid = stream_grid((n + 3) / 4, 256, 2);
   if (sh) hipLaunchKernelGGL((opt_flat_k<MODE, true>), dim3(grid), dim3(256), 0, st, p, g, s1, s2, sh, n, a);
   else hipLaunchKernelGGL((opt_flat_k<MODE, false>), dim3(grid), dim3(256), 0, st, p, g, s1, s2, sh, n, a);

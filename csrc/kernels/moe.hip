@@ -247,10 +247,8 @@ __global__ void __launch_bounds__(256) locations_k(const int64_t* __restrict__ i
 // Pass 1 counts each segment's hits; pass 2 starts every segment at the sum of its
 // predecessors' counts and ranks its own hits with the block scan of locations_k (segment 0
 // also sums the expert's gate probabilities, in a fixed order).
-constexpr int kLocCntMax = 1 << 16;
-static __device__ int g_loc_cnt[kLocCntMax];
-
-__global__ void __launch_bounds__(256) loc_count_k(const int64_t* __restrict__ idx, int T, int k, int seg, int S) {
+__global__ void __launch_bounds__(256) loc_count_k(const int64_t* __restrict__ idx, int* __restrict__ cnt, int T,
+                                                   int k, int seg, int S) {
   __shared__ int ws[4];
   const int e = blockIdx.x / S, sg = blockIdx.x - e * S;
   const int total = T * k;
@@ -264,12 +262,13 @@ __global__ void __launch_bounds__(256) loc_count_k(const int64_t* __restrict__ i
   for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = h;
   __syncthreads();
-  if (threadIdx.x == 0) g_loc_cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+  if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
 __global__ void __launch_bounds__(256) loc_scan_k(const int64_t* __restrict__ idx, const float* __restrict__ probs,
                                                   int64_t* __restrict__ loc, int* __restrict__ counts,
-                                                  float* __restrict__ psum, int T, int k, int E, int seg, int S) {
+                                                  float* __restrict__ psum, const int* __restrict__ cnt, int T, int k,
+                                                  int E, int seg, int S) {
   constexpr int PT = 8;
   __shared__ int wsum[4];
   __shared__ float fsum[4];
@@ -279,7 +278,7 @@ __global__ void __launch_bounds__(256) loc_scan_k(const int64_t* __restrict__ id
   const int c0 = sg * seg, c1 = min(total, c0 + seg);
   // this segment's start: the predecessors' hit counts
   int pre = 0;
-  for (int q = threadIdx.x; q < sg; q += 256) pre += g_loc_cnt[e * S + q];
+  for (int q = threadIdx.x; q < sg; q += 256) pre += cnt[e * S + q];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
   if (lane == 0) wsum[w] = pre;
@@ -582,24 +581,41 @@ HETU_API int hetu_moe_aux(const int* counts, const float* psum, float* coef, flo
   return (int)hipGetLastError();
 }
 
-HETU_API int hetu_moe_locations(const int64_t* idx, const float* probs, int64_t* loc, int* counts, float* psum,
-                                int T, int k, int E, hipStream_t s) {
-  if (E <= 0) return 0;
-  const int64_t total = (int64_t)T * k;
-  int seg = 2048;
+static void loc_segments(int64_t total, int& seg, int& S) {
+  seg = 2048;
   while ((total + seg - 1) / seg > 1024) seg *= 2;
-  const int S = (int)((total + seg - 1) / seg);
+  S = (int)((total + seg - 1) / seg);
+}
+
+// int32 workspace (per-segment hit counts) hetu_moe_locations2 needs; 0 = single-block scan
+HETU_API int64_t hetu_moe_locations_ws(int T, int k, int E) {
+  int seg, S;
+  loc_segments((int64_t)T * k, seg, S);
+  return S > 1 ? (int64_t)E * S : 0;
+}
+
+// ws: hetu_moe_locations_ws(T, k, E) ints (null, or HETU_MOE_LOC_SEGMENTED=0: one block per
+// expert scans every choice)
+HETU_API int hetu_moe_locations2(const int64_t* idx, const float* probs, int64_t* loc, int* counts, float* psum,
+                                 int T, int k, int E, int* ws, hipStream_t s) {
+  if (E <= 0) return 0;
+  int seg, S;
+  loc_segments((int64_t)T * k, seg, S);
   const char* env = getenv("HETU_MOE_LOC_SEGMENTED");
-  const bool segmented = (env == nullptr || env[0] != '0') && S > 1 && (int64_t)E * S <= kLocCntMax &&
-                         total <= (int64_t)seg * S;
+  const bool segmented = ws != nullptr && (env == nullptr || env[0] != '0') && S > 1;
   if (!segmented) {
     locations_k<<<E, 256, 0, s>>>(idx, probs, loc, counts, psum, T, k, E);
   } else {
-    loc_count_k<<<E * S, 256, 0, s>>>(idx, T, k, seg, S);
-    loc_scan_k<<<E * S, 256, 0, s>>>(idx, probs, loc, counts, psum, T, k, E, seg, S);
+    loc_count_k<<<E * S, 256, 0, s>>>(idx, ws, T, k, seg, S);
+    loc_scan_k<<<E * S, 256, 0, s>>>(idx, probs, loc, counts, psum, ws, T, k, E, seg, S);
   }
   HETU_LAUNCH_CHECK();
   return 0;
+}
+
+HETU_API int hetu_moe_locations(const int64_t* idx, const float* probs, int64_t* loc, int* counts, float* psum,
+                                int T, int k, int E, hipStream_t s) {
+  return hetu_moe_locations2(idx, probs, loc, counts, psum, T, k, E, nullptr, s);
 }
 
 HETU_API int hetu_moe_gate_backward(const float* probs, const int64_t* idx, const float* dgate,

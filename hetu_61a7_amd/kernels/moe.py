@@ -73,10 +73,13 @@ def locations(idx, num_experts, probs=None, inactive=False):
             fill_(loc, -1)
         counts = _NA.empty((E,), dtype=torch.int32, device=idx.device)
         psum = _NA.empty((E,), dtype=torch.float32, device=idx.device) if probs is not None else None
-        f = fn('hetu_moe_locations', [P, P, P, P, P, I32, I32, I32, P])
+        # per-segment hit counts of the segmented scan (an int32 workspace from the pool)
+        nws = int(fn('hetu_moe_locations_ws', [I32, I32, I32], I64)(T, k, E))
+        ws = _NA.empty((nws,), dtype=torch.int32, device=idx.device) if nws > 0 else None
+        f = fn('hetu_moe_locations2', [P, P, P, P, P, I32, I32, I32, P, P])
         check(f(idx.data_ptr(), probs.contiguous().data_ptr() if probs is not None else None, loc.data_ptr(),
-                counts.data_ptr(), psum.data_ptr() if psum is not None else None, T, k, E, stream_ptr()),
-              'moe_locations')
+                counts.data_ptr(), psum.data_ptr() if psum is not None else None, T, k, E,
+                ws.data_ptr() if ws is not None else None, stream_ptr()), 'moe_locations')
         return loc, counts, psum
     il = idx.long()
     on = (il >= 0).t().reshape(-1)

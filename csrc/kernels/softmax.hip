@@ -196,12 +196,21 @@ __global__ void __launch_bounds__(256) sce_sparse_fwd_k(const T* __restrict__ x,
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
   const T* xr = x + row * N;
+  const int64_t c = lab[row];
+  if (c == ignored || c < 0 || c >= N) {
+    // an ignored row's loss is 0 and its gradient 0 whatever its logits are (the BERT MLM
+    // head ignores ~85 % of its rows): the row is not read; its lse is not computed (0)
+    if (lane == 0) {
+      loss[row] = 0.f;
+      if (lse_out) lse_out[row] = 0.f;
+    }
+    return;
+  }
   float m, s;
   row_max_sum_vec(xr, N, lane, m, s);
   const float lse = m + __logf(s);
   if (lane == 0) {
-    const int64_t c = lab[row];
-    loss[row] = (c == ignored || c < 0 || c >= N) ? 0.f : lse - ld(xr, c);
+    loss[row] = lse - ld(xr, c);
     if (lse_out) lse_out[row] = lse;
   }
 }
@@ -219,6 +228,19 @@ __global__ void __launch_bounds__(256) sce_sparse_bwd_k(const T* __restrict__ x,
   const T* xr = x + row * N;
   const int64_t c = lab[row];
   const bool ign = (c == ignored || c < 0 || c >= N);
+  T* dr = dx + row * N;
+  if (ign) {   // zero gradient: the row's logits (and its lse) are not read
+    constexpr int V = Vec<T>::N;
+    const int h = row_head(dr, N);
+    if (lane < h) dr[lane] = from_f<T>(0.f);
+    const int nv = (N - h) / V;
+    float z[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) z[k] = 0.f;
+    for (int j = lane; j < nv; j += 64) store_vec<T>(dr + h + (int64_t)j * V, z);
+    for (int t = h + nv * V + lane; t < N; t += 64) dr[t] = from_f<T>(0.f);
+    return;
+  }
   float lse;
   if (lse_in) {
     lse = lse_in[row];
@@ -227,8 +249,7 @@ __global__ void __launch_bounds__(256) sce_sparse_bwd_k(const T* __restrict__ x,
     row_max_sum_vec(xr, N, lane, m, s);
     lse = m + __logf(s);
   }
-  const float gr = ign ? 0.f : (g_scalar ? g[0] : g[row]);
-  T* dr = dx + row * N;
+  const float gr = g_scalar ? g[0] : g[row];
   constexpr int V = Vec<T>::N;
   // x and dx share the row pitch; vector body only when their rows align alike
   const int h = row_head(xr, N);

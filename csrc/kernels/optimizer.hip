@@ -81,7 +81,7 @@ __device__ __forceinline__ void st_bf16x4_nt(unsigned short* p, const float (&v)
   __builtin_nontemporal_store(w, reinterpret_cast<nt_u2*>(p));
 }
 
-// Aligned form (n % 4 == 0, 16-byte aligned buffers): two float4 groups per thread and
+// Aligned form (16-byte aligned buffers; the n % 4 tail by one thread): two float4 groups per thread and
 // iteration with all their loads issued before the math, non-temporal loads and stores
 // (every byte is touched once per step: no reuse to keep in L2 / MALL).
 template <int MODE, bool SHADOW>
@@ -127,6 +127,25 @@ __global__ void __launch_bounds__(256) opt_flat2_k(float* __restrict__ p, float*
     if (MODE != OPT_SGD) st4_nt(s1 + b, x1);
     if (MODE >= OPT_ADAM) st4_nt(s2 + b, x2);
     if (SHADOW && MODE != OPT_LAMB) st_bf16x4_nt(shadow + b, pv);
+  }
+  // the n % 4 tail elements (the flat buffer ends with the last parameter's numel)
+  const int cnt = (int)(n - n4 * 4);
+  if (cnt > 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t b = n4 * 4;
+    float pv[4] = {0.f, 0.f, 0.f, 0.f}, gv[4] = {0.f, 0.f, 0.f, 0.f}, x1[4] = {0.f, 0.f, 0.f, 0.f},
+          x2[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < cnt; ++k) {
+      pv[k] = p[b + k]; gv[k] = g[b + k];
+      if (MODE != OPT_SGD) x1[k] = s1[b + k];
+      if (MODE >= OPT_ADAM) x2[k] = s2[b + k];
+    }
+    opt_rule4<MODE>(pv, gv, x1, x2, cnt, a, lr, b1t, b2t, gsc);
+    for (int k = 0; k < cnt; ++k) {
+      if (MODE != OPT_LAMB) p[b + k] = pv[k]; else g[b + k] = gv[k];
+      if (MODE != OPT_SGD) s1[b + k] = x1[k];
+      if (MODE >= OPT_ADAM) s2[b + k] = x2[k];
+      if (SHADOW && MODE != OPT_LAMB) shadow[b + k] = f_to_bf16_bits(pv[k]);
+    }
   }
 }
 
@@ -290,7 +309,7 @@ static void launch_opt(float* p, float* g, float* s1, float* s2, unsigned short*
     return e == nullptr || e[0] != '0';
   }();
   const uintptr_t al = (uintptr_t)p | (uintptr_t)g | (uintptr_t)s1 | (uintptr_t)s2 | (uintptr_t)sh;
-  if (v2 && (n & 3) == 0 && (al & 15) == 0 && (!sh || ((uintptr_t)sh & 7) == 0)) {
+  if (v2 && n >= 4 && (al & 15) == 0 && (!sh || ((uintptr_t)sh & 7) == 0)) {
     const int grid = stream_grid(n / 4, 256, 4);
     if (sh) hipLaunchKernelGGL((opt_flat2_k<MODE, true>), dim3(grid), dim3(256), 0, st, p, g, s1, s2, sh, n, a);
     else hipLaunchKernelGGL((opt_flat2_k<MODE, false>), dim3(grid), dim3(256), 0, st, p, g, s1, s2, sh, n, a);

@@ -229,27 +229,21 @@ __global__ void __launch_bounds__(256) sce_sparse_bwd_k(const T* __restrict__ x,
   const int64_t c = lab[row];
   const bool ign = (c == ignored || c < 0 || c >= N);
   T* dr = dx + row * N;
-  if (ign) {   // zero gradient: the row's logits (and its lse) are not read
-    constexpr int V = Vec<T>::N;
-    const int h = row_head(dr, N);
-    if (lane < h) dr[lane] = from_f<T>(0.f);
-    const int nv = (N - h) / V;
-    float z[V];
-#pragma unroll
-    for (int k = 0; k < V; ++k) z[k] = 0.f;
-    for (int j = lane; j < nv; j += 64) store_vec<T>(dr + h + (int64_t)j * V, z);
-    for (int t = h + nv * V + lane; t < N; t += 64) dr[t] = from_f<T>(0.f);
-    return;
-  }
+  // (an ignored row is written as g = 0 times the softmax below, not by a zero-fill path
+  // that skips the logits: the write-only rows measured slower, 216 vs 188 us per BERT step)
   float lse;
-  if (lse_in) {
+  if (ign) {
+    // the forward does not compute an ignored row's lse: +inf makes every exp(x - lse) 0,
+    // so the row is exactly 0 * (0 - 0) (a finite stand-in could overflow exp into 0 * inf)
+    lse = __builtin_inff();
+  } else if (lse_in) {
     lse = lse_in[row];
   } else {
     float m, s;
     row_max_sum_vec(xr, N, lane, m, s);
     lse = m + __logf(s);
   }
-  const float gr = g_scalar ? g[0] : g[row];
+  const float gr = ign ? 0.f : (g_scalar ? g[0] : g[row]);
   constexpr int V = Vec<T>::N;
   // x and dx share the row pitch; vector body only when their rows align alike
   const int h = row_head(xr, N);

@@ -150,7 +150,7 @@ def test_sparse_softmax_ce_unaligned_rows(dt, N):
         torch.testing.assert_close(dx.float(), refd, **_tol(dt))
 
 
-@pytest.mark.parametrize('n', [100003, 100000])   # 100000: the aligned, unrolled non-temporal kernel
+@pytest.mark.parametrize('n', [100003, 100000])   # the unrolled non-temporal kernel, with and without a tail
 @pytest.mark.parametrize('mode', ['sgd', 'momentum', 'nesterov', 'adagrad', 'adam', 'adamw', 'lamb'])
 def test_flat_optimizer(mode, n):
     p = torch.randn(n, device=DEV)

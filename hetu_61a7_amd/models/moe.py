@@ -89,9 +89,26 @@ def moe_top_bench(args, world, rank, local):
         from ..ops.moe_dts import DTSGatingOp
         g = [n for n in ex.subexecutor['train'].topo_order if isinstance(n, DTSGatingOp)][0]
 
+        def step():
+            if g.calls == 0 and g.budget > g.k_min:
+                # The budget only shrinks (dense to sparse), and each budget has its own expert
+                # capacity, i.e. its own GEMM shapes.  Run one (untimed, first warmup) step at
+                # every smaller budget first so that a budget change inside the timed window
+                # does not autotune the new shapes there; the histograms of these forced calls
+                # are dropped -- they must not steer the real budget.
+                keep = g.budget
+                for b in range(g.k_min, keep):
+                    g.budget = b
+                    ex.run('train', feed_dict=feed)
+                g.budget = keep
+                g._pending, g._tau_at, g.history = [], {}, []
+                g.pretuned_budgets = list(range(g.k_min, keep))
+            ex.run('train', feed_dict=feed)
+
         def extra():
             h = g.history[-1] if g.history else None
-            return {'dts': {'steps': g.calls, 'tau': round(g.temperature.value, 4), 'budget_k': g.budget,
+            return {'dts': {'steps': g.calls, 'pretuned_budgets': getattr(g, 'pretuned_budgets', []),
+                            'tau': round(g.temperature.value, 4), 'budget_k': g.budget,
                             'active_experts_per_token_last': round(h[3], 3) if h else None,
                             'active_experts_first_to_last': [round(x[3], 3) for x in g.history[::max(1, len(g.history) // 8)]]}}
         step.extra = extra

@@ -10,6 +10,7 @@
 //         (also emits d(residual) = dy' when a residual add was fused).
 // Each streaming kernel moves 16 B per lane (8 bf16 or 4 fp32 channels).
 #include "common.h"
+#include <stdlib.h>
 
 namespace hetu {
 
@@ -288,13 +289,38 @@ __device__ __forceinline__ uint8_t relu_bits(const float (&o)[V]) {
   return (uint8_t)m;
 }
 
+// Non-temporal vector loads (HETU_BN_NT=1): the apply passes read each input byte once
+typedef unsigned bn_u4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ void load_vec_nt(const T* p, float (&v)[Vec<T>::N]);
+template <>
+__device__ __forceinline__ void load_vec_nt<float>(const float* p, float (&v)[4]) {
+  const bn_u4 x = __builtin_nontemporal_load(reinterpret_cast<const bn_u4*>(p));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(x[i]);
+}
+template <>
+__device__ __forceinline__ void load_vec_nt<bf16>(const bf16* p, float (&v)[8]) {
+  const bn_u4 x = __builtin_nontemporal_load(reinterpret_cast<const bn_u4*>(p));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(x[i] << 16);
+    v[2 * i + 1] = __uint_as_float(x[i] & 0xffff0000u);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void ldv(const T* p, float (&v)[Vec<T>::N], int nt) {
+  if (nt) load_vec_nt<T>(p, v);
+  else load_vec<T>(p, v);
+}
+
 // MASK: also store the ReLU keep-bits (1 byte per 16-byte vector, 1/16 of y) so the
 // backward of a fused add+ReLU reads them instead of re-reading y
 template <typename T, bool RELU, bool RES, bool MASK = false>
 __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T* __restrict__ res,
                                                  const float* __restrict__ fa,
                                                  const float* __restrict__ fb, T* __restrict__ y,
-                                                 int64_t nvec, int C, uint8_t* __restrict__ mask) {
+                                                 int64_t nvec, int C, uint8_t* __restrict__ mask, int nt = 0) {
   // channel-stationary threads: the grid stride is a multiple of C/V, so every
   // thread keeps one channel group's folded affine in registers (no per-element
   // parameter loads, no 64-bit modulo) and streams U vectors per iteration
@@ -314,10 +340,10 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
   for (; i + (U - 1) * stride < nvec; i += U * stride) {
     float v[U][V], r[U][V];
 #pragma unroll
-    for (int u = 0; u < U; ++u) load_vec<T>(x + (i + u * stride) * V, v[u]);
+    for (int u = 0; u < U; ++u) ldv<T>(x + (i + u * stride) * V, v[u], nt);
     if (RES) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) load_vec<T>(res + (i + u * stride) * V, r[u]);
+      for (int u = 0; u < U; ++u) ldv<T>(res + (i + u * stride) * V, r[u], nt);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -334,8 +360,8 @@ __global__ void __launch_bounds__(256) bn_apply(const T* __restrict__ x, const T
   }
   for (; i < nvec; i += stride) {
     float v[V], r[V];
-    load_vec<T>(x + i * V, v);
-    if (RES) load_vec<T>(res + i * V, r);
+    ldv<T>(x + i * V, v, nt);
+    if (RES) ldv<T>(res + i * V, r, nt);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       float o = v[k] * a[k] + bb[k];
@@ -552,7 +578,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
                                                      const float* __restrict__ fmean,
                                                      const float* __restrict__ finvstd,
                                                      T* __restrict__ dx, T* __restrict__ dres,
-                                                     int64_t nvec, int C, BnSums bs = BnSums{}) {
+                                                     int64_t nvec, int C, BnSums bs = BnSums{}, int nt = 0) {
   // channel-stationary threads (see bn_apply): per-channel coefficients live in
   // registers for the whole grid-stride loop
   constexpr int V = Vec<T>::N;
@@ -597,13 +623,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
   for (; i + stride < nvec; i += 2 * stride) {   // two vectors in flight
     const int64_t j = i + stride;
     float g[V], xv[V], g2[V], xv2[V], yv[V], yv2[V];
-    load_vec<T>(dy + i * V, g);
-    load_vec<T>(x + i * V, xv);
-    load_vec<T>(dy + j * V, g2);
-    load_vec<T>(x + j * V, xv2);
+    ldv<T>(dy + i * V, g, nt);
+    ldv<T>(x + i * V, xv, nt);
+    ldv<T>(dy + j * V, g2, nt);
+    ldv<T>(x + j * V, xv2, nt);
     if (RELU == 1) {
-      load_vec<T>(y + i * V, yv);
-      load_vec<T>(y + j * V, yv2);
+      ldv<T>(y + i * V, yv, nt);
+      ldv<T>(y + j * V, yv2, nt);
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         g[k] = yv[k] > 0.f ? g[k] : 0.f;
@@ -638,11 +664,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
   }
   for (; i < nvec; i += stride) {
     float g[V], xv[V];
-    load_vec<T>(dy + i * V, g);
-    load_vec<T>(x + i * V, xv);
+    ldv<T>(dy + i * V, g, nt);
+    ldv<T>(x + i * V, xv, nt);
     if (RELU == 1) {
       float yv[V];
-      load_vec<T>(y + i * V, yv);
+      ldv<T>(y + i * V, yv, nt);
 #pragma unroll
       for (int k = 0; k < V; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
     } else if (RELU == 2) {
@@ -664,6 +690,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply(const T* __restrict__ dy, co
 }  // namespace hetu
 
 using namespace hetu;
+
+// HETU_BN_NT=1: non-temporal input loads in the BatchNorm apply passes (A/B switch)
+static int bn_nt() {
+  static const int v = [] {
+    const char* e = getenv("HETU_BN_NT");
+    return e != nullptr && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
 
 HETU_API void hetu_bn_tune(int chunk_target, int apply_blocks, int min_passes) {
   if (chunk_target > 0) g_bn_chunk_target = chunk_target;
@@ -708,17 +743,17 @@ static int bn_fwd_impl(const void* x, const void* res, void* y, int64_t M, int C
   const T* rr = (const T*)res;
   T* yr = (T*)y;
   if (relu && res && mask)
-    hipLaunchKernelGGL((bn_apply<T, true, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+    hipLaunchKernelGGL((bn_apply<T, true, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask, bn_nt());
   else if (relu && res)
-    hipLaunchKernelGGL((bn_apply<T, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+    hipLaunchKernelGGL((bn_apply<T, true, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask, bn_nt());
   else if (relu && mask)
-    hipLaunchKernelGGL((bn_apply<T, true, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+    hipLaunchKernelGGL((bn_apply<T, true, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask, bn_nt());
   else if (relu)
-    hipLaunchKernelGGL((bn_apply<T, true, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+    hipLaunchKernelGGL((bn_apply<T, true, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask, bn_nt());
   else if (res)
-    hipLaunchKernelGGL((bn_apply<T, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+    hipLaunchKernelGGL((bn_apply<T, false, true>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask, bn_nt());
   else
-    hipLaunchKernelGGL((bn_apply<T, false, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask);
+    hipLaunchKernelGGL((bn_apply<T, false, false>), dim3(grid), dim3(256), 0, st, xr, rr, fa, fb, yr, nvec, C, mask, bn_nt());
   HETU_LAUNCH_CHECK();
   return 0;
 }
@@ -768,10 +803,10 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const uint8_
     BnSums bs{bsums, bnext, dscale, dbias, scale, M};
     if (dres)
       hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true, true>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB, cC,
-                         scale, bias, mean, invstd, dx, dres, nvec, C, bs);
+                         scale, bias, mean, invstd, dx, dres, nvec, C, bs, bn_nt());
     else
       hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false, true>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB,
-                         cC, scale, bias, mean, invstd, dx, dres, nvec, C, bs);
+                         cC, scale, bias, mean, invstd, dx, dres, nvec, C, bs, bn_nt());
     return;
   }
   if (bsums) {
@@ -787,10 +822,10 @@ static void bn_bwd_launch(const BnGeom& g, const T* dy, const T* y, const uint8_
   const int grid = bn_apply_grid(nvec, C, V);
   if (dres)
     hipLaunchKernelGGL((bn_bwd_apply<T, RELU, true>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB, cC, scale,
-                       bias, mean, invstd, dx, dres, nvec, C);
+                       bias, mean, invstd, dx, dres, nvec, C, BnSums{}, bn_nt());
   else
     hipLaunchKernelGGL((bn_bwd_apply<T, RELU, false>), dim3(grid), dim3(256), 0, st, dy, y, mask, x, cA, cB, cC, scale,
-                       bias, mean, invstd, dx, dres, nvec, C);
+                       bias, mean, invstd, dx, dres, nvec, C, BnSums{}, bn_nt());
 }
 
 template <typename T>

@@ -304,7 +304,7 @@ HETU_RT_API int hetu_array_copy(void* dst, void* src, void* stream) {
 static void dl_deleter(DLManagedTensor* self) { array_release((Array*)self->manager_ctx); }
 
 // A DLManagedTensor over `a` (a new reference, dropped by the consumer's deleter call).
-// Device arrays export as kDLROCM, pinned host as kDLROCMHost, host as kDLCPU.
+// Device arrays export as kDLROCM, host arrays (pinned or not) as kDLCPU.
 HETU_RT_API void* hetu_array_to_dlpack(void* a) {
   Array* src = (Array*)a;
   // every export gets its own header (the DLManagedTensor lives inside it)
@@ -313,7 +313,9 @@ HETU_RT_API void* hetu_array_to_dlpack(void* a) {
                         src->shape, src->strides);
   DLManagedTensor* m = &x->dl;
   m->dl_tensor.data = (char*)x->alloc->ptr + x->offset;
-  m->dl_tensor.device.device_type = x->device_type == 2 ? kDLROCM : (x->alloc->mem == kPinned ? kDLCPU : kDLCPU);
+  // Pinned host memory exports as kDLCPU: it is host-addressable, and torch's DLPack importer
+  // rejects kDLROCMHost.  The allocation record keeps the placement (freed to the pinned pool).
+  m->dl_tensor.device.device_type = x->device_type == 2 ? kDLROCM : kDLCPU;
   m->dl_tensor.device.device_id = x->device_type == 2 ? x->device_id : 0;
   m->dl_tensor.ndim = x->ndim;
   m->dl_tensor.dtype = to_dl(x->dtype);
@@ -335,13 +337,22 @@ HETU_RT_API int hetu_array_from_dlpack(void* managed, int dtype, void** out) {
   a->mem = kBorrowed;
   a->borrowed = m;
   a->ptr = (char*)t.data + t.byte_offset;
+  // DLPack allows strides == NULL for compact row-major tensors: derive those strides
+  int64_t rm[kMaxDim];
+  int64_t acc = 1;
+  for (int d = t.ndim - 1; d >= 0; --d) { rm[d] = acc; acc *= t.shape[d]; }
+  const int64_t* st = t.strides ? t.strides : rm;
   int64_t span = 1;
-  for (int d = 0; d < t.ndim; ++d)
-    if (t.shape[d] > 0) span += (t.shape[d] - 1) * (t.strides ? t.strides[d] : 1);
+  bool empty = false;
+  for (int d = 0; d < t.ndim; ++d) {
+    if (t.shape[d] == 0) empty = true;
+    else span += (t.shape[d] - 1) * st[d];
+  }
+  if (empty) span = 0;
   a->bytes = span * dtype_size(dtype);
   g_live_allocs.fetch_add(1);
   const int dev_type = (t.device.device_type == kDLROCM || t.device.device_type == 2) ? 2 : 1;
-  *out = new_header(a, 0, dtype, dev_type, t.device.device_id, t.ndim, t.shape, t.strides);
+  *out = new_header(a, 0, dtype, dev_type, t.device.device_id, t.ndim, t.shape, st);
   return 0;
 }
 

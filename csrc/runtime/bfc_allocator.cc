@@ -620,7 +620,7 @@ HETU_RT_API void hetu_torch_pool_release(int64_t id) {
       a.compare_exchange_strong(cur, nullptr);
     }
     if (p->stats().bytes_in_use > 0) {
-      g_retiring.insert(p);   // still owns chunks: found by owner_of until its last free
+      g_retiring.insert(p);   // still owns chunks: found by hetu_torch_free until its last free
       return;
     }
     g_pools.erase(it);
@@ -628,15 +628,6 @@ HETU_RT_API void hetu_torch_pool_release(int64_t id) {
   }
   hipDeviceSynchronize();
   delete p;
-}
-
-static BFCAllocator* owner_of(int device, void* ptr) {
-  BFCAllocator* a = dev_alloc(device);
-  if (a && a->allocation_size(ptr)) return a;
-  std::lock_guard<std::mutex> g(g_dev_mu);
-  for (auto& kv : g_pools)
-    if (kv.second->allocation_size(ptr)) return kv.second;
-  return nullptr;
 }
 
 HETU_RT_API void* hetu_torch_alloc(ssize_t size, int device, hipStream_t stream) {
@@ -658,31 +649,45 @@ HETU_RT_API void* hetu_torch_alloc(ssize_t size, int device, hipStream_t stream)
 
 HETU_RT_API void hetu_torch_free(void* ptr, ssize_t size, int device, hipStream_t stream) {
   (void)size;
-  BFCAllocator* a = g_npools.load() == 0 ? dev_alloc(device) : owner_of(device, ptr);
-  if (!a) return;
-  a->deallocate(ptr, stream);
-  if (g_npools.load() != 0) {
-    BFCAllocator* dead = nullptr;
-    {
-      std::lock_guard<std::mutex> g(g_dev_mu);
-      if (g_retiring.count(a) && a->stats().bytes_in_use == 0) {
-        g_retiring.erase(a);
-        for (auto it = g_pools.begin(); it != g_pools.end(); ++it)
-          if (it->second == a) { g_pools.erase(it); break; }
-        g_npools.fetch_sub(1);
-        dead = a;
-      }
+  BFCAllocator* d = dev_alloc(device);
+  if (g_npools.load() == 0 || (d && d->allocation_size(ptr))) {
+    if (d) d->deallocate(ptr, stream);
+    return;
+  }
+  // A capture-pool chunk: the owner lookup, the free and the retire check run under one
+  // lock, so a concurrent free of another chunk of a retiring pool can never reach a pool
+  // that this free is about to delete.
+  BFCAllocator* dead = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    BFCAllocator* a = nullptr;
+    auto owner = g_pools.end();
+    for (auto it = g_pools.begin(); it != g_pools.end(); ++it)
+      if (it->second->allocation_size(ptr)) { a = it->second; owner = it; break; }
+    if (!a) return;
+    a->deallocate(ptr, stream);
+    if (g_retiring.count(a) && a->stats().bytes_in_use == 0) {
+      g_retiring.erase(a);
+      g_pools.erase(owner);
+      g_npools.fetch_sub(1);
+      dead = a;
     }
-    if (dead) {
-      hipDeviceSynchronize();
-      delete dead;
-    }
+  }
+  if (dead) {
+    hipDeviceSynchronize();
+    delete dead;
   }
 }
 
 HETU_RT_API void hetu_torch_record_stream(int device, void* ptr, hipStream_t stream) {
-  BFCAllocator* a = g_npools.load() == 0 ? dev_alloc(device) : owner_of(device, ptr);
-  if (a) a->record_stream(ptr, stream);
+  BFCAllocator* d = dev_alloc(device);
+  if (g_npools.load() == 0 || (d && d->allocation_size(ptr))) {
+    if (d) d->record_stream(ptr, stream);
+    return;
+  }
+  std::lock_guard<std::mutex> g(g_dev_mu);   // pool chunks: see hetu_torch_free
+  for (auto& kv : g_pools)
+    if (kv.second->allocation_size(ptr)) { kv.second->record_stream(ptr, stream); return; }
 }
 
 // a framework stream is being destroyed: the device allocator and every capture pool

@@ -21,6 +21,7 @@ MI355X execution model:
 from __future__ import annotations
 
 import os
+import sys
 import pickle
 import time
 from typing import Dict, List, Optional
@@ -547,6 +548,8 @@ class SubExecutor(object):
         cfg = self.config
         for n in self.mode_nodes:
             n.inference = self.inference
+        if not self.opt_ops:
+            _ps_drain_dense()
         if cfg.use_hipgraph and cfg.device.type == 'cuda' and not self.step_end_nodes:
             # (ops with per-step host schedules -- the DTS gate's temperature and budget --
             # change launch arguments and shapes between steps: not replayable, run eager)
@@ -679,6 +682,12 @@ _CHECK_LAYOUT = os.environ.get('HETU_CHECK_LAYOUT', '0') == '1'
 # (scripts/find_torch_kernels.py attributes device kernels to graph ops through it)
 _PROFILE_OPS = os.environ.get('HETU_PROFILE_OPS', '0') == '1'
 _LAYOUT_MISSES = {}
+
+
+def _ps_drain_dense():
+    t = sys.modules.get('hetu_61a7_amd.ps.table')
+    if t is not None and t._LIVE:
+        t.drain_dense()
 
 
 def layout_report():

@@ -467,6 +467,11 @@ class OptimizerOp(Op):
             b.pending = b.total
 
     def _reduce_bucket(self, b, async_op=True):
+        from .parallel.watchdog import labelled
+        with labelled('grad bucket [%d:%d] of %d' % (b.start, b.end, self.flat.padded)):
+            return self._reduce_bucket_inner(b, async_op)
+
+    def _reduce_bucket_inner(self, b, async_op):
         if self.trace:
             self._trace_launch(b)
         if not self.zero:

@@ -49,11 +49,14 @@ def backend_for_device(dev_is_gpu: bool) -> str:
 def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] = None) -> 'Communicator':
     """Initialise the global communicator (idempotent).
 
-    Failure detection (SURVEY §5.3 "RCCL watchdog"): collectives time out after
-    ``timeout_s`` (env ``HETU_COMM_TIMEOUT``, default 1800 s) and RCCL async
-    errors are handled by the process-group watchdog, which aborts the
-    communicator and raises in this process -- the launcher then restarts the
-    job, which resumes from the last checkpoint (``utils.checkpoint``)."""
+    Failure detection (SURVEY §5.3 "RCCL watchdog"): every GPU collective goes through
+    the in-house communicator, whose completion events and ``ncclCommGetAsyncError``
+    state the process's watchdog thread (``parallel/watchdog.py``) polls.  A collective
+    older than ``timeout_s`` (env ``HETU_COMM_TIMEOUT``, default 1800 s) or an async
+    error aborts every communicator and exits the process non-zero -- the launcher
+    (``heturun --max-restarts``) then restarts the group, which resumes from the last
+    checkpoint (``utils.checkpoint``).  The gloo bootstrap / host-tensor group keeps
+    torch's own ``timeout``."""
     global _WORLD
     if timeout_s is None:
         timeout_s = int(os.environ.get('HETU_COMM_TIMEOUT', '1800'))
@@ -204,30 +207,44 @@ class Communicator(object):
         # every rank parked in work.wait() of the first step's buckets)
         return t.is_cuda and self.group_backend == 'gloo'
 
+    def _exchange64(self, payload, device):
+        """all-gather of a <= 64-byte payload per rank (list of bytes, rank order)"""
+        buf = torch.zeros(64, dtype=torch.uint8)
+        buf[:len(payload)] = torch.tensor(list(payload), dtype=torch.uint8)
+        buf = buf.to(device)
+        out = torch.empty(64 * self.nrank, dtype=torch.uint8, device=device)
+        self.all_gather(out, buf)
+        host = out.cpu().numpy().tobytes()
+        return [host[64 * j:64 * (j + 1)] for j in range(self.nrank)]
+
     def _ipc_ar(self, device):
         """the one-shot IPC all-reduce of this communicator (built on first use: one handle
-        exchange over the communicator itself)"""
+        exchange over the communicator itself), or False when the ranks are not all on
+        this node (``hipIpcOpenMemHandle`` maps same-node peers only)"""
         ar = getattr(self, '_ipc', None)
         if ar is None:
+            import hashlib
+            import socket
+            node = hashlib.sha256(socket.gethostname().encode()).digest()[:32]
+            if any(h[:32] != node for h in self._exchange64(node, device)):
+                self._ipc = False
+                return False
             from .ipc_allreduce import IPCAllReduce
-
-            def exchange(hb):
-                buf = torch.zeros(64, dtype=torch.uint8)
-                buf[:len(hb)] = torch.tensor(list(hb), dtype=torch.uint8)
-                buf = buf.to(device)
-                out = torch.empty(64 * self.nrank, dtype=torch.uint8, device=device)
-                self.all_gather(out, buf)
-                host = out.cpu().numpy().tobytes()
-                return [host[64 * j:64 * (j + 1)] for j in range(self.nrank)]
-            ar = self._ipc = IPCAllReduce(self.rank, self.nrank, exchange, device=device)
+            ar = self._ipc = IPCAllReduce(self.rank, self.nrank, lambda hb: self._exchange64(hb, device),
+                                          device=device)
         return ar
 
     def all_reduce(self, t: torch.Tensor, op: str = 'sum', async_op: bool = False):
         if _IPC_SMALL and self.nrank > 1 and not async_op and op in ('sum', 'max') and t.is_cuda \
-                and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= 4096:
-            # opt-in: small fp32 reductions by the one-shot IPC kernel (no RCCL call)
-            self._ipc_ar(t.device)(t, op, out=t)
-            return None
+                and t.dtype == torch.float32 and t.is_contiguous() and t.numel() <= 4096 \
+                and getattr(self, '_ipc', None) is not False:
+            # opt-in: small fp32 reductions by the one-shot IPC kernel (no RCCL call);
+            # a peer timeout of any earlier call raises here (and in barrier / the watchdog)
+            ar = self._ipc_ar(t.device)
+            if ar:
+                ar.check()
+                ar(t, op, out=t)
+                return None
         if self.native is not None and t.is_cuda and t.is_contiguous():
             return self.native.all_reduce(t, op, async_op=async_op)
         if self._gloo_gpu(t):
@@ -319,12 +336,21 @@ class Communicator(object):
 
     def barrier(self):
         """host barrier: a 1-element all-reduce on the native communicator, then the host
-        waits for it (torch's barrier would create torch's own RCCL communicator)"""
+        waits for it under the watchdog's deadline (torch's barrier would create torch's
+        own RCCL communicator)"""
         if self.native is not None:
             if self._bar is None:
                 self._bar = torch.zeros(1, dtype=torch.float32, device='cuda')
             self.native.all_reduce(self._bar)
-            torch.cuda.current_stream().synchronize()
+            from ..runtime import DeviceEvent
+            from . import watchdog
+            ev = DeviceEvent().record(torch.cuda.current_stream())
+            if watchdog.enabled():
+                watchdog.get().wait(ev, 'barrier', self)
+            else:
+                ev.synchronize()
+            if getattr(self, '_ipc', None):
+                self._ipc.check()
         elif self.use_gpu and dist.get_backend(self.group) == 'nccl':
             dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
         else:
@@ -365,11 +391,15 @@ def stats():
 
 def destroy():
     global _WORLD
+    from . import watchdog
     for c in list(_GROUPS.values()) + ([_WORLD] if _WORLD is not None else []):
         if getattr(c, 'native', None) is not None:
             torch.cuda.synchronize()
             c.native.destroy()
             c.native = None
+        if getattr(c, '_ipc', None):
+            c._ipc.close()
+    watchdog.shutdown()
     _GROUPS.clear()
     _WORLD = None
     if dist.is_initialized():

@@ -12,11 +12,13 @@ RCCL ring's protocol.
 
     ar = IPCAllReduce(rank, nranks, exchange=lambda b: gathered_list_of_bytes, device=dev)
     y = ar(x)                 # fp32, x.numel() <= cap; op 'sum' or 'max'
-    ar.check()                # raises if a call timed out waiting for a peer
+    ar.check()                # raises if a call timed out waiting for a peer (host read)
 
 Opt-in (``HETU_IPC_ALLREDUCE=1`` routes ``Communicator.all_reduce`` of fp32 tensors up to
-``cap`` elements through it); the 2-process same-GPU test is
-``tests/test_ipc_allreduce_gpu.py``.
+``cap`` elements through it, when every rank of the communicator is on this node).  A
+timed-out call is reported by the next routed call, the next ``barrier()`` and the
+watchdog thread (``parallel/watchdog.py``), which exits the process.  The 2-process
+same-GPU tests are ``tests/test_ipc_allreduce_gpu.py``.
 """
 from __future__ import annotations
 
@@ -67,9 +69,15 @@ class IPCAllReduce(object):
                 check(L.hetu_ipcar_open(hb, ctypes.byref(p)), 'ipcar_open(rank %d)' % j)
                 self.ptrs[j] = p.value
                 self.opened.append(p)
-            from ..kernels.tensor import zeros
-            self.err = zeros((1,), torch.int32, self.device)
+            # the error word lives in pinned host memory (device-mapped): check() and the
+            # watchdog read it without a GPU call or a stream sync
+            self.err = _NA.empty((1,), dtype=torch.int32, device='cpu', pinned=True)
+            self.err.zero_()
         self.epoch = 0
+        from . import watchdog
+        if watchdog.enabled():
+            err = self.err
+            watchdog.get().register_flag(self, lambda: int(err[0]))
 
     def __call__(self, x, op='sum', out=None):
         from ..kernels import check, stream_ptr
@@ -87,8 +95,9 @@ class IPCAllReduce(object):
         return out
 
     def check(self):
-        """raise if any call so far timed out waiting for a peer (one host read)"""
-        e = int(self.err.item())
+        """raise if any completed call so far timed out waiting for a peer (one host read
+        of the mapped error word; calls still in flight are seen by a later check)"""
+        e = int(self.err[0])
         if e:
             raise RuntimeError('IPCAllReduce: call %d timed out waiting for a peer' % e)
 

@@ -133,6 +133,10 @@ class NativeComm(object):
         self._dstream = DeviceStream(priority=-1, persistent=True)
         self.stream = self._dstream.torch
         self._bf16_ws = {}
+        from . import watchdog
+        self._wd = watchdog.get() if watchdog.enabled() else None
+        if self._wd is not None:
+            self._wd.register(self)
 
     # ---- construction -----------------------------------------------------------
     @classmethod
@@ -178,15 +182,25 @@ class NativeComm(object):
             self.handle = ctypes.c_void_p()
 
     def async_error(self):
-        return lib().hcomm_async_error(self.handle)
+        """ncclCommGetAsyncError (0 = healthy; a destroyed communicator reads healthy)"""
+        h = self.handle
+        if not (h and h.value):
+            return 0
+        return lib().hcomm_async_error(h)
 
     # ---- stream plumbing --------------------------------------------------------
-    def _run(self, fn, tensors, async_op, post=None):
+    def _run(self, fn, tensors, async_op, post=None, what='collective'):
         """Run ``fn(stream_ptr)``: on the comm stream after the current stream's work
-        (async), or on the current stream itself (sync)."""
+        (async), or on the current stream itself (sync).  Outside hipGraph capture the
+        completion event goes to the watchdog (deadline ``HETU_COMM_TIMEOUT``)."""
+        from ..runtime import DeviceEvent
+        from ..utils.hipgraph import _CAPTURING
         cur = torch.cuda.current_stream()
+        wd = self._wd if not _CAPTURING[0] else None
         if not async_op:
             fn(cur.cuda_stream)
+            if wd is not None:
+                wd.track(DeviceEvent().record(cur), self._what(what, tensors), self)
             if post is not None:
                 post()
             return None
@@ -196,10 +210,16 @@ class NativeComm(object):
         for t in tensors:
             if t is not None and t.is_cuda:
                 record_stream(t, s)
-        from ..runtime import DeviceEvent
         ev = DeviceEvent(timing=_TIMING)
         ev.record(s)
+        if wd is not None:
+            wd.track(ev, self._what(what, tensors), self)
         return Work(ev, post)
+
+    @staticmethod
+    def _what(what, tensors):
+        t = next((x for x in tensors if x is not None), None)
+        return what if t is None else '%s(%d x %s)' % (what, t.numel(), str(t.dtype).replace('torch.', ''))
 
     # ---- collectives ------------------------------------------------------------
     def all_reduce(self, t, op='sum', async_op=False):
@@ -208,7 +228,7 @@ class NativeComm(object):
         nop = _NCCL_OP[op]
         return self._run(lambda st: _check(L.hcomm_all_reduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
                                                               _NCCL_DT[t.dtype], nop, st), 'all_reduce'),
-                         (t,), async_op)
+                         (t,), async_op, what='all_reduce')
 
     def reduce_scatter(self, out, inp, op='sum', async_op=False):
         inp = inp.contiguous()
@@ -217,7 +237,7 @@ class NativeComm(object):
         return self._run(lambda st: _check(L.hcomm_reduce_scatter(self.handle, inp.data_ptr(), out.data_ptr(),
                                                                   out.numel(), _NCCL_DT[inp.dtype], _NCCL_OP[op],
                                                                   st), 'reduce_scatter'),
-                         (out, inp), async_op)
+                         (out, inp), async_op, what='reduce_scatter')
 
     def all_gather(self, out, inp, async_op=False):
         inp = inp.contiguous()
@@ -225,21 +245,21 @@ class NativeComm(object):
         L = lib()
         return self._run(lambda st: _check(L.hcomm_all_gather(self.handle, inp.data_ptr(), out.data_ptr(),
                                                               inp.numel(), _NCCL_DT[inp.dtype], st), 'all_gather'),
-                         (out, inp), async_op)
+                         (out, inp), async_op, what='all_gather')
 
     def broadcast(self, t, root=0, async_op=False):
         assert t.is_contiguous()
         L = lib()
         return self._run(lambda st: _check(L.hcomm_broadcast(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
                                                              _NCCL_DT[t.dtype], int(root), st), 'broadcast'),
-                         (t,), async_op)
+                         (t,), async_op, what='broadcast')
 
     def reduce(self, t, root=0, op='sum', async_op=False):
         assert t.is_contiguous()
         L = lib()
         return self._run(lambda st: _check(L.hcomm_reduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
                                                           _NCCL_DT[t.dtype], _NCCL_OP[op], int(root), st),
-                                           'reduce'), (t,), async_op)
+                                           'reduce'), (t,), async_op, what='reduce')
 
     def all_to_all(self, out, inp, async_op=False):
         inp = inp.contiguous()
@@ -248,7 +268,7 @@ class NativeComm(object):
         chunk = inp.numel() // self.nrank
         return self._run(lambda st: _check(L.hcomm_all_to_all(self.handle, inp.data_ptr(), out.data_ptr(), chunk,
                                                               _NCCL_DT[inp.dtype], st), 'all_to_all'),
-                         (out, inp), async_op)
+                         (out, inp), async_op, what='all_to_all')
 
     def p2p(self, ops, async_op=True):
         """ops: [('send'|'recv', tensor, peer)] as one RCCL group."""
@@ -260,7 +280,8 @@ class NativeComm(object):
                 f = L.hcomm_send if kind == 'send' else L.hcomm_recv
                 _check(f(self.handle, t.data_ptr(), t.numel(), _NCCL_DT[t.dtype], int(peer), st), kind)
             _check(L.hcomm_group_end(), 'group_end')
-        return self._run(run, [t for _, t, _ in ops], async_op)
+        return self._run(run, [t for _, t, _ in ops], async_op,
+                         what='p2p[%s]' % ','.join('%s:%d' % (k, p) for k, _, p in ops))
 
     # ---- bf16 wire, fp32 accumulation --------------------------------------------
     def _ws(self, n, dtype, tag):
@@ -295,7 +316,7 @@ class NativeComm(object):
             KC.sum_chunks_bf16(recv, P, c, red, st)           # fp32 accumulate, bf16 out
             _check(L.hcomm_all_gather(self.handle, red.data_ptr(), send.data_ptr(), c, 9, st), 'all_gather')
             KC.cast_bf16_f32(send, t, st)
-        return self._run(run, (t, send, recv, red), async_op)
+        return self._run(run, (t, send, recv, red), async_op, what='all_reduce_bf16')
 
     def __repr__(self):
         return 'NativeComm(rank=%d, nrank=%d)' % (self.rank, self.nrank)

@@ -137,6 +137,14 @@ def close_all():
     _LIVE.clear()
 
 
+def drain_dense():
+    """finish every overlapped dense exchange in flight (an evaluation step must see the
+    parameters the last training step pulled)"""
+    for t in _LIVE:
+        if isinstance(t, PSDense):
+            t.drain()
+
+
 class PSTable(object):
     def __init__(self, node, config):
         _LIVE.append(self)
@@ -327,6 +335,7 @@ class PSDense(object):
     """Flat dense parameters held by the PS (pure PS mode)."""
 
     def __init__(self, flat, key, config, publish=None, overlap=None):
+        _LIVE.append(self)          # close_all() (worker_finish) drains the overlapped exchange
         self.flat = flat
         self.key = key
         self.agent = psw.get_agent()
@@ -406,6 +415,17 @@ class PSDense(object):
         """finish the exchange in flight (before a checkpoint, an evaluation or shutdown)"""
         if self._thread is not None:
             self._apply_inflight()
+
+    def close(self):
+        """drain, then stop the helper thread (before the agent finalises)"""
+        if self._thread is None:
+            return
+        try:
+            self.drain()
+        finally:
+            self._q.put(None)
+            self._thread.join(timeout=60)
+            self._thread = None
 
     def _step_overlapped(self, g, lr):
         if self._thread is None:

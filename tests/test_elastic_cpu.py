@@ -50,6 +50,22 @@ JOB = textwrap.dedent('''
         if (step + 1) % 3 == 0:
             checkpoint.save_resumable(ex, ckpt, step + 1)
         if attempt == 0 and rank == 1 and step + 1 == crash_at:
+            if len(sys.argv) > 4 and sys.argv[4] == 'watchdog':
+                # an RCCL async error surfaces while this rank is parked in a collective:
+                # the watchdog thread (not the training loop) must end the process
+                from hetu_61a7_amd.parallel import watchdog
+                import time
+
+                class FakeComm(object):
+                    def async_error(self):
+                        return 6          # ncclRemoteError
+                    def abort(self):
+                        sys.stderr.write('fake comm aborted\\n')
+                    def __repr__(self):
+                        return 'FakeComm'
+                fake = FakeComm()
+                watchdog.get().register(fake)
+                time.sleep(120)           # "stuck": only the watchdog can end this
             os._exit(3)
     if rank == 0:
         np.savez(out, start=start, **checkpoint.state_dict(ex))
@@ -57,11 +73,11 @@ JOB = textwrap.dedent('''
 ''')
 
 
-def _run(tmp_path, tag, crash_at, restarts, extra=()):
+def _run(tmp_path, tag, crash_at, restarts, extra=(), env_extra=None):
     script = tmp_path / 'job.py'
     script.write_text(JOB)
     ckpt, out = tmp_path / ('ckpt_' + tag), tmp_path / (tag + '.npz')
-    env = dict(os.environ, PYTHONPATH=ROOT, HETU_USE_CONFIG='0')
+    env = dict(os.environ, PYTHONPATH=ROOT, HETU_USE_CONFIG='0', **(env_extra or {}))
     env.pop('MASTER_PORT', None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'bin', 'heturun'), '-w', '2',
                         '--max-restarts', str(restarts), sys.executable, str(script),
@@ -82,6 +98,25 @@ def test_restart_resumes_from_last_snapshot(tmp_path):
         np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6)
     # keep=2: only the two newest snapshots survive, `latest` names the last one
     assert sorted(os.listdir(ckpt)) == ['latest', 'step_6', 'step_9']
+
+
+def test_watchdog_async_error_restarts_group(tmp_path):
+    """SURVEY §5.3 RCCL watchdog: an asynchronous communicator error on rank 1 (a fake
+    communicator registered with the process's watchdog) ends that worker with the
+    watchdog's exit code while its main thread is blocked; heturun relaunches the group,
+    which resumes from the last snapshot and ends with the uninterrupted parameters."""
+    ref, ref_out, _ = _run(tmp_path, 'wref', crash_at=-1, restarts=0)
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    r, out, _ = _run(tmp_path, 'wd', crash_at=7, restarts=1, extra=['watchdog'],
+                     env_extra={'HETU_WATCHDOG_POLL': '0.05'})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert 'hetu watchdog (rank 1): RCCL asynchronous error 6 on FakeComm' in r.stderr, r.stderr[-3000:]
+    assert 'fake comm aborted' in r.stderr
+    assert 'rc=75' in r.stderr and 'restart 1/1' in r.stderr
+    a, b = np.load(ref_out), np.load(out)
+    assert int(b['start']) == 6
+    for k in ('w1', 'w2'):
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6)
 
 
 def test_no_restart_propagates_failure(tmp_path):

@@ -182,3 +182,40 @@ def test_single_process_multi_device_comm():
     the test box): grouped all-reduce and all-to-all."""
     res = _spawn(_multi_device)
     assert res['n'] >= 1 and res['ar'] == 0.0 and res['a2a'] == 0.0, res
+
+
+def _watchdog_step(port, q):
+    try:
+        _env(port)
+        os.environ['HETU_FORCE_DP'] = '1'
+        os.environ['HETU_WATCHDOG_POLL'] = '0.02'
+        from hetu_61a7_amd.parallel import watchdog
+        rng = np.random.RandomState(0)
+        X = rng.randn(128, 64).astype(np.float32)
+        Y = np.eye(16, dtype=np.float32)[rng.randint(0, 16, 128)]
+        losses, info = _mlp(X, Y, True, 'fp32')
+        wd = watchdog.get()
+        from hetu_61a7_amd.parallel import comm as C
+        C.world().barrier()                       # host wait under the deadline
+        torch.cuda.synchronize()
+        import time
+        time.sleep(0.1)                           # a few polls after the last collective
+        st = wd.stats()
+        C.destroy()                               # stops the monitor thread
+        q.put(dict(stats=st, losses=losses, after=watchdog._WD is None and not wd.running,
+                   failed=wd.failed, **info))
+    except Exception as e:
+        q.put({'error': repr(e)})
+
+
+def test_watchdog_monitors_training_step():
+    """the watchdog starts with the native communicator, tracks the
+    bucketed all-reduces of forced single-rank DP steps until they complete, polls the
+    communicator's async error state, and stops cleanly at comm.destroy()."""
+    res = _spawn(_watchdog_step)
+    st = res['stats']
+    assert res['backend'] == 'hetu-rccl', res
+    assert st['running'] and st['polls'] >= 3 and st['communicators'] >= 1, st
+    assert st['tracked'] >= res['buckets'] and st['in_flight'] == 0, st
+    assert st['completed'] == st['tracked'], st
+    assert res['failed'] is None and res['after'], res

@@ -36,6 +36,11 @@ def parse():
                    help='wdl: do not prefetch the next batch rows with the push')
     p.add_argument('--model', default='resnet50', choices=['resnet50', 'wdl', 'bert', 'moe', 'logreg'])
     p.add_argument('--moe-gate', default='topk', choices=['topk', 'dts'])
+    p.add_argument('--moe-local-experts', type=int, default=2,
+                   help='moe: experts per GPU (the reference scripts: 2; the DTS schedule run: 16)')
+    p.add_argument('--dts-schedule', default=None,
+                   help='moe dts: "tau0,decay,tau_min" temperature schedule; every step is then timed '
+                        'alone and the JSON reports ms/step per expert budget and the budget changes')
     p.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     p.add_argument('--bucket-mb', type=float, default=32)
     p.add_argument('--zero', type=int, default=0, help='1: ZeRO-1 sharded optimizer state over the DP group')

@@ -57,6 +57,7 @@ struct Args {
   int B, NH;
   float scale, keep;
   uint64_t seed;
+  const uint64_t* rngo;    // step counter of the graph-safe RNG (common.h rng_seed)
   short* ws;              // split backward: P_drop^T then (scale dS)^T, [B*NH][S][S] bf16 each
 };
 
@@ -145,6 +146,7 @@ __device__ __forceinline__ void stage_t(const bf16* X, int64_t ld, short* T) {
 // -------------------------------------------------------------------------------------
 template <int KB>
 __global__ void __launch_bounds__(256) attn_fwd_k(Args a) {
+  a.seed = rng_seed(a.seed, a.rngo);
   constexpr int S = 32 * KB;
   constexpr int LT = S + PAD;
   __shared__ short vt[HD * LT];
@@ -244,6 +246,7 @@ __global__ void __launch_bounds__(256) attn_fwd_k(Args a) {
 // workgroups per CU at the cost of the workspace round trip
 template <int KB, int PH = 0>
 __global__ void __launch_bounds__(256) attn_bwd_k(Args a) {
+  a.seed = rng_seed(a.seed, a.rngo);
   constexpr int S = 32 * KB;
   constexpr int LT = S + PAD;
   constexpr int LP = PH == 0 ? LT : S;   // row stride of the P_drop^T / dS^T images
@@ -422,7 +425,7 @@ static Args make_args(const void* q, const void* k, const void* v, int64_t ldq, 
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv;
   a.mask = mask;
   a.B = B; a.NH = NH;
-  a.scale = scale; a.keep = keep; a.seed = (uint64_t)seed;
+  a.scale = scale; a.keep = keep; a.seed = (uint64_t)seed; a.rngo = hetu_rng_offset_ptr();
   return a;
 }
 

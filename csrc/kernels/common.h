@@ -117,6 +117,21 @@ struct Philox {
   }
 };
 
+// Graph-safe RNG: every seeded kernel draws from Philox(rng_seed(seed, off))
+// where `seed` is the launch's host seed -- fixed per op and per call within a step, so a
+// captured hipGraph replays the same launch arguments -- and `off` points at the device's
+// step counter, which the framework advances once per training step with
+// hetu_rng_advance (a one-thread kernel on the step's stream, captured with the step).
+// A replay therefore draws fresh masks, and eager and replayed steps draw the same ones.
+// The forward and the backward of a step read the same counter value.  off == nullptr
+// (no counter registered on this device): the host seed alone.
+constexpr uint64_t kRngMix = 0x9E3779B97F4A7C15ull;
+__device__ __forceinline__ uint64_t rng_seed(uint64_t seed, const uint64_t* off) {
+  return off ? seed + *off * kRngMix : seed;
+}
+// host: the registered step counter of the calling thread's current device (random.hip)
+uint64_t* hetu_rng_offset_ptr();
+
 // 16-byte vector load/store helpers (8 bf16 or 4 fp32 per lane)
 template <typename T> struct Vec;
 template <> struct Vec<float> { static constexpr int N = 4; typedef float4 type; };

@@ -57,6 +57,7 @@ struct FArgs {
   int B, NH, Sq, Sk;
   float scale, keep;
   uint64_t seed;
+  const uint64_t* rngo;      // step counter of the graph-safe RNG (common.h rng_seed)
   int causal;
 };
 
@@ -166,6 +167,7 @@ enum { MK_NONE = 0, MK_KEY = 1, MK_FULL = 2 };
 // more than 8 (P <= 256, exact in fp32 accumulation), which after the first blocks is rare.
 template <int D, bool DROP, int MK>
 __global__ void __launch_bounds__(256) flash_fwd_k(FArgs a) {
+  a.seed = rng_seed(a.seed, a.rngo);
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ short vt[2][D * LT];
   __shared__ __attribute__((aligned(16))) float msk[2][KBLK];
@@ -344,6 +346,7 @@ __global__ void __launch_bounds__(256) flash_dsum_k(FArgs a, float* dsum) {
 // double-buffered K^T image, one barrier per block)
 template <int D, bool DROP, int MK>
 __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
+  a.seed = rng_seed(a.seed, a.rngo);
   constexpr int DS = D / 16, DB = D / 32;
   constexpr bool PF = D <= 32;     // fragments a block ahead only where registers allow 2 waves / SIMD
   __shared__ short kt[2][D * LT];
@@ -482,6 +485,7 @@ __global__ void __launch_bounds__(256) flash_dq_k(FArgs a) {
 // that they would cost the second wave per SIMD).
 template <int D, bool DROP, int MK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? 2 : 1))) flash_dkdv_k(FArgs a) {
+  a.seed = rng_seed(a.seed, a.rngo);
   constexpr int DS = D / 16, DB = D / 32;
   constexpr bool PF = D <= 32;
   __shared__ short qt[2][D * LT];
@@ -763,7 +767,7 @@ HETU_API int hetu_flash_fwd(const void* q, const void* k, const void* v, const i
   a.mask = mask;
   if (mask) { a.mb = mst[0]; a.mh = mst[1]; a.mq = mst[2]; a.mk = mst[3]; }
   a.B = B; a.NH = NH; a.Sq = Sq; a.Sk = Sk;
-  a.scale = scale; a.keep = keep; a.seed = (uint64_t)seed; a.causal = causal;
+  a.scale = scale; a.keep = keep; a.seed = (uint64_t)seed; a.rngo = hetu_rng_offset_ptr(); a.causal = causal;
   if (D == 32) return fwd_d<32>(a, st);
   if (D == 64) return fwd_d<64>(a, st);
   return fwd_d<128>(a, st);
@@ -793,7 +797,7 @@ HETU_API int hetu_flash_bwd(const void* q, const void* k, const void* v, const i
   a.mask = mask;
   if (mask) { a.mb = mst[0]; a.mh = mst[1]; a.mq = mst[2]; a.mk = mst[3]; }
   a.B = B; a.NH = NH; a.Sq = Sq; a.Sk = Sk;
-  a.scale = scale; a.keep = keep; a.seed = (uint64_t)seed; a.causal = causal;
+  a.scale = scale; a.keep = keep; a.seed = (uint64_t)seed; a.rngo = hetu_rng_offset_ptr(); a.causal = causal;
   if (D == 32) return bwd_d<32>(a, dsum, st);
   if (D == 64) return bwd_d<64>(a, dsum, st);
   return bwd_d<128>(a, dsum, st);

@@ -35,6 +35,7 @@ static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin
   ep.C2 = C2;
   ep.drop_keep = drop_keep < 1.f ? drop_keep : 0.f;
   ep.drop_seed = drop_seed;
+  ep.drop_off = ep.drop_keep > 0.f ? hetu_rng_offset_ptr() : nullptr;
   ep.gmask = gmask;
   ep.gmask_scale = gmask_scale;
   if ((C2 || ep.drop_keep > 0.f || gmask) && (splitk > 1 || atomic)) return (int)hipErrorInvalidValue;

@@ -532,6 +532,8 @@ struct Epi {
   // that produces its input, from the forward's output alone
   const void* gmask;
   float gmask_scale;
+  // step counter of the graph-safe RNG (common.h rng_seed) for the epilogue dropout
+  const uint64_t* drop_off;
 };
 
 // column statistics of one epilogue: each thread holds sums of its 8 columns over
@@ -730,8 +732,9 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
   }
   if ((EX & 2) && ep.drop_keep > 0.f) {
     const uint64_t ctr = ((uint64_t)m * (uint64_t)N + (uint64_t)n) >> 2;
-    const uint4 r0 = Philox::gen(ep.drop_seed, ctr);
-    const uint4 r1 = Philox::gen(ep.drop_seed, ctr + 1);
+    const uint64_t sd = rng_seed(ep.drop_seed, ep.drop_off);
+    const uint4 r0 = Philox::gen(sd, ctr);
+    const uint4 r1 = Philox::gen(sd, ctr + 1);
     const uint32_t q[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
     const float inv = 1.f / ep.drop_keep;
 #pragma unroll

@@ -89,7 +89,8 @@ __global__ void col_sum2_k(const float* __restrict__ a, const float* __restrict_
 
 template <typename T>
 __global__ void __launch_bounds__(256) dropout_k(const T* __restrict__ x, T* __restrict__ y, int64_t n,
-                                                  float keep, uint64_t seed) {
+                                                  float keep, uint64_t seed_, const uint64_t* __restrict__ rngo) {
+  const uint64_t seed = rng_seed(seed_, rngo);
   const float inv = 1.f / keep;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
        i += (int64_t)gridDim.x * blockDim.x * 4) {
@@ -150,7 +151,9 @@ __global__ void __launch_bounds__(256) ln_fwd4_k(const T* __restrict__ x, const 
                                                   const float* __restrict__ g, const float* __restrict__ b,
                                                   T* __restrict__ y, T* __restrict__ sum_out,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                  int64_t R, int N, float eps, float keep, uint64_t seed) {
+                                                  int64_t R, int N, float eps, float keep, uint64_t seed_,
+                                                  const uint64_t* __restrict__ rngo) {
+  const uint64_t seed = rng_seed(seed_, rngo);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
@@ -222,10 +225,12 @@ __global__ void __launch_bounds__(64 * NW) ln_bwd4_k(const T* __restrict__ dy, c
                                                   const float* __restrict__ rstd, T* __restrict__ dsum,
                                                   T* __restrict__ dx_drop, float* __restrict__ pg,
                                                   float* __restrict__ pb, int64_t R, int N, int rpb, float keep,
-                                                  uint64_t seed, float* __restrict__ zero_a,
+                                                  uint64_t seed_, const uint64_t* __restrict__ rngo,
+                                                  float* __restrict__ zero_a,
                                                   float* __restrict__ zero_b, float* __restrict__ pd,
                                                   float* __restrict__ zero_d) {
   extern __shared__ float lds[];
+  const uint64_t seed = rng_seed(seed_, rngo);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nc = N >> 2;
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
@@ -470,7 +475,8 @@ static void launch_fwd4(const void* x, const void* res, const float* g, const fl
                         float* mean, float* rstd, int64_t R, int N, float eps, float keep, uint64_t seed,
                         hipStream_t st) {
   hipLaunchKernelGGL((ln_fwd4_k<T, CPL>), dim3((unsigned)((R + 3) / 4)), dim3(256), 0, st, (const T*)x,
-                     (const T*)res, g, b, (T*)y, (T*)sum_out, mean, rstd, R, N, eps, keep, seed);
+                     (const T*)res, g, b, (T*)y, (T*)sum_out, mean, rstd, R, N, eps, keep, seed,
+                     hetu_rng_offset_ptr());
 }
 
 // waves: rows in flight per block (4 or 8); the per-block partial-row count (nblk) is the
@@ -483,11 +489,11 @@ static void launch_bwd4(const void* dy, const void* xs, const float* g, const fl
   if (waves == 8)
     hipLaunchKernelGGL((ln_bwd4_k<T, CPL, 8>), dim3((unsigned)nblk), dim3(512), 8 * N * sizeof(float), st,
                        (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed,
-                       za, zb, pd, zd);
+                       hetu_rng_offset_ptr(), za, zb, pd, zd);
   else
     hipLaunchKernelGGL((ln_bwd4_k<T, CPL, 4>), dim3((unsigned)nblk), dim3(256), 4 * N * sizeof(float), st,
                        (const T*)dy, (const T*)xs, g, mean, rstd, (T*)dsum, (T*)dxd, pg, pb, R, N, rpb, keep, seed,
-                       za, zb, pd, zd);
+                       hetu_rng_offset_ptr(), za, zb, pd, zd);
 }
 
 #define HETU_CPL_DISPATCH(CPL_NEEDED, FN, ...)                 \
@@ -559,7 +565,8 @@ HETU_API int hetu_layernorm_bwd(const void* dy, const void* x, const float* g, c
 // experts' [65536 x 2048] dropouts at half the HBM bandwidth
 template <typename T>
 __global__ void __launch_bounds__(256) dropout8_k(const T* __restrict__ x, T* __restrict__ y, int64_t n8,
-                                                  float keep, uint64_t seed) {
+                                                  float keep, uint64_t seed_, const uint64_t* __restrict__ rngo) {
+  const uint64_t seed = rng_seed(seed_, rngo);
   const float inv = 1.f / keep;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n8; j += (int64_t)gridDim.x * blockDim.x) {
     float a[4], b[4];
@@ -582,14 +589,14 @@ HETU_API int hetu_dropout(const void* x, void* y, int64_t n, float keep, int64_t
                           hipStream_t st) {
   if ((n & 7) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
     const int g8 = stream_grid(n / 8, 256, 2);
-    if (is_bf16) hipLaunchKernelGGL(dropout8_k<bf16>, dim3(g8), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n / 8, keep, (uint64_t)seed);
-    else hipLaunchKernelGGL(dropout8_k<float>, dim3(g8), dim3(256), 0, st, (const float*)x, (float*)y, n / 8, keep, (uint64_t)seed);
+    if (is_bf16) hipLaunchKernelGGL(dropout8_k<bf16>, dim3(g8), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n / 8, keep, (uint64_t)seed, hetu_rng_offset_ptr());
+    else hipLaunchKernelGGL(dropout8_k<float>, dim3(g8), dim3(256), 0, st, (const float*)x, (float*)y, n / 8, keep, (uint64_t)seed, hetu_rng_offset_ptr());
     HETU_LAUNCH_CHECK();
     return 0;
   }
   int grid = stream_grid((n + 3) / 4, 256, 1);
-  if (is_bf16) hipLaunchKernelGGL(dropout_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n, keep, (uint64_t)seed);
-  else hipLaunchKernelGGL(dropout_k<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, n, keep, (uint64_t)seed);
+  if (is_bf16) hipLaunchKernelGGL(dropout_k<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n, keep, (uint64_t)seed, hetu_rng_offset_ptr());
+  else hipLaunchKernelGGL(dropout_k<float>, dim3(grid), dim3(256), 0, st, (const float*)x, (float*)y, n, keep, (uint64_t)seed, hetu_rng_offset_ptr());
   HETU_LAUNCH_CHECK();
   return 0;
 }

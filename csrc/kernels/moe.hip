@@ -106,74 +106,83 @@ template <typename T>
 __global__ void __launch_bounds__(256) dts_gate_k(const T* __restrict__ logits, float* __restrict__ probs,
                                                    int64_t* __restrict__ idx, float* __restrict__ val,
                                                    int* __restrict__ hist, int rows, int E, int k, float inv_tau,
-                                                   float thr, uint64_t seed, int noise) {
+                                                   float thr, uint64_t seed_, const uint64_t* __restrict__ rngo,
+                                                   int noise) {
+  // the active-choice histogram is folded per block in LDS (one global atomic per bin per
+  // block instead of one per token: 65536 tokens into <= 17 counters serialised on them)
+  __shared__ int bh[kMaxK + 1];
+  const uint64_t seed = rng_seed(seed_, rngo);
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const T* x = logits + (int64_t)row * E;
-  float v[kMaxEPL];
-  float m = -INFINITY;
-#pragma unroll
-  for (int i = 0; i < kMaxEPL; ++i) {
-    const int e = lane + 64 * i;
-    float z = -INFINITY;
-    if (e < E) {
-      z = to_f(x[e]);
-      if (noise) {
-        const float u = Philox::u01(Philox::gen(seed, (uint64_t)row * (uint64_t)E + (uint64_t)e).x);
-        z -= __logf(-__logf(u));
-      }
-      z *= inv_tau;
-    }
-    v[i] = z;
-    m = fmaxf(m, z);
-  }
-  m = wave_max(m);
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < kMaxEPL; ++i) {
-    const int e = lane + 64 * i;
-    v[i] = (e < E) ? __expf(v[i] - m) : 0.f;
-    s += v[i];
-  }
-  s = wave_sum(s);
-  const float inv = 1.f / s;
-#pragma unroll
-  for (int i = 0; i < kMaxEPL; ++i) {
-    const int e = lane + 64 * i;
-    if (e < E) {
-      v[i] *= inv;
-      probs[(int64_t)row * E + e] = v[i];
-    } else {
-      v[i] = -INFINITY;
-    }
-  }
-  int active = 0;
-  for (int j = 0; j < k; ++j) {
-    float bv = -INFINITY;
-    int be = 0x7fffffff;
-#pragma unroll
+  if (threadIdx.x <= kMaxK) bh[threadIdx.x] = 0;
+  __syncthreads();
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const T* x = logits + (int64_t)row * E;
+    float v[kMaxEPL];
+    float m = -INFINITY;
+  #pragma unroll
     for (int i = 0; i < kMaxEPL; ++i) {
       const int e = lane + 64 * i;
-      if (e < E && (v[i] > bv || (v[i] == bv && e < be))) { bv = v[i]; be = e; }
+      float z = -INFINITY;
+      if (e < E) {
+        z = to_f(x[e]);
+        if (noise) {
+          const float u = Philox::u01(Philox::gen(seed, (uint64_t)row * (uint64_t)E + (uint64_t)e).x);
+          z -= __logf(-__logf(u));
+        }
+        z *= inv_tau;
+      }
+      v[i] = z;
+      m = fmaxf(m, z);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oe = __shfl_xor(be, o, 64);
-      if (ov > bv || (ov == bv && oe < be)) { bv = ov; be = oe; }
+    m = wave_max(m);
+    float s = 0.f;
+  #pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i) {
+      const int e = lane + 64 * i;
+      v[i] = (e < E) ? __expf(v[i] - m) : 0.f;
+      s += v[i];
     }
-    const bool on = j == 0 || bv >= thr;     // wave-uniform
-    if (lane == 0) {
-      idx[(int64_t)row * k + j] = on ? be : -1;
-      val[(int64_t)row * k + j] = on ? bv : 0.f;
+    s = wave_sum(s);
+    const float inv = 1.f / s;
+  #pragma unroll
+    for (int i = 0; i < kMaxEPL; ++i) {
+      const int e = lane + 64 * i;
+      if (e < E) {
+        v[i] *= inv;
+        probs[(int64_t)row * E + e] = v[i];
+      } else {
+        v[i] = -INFINITY;
+      }
     }
-    active += on ? 1 : 0;
-#pragma unroll
-    for (int i = 0; i < kMaxEPL; ++i)
-      if (lane + 64 * i == be) v[i] = -INFINITY;
+    int active = 0;
+    for (int j = 0; j < k; ++j) {
+      float bv = -INFINITY;
+      int be = 0x7fffffff;
+  #pragma unroll
+      for (int i = 0; i < kMaxEPL; ++i) {
+        const int e = lane + 64 * i;
+        if (e < E && (v[i] > bv || (v[i] == bv && e < be))) { bv = v[i]; be = e; }
+      }
+  #pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oe = __shfl_xor(be, o, 64);
+        if (ov > bv || (ov == bv && oe < be)) { bv = ov; be = oe; }
+      }
+      const bool on = j == 0 || bv >= thr;     // wave-uniform
+      if (lane == 0) {
+        idx[(int64_t)row * k + j] = on ? be : -1;
+        val[(int64_t)row * k + j] = on ? bv : 0.f;
+      }
+      active += on ? 1 : 0;
+  #pragma unroll
+      for (int i = 0; i < kMaxEPL; ++i)
+        if (lane + 64 * i == be) v[i] = -INFINITY;
+    }
+    if (lane == 0 && hist != nullptr) atomicAdd(bh + active, 1);
   }
-  if (lane == 0 && hist != nullptr) atomicAdd(hist + active, 1);
+  __syncthreads();
+  if (hist != nullptr && threadIdx.x <= k && bh[threadIdx.x] != 0) atomicAdd(hist + threadIdx.x, bh[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------
@@ -548,14 +557,17 @@ HETU_API int hetu_moe_dts_gate(const void* logits, float* probs, int64_t* idx, f
     hipError_t e = hipMemsetAsync(hist, 0, (size_t)(k + 1) * sizeof(int), s);
     if (e != hipSuccess) return (int)e;
   }
-  const int g = (rows + 3) / 4;
+  // <= 8 blocks per CU of 4 tokens per pass: each block folds >= 32 tokens' histogram
+  int g = (rows + 3) / 4;
   if (g == 0) return 0;
+  if (g > 2048) g = 2048;
+  const uint64_t* ro = noise ? hetu_rng_offset_ptr() : nullptr;
   if (bf16_in)
     dts_gate_k<bf16><<<g, 256, 0, s>>>((const bf16*)logits, probs, idx, val, hist, rows, E, k, inv_tau, thr, seed,
-                                       noise);
+                                       ro, noise);
   else
     dts_gate_k<float><<<g, 256, 0, s>>>((const float*)logits, probs, idx, val, hist, rows, E, k, inv_tau, thr,
-                                        seed, noise);
+                                        seed, ro, noise);
   HETU_LAUNCH_CHECK();
   return 0;
 }

@@ -72,3 +72,44 @@ def check_call(ret):
             except AttributeError:
                 pass
         raise RuntimeError('native call failed (%d): %s' % (ret, msg))
+
+
+# ---- framework-owned execution state (the launch path asks torch nothing) ----
+# The current HIP stream of this thread (a raw hipStream_t; 0 = the device's null stream),
+# set only by ``runtime.use_stream`` (which keeps torch's current stream in step for the
+# few torch ops that still run), the current device of the process and whether a GPU is
+# present: read by every kernel launch and device allocation without a torch call.
+import threading as _threading
+
+_TLS = _threading.local()
+
+
+def cur_stream() -> int:
+    return getattr(_TLS, 'h', 0)
+
+
+_GPU = [None]
+
+
+def gpu_available() -> bool:
+    g = _GPU[0]
+    if g is None:
+        g = _GPU[0] = bool(torch.cuda.is_available())
+    return g
+
+
+_DEV = [None]
+
+
+def cur_device() -> int:
+    d = _DEV[0]
+    if d is None:
+        d = _DEV[0] = int(torch.cuda.current_device()) if gpu_available() else 0
+    return d
+
+
+def set_device(d: int):
+    """the process's device (torch's current device follows)"""
+    d = int(d)
+    torch.cuda.set_device(d)
+    _DEV[0] = d

@@ -110,10 +110,10 @@ class Dataloader(object):
         if self.device is None or self.device.type != 'cuda':
             return (b, None)
         hb = b.pin_memory()
-        with torch.cuda.stream(self._stream):
+        from .runtime import DeviceEvent, use_stream
+        with use_stream(self._stream):
             db = hb.to(self.device, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self._stream)
+            ev = DeviceEvent().record(self._stream)
         # the host batch rides along: a consumer that needs the values on the host (PS /
         # HET-cache lookups of sparse ids, ``ps.table.host_ids``) reads it instead of a
         # device-to-host copy that would wait for the GPU
@@ -130,9 +130,10 @@ class Dataloader(object):
         self.batch_index = nxt
         t = cur[0]
         if len(cur) > 1 and cur[1] is not None:
-            torch.cuda.current_stream().wait_event(cur[1])
+            cur[1].wait(None)                       # the framework's current stream
             from .memory_pool import record_stream
-            record_stream(t, torch.cuda.current_stream())
+            from ._base import cur_stream
+            record_stream(t, cur_stream())
         return t
 
     def get_next_arr(self):

@@ -79,7 +79,8 @@ def _mask_f32(mask):
         return None
     if mask.dtype == torch.float32 and mask.is_contiguous():
         return mask
-    if mask.is_cuda and torch.cuda.is_current_stream_capturing():
+    from ..utils.hipgraph import capturing
+    if mask.is_cuda and capturing():
         return _f32(mask)
     root = mask._base if mask._base is not None else mask     # ops hand in fresh views of it
     sig = (mask.data_ptr(), tuple(mask.shape), mask.stride(), mask._version)

@@ -5,10 +5,11 @@ kernels: the implicit-GEMM tiles of ``gemm_core.h`` (``hip`` 128x128, ``hip256``
 ``hip64`` 128x64, ``hip_lo`` single-stage), the 3x3 halo-tile kernels of
 ``conv3x3.hip`` (``hip33``), the direct stem kernels of ``stem.hip`` (``hip_stem``)
 and the role-swapped 64-channel weight gradient (``hip64t``); per shape the fastest of
-them is picked by measurement (``autotune.choose``).  MIOpen / hipBLASLt (``vendor``,
-``blas*``) are an explicit A/B switch only: ``HETU_CONV=vendor`` runs them, ``auto``
-times them together with the hand-written kernels; the default ``hip`` never does (a
-shape no hand-written kernel takes is counted in ``kernels.FALLBACKS``).
+them is picked by measurement (``autotune.choose``).  There is no library path: a device
+convolution no hand-written kernel takes raises ``NoKernelError`` (MIOpen / hipBLASLt
+comparisons live in the A/B harness ``scripts/vendor_ref.py``).  CPU tensors take the
+native OpenMP backend or torch's CPU convolution (the numerics reference).
+Reference: ``src/ops/CudnnConv2d.cu:54-245``, ``CudnnConv2dAddBias.cu:93``.
 """
 from __future__ import annotations
 
@@ -18,11 +19,9 @@ import torch
 import torch.nn.functional as F
 from .. import native_array as _NA
 
-from . import native, record_vendor
+from . import native, no_kernel  # noqa: F401
 
 CL = torch.channels_last
-# hip (default): hand-written kernels only; vendor: MIOpen / hipBLASLt (A/B switch); auto: both timed
-MODE = os.environ.get('HETU_CONV', 'hip')
 
 
 def _masked_store():
@@ -31,41 +30,24 @@ def _masked_store():
     return os.environ.get('HETU_BN_MASKED_STORE', '1') == '1'
 
 
-def _pick(key, hip, vendor, blas=None, tuned=None):
-    """hip: hand-written implicit GEMM; vendor: MIOpen; blas: a 1x1 convolution
-    run as the plain library GEMM it is (hipBLASLt), where applicable.
-    ``tuned()`` runs once the choice is made, before the call that produces the
-    result (candidates that write in place time against scratch until then)."""
-    if MODE == 'vendor':
-        record_vendor('conv')
-        return vendor()
+def _pick(key, hip, more=None, tuned=None):
+    """hip: the default hand-written implicit GEMM; more: other hand-written candidates
+    ({name: fn}, timed against it per shape).  ``tuned()`` runs once the choice is made,
+    before the call that produces the result (candidates that write in place time against
+    scratch until then).  No candidate takes the shape: NoKernelError."""
     from .autotune import choose
-    cands = {'hip': hip, 'vendor': vendor}
-    if blas is not None:
-        cands.update(blas)
-    c = choose(key, cands, MODE)
+    cands = {'hip': hip}
+    if more is not None:
+        cands.update(more)
+    c = choose(key, cands)
     if tuned is not None:
         tuned()
-    if c != 'vendor':
-        r = cands[c]()
-        if r is not None:
-            if not c.startswith('hip'):
-                record_vendor('conv')
-            return r
-        if c.startswith('hip'):
-            _fallback(key[0])
-    if c != 'hip':
-        r = hip() if MODE == 'hip' else None
-        if r is not None:
-            return r
-    record_vendor('conv')
-    return vendor()
-
-
-def _fallback(name):
-    if MODE == 'hip':
-        from . import record_fallback
-        record_fallback('conv_' + name)
+    r = cands[c]()
+    if r is None and c != 'hip':
+        r = hip()
+    if r is None:
+        no_kernel('conv_' + key[0], str(key[1:]))
+    return r
 
 
 def _zeros(shape, device, dtype=torch.float32):
@@ -148,18 +130,15 @@ def stats_replicas(x_shape, w_shape, stride, padding):
 
 def conv2d_with_stats(x, w, stride, padding, out_sums=None):
     """(y, sums): the convolution (no bias) and the [2*Cout] per-channel sum / sum of
-    squares of y that a following training-mode BatchNorm needs (the fused candidates:
-    [R * 2*Cout] replicas, R = stats_replicas, folded by the BN forward).  Every candidate
-    delivers both, so the per-shape choice prices the statistics pass in: the
-    hand-written kernels fuse it into their epilogue, the library convolutions pay a
-    separate column-statistics pass.  ``out_sums``: a zeroed [R * 2*Cout] fp32 buffer the
+    squares of y that a following training-mode BatchNorm needs ([R * 2*Cout] replicas,
+    R = stats_replicas, folded by the BN forward), fused into the epilogue of every
+    hand-written candidate.  ``out_sums``: a zeroed [R * 2*Cout] fp32 buffer the
     fused candidates accumulate into (a persistent one the BN re-zeroes: no fill launch
     per call); fresh zeros otherwise and while the shape is being timed."""
     x, w = _match(x, w)
     if not (x.is_cuda and x.dtype == torch.bfloat16):
         return conv2d(x, w, None, stride, padding), None
     from . import conv_igemm
-    from .norm import col_sums
     x = x.contiguous(memory_format=CL)
     w = w.contiguous(memory_format=CL)
     co = w.shape[0]
@@ -176,13 +155,7 @@ def conv2d_with_stats(x, w, stride, padding, out_sums=None):
             return None if y is None else (y, s)
         return f
 
-    def separate(run):
-        def f():
-            y = run()
-            return None if y is None else (y, col_sums(y))
-        return f
-    cands = {'hip': fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, colstats=s)),
-             'vendor': separate(lambda: F.conv2d(x, w, None, stride, padding))}
+    cands = {'hip': fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, colstats=s))}
     if co >= 128:
         cands['hip256'] = fused(lambda s: conv_igemm.try_forward(x, w, stride, padding, tile=1, colstats=s))
     if co <= 64:
@@ -193,27 +166,17 @@ def conv2d_with_stats(x, w, stride, padding, out_sums=None):
         cands['hip_stem'] = fused(lambda s: conv_igemm.try_stem_forward(x, w, stride, padding, colstats=s))
     if conv_igemm.conv3x3_ok(x.shape, w.shape, stride, padding):
         cands['hip33'] = fused(lambda s: conv_igemm.try_conv3x3_forward(x, w, stride, padding, colstats=s))
-    if _plain_1x1((x, w), w.shape, stride, padding):
-        n, _, h, ww_ = x.shape
-        cands['blas'] = separate(lambda: torch.mm(_rows(x), w.reshape(co, -1).t()).view(n, h, ww_, co)
-                                 .permute(0, 3, 1, 2))
-    elif _needs_pad(x, w):
+    if _needs_pad(x, w):
         cands['hip_pad'] = fused(lambda s: conv_igemm.try_forward(_pad_c(x), _pad_c(w), stride, padding,
                                                                    colstats=s))
-    if MODE == 'vendor':
-        record_vendor('conv')
-        return cands['vendor']()
     from .autotune import choose
-    c = choose(key, cands, MODE)
+    c = choose(key, cands)
     tgt[0] = out_sums
     r = cands[c]()
-    if r is not None and not c.startswith('hip'):
-        record_vendor('conv')
+    if r is None and c != 'hip':
+        r = cands['hip']()
     if r is None:
-        if c.startswith('hip'):
-            _fallback('fwd_stats')
-        record_vendor('conv')
-        r = cands['vendor']()
+        no_kernel('conv_fwd_stats', str(key[1:]))
     return r
 
 
@@ -267,25 +230,19 @@ def conv2d(x, w, b, stride, padding):
     from . import cpu_native
     if cpu_native.active(x, w, b) and x.dim() == 4:
         return cpu_native.conv2d(x, w, b, stride, padding)
-    if _f32(x, w) and MODE != 'vendor':
+    if _f32(x, w):
         x = x.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
         return _pick(('fwd32', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding), b is not None),
-                     lambda: _fwd_f32(x, w, b, stride, padding),
-                     lambda: F.conv2d(x, w, b.to(x.dtype) if b is not None else None, stride, padding))
+                     lambda: _fwd_f32(x, w, b, stride, padding))
     if x.is_cuda:
+        if x.dtype != torch.bfloat16:
+            no_kernel('conv_fwd', str(x.dtype))
         x = x.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
         from . import conv_igemm
         blas = None
-        if _plain_1x1((x, w), w.shape, stride, padding):
-            n, _, h, ww_ = x.shape
-            co = w.shape[0]
-
-            def blas_fwd():
-                return torch.mm(_rows(x), w.reshape(co, -1).t()).view(n, h, ww_, co).permute(0, 3, 1, 2)
-            blas = {'blas': blas_fwd}
-        elif _needs_pad(x, w):
+        if _needs_pad(x, w):
             blas = {'hip_pad': lambda: conv_igemm.try_forward(_pad_c(x), _pad_c(w), stride, padding)}
             if conv_igemm.stem_ok(x, w, stride, padding):
                 blas['hip_stem'] = lambda: conv_igemm.try_stem_forward(x, w, stride, padding)
@@ -302,8 +259,7 @@ def conv2d(x, w, b, stride, padding):
             blas = dict(blas or {})
             blas['hip33'] = lambda: conv_igemm.try_conv3x3_forward(x, w, stride, padding)
         y = _pick(('fwd', tuple(x.shape), tuple(w.shape), tuple(stride), tuple(padding)),
-                  lambda: conv_igemm.try_forward(x, w, stride, padding),
-                  lambda: F.conv2d(x, w, None, stride, padding), blas)
+                  lambda: conv_igemm.try_forward(x, w, stride, padding), blas)
         if b is not None:
             from .elementwise import binary
             n, c, h, ww = y.shape
@@ -316,10 +272,9 @@ def conv2d(x, w, b, stride, padding):
 def _scatter_s2(acc, x_shape):
     """[N, C, H/2, W/2] -> [N, C, H, W] with acc at the even positions, zeros elsewhere
     (fallback for the subgrid join when no hand-written kernel takes it)"""
-    full = _zeros(tuple(x_shape), acc.device, acc.dtype)
-    if acc.is_contiguous(memory_format=CL):
-        full = full.contiguous(memory_format=CL)
-    full[:, :, ::2, ::2] = acc
+    n, c, h, w = x_shape
+    full = _zeros((n, h, w, c), acc.device, acc.dtype).permute(0, 3, 1, 2)     # channels-last
+    _copy_into(full[:, :, ::2, ::2], acc)
     return full
 
 
@@ -339,7 +294,7 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     convolution of the same input, in compact form -- and is added at the even
     positions only (the ResNet downsample join, without scattering that gradient)."""
     if acc_s2:
-        if not (g.is_cuda and g.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and MODE != 'vendor'
+        if not (g.is_cuda and g.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
                 and acc.dtype == torch.bfloat16 and _plain_1x1((g, w), w.shape, stride, padding)
                 and x_shape[2] % 2 == 0 and x_shape[3] % 2 == 0):
             return conv2d_backward_data(g, w, x_shape, stride, padding, acc=_scatter_s2(acc, x_shape), bn=bn)
@@ -351,7 +306,7 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     if bn is not None:
         if not (g.is_cuda and g.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and
                 (acc is None or acc.dtype == torch.bfloat16) and bn[1].dtype == torch.bfloat16 and
-                bn[1].is_contiguous(memory_format=CL) and x_shape[1] % 8 == 0 and MODE != 'vendor'):
+                bn[1].is_contiguous(memory_format=CL) and x_shape[1] % 8 == 0):
             return conv2d_backward_data(g, w, x_shape, stride, padding, acc, acc_inplace)
         r, masked = _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn)
         r.hetu_bn_bsums = bn[0]
@@ -362,13 +317,17 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
     if cpu_native.active(g, w, acc):
         dx = cpu_native.conv2d_backward_data(g, w, x_shape, stride, padding)
         return dx + acc.float() if acc is not None else dx
-    if _f32(g, w) and MODE != 'vendor' and (acc is None or acc.dtype == torch.float32):
+    if _f32(g, w):
         acc32 = acc.contiguous(memory_format=CL) if acc is not None else None
+        if acc32 is not None and acc32.dtype != torch.float32:
+            acc32 = _copy_into(_NA.empty(tuple(acc32.shape), dtype=torch.float32, device=acc32.device,
+                                         memory_format=CL), acc32)
         return _pick(('dgrad32', tuple(g.shape), tuple(w.shape), tuple(x_shape), tuple(stride), tuple(padding),
                       acc is not None),
-                     lambda: _dgrad_f32(g, w, x_shape, stride, padding, acc32),
-                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc))
+                     lambda: _dgrad_f32(g, w, x_shape, stride, padding, acc32))
     if g.is_cuda:
+        if g.dtype != torch.bfloat16:
+            no_kernel('conv_dgrad', str(g.dtype))
         g = g.contiguous(memory_format=CL)
         w = w.contiguous(memory_format=CL)
         if acc is not None:
@@ -376,30 +335,7 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
         from . import conv_igemm
         blas = None
         tuned = None
-        if _plain_1x1((g, w), w.shape, stride, padding) and (acc is None or acc.dtype == torch.bfloat16):
-            n, ci, h, ww_ = x_shape
-            co = w.shape[0]
-            key = ('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None)
-            inplace = acc is not None and acc_inplace and acc.is_contiguous(memory_format=CL)
-            from .autotune import _decisions
-            # while the shape is being timed, the in-place candidate accumulates into scratch
-            dst = [acc.clone(memory_format=CL) if inplace and key not in _decisions else acc]
-
-            def blas_dgrad():
-                w2 = w.reshape(co, ci)
-                if acc is None:
-                    d = torch.mm(_rows(g), w2)
-                elif inplace:     # hipBLASLt beta = 1 into the dead join operand: no copy of it
-                    _rows(dst[0]).addmm_(_rows(g), w2)
-                    return dst[0]
-                else:
-                    d = torch.addmm(_rows(acc), _rows(g), w2)
-                return d.view(n, h, ww_, ci).permute(0, 3, 1, 2)
-            blas = {'blas': blas_dgrad}
-
-            def tuned():
-                dst[0] = acc
-        elif _needs_pad(_NA.empty(0, x_shape[1], 1, 1, dtype=g.dtype, device=g.device), w) and acc is None:
+        if _needs_pad(_NA.empty(0, x_shape[1], 1, 1, dtype=g.dtype, device=g.device), w) and acc is None:
             n, ci, h, ww_ = x_shape
             cp = -(-ci // 8) * 8
 
@@ -420,16 +356,14 @@ def conv2d_backward_data(g, w, x_shape, stride, padding, acc=None, acc_inplace=F
             blas = dict(blas or {})
             blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_data(g, w, x_shape, stride, padding, acc=acc)
         return _pick(('dgrad', tuple(g.shape), tuple(w.shape), tuple(stride), tuple(padding), acc is not None),
-                     lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc),
-                     lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc), blas, tuned)
-    return _vendor_dgrad(g, w, x_shape, stride, padding, acc)
+                     lambda: conv_igemm.try_backward_data(g, w, x_shape, stride, padding, acc=acc), blas, tuned)
+    return _ref_dgrad(g, w, x_shape, stride, padding, acc)
 
 
 def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
     """conv2d_backward_data with the BatchNorm-backward reduction (see there)"""
     from . import conv_igemm
     from .autotune import _decisions
-    from .norm import bn_bwd_sums
     sums, xb, mask = bn
     g = g.contiguous(memory_format=CL)
     w = w.contiguous(memory_format=CL)
@@ -448,14 +382,6 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
             return r
         return f
 
-    def separate(run):
-        def f():
-            r = run()
-            if r is not None:
-                bn_bwd_sums(r, xb, mask, tgt[0])
-            masked[0] = False
-            return r
-        return f
     blas = {}
     if x_shape[1] >= 128:
         blas['hip256'] = hip(1)
@@ -473,7 +399,7 @@ def _dgrad_bn(g, w, x_shape, stride, padding, acc, acc_inplace, bn):
 
     def tuned():
         tgt[0] = sums
-    r = _pick(key, hip(0), separate(lambda: _vendor_dgrad(g, w, x_shape, stride, padding, acc)), blas, tuned)
+    r = _pick(key, hip(0), blas, tuned)
     return r, masked[0]
 
 
@@ -500,13 +426,6 @@ def _dgrad_s2join(g, w, x_shape, acc, bn):
             return r
         return f
 
-    def vendor():
-        masked[0] = False
-        r = _vendor_dgrad(g, w, x_shape, (1, 1), (0, 0), _scatter_s2(acc, x_shape))
-        if bn is not None:
-            from .norm import bn_bwd_sums
-            bn_bwd_sums(r, bn[1], bn[2], tgt[0])
-        return r
     blas = {'hip_lo': hip(3)}
     if x_shape[1] >= 128:
         blas['hip256'] = hip(1)
@@ -516,30 +435,18 @@ def _dgrad_s2join(g, w, x_shape, acc, bn):
     def tuned():
         if bn is not None:
             tgt[0] = bn[0]
-    r = _pick(key, hip(0), vendor, blas, tuned)
+    r = _pick(key, hip(0), blas, tuned)
     return r, masked[0]
 
 
-def _layout_of(t):
-    """channels-last for channels-last GPU tensors, else NCHW (one layout per vendor call)"""
-    return CL if t.is_cuda and t.is_contiguous(memory_format=CL) else torch.contiguous_format
-
-
-def _vendor_dgrad(g, w, x_shape, stride, padding, acc=None):
-    dx = _vendor_dgrad0(g, w, x_shape, stride, padding)
-    if acc is not None:
-        dx = _add_cl(dx, acc)
-    return dx
-
-
-def _vendor_dgrad0(g, w, x_shape, stride, padding):
-    # MIOpen only reads x's shape + layout: allocate it directly (``empty(...)
-    # .contiguous(CL)`` was a full-size copy of garbage per call) in g's layout --
-    # a channels-last x with an NCHW g (the fp32 3-channel differential test)
-    # mixes layouts in one MIOpen call, which aborted intermittently
-    xs = _NA.empty(x_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
+def _ref_dgrad(g, w, x_shape, stride, padding, acc=None):
+    """the CPU reference data gradient (torch's CPU convolution backward)"""
+    assert not g.is_cuda
+    xs = torch.empty(x_shape, dtype=g.dtype)
     dx, _, _ = torch.ops.aten.convolution_backward(
         g, xs, w, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [True, False, False])
+    if acc is not None:
+        dx = dx + acc.to(dx.dtype)
     return dx
 
 
@@ -557,47 +464,18 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             _copy_into(out, dw)
             return out
         return dw
-    if _f32(g, x) and MODE != 'vendor':
-        def vendor32():
-            dw = _vendor_wgrad(g, x, w_shape, stride, padding)
-            if out is None:
-                return dw
-            _copy_into(out, dw)
-            return out
-        # both candidates overwrite ``out`` (no accumulation): timing repeats are harmless
+    if _f32(g, x):
+        # every candidate overwrites ``out`` (no accumulation): timing repeats are harmless
         return _pick(('wgrad32', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
-                     lambda: _wgrad_f32(g, x, w_shape, stride, padding, out), vendor32)
+                     lambda: _wgrad_f32(g, x, w_shape, stride, padding, out))
     if g.is_cuda:
+        if g.dtype != torch.bfloat16:
+            no_kernel('conv_wgrad', str(g.dtype))
         g = g.contiguous(memory_format=CL)
         x = x.contiguous(memory_format=CL)
         from . import conv_igemm
-
-        def vendor():
-            dw = _vendor_wgrad(g, x, w_shape, stride, padding)
-            if out is None:
-                return dw
-            _copy_into(out, dw)
-            return out
         blas = None
-        if _plain_1x1((g, x), w_shape, stride, padding):
-            from .gemm import _vendor_into, _vendor_splitk_into
-            co, ci = w_shape[0], w_shape[1]
-
-            def dest():
-                if out is not None:
-                    return out.reshape(co, ci)
-                return _NA.empty((co, ci), dtype=torch.float32, device=g.device)
-
-            def wrap(d):
-                if d is None:
-                    return None
-                return out if out is not None else d.view(co, ci, 1, 1)   # the caller's exact view
-            A, B = _rows(g).t(), _rows(x)
-            blas = {'blas': lambda: wrap(_vendor_into(A, B, dest()))}
-            for sk in (4, 16):
-                if A.shape[1] % sk == 0 and A.shape[1] // sk >= 2048:
-                    blas['blas_sk%d' % sk] = (lambda sk=sk: wrap(_vendor_splitk_into(A, B, dest(), sk)))
-        elif _needs_pad(x, g.new_empty((g.shape[1], 1, 1, 1))):
+        if _needs_pad(x, _NA.empty((g.shape[1], 1, 1, 1), dtype=g.dtype, device=g.device)):
             co, ci, kh, kw = w_shape
             cp = -(-ci // 8) * 8
 
@@ -611,7 +489,7 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
                 _copy_into(out, d[:, :ci])
                 return out
             blas = {'hip_pad': pad_wgrad}
-            if conv_igemm.stem_ok(x, g.new_empty(w_shape), stride, padding):
+            if conv_igemm.stem_ok(x, _NA.empty(tuple(w_shape), dtype=g.dtype, device=g.device), stride, padding):
                 blas['hip_stem'] = lambda: conv_igemm.try_stem_backward_filter(g, x, w_shape, stride, padding,
                                                                                out=out)
         if w_shape[0] >= 128:
@@ -646,17 +524,11 @@ def conv2d_backward_filter(g, x, w_shape, stride, padding, out=None):
             blas['hip33'] = lambda: conv_igemm.try_conv3x3_backward_filter(g, x, w_shape, stride, padding, out=out)
         return _pick(('wgrad', tuple(g.shape), tuple(x.shape), tuple(w_shape), tuple(stride), tuple(padding)),
                      lambda: conv_igemm.try_backward_filter(g, x, w_shape, stride, padding, out=out,
-                                                            accumulate=False),
-                     vendor, blas)
-    dw = _vendor_wgrad(g, x, w_shape, stride, padding)
+                                                            accumulate=False), blas)
+    ws = torch.empty(w_shape, dtype=g.dtype)
+    _, dw, _ = torch.ops.aten.convolution_backward(       # the CPU reference
+        g, x, ws, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [False, True, False])
     if out is not None:
         _copy_into(out, dw)
         return out
-    return dw
-
-
-def _vendor_wgrad(g, x, w_shape, stride, padding):
-    ws = _NA.empty(w_shape, dtype=g.dtype, device=g.device, memory_format=_layout_of(g))
-    _, dw, _ = torch.ops.aten.convolution_backward(
-        g, x, ws, None, list(stride), list(padding), [1, 1], False, [0, 0], 1, [False, True, False])
     return dw

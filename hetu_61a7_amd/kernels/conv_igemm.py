@@ -6,25 +6,22 @@ dgrad    : M = N*H*W pixels,  N = Cin,  K = KH*KW*Cout (stride handled by
 wgrad    : M = Cout, N = KH*KW*Cin, K = N*OH*OW, split-K with fp32 atomics
            straight into an fp32 gradient.
 
-Shapes with Cin or Cout not a multiple of 8 (the 3-channel stem) return None
-and run on the vendor path.  ``HETU_CONV=vendor`` forces the vendor path.
+Shapes with Cin or Cout not a multiple of 8 (the 3-channel stem) return None; the caller
+(kernels/conv.py) then takes a zero-padded or a direct (stem) hand-written kernel.
 """
 from __future__ import annotations
-
-import os
 
 import torch
 from .. import native_array as _NA
 
 from . import fn, stream_ptr, check, record_native, P, I32, I64
 
-MODE = os.environ.get('HETU_CONV', 'hip')
 CL = torch.channels_last
 _GEOM = [I32] * 11
 
 
 def _ok(a, b, *channels):
-    return (MODE != 'vendor' and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and
+    return (a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and
             a.is_contiguous(memory_format=CL) and b.is_contiguous(memory_format=CL) and
             all(c % 8 == 0 for c in channels) and a.data_ptr() % 16 == 0 and
             b.data_ptr() % 16 == 0)
@@ -33,7 +30,7 @@ def _ok(a, b, *channels):
 def _ok32(a, b, *channels):
     """fp32 operands for the exact-fp32 MFMA convolution (gemm_f32.hip): channels-last,
     16-byte aligned, channel counts multiples of 4 (16-byte chunks of 4 floats)."""
-    return (MODE != 'vendor' and a.dtype == torch.float32 and b.dtype == torch.float32 and
+    return (a.dtype == torch.float32 and b.dtype == torch.float32 and
             a.is_contiguous(memory_format=CL) and b.is_contiguous(memory_format=CL) and
             all(c % 4 == 0 for c in channels) and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
 

@@ -17,6 +17,8 @@ def dropout(x, keep_prob, seed):
         check(f(xc.data_ptr(), y.data_ptr(), xc.numel(), float(keep_prob), int(seed), is_bf16(x),
                 stream_ptr()), 'dropout')
         return y
+    if x.is_cuda:
+        raise RuntimeError('dropout: no hand-written kernel for %s on %s (fp32 / bf16 only)' % (x.dtype, x.device))
     from . import cpu_native
     if cpu_native.active(x):
         return cpu_native.dropout(x, keep_prob, seed)

@@ -1,24 +1,23 @@
-"""GEMM entry points.
+"""GEMM entry points (reference ``src/ops/MatrixMult.cu:22``, ``BatchMatrixMult.cu:31-36``,
+``Linear.cu:50-55``, ``Addmm.cu:29``).
 
-``matmul(a, b, ta, tb, bias, activation)``: 2-D product with optional fused bias
-and ReLU/GELU epilogue.  bf16 shapes that the hand-written MFMA kernel
-(``gemm.hip``: 128x128x64 tiles, 4 waves, LDS double buffer, hardware
-transpose reads for MN-contiguous operands, XCD-aware block remap, fused
-epilogue) supports run there; everything else is a plain library
-GEMM (hipBLASLt through torch) followed by the elementwise epilogue kernel.
+``matmul(a, b, ta, tb, bias, activation)``: 2-D product with optional fused bias and
+ReLU/GELU epilogue.  On the GPU every product runs on a hand-written MFMA kernel
+(``gemm.hip``: 128x128 / 256x256 / 128x96 tiles, LDS double buffer or two-ahead K loop,
+hardware transpose reads for MN-contiguous operands, XCD-aware block remap, fused
+epilogues, split-K, a one-wave-per-output kernel for tiny products, zero-padded aligned
+operands as the last resort), the candidates timed against each other per shape.  There
+is no library path: a device product no hand-written kernel takes raises
+``NoKernelError``.  The vendor GEMMs live in the A/B harnesses (``scripts/vendor_ref.py``,
+``csrc/bench/gemm_bench.hip``).  CPU tensors take the native OpenMP backend or torch's
+CPU GEMM (the numerics reference).
 """
 from __future__ import annotations
-
-import os
 
 import torch
 from .. import native_array as _NA
 
-from . import native, record_vendor
-
-# hip (default): the hand-written kernels only, timed against each other per shape;
-# vendor: hipBLASLt (A/B switch); auto: hand-written and library candidates timed together
-_MFMA = os.environ.get('HETU_GEMM', 'hip')
+from . import native, no_kernel
 
 
 def _sig(t):
@@ -42,7 +41,7 @@ def matmul_pre(a, b, ta, tb, bias, activation):
     plain GEMM plus a separate activation pass."""
     a, b = _match(a, b)
     A2, B2 = _tr(a, ta), _tr(b, tb)
-    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16 and A2.dim() in (2, 3):
+    if native(a) and a.dtype == torch.bfloat16 and A2.dim() in (2, 3):
         from . import gemm_mfma
         from .autotune import choose
         shape = tuple(A2.shape[:-1]) + (B2.shape[-1],)
@@ -78,7 +77,7 @@ def matmul_act_dropout(a, b, activation, keep, seed):
     dropout kernel's Philox counters over the output -- in the GEMM epilogue; tiles autotuned
     per shape.  Elsewhere: the plain GEMM with the activation epilogue, then the dropout kernel."""
     a, b = _match(a, b)
-    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16 and a.dim() == 2 \
+    if native(a) and a.dtype == torch.bfloat16 and a.dim() == 2 \
             and keep < 1.0 and b.shape[-1] % 8 == 0:
         from . import gemm_mfma
         from .autotune import choose
@@ -115,7 +114,7 @@ def matmul_relu_mask(a, b, ta, tb, g, scale):
     ``relu_grad_c`` elementwise kernel."""
     a, b = _match(a, b)
     A2, B2 = _tr(a, ta), _tr(b, tb)
-    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype == torch.bfloat16 and A2.dim() == 2 \
+    if native(a) and a.dtype == torch.bfloat16 and A2.dim() == 2 \
             and g.dtype == torch.bfloat16 and g.is_contiguous():
         from . import gemm_mfma
         from .autotune import choose
@@ -146,60 +145,48 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     if cpu_native.active(a, b, bias) and a.dim() == 2 and b.dim() == 2 and activation in (None, 'relu', 'gelu'):
         y = cpu_native.gemm(_tr(a, ta), _tr(b, tb), bias)
         return cpu_native.unary(activation, y) if activation else y
-    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype in (torch.bfloat16, torch.float32):
-        from . import gemm_mfma
-        from .autotune import choose
-        key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
-        cands = {'hip': lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)}
-        if a.dtype == torch.bfloat16 and _big_ok(a, b, ta, tb):
-            cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
-        if a.dtype == torch.bfloat16 and _tr(b, tb).shape[-1] <= 64:
-            cands['hip64'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=2)
-        if a.dtype == torch.bfloat16 and _tr(a, ta).shape[-1] <= 2048:   # short K: the 4-blocks-per-CU tile
-            cands['hip_lo'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=3)
-        A2, B2 = _tr(a, ta), _tr(b, tb)
-        if a.dtype == torch.bfloat16 and B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
-            # 128x96 tile: N = 768 products fill the CUs in one round (512 tiles at M 8192)
-            cands['hip96'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=5)
-        if a.dtype == torch.bfloat16 and A2.shape[-1] >= 3 * 64:
-            # two-ahead K loop (operand DMA two K-tiles ahead of the MFMAs)
-            cands['hip_2a'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=6)
-            if B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
-                cands['hip96_2a'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=7)
-        if a.dtype == torch.bfloat16 and A2.dim() == 2 and bias is None and activation is None and \
-                A2.shape[1] >= 8192:
-            # long reductions over few output tiles (the MLM head's data gradient, K = vocab):
-            # split K over fp32 slabs + one reduce
-            tiles = -(-A2.shape[0] // 128) * -(-B2.shape[1] // 128)
-            for s_ in (2, 4):
-                if tiles * s_ <= 2048:
-                    cands['hip_sk%d' % s_] = (lambda s_=s_: gemm_mfma.gemm(A2, B2, splitk=s_))
-        if A2.dim() == 2 and B2.dim() == 2 and A2.shape[0] * B2.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
-            cands['hip_small'] = lambda: gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
-        # any shape: zero-padded aligned operands on the MFMA tile (last hand-written resort)
-        cands['hip_pad'] = lambda: gemm_mfma.padded(A2, B2, bias=bias, act=activation)
-        cands['vendor'] = lambda: _vendor(a, b, ta, tb, bias, activation)
-        if bias is not None:
-            # hipBLASLt's bias-epilogue kernel choice is sometimes far slower than the
-            # plain GEMM + a separate bias pass: measure both
-            cands['vendor_nobias'] = lambda: _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
-        c = choose(key, cands, _MFMA)
-        if c.startswith('hip'):
-            y = cands[c]()
-            if y is None:
-                y = gemm_mfma.padded(A2, B2, bias=bias, act=activation)
-            if y is not None:
-                return y
-            _fallback('matmul')
-        elif c == 'vendor_nobias':
-            return _vendor(a, b, ta, tb, bias, activation, fuse_bias=False)
-    return _vendor(a, b, ta, tb, bias, activation)
-
-
-def _fallback(name):
-    if _MFMA == 'hip':
-        from . import record_fallback
-        record_fallback(name)
+    if not a.is_cuda:
+        return _cpu_matmul(a, b, ta, tb, bias, activation)
+    if not (native(a) and a.dtype in (torch.bfloat16, torch.float32)):
+        no_kernel('matmul', '%s %s' % (a.dtype, tuple(a.shape)))
+    from . import gemm_mfma
+    from .autotune import choose
+    key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
+    cands = {'hip': lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)}
+    if a.dtype == torch.bfloat16 and _big_ok(a, b, ta, tb):
+        cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
+    if a.dtype == torch.bfloat16 and _tr(b, tb).shape[-1] <= 64:
+        cands['hip64'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=2)
+    if a.dtype == torch.bfloat16 and _tr(a, ta).shape[-1] <= 2048:   # short K: the 4-blocks-per-CU tile
+        cands['hip_lo'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=3)
+    A2, B2 = _tr(a, ta), _tr(b, tb)
+    if a.dtype == torch.bfloat16 and B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
+        # 128x96 tile: N = 768 products fill the CUs in one round (512 tiles at M 8192)
+        cands['hip96'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=5)
+    if a.dtype == torch.bfloat16 and A2.shape[-1] >= 3 * 64:
+        # two-ahead K loop (operand DMA two K-tiles ahead of the MFMAs)
+        cands['hip_2a'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=6)
+        if B2.shape[-1] % 96 == 0 and A2.shape[-2] >= 1024:
+            cands['hip96_2a'] = lambda: gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=7)
+    if a.dtype == torch.bfloat16 and A2.dim() == 2 and bias is None and activation is None and \
+            A2.shape[1] >= 8192:
+        # long reductions over few output tiles (the MLM head's data gradient, K = vocab):
+        # split K over fp32 slabs + one reduce
+        tiles = -(-A2.shape[0] // 128) * -(-B2.shape[1] // 128)
+        for s_ in (2, 4):
+            if tiles * s_ <= 2048:
+                cands['hip_sk%d' % s_] = (lambda s_=s_: gemm_mfma.gemm(A2, B2, splitk=s_))
+    if A2.dim() == 2 and B2.dim() == 2 and A2.shape[0] * B2.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
+        cands['hip_small'] = lambda: gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
+    # any shape: zero-padded aligned operands on the MFMA tile (last hand-written resort)
+    cands['hip_pad'] = lambda: gemm_mfma.padded(A2, B2, bias=bias, act=activation)
+    c = choose(key, cands)
+    y = cands[c]()
+    if y is None:
+        y = gemm_mfma.padded(A2, B2, bias=bias, act=activation)
+    if y is None:
+        no_kernel('matmul', '%s x %s' % (tuple(A2.shape), tuple(B2.shape)))
+    return y
 
 
 def _big_ok(a, b, ta, tb):
@@ -222,12 +209,11 @@ def _as_dtype(t, dt):
     return t.to(dt)
 
 
-def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
-    if a.is_cuda:
-        record_vendor('gemm')
+def _cpu_matmul(a, b, ta, tb, bias, activation):
+    """the CPU reference product (torch's CPU GEMM) with the elementwise epilogue"""
     A, B = _tr(a, ta), _tr(b, tb)
-    if fuse_bias and bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
-        y = torch.addmm(_as_dtype(bias, A.dtype), A, B)     # bias in the hipBLASLt epilogue
+    if bias is not None and A.dim() == 2 and B.dim() == 2 and bias.dim() == 1:
+        y = torch.addmm(_as_dtype(bias, A.dtype), A, B)
         bias = None
     else:
         y = torch.matmul(A, B)
@@ -244,70 +230,29 @@ def _vendor(a, b, ta, tb, bias, activation, fuse_bias=True):
 
 def bmm(a, b, ta=False, tb=False):
     a, b = _match(a, b)
-    if native(a) and _MFMA not in ('off', 'vendor') and a.dtype in (torch.bfloat16, torch.float32):
-        from . import gemm_mfma
-        from .autotune import choose
-        key = ('bmm', _sig(a), _sig(b), ta, tb)
-        hip = lambda: gemm_mfma.try_bmm(a, b, ta, tb)
+    if not a.is_cuda:
+        return torch.matmul(_tr(a, ta), _tr(b, tb))
+    if not (native(a) and a.dtype in (torch.bfloat16, torch.float32)):
+        no_kernel('bmm', '%s %s' % (a.dtype, tuple(a.shape)))
+    from . import gemm_mfma
+    from .autotune import choose
+    key = ('bmm', _sig(a), _sig(b), ta, tb)
+    hip = lambda: gemm_mfma.try_bmm(a, b, ta, tb)
 
-        def hip_pad():
-            A, B = _tr(a, ta), _tr(b, tb)
-            if A.dim() < 3 or A.shape[:-2] != B.shape[:-2]:
-                return None
-            lead = A.shape[:-2]
-            y = gemm_mfma.padded(A.reshape(-1, *A.shape[-2:]), B.reshape(-1, *B.shape[-2:]))
-            return None if y is None else y.view(*lead, *y.shape[-2:])
-        c = choose(key, {'hip': hip, 'hip_pad': hip_pad, 'vendor': lambda: torch.matmul(_tr(a, ta), _tr(b, tb))},
-                   _MFMA)
-        if c.startswith('hip'):
-            y = hip() if c == 'hip' else None
-            if y is None:
-                y = hip_pad()
-            if y is not None:
-                return y
-            _fallback('bmm')
-    if a.is_cuda:
-        record_vendor('bmm')
-    return torch.matmul(_tr(a, ta), _tr(b, tb))
-
-
-_MM_DTYPE_OK = [None]   # aten::mm.dtype (bf16 x bf16 -> fp32 in the hipBLASLt epilogue) usable?
-
-
-def _vendor_into(A, B, out):
-    """out (fp32) = A @ B on the library GEMM, writing fp32 directly when the
-    bf16->fp32 ``mm.dtype`` overload is available (no bf16 round trip + copy)."""
-    record_vendor('gemm')
-    if _MM_DTYPE_OK[0] is not False and A.is_cuda and A.dtype == torch.bfloat16 and A.dim() == 2 \
-            and out.is_contiguous():
-        try:
-            torch.mm(A, B, out_dtype=torch.float32, out=out)
-            _MM_DTYPE_OK[0] = True
-            return out
-        except (RuntimeError, TypeError):
-            _MM_DTYPE_OK[0] = False
-    out.copy_(torch.matmul(A, B))
-    return out
-
-
-def _vendor_splitk_into(A, B, out, s=4):
-    """out = A @ B with K split into ``s`` batched hipBLASLt GEMMs (fp32 partials)
-    and one reduction -- s x more workgroups for long-K / small-MN products."""
-    M, K = A.shape
-    N = B.shape[1]
-    if K % s or not A.is_cuda:
-        return None
-    kc = K // s
-    record_vendor('gemm')
-    # [M, K] -> [s, M, kc] and [K, N] -> [s, kc, N] as strided views (no copies)
-    Av = A.as_strided((s, M, kc), (kc * A.stride(1), A.stride(0), A.stride(1)))
-    Bv = B.as_strided((s, kc, N), (kc * B.stride(0), B.stride(0), B.stride(1)))
-    try:
-        part = torch.bmm(Av, Bv, out_dtype=torch.float32)
-    except (RuntimeError, TypeError):
-        return None
-    _splitk_sum(part, out)
-    return out
+    def hip_pad():
+        A, B = _tr(a, ta), _tr(b, tb)
+        if A.dim() < 3 or A.shape[:-2] != B.shape[:-2]:
+            return None
+        lead = A.shape[:-2]
+        y = gemm_mfma.padded(A.reshape(-1, *A.shape[-2:]), B.reshape(-1, *B.shape[-2:]))
+        return None if y is None else y.view(*lead, *y.shape[-2:])
+    c = choose(key, {'hip': hip, 'hip_pad': hip_pad})
+    y = hip() if c == 'hip' else None
+    if y is None:
+        y = hip_pad()
+    if y is None:
+        no_kernel('bmm', '%s x %s' % (tuple(a.shape), tuple(b.shape)))
+    return y
 
 
 def _splitk_sum(part, out):
@@ -327,20 +272,19 @@ def _splitk_sum(part, out):
 
 
 def matmul_into(a, b, ta, tb, out):
-    """out (fp32, e.g. a slot of the flat gradient buffer) = op(a) @ op(b):
-    the MFMA kernel writes fp32 directly; the library path computes in the
-    input dtype and converts once.  Returns ``out``."""
+    """out (fp32, e.g. a slot of the flat gradient buffer) = op(a) @ op(b): the MFMA
+    kernels write fp32 directly (split-K candidates for long reductions).  Returns ``out``."""
     a, b = _match(a, b)
-    if native(a) and a.dtype in (torch.bfloat16, torch.float32) and _MFMA not in ('off', 'vendor'):
+    if not a.is_cuda:
+        out.copy_(torch.matmul(_tr(a, ta), _tr(b, tb)))
+        return out
+    if native(a) and a.dtype in (torch.bfloat16, torch.float32):
         from . import gemm_mfma
         from .autotune import choose
 
         def hip():
             return gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), out=out)
-
-        def vendor():
-            return _vendor_into(_tr(a, ta), _tr(b, tb), out)
-        cands = {'hip': hip, 'vendor': vendor}
+        cands = {'hip': hip}
         # weight gradients: small M x N output, long K (= tokens): too few 128x128
         # tiles to fill 256 CUs -> split K over more workgroups (fp32 slab + reduce)
         A, B = _tr(a, ta), _tr(b, tb)
@@ -375,8 +319,6 @@ def matmul_into(a, b, ta, tb, out):
                 for s in (2, 3, 4, 5, 6, 7, 8):
                     if t256 * s <= 512 and K // s >= 1024:
                         cands['hip256_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=1))
-            if K >= 2048:
-                cands['vendor_sk'] = lambda: _vendor_splitk_into(A, B, out)
             if M * N <= gemm_mfma.SMALL_MAX_OUT:
                 cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, out=out)
             if N < 8 and M % 8 == 0 and K >= 4096 and out.dtype == torch.float32 and out.is_contiguous():
@@ -392,15 +334,12 @@ def matmul_into(a, b, ta, tb, out):
         if A.dim() == 2:
             cands['hip_pad'] = lambda: gemm_mfma.padded(A, B, out=out)
         key = ('gemm_into', _sig(a), _sig(b), ta, tb)
-        c = choose(key, cands, _MFMA)
-        if c != 'vendor' and cands[c]() is not None:
+        c = choose(key, cands)
+        if cands[c]() is not None:
             return out
-        if c.startswith('hip'):
-            if A.dim() == 2 and gemm_mfma.padded(A, B, out=out) is not None:
-                return out
-            _fallback('matmul_into')
-        return vendor()
-    return _vendor_into(_tr(a, ta), _tr(b, tb), out)
+        if A.dim() == 2 and gemm_mfma.padded(A, B, out=out) is not None:
+            return out
+    no_kernel('matmul_into', '%s %s x %s' % (a.dtype, tuple(a.shape), tuple(b.shape)))
 
 
 def _pad8_into(A, B, out, splitk):
@@ -419,32 +358,22 @@ def _pad8_into(A, B, out, splitk):
 
 
 def matmul_acc(a, b, ta, tb, acc, inplace=False):
-    """op(a) @ op(b) + acc with the addition in the GEMM epilogue (beta = 1):
-    the MFMA kernel reads ``acc`` as Cin, hipBLASLt runs it as addmm.
-    ``inplace``: acc is dead after this call, so the library GEMM accumulates
-    into it (C == D) instead of first copying it into a new output."""
+    """op(a) @ op(b) + acc with the addition in the GEMM epilogue (beta = 1: the MFMA
+    kernel reads ``acc`` as Cin).  ``inplace`` (acc dead after this call) is accepted for
+    the graph rewrite's interface; the epilogue writes a new output either way."""
     a, b = _match(a, b)
     A, B = _tr(a, ta), _tr(b, tb)
+    if not A.is_cuda:
+        if A.dim() == 2 and acc.dim() == 2 and acc.dtype == A.dtype:
+            return torch.addmm(acc, A, B)
+        y = torch.matmul(A, B)
+        return y + acc.to(y.dtype)
     if native(a) and a.dtype in (torch.bfloat16, torch.float32) and A.dim() == 2 and \
-            tuple(acc.shape) == (A.shape[0], B.shape[1]) and _MFMA not in ('off', 'vendor'):
+            tuple(acc.shape) == (A.shape[0], B.shape[1]):
         from . import gemm_mfma
-        from .autotune import choose, _decisions
-        # the MFMA epilogue reads an fp32 acc as it is; the library GEMM gets it cast
-        # (natively) to the operand dtype, once, only if it runs
-        cc = [acc if acc.dtype == a.dtype else None]
-
-        def c():
-            if cc[0] is None:
-                from .tensor import copy_into
-                cc[0] = copy_into(_NA.empty_like(acc, dtype=a.dtype), acc)
-            return cc[0]
+        from .autotune import choose
         key = ('gemm_acc', _sig(a), _sig(b), ta, tb)
-        inplace = inplace and acc.dtype == a.dtype and acc.is_contiguous()
-        # while the shape is timed, the in-place candidate accumulates into scratch
-        dst = [acc.clone() if inplace and key not in _decisions and _MFMA != 'hip' else acc]
-        hip = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0)
-        vendor = (lambda: dst[0].addmm_(A, B)) if inplace else (lambda: torch.addmm(c(), A, B))
-        cands = {'hip': hip, 'vendor': vendor}
+        cands = {'hip': lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0)}
         bf = a.dtype == torch.bfloat16       # fp32: the exact-fp32 kernel (``hip``) only
         if bf and A.shape[0] >= 256 and B.shape[1] >= 256:
             cands['hip256'] = lambda: gemm_mfma.gemm(A, B, cin=acc, beta=1.0, tile=1)
@@ -459,20 +388,10 @@ def matmul_acc(a, b, ta, tb, acc, inplace=False):
         if A.shape[0] * B.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
             cands['hip_small'] = lambda: gemm_mfma.gemm_small(A, B, cin=acc, beta=1.0)
         cands['hip_pad'] = lambda: gemm_mfma.padded(A, B, cin=acc, beta=1.0)
-        ch = choose(key, cands, _MFMA)
-        dst[0] = acc
-        if ch != 'vendor':
-            y = cands[ch]()
-            if y is None and ch.startswith('hip'):
-                y = gemm_mfma.padded(A, B, cin=acc, beta=1.0)
-            if y is not None:
-                return y
-            _fallback('matmul_acc')
-        record_vendor('gemm')
-        return vendor()
-    if A.is_cuda:
-        record_vendor('gemm')
-    if A.dim() == 2 and acc.dim() == 2 and acc.dtype == A.dtype:
-        return torch.addmm(acc, A, B)
-    y = torch.matmul(A, B)
-    return y + acc.to(y.dtype)
+        ch = choose(key, cands)
+        y = cands[ch]()
+        if y is None:
+            y = gemm_mfma.padded(A, B, cin=acc, beta=1.0)
+        if y is not None:
+            return y
+    no_kernel('matmul_acc', '%s %s x %s + %s' % (a.dtype, tuple(A.shape), tuple(B.shape), tuple(acc.shape)))

@@ -22,7 +22,6 @@ _ARGS = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, I64, I32, I32, I32, I64, I
 # 1 = 256x256 tile, 8 waves, phase-interleaved K loop (one block per CU)
 TILES = (0, 1, 2, 3, 5, 6, 7)   # 128x128, 256x256, 128x64, 128x128 single-stage (4 blocks / CU), 128x96,
 #                               and 128x128 / 128x96 with the two-ahead K loop (plain GEMMs)
-MODE = os.environ.get('HETU_GEMM', 'hip')
 
 
 def _operand(t, rows_dim_last, q=8):
@@ -360,16 +359,12 @@ def padded(a, b, out=None, bias=None, act=None, cin=None, beta=0.0):
 
 
 def try_gemm(a, b, ta, tb, bias=None, activation=None):
-    if MODE in ('vendor', 'off'):
-        return None
     A = a.transpose(-1, -2) if ta else a
     B = b.transpose(-1, -2) if tb else b
     return gemm(A, B, bias=bias, act=activation)
 
 
 def try_bmm(a, b, ta, tb):
-    if MODE in ('vendor', 'off'):
-        return None
     A = a.transpose(-1, -2) if ta else a
     B = b.transpose(-1, -2) if tb else b
     lead = A.shape[:-2]

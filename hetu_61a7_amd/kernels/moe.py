@@ -171,7 +171,7 @@ def dts_gate(logits, k, inv_tau, threshold, seed, noise=True):
     idx -1, value 0).  Returns (val [T, k] fp32, idx [T, k] int64, probs [T, E] fp32,
     hist [k + 1] int32: tokens by number of active choices)."""
     T, E = logits.shape
-    seed = int(seed) & ((1 << 63) - 1)
+    seed = int(seed) & ((1 << 64) - 1)
     if native(logits) and supported_float(logits) and E <= 512 and 1 <= k <= min(MAX_K, E):
         x = logits.contiguous()
         probs = _NA.empty((T, E), dtype=torch.float32, device=x.device)

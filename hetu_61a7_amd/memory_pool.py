@@ -168,7 +168,14 @@ def record_stream(t, stream):
     """``t.record_stream(stream)`` for whichever device allocator owns t: the BFC
     pool's own side-stream hold when it is the process allocator (torch's pluggable
     allocator interface has no record_stream hook), torch's caching allocator
-    otherwise.  ``stream``: a torch stream or a runtime.DeviceStream."""
+    otherwise.  ``stream``: a torch stream, a runtime.DeviceStream, or a raw handle (the
+    framework's current stream: ``runtime.current_stream()``)."""
+    if isinstance(stream, int):
+        if _torch_bfc:
+            lib().hetu_torch_record_stream(t.device.index or 0, t.untyped_storage().data_ptr(), stream)
+            return
+        from .runtime import _torch_view
+        stream = _torch_view(stream)[1]
     if _torch_bfc:
         h = stream.handle if hasattr(stream, 'handle') else stream.cuda_stream
         # the allocation's start: a view with an offset (t.data_ptr()) would miss the block

@@ -191,13 +191,28 @@ def wdl_criteo_bench(args, world, rank, local):
     emb = int(getattr(args, 'emb', 0) or 128)
     lr = float(getattr(args, 'lr', 0) or 0.01)
     bsp = int(getattr(args, 'bsp', -1))
-    dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100 + (0 if same else rank),
-                                             zipf=1.05 if dist == 'zipf' else 0)
-    if same and world > 1:
-        # the dataloader shards its data over the workers (contiguous 1/world slices): tile
-        # the block so that every worker's shard -- and so every batch -- is the same
-        import numpy as np
-        dense, sparse, labels = (np.concatenate([a] * world, 0) for a in (dense, sparse, labels))
+    import numpy as np
+    inter = int(getattr(args, 'interleave_workers', 0) or 0)
+    if same:
+        dense, sparse, labels = synthetic_criteo(B * nb, rows, seed=100, zipf=1.05 if dist == 'zipf' else 0)
+        if world > 1:
+            # the dataloader shards its data over the workers (contiguous 1/world slices): tile
+            # the block so that every worker's shard -- and so every batch -- is the same
+            dense, sparse, labels = (np.concatenate([a] * world, 0) for a in (dense, sparse, labels))
+    elif inter > 1:
+        # the single-worker reference of a ``inter``-worker job (rehearsal): the same global
+        # data, reordered so that this worker's batch j (of inter x the per-worker batch) is
+        # the concatenation of every worker's batch j
+        b0 = B // inter
+        dense, sparse, labels = synthetic_criteo(b0 * nb * inter, rows, seed=100, zipf=1.05 if dist == 'zipf' else 0)
+        S = b0 * nb
+        order = np.concatenate([np.arange(r * S + j * b0, r * S + (j + 1) * b0)
+                                for j in range(nb) for r in range(inter)])
+        dense, sparse, labels = dense[order], sparse[order], labels[order]
+    else:
+        # one global data set (identical on every worker) that the dataloader shards: every
+        # worker reads distinct ids, as the reference's run_hetu.py workers read their shard
+        dense, sparse, labels = synthetic_criteo(B * nb * world, rows, seed=100, zipf=1.05 if dist == 'zipf' else 0)
     # dataloader-fed inputs, as the reference's run_hetu.py: the executor knows the
     # next batch's sparse ids and prefetches their rows with this step's push
     xd = ht.dataloader_op([ht.Dataloader(dense, B, 'train')])

@@ -21,7 +21,7 @@ def moe_experts(model_dim, hidden_size, num_local_experts, rank=0, dropout_rate=
 
 
 def moe_top(x, y_, batch_size, num_tokens, model_dim, hidden_size, num_local_experts, world=1, rank=0,
-            top=2, gate='topk', dropout_rate=0.1, hash_ids=None):
+            top=2, gate='topk', dropout_rate=0.1, hash_ids=None, temperature=None):
     """Returns (loss, y).  ``x`` [B, T, d]; ``y_`` the NLL targets [B]."""
     E = num_local_experts * world
     ntok = batch_size * num_tokens
@@ -30,7 +30,8 @@ def moe_top(x, y_, batch_size, num_tokens, model_dim, hidden_size, num_local_exp
     if gate == 'topk':
         out = MoELayer(TopKGate(model_dim, ntok, E, k=top), experts, num_tokens, model_dim, world, top=top)(x)
     elif gate == 'dts':
-        out = MoELayer(DenseToSparseGate(model_dim, ntok, E, k=top), experts, num_tokens, model_dim, world)(x)
+        out = MoELayer(DenseToSparseGate(model_dim, ntok, E, k=top, temperature=temperature), experts, num_tokens,
+                       model_dim, world)(x)
     elif gate == 'ktop1':
         out = KTop1Layer(KTop1Gate(model_dim, ntok, E, k=top), experts, num_tokens, model_dim, world, k=top)(x)
     elif gate == 'sam':
@@ -64,10 +65,17 @@ def moe_top_bench(args, world, rank, local):
     is one token."""
     import torch
     import hetu_61a7_amd as H
-    B, T, d, ffn, nle = args.batch or 64, 1024, 2048, 2048, 2
+    B, T, d, ffn = args.batch or 64, 1024, 2048, 2048
+    nle = int(getattr(args, 'moe_local_experts', 2) or 2)
     gate = getattr(args, 'moe_gate', 'topk')
+    sched = getattr(args, 'dts_schedule', None)
+    temp = None
+    if gate == 'dts' and sched:
+        from ..layers.moe import DTSTemperature
+        tau0, decay, tau_min = (float(v) for v in sched.split(','))
+        temp = DTSTemperature(tau0=tau0, tau_min=tau_min, decay=decay)
     x, y_ = H.Variable(name='x', trainable=False), H.Variable(name='y_', trainable=False)
-    loss, y = moe_top(x, y_, B, T, d, ffn, nle, world, rank, top=2, gate=gate)
+    loss, y = moe_top(x, y_, B, T, d, ffn, nle, world, rank, top=2, gate=gate, temperature=temp)
     train = H.optim.SGDOptimizer(learning_rate=0.125).minimize(loss)
     kw = dict(mixed_precision=args.dtype, seed=1234)
     if world > 1:
@@ -89,7 +97,13 @@ def moe_top_bench(args, world, rank, local):
         from ..ops.moe_dts import DTSGatingOp
         g = [n for n in ex.subexecutor['train'].topo_order if isinstance(n, DTSGatingOp)][0]
 
+        timeline = []      # (step, budget, ms): per-step timing of the schedule run
+
         def step():
+            import time
+            if sched:
+                torch.cuda.synchronize()
+                t0, b0 = time.perf_counter(), g.budget
             if g.calls == 0 and g.budget > g.k_min:
                 # The budget only shrinks (dense to sparse), and each budget has its own expert
                 # capacity, i.e. its own GEMM shapes.  Run one (untimed, first warmup) step at
@@ -103,17 +117,39 @@ def moe_top_bench(args, world, rank, local):
                 g.budget = keep
                 g._pending, g._tau_at, g.history = [], {}, []
                 g.pretuned_budgets = list(range(g.k_min, keep))
+                if sched:
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()       # the pretuning steps are not the schedule's
             ex.run('train', feed_dict=feed)
+            if sched:
+                torch.cuda.synchronize()
+                timeline.append((g.calls, b0, (time.perf_counter() - t0) * 1e3))
 
         def extra():
             h = g.history[-1] if g.history else None
-            return {'dts': {'steps': g.calls, 'pretuned_budgets': getattr(g, 'pretuned_budgets', []),
-                            'tau': round(g.temperature.value, 4), 'budget_k': g.budget,
-                            'active_experts_per_token_last': round(h[3], 3) if h else None,
-                            'active_experts_first_to_last': [round(x[3], 3) for x in g.history[::max(1, len(g.history) // 8)]]}}
+            out = {'steps': g.calls, 'pretuned_budgets': getattr(g, 'pretuned_budgets', []),
+                   'tau': round(g.temperature.value, 4), 'budget_k': g.budget,
+                   'active_experts_per_token_last': round(h[3], 3) if h else None,
+                   'active_experts_first_to_last': [round(x[3], 3) for x in g.history[::max(1, len(g.history) // 8)]]}
+            if sched:
+                per, changes, prev = {}, [], None
+                for call, b, ms in timeline[1:]:          # step 1 carries the pretuning
+                    per.setdefault(b, []).append(ms)
+                for call, b, ms in timeline:
+                    if prev is not None and b != prev:
+                        changes.append({'step': call, 'from': prev, 'to': b})
+                    prev = b
+                out['schedule'] = sched
+                out['budget_changes'] = changes
+                out['ms_per_step_by_budget'] = {str(b): round(sum(v) / len(v), 3) for b, v in sorted(per.items())}
+                out['steps_by_budget'] = {str(b): len(v) for b, v in sorted(per.items())}
+                out['tokens_per_s_by_budget'] = {str(b): round(B * T * world * 1e3 / (sum(v) / len(v)), 1)
+                                                 for b, v in sorted(per.items())}
+            return {'dts': out}
         step.extra = extra
 
-    cfg = {'model': 'MoE top-2 (examples/moe/test_moe_top.py: d=2048, ffn=2048, 2 experts/GPU)',
+    cfg = {'model': 'MoE %s (examples/moe/test_moe_top.py: d=2048, ffn=2048, %d experts/GPU)'
+                    % ('top-2' if gate == 'topk' else gate, nle),
            'global_batch': B * world, 'seq_len': T, 'parallelism': 'ep%d (all-to-all) + dp%d gate' % (world, world),
            'gate': gate, 'experts': nle * world, 'optimizer': 'sgd', 'per_gpu_batch': B}
     return step, B * T * world, cfg, 'tokens/sec (whole node) MoE %s gate, expert all-to-all' % gate, None

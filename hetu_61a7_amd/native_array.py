@@ -18,6 +18,8 @@ import os
 
 import torch
 
+from . import _base
+
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5,
        torch.float64: 6, torch.int8: 7, torch.bool: 8}
 _DT_INV = {v: k for k, v in _DT.items()}
@@ -108,9 +110,9 @@ class Array(object):
         shape = tuple(int(s) for s in shape)
         h = ctypes.c_void_p()
         dev_type = 2 if device.type == 'cuda' else 1
-        dev_id = (device.index if device.index is not None else torch.cuda.current_device()) if dev_type == 2 else 0
+        dev_id = (device.index if device.index is not None else _base.cur_device()) if dev_type == 2 else 0
         if dev_type == 2 and stream is None:
-            stream = torch.cuda.current_stream(dev_id).cuda_stream
+            stream = _base.cur_stream()
         rc = lib().hetu_array_empty(len(shape), _i64(shape), _DT[dtype], dev_type, dev_id, int(bool(pinned)),
                                     stream, ctypes.byref(h))
         if rc == 2:
@@ -188,9 +190,8 @@ class Array(object):
         return self.view(shape, st)
 
     def copy_from(self, src, stream=None):
-        if stream is None and torch.cuda.is_available():
-            from .kernels import stream_ptr
-            stream = stream_ptr()
+        if stream is None and _base.gpu_available():
+            stream = _base.cur_stream()
         rc = lib().hetu_array_copy(self.h, src.h, stream)
         if rc == 4:     # general strides: the device copy kernel through torch views
             from .kernels.tensor import copy_into
@@ -229,7 +230,6 @@ def _cl_strides(shape):
     return (h * w * c, 1, w * c, c)
 
 
-_raw_stream = getattr(torch._C, '_cuda_getCurrentRawStream', None)
 _CL = torch.channels_last
 _CUDA = torch.device('cuda')
 
@@ -281,16 +281,15 @@ def empty(*size, dtype=torch.float32, device=None, memory_format=None, pinned=Fa
     if fm is False or not _AVAILABLE[0] or not _device_ok(device):
         kw = {'memory_format': memory_format} if memory_format is not None else {}
         t = torch.empty(shape, dtype=dtype, device=device, **kw)
-        return t.pin_memory() if pinned and not t.is_cuda and torch.cuda.is_available() else t
+        return t.pin_memory() if pinned and not t.is_cuda and _base.gpu_available() else t
     cl = memory_format is _CL and len(shape) == 4
     if cl:
         shape = (shape[0], shape[2], shape[3], shape[1])
     if device.type == 'cuda':
-        idx = device.index if device.index is not None else torch.cuda.current_device()
-        st = _raw_stream(idx) if _raw_stream is not None else torch.cuda.current_stream(idx).cuda_stream
-        cap = fm.empty(shape, _DT[dtype], 2, idx, 0, st)
+        idx = device.index if device.index is not None else _base.cur_device()
+        cap = fm.empty(shape, _DT[dtype], 2, idx, 0, _base.cur_stream())
     else:
-        cap = fm.empty(shape, _DT[dtype], 1, 0, 1 if (pinned and torch.cuda.is_available()) else 0, 0)
+        cap = fm.empty(shape, _DT[dtype], 1, 0, 1 if (pinned and _base.gpu_available()) else 0, 0)
     STATS['arrays'] += 1
     t = _from_dlpack(cap)
     return t.permute(0, 3, 1, 2) if cl else t

@@ -4,13 +4,14 @@ Parity target: reference ``python/hetu/ndarray.py`` (DLContext ``:10-57``,
 NDArray ``:140-402``, ``array``/``empty`` ``:405-444``, CSR ``:460-504``,
 IndexedSlices ``:507-618``).
 
-MI355X design: an ``NDArray`` is a thin handle over a ``torch.Tensor`` that lives
-either in HBM (``gpu(i)`` -> ``cuda:i`` on ROCm) or in host DRAM (``cpu``).  All
-device memory therefore comes from the stream-ordered caching allocator of the
-HIP runtime as used by torch-ROCm; host staging buffers for PS/cache traffic are
-pinned (``hipHostMalloc`` through ``pin_memory``) so H2D/D2H copies can run
-asynchronously on side streams.  Unlike the reference (fp32 only, float-encoded
-indices) arrays carry a real dtype: fp32 / bf16 / fp16 / int32 / int64.
+MI355X design: the memory behind an ``NDArray`` is a framework-owned native array
+(``csrc/runtime/array.cc``: refcounted strided header over a BFC-pool allocation -- HBM
+of ``gpu(i)``, pinned host DRAM for PS / cache staging, or plain host memory), allocated
+stream-ordered on the framework's current HIP stream (``runtime.use_stream``).  The
+Python-side handle is a non-owning ``torch.Tensor`` view of it (DLPack, zero copy), used
+as the op vocabulary of the CPU reference paths; torch owns neither the memory nor the
+streams.  Unlike the reference (fp32 only, float-encoded indices) arrays carry a real
+dtype: fp32 / bf16 / fp16 / int32 / int64.
 """
 from __future__ import annotations
 
@@ -210,16 +211,18 @@ class NDArray(object):
     def async_h2d(self, source, stream_handle=None, event_handle=None):
         """Copy a host array into this device array on ``stream_handle``."""
         src = source.tensor if isinstance(source, NDArray) else source
-        s = stream_handle.torch_stream if stream_handle is not None else None
-        with torch.cuda.stream(s) if s is not None else _null():
+        from .runtime import use_stream
+        with use_stream(stream_handle if stream_handle is not None and stream_handle.torch_stream is not None
+                        else None):
             self.tensor.copy_(src, non_blocking=True)
             if event_handle is not None:
                 event_handle.record(stream_handle)
 
     def async_d2h(self, source, stream_handle=None, event_handle=None):
         src = source.tensor if isinstance(source, NDArray) else source
-        s = stream_handle.torch_stream if stream_handle is not None else None
-        with torch.cuda.stream(s) if s is not None else _null():
+        from .runtime import use_stream
+        with use_stream(stream_handle if stream_handle is not None and stream_handle.torch_stream is not None
+                        else None):
             self.tensor.copy_(src, non_blocking=True)
             if event_handle is not None:
                 event_handle.record(stream_handle)

@@ -35,9 +35,9 @@ def _scores(q, k, mask, scale, causal):
 
 
 
-def _note_random():
-    from ..utils.hipgraph import note_host_random
-    note_host_random()
+def _next_seed(key, x):
+    from .nn import _next_seed as ns
+    return ns(key, x)
 
 
 class AttentionOp(Op):
@@ -61,11 +61,7 @@ class AttentionOp(Op):
         if q.is_cuda and KA.flash_ok(q, k, v):
             # one fused kernel: scores, mask, causal mask, online softmax, dropout, P.V
             keep = 1.0 if self.inference else self.keep_prob
-            seed = 0
-            if keep < 1.0:
-                self.seed += 1
-                _note_random()
-                seed = (self.id << 32) + self.seed
+            seed = _next_seed(self.id, q) if keep < 1.0 else 0
             o, lse = KA.flash_fwd(q, k, v, mask, self.causal, keep, seed, self._scale(q.shape[-1]))
             return AuxResult(o, ('flash', lse, keep, seed))
         if q.is_cuda:
@@ -76,9 +72,7 @@ class AttentionOp(Op):
         seed = None
         pd = p
         if self.keep_prob < 1.0 and not self.inference:
-            self.seed += 1
-            _note_random()
-            seed = (self.id << 32) + self.seed
+            seed = _next_seed(self.id, q)
             pd = KD.dropout(p, self.keep_prob, seed)
         o = KG.bmm(pd.to(v.dtype), v, False, False)
         return AuxResult(o, (p, seed))
@@ -159,11 +153,7 @@ class PackedAttentionOp(Op):
         qkv = input_vals[0]
         mask = input_vals[1].reshape(self.B, self.S) if self.has_mask else None
         keep = 1.0 if self.inference else self.keep_prob
-        seed = 0
-        if keep < 1.0:
-            self.seed += 1
-            _note_random()
-            seed = (self.id << 32) + self.seed
+        seed = _next_seed(self.id, qkv) if keep < 1.0 else 0
         out, saved = KA.attention_fwd(qkv.contiguous(), mask, self.B, self.S, self.NH, keep, seed, self.scale)
         return AuxResult(out, (saved, keep, seed))
 

@@ -921,7 +921,7 @@ class FullOp(Op):
         self.size, self.fill_value = tuple(size), fill_value
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        return torch.full(self.size, self.fill_value, dtype=torch.float32, device=self.device)
+        return _full(self.size, self.fill_value, self.device)
 
     def gradient(self, output_grad):
         return []
@@ -938,13 +938,22 @@ class FullLikeOp(Op):
         self.fill_value = fill_value
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        return torch.full(tuple(input_vals[0]), self.fill_value, dtype=torch.float32, device=self.device)
+        return _full(tuple(input_vals[0]), self.fill_value, self.device)
 
     def gradient(self, output_grad):
         return [None]
 
     def infer_shape(self, input_shapes):
         return input_shapes[0]
+
+
+def _full(size, value, device):
+    """fp32 constant tensor: the native fill kernel on the GPU (reference ArraySet.cu)"""
+    if device.type == 'cuda':
+        from .. import native_array as _NA
+        from ..kernels.tensor import fill_
+        return fill_(_NA.empty(tuple(size), dtype=torch.float32, device=device), float(value))
+    return torch.full(tuple(size), value, dtype=torch.float32, device=device)
 
 
 def full_op(size, fill_value, ctx=None):
@@ -961,7 +970,16 @@ class RandOp(Op):
         self.size = tuple(size)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        return torch.rand(self.size, device=self.device)
+        from ..kernels import rng
+        dev = self.device
+        seed = rng.next_seed(self.id, on_gpu=dev.type == 'cuda')
+        if dev.type == 'cuda':
+            # Philox uniform kernel (random.hip; reference Initializers.cu uniform fill)
+            from .. import native_array as _NA
+            return rng.uniform_(_NA.empty(self.size, dtype=torch.float32, device=dev), 0.0, 1.0, seed=seed)
+        g = torch.Generator()
+        g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
+        return torch.rand(self.size, generator=g)
 
     def gradient(self, output_grad):
         return []
@@ -980,6 +998,9 @@ class ArangeOp(Op):
         self.start, self.end, self.step = start, end, step
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        if self.device.type == 'cuda':
+            from ..kernels import rng
+            return rng.arange(self.infer_shape(None)[0], self.start, self.step, device=self.device)
         return torch.arange(self.start, self.end, self.step, dtype=torch.float32, device=self.device)
 
     def gradient(self, output_grad):

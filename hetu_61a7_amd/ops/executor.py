@@ -11,9 +11,10 @@ MI355X execution model:
 * Everything is issued asynchronously on the device's current HIP stream; no
   host-side ``event.sync()`` per dependency (reference ``executor.py:1034-1036``).
   Gradient buckets are all-reduced on RCCL's stream as soon as they complete.
-* ``use_hipgraph=True`` captures the whole steady-state step into a HIP graph
-  after a warm-up and replays it (launch-bound models: MLP, Wide&Deep), with
-  feeds copied into static device buffers.
+* hipGraph replay (default for single-GPU executors, ``use_hipgraph`` / HETU_HIPGRAPH):
+  the whole steady-state step is captured after a warm-up and replayed, with feeds
+  copied into static device buffers; random ops stay fresh through the device step
+  counter of ``kernels/rng.py``.
 * Mixed precision (``mixed_precision='bf16'``): fp32 master weights in the
   optimizer's flat buffer, bf16 compute copies refreshed by the fused update
   kernel, bf16 activations, fp32 BN/LN statistics and fp32 losses.
@@ -28,6 +29,9 @@ from typing import Dict, List, Optional
 
 import numpy as np
 import torch
+
+from .._base import gpu_available, set_device
+from ..kernels import rng as _RNG
 
 from .node import Op
 from .variable import PlaceholderOp
@@ -136,7 +140,7 @@ class HetuConfig(object):
     def __init__(self, eval_node_list, ctx=None, seed=None, comm_mode=None, use_sparse_pull=True,
                  cstable_policy=None, bsp=-1, prefetch=True, enable_lazy=False, cache_bound=100,
                  log_path=None, pipeline=None, dist_strategy=None, use_preduce=False, overlap=True,
-                 use_nccl_collectives=True, mixed_precision=None, bucket_mb=32, use_hipgraph=False,
+                 use_nccl_collectives=True, mixed_precision=None, bucket_mb=32, use_hipgraph=None,
                  timing=None, zero=0, deterministic=None, **kwargs):
         self.eval_node_list = eval_node_list
         if deterministic is not None:
@@ -147,6 +151,7 @@ class HetuConfig(object):
         if seed is None and os.environ.get('HETU_SEED') is None:
             # identical seeds on every data-parallel rank keep parameters identical
             self.seed = 1234
+        _RNG.set_base_seed(self.seed)
         self.comm_mode = comm_mode
         self.use_sparse_pull, self.cstable_policy, self.bsp = use_sparse_pull, cstable_policy, bsp
         self.prefetch, self.enable_lazy, self.cache_bound = prefetch, enable_lazy, cache_bound
@@ -155,7 +160,6 @@ class HetuConfig(object):
         self.mixed_precision = mixed_precision in ('bf16', 'bfloat16', True)
         self.bucket_mb = bucket_mb
         self.zero = int(zero)   # 1: ZeRO-1 sharded optimizer state (optimizer.py _make_zero_buckets)
-        self.use_hipgraph = use_hipgraph or os.environ.get('HETU_HIPGRAPH', '0') == '1'
         self.timing = timing
         self.h2d_ops, self.d2h_ops = {}, {}
         self.placeholder_to_arr_map: Dict[Op, torch.Tensor] = {}
@@ -174,7 +178,7 @@ class HetuConfig(object):
         if ctx is None:
             ctx = get_current_context()
         if ctx is None:
-            ctx = ndarray.gpu(local) if (torch.cuda.is_available() and world > 1) else ndarray.cpu(0)
+            ctx = ndarray.gpu(local) if (gpu_available() and world > 1) else ndarray.cpu(0)
         launch_mpi = launch_ps = False
         if isinstance(ctx, DeviceGroup) or isinstance(ctx, (list, tuple)):
             dg = ctx if isinstance(ctx, DeviceGroup) else DeviceGroup(list(ctx))
@@ -196,7 +200,7 @@ class HetuConfig(object):
         self.spmd = bool(PENDING_MESHES)
         if pipeline is not None or self.spmd:
             # one process per GPU: this rank's device is its own GPU ordinal
-            self.context = ndarray.gpu(local) if torch.cuda.is_available() else ndarray.cpu(0)
+            self.context = ndarray.gpu(local) if gpu_available() else ndarray.cpu(0)
             launch_mpi = launch_ps = False
         if comm_mode is None:
             if launch_mpi and launch_ps:
@@ -208,19 +212,19 @@ class HetuConfig(object):
             elif world > 1 and dist_strategy is None and pipeline is None:
                 comm_mode = None
         self.comm_mode = comm_mode
-        self.cpu_only = not torch.cuda.is_available()
-        if ndarray.is_gpu_ctx(self.context) and not torch.cuda.is_available():
+        self.cpu_only = not gpu_available()
+        if ndarray.is_gpu_ctx(self.context) and not gpu_available():
             # CPU-only process (tests / gloo rehearsal of the distributed path)
             self.context = ndarray.cpu(0)
             for n in find_topo_sort(eval_node_list):
                 if ndarray.is_gpu_ctx(n.ctx):
                     n.ctx = self.context
-        if self.context is not None and ndarray.is_gpu_ctx(self.context) and torch.cuda.is_available():
+        if self.context is not None and ndarray.is_gpu_ctx(self.context) and gpu_available():
             n_dev = torch.cuda.device_count()
             if self.context.device_id >= n_dev and os.environ.get('HETU_DIST_BACKEND') == 'gloo':
                 # multi-rank rehearsal on a box with fewer GPUs than ranks (gloo only)
                 self.context = ndarray.gpu(self.context.device_id % n_dev)
-            torch.cuda.set_device(self.context.device_id)
+            set_device(self.context.device_id)
 
         # ---- communicators ------------------------------------------------------------
         # HETU_FORCE_DP=1: run the data-parallel gradient path (buckets, async all-reduce on
@@ -241,10 +245,25 @@ class HetuConfig(object):
             self.ps_comm = psw.get_worker(self)
 
         # ---- streams (reference executor.py:319-334) -------------------------------------
-        self.comp_stream = Stream(self.context, torch_stream=torch.cuda.current_stream() if ndarray.is_gpu_ctx(self.context) and torch.cuda.is_available() else None)
+        if ndarray.is_gpu_ctx(self.context) and gpu_available():
+            from ..runtime import _torch_view, current_stream
+            self.comp_stream = Stream(self.context, torch_stream=_torch_view(current_stream())[1])
+        else:
+            self.comp_stream = Stream(self.context, torch_stream=None)
         self.h2d_stream = Stream(self.context)
         self.d2h_stream = Stream(self.context)
         self.nccl_stream = None
+
+        # ---- hipGraph replay: on by default for single-GPU executors --------
+        # ``use_hipgraph`` True / False forces it; None follows HETU_HIPGRAPH (1 / 0, default
+        # auto: one GPU process, no communicator, no PS, no pipeline).  Replay-unsafe steps
+        # (per-step host schedules, failed captures) fall back to eager execution.
+        env = os.environ.get('HETU_HIPGRAPH', 'auto')
+        if use_hipgraph is None:
+            use_hipgraph = env == '1' or (env == 'auto' and gpu_available() and ndarray.is_gpu_ctx(self.context)
+                                          and world == 1 and self.comm is None and self.ps_comm is None
+                                          and self.comm_mode is None and pipeline is None and not self.spmd)
+        self.use_hipgraph = bool(use_hipgraph)
 
         # ---- hooks (pre-order backward_hook, post-order forward_hook) ------------------------
         self.topo_sort_with_hook(eval_node_list)
@@ -584,6 +603,7 @@ class SubExecutor(object):
         cfg = self.config
         if vals is None:
             vals = self._prepare_inputs(feed_dict)
+        _RNG.new_step()            # per-step random state (kernels/rng.py: replay-safe seeds)
         aux = {}
         shapes = {}
         for op in self.opt_ops:

@@ -158,7 +158,7 @@ class MatMulActDropoutOp(Op):
         keep = 1.0 if self.inference else self.keep_prob
         if keep >= 1.0:
             return KG.matmul(a, b, activation=self.activation)
-        return KG.matmul_act_dropout(a, b, self.activation, keep, _next_seed())
+        return KG.matmul_act_dropout(a, b, self.activation, keep, _next_seed(self.id, a))
 
     def gradient(self, output_grad):
         if type(output_grad) is MatMulOp and len(output_grad.inputs) == 2 and _GMASK_EPI:

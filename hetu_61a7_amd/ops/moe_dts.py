@@ -113,7 +113,7 @@ class DTSGatingOp(Op):
             self._update_budget()
         tau = float(self.temperature.value)
         from .nn import _next_seed
-        seed = _next_seed() if train else 0
+        seed = _next_seed(self.id, x) if train else 0
         val, idx, probs, hist = KM.dts_gate(x, self.budget, 1.0 / tau, self.threshold, seed, noise=train)
         loc, counts, psum = KM.locations(idx, self.num_experts, probs, inactive=True)
         coef, l_aux = KM.aux_terms(counts, psum, T)
@@ -177,7 +177,7 @@ class GumbelSoftmaxOp(Op):
         E = x.shape[-1]
         tau = float(self.temperature.value)
         from .nn import _next_seed
-        seed = _next_seed() if not self.inference else 0
+        seed = _next_seed(self.id, x) if not self.inference else 0
         _, _, probs, _ = KM.dts_gate(x.reshape(-1, E), 1, 1.0 / tau, 0.0, seed, noise=not self.inference)
         return AuxResult(probs.reshape(x.shape), tau)
 

@@ -589,7 +589,7 @@ class DropoutAddLayerNormOp(Op):
         res = input_vals[1] if self.has_res else None
         g, b = input_vals[-2], input_vals[-1]
         keep = 1.0 if self.inference else self.keep_prob
-        seed = _next_seed() if keep < 1.0 else 0
+        seed = _next_seed(self.id, x) if keep < 1.0 else 0
         if res is not None and res.dtype != x.dtype:
             res = res.to(x.dtype)
         y, sm, mean, rstd = KLN.layer_norm_fused(x, res, g, b, self.eps, keep, seed)
@@ -710,14 +710,16 @@ def instance_normalization2d_gradient_op(out_gradient, in_node, forward_node, ct
 
 # ---------------------------------------------------------------------------
 # dropout (Philox, recompute mask in backward)
-_SEED_COUNTER = [int(time.time() * 1000) & 0xFFFFFFF]
+def _next_seed(key, x=None):
+    """host seed of op ``key``'s next draw (kernels/rng.py: fixed per op and call within a
+    step; the device step counter varies it between steps, replay-safe under hipGraph)"""
+    from ..kernels import rng
+    return rng.next_seed(key, on_gpu=x.is_cuda if x is not None else _base_gpu())
 
 
-def _next_seed():
-    from ..utils.hipgraph import note_host_random
-    note_host_random()
-    _SEED_COUNTER[0] = (_SEED_COUNTER[0] * 6364136223846793005 + 1442695040888963407) & ((1 << 62) - 1)
-    return _SEED_COUNTER[0]
+def _base_gpu():
+    from .._base import gpu_available
+    return gpu_available()
 
 
 class DropoutOp(Op):
@@ -730,7 +732,7 @@ class DropoutOp(Op):
         x = input_vals[0]
         if self.inference or self.keep_prob >= 1.0:
             return AuxResult(x, 0)
-        seed = _next_seed()
+        seed = _next_seed(self.id, x)
         return AuxResult(KD.dropout(x, self.keep_prob, seed), seed)
 
     def gradient(self, output_grad):
@@ -784,12 +786,10 @@ class Dropout2dOp(Op):
         x = input_vals[0]
         if self.inference:
             return AuxResult(x, None)
-        n, c = x.shape[:2]
-        seed = _next_seed()
-        g = torch.Generator(device=x.device)
-        g.manual_seed(seed & 0x7FFFFFFF)
-        mask = (torch.rand((n, c, 1, 1), generator=g, device=x.device) < self.keep_prob).to(x.dtype) / self.keep_prob
-        return AuxResult(x * mask, mask)
+        if self.keep_prob >= 1.0:
+            return AuxResult(x, None)
+        seed = _next_seed(self.id, x)
+        return AuxResult(_dropout2d(x, self.keep_prob, seed), seed)
 
     def gradient(self, output_grad):
         return [dropout2d_gradient_op(output_grad, self.keep_prob, self, ctx=self.raw_ctx)]
@@ -803,16 +803,39 @@ class Dropout2d_GradientOp(Op):
 
     def __init__(self, grad, keep_prob, forward_node, ctx=None):
         super().__init__(Dropout2d_GradientOp, [grad, forward_node], ctx)
+        self.keep_prob = keep_prob
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        g, mask = input_vals
-        return g if mask is None else g * mask
+        g, seed = input_vals
+        # the forward's plane mask regenerated from its seed (same planes, same 1 / keep)
+        return g if seed is None else _dropout2d(g, self.keep_prob, seed)
 
     def gradient(self, output_grad):
         raise NotImplementedError
 
     def infer_shape(self, input_shapes):
         return input_shapes[0]
+
+
+def _dropout2d(x, keep, seed):
+    """channel dropout: the HIP kernel on the GPU (random.hip, reference Dropout2d.cu:4),
+    the same Philox(seed, plane) draws on the CPU"""
+    if x.is_cuda:
+        from ..kernels import rng
+        return rng.dropout2d(x, keep, seed)
+    n, c = int(x.shape[0]), int(x.shape[1])
+    planes = torch.arange(n * c, dtype=torch.int64)
+    u = _philox_u01_host(seed, planes)
+    mask = (u < keep).to(x.dtype).reshape((n, c) + (1,) * (x.dim() - 2)) / keep
+    return x * mask
+
+
+def _philox_u01_host(seed, ctr):
+    """Philox4x32-10 word 0 of (seed, counter) as (0,1] floats -- the kernels' draw on the host"""
+    import numpy as np
+    from ..kernels.moe import philox4
+    x = philox4(int(seed), ctr.numpy().astype(np.uint64))[0]
+    return torch.from_numpy(((x >> np.uint64(8)).astype(np.float32) + 0.5) / 16777216.0)
 
 
 def dropout2d_op(node_in, keep_prob, ctx=None):

@@ -67,7 +67,8 @@ def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] 
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     if use_gpu:
-        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        from .._base import set_device
+        set_device(local % max(torch.cuda.device_count(), 1))
     if not dist.is_initialized():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         if 'MASTER_PORT' not in os.environ:
@@ -344,7 +345,7 @@ class Communicator(object):
             self.native.all_reduce(self._bar)
             from ..runtime import DeviceEvent
             from . import watchdog
-            ev = DeviceEvent().record(torch.cuda.current_stream())
+            ev = DeviceEvent().record(None)
             if watchdog.enabled():
                 watchdog.get().wait(ev, 'barrier', self)
             else:

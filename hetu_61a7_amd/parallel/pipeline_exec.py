@@ -404,6 +404,8 @@ class PipelineSubExecutor(object):
         cfg = self.config
         feed_dict = feed_dict or {}
         m = int(batch_num or 1)
+        from ..kernels import rng
+        rng.new_step()
         for n in find_topo_sort(self.eval_node_list):
             if hasattr(n, 'inference'):
                 n.inference = self.inference

@@ -25,6 +25,7 @@ from typing import Optional
 
 import torch
 from ..memory_pool import record_stream
+from .._base import cur_stream
 
 _LIB = None
 _NCCL_DT = {torch.float32: 7, torch.float16: 6, torch.bfloat16: 9, torch.int32: 2, torch.int64: 4,
@@ -105,7 +106,7 @@ class Work(object):
         self.event, self.post = event, post
 
     def wait(self):
-        self.event.wait(torch.cuda.current_stream())
+        self.event.wait(None)          # the framework's current stream
         if self.post is not None:
             self.post()
             self.post = None
@@ -195,10 +196,10 @@ class NativeComm(object):
         completion event goes to the watchdog (deadline ``HETU_COMM_TIMEOUT``)."""
         from ..runtime import DeviceEvent
         from ..utils.hipgraph import _CAPTURING
-        cur = torch.cuda.current_stream()
+        cur = cur_stream()
         wd = self._wd if not _CAPTURING[0] else None
         if not async_op:
-            fn(cur.cuda_stream)
+            fn(cur)
             if wd is not None:
                 wd.track(DeviceEvent().record(cur), self._what(what, tensors), self)
             if post is not None:
@@ -206,7 +207,7 @@ class NativeComm(object):
             return None
         s = self.stream
         self._dstream.wait_stream(cur)
-        fn(s.cuda_stream)
+        fn(self._dstream.handle)
         for t in tensors:
             if t is not None and t.is_cuda:
                 record_stream(t, s)
@@ -303,7 +304,7 @@ class NativeComm(object):
             # the workspaces are shared with async calls on the comm stream: a sync call on
             # the caller's stream must not overtake a bucket still using them
             from ..runtime import DeviceEvent
-            DeviceEvent().record(self.stream).wait(torch.cuda.current_stream())
+            DeviceEvent().record(self._dstream).wait(None)
         c = -(-n // (8 * P)) * 8
         send = self._ws(c * P, torch.bfloat16, 'send')
         recv = self._ws(c * P, torch.bfloat16, 'recv')

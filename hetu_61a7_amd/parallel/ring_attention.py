@@ -119,6 +119,14 @@ def _flash_ring_ok(qkv, NH):
             and qkv.stride(1) == 1 and qkv.stride(0) % 8 == 0 and qkv.data_ptr() % 16 == 0)
 
 
+def _cpu_only(qkv, NH):
+    """the per-block torch math below is the CPU reference (gloo rehearsals); on the GPU
+    every ring block runs on the flash kernels (bf16, head dim 32 / 64 / 128)"""
+    if qkv.is_cuda:
+        from ..kernels import no_kernel
+        no_kernel('ring_attention', '%s, head dim %d' % (qkv.dtype, qkv.shape[1] // 3 // NH))
+
+
 def _kv_heads(kv, B, S_l, NH, D):
     """[B*S_l, 2H] travelling block -> k, v as [B, NH, S_l, D] views"""
     x = kv.view(B, S_l, 2, NH, D)
@@ -214,6 +222,7 @@ def ring_attention_fwd(qkv, kmask, comm, B, S_l, NH, causal=False, scale=None):
     if _flash_ring_ok(qkv, NH):
         return _ring_fwd_flash(qkv, kmask, comm, B, S_l, NH, causal,
                                scale or 1.0 / math.sqrt(qkv.shape[1] // 3 // NH))
+    _cpu_only(qkv, NH)
     P, r = comm.nrank, comm.rank
     H = qkv.shape[1] // 3
     D = H // NH
@@ -246,6 +255,7 @@ def ring_attention_bwd(dout, qkv, kmask, out, lse, comm, B, S_l, NH, causal=Fals
     if _flash_ring_ok(qkv, NH):
         return _ring_bwd_flash(dout, qkv, kmask, out, lse, comm, B, S_l, NH, causal,
                                scale or 1.0 / math.sqrt(qkv.shape[1] // 3 // NH))
+    _cpu_only(qkv, NH)
     P, r = comm.nrank, comm.rank
     H = qkv.shape[1] // 3
     D = H // NH

@@ -102,10 +102,8 @@ class UlyssesAttentionOp(Op):
         keep = 1.0 if self.inference else self.keep_prob
         seed = 0
         if keep < 1.0:
-            self.seed += 1
-            from ..utils.hipgraph import note_host_random
-            note_host_random()
-            seed = (self.id << 32) + (self.seed << 8) + comm.rank    # distinct masks per head group
+            from ..ops.nn import _next_seed
+            seed = _next_seed(self.id, qkv) ^ ((comm.rank + 1) << 48)   # distinct masks per head group
         qkv_full = scatter_heads(qkv, comm, self.B, self.S_l, self.NH, D)
         out_full, saved = KA.attention_fwd(qkv_full, mask, self.B, S, self.NH // P, keep, seed, self.scale)
         out = gather_heads(out_full, comm, self.B, self.S_l, self.NH, D)

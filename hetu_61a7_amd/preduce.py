@@ -47,7 +47,8 @@ class PartialReduce(object):
         t = array.tensor if hasattr(array, 'tensor') else array
         comm = self._get_comm(partner)
         if stream is not None and hasattr(stream, 'torch_stream') and stream.torch_stream is not None:
-            with torch.cuda.stream(stream.torch_stream):
+            from .runtime import use_stream
+            with use_stream(stream):
                 comm.all_reduce(t, 'mean')
         else:
             comm.all_reduce(t, 'mean')

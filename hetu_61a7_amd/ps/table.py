@@ -19,6 +19,8 @@ import torch
 from . import worker as psw
 from .worker import PARAM_DENSE, PARAM_SPARSE, PARAM_CACHE
 from ..memory_pool import record_stream
+from ..runtime import DeviceEvent, use_stream
+from .._base import cur_stream, gpu_available
 from .. import native_array as _NA
 
 
@@ -72,15 +74,12 @@ def side_streams(device):
     s = _STREAMS.get(device)
     if s is None:
         from ..runtime import DeviceStream
+        from .._base import cur_device
         idx = torch.device(device).index
-        idx = torch.cuda.current_device() if idx is None else idx
-        owned = (DeviceStream(idx, persistent=True), DeviceStream(idx, persistent=True))   # framework-created HIP streams
-        s = _STREAMS[device] = (owned[0].torch, owned[1].torch)
-        _OWNED.append(owned)
+        idx = cur_device() if idx is None else idx
+        # framework-created HIP streams, used through runtime.use_stream
+        s = _STREAMS[device] = (DeviceStream(idx, persistent=True), DeviceStream(idx, persistent=True))
     return s
-
-
-_OWNED = []
 
 
 def host_ids(t):
@@ -94,12 +93,11 @@ def host_ids(t):
     if not t.is_cuda:
         return t.long().contiguous()
     _, d2h = side_streams(t.device)
-    d2h.wait_stream(torch.cuda.current_stream(t.device))
+    d2h.wait_stream(None)                      # after the producer on the current stream
     out = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-    with torch.cuda.stream(d2h):
+    with use_stream(d2h):
         out.copy_(t, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(d2h)
+        ev = DeviceEvent().record(d2h)
     record_stream(t, d2h)
     ev.synchronize()
     return out.long()
@@ -122,9 +120,8 @@ class _Staging(object):
         return self.buf[:n]
 
     def guard(self, stream=None):
-        if torch.cuda.is_available():
-            self.event = torch.cuda.Event()
-            self.event.record(stream)
+        if gpu_available():
+            self.event = DeviceEvent().record(stream)
 
 
 _LIVE = []
@@ -247,12 +244,11 @@ class PSTable(object):
         if self.device.type == 'cuda':
             # H2D on the copy stream; the compute stream waits for it by event only
             h2d, _ = side_streams(self.device)
-            cur = torch.cuda.current_stream(self.device)
-            with torch.cuda.stream(h2d):
+            with use_stream(h2d):
                 out = dest.to(self.device, non_blocking=True)
                 stage.guard(h2d)
-            cur.wait_stream(h2d)
-            record_stream(out, cur)
+            DeviceEvent().record(h2d).wait(None)     # the current stream waits for the copy
+            record_stream(out, cur_stream())
             if out_dtype is not None and out_dtype != out.dtype:
                 from ..kernels.elementwise import cast
                 out = cast(out, out_dtype)
@@ -271,8 +267,8 @@ class PSTable(object):
         if scaled.is_cuda:
             # D2H on the copy stream after the scaling kernel; the compute stream goes on
             _, d2h = side_streams(scaled.device)
-            d2h.wait_stream(torch.cuda.current_stream(scaled.device))
-            with torch.cuda.stream(d2h):
+            d2h.wait_stream(None)
+            with use_stream(d2h):
                 host.copy_(scaled, non_blocking=True)
                 self.grad_stage.guard(d2h)
             record_stream(scaled, d2h)
@@ -434,11 +430,10 @@ class PSDense(object):
         n = self.flat.numel
         scaled = _scaled_f32(g, -lr)
         _, d2h = side_streams(g.device)
-        d2h.wait_stream(torch.cuda.current_stream(g.device))
-        with torch.cuda.stream(d2h):
+        d2h.wait_stream(None)
+        with use_stream(d2h):
             self.push_buf[:n].copy_(scaled, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(d2h)
+            ev = DeviceEvent().record(d2h)
         record_stream(scaled, d2h)
         self.version += 1
         self._done.clear()
@@ -458,8 +453,8 @@ class PSDense(object):
         if self.overlap and g.is_cuda:
             return self._step_overlapped(g, lr)
         self.push_buf[:n].copy_(_scaled_f32(g, -lr), non_blocking=True)
-        if torch.cuda.is_available() and g.is_cuda:
-            torch.cuda.current_stream().synchronize()
+        if g.is_cuda:
+            DeviceEvent().record(None).synchronize()
         self.version += 1
         if self.bsp == 0:
             t = self.agent.Push(self.key, self.push_buf)

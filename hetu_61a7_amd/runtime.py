@@ -17,6 +17,7 @@ import os
 
 import torch
 
+from . import _base
 from ._base import _LIB_DIR
 
 _PATH = os.path.join(_LIB_DIR, 'libhetu_alloc.so')
@@ -62,13 +63,85 @@ def _check(r, what):
 
 
 def _handle(stream):
-    """raw hipStream_t of a DeviceStream, a torch stream, or None (torch's current stream)"""
+    """raw hipStream_t of a DeviceStream, a torch stream, an int handle, or None (the
+    framework's current stream of this thread)"""
     if stream is None:
-        from .kernels import stream_ptr
-        return stream_ptr()
+        return _base.cur_stream()
     if isinstance(stream, DeviceStream):
         return stream.handle
+    if isinstance(stream, int):
+        return stream
+    h = getattr(stream, 'handle', None)        # stream.Stream
+    if h is not None and not hasattr(stream, 'cuda_stream'):
+        return h
     return stream.cuda_stream
+
+
+_DEFAULT_TS = {}
+
+
+def _default_torch_stream(dev):
+    t = _DEFAULT_TS.get(dev)
+    if t is None:
+        t = _DEFAULT_TS[dev] = torch.cuda.default_stream(dev)
+    return t
+
+
+def _set_torch(ts):
+    torch._C._cuda_setStream(stream_id=ts.stream_id, device_index=ts.device_index, device_type=ts.device_type)
+
+
+def _torch_view(stream):
+    """(raw handle, torch stream object) of a stream argument"""
+    if isinstance(stream, DeviceStream):
+        return stream.handle, stream.torch
+    if isinstance(stream, int):
+        if stream == 0:
+            return 0, _default_torch_stream(_base.cur_device())
+        return stream, torch.cuda.ExternalStream(stream, device=torch.device('cuda', _base.cur_device()))
+    ts = getattr(stream, 'torch_stream', None)   # stream.Stream
+    if ts is not None or hasattr(stream, 'native'):
+        if ts is None:
+            return None, None
+        return ts.cuda_stream, ts
+    return stream.cuda_stream, stream
+
+
+class use_stream(object):
+    """``with use_stream(s):`` makes ``s`` this thread's current stream: framework kernel
+    launches, device allocations and collectives read it (``_base.cur_stream``, no torch
+    call), and torch's current stream follows it (``_cuda_setStream``) for the few torch
+    ops that still run.  ``s``: a DeviceStream, a torch stream, a ``stream.Stream``, a raw
+    handle, or None (no change).  The reference routes ops to streams per call
+    (``gpu_ops/executor.py`` stream_handle arguments); here the stream is ambient."""
+    __slots__ = ('h', 'ts', 'prev')
+
+    def __init__(self, stream):
+        self.h, self.ts = (None, None) if stream is None else _torch_view(stream)
+
+    def __enter__(self):
+        if self.h is None:
+            self.prev = None
+            return self
+        tls = _base._TLS
+        self.prev = (getattr(tls, 'h', 0), getattr(tls, 'ts', None))
+        tls.h, tls.ts = self.h, self.ts
+        _set_torch(self.ts)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is None:
+            return False
+        tls = _base._TLS
+        h, ts = self.prev
+        tls.h, tls.ts = h, ts
+        _set_torch(ts if ts is not None else _default_torch_stream(self.ts.device_index))
+        return False
+
+
+def current_stream():
+    """this thread's current stream as a raw handle (0: the null stream)"""
+    return _base.cur_stream()
 
 
 _PERSISTENT = []   # streams that live as long as the process (see DeviceStream(persistent=True))
@@ -82,7 +155,7 @@ class DeviceStream(object):
 
     def __init__(self, device=None, priority=0, persistent=False):
         self.persistent = persistent
-        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.device = _base.cur_device() if device is None else int(device)
         h = ctypes.c_void_p()
         _check(lib().hetu_stream_create(self.device, int(priority), ctypes.byref(h)), 'stream create')
         self.handle = h.value
@@ -130,7 +203,7 @@ class DeviceEvent(object):
     def __init__(self, device=None, timing=False, enable_timing=None):
         if enable_timing is not None:
             timing = enable_timing
-        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.device = _base.cur_device() if device is None else int(device)
         h = ctypes.c_void_p()
         _check(lib().hetu_event_create(self.device, int(bool(timing)), ctypes.byref(h)), 'event create')
         self.handle = h.value

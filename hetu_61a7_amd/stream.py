@@ -6,7 +6,8 @@ On MI355X a ``Stream`` is a HIP stream created by the framework's device runtime
 and comm work to separate streams and links them with ``hipStreamWaitEvent``
 (``Stream.wait_event``) instead of the reference's host-side ``event.sync()``.  Kernels
 launched inside ``with stream:`` run on it (``torch_stream`` is the non-owning
-``torch.cuda.ExternalStream`` view that makes it torch's current stream).
+``torch.cuda.ExternalStream`` view torch's current stream follows; framework launches
+read the thread's current stream from ``runtime.use_stream``, not from torch).
 """
 from __future__ import annotations
 
@@ -46,7 +47,8 @@ class Stream(object):
 
     def __enter__(self):
         if self.torch_stream is not None:
-            self._ctx = torch.cuda.stream(self.torch_stream)
+            from .runtime import use_stream
+            self._ctx = use_stream(self.native if self.native is not None else self.torch_stream)
             self._ctx.__enter__()
         return self
 

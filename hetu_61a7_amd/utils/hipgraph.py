@@ -13,27 +13,22 @@ import torch
 from .. import native_array as _NA
 
 _CAPTURING = [0]
-# per-call host random draws (dropout seeds, attention dropout counters): a captured graph
-# would replay the draws of the capture step forever -- the same dropout masks every step
+# host seed draws (kernels/rng.next_seed counts them): whether a captured step has random
+# ops (reported; replay-safe through the device step counter)
 _HOST_RANDOM = [0]
 
 
 def note_host_random():
-    """called by every op that draws a host-side seed for its kernel launch"""
+    """called by every host seed draw (kernels/rng.py)"""
     _HOST_RANDOM[0] += 1
 
 
 def capturing():
-    """True while a step is being captured into a graph (framework capture or torch's):
-    ops that keep per-call host state (e.g. double-buffered BatchNorm totals flipped by
-    a Python counter) must use a replay-safe form then -- a replay repeats the captured
-    call, not the host logic around it"""
-    if _CAPTURING[0]:
-        return True
-    try:
-        return bool(torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
-    except RuntimeError:
-        return False
+    """True while a step is being captured into a graph (every capture of a framework step
+    goes through GraphRunner, which counts it): ops that keep per-call host state (e.g.
+    double-buffered BatchNorm totals flipped by a Python counter) must use a replay-safe
+    form then -- a replay repeats the captured call, not the host logic around it"""
+    return _CAPTURING[0] > 0
 
 
 class GraphRunner(object):
@@ -113,36 +108,65 @@ class GraphRunner(object):
             base.update(self.static_in)
             torch.cuda.synchronize()
             from .. import memory_pool as MP
-            if MP.torch_bfc_enabled():
-                self._capture_native(sub, base)
-            else:
-                self.graph = torch.cuda.CUDAGraph()
-                _CAPTURING[0] += 1
-                try:
-                    with torch.cuda.graph(self.graph):
-                        self.static_vals = sub._run_eager(None, vals=dict(base))
-                finally:
-                    _CAPTURING[0] -= 1
-            for op in sub.opt_ops:
-                op.step -= 1  # the capture itself executes nothing
-            if _HOST_RANDOM[0] != r0:
-                # the step draws host seeds (dropout): a replay would repeat this step's masks
-                # forever -- keep running eagerly (correct randomness beats the launch savings)
+            steps0 = [op.step for op in sub.opt_ops]
+            try:
+                if MP.torch_bfc_enabled():
+                    self._capture_native(sub, base)
+                else:
+                    self._capture_torch(sub, base)
+            except Exception as e:          # noqa: BLE001 -- an op that cannot be captured
                 import sys
-                print('hipgraph: step draws host-side random seeds (dropout); running eagerly instead',
-                      file=sys.stderr)
+                print('hipgraph: capture failed (%s: %s); running this executor eagerly'
+                      % (type(e).__name__, e), file=sys.stderr)
                 self.close()
                 self.eager_only = True
+                torch.cuda.synchronize()
+                for op, st in zip(sub.opt_ops, steps0):
+                    op.step = st            # the failed capture executed nothing
                 base = {p: sub.config.compute_value(p) for p in sub.param_nodes}
                 base.update(new_in)
                 vals = sub._run_eager(None, vals=base)
                 return sub._collect(vals, convert)
+            for op in sub.opt_ops:
+                op.step -= 1  # the capture itself executes nothing
+            # (random ops are replay-safe: their host seeds are fixed per op and call, and
+            # the captured rng_advance kernel moves the device step counter every replay --
+            # kernels/rng.py)
+            self.random_ops = _HOST_RANDOM[0] != r0
         for n, v in new_in.items():
             self.static_in[n].copy_(v, non_blocking=True)
         self.graph.replay()
         for op in sub.opt_ops:
             op.step += 1
-        return sub._collect(self.static_vals, convert)
+        return self._collect_outputs(convert)
+
+    def _collect_outputs(self, convert):
+        """outputs of the replayed step: the graph's static buffers are overwritten by the
+        next replay, so unconverted device outputs are handed out as copies (native copy
+        kernel), never as aliases"""
+        if convert:
+            return self.sub._collect(self.static_vals, True)
+        from ..kernels.tensor import copy_into
+        vals = {}
+        for n in self.sub.eval_node_list:
+            v = self.static_vals.get(n)
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                v = copy_into(_NA.empty(tuple(v.shape), dtype=v.dtype, device=v.device), v)
+            vals[n] = v
+        return self.sub._collect(vals, False)
+
+    def _capture_torch(self, sub, base):
+        """capture through torch's graph API (torch's caching allocator owns device memory)"""
+        from .. import runtime as RT
+        self.graph = torch.cuda.CUDAGraph()
+        cap = self.capture_stream = RT.DeviceStream(persistent=True)
+        _CAPTURING[0] += 1
+        try:
+            # torch captures on `cap`; the framework's launches follow it there
+            with torch.cuda.graph(self.graph, stream=cap.torch), RT.use_stream(cap):
+                self.static_vals = sub._run_eager(None, vals=dict(base))
+        finally:
+            _CAPTURING[0] -= 1
 
     def _capture_native(self, sub, base):
         """Capture on a framework stream into a native HIP graph, every allocation of
@@ -152,10 +176,10 @@ class GraphRunner(object):
         from .. import runtime as RT
         dev = sub.config.device.index or 0
         cap = RT.DeviceStream(dev, persistent=True)
-        cap.wait_stream(torch.cuda.current_stream())
+        cap.wait_stream(None)                 # after the work queued on the current stream
         g = RT.Graph()
         self.pool = MP.capture_pool(dev, cap)
-        with self.pool, torch.cuda.stream(cap.torch):
+        with self.pool, RT.use_stream(cap):
             g.begin(cap)
             _CAPTURING[0] += 1
             try:
@@ -174,4 +198,5 @@ class _NativeReplay(object):
         self.g = g
 
     def replay(self):
-        self.g.replay(torch.cuda.current_stream())
+        from .._base import cur_stream
+        self.g.replay(cur_stream())

@@ -1,7 +1,7 @@
 """Per-shape timing of every ResNet-50 (bs 256, bf16, NHWC) convolution pass
-through the framework's autotuned dispatch: every candidate (hand-written
-implicit-GEMM MFMA kernel 'hip', MIOpen 'vendor', hipBLASLt 'blas*' for 1x1
-convolutions, channel-padded 'hip_pad' for the 3-channel stem) is timed, with
+through the framework's autotuned dispatch: every hand-written candidate (implicit-GEMM
+MFMA tiles 'hip*', halo-tile 'hip33', stem 'hip_stem', channel-padded 'hip_pad' for the
+3-channel stem) is timed (MIOpen references: scripts/vendor_ref.py), with
 achieved TFLOP/s and HBM GB/s (compulsory bytes) of the chosen one.
 
     python scripts/bench_conv_resnet.py [batch] [out.txt]

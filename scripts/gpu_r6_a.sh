@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 6: comm watchdog / IPC tests, then the driver bench line.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_rccl_gpu.py tests/test_ipc_allreduce_gpu.py > gpurun_out/r6a_tests.log 2>&1
+rc=$?; tail -25 gpurun_out/r6a_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/r6a_bench.json 2> gpurun_out/r6a_bench.err
+rc=$?; tail -2 gpurun_out/r6a_bench.json; exit $rc

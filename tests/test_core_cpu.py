@@ -168,7 +168,7 @@ def test_deterministic_flag_toggles_fixed_kernel_choice():
     K.set_deterministic(True)
     try:
         assert K.deterministic() and torch.are_deterministic_algorithms_enabled()
-        assert autotune.choose(('det-test',), {'hip': lambda: 1, 'vendor': lambda: 2}) == 'hip'
+        assert autotune.choose(('det-test',), {'hip': lambda: 1, 'hip_b': lambda: 2}) == 'hip'
     finally:
         K.set_deterministic(False)
     assert not K.deterministic() and not torch.are_deterministic_algorithms_enabled()

@@ -119,35 +119,52 @@ def test_hipgraph_recaptures_when_feed_shape_changes():
     np.testing.assert_allclose(out[0], out[1], rtol=1e-4, atol=1e-5)
 
 
-def test_hipgraph_declines_steps_that_draw_host_seeds():
-    """a step with dropout draws a host-side seed per call: a captured graph would replay the
-    capture step's masks forever, so the runner falls back to eager execution for good"""
+def test_hipgraph_replays_dropout_steps_like_eager():
+    """dropout seeds are replay-safe (kernels/rng.py: fixed host seed per op
+    and call, a device step counter advanced by a captured kernel), so a step with dropout
+    is captured and replayed -- and draws exactly the eager executor's masks every step"""
     rng = np.random.RandomState(5)
     X = rng.randn(64, 784).astype(np.float32)
     Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 64)]
-    x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
-    W = ht.init.xavier_normal((784, 10), name='Wd')
-    h = ht.dropout_op(x, 0.8)
-    loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(h, W), y_), [0])
-    train = ht.optim.SGDOptimizer(0.1).minimize(loss)
-    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, use_hipgraph=True)
-    ls = [float(np.asarray(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0])
-                .reshape(-1)[0]) for _ in range(8)]
-    runner = ex.subexecutor['train'].graph
-    assert getattr(runner, 'eager_only', False) and runner.graph is None
-    assert np.isfinite(ls).all()
-    assert len(set(round(v, 6) for v in ls[4:])) > 1      # fresh masks (and updates) every step
+    out, runners = [], []
+    from hetu_61a7_amd.ops import node as _node
+    for g in (False, True):
+        _node.G_NODE_ID = 0
+        x, y_ = ht.Variable(name='x'), ht.Variable(name='y_')
+        W = ht.init.xavier_normal((784, 10), name='Wd')
+        h = ht.dropout_op(x, 0.8)
+        loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(h, W), y_), [0])
+        train = ht.optim.SGDOptimizer(0.1).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, use_hipgraph=g)
+        out.append([float(np.asarray(ex.run('train', feed_dict={x: X, y_: Y}, convert_to_numpy_ret_vals=True)[0])
+                          .reshape(-1)[0]) for _ in range(8)])
+        runners.append(ex.subexecutor['train'].graph)
+    runner = runners[1]
+    assert runner.graph is not None and not getattr(runner, 'eager_only', False) and runner.random_ops
+    assert np.isfinite(out[1]).all()
+    assert len(set(round(v, 6) for v in out[1][4:])) > 1      # fresh masks (and updates) every replay
+    np.testing.assert_allclose(out[0], out[1], rtol=1e-5, atol=1e-6)
 
 
-def _tiny_bert_losses(ctx, mp=None, steps=4):
+def test_hipgraph_bert_with_dropout_matches_eager():
+    """a BERT pretraining step (hidden / attention dropout in the fused LayerNorm,
+    attention and GEMM-epilogue kernels) replays under hipGraph with the eager losses"""
+    out = []
+    for g in (False, True):
+        out.append(_tiny_bert_losses(ht.gpu(0), mp='bf16', steps=6, hipgraph=g, dropout=0.1))
+    assert np.isfinite(out[1]).all()
+    np.testing.assert_allclose(out[0], out[1], rtol=2e-3, atol=2e-3)
+
+
+def _tiny_bert_losses(ctx, mp=None, steps=4, hipgraph=False, dropout=0.0):
     from hetu_61a7_amd.models.bert import BertConfig, bert_pretrain_graph, synthetic_bert_batch
     from hetu_61a7_amd.ops import node as _node
     _node.G_NODE_ID = 0
     cfg = BertConfig(vocab_size=1200, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
                      intermediate_size=128, batch_size=4, seq_len=16, max_position_embeddings=16,
-                     hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+                     hidden_dropout_prob=dropout, attention_probs_dropout_prob=dropout)
     feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-3)
-    ex = ht.Executor({'train': [loss, train]}, ctx=ctx, seed=5, mixed_precision=mp)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ctx, seed=5, mixed_precision=mp, use_hipgraph=hipgraph)
     fd = {feeds[k]: v for k, v in synthetic_bert_batch(cfg, seed=1).items()}
     return [float(np.asarray(ex.run('train', feed_dict=fd, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0])
             for _ in range(steps)]

@@ -183,17 +183,18 @@ def _ps_server(env):
     server.server_finish(timeout_s=300)
 
 
-def _wdl_worker(rank, world, port, q, env, lr):
+def _wdl_worker(rank, world, port, q, env, lr, same=True, batch=16, inter=0):
     _env(rank, world, port)
     os.environ.update(env)
     os.environ.update(DMLC_ROLE='worker')
     import types
     from hetu_61a7_amd.models.ctr import wdl_criteo_bench
     # bench.py --model wdl (BASELINE config 3: --comm PS, dense parameters on the server too)
-    # in BSP mode with every worker on the same batches, no cache: 8 summed pushes of the
-    # same gradient == one worker at 8 x the lr
-    args = types.SimpleNamespace(batch=16, criteo_rows=3000, emb=8, lr=lr, bsp=0, cache=None, same_data=True,
-                                 rehearse_cpu=True, comm='PS', dtype='fp32', ids='zipf', steps=4, prefetch=False)
+    # in BSP mode, no cache.  same: every worker on the same batches -- 8 summed pushes of
+    # the same gradient == one worker at 8 x the lr; else each worker reads its own shard
+    args = types.SimpleNamespace(batch=batch, criteo_rows=3000, emb=8, lr=lr, bsp=0, cache=None, same_data=same,
+                                 interleave_workers=inter, rehearse_cpu=True, comm='PS', dtype='fp32', ids='zipf',
+                                 steps=4, prefetch=False)
     step, samples, cfg, metric, finish = wdl_criteo_bench(args, world, rank, rank)
     for _ in range(4):
         step()
@@ -201,7 +202,7 @@ def _wdl_worker(rank, world, port, q, env, lr):
     finish()
 
 
-def _run_wdl(world, lr):
+def _run_wdl(world, lr, *extra):
     import uuid
     env = dict(DMLC_PS_ROOT_PORT=str(20000 + uuid.uuid4().int % 30000), DMLC_NUM_WORKER=str(world),
                DMLC_NUM_SERVER='1', HETU_PS_HEAP_GB='0.2')
@@ -209,7 +210,7 @@ def _run_wdl(world, lr):
     srv = ctx.Process(target=_ps_server, args=(env,))
     srv.start()
     try:
-        return _run(_wdl_worker, world, env, lr)
+        return _run(_wdl_worker, world, env, lr, *extra)
     finally:
         srv.join(120)
         assert srv.exitcode == 0
@@ -224,6 +225,20 @@ def test_wdl_ps_eight_workers_bsp_matches_one_worker():
         assert len(losses) == 4
         np.testing.assert_allclose(losses, ref[1], rtol=2e-4, atol=1e-6, err_msg='worker %d' % rank)
     assert ref[1][-1] != ref[1][0]               # the updates moved the loss
+
+
+def test_wdl_ps_eight_workers_distinct_shards_bsp_matches_concatenated_batch():
+    """every worker reads its own shard of the global data (distinct id
+    streams into the server).  Under BSP the server applies the sum of the 8 pushes, which
+    equals one worker fed the concatenation of the 8 batches (mean loss) at 8 x the lr: the
+    mean of the workers' losses equals that worker's loss every step."""
+    ref = _run_wdl(1, 0.08, False, 16 * WORLD, WORLD)[0]
+    res = _run_wdl(WORLD, 0.01, False, 16, 0)
+    per = np.array([losses for _, losses, _, _ in sorted(res, key=lambda r: r[0])])
+    assert per.shape == (WORLD, 4)
+    assert np.ptp(per[:, 0]) > 1e-4               # the workers really read different batches
+    np.testing.assert_allclose(per.mean(0), ref[1], rtol=2e-4, atol=1e-6)
+    assert ref[1][-1] != ref[1][0]
 
 
 # ---- MoE EP8 equivalence: 8 ranks x 2 experts == one process holding all 16 experts -------

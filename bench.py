@@ -93,10 +93,15 @@ def _kernel_census(step):
     kernels.  Every rank runs it (collectives stay matched)."""
     import torch
     from torch.profiler import profile, ProfilerActivity
+    from hetu_61a7_amd.utils import hipgraph
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
-        step()
-        torch.cuda.synchronize()
+    hipgraph.FORCE_EAGER[0] += 1          # the kernels of the step, not one graph launch
+    try:
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            step()
+            torch.cuda.synchronize()
+    finally:
+        hipgraph.FORCE_EAGER[0] -= 1
     n = aten = vendor = 0
     names = {}
     for e in prof.events():
@@ -235,11 +240,23 @@ def main():
     # convolution calls and ops that left the native path, then a kernel census of one
     # more (untimed) step
     cfg['vendor_calls'] = dict(K.VENDOR_CALLS)
+    if not cpu_only and args.model == 'resnet50':
+        sub = ex.subexecutor['train']
+        cfg['hipgraph'] = bool(sub.config.use_hipgraph and getattr(sub, 'graph', None) is not None
+                               and getattr(sub.graph, 'graph', None) is not None)
     cfg['fallbacks'] = dict(K.FALLBACKS)
     if not cpu_only and os.environ.get('HETU_BENCH_CENSUS', '1') == '1':
         cfg.update(_kernel_census(step))
     if hasattr(step, 'extra'):
-        cfg.update(step.extra())
+        ex_ = step.extra()
+        cfg.update(ex_)
+        if world > 1 and args.model == 'wdl':
+            # every worker's HET cache hit rate and step breakdown (server wait = ps_wait)
+            import torch.distributed as dist
+            allx = [None] * world
+            dist.all_gather_object(allx, {'cache_hit_rate': ex_.get('cache_hit_rate'),
+                                          'step_breakdown_ms': ex_.get('step_breakdown_ms')})
+            cfg['per_worker'] = allx
     if rank == 0 and os.environ.get('HETU_BENCH_PYPROF'):
         # host-side profile of extra (untimed) steady-state steps: where the Python time goes
         import cProfile

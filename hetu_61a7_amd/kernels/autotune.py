@@ -35,7 +35,7 @@ def choose(key, candidates, mode=None):
     """the fastest candidate for ``key`` (cached); candidates return None for shapes they
     do not take.  (``mode`` is ignored: every candidate is a hand-written kernel.)"""
     d = _decisions.get(key)
-    if d is not None:
+    if d is not None and d in candidates:
         return d
     names = list(candidates)
     from . import deterministic

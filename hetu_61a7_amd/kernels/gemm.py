@@ -21,7 +21,7 @@ from . import native, no_kernel
 
 
 def _sig(t):
-    return (tuple(t.shape), tuple(t.stride()))
+    return (tuple(t.shape), tuple(t.stride()), t.dtype)
 
 
 def _match(a, b):

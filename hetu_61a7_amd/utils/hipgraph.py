@@ -16,6 +16,9 @@ _CAPTURING = [0]
 # host seed draws (kernels/rng.next_seed counts them): whether a captured step has random
 # ops (reported; replay-safe through the device step counter)
 _HOST_RANDOM = [0]
+# >0: GraphRunner runs the next steps eagerly (a profiler census of the kernels a replayed
+# step launches: a graph launch hides them from the activity trace)
+FORCE_EAGER = [0]
 
 
 def note_host_random():
@@ -83,7 +86,7 @@ class GraphRunner(object):
         sub = self.sub
         self.calls += 1
         self._update_dyn()
-        if self.calls <= self.warmup or getattr(self, 'eager_only', False):
+        if self.calls <= self.warmup or getattr(self, 'eager_only', False) or FORCE_EAGER[0]:
             vals = sub._run_eager(feed_dict)
             return sub._collect(vals, convert)
         new_in = self._inputs(feed_dict)

@@ -52,22 +52,24 @@ def _steps(run, k=5):
     return c.n
 
 
-def test_bert_step_asks_torch_nothing():
+@pytest.mark.parametrize('graph', [False, True])
+def test_bert_step_asks_torch_nothing(graph):
     from hetu_61a7_amd.models.bert import BertConfig, bert_pretrain_graph, synthetic_bert_batch
     cfg = BertConfig(vocab_size=1200, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
                      intermediate_size=128, batch_size=4, seq_len=16, max_position_embeddings=16,
                      hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.1)
     feeds, loss, train = bert_pretrain_graph(cfg, lr=1e-3)
-    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=5, mixed_precision='bf16')
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=5, mixed_precision='bf16', use_hipgraph=graph)
     fd = {feeds[k]: v for k, v in synthetic_bert_batch(cfg, seed=1).items()}
-    for _ in range(3):
+    for _ in range(6):           # past the warm-up and the hipGraph capture (steady state)
         ex.run('train', feed_dict=fd)
     torch.cuda.synchronize()
     n = _steps(lambda: ex.run('train', feed_dict=fd))
     assert n == {}, n
 
 
-def test_cnn_step_asks_torch_nothing():
+@pytest.mark.parametrize('graph', [False, True])
+def test_cnn_step_asks_torch_nothing(graph):
     rng = np.random.RandomState(0)
     X = rng.randn(8, 3, 32, 32).astype(np.float32)
     Y = np.eye(10, dtype=np.float32)[rng.randint(0, 10, 8)]
@@ -80,8 +82,8 @@ def test_cnn_step_asks_torch_nothing():
     w2 = ht.init.xavier_normal((16 * 16 * 16, 10), name='fc')
     loss = ht.reduce_mean_op(ht.softmaxcrossentropy_op(ht.matmul_op(h, w2), y_), [0])
     train = ht.optim.MomentumOptimizer(0.01, 0.9).minimize(loss)
-    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, mixed_precision='bf16')
-    for _ in range(3):
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, mixed_precision='bf16', use_hipgraph=graph)
+    for _ in range(6):
         ex.run('train', feed_dict={x: X, y_: Y})
     torch.cuda.synchronize()
     n = _steps(lambda: ex.run('train', feed_dict={x: X, y_: Y}))

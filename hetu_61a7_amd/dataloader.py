@@ -17,6 +17,10 @@ from .ops.node import Op
 from . import ndarray
 
 
+_TORCH_DT = {'<f4': torch.float32, '<i8': torch.int64, '<i4': torch.int32, '<f8': torch.float64,
+             '|u1': torch.uint8, '<f2': torch.float16, '|b1': torch.bool}
+
+
 class Dataloader(object):
     def __init__(self, raw_data, batch_size, name='default', func=None, drop_last=True,
                  shuffle=False, dtype=None):
@@ -69,6 +73,12 @@ class Dataloader(object):
         self.order = np.arange(self.samples_num)
         self._ring = []
         self._pending = None
+        # pinned staging ring: batch i goes through host slot i % 3 (no pin_memory call and
+        # no event creation per batch; a slot is rewritten two batches after its H2D copy
+        # was queued, and its event is waited for before that)
+        self._pin = [None] * 3
+        self._pev = [None] * 3
+        self._slot = 0
         if device is not None and device.type == 'cuda':
             from .runtime import DeviceStream
             self._dstream = DeviceStream(torch.device(device).index, persistent=True)   # framework-created prefetch stream
@@ -106,19 +116,39 @@ class Dataloader(object):
         return np.ascontiguousarray(b)
 
     def _stage(self, idx):
-        b = torch.from_numpy(self._host_batch(idx))
         if self.device is None or self.device.type != 'cuda':
-            return (b, None)
-        hb = b.pin_memory()
+            return (torch.from_numpy(self._host_batch(idx)), None)
         from .runtime import DeviceEvent, use_stream
+        from . import native_array as _NA
+        src = self._host_src(idx)
+        k = self._slot = (self._slot + 1) % 3
+        buf, ev = self._pin[k], self._pev[k]
+        n = int(np.prod(src.shape))
+        if buf is None or buf.numel() < n or buf.dtype != _TORCH_DT.get(src.dtype.str, buf.dtype):
+            buf = self._pin[k] = torch.from_numpy(np.ascontiguousarray(src)).reshape(-1).pin_memory()
+        if ev is None:
+            ev = self._pev[k] = DeviceEvent()
+        else:
+            ev.synchronize()                   # the last H2D copy out of this slot is done
+        hb = buf[:n].view(src.shape)
+        np.copyto(hb.numpy(), src)
         with use_stream(self._stream):
-            db = hb.to(self.device, non_blocking=True)
-            ev = DeviceEvent().record(self._stream)
+            db = _NA.empty(tuple(src.shape), dtype=hb.dtype, device=self.device)
+            db.copy_(hb, non_blocking=True)
+            ev.record(self._stream)
         # the host batch rides along: a consumer that needs the values on the host (PS /
         # HET-cache lookups of sparse ids, ``ps.table.host_ids``) reads it instead of a
         # device-to-host copy that would wait for the GPU
         db.hetu_host = hb
         return (db, ev, hb)
+
+    def _host_src(self, idx):
+        """the rows of batch idx as a numpy view when possible (copied once, into the
+        pinned slot), else a gathered copy"""
+        if self.shuffle or self.slices is not None:
+            return self._host_batch(idx)
+        st = idx * self.batch_size
+        return self.data[st:min(st + self.batch_size, self.samples_num)]
 
     def get_arr(self):
         """Current batch on the device; prefetches the next one."""

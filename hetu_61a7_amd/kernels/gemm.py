@@ -150,8 +150,15 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     if not (native(a) and a.dtype in (torch.bfloat16, torch.float32)):
         no_kernel('matmul', '%s %s' % (a.dtype, tuple(a.shape)))
     from . import gemm_mfma
-    from .autotune import choose
+    from .autotune import choose, _decisions
     key = ('gemm', _sig(a), _sig(b), ta, tb, bias is not None, activation)
+    d = _decisions.get(key)
+    if d is not None:
+        # decided shape: run the chosen tile directly (building every candidate closure
+        # per call cost more host time than the launch on the launch-bound models)
+        y = _run_decided(gemm_mfma, d, a, b, ta, tb, bias, activation)
+        if y is not None:
+            return y
     cands = {'hip': lambda: gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)}
     if a.dtype == torch.bfloat16 and _big_ok(a, b, ta, tb):
         cands['hip256'] = lambda: gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), bias=bias, act=activation, tile=1)
@@ -187,6 +194,26 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     if y is None:
         no_kernel('matmul', '%s x %s' % (tuple(A2.shape), tuple(B2.shape)))
     return y
+
+
+_TILE_OF = {'hip256': 1, 'hip64': 2, 'hip_lo': 3, 'hip96': 5, 'hip_2a': 6, 'hip96_2a': 7}
+
+
+def _run_decided(gemm_mfma, d, a, b, ta, tb, bias, activation):
+    """the autotuned candidate ``d`` of ``matmul`` (None: not a plain tile choice / refused)"""
+    if d == 'hip':
+        return gemm_mfma.try_gemm(a, b, ta, tb, bias, activation)
+    A2, B2 = _tr(a, ta), _tr(b, tb)
+    t = _TILE_OF.get(d)
+    if t is not None:
+        return gemm_mfma.gemm(A2, B2, bias=bias, act=activation, tile=t)
+    if d == 'hip_small':
+        return gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
+    if d == 'hip_pad':
+        return gemm_mfma.padded(A2, B2, bias=bias, act=activation)
+    if d.startswith('hip_sk'):
+        return gemm_mfma.gemm(A2, B2, splitk=int(d[6:]))
+    return None
 
 
 def _big_ok(a, b, ta, tb):
@@ -280,7 +307,11 @@ def matmul_into(a, b, ta, tb, out):
         return out
     if native(a) and a.dtype in (torch.bfloat16, torch.float32):
         from . import gemm_mfma
-        from .autotune import choose
+        from .autotune import choose, _decisions
+        key = ('gemm_into', _sig(a), _sig(b), ta, tb)
+        d = _decisions.get(key)
+        if d is not None and _into_decided(gemm_mfma, d, _tr(a, ta), _tr(b, tb), out) is not None:
+            return out
 
         def hip():
             return gemm_mfma.gemm(_tr(a, ta), _tr(b, tb), out=out)
@@ -333,13 +364,32 @@ def matmul_into(a, b, ta, tb, out):
                 cands['hip_lk'] = lambda: gemm_mfma.wgrad_longk(A.t(), B, out)
         if A.dim() == 2:
             cands['hip_pad'] = lambda: gemm_mfma.padded(A, B, out=out)
-        key = ('gemm_into', _sig(a), _sig(b), ta, tb)
         c = choose(key, cands)
         if cands[c]() is not None:
             return out
         if A.dim() == 2 and gemm_mfma.padded(A, B, out=out) is not None:
             return out
     no_kernel('matmul_into', '%s %s x %s' % (a.dtype, tuple(a.shape), tuple(b.shape)))
+
+
+_INTO_TILE = {'hip': 0, 'hip_lo': 3, 'hip_2a': 6, 'hip256': 1}
+
+
+def _into_decided(gemm_mfma, d, A, B, out):
+    """the autotuned candidate ``d`` of ``matmul_into`` (None: refused / unknown name)"""
+    if d == 'hip_small':
+        return gemm_mfma.gemm_small(A, B, out=out)
+    if d == 'hip_pad':
+        return gemm_mfma.padded(A, B, out=out)
+    if d == 'hip_lk':
+        return gemm_mfma.wgrad_longk(A.t(), B, out)
+    if d.startswith('hip_pad8_sk'):
+        return _pad8_into(A, B, out, int(d[11:]))
+    base, _, sk = d.partition('_sk') if '_sk' in d else (d, '', '')
+    t = _INTO_TILE.get(base)
+    if t is None:
+        return None
+    return gemm_mfma.gemm(A, B, out=out, splitk=int(sk) if sk else 1, tile=t)
 
 
 def _pad8_into(A, B, out, splitk):

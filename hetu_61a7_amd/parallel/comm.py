@@ -36,14 +36,25 @@ def _free_port():
 
 
 def backend_for_device(dev_is_gpu: bool) -> str:
-    """RCCL ('nccl' on ROCm) for GPU tensors, gloo for host tensors.
-    ``HETU_DIST_BACKEND=gloo`` forces gloo for GPU tensors too: several ranks
-    can then share one GPU (RCCL refuses duplicate devices), which rehearses
-    the multi-rank GPU path on a one-GPU box."""
+    """The torch.distributed backend: gloo -- the TCP-store rendezvous, host-tensor
+    collectives and host barriers only.  Every GPU collective runs on the in-house RCCL
+    communicator (``parallel/rccl.py``), so torch never creates an RCCL communicator of its
+    own (no ProcessGroupNCCL next to ours).  ``HETU_COMM=torch`` (A/B: torch's RCCL path)
+    selects 'nccl'.  ``HETU_DIST_BACKEND=gloo`` forces gloo for GPU tensors too, without
+    the native communicator: several ranks can then share one GPU (RCCL refuses duplicate
+    devices), which rehearses the multi-rank GPU path on a one-GPU box."""
     forced = os.environ.get('HETU_DIST_BACKEND')
     if forced:
         return forced
-    return 'nccl' if dev_is_gpu else 'gloo'
+    if dev_is_gpu and os.environ.get('HETU_COMM', 'native') == 'torch':
+        return 'nccl'
+    return 'gloo'
+
+
+def native_gpu_comm(use_gpu: bool) -> bool:
+    """GPU collectives on the in-house RCCL communicator (the default for GPU processes)"""
+    return bool(use_gpu) and os.environ.get('HETU_COMM', 'native') != 'torch' and \
+        not os.environ.get('HETU_DIST_BACKEND')
 
 
 def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] = None) -> 'Communicator':
@@ -76,9 +87,8 @@ def init_process_group(use_gpu: Optional[bool] = None, timeout_s: Optional[int] 
             os.environ['MASTER_PORT'] = str(_free_port()) if world == 1 else '29517'
         os.environ.setdefault('RANK', str(rank))
         os.environ.setdefault('WORLD_SIZE', str(world))
-        # no device_id: torch's ProcessGroupNCCL then creates its RCCL communicator lazily,
-        # on a first torch collective that the native path never issues -- one RCCL
-        # communicator per rank (the in-house one, parallel/rccl.py), not two
+        # gloo bootstrap (backend_for_device): one RCCL communicator per rank -- the
+        # in-house one (parallel/rccl.py), created from this group's TCP store
         kw = dict(backend=backend_for_device(use_gpu), rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
         dist.init_process_group(**kw)
@@ -158,7 +168,7 @@ class Communicator(object):
         # ncclCommInitRank per group; non-members take part in the split with no colour.
         # Partial-reduce groups (local_sync: only the members call) rendezvous by store.
         self.native = None
-        if use_gpu and os.environ.get('HETU_COMM', 'native') != 'torch' and dist.get_backend() == 'nccl':
+        if native_gpu_comm(use_gpu):
             from . import rccl
             if rccl.available():
                 w = _WORLD.native if _WORLD is not None else None

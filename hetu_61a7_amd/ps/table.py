@@ -19,7 +19,7 @@ import torch
 from . import worker as psw
 from .worker import PARAM_DENSE, PARAM_SPARSE, PARAM_CACHE
 from ..memory_pool import record_stream
-from ..runtime import DeviceEvent, use_stream
+from ..runtime import DeviceEvent, use_stream, stream_edge
 from .._base import cur_stream, gpu_available
 from .. import native_array as _NA
 
@@ -121,7 +121,11 @@ class _Staging(object):
 
     def guard(self, stream=None):
         if gpu_available():
-            self.event = DeviceEvent().record(stream)
+            # one event per buffer, re-recorded: its last use is what a reuse waits for
+            ev = getattr(self, '_ev', None)
+            if ev is None:
+                ev = self._ev = DeviceEvent()
+            self.event = ev.record(stream)
 
 
 _LIVE = []
@@ -247,7 +251,7 @@ class PSTable(object):
             with use_stream(h2d):
                 out = dest.to(self.device, non_blocking=True)
                 stage.guard(h2d)
-            DeviceEvent().record(h2d).wait(None)     # the current stream waits for the copy
+            stream_edge(h2d)                         # the current stream waits for the copy
             record_stream(out, cur_stream())
             if out_dtype is not None and out_dtype != out.dtype:
                 from ..kernels.elementwise import cast

@@ -139,6 +139,20 @@ class use_stream(object):
         return False
 
 
+_EDGE = {}
+
+
+def stream_edge(src, dst=None):
+    """``dst`` (default: the current stream) waits for the work queued so far on ``src``,
+    through a cached event per source stream (no event creation per edge)"""
+    h = _handle(src)
+    ev = _EDGE.get(h)
+    if ev is None:
+        ev = _EDGE[h] = DeviceEvent()
+    ev.record(src)
+    ev.wait(dst)
+
+
 def current_stream():
     """this thread's current stream as a raw handle (0: the null stream)"""
     return _base.cur_stream()
@@ -179,8 +193,12 @@ class DeviceStream(object):
         event.wait(self)
 
     def wait_stream(self, other):
-        """device-side: this stream waits for the work queued so far on ``other``"""
-        ev = DeviceEvent(self.device)
+        """device-side: this stream waits for the work queued so far on ``other`` (one
+        cached event per stream: hipStreamWaitEvent takes the event's state at the call,
+        so re-recording it for the next edge is safe)"""
+        ev = getattr(self, '_edge_ev', None)
+        if ev is None:
+            ev = self._edge_ev = DeviceEvent(self.device)
         ev.record(other)
         ev.wait(self)
 

@@ -34,6 +34,10 @@ def main():
     p.add_argument('--tiny', action='store_true', help='bert: the 2-layer config of tests/test_native_dispatch_gpu.py')
     a = p.parse_args()
     os.environ['HETU_PROFILE_OPS'] = '1'
+    if a.model == 'wdl':
+        # the PS server process, started before anything in this process touches the GPU
+        import bench
+        server = bench.start_ps_server(1, 0)
     import torch
     from torch.profiler import profile, ProfilerActivity
     sys.argv = ['bench.py', '--model', a.model, '--steps', '1', '--warmup', '0'] + \
@@ -86,6 +90,12 @@ def main():
     print('kernel classes in one step:', dict(counts))
     for name, fr in sorted(where.items(), key=lambda kv: -sum(kv[1].values())):
         print('%4d  %s' % (sum(fr.values()), name))
+        for f, c in fr.most_common(3):
+            print('        %4d  %s' % (c, f))
+    if a.model == 'wdl':
+        from hetu_61a7_amd.ps import worker
+        worker.worker_finish()
+        server.wait(timeout=60)
         for f, n in fr.most_common(4):
             print('        %3d  %s' % (n, f))
 

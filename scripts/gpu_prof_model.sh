@@ -5,7 +5,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
 M=${MODEL:-bert}
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$M -o run --output-format csv \
+cd /tmp && HETU_HIPGRAPH=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$M -o run --output-format csv \
   -- python3 $R/bench.py --model $M --steps 5 --warmup 3 > $R/gpurun_out/prof_$M.log 2>&1
 rc=$?; cd $R; tail -2 gpurun_out/prof_$M.log
 [ $rc -eq 0 ] || exit $rc

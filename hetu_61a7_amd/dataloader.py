@@ -10,6 +10,8 @@ here the executor calls it).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -79,6 +81,20 @@ class Dataloader(object):
         self._pin = [None] * 3
         self._pev = [None] * 3
         self._slot = 0
+        self._resident = None
+        budget = float(os.environ.get('HETU_DATALOADER_RESIDENT_MB', '4096')) * (1 << 20)
+        if device is not None and device.type == 'cuda' and not self.shuffle and self.slices is None \
+                and self.data.nbytes <= budget:
+            # HBM-resident split (288 GB per GPU): copied once, then every batch is a view of
+            # it -- no per-step staging copy, event or kernel; the host rows ride along for
+            # the PS / HET-cache lookups of sparse ids
+            host = torch.from_numpy(np.ascontiguousarray(self.data))
+            from . import native_array as _NA
+            dev = _NA.empty(tuple(host.shape), dtype=host.dtype, device=device)
+            dev.copy_(host.pin_memory() if host.numel() else host)
+            torch.cuda.synchronize(device)
+            self._resident = (dev, host)
+            self._resident_cast = {}
         if device is not None and device.type == 'cuda':
             from .runtime import DeviceStream
             self._dstream = DeviceStream(torch.device(device).index, persistent=True)   # framework-created prefetch stream
@@ -150,8 +166,28 @@ class Dataloader(object):
         st = idx * self.batch_size
         return self.data[st:min(st + self.batch_size, self.samples_num)]
 
+    def _resident_batch(self, idx):
+        dev, host = self._resident
+        st = idx * self.batch_size
+        en = min(st + self.batch_size, self.samples_num)
+        t = dev[st:en]
+        t.hetu_host = host[st:en]
+        return t
+
+    def resident_cast(self, dtype):
+        """the resident split in ``dtype`` (cast once: mixed-precision feeds)"""
+        c = self._resident_cast.get(dtype)
+        if c is None:
+            from .kernels.elementwise import cast
+            c = self._resident_cast[dtype] = cast(self._resident[0], dtype)
+        return c
+
     def get_arr(self):
         """Current batch on the device; prefetches the next one."""
+        if self._resident is not None:
+            t = self._resident_batch(self.batch_index)
+            self.batch_index = (self.batch_index + 1) % self.batch_num
+            return t
         if self._pending is None:
             self._pending = self._stage(self.batch_index)
         cur = self._pending
@@ -172,6 +208,9 @@ class Dataloader(object):
     def peek_next_arr(self):
         """The batch the next ``get_arr`` will return (already staged), without
         advancing; None before the first batch."""
+        if self.initialized and self._resident is not None:
+            st = self.batch_index * self.batch_size
+            return self._resident[1][st:min(st + self.batch_size, self.samples_num)]
         if not self.initialized or self._pending is None:
             return None
         return self._pending[2] if len(self._pending) > 2 else self._pending[0]
@@ -214,6 +253,16 @@ class DataloaderOp(Op):
             if getattr(self, 'host_feed', False):
                 dev = torch.device('cpu')
             dl.init_states(dev)
+        if getattr(dl, '_resident', None) is not None and config is not None and config.mixed_precision and \
+                dl._resident[0].dtype == torch.float32 and not self.keep_fp32:
+            # a resident fp32 split is cast once; batches are views of the bf16 copy
+            i = dl.batch_index
+            t = dl.get_arr()
+            c = dl.resident_cast(torch.bfloat16)
+            st = i * dl.batch_size
+            v = c[st:st + t.shape[0]]
+            v.hetu_host = t.hetu_host
+            return v
         t = dl.get_arr()
         if config is not None and config.mixed_precision and t.is_cuda and t.dtype == torch.float32 \
                 and not self.keep_fp32:

@@ -297,6 +297,69 @@ def attention_bwd_blocks(dout, q, k, v, out, lse, mask, B, S, NH, scale):
 
 
 # ---------------------------------------------------------------------------
+# BERT-length fast path for [B, NH, S, D] views (attention_op): when Q / K / V are head
+# views of token-major rows ([B, S, NH*64]-like storage: strides (S*ld, 64, ld, 1)), S is a
+# multiple of 32 up to 128 and the mask is a key mask, the one-workgroup-per-head kernels of
+# ``attention.hip`` take them as they are -- at S = 128 they run 1.3-1.5x faster than the
+# general flash tiles.  Same softmax statistics and Philox dropout layout as flash.
+
+def _rows_ld(t, S):
+    """row stride of a [B, NH, S, 64] head view of token-major rows, or None"""
+    B, NH, S_, D = t.shape
+    if D != 64 or S_ != S or t.stride(3) != 1 or t.stride(1) != 64:
+        return None
+    ld = t.stride(2)
+    if t.stride(0) != S * ld or ld % 8 or t.data_ptr() % 16:
+        return None
+    return ld
+
+
+def seqblock_ok(q, k, v, mask, causal):
+    if causal or not all(native(t) and t.dtype == torch.bfloat16 and t.dim() == 4 for t in (q, k, v)):
+        return False
+    B, NH, S, D = q.shape
+    if D != 64 or S % 32 or not 0 < S <= 128 or tuple(k.shape) != tuple(q.shape) or tuple(v.shape) != tuple(q.shape):
+        return False
+    if any(_rows_ld(t, S) is None for t in (q, k, v)):
+        return False
+    if mask is not None:
+        # a key mask only: [B, 1, 1, S] / [B, S] (broadcast over heads and queries)
+        if mask.numel() != B * S or (mask.dim() == 4 and (mask.shape[1] != 1 or mask.shape[2] != 1)):
+            return False
+    return True
+
+
+def seqblock_fwd(q, k, v, mask, keep, seed, scale):
+    """-> (o [B, NH, S, 64] view of token-major rows, lse [B*NH*S] fp32)"""
+    B, NH, S, D = q.shape
+    H = NH * D
+    o = _NA.empty((B, S, H), dtype=q.dtype, device=q.device)
+    lse = _NA.empty((B * NH * S,), dtype=torch.float32, device=q.device)
+    m = _mask_f32(mask.reshape(B, S)) if mask is not None else None
+    f = fn('hetu_attn_fwd', [P, P, P, I64, I64, I64, P, P, I64, P, I32, I32, I32, F32, F32, I64, P])
+    check(f(q.data_ptr(), k.data_ptr(), v.data_ptr(), _rows_ld(q, S), _rows_ld(k, S), _rows_ld(v, S),
+            m.data_ptr() if m is not None else None, o.data_ptr(), H, lse.data_ptr(), B, NH, S,
+            float(scale), float(keep), int(seed), stream_ptr()), 'attn_fwd')
+    return o.view(B, S, NH, D).permute(0, 2, 1, 3), lse
+
+
+def seqblock_bwd(do, q, k, v, o, lse, mask, keep, seed, scale):
+    """(dq, dk, dv) as [B, NH, S, 64] views of token-major rows"""
+    B, NH, S, D = q.shape
+    H = NH * D
+    if do.dtype != q.dtype or _rows_ld(do, S) is None:
+        from .tensor import copy_into
+        do = copy_into(_NA.empty((B, S, NH, D), dtype=q.dtype, device=q.device).permute(0, 2, 1, 3), do)
+    grads = [_NA.empty((B, S, H), dtype=q.dtype, device=q.device) for _ in range(3)]
+    m = _mask_f32(mask.reshape(B, S)) if mask is not None else None
+    _bwd_call(q.data_ptr(), k.data_ptr(), v.data_ptr(), _rows_ld(q, S), _rows_ld(k, S), _rows_ld(v, S),
+              m.data_ptr() if m is not None else None, o.data_ptr(), _rows_ld(o, S), lse.data_ptr(),
+              do.data_ptr(), _rows_ld(do, S), grads[0].data_ptr(), grads[1].data_ptr(), grads[2].data_ptr(),
+              H, H, H, B, NH, S, float(scale), float(keep), int(seed), device=q.device)
+    return tuple(g.view(B, S, NH, D).permute(0, 2, 1, 3) for g in grads)
+
+
+# ---------------------------------------------------------------------------
 # General fused attention (``flash_attn.hip``): any Sq / Sk, head dim 32 / 64 / 128,
 # causal, an additive mask broadcastable to [B, NH, Sq, Sk], dropout; Q / K / V / O
 # as strided [B, NH, S, D] views (head dim contiguous), so packed projections and

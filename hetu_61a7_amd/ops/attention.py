@@ -58,6 +58,12 @@ class AttentionOp(Op):
         q, k, v = input_vals[:3]
         mask = input_vals[3] if self.has_mask else None
         from ..kernels import attention as KA
+        if q.is_cuda and KA.seqblock_ok(q, k, v, mask, self.causal):
+            # BERT-length head views of token-major rows: the one-workgroup-per-head kernels
+            keep = 1.0 if self.inference else self.keep_prob
+            seed = _next_seed(self.id, q) if keep < 1.0 else 0
+            o, lse = KA.seqblock_fwd(q, k, v, mask, keep, seed, self._scale(q.shape[-1]))
+            return AuxResult(o, ('seqblock', lse, keep, seed))
         if q.is_cuda and KA.flash_ok(q, k, v):
             # one fused kernel: scores, mask, causal mask, online softmax, dropout, P.V
             keep = 1.0 if self.inference else self.keep_prob
@@ -100,6 +106,11 @@ class AttentionGradientOp(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         do, (o, aux), q, k, v = input_vals[:5]
         f = self.fwd
+        if aux[0] == 'seqblock':
+            from ..kernels import attention as KA
+            _, lse, keep, seed = aux
+            mask = input_vals[5] if f.has_mask else None
+            return KA.seqblock_bwd(do, q, k, v, o, lse, mask, keep, seed, f._scale(q.shape[-1]))
         if aux[0] == 'flash':
             from ..kernels import attention as KA
             _, lse, keep, seed = aux

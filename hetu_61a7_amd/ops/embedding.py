@@ -48,6 +48,21 @@ class EmbeddingLookUp(Op):
         return tuple(input_shapes[1]) + (input_shapes[0][-1],)
 
 
+def _rows(t, width):
+    """t as [-1] / [-1, width]: a view when the layout allows, else a native copy (a strided
+    gradient -- e.g. of a broadcast / transposed consumer -- would otherwise go through
+    torch's copy kernel on the device)"""
+    shape = (-1,) if width is None else (-1, width)
+    try:
+        return t.view(*shape)
+    except RuntimeError:
+        if t.is_cuda:
+            from .. import native_array as _NA
+            from ..kernels.tensor import copy_into
+            t = copy_into(_NA.empty(tuple(t.shape), dtype=t.dtype, device=t.device), t)
+        return t.reshape(*shape)
+
+
 class EmbeddingLookUp_Gradient(Op):
     shape_only_inputs = (2,)
 
@@ -58,7 +73,7 @@ class EmbeddingLookUp_Gradient(Op):
     def compute(self, input_vals, output_val=None, stream_handle=None):
         g, idx, shape = input_vals
         width = tuple(shape)[-1]
-        return ndarray.IndexedSlices(idx.reshape(-1), g.reshape(-1, width), tuple(shape))
+        return ndarray.IndexedSlices(_rows(idx, None), _rows(g, width), tuple(shape))
 
     def gradient(self, output_grad):
         raise NotImplementedError

@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('trace')
     ap.add_argument('--last', type=int, default=3)
-    ap.add_argument('--marker', default='opt_flat_k')
+    ap.add_argument('--marker', default='opt_flat')
     ap.add_argument('--top', type=int, default=40)
     ap.add_argument('--context', action='append', default=[],
                     help='category substring: list each launch of it in the last step with its neighbours')

@@ -143,3 +143,63 @@ def test_transformer_step_launches_no_torch_kernels():
                               ('at::native' in e.name or 'Cijk' in e.name or 'MIOpen' in e.name))
     assert not bad, dict(bad)
     assert not K.VENDOR_CALLS and not K.FALLBACKS, (K.VENDOR_CALLS, K.FALLBACKS)
+
+
+@pytest.mark.parametrize('S,keep,masked', [(128, 1.0, True), (128, 0.9, False), (64, 0.9, True), (96, 1.0, False)])
+def test_seqblock_fast_path_matches_flash(S, keep, masked):
+    """attention_op's BERT-length fast path (one workgroup per head, attention.hip) on head
+    views of token-major rows equals the flash kernels on the same views -- outputs,
+    gradients, and the dropout mask (same Philox layout) -- and is the path taken"""
+    B, NH, D = 3, 4, 64
+    g = torch.Generator(device='cuda').manual_seed(S)
+    rows = [torch.randn(B, S, NH * D, generator=g, device='cuda').bfloat16() for _ in range(4)]
+    q, k, v, do = (r.view(B, S, NH, D).permute(0, 2, 1, 3) for r in rows)
+    mask = None
+    if masked:
+        mask = torch.zeros(B, 1, 1, S, device='cuda')
+        mask[:, :, :, S - 17:] = -10000.0
+    assert KA.seqblock_ok(q, k, v, mask, False) and not KA.seqblock_ok(q, k, v, mask, True)
+    scale, seed = 1.0 / math.sqrt(D), 987654321
+    o1, l1 = KA.seqblock_fwd(q, k, v, mask, keep, seed, scale)
+    g1 = KA.seqblock_bwd(do, q, k, v, o1, l1, mask, keep, seed, scale)
+    o2, l2 = KA.flash_fwd(q, k, v, mask, False, keep, seed, scale)
+    g2 = KA.flash_bwd(do, q, k, v, o2, l2, mask, False, keep, seed, scale)
+    torch.cuda.synchronize()
+    assert _rel(o1, o2) < 1e-2
+    assert _rel(l1.reshape(-1), l2.reshape(-1)) < 1e-4
+    for a, b in zip(g1, g2):
+        assert _rel(a, b) < 2e-2
+
+
+def test_attention_op_takes_seqblock_path(monkeypatch):
+    import hetu_61a7_amd as ht
+    calls = {'fwd': 0, 'bwd': 0}
+    f0, b0 = KA.seqblock_fwd, KA.seqblock_bwd
+
+    def fwd(*a, **k):
+        calls['fwd'] += 1
+        return f0(*a, **k)
+
+    def bwd(*a, **k):
+        calls['bwd'] += 1
+        return b0(*a, **k)
+    monkeypatch.setattr(KA, 'seqblock_fwd', fwd)
+    monkeypatch.setattr(KA, 'seqblock_bwd', bwd)
+    B, NH, S, D = 2, 4, 128, 64
+    rng = np.random.RandomState(0)
+    X = rng.randn(B, S, NH * D).astype(np.float32)
+    x = ht.Variable(name='x')
+    wq, wk, wv = (ht.init.xavier_normal((NH * D, NH * D), name=n) for n in ('wq', 'wk', 'wv'))
+
+    def heads(t):
+        return ht.transpose_op(ht.array_reshape_op(t, (B, S, NH, D)), (0, 2, 1, 3))
+    x2 = ht.array_reshape_op(x, (B * S, NH * D))
+    q, k, v = (heads(ht.matmul_op(x2, w)) for w in (wq, wk, wv))
+    att = ht.attention_op(q, k, v, dropout=0.1)
+    loss = ht.reduce_mean_op(ht.mul_op(att, att), [0, 1, 2, 3])
+    train = ht.optim.SGDOptimizer(0.1).minimize(loss)
+    ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=1, mixed_precision='bf16', use_hipgraph=False)
+    ls = [float(np.asarray(ex.run('train', feed_dict={x: X}, convert_to_numpy_ret_vals=True)[0]).reshape(-1)[0])
+          for _ in range(3)]
+    assert np.isfinite(ls).all()
+    assert calls == {'fwd': 3, 'bwd': 3}, calls

@@ -284,9 +284,18 @@ def main():
         if args.comm_trace and args.model == 'resnet50':
             tr = [op.comm_trace() for op in ex.optimizer_ops('train')] if hasattr(ex, 'optimizer_ops') else []
             cfg['comm_trace_last_step'] = tr[0] if tr else []
+    # devices actually used: ranks of a gloo rehearsal share the node's GPUs (8 WDL workers on
+    # one MI355X are 8 workers, 1 GPU)
+    # (the CPU rehearsal of the driver's N-rank line keeps N)
+    n_dev = 0 if args.model == 'logreg' else world
+    if not cpu_only and os.environ.get('HETU_DIST_BACKEND') == 'gloo':
+        n_dev = min(world, torch.cuda.device_count())
+    if n_dev != world and args.model != 'logreg':
+        cfg = dict(cfg)
+        cfg['workers'] = world
     if rank == 0:
         out = {'metric': metric, 'value': round(value, 2), 'unit': 'tokens/s' if args.model == 'moe' else 'samples/s',
-               'n_gpus': 0 if args.model == 'logreg' else world,
+               'n_gpus': n_dev,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
                'dtype': 'fp32' if cpu_only else args.dtype, 'data': 'synthetic (random-init weights)', 'config': cfg}
@@ -294,6 +303,9 @@ def main():
     if rank == 0 and os.environ.get('HETU_AUTOTUNE_DUMP'):
         from hetu_61a7_amd.kernels import autotune
         autotune.dump(os.environ['HETU_AUTOTUNE_DUMP'])
+    if rank == 0 and os.environ.get('HETU_AUTOTUNE_SAVE'):
+        from hetu_61a7_amd.kernels import autotune
+        autotune.save(os.environ['HETU_AUTOTUNE_SAVE'])
     if finish is not None:
         finish()
     if server is not None:

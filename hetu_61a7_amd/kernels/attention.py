@@ -23,18 +23,34 @@ from . import fn, native, stream_ptr, check, record_native, P, I64, I32, F32
 
 
 
-# HETU_ATTN_BWD_SPLIT (default 1; BERT-base 4715/4715 vs 4691/4663 samples/s fused): the backward as two launches with P_drop^T / dS^T through a global
-# workspace (small LDS, several workgroups per CU) instead of one ~122 KiB-LDS workgroup
-_BWD_SPLIT = os.environ.get('HETU_ATTN_BWD_SPLIT', '1') == '1'
+# HETU_ATTN_BWD: the fixed-length backward's form.
+#   split -- two launches, P_drop^T / dS^T through a 2 x S^2 bf16 global workspace per head
+#            (small LDS, several workgroups per CU; BERT-base 4715/4715 vs 4691/4663
+#            samples/s against fused in round 4);
+#   fused -- one 4-wave launch with the images in ~122 KiB of LDS (one wave per SIMD);
+#   w8    -- one 8-wave launch, same images plus a 32 KiB dQ exchange (two waves per SIMD).
+# (HETU_ATTN_BWD_SPLIT=0 / 1 is the older spelling of fused / split.)
+# Default w8: 53.9 us vs split 65.1 / fused 57.6 at BERT-base's shape with dropout 0.1
+# (profiles/attention_kernels_r6.txt).
+_BWD_MODE = os.environ.get('HETU_ATTN_BWD') or {'0': 'fused', '1': 'split'}.get(
+    os.environ.get('HETU_ATTN_BWD_SPLIT', ''), 'w8')
+_BWD_SPLIT = _BWD_MODE == 'split'
 
 
 def _bwd_call(*args, device=None):
-    """hetu_attn_bwd2 (fused, or split with a workspace); args as hetu_attn_bwd's up to seed"""
+    """hetu_attn_bwd2 (fused, or split with a workspace) / hetu_attn_bwd8; args as
+    hetu_attn_bwd's up to seed"""
+    if _BWD_MODE == 'w8':
+        f = fn('hetu_attn_bwd8', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
+                                  I32, I32, I32, F32, F32, I64, P])
+        check(f(*args, stream_ptr()), 'attn_bwd8')
+        return
     B, NH, S = args[18], args[19], args[20]
     ws = _NA.empty(2 * B * NH * S * S, dtype=torch.bfloat16, device=device) if _BWD_SPLIT else None
     f = fn('hetu_attn_bwd2', [P, P, P, I64, I64, I64, P, P, I64, P, P, I64, P, P, P, I64, I64, I64,
                               I32, I32, I32, F32, F32, I64, P, P])
     check(f(*args, ws.data_ptr() if ws is not None else None, stream_ptr()), 'attn_bwd')
+
 
 def fused_ok(qkv, S, D, need_bwd=True):
     return (native(qkv) and qkv.dtype == torch.bfloat16 and D == 64 and S % 32 == 0 and 0 < S <= (128 if need_bwd else 256)

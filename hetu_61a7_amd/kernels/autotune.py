@@ -6,6 +6,12 @@ best round per candidate) and caches the fastest.
 Used to pick, per convolution / GEMM shape, among the hand-written kernels (tile
 shapes, split-K depths, K-loop forms).  Never measures inside a hipGraph capture
 (returns the first candidate there; warm-up steps run eagerly before capture).
+
+Decisions persist across processes: ``save(path)`` writes them as JSON (keys by ``repr``),
+and ``HETU_AUTOTUNE_CACHE=path`` (or ``load(path)``) makes a later process take them
+without measuring -- a production job skips its tuning steps, and a profiling run whose
+serialised dispatches would time candidates differently (``rocprofv3 --pmc``) runs the
+kernels the plain run chose.
 """
 from __future__ import annotations
 
@@ -17,6 +23,7 @@ from ..runtime import DeviceEvent
 
 _decisions = {}
 _times = {}
+_loaded = {}     # repr(key) -> candidate name, from a saved cache
 REPS = int(os.environ.get('HETU_AUTOTUNE_REPS', '5'))
 ROUNDS = int(os.environ.get('HETU_AUTOTUNE_ROUNDS', '3'))
 
@@ -37,6 +44,11 @@ def choose(key, candidates, mode=None):
     d = _decisions.get(key)
     if d is not None and d in candidates:
         return d
+    if _loaded:
+        d = _loaded.get(repr(key))
+        if d is not None and d in candidates:
+            _decisions[key] = d
+            return d
     names = list(candidates)
     from . import deterministic
     if deterministic():
@@ -90,3 +102,22 @@ def dump(path):
     with open(path, 'w') as f:
         for k, (c, t) in report().items():
             f.write('%s -> %s  %s\n' % (k, c, ' '.join('%s=%.1fus' % (n, v * 1e3) for n, v in t.items())))
+
+
+def save(path):
+    """the decisions so far as JSON {repr(key): candidate}"""
+    import json
+    with open(path, 'w') as f:
+        json.dump({repr(k): v for k, v in _decisions.items()}, f, indent=0, sort_keys=True)
+
+
+def load(path):
+    """take the decisions of a saved cache (measured choices of this process win)"""
+    import json
+    with open(path) as f:
+        _loaded.update(json.load(f))
+    return len(_loaded)
+
+
+if os.environ.get('HETU_AUTOTUNE_CACHE') and os.path.exists(os.environ['HETU_AUTOTUNE_CACHE']):
+    load(os.environ['HETU_AUTOTUNE_CACHE'])

@@ -66,8 +66,12 @@ def packed_case(B, S, NH, D, keep):
     if KA.fused_ok(qkv, S, D):
         t = timeit(lambda: KA.attention_fwd(qkv, mask, B, S, NH, keep, 7))
         rows.append(('fused', 'fwd', t, fl_f / t * 1e-6))
-        t = timeit(lambda: KA.attention_bwd(do, qkv, out, lse, mask, B, S, NH, keep, 7))
-        rows.append(('fused', 'bwd', t, 2.5 * fl_f / t * 1e-6))
+        mode0 = KA._BWD_MODE
+        for mode in ('split', 'fused', 'w8'):   # the backward's forms (kernels/attention.py)
+            KA._BWD_MODE, KA._BWD_SPLIT = mode, mode == 'split'
+            t = timeit(lambda: KA.attention_bwd(do, qkv, out, lse, mask, B, S, NH, keep, 7))
+            rows.append(('fused', 'bwd-' + mode, t, 2.5 * fl_f / t * 1e-6))
+        KA._BWD_MODE, KA._BWD_SPLIT = mode0, mode0 == 'split'
     q, k, v = KA.packed_heads(qkv, B, S, NH)
     m4 = mask.reshape(B, 1, 1, S)
     o4 = out.view(B, S, NH, D).permute(0, 2, 1, 3)
@@ -83,7 +87,7 @@ def packed_case(B, S, NH, D, keep):
             t = timeit(lambda: KA.flash_bwd(g4, q, k, v, o4, lse, m4, False, keep, 7))
             rows.append(('alt', 'bwd', t, 2.5 * fl_f / t * 1e-6))
     for r in rows:
-        print('B %3d S %4d NH %2d D %3d keep %.1f | %-5s %s %8.1f us %6.1f TF/s' % ((B, S, NH, D, keep) + r),
+        print('B %3d S %4d NH %2d D %3d keep %.1f | %-5s %-9s %8.1f us %6.1f TF/s' % ((B, S, NH, D, keep) + r),
               flush=True)
 
 

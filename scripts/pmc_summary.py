@@ -4,7 +4,8 @@
 
 Per kernel family (template arguments and parameter lists stripped) it sums the
 counters over every dispatch and derives:
-  ms       = summed dispatch time (the --pmc run serialises dispatches)
+  calls/ms = dispatches / summed dispatch time per step with --steps S (the --pmc run
+             serialises dispatches), else over the whole window
   clk_GHz  = GRBM_GUI_ACTIVE / 8 / time (GRBM is summed over the 8 XCDs)
   mfma_pk  = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * GRBM_GUI_ACTIVE / 8): the
              fraction of the chip's matrix-pipe cycles that were busy, i.e. the
@@ -35,6 +36,7 @@ def family(name):
 
 STEPS = 1
 LAST = 0   # --last N: only the N most recent dispatches of each pass (steady state, no autotune)
+MARKER = ''   # --marker K: the window is the last --steps steps, delimited by kernel K (once per step)
 
 
 def load(d):
@@ -43,7 +45,15 @@ def load(d):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     seen = {}
     rows = [r for f in files for r in csv.DictReader(open(f))]
-    if LAST:
+    if MARKER:
+        # exactly STEPS steps: the dispatches after the (STEPS+1)-th last launch of the
+        # once-per-step marker kernel up to and including the last one
+        ids = sorted({int(r['Dispatch_Id']) for r in rows if MARKER in r['Kernel_Name']})
+        if len(ids) < STEPS + 1:
+            raise SystemExit('only %d %s dispatches' % (len(ids), MARKER))
+        lo, hi = ids[-STEPS - 1], ids[-1]
+        rows = [r for r in rows if lo < int(r['Dispatch_Id']) <= hi]
+    elif LAST:
         ids = sorted({int(r['Dispatch_Id']) for r in rows})[-LAST:]
         keep = set(ids)
         rows = [r for r in rows if int(r['Dispatch_Id']) in keep]
@@ -82,7 +92,8 @@ def main(dirs):
         w = wr[0].get(k, {}).get('WRITE_SIZE', 0) * 1024 / tw / 1e12 if tw else float('nan')
         tmo = mops[2].get(k, 0) * 1e-9
         tf = 512 * mops[0].get(k, {}).get('SQ_INSTS_VALU_MFMA_MOPS_BF16', 0) / tmo / 1e12 if tmo else float('nan')
-        print('%-64s %6d %8.2f %8.2f %8.3f %8.3f %8.3f %8.2f %7.2f %7.0f' % (k[:64], calls[k], t * 1e3, clk, mf, wait,
+        print('%-64s %6.4g %8.3f %8.2f %8.3f %8.3f %8.3f %8.2f %7.2f %7.0f' % (k[:64], calls[k] / STEPS, t * 1e3 / STEPS,
+                                                                             clk, mf, wait,
                                                                              lc, rd, w, tf))
     # HBM traffic of the whole window (the --last dispatches; per step with --steps S)
     rd_b = sum(2 * c.get('FETCH_SIZE', 0) * 1024 for c in mem[0].values()) if mem[0] else 0.0
@@ -102,9 +113,11 @@ def main(dirs):
 
 if __name__ == '__main__':
     a = sys.argv[1:]
-    while a and a[0] in ('--last', '--steps'):
+    while a and a[0] in ('--last', '--steps', '--marker'):
         if a[0] == '--last':
             LAST = int(a[1])
+        elif a[0] == '--marker':
+            MARKER = a[1]
         else:
             STEPS = int(a[1])
         a = a[2:]

@@ -123,3 +123,28 @@ def test_gelu_grad_colsum_matches_torch(dt, R, N):
     tol = 2e-2 if dt == torch.bfloat16 else 1e-5
     torch.testing.assert_close(g.float(), ref, rtol=tol, atol=tol)
     torch.testing.assert_close(cs, ref.sum(0), rtol=tol, atol=tol * (R ** 0.5) * 4)
+
+
+@pytest.mark.parametrize('mode', ['split', 'fused', 'w8'])
+@pytest.mark.parametrize('S,keep', [(32, 1.0), (96, 0.9), (128, 1.0), (128, 0.9)])
+def test_packed_attention_backward_forms(monkeypatch, mode, S, keep):
+    """every form of the fixed-length backward (two-launch workspace, one 4-wave launch,
+    one 8-wave launch with the dQ exchange in LDS) against the fp32 reference, and the
+    forms against each other on the same operands"""
+    from hetu_61a7_amd.kernels import attention as KA
+    from test_bert_cpu import packed_attention_check
+    monkeypatch.setattr(KA, '_BWD_MODE', mode)
+    monkeypatch.setattr(KA, '_BWD_SPLIT', mode == 'split')
+    packed_attention_check('cuda', torch.bfloat16, B=3, S=S, NH=2, D=64, keep=keep, tol=2.5e-2)
+    B, NH, D = 4, 3, 64
+    g = torch.Generator(device='cuda').manual_seed(S)
+    qkv = (torch.randn((B * S, 3 * NH * D), device='cuda', generator=g) * 0.5).bfloat16()
+    mask = torch.zeros(B, S, device='cuda')
+    mask[1, S - 7:] = -10000.0
+    out, lse = KA.attention_fwd(qkv, mask, B, S, NH, keep, 77)
+    do = torch.randn(out.shape, device='cuda', generator=g).bfloat16()
+    got = KA.attention_bwd(do, qkv, out, lse, mask, B, S, NH, keep, 77).float()
+    monkeypatch.setattr(KA, '_BWD_MODE', 'split')
+    monkeypatch.setattr(KA, '_BWD_SPLIT', True)
+    ref = KA.attention_bwd(do, qkv, out, lse, mask, B, S, NH, keep, 77).float()
+    assert float((got - ref).norm() / ref.norm()) < 1e-2

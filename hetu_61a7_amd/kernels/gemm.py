@@ -298,6 +298,32 @@ def _splitk_sum(part, out):
     return out
 
 
+def matmul_out(a, b, out):
+    """out[M, N] = a[M, K] @ b[K, N] written into ``out`` -- a bf16 row block of a larger
+    buffer (row stride >= N): the producers of a row concatenation write their slices in
+    place (ops.linalg.RowConcatMatMulOp).  Autotuned over the MFMA tiles.  Returns ``out``."""
+    a, b = _match(a, b)
+    if not a.is_cuda:
+        out.copy_(torch.matmul(a, b))
+        return out
+    if not (native(a) and a.dtype == torch.bfloat16 and out.dtype == torch.bfloat16):
+        no_kernel('matmul_out', '%s %s -> %s' % (a.dtype, tuple(a.shape), out.dtype))
+    from . import gemm_mfma
+    from .autotune import choose
+    key = ('gemm_out', _sig(a), _sig(b), _sig(out))
+    cands = {'hip': lambda: gemm_mfma.gemm(a, b, out=out)}
+    if _big_ok(a, b, False, False):
+        cands['hip256'] = lambda: gemm_mfma.gemm(a, b, out=out, tile=1)
+    if a.shape[-1] <= 2048:
+        cands['hip_lo'] = lambda: gemm_mfma.gemm(a, b, out=out, tile=3)
+    if a.shape[-1] >= 3 * 64:
+        cands['hip_2a'] = lambda: gemm_mfma.gemm(a, b, out=out, tile=6)
+    c = choose(key, cands)
+    if cands[c]() is None and (c == 'hip' or gemm_mfma.gemm(a, b, out=out) is None):
+        no_kernel('matmul_out', '%s x %s' % (tuple(a.shape), tuple(b.shape)))
+    return out
+
+
 def matmul_into(a, b, ta, tb, out):
     """out (fp32, e.g. a slot of the flat gradient buffer) = op(a) @ op(b): the MFMA
     kernels write fp32 directly (split-K candidates for long reductions).  Returns ``out``."""

@@ -11,6 +11,7 @@ data-parallel all-reduce.
 """
 from __future__ import annotations
 
+import os
 import math
 
 import numpy as np
@@ -256,27 +257,43 @@ class Expert(BaseLayer):
         self.name = name if name.startswith('expert') else 'expert_' + name
 
     def __call__(self, x):
+        if not self.bias:
+            h, w2 = self.hidden(x)
+            return O.matmul_op(h, w2)
         w1 = self.initializer(shape=(self.embed_dim, self.ffn_dim), name=self.name + '_weight_1')
         w2 = self.initializer(shape=(self.ffn_dim, self.embed_dim), name=self.name + '_weight_2')
         x = O.array_reshape_op(x, [-1, self.embed_dim])
-        if self.bias:
-            b1 = init.zeros(shape=(self.ffn_dim,), name=self.name + '_bias_1')
-            x = O.linear_op(x, w1, b1, activation='relu' if self.activation is O.relu_op else None)
-            if self.activation is not None and self.activation is not O.relu_op:
-                x = self.activation(x)
-        elif self.activation is O.relu_op and self.keep_prob < 1.0:
+        b1 = init.zeros(shape=(self.ffn_dim,), name=self.name + '_bias_1')
+        x = O.linear_op(x, w1, b1, activation='relu' if self.activation is O.relu_op else None)
+        if self.activation is not None and self.activation is not O.relu_op:
+            x = self.activation(x)
+        if self.keep_prob < 1.0:
+            x = O.dropout_op(x, self.keep_prob)
+        b2 = init.zeros(shape=(self.embed_dim,), name=self.name + '_bias_2')
+        return O.linear_op(x, w2, b2)
+
+    def hidden(self, x):
+        """bias-free expert: (the FFN's hidden activations [tokens, ffn], the second weight)
+        -- the caller runs the second GEMM (alone, or as a row block of the local experts'
+        concatenated output)"""
+        assert not self.bias
+        w1 = self.initializer(shape=(self.embed_dim, self.ffn_dim), name=self.name + '_weight_1')
+        w2 = self.initializer(shape=(self.ffn_dim, self.embed_dim), name=self.name + '_weight_2')
+        x = O.array_reshape_op(x, [-1, self.embed_dim])
+        if self.activation is O.relu_op and self.keep_prob < 1.0:
             # ReLU and dropout in the first GEMM's epilogue (ops/linalg.py MatMulActDropoutOp)
             x = O.matmul_act_dropout_op(x, w1, 'relu', self.keep_prob)
         else:
             x = O.matmul_op(x, w1)
             if self.activation is not None:
                 x = self.activation(x)
-        if self.keep_prob < 1.0 and not (not self.bias and self.activation is O.relu_op):
-            x = O.dropout_op(x, self.keep_prob)
-        if self.bias:
-            b2 = init.zeros(shape=(self.embed_dim,), name=self.name + '_bias_2')
-            return O.linear_op(x, w2, b2)
-        return O.matmul_op(x, w2)
+            if self.keep_prob < 1.0:
+                x = O.dropout_op(x, self.keep_prob)
+        return x, w2
+
+
+# HETU_MOE_ROW_CONCAT=0: the local experts' outputs through a concatenation (A/B switch)
+_ROW_CONCAT = os.environ.get('HETU_MOE_ROW_CONCAT', '1') == '1'
 
 
 def _dispatch_and_run(layer, reshaped, indices_s, location_s, gates_s, capacity):
@@ -286,10 +303,17 @@ def _dispatch_and_run(layer, reshaped, indices_s, location_s, gates_s, capacity)
     disp = O.alltoall_op(disp)
     disp = O.array_reshape_op(disp, [layer.all2all_size, n_local, -1, layer.embed_dim])
     outs = []
-    for i in range(n_local):
-        tok = O.split_op(disp, axes=[1], indices=[i], splits=[n_local])
-        outs.append(O.array_reshape_op(layer.experts[i](tok), [layer.all2all_size, 1, -1, layer.embed_dim]))
-    y = O.concatenate_op(outs, axis=1) if n_local > 1 else outs[0]
+    if _ROW_CONCAT and n_local > 1 and layer.all2all_size == 1 and all(isinstance(e, Expert) and not e.bias for e in layer.experts):
+        # one process holds every expert: their second GEMMs write row blocks of one output
+        # (concatenating [1, 1, C, d] pieces along axis 1 is a row concatenation)
+        hs, w2s = zip(*(layer.experts[i].hidden(O.split_op(disp, axes=[1], indices=[i], splits=[n_local]))
+                        for i in range(n_local)))
+        y = O.row_concat_matmul_op(list(hs), list(w2s))
+    else:
+        for i in range(n_local):
+            tok = O.split_op(disp, axes=[1], indices=[i], splits=[n_local])
+            outs.append(O.array_reshape_op(layer.experts[i](tok), [layer.all2all_size, 1, -1, layer.embed_dim]))
+        y = O.concatenate_op(outs, axis=1) if n_local > 1 else outs[0]
     y = O.alltoall_op(O.array_reshape_op(y, [-1, layer.embed_dim]))
     y = O.array_reshape_op(y, [-1, layer.embed_dim])
     if gates_s is None:

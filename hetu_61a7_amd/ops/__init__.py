@@ -21,7 +21,7 @@ from .shape import (array_reshape_op, array_reshape_gradient_op, transpose_op, b
 from .reduce import (reduce_sum_op, reduce_mean_op, reducesumaxiszero_op, sum_op, norm_op,
                      norm_gradient_op, argmax_op, argsort_op, topk_idx_op, topk_val_op,
                      cumsum_with_bias_op)
-from .linalg import (matmul_op, matmul_act_dropout_op, linear_op, addmm_op, addmm_gradient_op, baddbmm_op,
+from .linalg import (matmul_op, matmul_act_dropout_op, row_concat_matmul_op, RowConcatMatMulOp, linear_op, addmm_op, addmm_gradient_op, baddbmm_op,
                      batch_matmul_op, csrmv_op, csrmm_op)
 from .nn import (conv2d_op, conv2d_gradient_of_data_op, conv2d_gradient_of_filter_op,
                  conv2d_add_bias_op, avg_pool2d_op, avg_pool2d_gradient_op, max_pool2d_op,

@@ -96,6 +96,53 @@ def matmul_op(node_A, node_B, trans_A=False, trans_B=False, ctx=None):
     return MatMulOp(node_A, node_B, trans_A, trans_B, ctx=ctx)
 
 
+class RowConcatMatMulOp(Op):
+    """concat([x_0 @ w_0, ..., x_{n-1} @ w_{n-1}], axis=0) with every product written into
+    its row block of one output (kernels.gemm.matmul_out) -- no per-product output and no
+    concatenation copy.  The MoE layer's local experts' second GEMMs (layers/moe.py
+    _dispatch_and_run; the reference concatenates the expert outputs,
+    python/hetu/layers/moe_layer.py).  Gradient: row-block views of the output gradient
+    into the per-expert data / weight gradient GEMMs."""
+
+    def __init__(self, xs, ws, ctx=None):
+        assert len(xs) == len(ws) and len(xs) > 0
+        super().__init__(RowConcatMatMulOp, list(xs) + list(ws), ctx)
+        self.n = len(xs)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        xs, ws = input_vals[:self.n], input_vals[self.n:]
+        N = ws[0].shape[1]
+        rows = [x.shape[0] for x in xs]
+        if not xs[0].is_cuda or xs[0].dtype != torch.bfloat16:
+            from ..kernels import tensor as KT
+            return KT.concat([KG.matmul(x, w) for x, w in zip(xs, ws)], 0)
+        out = _NA.empty((sum(rows), N), dtype=xs[0].dtype, device=xs[0].device)
+        r = 0
+        for x, w, m in zip(xs, ws, rows):
+            KG.matmul_out(x, w, out[r:r + m])
+            r += m
+        return out
+
+    def gradient(self, output_grad):
+        from .shape import split_op
+        xs, ws = self.inputs[:self.n], self.inputs[self.n:]
+        c = self.raw_ctx
+        gx, gw = [], []
+        for i in range(self.n):
+            g = split_op(output_grad, axes=[0], indices=[i], splits=[self.n], ctx=c)
+            gx.append(matmul_op(g, ws[i], False, True, ctx=c))
+            gw.append(matmul_op(xs[i], g, True, False, ctx=c))
+        return gx + gw
+
+    def infer_shape(self, input_shapes):
+        xs, ws = input_shapes[:self.n], input_shapes[self.n:]
+        return (sum(x[0] for x in xs), ws[0][1])
+
+
+def row_concat_matmul_op(xs, ws, ctx=None):
+    return RowConcatMatMulOp(xs, ws, ctx=ctx)
+
+
 class LinearOp(Op):
     """A @ B + bias with the bias (and optional activation) fused in the GEMM
     epilogue."""

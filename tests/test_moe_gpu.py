@@ -76,3 +76,49 @@ def test_cumsum_long_column_scan_matches_cpu():
     X = (np.random.RandomState(0).rand(16384, 2) > 0.5).astype(np.float32)
     got = ht.Executor([y], ctx=ht.gpu(0)).run(feed_dict={x: X}, convert_to_numpy_ret_vals=True)[0]
     np.testing.assert_array_equal(got, np.cumsum(X, 0) - 1)
+
+
+def test_matmul_out_row_blocks_match_fp32():
+    """kernels.gemm.matmul_out writes each product into its row block of one bf16 buffer
+    (the MoE experts' concatenated output) -- against fp32 math, blocks untouched outside"""
+    from hetu_61a7_amd.kernels import gemm as KG
+    g = torch.Generator(device='cuda').manual_seed(0)
+    xs = [torch.randn(m, 256, device='cuda', generator=g).bfloat16() for m in (512, 384, 640)]
+    ws = [(torch.randn(256, 384, device='cuda', generator=g) * 0.05).bfloat16() for _ in xs]
+    out = torch.full((sum(x.shape[0] for x in xs), 384), 7.0, device='cuda').bfloat16()
+    r = 0
+    for x, w in zip(xs, ws):
+        KG.matmul_out(x, w, out[r:r + x.shape[0]])
+        r += x.shape[0]
+    ref = torch.cat([x.float() @ w.float() for x, w in zip(xs, ws)], 0)
+    assert float((out.float() - ref).norm() / ref.norm()) < 1e-2
+
+
+def test_moe_row_concat_experts_match_concat_path(monkeypatch):
+    """the MoE bench layer with the local experts' second GEMMs as row blocks of one output
+    trains like the concatenation path (same losses, bf16 noise)"""
+    import hetu_61a7_amd.layers.moe as LM
+    from hetu_61a7_amd.ops import node as _node
+    losses, init = {}, None
+    for rc in (True, False):
+        monkeypatch.setattr(LM, '_ROW_CONCAT', rc)
+        _node.G_NODE_ID = 0
+        rng = np.random.RandomState(0)
+        T, d, E = 512, 128, 4
+        x = ht.Variable(name='x')
+        gate = LM.TopKGate(embed_dim=d, num_tokens=T, num_experts=E, k=2)
+        experts = [LM.Expert(d, 256, activation='relu', name='expert_%d' % i) for i in range(E)]
+        y, l_aux = LM.MoELayer(gate=gate, experts=experts, num_tokens=T, embed_dim=d)(x)
+        loss = ht.add_op(ht.reduce_mean_op(ht.mul_op(y, y), [0, 1]), l_aux)
+        train = ht.optim.SGDOptimizer(0.1).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, mixed_precision='bf16')
+        pm = {n.name: t for n, t in ex.config.placeholder_to_arr_map.items() if n.trainable}
+        if init is None:
+            init = {k: v.detach().clone() for k, v in pm.items()}
+        else:
+            for k, v in pm.items():
+                v.copy_(init[k])
+        X = rng.randn(T, d).astype(np.float32)
+        losses[rc] = [float(np.asarray(ex.run('train', feed_dict={x: X}, convert_to_numpy_ret_vals=True)[0])
+                            .reshape(-1)[0]) for _ in range(4)]
+    np.testing.assert_allclose(losses[True], losses[False], rtol=2e-2)

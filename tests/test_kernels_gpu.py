@@ -195,6 +195,13 @@ def test_reductions():
     torch.testing.assert_close(KR.reduce_mid(x), x.sum(1), rtol=1e-4, atol=1e-3)
     y = torch.randn(5000, 300, device=DEV)
     torch.testing.assert_close(KR.reduce_last(y), y.sum(1), rtol=1e-4, atol=1e-3)
+    # 16-byte vector form (C % 8 == 0 bf16 / C % 4 == 0 fp32) and the scalar form, bf16 rows
+    for R, C in ((4096, 2048), (333, 1000), (70, 36), (9, 4104)):
+        yb = torch.randn(R, C, device=DEV).bfloat16()
+        ref = yb.float().sum(1)
+        got = KR.reduce_last(yb, out_dtype=torch.float32)
+        torch.testing.assert_close(got, ref, rtol=1e-3, atol=1e-2 * C ** 0.5)
+        torch.testing.assert_close(KR.reduce_last(yb, 0.5).float(), 0.5 * ref, rtol=2e-2, atol=2e-2 * C ** 0.5)
     g = torch.randn(32, 16, 128, device=DEV)
     torch.testing.assert_close(KR.sum_to_shape(g, (128,)), g.sum((0, 1)), rtol=1e-4, atol=1e-3)
 

@@ -9,6 +9,9 @@ Adam bias corrections) live in a device tensor read by the fused update kernel
 """
 from __future__ import annotations
 
+import atexit
+import weakref
+
 import torch
 from .. import native_array as _NA
 
@@ -34,8 +37,33 @@ def capturing():
     return _CAPTURING[0] > 0
 
 
+# live runners: their graphs are dropped at interpreter exit while the HIP runtime and
+# torch's allocator are still up (a torch CUDAGraph collected during module teardown fails
+# its destructor's HIP call and aborts the process after a clean run)
+_RUNNERS = weakref.WeakSet()
+
+
+def _close_all():
+    runners = list(_RUNNERS)
+    if not runners:
+        return
+    try:
+        torch.cuda.synchronize()
+    except Exception:       # noqa: BLE001
+        pass
+    for r in runners:
+        try:
+            r.close()
+        except Exception:   # noqa: BLE001
+            pass
+
+
+atexit.register(_close_all)
+
+
 class GraphRunner(object):
     def __init__(self, sub, warmup=3):
+        _RUNNERS.add(self)
         self.sub = sub
         self.warmup = warmup
         self.calls = 0
@@ -165,8 +193,10 @@ class GraphRunner(object):
         cap = self.capture_stream = RT.DeviceStream(persistent=True)
         _CAPTURING[0] += 1
         try:
-            # torch captures on `cap`; the framework's launches follow it there
-            with torch.cuda.graph(self.graph, stream=cap.torch), RT.use_stream(cap):
+            # torch captures on `cap`; the framework's launches follow it there.  use_stream
+            # is the OUTER context: on exit it restores torch's stream to the framework's
+            # previous one, which must happen after the graph's capture_end ran on `cap`
+            with RT.use_stream(cap), torch.cuda.graph(self.graph, stream=cap.torch):
                 self.static_vals = sub._run_eager(None, vals=dict(base))
         finally:
             _CAPTURING[0] -= 1

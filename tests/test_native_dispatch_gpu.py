@@ -20,9 +20,16 @@ def _census(step, warm=3):
     for _ in range(warm):
         step()
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
-        step()
-        torch.cuda.synchronize()
+    # the census step runs eagerly: a replayed hipGraph (the single-GPU default) is one
+    # graph launch in the activity trace and would hide the kernels it replays
+    from hetu_61a7_amd.utils import hipgraph
+    hipgraph.FORCE_EAGER[0] += 1
+    try:
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            step()
+            torch.cuda.synchronize()
+    finally:
+        hipgraph.FORCE_EAGER[0] -= 1
     torch_k = collections.Counter()
     n = 0
     vendor = ('Cijk', 'igemm', 'SubTensorOp', 'naive_conv', 'MIOpen', 'miopen', 'ck::', '_ZN2ck', 'gridwise_')

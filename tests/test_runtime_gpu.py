@@ -15,9 +15,11 @@ def test_stream_event_ordering_and_timing():
     x = torch.randn(1 << 22, device='cuda')
     start = RT.DeviceEvent(timing=True).record(s)
     s.wait_stream(torch.cuda.current_stream())          # x is ready before s runs
-    with torch.cuda.stream(s.torch):
+    with RT.use_stream(s):                               # the framework's current stream
         assert K.stream_ptr() == s.handle                 # hand-written kernels launch on it
+        assert torch.cuda.current_stream().cuda_stream == s.handle   # torch follows it
         y = KE.unary('mul_c', x, 3.0)
+    assert K.stream_ptr() != s.handle
     end = RT.DeviceEvent(timing=True).record(s)
     end.wait(torch.cuda.current_stream())               # the current stream waits for y
     torch.testing.assert_close(y, x * 3.0)

@@ -811,8 +811,14 @@ __device__ __forceinline__ void lds_barrier() {
 // ST == 1 is also the high-occupancy form for short-K, memory-bound shapes (1x1 convolutions,
 // their gradient joins): one 32 KiB LDS buffer restaged per K-tile behind a barrier and at most
 // 128 VGPRs, so 4 blocks share a CU and hide each other's DMA / epilogue latency.
+// HETU_BNX_PRE1 (build flag, default on): the single-stage BN-backward tile also prefetches
+// its gradient-join rows before the epilogue staging, at 3 blocks per CU -- ResNet-50
+// 10 898 / 10 859 vs 10 808 / 10 812 img/s interleaved (profiles/bnx_prefetch_ab_r6.txt)
+#ifndef HETU_BNX_PRE1
+#define HETU_BNX_PRE1 1
+#endif
 template <class LA, class LB, int ST, int WN = 4, bool BNX = false, int EX = 0>
-__global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
+__global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : (ST == 1 && HETU_BNX_PRE1 ? 3 : 2))) void gemm_kernel(LA la, LB lb, Epi ep, int64_t M, int64_t N,
                                                                      int64_t K, int tiles_m, int tiles_n, int ktps) {
   constexpr bool DB = ST >= 2;
   constexpr int TBN = 32 * WN;                 // block tile columns
@@ -958,7 +964,7 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : 2)) void gemm_kernel(LA 
   // (not in the single-stage 4-blocks-per-CU build: at 128 registers the prefetch spills,
   // and its neighbours on the CU hide the epilogue latency instead)
   uint4 cpre[NPASS];
-  const bool use_pre = ST == 2 && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec && !(BNX && ep.cin_w);
+  const bool use_pre = (ST == 2 || (HETU_BNX_PRE1 && ST == 1 && BNX)) && eo.Cinb && !ep.cin_f32 && !ep.atomic && !ep.slab && eo.ivec && !(BNX && ep.cin_w);
   const int64_t pre_n = (int64_t)tn * TBN + ec;
   auto pre_load = [&](int h, int pss) {
     const int rr = pss * RPP + tid / TPR;

@@ -33,7 +33,14 @@ def _load(name):
         return e, path
 
 
-_KLIB, _KPATH = _load('libhetu_kernels.so')
+if os.environ.get('HETU_KERNELS_LIB'):   # A/B runs: a kernel library built with other flags
+    _KPATH = os.path.abspath(os.environ['HETU_KERNELS_LIB'])
+    try:
+        _KLIB = ctypes.CDLL(_KPATH, mode=ctypes.RTLD_GLOBAL) if os.path.exists(_KPATH) else None
+    except OSError as _e:  # pragma: no cover
+        _KLIB = _e
+else:
+    _KLIB, _KPATH = _load('libhetu_kernels.so')
 _RLIB, _RPATH = _load('libhetu_runtime.so')
 
 

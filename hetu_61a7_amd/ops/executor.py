@@ -264,6 +264,13 @@ class HetuConfig(object):
                                           and world == 1 and self.comm is None and self.ps_comm is None
                                           and self.comm_mode is None and pipeline is None and not self.spmd)
         self.use_hipgraph = bool(use_hipgraph)
+        # piecewise replay (utils/piecewise.py) for single-GPU PS steps: the device segments
+        # between the host-bound ops (PS lookups, gradient staging, the PS optimizer) are
+        # captured and replayed; HETU_PIECEWISE_GRAPH=0 / 1 forces it off / on
+        pw = os.environ.get('HETU_PIECEWISE_GRAPH', 'auto')
+        self.use_piecewise = not self.use_hipgraph and (pw == '1' or (
+            pw == 'auto' and gpu_available() and ndarray.is_gpu_ctx(self.context) and world == 1
+            and self.comm is None and self.ps_comm is not None and pipeline is None and not self.spmd))
 
         # ---- hooks (pre-order backward_hook, post-order forward_hook) ------------------------
         self.topo_sort_with_hook(eval_node_list)
@@ -471,6 +478,7 @@ class SubExecutor(object):
         self._build_plan()
         self.timer = None
         self.graph = None
+        self.piecewise = None
         self.graph_state = None
         self.step_count = 0
 
@@ -573,6 +581,14 @@ class SubExecutor(object):
             # (ops with per-step host schedules -- the DTS gate's temperature and budget --
             # change launch arguments and shapes between steps: not replayable, run eager)
             return self._run_graph(feed_dict, convert_to_numpy_ret_vals)
+        if getattr(cfg, 'use_piecewise', False) and cfg.device.type == 'cuda' and not self.step_end_nodes \
+                and self.opt_ops and self.timer is None:
+            from .. import memory_pool as _MP
+            if _MP.torch_bfc_enabled():
+                if self.piecewise is None:
+                    from ..utils.piecewise import PiecewiseRunner
+                    self.piecewise = PiecewiseRunner(self)
+                return self.piecewise.run(feed_dict, convert_to_numpy_ret_vals)
         vals = self._run_eager(feed_dict)
         if self.opt_ops and not self.inference:
             for n in self.step_end_nodes:

@@ -610,7 +610,7 @@ class OptimizerOp(Op):
         elif self.flat is not None and self.flat.numel > 0:
             self.optimizer.dense_update(self.flat, self.step, getattr(self, 'dyn', None))
         for table in self._pending_ps:
-            table.flush_grad()
+            table.flush_grad(force=False)     # ASP + prefetch: behind the next step's staging
         self._pending_ps = []
         for p, sl in self._pending_sparse:
             table = self.config.placeholder_to_arr_map[p]

@@ -14,6 +14,7 @@ push and pull), >0 SSP with that staleness bound.
 """
 from __future__ import annotations
 
+import os
 import torch
 
 from . import worker as psw
@@ -110,6 +111,7 @@ class _Staging(object):
         self.buf = None
         self.dtype = dtype
         self.event = None
+        self.ticket = None       # the push that reads this buffer (gradient staging)
 
     def get(self, n):
         if self.event is not None:
@@ -129,6 +131,12 @@ class _Staging(object):
 
 
 _LIVE = []
+# HETU_PS_DEFER_PUSH=1: push a step's embedding gradient behind the next step's staging
+# instead of at the step's end.  Off: with the double-buffered staging the end-of-step push
+# no longer waits for the previous one, and deferring measured slower (the next lookup then
+# waits for the prefetch queued behind the push): WDL 187-191 k vs 121-144 k samples/s
+# (profiles/wdl_ps_push_ab_r6.txt)
+_DEFER_PUSH = os.environ.get('HETU_PS_DEFER_PUSH', '0') == '1'
 
 
 def close_all():
@@ -172,9 +180,13 @@ class PSTable(object):
         else:
             self.agent.BarrierWorker()
         self.out_stage = _Staging()
-        self.grad_stage = _Staging()
+        # gradient staging, double-buffered: a deferred push still reads one buffer while
+        # the next step's gradient lands in the other
+        self.grad_stages = (_Staging(), _Staging())
+        self.gs_flip = 0
         self.pending = None
         self.pending_push = None
+        self._prefetch_due = False
         self.version = 0
         # prefetch (reference executor.py:531-536, HetuConfig(prefetch=True)): when the
         # ids of the NEXT batch are known (dataloader-fed lookups) and training is
@@ -196,15 +208,31 @@ class PSTable(object):
     def numel(self):
         return self.rows * self.width
 
+    def _wait_ticket(self, t):
+        with _waiting():
+            if self.cache is not None:
+                self.cache.wait(t)
+            else:
+                self.agent.WaitTicket(t)
+
     def _wait_push(self):
-        if self.pending is not None:
-            with _waiting():
-                if self.cache is not None:
-                    self.cache.wait(self.pending)
-                else:
-                    self.agent.WaitTicket(self.pending)
-            self.pending = None
-            self.pending_push = None
+        """every push issued so far (a deferred one is issued first) has completed"""
+        if self.pending_push is not None:
+            self.flush_grad(force=True)
+        for st in self.grad_stages:
+            if st.ticket is not None:
+                self._wait_ticket(st.ticket)
+                st.ticket = None
+        self.pending = None
+
+    def _deferrable(self):
+        """ASP with prefetch: a step's gradient push waits for the next step's gradient
+        staging (by then its D2H copy has long completed), and the prefetch of the batch
+        after next is issued right behind it -- the host never blocks on this step's device
+        work, and prefetched rows still carry every push up to the step before (staleness 1,
+        as the un-deferred schedule)"""
+        return (_DEFER_PUSH and self.cache is not None and self.next_ids_fn is not None
+                and self.bsp is not None and self.bsp < 0)
 
     def _take_prefetched(self, ids):
         pf, self.prefetched = self.prefetched, None
@@ -244,7 +272,10 @@ class PSTable(object):
                 else:
                     t = self.agent.SparsePull(self.key, ids, dest)
                     self.agent.WaitTicket(t)
-        self._prefetch_next()
+        if self.pending_push is not None and self._deferrable():
+            self._prefetch_due = True        # issued behind the deferred push (stage_grad)
+        else:
+            self._prefetch_next()
         if self.device.type == 'cuda':
             # H2D on the copy stream; the compute stream waits for it by event only
             h2d, _ = side_streams(self.device)
@@ -263,36 +294,50 @@ class PSTable(object):
     def stage_grad(self, slices, lr):
         """Scale by -lr on the device and start the D2H copy (called as soon as the
         gradient exists, so it overlaps the rest of backward)."""
-        self._wait_push()          # the last push may still read the staging buffer
+        if self.pending_push is not None:
+            self.flush_grad(force=True)      # the previous step's deferred push
+        if self._prefetch_due:
+            self._prefetch_due = False
+            self._prefetch_next()
+        stage = self.grad_stages[self.gs_flip]
+        self.gs_flip ^= 1
+        if stage.ticket is not None:         # the push that last read this buffer
+            self._wait_ticket(stage.ticket)
+            stage.ticket = None
         ids = host_ids(slices.indices)
         vals = slices.values.reshape(-1, self.width)
         scaled = _scaled_f32(vals, -lr)
-        host = self.grad_stage.get(scaled.numel()).view(-1, self.width)
+        host = stage.get(scaled.numel()).view(-1, self.width)
         if scaled.is_cuda:
             # D2H on the copy stream after the scaling kernel; the compute stream goes on
             _, d2h = side_streams(scaled.device)
             d2h.wait_stream(None)
             with use_stream(d2h):
                 host.copy_(scaled, non_blocking=True)
-                self.grad_stage.guard(d2h)
+                stage.guard(d2h)
             record_stream(scaled, d2h)
         else:
             host.copy_(scaled)
-        self.pending_push = (ids, host)
+        self.pending_push = (ids, host, stage)
 
-    def flush_grad(self):
-        """Push the staged gradient (after its D2H copy completed)."""
+    def flush_grad(self, force=True):
+        """Push the staged gradient (after its D2H copy completed).  ``force=False`` (the
+        optimizer's end of step) leaves it to the next step's staging when deferrable."""
         if self.pending_push is None:
             return
-        ids, host = self.pending_push
-        if self.grad_stage.event is not None:
+        if not force and self._deferrable():
+            return
+        ids, host, stage = self.pending_push
+        self.pending_push = None
+        if stage.event is not None:
             with _waiting():
-                self.grad_stage.event.synchronize()
+                stage.event.synchronize()
+            stage.event = None
         if self.cache is not None:
             self.pending = self.cache.embedding_update(ids, host)
         else:
             self.pending = self.agent.SparsePush(self.key, ids, host)
-        self.pending_push = None
+        stage.ticket = self.pending
         self.version += 1
         if self.bsp == 0:
             self._wait_push()

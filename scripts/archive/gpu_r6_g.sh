@@ -29,4 +29,4 @@ for k, c in sorted(agg.items()):
 " > $O/r6g_attn_lds.txt; cat $O/r6g_attn_lds.txt
 rm -rf $O/r6g_attn_pmc
 cd $R
-PMC_MODEL=bert bash scripts/gpu_r6_pmc.sh && PMC_MODEL=resnet50 bash scripts/gpu_r6_pmc.sh
+PMC_MODEL=bert bash scripts/gpu_pmc_steady.sh && PMC_MODEL=resnet50 bash scripts/gpu_pmc_steady.sh

@@ -12,4 +12,4 @@ for i in 1 2; do
     echo "$m $i $(python3 -c "import json;d=json.loads(open('$O/r6h_bert_$m$i.json').read().strip().splitlines()[-1]);print(d['value'], d['ms_per_step'], d['config'].get('aten_kernels_per_step'))")"
   done
 done
-PMC_MODEL=bert bash scripts/gpu_r6_pmc.sh && PMC_MODEL=resnet50 bash scripts/gpu_r6_pmc.sh
+PMC_MODEL=bert bash scripts/gpu_pmc_steady.sh && PMC_MODEL=resnet50 bash scripts/gpu_pmc_steady.sh

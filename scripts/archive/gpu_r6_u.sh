@@ -14,4 +14,4 @@ for i in 1 2; do
     echo "defer=$d $i $(python3 -c "import json;d=json.loads(open('$O/r6u_wdl_$d$i.json').read().strip().splitlines()[-1]);c=d['config'];print(d['value'], d['ms_per_step'], c.get('step_breakdown_ms'), c.get('cache_hit_rate'), c.get('prefetch_hits'))")"
   done
 done
-STEPS=100 WARMUP=20 bash scripts/gpu_r6_wdl8.sh > /dev/null 2>&1; tail -1 $O/wdl8.json | cut -c1-240
+STEPS=100 WARMUP=20 bash scripts/gpu_wdl8_one_gpu.sh > /dev/null 2>&1; tail -1 $O/wdl8.json | cut -c1-240

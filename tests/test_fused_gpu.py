@@ -170,3 +170,4 @@ def test_ln_backward_waves(monkeypatch, waves, R, N, keep):
     for a, b in zip(got, ref):
         a, b = a.float(), b.float()
         assert float((a - b).norm() / b.norm().clamp_min(1e-12)) < 1e-2
+

@@ -39,8 +39,14 @@ class BertConfig(object):
     def __init__(self, vocab_size=30522, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
                  intermediate_size=3072, hidden_act='gelu', hidden_dropout_prob=0.1,
                  attention_probs_dropout_prob=0.1, max_position_embeddings=512, type_vocab_size=2,
-                 initializer_range=0.02, batch_size=64, seq_len=128, fused_attention=True, vocab_multiple=64):
+                 initializer_range=0.02, batch_size=64, seq_len=128, fused_attention=True, vocab_multiple=64,
+                 max_predictions_per_seq=None):
         self.vocab_size = vocab_size
+        # max_predictions_per_seq (the original BERT's data contract: at most this many
+        # labelled positions per sequence): the MLM head runs over the labelled rows only,
+        # compacted into that many slots per sequence (ops/mlm.py) -- same loss and
+        # gradients; None scores every position as the reference does
+        self.max_predictions_per_seq = max_predictions_per_seq
         # the word-embedding table / MLM decoder are padded to a multiple of vocab_multiple
         # rows (Megatron's make-vocab-size-divisible-by): 30522 -> 30528 keeps every MLM-head
         # GEMM leading dimension a multiple of the MFMA loaders' 16-byte chunks.  The pad
@@ -232,10 +238,23 @@ class BertForPreTraining(object):
                  next_sentence_label=None):
         seq, pooled = self.bert(input_ids, token_type_ids, attention_mask)
         with _stage_ctx(self.placement, len(self.bert.layers) + 1):
+            C = self.cfg.max_predictions_per_seq
+            if C and masked_lm_labels is not None:
+                # the labelled rows only (C slots per sequence); the mean of the per-slot
+                # losses times C / S equals the reference's mean over all B*S rows (unlabelled
+                # rows contribute 0): ``mlm_mean_scale``
+                pos = ht.masked_positions_op(masked_lm_labels, C)
+                self.masked_positions = pos
+                seq = ht.take_rows_op(seq, pos)
+                labels = ht.take_rows_op(masked_lm_labels, pos, fill_neg1=True)
+            else:
+                labels = masked_lm_labels
             scores, nsp = self.cls(seq, pooled)
             out = [scores, nsp]
             if masked_lm_labels is not None and next_sentence_label is not None:
-                mlm = ht.softmaxcrossentropy_sparse_op(scores, masked_lm_labels, ignored_index=-1)
+                mlm = ht.softmaxcrossentropy_sparse_op(scores, labels, ignored_index=-1)
+                # per-slot losses: their mean times C / S is the reference's mean over all rows
+                self.mlm_mean_scale = float(C) / self.cfg.seq_len if C else 1.0
                 ns = ht.softmaxcrossentropy_sparse_op(nsp, next_sentence_label, ignored_index=-1)
                 out += [mlm, ns]
         return out
@@ -311,7 +330,10 @@ def bert_pretrain_graph(cfg, lr=1e-5, optimizer=None, plan=None, placement=None)
     model = BertForPreTraining(cfg, placement)
     _, _, mlm, nsp = model(input_ids, token_type_ids, attention_mask, mlm_labels, nsp_labels)
     with _stage_ctx(placement, cfg.num_hidden_layers + 1):
-        loss = ht.reduce_mean_op(mlm, [0]) + ht.reduce_mean_op(nsp, [0])
+        mlm_mean = ht.reduce_mean_op(mlm, [0])
+        if getattr(model, 'mlm_mean_scale', 1.0) != 1.0:
+            mlm_mean = ht.mul_byconst_op(mlm_mean, model.mlm_mean_scale)
+        loss = mlm_mean + ht.reduce_mean_op(nsp, [0])
         opt = optimizer or optim.AdamOptimizer(learning_rate=lr)
         train = opt.minimize(loss)
     feeds = dict(input_ids=input_ids, token_type_ids=token_type_ids, attention_mask=attention_mask,
@@ -320,13 +342,25 @@ def bert_pretrain_graph(cfg, lr=1e-5, optimizer=None, plan=None, placement=None)
 
 
 def synthetic_bert_batch(cfg, seed=0, mask_prob=0.15):
+    """Random ids; each token labelled with probability ``mask_prob`` -- or, with
+    ``cfg.max_predictions_per_seq`` set, exactly min(max_predictions_per_seq,
+    max(1, round(S * mask_prob))) labelled positions per sequence, as the original BERT's
+    create_pretraining_data draws them"""
     rng = np.random.default_rng(seed)
     B, S = cfg.batch_size, cfg.seq_len
     ids = rng.integers(min(1000, cfg.vocab_size // 2), cfg.vocab_size, (B, S)).astype(np.int64)
     types = np.zeros((B, S), np.int64)
     types[:, S // 2:] = 1
     mask = np.ones((B, S), np.float32)
-    mlm = np.where(rng.random((B, S)) < mask_prob, ids, -1).astype(np.int64)
+    C = getattr(cfg, 'max_predictions_per_seq', None)
+    if C:
+        n = min(int(C), max(1, int(round(S * mask_prob))))
+        sel = np.argsort(rng.random((B, S)), axis=1)[:, :n]
+        lab = np.zeros((B, S), bool)
+        np.put_along_axis(lab, sel, True, axis=1)
+        mlm = np.where(lab, ids, -1).astype(np.int64)
+    else:
+        mlm = np.where(rng.random((B, S)) < mask_prob, ids, -1).astype(np.int64)
     nsp = rng.integers(0, 2, (B,)).astype(np.int64)
     return dict(input_ids=ids, token_type_ids=types, attention_mask=mask, masked_lm_labels=mlm,
                 next_sentence_label=nsp)
@@ -357,7 +391,11 @@ def bert_bench(args, world, rank, local):
     import hetu_61a7_amd as H
     from ..parallel.galvatron import GalvatronPlanner, Hardware, bert_layers
     B = args.batch or 64
-    cfg = getattr(args, 'bert_config', None) or BertConfig.base(batch_size=B, seq_len=128)
+    # the MLM head over the labelled positions only, 20 slots per sequence (the original
+    # BERT's max_predictions_per_seq; HETU_BERT_MAX_PRED=0 scores every position)
+    max_pred = int(os.environ.get('HETU_BERT_MAX_PRED', '20')) or None
+    cfg = getattr(args, 'bert_config', None) or BertConfig.base(batch_size=B, seq_len=128,
+                                                                 max_predictions_per_seq=max_pred)
     cfg.batch_size = B
     specs = bert_layers(cfg.hidden_size, cfg.num_hidden_layers, cfg.seq_len, cfg.vocab_size)
     planner = GalvatronPlanner(specs, hw=Hardware(gpus=world), max_tp=int(os.environ.get('HETU_GALVATRON_MAX_TP', '1')))
@@ -408,8 +446,17 @@ def bert_bench(args, world, rank, local):
 
     conf = {'model': 'BERT-base (L12 H768 A12, MLM+NSP)', 'global_batch': B * world, 'seq_len': cfg.seq_len,
             'parallelism': parallelism, 'optimizer': 'adam', 'per_gpu_batch': B,
+            'mlm_head': ('labelled positions only, max_predictions_per_seq %d' % cfg.max_predictions_per_seq
+                         if getattr(cfg, 'max_predictions_per_seq', None) else 'every position'),
             'plan': {'pp': plan.pp, 'micro_batches': plan.micro_batches, 'stages': plan.stages,
                      'est_ms': round(plan.time * 1e3, 3)}}
     step.executor = ex
     step.plan = plan
-    return step, B * world, conf, 'samples/sec (whole node) BERT-base pretraining', None
+
+    def finish():
+        from ..ops.mlm import MaskedPositionsOp
+        for sub in getattr(ex, 'subexecutor', {}).values():
+            for n in getattr(sub, 'topo_order', ()):
+                if isinstance(n, MaskedPositionsOp):
+                    n.check()      # no sequence had more labels than slots
+    return step, B * world, conf, 'samples/sec (whole node) BERT-base pretraining', finish

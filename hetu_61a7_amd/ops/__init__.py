@@ -56,3 +56,4 @@ from .ps_ops import (parameterServerCommunicate_op, parameterServerSparsePull_op
 from .executor import Executor, HetuConfig, gradients, find_topo_sort
 from .attention import attention_op, AttentionOp, AttentionGradientOp, packed_attention_op
 from .distgcn import distgcn_15d_op, DistGCN_15dOp, make_15d_groups, partition_15d
+from .mlm import masked_positions_op, take_rows_op, MaskedPositionsOp, TakeRowsOp, PutRowsOp

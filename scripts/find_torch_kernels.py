@@ -55,9 +55,12 @@ def main():
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
+    from hetu_61a7_amd.utils import hipgraph
+    hipgraph.FORCE_EAGER[0] += 1      # an eager step: a graph replay would hide its kernels
     with profile(activities=[ProfilerActivity.CUDA, ProfilerActivity.CPU], with_stack=True) as prof:
         step()
         torch.cuda.synchronize()
+    hipgraph.FORCE_EAGER[0] -= 1
     counts = collections.Counter()
     where = collections.defaultdict(collections.Counter)
     for e in prof.events():

@@ -313,6 +313,52 @@ def test_moe_ep8_matches_one_process_with_all_experts():
             np.testing.assert_allclose(v, ref[3][k], rtol=1e-4, atol=1e-6, err_msg='%s rank %d' % (k, rank))
 
 
+def _moe_drop_worker(rank, world, port, q, n_exp_total, T_local, cf):
+    """forward of the EP layer at capacity factor ``cf`` (tokens dropped at every rank's
+    full expert slots); world == 1: the per-shard reference -- the same layer, all experts
+    local, run on each rank's shard of the tokens in turn (each shard's capacity)"""
+    _env(rank, world, port)
+    import hetu_61a7_amd as ht
+    from hetu_61a7_amd.layers.moe import TopKGate, Expert, MoELayer
+    from hetu_61a7_amd.utils.checkpoint import load_dict
+    d, hidden = 8, 16
+    E = n_exp_total
+    n_local = E // world
+    Xall = np.random.RandomState(7).randn(WORLD * T_local, d).astype(np.float32)
+    x = ht.Variable(name='x')
+    experts = [Expert(d, hidden, activation='relu', name='expert_%d' % (rank * n_local + i)) for i in range(n_local)]
+    gate = TopKGate(d, T_local, E, k=2, capacity_factor=cf)
+    y, l_aux = MoELayer(gate, experts, T_local, d, all2all_size=world)(x)
+    kw = dict(comm_mode='AllReduce') if world > 1 else dict(ctx=ht.cpu(0))
+    ex = ht.Executor({'fwd': [y]}, **kw)
+    names = [n.name for n in ex.config.placeholder_to_arr_map if getattr(n, 'trainable', False)]
+    load_dict(ex, _moe_params(names, d, hidden, E))
+    shards = [rank] if world > 1 else list(range(WORLD))
+    ys = {}
+    for r in shards:
+        X = Xall[r * T_local:(r + 1) * T_local]
+        ys[r] = np.asarray(ex.run('fwd', feed_dict={x: X}, convert_to_numpy_ret_vals=True)[0]).reshape(T_local, d)
+    if world > 1:
+        from hetu_61a7_amd.parallel import comm
+        comm.destroy()
+    q.put((rank, ys))
+
+
+def test_moe_ep8_capacity_drops_match_per_shard_reference():
+    """expert parallelism with tokens DROPPED at capacity (factor 1, top-2,
+    16 experts, 8 tokens per rank).  Each rank's gate fills its own slots of every expert, so
+    the EP8 layer must equal the same layer run with all 16 experts in one process on each
+    rank's shard of the tokens (that shard's capacity): routing, drop decisions, the
+    all-to-all round trip and the combine agree token by token."""
+    ref = _run(_moe_drop_worker, 1, 16, 8, 1.0)[0][1]
+    res = _run(_moe_drop_worker, WORLD, 16, 8, 1.0)
+    dropped = 0
+    for rank, ys in res:
+        np.testing.assert_allclose(ys[rank], ref[rank], rtol=1e-5, atol=1e-6, err_msg='rank %d' % rank)
+        dropped += int((np.abs(ref[rank]).sum(1) == 0).sum())
+    assert dropped > 0          # capacity actually dropped tokens (their output rows are zero)
+
+
 def test_bench_torchrun_eight_ranks_prints_driver_json():
     """A dry run of the driver's scaling launch (python -m torch.distributed.run
     --nproc-per-node 8 ... bench.py --gpus 8) on the CPU with gloo: rank 0 prints ONE JSON

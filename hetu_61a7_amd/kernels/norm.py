@@ -8,6 +8,22 @@ from .. import native_array as _NA
 from . import fn, native, stream_ptr, is_bf16, check, P, I64, I32, F32
 
 
+_TUNED = [False]
+
+
+def _tune_once():
+    """HETU_BN_TUNE=chunks,apply_blocks,min_passes (0 keeps a default): the BatchNorm
+    kernels' launch shapes (hetu_bn_tune; scripts/bench_bn.py sweeps them)"""
+    if _TUNED[0]:
+        return
+    _TUNED[0] = True
+    import os
+    v = os.environ.get('HETU_BN_TUNE')
+    if v:
+        a = [int(t) for t in v.split(',')] + [0, 0, 0]
+        fn('hetu_bn_tune', [I32, I32, I32], restype=None)(a[0], a[1], a[2])
+
+
 def _as_rows(x):
     """View x as [M, C] channels-last rows; returns (rows, restore_fn) or None."""
     if x.dim() == 2:
@@ -27,6 +43,7 @@ def _like_rows(x):
 
 
 def _ws(M, C, bf, device):
+    _tune_once()
     f = fn('hetu_bn_workspace_floats', [I64, I32, I32], restype=I64)
     n = f(M, C, bf)
     return _NA.empty(n, dtype=torch.float32, device=device)

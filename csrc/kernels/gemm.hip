@@ -29,7 +29,7 @@ static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin
                           float alpha, float beta, int act, int out_f32, int cin_f32,
                           int bias_on_m, int splitk, int atomic, float* ws, int tile, void* C2,
                           float drop_keep, uint64_t drop_seed, hipStream_t st, const void* gmask = nullptr,
-                          float gmask_scale = 1.f) {
+                          float gmask_scale = 1.f, int gmask_bits = 0, uint8_t* mbits_out = nullptr) {
   Epi ep{C, Cin, bias, ldc, ldcin, sC, sCin, alpha, beta, act, out_f32, cin_f32, atomic,
          bias_on_m, ws, 0};
   ep.C2 = C2;
@@ -38,6 +38,10 @@ static int gemm_bf16_impl(const void* A, const void* B, void* C, const void* Cin
   ep.drop_off = ep.drop_keep > 0.f ? hetu_rng_offset_ptr() : nullptr;
   ep.gmask = gmask;
   ep.gmask_scale = gmask_scale;
+  ep.gmask_bits = gmask ? gmask_bits : 0;
+  ep.mbits_out = ep.drop_keep > 0.f ? mbits_out : nullptr;
+  if ((ep.gmask_bits || mbits_out) && ldc % 8) return (int)hipErrorInvalidValue;
+  if (mbits_out && !ep.mbits_out) return (int)hipErrorInvalidValue;
   if ((C2 || ep.drop_keep > 0.f || gmask) && (splitk > 1 || atomic)) return (int)hipErrorInvalidValue;
   if (gmask && (batch != 1 || out_f32 || ((uintptr_t)gmask & 15))) return (int)hipErrorInvalidValue;
   if (ep.drop_keep > 0.f && (N % 8 || batch != 1)) return (int)hipErrorInvalidValue;
@@ -107,6 +111,27 @@ HETU_API int hetu_gemm_bf16_gmask(const void* A, const void* B, void* C, const v
   if (!G) return (int)hipErrorInvalidValue;
   return gemm_bf16_impl(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, 1, 0, 0, 0, 0, 1.f,
                         0.f, 0, 0, 0, 0, 1, 0, nullptr, tile, nullptr, 0.f, 0, st, G, scale);
+}
+
+// dropout(act(A @ B)) as hetu_gemm_bf16_ex (keep < 1, batch 1), also writing the keep bits of
+// the stored output to `bits` (one byte per 8 elements of C, ldc % 8 == 0): the mask that
+// hetu_gemm_bf16_gbits reads in the backward instead of the bf16 output
+HETU_API int hetu_gemm_bf16_drop_bits(const void* A, const void* B, void* C, uint8_t* bits, int64_t M, int64_t N,
+                                      int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmaj, int b_kmaj,
+                                      int act, int tile, float keep, int64_t seed, hipStream_t st) {
+  if (!bits || !(keep < 1.f)) return (int)hipErrorInvalidValue;
+  return gemm_bf16_impl(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, 1, 0, 0, 0, 0, 1.f,
+                        0.f, act, 0, 0, 0, 1, 0, nullptr, tile, nullptr, keep, (uint64_t)seed, st, nullptr, 1.f, 0,
+                        bits);
+}
+
+// hetu_gemm_bf16_gmask with the mask given as those keep bits
+HETU_API int hetu_gemm_bf16_gbits(const void* A, const void* B, void* C, const uint8_t* bits, float scale, int64_t M,
+                                  int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmaj, int b_kmaj,
+                                  int tile, hipStream_t st) {
+  if (!bits) return (int)hipErrorInvalidValue;
+  return gemm_bf16_impl(A, B, C, nullptr, nullptr, M, N, K, lda, ldb, ldc, 0, a_kmaj, b_kmaj, 1, 0, 0, 0, 0, 1.f,
+                        0.f, 0, 0, 0, 0, 1, 0, nullptr, tile, nullptr, 0.f, 0, st, bits, scale, 1);
 }
 
 HETU_API int hetu_gemm_pick_splitk(int64_t M, int64_t N, int64_t K) { return pick_splitk(M, N, K); }

@@ -532,6 +532,13 @@ struct Epi {
   // that produces its input, from the forward's output alone
   const void* gmask;
   float gmask_scale;
+  // gmask_bits: gmask holds keep bits instead (one byte per 8 consecutive elements of C's
+  // layout, bit t = element n + t; ldc % 8 == 0) -- 1/16 of the bf16 mask's bytes
+  int gmask_bits;
+  // keep-bit output of the epilogue dropout (EX bit 1; null: none): the byte for elements
+  // n..n+7 of a row gets bit t set where the stored value is positive, in gmask_bits' layout
+  // -- the forward writes the mask its backward GEMM reads
+  uint8_t* mbits_out;
   // step counter of the graph-safe RNG (common.h rng_seed) for the epilogue dropout
   const uint64_t* drop_off;
 };
@@ -694,7 +701,11 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] += ep.beta * cv[t];
   }
-  if ((EX & 4) && ep.gmask) {   // ReLU / dropout backward: keep where the forward output is positive
+  if ((EX & 4) && ep.gmask && ep.gmask_bits) {   // the same from the forward's keep bits
+    const unsigned kb = has_gm ? gmv.x : (unsigned)((const uint8_t*)ep.gmask)[off >> 3];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = (kb >> t) & 1u ? v[t] * ep.gmask_scale : 0.f;
+  } else if ((EX & 4) && ep.gmask) {   // ReLU / dropout backward: keep where the forward output is positive
     const bf16* G = (const bf16*)ep.gmask + off;
     float gv[8];
     if (has_gm && full) {   // prefetched by the caller (this row piece, C's alignment)
@@ -739,6 +750,12 @@ __device__ __forceinline__ void epi_row8(const Epi& ep, const EpiOut& o, float (
     const float inv = 1.f / ep.drop_keep;
 #pragma unroll
     for (int t = 0; t < 8; ++t) v[t] = Philox::u01(q[t]) < ep.drop_keep ? v[t] * inv : 0.f;
+    if (ep.mbits_out) {
+      unsigned kb = 0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) kb |= (v[t] > 0.f ? 1u : 0u) << t;
+      ep.mbits_out[off >> 3] = (uint8_t)kb;
+    }
   }
   if (ep.out_f32) {
     float* Cf = (float*)o.Cb + off;
@@ -977,6 +994,25 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : (ST == 1 && HETU_BNX_PRE
 #pragma unroll
     for (int pss = 0; pss < NPASS; ++pss) pre_load(0, pss);
   }
+  // keep bits of the gradient mask (Epi::gmask_bits): all of this thread's row pieces,
+  // one byte each, requested together before the staging (NPASS <= 4: one word per half)
+  uint32_t gbw[2] = {0u, 0u};
+  const bool use_gb = (EX & 4) && ep.gmask && ep.gmask_bits;
+  if constexpr ((EX & 4) != 0) {
+    if (use_gb) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int pss = 0; pss < NPASS; ++pss) {
+          const int rr = pss * RPP + tid / TPR;
+          const int64_t m = (int64_t)tm * BM + h * 64 + rr;
+          const uint32_t b = (erow && rr < 64 && m < Mb && pre_n < N)
+                                 ? (uint32_t)((const uint8_t*)ep.gmask)[(la.out_row(m) * ep.ldc + pre_n) >> 3]
+                                 : 0u;
+          gbw[h] |= b << (8 * pss);
+        }
+    }
+  }
 
   // epilogue: lane holds C[m][n..n+3]
   if (ep.slab) {  // split-K partial: plain fp32 stores into this slice's slab
@@ -1036,7 +1072,11 @@ __global__ __launch_bounds__(NT, (ST == 1 && !BNX ? 4 : (ST == 1 && HETU_BNX_PRE
           v4f a1 = *reinterpret_cast<const v4f*>(stg + rr * SROW + ec + 4);
 #pragma unroll
           for (int t = 0; t < 4; ++t) { v[t] = a0[t] * ep.alpha; v[4 + t] = a1[t] * ep.alpha; }
-          epi_row8<BNX, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss]);
+          if constexpr ((EX & 4) != 0)
+            epi_row8<BNX, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss], use_gb,
+                              make_uint4((gbw[half] >> (8 * pss)) & 0xffu, 0u, 0u, 0u));
+          else
+            epi_row8<BNX, EX>(ep, eo, v, m, n, N, la.out_row(m), cs, cq, use_pre, cpre[pss]);
         }
         if (use_pre && half == 0) pre_load(1, pss);
       }
@@ -1280,9 +1320,13 @@ __global__ __launch_bounds__(BIG_NT, 1) void gemm_big_kernel(LA la, LB lb, Epi e
         for (int sp = 0; sp < 4; ++sp) {
           const int64_t m = (int64_t)tm * BIG + pass * 64 + sp * 16 + (tid >> 5);
           const int64_t n = (int64_t)tn * BIG + c;
-          gpre[sp] = (m < Mb && n + 7 < N)
-                         ? *reinterpret_cast<const uint4*>((const bf16*)ep.gmask + la.out_row(m) * ep.ldc + n)
-                         : make_uint4(0, 0, 0, 0);
+          if (ep.gmask_bits)
+            gpre[sp] = make_uint4(m < Mb && n < N ? ((const uint8_t*)ep.gmask)[(la.out_row(m) * ep.ldc + n) >> 3] : 0u,
+                                  0u, 0u, 0u);
+          else
+            gpre[sp] = (m < Mb && n + 7 < N)
+                           ? *reinterpret_cast<const uint4*>((const bf16*)ep.gmask + la.out_row(m) * ep.ldc + n)
+                           : make_uint4(0, 0, 0, 0);
         }
       }
     }

@@ -139,6 +139,70 @@ def matmul_relu_mask(a, b, ta, tb, g, scale):
     return binary('relu_grad_c', g.contiguous(), y.contiguous(), float(scale))
 
 
+def matmul_act_dropout_bits(a, b, activation, keep, seed):
+    """(y, mask): ``matmul_act_dropout`` and the mask its backward reads -- uint8 keep bits
+    (one byte per 8 outputs) from the same epilogue on the native bf16 path, else y itself
+    (its positive elements are the kept ones)"""
+    a, b = _match(a, b)
+    if native(a) and a.dtype == torch.bfloat16 and a.dim() == 2 \
+            and keep < 1.0 and b.shape[-1] % 8 == 0:
+        from . import gemm_mfma
+        from .autotune import choose
+
+        def cand(tile):
+            return lambda: gemm_mfma.gemm_drop_bits(a, b, activation, keep, seed, tile=tile)
+        cands = {'hip': cand(0)}
+        if _big_ok(a, b, False, False):
+            cands['hip256'] = cand(1)
+        if a.shape[-1] <= 2048:
+            cands['hip_lo'] = cand(3)
+        if b.shape[-1] % 96 == 0 and a.shape[0] >= 1024:
+            cands['hip96'] = cand(5)
+        if a.shape[-1] >= 3 * 64:
+            cands['hip_2a'] = cand(6)
+            if b.shape[-1] % 96 == 0 and a.shape[0] >= 1024:
+                cands['hip96_2a'] = cand(7)
+        c = choose(('gemm_dropb', _sig(a), _sig(b), activation), cands, 'hip')
+        r = cands[c]()
+        if r is None and c != 'hip':
+            r = cands['hip']()
+        if r is not None:
+            return r
+    y = matmul_act_dropout(a, b, activation, keep, seed)
+    return y, y
+
+
+def matmul_mask(a, b, ta, tb, mask, scale):
+    """``matmul_relu_mask`` with the mask of ``matmul_act_dropout_bits``: keep bits (uint8)
+    read by the GEMM epilogue, or the bf16 forward output"""
+    if mask.dtype != torch.uint8:
+        return matmul_relu_mask(a, b, ta, tb, mask.contiguous(), scale)
+    a, b = _match(a, b)
+    A2, B2 = _tr(a, ta), _tr(b, tb)
+    if native(a) and a.dtype == torch.bfloat16 and A2.dim() == 2:
+        from . import gemm_mfma
+        from .autotune import choose
+
+        def cand(tile):
+            return lambda: gemm_mfma.gemm_gbits(A2, B2, mask, scale, tile=tile)
+        cands = {'hip': cand(0)}
+        if _big_ok(a, b, ta, tb):
+            cands['hip256'] = cand(1)
+        if A2.shape[-1] <= 2048:
+            cands['hip_lo'] = cand(3)
+        if A2.shape[-1] >= 3 * 64:
+            cands['hip_2a'] = cand(6)
+        c = choose(('gemm_gbits', _sig(a), _sig(b), ta, tb), cands, 'hip')
+        y = cands[c]()
+        if y is None and c != 'hip':
+            y = cands['hip']()
+        if y is not None:
+            return y
+    y = matmul(a, b, ta, tb)
+    keep = (mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    return torch.where(keep.view(y.shape).bool(), y * scale, torch.zeros((), dtype=y.dtype, device=y.device))
+
+
 def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
     a, b = _match(a, b)
     from . import cpu_native

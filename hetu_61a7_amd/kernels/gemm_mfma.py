@@ -251,6 +251,49 @@ def gemm_gmask(a, b, g, scale, tile=0, out=None):
     return out
 
 
+def gemm_drop_bits(a, b, act, keep, seed, tile=0):
+    """(out, bits): bf16 out = dropout(act(a @ b)) as ``_gemm_ex`` (2-D, N % 8 == 0) and the
+    keep bits of out (uint8, one byte per 8 elements of a row, bit t set where out > 0) from
+    the same epilogue -- the mask ``gemm_gbits`` reads in the backward.  None when unsupported."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2 or not keep < 1.0:
+        return _reject(25, a, b, None)
+    M, K = a.shape
+    N = b.shape[1]
+    da = _operand(a, False)
+    db = _operand(b.t(), False)
+    if da is None or db is None or not _aligned(a, b) or N % 8:
+        return _reject(26, a, b, None)
+    out = _NA.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    bits = _NA.empty((M * N // 8,), dtype=torch.uint8, device=a.device)
+    f = fn('hetu_gemm_bf16_drop_bits', [P, P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I32, I32, F32, I64, P])
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), bits.data_ptr(), M, N, K, da[1], db[1], N, int(da[0]),
+            int(db[0]), _ACT[act], int(tile), float(keep), int(seed), stream_ptr()), 'gemm_bf16_drop_bits')
+    record_native('gemm_bf16')
+    return out, bits
+
+
+def gemm_gbits(a, b, bits, scale, tile=0):
+    """bf16 out = (a @ b) * scale where the keep bit is set, else 0 (2-D; ``bits`` from
+    ``gemm_drop_bits`` over an output of this shape): ``gemm_gmask`` reading 1/16 of the
+    bytes.  None when unsupported."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or a.dim() != 2 or b.dim() != 2:
+        return _reject(27, a, b, None)
+    M, K = a.shape
+    N = b.shape[1]
+    da = _operand(a, False)
+    db = _operand(b.t(), False)
+    if da is None or db is None or not _aligned(a, b):
+        return _reject(28, a, b, None)
+    if N % 8 or bits.dtype != torch.uint8 or bits.numel() != M * N // 8 or not bits.is_contiguous():
+        return _reject(29, a, b, None)
+    out = _NA.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    f = fn('hetu_gemm_bf16_gbits', [P, P, P, P, F32, I64, I64, I64, I64, I64, I64, I32, I32, I32, P])
+    check(f(a.data_ptr(), b.data_ptr(), out.data_ptr(), bits.data_ptr(), float(scale), M, N, K, da[1], db[1], N,
+            int(da[0]), int(db[0]), int(tile), stream_ptr()), 'gemm_bf16_gbits')
+    record_native('gemm_bf16')
+    return out
+
+
 SMALL_MAX_OUT = 1 << 16
 
 

@@ -198,21 +198,30 @@ class MatMulActDropoutOp(Op):
         assert activation == 'relu', activation
         self.activation, self.keep_prob = activation, keep_prob
         self.inference = False
+        self.emit_bits = False   # set by gradient(): aux = the keep bits the backward GEMM reads
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
-        from .nn import _next_seed
+        from .nn import _next_seed, AuxResult
         a, b = input_vals
         keep = 1.0 if self.inference else self.keep_prob
         if keep >= 1.0:
-            return KG.matmul(a, b, activation=self.activation)
+            y = KG.matmul(a, b, activation=self.activation)
+            return AuxResult(y, y) if self.emit_bits else y
+        if self.emit_bits:
+            y, mask = KG.matmul_act_dropout_bits(a, b, self.activation, keep, _next_seed(self.id, a))
+            return AuxResult(y, mask)
         return KG.matmul_act_dropout(a, b, self.activation, keep, _next_seed(self.id, a))
 
     def gradient(self, output_grad):
         if type(output_grad) is MatMulOp and len(output_grad.inputs) == 2 and _GMASK_EPI:
             # the gradient arriving here is the next layer's data-gradient GEMM: mask it in
-            # that GEMM's epilogue (one pass less over the [tokens, hidden] activation)
+            # that GEMM's epilogue (one pass less over the [tokens, hidden] activation);
+            # HETU_GMASK_BITS (default on, dropout layers): the forward epilogue also stores
+            # its keep bits and the backward epilogue reads those, 1/16 of the output's bytes
+            self.emit_bits = _GMASK_BITS and self.keep_prob < 1.0
             G = MatMulReluMaskOp(output_grad.inputs[0], output_grad.inputs[1], output_grad.matmul_attr_trans_A,
-                                 output_grad.matmul_attr_trans_B, self, self.keep_prob, ctx=self.raw_ctx)
+                                 output_grad.matmul_attr_trans_B, self, self.keep_prob, ctx=self.raw_ctx,
+                                 bits=self.emit_bits)
         else:
             G = ReluDropoutGradOp(output_grad, self, self.keep_prob, ctx=self.raw_ctx)
         mm = MatMulOp(self.inputs[0], self.inputs[1], False, False)
@@ -252,13 +261,17 @@ class MatMulReluMaskOp(Op):
     gradient of a MatMulActDropoutOp's output, produced and masked by one GEMM
     (``HETU_GMASK_EPILOGUE=0``: the plain GEMM + ReluDropoutGradOp)."""
 
-    def __init__(self, a, b, trans_A, trans_B, fwd, keep_prob, ctx=None):
+    def __init__(self, a, b, trans_A, trans_B, fwd, keep_prob, ctx=None, bits=False):
         super().__init__(MatMulReluMaskOp, [a, b, fwd], ctx)
         self.matmul_attr_trans_A, self.matmul_attr_trans_B = trans_A, trans_B
         self.keep_prob = keep_prob
+        if bits:
+            self.aux_inputs = (2,)   # the forward's mask (keep bits), not its output
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
         a, b, y = input_vals
+        if getattr(self, 'aux_inputs', None):
+            return KG.matmul_mask(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, y, 1.0 / self.keep_prob)
         return KG.matmul_relu_mask(a, b, self.matmul_attr_trans_A, self.matmul_attr_trans_B, y.contiguous(),
                                    1.0 / self.keep_prob)
 
@@ -270,6 +283,7 @@ class MatMulReluMaskOp(Op):
 
 
 _GMASK_EPI = os.environ.get('HETU_GMASK_EPILOGUE', '1') != '0'
+_GMASK_BITS = os.environ.get('HETU_GMASK_BITS', '1') != '0'
 
 
 def matmul_act_dropout_op(a, b, activation='relu', keep_prob=1.0, ctx=None):

@@ -418,6 +418,38 @@ def test_gemm_relu_mask_epilogue(M, N, K, tb, tile):
     assert _rel(auto, ref) < _tol(auto)
 
 
+@pytest.mark.parametrize('tile', [0, 1, 3, 5, 6])
+@pytest.mark.parametrize('M,N,K', [(4096, 2048, 512), (1000, 264, 200), (512, 768, 2048)])
+def test_dropout_keep_bits_roundtrip(M, N, K, tile):
+    """The forward dropout epilogue's keep bits (one byte per 8 outputs) equal out > 0 of
+    the output it stores; the backward GEMM masked by those bits equals the one masked by
+    the bf16 output, for every tile either side takes"""
+    from hetu_61a7_amd.kernels import gemm as KG
+    torch.manual_seed(3)
+    keep, seed = 0.9, 777
+    a = (torch.randn(M, K, device=DEV) * 0.5).bfloat16()
+    w = (torch.randn(K, N, device=DEV) * 0.05).bfloat16()
+    r = G.gemm_drop_bits(a, w, 'relu', keep, seed, tile=tile)
+    if r is None:
+        pytest.skip('tile %d does not take this shape' % tile)
+    y, bits = r
+    ref_y = KG.matmul_act_dropout(a, w, 'relu', keep, seed)
+    assert bool((y == ref_y).all())
+    unpacked = (bits.view(-1, 1) >> torch.arange(8, device=DEV, dtype=torch.uint8)) & 1
+    assert bool((unpacked.view(M, N).bool() == (y > 0)).all())
+    g = torch.randn(M, 384, device=DEV).bfloat16()
+    w2 = torch.randn(N, 384, device=DEV).bfloat16()
+    out = G.gemm_gbits(g, w2.t(), bits, 1.0 / keep, tile=tile)
+    if out is None:
+        pytest.skip('tile %d does not take the backward shape' % tile)
+    ref = G.gemm_gmask(g, w2.t(), y, 1.0 / keep, tile=tile)
+    assert bool((out == ref).all())
+    y2, mask = KG.matmul_act_dropout_bits(a, w, 'relu', keep, seed)
+    assert mask.dtype == torch.uint8 and bool((y2 == ref_y).all())
+    auto = KG.matmul_mask(g, w2, False, True, mask, 1.0 / keep)
+    assert _rel(auto, (g.float() @ w2.float().t()) * (y > 0).float() / keep) < _tol(auto)
+
+
 @pytest.mark.parametrize('tile', G.TILES)
 @pytest.mark.parametrize('M,N,K,ta,tb', [(4096, 2, 2048, False, False), (4096, 2, 2048, False, True),
                                          (2048, 2, 4096, True, False), (4096, 8, 2048, False, True)])

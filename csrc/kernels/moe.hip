@@ -473,7 +473,27 @@ __global__ void __launch_bounds__(256) combine_k(const T* __restrict__ y, const 
   }
   T* o = out + (int64_t)t * d;
   if (vec) {
-    for (int c = lane * N; c < d; c += 64 * N) {
+    // four 16-byte pieces of a source row per lane in flight at once (row_scale_copy)
+    int c = lane * N;
+    for (; c + 3 * 64 * N < d; c += 4 * 64 * N) {
+      float acc[4][N];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < N; ++q) acc[u][q] = 0.f;
+      for (int r = 0; r < nv; ++r) {
+        float v[4][N];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load_vec<T>(rows[r] + c + u * 64 * N, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < N; ++q) acc[u][q] += ws[r] * v[u][q];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) store_vec<T>(o + c + u * 64 * N, acc[u]);
+    }
+    for (; c < d; c += 64 * N) {
       float acc[N];
 #pragma unroll
       for (int q = 0; q < N; ++q) acc[q] = 0.f;
@@ -511,7 +531,21 @@ __global__ void __launch_bounds__(256) gate_grad_k(const T* __restrict__ g, cons
   const T* yr = y + ((int64_t)idx[i] * cap + l) * d;
   float s = 0.f;
   if (vec) {
-    for (int c = lane * N; c < d; c += 64 * N) {
+    // four 16-byte pieces of both rows per lane in flight at once
+    int c = lane * N;
+    for (; c + 3 * 64 * N < d; c += 4 * 64 * N) {
+      float a[4][N], b[4][N];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        load_vec<T>(gr + c + u * 64 * N, a[u]);
+        load_vec<T>(yr + c + u * 64 * N, b[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < N; ++q) s += a[u][q] * b[u][q];
+    }
+    for (; c < d; c += 64 * N) {
       float a[N], b[N];
       load_vec<T>(gr + c, a);
       load_vec<T>(yr + c, b);
@@ -523,6 +557,83 @@ __global__ void __launch_bounds__(256) gate_grad_k(const T* __restrict__ g, cons
   }
   s = wave_sum(s);
   if (lane == 0) out[i] = s;
+}
+
+// Backward of the gate-weighted combine, both gradients from one read of the token
+// gradient g: wave s (slot) writes dslot[s] = w[si] * g[si / k] (zeros for an empty slot)
+// and the gate gradient gout[si] = <g[si / k], y[s]>; wave i < Tk also zeroes gout[i] of a
+// (token, choice) pair dropped at capacity.  (gather_slots_k + gate_grad_k read g twice.)
+template <typename T>
+__global__ void __launch_bounds__(256) gather_slots_gate_k(const T* __restrict__ g, const T* __restrict__ y,
+                                                           const int* __restrict__ slot_src,
+                                                           const float* __restrict__ w,
+                                                           const int64_t* __restrict__ loc, T* __restrict__ out,
+                                                           float* __restrict__ gout, int nslots, int Tk, int d,
+                                                           int k, int cap, int vec) {
+  constexpr int N = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s < Tk && lane == 0) {
+    const int64_t l = loc[s];
+    if (l >= cap || l < 0) gout[s] = 0.f;
+  }
+  if (s >= nslots) return;
+  const int si = slot_src[s];
+  T* o = out + (int64_t)s * d;
+  if (si < 0) {
+    if (vec) {
+      float z[N];
+#pragma unroll
+      for (int q = 0; q < N; ++q) z[q] = 0.f;
+      for (int c = lane * N; c < d; c += 64 * N) store_vec<T>(o + c, z);
+    } else {
+      for (int c = lane; c < d; c += 64) o[c] = from_f<T>(0.f);
+    }
+    return;
+  }
+  const float ww = w != nullptr ? w[si] : 1.f;
+  const T* gr = g + (int64_t)(si / k) * d;
+  const T* yr = y + (int64_t)s * d;
+  float acc = 0.f;
+  if (vec) {
+    int c = lane * N;
+    for (; c + 3 * 64 * N < d; c += 4 * 64 * N) {
+      float a[4][N], b[4][N];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        load_vec<T>(gr + c + u * 64 * N, a[u]);
+        load_vec<T>(yr + c + u * 64 * N, b[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+          acc += a[u][q] * b[u][q];
+          a[u][q] *= ww;
+        }
+        store_vec<T>(o + c + u * 64 * N, a[u]);
+      }
+    }
+    for (; c < d; c += 64 * N) {
+      float a[N], b[N];
+      load_vec<T>(gr + c, a);
+      load_vec<T>(yr + c, b);
+#pragma unroll
+      for (int q = 0; q < N; ++q) {
+        acc += a[q] * b[q];
+        a[q] *= ww;
+      }
+      store_vec<T>(o + c, a);
+    }
+  } else {
+    for (int c = lane; c < d; c += 64) {
+      const float a = to_f(gr[c]);
+      acc += a * to_f(yr[c]);
+      o[c] = from_f<T>(ww * a);
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) gout[si] = acc;
 }
 
 template <typename T>
@@ -675,6 +786,26 @@ HETU_API int hetu_moe_combine(const void* y, const int64_t* idx, const int64_t* 
   else
     combine_k<float><<<g, 256, 0, s>>>((const float*)y, idx, loc, w, (float*)out, T, k, cap, d,
                                        vec_ok<float>(y, out, d));
+  HETU_LAUNCH_CHECK();
+  return 0;
+}
+
+// both gradients of the gate-weighted combine (gather_slots_gate_k): y [nslots, d] the
+// expert outputs the forward combined, g [T, d], out [nslots, d], gout [Tk] fp32
+HETU_API int hetu_moe_gather_slots_gate(const void* g, const void* y, const int* slot_src, const float* w,
+                                        const int64_t* loc, void* out, float* gout, int nslots, int Tk, int d, int k,
+                                        int cap, int bf16_io, hipStream_t s) {
+  const int n = nslots > Tk ? nslots : Tk;
+  const int gr = (n + 3) / 4;
+  if (gr == 0) return 0;
+  if (bf16_io)
+    gather_slots_gate_k<bf16><<<gr, 256, 0, s>>>((const bf16*)g, (const bf16*)y, slot_src, w, loc, (bf16*)out, gout,
+                                                 nslots, Tk, d, k, cap,
+                                                 vec_ok<bf16>(g, y, d) && vec_ok<bf16>(out, out, d));
+  else
+    gather_slots_gate_k<float><<<gr, 256, 0, s>>>((const float*)g, (const float*)y, slot_src, w, loc, (float*)out,
+                                                  gout, nslots, Tk, d, k, cap,
+                                                  vec_ok<float>(g, y, d) && vec_ok<float>(out, out, d));
   HETU_LAUNCH_CHECK();
   return 0;
 }

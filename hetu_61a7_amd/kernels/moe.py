@@ -297,6 +297,27 @@ def reverse_layout_transform_backward_data(g, indices, locations, gates, capacit
     return out.to(g.dtype)
 
 
+def reverse_layout_transform_backward_fused(g, y, indices, locations, gates, capacity, num_slots):
+    """(``reverse_layout_transform_backward_data``, ``reverse_layout_transform_backward_gate``)
+    -- on the GPU one kernel reading the token gradient once"""
+    T = indices.shape[0]
+    idx, loc = _ik(indices, T), _ik(locations, T)
+    k = idx.shape[1]
+    d = g.shape[-1]
+    if _io_ok(g, y) and tuple(y.shape) == (num_slots, d):
+        g, y = _dc(g), _dc(y)
+        smap = _slot_map(idx, loc, capacity, num_slots)
+        wf = _dc(gates.reshape(T, k), torch.float32) if gates is not None else None
+        out = _NA.empty((num_slots, d), dtype=g.dtype, device=g.device)
+        gout = _NA.empty((T, k), dtype=torch.float32, device=g.device)
+        f = fn('hetu_moe_gather_slots_gate', [P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, P])
+        check(f(g.data_ptr(), y.data_ptr(), smap.data_ptr(), ptr_or_none(wf), loc.data_ptr(), out.data_ptr(),
+                gout.data_ptr(), num_slots, T * k, d, k, capacity, is_bf16(g), stream_ptr()), 'moe_gather_slots_gate')
+        return out, gout.reshape(indices.shape)
+    return (reverse_layout_transform_backward_data(g, indices, locations, gates, capacity, num_slots),
+            reverse_layout_transform_backward_gate(g, y, indices, locations, capacity))
+
+
 def reverse_layout_transform_backward_gate(g, y, indices, locations, capacity):
     T = indices.shape[0]
     idx, loc = _ik(indices, T), _ik(locations, T)

@@ -9,6 +9,7 @@ no atomics on the forward combine.
 """
 from __future__ import annotations
 
+import os
 import torch
 from .. import native_array as _NA
 
@@ -118,6 +119,11 @@ class ReverseLayoutTransformOp(Op):
     def gradient(self, output_grad):
         k = self.k
         ins = self.inputs
+        if self.has_gate and k == 1 and _FUSED_COMBINE_BWD:
+            # one [T, k] index tensor: both gradients from one kernel reading output_grad once
+            gd = ReverseLayoutTransformGradientDataOp(output_grad, ins[1:2], ins[2:3], ins[3:4], self.capacity,
+                                                      self.num_experts, ctx=self.raw_ctx, y=ins[0])
+            return [gd, None, None, CombineGateGradOp(gd, ins[1], ctx=self.raw_ctx)]
         gd = ReverseLayoutTransformGradientDataOp(output_grad, ins[1:1 + k], ins[1 + k:1 + 2 * k],
                                                   ins[1 + 2 * k:1 + 3 * k] if self.has_gate else None,
                                                   self.capacity, self.num_experts, ctx=self.raw_ctx)
@@ -133,19 +139,30 @@ class ReverseLayoutTransformOp(Op):
 
 
 class ReverseLayoutTransformGradientDataOp(Op):
-    def __init__(self, grad, indices_s, location_s, gates, capacity, num_experts, ctx=None):
+    """Expert-slot gradient of the combine.  ``y`` (the combined expert outputs; one [T, k]
+    index tensor): also the gate gradient, as the aux value read by a CombineGateGradOp --
+    one kernel reads the token gradient once for both."""
+
+    def __init__(self, grad, indices_s, location_s, gates, capacity, num_experts, ctx=None, y=None):
         indices_s = list(indices_s) if isinstance(indices_s, (list, tuple)) else [indices_s]
         location_s = list(location_s) if isinstance(location_s, (list, tuple)) else [location_s]
         gates = (list(gates) if isinstance(gates, (list, tuple)) else [gates]) if gates is not None else []
-        super().__init__(ReverseLayoutTransformGradientDataOp, [grad] + indices_s + location_s + gates, ctx)
+        super().__init__(ReverseLayoutTransformGradientDataOp,
+                         [grad] + indices_s + location_s + gates + ([y] if y is not None else []), ctx)
         self.k, self.has_gate = len(indices_s), len(gates) > 0
+        self.with_gate_grad = y is not None
         self.capacity, self.num_experts = _keep(capacity), int(num_experts)
 
     def compute(self, input_vals, output_val=None, stream_handle=None):
+        from .nn import AuxResult
         k = self.k
         idx, loc = _stack(input_vals[1:1 + k]), _stack(input_vals[1 + k:1 + 2 * k])
         gates = _stack(input_vals[1 + 2 * k:1 + 3 * k]) if self.has_gate else None
         cap = _cap(self.capacity)
+        if self.with_gate_grad:
+            d, dg = KM.reverse_layout_transform_backward_fused(input_vals[0], input_vals[-1], idx, loc, gates, cap,
+                                                               cap * self.num_experts)
+            return AuxResult(d, dg)
         return KM.reverse_layout_transform_backward_data(input_vals[0], idx, loc, gates, cap, cap * self.num_experts)
 
     def gradient(self, output_grad):
@@ -153,6 +170,27 @@ class ReverseLayoutTransformGradientDataOp(Op):
 
     def infer_shape(self, input_shapes):
         return (_cap(self.capacity) * self.num_experts, input_shapes[0][-1])
+
+
+class CombineGateGradOp(Op):
+    """The gate gradient computed by a fused ReverseLayoutTransformGradientDataOp (its aux)"""
+    aux_inputs = (0,)
+    shape_only_inputs = (1,)
+
+    def __init__(self, data_grad, indices, ctx=None):
+        super().__init__(CombineGateGradOp, [data_grad, indices], ctx)
+
+    def compute(self, input_vals, output_val=None, stream_handle=None):
+        return input_vals[0].reshape(tuple(input_vals[1]))
+
+    def gradient(self, output_grad):
+        raise NotImplementedError
+
+    def infer_shape(self, input_shapes):
+        return input_shapes[1]
+
+
+_FUSED_COMBINE_BWD = os.environ.get('HETU_MOE_FUSED_COMBINE_BWD', '1') != '0'
 
 
 class ReverseLayoutTransformGradientGateOp(Op):

@@ -122,3 +122,30 @@ def test_moe_row_concat_experts_match_concat_path(monkeypatch):
         losses[rc] = [float(np.asarray(ex.run('train', feed_dict={x: X}, convert_to_numpy_ret_vals=True)[0])
                             .reshape(-1)[0]) for _ in range(4)]
     np.testing.assert_allclose(losses[True], losses[False], rtol=2e-2)
+
+
+@pytest.mark.parametrize('dt,tol', [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize('T,d,E,k,cap', [(64, 256, 8, 2, 12), (300, 2048, 4, 2, 100), (33, 130, 4, 1, 9)])
+def test_fused_combine_backward_matches_separate_kernels(dt, tol, T, d, E, k, cap):
+    """Both gradients of the gate-weighted combine from one kernel (the token gradient read
+    once) equal the slot-gather and gate-gradient kernels and the CPU reference, with
+    pairs dropped at capacity (gate gradient 0) and empty slots (zero rows)"""
+    rng = np.random.RandomState(T + d)
+    idx = torch.tensor(rng.randint(0, E, size=(T, k)).astype(np.int64))
+    probs = torch.tensor(rng.rand(T, E).astype(np.float32))
+    loc, _, _ = KM.locations(idx, E, probs)
+    gates = torch.tensor(rng.rand(T, k).astype(np.float32))
+    g = torch.tensor(rng.randn(T, d).astype(np.float32)).to(dt)
+    y = torch.tensor(rng.randn(E * cap, d).astype(np.float32)).to(dt)
+    assert bool((loc >= cap).any()), 'the case should drop some pairs'
+    dc, gc = KM.reverse_layout_transform_backward_fused(g, y, idx, loc, gates, cap, E * cap)   # CPU reference
+    i, l, w = idx.cuda(), loc.cuda(), gates.cuda()
+    d1, g1 = KM.reverse_layout_transform_backward_fused(g.cuda(), y.cuda(), i, l, w, cap, E * cap)
+    d0 = KM.reverse_layout_transform_backward_data(g.cuda(), i, l, w, cap, E * cap)
+    g0 = KM.reverse_layout_transform_backward_gate(g.cuda(), y.cuda(), i, l, cap)
+    assert d1.dtype == dt and g1.dtype == torch.float32 and tuple(g1.shape) == (T, k)
+    assert bool((d1 == d0).all())
+    np.testing.assert_allclose(g1.cpu().numpy(), g0.cpu().numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(d1.float().cpu().numpy(), dc.float().numpy(), rtol=tol, atol=tol)
+    np.testing.assert_allclose(g1.cpu().numpy(), gc.float().numpy(), rtol=tol, atol=tol * d ** 0.5)
+    assert bool((g1.cpu()[loc >= cap] == 0).all())

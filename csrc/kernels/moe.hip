@@ -329,9 +329,18 @@ __global__ void __launch_bounds__(256) loc_scan_k(const int64_t* __restrict__ id
   }
   if (sg == S - 1 && threadIdx.x == 0) counts[e] = base;
   if (probs != nullptr && psum != nullptr && sg == 0) {
-    // the tokens' gate probabilities, in a fixed order (deterministic balance loss)
-    float sp = 0.f;
-    for (int t = threadIdx.x; t < T; t += 256) sp += probs[(int64_t)t * E + e];
+    // the tokens' gate probabilities, in a fixed order (deterministic balance loss); eight
+    // independent loads per thread in flight (one block walks all T tokens)
+    float sq[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sq[u] = 0.f;
+    int t = threadIdx.x;
+    for (; t + 7 * 256 < T; t += 8 * 256) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sq[u] += probs[(int64_t)(t + u * 256) * E + e];
+    }
+    for (; t < T; t += 256) sq[0] += probs[(int64_t)t * E + e];
+    float sp = ((sq[0] + sq[1]) + (sq[2] + sq[3])) + ((sq[4] + sq[5]) + (sq[6] + sq[7]));
     sp = wave_sum(sp);
     if (lane == 0) fsum[w] = sp;
     __syncthreads();

@@ -538,6 +538,10 @@ HETU_API int hetu_reduce_mid(const void* x, void* y, int64_t B, int64_t R, int64
   // never more chunks than the workspace sized by hetu_reduce_mid_ws holds
   const int64_t ws_chunks = hetu_reduce_mid_ws(B, R, C) / (B * C);
   if (chunks > ws_chunks) chunks = ws_chunks;
+  // a few output columns (e.g. [T, E] gate statistics over T): the final pass is a handful
+  // of blocks walking every chunk partial -- 1024 chunks kept one block busy for 24 us
+  // after a 5 us first pass; 256 balances the two
+  if (B * C <= 16 * 64 && chunks > 256) chunks = 256;
   int64_t rpc = (R + chunks - 1) / chunks;
   dim3 grid((unsigned)ctiles, (unsigned)B, (unsigned)chunks);
   if (vec) {

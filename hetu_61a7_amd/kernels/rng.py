@@ -54,6 +54,8 @@ def set_base_seed(seed):
     """a new executor's random stream: base seed ``seed``, the step counters restart at 0
     (so an executor's masks depend on its seed and step index alone)"""
     _BASE[0] = int(seed) & _M64
+    _EPOCH[0] = 0                        # the CPU seeds mix the step index in directly
+    _CALLS.clear()
     _ADVANCED.clear()
     for c in _CTR.values():
         c.zero_()

@@ -26,6 +26,7 @@ from . import fn, check, stream_ptr, P, I64, I32, F32
 
 _BASE = [1234]
 _EPOCH = [0]          # host step index (bumped by the executors at every step start)
+_EPOCH0 = [0]         # _EPOCH at the last set_base_seed
 _ADVANCED = {}        # device -> epoch its counter was last advanced for
 _CALLS = {}           # key -> draws in the current step
 _CTR = {}             # device -> int64 [1] device counter (kept alive for the process)
@@ -54,8 +55,7 @@ def set_base_seed(seed):
     """a new executor's random stream: base seed ``seed``, the step counters restart at 0
     (so an executor's masks depend on its seed and step index alone)"""
     _BASE[0] = int(seed) & _M64
-    _EPOCH[0] = 0                        # the CPU seeds mix the step index in directly
-    _CALLS.clear()
+    _EPOCH0[0] = _EPOCH[0]               # CPU seeds mix in the step index since this point
     _ADVANCED.clear()
     for c in _CTR.values():
         c.zero_()
@@ -104,7 +104,7 @@ def next_seed(key, on_gpu=True):
     _HOST_RANDOM[0] += 1
     s = _mix(_BASE[0] ^ _mix((int(key) << 20) ^ c))
     if not on_gpu:
-        s = _mix(s ^ e)                  # no device counter: the step varies the seed
+        s = _mix(s ^ (e - _EPOCH0[0]))   # no device counter: the step varies the seed
     s &= (1 << 63) - 1                   # int64 launch argument
     return s or 1
 

@@ -10,6 +10,8 @@ Adam bias corrections) live in a device tensor read by the fused update kernel
 from __future__ import annotations
 
 import atexit
+import contextlib
+import gc
 import weakref
 
 import torch
@@ -27,6 +29,23 @@ FORCE_EAGER = [0]
 def note_host_random():
     """called by every host seed draw (kernels/rng.py)"""
     _HOST_RANDOM[0] += 1
+
+
+@contextlib.contextmanager
+def no_gc():
+    """Python's cycle collector stays off while a step is captured: a finaliser running
+    inside the capture (a runner or pool of an earlier executor freeing device memory,
+    destroying its graph, stream or events) invalidates it -- seen as hipError 901 at the
+    next launch, depending on when the collector happened to run.  One collection first,
+    outside the capture (torch.cuda.graph does the same)."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def capturing():
@@ -196,7 +215,7 @@ class GraphRunner(object):
             # torch captures on `cap`; the framework's launches follow it there.  use_stream
             # is the OUTER context: on exit it restores torch's stream to the framework's
             # previous one, which must happen after the graph's capture_end ran on `cap`
-            with RT.use_stream(cap), torch.cuda.graph(self.graph, stream=cap.torch):
+            with no_gc(), RT.use_stream(cap), torch.cuda.graph(self.graph, stream=cap.torch):
                 self.static_vals = sub._run_eager(None, vals=dict(base))
         finally:
             _CAPTURING[0] -= 1
@@ -212,7 +231,7 @@ class GraphRunner(object):
         cap.wait_stream(None)                 # after the work queued on the current stream
         g = RT.Graph()
         self.pool = MP.capture_pool(dev, cap)
-        with self.pool, RT.use_stream(cap):
+        with no_gc(), self.pool, RT.use_stream(cap):
             g.begin(cap)
             _CAPTURING[0] += 1
             try:

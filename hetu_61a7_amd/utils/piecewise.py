@@ -246,7 +246,7 @@ class PiecewiseRunner(object):
         g = RT.Graph()
         s.pool = MP.capture_pool(dev, cap)
         try:
-            with s.pool, RT.use_stream(cap):
+            with hipgraph.no_gc(), s.pool, RT.use_stream(cap):
                 g.begin(cap)
                 hipgraph._CAPTURING[0] += 1
                 try:

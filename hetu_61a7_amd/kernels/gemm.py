@@ -243,10 +243,13 @@ def matmul(a, b, ta=False, tb=False, bias=None, activation=None):
             A2.shape[1] >= 8192:
         # long reductions over few output tiles (the MLM head's data gradient, K = vocab):
         # split K over fp32 slabs + one reduce
+        # (BERT's masked-position head: 60 tiles at K = 30 528 -- 4 slices left 240 blocks
+        # on 256 CUs; the single-stage tile holds 4 blocks per CU)
         tiles = -(-A2.shape[0] // 128) * -(-B2.shape[1] // 128)
-        for s_ in (2, 4):
-            if tiles * s_ <= 2048:
+        for s_ in (2, 4, 6, 8, 12, 16):
+            if tiles * s_ <= 2048 and A2.shape[1] // s_ >= 512:
                 cands['hip_sk%d' % s_] = (lambda s_=s_: gemm_mfma.gemm(A2, B2, splitk=s_))
+                cands['hip_lo_sk%d' % s_] = (lambda s_=s_: gemm_mfma.gemm(A2, B2, splitk=s_, tile=3))
     if A2.dim() == 2 and B2.dim() == 2 and A2.shape[0] * B2.shape[1] <= gemm_mfma.SMALL_MAX_OUT:
         cands['hip_small'] = lambda: gemm_mfma.gemm_small(A2, B2, bias=bias, act=activation)
     # any shape: zero-padded aligned operands on the MFMA tile (last hand-written resort)
@@ -277,6 +280,8 @@ def _run_decided(gemm_mfma, d, a, b, ta, tb, bias, activation):
         return gemm_mfma.padded(A2, B2, bias=bias, act=activation)
     if d.startswith('hip_sk'):
         return gemm_mfma.gemm(A2, B2, splitk=int(d[6:]))
+    if d.startswith('hip_lo_sk'):
+        return gemm_mfma.gemm(A2, B2, splitk=int(d[9:]), tile=3)
     return None
 
 

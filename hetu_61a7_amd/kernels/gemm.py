@@ -422,19 +422,19 @@ def matmul_into(a, b, ta, tb, out):
         elif A.dim() == 2:
             M, K, N = A.shape[0], A.shape[1], B.shape[1]
             tiles = -(-M // 128) * -(-N // 128)
-            for s in (2, 3, 4, 6, 8):
+            for s in (2, 3, 4, 6, 8, 12, 16):
                 if tiles * s <= 1536 and K // s >= 512:
                     cands['hip_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s))
             # the single-stage tile at 4 blocks per CU: 892 vs 592 TF for the 2-stage tile on
             # 3072x3072x8192 TN (profiles/gemm_tn_r4.txt) -- and 1024 resident slots for splits
             if K >= 1024:
                 cands['hip_lo'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=3)
-                for s in (2, 3, 4, 5, 6, 7, 8):
+                for s in (2, 3, 4, 5, 6, 7, 8, 12, 16):
                     if tiles * s <= 2048 and K // s >= 512:
                         cands['hip_lo_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=3))
             if K >= 3 * 64:
                 cands['hip_2a'] = lambda: gemm_mfma.gemm(A, B, out=out, tile=6)
-                for s in (2, 3, 4, 6, 8):
+                for s in (2, 3, 4, 6, 8, 12, 16):
                     if tiles * s <= 1536 and K // s >= 512:
                         cands['hip_2a_sk%d' % s] = (lambda s=s: gemm_mfma.gemm(A, B, out=out, splitk=s, tile=6))
             if M >= 256 and N >= 256:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 closing check: the driver-form GPU tier (smoke + pytest -m gpu), then the default
-# bench line and the MoE / BERT bench lines at HEAD
+# bench line and the MoE / BERT / Wide&Deep bench lines at HEAD
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out
@@ -14,3 +14,5 @@ for i in 1 2; do
 done
 timeout -k 10 300 python -u bench.py --model bert --steps 20 --warmup 5 > $O/fin_bert.json 2> $O/fin_bert.err || exit $?
 tail -1 $O/fin_bert.json | cut -c1-160
+timeout -k 10 300 python -u bench.py --model wdl --steps 200 --warmup 20 > $O/fin_wdl.json 2> $O/fin_wdl.err || exit $?
+tail -1 $O/fin_wdl.json | cut -c1-160

@@ -193,6 +193,11 @@ def test_pooling(dt, k, s, p, h):
 def test_reductions():
     x = torch.randn(64, 1000, 37, device=DEV)
     torch.testing.assert_close(KR.reduce_mid(x), x.sum(1), rtol=1e-4, atol=1e-3)
+    # few output columns over a long axis (the MoE gate statistics [T, E] over T): the
+    # chunk count is capped so the final pass stays short -- every row still summed once
+    for shape in ((1, 65536, 2), (3, 40000, 5), (1, 1000003, 1)):
+        x = torch.rand(*shape, device=DEV)
+        torch.testing.assert_close(KR.reduce_mid(x), x.double().sum(1).float(), rtol=2e-5, atol=1e-3)
     y = torch.randn(5000, 300, device=DEV)
     torch.testing.assert_close(KR.reduce_last(y), y.sum(1), rtol=1e-4, atol=1e-3)
     # 16-byte vector form (C % 8 == 0 bf16 / C % 4 == 0 fp32) and the scalar form, bf16 rows

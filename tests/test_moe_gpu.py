@@ -149,3 +149,35 @@ def test_fused_combine_backward_matches_separate_kernels(dt, tol, T, d, E, k, ca
     np.testing.assert_allclose(d1.float().cpu().numpy(), dc.float().numpy(), rtol=tol, atol=tol)
     np.testing.assert_allclose(g1.cpu().numpy(), gc.float().numpy(), rtol=tol, atol=tol * d ** 0.5)
     assert bool((g1.cpu()[loc >= cap] == 0).all())
+
+
+def test_moe_keep_bit_mask_trains_like_bf16_mask(monkeypatch):
+    """experts with dropout: the backward mask GEMM reading the forward's 1-bit keep masks
+    (HETU_GMASK_BITS) trains exactly like reading the bf16 forward output"""
+    import hetu_61a7_amd.layers.moe as LM
+    import hetu_61a7_amd.ops.linalg as OL
+    from hetu_61a7_amd.ops import node as _node
+    losses, init = {}, None
+    for bits in (True, False):
+        monkeypatch.setattr(OL, '_GMASK_BITS', bits)
+        _node.G_NODE_ID = 0
+        rng = np.random.RandomState(0)
+        T, d, E = 512, 128, 4
+        x = ht.Variable(name='x')
+        gate = LM.TopKGate(embed_dim=d, num_tokens=T, num_experts=E, k=2)
+        experts = [LM.Expert(d, 256, activation='relu', dropout_rate=0.1, name='expert_%d' % i) for i in range(E)]
+        y, l_aux = LM.MoELayer(gate=gate, experts=experts, num_tokens=T, embed_dim=d)(x)
+        loss = ht.add_op(ht.reduce_mean_op(ht.mul_op(y, y), [0, 1]), l_aux)
+        train = ht.optim.SGDOptimizer(0.1).minimize(loss)
+        ex = ht.Executor({'train': [loss, train]}, ctx=ht.gpu(0), seed=3, mixed_precision='bf16')
+        pm = {n.name: t for n, t in ex.config.placeholder_to_arr_map.items() if n.trainable}
+        if init is None:
+            init = {k: v.detach().clone() for k, v in pm.items()}
+        else:
+            for k, v in pm.items():
+                v.copy_(init[k])
+        X = rng.randn(T, d).astype(np.float32)
+        losses[bits] = [float(np.asarray(ex.run('train', feed_dict={x: X}, convert_to_numpy_ret_vals=True)[0])
+                              .reshape(-1)[0]) for _ in range(4)]
+    assert len(set(losses[True])) > 1
+    np.testing.assert_allclose(losses[True], losses[False], rtol=1e-5)

@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) stem_pack_w_k(const bf16* __restrict__ w,
 __global__ void __launch_bounds__(256) stem_fwd_k(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                                                   bf16* __restrict__ y, float* __restrict__ colstats, int csrep,
                                                   int H, int W, int C, int KH, int KW, int s, int p, int OH, int OW,
-                                                  int KS, int RS) {
+                                                  int KS, int RS, int vec) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* patch = reinterpret_cast<bf16*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -58,13 +58,53 @@ __global__ void __launch_bounds__(256) stem_fwd_k(const bf16* __restrict__ x, co
   // 1. input rows oh0*s - p ... into LDS; patch column j <-> input element j - p*C of the row
   const int64_t img = (int64_t)n * H * W * C;
   const int WC = W * C;
-  for (int rr = 0; rr < IR; ++rr) {
-    const int ih = oh0 * s - p + rr;
-    const bool rok = ih >= 0 && ih < H;
-    const bf16* src = x + img + (int64_t)ih * WC - p * C;
-    for (int j = tid; j < RS; j += 256) {
-      const int e = j - p * C;
-      patch[rr * RS + j] = (rok && e >= 0 && e < WC) ? src[j] : __float2bfloat16(0.f);
+  if (vec) {
+    // rows as 16-byte pieces, four per thread in flight before their LDS writes (element
+    // by element: the halo offset p*C is odd for C = 3); then the halo columns.  (The
+    // element-wise loop below waits one memory latency per element it stages.)
+    const int pC = p * C, nvr = WC / 8, tot = IR * nvr;
+    unsigned short* pu = reinterpret_cast<unsigned short*>(patch);
+    for (int b0 = 0; b0 < tot; b0 += 4 * 256) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = b0 + u * 256 + tid;
+        v[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (i < tot) {
+          const int rr = i / nvr, q = i - rr * nvr;
+          const int ih = oh0 * s - p + rr;
+          if (ih >= 0 && ih < H) v[u] = *reinterpret_cast<const uint4*>(x + img + (int64_t)ih * WC + q * 8);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = b0 + u * 256 + tid;
+        if (i < tot) {
+          const int rr = i / nvr, q = i - rr * nvr;
+          unsigned short* d = pu + rr * RS + pC + q * 8;
+          const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            d[2 * t] = (unsigned short)(w4[t] & 0xffffu);
+            d[2 * t + 1] = (unsigned short)(w4[t] >> 16);
+          }
+        }
+      }
+    }
+    const int hz = RS - WC;   // zero columns per row: [0, pC) and [pC + WC, RS)
+    for (int i = tid; i < IR * hz; i += 256) {
+      const int rr = i / hz, c = i - rr * hz;
+      pu[rr * RS + (c < pC ? c : c + WC)] = 0;
+    }
+  } else {
+    for (int rr = 0; rr < IR; ++rr) {
+      const int ih = oh0 * s - p + rr;
+      const bool rok = ih >= 0 && ih < H;
+      const bf16* src = x + img + (int64_t)ih * WC - p * C;
+      for (int j = tid; j < RS; j += 256) {
+        const int e = j - p * C;
+        patch[rr * RS + j] = (rok && e >= 0 && e < WC) ? src[j] : __float2bfloat16(0.f);
+      }
     }
   }
 
@@ -375,8 +415,10 @@ HETU_API int hetu_stem_fwd(const void* x, const void* w, void* wp, void* y, floa
   hipLaunchKernelGGL(stem_pack_w_k, dim3((CO * KP + 255) / 256), dim3(256), 0, st, (const bf16*)w, (bf16*)wp, KH,
                      KW, C, KP);
   const int blocks = N * ((OH + R - 1) / R);
+  // 16-byte staging: whole rows of 16-byte pieces, each landing inside the patch row
+  const int vec = (W * C) % 8 == 0 && ((uintptr_t)x & 15) == 0 && p * C + W * C <= RS && !getenv("HETU_STEM_SCALAR");
   hipLaunchKernelGGL(stem_fwd_k, dim3(blocks), dim3(256), lds, st, (const bf16*)x, (const bf16*)wp, (bf16*)y,
-                     colstats, csrep, H, W, C, KH, KW, s, p, OH, OW, KS, RS);
+                     colstats, csrep, H, W, C, KH, KW, s, p, OH, OW, KS, RS, vec);
   return (int)hipGetLastError();
 }
 

@@ -216,6 +216,63 @@ __global__ void __launch_bounds__(256) maxpool_bwd_vec(const T* __restrict__ dy,
   }
 }
 
+// The same backward for pools where at most 2 x 2 windows hold a pixel, one block per input
+// row (n, h): the row's output-window range is block-uniform and each thread keeps one
+// channel group, stepping over w -- the flat form's six integer divisions per 16-byte
+// output (index decomposition) made it ALU-bound (254 us at ResNet-50's 112 x 112 x 64 x 256).
+// Requires 256 % (C / V) == 0.
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_bwd_rows(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                         T* __restrict__ dx, int H, int W, int C, int Ho, int Wo,
+                                                         int kh, int kw, int sh, int sw, int ph, int pw) {
+  constexpr int V = Vec<T>::N;
+  const int cv = C / V;
+  const int h = blockIdx.x, n = blockIdx.y;
+  int ho0 = (h + ph - kh + sh) / sh; if (h + ph - kh + 1 < 0) ho0 = 0;
+  int ho1 = (h + ph) / sh; if (ho1 >= Ho) ho1 = Ho - 1;
+  const int cg = threadIdx.x % cv, wstep = 256 / cv;
+  T* drow = dx + ((int64_t)n * H + h) * W * C + cg * V;
+  for (int w = threadIdx.x / cv; w < W; w += wstep) {
+    int wo0 = (w + pw - kw + sw) / sw; if (w + pw - kw + 1 < 0) wo0 = 0;
+    int wo1 = (w + pw) / sw; if (wo1 >= Wo) wo1 = Wo - 1;
+    uint2 pk[4];
+    float g[4][V];
+    int tp[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ho = ho0 + (q >> 1), wo = wo0 + (q & 1);
+      const int a = h + ph - ho * sh, b = w + pw - wo * sw;
+      const bool ok = ho <= ho1 && wo <= wo1 && a >= 0 && a < kh && b >= 0 && b < kw;
+      tp[q] = ok ? a * kw + b : -1;
+      const int64_t o = ok ? ((int64_t)(n * Ho + ho) * Wo + wo) * C + cg * V : 0;
+      if (V == 8) {
+        pk[q] = ok ? *reinterpret_cast<const uint2*>(idx + o) : make_uint2(0, 0);
+      } else {
+        pk[q] = make_uint2(ok ? *reinterpret_cast<const uint32_t*>(idx + o) : 0u, 0u);
+      }
+      if (ok) {
+        load_vec<T>(dy + o, g[q]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k) g[q][k] = 0.f;
+      }
+    }
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const uint32_t word = k < 4 ? pk[q].x : pk[q].y;
+        const int ix = (int)((word >> (8 * (k & 3))) & 255u);
+        if (ix == tp[q]) acc[k] += g[q][k];
+      }
+    }
+    store_vec<T>(drow + (int64_t)w * C, acc);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, int N,
                                                       int H, int W, int C, int Ho, int Wo, int kh,
@@ -471,6 +528,14 @@ HETU_API int hetu_maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int 
                               int pw, int is_bf16, hipStream_t st) {
   int64_t total = (int64_t)N * H * W * C;
   const int V = is_bf16 ? 8 : 4;
+  if (C % V == 0 && 256 % (C / V) == 0 && kh <= sh + 1 && kw <= sw + 1 && H <= 65535 && N <= 65535 &&
+      !getenv("HETU_MAXPOOL_FLAT")) {
+    const dim3 grid((unsigned)H, (unsigned)N);
+    if (is_bf16) hipLaunchKernelGGL(maxpool_bwd_rows<bf16>, grid, dim3(256), 0, st, (const bf16*)dy, idx, (bf16*)dx, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+    else hipLaunchKernelGGL(maxpool_bwd_rows<float>, grid, dim3(256), 0, st, (const float*)dy, idx, (float*)dx, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw);
+    HETU_LAUNCH_CHECK();
+    return 0;
+  }
   if (C % V == 0 && total < (1LL << 31)) {
     int64_t nb = (total / V + 255) / 256;
     int grid = (int)(nb < 65536 ? nb : 65536);

@@ -441,6 +441,51 @@ __global__ __launch_bounds__(WG_NW * 64, 1) void conv3x3_c64_wgrad_k(const bf16*
 }
 
 // dw[i] (+)= sum over nb slabs of slab[b][i], i over 64*9*64 fp32 (float4 per thread)
+// first pass of the two-pass slab sum: group blockIdx.y adds slabs [g*per, (g+1)*per) (eight
+// loads in flight per thread) and writes the total over its own first slab (each thread reads
+// its element of every slab of the group before it writes that element).  One pass over all
+// N = 256 per-image slabs left 36 blocks each walking 256 slabs two at a time (35 us).
+__global__ void __launch_bounds__(256) wgrad_slab_group_k(float4* __restrict__ slab, int nb, int per, int n4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int k0 = blockIdx.y * per, k1 = min(nb, k0 + per);
+  float4 a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = k0;
+  for (; k + 7 < k1; k += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = slab[(int64_t)(k + u) * n4 + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { a[u].x += v[u].x; a[u].y += v[u].y; a[u].z += v[u].z; a[u].w += v[u].w; }
+  }
+  for (; k < k1; ++k) {
+    const float4 v = slab[(int64_t)k * n4 + i];
+    a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+  }
+#pragma unroll
+  for (int u = 1; u < 8; ++u) { a[0].x += a[u].x; a[0].y += a[u].y; a[0].z += a[u].z; a[0].w += a[u].w; }
+  if (k0 < k1) slab[(int64_t)k0 * n4 + i] = a[0];
+}
+
+// second pass: dw (+)= the group totals (slabs 0, per, 2 per, ...)
+__global__ void __launch_bounds__(256) wgrad_slab_final_k(const float4* __restrict__ slab, int nb, int per,
+                                                          float4* __restrict__ dw, int n4, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < nb; k += per) {
+    const float4 v = slab[(int64_t)k * n4 + i];
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  if (accumulate) {
+    const float4 o = dw[i];
+    a.x += o.x; a.y += o.y; a.z += o.z; a.w += o.w;
+  }
+  dw[i] = a;
+}
+
 __global__ void __launch_bounds__(256) wgrad_slab_reduce_k(const float4* __restrict__ slab, int nb,
                                                            float4* __restrict__ dw, int n4, int accumulate) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -858,8 +903,16 @@ HETU_API int hetu_conv3x3_c64_wgrad(const void* x, const void* dy, float* dw, fl
                        (const bf16*)dy, ws, H);
   HETU_LAUNCH_CHECK();
   const int n4 = 9 * CH * CH / 4;
-  hipLaunchKernelGGL(wgrad_slab_reduce_k, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws, N,
-                     (float4*)dw, n4, accumulate);
+  if (N >= 64 && !getenv("HETU_SLAB_ONEPASS")) {
+    const int G = 16, per = (N + G - 1) / G;
+    hipLaunchKernelGGL(wgrad_slab_group_k, dim3((n4 + 255) / 256, (N + per - 1) / per), dim3(256), 0, st,
+                       (float4*)ws, N, per, n4);
+    hipLaunchKernelGGL(wgrad_slab_final_k, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws, N, per,
+                       (float4*)dw, n4, accumulate);
+  } else {
+    hipLaunchKernelGGL(wgrad_slab_reduce_k, dim3((n4 + 255) / 256), dim3(256), 0, st, (const float4*)ws, N,
+                       (float4*)dw, n4, accumulate);
+  }
   return (int)hipGetLastError();
 }
 

@@ -224,7 +224,7 @@ def test_no_library_fallback_raises():
         KG.matmul(a, a)
 
 
-@pytest.mark.parametrize('n,h', [(2, 56), (3, 57), (1, 5)])
+@pytest.mark.parametrize('n,h', [(2, 56), (3, 57), (1, 5), (70, 5)])   # n >= 64: two-pass slab sum
 def test_conv3x3_c64_halo_kernel(n, h):
     """3x3/s1/p1 64->64 halo-tile kernel: forward (+ fused BN statistics) and data
     gradient (+ bf16 / fp32 join) against fp32 autograd on the same bf16 operands."""
